@@ -1,0 +1,849 @@
+/*
+ * sentinel_oracle.c -- CPU restatement of Sentinel's sliding-window token-decision path.
+ *
+ * TEST INFRASTRUCTURE ONLY (parity checker + "port" CPU baseline).  See sentinel_oracle.h.
+ * Compiled with -O2 -ffp-contract=off and no fast-math so every double operation is one IEEE
+ * operation in Java source order (JLS 15.17-15.18; strictfp is the default since Java 17 and
+ * HotSpot on x86-64 SSE2 already behaves that way for Java 7/8).
+ *
+ * Reference paths (under /root/reference):
+ *   LA  = sentinel-core/src/main/java/com/alibaba/csp/sentinel/slots/statistic/base/LeapArray.java
+ *   CM  = sentinel-cluster/sentinel-cluster-server-default/src/main/java/com/alibaba/csp/sentinel/
+ *         cluster/flow/statistic/metric/ClusterMetric.java
+ *   CMLA= .../cluster/flow/statistic/metric/ClusterMetricLeapArray.java
+ *   CFC = .../cluster/flow/ClusterFlowChecker.java
+ *   DTS = .../cluster/flow/DefaultTokenService.java
+ *   RL  = .../cluster/flow/statistic/limit/RequestLimiter.java
+ *   GRL = .../cluster/flow/statistic/limit/GlobalRequestLimiter.java
+ *   CPM = .../cluster/flow/statistic/metric/ClusterParamMetric.java
+ *   CPFC= .../cluster/flow/ClusterParamFlowChecker.java
+ *   SCFC= sentinel-cluster/sentinel-cluster-server-envoy-rls/.../rls/flow/SimpleClusterFlowChecker.java
+ *   SN  = sentinel-core/.../node/StatisticNode.java
+ *   DC  = sentinel-core/.../slots/block/flow/controller/DefaultController.java
+ *   PFC = sentinel-extension/sentinel-parameter-flow-control/.../slots/block/flow/param/ParamFlowChecker.java
+ */
+#include "sentinel_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ Java numerics */
+
+/* JLS 5.1.3 narrowing double -> int: NaN -> 0, saturate at the int range, else truncate. */
+int32_t orc_java_d2i(double d) {
+    if (d != d) return 0;
+    if (d >= 2147483647.0) return INT32_MAX;
+    if (d <= -2147483648.0) return INT32_MIN;
+    return (int32_t)d;
+}
+
+int64_t orc_java_d2l(double d) {
+    if (d != d) return 0;
+    if (d >= 9223372036854775807.0) return INT64_MAX;
+    if (d <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)d;
+}
+
+/* java.lang.String.hashCode: s[0]*31^(n-1) + ... with int overflow. */
+int32_t orc_java_string_hash(const uint16_t *s, int64_t n) {
+    uint32_t h = 0;
+    for (int64_t i = 0; i < n; i++) h = 31u * h + (uint32_t)s[i];
+    return (int32_t)h;
+}
+
+static int64_t wrap_add64(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+static int64_t wrap_mul64(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
+
+/* ------------------------------------------------------------------ LeapArray core */
+/* The slot array of LA:41-78: sampleCount WindowWraps {windowStart, value}. */
+typedef struct {
+    int n, win, interval;
+    double interval_sec;     /* LA:74 intervalInMs / 1000.0 */
+    int64_t *start;
+    uint8_t *present;
+} leap;
+
+enum { LA_SAME = 0, LA_NEW = 1, LA_RESET = 2, LA_DETACHED = 3, LA_NULL = 4 };
+
+static void leap_init(leap *a, int n, int interval_ms) {
+    a->n = n;
+    a->interval = interval_ms;
+    a->win = interval_ms / n;                 /* LA:72 */
+    a->interval_sec = interval_ms / 1000.0;   /* LA:74 */
+    a->start = (int64_t *)calloc((size_t)n, sizeof(int64_t));
+    a->present = (uint8_t *)calloc((size_t)n, 1);
+}
+
+static void leap_free(leap *a) { free(a->start); free(a->present); }
+
+/* LA:112-124 calculateTimeIdx */
+static int leap_idx(const leap *a, int64_t t) { return (int)((t / a->win) % a->n); }
+
+/* LA:149-248 currentWindow(t), single-threaded: the CAS always wins and tryLock always succeeds.
+ * Returns the action; *idx = slot.  The caller applies newEmptyBucket / resetWindowTo. */
+static int leap_locate(leap *a, int64_t t, int *idx) {
+    if (t < 0) return LA_NULL;                        /* LA:150-152 */
+    int i = leap_idx(a, t);
+    int64_t ws = t - t % a->win;                      /* LA:140 */
+    *idx = i;
+    if (!a->present[i]) {                             /* LA:172-194 */
+        a->present[i] = 1;
+        a->start[i] = ws;
+        return LA_NEW;
+    }
+    if (ws == a->start[i]) return LA_SAME;            /* LA:195-209 */
+    if (ws > a->start[i]) {                           /* LA:210-240 resetWindowTo */
+        a->start[i] = ws;                             /* WindowWrap.resetTo */
+        return LA_RESET;
+    }
+    return LA_DETACHED;                               /* LA:241-246: a fresh, unshared wrap */
+}
+
+/* LA:316-318 isWindowDeprecated(time, w) */
+static int leap_deprecated(const leap *a, int64_t t, int i) { return t - a->start[i] > a->interval; }
+
+/* ------------------------------------------------------------------ ClusterMetric */
+struct orc_cluster_metric {
+    leap la;
+    int64_t *c;                 /* n x 7 ClusterMetricBucket counters */
+    int64_t occ[ORC_NEVENTS];   /* CMLA:129 occupyCounter */
+    int has_occupied;           /* CMLA:130 */
+    int64_t scratch[ORC_NEVENTS];
+};
+
+orc_cluster_metric *orc_cm_new(int sample_count, int interval_ms) {
+    if (sample_count <= 0 || interval_ms <= 0 || interval_ms % sample_count != 0) return NULL; /* CM:33-35 */
+    orc_cluster_metric *m = (orc_cluster_metric *)calloc(1, sizeof(*m));
+    leap_init(&m->la, sample_count, interval_ms);
+    m->c = (int64_t *)calloc((size_t)sample_count * ORC_NEVENTS, sizeof(int64_t));
+    return m;
+}
+
+void orc_cm_free(orc_cluster_metric *m) {
+    if (!m) return;
+    leap_free(&m->la);
+    free(m->c);
+    free(m);
+}
+
+/* LA currentWindow + CMLA:141-161 (newEmptyBucket / resetWindowTo + transferOccupyToBucket). */
+static int64_t *cm_current(orc_cluster_metric *m, int64_t t) {
+    int i = 0;
+    int act = leap_locate(&m->la, t, &i);
+    if (act == LA_NULL) return NULL;
+    if (act == LA_DETACHED) {
+        memset(m->scratch, 0, sizeof(m->scratch));
+        return m->scratch;
+    }
+    int64_t *b = m->c + (size_t)i * ORC_NEVENTS;
+    if (act == LA_NEW) {
+        memset(b, 0, sizeof(int64_t) * ORC_NEVENTS);  /* CMLA:142-144 new ClusterMetricBucket() */
+    } else if (act == LA_RESET) {
+        memset(b, 0, sizeof(int64_t) * ORC_NEVENTS);  /* CMLA:149 reset() */
+        if (m->has_occupied) {                        /* CMLA:154-161 */
+            b[ORC_OCCUPIED_PASS] = wrap_add64(b[ORC_OCCUPIED_PASS], m->occ[ORC_PASS]);
+            b[ORC_PASS] = wrap_add64(b[ORC_PASS], m->occ[ORC_PASS]);
+            m->occ[ORC_PASS] = 0;
+            b[ORC_PASS_REQUEST] = wrap_add64(b[ORC_PASS_REQUEST], m->occ[ORC_PASS_REQUEST]);
+            m->occ[ORC_PASS_REQUEST] = 0;
+            m->has_occupied = 0;
+        }
+    }
+    return b;
+}
+
+/* CM:39-41 */
+void orc_cm_add(orc_cluster_metric *m, int64_t t, int event, int64_t count) {
+    int64_t *b = cm_current(m, t);
+    if (b) b[event] = wrap_add64(b[event], count);
+}
+
+/* CM:43-45 */
+int64_t orc_cm_get_current_count(orc_cluster_metric *m, int64_t t, int event) {
+    int64_t *b = cm_current(m, t);
+    return b ? b[event] : 0;
+}
+
+/* CM:53-62: currentWindow(); sum over values() (LA:375-390). */
+int64_t orc_cm_get_sum(orc_cluster_metric *m, int64_t t, int event) {
+    cm_current(m, t);
+    if (t < 0) return 0;
+    int64_t sum = 0;
+    for (int i = 0; i < m->la.n; i++) {
+        if (!m->la.present[i] || leap_deprecated(&m->la, t, i)) continue;
+        sum = wrap_add64(sum, m->c[(size_t)i * ORC_NEVENTS + event]);
+    }
+    return sum;
+}
+
+/* CM:70-72: long / double */
+double orc_cm_get_avg(orc_cluster_metric *m, int64_t t, int event) {
+    return (double)orc_cm_get_sum(m, t, event) / m->la.interval_sec;
+}
+
+/* CMLA:181-190 getFirstCountOfWindow via LA:399-409 getValidHead(t). */
+static int64_t cm_first_count(orc_cluster_metric *m, int64_t t, int event) {
+    int i = leap_idx(&m->la, t + m->la.win);
+    if (!m->la.present[i] || leap_deprecated(&m->la, t, i)) return 0;
+    return m->c[(size_t)i * ORC_NEVENTS + event];
+}
+
+/* CM:79-98 */
+int orc_cm_try_occupy_next(orc_cluster_metric *m, int64_t t, int event, int acquire, double threshold) {
+    double latest = orc_cm_get_avg(m, t, ORC_PASS);
+    int64_t head = cm_first_count(m, t, event);
+    int64_t occupied = m->occ[event];
+    /* latestQps + (acquireCount + occupiedCount) - headPass <= threshold  (int+long -> long) */
+    int64_t inner = wrap_add64((int64_t)acquire, occupied);
+    double lhs = (latest + (double)inner) - (double)head;
+    if (!(lhs <= threshold)) return 0;
+    m->occ[ORC_PASS] = wrap_add64(m->occ[ORC_PASS], acquire);        /* CMLA:171-175 */
+    m->occ[ORC_PASS_REQUEST] = wrap_add64(m->occ[ORC_PASS_REQUEST], 1);
+    m->has_occupied = 1;
+    orc_cm_add(m, t, ORC_WAITING, acquire);
+    return 1000 / m->la.n;                                            /* CM:86 */
+}
+
+void orc_cm_dump(const orc_cluster_metric *m, int64_t *out) {
+    int n = m->la.n;
+    for (int i = 0; i < n; i++) {
+        int64_t *o = out + (size_t)i * (1 + ORC_NEVENTS);
+        o[0] = m->la.present[i] ? m->la.start[i] : -1;
+        for (int e = 0; e < ORC_NEVENTS; e++) o[1 + e] = m->la.present[i] ? m->c[(size_t)i * ORC_NEVENTS + e] : 0;
+    }
+    int64_t *o = out + (size_t)n * (1 + ORC_NEVENTS);
+    for (int e = 0; e < ORC_NEVENTS; e++) o[e] = m->occ[e];
+    o[ORC_NEVENTS] = m->has_occupied;
+}
+
+int orc_cm_list_count(const orc_cluster_metric *m, int64_t t) {
+    int k = 0;
+    for (int i = 0; i < m->la.n; i++)
+        if (m->la.present[i] && !leap_deprecated(&m->la, t, i)) k++;
+    return k;
+}
+
+int64_t orc_cm_first_count(orc_cluster_metric *m, int64_t t, int event) { return cm_first_count(m, t, event); }
+
+int64_t orc_cm_window_start(orc_cluster_metric *m, int64_t t) {
+    int i = 0;
+    if (t < 0) return -1;
+    int64_t *b = cm_current(m, t);
+    (void)b;
+    i = leap_idx(&m->la, t);
+    return m->la.start[i] == t - t % m->la.win ? m->la.start[i] : t - t % m->la.win;
+}
+
+/* ------------------------------------------------------------------ RequestLimiter */
+/* RL:35-37: UnaryLeapArray(10, 1000) (core/.../base/UnaryLeapArray.java:21-38). */
+struct orc_limiter {
+    leap la;
+    int64_t *v;
+    double qps_allowed;
+};
+
+orc_limiter *orc_limiter_new(double qps_allowed) {
+    orc_limiter *l = (orc_limiter *)calloc(1, sizeof(*l));
+    leap_init(&l->la, 10, 1000);
+    l->v = (int64_t *)calloc(10, sizeof(int64_t));
+    l->qps_allowed = qps_allowed;
+    return l;
+}
+
+void orc_limiter_free(orc_limiter *l) {
+    if (!l) return;
+    leap_free(&l->la);
+    free(l->v);
+    free(l);
+}
+
+static int64_t lim_scratch;
+static int64_t *lim_current(orc_limiter *l, int64_t t) {
+    int i = 0;
+    int act = leap_locate(&l->la, t, &i);
+    if (act == LA_NULL) return NULL;
+    if (act == LA_DETACHED) { lim_scratch = 0; return &lim_scratch; }
+    if (act == LA_NEW || act == LA_RESET) l->v[i] = 0;   /* UnaryLeapArray.java:28-37 */
+    return &l->v[i];
+}
+
+void orc_limiter_add(orc_limiter *l, int64_t t, int x) {   /* RL:49-51 */
+    int64_t *p = lim_current(l, t);
+    if (p) *p = wrap_add64(*p, x);
+}
+
+int64_t orc_limiter_get_sum(orc_limiter *l, int64_t t) {   /* RL:53-62 */
+    lim_current(l, t);
+    int64_t s = 0;
+    for (int i = 0; i < l->la.n; i++)
+        if (l->la.present[i] && !leap_deprecated(&l->la, t, i)) s = wrap_add64(s, l->v[i]);
+    return s;
+}
+
+double orc_limiter_get_qps(orc_limiter *l, int64_t t) {    /* RL:64-66 */
+    return (double)orc_limiter_get_sum(l, t) / l->la.interval_sec;
+}
+
+int orc_limiter_can_pass(orc_limiter *l, int64_t t) {      /* RL:72-74 */
+    return orc_limiter_get_qps(l, t) + 1 <= l->qps_allowed;
+}
+
+int orc_limiter_try_pass(orc_limiter *l, int64_t t) {      /* RL:81-87 */
+    if (orc_limiter_can_pass(l, t)) {
+        orc_limiter_add(l, t, 1);
+        return 1;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ exact key->count map */
+typedef struct {
+    uint64_t *k;
+    int64_t *v;
+    uint8_t *used;
+    int64_t cap, size;
+} kvmap;
+
+static void kv_init(kvmap *m) { memset(m, 0, sizeof(*m)); }
+static void kv_free(kvmap *m) { free(m->k); free(m->v); free(m->used); memset(m, 0, sizeof(*m)); }
+static void kv_clear(kvmap *m) { if (m->used) memset(m->used, 0, (size_t)m->cap); m->size = 0; }
+
+static uint64_t mix64(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+    return x;
+}
+
+static int64_t *kv_find(kvmap *m, uint64_t key) {
+    if (!m->cap) return NULL;
+    uint64_t h = mix64(key) & (uint64_t)(m->cap - 1);
+    while (m->used[h]) {
+        if (m->k[h] == key) return &m->v[h];
+        h = (h + 1) & (uint64_t)(m->cap - 1);
+    }
+    return NULL;
+}
+
+static int64_t *kv_insert(kvmap *m, uint64_t key, int64_t init) {
+    int64_t *p = kv_find(m, key);
+    if (p) return p;
+    if ((m->size + 1) * 2 > m->cap) {
+        kvmap n;
+        n.cap = m->cap ? m->cap * 2 : 16;
+        n.size = 0;
+        n.k = (uint64_t *)calloc((size_t)n.cap, sizeof(uint64_t));
+        n.v = (int64_t *)calloc((size_t)n.cap, sizeof(int64_t));
+        n.used = (uint8_t *)calloc((size_t)n.cap, 1);
+        for (int64_t i = 0; i < m->cap; i++)
+            if (m->used[i]) *kv_insert(&n, m->k[i], m->v[i]) = m->v[i];
+        kv_free(m);
+        *m = n;
+    }
+    uint64_t h = mix64(key) & (uint64_t)(m->cap - 1);
+    while (m->used[h]) h = (h + 1) & (uint64_t)(m->cap - 1);
+    m->used[h] = 1;
+    m->k[h] = key;
+    m->v[h] = init;
+    m->size++;
+    return &m->v[h];
+}
+
+/* ------------------------------------------------------------------ ClusterParamMetric */
+/* Each bucket is a CacheMap<Object, LongAdder> (ClusterParameterLeapArray.java:40-49).  The LRU
+ * eviction of ConcurrentLinkedHashMap (capacity 4000) is NOT restated: exact counters only, and
+ * `overflow` records that a bucket exceeded its capacity (parity unpinned past that point). */
+struct orc_param_metric {
+    leap la;
+    kvmap *b;
+    kvmap scratch;
+    int max_capacity;
+    int overflow;
+};
+
+orc_param_metric *orc_pm_new(int sample_count, int interval_ms, int max_capacity) {
+    if (sample_count <= 0 || interval_ms <= 0 || interval_ms % sample_count != 0 || max_capacity <= 0) return NULL;
+    orc_param_metric *m = (orc_param_metric *)calloc(1, sizeof(*m));
+    leap_init(&m->la, sample_count, interval_ms);
+    m->b = (kvmap *)calloc((size_t)sample_count, sizeof(kvmap));
+    kv_init(&m->scratch);
+    m->max_capacity = max_capacity;
+    return m;
+}
+
+void orc_pm_free(orc_param_metric *m) {
+    if (!m) return;
+    for (int i = 0; i < m->la.n; i++) kv_free(&m->b[i]);
+    kv_free(&m->scratch);
+    free(m->b);
+    leap_free(&m->la);
+    free(m);
+}
+
+static kvmap *pm_current(orc_param_metric *m, int64_t t) {
+    int i = 0;
+    int act = leap_locate(&m->la, t, &i);
+    if (act == LA_NULL) return NULL;
+    if (act == LA_DETACHED) { kv_clear(&m->scratch); return &m->scratch; }
+    if (act == LA_NEW || act == LA_RESET) kv_clear(&m->b[i]);   /* new map / clear() */
+    return &m->b[i];
+}
+
+void orc_pm_add_value(orc_param_metric *m, int64_t t, uint64_t key, int count) {   /* CPM:66-78 */
+    kvmap *b = pm_current(m, t);
+    if (!b) return;
+    int64_t *p = kv_insert(b, key, 0);
+    *p = wrap_add64(*p, count);
+    if (b->size > m->max_capacity) m->overflow = 1;
+}
+
+int64_t orc_pm_get_sum(orc_param_metric *m, int64_t t, uint64_t key) {             /* CPM:46-60 */
+    pm_current(m, t);
+    int64_t s = 0;
+    for (int i = 0; i < m->la.n; i++) {
+        if (!m->la.present[i] || leap_deprecated(&m->la, t, i)) continue;
+        int64_t *p = kv_find(&m->b[i], key);
+        if (p) s = wrap_add64(s, *p);
+    }
+    return s;
+}
+
+double orc_pm_get_avg(orc_param_metric *m, int64_t t, uint64_t key) {              /* CPM:80-82 */
+    return (double)orc_pm_get_sum(m, t, key) / m->la.interval_sec;
+}
+
+typedef struct { uint64_t k; int64_t v; int64_t ord; } kvent;
+static int cmp_top(const void *pa, const void *pb) {
+    const kvent *a = (const kvent *)pa, *b = (const kvent *)pb;
+    /* CPM:107-113: (int) b - (int) a, descending by (int)value; ties keep insertion order. */
+    int32_t ia = (int32_t)a->v, ib = (int32_t)b->v;
+    int32_t d = (int32_t)((uint32_t)ib - (uint32_t)ia);
+    if (d != 0) return d < 0 ? -1 : 1;
+    return a->ord < b->ord ? -1 : (a->ord > b->ord);
+}
+
+int orc_pm_top_values(orc_param_metric *m, int64_t t, int number, uint64_t *keys, double *avgs) {  /* CPM:84-127 */
+    if (number <= 0) return -1;
+    pm_current(m, t);
+    kvmap merged;
+    kv_init(&merged);
+    for (int i = 0; i < m->la.n; i++) {
+        if (!m->la.present[i] || leap_deprecated(&m->la, t, i)) continue;
+        for (int64_t j = 0; j < m->b[i].cap; j++) {
+            if (!m->b[i].used[j]) continue;
+            int64_t *p = kv_insert(&merged, m->b[i].k[j], 0);
+            *p = wrap_add64(*p, m->b[i].v[j]);
+        }
+    }
+    kvent *ents = (kvent *)calloc((size_t)(merged.size ? merged.size : 1), sizeof(kvent));
+    int64_t ne = 0;
+    for (int64_t j = 0; j < merged.cap; j++)
+        if (merged.used[j]) { ents[ne].k = merged.k[j]; ents[ne].v = merged.v[j]; ents[ne].ord = ne; ne++; }
+    /* Java HashMap iteration order is unspecified; sort ties by key for determinism. */
+    for (int64_t a = 0; a < ne; a++) ents[a].ord = (int64_t)ents[a].k;
+    qsort(ents, (size_t)ne, sizeof(kvent), cmp_top);
+    int size = ne > number ? number : (int)ne;
+    int out = 0;
+    for (int i = 0; i < size; i++) {
+        if (ents[i].v == 0) break;
+        keys[out] = ents[i].k;
+        avgs[out] = (double)ents[i].v / m->la.interval_sec;
+        out++;
+    }
+    free(ents);
+    kv_free(&merged);
+    return out;
+}
+
+int orc_pm_overflowed(const orc_param_metric *m) { return m->overflow; }
+
+/* ------------------------------------------------------------------ engine (DefaultTokenService) */
+typedef struct {
+    orc_param_rule r;
+    orc_param_metric *pm;
+} param_entry;
+
+struct orc_engine {
+    orc_server_config cfg;
+    orc_namespace *ns;
+    orc_limiter **lim;
+    int n_ns;
+    orc_flow_rule *rules;
+    orc_cluster_metric **cm;
+    int n_rules;
+    param_entry *prules;
+    int n_prules;
+    uint64_t *hot_keys;
+    int32_t *hot_counts;
+    int n_hot;
+};
+
+orc_engine *orc_engine_new(const orc_server_config *cfg, const orc_namespace *ns, int n_ns) {
+    orc_engine *e = (orc_engine *)calloc(1, sizeof(*e));
+    e->cfg = *cfg;
+    e->n_ns = n_ns;
+    e->ns = (orc_namespace *)calloc((size_t)(n_ns > 0 ? n_ns : 1), sizeof(orc_namespace));
+    e->lim = (orc_limiter **)calloc((size_t)(n_ns > 0 ? n_ns : 1), sizeof(orc_limiter *));
+    for (int i = 0; i < n_ns; i++) {
+        e->ns[i] = ns[i];
+        /* GRL:32-37 initIfAbsent -> new RequestLimiter(maxAllowedQps) */
+        if (ns[i].has_limiter) e->lim[i] = orc_limiter_new(ns[i].max_allowed_qps);
+    }
+    return e;
+}
+
+void orc_engine_free(orc_engine *e) {
+    if (!e) return;
+    for (int i = 0; i < e->n_ns; i++) orc_limiter_free(e->lim[i]);
+    for (int i = 0; i < e->n_rules; i++) orc_cm_free(e->cm[i]);
+    for (int i = 0; i < e->n_prules; i++) orc_pm_free(e->prules[i].pm);
+    free(e->ns); free(e->lim); free(e->rules); free(e->cm); free(e->prules);
+    free(e->hot_keys); free(e->hot_counts);
+    free(e);
+}
+
+/* ClusterFlowRuleManager.applyClusterFlowRule (ClusterFlowRuleManager.java:325-372): one
+ * ClusterMetric per flowId with the rule's (sampleCount, windowIntervalMs). */
+int orc_engine_load_flow_rules(orc_engine *e, const orc_flow_rule *rules, int n) {
+    for (int i = 0; i < e->n_rules; i++) orc_cm_free(e->cm[i]);
+    free(e->rules); free(e->cm);
+    e->rules = (orc_flow_rule *)calloc((size_t)(n > 0 ? n : 1), sizeof(orc_flow_rule));
+    e->cm = (orc_cluster_metric **)calloc((size_t)(n > 0 ? n : 1), sizeof(orc_cluster_metric *));
+    e->n_rules = n;
+    for (int i = 0; i < n; i++) {
+        e->rules[i] = rules[i];
+        e->cm[i] = orc_cm_new(rules[i].sample_count, rules[i].window_interval_ms);  /* NULL => FAIL */
+    }
+    return 0;
+}
+
+/* GRL:46-55 tryPass(namespace) */
+static int engine_allow_proceed(orc_engine *e, int32_t ns, int64_t t) {
+    if (ns < 0 || ns >= e->n_ns) return 0;          /* namespace == null -> false */
+    if (!e->lim[ns]) return 1;                      /* no limiter -> true */
+    return orc_limiter_try_pass(e->lim[ns], t);
+}
+
+/* CFC:38-48 calcGlobalThreshold */
+static double calc_global_threshold(const orc_engine *e, const orc_flow_rule *r) {
+    double count = r->count;
+    if (r->threshold_type == 1) return count;
+    int connected = (r->namespace_idx >= 0 && r->namespace_idx < e->n_ns) ? e->ns[r->namespace_idx].connected_count : 0;
+    return count * (double)connected;
+}
+
+static void set_result(int8_t *st, int32_t *rem, int32_t *wait, int s, int32_t r, int32_t w) {
+    *st = (int8_t)s;
+    *rem = r;
+    if (wait) *wait = w;
+}
+
+/* CFC:55-112 acquireClusterToken */
+static void cluster_flow_check(orc_engine *e, int32_t idx, int32_t acquire, int prio, int64_t t,
+                               int8_t *st, int32_t *rem, int32_t *wait) {
+    const orc_flow_rule *r = &e->rules[idx];
+    if (!engine_allow_proceed(e, r->namespace_idx, t)) { set_result(st, rem, wait, ORC_TOO_MANY_REQUEST, 0, 0); return; }
+    orc_cluster_metric *m = e->cm[idx];
+    if (!m) { set_result(st, rem, wait, ORC_FAIL, 0, 0); return; }
+    double latest = orc_cm_get_avg(m, t, ORC_PASS);
+    double global = calc_global_threshold(e, r) * e->cfg.exceed_count;
+    double next = (global - latest) - (double)acquire;
+    if (next >= 0) {
+        orc_cm_add(m, t, ORC_PASS, acquire);
+        orc_cm_add(m, t, ORC_PASS_REQUEST, 1);
+        if (prio) orc_cm_add(m, t, ORC_OCCUPIED_PASS, acquire);
+        set_result(st, rem, wait, ORC_OK, orc_java_d2i(next), 0);
+        return;
+    }
+    if (prio) {
+        double occupy_avg = orc_cm_get_avg(m, t, ORC_WAITING);
+        if (occupy_avg <= e->cfg.max_occupy_ratio * global) {
+            int w = orc_cm_try_occupy_next(m, t, ORC_PASS, acquire, global);
+            if (w > 0) { set_result(st, rem, wait, ORC_SHOULD_WAIT, 0, w); return; }
+        }
+    }
+    orc_cm_add(m, t, ORC_BLOCK, acquire);
+    orc_cm_add(m, t, ORC_BLOCK_REQUEST, 1);
+    if (prio) orc_cm_add(m, t, ORC_OCCUPIED_BLOCK, acquire);
+    set_result(st, rem, wait, ORC_BLOCKED, 0, 0);
+}
+
+/* SCFC:33-65 (Envoy RLS): no limiter, no priority, threshold = count * exceedCount. */
+static void simple_flow_check(orc_engine *e, int32_t idx, int32_t acquire, int64_t t,
+                              int8_t *st, int32_t *rem, int32_t *wait) {
+    const orc_flow_rule *r = &e->rules[idx];
+    orc_cluster_metric *m = e->cm[idx];
+    if (!m) { set_result(st, rem, wait, ORC_FAIL, 0, 0); return; }
+    double latest = orc_cm_get_avg(m, t, ORC_PASS);
+    double global = r->count * e->cfg.exceed_count;
+    double next = (global - latest) - (double)acquire;
+    if (next >= 0) {
+        orc_cm_add(m, t, ORC_PASS, acquire);
+        orc_cm_add(m, t, ORC_PASS_REQUEST, 1);
+        set_result(st, rem, wait, ORC_OK, orc_java_d2i(next), 0);
+    } else {
+        orc_cm_add(m, t, ORC_BLOCK, acquire);
+        orc_cm_add(m, t, ORC_BLOCK_REQUEST, 1);
+        set_result(st, rem, wait, ORC_BLOCKED, 0, 0);
+    }
+}
+
+/* DTS:37-48 requestToken (validation + rule lookup), then the rule's checker. */
+void orc_request_token(orc_engine *e, int32_t idx, int32_t acquire, int prio, int64_t t,
+                       int8_t *st, int32_t *rem, int32_t *wait) {
+    if (idx == -2 || acquire <= 0) { set_result(st, rem, wait, ORC_BAD_REQUEST, 0, 0); return; }
+    if (idx < 0 || idx >= e->n_rules) { set_result(st, rem, wait, ORC_NO_RULE_EXISTS, 0, 0); return; }
+    if (e->rules[idx].checker == 1) simple_flow_check(e, idx, acquire, t, st, rem, wait);
+    else cluster_flow_check(e, idx, acquire, prio, t, st, rem, wait);
+}
+
+void orc_flow_replay(orc_engine *e, int64_t n, const int32_t *flow_idx, const int32_t *acquire,
+                     const uint8_t *flags, const int64_t *ts,
+                     int8_t *status, int32_t *remaining, int32_t *wait_ms) {
+    for (int64_t i = 0; i < n; i++)
+        orc_request_token(e, flow_idx[i], acquire[i], flags ? (flags[i] & 1) : 0, ts[i],
+                          &status[i], &remaining[i], wait_ms ? &wait_ms[i] : NULL);
+}
+
+int orc_engine_dump_flow(const orc_engine *e, int32_t idx, int64_t *out) {
+    if (idx < 0 || idx >= e->n_rules || !e->cm[idx]) return -1;
+    orc_cm_dump(e->cm[idx], out);
+    return e->cm[idx]->la.n * (1 + ORC_NEVENTS) + ORC_NEVENTS + 1;
+}
+
+int64_t orc_engine_limiter_sum(orc_engine *e, int32_t ns, int64_t t) {
+    if (ns < 0 || ns >= e->n_ns || !e->lim[ns]) return -1;
+    return orc_limiter_get_sum(e->lim[ns], t);
+}
+
+/* ---- cluster hot-parameter path ---- */
+int orc_engine_load_param_rules(orc_engine *e, const orc_param_rule *rules, int n,
+                                const uint64_t *hot_keys, const int32_t *hot_counts, int n_hot) {
+    for (int i = 0; i < e->n_prules; i++) orc_pm_free(e->prules[i].pm);
+    free(e->prules); free(e->hot_keys); free(e->hot_counts);
+    e->prules = (param_entry *)calloc((size_t)(n > 0 ? n : 1), sizeof(param_entry));
+    e->n_prules = n;
+    for (int i = 0; i < n; i++) {
+        e->prules[i].r = rules[i];
+        /* ClusterParamFlowRuleManager.java:355 -> ClusterParamMetric(sampleCount, windowIntervalMs), cap 4000 */
+        e->prules[i].pm = orc_pm_new(rules[i].sample_count, rules[i].window_interval_ms, 4000);
+    }
+    e->n_hot = n_hot;
+    e->hot_keys = (uint64_t *)calloc((size_t)(n_hot > 0 ? n_hot : 1), sizeof(uint64_t));
+    e->hot_counts = (int32_t *)calloc((size_t)(n_hot > 0 ? n_hot : 1), sizeof(int32_t));
+    if (n_hot > 0) {
+        memcpy(e->hot_keys, hot_keys, sizeof(uint64_t) * (size_t)n_hot);
+        memcpy(e->hot_counts, hot_counts, sizeof(int32_t) * (size_t)n_hot);
+    }
+    return 0;
+}
+
+/* CPFC:101-120 calcGlobalThreshold(rule, value) */
+static double param_threshold(const orc_engine *e, const orc_param_rule *r, uint64_t v) {
+    double count = r->count;
+    for (int i = 0; i < r->hot_n; i++)                       /* ParamFlowRule.java:157-162 */
+        if (e->hot_keys[r->hot_begin + i] == v) { count = (double)e->hot_counts[r->hot_begin + i]; break; }
+    if (r->threshold_type == 1) return count;
+    int connected = (r->namespace_idx >= 0 && r->namespace_idx < e->n_ns) ? e->ns[r->namespace_idx].connected_count : 0;
+    return count * (double)connected;
+}
+
+/* DTS:51-62 + CPFC:42-87 */
+void orc_request_param_token(orc_engine *e, int32_t idx, int32_t acquire, int64_t t,
+                             const uint64_t *values, int n_values, int8_t *st, int32_t *rem) {
+    if (idx == -2 || acquire <= 0 || n_values <= 0) { *st = ORC_BAD_REQUEST; *rem = 0; return; }
+    if (idx < 0 || idx >= e->n_prules) { *st = ORC_NO_RULE_EXISTS; *rem = 0; return; }
+    const orc_param_rule *r = &e->prules[idx].r;
+    if (!engine_allow_proceed(e, r->namespace_idx, t)) { *st = ORC_TOO_MANY_REQUEST; *rem = 0; return; }
+    orc_param_metric *m = e->prules[idx].pm;
+    if (!m) { *st = ORC_FAIL; *rem = 0; return; }
+    double remaining = -1;
+    int passed = 1;
+    for (int i = 0; i < n_values; i++) {
+        double latest = orc_pm_get_avg(m, t, values[i]);
+        double thr = param_threshold(e, r, values[i]);
+        double next = (thr - latest) - (double)acquire;
+        remaining = next;
+        if (next < 0) { passed = 0; break; }
+    }
+    if (passed)
+        for (int i = 0; i < n_values; i++) orc_pm_add_value(m, t, values[i], acquire);
+    if (n_values > 1) remaining = -1;
+    if (passed) { *st = ORC_OK; *rem = orc_java_d2i(remaining); }
+    else { *st = ORC_BLOCKED; *rem = 0; }
+}
+
+void orc_param_replay(orc_engine *e, int64_t n, const int32_t *rule_idx, const int32_t *acquire,
+                      const uint64_t *param_key, const int64_t *ts, int8_t *status, int32_t *remaining) {
+    for (int64_t i = 0; i < n; i++)
+        orc_request_param_token(e, rule_idx[i], acquire[i], ts[i], &param_key[i], 1, &status[i], &remaining[i]);
+}
+
+int64_t orc_engine_param_sum(orc_engine *e, int32_t idx, int64_t t, uint64_t key) {
+    if (idx < 0 || idx >= e->n_prules || !e->prules[idx].pm) return 0;
+    return orc_pm_get_sum(e->prules[idx].pm, t, key);
+}
+
+int orc_engine_param_overflowed(const orc_engine *e) {
+    for (int i = 0; i < e->n_prules; i++)
+        if (e->prules[i].pm && e->prules[i].pm->overflow) return 1;
+    return 0;
+}
+
+/* ------------------------------------------------------------------ local StatisticNode */
+/* SN:96-103: rollingCounterInSecond = ArrayMetric(SAMPLE_COUNT=2, INTERVAL=1000) with occupy
+ * (OccupiableBucketLeapArray), rollingCounterInMinute = ArrayMetric(60, 60000, false).
+ * Only the non-prioritized path is restated: the borrow array (FutureBucketLeapArray) is only
+ * written by addWaiting (prioritized occupy), so newEmptyBucket/resetWindowTo never borrow here. */
+typedef struct {
+    leap la;
+    int64_t *c;          /* n x 6 MetricBucket counters */
+    int64_t scratch[ORC_M_NEVENTS];
+} bucket_array;
+
+struct orc_stat_node {
+    bucket_array sec, min;
+};
+
+static void ba_init(bucket_array *a, int n, int interval) {
+    leap_init(&a->la, n, interval);
+    a->c = (int64_t *)calloc((size_t)n * ORC_M_NEVENTS, sizeof(int64_t));
+}
+
+static int64_t *ba_current(bucket_array *a, int64_t t) {
+    int i = 0;
+    int act = leap_locate(&a->la, t, &i);
+    if (act == LA_NULL) return NULL;
+    if (act == LA_DETACHED) { memset(a->scratch, 0, sizeof(a->scratch)); return a->scratch; }
+    int64_t *b = a->c + (size_t)i * ORC_M_NEVENTS;
+    if (act != LA_SAME) memset(b, 0, sizeof(int64_t) * ORC_M_NEVENTS);   /* MetricBucket.reset() */
+    return b;
+}
+
+static int64_t ba_sum(bucket_array *a, int64_t t, int ev) {   /* ArrayMetric.pass()/block() */
+    ba_current(a, t);
+    int64_t s = 0;
+    for (int i = 0; i < a->la.n; i++)
+        if (a->la.present[i] && !leap_deprecated(&a->la, t, i)) s = wrap_add64(s, a->c[(size_t)i * ORC_M_NEVENTS + ev]);
+    return s;
+}
+
+static void ba_add(bucket_array *a, int64_t t, int ev, int64_t x) {
+    int64_t *b = ba_current(a, t);
+    if (b) b[ev] = wrap_add64(b[ev], x);
+}
+
+orc_stat_node *orc_node_new(int sample_count, int interval_ms) {
+    orc_stat_node *nd = (orc_stat_node *)calloc(1, sizeof(*nd));
+    ba_init(&nd->sec, sample_count, interval_ms);
+    ba_init(&nd->min, 60, 60 * 1000);
+    return nd;
+}
+
+void orc_node_free(orc_stat_node *nd) {
+    if (!nd) return;
+    leap_free(&nd->sec.la); free(nd->sec.c);
+    leap_free(&nd->min.la); free(nd->min.c);
+    free(nd);
+}
+
+int64_t orc_node_pass_sum(orc_stat_node *nd, int64_t t) { return ba_sum(&nd->sec, t, ORC_M_PASS); }
+int64_t orc_node_block_sum(orc_stat_node *nd, int64_t t) { return ba_sum(&nd->sec, t, ORC_M_BLOCK); }
+int64_t orc_node_total_pass(orc_stat_node *nd, int64_t t) { return ba_sum(&nd->min, t, ORC_M_PASS); }
+
+double orc_node_pass_qps(orc_stat_node *nd, int64_t t) {          /* SN:200-202 */
+    return (double)orc_node_pass_sum(nd, t) / nd->sec.la.interval_sec;
+}
+
+void orc_node_add_pass_request(orc_stat_node *nd, int64_t t, int count) {   /* SN:246-249 */
+    ba_add(&nd->sec, t, ORC_M_PASS, count);
+    ba_add(&nd->min, t, ORC_M_PASS, count);
+}
+
+void orc_node_increase_block_qps(orc_stat_node *nd, int64_t t, int count) { /* SN:261-264 */
+    ba_add(&nd->sec, t, ORC_M_BLOCK, count);
+    ba_add(&nd->min, t, ORC_M_BLOCK, count);
+}
+
+/* DC:49-76 (non-prioritized): curCount + acquireCount > count  -> block. int + int wraps. */
+int orc_default_controller_can_pass(orc_stat_node *nd, double count, int grade, int acquire,
+                                    int32_t cur_thread_num, int64_t t) {
+    int32_t cur = grade == 0 ? cur_thread_num : orc_java_d2i(orc_node_pass_qps(nd, t));
+    int32_t sum = (int32_t)((uint32_t)cur + (uint32_t)acquire);
+    return !((double)sum > count);
+}
+
+int orc_default_controller_check(double node_value, double count, int grade, int acquire) {
+    int32_t cur = grade == 0 ? (int32_t)node_value : orc_java_d2i(node_value);
+    int32_t sum = (int32_t)((uint32_t)cur + (uint32_t)acquire);
+    return !((double)sum > count);
+}
+
+void orc_local_replay(orc_stat_node *nd, double count, int64_t n, const int32_t *acquire,
+                      const int64_t *ts, uint8_t *out_pass) {
+    for (int64_t i = 0; i < n; i++) {
+        int ok = orc_default_controller_can_pass(nd, count, 1, acquire[i], 0, ts[i]);
+        if (ok) orc_node_add_pass_request(nd, ts[i], acquire[i]);     /* StatisticSlot.java:64-70 */
+        else orc_node_increase_block_qps(nd, ts[i], acquire[i]);      /* StatisticSlot.java:96-104 */
+        out_pass[i] = (uint8_t)ok;
+    }
+}
+
+/* ------------------------------------------------------------------ local param token bucket */
+/* PFC:127-202 passDefaultLocalCheck, single-threaded (every CAS succeeds). The two CacheMaps are
+ * ParameterMetric's ruleTokenCounter / ruleTimeCounter (ParameterMetric.java:95-118); LRU
+ * eviction is not restated (exact parity only below the capacity). */
+struct orc_param_bucket {
+    kvmap time_ctr;
+    kvmap token_ctr;
+};
+
+orc_param_bucket *orc_pbucket_new(void) {
+    orc_param_bucket *b = (orc_param_bucket *)calloc(1, sizeof(*b));
+    kv_init(&b->time_ctr);
+    kv_init(&b->token_ctr);
+    return b;
+}
+
+void orc_pbucket_free(orc_param_bucket *b) {
+    if (!b) return;
+    kv_free(&b->time_ctr);
+    kv_free(&b->token_ctr);
+    free(b);
+}
+
+int orc_pbucket_pass_default(orc_param_bucket *b, uint64_t key, int64_t token_count, int64_t burst,
+                             int64_t duration_sec, int acquire, int64_t t) {
+    if (token_count == 0) return 0;                                   /* PFC:143-145 */
+    int64_t max_count = wrap_add64(token_count, burst);               /* PFC:147 */
+    if ((int64_t)acquire > max_count) return 0;                       /* PFC:148-150 */
+    int64_t *last = kv_find(&b->time_ctr, key);
+    if (!last) {                                                      /* PFC:155-160 */
+        kv_insert(&b->time_ctr, key, t);
+        if (!kv_find(&b->token_ctr, key)) kv_insert(&b->token_ctr, key, max_count - acquire);
+        return 1;
+    }
+    int64_t pass_time = t - *last;                                    /* PFC:163 */
+    int64_t dur_ms = wrap_mul64(duration_sec, 1000);
+    if (pass_time > dur_ms) {                                         /* PFC:165 */
+        int64_t *old = kv_find(&b->token_ctr, key);
+        if (!old) {
+            kv_insert(&b->token_ctr, key, max_count - acquire);
+            *kv_find(&b->time_ctr, key) = t;
+            return 1;
+        }
+        int64_t rest = *old;
+        int64_t to_add = wrap_mul64(pass_time, token_count) / dur_ms;  /* long arithmetic, wraps */
+        int64_t new_qps = wrap_add64(to_add, rest) > max_count ? (max_count - acquire)
+                                                               : wrap_add64(rest, to_add) - acquire;
+        if (new_qps < 0) return 0;
+        *old = new_qps;
+        *kv_find(&b->time_ctr, key) = t;
+        return 1;
+    }
+    int64_t *old = kv_find(&b->token_ctr, key);                       /* PFC:186-198 */
+    if (old) {
+        if (*old - acquire >= 0) { *old -= acquire; return 1; }
+        return 0;
+    }
+    return -1;   /* time counter present, token counter absent: only after LRU eviction (unpinned) */
+}

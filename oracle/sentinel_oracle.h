@@ -1,0 +1,181 @@
+/*
+ * sentinel_oracle.h -- CPU restatement of Sentinel's sliding-window token-decision path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity checker (and the "port" CPU baseline in
+ * bench.py).  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * it.  The product path (sentinel_amd/, libsentinel_amd.so) never links or calls it.
+ *
+ * Restated from the reference Java (paths relative to /root/reference), with an injected
+ * clock: every call takes the event timestamp `t` that TimeUtil.currentTimeMillis() would
+ * have returned (sentinel-core/.../util/TimeUtil.java:49-51).
+ *
+ * Pinned by the reference's own known-answer tests, transcribed under tests/golden/kat_*.json
+ * (see tests/test_oracle_kat.py and DESIGN.md "Oracle").
+ */
+#ifndef SENTINEL_ORACLE_H
+#define SENTINEL_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ClusterFlowEvent ordinals (srv/flow/statistic/data/ClusterFlowEvent.java:22-52). */
+enum {
+    ORC_PASS = 0, ORC_BLOCK = 1, ORC_PASS_REQUEST = 2, ORC_BLOCK_REQUEST = 3,
+    ORC_OCCUPIED_PASS = 4, ORC_OCCUPIED_BLOCK = 5, ORC_WAITING = 6, ORC_NEVENTS = 7
+};
+
+/* MetricEvent ordinals (core/slots/statistic/MetricEvent.java:21-39). */
+enum {
+    ORC_M_PASS = 0, ORC_M_BLOCK = 1, ORC_M_EXCEPTION = 2, ORC_M_SUCCESS = 3,
+    ORC_M_RT = 4, ORC_M_OCCUPIED_PASS = 5, ORC_M_NEVENTS = 6
+};
+
+/* ---------------- ClusterMetric (srv/flow/statistic/metric/ClusterMetric.java) ---------------- */
+typedef struct orc_cluster_metric orc_cluster_metric;
+orc_cluster_metric *orc_cm_new(int sample_count, int interval_ms);
+void    orc_cm_free(orc_cluster_metric *m);
+void    orc_cm_add(orc_cluster_metric *m, int64_t t, int event, int64_t count);
+int64_t orc_cm_get_current_count(orc_cluster_metric *m, int64_t t, int event);   /* CM:43-45 */
+int64_t orc_cm_get_sum(orc_cluster_metric *m, int64_t t, int event);
+double  orc_cm_get_avg(orc_cluster_metric *m, int64_t t, int event);
+int     orc_cm_try_occupy_next(orc_cluster_metric *m, int64_t t, int event, int acquire, double threshold);
+/* out: sample_count * (1 start + 7 counters) then occupy[7] then has_occupied (1). start=-1 => slot absent */
+void    orc_cm_dump(const orc_cluster_metric *m, int64_t *out);
+/* LA:330-343 list(validTime).size() -- no roll. */
+int     orc_cm_list_count(const orc_cluster_metric *m, int64_t t);
+/* CMLA:181-190 getFirstCountOfWindow(event) at time t (LA:399-409 getValidHead). */
+int64_t orc_cm_first_count(orc_cluster_metric *m, int64_t t, int event);
+/* Current-window start for t after the roll (LA:149-248), -1 for t<0. */
+int64_t orc_cm_window_start(orc_cluster_metric *m, int64_t t);
+
+/* ---------------- RequestLimiter (srv/flow/statistic/limit/RequestLimiter.java) ---------------- */
+typedef struct orc_limiter orc_limiter;
+orc_limiter *orc_limiter_new(double qps_allowed);
+void    orc_limiter_free(orc_limiter *l);
+void    orc_limiter_add(orc_limiter *l, int64_t t, int x);
+int64_t orc_limiter_get_sum(orc_limiter *l, int64_t t);
+double  orc_limiter_get_qps(orc_limiter *l, int64_t t);
+int     orc_limiter_can_pass(orc_limiter *l, int64_t t);
+int     orc_limiter_try_pass(orc_limiter *l, int64_t t);
+
+/* ---------------- ClusterParamMetric (srv/flow/statistic/metric/ClusterParamMetric.java) ------- */
+typedef struct orc_param_metric orc_param_metric;
+orc_param_metric *orc_pm_new(int sample_count, int interval_ms, int max_capacity);
+void    orc_pm_free(orc_param_metric *m);
+void    orc_pm_add_value(orc_param_metric *m, int64_t t, uint64_t key, int count);
+int64_t orc_pm_get_sum(orc_param_metric *m, int64_t t, uint64_t key);
+double  orc_pm_get_avg(orc_param_metric *m, int64_t t, uint64_t key);
+/* top-k as in getTopValues: returns k' <= k entries (keys, avg). */
+int     orc_pm_top_values(orc_param_metric *m, int64_t t, int number, uint64_t *keys, double *avgs);
+int     orc_pm_overflowed(const orc_param_metric *m);   /* 1 if any bucket exceeded max_capacity */
+
+/* ---------------- Rule tables & the token service (DefaultTokenService) ---------------- */
+/* Mirrors include/sentinel_amd.h's sentinel_flow_rule_t field-for-field. */
+typedef struct {
+    int64_t flow_id;            /* ClusterFlowConfig.flowId */
+    double  count;              /* FlowRule.count */
+    int32_t threshold_type;     /* ClusterRuleConstant: 0 AVG_LOCAL, 1 GLOBAL */
+    int32_t sample_count;       /* ClusterFlowConfig.sampleCount (default 10) */
+    int32_t window_interval_ms; /* ClusterFlowConfig.windowIntervalMs (default 1000) */
+    int32_t namespace_idx;      /* index into the namespace table, -1 = no namespace */
+    int32_t checker;            /* 0 = ClusterFlowChecker (TokenService), 1 = SimpleClusterFlowChecker (RLS) */
+    int32_t reserved;
+} orc_flow_rule;
+
+typedef struct {
+    int32_t connected_count;    /* ConnectionManager.getConnectedCount(namespace) */
+    int32_t has_limiter;        /* GlobalRequestLimiter.initIfAbsent(namespace) was called */
+    double  max_allowed_qps;    /* ServerFlowConfig.maxAllowedQps (default 30000) */
+} orc_namespace;
+
+typedef struct {
+    double exceed_count;        /* ServerFlowConfig.exceedCount (default 1.0) */
+    double max_occupy_ratio;    /* ServerFlowConfig.maxOccupyRatio (default 1.0) */
+} orc_server_config;
+
+typedef struct orc_engine orc_engine;
+orc_engine *orc_engine_new(const orc_server_config *cfg, const orc_namespace *ns, int n_ns);
+void orc_engine_free(orc_engine *e);
+int  orc_engine_load_flow_rules(orc_engine *e, const orc_flow_rule *rules, int n);
+
+/* Token-result status codes (core/cluster/TokenResultStatus.java:27-69). */
+enum {
+    ORC_BAD_REQUEST = -4, ORC_TOO_MANY_REQUEST = -2, ORC_FAIL = -1, ORC_OK = 0,
+    ORC_BLOCKED = 1, ORC_SHOULD_WAIT = 2, ORC_NO_RULE_EXISTS = 3
+};
+
+/* flow_idx: index into the loaded rule table; -1 => unknown rule (NO_RULE_EXISTS),
+ * -2 => invalid id (null or <= 0: BAD_REQUEST).  flags bit0 = prioritized. */
+void orc_request_token(orc_engine *e, int32_t flow_idx, int32_t acquire, int prioritized, int64_t t,
+                       int8_t *status, int32_t *remaining, int32_t *wait_ms);
+/* Sequential replay of a batch in arrival (seq) order. flags may be NULL; wait_ms may be NULL. */
+void orc_flow_replay(orc_engine *e, int64_t n, const int32_t *flow_idx, const int32_t *acquire,
+                     const uint8_t *flags, const int64_t *ts,
+                     int8_t *status, int32_t *remaining, int32_t *wait_ms);
+/* Dump flow metric state, orc_cm_dump format. Returns words written or -1. */
+int  orc_engine_dump_flow(const orc_engine *e, int32_t flow_idx, int64_t *out);
+int64_t orc_engine_limiter_sum(orc_engine *e, int32_t ns, int64_t t);
+
+/* ---- cluster hot-parameter path (ClusterParamFlowChecker) ---- */
+typedef struct {
+    int64_t flow_id;
+    double  count;              /* ParamFlowRule.count */
+    int32_t threshold_type;
+    int32_t sample_count;
+    int32_t window_interval_ms;
+    int32_t namespace_idx;
+    int32_t hot_begin;          /* [hot_begin, hot_begin+hot_n) into the hot-item arrays */
+    int32_t hot_n;
+} orc_param_rule;
+
+int  orc_engine_load_param_rules(orc_engine *e, const orc_param_rule *rules, int n,
+                                 const uint64_t *hot_keys, const int32_t *hot_counts, int n_hot);
+/* One requestParamToken call: values[0..n_values). */
+void orc_request_param_token(orc_engine *e, int32_t rule_idx, int32_t acquire, int64_t t,
+                             const uint64_t *values, int n_values, int8_t *status, int32_t *remaining);
+/* Batch of single-value requests in seq order. */
+void orc_param_replay(orc_engine *e, int64_t n, const int32_t *rule_idx, const int32_t *acquire,
+                      const uint64_t *param_key, const int64_t *ts, int8_t *status, int32_t *remaining);
+int64_t orc_engine_param_sum(orc_engine *e, int32_t rule_idx, int64_t t, uint64_t key);
+int  orc_engine_param_overflowed(const orc_engine *e);
+
+/* ---------------- Local path: StatisticNode + DefaultController (config 1) ---------------- */
+typedef struct orc_stat_node orc_stat_node;
+orc_stat_node *orc_node_new(int sample_count, int interval_ms);
+void   orc_node_free(orc_stat_node *nd);
+double orc_node_pass_qps(orc_stat_node *nd, int64_t t);
+int64_t orc_node_pass_sum(orc_stat_node *nd, int64_t t);       /* rollingCounterInSecond.pass() */
+int64_t orc_node_block_sum(orc_stat_node *nd, int64_t t);
+int64_t orc_node_total_pass(orc_stat_node *nd, int64_t t);     /* rollingCounterInMinute.pass() */
+void   orc_node_add_pass_request(orc_stat_node *nd, int64_t t, int count);
+void   orc_node_increase_block_qps(orc_stat_node *nd, int64_t t, int count);
+/* DefaultController.canPass(node, acquire) for QPS grade (grade=1) or THREAD grade (0). */
+int    orc_default_controller_can_pass(orc_stat_node *nd, double count, int grade, int acquire,
+                                       int32_t cur_thread_num, int64_t t);
+/* FlowQpsDemo-style replay: for each entry check DefaultController(QPS) then book pass/block
+ * like StatisticSlot (core/slots/statistic/StatisticSlot.java:55-116). out_pass[i] = 1/0. */
+/* DC:49-76 with a mocked Node value (DefaultControllerTest): cur = passQps or curThreadNum. */
+int    orc_default_controller_check(double node_value, double count, int grade, int acquire);
+void   orc_local_replay(orc_stat_node *nd, double count, int64_t n, const int32_t *acquire,
+                        const int64_t *ts, uint8_t *out_pass);
+
+/* ---------------- Local param token bucket (ParamFlowChecker.passDefaultLocalCheck) ----------- */
+typedef struct orc_param_bucket orc_param_bucket;
+orc_param_bucket *orc_pbucket_new(void);
+void orc_pbucket_free(orc_param_bucket *b);
+/* token_count = hot-item count or (long)rule.count; returns 1 pass / 0 block. */
+int  orc_pbucket_pass_default(orc_param_bucket *b, uint64_t key, int64_t token_count, int64_t burst,
+                              int64_t duration_sec, int acquire, int64_t t);
+
+/* ---------------- Java numerics ---------------- */
+int32_t orc_java_d2i(double d);
+int64_t orc_java_d2l(double d);
+int32_t orc_java_string_hash(const uint16_t *utf16, int64_t n);   /* String.hashCode */
+
+#ifdef __cplusplus
+}
+#endif
+#endif
