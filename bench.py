@@ -1,0 +1,238 @@
+"""bench.py -- token decisions/sec of the MI355X engine on BASELINE config 3.
+
+Workload (BASELINE.json configs[2], the config the headline metric is quoted on): a universe of
+1M flowIds (cluster FlowRules, GLOBAL threshold count ~ U{10..1000}, default cluster window
+sampleCount=10 / windowIntervalMs=1000 -> 10 x 100 ms buckets), hash-sharded over the ranks by
+splitmix64(flowId) mod N.  Every rank decides a fixed 8M-event batch per step over its own flows
+(uniform, acquire 1, monotone timestamps at 2x the shard's summed thresholds): weak scaling, no
+collective on the decision path.  A step = one batch through DefaultTokenService.requestToken
+semantics (validation, window roll, ClusterFlowChecker admission, verdict write-back), inputs
+already resident in HBM.
+
+Prints ONE JSON line (rank 0).  Extra fields: p99 device batch latency, per-kernel profile,
+the roofline of the dominant kernel, and the CPU oracle ("port") timed on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+# Algorithmic bytes per processed event for each kernel of the pipeline (DESIGN.md "Kernels").
+KERNEL_BYTES_PER_EVENT = {
+    "flow_prep": 20.0,        # read flow_idx 4 + acquire 4 + ts 8, write key 4
+    "radix_hist": 4.0,        # read key
+    "radix_scatter": 16.0,    # read key+seq, write key+seq (first pass reads key only: 12)
+    "scan_tiles": 8.0,
+    "scan_add": 8.0,
+    "count_valid": 4.0,
+    "gather_sorted": 33.0,    # read skey+sseq 8, gather ts 8 + acquire 4 + flags 1, write epoch 8 + acq 4 + fl 1
+    "heads": 16.0,            # read skey 4 + epoch 8, write head 4
+    "seg_start": 4.0,
+    "seg_het": 13.0,
+    "verdict": 25.0,          # read segid 4 + sseq 4 + skey 4 + acq 4 + segment record ~8, write status 1 + remaining 4
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--events-per-gpu", type=int, default=8 * 1024 * 1024)
+    ap.add_argument("--flows", type=int, default=1_000_000)
+    ap.add_argument("--sample-count", type=int, default=10)
+    ap.add_argument("--interval-ms", type=int, default=1000)
+    ap.add_argument("--cpu-sample-events", type=int, default=4 * 1024 * 1024)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    import sentinel_amd as sa
+    from sentinel_amd import trace as T
+
+    # ---- rule universe (identical on every rank), then this rank's shard
+    rng = np.random.default_rng(3)
+    rules = T.make_rules(args.flows, rng, sample_count=args.sample_count, window_interval_ms=args.interval_ms)
+    mine = np.nonzero(T.shard_of(rules.flow_id, world) == rank)[0] if world > 1 else np.arange(len(rules))
+    shard = rules.subset(mine)
+    F = len(shard)
+
+    svc = sa.GpuTokenService(local)
+    svc.load_rules_array(shard.flow_id, shard.count, shard.threshold_type, shard.sample_count,
+                         shard.window_interval_ms, shard.namespace, shard.checker)
+
+    N = args.events_per_gpu
+    steps_total = args.warmup + args.steps
+    rate = 2.0 * float(shard.count.sum())          # offered rate: 2x the shard's thresholds (per second)
+    ms_per_event = 1000.0 / rate
+    t0 = T.T0_ALIGNED
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    idx_b, ts_b = [], []
+    for s in range(steps_total):
+        idx_b.append(torch.randint(0, F, (N,), dtype=torch.int32, device=dev, generator=gen))
+        base = torch.arange(s * N, (s + 1) * N, device=dev, dtype=torch.float64)
+        ts_b.append((t0 + torch.floor(base * ms_per_event)).to(torch.int64))
+    acq = torch.ones(N, dtype=torch.int32, device=dev)
+    status = torch.empty(N, dtype=torch.int8, device=dev)
+    remaining = torch.empty(N, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    ext = torch.cuda.ExternalStream(svc.stream, device=dev)
+    for s in range(args.warmup):
+        svc.submit_flow_batch(idx_b[s], acq, ts_b[s], status=status, remaining=remaining)
+    svc.synchronize()
+
+    if not args.no_profile:
+        svc._L.sentinel_profile_enable(svc.handle, 1)
+    ev_a = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ev_b = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        s = args.warmup + k
+        ev_a[k].record(ext)
+        svc.submit_flow_batch(idx_b[s], acq, ts_b[s], status=status, remaining=remaining)
+        ev_b[k].record(ext)
+    svc.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    lat = sorted(ev_a[k].elapsed_time(ev_b[k]) for k in range(args.steps))
+    p99 = lat[min(len(lat) - 1, int(np.ceil(0.99 * len(lat))) - 1)]
+
+    # ---- per-kernel profile (HIP events on the engine stream, over the timed region)
+    prof = {}
+    if not args.no_profile:
+        import ctypes as C
+        mx = 64
+        names = C.create_string_buffer(32 * mx)
+        tot = (C.c_double * mx)()
+        calls = (C.c_int64 * mx)()
+        units = (C.c_int64 * mx)()
+        k = svc._L.sentinel_profile_read(svc.handle, mx, names, tot, calls, units)
+        for i in range(k):
+            nm = names.raw[32 * i:32 * i + 32].split(b"\0")[0].decode()
+            prof[nm] = dict(total_ms=tot[i], calls=calls[i], avg_us=1000.0 * tot[i] / max(calls[i], 1),
+                            units_per_call=units[i] / max(calls[i], 1))
+        svc._L.sentinel_profile_enable(svc.handle, 0)
+
+    # ---- snapshot + RCCL all-gather (config 3's ClusterMetric snapshot; off the decision path)
+    t_snap = int(ts_b[-1][-1].item()) + 1
+    snap = torch.empty((F, 3), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    ts0 = time.perf_counter()
+    svc.snapshot_device(t_snap, snap)
+    svc.synchronize()
+    if world > 1:
+        maxf = torch.tensor([F], device=dev)
+        dist.all_reduce(maxf, op=dist.ReduceOp.MAX)
+        pad = torch.zeros((int(maxf.item()), 3), dtype=torch.int64, device=dev)
+        pad[:F] = snap
+        gathered = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(gathered, pad)
+        torch.cuda.synchronize()
+    snap_ms = (time.perf_counter() - ts0) * 1000.0
+
+    total_events = float(N) * args.steps * world
+    value = total_events / elapsed
+
+    # ---- roofline of the dominant kernel
+    roof = None
+    if prof:
+        dom = max(prof, key=lambda k: prof[k]["total_ms"])
+        d = prof[dom]
+        bpe = KERNEL_BYTES_PER_EVENT.get(dom)
+        if dom == "process":
+            # per touched flow: read n epochs + n PASS, write epoch + 4 counters; per event: segment record
+            e_f = N / max(1, F)
+            bpe = (args.sample_count * 16 + 40 + 24) / max(1.0, min(e_f, 1e9)) if F else 0.0
+        if dom == "radix_scatter":
+            bpe = 16.0
+        ach = (bpe or 0.0) * d["units_per_call"] / (d["avg_us"] * 1e-6) / 1e9
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "bytes_per_event": bpe, "avg_us": round(d["avg_us"], 2)}
+
+    # ---- CPU baseline: the oracle ("port") on a bounded sample of the same workload, rank 0, N=1
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+        m = min(args.cpu_sample_events, N)
+        orc = O.TokenServiceOracle.from_arrays(shard.flow_id, shard.count, shard.threshold_type, shard.sample_count,
+                                               shard.window_interval_ms, shard.namespace, shard.checker)
+        idx_c = idx_b[0][:m].cpu().numpy()
+        ts_c = ts_b[0][:m].cpu().numpy()
+        acq_c = np.ones(m, np.int32)
+        c0 = time.perf_counter()
+        orc.replay(idx_c, acq_c, ts_c)
+        cdt = time.perf_counter() - c0
+        cpu = {"value": round(m / cdt, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
+               "sample": f"{m} events of step 0 of this workload (same rules, same trace), sequential oracle replay, "
+                         f"{cdt:.1f} s"}
+
+    pipeline_bytes = 21.0 + (args.sample_count * 64 + 64 + 16) / max(1.0, N / max(1, F))
+    out = {
+        "metric": "token decisions/sec (whole node) at 1M flowIds; p99 batch latency",
+        "value": round(value, 1),
+        "unit": "decisions/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1000.0 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64+f64",
+        "data": "synthetic (seeded uniform events over the shard's flows; random-init rule table)",
+        "config": {"workload": "config3: 1M flowIds hash-sharded (splitmix64 mod N), cluster GLOBAL rules "
+                               "count~U{10..1000}, n=10 w=100ms, uniform flows, acquire=1, 2x offered load",
+                   "flows_total": args.flows, "flows_this_rank": F, "events_per_gpu_per_step": N,
+                   "parallelism": f"flowid-shard x{world}"},
+        "p99_batch_ms": round(p99, 4),
+        "median_batch_ms": round(lat[len(lat) // 2], 4),
+        "snapshot_allgather_ms": round(snap_ms, 3),
+        "pipeline_bytes_per_decision": round(pipeline_bytes, 2),
+        "pipeline_hbm_frac": round(value / world * pipeline_bytes / (HBM_PEAK_GBS * 1e9), 4),
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "kernels": {k: {"avg_us": round(v["avg_us"], 2), "calls": v["calls"]} for k, v in prof.items()},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

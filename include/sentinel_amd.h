@@ -1,0 +1,196 @@
+/*
+ * sentinel_amd.h -- C ABI of the MI355X batched token-decision engine (libsentinel_amd.so).
+ *
+ * This is the drop-in boundary for Sentinel's cluster token server.  Every entry point below
+ * replaces one reference interface (paths relative to the reference repo root):
+ *
+ *   TokenService.requestToken        sentinel-core/src/main/java/com/alibaba/csp/sentinel/cluster/TokenService.java:36
+ *   TokenService.requestParamToken   sentinel-core/src/main/java/com/alibaba/csp/sentinel/cluster/TokenService.java:46
+ *   DefaultTokenService              sentinel-cluster/sentinel-cluster-server-default/src/main/java/com/alibaba/csp/sentinel/cluster/flow/DefaultTokenService.java:37-62
+ *   ClusterFlowRuleManager (load)    .../cluster/flow/rule/ClusterFlowRuleManager.java:325-372
+ *   ClusterParamFlowRuleManager      .../cluster/flow/rule/ClusterParamFlowRuleManager.java:318-360
+ *   ClusterServerConfigManager       .../cluster/server/config/ClusterServerConfigManager.java:218-258 (namespace set, limiter)
+ *   ServerFlowConfig                 .../cluster/server/config/ServerFlowConfig.java:26-40
+ *   ConnectionManager.getConnectedCount .../cluster/server/connection/ConnectionManager.java:47-51
+ *   ClusterMetricNodeGenerator       .../cluster/flow/statistic/ClusterMetricNodeGenerator.java:70-86 (snapshot)
+ *   SimpleClusterFlowChecker (RLS)   sentinel-cluster/sentinel-cluster-server-envoy-rls/.../rls/flow/SimpleClusterFlowChecker.java:33-65
+ *
+ * Conventions: plain C types only; every call returns 0 on success or a negative
+ * SENTINEL_E_* code (message via sentinel_last_error()).  An engine that cannot run (no GPU,
+ * device fault) answers every event with status FAIL (-1) and returns SENTINEL_E_DEVICE, so the
+ * reference clients' fallbackToLocalWhenFail path (FlowRuleChecker.java:166-209) still works.
+ * Time is explicit: every event carries the millisecond timestamp the reference would have read
+ * from TimeUtil.currentTimeMillis() (sentinel-core/.../util/TimeUtil.java:49-51).
+ */
+#ifndef SENTINEL_AMD_H
+#define SENTINEL_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* TokenResultStatus (sentinel-core/.../cluster/TokenResultStatus.java:27-69) */
+#define SENTINEL_STATUS_BAD_REQUEST       (-4)
+#define SENTINEL_STATUS_TOO_MANY_REQUEST  (-2)
+#define SENTINEL_STATUS_FAIL              (-1)
+#define SENTINEL_STATUS_OK                (0)
+#define SENTINEL_STATUS_BLOCKED           (1)
+#define SENTINEL_STATUS_SHOULD_WAIT       (2)
+#define SENTINEL_STATUS_NO_RULE_EXISTS    (3)
+
+/* Special flow/rule indices in an event (the host maps flowId -> dense index). */
+#define SENTINEL_IDX_NO_RULE   (-1)   /* flowId not loaded   -> NO_RULE_EXISTS */
+#define SENTINEL_IDX_BAD_ID    (-2)   /* flowId null or <= 0 -> BAD_REQUEST    */
+
+/* ClusterRuleConstant (sentinel-core/.../slots/block/ClusterRuleConstant.java:27-28) */
+#define SENTINEL_THRESHOLD_AVG_LOCAL  0
+#define SENTINEL_THRESHOLD_GLOBAL     1
+
+/* Which reference checker decides a flow. */
+#define SENTINEL_CHECKER_CLUSTER  0   /* ClusterFlowChecker via DefaultTokenService */
+#define SENTINEL_CHECKER_SIMPLE   1   /* SimpleClusterFlowChecker (Envoy RLS)       */
+
+/* Event flags */
+#define SENTINEL_FLAG_PRIORITIZED  1u /* requestToken(..., prioritized=true) */
+
+/* Error codes */
+#define SENTINEL_OK            0
+#define SENTINEL_E_INVALID    (-1)
+#define SENTINEL_E_DEVICE     (-2)
+#define SENTINEL_E_NOMEM      (-3)
+#define SENTINEL_E_STATE      (-4)
+
+/* Number of ClusterFlowEvent counters per bucket (ClusterFlowEvent.java:22-52):
+ * PASS, BLOCK, PASS_REQUEST, BLOCK_REQUEST, OCCUPIED_PASS, OCCUPIED_BLOCK, WAITING */
+#define SENTINEL_NEVENTS 7
+
+typedef struct sentinel_engine sentinel_engine_t;
+
+/* ServerFlowConfig (ServerFlowConfig.java:26-40). Defaults: 1.0, 1.0. */
+typedef struct {
+    double exceed_count;
+    double max_occupy_ratio;
+} sentinel_server_config_t;
+
+/* One namespace of the server namespace set. */
+typedef struct {
+    int32_t connected_count;   /* ConnectionManager.getConnectedCount(namespace) */
+    int32_t has_limiter;       /* GlobalRequestLimiter.initIfAbsent(namespace) was called */
+    double  max_allowed_qps;   /* RequestLimiter qpsAllowed (ServerFlowConfig.maxAllowedQps, default 30000) */
+} sentinel_namespace_t;
+
+/* A cluster FlowRule as loaded by ClusterFlowRuleManager.applyClusterFlowRule. */
+typedef struct {
+    int64_t flow_id;             /* ClusterFlowConfig.flowId (> 0) */
+    double  count;               /* FlowRule.count (>= 0) */
+    int32_t threshold_type;      /* SENTINEL_THRESHOLD_* (ClusterFlowConfig.thresholdType) */
+    int32_t sample_count;        /* ClusterFlowConfig.sampleCount (default 10) */
+    int32_t window_interval_ms;  /* ClusterFlowConfig.windowIntervalMs (default 1000) */
+    int32_t namespace_idx;       /* index into the namespace table; -1 = no namespace */
+    int32_t checker;             /* SENTINEL_CHECKER_* */
+    int32_t reserved;
+} sentinel_flow_rule_t;
+
+/* A cluster ParamFlowRule (ClusterParamFlowRuleManager.java:318-360).  Hot items are passed as
+ * parallel arrays; [hot_begin, hot_begin + hot_n) indexes them. */
+typedef struct {
+    int64_t flow_id;
+    double  count;               /* ParamFlowRule.count */
+    int32_t threshold_type;
+    int32_t sample_count;
+    int32_t window_interval_ms;
+    int32_t namespace_idx;
+    int32_t hot_begin;
+    int32_t hot_n;
+} sentinel_param_rule_t;
+
+/* TokenResult (sentinel-core/.../cluster/TokenResult.java:26-98), the per-call result. */
+typedef struct {
+    int32_t status;
+    int32_t remaining;
+    int32_t wait_in_ms;
+    int32_t reserved;
+} sentinel_token_result_t;
+
+/* ClusterMetricNode subset produced by the snapshot (ClusterMetricNodeGenerator.java:70-86). */
+typedef struct {
+    int64_t flow_id;
+    double  pass_qps;
+    double  block_qps;
+} sentinel_flow_snapshot_t;
+
+/* ---- lifecycle ---- */
+int  sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sentinel_engine_t **out);
+int  sentinel_engine_destroy(sentinel_engine_t *eng);
+const char *sentinel_last_error(void);
+int  sentinel_device_count(void);
+
+/* ---- rules & config (host-side tables, uploaded to HBM) ---- */
+int  sentinel_set_server_config(sentinel_engine_t *eng, const sentinel_server_config_t *cfg);
+int  sentinel_set_namespaces(sentinel_engine_t *eng, const sentinel_namespace_t *ns, int32_t n);
+int  sentinel_set_connected_count(sentinel_engine_t *eng, int32_t namespace_idx, int32_t connected);
+/* Loads the flow rule table.  Invalid rules (FlowRuleUtil.isValidRule: flowId <= 0, count < 0,
+ * bad window config) are dropped exactly like ClusterFlowRuleManager does; their index maps to
+ * SENTINEL_IDX_NO_RULE.  Metrics of flowIds present before and after the load are kept
+ * (ClusterMetricStatistics.putMetricIfAbsent); new flowIds start empty. */
+int  sentinel_load_flow_rules(sentinel_engine_t *eng, const sentinel_flow_rule_t *rules, int32_t n);
+int  sentinel_load_param_rules(sentinel_engine_t *eng, const sentinel_param_rule_t *rules, int32_t n,
+                               const uint64_t *hot_keys, const int32_t *hot_counts, int32_t n_hot);
+int32_t sentinel_flow_count(sentinel_engine_t *eng);
+/* flowId -> dense index (or SENTINEL_IDX_NO_RULE / SENTINEL_IDX_BAD_ID), host side. */
+int  sentinel_lookup_flow_idx(sentinel_engine_t *eng, int64_t n, const int64_t *flow_ids, int32_t *idx_out);
+int  sentinel_lookup_param_idx(sentinel_engine_t *eng, int64_t n, const int64_t *flow_ids, int32_t *idx_out);
+
+/* ---- the batched hot path: DefaultTokenService.requestToken over a batch ----
+ * Events in arrival (seq) order; pointers are DEVICE pointers; `stream` is a hipStream_t (NULL =
+ * the engine's stream).  Verdicts equal a sequential replay of the batch through the reference
+ * checker with the given timestamps.  flags and wait_ms may be NULL. Asynchronous. */
+int  sentinel_submit_flow_batch(sentinel_engine_t *eng, int64_t n, const int32_t *flow_idx,
+                                const int32_t *acquire, const uint8_t *flags, const int64_t *ts,
+                                int8_t *status, int32_t *remaining, int32_t *wait_ms, void *stream);
+/* Same with HOST pointers (pinned or pageable): H2D, decide, D2H, synchronous. */
+int  sentinel_submit_flow_batch_host(sentinel_engine_t *eng, int64_t n, const int32_t *flow_idx,
+                                     const int32_t *acquire, const uint8_t *flags, const int64_t *ts,
+                                     int8_t *status, int32_t *remaining, int32_t *wait_ms);
+/* Single-value DefaultTokenService.requestParamToken over a batch (DEVICE pointers). */
+int  sentinel_submit_param_batch(sentinel_engine_t *eng, int64_t n, const int32_t *rule_idx,
+                                 const int32_t *acquire, const uint64_t *param_key, const int64_t *ts,
+                                 int8_t *status, int32_t *remaining, void *stream);
+int  sentinel_submit_param_batch_host(sentinel_engine_t *eng, int64_t n, const int32_t *rule_idx,
+                                      const int32_t *acquire, const uint64_t *param_key, const int64_t *ts,
+                                      int8_t *status, int32_t *remaining);
+
+/* ---- per-call TokenService mirror (one event, synchronous) ---- */
+int  sentinel_request_token(sentinel_engine_t *eng, int64_t flow_id, int32_t acquire_count,
+                            int32_t prioritized, int64_t ts, sentinel_token_result_t *out);
+int  sentinel_request_param_token(sentinel_engine_t *eng, int64_t flow_id, int32_t acquire_count,
+                                  uint64_t param_key, int64_t ts, sentinel_token_result_t *out);
+
+/* ---- observability / parity ---- */
+int  sentinel_synchronize(sentinel_engine_t *eng);
+/* Flow metric dump: sample_count x {window start ms (-1 = absent), 7 counters}, then 7 occupy
+ * counters, then has_occupied (same layout as the oracle's orc_cm_dump). */
+int  sentinel_dump_flow(sentinel_engine_t *eng, int32_t flow_idx, int64_t *out, int32_t out_len);
+/* Sum of one param value's counters over the valid window at ts (ClusterParamMetric.getSum). */
+int  sentinel_param_sum(sentinel_engine_t *eng, int32_t rule_idx, uint64_t param_key, int64_t ts, int64_t *out);
+/* Snapshot of every loaded flow at ts: getAvg(BLOCK), getAvg(PASS) (each read rolls the window,
+ * as the reference does).  out has sentinel_flow_count() entries (host memory). */
+int  sentinel_snapshot(sentinel_engine_t *eng, int64_t ts, sentinel_flow_snapshot_t *out);
+/* Device-pointer variant (for the RCCL all-gather), asynchronous on `stream`. */
+int  sentinel_snapshot_device(sentinel_engine_t *eng, int64_t ts, sentinel_flow_snapshot_t *d_out, void *stream);
+/* The engine's own stream (hipStream_t). */
+void *sentinel_engine_stream(sentinel_engine_t *eng);
+/* Per-kernel timing with HIP events recorded on the launch stream (for roofline reporting).
+ * enable=1 starts (and clears) the record, 0 stops.  profile_read synchronises, then fills up to
+ * `max` entries: names (32 chars each), total milliseconds, launch count and events processed
+ * (summed over launches); returns the number of entries. */
+int  sentinel_profile_enable(sentinel_engine_t *eng, int enable);
+int  sentinel_profile_read(sentinel_engine_t *eng, int max, char *names32, double *total_ms,
+                           int64_t *calls, int64_t *units);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -271,6 +271,31 @@ class TokenServiceOracle:
         if param_rules is not None:
             self.load_param_rules(param_rules, hot_items or {})
 
+    @classmethod
+    def from_arrays(cls, flow_id, count, threshold_type, sample_count, window_interval_ms, namespace, checker,
+                    namespaces=None, exceed_count=1.0, max_occupy_ratio=1.0):
+        """Vectorised constructor for large rule tables (the FlowRule struct is filled from numpy)."""
+        self = cls.__new__(cls)
+        namespaces = namespaces if namespaces is not None else [dict(connected_count=0, has_limiter=0, max_allowed_qps=30000.0)]
+        ns = (Namespace * max(len(namespaces), 1))()
+        for i, n in enumerate(namespaces):
+            ns[i] = Namespace(int(n.get("connected_count", 0)), int(n.get("has_limiter", 0)),
+                              float(n.get("max_allowed_qps", 30000.0)))
+        cfg = ServerConfig(exceed_count, max_occupy_ratio)
+        self.h = lib().orc_engine_new(C.byref(cfg), ns, len(namespaces))
+        n = len(flow_id)
+        rec = np.zeros(n, dtype=[("flow_id", "<i8"), ("count", "<f8"), ("threshold_type", "<i4"),
+                                 ("sample_count", "<i4"), ("window_interval_ms", "<i4"),
+                                 ("namespace_idx", "<i4"), ("checker", "<i4"), ("reserved", "<i4")])
+        rec["flow_id"], rec["count"], rec["threshold_type"] = flow_id, count, threshold_type
+        rec["sample_count"], rec["window_interval_ms"] = sample_count, window_interval_ms
+        rec["namespace_idx"], rec["checker"] = namespace, checker
+        self._rec = rec
+        self.rules = None
+        self._sample_count = np.asarray(sample_count)
+        lib().orc_engine_load_flow_rules(self.h, C.c_void_p(rec.ctypes.data), n)
+        return self
+
     def __del__(self):
         if getattr(self, "h", None):
             lib().orc_engine_free(self.h)
@@ -335,7 +360,7 @@ class TokenServiceOracle:
         return bool(lib().orc_engine_param_overflowed(self.h))
 
     def dump_flow(self, idx) -> np.ndarray:
-        n = int(self.rules[idx].get("sample_count", 10))
+        n = int(self.rules[idx].get("sample_count", 10)) if self.rules is not None else int(self._rec["sample_count"][idx])
         out = np.zeros(n * 8 + 8, dtype=np.int64)
         w = lib().orc_engine_dump_flow(self.h, idx, _p(out))
         if w < 0:

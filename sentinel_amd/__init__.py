@@ -1,0 +1,9 @@
+"""sentinel_amd -- MI355X-native batched token-decision engine for Sentinel's sliding-window
+flow-control hot path (LeapArray/ClusterMetric + ClusterFlowChecker/ClusterParamFlowChecker behind
+the TokenService SPI).  See DESIGN.md."""
+from ._lib import SentinelError, load as load_library  # noqa: F401
+from .token_service import (ClusterFlowConfig, ClusterRuleConstant, FlowRule, GpuTokenService,  # noqa: F401
+                            ParamFlowRule, ServerNamespace, TokenResult, TokenResultStatus)
+
+__all__ = ["GpuTokenService", "FlowRule", "ParamFlowRule", "ClusterFlowConfig", "ClusterRuleConstant",
+           "ServerNamespace", "TokenResult", "TokenResultStatus", "SentinelError", "load_library"]

@@ -1,0 +1,133 @@
+"""ctypes binding of libsentinel_amd.so (the C ABI declared in include/sentinel_amd.h).
+
+The product path: there is no CPU fallback.  If the HIP library is missing or cannot load, every
+entry point raises -- it never routes through the oracle.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsentinel_amd.so")
+
+STATUS_BAD_REQUEST = -4
+STATUS_TOO_MANY_REQUEST = -2
+STATUS_FAIL = -1
+STATUS_OK = 0
+STATUS_BLOCKED = 1
+STATUS_SHOULD_WAIT = 2
+STATUS_NO_RULE_EXISTS = 3
+
+IDX_NO_RULE = -1
+IDX_BAD_ID = -2
+
+THRESHOLD_AVG_LOCAL = 0
+THRESHOLD_GLOBAL = 1
+CHECKER_CLUSTER = 0
+CHECKER_SIMPLE = 1
+FLAG_PRIORITIZED = 1
+
+# every symbol include/sentinel_amd.h declares
+EXPORTS = [
+    "sentinel_engine_create", "sentinel_engine_destroy", "sentinel_last_error", "sentinel_device_count",
+    "sentinel_set_server_config", "sentinel_set_namespaces", "sentinel_set_connected_count",
+    "sentinel_load_flow_rules", "sentinel_load_param_rules", "sentinel_flow_count",
+    "sentinel_lookup_flow_idx", "sentinel_lookup_param_idx",
+    "sentinel_submit_flow_batch", "sentinel_submit_flow_batch_host",
+    "sentinel_submit_param_batch", "sentinel_submit_param_batch_host",
+    "sentinel_request_token", "sentinel_request_param_token",
+    "sentinel_synchronize", "sentinel_dump_flow", "sentinel_param_sum",
+    "sentinel_snapshot", "sentinel_snapshot_device", "sentinel_engine_stream",
+    "sentinel_profile_enable", "sentinel_profile_read",
+]
+
+
+class ServerConfig(C.Structure):
+    _fields_ = [("exceed_count", C.c_double), ("max_occupy_ratio", C.c_double)]
+
+
+class Namespace(C.Structure):
+    _fields_ = [("connected_count", C.c_int32), ("has_limiter", C.c_int32), ("max_allowed_qps", C.c_double)]
+
+
+class FlowRuleC(C.Structure):
+    _fields_ = [("flow_id", C.c_int64), ("count", C.c_double), ("threshold_type", C.c_int32),
+                ("sample_count", C.c_int32), ("window_interval_ms", C.c_int32),
+                ("namespace_idx", C.c_int32), ("checker", C.c_int32), ("reserved", C.c_int32)]
+
+
+class ParamRuleC(C.Structure):
+    _fields_ = [("flow_id", C.c_int64), ("count", C.c_double), ("threshold_type", C.c_int32),
+                ("sample_count", C.c_int32), ("window_interval_ms", C.c_int32),
+                ("namespace_idx", C.c_int32), ("hot_begin", C.c_int32), ("hot_n", C.c_int32)]
+
+
+class TokenResultC(C.Structure):
+    _fields_ = [("status", C.c_int32), ("remaining", C.c_int32), ("wait_in_ms", C.c_int32), ("reserved", C.c_int32)]
+
+
+class FlowSnapshotC(C.Structure):
+    _fields_ = [("flow_id", C.c_int64), ("pass_qps", C.c_double), ("block_qps", C.c_double)]
+
+
+class SentinelError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load the HIP engine; raises SentinelError when it is absent (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:   # share one HIP runtime with PyTorch when it is present (both sonames are libamdhip64.so.7)
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise SentinelError(f"{LIB_PATH} not built: run `python __graft_entry__.py build` (hipcc, gfx950)")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64, u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64
+    sig = {
+        "sentinel_engine_create": (C.c_int, [C.c_int, vp, C.POINTER(vp)]),
+        "sentinel_engine_destroy": (C.c_int, [vp]),
+        "sentinel_last_error": (C.c_char_p, []),
+        "sentinel_device_count": (C.c_int, []),
+        "sentinel_set_server_config": (C.c_int, [vp, vp]),
+        "sentinel_set_namespaces": (C.c_int, [vp, vp, i32]),
+        "sentinel_set_connected_count": (C.c_int, [vp, i32, i32]),
+        "sentinel_load_flow_rules": (C.c_int, [vp, vp, i32]),
+        "sentinel_load_param_rules": (C.c_int, [vp, vp, i32, vp, vp, i32]),
+        "sentinel_flow_count": (i32, [vp]),
+        "sentinel_lookup_flow_idx": (C.c_int, [vp, i64, vp, vp]),
+        "sentinel_lookup_param_idx": (C.c_int, [vp, i64, vp, vp]),
+        "sentinel_submit_flow_batch": (C.c_int, [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "sentinel_submit_flow_batch_host": (C.c_int, [vp, i64, vp, vp, vp, vp, vp, vp, vp]),
+        "sentinel_submit_param_batch": (C.c_int, [vp, i64, vp, vp, vp, vp, vp, vp, vp]),
+        "sentinel_submit_param_batch_host": (C.c_int, [vp, i64, vp, vp, vp, vp, vp, vp]),
+        "sentinel_request_token": (C.c_int, [vp, i64, i32, i32, i64, vp]),
+        "sentinel_request_param_token": (C.c_int, [vp, i64, i32, u64, i64, vp]),
+        "sentinel_synchronize": (C.c_int, [vp]),
+        "sentinel_dump_flow": (C.c_int, [vp, i32, vp, i32]),
+        "sentinel_param_sum": (C.c_int, [vp, i32, u64, i64, vp]),
+        "sentinel_snapshot": (C.c_int, [vp, i64, vp]),
+        "sentinel_snapshot_device": (C.c_int, [vp, i64, vp, vp]),
+        "sentinel_engine_stream": (vp, [vp]),
+        "sentinel_profile_enable": (C.c_int, [vp, C.c_int]),
+        "sentinel_profile_read": (C.c_int, [vp, C.c_int, vp, vp, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc < 0:
+        msg = load().sentinel_last_error()
+        raise SentinelError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")

@@ -1,0 +1,32 @@
+"""Build libsentinel_amd.so for gfx950 in-tree with hipcc (no JIT cache, travels with the repo)."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(_HERE)
+SOURCES = [os.path.join(_HERE, "csrc", "engine.hip")]
+DEPS = SOURCES + [os.path.join(_HERE, "csrc", f) for f in ("common.hpp", "scan_sort.hpp", "admission.hpp")] + [
+    os.path.join(ROOT, "include", "sentinel_amd.h")]
+OUT = os.path.join(_HERE, "libsentinel_amd.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off", "-Wall"]
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    return any(os.path.getmtime(d) > t for d in DEPS)
+
+
+def build(force: bool = False) -> str:
+    if force or needs_build():
+        cmd = [HIPCC, *FLAGS, "-o", OUT, *SOURCES]
+        subprocess.run(cmd, check=True)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force=True))

@@ -1,0 +1,60 @@
+// common.hpp -- device helpers shared by the gfx950 kernels of the token-decision engine.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sentinel {
+
+constexpr int WAVE = 64;                 // CDNA wavefront width
+constexpr int64_t EPOCH_ABSENT = -1;     // slot never created (LeapArray slot == null)
+constexpr uint32_t KEY_INVALID = 0xFFFFFFFFu;
+
+// ClusterFlowEvent ordinals (srv/flow/statistic/data/ClusterFlowEvent.java:22-52)
+enum : int { EV_PASS = 0, EV_BLOCK = 1, EV_PASS_REQUEST = 2, EV_BLOCK_REQUEST = 3,
+             EV_OCCUPIED_PASS = 4, EV_OCCUPIED_BLOCK = 5, EV_WAITING = 6, NEV = 7 };
+
+// TokenResultStatus (core/cluster/TokenResultStatus.java:27-69)
+enum : int8_t { ST_BAD_REQUEST = -4, ST_TOO_MANY_REQUEST = -2, ST_FAIL = -1, ST_OK = 0,
+                ST_BLOCKED = 1, ST_SHOULD_WAIT = 2, ST_NO_RULE_EXISTS = 3 };
+
+// Key kinds of the segmented-admission pipeline.
+enum : uint8_t { KIND_CLUSTER = 0,   // ClusterFlowChecker (srv/flow/ClusterFlowChecker.java:55-112)
+                 KIND_SIMPLE = 1,    // SimpleClusterFlowChecker (rls/flow/SimpleClusterFlowChecker.java:33-65)
+                 KIND_LIMITER = 2,   // RequestLimiter.tryPass (srv/flow/statistic/limit/RequestLimiter.java:72-87)
+                 KIND_PARAM = 3 };   // ClusterParamFlowChecker single value (srv/flow/ClusterParamFlowChecker.java:42-87)
+
+// JLS 5.1.3 double -> int: NaN -> 0, saturating.
+__host__ __device__ inline int32_t java_d2i(double d) {
+    if (d != d) return 0;
+    if (d >= 2147483647.0) return 2147483647;
+    if (d <= -2147483648.0) return (int32_t)0x80000000u;
+    return (int32_t)d;
+}
+
+__host__ __device__ inline int64_t wrap_add(int64_t a, int64_t b) {
+    return (int64_t)((uint64_t)a + (uint64_t)b);
+}
+
+__host__ __device__ inline int64_t wrap_mul(int64_t a, int64_t b) {
+    return (int64_t)((uint64_t)a * (uint64_t)b);
+}
+
+// epoch(t) = floor(t / w) for 0 <= t < 2^53 without a 64-bit integer divide: the double quotient
+// is within one of the true quotient (|err| <= t/w * 2^-52 < 1), fixed by one remainder check.
+__device__ inline int64_t epoch_of(int64_t t, int32_t w, double rcp_w) {
+    int64_t e = (int64_t)((double)t * rcp_w);
+    int64_t r = t - e * (int64_t)w;
+    if (r < 0) e -= 1;
+    else if (r >= (int64_t)w) e += 1;
+    return e;
+}
+
+__device__ inline uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+// popcount(mask & lanes-below-me)
+__device__ inline uint32_t mask_rank(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+}  // namespace sentinel

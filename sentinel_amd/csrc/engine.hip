@@ -1,0 +1,1136 @@
+// engine.hip -- MI355X token-decision engine: rule tables in HBM, batch pipeline, C ABI.
+//
+// Implements include/sentinel_amd.h.  One engine = one GPU = one shard of the flowId space.
+// The batched path replaces DefaultTokenService.requestToken / requestParamToken
+// (srv/flow/DefaultTokenService.java:37-62) for a whole batch of events at once:
+//
+//   k_flow_prep     validation + rule lookup + namespace check (DTS:37-48, CFC:50-60)
+//   [limiter run]   GlobalRequestLimiter.tryPass per namespace (GlobalRequestLimiter.java:46-55)
+//   K2 radix sort   group by flow, keep arrival order
+//   K1+K3           window roll + segmented admission (admission.hpp)
+//   verdict         scatter {status, remaining, waitInMs} back to arrival order
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/sentinel_amd.h"
+#include "admission.hpp"
+#include "common.hpp"
+#include "scan_sort.hpp"
+
+using namespace sentinel;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_OK(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess) return fail(SENTINEL_E_DEVICE, std::string(#expr ": ") + hipGetErrorString(_e)); \
+    } while (0)
+
+int bits_for(int64_t nkeys) {     // smallest b with 2^b - 1 >= nkeys (room for the invalid key)
+    int b = 1;
+    while (((int64_t)1 << b) - 1 < nkeys) ++b;
+    return b;
+}
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t want) {
+        if (want <= bytes) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        size_t b = std::max<size_t>(want, 256);
+        if (hipMalloc(&p, b) != hipSuccess) return fail(SENTINEL_E_NOMEM, "hipMalloc failed");
+        bytes = b;
+        return 0;
+    }
+    template <class T> T *as() const { return (T *)p; }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+template <class T>
+int upload(DevBuf &b, const std::vector<T> &v) {
+    int rc = b.ensure(std::max<size_t>(v.size() * sizeof(T), sizeof(T)));
+    if (rc) return rc;
+    if (!v.empty()) HIP_OK(hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return 0;
+}
+
+// Device-side key tables (SoA).
+struct TableBufs {
+    DevBuf off, n, w, rcp, Is, thr, kind, state, occ, has_occ;
+    void release() {
+        for (DevBuf *b : {&off, &n, &w, &rcp, &Is, &thr, &kind, &state, &occ, &has_occ}) b->release();
+    }
+};
+
+// ------------------------------------------------------------------ prep kernels
+
+// DefaultTokenService.requestToken validation (DTS:37-48) + namespace / limiter routing
+// (ClusterFlowChecker.allowProceed, CFC:50-53).  Decided events get their final verdict here.
+__global__ __launch_bounds__(256) void k_flow_prep(int64_t n, const int32_t *__restrict__ flow_idx,
+                                                   const int32_t *__restrict__ acquire,
+                                                   const int64_t *__restrict__ ts, int32_t nflows,
+                                                   const int32_t *__restrict__ flow_ns,
+                                                   const uint8_t *__restrict__ flow_kind,
+                                                   const int32_t *__restrict__ ns_limiter, int32_t nns,
+                                                   int8_t *status, int32_t *remaining, int32_t *wait_ms,
+                                                   uint32_t *fkey, uint32_t finvalid, uint32_t *lkey,
+                                                   uint32_t linvalid) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int32_t idx = flow_idx[i];
+    const int32_t a = acquire[i];
+    int8_t st = 127;   // undecided
+    uint32_t k = finvalid, l = linvalid;
+    if (idx == SENTINEL_IDX_BAD_ID || a <= 0) st = ST_BAD_REQUEST;
+    else if (idx < 0 || idx >= nflows) st = ST_NO_RULE_EXISTS;
+    else {
+        if (flow_kind[idx] == KIND_CLUSTER) {
+            const int32_t ns = flow_ns[idx];
+            if (ns < 0 || ns >= nns) st = ST_TOO_MANY_REQUEST;        // namespace == null
+            else if (ns_limiter[ns] >= 0) l = (uint32_t)ns_limiter[ns];
+        }
+        if (st == 127 && ts[i] < 0) st = ST_FAIL;                    // reference: NPE in LeapArray
+        if (st == 127) k = (uint32_t)idx;
+        else l = linvalid;
+    }
+    fkey[i] = k;
+    if (lkey) lkey[i] = l;
+    if (st != 127) {
+        status[i] = st;
+        remaining[i] = 0;
+        if (wait_ms) wait_ms[i] = 0;
+    }
+}
+
+// requestParamToken validation (DTS:51-62) + param slot lookup/insert in the open-addressing
+// table (exact per-value counters: ClusterParamMetric.java:46-82).
+__device__ inline uint64_t mix64(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+    return x;
+}
+
+constexpr uint64_t PKEY_EMPTY = 0xFFFFFFFFFFFFFFFFull;
+
+__global__ __launch_bounds__(256) void k_param_prep(int64_t n, const int32_t *__restrict__ rule_idx,
+                                                    const int32_t *__restrict__ acquire,
+                                                    const uint64_t *__restrict__ pkey,
+                                                    const int64_t *__restrict__ ts, int32_t nrules,
+                                                    const int32_t *__restrict__ rule_ns, const int32_t *__restrict__ ns_limiter,
+                                                    int32_t nns, unsigned long long *table, uint64_t cap_mask,
+                                                    int32_t *slot_rule, int8_t *status, int32_t *remaining,
+                                                    uint32_t *fkey, uint32_t finvalid, uint32_t *lkey, uint32_t linvalid) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int32_t r = rule_idx[i];
+    const int32_t a = acquire[i];
+    int8_t st = 127;
+    uint32_t k = finvalid, l = linvalid;
+    if (r == SENTINEL_IDX_BAD_ID || a <= 0) st = ST_BAD_REQUEST;
+    else if (r < 0 || r >= nrules) st = ST_NO_RULE_EXISTS;
+    else {
+        const int32_t ns = rule_ns[r];
+        if (ns < 0 || ns >= nns) st = ST_TOO_MANY_REQUEST;
+        else if (ns_limiter[ns] >= 0) l = (uint32_t)ns_limiter[ns];
+        if (st == 127 && ts[i] < 0) st = ST_FAIL;
+        if (st == 127) {
+            const unsigned long long key = (unsigned long long)pkey[i];
+            uint64_t h = mix64(key) & cap_mask;
+            uint64_t probes = 0;
+            for (;;) {
+                const unsigned long long prev = atomicCAS(&table[h], (unsigned long long)PKEY_EMPTY, key);
+                if (prev == PKEY_EMPTY || prev == key) break;
+                h = (h + 1) & cap_mask;
+                if (++probes > cap_mask) { st = ST_FAIL; break; }    // table full
+            }
+            if (st == 127) {
+                k = (uint32_t)h;
+                slot_rule[h] = r;          // identical value from every writer of this slot
+            }
+        }
+        if (st != 127) l = linvalid;
+    }
+    fkey[i] = k;
+    if (lkey) lkey[i] = l;
+    if (st != 127) {
+        status[i] = st;
+        remaining[i] = 0;
+    }
+}
+
+// Per event: refresh the per-slot parameters of its param slot from the rule (identical writes).
+__global__ __launch_bounds__(256) void k_param_meta(int64_t n, const uint32_t *__restrict__ fkey, uint32_t finvalid,
+                                                    const uint64_t *__restrict__ pkey,
+                                                    const int32_t *__restrict__ slot_rule,
+                                                    const int32_t *__restrict__ rule_n, const int32_t *__restrict__ rule_w,
+                                                    const double *__restrict__ rule_rcp, const double *__restrict__ rule_Is,
+                                                    const double *__restrict__ rule_thr,
+                                                    const unsigned long long *__restrict__ hot_table, uint64_t hot_mask,
+                                                    const double *__restrict__ hot_thr,
+                                                    int32_t *slot_n, int32_t *slot_w, double *slot_rcp, double *slot_Is,
+                                                    double *slot_thr, uint8_t *slot_kind) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = fkey[i];
+    if (s == finvalid) return;
+    const int32_t r = slot_rule[s];
+    double thr = rule_thr[r];
+    if (hot_table) {   // ClusterParamFlowChecker.getRawThreshold (CPFC:113-120)
+        const unsigned long long key = (unsigned long long)pkey[i];
+        uint64_t h = mix64(key) & hot_mask;
+        for (uint64_t p = 0; p <= hot_mask; ++p) {
+            const unsigned long long x = hot_table[h];
+            if (x == PKEY_EMPTY) break;
+            if (x == key) { thr = hot_thr[h]; break; }
+            h = (h + 1) & hot_mask;
+        }
+    }
+    slot_n[s] = rule_n[r];
+    slot_w[s] = rule_w[r];
+    slot_rcp[s] = rule_rcp[r];
+    slot_Is[s] = rule_Is[r];
+    slot_thr[s] = thr;
+    slot_kind[s] = KIND_PARAM;
+}
+
+// nvalid = number of sorted keys below the invalid key.
+__global__ __launch_bounds__(256) void k_count_valid(const uint32_t *__restrict__ skey, int64_t n, uint32_t invalid,
+                                                     uint32_t *nvalid) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const bool v = skey[i] != invalid;
+    if (i == 0 && !v) *nvalid = 0;
+    if (v && (i == n - 1 || skey[i + 1] == invalid)) *nvalid = (uint32_t)(i + 1);
+}
+
+// Snapshot of one flow: getAvg(BLOCK) then getAvg(PASS) at ts (ClusterMetricNodeGenerator.java:79-84).
+__global__ __launch_bounds__(256) void k_snapshot(KeyTable T, int32_t nflows, int64_t ts,
+                                                  const int64_t *__restrict__ flow_ids,
+                                                  sentinel_flow_snapshot_t *out) {
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nflows) return;
+    const int64_t off = T.state_off[f];
+    const int n = T.n[f];
+    const int64_t E = epoch_of(ts, T.w[f], T.rcp_w[f]);
+    roll(T, (int)f, off, n, E);
+    const double block = (double)window_sum(T, off, n, E, EV_BLOCK) / T.I_s[f];
+    roll(T, (int)f, off, n, E);
+    const double pass = (double)window_sum(T, off, n, E, EV_PASS) / T.I_s[f];
+    out[f].flow_id = flow_ids[f];
+    out[f].pass_qps = pass;
+    out[f].block_qps = block;
+}
+
+// Initialise a key range's state: epochs absent, counters zero.
+__global__ void k_init_state(int64_t *state, const int64_t *__restrict__ off, int64_t stride,
+                             const int32_t *__restrict__ nn, int32_t fixed_n, int32_t ncounters, int64_t nkeys) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nkeys) return;
+    const int64_t o = off ? off[k] : k * stride;
+    const int n = nn ? nn[k] : fixed_n;
+    for (int j = 0; j < n; ++j) state[o + j] = EPOCH_ABSENT;
+    for (int64_t j = n; j < (int64_t)(1 + ncounters) * n; ++j) state[o + j] = 0;
+}
+
+inline unsigned grid_for(int64_t n, int threads = 256) { return (unsigned)std::max<int64_t>(1, (n + threads - 1) / threads); }
+
+}  // namespace
+
+// ==================================================================== engine
+struct sentinel_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    sentinel_server_config_t cfg{1.0, 1.0};
+    std::vector<sentinel_namespace_t> ns;
+
+    // flows
+    std::vector<sentinel_flow_rule_t> rules;
+    std::unordered_map<int64_t, int32_t> flow_index;
+    std::vector<int32_t> h_flow_ns;
+    std::vector<int32_t> h_flow_n;
+    std::vector<int32_t> h_flow_w;
+    std::vector<int64_t> h_flow_off;
+    TableBufs ft;
+    DevBuf d_flow_ns, d_flow_ids;
+    int64_t flow_state_words = 0;
+
+    // namespace limiters (RequestLimiter = UnaryLeapArray(10, 1000))
+    std::vector<int32_t> h_ns_limiter;   // namespace -> limiter key or -1
+    int32_t nlimiters = 0;
+    TableBufs lt;
+    DevBuf d_ns_limiter;
+
+    // param rules + slots
+    std::vector<sentinel_param_rule_t> prules;
+    std::unordered_map<int64_t, int32_t> param_index;
+    DevBuf d_prule_ns, d_prule_n, d_prule_w, d_prule_rcp, d_prule_Is, d_prule_thr;
+    DevBuf d_ptable, d_slot_rule, d_hot_table, d_hot_thr;
+    TableBufs pt;
+    uint64_t pcap = (uint64_t)1 << 22;
+    int32_t pmax_n = 1;
+    uint64_t hot_mask = 0;
+    bool has_hot = false;
+
+    // per-kernel profiling (HIP events on the launch stream)
+    struct ProfRec { const char *name; hipEvent_t a, b; int64_t units; };
+    struct ProfAcc { double ms = 0; int64_t calls = 0; int64_t units = 0; };
+    bool prof = false;
+    std::vector<ProfRec> prof_pending;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<std::string, ProfAcc>> prof_acc;
+
+    hipEvent_t get_ev() {
+        if (!ev_pool.empty()) { hipEvent_t e = ev_pool.back(); ev_pool.pop_back(); return e; }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+
+    template <class F>
+    void launch(const char *name, int64_t units, hipStream_t s, F &&f) {
+        if (!prof) { f(); return; }
+        hipEvent_t a = get_ev(), b = get_ev();
+        (void)hipEventRecord(a, s);
+        f();
+        (void)hipEventRecord(b, s);
+        prof_pending.push_back({name, a, b, units});
+    }
+
+    void prof_collect() {
+        for (auto &r : prof_pending) {
+            (void)hipEventSynchronize(r.b);
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, r.a, r.b);
+            auto it = std::find_if(prof_acc.begin(), prof_acc.end(), [&](auto &x) { return x.first == r.name; });
+            if (it == prof_acc.end()) { prof_acc.emplace_back(r.name, ProfAcc{}); it = prof_acc.end() - 1; }
+            it->second.ms += ms;
+            it->second.calls += 1;
+            it->second.units += r.units;
+            ev_pool.push_back(r.a);
+            ev_pool.push_back(r.b);
+        }
+        prof_pending.clear();
+    }
+
+    void scan_incl(uint32_t *buf, int64_t n, hipStream_t s) {
+        if (n <= 0) return;
+        const int64_t nb = scan_parts(n);
+        uint32_t *parts = w_parts.as<uint32_t>();
+        launch("scan_tiles", n, s, [&] { k_scan_tiles<false><<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, buf, n, parts); });
+        launch("scan_partials", nb, s, [&] { k_scan_partials<<<1, SCAN_THREADS, 0, s>>>(parts, nb, nullptr); });
+        launch("scan_add", n, s, [&] { k_scan_add<<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, n, parts); });
+    }
+
+    void scan_excl(uint32_t *buf, int64_t n, hipStream_t s) {
+        if (n <= 0) return;
+        const int64_t nb = scan_parts(n);
+        uint32_t *parts = w_parts.as<uint32_t>();
+        launch("scan_tiles", n, s, [&] { k_scan_tiles<true><<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, buf, n, parts); });
+        launch("scan_partials", nb, s, [&] { k_scan_partials<<<1, SCAN_THREADS, 0, s>>>(parts, nb, nullptr); });
+        launch("scan_add", n, s, [&] { k_scan_add<<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, n, parts); });
+    }
+
+    // K2: stable LSD radix sort of (key, seq) by the low `bits` key bits into (skey, sseq).
+    void sort(const uint32_t *keys_in, int64_t n, int bits, hipStream_t s) {
+        const int64_t nb = sort_blocks(n);
+        const int passes = (bits + RADIX_BITS - 1) / RADIX_BITS;
+        uint32_t *kb[2], *vb[2];
+        if (passes % 2 == 1) { kb[0] = w_skey.as<uint32_t>(); vb[0] = w_sseq.as<uint32_t>(); kb[1] = w_ktmp.as<uint32_t>(); vb[1] = w_vtmp.as<uint32_t>(); }
+        else { kb[0] = w_ktmp.as<uint32_t>(); vb[0] = w_vtmp.as<uint32_t>(); kb[1] = w_skey.as<uint32_t>(); vb[1] = w_sseq.as<uint32_t>(); }
+        const uint32_t *kin = keys_in;
+        const uint32_t *vin = nullptr;
+        uint32_t *hist = w_hist.as<uint32_t>();
+        for (int p = 0; p < passes; ++p) {
+            const int shift = p * RADIX_BITS;
+            launch("radix_hist", n, s, [&] { k_radix_hist<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(kin, n, shift, hist, nb); });
+            scan_excl(hist, nb * RADIX, s);
+            uint32_t *ko = kb[p % 2], *vo = vb[p % 2];
+            launch("radix_scatter", n, s, [&] { k_radix_scatter<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(kin, vin, ko, vo, n, shift, hist, nb); });
+            kin = ko;
+            vin = vo;
+        }
+    }
+
+    // batch workspace
+    DevBuf w_fkey, w_lkey, w_skey, w_sseq, w_ktmp, w_vtmp, w_hist, w_parts, w_epoch, w_acq, w_fl, w_segid,
+        w_segstart, w_het, w_done, w_s0, w_k, w_counters;
+    DevBuf io_idx, io_acq, io_fl, io_ts, io_st, io_rem, io_wait, io_pkey;
+    int64_t ws_cap = 0;
+
+    int ensure_ws(int64_t n) {
+        if (n <= ws_cap) return 0;
+        int64_t c = std::max<int64_t>(n, 1024);
+        int rc = 0;
+        rc |= w_fkey.ensure(c * 4);
+        rc |= w_lkey.ensure(c * 4);
+        rc |= w_skey.ensure(c * 4);
+        rc |= w_sseq.ensure(c * 4);
+        rc |= w_ktmp.ensure(c * 4);
+        rc |= w_vtmp.ensure(c * 4);
+        rc |= w_hist.ensure((size_t)sort_hist_words(c) * 4);
+        rc |= w_parts.ensure((size_t)(scan_parts(std::max<int64_t>(c, sort_hist_words(c))) + 16) * 4);
+        rc |= w_epoch.ensure(c * 8);
+        rc |= w_acq.ensure(c * 4);
+        rc |= w_fl.ensure(c);
+        rc |= w_segid.ensure(c * 4);
+        rc |= w_segstart.ensure((c + 1) * 4);
+        rc |= w_het.ensure(c);
+        rc |= w_done.ensure(c);
+        rc |= w_s0.ensure(c * 8);
+        rc |= w_k.ensure(c * 4);
+        rc |= w_counters.ensure(64);
+        if (rc) return SENTINEL_E_NOMEM;
+        ws_cap = c;
+        return 0;
+    }
+
+    BatchWork work() {
+        BatchWork W;
+        W.skey = w_skey.as<uint32_t>();
+        W.sseq = w_sseq.as<uint32_t>();
+        W.s_epoch = w_epoch.as<int64_t>();
+        W.s_acq = w_acq.as<int32_t>();
+        W.s_fl = w_fl.as<uint8_t>();
+        W.segid = w_segid.as<uint32_t>();
+        W.seg_start = w_segstart.as<uint32_t>();
+        W.seg_het = w_het.as<uint8_t>();
+        W.seg_done = w_done.as<uint8_t>();
+        W.seg_s0 = w_s0.as<int64_t>();
+        W.seg_k = w_k.as<uint32_t>();
+        W.nvalid = w_counters.as<uint32_t>();
+        W.nseg = w_counters.as<uint32_t>() + 1;
+        return W;
+    }
+
+    KeyTable table(TableBufs &b, int ncounters, int64_t stride) {
+        KeyTable T;
+        T.state_off = stride ? nullptr : b.off.as<int64_t>();
+        T.state_stride = stride;
+        T.n = b.n.as<int32_t>();
+        T.w = b.w.as<int32_t>();
+        T.rcp_w = b.rcp.as<double>();
+        T.I_s = b.Is.as<double>();
+        T.thr = b.thr.as<double>();
+        T.kind = b.kind.as<uint8_t>();
+        T.state = b.state.as<int64_t>();
+        T.occ = b.occ.as<int64_t>();
+        T.has_occ = b.has_occ.as<uint8_t>();
+        T.ncounters = ncounters;
+        T.max_occupy_ratio = cfg.max_occupy_ratio;
+        return T;
+    }
+
+    // The generic pipeline: sort by key, segment, decide, scatter.
+    void run_pipeline(const KeyTable &T, const uint32_t *keys, int64_t n, int bits, const int64_t *ts,
+                      const int32_t *acquire, const uint8_t *flags, const Verdicts &V, hipStream_t s) {
+        BatchWork W = work();
+        const uint32_t invalid = ((uint32_t)1 << bits) - 1;
+        sort(keys, n, bits, s);
+        const unsigned g = grid_for(n);
+        launch("count_valid", n, s, [&] { k_count_valid<<<g, 256, 0, s>>>(W.skey, n, invalid, W.nvalid); });
+        launch("gather_sorted", n, s, [&] { k_gather_sorted<<<g, 256, 0, s>>>(T, W, ts, acquire, flags, n); });
+        launch("heads", n, s, [&] { k_heads<<<g, 256, 0, s>>>(W, n); });
+        scan_incl(W.segid, n, s);
+        launch("seg_start", n, s, [&] { k_seg_start<<<g, 256, 0, s>>>(W, n); });
+        launch("seg_het", n, s, [&] { k_seg_het<<<g, 256, 0, s>>>(T, W, n); });
+        launch("process", n, s, [&] { k_process<<<g, 256, 0, s>>>(T, W, V, n); });
+        launch("verdict", n, s, [&] { k_verdict<<<g, 256, 0, s>>>(T, W, V, n); });
+    }
+
+    int rebuild_flow_thresholds();
+    int rebuild_limiters();
+};
+
+// Host mirror of ClusterFlowChecker.calcGlobalThreshold * exceedCount (CFC:38-48, 68) and
+// SimpleClusterFlowChecker (SCFC:42), evaluated in double exactly as Java does.
+int sentinel_engine::rebuild_flow_thresholds() {
+    std::vector<double> thr(rules.size());
+    for (size_t i = 0; i < rules.size(); ++i) {
+        const sentinel_flow_rule_t &r = rules[i];
+        if (r.checker == SENTINEL_CHECKER_SIMPLE) {
+            thr[i] = r.count * cfg.exceed_count;
+        } else {
+            double g;
+            if (r.threshold_type == SENTINEL_THRESHOLD_GLOBAL) g = r.count;
+            else {
+                const int32_t c = (r.namespace_idx >= 0 && r.namespace_idx < (int32_t)ns.size()) ? ns[r.namespace_idx].connected_count : 0;
+                g = r.count * (double)c;
+            }
+            thr[i] = g * cfg.exceed_count;
+        }
+    }
+    return upload(ft.thr, thr);
+}
+
+// One RequestLimiter per namespace with has_limiter (GlobalRequestLimiter.java:32-37):
+// UnaryLeapArray(10, 1000) -> n = 10, w = 100, intervalInSecond = 1.0.
+int sentinel_engine::rebuild_limiters() {
+    h_ns_limiter.assign(ns.size(), -1);
+    std::vector<int32_t> n, w;
+    std::vector<double> rcp, Is, thr;
+    std::vector<uint8_t> kind;
+    for (size_t i = 0; i < ns.size(); ++i) {
+        if (!ns[i].has_limiter) continue;
+        h_ns_limiter[i] = (int32_t)n.size();
+        n.push_back(10);
+        w.push_back(100);
+        rcp.push_back(1.0 / 100.0);
+        Is.push_back(1000 / 1000.0);
+        thr.push_back(ns[i].max_allowed_qps);
+        kind.push_back(KIND_LIMITER);
+    }
+    nlimiters = (int32_t)n.size();
+    int rc = 0;
+    rc |= upload(d_ns_limiter, h_ns_limiter);
+    rc |= upload(lt.n, n);
+    rc |= upload(lt.w, w);
+    rc |= upload(lt.rcp, rcp);
+    rc |= upload(lt.Is, Is);
+    rc |= upload(lt.thr, thr);
+    rc |= upload(lt.kind, kind);
+    if (rc) return rc;
+    const int64_t stride = 2 * 10;
+    rc = lt.state.ensure(std::max<int64_t>(1, nlimiters) * stride * 8);
+    if (rc) return rc;
+    if (nlimiters > 0) {
+        k_init_state<<<grid_for(nlimiters), 256, 0, stream>>>(lt.state.as<int64_t>(), nullptr, stride, nullptr, 10, 1, nlimiters);
+        HIP_OK(hipStreamSynchronize(stream));
+    }
+    return 0;
+}
+
+// ==================================================================== C ABI
+extern "C" {
+
+const char *sentinel_last_error(void) { return g_err.c_str(); }
+
+int sentinel_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sentinel_engine_t **out) {
+    if (!out) return fail(SENTINEL_E_INVALID, "out is null");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(SENTINEL_E_DEVICE, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(SENTINEL_E_INVALID, "bad device index");
+    HIP_OK(hipSetDevice(device));
+    sentinel_engine *e = new sentinel_engine();
+    e->device = device;
+    if (cfg) e->cfg = *cfg;
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete e;
+        return fail(SENTINEL_E_DEVICE, "hipStreamCreate failed");
+    }
+    if (const char *c = getenv("SENTINEL_PARAM_CAPACITY")) {
+        uint64_t v = strtoull(c, nullptr, 10);
+        uint64_t p = 1024;
+        while (p < v) p <<= 1;
+        e->pcap = p;
+    }
+    // default namespace set: one namespace ("default"), no limiter, connectedCount 0
+    e->ns.push_back(sentinel_namespace_t{0, 0, 30000.0});
+    int rc = e->rebuild_limiters();
+    if (rc) {
+        delete e;
+        return rc;
+    }
+    *out = e;
+    return 0;
+}
+
+int sentinel_engine_destroy(sentinel_engine_t *e) {
+    if (!e) return 0;
+    (void)hipSetDevice(e->device);
+    (void)hipStreamSynchronize(e->stream);
+    e->ft.release();
+    e->lt.release();
+    e->pt.release();
+    for (DevBuf *b : {&e->d_flow_ns, &e->d_flow_ids, &e->d_ns_limiter, &e->d_prule_ns, &e->d_prule_n, &e->d_prule_w,
+                      &e->d_prule_rcp, &e->d_prule_Is, &e->d_prule_thr, &e->d_ptable, &e->d_slot_rule,
+                      &e->d_hot_table, &e->d_hot_thr, &e->w_fkey, &e->w_lkey, &e->w_skey, &e->w_sseq, &e->w_ktmp,
+                      &e->w_vtmp, &e->w_hist, &e->w_parts, &e->w_epoch, &e->w_acq, &e->w_fl, &e->w_segid,
+                      &e->w_segstart, &e->w_het, &e->w_done, &e->w_s0, &e->w_k, &e->w_counters, &e->io_idx,
+                      &e->io_acq, &e->io_fl, &e->io_ts, &e->io_st, &e->io_rem, &e->io_wait, &e->io_pkey})
+        b->release();
+    (void)hipStreamDestroy(e->stream);
+    delete e;
+    return 0;
+}
+
+void *sentinel_engine_stream(sentinel_engine_t *e) { return e ? (void *)e->stream : nullptr; }
+
+int sentinel_profile_enable(sentinel_engine_t *e, int enable) {
+    if (!e) return fail(SENTINEL_E_INVALID, "null engine");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    e->prof_collect();
+    e->prof_acc.clear();
+    e->prof = enable != 0;
+    return 0;
+}
+
+int sentinel_profile_read(sentinel_engine_t *e, int max, char *names32, double *total_ms, int64_t *calls,
+                          int64_t *units) {
+    if (!e || max < 0 || (max > 0 && (!names32 || !total_ms || !calls || !units))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    e->prof_collect();
+    int k = 0;
+    for (auto &x : e->prof_acc) {
+        if (k >= max) break;
+        std::memset(names32 + 32 * k, 0, 32);
+        std::strncpy(names32 + 32 * k, x.first.c_str(), 31);
+        total_ms[k] = x.second.ms;
+        calls[k] = x.second.calls;
+        units[k] = x.second.units;
+        ++k;
+    }
+    return k;
+}
+
+int sentinel_set_server_config(sentinel_engine_t *e, const sentinel_server_config_t *cfg) {
+    if (!e || !cfg) return fail(SENTINEL_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    e->cfg = *cfg;
+    return e->rebuild_flow_thresholds();
+}
+
+int sentinel_set_namespaces(sentinel_engine_t *e, const sentinel_namespace_t *ns, int32_t n) {
+    if (!e || (n > 0 && !ns) || n < 0) return fail(SENTINEL_E_INVALID, "bad namespaces");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    e->ns.assign(ns, ns + n);
+    int rc = e->rebuild_limiters();
+    if (rc) return rc;
+    return e->rebuild_flow_thresholds();
+}
+
+int sentinel_set_connected_count(sentinel_engine_t *e, int32_t nsi, int32_t connected) {
+    if (!e || nsi < 0) return fail(SENTINEL_E_INVALID, "bad namespace");
+    std::lock_guard<std::mutex> g(e->mu);
+    if (nsi >= (int32_t)e->ns.size()) return fail(SENTINEL_E_INVALID, "bad namespace");
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    e->ns[nsi].connected_count = connected;
+    return e->rebuild_flow_thresholds();
+}
+
+static bool valid_window(int32_t n, int32_t interval) {  // FlowRuleUtil.isWindowConfigValid (FlowRuleUtil.java:229-231)
+    return n > 0 && interval > 0 && interval % n == 0;
+}
+
+int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *rules, int32_t n) {
+    if (!e || (n > 0 && !rules) || n < 0) return fail(SENTINEL_E_INVALID, "bad rules");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    // keep the old state to carry metrics of surviving flowIds (putMetricIfAbsent, CFRM:361)
+    std::unordered_map<int64_t, int32_t> old_index = e->flow_index;
+    std::vector<int64_t> old_off = e->h_flow_off;
+    std::vector<int32_t> old_n = e->h_flow_n, old_w = e->h_flow_w;
+    std::vector<int64_t> old_state;
+    if (e->flow_state_words > 0) {
+        old_state.resize(e->flow_state_words);
+        HIP_OK(hipMemcpy(old_state.data(), e->ft.state.p, old_state.size() * 8, hipMemcpyDeviceToHost));
+    }
+    std::vector<int64_t> old_occ(2 * old_index.size());
+    std::vector<uint8_t> old_hocc(old_index.size());
+    if (!old_index.empty()) {
+        HIP_OK(hipMemcpy(old_occ.data(), e->ft.occ.p, old_occ.size() * 8, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(old_hocc.data(), e->ft.has_occ.p, old_hocc.size(), hipMemcpyDeviceToHost));
+    }
+
+    e->rules.clear();
+    e->flow_index.clear();
+    for (int32_t i = 0; i < n; ++i) {
+        const sentinel_flow_rule_t &r = rules[i];
+        // FlowRuleUtil.isValidRule / checkClusterField (FlowRuleUtil.java:184-227)
+        if (r.flow_id <= 0 || !(r.count >= 0) || !valid_window(r.sample_count, r.window_interval_ms)) continue;
+        auto it = e->flow_index.find(r.flow_id);
+        if (it != e->flow_index.end()) { e->rules[it->second] = r; continue; }   // ruleMap.put: last wins
+        e->flow_index.emplace(r.flow_id, (int32_t)e->rules.size());
+        e->rules.push_back(r);
+    }
+    const size_t F = e->rules.size();
+    std::vector<int64_t> off(F), ids(F);
+    std::vector<int32_t> nn(F), ww(F), nsv(F);
+    std::vector<double> rcp(F), Is(F);
+    std::vector<uint8_t> kind(F);
+    int64_t words = 0;
+    for (size_t i = 0; i < F; ++i) {
+        const sentinel_flow_rule_t &r = e->rules[i];
+        off[i] = words;
+        nn[i] = r.sample_count;
+        ww[i] = r.window_interval_ms / r.sample_count;
+        rcp[i] = 1.0 / (double)ww[i];
+        Is[i] = r.window_interval_ms / 1000.0;   // LeapArray.java:74
+        nsv[i] = r.namespace_idx;
+        kind[i] = r.checker == SENTINEL_CHECKER_SIMPLE ? KIND_SIMPLE : KIND_CLUSTER;
+        ids[i] = r.flow_id;
+        words += (int64_t)(1 + NEV) * r.sample_count;
+    }
+    // new state image: fresh, then carry surviving flows whose window shape is unchanged
+    std::vector<int64_t> st(std::max<int64_t>(words, 1), 0);
+    std::vector<int64_t> occ(2 * std::max<size_t>(F, 1), 0);
+    std::vector<uint8_t> hocc(std::max<size_t>(F, 1), 0);
+    for (size_t i = 0; i < F; ++i) {
+        for (int j = 0; j < nn[i]; ++j) st[off[i] + j] = EPOCH_ABSENT;
+        auto it = old_index.find(ids[i]);
+        if (it == old_index.end()) continue;
+        const int32_t o = it->second;
+        // ClusterMetric is kept as constructed with the OLD (n, interval): only carry when equal
+        if (old_n[o] != nn[i] || old_w[o] != ww[i]) continue;
+        std::copy(old_state.begin() + old_off[o], old_state.begin() + old_off[o] + (1 + NEV) * nn[i], st.begin() + off[i]);
+        occ[2 * i] = old_occ[2 * o];
+        occ[2 * i + 1] = old_occ[2 * o + 1];
+        hocc[i] = old_hocc[o];
+    }
+    int rc = 0;
+    rc |= upload(e->ft.off, off);
+    rc |= upload(e->ft.n, nn);
+    rc |= upload(e->ft.w, ww);
+    rc |= upload(e->ft.rcp, rcp);
+    rc |= upload(e->ft.Is, Is);
+    rc |= upload(e->ft.kind, kind);
+    rc |= upload(e->ft.state, st);
+    rc |= upload(e->ft.occ, occ);
+    rc |= upload(e->ft.has_occ, hocc);
+    rc |= upload(e->d_flow_ns, nsv);
+    rc |= upload(e->d_flow_ids, ids);
+    if (rc) return rc;
+    e->h_flow_off = off;
+    e->h_flow_n = nn;
+    e->h_flow_w = ww;
+    e->h_flow_ns = nsv;
+    e->flow_state_words = words;
+    return e->rebuild_flow_thresholds();
+}
+
+int32_t sentinel_flow_count(sentinel_engine_t *e) { return e ? (int32_t)e->rules.size() : 0; }
+
+int sentinel_lookup_flow_idx(sentinel_engine_t *e, int64_t n, const int64_t *ids, int32_t *out) {
+    if (!e || n < 0 || (n > 0 && (!ids || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    for (int64_t i = 0; i < n; ++i) {
+        if (ids[i] <= 0) { out[i] = SENTINEL_IDX_BAD_ID; continue; }   // ClusterRuleUtil.validId
+        auto it = e->flow_index.find(ids[i]);
+        out[i] = it == e->flow_index.end() ? SENTINEL_IDX_NO_RULE : it->second;
+    }
+    return 0;
+}
+
+int sentinel_lookup_param_idx(sentinel_engine_t *e, int64_t n, const int64_t *ids, int32_t *out) {
+    if (!e || n < 0 || (n > 0 && (!ids || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    for (int64_t i = 0; i < n; ++i) {
+        if (ids[i] <= 0) { out[i] = SENTINEL_IDX_BAD_ID; continue; }
+        auto it = e->param_index.find(ids[i]);
+        out[i] = it == e->param_index.end() ? SENTINEL_IDX_NO_RULE : it->second;
+    }
+    return 0;
+}
+
+static uint64_t host_mix64(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+    return x;
+}
+
+int sentinel_load_param_rules(sentinel_engine_t *e, const sentinel_param_rule_t *rules, int32_t n,
+                              const uint64_t *hot_keys, const int32_t *hot_counts, int32_t n_hot) {
+    if (!e || n < 0 || (n > 0 && !rules) || n_hot < 0 || (n_hot > 0 && (!hot_keys || !hot_counts)))
+        return fail(SENTINEL_E_INVALID, "bad param rules");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    e->prules.clear();
+    e->param_index.clear();
+    std::vector<int32_t> nsv, nn, ww;
+    std::vector<double> rcp, Is, thr;
+    std::vector<std::pair<uint64_t, double>> hot;
+    int32_t maxn = 1;
+    for (int32_t i = 0; i < n; ++i) {
+        const sentinel_param_rule_t &r = rules[i];
+        if (r.flow_id <= 0 || !(r.count >= 0) || !valid_window(r.sample_count, r.window_interval_ms)) continue;
+        if (e->param_index.count(r.flow_id)) continue;
+        e->param_index.emplace(r.flow_id, (int32_t)e->prules.size());
+        e->prules.push_back(r);
+        nsv.push_back(r.namespace_idx);
+        nn.push_back(r.sample_count);
+        ww.push_back(r.window_interval_ms / r.sample_count);
+        rcp.push_back(1.0 / (double)ww.back());
+        Is.push_back(r.window_interval_ms / 1000.0);
+        // calcGlobalThreshold(rule, value) without hot item: count or count*connectedCount (CPFC:101-111)
+        double c = r.count;
+        if (r.threshold_type != SENTINEL_THRESHOLD_GLOBAL) {
+            const int32_t cc = (r.namespace_idx >= 0 && r.namespace_idx < (int32_t)e->ns.size()) ? e->ns[r.namespace_idx].connected_count : 0;
+            c = c * (double)cc;
+        }
+        thr.push_back(c);
+        maxn = std::max(maxn, r.sample_count);
+        for (int32_t h = 0; h < r.hot_n; ++h) {
+            const int32_t j = r.hot_begin + h;
+            if (j < 0 || j >= n_hot) return fail(SENTINEL_E_INVALID, "hot item range out of bounds");
+            double hc = (double)hot_counts[j];
+            if (r.threshold_type != SENTINEL_THRESHOLD_GLOBAL) {
+                const int32_t cc = (r.namespace_idx >= 0 && r.namespace_idx < (int32_t)e->ns.size()) ? e->ns[r.namespace_idx].connected_count : 0;
+                hc = hc * (double)cc;
+            }
+            hot.emplace_back(hot_keys[j], hc);
+        }
+    }
+    e->pmax_n = maxn;
+    int rc = 0;
+    rc |= upload(e->d_prule_ns, nsv);
+    rc |= upload(e->d_prule_n, nn);
+    rc |= upload(e->d_prule_w, ww);
+    rc |= upload(e->d_prule_rcp, rcp);
+    rc |= upload(e->d_prule_Is, Is);
+    rc |= upload(e->d_prule_thr, thr);
+    // hot-item table keyed by param key (param keys are unique per (rule, value))
+    uint64_t hcap = 16;
+    while (hcap < 2 * hot.size() + 2) hcap <<= 1;
+    std::vector<uint64_t> hk(hcap, PKEY_EMPTY);
+    std::vector<double> hv(hcap, 0.0);
+    for (auto &kv : hot) {
+        uint64_t h = host_mix64(kv.first) & (hcap - 1);
+        while (hk[h] != PKEY_EMPTY && hk[h] != kv.first) h = (h + 1) & (hcap - 1);
+        hk[h] = kv.first;
+        hv[h] = kv.second;
+    }
+    e->hot_mask = hcap - 1;
+    e->has_hot = !hot.empty();
+    rc |= upload(e->d_hot_table, hk);
+    rc |= upload(e->d_hot_thr, hv);
+    // slot table + per-slot state (fresh on every load)
+    const uint64_t P = e->pcap;
+    rc |= e->d_ptable.ensure(P * 8);
+    rc |= e->d_slot_rule.ensure(P * 4);
+    rc |= e->pt.n.ensure(P * 4);
+    rc |= e->pt.w.ensure(P * 4);
+    rc |= e->pt.rcp.ensure(P * 8);
+    rc |= e->pt.Is.ensure(P * 8);
+    rc |= e->pt.thr.ensure(P * 8);
+    rc |= e->pt.kind.ensure(P);
+    const int64_t stride = 2 * (int64_t)maxn;
+    rc |= e->pt.state.ensure(P * stride * 8);
+    if (rc) return rc ? SENTINEL_E_NOMEM : 0;
+    HIP_OK(hipMemsetAsync(e->d_ptable.p, 0xFF, P * 8, e->stream));
+    HIP_OK(hipMemsetAsync(e->pt.n.p, 0, P * 4, e->stream));
+    k_init_state<<<grid_for((int64_t)P), 256, 0, e->stream>>>(e->pt.state.as<int64_t>(), nullptr, stride, nullptr, maxn, 1, (int64_t)P);
+    HIP_OK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+static int submit_flow(sentinel_engine_t *e, int64_t n, const int32_t *idx, const int32_t *acq, const uint8_t *fl,
+                       const int64_t *ts, int8_t *st, int32_t *rem, int32_t *wt, hipStream_t s) {
+    if (n <= 0) return 0;
+    if (n > (int64_t)0x7FFFFFF0) return fail(SENTINEL_E_INVALID, "batch too large (max 2^31 events)");
+    int rc = e->ensure_ws(n);
+    if (rc) return rc;
+    const int32_t F = (int32_t)e->rules.size();
+    const int fbits = bits_for(F);
+    const uint32_t finvalid = ((uint32_t)1 << fbits) - 1;
+    const bool lim = e->nlimiters > 0;
+    const int lbits = bits_for(e->nlimiters);
+    const uint32_t linvalid = ((uint32_t)1 << lbits) - 1;
+    uint32_t *fkey = e->w_fkey.as<uint32_t>();
+    uint32_t *lkey = lim ? e->w_lkey.as<uint32_t>() : nullptr;
+    e->launch("flow_prep", n, s, [&] {
+        k_flow_prep<<<grid_for(n), 256, 0, s>>>(n, idx, acq, ts, F, e->d_flow_ns.as<int32_t>(), e->ft.kind.as<uint8_t>(),
+                                                e->d_ns_limiter.as<int32_t>(), (int32_t)e->ns.size(), st, rem, wt, fkey,
+                                                finvalid, lkey, linvalid);
+    });
+    Verdicts V{st, rem, wt, fkey, finvalid};
+    if (lim) {
+        KeyTable LT = e->table(e->lt, 1, 20);
+        e->run_pipeline(LT, lkey, n, lbits, ts, nullptr, nullptr, V, s);
+    }
+    if (F > 0) {
+        KeyTable FT = e->table(e->ft, NEV, 0);
+        e->run_pipeline(FT, fkey, n, fbits, ts, acq, fl, V, s);
+    }
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int sentinel_submit_flow_batch(sentinel_engine_t *e, int64_t n, const int32_t *idx, const int32_t *acq,
+                               const uint8_t *fl, const int64_t *ts, int8_t *st, int32_t *rem, int32_t *wt,
+                               void *stream) {
+    if (!e || n < 0 || (n > 0 && (!idx || !acq || !ts || !st || !rem))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    return submit_flow(e, n, idx, acq, fl, ts, st, rem, wt, s);
+}
+
+int sentinel_submit_flow_batch_host(sentinel_engine_t *e, int64_t n, const int32_t *idx, const int32_t *acq,
+                                    const uint8_t *fl, const int64_t *ts, int8_t *st, int32_t *rem, int32_t *wt) {
+    if (!e || n < 0 || (n > 0 && (!idx || !acq || !ts || !st || !rem))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    hipStream_t s = e->stream;
+    int rc = 0;
+    rc |= e->io_idx.ensure(n * 4);
+    rc |= e->io_acq.ensure(n * 4);
+    rc |= e->io_fl.ensure(n);
+    rc |= e->io_ts.ensure(n * 8);
+    rc |= e->io_st.ensure(n);
+    rc |= e->io_rem.ensure(n * 4);
+    rc |= e->io_wait.ensure(n * 4);
+    if (rc) return SENTINEL_E_NOMEM;
+    HIP_OK(hipMemcpyAsync(e->io_idx.p, idx, n * 4, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(e->io_acq.p, acq, n * 4, hipMemcpyHostToDevice, s));
+    if (fl) HIP_OK(hipMemcpyAsync(e->io_fl.p, fl, n, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(e->io_ts.p, ts, n * 8, hipMemcpyHostToDevice, s));
+    rc = submit_flow(e, n, e->io_idx.as<int32_t>(), e->io_acq.as<int32_t>(), fl ? e->io_fl.as<uint8_t>() : nullptr,
+                     e->io_ts.as<int64_t>(), e->io_st.as<int8_t>(), e->io_rem.as<int32_t>(),
+                     wt ? e->io_wait.as<int32_t>() : nullptr, s);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(st, e->io_st.p, n, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(rem, e->io_rem.p, n * 4, hipMemcpyDeviceToHost, s));
+    if (wt) HIP_OK(hipMemcpyAsync(wt, e->io_wait.p, n * 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    return 0;
+}
+
+static int submit_param(sentinel_engine_t *e, int64_t n, const int32_t *ridx, const int32_t *acq, const uint64_t *pkey,
+                        const int64_t *ts, int8_t *st, int32_t *rem, hipStream_t s) {
+    if (n <= 0) return 0;
+    if (n > (int64_t)0x7FFFFFF0) return fail(SENTINEL_E_INVALID, "batch too large");
+    int rc = e->ensure_ws(n);
+    if (rc) return rc;
+    const int32_t R = (int32_t)e->prules.size();
+    const uint64_t P = e->pcap;
+    const int pbits = bits_for((int64_t)P);
+    const uint32_t pinvalid = ((uint32_t)1 << pbits) - 1;
+    const bool lim = e->nlimiters > 0;
+    const int lbits = bits_for(e->nlimiters);
+    const uint32_t linvalid = ((uint32_t)1 << lbits) - 1;
+    uint32_t *fkey = e->w_fkey.as<uint32_t>();
+    uint32_t *lkey = lim ? e->w_lkey.as<uint32_t>() : nullptr;
+    if (R == 0 || !e->d_ptable.p) {
+        // no param rules: every valid request is NO_RULE_EXISTS (DTS:54-58)
+        k_param_prep<<<grid_for(n), 256, 0, s>>>(n, ridx, acq, pkey, ts, 0, nullptr, nullptr, 0, nullptr, 0, nullptr,
+                                                 st, rem, fkey, pinvalid, nullptr, linvalid);
+        HIP_OK(hipGetLastError());
+        return 0;
+    }
+    k_param_prep<<<grid_for(n), 256, 0, s>>>(n, ridx, acq, pkey, ts, R, e->d_prule_ns.as<int32_t>(),
+                                             e->d_ns_limiter.as<int32_t>(), (int32_t)e->ns.size(),
+                                             e->d_ptable.as<unsigned long long>(), P - 1, e->d_slot_rule.as<int32_t>(),
+                                             st, rem, fkey, pinvalid, lkey, linvalid);
+    k_param_meta<<<grid_for(n), 256, 0, s>>>(n, fkey, pinvalid, pkey, e->d_slot_rule.as<int32_t>(),
+                                             e->d_prule_n.as<int32_t>(), e->d_prule_w.as<int32_t>(),
+                                             e->d_prule_rcp.as<double>(), e->d_prule_Is.as<double>(),
+                                             e->d_prule_thr.as<double>(),
+                                             e->has_hot ? e->d_hot_table.as<unsigned long long>() : nullptr, e->hot_mask,
+                                             e->d_hot_thr.as<double>(), e->pt.n.as<int32_t>(), e->pt.w.as<int32_t>(),
+                                             e->pt.rcp.as<double>(), e->pt.Is.as<double>(), e->pt.thr.as<double>(),
+                                             e->pt.kind.as<uint8_t>());
+    Verdicts V{st, rem, nullptr, fkey, pinvalid};
+    if (lim) {
+        KeyTable LT = e->table(e->lt, 1, 20);
+        e->run_pipeline(LT, lkey, n, lbits, ts, nullptr, nullptr, V, s);
+    }
+    KeyTable PT = e->table(e->pt, 1, 2 * (int64_t)e->pmax_n);
+    e->run_pipeline(PT, fkey, n, pbits, ts, acq, nullptr, V, s);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int sentinel_submit_param_batch(sentinel_engine_t *e, int64_t n, const int32_t *ridx, const int32_t *acq,
+                                const uint64_t *pkey, const int64_t *ts, int8_t *st, int32_t *rem, void *stream) {
+    if (!e || n < 0 || (n > 0 && (!ridx || !acq || !pkey || !ts || !st || !rem))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    return submit_param(e, n, ridx, acq, pkey, ts, st, rem, stream ? (hipStream_t)stream : e->stream);
+}
+
+int sentinel_submit_param_batch_host(sentinel_engine_t *e, int64_t n, const int32_t *ridx, const int32_t *acq,
+                                     const uint64_t *pkey, const int64_t *ts, int8_t *st, int32_t *rem) {
+    if (!e || n < 0 || (n > 0 && (!ridx || !acq || !pkey || !ts || !st || !rem))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    hipStream_t s = e->stream;
+    int rc = 0;
+    rc |= e->io_idx.ensure(n * 4);
+    rc |= e->io_acq.ensure(n * 4);
+    rc |= e->io_pkey.ensure(n * 8);
+    rc |= e->io_ts.ensure(n * 8);
+    rc |= e->io_st.ensure(n);
+    rc |= e->io_rem.ensure(n * 4);
+    if (rc) return SENTINEL_E_NOMEM;
+    HIP_OK(hipMemcpyAsync(e->io_idx.p, ridx, n * 4, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(e->io_acq.p, acq, n * 4, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(e->io_pkey.p, pkey, n * 8, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(e->io_ts.p, ts, n * 8, hipMemcpyHostToDevice, s));
+    rc = submit_param(e, n, e->io_idx.as<int32_t>(), e->io_acq.as<int32_t>(), e->io_pkey.as<uint64_t>(),
+                      e->io_ts.as<int64_t>(), e->io_st.as<int8_t>(), e->io_rem.as<int32_t>(), s);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(st, e->io_st.p, n, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(rem, e->io_rem.p, n * 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    return 0;
+}
+
+int sentinel_request_token(sentinel_engine_t *e, int64_t flow_id, int32_t acquire, int32_t prio, int64_t ts,
+                           sentinel_token_result_t *out) {
+    if (!e || !out) return fail(SENTINEL_E_INVALID, "null argument");
+    int32_t idx;
+    sentinel_lookup_flow_idx(e, 1, &flow_id, &idx);
+    uint8_t fl = prio ? SENTINEL_FLAG_PRIORITIZED : 0;
+    int8_t st = SENTINEL_STATUS_FAIL;
+    int32_t rem = 0, wt = 0;
+    int rc = sentinel_submit_flow_batch_host(e, 1, &idx, &acquire, &fl, &ts, &st, &rem, &wt);
+    out->status = rc ? SENTINEL_STATUS_FAIL : st;
+    out->remaining = rc ? 0 : rem;
+    out->wait_in_ms = rc ? 0 : wt;
+    out->reserved = 0;
+    return rc;
+}
+
+int sentinel_request_param_token(sentinel_engine_t *e, int64_t flow_id, int32_t acquire, uint64_t param_key,
+                                 int64_t ts, sentinel_token_result_t *out) {
+    if (!e || !out) return fail(SENTINEL_E_INVALID, "null argument");
+    int32_t idx;
+    sentinel_lookup_param_idx(e, 1, &flow_id, &idx);
+    int8_t st = SENTINEL_STATUS_FAIL;
+    int32_t rem = 0;
+    int rc = sentinel_submit_param_batch_host(e, 1, &idx, &acquire, &param_key, &ts, &st, &rem);
+    out->status = rc ? SENTINEL_STATUS_FAIL : st;
+    out->remaining = rc ? 0 : rem;
+    out->wait_in_ms = 0;
+    out->reserved = 0;
+    return rc;
+}
+
+int sentinel_synchronize(sentinel_engine_t *e) {
+    if (!e) return fail(SENTINEL_E_INVALID, "null engine");
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int sentinel_dump_flow(sentinel_engine_t *e, int32_t idx, int64_t *out, int32_t out_len) {
+    if (!e || !out) return fail(SENTINEL_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(e->mu);
+    if (idx < 0 || idx >= (int32_t)e->rules.size()) return fail(SENTINEL_E_INVALID, "bad flow index");
+    const int n = e->h_flow_n[idx];
+    const int need = n * (1 + NEV) + NEV + 1;
+    if (out_len < need) return fail(SENTINEL_E_INVALID, "output too small");
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    std::vector<int64_t> st((1 + NEV) * n);
+    HIP_OK(hipMemcpy(st.data(), e->ft.state.as<int64_t>() + e->h_flow_off[idx], st.size() * 8, hipMemcpyDeviceToHost));
+    int64_t occ[2];
+    uint8_t hocc;
+    HIP_OK(hipMemcpy(occ, e->ft.occ.as<int64_t>() + 2 * idx, 16, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(&hocc, e->ft.has_occ.as<uint8_t>() + idx, 1, hipMemcpyDeviceToHost));
+    const int64_t w = e->h_flow_w[idx];
+    for (int j = 0; j < n; ++j) {
+        int64_t *o = out + j * (1 + NEV);
+        const bool present = st[j] != EPOCH_ABSENT;
+        o[0] = present ? st[j] * w : -1;
+        for (int c = 0; c < NEV; ++c) o[1 + c] = present ? st[(1 + c) * n + j] : 0;
+    }
+    int64_t *o = out + n * (1 + NEV);
+    for (int c = 0; c < NEV; ++c) o[c] = 0;
+    o[EV_PASS] = occ[0];
+    o[EV_PASS_REQUEST] = occ[1];
+    o[NEV] = hocc;
+    return need;
+}
+
+int sentinel_param_sum(sentinel_engine_t *e, int32_t ridx, uint64_t pkey, int64_t ts, int64_t *out) {
+    if (!e || !out) return fail(SENTINEL_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(e->mu);
+    if (ridx < 0 || ridx >= (int32_t)e->prules.size()) return fail(SENTINEL_E_INVALID, "bad rule index");
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    *out = 0;
+    // find the slot on the host (read-only probe of the device table)
+    const uint64_t P = e->pcap;
+    std::vector<uint64_t> table(P);
+    HIP_OK(hipMemcpy(table.data(), e->d_ptable.p, P * 8, hipMemcpyDeviceToHost));
+    uint64_t h = host_mix64(pkey) & (P - 1);
+    for (uint64_t p = 0; p < P; ++p) {
+        if (table[h] == PKEY_EMPTY) return 0;
+        if (table[h] == pkey) break;
+        h = (h + 1) & (P - 1);
+    }
+    const sentinel_param_rule_t &r = e->prules[ridx];
+    const int n = r.sample_count;
+    const int64_t w = r.window_interval_ms / n;
+    const int64_t stride = 2 * (int64_t)e->pmax_n;
+    std::vector<int64_t> st(2 * n);
+    HIP_OK(hipMemcpy(st.data(), e->pt.state.as<int64_t>() + h * stride, st.size() * 8, hipMemcpyDeviceToHost));
+    const int64_t E = ts / w;   // read-only view (no roll): valid slots are epochs in (E - n, ...]
+    int64_t s = 0;
+    for (int j = 0; j < n; ++j)
+        if (st[j] != EPOCH_ABSENT && st[j] > E - n && st[j] <= E) s += st[n + j];
+    *out = s;
+    return 0;
+}
+
+int sentinel_snapshot_device(sentinel_engine_t *e, int64_t ts, sentinel_flow_snapshot_t *d_out, void *stream) {
+    if (!e || !d_out) return fail(SENTINEL_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    const int32_t F = (int32_t)e->rules.size();
+    if (F == 0) return 0;
+    if (ts < 0) return fail(SENTINEL_E_INVALID, "negative timestamp");
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    KeyTable FT = e->table(e->ft, NEV, 0);
+    k_snapshot<<<grid_for(F), 256, 0, s>>>(FT, F, ts, e->d_flow_ids.as<int64_t>(), d_out);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int sentinel_snapshot(sentinel_engine_t *e, int64_t ts, sentinel_flow_snapshot_t *out) {
+    if (!e || !out) return fail(SENTINEL_E_INVALID, "null argument");
+    const int32_t F = (int32_t)e->rules.size();
+    if (F == 0) return 0;
+    void *d = nullptr;
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipMalloc(&d, (size_t)F * sizeof(sentinel_flow_snapshot_t)));
+    int rc = sentinel_snapshot_device(e, ts, (sentinel_flow_snapshot_t *)d, nullptr);
+    if (!rc) {
+        if (hipMemcpyAsync(out, d, (size_t)F * sizeof(sentinel_flow_snapshot_t), hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+            hipStreamSynchronize(e->stream) != hipSuccess)
+            rc = fail(SENTINEL_E_DEVICE, "snapshot copy failed");
+    }
+    (void)hipFree(d);
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,252 @@
+// scan_sort.hpp -- device-wide prefix scan and stable LSD radix sort (key u32, value u32) for gfx950.
+//
+// K2 of the engine ("radix sort keys each batch by (flowId, seq)"): keys are dense flow (or
+// namespace / param-slot) indices, values are arrival positions (seq).  LSD radix sort is stable,
+// so events of one key stay in arrival order -- exactly the per-flow serialisation the reference
+// gets from one ClusterMetric per flowId (srv/flow/statistic/ClusterMetricStatistics.java:56-58).
+//
+// Wave-64 design: a 256-thread workgroup = 4 waves owns a 4096-key tile; each wave ranks its
+// 1024 keys (16 per lane, lane-striped so coalesced loads keep arrival order) with 8 ballots per
+// item (64-bit match masks) and a wave-private LDS digit counter -- no LDS atomics, no 32-lane
+// warp idioms.
+#pragma once
+
+#include "common.hpp"
+
+namespace sentinel {
+
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_ITEMS = 16;
+constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;     // 4096
+
+constexpr int RADIX_BITS = 8;
+constexpr int RADIX = 1 << RADIX_BITS;
+constexpr int SORT_THREADS = 256;
+constexpr int SORT_WAVES = SORT_THREADS / WAVE;
+constexpr int SORT_ITEMS = 16;
+constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;     // 4096
+
+__device__ inline uint32_t wave_inclusive_scan(uint32_t v) {
+    const int lane = (int)lane_id();
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) {
+        uint32_t u = __shfl_up(v, off, WAVE);
+        if (lane >= off) v += u;
+    }
+    return v;
+}
+
+// Block-wide exclusive scan of one value per thread (blockDim = SCAN_THREADS); returns the
+// exclusive prefix and the block total through *total.
+__device__ inline uint32_t block_exclusive_scan(uint32_t v, uint32_t *lds_waves, uint32_t *total) {
+    const int lane = (int)lane_id();
+    const int wave = threadIdx.x / WAVE;
+    uint32_t inc = wave_inclusive_scan(v);
+    if (lane == WAVE - 1) lds_waves[wave] = inc;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+    const int nw = blockDim.x / WAVE;
+    for (int w = 0; w < nw; ++w) {
+        uint32_t x = lds_waves[w];
+        if (w < wave) base += x;
+        tot += x;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + inc - v;
+}
+
+// Pass A: per-tile scan into out, tile totals into partials.
+template <bool EXCLUSIVE>
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_tiles(const uint32_t *__restrict__ in,
+                                                             uint32_t *__restrict__ out, int64_t n,
+                                                             uint32_t *__restrict__ partials) {
+    __shared__ uint32_t tile[SCAN_TILE];
+    __shared__ uint32_t waves[SCAN_THREADS / WAVE];
+    const int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        int64_t i = base + j * SCAN_THREADS + threadIdx.x;
+        tile[j * SCAN_THREADS + threadIdx.x] = i < n ? in[i] : 0u;
+    }
+    __syncthreads();
+    uint32_t loc[SCAN_ITEMS];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        loc[j] = tile[threadIdx.x * SCAN_ITEMS + j];
+        sum += loc[j];
+    }
+    uint32_t total;
+    uint32_t run = block_exclusive_scan(sum, waves, &total);
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        uint32_t x = loc[j];
+        if (EXCLUSIVE) { tile[threadIdx.x * SCAN_ITEMS + j] = run; run += x; }
+        else { run += x; tile[threadIdx.x * SCAN_ITEMS + j] = run; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        int64_t i = base + j * SCAN_THREADS + threadIdx.x;
+        if (i < n) out[i] = tile[j * SCAN_THREADS + threadIdx.x];
+    }
+    if (threadIdx.x == 0) partials[blockIdx.x] = total;
+}
+
+// Pass B: exclusive scan of the tile totals, one workgroup; total into *grand_total.
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_partials(uint32_t *partials, int64_t nparts,
+                                                                uint32_t *grand_total) {
+    __shared__ uint32_t waves[SCAN_THREADS / WAVE];
+    uint32_t carry = 0;
+    for (int64_t b = 0; b < nparts; b += SCAN_THREADS) {
+        int64_t i = b + threadIdx.x;
+        uint32_t v = i < nparts ? partials[i] : 0u;
+        uint32_t total;
+        uint32_t ex = block_exclusive_scan(v, waves, &total);
+        if (i < nparts) partials[i] = carry + ex;
+        carry += total;
+    }
+    if (threadIdx.x == 0 && grand_total) *grand_total = carry;
+}
+
+// Pass C: add the tile offsets.
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_add(uint32_t *__restrict__ out, int64_t n,
+                                                           const uint32_t *__restrict__ partials) {
+    const uint32_t off = partials[blockIdx.x];
+    if (off == 0) return;
+    const int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        int64_t i = base + j * SCAN_THREADS + threadIdx.x;
+        if (i < n) out[i] += off;
+    }
+}
+
+inline int64_t scan_parts(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
+
+// Device-wide scan (in may alias out).  partials needs scan_parts(n) words.
+template <bool EXCLUSIVE>
+inline void device_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *partials,
+                        uint32_t *grand_total, hipStream_t s) {
+    if (n <= 0) return;
+    const int64_t nb = scan_parts(n);
+    k_scan_tiles<EXCLUSIVE><<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(in, out, n, partials);
+    k_scan_partials<<<1, SCAN_THREADS, 0, s>>>(partials, nb, grand_total);
+    k_scan_add<<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(out, n, partials);
+}
+
+// ---------------------------------------------------------------- radix sort
+
+__global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t *__restrict__ keys, int64_t n,
+                                                             int shift, uint32_t *__restrict__ hist,
+                                                             int64_t nblocks) {
+    __shared__ uint32_t h[RADIX];
+    for (int d = threadIdx.x; d < RADIX; d += SORT_THREADS) h[d] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * SORT_TILE;
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        int64_t i = base + j * SORT_THREADS + threadIdx.x;
+        if (i < n) atomicAdd(&h[(keys[i] >> shift) & (RADIX - 1)], 1u);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < RADIX; d += SORT_THREADS) hist[(int64_t)d * nblocks + blockIdx.x] = h[d];
+}
+
+// Stable scatter.  offsets = exclusive scan of the digit-major histogram.
+// vals_in == nullptr means "value = index" (first pass: seq is implicit).
+__global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
+    const uint32_t *__restrict__ keys_in, const uint32_t *__restrict__ vals_in,
+    uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out, int64_t n, int shift,
+    const uint32_t *__restrict__ offsets, int64_t nblocks) {
+    __shared__ uint32_t cnt[SORT_WAVES][RADIX];
+    __shared__ uint32_t goff[RADIX];
+    const int wave = threadIdx.x / WAVE;
+    const uint32_t lane = lane_id();
+    for (int d = threadIdx.x; d < RADIX; d += SORT_THREADS) {
+#pragma unroll
+        for (int w = 0; w < SORT_WAVES; ++w) cnt[w][d] = 0;
+        goff[d] = offsets[(int64_t)d * nblocks + blockIdx.x];
+    }
+    __syncthreads();
+
+    const int64_t base = (int64_t)blockIdx.x * SORT_TILE + (int64_t)wave * (SORT_ITEMS * WAVE);
+    uint32_t key[SORT_ITEMS], val[SORT_ITEMS], rank[SORT_ITEMS];
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const int64_t i = base + j * WAVE + lane;
+        const bool valid = i < n;
+        key[j] = valid ? keys_in[i] : 0u;
+        val[j] = valid ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
+        const uint32_t d = (key[j] >> shift) & (RADIX - 1);
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < RADIX_BITS; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bal = __ballot(valid && bit);
+            peers &= bit ? bal : ~bal;
+        }
+        uint32_t r = 0;
+        if (valid) {
+            r = cnt[wave][d] + mask_rank(peers);
+        }
+        // every lane has read its counter; the group leader publishes the new count
+        __builtin_amdgcn_wave_barrier();
+        if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane)
+            cnt[wave][d] += (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        rank[j] = valid ? r : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < RADIX; d += SORT_THREADS) {
+        uint32_t run = 0;
+#pragma unroll
+        for (int w = 0; w < SORT_WAVES; ++w) {
+            uint32_t c = cnt[w][d];
+            cnt[w][d] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        if (rank[j] == 0xFFFFFFFFu) continue;
+        const uint32_t d = (key[j] >> shift) & (RADIX - 1);
+        const uint32_t dst = goff[d] + cnt[wave][d] + rank[j];
+        keys_out[dst] = key[j];
+        vals_out[dst] = val[j];
+    }
+}
+
+inline int64_t sort_blocks(int64_t n) { return (n + SORT_TILE - 1) / SORT_TILE; }
+
+// Workspace sizing for radix_sort_pairs.
+inline int64_t sort_hist_words(int64_t n) { return sort_blocks(n) * RADIX; }
+
+// Sorts (keys, vals=seq) by the low `bits` bits of the key.  Results land in (k_out, v_out);
+// (k_tmp, v_tmp) are ping-pong buffers.  keys_in is not modified.
+inline void radix_sort_pairs(const uint32_t *keys_in, int64_t n, int bits, uint32_t *k_out, uint32_t *v_out,
+                             uint32_t *k_tmp, uint32_t *v_tmp, uint32_t *hist, uint32_t *partials,
+                             hipStream_t s) {
+    if (n <= 0) return;
+    const int64_t nb = sort_blocks(n);
+    const int passes = bits <= 0 ? 1 : (bits + RADIX_BITS - 1) / RADIX_BITS;
+    // choose buffer order so the last pass writes (k_out, v_out)
+    uint32_t *kb[2], *vb[2];
+    if (passes % 2 == 1) { kb[0] = k_out; vb[0] = v_out; kb[1] = k_tmp; vb[1] = v_tmp; }
+    else { kb[0] = k_tmp; vb[0] = v_tmp; kb[1] = k_out; vb[1] = v_out; }
+    const uint32_t *kin = keys_in;
+    const uint32_t *vin = nullptr;
+    for (int p = 0; p < passes; ++p) {
+        const int shift = p * RADIX_BITS;
+        k_radix_hist<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(kin, n, shift, hist, nb);
+        device_scan<true>(hist, hist, nb * RADIX, partials, nullptr, s);
+        k_radix_scatter<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(kin, vin, kb[p % 2], vb[p % 2], n,
+                                                                          shift, hist, nb);
+        kin = kb[p % 2];
+        vin = vb[p % 2];
+    }
+}
+
+}  // namespace sentinel

@@ -1,0 +1,326 @@
+"""Host-side mirror of Sentinel's cluster TokenService SPI over the MI355X engine.
+
+Mirrors (paths relative to the reference repo):
+  TokenService        sentinel-core/src/main/java/com/alibaba/csp/sentinel/cluster/TokenService.java:26-63
+  TokenResult         sentinel-core/src/main/java/com/alibaba/csp/sentinel/cluster/TokenResult.java:26-98
+  TokenResultStatus   sentinel-core/src/main/java/com/alibaba/csp/sentinel/cluster/TokenResultStatus.java:22-73
+  ClusterFlowConfig   sentinel-core/src/main/java/com/alibaba/csp/sentinel/slots/block/flow/ClusterFlowConfig.java:39-51
+  DefaultTokenService sentinel-cluster/sentinel-cluster-server-default/.../cluster/flow/DefaultTokenService.java:37-62
+
+The per-call methods (request_token / request_param_token) keep the reference's names, argument
+meaning and error convention (status codes, never exceptions for bad input).  The batched methods
+(submit_*) are the hot path: one call decides a whole batch of events on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import time
+from dataclasses import dataclass, field
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import SentinelError, check
+
+
+class TokenResultStatus:
+    BAD_REQUEST = -4
+    TOO_MANY_REQUEST = -2
+    FAIL = -1
+    OK = 0
+    BLOCKED = 1
+    SHOULD_WAIT = 2
+    NO_RULE_EXISTS = 3
+    NO_REF_RULE_EXISTS = 4
+    NOT_AVAILABLE = 5
+    RELEASE_OK = 6
+    ALREADY_RELEASE = 7
+
+
+class ClusterRuleConstant:
+    FLOW_THRESHOLD_AVG_LOCAL = 0
+    FLOW_THRESHOLD_GLOBAL = 1
+    DEFAULT_CLUSTER_SAMPLE_COUNT = 10
+
+
+@dataclass
+class TokenResult:
+    status: int
+    remaining: int = 0
+    wait_in_ms: int = 0
+    token_id: int = 0
+
+
+@dataclass
+class ClusterFlowConfig:
+    flow_id: Optional[int] = None
+    threshold_type: int = ClusterRuleConstant.FLOW_THRESHOLD_AVG_LOCAL
+    sample_count: int = ClusterRuleConstant.DEFAULT_CLUSTER_SAMPLE_COUNT
+    window_interval_ms: int = 1000
+    fallback_to_local_when_fail: bool = True
+
+
+@dataclass
+class FlowRule:
+    """Cluster-mode FlowRule (only the fields the cluster checkers read)."""
+    resource: str = ""
+    count: float = 0.0
+    cluster_mode: bool = True
+    cluster_config: ClusterFlowConfig = field(default_factory=ClusterFlowConfig)
+    namespace: int = 0                 # index into the server namespace set
+    checker: int = _lib.CHECKER_CLUSTER
+
+
+@dataclass
+class ParamFlowRule:
+    resource: str = ""
+    count: float = 0.0
+    cluster_config: ClusterFlowConfig = field(default_factory=ClusterFlowConfig)
+    namespace: int = 0
+    hot_items: dict = field(default_factory=dict)   # param key -> int count
+
+
+@dataclass
+class ServerNamespace:
+    connected_count: int = 0
+    has_limiter: bool = False
+    max_allowed_qps: float = 30000.0   # ServerFlowConfig.DEFAULT_MAX_ALLOWED_QPS
+
+
+def _p(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def _now_ms() -> int:
+    return int(time.time() * 1000)
+
+
+class GpuTokenService:
+    """TokenService implemented on one MI355X (one shard of the flowId space)."""
+
+    def __init__(self, device: int = 0, exceed_count: float = 1.0, max_occupy_ratio: float = 1.0,
+                 namespaces: Optional[Sequence[ServerNamespace]] = None):
+        self._L = _lib.load()
+        self._h = C.c_void_p()
+        cfg = _lib.ServerConfig(exceed_count, max_occupy_ratio)
+        check(self._L.sentinel_engine_create(device, C.byref(cfg), C.byref(self._h)), "sentinel_engine_create")
+        self.device = device
+        self.sample_counts = {}
+        self._flow_rules = []
+        if namespaces is not None:
+            self.set_namespaces(namespaces)
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._L.sentinel_engine_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def stream(self) -> int:
+        return int(self._L.sentinel_engine_stream(self._h) or 0)
+
+    # ---------------------------------------------------------------- config
+    def set_server_config(self, exceed_count=1.0, max_occupy_ratio=1.0):
+        cfg = _lib.ServerConfig(exceed_count, max_occupy_ratio)
+        check(self._L.sentinel_set_server_config(self._h, C.byref(cfg)), "set_server_config")
+
+    def set_namespaces(self, namespaces: Sequence[ServerNamespace]):
+        arr = (_lib.Namespace * max(len(namespaces), 1))()
+        for i, ns in enumerate(namespaces):
+            arr[i] = _lib.Namespace(int(ns.connected_count), int(bool(ns.has_limiter)), float(ns.max_allowed_qps))
+        check(self._L.sentinel_set_namespaces(self._h, arr, len(namespaces)), "set_namespaces")
+
+    def set_connected_count(self, namespace: int, connected: int):
+        check(self._L.sentinel_set_connected_count(self._h, namespace, connected), "set_connected_count")
+
+    def load_flow_rules(self, rules: Sequence[FlowRule]):
+        """ClusterFlowRuleManager.loadRules for the server (ClusterFlowRuleManager.java:325-372)."""
+        arr = (_lib.FlowRuleC * max(len(rules), 1))()
+        for i, r in enumerate(rules):
+            cc = r.cluster_config
+            fid = cc.flow_id if cc.flow_id is not None else 0
+            arr[i] = _lib.FlowRuleC(int(fid), float(r.count), int(cc.threshold_type), int(cc.sample_count),
+                                    int(cc.window_interval_ms), int(r.namespace), int(r.checker), 0)
+        check(self._L.sentinel_load_flow_rules(self._h, arr, len(rules)), "load_flow_rules")
+        self._flow_rules = list(rules)
+
+    def load_rules_array(self, flow_ids, counts, threshold_type=1, sample_count=10, window_interval_ms=1000,
+                         namespace=0, checker=0):
+        """Vectorised rule load for large synthetic tables (1M flows)."""
+        n = len(flow_ids)
+        rec = np.zeros(n, dtype=[("flow_id", "<i8"), ("count", "<f8"), ("threshold_type", "<i4"),
+                                 ("sample_count", "<i4"), ("window_interval_ms", "<i4"),
+                                 ("namespace_idx", "<i4"), ("checker", "<i4"), ("reserved", "<i4")])
+        rec["flow_id"] = flow_ids
+        rec["count"] = counts
+        rec["threshold_type"] = threshold_type
+        rec["sample_count"] = sample_count
+        rec["window_interval_ms"] = window_interval_ms
+        rec["namespace_idx"] = namespace
+        rec["checker"] = checker
+        check(self._L.sentinel_load_flow_rules(self._h, C.c_void_p(rec.ctypes.data), n), "load_flow_rules")
+
+    def load_param_rules(self, rules: Sequence[ParamFlowRule]):
+        arr = (_lib.ParamRuleC * max(len(rules), 1))()
+        keys, counts = [], []
+        for i, r in enumerate(rules):
+            cc = r.cluster_config
+            fid = cc.flow_id if cc.flow_id is not None else 0
+            arr[i] = _lib.ParamRuleC(int(fid), float(r.count), int(cc.threshold_type), int(cc.sample_count),
+                                     int(cc.window_interval_ms), int(r.namespace), len(keys), len(r.hot_items))
+            for k, c in r.hot_items.items():
+                keys.append(k)
+                counts.append(c)
+        hk = np.array(keys or [0], dtype=np.uint64)
+        hc = np.array(counts or [0], dtype=np.int32)
+        check(self._L.sentinel_load_param_rules(self._h, arr, len(rules), _p(hk), _p(hc), len(keys)),
+              "load_param_rules")
+
+    def flow_count(self) -> int:
+        return int(self._L.sentinel_flow_count(self._h))
+
+    def lookup_flow_idx(self, flow_ids) -> np.ndarray:
+        ids = np.ascontiguousarray(flow_ids, dtype=np.int64)
+        out = np.empty(len(ids), dtype=np.int32)
+        check(self._L.sentinel_lookup_flow_idx(self._h, len(ids), _p(ids), _p(out)), "lookup_flow_idx")
+        return out
+
+    def lookup_param_idx(self, flow_ids) -> np.ndarray:
+        ids = np.ascontiguousarray(flow_ids, dtype=np.int64)
+        out = np.empty(len(ids), dtype=np.int32)
+        check(self._L.sentinel_lookup_param_idx(self._h, len(ids), _p(ids), _p(out)), "lookup_param_idx")
+        return out
+
+    # ---------------------------------------------------------------- TokenService (per call)
+    def request_token(self, rule_id: Optional[int], acquire_count: int, prioritized: bool,
+                      ts: Optional[int] = None) -> TokenResult:
+        """TokenService.requestToken (TokenService.java:36)."""
+        out = _lib.TokenResultC()
+        fid = 0 if rule_id is None else int(rule_id)
+        rc = self._L.sentinel_request_token(self._h, fid, int(acquire_count), int(bool(prioritized)),
+                                            _now_ms() if ts is None else int(ts), C.byref(out))
+        check(rc, "request_token")
+        return TokenResult(out.status, out.remaining, out.wait_in_ms)
+
+    def request_param_token(self, rule_id: Optional[int], acquire_count: int, params: Iterable[int],
+                            ts: Optional[int] = None) -> TokenResult:
+        """TokenService.requestParamToken (TokenService.java:46) for one parameter value.  Values are
+        64-bit param keys (the host's injective encoding of the Java typed value)."""
+        params = list(params) if params is not None else []
+        if rule_id is None or int(rule_id) <= 0 or acquire_count <= 0 or not params:
+            return TokenResult(TokenResultStatus.BAD_REQUEST)       # DefaultTokenService.java:53-55
+        if len(params) != 1:
+            raise NotImplementedError("multi-value param requests: round-2 item (sequential all-or-nothing path)")
+        out = _lib.TokenResultC()
+        check(self._L.sentinel_request_param_token(self._h, int(rule_id), int(acquire_count), int(params[0]),
+                                                   _now_ms() if ts is None else int(ts), C.byref(out)),
+              "request_param_token")
+        return TokenResult(out.status, out.remaining, out.wait_in_ms)
+
+    def request_concurrent_token(self, client_address, rule_id, acquire_count):
+        raise NotImplementedError("concurrent (thread-grade) cluster tokens are a SURVEY §8(f) 'next' row")
+
+    def release_concurrent_token(self, token_id):
+        raise NotImplementedError("concurrent (thread-grade) cluster tokens are a SURVEY §8(f) 'next' row")
+
+    # ---------------------------------------------------------------- batched hot path
+    def submit_flow_batch(self, flow_idx, acquire, ts, flags=None, status=None, remaining=None, wait_ms=None,
+                          stream=None):
+        """Decide a batch of device-resident events (torch tensors on this GPU).  Asynchronous on
+        `stream` (a torch.cuda.Stream or raw hipStream_t int; default: the engine stream)."""
+        import torch
+        n = int(flow_idx.numel())
+        dev = flow_idx.device
+        if status is None:
+            status = torch.empty(n, dtype=torch.int8, device=dev)
+        if remaining is None:
+            remaining = torch.empty(n, dtype=torch.int32, device=dev)
+        s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        rc = self._L.sentinel_submit_flow_batch(
+            self._h, n, C.c_void_p(flow_idx.data_ptr()), C.c_void_p(acquire.data_ptr()),
+            None if flags is None else C.c_void_p(flags.data_ptr()), C.c_void_p(ts.data_ptr()),
+            C.c_void_p(status.data_ptr()), C.c_void_p(remaining.data_ptr()),
+            None if wait_ms is None else C.c_void_p(wait_ms.data_ptr()), None if s is None else C.c_void_p(s))
+        check(rc, "submit_flow_batch")
+        return status, remaining, wait_ms
+
+    def submit_flow_batch_host(self, flow_idx, acquire, ts, flags=None):
+        n = len(ts)
+        flow_idx = np.ascontiguousarray(flow_idx, dtype=np.int32)
+        acquire = np.ascontiguousarray(acquire, dtype=np.int32)
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        flags = None if flags is None else np.ascontiguousarray(flags, dtype=np.uint8)
+        status = np.empty(n, dtype=np.int8)
+        remaining = np.empty(n, dtype=np.int32)
+        wait = np.empty(n, dtype=np.int32)
+        check(self._L.sentinel_submit_flow_batch_host(self._h, n, _p(flow_idx), _p(acquire), _p(flags), _p(ts),
+                                                      _p(status), _p(remaining), _p(wait)), "submit_flow_batch_host")
+        return status, remaining, wait
+
+    def submit_param_batch(self, rule_idx, acquire, param_key, ts, status=None, remaining=None, stream=None):
+        import torch
+        n = int(rule_idx.numel())
+        dev = rule_idx.device
+        if status is None:
+            status = torch.empty(n, dtype=torch.int8, device=dev)
+        if remaining is None:
+            remaining = torch.empty(n, dtype=torch.int32, device=dev)
+        s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        check(self._L.sentinel_submit_param_batch(
+            self._h, n, C.c_void_p(rule_idx.data_ptr()), C.c_void_p(acquire.data_ptr()),
+            C.c_void_p(param_key.data_ptr()), C.c_void_p(ts.data_ptr()), C.c_void_p(status.data_ptr()),
+            C.c_void_p(remaining.data_ptr()), None if s is None else C.c_void_p(s)), "submit_param_batch")
+        return status, remaining
+
+    def submit_param_batch_host(self, rule_idx, acquire, param_key, ts):
+        n = len(ts)
+        rule_idx = np.ascontiguousarray(rule_idx, dtype=np.int32)
+        acquire = np.ascontiguousarray(acquire, dtype=np.int32)
+        param_key = np.ascontiguousarray(param_key, dtype=np.uint64)
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        status = np.empty(n, dtype=np.int8)
+        remaining = np.empty(n, dtype=np.int32)
+        check(self._L.sentinel_submit_param_batch_host(self._h, n, _p(rule_idx), _p(acquire), _p(param_key), _p(ts),
+                                                       _p(status), _p(remaining)), "submit_param_batch_host")
+        return status, remaining
+
+    def synchronize(self):
+        check(self._L.sentinel_synchronize(self._h), "synchronize")
+
+    # ---------------------------------------------------------------- observability
+    def dump_flow(self, idx: int, sample_count: int) -> np.ndarray:
+        out = np.zeros(sample_count * 8 + 8, dtype=np.int64)
+        check(self._L.sentinel_dump_flow(self._h, int(idx), _p(out), len(out)), "dump_flow")
+        return out
+
+    def param_sum(self, rule_idx: int, key: int, ts: int) -> int:
+        v = C.c_int64()
+        check(self._L.sentinel_param_sum(self._h, rule_idx, key, ts, C.byref(v)), "param_sum")
+        return v.value
+
+    def snapshot(self, ts: int) -> np.ndarray:
+        n = self.flow_count()
+        out = np.zeros(n, dtype=[("flow_id", "<i8"), ("pass_qps", "<f8"), ("block_qps", "<f8")])
+        check(self._L.sentinel_snapshot(self._h, int(ts), C.c_void_p(out.ctypes.data)), "snapshot")
+        return out
+
+    def snapshot_device(self, ts: int, out_tensor, stream=None):
+        s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        check(self._L.sentinel_snapshot_device(self._h, int(ts), C.c_void_p(out_tensor.data_ptr()),
+                                               None if s is None else C.c_void_p(s)), "snapshot_device")
+        return out_tensor
+
+
+def device_count() -> int:
+    return int(_lib.load().sentinel_device_count())
