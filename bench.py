@@ -29,17 +29,14 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-leve
 
 # Algorithmic bytes per processed event for each kernel of the pipeline (DESIGN.md "Kernels").
 KERNEL_BYTES_PER_EVENT = {
-    "flow_prep": 20.0,        # read flow_idx 4 + acquire 4 + ts 8, write key 4
+    "flow_prep": 20.0,        # read the 16-B event, write the 4-B sort key (histograms stay in LDS)
     "radix_hist": 4.0,        # read key
     "radix_scatter": 16.0,    # read key+seq, write key+seq (first pass reads key only: 12)
     "scan_tiles": 8.0,
     "scan_add": 8.0,
-    "count_valid": 4.0,
-    "gather_sorted": 33.0,    # read skey+sseq 8, gather ts 8 + acquire 4 + flags 1, write epoch 8 + acq 4 + fl 1
-    "heads": 16.0,            # read skey 4 + epoch 8, write head 4
-    "seg_start": 4.0,
-    "seg_het": 13.0,
-    "verdict": 25.0,          # read segid 4 + sseq 4 + skey 4 + acq 4 + segment record ~8, write status 1 + remaining 4
+    "seg_heads": 29.0,        # read skey+sseq 8, gather the 16-B event, write head 4 + bad 1
+    "seg_mark": 5.0,          # read segid 4 + bad 1 (segment records are per segment)
+    "verdict": 16.0,          # read segid 4 + sseq 4, write the 8-B verdict
 }
 
 
@@ -90,35 +87,37 @@ def main():
     rate = 2.0 * float(shard.count.sum())          # offered rate: 2x the shard's thresholds (per second)
     ms_per_event = 1000.0 / rate
     t0 = T.T0_ALIGNED
+    from sentinel_amd.token_service import device_events
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
-    idx_b, ts_b = [], []
-    for s in range(steps_total):
-        idx_b.append(torch.randint(0, F, (N,), dtype=torch.int32, device=dev, generator=gen))
-        base = torch.arange(s * N, (s + 1) * N, device=dev, dtype=torch.float64)
-        ts_b.append((t0 + torch.floor(base * ms_per_event)).to(torch.int64))
+    ev_b = []
     acq = torch.ones(N, dtype=torch.int32, device=dev)
-    status = torch.empty(N, dtype=torch.int8, device=dev)
-    remaining = torch.empty(N, dtype=torch.int32, device=dev)
+    for s in range(steps_total):
+        idx = torch.randint(0, F, (N,), dtype=torch.int32, device=dev, generator=gen)
+        base = torch.arange(s * N, (s + 1) * N, device=dev, dtype=torch.float64)
+        ts = (t0 + torch.floor(base * ms_per_event)).to(torch.int64)
+        ev_b.append(device_events(idx, acq, ts))
+        del idx, base, ts
+    verdicts = torch.empty(N, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
 
     ext = torch.cuda.ExternalStream(svc.stream, device=dev)
     for s in range(args.warmup):
-        svc.submit_flow_batch(idx_b[s], acq, ts_b[s], status=status, remaining=remaining)
+        svc.submit_flow_batch(ev_b[s], verdicts=verdicts)
     svc.synchronize()
 
     if not args.no_profile:
         svc._L.sentinel_profile_enable(svc.handle, 1)
-    ev_a = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ev_b = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    tev_a = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    tev_b = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for k in range(args.steps):
         s = args.warmup + k
-        ev_a[k].record(ext)
-        svc.submit_flow_batch(idx_b[s], acq, ts_b[s], status=status, remaining=remaining)
-        ev_b[k].record(ext)
+        tev_a[k].record(ext)
+        svc.submit_flow_batch(ev_b[s], verdicts=verdicts)
+        tev_b[k].record(ext)
     svc.synchronize()
     torch.cuda.synchronize()
     if world > 1:
@@ -128,7 +127,7 @@ def main():
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
-    lat = sorted(ev_a[k].elapsed_time(ev_b[k]) for k in range(args.steps))
+    lat = sorted(tev_a[k].elapsed_time(tev_b[k]) for k in range(args.steps))
     p99 = lat[min(len(lat) - 1, int(np.ceil(0.99 * len(lat))) - 1)]
 
     # ---- per-kernel profile (HIP events on the engine stream, over the timed region)
@@ -148,7 +147,7 @@ def main():
         svc._L.sentinel_profile_enable(svc.handle, 0)
 
     # ---- snapshot + RCCL all-gather (config 3's ClusterMetric snapshot; off the decision path)
-    t_snap = int(ts_b[-1][-1].item()) + 1
+    t_snap = int(ev_b[-1][-1, 1].item()) + 1
     snap = torch.empty((F, 3), dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
     ts0 = time.perf_counter()
@@ -191,8 +190,9 @@ def main():
         m = min(args.cpu_sample_events, N)
         orc = O.TokenServiceOracle.from_arrays(shard.flow_id, shard.count, shard.threshold_type, shard.sample_count,
                                                shard.window_interval_ms, shard.namespace, shard.checker)
-        idx_c = idx_b[0][:m].cpu().numpy()
-        ts_c = ts_b[0][:m].cpu().numpy()
+        e0 = ev_b[0][:m].cpu().numpy()
+        idx_c = (e0[:, 0] & 0xFFFFFFFF).astype(np.int32)
+        ts_c = e0[:, 1].copy()
         acq_c = np.ones(m, np.int32)
         c0 = time.perf_counter()
         orc.replay(idx_c, acq_c, ts_c)

@@ -144,23 +144,44 @@ int  sentinel_lookup_flow_idx(sentinel_engine_t *eng, int64_t n, const int64_t *
 int  sentinel_lookup_param_idx(sentinel_engine_t *eng, int64_t n, const int64_t *flow_ids, int32_t *idx_out);
 
 /* ---- the batched hot path: DefaultTokenService.requestToken over a batch ----
- * Events in arrival (seq) order; pointers are DEVICE pointers; `stream` is a hipStream_t (NULL =
- * the engine's stream).  Verdicts equal a sequential replay of the batch through the reference
- * checker with the given timestamps.  flags and wait_ms may be NULL. Asynchronous. */
-int  sentinel_submit_flow_batch(sentinel_engine_t *eng, int64_t n, const int32_t *flow_idx,
-                                const int32_t *acquire, const uint8_t *flags, const int64_t *ts,
-                                int8_t *status, int32_t *remaining, int32_t *wait_ms, void *stream);
+ * Events in arrival (seq) order; verdicts land at the same positions.  Verdicts equal a
+ * sequential replay of the batch through the reference checker with the given timestamps. */
+
+/* One requestToken call (TokenService.java:36): ruleId -> dense flow index (see lookup), acquireCount,
+ * and the TimeUtil.currentTimeMillis() value of the call.  16 bytes. */
+typedef struct {
+    int32_t flow_idx;
+    int32_t acquire;
+    int64_t ts;
+} sentinel_event_t;
+
+/* One single-value requestParamToken call (TokenService.java:46).  param_key is the host's
+ * injective 64-bit encoding of (rule, Java-typed value); 0xFFFFFFFFFFFFFFFF is reserved.  24 bytes. */
+typedef struct {
+    int32_t rule_idx;
+    int32_t acquire;
+    int64_t ts;
+    uint64_t param_key;
+} sentinel_param_event_t;
+
+/* Packed TokenResult {status, remaining, waitInMs}: one 8-byte store per event. */
+typedef struct {
+    int32_t  remaining;
+    int16_t  status;
+    uint16_t wait_in_ms;
+} sentinel_verdict_t;
+
+/* DEVICE pointers; flags (bit0 = prioritized) may be NULL; `stream` is a hipStream_t (NULL = the
+ * engine's stream).  Asynchronous. */
+int  sentinel_submit_flow_batch(sentinel_engine_t *eng, int64_t n, const sentinel_event_t *events,
+                                const uint8_t *flags, sentinel_verdict_t *verdicts, void *stream);
 /* Same with HOST pointers (pinned or pageable): H2D, decide, D2H, synchronous. */
-int  sentinel_submit_flow_batch_host(sentinel_engine_t *eng, int64_t n, const int32_t *flow_idx,
-                                     const int32_t *acquire, const uint8_t *flags, const int64_t *ts,
-                                     int8_t *status, int32_t *remaining, int32_t *wait_ms);
-/* Single-value DefaultTokenService.requestParamToken over a batch (DEVICE pointers). */
-int  sentinel_submit_param_batch(sentinel_engine_t *eng, int64_t n, const int32_t *rule_idx,
-                                 const int32_t *acquire, const uint64_t *param_key, const int64_t *ts,
-                                 int8_t *status, int32_t *remaining, void *stream);
-int  sentinel_submit_param_batch_host(sentinel_engine_t *eng, int64_t n, const int32_t *rule_idx,
-                                      const int32_t *acquire, const uint64_t *param_key, const int64_t *ts,
-                                      int8_t *status, int32_t *remaining);
+int  sentinel_submit_flow_batch_host(sentinel_engine_t *eng, int64_t n, const sentinel_event_t *events,
+                                     const uint8_t *flags, sentinel_verdict_t *verdicts);
+int  sentinel_submit_param_batch(sentinel_engine_t *eng, int64_t n, const sentinel_param_event_t *events,
+                                 sentinel_verdict_t *verdicts, void *stream);
+int  sentinel_submit_param_batch_host(sentinel_engine_t *eng, int64_t n, const sentinel_param_event_t *events,
+                                      sentinel_verdict_t *verdicts);
 
 /* ---- per-call TokenService mirror (one event, synchronous) ---- */
 int  sentinel_request_token(sentinel_engine_t *eng, int64_t flow_id, int32_t acquire_count,

@@ -8,6 +8,8 @@ from __future__ import annotations
 import ctypes as C
 import os
 
+import numpy as np
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsentinel_amd.so")
 
@@ -71,6 +73,12 @@ class FlowSnapshotC(C.Structure):
     _fields_ = [("flow_id", C.c_int64), ("pass_qps", C.c_double), ("block_qps", C.c_double)]
 
 
+# AoS records of include/sentinel_amd.h
+EVENT_DTYPE = np.dtype([("flow_idx", "<i4"), ("acquire", "<i4"), ("ts", "<i8")])
+PARAM_EVENT_DTYPE = np.dtype([("rule_idx", "<i4"), ("acquire", "<i4"), ("ts", "<i8"), ("param_key", "<u8")])
+VERDICT_DTYPE = np.dtype([("remaining", "<i4"), ("status", "<i2"), ("wait_in_ms", "<u2")])
+
+
 class SentinelError(RuntimeError):
     pass
 
@@ -104,10 +112,10 @@ def load():
         "sentinel_flow_count": (i32, [vp]),
         "sentinel_lookup_flow_idx": (C.c_int, [vp, i64, vp, vp]),
         "sentinel_lookup_param_idx": (C.c_int, [vp, i64, vp, vp]),
-        "sentinel_submit_flow_batch": (C.c_int, [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
-        "sentinel_submit_flow_batch_host": (C.c_int, [vp, i64, vp, vp, vp, vp, vp, vp, vp]),
-        "sentinel_submit_param_batch": (C.c_int, [vp, i64, vp, vp, vp, vp, vp, vp, vp]),
-        "sentinel_submit_param_batch_host": (C.c_int, [vp, i64, vp, vp, vp, vp, vp, vp]),
+        "sentinel_submit_flow_batch": (C.c_int, [vp, i64, vp, vp, vp, vp]),
+        "sentinel_submit_flow_batch_host": (C.c_int, [vp, i64, vp, vp, vp]),
+        "sentinel_submit_param_batch": (C.c_int, [vp, i64, vp, vp, vp]),
+        "sentinel_submit_param_batch_host": (C.c_int, [vp, i64, vp, vp]),
         "sentinel_request_token": (C.c_int, [vp, i64, i32, i32, i64, vp]),
         "sentinel_request_param_token": (C.c_int, [vp, i64, i32, u64, i64, vp]),
         "sentinel_synchronize": (C.c_int, [vp]),

@@ -4,11 +4,12 @@
 // The batched path replaces DefaultTokenService.requestToken / requestParamToken
 // (srv/flow/DefaultTokenService.java:37-62) for a whole batch of events at once:
 //
-//   k_flow_prep     validation + rule lookup + namespace check (DTS:37-48, CFC:50-60)
+//   k_flow_prep     validation + rule lookup + namespace routing (DTS:37-48, CFC:50-60), and the
+//                   digit histograms of every radix pass (one read of the batch)
 //   [limiter run]   GlobalRequestLimiter.tryPass per namespace (GlobalRequestLimiter.java:46-55)
-//   K2 radix sort   group by flow, keep arrival order
-//   K1+K3           window roll + segmented admission (admission.hpp)
-//   verdict         scatter {status, remaining, waitInMs} back to arrival order
+//   K2 radix sort   group by flow, keep arrival order (scan_sort.hpp)
+//   K1+K3           segment heads, window roll + segmented admission (admission.hpp)
+//   verdict         scatter packed {remaining, status, waitInMs} back to arrival order
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -27,6 +28,10 @@
 #include "scan_sort.hpp"
 
 using namespace sentinel;
+
+static_assert(sizeof(Event) == sizeof(sentinel_event_t), "event layout");
+static_assert(sizeof(ParamEvent) == sizeof(sentinel_param_event_t), "param event layout");
+static_assert(sizeof(sentinel_verdict_t) == 8, "verdict layout");
 
 namespace {
 
@@ -48,6 +53,8 @@ int bits_for(int64_t nkeys) {     // smallest b with 2^b - 1 >= nkeys (room for 
     while (((int64_t)1 << b) - 1 < nkeys) ++b;
     return b;
 }
+
+constexpr int64_t MAX_BATCH = (int64_t)1 << 28;
 
 struct DevBuf {
     void *p = nullptr;
@@ -86,48 +93,9 @@ struct TableBufs {
     }
 };
 
-// ------------------------------------------------------------------ prep kernels
+constexpr int32_t ROUTE_TOO_MANY = -1;   // CLUSTER rule whose namespace is null (GRL:47-49)
+constexpr int32_t ROUTE_PLAIN = -2;      // no limiter for the namespace (GRL:51-53)
 
-// DefaultTokenService.requestToken validation (DTS:37-48) + namespace / limiter routing
-// (ClusterFlowChecker.allowProceed, CFC:50-53).  Decided events get their final verdict here.
-__global__ __launch_bounds__(256) void k_flow_prep(int64_t n, const int32_t *__restrict__ flow_idx,
-                                                   const int32_t *__restrict__ acquire,
-                                                   const int64_t *__restrict__ ts, int32_t nflows,
-                                                   const int32_t *__restrict__ flow_ns,
-                                                   const uint8_t *__restrict__ flow_kind,
-                                                   const int32_t *__restrict__ ns_limiter, int32_t nns,
-                                                   int8_t *status, int32_t *remaining, int32_t *wait_ms,
-                                                   uint32_t *fkey, uint32_t finvalid, uint32_t *lkey,
-                                                   uint32_t linvalid) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int32_t idx = flow_idx[i];
-    const int32_t a = acquire[i];
-    int8_t st = 127;   // undecided
-    uint32_t k = finvalid, l = linvalid;
-    if (idx == SENTINEL_IDX_BAD_ID || a <= 0) st = ST_BAD_REQUEST;
-    else if (idx < 0 || idx >= nflows) st = ST_NO_RULE_EXISTS;
-    else {
-        if (flow_kind[idx] == KIND_CLUSTER) {
-            const int32_t ns = flow_ns[idx];
-            if (ns < 0 || ns >= nns) st = ST_TOO_MANY_REQUEST;        // namespace == null
-            else if (ns_limiter[ns] >= 0) l = (uint32_t)ns_limiter[ns];
-        }
-        if (st == 127 && ts[i] < 0) st = ST_FAIL;                    // reference: NPE in LeapArray
-        if (st == 127) k = (uint32_t)idx;
-        else l = linvalid;
-    }
-    fkey[i] = k;
-    if (lkey) lkey[i] = l;
-    if (st != 127) {
-        status[i] = st;
-        remaining[i] = 0;
-        if (wait_ms) wait_ms[i] = 0;
-    }
-}
-
-// requestParamToken validation (DTS:51-62) + param slot lookup/insert in the open-addressing
-// table (exact per-value counters: ClusterParamMetric.java:46-82).
 __device__ inline uint64_t mix64(uint64_t x) {
     x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
     return x;
@@ -135,55 +103,117 @@ __device__ inline uint64_t mix64(uint64_t x) {
 
 constexpr uint64_t PKEY_EMPTY = 0xFFFFFFFFFFFFFFFFull;
 
-__global__ __launch_bounds__(256) void k_param_prep(int64_t n, const int32_t *__restrict__ rule_idx,
-                                                    const int32_t *__restrict__ acquire,
-                                                    const uint64_t *__restrict__ pkey,
-                                                    const int64_t *__restrict__ ts, int32_t nrules,
-                                                    const int32_t *__restrict__ rule_ns, const int32_t *__restrict__ ns_limiter,
-                                                    int32_t nns, unsigned long long *table, uint64_t cap_mask,
-                                                    int32_t *slot_rule, int8_t *status, int32_t *remaining,
-                                                    uint32_t *fkey, uint32_t finvalid, uint32_t *lkey, uint32_t linvalid) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int32_t r = rule_idx[i];
-    const int32_t a = acquire[i];
-    int8_t st = 127;
-    uint32_t k = finvalid, l = linvalid;
-    if (r == SENTINEL_IDX_BAD_ID || a <= 0) st = ST_BAD_REQUEST;
-    else if (r < 0 || r >= nrules) st = ST_NO_RULE_EXISTS;
-    else {
-        const int32_t ns = rule_ns[r];
-        if (ns < 0 || ns >= nns) st = ST_TOO_MANY_REQUEST;
-        else if (ns_limiter[ns] >= 0) l = (uint32_t)ns_limiter[ns];
-        if (st == 127 && ts[i] < 0) st = ST_FAIL;
-        if (st == 127) {
-            const unsigned long long key = (unsigned long long)pkey[i];
-            uint64_t h = mix64(key) & cap_mask;
-            uint64_t probes = 0;
-            for (;;) {
-                const unsigned long long prev = atomicCAS(&table[h], (unsigned long long)PKEY_EMPTY, key);
-                if (prev == PKEY_EMPTY || prev == key) break;
-                h = (h + 1) & cap_mask;
-                if (++probes > cap_mask) { st = ST_FAIL; break; }    // table full
-            }
-            if (st == 127) {
-                k = (uint32_t)h;
-                slot_rule[h] = r;          // identical value from every writer of this slot
+// ------------------------------------------------------------------ prep kernels
+
+// DefaultTokenService.requestToken validation (DTS:37-48) + namespace / limiter routing
+// (ClusterFlowChecker.allowProceed, CFC:50-53).  Decided events get their final verdict here.
+// Also builds the per-tile digit histograms of every radix pass of the flow keys (and of the
+// limiter keys) from this single read of the batch.
+__global__ __launch_bounds__(SORT_THREADS) void k_flow_prep(
+    int64_t n, const Event *__restrict__ ev, int32_t nflows, const int32_t *__restrict__ route,
+    uint64_t *__restrict__ out, uint32_t *__restrict__ fkey, uint32_t finvalid, int fpasses,
+    uint32_t *__restrict__ fhist, uint32_t *__restrict__ lkey, uint32_t linvalid, int lpasses,
+    uint32_t *__restrict__ lhist, int64_t nblocks) {
+    __shared__ uint32_t hf[MAX_PASSES][RADIX];
+    __shared__ uint32_t hl[MAX_PASSES][RADIX];
+    for (int d = threadIdx.x; d < MAX_PASSES * RADIX; d += SORT_THREADS) {
+        (&hf[0][0])[d] = 0;
+        (&hl[0][0])[d] = 0;
+    }
+    __syncthreads();
+    const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
+#pragma unroll 4
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
+        if (i >= n) break;
+        const Event e = ev[i];
+        int st = 127;   // undecided
+        uint32_t k = finvalid, l = linvalid;
+        if (e.idx == SENTINEL_IDX_BAD_ID || e.acquire <= 0) st = ST_BAD_REQUEST;
+        else if (e.idx < 0 || e.idx >= nflows) st = ST_NO_RULE_EXISTS;
+        else {
+            const int32_t r = route ? route[e.idx] : ROUTE_PLAIN;
+            if (r == ROUTE_TOO_MANY) st = ST_TOO_MANY_REQUEST;      // namespace == null
+            else if (e.ts < 0) st = ST_FAIL;                          // reference: NPE in LeapArray
+            else {
+                k = (uint32_t)e.idx;
+                if (r >= 0) l = (uint32_t)r;
             }
         }
-        if (st != 127) l = linvalid;
+        fkey[i] = k;
+        tile_hist_accumulate(hf, k, fpasses);
+        if (lkey) {
+            lkey[i] = l;
+            tile_hist_accumulate(hl, l, lpasses);
+        }
+        if (st != 127) put_verdict(out, (uint32_t)i, st, 0, 0);
     }
-    fkey[i] = k;
-    if (lkey) lkey[i] = l;
-    if (st != 127) {
-        status[i] = st;
-        remaining[i] = 0;
+    __syncthreads();
+    tile_hist_store(hf, fhist, fpasses, nblocks);
+    if (lkey) tile_hist_store(hl, lhist, lpasses, nblocks);
+}
+
+// requestParamToken validation (DTS:51-62) + param slot lookup/insert in the open-addressing
+// table (exact per-value counters: ClusterParamMetric.java:46-82).  Param keys are unique per
+// (rule, value): the host's injective encoding of the Java typed value.
+__global__ __launch_bounds__(SORT_THREADS) void k_param_prep(
+    int64_t n, const ParamEvent *__restrict__ ev, int32_t nrules, const int32_t *__restrict__ route,
+    unsigned long long *table, uint64_t cap_mask, int32_t *slot_rule, uint64_t *__restrict__ out,
+    uint32_t *__restrict__ fkey, uint32_t finvalid, int fpasses, uint32_t *__restrict__ fhist,
+    uint32_t *__restrict__ lkey, uint32_t linvalid, int lpasses, uint32_t *__restrict__ lhist, int64_t nblocks) {
+    __shared__ uint32_t hf[MAX_PASSES][RADIX];
+    __shared__ uint32_t hl[MAX_PASSES][RADIX];
+    for (int d = threadIdx.x; d < MAX_PASSES * RADIX; d += SORT_THREADS) {
+        (&hf[0][0])[d] = 0;
+        (&hl[0][0])[d] = 0;
     }
+    __syncthreads();
+    const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
+        if (i >= n) break;
+        const ParamEvent e = ev[i];
+        int st = 127;
+        uint32_t k = finvalid, l = linvalid;
+        if (e.idx == SENTINEL_IDX_BAD_ID || e.acquire <= 0) st = ST_BAD_REQUEST;
+        else if (e.idx < 0 || e.idx >= nrules) st = ST_NO_RULE_EXISTS;
+        else {
+            const int32_t r = route ? route[e.idx] : ROUTE_PLAIN;
+            if (r == ROUTE_TOO_MANY) st = ST_TOO_MANY_REQUEST;
+            else if (e.ts < 0) st = ST_FAIL;
+            else {
+                const unsigned long long key = (unsigned long long)e.key;
+                uint64_t h = mix64(key) & cap_mask;
+                uint64_t probes = 0;
+                for (;;) {
+                    const unsigned long long prev = atomicCAS(&table[h], (unsigned long long)PKEY_EMPTY, key);
+                    if (prev == PKEY_EMPTY || prev == key) break;
+                    h = (h + 1) & cap_mask;
+                    if (++probes > cap_mask) { st = ST_FAIL; break; }    // table full
+                }
+                if (st == 127) {
+                    k = (uint32_t)h;
+                    slot_rule[h] = e.idx;    // identical value from every writer of this slot
+                    if (r >= 0) l = (uint32_t)r;
+                }
+            }
+        }
+        fkey[i] = k;
+        tile_hist_accumulate(hf, k, fpasses);
+        if (lkey) {
+            lkey[i] = l;
+            tile_hist_accumulate(hl, l, lpasses);
+        }
+        if (st != 127) put_verdict(out, (uint32_t)i, st, 0, 0);
+    }
+    __syncthreads();
+    tile_hist_store(hf, fhist, fpasses, nblocks);
+    if (lkey) tile_hist_store(hl, lhist, lpasses, nblocks);
 }
 
 // Per event: refresh the per-slot parameters of its param slot from the rule (identical writes).
 __global__ __launch_bounds__(256) void k_param_meta(int64_t n, const uint32_t *__restrict__ fkey, uint32_t finvalid,
-                                                    const uint64_t *__restrict__ pkey,
+                                                    const ParamEvent *__restrict__ ev,
                                                     const int32_t *__restrict__ slot_rule,
                                                     const int32_t *__restrict__ rule_n, const int32_t *__restrict__ rule_w,
                                                     const double *__restrict__ rule_rcp, const double *__restrict__ rule_Is,
@@ -199,7 +229,7 @@ __global__ __launch_bounds__(256) void k_param_meta(int64_t n, const uint32_t *_
     const int32_t r = slot_rule[s];
     double thr = rule_thr[r];
     if (hot_table) {   // ClusterParamFlowChecker.getRawThreshold (CPFC:113-120)
-        const unsigned long long key = (unsigned long long)pkey[i];
+        const unsigned long long key = (unsigned long long)ev[i].key;
         uint64_t h = mix64(key) & hot_mask;
         for (uint64_t p = 0; p <= hot_mask; ++p) {
             const unsigned long long x = hot_table[h];
@@ -216,43 +246,34 @@ __global__ __launch_bounds__(256) void k_param_meta(int64_t n, const uint32_t *_
     slot_kind[s] = KIND_PARAM;
 }
 
-// nvalid = number of sorted keys below the invalid key.
-__global__ __launch_bounds__(256) void k_count_valid(const uint32_t *__restrict__ skey, int64_t n, uint32_t invalid,
-                                                     uint32_t *nvalid) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const bool v = skey[i] != invalid;
-    if (i == 0 && !v) *nvalid = 0;
-    if (v && (i == n - 1 || skey[i + 1] == invalid)) *nvalid = (uint32_t)(i + 1);
-}
-
 // Snapshot of one flow: getAvg(BLOCK) then getAvg(PASS) at ts (ClusterMetricNodeGenerator.java:79-84).
 __global__ __launch_bounds__(256) void k_snapshot(KeyTable T, int32_t nflows, int64_t ts,
                                                   const int64_t *__restrict__ flow_ids,
                                                   sentinel_flow_snapshot_t *out) {
     const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= nflows) return;
-    const int64_t off = T.state_off[f];
-    const int n = T.n[f];
+    const KeyState ks = key_state(T, (uint32_t)f);
     const int64_t E = epoch_of(ts, T.w[f], T.rcp_w[f]);
-    roll(T, (int)f, off, n, E);
-    const double block = (double)window_sum(T, off, n, E, EV_BLOCK) / T.I_s[f];
-    roll(T, (int)f, off, n, E);
-    const double pass = (double)window_sum(T, off, n, E, EV_PASS) / T.I_s[f];
+    roll(T, (uint32_t)f, ks, E);
+    const double block = (double)window_sum(ks, E, EV_BLOCK) / T.I_s[f];
+    roll(T, (uint32_t)f, ks, E);
+    const double pass = (double)window_sum(ks, E, EV_PASS) / T.I_s[f];
     out[f].flow_id = flow_ids[f];
     out[f].pass_qps = pass;
     out[f].block_qps = block;
 }
 
-// Initialise a key range's state: epochs absent, counters zero.
+// Initialise state records: epochs absent, counters zero.
 __global__ void k_init_state(int64_t *state, const int64_t *__restrict__ off, int64_t stride,
-                             const int32_t *__restrict__ nn, int32_t fixed_n, int32_t ncounters, int64_t nkeys) {
+                             const int32_t *__restrict__ nn, int32_t fixed_n, int64_t words_per_key_fixed,
+                             int64_t nkeys) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nkeys) return;
     const int64_t o = off ? off[k] : k * stride;
     const int n = nn ? nn[k] : fixed_n;
+    const int64_t words = nn ? flow_record_words(n) : words_per_key_fixed;
     for (int j = 0; j < n; ++j) state[o + j] = EPOCH_ABSENT;
-    for (int64_t j = n; j < (int64_t)(1 + ncounters) * n; ++j) state[o + j] = 0;
+    for (int64_t j = n; j < words; ++j) state[o + j] = 0;
 }
 
 inline unsigned grid_for(int64_t n, int threads = 256) { return (unsigned)std::max<int64_t>(1, (n + threads - 1) / threads); }
@@ -270,25 +291,25 @@ struct sentinel_engine {
     // flows
     std::vector<sentinel_flow_rule_t> rules;
     std::unordered_map<int64_t, int32_t> flow_index;
-    std::vector<int32_t> h_flow_ns;
-    std::vector<int32_t> h_flow_n;
-    std::vector<int32_t> h_flow_w;
+    std::vector<int32_t> h_flow_n, h_flow_w;
     std::vector<int64_t> h_flow_off;
     TableBufs ft;
-    DevBuf d_flow_ns, d_flow_ids;
+    DevBuf d_flow_route, d_flow_ids;
+    bool flow_plain = true;          // no flow needs a limiter or namespace check
     int64_t flow_state_words = 0;
 
     // namespace limiters (RequestLimiter = UnaryLeapArray(10, 1000))
     std::vector<int32_t> h_ns_limiter;   // namespace -> limiter key or -1
     int32_t nlimiters = 0;
     TableBufs lt;
-    DevBuf d_ns_limiter;
+    int64_t lim_stride = header_words(10);
 
     // param rules + slots
     std::vector<sentinel_param_rule_t> prules;
     std::unordered_map<int64_t, int32_t> param_index;
-    DevBuf d_prule_ns, d_prule_n, d_prule_w, d_prule_rcp, d_prule_Is, d_prule_thr;
+    DevBuf d_prule_route, d_prule_n, d_prule_w, d_prule_rcp, d_prule_Is, d_prule_thr;
     DevBuf d_ptable, d_slot_rule, d_hot_table, d_hot_thr;
+    bool param_plain = true;
     TableBufs pt;
     uint64_t pcap = (uint64_t)1 << 22;
     int32_t pmax_n = 1;
@@ -336,72 +357,25 @@ struct sentinel_engine {
         prof_pending.clear();
     }
 
-    void scan_incl(uint32_t *buf, int64_t n, hipStream_t s) {
-        if (n <= 0) return;
-        const int64_t nb = scan_parts(n);
-        uint32_t *parts = w_parts.as<uint32_t>();
-        launch("scan_tiles", n, s, [&] { k_scan_tiles<false><<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, buf, n, parts); });
-        launch("scan_partials", nb, s, [&] { k_scan_partials<<<1, SCAN_THREADS, 0, s>>>(parts, nb, nullptr); });
-        launch("scan_add", n, s, [&] { k_scan_add<<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, n, parts); });
-    }
-
-    void scan_excl(uint32_t *buf, int64_t n, hipStream_t s) {
-        if (n <= 0) return;
-        const int64_t nb = scan_parts(n);
-        uint32_t *parts = w_parts.as<uint32_t>();
-        launch("scan_tiles", n, s, [&] { k_scan_tiles<true><<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, buf, n, parts); });
-        launch("scan_partials", nb, s, [&] { k_scan_partials<<<1, SCAN_THREADS, 0, s>>>(parts, nb, nullptr); });
-        launch("scan_add", n, s, [&] { k_scan_add<<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, n, parts); });
-    }
-
-    // K2: stable LSD radix sort of (key, seq) by the low `bits` key bits into (skey, sseq).
-    void sort(const uint32_t *keys_in, int64_t n, int bits, hipStream_t s) {
-        const int64_t nb = sort_blocks(n);
-        const int passes = (bits + RADIX_BITS - 1) / RADIX_BITS;
-        uint32_t *kb[2], *vb[2];
-        if (passes % 2 == 1) { kb[0] = w_skey.as<uint32_t>(); vb[0] = w_sseq.as<uint32_t>(); kb[1] = w_ktmp.as<uint32_t>(); vb[1] = w_vtmp.as<uint32_t>(); }
-        else { kb[0] = w_ktmp.as<uint32_t>(); vb[0] = w_vtmp.as<uint32_t>(); kb[1] = w_skey.as<uint32_t>(); vb[1] = w_sseq.as<uint32_t>(); }
-        const uint32_t *kin = keys_in;
-        const uint32_t *vin = nullptr;
-        uint32_t *hist = w_hist.as<uint32_t>();
-        for (int p = 0; p < passes; ++p) {
-            const int shift = p * RADIX_BITS;
-            launch("radix_hist", n, s, [&] { k_radix_hist<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(kin, n, shift, hist, nb); });
-            scan_excl(hist, nb * RADIX, s);
-            uint32_t *ko = kb[p % 2], *vo = vb[p % 2];
-            launch("radix_scatter", n, s, [&] { k_radix_scatter<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(kin, vin, ko, vo, n, shift, hist, nb); });
-            kin = ko;
-            vin = vo;
-        }
-    }
-
     // batch workspace
-    DevBuf w_fkey, w_lkey, w_skey, w_sseq, w_ktmp, w_vtmp, w_hist, w_parts, w_epoch, w_acq, w_fl, w_segid,
-        w_segstart, w_het, w_done, w_s0, w_k, w_counters;
-    DevBuf io_idx, io_acq, io_fl, io_ts, io_st, io_rem, io_wait, io_pkey;
+    DevBuf w_fkey, w_lkey, w_skey, w_sseq, w_ktmp, w_vtmp, w_fhist, w_lhist, w_parts, w_segid, w_bad, w_hep,
+        w_hacq, w_segstart, w_segkey, w_segep, w_segacq, w_het, w_done, w_s0, w_k, w_counters;
+    DevBuf io_ev, io_fl, io_out;
     int64_t ws_cap = 0;
 
     int ensure_ws(int64_t n) {
         if (n <= ws_cap) return 0;
-        int64_t c = std::max<int64_t>(n, 1024);
+        int64_t c = std::max<int64_t>(n, 4096);
         int rc = 0;
-        rc |= w_fkey.ensure(c * 4);
-        rc |= w_lkey.ensure(c * 4);
-        rc |= w_skey.ensure(c * 4);
-        rc |= w_sseq.ensure(c * 4);
-        rc |= w_ktmp.ensure(c * 4);
-        rc |= w_vtmp.ensure(c * 4);
-        rc |= w_hist.ensure((size_t)sort_hist_words(c) * 4);
-        rc |= w_parts.ensure((size_t)(scan_parts(std::max<int64_t>(c, sort_hist_words(c))) + 16) * 4);
-        rc |= w_epoch.ensure(c * 8);
-        rc |= w_acq.ensure(c * 4);
-        rc |= w_fl.ensure(c);
-        rc |= w_segid.ensure(c * 4);
+        for (DevBuf *b : {&w_fkey, &w_lkey, &w_skey, &w_sseq, &w_ktmp, &w_vtmp, &w_segid, &w_segkey, &w_k, &w_hacq,
+                          &w_segacq})
+            rc |= b->ensure(c * 4);
+        for (DevBuf *b : {&w_hep, &w_segep, &w_s0}) rc |= b->ensure(c * 8);
+        for (DevBuf *b : {&w_bad, &w_het, &w_done}) rc |= b->ensure(c);
+        rc |= w_fhist.ensure((size_t)hist_words(c, MAX_PASSES) * 4);
+        rc |= w_lhist.ensure((size_t)hist_words(c, MAX_PASSES) * 4);
+        rc |= w_parts.ensure((size_t)(scan_parts(std::max<int64_t>(c, hist_words(c, MAX_PASSES))) + 16) * 4);
         rc |= w_segstart.ensure((c + 1) * 4);
-        rc |= w_het.ensure(c);
-        rc |= w_done.ensure(c);
-        rc |= w_s0.ensure(c * 8);
-        rc |= w_k.ensure(c * 4);
         rc |= w_counters.ensure(64);
         if (rc) return SENTINEL_E_NOMEM;
         ws_cap = c;
@@ -412,11 +386,14 @@ struct sentinel_engine {
         BatchWork W;
         W.skey = w_skey.as<uint32_t>();
         W.sseq = w_sseq.as<uint32_t>();
-        W.s_epoch = w_epoch.as<int64_t>();
-        W.s_acq = w_acq.as<int32_t>();
-        W.s_fl = w_fl.as<uint8_t>();
         W.segid = w_segid.as<uint32_t>();
+        W.bad = w_bad.as<uint8_t>();
+        W.h_epoch = w_hep.as<int64_t>();
+        W.h_acq = w_hacq.as<int32_t>();
         W.seg_start = w_segstart.as<uint32_t>();
+        W.seg_key = w_segkey.as<uint32_t>();
+        W.seg_epoch = w_segep.as<int64_t>();
+        W.seg_acq = w_segacq.as<int32_t>();
         W.seg_het = w_het.as<uint8_t>();
         W.seg_done = w_done.as<uint8_t>();
         W.seg_s0 = w_s0.as<int64_t>();
@@ -444,25 +421,70 @@ struct sentinel_engine {
         return T;
     }
 
+    void scan(uint32_t *buf, int64_t n, bool exclusive, hipStream_t s) {
+        if (n <= 0) return;
+        const int64_t nb = scan_parts(n);
+        uint32_t *parts = w_parts.as<uint32_t>();
+        launch("scan_tiles", n, s, [&] {
+            if (exclusive) k_scan_tiles<true><<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, buf, n, parts);
+            else k_scan_tiles<false><<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, buf, n, parts);
+        });
+        launch("scan_partials", nb, s, [&] { k_scan_partials<<<1, SCAN_THREADS, 0, s>>>(parts, nb); });
+        launch("scan_add", n, s, [&] { k_scan_add<<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, n, parts); });
+    }
+
+    // K2: stable LSD radix sort of (key, seq) by the low `bits` key bits into (skey, sseq).
+    // `hist` already holds pass 0's per-tile digit histograms (built by the prep kernel from the
+    // same tiles); later passes histogram their own input (the previous pass's output tiles).
+    void sort(const uint32_t *keys_in, int64_t n, int bits, uint32_t *hist, hipStream_t s) {
+        const int64_t nb = sort_blocks(n);
+        const int passes = passes_for(bits);
+        uint32_t *kb[2], *vb[2];
+        if (passes % 2 == 1) { kb[0] = w_skey.as<uint32_t>(); vb[0] = w_sseq.as<uint32_t>(); kb[1] = w_ktmp.as<uint32_t>(); vb[1] = w_vtmp.as<uint32_t>(); }
+        else { kb[0] = w_ktmp.as<uint32_t>(); vb[0] = w_vtmp.as<uint32_t>(); kb[1] = w_skey.as<uint32_t>(); vb[1] = w_sseq.as<uint32_t>(); }
+        const uint32_t *kin = keys_in;
+        const uint32_t *vin = nullptr;
+        for (int p = 0; p < passes; ++p) {
+            const int shift = p * RADIX_BITS;
+            if (p > 0)
+                launch("radix_hist", n, s, [&] {
+                    k_radix_hist_pass<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(kin, n, shift, hist, nb);
+                });
+            scan(hist, nb * RADIX, true, s);
+            uint32_t *ko = kb[p % 2], *vo = vb[p % 2];
+            launch("radix_scatter", n, s, [&] {
+                k_radix_scatter<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(kin, vin, ko, vo, n, shift, hist, nb, 0u);
+            });
+            kin = ko;
+            vin = vo;
+        }
+    }
+
+    void hist_pass0(const uint32_t *keys, int64_t n, uint32_t *hist, hipStream_t s) {
+        const int64_t nb = sort_blocks(n);
+        launch("radix_hist", n, s, [&] {
+            k_radix_hist_pass<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(keys, n, 0, hist, nb);
+        });
+    }
+
     // The generic pipeline: sort by key, segment, decide, scatter.
-    void run_pipeline(const KeyTable &T, const uint32_t *keys, int64_t n, int bits, const int64_t *ts,
-                      const int32_t *acquire, const uint8_t *flags, const Verdicts &V, hipStream_t s) {
+    void run_pipeline(const KeyTable &T, const uint32_t *keys, uint32_t *hist, int64_t n, int bits,
+                      const EventSrc &src, const Verdicts &V, hipStream_t s) {
         BatchWork W = work();
         const uint32_t invalid = ((uint32_t)1 << bits) - 1;
-        sort(keys, n, bits, s);
+        sort(keys, n, bits, hist, s);
         const unsigned g = grid_for(n);
-        launch("count_valid", n, s, [&] { k_count_valid<<<g, 256, 0, s>>>(W.skey, n, invalid, W.nvalid); });
-        launch("gather_sorted", n, s, [&] { k_gather_sorted<<<g, 256, 0, s>>>(T, W, ts, acquire, flags, n); });
-        launch("heads", n, s, [&] { k_heads<<<g, 256, 0, s>>>(W, n); });
-        scan_incl(W.segid, n, s);
-        launch("seg_start", n, s, [&] { k_seg_start<<<g, 256, 0, s>>>(W, n); });
-        launch("seg_het", n, s, [&] { k_seg_het<<<g, 256, 0, s>>>(T, W, n); });
-        launch("process", n, s, [&] { k_process<<<g, 256, 0, s>>>(T, W, V, n); });
+        launch("seg_heads", n, s, [&] { k_seg_heads<<<g, 256, 0, s>>>(T, W, src, n, invalid); });
+        scan(W.segid, n, false, s);
+        (void)hipMemsetAsync(W.seg_het, 0, (size_t)n, s);
+        launch("seg_mark", n, s, [&] { k_seg_mark<<<g, 256, 0, s>>>(W, n); });
+        launch("process", n, s, [&] { k_process<<<g, 256, 0, s>>>(T, W, src, V, n); });
         launch("verdict", n, s, [&] { k_verdict<<<g, 256, 0, s>>>(T, W, V, n); });
     }
 
     int rebuild_flow_thresholds();
     int rebuild_limiters();
+    int rebuild_routes();
 };
 
 // Host mirror of ClusterFlowChecker.calcGlobalThreshold * exceedCount (CFC:38-48, 68) and
@@ -486,6 +508,35 @@ int sentinel_engine::rebuild_flow_thresholds() {
     return upload(ft.thr, thr);
 }
 
+// Per-rule routing: TOO_MANY_REQUEST for a null namespace, limiter id, or plain.
+int sentinel_engine::rebuild_routes() {
+    std::vector<int32_t> route(rules.size());
+    flow_plain = true;
+    for (size_t i = 0; i < rules.size(); ++i) {
+        const sentinel_flow_rule_t &r = rules[i];
+        int32_t v = ROUTE_PLAIN;
+        if (r.checker == SENTINEL_CHECKER_CLUSTER) {
+            if (r.namespace_idx < 0 || r.namespace_idx >= (int32_t)ns.size()) v = ROUTE_TOO_MANY;
+            else if (h_ns_limiter[r.namespace_idx] >= 0) v = h_ns_limiter[r.namespace_idx];
+        }
+        route[i] = v;
+        if (v != ROUTE_PLAIN) flow_plain = false;
+    }
+    int rc = upload(d_flow_route, route);
+    if (rc) return rc;
+    std::vector<int32_t> proute(prules.size());
+    param_plain = true;
+    for (size_t i = 0; i < prules.size(); ++i) {
+        const sentinel_param_rule_t &r = prules[i];
+        int32_t v = ROUTE_PLAIN;
+        if (r.namespace_idx < 0 || r.namespace_idx >= (int32_t)ns.size()) v = ROUTE_TOO_MANY;
+        else if (h_ns_limiter[r.namespace_idx] >= 0) v = h_ns_limiter[r.namespace_idx];
+        proute[i] = v;
+        if (v != ROUTE_PLAIN) param_plain = false;
+    }
+    return upload(d_prule_route, proute);
+}
+
 // One RequestLimiter per namespace with has_limiter (GlobalRequestLimiter.java:32-37):
 // UnaryLeapArray(10, 1000) -> n = 10, w = 100, intervalInSecond = 1.0.
 int sentinel_engine::rebuild_limiters() {
@@ -505,7 +556,6 @@ int sentinel_engine::rebuild_limiters() {
     }
     nlimiters = (int32_t)n.size();
     int rc = 0;
-    rc |= upload(d_ns_limiter, h_ns_limiter);
     rc |= upload(lt.n, n);
     rc |= upload(lt.w, w);
     rc |= upload(lt.rcp, rcp);
@@ -513,14 +563,109 @@ int sentinel_engine::rebuild_limiters() {
     rc |= upload(lt.thr, thr);
     rc |= upload(lt.kind, kind);
     if (rc) return rc;
-    const int64_t stride = 2 * 10;
-    rc = lt.state.ensure(std::max<int64_t>(1, nlimiters) * stride * 8);
+    rc = lt.state.ensure(std::max<int64_t>(1, nlimiters) * lim_stride * 8);
     if (rc) return rc;
     if (nlimiters > 0) {
-        k_init_state<<<grid_for(nlimiters), 256, 0, stream>>>(lt.state.as<int64_t>(), nullptr, stride, nullptr, 10, 1, nlimiters);
+        k_init_state<<<grid_for(nlimiters), 256, 0, stream>>>(lt.state.as<int64_t>(), nullptr, lim_stride, nullptr, 10,
+                                                              lim_stride, nlimiters);
         HIP_OK(hipStreamSynchronize(stream));
     }
+    return rebuild_routes();
+}
+
+static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
+                       hipStream_t s) {
+    if (n <= 0) return 0;
+    if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
+    int rc = e->ensure_ws(n);
+    if (rc) return rc;
+    const int32_t F = (int32_t)e->rules.size();
+    const int fbits = bits_for(F);
+    const uint32_t finvalid = ((uint32_t)1 << fbits) - 1;
+    const bool lim = e->nlimiters > 0 && !e->flow_plain;
+    const int lbits = bits_for(e->nlimiters);
+    const uint32_t linvalid = ((uint32_t)1 << lbits) - 1;
+    uint32_t *fkey = e->w_fkey.as<uint32_t>();
+    uint32_t *lkey = lim ? e->w_lkey.as<uint32_t>() : nullptr;
+    const int64_t nb = sort_blocks(n);
+    e->launch("flow_prep", n, s, [&] {
+        k_flow_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
+            n, ev, F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, fkey, finvalid, 1,
+            e->w_fhist.as<uint32_t>(), lkey, linvalid, 1, e->w_lhist.as<uint32_t>(), nb);
+    });
+    Verdicts V{out, fkey, finvalid};
+    EventSrc src{ev, nullptr, fl, false};
+    if (lim) {
+        KeyTable LT = e->table(e->lt, 1, e->lim_stride);
+        EventSrc lsrc{ev, nullptr, nullptr, true};
+        e->run_pipeline(LT, lkey, e->w_lhist.as<uint32_t>(), n, lbits, lsrc, V, s);
+        e->hist_pass0(fkey, n, e->w_fhist.as<uint32_t>(), s);   // the limiter invalidated some keys
+    }
+    if (F > 0) {
+        KeyTable FT = e->table(e->ft, NEV, 0);
+        e->run_pipeline(FT, fkey, e->w_fhist.as<uint32_t>(), n, fbits, src, V, s);
+    }
+    HIP_OK(hipGetLastError());
     return 0;
+}
+
+static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, uint64_t *out, hipStream_t s) {
+    if (n <= 0) return 0;
+    if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
+    int rc = e->ensure_ws(n);
+    if (rc) return rc;
+    const int32_t R = (int32_t)e->prules.size();
+    const uint64_t P = e->pcap;
+    const int pbits = bits_for((int64_t)P);
+    const uint32_t pinvalid = ((uint32_t)1 << pbits) - 1;
+    const bool lim = e->nlimiters > 0 && !e->param_plain && R > 0;
+    const int lbits = bits_for(e->nlimiters);
+    const uint32_t linvalid = ((uint32_t)1 << lbits) - 1;
+    uint32_t *fkey = e->w_fkey.as<uint32_t>();
+    uint32_t *lkey = lim ? e->w_lkey.as<uint32_t>() : nullptr;
+    const int64_t nb = sort_blocks(n);
+    const bool have = R > 0 && e->d_ptable.p;
+    e->launch("param_prep", n, s, [&] {
+        k_param_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
+            n, ev, have ? R : 0, e->param_plain ? nullptr : e->d_prule_route.as<int32_t>(),
+            e->d_ptable.as<unsigned long long>(), P - 1, e->d_slot_rule.as<int32_t>(), out, fkey, pinvalid,
+            1, e->w_fhist.as<uint32_t>(), lkey, linvalid, 1, e->w_lhist.as<uint32_t>(), nb);
+    });
+    if (!have) {
+        HIP_OK(hipGetLastError());
+        return 0;
+    }
+    e->launch("param_meta", n, s, [&] {
+        k_param_meta<<<grid_for(n), 256, 0, s>>>(n, fkey, pinvalid, ev, e->d_slot_rule.as<int32_t>(),
+                                                 e->d_prule_n.as<int32_t>(), e->d_prule_w.as<int32_t>(),
+                                                 e->d_prule_rcp.as<double>(), e->d_prule_Is.as<double>(),
+                                                 e->d_prule_thr.as<double>(),
+                                                 e->has_hot ? e->d_hot_table.as<unsigned long long>() : nullptr,
+                                                 e->hot_mask, e->d_hot_thr.as<double>(), e->pt.n.as<int32_t>(),
+                                                 e->pt.w.as<int32_t>(), e->pt.rcp.as<double>(), e->pt.Is.as<double>(),
+                                                 e->pt.thr.as<double>(), e->pt.kind.as<uint8_t>());
+    });
+    Verdicts V{out, fkey, pinvalid};
+    if (lim) {
+        KeyTable LT = e->table(e->lt, 1, e->lim_stride);
+        EventSrc lsrc{nullptr, ev, nullptr, true};
+        e->run_pipeline(LT, lkey, e->w_lhist.as<uint32_t>(), n, lbits, lsrc, V, s);
+        e->hist_pass0(fkey, n, e->w_fhist.as<uint32_t>(), s);
+    }
+    KeyTable PT = e->table(e->pt, 1, header_words(e->pmax_n));
+    EventSrc src{nullptr, ev, nullptr, false};
+    e->run_pipeline(PT, fkey, e->w_fhist.as<uint32_t>(), n, pbits, src, V, s);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+static uint64_t host_mix64(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+    return x;
+}
+
+static bool valid_window(int32_t n, int32_t interval) {  // FlowRuleUtil.isWindowConfigValid (FlowRuleUtil.java:229-231)
+    return n > 0 && interval > 0 && interval % n == 0;
 }
 
 // ==================================================================== C ABI
@@ -569,15 +714,17 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
     if (!e) return 0;
     (void)hipSetDevice(e->device);
     (void)hipStreamSynchronize(e->stream);
+    e->prof_collect();
+    for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
     e->ft.release();
     e->lt.release();
     e->pt.release();
-    for (DevBuf *b : {&e->d_flow_ns, &e->d_flow_ids, &e->d_ns_limiter, &e->d_prule_ns, &e->d_prule_n, &e->d_prule_w,
+    for (DevBuf *b : {&e->d_flow_route, &e->d_flow_ids, &e->d_prule_route, &e->d_prule_n, &e->d_prule_w,
                       &e->d_prule_rcp, &e->d_prule_Is, &e->d_prule_thr, &e->d_ptable, &e->d_slot_rule,
                       &e->d_hot_table, &e->d_hot_thr, &e->w_fkey, &e->w_lkey, &e->w_skey, &e->w_sseq, &e->w_ktmp,
-                      &e->w_vtmp, &e->w_hist, &e->w_parts, &e->w_epoch, &e->w_acq, &e->w_fl, &e->w_segid,
-                      &e->w_segstart, &e->w_het, &e->w_done, &e->w_s0, &e->w_k, &e->w_counters, &e->io_idx,
-                      &e->io_acq, &e->io_fl, &e->io_ts, &e->io_st, &e->io_rem, &e->io_wait, &e->io_pkey})
+                      &e->w_vtmp, &e->w_fhist, &e->w_lhist, &e->w_parts, &e->w_segid, &e->w_bad, &e->w_hep,
+                      &e->w_hacq, &e->w_segstart, &e->w_segkey, &e->w_segep, &e->w_segacq, &e->w_het, &e->w_done,
+                      &e->w_s0, &e->w_k, &e->w_counters, &e->io_ev, &e->io_fl, &e->io_out})
         b->release();
     (void)hipStreamDestroy(e->stream);
     delete e;
@@ -645,10 +792,6 @@ int sentinel_set_connected_count(sentinel_engine_t *e, int32_t nsi, int32_t conn
     return e->rebuild_flow_thresholds();
 }
 
-static bool valid_window(int32_t n, int32_t interval) {  // FlowRuleUtil.isWindowConfigValid (FlowRuleUtil.java:229-231)
-    return n > 0 && interval > 0 && interval % n == 0;
-}
-
 int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *rules, int32_t n) {
     if (!e || (n > 0 && !rules) || n < 0) return fail(SENTINEL_E_INVALID, "bad rules");
     std::lock_guard<std::mutex> g(e->mu);
@@ -659,7 +802,7 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
     std::vector<int64_t> old_off = e->h_flow_off;
     std::vector<int32_t> old_n = e->h_flow_n, old_w = e->h_flow_w;
     std::vector<int64_t> old_state;
-    if (e->flow_state_words > 0) {
+    if (e->flow_state_words > 0 && !old_index.empty()) {
         old_state.resize(e->flow_state_words);
         HIP_OK(hipMemcpy(old_state.data(), e->ft.state.p, old_state.size() * 8, hipMemcpyDeviceToHost));
     }
@@ -683,7 +826,7 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
     }
     const size_t F = e->rules.size();
     std::vector<int64_t> off(F), ids(F);
-    std::vector<int32_t> nn(F), ww(F), nsv(F);
+    std::vector<int32_t> nn(F), ww(F);
     std::vector<double> rcp(F), Is(F);
     std::vector<uint8_t> kind(F);
     int64_t words = 0;
@@ -694,10 +837,9 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
         ww[i] = r.window_interval_ms / r.sample_count;
         rcp[i] = 1.0 / (double)ww[i];
         Is[i] = r.window_interval_ms / 1000.0;   // LeapArray.java:74
-        nsv[i] = r.namespace_idx;
         kind[i] = r.checker == SENTINEL_CHECKER_SIMPLE ? KIND_SIMPLE : KIND_CLUSTER;
         ids[i] = r.flow_id;
-        words += (int64_t)(1 + NEV) * r.sample_count;
+        words += flow_record_words(r.sample_count);
     }
     // new state image: fresh, then carry surviving flows whose window shape is unchanged
     std::vector<int64_t> st(std::max<int64_t>(words, 1), 0);
@@ -710,7 +852,8 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
         const int32_t o = it->second;
         // ClusterMetric is kept as constructed with the OLD (n, interval): only carry when equal
         if (old_n[o] != nn[i] || old_w[o] != ww[i]) continue;
-        std::copy(old_state.begin() + old_off[o], old_state.begin() + old_off[o] + (1 + NEV) * nn[i], st.begin() + off[i]);
+        std::copy(old_state.begin() + old_off[o], old_state.begin() + old_off[o] + flow_record_words(nn[i]),
+                  st.begin() + off[i]);
         occ[2 * i] = old_occ[2 * o];
         occ[2 * i + 1] = old_occ[2 * o + 1];
         hocc[i] = old_hocc[o];
@@ -725,14 +868,14 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
     rc |= upload(e->ft.state, st);
     rc |= upload(e->ft.occ, occ);
     rc |= upload(e->ft.has_occ, hocc);
-    rc |= upload(e->d_flow_ns, nsv);
     rc |= upload(e->d_flow_ids, ids);
     if (rc) return rc;
     e->h_flow_off = off;
     e->h_flow_n = nn;
     e->h_flow_w = ww;
-    e->h_flow_ns = nsv;
     e->flow_state_words = words;
+    rc = e->rebuild_routes();
+    if (rc) return rc;
     return e->rebuild_flow_thresholds();
 }
 
@@ -758,11 +901,6 @@ int sentinel_lookup_param_idx(sentinel_engine_t *e, int64_t n, const int64_t *id
     return 0;
 }
 
-static uint64_t host_mix64(uint64_t x) {
-    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
-    return x;
-}
-
 int sentinel_load_param_rules(sentinel_engine_t *e, const sentinel_param_rule_t *rules, int32_t n,
                               const uint64_t *hot_keys, const int32_t *hot_counts, int32_t n_hot) {
     if (!e || n < 0 || (n > 0 && !rules) || n_hot < 0 || (n_hot > 0 && (!hot_keys || !hot_counts)))
@@ -772,7 +910,7 @@ int sentinel_load_param_rules(sentinel_engine_t *e, const sentinel_param_rule_t 
     HIP_OK(hipStreamSynchronize(e->stream));
     e->prules.clear();
     e->param_index.clear();
-    std::vector<int32_t> nsv, nn, ww;
+    std::vector<int32_t> nn, ww;
     std::vector<double> rcp, Is, thr;
     std::vector<std::pair<uint64_t, double>> hot;
     int32_t maxn = 1;
@@ -782,33 +920,26 @@ int sentinel_load_param_rules(sentinel_engine_t *e, const sentinel_param_rule_t 
         if (e->param_index.count(r.flow_id)) continue;
         e->param_index.emplace(r.flow_id, (int32_t)e->prules.size());
         e->prules.push_back(r);
-        nsv.push_back(r.namespace_idx);
         nn.push_back(r.sample_count);
         ww.push_back(r.window_interval_ms / r.sample_count);
         rcp.push_back(1.0 / (double)ww.back());
         Is.push_back(r.window_interval_ms / 1000.0);
         // calcGlobalThreshold(rule, value) without hot item: count or count*connectedCount (CPFC:101-111)
+        const int32_t cc = (r.namespace_idx >= 0 && r.namespace_idx < (int32_t)e->ns.size()) ? e->ns[r.namespace_idx].connected_count : 0;
         double c = r.count;
-        if (r.threshold_type != SENTINEL_THRESHOLD_GLOBAL) {
-            const int32_t cc = (r.namespace_idx >= 0 && r.namespace_idx < (int32_t)e->ns.size()) ? e->ns[r.namespace_idx].connected_count : 0;
-            c = c * (double)cc;
-        }
+        if (r.threshold_type != SENTINEL_THRESHOLD_GLOBAL) c = c * (double)cc;
         thr.push_back(c);
         maxn = std::max(maxn, r.sample_count);
         for (int32_t h = 0; h < r.hot_n; ++h) {
             const int32_t j = r.hot_begin + h;
             if (j < 0 || j >= n_hot) return fail(SENTINEL_E_INVALID, "hot item range out of bounds");
             double hc = (double)hot_counts[j];
-            if (r.threshold_type != SENTINEL_THRESHOLD_GLOBAL) {
-                const int32_t cc = (r.namespace_idx >= 0 && r.namespace_idx < (int32_t)e->ns.size()) ? e->ns[r.namespace_idx].connected_count : 0;
-                hc = hc * (double)cc;
-            }
+            if (r.threshold_type != SENTINEL_THRESHOLD_GLOBAL) hc = hc * (double)cc;
             hot.emplace_back(hot_keys[j], hc);
         }
     }
     e->pmax_n = maxn;
     int rc = 0;
-    rc |= upload(e->d_prule_ns, nsv);
     rc |= upload(e->d_prule_n, nn);
     rc |= upload(e->d_prule_w, ww);
     rc |= upload(e->d_prule_rcp, rcp);
@@ -839,166 +970,68 @@ int sentinel_load_param_rules(sentinel_engine_t *e, const sentinel_param_rule_t 
     rc |= e->pt.Is.ensure(P * 8);
     rc |= e->pt.thr.ensure(P * 8);
     rc |= e->pt.kind.ensure(P);
-    const int64_t stride = 2 * (int64_t)maxn;
+    const int64_t stride = header_words(maxn);
     rc |= e->pt.state.ensure(P * stride * 8);
-    if (rc) return rc ? SENTINEL_E_NOMEM : 0;
+    if (rc) return SENTINEL_E_NOMEM;
     HIP_OK(hipMemsetAsync(e->d_ptable.p, 0xFF, P * 8, e->stream));
-    HIP_OK(hipMemsetAsync(e->pt.n.p, 0, P * 4, e->stream));
-    k_init_state<<<grid_for((int64_t)P), 256, 0, e->stream>>>(e->pt.state.as<int64_t>(), nullptr, stride, nullptr, maxn, 1, (int64_t)P);
+    k_init_state<<<grid_for((int64_t)P), 256, 0, e->stream>>>(e->pt.state.as<int64_t>(), nullptr, stride, nullptr, maxn,
+                                                              stride, (int64_t)P);
     HIP_OK(hipStreamSynchronize(e->stream));
-    return 0;
+    return e->rebuild_routes();
 }
 
-static int submit_flow(sentinel_engine_t *e, int64_t n, const int32_t *idx, const int32_t *acq, const uint8_t *fl,
-                       const int64_t *ts, int8_t *st, int32_t *rem, int32_t *wt, hipStream_t s) {
-    if (n <= 0) return 0;
-    if (n > (int64_t)0x7FFFFFF0) return fail(SENTINEL_E_INVALID, "batch too large (max 2^31 events)");
-    int rc = e->ensure_ws(n);
-    if (rc) return rc;
-    const int32_t F = (int32_t)e->rules.size();
-    const int fbits = bits_for(F);
-    const uint32_t finvalid = ((uint32_t)1 << fbits) - 1;
-    const bool lim = e->nlimiters > 0;
-    const int lbits = bits_for(e->nlimiters);
-    const uint32_t linvalid = ((uint32_t)1 << lbits) - 1;
-    uint32_t *fkey = e->w_fkey.as<uint32_t>();
-    uint32_t *lkey = lim ? e->w_lkey.as<uint32_t>() : nullptr;
-    e->launch("flow_prep", n, s, [&] {
-        k_flow_prep<<<grid_for(n), 256, 0, s>>>(n, idx, acq, ts, F, e->d_flow_ns.as<int32_t>(), e->ft.kind.as<uint8_t>(),
-                                                e->d_ns_limiter.as<int32_t>(), (int32_t)e->ns.size(), st, rem, wt, fkey,
-                                                finvalid, lkey, linvalid);
-    });
-    Verdicts V{st, rem, wt, fkey, finvalid};
-    if (lim) {
-        KeyTable LT = e->table(e->lt, 1, 20);
-        e->run_pipeline(LT, lkey, n, lbits, ts, nullptr, nullptr, V, s);
-    }
-    if (F > 0) {
-        KeyTable FT = e->table(e->ft, NEV, 0);
-        e->run_pipeline(FT, fkey, n, fbits, ts, acq, fl, V, s);
-    }
-    HIP_OK(hipGetLastError());
-    return 0;
-}
-
-int sentinel_submit_flow_batch(sentinel_engine_t *e, int64_t n, const int32_t *idx, const int32_t *acq,
-                               const uint8_t *fl, const int64_t *ts, int8_t *st, int32_t *rem, int32_t *wt,
-                               void *stream) {
-    if (!e || n < 0 || (n > 0 && (!idx || !acq || !ts || !st || !rem))) return fail(SENTINEL_E_INVALID, "bad arguments");
+int sentinel_submit_flow_batch(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev, const uint8_t *flags,
+                               sentinel_verdict_t *out, void *stream) {
+    if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
-    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
-    return submit_flow(e, n, idx, acq, fl, ts, st, rem, wt, s);
+    return submit_flow(e, n, (const Event *)ev, flags, (uint64_t *)out, stream ? (hipStream_t)stream : e->stream);
 }
 
-int sentinel_submit_flow_batch_host(sentinel_engine_t *e, int64_t n, const int32_t *idx, const int32_t *acq,
-                                    const uint8_t *fl, const int64_t *ts, int8_t *st, int32_t *rem, int32_t *wt) {
-    if (!e || n < 0 || (n > 0 && (!idx || !acq || !ts || !st || !rem))) return fail(SENTINEL_E_INVALID, "bad arguments");
+int sentinel_submit_flow_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev,
+                                    const uint8_t *flags, sentinel_verdict_t *out) {
+    if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
     if (n == 0) return 0;
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
     hipStream_t s = e->stream;
     int rc = 0;
-    rc |= e->io_idx.ensure(n * 4);
-    rc |= e->io_acq.ensure(n * 4);
+    rc |= e->io_ev.ensure(n * sizeof(Event));
     rc |= e->io_fl.ensure(n);
-    rc |= e->io_ts.ensure(n * 8);
-    rc |= e->io_st.ensure(n);
-    rc |= e->io_rem.ensure(n * 4);
-    rc |= e->io_wait.ensure(n * 4);
+    rc |= e->io_out.ensure(n * 8);
     if (rc) return SENTINEL_E_NOMEM;
-    HIP_OK(hipMemcpyAsync(e->io_idx.p, idx, n * 4, hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(e->io_acq.p, acq, n * 4, hipMemcpyHostToDevice, s));
-    if (fl) HIP_OK(hipMemcpyAsync(e->io_fl.p, fl, n, hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(e->io_ts.p, ts, n * 8, hipMemcpyHostToDevice, s));
-    rc = submit_flow(e, n, e->io_idx.as<int32_t>(), e->io_acq.as<int32_t>(), fl ? e->io_fl.as<uint8_t>() : nullptr,
-                     e->io_ts.as<int64_t>(), e->io_st.as<int8_t>(), e->io_rem.as<int32_t>(),
-                     wt ? e->io_wait.as<int32_t>() : nullptr, s);
+    HIP_OK(hipMemcpyAsync(e->io_ev.p, ev, n * sizeof(Event), hipMemcpyHostToDevice, s));
+    if (flags) HIP_OK(hipMemcpyAsync(e->io_fl.p, flags, n, hipMemcpyHostToDevice, s));
+    rc = submit_flow(e, n, e->io_ev.as<Event>(), flags ? e->io_fl.as<uint8_t>() : nullptr, e->io_out.as<uint64_t>(), s);
     if (rc) return rc;
-    HIP_OK(hipMemcpyAsync(st, e->io_st.p, n, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipMemcpyAsync(rem, e->io_rem.p, n * 4, hipMemcpyDeviceToHost, s));
-    if (wt) HIP_OK(hipMemcpyAsync(wt, e->io_wait.p, n * 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     return 0;
 }
 
-static int submit_param(sentinel_engine_t *e, int64_t n, const int32_t *ridx, const int32_t *acq, const uint64_t *pkey,
-                        const int64_t *ts, int8_t *st, int32_t *rem, hipStream_t s) {
-    if (n <= 0) return 0;
-    if (n > (int64_t)0x7FFFFFF0) return fail(SENTINEL_E_INVALID, "batch too large");
-    int rc = e->ensure_ws(n);
-    if (rc) return rc;
-    const int32_t R = (int32_t)e->prules.size();
-    const uint64_t P = e->pcap;
-    const int pbits = bits_for((int64_t)P);
-    const uint32_t pinvalid = ((uint32_t)1 << pbits) - 1;
-    const bool lim = e->nlimiters > 0;
-    const int lbits = bits_for(e->nlimiters);
-    const uint32_t linvalid = ((uint32_t)1 << lbits) - 1;
-    uint32_t *fkey = e->w_fkey.as<uint32_t>();
-    uint32_t *lkey = lim ? e->w_lkey.as<uint32_t>() : nullptr;
-    if (R == 0 || !e->d_ptable.p) {
-        // no param rules: every valid request is NO_RULE_EXISTS (DTS:54-58)
-        k_param_prep<<<grid_for(n), 256, 0, s>>>(n, ridx, acq, pkey, ts, 0, nullptr, nullptr, 0, nullptr, 0, nullptr,
-                                                 st, rem, fkey, pinvalid, nullptr, linvalid);
-        HIP_OK(hipGetLastError());
-        return 0;
-    }
-    k_param_prep<<<grid_for(n), 256, 0, s>>>(n, ridx, acq, pkey, ts, R, e->d_prule_ns.as<int32_t>(),
-                                             e->d_ns_limiter.as<int32_t>(), (int32_t)e->ns.size(),
-                                             e->d_ptable.as<unsigned long long>(), P - 1, e->d_slot_rule.as<int32_t>(),
-                                             st, rem, fkey, pinvalid, lkey, linvalid);
-    k_param_meta<<<grid_for(n), 256, 0, s>>>(n, fkey, pinvalid, pkey, e->d_slot_rule.as<int32_t>(),
-                                             e->d_prule_n.as<int32_t>(), e->d_prule_w.as<int32_t>(),
-                                             e->d_prule_rcp.as<double>(), e->d_prule_Is.as<double>(),
-                                             e->d_prule_thr.as<double>(),
-                                             e->has_hot ? e->d_hot_table.as<unsigned long long>() : nullptr, e->hot_mask,
-                                             e->d_hot_thr.as<double>(), e->pt.n.as<int32_t>(), e->pt.w.as<int32_t>(),
-                                             e->pt.rcp.as<double>(), e->pt.Is.as<double>(), e->pt.thr.as<double>(),
-                                             e->pt.kind.as<uint8_t>());
-    Verdicts V{st, rem, nullptr, fkey, pinvalid};
-    if (lim) {
-        KeyTable LT = e->table(e->lt, 1, 20);
-        e->run_pipeline(LT, lkey, n, lbits, ts, nullptr, nullptr, V, s);
-    }
-    KeyTable PT = e->table(e->pt, 1, 2 * (int64_t)e->pmax_n);
-    e->run_pipeline(PT, fkey, n, pbits, ts, acq, nullptr, V, s);
-    HIP_OK(hipGetLastError());
-    return 0;
-}
-
-int sentinel_submit_param_batch(sentinel_engine_t *e, int64_t n, const int32_t *ridx, const int32_t *acq,
-                                const uint64_t *pkey, const int64_t *ts, int8_t *st, int32_t *rem, void *stream) {
-    if (!e || n < 0 || (n > 0 && (!ridx || !acq || !pkey || !ts || !st || !rem))) return fail(SENTINEL_E_INVALID, "bad arguments");
+int sentinel_submit_param_batch(sentinel_engine_t *e, int64_t n, const sentinel_param_event_t *ev,
+                                sentinel_verdict_t *out, void *stream) {
+    if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
-    return submit_param(e, n, ridx, acq, pkey, ts, st, rem, stream ? (hipStream_t)stream : e->stream);
+    return submit_param(e, n, (const ParamEvent *)ev, (uint64_t *)out, stream ? (hipStream_t)stream : e->stream);
 }
 
-int sentinel_submit_param_batch_host(sentinel_engine_t *e, int64_t n, const int32_t *ridx, const int32_t *acq,
-                                     const uint64_t *pkey, const int64_t *ts, int8_t *st, int32_t *rem) {
-    if (!e || n < 0 || (n > 0 && (!ridx || !acq || !pkey || !ts || !st || !rem))) return fail(SENTINEL_E_INVALID, "bad arguments");
+int sentinel_submit_param_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_param_event_t *ev,
+                                     sentinel_verdict_t *out) {
+    if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
     if (n == 0) return 0;
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
     hipStream_t s = e->stream;
     int rc = 0;
-    rc |= e->io_idx.ensure(n * 4);
-    rc |= e->io_acq.ensure(n * 4);
-    rc |= e->io_pkey.ensure(n * 8);
-    rc |= e->io_ts.ensure(n * 8);
-    rc |= e->io_st.ensure(n);
-    rc |= e->io_rem.ensure(n * 4);
+    rc |= e->io_ev.ensure(n * sizeof(ParamEvent));
+    rc |= e->io_out.ensure(n * 8);
     if (rc) return SENTINEL_E_NOMEM;
-    HIP_OK(hipMemcpyAsync(e->io_idx.p, ridx, n * 4, hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(e->io_acq.p, acq, n * 4, hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(e->io_pkey.p, pkey, n * 8, hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(e->io_ts.p, ts, n * 8, hipMemcpyHostToDevice, s));
-    rc = submit_param(e, n, e->io_idx.as<int32_t>(), e->io_acq.as<int32_t>(), e->io_pkey.as<uint64_t>(),
-                      e->io_ts.as<int64_t>(), e->io_st.as<int8_t>(), e->io_rem.as<int32_t>(), s);
+    HIP_OK(hipMemcpyAsync(e->io_ev.p, ev, n * sizeof(ParamEvent), hipMemcpyHostToDevice, s));
+    rc = submit_param(e, n, e->io_ev.as<ParamEvent>(), e->io_out.as<uint64_t>(), s);
     if (rc) return rc;
-    HIP_OK(hipMemcpyAsync(st, e->io_st.p, n, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipMemcpyAsync(rem, e->io_rem.p, n * 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     return 0;
 }
@@ -1006,15 +1039,16 @@ int sentinel_submit_param_batch_host(sentinel_engine_t *e, int64_t n, const int3
 int sentinel_request_token(sentinel_engine_t *e, int64_t flow_id, int32_t acquire, int32_t prio, int64_t ts,
                            sentinel_token_result_t *out) {
     if (!e || !out) return fail(SENTINEL_E_INVALID, "null argument");
-    int32_t idx;
-    sentinel_lookup_flow_idx(e, 1, &flow_id, &idx);
+    sentinel_event_t ev;
+    sentinel_lookup_flow_idx(e, 1, &flow_id, &ev.flow_idx);
+    ev.acquire = acquire;
+    ev.ts = ts;
     uint8_t fl = prio ? SENTINEL_FLAG_PRIORITIZED : 0;
-    int8_t st = SENTINEL_STATUS_FAIL;
-    int32_t rem = 0, wt = 0;
-    int rc = sentinel_submit_flow_batch_host(e, 1, &idx, &acquire, &fl, &ts, &st, &rem, &wt);
-    out->status = rc ? SENTINEL_STATUS_FAIL : st;
-    out->remaining = rc ? 0 : rem;
-    out->wait_in_ms = rc ? 0 : wt;
+    sentinel_verdict_t v{0, SENTINEL_STATUS_FAIL, 0};
+    int rc = sentinel_submit_flow_batch_host(e, 1, &ev, &fl, &v);
+    out->status = rc ? SENTINEL_STATUS_FAIL : v.status;
+    out->remaining = rc ? 0 : v.remaining;
+    out->wait_in_ms = rc ? 0 : v.wait_in_ms;
     out->reserved = 0;
     return rc;
 }
@@ -1022,13 +1056,15 @@ int sentinel_request_token(sentinel_engine_t *e, int64_t flow_id, int32_t acquir
 int sentinel_request_param_token(sentinel_engine_t *e, int64_t flow_id, int32_t acquire, uint64_t param_key,
                                  int64_t ts, sentinel_token_result_t *out) {
     if (!e || !out) return fail(SENTINEL_E_INVALID, "null argument");
-    int32_t idx;
-    sentinel_lookup_param_idx(e, 1, &flow_id, &idx);
-    int8_t st = SENTINEL_STATUS_FAIL;
-    int32_t rem = 0;
-    int rc = sentinel_submit_param_batch_host(e, 1, &idx, &acquire, &param_key, &ts, &st, &rem);
-    out->status = rc ? SENTINEL_STATUS_FAIL : st;
-    out->remaining = rc ? 0 : rem;
+    sentinel_param_event_t ev;
+    sentinel_lookup_param_idx(e, 1, &flow_id, &ev.rule_idx);
+    ev.acquire = acquire;
+    ev.ts = ts;
+    ev.param_key = param_key;
+    sentinel_verdict_t v{0, SENTINEL_STATUS_FAIL, 0};
+    int rc = sentinel_submit_param_batch_host(e, 1, &ev, &v);
+    out->status = rc ? SENTINEL_STATUS_FAIL : v.status;
+    out->remaining = rc ? 0 : v.remaining;
     out->wait_in_ms = 0;
     out->reserved = 0;
     return rc;
@@ -1050,18 +1086,20 @@ int sentinel_dump_flow(sentinel_engine_t *e, int32_t idx, int64_t *out, int32_t 
     if (out_len < need) return fail(SENTINEL_E_INVALID, "output too small");
     HIP_OK(hipSetDevice(e->device));
     HIP_OK(hipStreamSynchronize(e->stream));
-    std::vector<int64_t> st((1 + NEV) * n);
+    std::vector<int64_t> st(flow_record_words(n));
     HIP_OK(hipMemcpy(st.data(), e->ft.state.as<int64_t>() + e->h_flow_off[idx], st.size() * 8, hipMemcpyDeviceToHost));
     int64_t occ[2];
     uint8_t hocc;
     HIP_OK(hipMemcpy(occ, e->ft.occ.as<int64_t>() + 2 * idx, 16, hipMemcpyDeviceToHost));
     HIP_OK(hipMemcpy(&hocc, e->ft.has_occ.as<uint8_t>() + idx, 1, hipMemcpyDeviceToHost));
     const int64_t w = e->h_flow_w[idx];
+    const int64_t hw = header_words(n);
     for (int j = 0; j < n; ++j) {
         int64_t *o = out + j * (1 + NEV);
         const bool present = st[j] != EPOCH_ABSENT;
         o[0] = present ? st[j] * w : -1;
-        for (int c = 0; c < NEV; ++c) o[1 + c] = present ? st[(1 + c) * n + j] : 0;
+        o[1 + EV_PASS] = present ? st[n + j] : 0;
+        for (int c = 1; c < NEV; ++c) o[1 + c] = present ? st[hw + 8 * j + (c - 1)] : 0;
     }
     int64_t *o = out + n * (1 + NEV);
     for (int c = 0; c < NEV; ++c) o[c] = 0;
@@ -1078,7 +1116,6 @@ int sentinel_param_sum(sentinel_engine_t *e, int32_t ridx, uint64_t pkey, int64_
     HIP_OK(hipSetDevice(e->device));
     HIP_OK(hipStreamSynchronize(e->stream));
     *out = 0;
-    // find the slot on the host (read-only probe of the device table)
     const uint64_t P = e->pcap;
     std::vector<uint64_t> table(P);
     HIP_OK(hipMemcpy(table.data(), e->d_ptable.p, P * 8, hipMemcpyDeviceToHost));
@@ -1091,10 +1128,10 @@ int sentinel_param_sum(sentinel_engine_t *e, int32_t ridx, uint64_t pkey, int64_
     const sentinel_param_rule_t &r = e->prules[ridx];
     const int n = r.sample_count;
     const int64_t w = r.window_interval_ms / n;
-    const int64_t stride = 2 * (int64_t)e->pmax_n;
+    const int64_t stride = header_words(e->pmax_n);
     std::vector<int64_t> st(2 * n);
     HIP_OK(hipMemcpy(st.data(), e->pt.state.as<int64_t>() + h * stride, st.size() * 8, hipMemcpyDeviceToHost));
-    const int64_t E = ts / w;   // read-only view (no roll): valid slots are epochs in (E - n, ...]
+    const int64_t E = ts / w;   // read-only view (no roll): valid slots are epochs in (E - n, E]
     int64_t s = 0;
     for (int j = 0; j < n; ++j)
         if (st[j] != EPOCH_ABSENT && st[j] > E - n && st[j] <= E) s += st[n + j];

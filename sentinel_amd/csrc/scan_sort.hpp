@@ -7,8 +7,10 @@
 //
 // Wave-64 design: a 256-thread workgroup = 4 waves owns a 4096-key tile; each wave ranks its
 // 1024 keys (16 per lane, lane-striped so coalesced loads keep arrival order) with 8 ballots per
-// item (64-bit match masks) and a wave-private LDS digit counter -- no LDS atomics, no 32-lane
-// warp idioms.
+// item (64-bit match masks) and a wave-private LDS digit counter -- no LDS atomics.  The ranked
+// tile is staged in LDS in digit order and written out as contiguous per-digit runs.
+// Pass 0's per-tile digit histogram is fused into the producer of the keys (the prep kernel);
+// each later pass histograms its own input tiles (per-tile offsets need the pass's tiling).
 #pragma once
 
 #include "common.hpp"
@@ -21,6 +23,7 @@ constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;     // 4096
 
 constexpr int RADIX_BITS = 8;
 constexpr int RADIX = 1 << RADIX_BITS;
+constexpr int MAX_PASSES = 4;
 constexpr int SORT_THREADS = 256;
 constexpr int SORT_WAVES = SORT_THREADS / WAVE;
 constexpr int SORT_ITEMS = 16;
@@ -36,8 +39,8 @@ __device__ inline uint32_t wave_inclusive_scan(uint32_t v) {
     return v;
 }
 
-// Block-wide exclusive scan of one value per thread (blockDim = SCAN_THREADS); returns the
-// exclusive prefix and the block total through *total.
+// Block-wide exclusive scan of one value per thread; returns the exclusive prefix and the block
+// total through *total.
 __device__ inline uint32_t block_exclusive_scan(uint32_t v, uint32_t *lds_waves, uint32_t *total) {
     const int lane = (int)lane_id();
     const int wave = threadIdx.x / WAVE;
@@ -94,9 +97,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_tiles(const uint32_t *__r
     if (threadIdx.x == 0) partials[blockIdx.x] = total;
 }
 
-// Pass B: exclusive scan of the tile totals, one workgroup; total into *grand_total.
-__global__ __launch_bounds__(SCAN_THREADS) void k_scan_partials(uint32_t *partials, int64_t nparts,
-                                                                uint32_t *grand_total) {
+// Pass B: exclusive scan of the tile totals, one workgroup.
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_partials(uint32_t *partials, int64_t nparts) {
     __shared__ uint32_t waves[SCAN_THREADS / WAVE];
     uint32_t carry = 0;
     for (int64_t b = 0; b < nparts; b += SCAN_THREADS) {
@@ -107,7 +109,6 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_partials(uint32_t *partia
         if (i < nparts) partials[i] = carry + ex;
         carry += total;
     }
-    if (threadIdx.x == 0 && grand_total) *grand_total = carry;
 }
 
 // Pass C: add the tile offsets.
@@ -125,27 +126,33 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_add(uint32_t *__restrict_
 
 inline int64_t scan_parts(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 
-// Device-wide scan (in may alias out).  partials needs scan_parts(n) words.
-template <bool EXCLUSIVE>
-inline void device_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *partials,
-                        uint32_t *grand_total, hipStream_t s) {
-    if (n <= 0) return;
-    const int64_t nb = scan_parts(n);
-    k_scan_tiles<EXCLUSIVE><<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(in, out, n, partials);
-    k_scan_partials<<<1, SCAN_THREADS, 0, s>>>(partials, nb, grand_total);
-    k_scan_add<<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(out, n, partials);
-}
-
 // ---------------------------------------------------------------- radix sort
 
-__global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t *__restrict__ keys, int64_t n,
-                                                             int shift, uint32_t *__restrict__ hist,
-                                                             int64_t nblocks) {
+inline int64_t sort_blocks(int64_t n) { return (n + SORT_TILE - 1) / SORT_TILE; }
+inline int passes_for(int bits) { return bits <= 0 ? 1 : (bits + RADIX_BITS - 1) / RADIX_BITS; }
+// digit-major histograms of all passes: hist[(p * RADIX + d) * nblocks + b]
+inline int64_t hist_words(int64_t n, int passes) { return sort_blocks(n) * RADIX * passes; }
+
+// Per-tile digit histograms of every pass, from one read of the keys.  The tile of block b is
+// [b*SORT_TILE, (b+1)*SORT_TILE): the same tiling k_radix_scatter uses.
+__device__ inline void tile_hist_accumulate(uint32_t (*h)[RADIX], uint32_t key, int passes) {
+    for (int p = 0; p < passes; ++p) atomicAdd(&h[p][(key >> (p * RADIX_BITS)) & (RADIX - 1)], 1u);
+}
+
+__device__ inline void tile_hist_store(uint32_t (*h)[RADIX], uint32_t *hist, int passes, int64_t nblocks) {
+    for (int p = 0; p < passes; ++p)
+        for (int d = threadIdx.x; d < RADIX; d += blockDim.x)
+            hist[((int64_t)p * RADIX + d) * nblocks + blockIdx.x] = h[p][d];
+}
+
+__global__ __launch_bounds__(SORT_THREADS) void k_radix_hist_pass(const uint32_t *__restrict__ keys, int64_t n,
+                                                                  int shift, uint32_t *__restrict__ hist,
+                                                                  int64_t nblocks) {
     __shared__ uint32_t h[RADIX];
     for (int d = threadIdx.x; d < RADIX; d += SORT_THREADS) h[d] = 0;
     __syncthreads();
     const int64_t base = (int64_t)blockIdx.x * SORT_TILE;
-#pragma unroll
+#pragma unroll 4
     for (int j = 0; j < SORT_ITEMS; ++j) {
         int64_t i = base + j * SORT_THREADS + threadIdx.x;
         if (i < n) atomicAdd(&h[(keys[i] >> shift) & (RADIX - 1)], 1u);
@@ -154,24 +161,30 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t *__r
     for (int d = threadIdx.x; d < RADIX; d += SORT_THREADS) hist[(int64_t)d * nblocks + blockIdx.x] = h[d];
 }
 
-// Stable scatter.  offsets = exclusive scan of the digit-major histogram.
+// Stable scatter of one pass.  offsets = the exclusive scan of all passes' digit-major
+// histograms; pass p's offsets carry p*n from the concatenation, removed via `bias`.
 // vals_in == nullptr means "value = index" (first pass: seq is implicit).
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t *__restrict__ keys_in, const uint32_t *__restrict__ vals_in,
     uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out, int64_t n, int shift,
-    const uint32_t *__restrict__ offsets, int64_t nblocks) {
+    const uint32_t *__restrict__ offsets, int64_t nblocks, uint32_t bias) {
     __shared__ uint32_t cnt[SORT_WAVES][RADIX];
-    __shared__ uint32_t goff[RADIX];
+    __shared__ uint32_t goff[RADIX];       // global start of digit d for this tile
+    __shared__ uint32_t loff[RADIX];       // start of digit d inside the staged tile
+    __shared__ uint32_t waves_tot[SORT_WAVES];
+    __shared__ uint32_t skeys[SORT_TILE];
+    __shared__ uint32_t svals[SORT_TILE];
     const int wave = threadIdx.x / WAVE;
     const uint32_t lane = lane_id();
     for (int d = threadIdx.x; d < RADIX; d += SORT_THREADS) {
 #pragma unroll
         for (int w = 0; w < SORT_WAVES; ++w) cnt[w][d] = 0;
-        goff[d] = offsets[(int64_t)d * nblocks + blockIdx.x];
+        goff[d] = offsets[(int64_t)d * nblocks + blockIdx.x] - bias;
     }
     __syncthreads();
 
-    const int64_t base = (int64_t)blockIdx.x * SORT_TILE + (int64_t)wave * (SORT_ITEMS * WAVE);
+    const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
+    const int64_t base = tile0 + (int64_t)wave * (SORT_ITEMS * WAVE);
     uint32_t key[SORT_ITEMS], val[SORT_ITEMS], rank[SORT_ITEMS];
 #pragma unroll
     for (int j = 0; j < SORT_ITEMS; ++j) {
@@ -179,6 +192,11 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
         const bool valid = i < n;
         key[j] = valid ? keys_in[i] : 0u;
         val[j] = valid ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const int64_t i = base + j * WAVE + lane;
+        const bool valid = i < n;
         const uint32_t d = (key[j] >> shift) & (RADIX - 1);
         uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -188,10 +206,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
             peers &= bit ? bal : ~bal;
         }
         uint32_t r = 0;
-        if (valid) {
-            r = cnt[wave][d] + mask_rank(peers);
-        }
-        // every lane has read its counter; the group leader publishes the new count
+        if (valid) r = cnt[wave][d] + mask_rank(peers);
         __builtin_amdgcn_wave_barrier();
         if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane)
             cnt[wave][d] += (uint32_t)__popcll(peers);
@@ -199,53 +214,40 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
         rank[j] = valid ? r : 0xFFFFFFFFu;
     }
     __syncthreads();
-    for (int d = threadIdx.x; d < RADIX; d += SORT_THREADS) {
+    // per digit: exclusive prefix over waves; tile-local digit starts
+    uint32_t dtot = 0;
+    const int d0 = threadIdx.x;   // SORT_THREADS == RADIX
+    {
         uint32_t run = 0;
 #pragma unroll
         for (int w = 0; w < SORT_WAVES; ++w) {
-            uint32_t c = cnt[w][d];
-            cnt[w][d] = run;
+            uint32_t c = cnt[w][d0];
+            cnt[w][d0] = run;
             run += c;
         }
+        dtot = run;
     }
+    uint32_t total;
+    const uint32_t lstart = block_exclusive_scan(dtot, waves_tot, &total);
+    loff[d0] = lstart;
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < SORT_ITEMS; ++j) {
         if (rank[j] == 0xFFFFFFFFu) continue;
         const uint32_t d = (key[j] >> shift) & (RADIX - 1);
-        const uint32_t dst = goff[d] + cnt[wave][d] + rank[j];
-        keys_out[dst] = key[j];
-        vals_out[dst] = val[j];
+        const uint32_t p = loff[d] + cnt[wave][d] + rank[j];
+        skeys[p] = key[j];
+        svals[p] = val[j];
     }
-}
-
-inline int64_t sort_blocks(int64_t n) { return (n + SORT_TILE - 1) / SORT_TILE; }
-
-// Workspace sizing for radix_sort_pairs.
-inline int64_t sort_hist_words(int64_t n) { return sort_blocks(n) * RADIX; }
-
-// Sorts (keys, vals=seq) by the low `bits` bits of the key.  Results land in (k_out, v_out);
-// (k_tmp, v_tmp) are ping-pong buffers.  keys_in is not modified.
-inline void radix_sort_pairs(const uint32_t *keys_in, int64_t n, int bits, uint32_t *k_out, uint32_t *v_out,
-                             uint32_t *k_tmp, uint32_t *v_tmp, uint32_t *hist, uint32_t *partials,
-                             hipStream_t s) {
-    if (n <= 0) return;
-    const int64_t nb = sort_blocks(n);
-    const int passes = bits <= 0 ? 1 : (bits + RADIX_BITS - 1) / RADIX_BITS;
-    // choose buffer order so the last pass writes (k_out, v_out)
-    uint32_t *kb[2], *vb[2];
-    if (passes % 2 == 1) { kb[0] = k_out; vb[0] = v_out; kb[1] = k_tmp; vb[1] = v_tmp; }
-    else { kb[0] = k_tmp; vb[0] = v_tmp; kb[1] = k_out; vb[1] = v_out; }
-    const uint32_t *kin = keys_in;
-    const uint32_t *vin = nullptr;
-    for (int p = 0; p < passes; ++p) {
-        const int shift = p * RADIX_BITS;
-        k_radix_hist<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(kin, n, shift, hist, nb);
-        device_scan<true>(hist, hist, nb * RADIX, partials, nullptr, s);
-        k_radix_scatter<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(kin, vin, kb[p % 2], vb[p % 2], n,
-                                                                          shift, hist, nb);
-        kin = kb[p % 2];
-        vin = vb[p % 2];
+    __syncthreads();
+    // contiguous per-digit runs: consecutive threads write consecutive addresses
+    const int64_t valid_in_tile = (n - tile0) < SORT_TILE ? (n - tile0) : SORT_TILE;
+    for (int p = threadIdx.x; p < valid_in_tile; p += SORT_THREADS) {
+        const uint32_t k = skeys[p];
+        const uint32_t d = (k >> shift) & (RADIX - 1);
+        const uint32_t dst = goff[d] + (uint32_t)p - loff[d];
+        keys_out[dst] = k;
+        vals_out[dst] = svals[p];
     }
 }
 

@@ -235,65 +235,65 @@ class GpuTokenService:
         raise NotImplementedError("concurrent (thread-grade) cluster tokens are a SURVEY §8(f) 'next' row")
 
     # ---------------------------------------------------------------- batched hot path
-    def submit_flow_batch(self, flow_idx, acquire, ts, flags=None, status=None, remaining=None, wait_ms=None,
-                          stream=None):
-        """Decide a batch of device-resident events (torch tensors on this GPU).  Asynchronous on
-        `stream` (a torch.cuda.Stream or raw hipStream_t int; default: the engine stream)."""
+    @staticmethod
+    def pack_events(flow_idx, acquire, ts) -> np.ndarray:
+        ev = np.empty(len(ts), dtype=_lib.EVENT_DTYPE)
+        ev["flow_idx"] = flow_idx
+        ev["acquire"] = acquire
+        ev["ts"] = ts
+        return ev
+
+    @staticmethod
+    def pack_param_events(rule_idx, acquire, param_key, ts) -> np.ndarray:
+        ev = np.empty(len(ts), dtype=_lib.PARAM_EVENT_DTYPE)
+        ev["rule_idx"] = rule_idx
+        ev["acquire"] = acquire
+        ev["ts"] = ts
+        ev["param_key"] = param_key
+        return ev
+
+    def submit_flow_batch(self, events, flags=None, verdicts=None, stream=None):
+        """Decide a batch of device-resident events.  `events` is a torch int64 tensor of shape
+        (n, 2) holding sentinel_event_t records (word0 = acquire << 32 | flow_idx, word1 = ts);
+        verdicts is an int64 tensor (n,) of packed sentinel_verdict_t.  Asynchronous on `stream`
+        (torch stream or raw hipStream_t; default the engine stream)."""
         import torch
-        n = int(flow_idx.numel())
-        dev = flow_idx.device
-        if status is None:
-            status = torch.empty(n, dtype=torch.int8, device=dev)
-        if remaining is None:
-            remaining = torch.empty(n, dtype=torch.int32, device=dev)
+        n = int(events.shape[0])
+        if verdicts is None:
+            verdicts = torch.empty(n, dtype=torch.int64, device=events.device)
         s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
         rc = self._L.sentinel_submit_flow_batch(
-            self._h, n, C.c_void_p(flow_idx.data_ptr()), C.c_void_p(acquire.data_ptr()),
-            None if flags is None else C.c_void_p(flags.data_ptr()), C.c_void_p(ts.data_ptr()),
-            C.c_void_p(status.data_ptr()), C.c_void_p(remaining.data_ptr()),
-            None if wait_ms is None else C.c_void_p(wait_ms.data_ptr()), None if s is None else C.c_void_p(s))
+            self._h, n, C.c_void_p(events.data_ptr()), None if flags is None else C.c_void_p(flags.data_ptr()),
+            C.c_void_p(verdicts.data_ptr()), None if s is None else C.c_void_p(s))
         check(rc, "submit_flow_batch")
-        return status, remaining, wait_ms
+        return verdicts
 
     def submit_flow_batch_host(self, flow_idx, acquire, ts, flags=None):
-        n = len(ts)
-        flow_idx = np.ascontiguousarray(flow_idx, dtype=np.int32)
-        acquire = np.ascontiguousarray(acquire, dtype=np.int32)
-        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        """Host arrays in, (status, remaining, wait_in_ms) numpy arrays out (synchronous)."""
+        ev = self.pack_events(flow_idx, acquire, ts)
         flags = None if flags is None else np.ascontiguousarray(flags, dtype=np.uint8)
-        status = np.empty(n, dtype=np.int8)
-        remaining = np.empty(n, dtype=np.int32)
-        wait = np.empty(n, dtype=np.int32)
-        check(self._L.sentinel_submit_flow_batch_host(self._h, n, _p(flow_idx), _p(acquire), _p(flags), _p(ts),
-                                                      _p(status), _p(remaining), _p(wait)), "submit_flow_batch_host")
-        return status, remaining, wait
+        out = np.empty(len(ev), dtype=_lib.VERDICT_DTYPE)
+        check(self._L.sentinel_submit_flow_batch_host(self._h, len(ev), _p(ev), _p(flags), _p(out)),
+              "submit_flow_batch_host")
+        return out["status"].astype(np.int8), out["remaining"].copy(), out["wait_in_ms"].astype(np.int32)
 
-    def submit_param_batch(self, rule_idx, acquire, param_key, ts, status=None, remaining=None, stream=None):
+    def submit_param_batch(self, events, verdicts=None, stream=None):
+        """events: torch int64 tensor (n, 3) of sentinel_param_event_t records."""
         import torch
-        n = int(rule_idx.numel())
-        dev = rule_idx.device
-        if status is None:
-            status = torch.empty(n, dtype=torch.int8, device=dev)
-        if remaining is None:
-            remaining = torch.empty(n, dtype=torch.int32, device=dev)
+        n = int(events.shape[0])
+        if verdicts is None:
+            verdicts = torch.empty(n, dtype=torch.int64, device=events.device)
         s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
-        check(self._L.sentinel_submit_param_batch(
-            self._h, n, C.c_void_p(rule_idx.data_ptr()), C.c_void_p(acquire.data_ptr()),
-            C.c_void_p(param_key.data_ptr()), C.c_void_p(ts.data_ptr()), C.c_void_p(status.data_ptr()),
-            C.c_void_p(remaining.data_ptr()), None if s is None else C.c_void_p(s)), "submit_param_batch")
-        return status, remaining
+        check(self._L.sentinel_submit_param_batch(self._h, n, C.c_void_p(events.data_ptr()),
+                                                  C.c_void_p(verdicts.data_ptr()), None if s is None else C.c_void_p(s)),
+              "submit_param_batch")
+        return verdicts
 
     def submit_param_batch_host(self, rule_idx, acquire, param_key, ts):
-        n = len(ts)
-        rule_idx = np.ascontiguousarray(rule_idx, dtype=np.int32)
-        acquire = np.ascontiguousarray(acquire, dtype=np.int32)
-        param_key = np.ascontiguousarray(param_key, dtype=np.uint64)
-        ts = np.ascontiguousarray(ts, dtype=np.int64)
-        status = np.empty(n, dtype=np.int8)
-        remaining = np.empty(n, dtype=np.int32)
-        check(self._L.sentinel_submit_param_batch_host(self._h, n, _p(rule_idx), _p(acquire), _p(param_key), _p(ts),
-                                                       _p(status), _p(remaining)), "submit_param_batch_host")
-        return status, remaining
+        ev = self.pack_param_events(rule_idx, acquire, param_key, ts)
+        out = np.empty(len(ev), dtype=_lib.VERDICT_DTYPE)
+        check(self._L.sentinel_submit_param_batch_host(self._h, len(ev), _p(ev), _p(out)), "submit_param_batch_host")
+        return out["status"].astype(np.int8), out["remaining"].copy()
 
     def synchronize(self):
         check(self._L.sentinel_synchronize(self._h), "synchronize")
@@ -320,6 +320,20 @@ class GpuTokenService:
         check(self._L.sentinel_snapshot_device(self._h, int(ts), C.c_void_p(out_tensor.data_ptr()),
                                                None if s is None else C.c_void_p(s)), "snapshot_device")
         return out_tensor
+
+
+def decode_verdicts(v):
+    """Packed int64 verdicts (torch or numpy) -> (status int16, remaining int32, wait uint16) numpy."""
+    a = v.cpu().numpy() if hasattr(v, "cpu") else np.asarray(v)
+    a = a.view(_lib.VERDICT_DTYPE)
+    return a["status"], a["remaining"], a["wait_in_ms"]
+
+
+def device_events(flow_idx, acquire, ts):
+    """Build the (n, 2) int64 device tensor of sentinel_event_t records from torch tensors."""
+    import torch
+    w0 = (acquire.to(torch.int64) << 32) | (flow_idx.to(torch.int64) & 0xFFFFFFFF)
+    return torch.stack([w0, ts.to(torch.int64)], dim=1).contiguous()
 
 
 def device_count() -> int:

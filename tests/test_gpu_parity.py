@@ -226,9 +226,11 @@ def test_full_size_properties_config3():
     acq = torch.ones(n, dtype=torch.int32, device="cuda")
     rate = 2.0 * float(rules.count.sum())
     ts = (T.T0_ALIGNED + torch.floor(torch.arange(n, device="cuda", dtype=torch.float64) * (1000.0 / rate))).to(torch.int64)
-    st, rem, _ = svc.submit_flow_batch(idx, acq, ts)
-    torch.cuda.synchronize()
-    st_c = st.cpu().numpy()
+    from sentinel_amd.token_service import decode_verdicts, device_events
+    ev = device_events(idx, acq, ts)
+    v = svc.submit_flow_batch(ev)
+    svc.synchronize()
+    st_c, rem_c, _ = decode_verdicts(v)
     assert set(np.unique(st_c)).issubset({0, 1})
     # conservation: passes per flow == PASS counter growth; admission bound: passes <= threshold
     passes = np.bincount(idx.cpu().numpy()[st_c == 0], minlength=len(rules))
@@ -239,6 +241,6 @@ def test_full_size_properties_config3():
         assert passes[f] <= rules.count[f] * 1.0 + 1e-9
     # determinism: a fresh engine on the same input gives identical verdicts
     svc2 = _engine(rules)
-    st2, rem2, _ = svc2.submit_flow_batch(idx, acq, ts)
-    torch.cuda.synchronize()
-    assert torch.equal(st, st2) and torch.equal(rem, rem2)
+    v2 = svc2.submit_flow_batch(ev)
+    svc2.synchronize()
+    assert torch.equal(v, v2)
