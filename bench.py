@@ -31,12 +31,12 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-leve
 KERNEL_BYTES_PER_EVENT = {
     "flow_prep": 20.0,        # read the 16-B event, write the 4-B sort key (histograms stay in LDS)
     "radix_hist": 4.0,        # read key
-    "radix_scatter": 16.0,    # read key+seq, write key+seq (first pass reads key only: 12)
+    "radix_scatter": None,    # per pass: read key 4 + value 8, write 12; pass 0 reads the 16-B event instead of a value
     "scan_tiles": 8.0,
     "scan_add": 8.0,
-    "seg_heads": 29.0,        # read skey+sseq 8, gather the 16-B event, write head 4 + bad 1
-    "seg_mark": 5.0,          # read segid 4 + bad 1 (segment records are per segment)
-    "verdict": 16.0,          # read segid 4 + sseq 4, write the 8-B verdict
+    "seg_heads": 17.0,        # read key 4 + value 8, write head 4 + homogeneity flag 1
+    "seg_mark": 5.0,          # read segid 4 + flag 1 (segment records are per segment)
+    "verdict": 20.0,          # read segid 4 + value 8, write the 8-B verdict
 }
 
 
@@ -177,7 +177,8 @@ def main():
             e_f = N / max(1, F)
             bpe = (args.sample_count * 16 + 40 + 24) / max(1.0, min(e_f, 1e9)) if F else 0.0
         if dom == "radix_scatter":
-            bpe = 16.0
+            passes = max(1, round(d["calls"] / max(1, args.steps)))
+            bpe = (32.0 + 24.0 * (passes - 1)) / passes
         ach = (bpe or 0.0) * d["units_per_call"] / (d["avg_us"] * 1e-6) / 1e9
         roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,

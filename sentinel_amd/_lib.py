@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsentinel_amd.so")
+LIB_PATH = os.environ.get("SENTINEL_LIB") or os.path.join(_HERE, "libsentinel_amd.so")
 
 STATUS_BAD_REQUEST = -4
 STATUS_TOO_MANY_REQUEST = -2

@@ -21,11 +21,11 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in DEPS)
 
 
-def build(force: bool = False) -> str:
-    if force or needs_build():
-        cmd = [HIPCC, *FLAGS, "-o", OUT, *SOURCES]
+def build(force: bool = False, out: str = OUT, defines=()) -> str:
+    if force or needs_build() or out != OUT:
+        cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-o", out, *SOURCES]
         subprocess.run(cmd, check=True)
-    return OUT
+    return out
 
 
 if __name__ == "__main__":

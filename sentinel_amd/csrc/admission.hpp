@@ -16,13 +16,14 @@
 // slot (E + 1) mod n under the same validity test.  The proof is in DESIGN.md ("Window algebra").
 //
 // State layout per key (int64 words, 64-byte aligned records):
-//   header  : epoch[n], pass[n]            (padded to a multiple of 8 words)
+//   header  : {epoch_j, pass_j} pairs      (16 B per slot, padded to a multiple of 64 B)
 //   rest    : n slots x 8 words            (only for 7-counter flow keys)
 //             {BLOCK, PASS_REQUEST, BLOCK_REQUEST, OCCUPIED_PASS, OCCUPIED_BLOCK, WAITING, -, -}
 // The fast path reads only the header (16n bytes) and writes one header word pair + one rest line.
 #pragma once
 
 #include "common.hpp"
+#include "scan_sort.hpp"
 
 namespace sentinel {
 
@@ -59,6 +60,16 @@ struct KeyTable {
     double max_occupy_ratio; // ServerFlowConfig.maxOccupyRatio
 };
 
+// The sorted 64-bit value of an event: [0,28) arrival position, [28] prioritized flag,
+// [29,53) ts - T0 (signed 24 bits), [53,64) acquire (11 bits).  Out-of-range ts deltas or
+// acquire counts use the all-ones escape and are read back from the event itself.
+constexpr uint32_t SEQ_MASK = 0x0FFFFFFFu;
+constexpr uint64_t VAL_PRIO = 1ull << 28;
+constexpr int VAL_DT_SHIFT = 29;
+constexpr uint32_t VAL_DT_ESC = 0xFFFFFFu;      // 24 bits
+constexpr int VAL_ACQ_SHIFT = 53;
+constexpr uint32_t VAL_ACQ_ESC = 0x7FFu;        // 11 bits
+
 // Where the events of a pipeline run come from (one of the two is non-null).
 struct EventSrc {
     const Event *ev;
@@ -72,11 +83,40 @@ struct EventSrc {
         if (unit_acquire) a = 1;
         fl = flags ? flags[s] : 0;
     }
+
+    __device__ inline int64_t t0() const { return ev ? ev[0].ts : pev[0].ts; }
+
+    // Sorted value of arrival position s (layout above).
+    __device__ inline uint64_t pack(uint32_t s, int64_t T0) const {
+        int64_t t;
+        int32_t a;
+        uint8_t fl;
+        load(s, t, a, fl);
+        const int64_t dt = t - T0;
+        const uint32_t dtf = (dt > -(1 << 23) && dt < (1 << 23) - 1) ? ((uint32_t)dt & VAL_DT_ESC) : VAL_DT_ESC;
+        const uint32_t af = (a > 0 && a < (int32_t)VAL_ACQ_ESC) ? (uint32_t)a : VAL_ACQ_ESC;
+        return (uint64_t)s | ((fl & 1u) ? VAL_PRIO : 0ull) | ((uint64_t)dtf << VAL_DT_SHIFT) | ((uint64_t)af << VAL_ACQ_SHIFT);
+    }
+
+    // Timestamp, acquire and prioritized flag of a sorted value (exact: escapes read the event).
+    __device__ inline void unpack(uint64_t v, int64_t T0, int64_t &t, int32_t &a, bool &prio) const {
+        const uint32_t dtf = (uint32_t)(v >> VAL_DT_SHIFT) & VAL_DT_ESC;
+        const uint32_t af = (uint32_t)(v >> VAL_ACQ_SHIFT) & VAL_ACQ_ESC;
+        prio = (v & VAL_PRIO) != 0;
+        if (dtf == VAL_DT_ESC || af == VAL_ACQ_ESC) {
+            uint8_t fl;
+            load((uint32_t)v & SEQ_MASK, t, a, fl);
+            return;
+        }
+        t = T0 + (int64_t)((int32_t)(dtf << 8) >> 8);
+        a = unit_acquire ? 1 : (int32_t)af;
+    }
 };
 
 // Batch working set, all device pointers, sized for n events.
 struct BatchWork {
-    uint32_t *skey, *sseq;       // sorted keys / arrival positions
+    uint32_t *skey;              // sorted keys
+    uint64_t *sval;              // sorted values (arrival position, prio, ts - T0, acquire)
     uint32_t *segid;             // head flags, scanned in place (1-based segment id)
     uint8_t *bad;                // element breaks segment homogeneity (acquire differs / prioritized)
     int64_t *h_epoch;            // epoch at head positions (sparse)
@@ -94,9 +134,11 @@ struct BatchWork {
 };
 
 // Packed TokenResult: {int32 remaining; int16 status; uint16 waitInMs} as one 8-byte store.
+__device__ inline uint64_t pack_verdict(int status, int32_t remaining, int wait) {
+    return (uint64_t)(uint32_t)remaining | ((uint64_t)(uint16_t)(int16_t)status << 32) | ((uint64_t)(uint16_t)wait << 48);
+}
 __device__ inline void put_verdict(uint64_t *out, uint32_t seq, int status, int32_t remaining, int wait) {
-    out[seq] = (uint64_t)(uint32_t)remaining | ((uint64_t)(uint16_t)(int16_t)status << 32) |
-               ((uint64_t)(uint16_t)wait << 48);
+    out[seq] = pack_verdict(status, remaining, wait);
 }
 
 // Outputs of one pipeline run.
@@ -111,12 +153,12 @@ struct KeyState {
     int64_t *base;
     int n;
     bool seven;   // 7-counter flow layout
-    __device__ inline int64_t *epoch() const { return base; }
-    __device__ inline int64_t *pass() const { return base + n; }
+    __device__ inline int64_t &ep(int slot) const { return base[2 * slot]; }
     __device__ inline int64_t &cnt(int ev, int slot) const {
-        if (ev == EV_PASS || !seven) return base[n + slot];
-        return base[header_words(n) + 8 * (int64_t)slot + (ev - 1)];
+        if (ev == EV_PASS || !seven) return base[2 * slot + 1];
+        return rest(slot)[ev - 1];
     }
+    __device__ inline int64_t *rest(int slot) const { return base + header_words(n) + 8 * (int64_t)slot; }
 };
 
 __device__ inline KeyState key_state(const KeyTable &T, uint32_t key) {
@@ -131,13 +173,12 @@ __device__ inline KeyState key_state(const KeyTable &T, uint32_t key) {
 // LeapArray.currentWindow(t) on epochs: returns the slot, or -1 for the detached wrap (clock
 // went backwards: LeapArray.java:241-246, writes to it are lost).
 __device__ inline int roll(const KeyTable &T, uint32_t key, const KeyState &S, int64_t E) {
-    int64_t *ep = S.epoch();
     const int slot = (int)(E % S.n);
-    const int64_t cur = ep[slot];
+    const int64_t cur = S.ep(slot);
     if (cur == E) return slot;                                  // LA:195-209 same window
     if (cur != EPOCH_ABSENT && cur > E) return -1;              // LA:241-246 detached
     const bool reset = cur != EPOCH_ABSENT;                     // LA:210-240 vs LA:172-194
-    ep[slot] = E;
+    S.ep(slot) = E;
     S.cnt(EV_PASS, slot) = 0;
     if (S.seven) {
         int64_t *r = &S.cnt(EV_BLOCK, slot);
@@ -158,10 +199,9 @@ __device__ inline int roll(const KeyTable &T, uint32_t key, const KeyState &S, i
 }
 
 __device__ inline int64_t window_sum(const KeyState &S, int64_t E, int ev) {
-    const int64_t *ep = S.epoch();
     int64_t s = 0;
     for (int j = 0; j < S.n; ++j) {
-        const int64_t e = ep[j];
+        const int64_t e = S.ep(j);
         if (e != EPOCH_ABSENT && e > E - S.n) s = wrap_add(s, S.cnt(ev, j));
     }
     return s;
@@ -235,7 +275,7 @@ __device__ inline void seq_event(const KeyTable &T, uint32_t key, const KeyState
             roll(T, key, S, E);
             const double latest = (double)window_sum(S, E, EV_PASS) / I_s;
             const int hs = (int)((E + 1) % S.n);
-            const int64_t he = S.epoch()[hs];
+            const int64_t he = S.ep(hs);
             const int64_t head = (he != EPOCH_ABSENT && he > E - S.n) ? S.cnt(EV_PASS, hs) : 0;
             int64_t *o = T.occ + 2 * (int64_t)key;
             const int64_t inner = wrap_add((int64_t)a, o[0]);
@@ -259,6 +299,96 @@ __device__ inline void seq_event(const KeyTable &T, uint32_t key, const KeyState
     put_verdict(V.out, seq, ST_BLOCKED, 0, 0);
 }
 
+// K2 pass with payload: stable scatter of (key, seq|prio, payload) by one 8-bit digit.  The first
+// pass (FIRST) reads the arrival-ordered events themselves, so the sorted events never have to
+// be gathered back by position: later kernels read key, seq and {ts - T0, acquire} coalesced.
+// Tile = 4096 (4 waves x 16 items, lane-striped to keep arrival order), ranked with 8 ballots
+// per item, staged in LDS in digit order and written as contiguous per-digit runs.
+template <bool FIRST>
+__global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter_p(
+    const uint32_t *__restrict__ keys_in, const uint64_t *__restrict__ vals_in, EventSrc src,
+    uint32_t *__restrict__ keys_out, uint64_t *__restrict__ vals_out, int64_t n, int shift,
+    const uint32_t *__restrict__ offsets, int64_t nblocks) {
+    __shared__ uint32_t cnt[SORT_WAVES][RADIX];
+    __shared__ uint32_t goff[RADIX];
+    __shared__ uint32_t loff[RADIX];
+    __shared__ uint32_t waves_tot[SORT_WAVES];
+    __shared__ uint32_t skeys[SORT_TILE];
+    __shared__ uint64_t svals[SORT_TILE];
+    const int wave = threadIdx.x / WAVE;
+    const uint32_t lane = lane_id();
+    for (int d = threadIdx.x; d < RADIX; d += SORT_THREADS) {
+#pragma unroll
+        for (int w = 0; w < SORT_WAVES; ++w) cnt[w][d] = 0;
+        goff[d] = offsets[(int64_t)d * nblocks + blockIdx.x];
+    }
+    __syncthreads();
+    const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
+    const int64_t base = tile0 + (int64_t)wave * (SORT_ITEMS * WAVE);
+    const int64_t T0 = FIRST ? src.t0() : 0;
+    uint32_t key[SORT_ITEMS], rank[SORT_ITEMS];
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const int64_t i = base + j * WAVE + lane;
+        key[j] = i < n ? keys_in[i] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const int64_t i = base + j * WAVE + lane;
+        const bool valid = i < n;
+        const uint32_t d = (key[j] >> shift) & (RADIX - 1);
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < RADIX_BITS; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bal = __ballot(valid && bit);
+            peers &= bit ? bal : ~bal;
+        }
+        uint32_t r = 0;
+        if (valid) r = cnt[wave][d] + mask_rank(peers);
+        __builtin_amdgcn_wave_barrier();
+        if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane)
+            cnt[wave][d] += (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        rank[j] = valid ? r : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    uint32_t dtot = 0;
+    const int d0 = threadIdx.x;   // one thread per digit (SORT_THREADS >= RADIX)
+    if (d0 < RADIX) {
+        uint32_t run = 0;
+#pragma unroll
+        for (int w = 0; w < SORT_WAVES; ++w) {
+            const uint32_t c = cnt[w][d0];
+            cnt[w][d0] = run;
+            run += c;
+        }
+        dtot = run;
+    }
+    uint32_t total;
+    const uint32_t lst = block_exclusive_scan(dtot, waves_tot, &total);
+    if (d0 < RADIX) loff[d0] = lst;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        if (rank[j] == 0xFFFFFFFFu) continue;
+        const int64_t i = base + j * WAVE + lane;
+        const uint32_t d = (key[j] >> shift) & (RADIX - 1);
+        const uint32_t p = loff[d] + cnt[wave][d] + rank[j];
+        skeys[p] = key[j];
+        svals[p] = FIRST ? src.pack((uint32_t)i, T0) : vals_in[i];
+    }
+    __syncthreads();
+    const int64_t valid_in_tile = (n - tile0) < SORT_TILE ? (n - tile0) : SORT_TILE;
+    for (int p = threadIdx.x; p < valid_in_tile; p += SORT_THREADS) {
+        const uint32_t k = skeys[p];
+        const uint32_t d = (k >> shift) & (RADIX - 1);
+        const uint32_t dst = goff[d] + (uint32_t)p - loff[d];
+        keys_out[dst] = k;
+        vals_out[dst] = svals[p];
+    }
+}
+
 // ------------------------------------------------------------------------- kernels
 
 // Segment heads.  Each sorted event's epoch is computed once; neighbours are exchanged in LDS.
@@ -270,15 +400,16 @@ __global__ __launch_bounds__(256) void k_seg_heads(KeyTable T, BatchWork W, Even
     __shared__ int64_t s_ep[256];
     __shared__ int32_t s_acq[256];
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t T0 = src.t0();
     uint32_t key = invalid;
     int64_t E = 0;
     int32_t a = 0;
-    uint8_t fl = 0;
+    bool prio = false;
     if (i < n) {
         key = W.skey[i];
         if (key != invalid) {
             int64_t t;
-            src.load(W.sseq[i], t, a, fl);
+            src.unpack(W.sval[i], T0, t, a, prio);
             E = epoch_of(t, T.w[key], T.rcp_w[key]);
         }
     }
@@ -300,13 +431,13 @@ __global__ __launch_bounds__(256) void k_seg_heads(KeyTable T, BatchWork W, Even
     else {
         pk = W.skey[i - 1];
         int64_t t;
-        uint8_t f2;
-        src.load(W.sseq[i - 1], t, pa, f2);
+        bool pp;
+        src.unpack(W.sval[i - 1], T0, t, pa, pp);
         pE = epoch_of(t, T.w[pk], T.rcp_w[pk]);
     }
     const bool head = pk != key || pE != E;
     W.segid[i] = head ? 1u : 0u;
-    const bool prio = (fl & 1u) && T.kind[key] == KIND_CLUSTER;
+    prio = prio && T.kind[key] == KIND_CLUSTER;
     W.bad[i] = (!head && pa != a) || prio;
     if (head) { W.h_epoch[i] = E; W.h_acq[i] = a; }
     if (i == n - 1 || W.skey[i + 1] == invalid) *W.nvalid = (uint32_t)(i + 1);
@@ -351,14 +482,14 @@ __global__ __launch_bounds__(256) void k_process(KeyTable T, BatchWork W, EventS
         const int64_t E = W.seg_epoch[g];
         // fast path eligibility: homogeneous, and time did not move backwards for this key
         bool fast = !W.seg_het[g];
+        if (fast && ks.seven && kind == KIND_CLUSTER && T.has_occ[key]) fast = false;   // occupy transfer pending
         if (fast) {
-            const int64_t *ep = ks.epoch();
             for (int j = 0; j < ks.n; ++j)
-                if (ep[j] != EPOCH_ABSENT && ep[j] > E) { fast = false; break; }
+                if (ks.ep(j) != EPOCH_ABSENT && ks.ep(j) > E) { fast = false; break; }
         }
         if (!fast) {
             for (uint32_t i = st; i < st + len; ++i) {
-                const uint32_t seq = W.sseq[i];
+                const uint32_t seq = (uint32_t)W.sval[i] & SEQ_MASK;
                 int64_t t;
                 int32_t a;
                 uint8_t fl;
@@ -391,7 +522,251 @@ __global__ __launch_bounds__(256) void k_process(KeyTable T, BatchWork W, EventS
     }
 }
 
+// K1+K3, one thread per key with the key's header {epoch, pass} pairs held in registers
+// (NMAX >= n).  All header lines are requested at once with 16-byte loads, so each line of the
+// state crosses the memory system once per batch; only the rolled slot's pair and its rest line
+// are written back.  Slow segments fall back to the sequential path on global memory.
+template <int NMAX>
+__global__ __launch_bounds__(256) void k_process_reg(KeyTable T, BatchWork W, EventSrc src, Verdicts V, int64_t n) {
+    const int64_t g0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t S = (int64_t)*W.nseg;
+    if (g0 >= S || (int64_t)*W.nvalid == 0) return;
+    const uint32_t key = W.seg_key[g0];
+    if (g0 > 0 && W.seg_key[g0 - 1] == key) return;    // not the first segment of its key
+    const KeyState ks = key_state(T, key);
+    const int nsc = ks.n;
+    const uint8_t kind = T.kind[key];
+    const double thr = T.thr[key];
+    const double I_s = T.I_s[key];
+    int64_t ep[NMAX], ps[NMAX];
+    uint32_t dirty = 0;
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+        if (j < nsc) {
+            const longlong2 v = *reinterpret_cast<const longlong2 *>(ks.base + 2 * j);
+            ep[j] = v.x;
+            ps[j] = v.y;
+        } else {
+            ep[j] = EPOCH_ABSENT;
+            ps[j] = 0;
+        }
+    }
+    bool occ_pending = ks.seven && kind == KIND_CLUSTER && T.has_occ[key];
+    for (int64_t g = g0; g < S; ++g) {
+        if (g > g0 && W.seg_key[g] != key) break;
+        const uint32_t st = W.seg_start[g];
+        const uint32_t len = W.seg_start[g + 1] - st;
+        const int64_t E = W.seg_epoch[g];
+        bool slow = W.seg_het[g] || occ_pending;
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j) slow |= (ep[j] != EPOCH_ABSENT && ep[j] > E);
+        if (slow) {
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j)
+                if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.base + 2 * j) = longlong2{ep[j], ps[j]};
+            dirty = 0;
+            for (uint32_t i = st; i < st + len; ++i) {
+                const uint32_t seq = (uint32_t)W.sval[i] & SEQ_MASK;
+                int64_t t;
+                int32_t a;
+                uint8_t fl;
+                src.load(seq, t, a, fl);
+                seq_event(T, key, ks, E, a, fl, seq, V);
+            }
+            W.seg_done[g] = 1;
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j)
+                if (j < nsc) { ep[j] = ks.ep(j); ps[j] = ks.cnt(EV_PASS, j); }
+            // the sequential path may have left an occupy transfer pending
+            occ_pending = ks.seven && kind == KIND_CLUSTER && T.has_occ[key];
+            continue;
+        }
+        const int32_t a = W.seg_acq[g];
+        const int slot = (int)(E % nsc);
+        bool fresh = false;
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j)
+            if (j == slot && ep[j] != E) { fresh = true; ep[j] = E; ps[j] = 0; }
+        int64_t s0 = 0;
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j)
+            if (ep[j] != EPOCH_ABSENT && ep[j] > E - nsc) s0 = wrap_add(s0, ps[j]);
+        uint32_t lo = 0, hi = len;                      // K = first p with !admits(S0 + p*a)
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            if (admits(kind, thr, I_s, wrap_add(s0, wrap_mul((int64_t)mid, a)), a)) lo = mid + 1;
+            else hi = mid;
+        }
+        const uint32_t K = lo;
+        const int64_t nb = (int64_t)(len - K);
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j)
+            if (j == slot) { ps[j] = wrap_add(ps[j], wrap_mul((int64_t)K, a)); dirty |= 1u << j; }
+        if (ks.seven) {
+            int64_t *r = ks.rest(slot);
+            int64_t blk = 0, preq = 0, breq = 0;
+            if (!fresh) { blk = r[0]; preq = r[1]; breq = r[2]; }
+            *reinterpret_cast<longlong2 *>(r) = longlong2{wrap_add(blk, wrap_mul(nb, a)), wrap_add(preq, (int64_t)K)};
+            r[2] = wrap_add(breq, nb);
+            if (fresh) {
+                *reinterpret_cast<longlong2 *>(r + 3) = longlong2{0, 0};
+                *reinterpret_cast<longlong2 *>(r + 5) = longlong2{0, 0};
+            }
+        }
+        W.seg_s0[g] = s0;
+        W.seg_k[g] = K;
+        W.seg_done[g] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j)
+        if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.base + 2 * j) = longlong2{ep[j], ps[j]};
+}
+
+// K1+K3 with a lane group per key (G lanes, up to PROC_SLOTS_PER_LANE slots per lane, so
+// n <= G * PROC_SLOTS_PER_LANE): the header {epoch, pass} pairs of one key are read by the group
+// with coalesced 16-byte loads, the window sum is a group reduction, and only the rolled slot is
+// written back.  Segments that are heterogeneous, prioritized, behind the key's newest epoch or
+// carry a pending occupy transfer run the sequential path on lane 0 of the group.
+constexpr int PROC_G = 16;
+constexpr int PROC_SLOTS_PER_LANE = 4;
+
+__device__ inline int64_t group_sum(int64_t v) {
+#pragma unroll
+    for (int m = PROC_G / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, PROC_G);
+    return v;
+}
+
+__device__ inline bool group_any(bool p) {
+    int v = p ? 1 : 0;
+#pragma unroll
+    for (int m = PROC_G / 2; m >= 1; m >>= 1) v |= __shfl_xor(v, m, PROC_G);
+    return v != 0;
+}
+
+__device__ inline void process_key_group(const KeyTable &T, const BatchWork &W, const EventSrc &src,
+                                         const Verdicts &V, int64_t g0, int64_t S, int lg) {
+    const uint32_t key = W.seg_key[g0];
+    const KeyState ks = key_state(T, key);
+    const int nsc = ks.n;
+    const uint8_t kind = T.kind[key];
+    const double thr = T.thr[key];
+    const double I_s = T.I_s[key];
+    int64_t ep[PROC_SLOTS_PER_LANE], ps[PROC_SLOTS_PER_LANE];
+    bool dirty[PROC_SLOTS_PER_LANE];
+#pragma unroll
+    for (int q = 0; q < PROC_SLOTS_PER_LANE; ++q) {
+        const int j = lg + PROC_G * q;
+        dirty[q] = false;
+        if (j < nsc) {
+            ep[q] = ks.ep(j);
+            ps[q] = ks.cnt(EV_PASS, j);
+        } else {
+            ep[q] = EPOCH_ABSENT;
+            ps[q] = 0;
+        }
+    }
+    for (int64_t g = g0; g < S; ++g) {
+        if (g > g0 && W.seg_key[g] != key) break;
+        const uint32_t st = W.seg_start[g];
+        const uint32_t len = W.seg_start[g + 1] - st;
+        const int64_t E = W.seg_epoch[g];
+        bool fut = false;
+#pragma unroll
+        for (int q = 0; q < PROC_SLOTS_PER_LANE; ++q) fut |= (ep[q] != EPOCH_ABSENT && ep[q] > E);
+        bool slow = W.seg_het[g] || group_any(fut);
+        if (!slow && ks.seven && kind == KIND_CLUSTER && T.has_occ[key]) slow = true;
+        if (slow) {
+#pragma unroll
+            for (int q = 0; q < PROC_SLOTS_PER_LANE; ++q) {
+                const int j = lg + PROC_G * q;
+                if (dirty[q]) { ks.ep(j) = ep[q]; ks.cnt(EV_PASS, j) = ps[q]; dirty[q] = false; }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            if (lg == 0) {
+                for (uint32_t i = st; i < st + len; ++i) {
+                    const uint32_t seq = (uint32_t)W.sval[i] & SEQ_MASK;
+                    int64_t t;
+                    int32_t a;
+                    uint8_t fl;
+                    src.load(seq, t, a, fl);
+                    seq_event(T, key, ks, E, a, fl, seq, V);
+                }
+                W.seg_done[g] = 1;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#pragma unroll
+            for (int q = 0; q < PROC_SLOTS_PER_LANE; ++q) {
+                const int j = lg + PROC_G * q;
+                if (j < nsc) { ep[q] = ks.ep(j); ps[q] = ks.cnt(EV_PASS, j); }
+            }
+            continue;
+        }
+        const int32_t a = W.seg_acq[g];
+        const int slot = (int)(E % nsc);
+        const int owner = slot % PROC_G;
+        const int qs = slot / PROC_G;
+        int64_t cur = EPOCH_ABSENT;
+#pragma unroll
+        for (int q = 0; q < PROC_SLOTS_PER_LANE; ++q) if (q == qs) cur = ep[q];
+        cur = __shfl(cur, owner, PROC_G);
+        if (cur != E) {                                            // NEW or RESET: fresh bucket
+            if (lg == owner) {
+#pragma unroll
+                for (int q = 0; q < PROC_SLOTS_PER_LANE; ++q) if (q == qs) { ep[q] = E; ps[q] = 0; dirty[q] = true; }
+            }
+            if (ks.seven && lg < 6) ks.rest(slot)[lg] = 0;
+        }
+        int64_t part = 0;
+#pragma unroll
+        for (int q = 0; q < PROC_SLOTS_PER_LANE; ++q)
+            if (ep[q] != EPOCH_ABSENT && ep[q] > E - nsc) part = wrap_add(part, ps[q]);
+        const int64_t s0 = group_sum(part);
+        uint32_t lo = 0, hi = len;                      // K = first p with !admits(S0 + p*a)
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            if (admits(kind, thr, I_s, wrap_add(s0, wrap_mul((int64_t)mid, a)), a)) lo = mid + 1;
+            else hi = mid;
+        }
+        const uint32_t K = lo;
+        const int64_t nb = (int64_t)(len - K);
+        if (lg == owner) {
+#pragma unroll
+            for (int q = 0; q < PROC_SLOTS_PER_LANE; ++q)
+                if (q == qs) { ps[q] = wrap_add(ps[q], wrap_mul((int64_t)K, a)); dirty[q] = true; }
+        }
+        if (ks.seven) {
+            int64_t *r = ks.rest(slot);
+            if (lg == EV_PASS_REQUEST - 1) r[lg] = wrap_add(r[lg], (int64_t)K);
+            else if (lg == EV_BLOCK - 1) r[lg] = wrap_add(r[lg], wrap_mul(nb, a));
+            else if (lg == EV_BLOCK_REQUEST - 1) r[lg] = wrap_add(r[lg], nb);
+        }
+        if (lg == 0) {
+            W.seg_s0[g] = s0;
+            W.seg_k[g] = K;
+            W.seg_done[g] = 0;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < PROC_SLOTS_PER_LANE; ++q) {
+        const int j = lg + PROC_G * q;
+        if (dirty[q]) { ks.ep(j) = ep[q]; ks.cnt(EV_PASS, j) = ps[q]; }
+    }
+}
+
+// Grid-stride over segments: a group takes segment g0 when it starts its key's run.
+__global__ __launch_bounds__(256) void k_process_grp(KeyTable T, BatchWork W, EventSrc src, Verdicts V, int64_t n) {
+    const int lg = threadIdx.x % PROC_G;
+    const int64_t S = (int64_t)*W.nseg;
+    if (*W.nvalid == 0) return;
+    const int64_t ngroups = (int64_t)gridDim.x * (blockDim.x / PROC_G);
+    for (int64_t g0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / PROC_G; g0 < S; g0 += ngroups) {
+        if (g0 > 0 && W.seg_key[g0 - 1] == W.seg_key[g0]) continue;   // group-uniform
+        process_key_group(T, W, src, V, g0, S, lg);
+    }
+}
+
 // Per sorted event: rank inside its segment decides; scatter the verdict to its arrival slot.
+template <bool LIMITER, bool NT>
 __global__ __launch_bounds__(256) void k_verdict(KeyTable T, BatchWork W, Verdicts V, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -401,20 +776,22 @@ __global__ __launch_bounds__(256) void k_verdict(KeyTable T, BatchWork W, Verdic
     if (W.seg_done[g]) return;
     const uint32_t rank = (uint32_t)i - W.seg_start[g];
     const uint32_t K = W.seg_k[g];
-    const uint32_t seq = W.sseq[i];
+    const uint32_t seq = (uint32_t)W.sval[i] & SEQ_MASK;
     const uint32_t key = W.seg_key[g];
-    const uint8_t kind = T.kind[key];
-    if (kind == KIND_LIMITER) {
+    if (LIMITER) {
         if (rank >= K) reject_limited(V, seq);
         return;
     }
+    uint64_t v;
     if (rank < K) {
         const int32_t a = W.seg_acq[g];
         const int64_t x = wrap_add(W.seg_s0[g], wrap_mul((int64_t)rank, a));
-        put_verdict(V.out, seq, ST_OK, java_d2i(remaining_of(T.thr[key], T.I_s[key], x, a)), 0);
+        v = pack_verdict(ST_OK, java_d2i(remaining_of(T.thr[key], T.I_s[key], x, a)), 0);
     } else {
-        put_verdict(V.out, seq, ST_BLOCKED, 0, 0);
+        v = pack_verdict(ST_BLOCKED, 0, 0);
     }
+    if (NT) __builtin_nontemporal_store(v, V.out + seq);
+    else V.out[seq] = v;
 }
 
 }  // namespace sentinel

@@ -272,8 +272,7 @@ __global__ void k_init_state(int64_t *state, const int64_t *__restrict__ off, in
     const int64_t o = off ? off[k] : k * stride;
     const int n = nn ? nn[k] : fixed_n;
     const int64_t words = nn ? flow_record_words(n) : words_per_key_fixed;
-    for (int j = 0; j < n; ++j) state[o + j] = EPOCH_ABSENT;
-    for (int64_t j = n; j < words; ++j) state[o + j] = 0;
+    for (int64_t j = 0; j < words; ++j) state[o + j] = (j < 2 * n && (j & 1) == 0) ? EPOCH_ABSENT : 0;
 }
 
 inline unsigned grid_for(int64_t n, int threads = 256) { return (unsigned)std::max<int64_t>(1, (n + threads - 1) / threads); }
@@ -296,6 +295,9 @@ struct sentinel_engine {
     TableBufs ft;
     DevBuf d_flow_route, d_flow_ids;
     bool flow_plain = true;          // no flow needs a limiter or namespace check
+    int32_t flow_max_n = 1;
+    int process_impl = 0;
+    bool verdict_nt = false;   // SENTINEL_VERDICT_NT=1: non-temporal verdict stores   // SENTINEL_PROCESS: 0 reg (default), 1 group, 2 thread-in-memory
     int64_t flow_state_words = 0;
 
     // namespace limiters (RequestLimiter = UnaryLeapArray(10, 1000))
@@ -358,7 +360,7 @@ struct sentinel_engine {
     }
 
     // batch workspace
-    DevBuf w_fkey, w_lkey, w_skey, w_sseq, w_ktmp, w_vtmp, w_fhist, w_lhist, w_parts, w_segid, w_bad, w_hep,
+    DevBuf w_fkey, w_lkey, w_skey, w_sval, w_ktmp, w_vtmp, w_fhist, w_lhist, w_parts, w_segid, w_bad, w_hep,
         w_hacq, w_segstart, w_segkey, w_segep, w_segacq, w_het, w_done, w_s0, w_k, w_counters;
     DevBuf io_ev, io_fl, io_out;
     int64_t ws_cap = 0;
@@ -367,10 +369,9 @@ struct sentinel_engine {
         if (n <= ws_cap) return 0;
         int64_t c = std::max<int64_t>(n, 4096);
         int rc = 0;
-        for (DevBuf *b : {&w_fkey, &w_lkey, &w_skey, &w_sseq, &w_ktmp, &w_vtmp, &w_segid, &w_segkey, &w_k, &w_hacq,
-                          &w_segacq})
+        for (DevBuf *b : {&w_fkey, &w_lkey, &w_skey, &w_ktmp, &w_segid, &w_segkey, &w_k, &w_hacq, &w_segacq})
             rc |= b->ensure(c * 4);
-        for (DevBuf *b : {&w_hep, &w_segep, &w_s0}) rc |= b->ensure(c * 8);
+        for (DevBuf *b : {&w_hep, &w_segep, &w_s0, &w_sval, &w_vtmp}) rc |= b->ensure(c * 8);
         for (DevBuf *b : {&w_bad, &w_het, &w_done}) rc |= b->ensure(c);
         rc |= w_fhist.ensure((size_t)hist_words(c, MAX_PASSES) * 4);
         rc |= w_lhist.ensure((size_t)hist_words(c, MAX_PASSES) * 4);
@@ -385,7 +386,7 @@ struct sentinel_engine {
     BatchWork work() {
         BatchWork W;
         W.skey = w_skey.as<uint32_t>();
-        W.sseq = w_sseq.as<uint32_t>();
+        W.sval = w_sval.as<uint64_t>();
         W.segid = w_segid.as<uint32_t>();
         W.bad = w_bad.as<uint8_t>();
         W.h_epoch = w_hep.as<int64_t>();
@@ -433,17 +434,23 @@ struct sentinel_engine {
         launch("scan_add", n, s, [&] { k_scan_add<<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, n, parts); });
     }
 
-    // K2: stable LSD radix sort of (key, seq) by the low `bits` key bits into (skey, sseq).
-    // `hist` already holds pass 0's per-tile digit histograms (built by the prep kernel from the
-    // same tiles); later passes histogram their own input (the previous pass's output tiles).
-    void sort(const uint32_t *keys_in, int64_t n, int bits, uint32_t *hist, hipStream_t s) {
+    // K2: stable LSD radix sort of (key, seq|prio, payload) by the low `bits` key bits into
+    // (skey, sval).  `hist` holds pass 0's per-tile digit histograms (built by the prep
+    // kernel from the same tiles); later passes histogram their own input.
+    void sort(const uint32_t *keys_in, int64_t n, int bits, uint32_t *hist, const EventSrc &src, hipStream_t s) {
         const int64_t nb = sort_blocks(n);
         const int passes = passes_for(bits);
-        uint32_t *kb[2], *vb[2];
-        if (passes % 2 == 1) { kb[0] = w_skey.as<uint32_t>(); vb[0] = w_sseq.as<uint32_t>(); kb[1] = w_ktmp.as<uint32_t>(); vb[1] = w_vtmp.as<uint32_t>(); }
-        else { kb[0] = w_ktmp.as<uint32_t>(); vb[0] = w_vtmp.as<uint32_t>(); kb[1] = w_skey.as<uint32_t>(); vb[1] = w_sseq.as<uint32_t>(); }
+        uint32_t *kb[2];
+        uint64_t *vb[2];
+        if (passes % 2 == 1) {
+            kb[0] = w_skey.as<uint32_t>(); vb[0] = w_sval.as<uint64_t>();
+            kb[1] = w_ktmp.as<uint32_t>(); vb[1] = w_vtmp.as<uint64_t>();
+        } else {
+            kb[0] = w_ktmp.as<uint32_t>(); vb[0] = w_vtmp.as<uint64_t>();
+            kb[1] = w_skey.as<uint32_t>(); vb[1] = w_sval.as<uint64_t>();
+        }
         const uint32_t *kin = keys_in;
-        const uint32_t *vin = nullptr;
+        const uint64_t *vin = nullptr;
         for (int p = 0; p < passes; ++p) {
             const int shift = p * RADIX_BITS;
             if (p > 0)
@@ -451,10 +458,18 @@ struct sentinel_engine {
                     k_radix_hist_pass<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(kin, n, shift, hist, nb);
                 });
             scan(hist, nb * RADIX, true, s);
-            uint32_t *ko = kb[p % 2], *vo = vb[p % 2];
-            launch("radix_scatter", n, s, [&] {
-                k_radix_scatter<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(kin, vin, ko, vo, n, shift, hist, nb, 0u);
-            });
+            uint32_t *ko = kb[p % 2];
+            uint64_t *vo = vb[p % 2];
+            if (p == 0)
+                launch("radix_scatter", n, s, [&] {
+                    k_radix_scatter_p<true><<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(kin, vin, src, ko, vo, n,
+                                                                                               shift, hist, nb);
+                });
+            else
+                launch("radix_scatter", n, s, [&] {
+                    k_radix_scatter_p<false><<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(kin, vin, src, ko, vo, n,
+                                                                                                shift, hist, nb);
+                });
             kin = ko;
             vin = vo;
         }
@@ -469,17 +484,32 @@ struct sentinel_engine {
 
     // The generic pipeline: sort by key, segment, decide, scatter.
     void run_pipeline(const KeyTable &T, const uint32_t *keys, uint32_t *hist, int64_t n, int bits,
-                      const EventSrc &src, const Verdicts &V, hipStream_t s) {
+                      const EventSrc &src, const Verdicts &V, hipStream_t s, int max_n, bool limiter) {
         BatchWork W = work();
         const uint32_t invalid = ((uint32_t)1 << bits) - 1;
-        sort(keys, n, bits, hist, s);
+        sort(keys, n, bits, hist, src, s);
         const unsigned g = grid_for(n);
         launch("seg_heads", n, s, [&] { k_seg_heads<<<g, 256, 0, s>>>(T, W, src, n, invalid); });
         scan(W.segid, n, false, s);
         (void)hipMemsetAsync(W.seg_het, 0, (size_t)n, s);
         launch("seg_mark", n, s, [&] { k_seg_mark<<<g, 256, 0, s>>>(W, n); });
-        launch("process", n, s, [&] { k_process<<<g, 256, 0, s>>>(T, W, src, V, n); });
-        launch("verdict", n, s, [&] { k_verdict<<<g, 256, 0, s>>>(T, W, V, n); });
+        if (max_n <= PROC_G * PROC_SLOTS_PER_LANE && process_impl == 1)
+            launch("process", n, s, [&] {
+                k_process_grp<<<std::min<unsigned>(grid_for(n * PROC_G), 8192), 256, 0, s>>>(T, W, src, V, n);
+            });
+        else if (max_n <= 2 && process_impl == 0)
+            launch("process", n, s, [&] { k_process_reg<2><<<g, 256, 0, s>>>(T, W, src, V, n); });
+        else if (max_n <= 4 && process_impl == 0)
+            launch("process", n, s, [&] { k_process_reg<4><<<g, 256, 0, s>>>(T, W, src, V, n); });
+        else if (max_n <= 10 && process_impl == 0)
+            launch("process", n, s, [&] { k_process_reg<10><<<g, 256, 0, s>>>(T, W, src, V, n); });
+        else if (max_n <= 16 && process_impl == 0)
+            launch("process", n, s, [&] { k_process_reg<16><<<g, 256, 0, s>>>(T, W, src, V, n); });
+        else
+            launch("process", n, s, [&] { k_process<<<g, 256, 0, s>>>(T, W, src, V, n); });
+        if (limiter) launch("verdict", n, s, [&] { k_verdict<true, false><<<g, 256, 0, s>>>(T, W, V, n); });
+        else if (verdict_nt) launch("verdict", n, s, [&] { k_verdict<false, true><<<g, 256, 0, s>>>(T, W, V, n); });
+        else launch("verdict", n, s, [&] { k_verdict<false, false><<<g, 256, 0, s>>>(T, W, V, n); });
     }
 
     int rebuild_flow_thresholds();
@@ -588,6 +618,7 @@ static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const u
     uint32_t *fkey = e->w_fkey.as<uint32_t>();
     uint32_t *lkey = lim ? e->w_lkey.as<uint32_t>() : nullptr;
     const int64_t nb = sort_blocks(n);
+    HIP_OK(hipMemsetAsync(e->w_counters.p, 0, 16, s));
     e->launch("flow_prep", n, s, [&] {
         k_flow_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
             n, ev, F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, fkey, finvalid, 1,
@@ -598,12 +629,12 @@ static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const u
     if (lim) {
         KeyTable LT = e->table(e->lt, 1, e->lim_stride);
         EventSrc lsrc{ev, nullptr, nullptr, true};
-        e->run_pipeline(LT, lkey, e->w_lhist.as<uint32_t>(), n, lbits, lsrc, V, s);
+        e->run_pipeline(LT, lkey, e->w_lhist.as<uint32_t>(), n, lbits, lsrc, V, s, 10, true);
         e->hist_pass0(fkey, n, e->w_fhist.as<uint32_t>(), s);   // the limiter invalidated some keys
     }
     if (F > 0) {
         KeyTable FT = e->table(e->ft, NEV, 0);
-        e->run_pipeline(FT, fkey, e->w_fhist.as<uint32_t>(), n, fbits, src, V, s);
+        e->run_pipeline(FT, fkey, e->w_fhist.as<uint32_t>(), n, fbits, src, V, s, e->flow_max_n, false);
     }
     HIP_OK(hipGetLastError());
     return 0;
@@ -625,6 +656,7 @@ static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, u
     uint32_t *lkey = lim ? e->w_lkey.as<uint32_t>() : nullptr;
     const int64_t nb = sort_blocks(n);
     const bool have = R > 0 && e->d_ptable.p;
+    HIP_OK(hipMemsetAsync(e->w_counters.p, 0, 16, s));
     e->launch("param_prep", n, s, [&] {
         k_param_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
             n, ev, have ? R : 0, e->param_plain ? nullptr : e->d_prule_route.as<int32_t>(),
@@ -649,12 +681,12 @@ static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, u
     if (lim) {
         KeyTable LT = e->table(e->lt, 1, e->lim_stride);
         EventSrc lsrc{nullptr, ev, nullptr, true};
-        e->run_pipeline(LT, lkey, e->w_lhist.as<uint32_t>(), n, lbits, lsrc, V, s);
+        e->run_pipeline(LT, lkey, e->w_lhist.as<uint32_t>(), n, lbits, lsrc, V, s, 10, true);
         e->hist_pass0(fkey, n, e->w_fhist.as<uint32_t>(), s);
     }
     KeyTable PT = e->table(e->pt, 1, header_words(e->pmax_n));
     EventSrc src{nullptr, ev, nullptr, false};
-    e->run_pipeline(PT, fkey, e->w_fhist.as<uint32_t>(), n, pbits, src, V, s);
+    e->run_pipeline(PT, fkey, e->w_fhist.as<uint32_t>(), n, pbits, src, V, s, e->pmax_n, false);
     HIP_OK(hipGetLastError());
     return 0;
 }
@@ -693,6 +725,11 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
         delete e;
         return fail(SENTINEL_E_DEVICE, "hipStreamCreate failed");
     }
+    if (const char *c = getenv("SENTINEL_PROCESS")) {
+        const std::string v(c);
+        e->process_impl = v == "group" ? 1 : v == "thread" ? 2 : 0;
+    }
+    if (const char *c = getenv("SENTINEL_VERDICT_NT")) e->verdict_nt = std::string(c) == "1";
     if (const char *c = getenv("SENTINEL_PARAM_CAPACITY")) {
         uint64_t v = strtoull(c, nullptr, 10);
         uint64_t p = 1024;
@@ -721,7 +758,7 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
     e->pt.release();
     for (DevBuf *b : {&e->d_flow_route, &e->d_flow_ids, &e->d_prule_route, &e->d_prule_n, &e->d_prule_w,
                       &e->d_prule_rcp, &e->d_prule_Is, &e->d_prule_thr, &e->d_ptable, &e->d_slot_rule,
-                      &e->d_hot_table, &e->d_hot_thr, &e->w_fkey, &e->w_lkey, &e->w_skey, &e->w_sseq, &e->w_ktmp,
+                      &e->d_hot_table, &e->d_hot_thr, &e->w_fkey, &e->w_lkey, &e->w_skey, &e->w_sval, &e->w_ktmp,
                       &e->w_vtmp, &e->w_fhist, &e->w_lhist, &e->w_parts, &e->w_segid, &e->w_bad, &e->w_hep,
                       &e->w_hacq, &e->w_segstart, &e->w_segkey, &e->w_segep, &e->w_segacq, &e->w_het, &e->w_done,
                       &e->w_s0, &e->w_k, &e->w_counters, &e->io_ev, &e->io_fl, &e->io_out})
@@ -846,7 +883,7 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
     std::vector<int64_t> occ(2 * std::max<size_t>(F, 1), 0);
     std::vector<uint8_t> hocc(std::max<size_t>(F, 1), 0);
     for (size_t i = 0; i < F; ++i) {
-        for (int j = 0; j < nn[i]; ++j) st[off[i] + j] = EPOCH_ABSENT;
+        for (int j = 0; j < nn[i]; ++j) st[off[i] + 2 * j] = EPOCH_ABSENT;
         auto it = old_index.find(ids[i]);
         if (it == old_index.end()) continue;
         const int32_t o = it->second;
@@ -874,6 +911,7 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
     e->h_flow_n = nn;
     e->h_flow_w = ww;
     e->flow_state_words = words;
+    e->flow_max_n = nn.empty() ? 1 : *std::max_element(nn.begin(), nn.end());
     rc = e->rebuild_routes();
     if (rc) return rc;
     return e->rebuild_flow_thresholds();
@@ -1096,9 +1134,9 @@ int sentinel_dump_flow(sentinel_engine_t *e, int32_t idx, int64_t *out, int32_t 
     const int64_t hw = header_words(n);
     for (int j = 0; j < n; ++j) {
         int64_t *o = out + j * (1 + NEV);
-        const bool present = st[j] != EPOCH_ABSENT;
-        o[0] = present ? st[j] * w : -1;
-        o[1 + EV_PASS] = present ? st[n + j] : 0;
+        const bool present = st[2 * j] != EPOCH_ABSENT;
+        o[0] = present ? st[2 * j] * w : -1;
+        o[1 + EV_PASS] = present ? st[2 * j + 1] : 0;
         for (int c = 1; c < NEV; ++c) o[1 + c] = present ? st[hw + 8 * j + (c - 1)] : 0;
     }
     int64_t *o = out + n * (1 + NEV);
@@ -1134,7 +1172,7 @@ int sentinel_param_sum(sentinel_engine_t *e, int32_t ridx, uint64_t pkey, int64_
     const int64_t E = ts / w;   // read-only view (no roll): valid slots are epochs in (E - n, E]
     int64_t s = 0;
     for (int j = 0; j < n; ++j)
-        if (st[j] != EPOCH_ABSENT && st[j] > E - n && st[j] <= E) s += st[n + j];
+        if (st[2 * j] != EPOCH_ABSENT && st[2 * j] > E - n && st[2 * j] <= E) s += st[2 * j + 1];
     *out = s;
     return 0;
 }

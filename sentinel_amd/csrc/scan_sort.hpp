@@ -1,4 +1,4 @@
-// scan_sort.hpp -- device-wide prefix scan and stable LSD radix sort (key u32, value u32) for gfx950.
+// scan_sort.hpp -- device-wide prefix scan and radix-sort building blocks for gfx950.
 //
 // K2 of the engine ("radix sort keys each batch by (flowId, seq)"): keys are dense flow (or
 // namespace / param-slot) indices, values are arrival positions (seq).  LSD radix sort is stable,
@@ -24,10 +24,17 @@ constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;     // 4096
 constexpr int RADIX_BITS = 8;
 constexpr int RADIX = 1 << RADIX_BITS;
 constexpr int MAX_PASSES = 4;
-constexpr int SORT_THREADS = 256;
+#ifndef SENTINEL_SORT_THREADS
+#define SENTINEL_SORT_THREADS 512
+#endif
+#ifndef SENTINEL_SORT_ITEMS
+#define SENTINEL_SORT_ITEMS 8
+#endif
+constexpr int SORT_THREADS = SENTINEL_SORT_THREADS;   // >= RADIX
 constexpr int SORT_WAVES = SORT_THREADS / WAVE;
-constexpr int SORT_ITEMS = 16;
-constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;     // 4096
+constexpr int SORT_ITEMS = SENTINEL_SORT_ITEMS;
+constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;     // 4096 by default
+static_assert(SORT_THREADS >= 256 && SORT_THREADS % 64 == 0, "one thread per digit");
 
 __device__ inline uint32_t wave_inclusive_scan(uint32_t v) {
     const int lane = (int)lane_id();
@@ -159,96 +166,6 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist_pass(const uint32_t
     }
     __syncthreads();
     for (int d = threadIdx.x; d < RADIX; d += SORT_THREADS) hist[(int64_t)d * nblocks + blockIdx.x] = h[d];
-}
-
-// Stable scatter of one pass.  offsets = the exclusive scan of all passes' digit-major
-// histograms; pass p's offsets carry p*n from the concatenation, removed via `bias`.
-// vals_in == nullptr means "value = index" (first pass: seq is implicit).
-__global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
-    const uint32_t *__restrict__ keys_in, const uint32_t *__restrict__ vals_in,
-    uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out, int64_t n, int shift,
-    const uint32_t *__restrict__ offsets, int64_t nblocks, uint32_t bias) {
-    __shared__ uint32_t cnt[SORT_WAVES][RADIX];
-    __shared__ uint32_t goff[RADIX];       // global start of digit d for this tile
-    __shared__ uint32_t loff[RADIX];       // start of digit d inside the staged tile
-    __shared__ uint32_t waves_tot[SORT_WAVES];
-    __shared__ uint32_t skeys[SORT_TILE];
-    __shared__ uint32_t svals[SORT_TILE];
-    const int wave = threadIdx.x / WAVE;
-    const uint32_t lane = lane_id();
-    for (int d = threadIdx.x; d < RADIX; d += SORT_THREADS) {
-#pragma unroll
-        for (int w = 0; w < SORT_WAVES; ++w) cnt[w][d] = 0;
-        goff[d] = offsets[(int64_t)d * nblocks + blockIdx.x] - bias;
-    }
-    __syncthreads();
-
-    const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
-    const int64_t base = tile0 + (int64_t)wave * (SORT_ITEMS * WAVE);
-    uint32_t key[SORT_ITEMS], val[SORT_ITEMS], rank[SORT_ITEMS];
-#pragma unroll
-    for (int j = 0; j < SORT_ITEMS; ++j) {
-        const int64_t i = base + j * WAVE + lane;
-        const bool valid = i < n;
-        key[j] = valid ? keys_in[i] : 0u;
-        val[j] = valid ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
-    }
-#pragma unroll
-    for (int j = 0; j < SORT_ITEMS; ++j) {
-        const int64_t i = base + j * WAVE + lane;
-        const bool valid = i < n;
-        const uint32_t d = (key[j] >> shift) & (RADIX - 1);
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < RADIX_BITS; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t bal = __ballot(valid && bit);
-            peers &= bit ? bal : ~bal;
-        }
-        uint32_t r = 0;
-        if (valid) r = cnt[wave][d] + mask_rank(peers);
-        __builtin_amdgcn_wave_barrier();
-        if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane)
-            cnt[wave][d] += (uint32_t)__popcll(peers);
-        __builtin_amdgcn_wave_barrier();
-        rank[j] = valid ? r : 0xFFFFFFFFu;
-    }
-    __syncthreads();
-    // per digit: exclusive prefix over waves; tile-local digit starts
-    uint32_t dtot = 0;
-    const int d0 = threadIdx.x;   // SORT_THREADS == RADIX
-    {
-        uint32_t run = 0;
-#pragma unroll
-        for (int w = 0; w < SORT_WAVES; ++w) {
-            uint32_t c = cnt[w][d0];
-            cnt[w][d0] = run;
-            run += c;
-        }
-        dtot = run;
-    }
-    uint32_t total;
-    const uint32_t lstart = block_exclusive_scan(dtot, waves_tot, &total);
-    loff[d0] = lstart;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < SORT_ITEMS; ++j) {
-        if (rank[j] == 0xFFFFFFFFu) continue;
-        const uint32_t d = (key[j] >> shift) & (RADIX - 1);
-        const uint32_t p = loff[d] + cnt[wave][d] + rank[j];
-        skeys[p] = key[j];
-        svals[p] = val[j];
-    }
-    __syncthreads();
-    // contiguous per-digit runs: consecutive threads write consecutive addresses
-    const int64_t valid_in_tile = (n - tile0) < SORT_TILE ? (n - tile0) : SORT_TILE;
-    for (int p = threadIdx.x; p < valid_in_tile; p += SORT_THREADS) {
-        const uint32_t k = skeys[p];
-        const uint32_t d = (k >> shift) & (RADIX - 1);
-        const uint32_t dst = goff[d] + (uint32_t)p - loff[d];
-        keys_out[dst] = k;
-        vals_out[dst] = svals[p];
-    }
 }
 
 }  // namespace sentinel

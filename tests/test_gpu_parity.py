@@ -82,6 +82,20 @@ def test_homogeneous_acquire_gt1(oracle_mod):
     _compare(_engine(rules), _oracle(oracle_mod, rules), rules, ev, batches=2)
 
 
+def test_large_acquire_escape(oracle_mod):
+    """acquireCount >= 2047 does not fit the 11-bit field of the sorted value (escape path)."""
+    rng = np.random.default_rng(37)
+    rules = T.make_rules(80, rng, count_lo=20_000, count_hi=400_000)
+    n = 30_000
+    acq = np.where(rng.random(n) < 0.5, 3000, 2047).astype(np.int32)
+    acq[::7] = 1
+    ev = T.Events(rng.integers(0, 80, size=n).astype(np.int32), acq, T.timestamps(n, 30_000.0, T.T0_ALIGNED))
+    _compare(_engine(rules), _oracle(oracle_mod, rules), rules, ev, batches=2)
+    ev = T.Events(rng.integers(0, 80, size=n).astype(np.int32), np.full(n, 5000, np.int32),
+                  T.timestamps(n, 30_000.0, T.T0_ALIGNED + 2000))
+    _compare(_engine(rules), _oracle(oracle_mod, rules), rules, ev, batches=1)
+
+
 def test_prioritized_occupy(oracle_mod):
     rng = np.random.default_rng(13)
     rules = T.make_rules(50, rng, count_lo=3, count_hi=40, sample_count=5, window_interval_ms=1000)
@@ -126,6 +140,18 @@ def test_clock_backwards_sequential_path(oracle_mod):
     ts = ts + np.where(rng.random(n) < 0.05, jitter, 0)
     ev = T.Events(rng.integers(0, 40, size=n).astype(np.int32), np.ones(n, np.int32), ts.astype(np.int64))
     _compare(_engine(rules), _oracle(oracle_mod, rules), rules, ev, batches=2)
+
+
+def test_wide_timestamp_span_fallback(oracle_mod):
+    """A batch spanning 30 days: ts - T0 overflows the 24-bit delta of the sorted value, so those
+    events are read back by position; verdicts must not change."""
+    rng = np.random.default_rng(31)
+    rules = T.make_rules(60, rng, count_lo=3, count_hi=40, sample_count=2, window_interval_ms=1000)
+    n = 20_000
+    ts = T.timestamps(n, 5000.0, T.T0_ALIGNED)
+    ts[n // 2:] += 30 * 24 * 3600 * 1000        # +30 days
+    ev = T.Events(rng.integers(0, 60, size=n).astype(np.int32), np.ones(n, np.int32), ts.astype(np.int64))
+    _compare(_engine(rules), _oracle(oracle_mod, rules), rules, ev, batches=1)
 
 
 def test_empty_single_and_all_invalid(oracle_mod):
