@@ -384,6 +384,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter_p(
         const uint32_t k = skeys[p];
         const uint32_t d = (k >> shift) & (RADIX - 1);
         const uint32_t dst = goff[d] + (uint32_t)p - loff[d];
+        if (dst >= (uint64_t)n) continue;          // guard: a corrupt offset must never write out of bounds
         keys_out[dst] = k;
         vals_out[dst] = svals[p];
     }
@@ -441,6 +442,131 @@ __global__ __launch_bounds__(256) void k_seg_heads(KeyTable T, BatchWork W, Even
     W.bad[i] = (!head && pa != a) || prio;
     if (head) { W.h_epoch[i] = E; W.h_acq[i] = a; }
     if (i == n - 1 || W.skey[i + 1] == invalid) *W.nvalid = (uint32_t)(i + 1);
+}
+
+// Segment construction in one pass (replaces heads -> scan -> mark): per 4096-element tile of the
+// sorted batch, compute each event's epoch, (key, epoch) run heads and homogeneity; a block scan
+// plus decoupled look-back gives every event its global segment id; heads write the segment
+// records {start, key, epoch, acquire}, non-homogeneous events flag their segment.  seg_het must
+// be zeroed and the look-back status/ticket words cleared before the launch.
+constexpr int SEG_THREADS = 256;
+constexpr int SEG_ITEMS = 16;
+constexpr int SEG_TILE = SEG_THREADS * SEG_ITEMS;
+
+__global__ __launch_bounds__(SEG_THREADS) void k_segments(KeyTable T, BatchWork W, EventSrc src, int64_t n,
+                                                          uint32_t invalid, unsigned long long *status,
+                                                          uint32_t *ticket) {
+    __shared__ uint32_t s_key[SEG_TILE];
+    __shared__ uint64_t s_val[SEG_TILE];
+    __shared__ uint32_t l_key[SEG_THREADS];
+    __shared__ int64_t l_ep[SEG_THREADS];
+    __shared__ int32_t l_acq[SEG_THREADS];
+    __shared__ uint32_t waves[SEG_THREADS / WAVE];
+    __shared__ uint32_t s_bid, s_prefix;
+    __shared__ uint32_t p_key;
+    __shared__ int64_t p_ep;
+    __shared__ int32_t p_acq;
+    if (threadIdx.x == 0) s_bid = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int64_t bid = s_bid;
+    const int64_t base = bid * SEG_TILE;
+    const int64_t T0 = src.t0();
+#pragma unroll
+    for (int j = 0; j < SEG_ITEMS; ++j) {
+        const int64_t i = base + j * SEG_THREADS + threadIdx.x;
+        const bool in = i < n;
+        s_key[j * SEG_THREADS + threadIdx.x] = in ? W.skey[i] : invalid;
+        s_val[j * SEG_THREADS + threadIdx.x] = in ? W.sval[i] : 0ull;
+    }
+    if (threadIdx.x == 0) {           // the element just before this tile
+        p_key = invalid;
+        p_ep = 0;
+        p_acq = 0;
+        if (base > 0 && base - 1 < n) {
+            const uint32_t k = W.skey[base - 1];
+            if (k != invalid) {
+                int64_t t;
+                int32_t a;
+                bool pr;
+                src.unpack(W.sval[base - 1], T0, t, a, pr);
+                p_key = k;
+                p_ep = epoch_of(t, T.w[k], T.rcp_w[k]);
+                p_acq = a;
+            }
+        }
+    }
+    __syncthreads();
+    // this thread's contiguous run of SEG_ITEMS sorted events
+    uint32_t key[SEG_ITEMS];
+    int64_t ep[SEG_ITEMS];
+    int32_t acq[SEG_ITEMS];
+    bool prio[SEG_ITEMS];
+#pragma unroll
+    for (int j = 0; j < SEG_ITEMS; ++j) {
+        const int q = threadIdx.x * SEG_ITEMS + j;
+        key[j] = s_key[q];
+        ep[j] = 0;
+        acq[j] = 0;
+        prio[j] = false;
+        if (key[j] != invalid) {
+            int64_t t;
+            src.unpack(s_val[q], T0, t, acq[j], prio[j]);
+            ep[j] = epoch_of(t, T.w[key[j]], T.rcp_w[key[j]]);
+            prio[j] = prio[j] && T.kind[key[j]] == KIND_CLUSTER;
+        }
+    }
+    l_key[threadIdx.x] = key[SEG_ITEMS - 1];
+    l_ep[threadIdx.x] = ep[SEG_ITEMS - 1];
+    l_acq[threadIdx.x] = acq[SEG_ITEMS - 1];
+    __syncthreads();
+    uint32_t pk = threadIdx.x ? l_key[threadIdx.x - 1] : p_key;
+    int64_t pe = threadIdx.x ? l_ep[threadIdx.x - 1] : p_ep;
+    int32_t pa = threadIdx.x ? l_acq[threadIdx.x - 1] : p_acq;
+    uint32_t headmask = 0, badmask = 0;
+#pragma unroll
+    for (int j = 0; j < SEG_ITEMS; ++j) {
+        if (key[j] != invalid) {
+            const bool head = pk != key[j] || pe != ep[j];
+            if (head) headmask |= 1u << j;
+            if ((!head && pa != acq[j]) || prio[j]) badmask |= 1u << j;
+        }
+        pk = key[j];
+        pe = ep[j];
+        pa = acq[j];
+    }
+    uint32_t total;
+    uint32_t g = block_exclusive_scan((uint32_t)__popc(headmask), waves, &total);
+    tile_lookback(bid, total, status, ticket + 1, &s_prefix);
+    __syncthreads();
+    g += s_prefix;                   // segments started before this thread's run
+#pragma unroll
+    for (int j = 0; j < SEG_ITEMS; ++j) {
+        const int q = threadIdx.x * SEG_ITEMS + j;
+        const int64_t i = base + q;
+        if (key[j] == invalid) { s_key[q] = 0; continue; }
+        if (headmask & (1u << j)) {
+            ++g;
+            W.seg_start[g - 1] = (uint32_t)i;
+            W.seg_key[g - 1] = key[j];
+            W.seg_epoch[g - 1] = ep[j];
+            W.seg_acq[g - 1] = acq[j];
+        }
+        if (badmask & (1u << j)) W.seg_het[g - 1] = 1;
+        s_key[q] = g;                // 1-based segment id
+        const bool last = (i == n - 1) || (j + 1 < SEG_ITEMS ? key[j + 1] == invalid : W.skey[i + 1] == invalid);
+        if (last) {
+            *W.nvalid = (uint32_t)(i + 1);
+            *W.nseg = g;
+            W.seg_start[g] = (uint32_t)(i + 1);
+        }
+    }
+    if (bid == 0 && threadIdx.x == 0 && key[0] == invalid) { *W.nvalid = 0; *W.nseg = 0; }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SEG_ITEMS; ++j) {
+        const int64_t i = base + j * SEG_THREADS + threadIdx.x;
+        if (i < n) W.segid[i] = s_key[j * SEG_THREADS + threadIdx.x];
+    }
 }
 
 // After the inclusive scan of heads: per-segment records.  seg_het must be zeroed beforehand.
@@ -766,7 +892,7 @@ __global__ __launch_bounds__(256) void k_process_grp(KeyTable T, BatchWork W, Ev
 }
 
 // Per sorted event: rank inside its segment decides; scatter the verdict to its arrival slot.
-template <bool LIMITER, bool NT>
+template <bool LIMITER, bool NT, bool LINEAR = false>
 __global__ __launch_bounds__(256) void k_verdict(KeyTable T, BatchWork W, Verdicts V, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -790,7 +916,8 @@ __global__ __launch_bounds__(256) void k_verdict(KeyTable T, BatchWork W, Verdic
     } else {
         v = pack_verdict(ST_BLOCKED, 0, 0);
     }
-    if (NT) __builtin_nontemporal_store(v, V.out + seq);
+    if (LINEAR) V.out[i] = v;          // diagnostic build only: wrong positions, measures scatter cost
+    else if (NT) __builtin_nontemporal_store(v, V.out + seq);
     else V.out[seq] = v;
 }
 

@@ -297,7 +297,10 @@ struct sentinel_engine {
     bool flow_plain = true;          // no flow needs a limiter or namespace check
     int32_t flow_max_n = 1;
     int process_impl = 0;
-    bool verdict_nt = false;   // SENTINEL_VERDICT_NT=1: non-temporal verdict stores   // SENTINEL_PROCESS: 0 reg (default), 1 group, 2 thread-in-memory
+    bool verdict_nt = false;   // SENTINEL_VERDICT_NT=1: non-temporal verdict stores
+    bool use_lookback = true;  // SENTINEL_SCAN=3pass selects the three-kernel scan
+    bool fused_segments = true; // SENTINEL_SEGMENTS=split selects heads -> scan -> mark
+    bool diag_linear = false;  // SENTINEL_DIAG_LINEAR=1: verdicts in sorted order (cost diagnostic, wrong output)   // SENTINEL_PROCESS: 0 reg (default), 1 group, 2 thread-in-memory
     int64_t flow_state_words = 0;
 
     // namespace limiters (RequestLimiter = UnaryLeapArray(10, 1000))
@@ -375,7 +378,7 @@ struct sentinel_engine {
         for (DevBuf *b : {&w_bad, &w_het, &w_done}) rc |= b->ensure(c);
         rc |= w_fhist.ensure((size_t)hist_words(c, MAX_PASSES) * 4);
         rc |= w_lhist.ensure((size_t)hist_words(c, MAX_PASSES) * 4);
-        rc |= w_parts.ensure((size_t)(scan_parts(std::max<int64_t>(c, hist_words(c, MAX_PASSES))) + 16) * 4);
+        rc |= w_parts.ensure((size_t)(scan_parts(std::max<int64_t>(c, hist_words(c, MAX_PASSES))) + 16) * 8);
         rc |= w_segstart.ensure((c + 1) * 4);
         rc |= w_counters.ensure(64);
         if (rc) return SENTINEL_E_NOMEM;
@@ -425,6 +428,17 @@ struct sentinel_engine {
     void scan(uint32_t *buf, int64_t n, bool exclusive, hipStream_t s) {
         if (n <= 0) return;
         const int64_t nb = scan_parts(n);
+        if (use_lookback) {
+            // status words (8 B per tile) then the ticket and error words, zeroed together
+            unsigned long long *status = w_parts.as<unsigned long long>();
+            uint32_t *ticket = (uint32_t *)(status + nb);
+            (void)hipMemsetAsync(status, 0, (size_t)nb * 8 + 16, s);
+            launch("scan", n, s, [&] {
+                if (exclusive) k_scan_lookback<true><<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, buf, n, status, ticket, ticket + 1);
+                else k_scan_lookback<false><<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, buf, n, status, ticket, ticket + 1);
+            });
+            return;
+        }
         uint32_t *parts = w_parts.as<uint32_t>();
         launch("scan_tiles", n, s, [&] {
             if (exclusive) k_scan_tiles<true><<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, buf, n, parts);
@@ -489,10 +503,20 @@ struct sentinel_engine {
         const uint32_t invalid = ((uint32_t)1 << bits) - 1;
         sort(keys, n, bits, hist, src, s);
         const unsigned g = grid_for(n);
-        launch("seg_heads", n, s, [&] { k_seg_heads<<<g, 256, 0, s>>>(T, W, src, n, invalid); });
-        scan(W.segid, n, false, s);
         (void)hipMemsetAsync(W.seg_het, 0, (size_t)n, s);
-        launch("seg_mark", n, s, [&] { k_seg_mark<<<g, 256, 0, s>>>(W, n); });
+        if (fused_segments) {
+            const int64_t nt = (n + SEG_TILE - 1) / SEG_TILE;
+            unsigned long long *status = w_parts.as<unsigned long long>();
+            uint32_t *ticket = (uint32_t *)(status + nt);
+            (void)hipMemsetAsync(status, 0, (size_t)nt * 8 + 16, s);
+            launch("segments", n, s, [&] {
+                k_segments<<<dim3((unsigned)nt), dim3(SEG_THREADS), 0, s>>>(T, W, src, n, invalid, status, ticket);
+            });
+        } else {
+            launch("seg_heads", n, s, [&] { k_seg_heads<<<g, 256, 0, s>>>(T, W, src, n, invalid); });
+            scan(W.segid, n, false, s);
+            launch("seg_mark", n, s, [&] { k_seg_mark<<<g, 256, 0, s>>>(W, n); });
+        }
         if (max_n <= PROC_G * PROC_SLOTS_PER_LANE && process_impl == 1)
             launch("process", n, s, [&] {
                 k_process_grp<<<std::min<unsigned>(grid_for(n * PROC_G), 8192), 256, 0, s>>>(T, W, src, V, n);
@@ -509,6 +533,7 @@ struct sentinel_engine {
             launch("process", n, s, [&] { k_process<<<g, 256, 0, s>>>(T, W, src, V, n); });
         if (limiter) launch("verdict", n, s, [&] { k_verdict<true, false><<<g, 256, 0, s>>>(T, W, V, n); });
         else if (verdict_nt) launch("verdict", n, s, [&] { k_verdict<false, true><<<g, 256, 0, s>>>(T, W, V, n); });
+        else if (diag_linear) launch("verdict", n, s, [&] { k_verdict<false, false, true><<<g, 256, 0, s>>>(T, W, V, n); });
         else launch("verdict", n, s, [&] { k_verdict<false, false><<<g, 256, 0, s>>>(T, W, V, n); });
     }
 
@@ -730,6 +755,9 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
         e->process_impl = v == "group" ? 1 : v == "thread" ? 2 : 0;
     }
     if (const char *c = getenv("SENTINEL_VERDICT_NT")) e->verdict_nt = std::string(c) == "1";
+    if (const char *c = getenv("SENTINEL_SCAN")) e->use_lookback = std::string(c) != "3pass";
+    if (const char *c = getenv("SENTINEL_DIAG_LINEAR")) e->diag_linear = std::string(c) == "1";
+    if (const char *c = getenv("SENTINEL_SEGMENTS")) e->fused_segments = std::string(c) != "split";
     if (const char *c = getenv("SENTINEL_PARAM_CAPACITY")) {
         uint64_t v = strtoull(c, nullptr, 10);
         uint64_t p = 1024;

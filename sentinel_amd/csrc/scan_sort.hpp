@@ -133,6 +133,102 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_add(uint32_t *__restrict_
 
 inline int64_t scan_parts(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 
+// Single-pass device scan with decoupled look-back (one launch instead of three).  Tiles take a
+// dynamic id from an atomic ticket, so every tile's predecessors have started; a tile publishes
+// its aggregate, then its inclusive prefix, in ONE 64-bit word {flag:2 | value:32} with agent-scope
+// relaxed atomics (the payload is the flag: no separate release/acquire pair is needed).  One wave
+// looks back over 64 predecessors at a time.  Spins are bounded; on timeout the tile records an
+// error word and proceeds (wrong result, never a hang).
+constexpr uint64_t LB_AGG = 1ull << 62;
+constexpr uint64_t LB_PREFIX = 2ull << 62;
+constexpr uint64_t LB_FLAGS = 3ull << 62;
+
+
+// Decoupled look-back for tile b with aggregate `total`: wave 0 publishes the aggregate, sums
+// predecessors 64 at a time until it meets an inclusive prefix, publishes its own prefix and
+// leaves the exclusive prefix in *s_prefix (LDS).  Call from every thread of the block; a
+// __syncthreads() must follow before *s_prefix is read.
+__device__ inline void tile_lookback(int64_t b, uint32_t total, unsigned long long *status, uint32_t *error,
+                                     uint32_t *s_prefix) {
+    if (threadIdx.x >= WAVE) return;
+    const int lane = threadIdx.x;
+    uint32_t prefix = 0;
+    if (b == 0) {
+        if (lane == 0) __hip_atomic_store(&status[0], LB_PREFIX | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        if (lane == 0) __hip_atomic_store(&status[b], LB_AGG | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int64_t hi = b - 1;
+        uint32_t spins = 0;
+        for (;;) {
+            const int64_t p = hi - lane;
+            const uint64_t st = p >= 0 ? __hip_atomic_load(&status[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                       : LB_PREFIX;
+            const uint64_t not_ready = __ballot((st & LB_FLAGS) == 0);
+            const uint64_t is_prefix = __ballot((st & LB_FLAGS) == LB_PREFIX);
+            const int first_prefix = is_prefix ? __ffsll((unsigned long long)is_prefix) - 1 : WAVE;
+            const uint64_t need = first_prefix >= WAVE - 1 ? ~0ull : ((2ull << first_prefix) - 1);
+            if (not_ready & need) {
+                if (++spins > (1u << 22)) { if (lane == 0) *error = 1; break; }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            uint32_t v = (lane <= first_prefix) ? (uint32_t)st : 0u;
+#pragma unroll
+            for (int m = WAVE / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, WAVE);
+            prefix += v;
+            if (first_prefix < WAVE) break;
+            hi -= WAVE;
+        }
+        if (lane == 0)
+            __hip_atomic_store(&status[b], LB_PREFIX | (uint32_t)(prefix + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) *s_prefix = prefix;
+}
+
+template <bool EXCLUSIVE>
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_lookback(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                                int64_t n, unsigned long long *status, uint32_t *ticket,
+                                                                uint32_t *error) {
+    __shared__ uint32_t tile[SCAN_TILE];
+    __shared__ uint32_t waves[SCAN_THREADS / WAVE];
+    __shared__ uint32_t s_bid, s_prefix;
+    if (threadIdx.x == 0) s_bid = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int64_t b = s_bid;
+    const int64_t base = b * SCAN_TILE;
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        const int64_t i = base + j * SCAN_THREADS + threadIdx.x;
+        tile[j * SCAN_THREADS + threadIdx.x] = i < n ? in[i] : 0u;
+    }
+    __syncthreads();
+    uint32_t loc[SCAN_ITEMS];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        loc[j] = tile[threadIdx.x * SCAN_ITEMS + j];
+        sum += loc[j];
+    }
+    uint32_t total;
+    uint32_t run = block_exclusive_scan(sum, waves, &total);
+    tile_lookback(b, total, status, error, &s_prefix);
+    __syncthreads();
+    run += s_prefix;
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        const uint32_t x = loc[j];
+        if (EXCLUSIVE) { tile[threadIdx.x * SCAN_ITEMS + j] = run; run += x; }
+        else { run += x; tile[threadIdx.x * SCAN_ITEMS + j] = run; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        const int64_t i = base + j * SCAN_THREADS + threadIdx.x;
+        if (i < n) out[i] = tile[j * SCAN_THREADS + threadIdx.x];
+    }
+}
+
+
 // ---------------------------------------------------------------- radix sort
 
 inline int64_t sort_blocks(int64_t n) { return (n + SORT_TILE - 1) / SORT_TILE; }
