@@ -49,7 +49,9 @@ def parse():
     ap.add_argument("--flows", type=int, default=1_000_000)
     ap.add_argument("--sample-count", type=int, default=10)
     ap.add_argument("--interval-ms", type=int, default=1000)
-    ap.add_argument("--cpu-sample-events", type=int, default=4 * 1024 * 1024)
+    ap.add_argument("--cpu-steps-1core", type=int, default=2)
+    ap.add_argument("--cpu-steps-mt", type=int, default=12)
+    ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     return ap.parse_args()
@@ -184,23 +186,41 @@ def main():
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "bytes_per_event": bpe, "avg_us": round(d["avg_us"], 2)}
 
-    # ---- CPU baseline: the oracle ("port") on a bounded sample of the same workload, rank 0, N=1
-    cpu = None
+    # ---- CPU baseline: the oracle ("port") on bounded samples of the same workload, rank 0, N=1.
+    # cpu_baseline = the flow-sharded multi-threaded replay on the box's CPU share (16 threads per
+    # GPU); cpu_baseline_1core = the sequential replay (what one reference JVM thread does per call).
+    cpu = cpu1 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
-        m = min(args.cpu_sample_events, N)
-        orc = O.TokenServiceOracle.from_arrays(shard.flow_id, shard.count, shard.threshold_type, shard.sample_count,
-                                               shard.window_interval_ms, shard.namespace, shard.checker)
-        e0 = ev_b[0][:m].cpu().numpy()
-        idx_c = (e0[:, 0] & 0xFFFFFFFF).astype(np.int32)
-        ts_c = e0[:, 1].copy()
-        acq_c = np.ones(m, np.int32)
+
+        def host_steps(k):
+            e = torch.cat([ev_b[s] for s in range(min(k, steps_total))]).cpu().numpy()
+            return (e[:, 0] & 0xFFFFFFFF).astype(np.int32), e[:, 1].copy()
+
+        def fresh():
+            return O.TokenServiceOracle.from_arrays(shard.flow_id, shard.count, shard.threshold_type,
+                                                    shard.sample_count, shard.window_interval_ms,
+                                                    shard.namespace, shard.checker)
+        idx_c, ts_c = host_steps(args.cpu_steps_1core)
+        m = len(ts_c)
+        orc = fresh()
         c0 = time.perf_counter()
-        orc.replay(idx_c, acq_c, ts_c)
+        orc.replay(idx_c, np.ones(m, np.int32), ts_c)
         cdt = time.perf_counter() - c0
-        cpu = {"value": round(m / cdt, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
-               "sample": f"{m} events of step 0 of this workload (same rules, same trace), sequential oracle replay, "
-                         f"{cdt:.1f} s"}
+        cpu1 = {"value": round(m / cdt, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
+                "sample": f"steps 0..{min(args.cpu_steps_1core, steps_total) - 1} of this workload ({m} events, same rules and trace), "
+                          f"sequential oracle replay, {cdt:.1f} s"}
+        del idx_c, ts_c
+        idx_c, ts_c = host_steps(args.cpu_steps_mt)
+        m = len(ts_c)
+        orc = fresh()
+        c0 = time.perf_counter()
+        used = orc.replay_mt(idx_c, np.ones(m, np.int32), ts_c, args.cpu_threads)[3]
+        cdt = time.perf_counter() - c0
+        cpu = {"value": round(m / cdt, 1), "unit": "decisions/s", "cores": int(used), "kind": "port",
+               "sample": f"steps 0..{min(args.cpu_steps_mt, steps_total) - 1} of this workload ({m} events, same rules and trace), "
+                         f"oracle replay sharded by flow over {used} pthreads, {cdt:.1f} s wall"}
+        del idx_c, ts_c
 
     pipeline_bytes = 21.0 + (args.sample_count * 64 + 64 + 16) / max(1.0, N / max(1, F))
     out = {
@@ -227,6 +247,7 @@ def main():
         "pipeline_hbm_frac": round(value / world * pipeline_bytes / (HBM_PEAK_GBS * 1e9), 4),
         "roofline": roof,
         "cpu_baseline": cpu,
+        "cpu_baseline_1core": cpu1,
         "kernels": {k: {"avg_us": round(v["avg_us"], 2), "calls": v["calls"]} for k, v in prof.items()},
     }
     if rank == 0:

@@ -189,6 +189,16 @@ int  sentinel_request_token(sentinel_engine_t *eng, int64_t flow_id, int32_t acq
 int  sentinel_request_param_token(sentinel_engine_t *eng, int64_t flow_id, int32_t acquire_count,
                                   uint64_t param_key, int64_t ts, sentinel_token_result_t *out);
 
+/* ---- concurrent per-call front door (TokenService contract under many threads) ----
+ * Callers block in request_token; a dispatcher thread batches concurrent requests (up to
+ * max_batch, or max_wait_us after the first) into one GPU batch in arrival order. */
+typedef struct sentinel_batcher sentinel_batcher_t;
+int  sentinel_batcher_create(sentinel_engine_t *eng, int32_t max_batch, int32_t max_wait_us, sentinel_batcher_t **out);
+int  sentinel_batcher_destroy(sentinel_batcher_t *b);
+int  sentinel_batcher_request_token(sentinel_batcher_t *b, int64_t flow_id, int32_t acquire_count,
+                                    int32_t prioritized, int64_t ts, sentinel_token_result_t *out);
+int  sentinel_batcher_stats(sentinel_batcher_t *b, int64_t *batches, int64_t *requests);
+
 /* ---- observability / parity ---- */
 int  sentinel_synchronize(sentinel_engine_t *eng);
 /* Flow metric dump: sample_count x {window start ms (-1 = absent), 7 counters}, then 7 occupy

@@ -91,6 +91,7 @@ def lib():
         "orc_engine_load_flow_rules": (C.c_int, [vp, vp, C.c_int]),
         "orc_request_token": (None, [vp, i32, i32, C.c_int, i64, vp, vp, vp]),
         "orc_flow_replay": (None, [vp, i64, vp, vp, vp, vp, vp, vp, vp]),
+        "orc_flow_replay_mt": (C.c_int, [vp, i64, vp, vp, vp, vp, vp, vp, vp, C.c_int]),
         "orc_engine_dump_flow": (C.c_int, [vp, i32, vp]),
         "orc_engine_limiter_sum": (i64, [vp, i32, i64]),
         "orc_engine_load_param_rules": (C.c_int, [vp, vp, C.c_int, vp, vp, C.c_int]),
@@ -335,6 +336,20 @@ class TokenServiceOracle:
         lib().orc_flow_replay(self.h, n, _p(flow_idx), _p(acquire), _p(flags), _p(ts),
                               _p(status), _p(remaining), _p(wait))
         return status, remaining, wait
+
+    def replay_mt(self, flow_idx, acquire, ts, nthreads, flags=None):
+        """Flow-sharded multi-threaded replay; returns (status, remaining, wait, threads_used)."""
+        n = len(ts)
+        flow_idx = np.ascontiguousarray(flow_idx, dtype=np.int32)
+        acquire = np.ascontiguousarray(acquire, dtype=np.int32)
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        flags = None if flags is None else np.ascontiguousarray(flags, dtype=np.uint8)
+        status = np.zeros(n, dtype=np.int8)
+        remaining = np.zeros(n, dtype=np.int32)
+        wait = np.zeros(n, dtype=np.int32)
+        used = lib().orc_flow_replay_mt(self.h, n, _p(flow_idx), _p(acquire), _p(flags), _p(ts), _p(status),
+                                        _p(remaining), _p(wait), int(nthreads))
+        return status, remaining, wait, used
 
     def request_param_token(self, rule_idx, acquire, t, values):
         v = np.ascontiguousarray(values, dtype=np.uint64)

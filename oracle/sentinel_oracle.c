@@ -25,6 +25,7 @@
 #include "sentinel_oracle.h"
 
 #include <math.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -602,6 +603,52 @@ void orc_flow_replay(orc_engine *e, int64_t n, const int32_t *flow_idx, const in
     for (int64_t i = 0; i < n; i++)
         orc_request_token(e, flow_idx[i], acquire[i], flags ? (flags[i] & 1) : 0, ts[i],
                           &status[i], &remaining[i], wait_ms ? &wait_ms[i] : NULL);
+}
+
+/* Multi-threaded replay for the CPU baseline (BASELINE.md §2 mode ii): thread k owns the flows
+ * with flow_idx mod T == k and processes their events in arrival order, so each flow still sees a
+ * sequential replay.  Only valid without namespace limiters (they couple flows). */
+typedef struct {
+    orc_engine *e;
+    int64_t n;
+    const int32_t *flow_idx, *acquire;
+    const uint8_t *flags;
+    const int64_t *ts;
+    int8_t *status;
+    int32_t *remaining, *wait_ms;
+    int T, k;
+} mt_arg;
+
+static void *mt_worker(void *p) {
+    mt_arg *a = (mt_arg *)p;
+    for (int64_t i = 0; i < a->n; i++) {
+        const int32_t f = a->flow_idx[i];
+        const int owner = f >= 0 ? (int)(f % a->T) : 0;
+        if (owner != a->k) continue;
+        orc_request_token(a->e, f, a->acquire[i], a->flags ? (a->flags[i] & 1) : 0, a->ts[i],
+                          &a->status[i], &a->remaining[i], a->wait_ms ? &a->wait_ms[i] : NULL);
+    }
+    return NULL;
+}
+
+int orc_flow_replay_mt(orc_engine *e, int64_t n, const int32_t *flow_idx, const int32_t *acquire,
+                       const uint8_t *flags, const int64_t *ts, int8_t *status, int32_t *remaining,
+                       int32_t *wait_ms, int nthreads) {
+    for (int i = 0; i < e->n_ns; i++)
+        if (e->lim[i]) nthreads = 1;
+    if (nthreads <= 1) {
+        orc_flow_replay(e, n, flow_idx, acquire, flags, ts, status, remaining, wait_ms);
+        return 1;
+    }
+    pthread_t th[256];
+    mt_arg args[256];
+    if (nthreads > 256) nthreads = 256;
+    for (int k = 0; k < nthreads; k++) {
+        args[k] = (mt_arg){e, n, flow_idx, acquire, flags, ts, status, remaining, wait_ms, nthreads, k};
+        pthread_create(&th[k], NULL, mt_worker, &args[k]);
+    }
+    for (int k = 0; k < nthreads; k++) pthread_join(th[k], NULL);
+    return nthreads;
 }
 
 int orc_engine_dump_flow(const orc_engine *e, int32_t idx, int64_t *out) {

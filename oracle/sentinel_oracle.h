@@ -115,6 +115,10 @@ void orc_request_token(orc_engine *e, int32_t flow_idx, int32_t acquire, int pri
 void orc_flow_replay(orc_engine *e, int64_t n, const int32_t *flow_idx, const int32_t *acquire,
                      const uint8_t *flags, const int64_t *ts,
                      int8_t *status, int32_t *remaining, int32_t *wait_ms);
+/* Flow-sharded multi-threaded replay (CPU baseline); returns the threads used (1 with limiters). */
+int  orc_flow_replay_mt(orc_engine *e, int64_t n, const int32_t *flow_idx, const int32_t *acquire,
+                        const uint8_t *flags, const int64_t *ts, int8_t *status, int32_t *remaining,
+                        int32_t *wait_ms, int nthreads);
 /* Dump flow metric state, orc_cm_dump format. Returns words written or -1. */
 int  orc_engine_dump_flow(const orc_engine *e, int32_t flow_idx, int64_t *out);
 int64_t orc_engine_limiter_sum(orc_engine *e, int32_t ns, int64_t t);

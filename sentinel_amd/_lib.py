@@ -42,6 +42,7 @@ EXPORTS = [
     "sentinel_synchronize", "sentinel_dump_flow", "sentinel_param_sum",
     "sentinel_snapshot", "sentinel_snapshot_device", "sentinel_engine_stream",
     "sentinel_profile_enable", "sentinel_profile_read",
+    "sentinel_batcher_create", "sentinel_batcher_destroy", "sentinel_batcher_request_token", "sentinel_batcher_stats",
 ]
 
 
@@ -126,6 +127,10 @@ def load():
         "sentinel_engine_stream": (vp, [vp]),
         "sentinel_profile_enable": (C.c_int, [vp, C.c_int]),
         "sentinel_profile_read": (C.c_int, [vp, C.c_int, vp, vp, vp, vp]),
+        "sentinel_batcher_create": (C.c_int, [vp, i32, i32, C.POINTER(vp)]),
+        "sentinel_batcher_destroy": (C.c_int, [vp]),
+        "sentinel_batcher_request_token": (C.c_int, [vp, i64, i32, i32, i64, vp]),
+        "sentinel_batcher_stats": (C.c_int, [vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

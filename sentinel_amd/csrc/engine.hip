@@ -17,7 +17,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -1234,6 +1238,140 @@ int sentinel_snapshot(sentinel_engine_t *e, int64_t ts, sentinel_flow_snapshot_t
     }
     (void)hipFree(d);
     return rc;
+}
+
+}  // extern "C"
+
+// ==================================================================== request batcher
+// The reference TokenService is synchronous per call and called concurrently from Netty worker
+// threads (NettyTransportServer.java:53-54, FlowRequestProcessor.java:36-45).  The batcher keeps
+// that contract: callers block in sentinel_batcher_request_token while a dispatcher thread gathers
+// concurrent requests (up to max_batch, or max_wait_us after the first one) into pinned host
+// buffers, decides them as one GPU batch in arrival order, and wakes the callers.  Double-buffered:
+// the next batch is gathered while the current one is on the GPU.
+struct BatchReq {
+    sentinel_event_t ev;
+    uint8_t flag;
+    sentinel_verdict_t out;
+    int rc;
+    std::atomic<int> done{0};
+};
+
+struct sentinel_batcher {
+    sentinel_engine *e = nullptr;
+    int32_t max_batch = 4096;
+    int32_t max_wait_us = 50;
+    std::mutex mu;
+    std::condition_variable cv_in, cv_out;
+    std::vector<BatchReq *> queue;
+    std::thread th;
+    bool stop = false;
+    sentinel_event_t *h_ev = nullptr;
+    uint8_t *h_fl = nullptr;
+    sentinel_verdict_t *h_out = nullptr;
+    std::atomic<int64_t> batches{0}, requests{0};
+
+    void run() {
+        std::vector<BatchReq *> cur;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv_in.wait(lk, [&] { return stop || !queue.empty(); });
+                if (stop && queue.empty()) return;
+                if ((int32_t)queue.size() < max_batch && max_wait_us > 0) {
+                    cv_in.wait_for(lk, std::chrono::microseconds(max_wait_us),
+                                   [&] { return stop || (int32_t)queue.size() >= max_batch; });
+                }
+                const size_t take = std::min<size_t>(queue.size(), (size_t)max_batch);
+                cur.assign(queue.begin(), queue.begin() + take);
+                queue.erase(queue.begin(), queue.begin() + take);
+            }
+            const int64_t n = (int64_t)cur.size();
+            for (int64_t i = 0; i < n; ++i) {
+                h_ev[i] = cur[i]->ev;
+                h_fl[i] = cur[i]->flag;
+            }
+            const int rc = sentinel_submit_flow_batch_host(e, n, h_ev, h_fl, h_out);
+            for (int64_t i = 0; i < n; ++i) {
+                cur[i]->out = h_out[i];
+                cur[i]->rc = rc;
+                cur[i]->done.store(1, std::memory_order_release);
+            }
+            batches.fetch_add(1);
+            requests.fetch_add(n);
+            {
+                std::lock_guard<std::mutex> lk(mu);
+            }
+            cv_out.notify_all();
+        }
+    }
+};
+
+extern "C" {
+
+int sentinel_batcher_create(sentinel_engine_t *e, int32_t max_batch, int32_t max_wait_us, sentinel_batcher_t **out) {
+    if (!e || !out || max_batch <= 0 || max_wait_us < 0) return fail(SENTINEL_E_INVALID, "bad batcher arguments");
+    sentinel_batcher *b = new sentinel_batcher();
+    b->e = e;
+    b->max_batch = max_batch;
+    b->max_wait_us = max_wait_us;
+    (void)hipSetDevice(e->device);
+    if (hipHostMalloc((void **)&b->h_ev, (size_t)max_batch * sizeof(sentinel_event_t), 0) != hipSuccess ||
+        hipHostMalloc((void **)&b->h_fl, (size_t)max_batch, 0) != hipSuccess ||
+        hipHostMalloc((void **)&b->h_out, (size_t)max_batch * sizeof(sentinel_verdict_t), 0) != hipSuccess) {
+        delete b;
+        return fail(SENTINEL_E_NOMEM, "hipHostMalloc failed");
+    }
+    b->th = std::thread([b] { b->run(); });
+    *out = b;
+    return 0;
+}
+
+int sentinel_batcher_destroy(sentinel_batcher_t *b) {
+    if (!b) return 0;
+    {
+        std::lock_guard<std::mutex> lk(b->mu);
+        b->stop = true;
+    }
+    b->cv_in.notify_all();
+    if (b->th.joinable()) b->th.join();
+    (void)hipHostFree(b->h_ev);
+    (void)hipHostFree(b->h_fl);
+    (void)hipHostFree(b->h_out);
+    delete b;
+    return 0;
+}
+
+int sentinel_batcher_request_token(sentinel_batcher_t *b, int64_t flow_id, int32_t acquire, int32_t prio, int64_t ts,
+                                   sentinel_token_result_t *out) {
+    if (!b || !out) return fail(SENTINEL_E_INVALID, "null argument");
+    BatchReq r;
+    sentinel_lookup_flow_idx(b->e, 1, &flow_id, &r.ev.flow_idx);
+    r.ev.acquire = acquire;
+    r.ev.ts = ts;
+    r.flag = prio ? SENTINEL_FLAG_PRIORITIZED : 0;
+    {
+        std::lock_guard<std::mutex> lk(b->mu);
+        if (b->stop) return fail(SENTINEL_E_STATE, "batcher stopped");
+        b->queue.push_back(&r);
+        if ((int32_t)b->queue.size() == 1 || (int32_t)b->queue.size() >= b->max_batch) b->cv_in.notify_one();
+    }
+    {
+        std::unique_lock<std::mutex> lk(b->mu);
+        b->cv_out.wait(lk, [&] { return r.done.load(std::memory_order_acquire) != 0; });
+    }
+    out->status = r.rc ? SENTINEL_STATUS_FAIL : r.out.status;   // engine down -> FAIL (client falls back)
+    out->remaining = r.rc ? 0 : r.out.remaining;
+    out->wait_in_ms = r.rc ? 0 : r.out.wait_in_ms;
+    out->reserved = 0;
+    return r.rc;
+}
+
+int sentinel_batcher_stats(sentinel_batcher_t *b, int64_t *batches, int64_t *requests) {
+    if (!b) return fail(SENTINEL_E_INVALID, "null batcher");
+    if (batches) *batches = b->batches.load();
+    if (requests) *requests = b->requests.load();
+    return 0;
 }
 
 }  // extern "C"

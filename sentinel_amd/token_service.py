@@ -322,6 +322,42 @@ class GpuTokenService:
         return out_tensor
 
 
+class TokenBatcher:
+    """Concurrent per-call front door: thread-safe request_token that is batched on the GPU
+    (sentinel_batcher_*).  ctypes releases the GIL during the call, so Python threads really wait
+    in parallel; the Java shim uses the same entry point from Netty worker threads."""
+
+    def __init__(self, svc: "GpuTokenService", max_batch: int = 4096, max_wait_us: int = 50):
+        self._svc = svc
+        self._L = svc._L
+        self._b = C.c_void_p()
+        check(self._L.sentinel_batcher_create(svc.handle, max_batch, max_wait_us, C.byref(self._b)), "batcher_create")
+
+    def request_token(self, rule_id, acquire_count, prioritized=False, ts=None) -> TokenResult:
+        out = _lib.TokenResultC()
+        fid = 0 if rule_id is None else int(rule_id)
+        check(self._L.sentinel_batcher_request_token(self._b, fid, int(acquire_count), int(bool(prioritized)),
+                                                     _now_ms() if ts is None else int(ts), C.byref(out)),
+              "batcher_request_token")
+        return TokenResult(out.status, out.remaining, out.wait_in_ms)
+
+    def stats(self):
+        b, r = C.c_int64(), C.c_int64()
+        check(self._L.sentinel_batcher_stats(self._b, C.byref(b), C.byref(r)), "batcher_stats")
+        return b.value, r.value
+
+    def close(self):
+        if self._b.value:
+            self._L.sentinel_batcher_destroy(self._b)
+            self._b = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def decode_verdicts(v):
     """Packed int64 verdicts (torch or numpy) -> (status int16, remaining int32, wait uint16) numpy."""
     a = v.cpu().numpy() if hasattr(v, "cpu") else np.asarray(v)

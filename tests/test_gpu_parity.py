@@ -270,3 +270,38 @@ def test_full_size_properties_config3():
     v2 = svc2.submit_flow_batch(ev)
     svc2.synchronize()
     assert torch.equal(v, v2)
+
+
+def test_batcher_concurrent_threads():
+    """Many threads calling the per-call API concurrently: batched on the GPU, and the result set
+    equals a sequential replay in some arrival order (homogeneous acquire => order-free counts)."""
+    import threading
+    import sentinel_amd as sa
+    from sentinel_amd.token_service import TokenBatcher
+    svc = sa.GpuTokenService(0)
+    svc.load_flow_rules([sa.FlowRule(count=50, cluster_config=sa.ClusterFlowConfig(
+        flow_id=777, threshold_type=1, sample_count=2, window_interval_ms=1000))])
+    b = TokenBatcher(svc, max_batch=256, max_wait_us=200)
+    results = []
+    lock = threading.Lock()
+    t = T.T0_ALIGNED + 10
+
+    def worker():
+        for _ in range(25):
+            r = b.request_token(777, 1, False, ts=t)
+            with lock:
+                results.append(r)
+
+    th = [threading.Thread(target=worker) for _ in range(16)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    ok = sorted(r.remaining for r in results if r.status == 0)
+    assert len(results) == 400
+    assert ok == list(range(50))[::-1][::-1] and len(ok) == 50
+    assert sum(1 for r in results if r.status == 1) == 350
+    nb, nr = b.stats()
+    assert nr == 400 and 1 <= nb <= 400
+    assert b.request_token(None, 1, False, ts=t).status == sa.TokenResultStatus.BAD_REQUEST
+    b.close()

@@ -153,3 +153,14 @@ def test_kat_java_numerics(oracle_mod):
     for d, i in kat["d2i"]:
         d = math.nan if d == "nan" else d
         assert oracle_mod.lib().orc_java_d2i(d) == i
+
+
+def test_mt_replay_equals_sequential(oracle_mod):
+    """The multi-threaded CPU baseline (flow-sharded) is the same replay as the sequential oracle."""
+    from sentinel_amd import trace as T
+    rules, ev = T.config2(200_000, seed=9, n_flows=2000)
+    a = oracle_mod.TokenServiceOracle(rules.as_dicts()).replay(ev.flow_idx, ev.acquire, ev.ts)
+    b = oracle_mod.TokenServiceOracle(rules.as_dicts()).replay_mt(ev.flow_idx, ev.acquire, ev.ts, 4)
+    assert b[3] == 4
+    for x, y in zip(a, b[:3]):
+        assert (x == y).all()
