@@ -183,6 +183,69 @@ int  sentinel_submit_param_batch(sentinel_engine_t *eng, int64_t n, const sentin
 int  sentinel_submit_param_batch_host(sentinel_engine_t *eng, int64_t n, const sentinel_param_event_t *events,
                                       sentinel_verdict_t *verdicts);
 
+/* ---- hot-parameter requests beyond one value, count-min mode, local token bucket ---- */
+
+/* One requestParamToken call with any number of values (TokenService.java:46;
+ * ClusterParamFlowChecker.acquireClusterToken, sentinel-cluster/.../cluster/flow/ClusterParamFlowChecker.java:42-87),
+ * or one local ParamFlowChecker.passLocalCheck over a collection / array argument
+ * (sentinel-extension/sentinel-parameter-flow-control/.../param/ParamFlowChecker.java:78-103).
+ * Its values are values[value_begin, value_begin + value_count) of the batch's value array, each
+ * the host's injective 64-bit encoding of (rule, Java-typed value).  24 bytes; the first 16 are
+ * laid out like sentinel_event_t. */
+typedef struct {
+    int32_t rule_idx;
+    int32_t acquire;
+    int64_t ts;
+    int32_t value_begin;
+    int32_t value_count;
+} sentinel_param_multi_event_t;
+
+/* Cluster param requests with value lists: the values are checked in order, the first whose
+ * remaining would be negative blocks the request and no counter is touched; otherwise every
+ * value's counter is incremented (a repeated value twice).  remaining is that of the last value,
+ * -1 for more than one value (CPFC:81-84).  Events of one rule are decided in arrival order by
+ * one lane, so mixing them with single-value batches keeps the sequential semantics.  DEVICE
+ * pointers, asynchronous. */
+int  sentinel_submit_param_multi_batch(sentinel_engine_t *eng, int64_t n, const sentinel_param_multi_event_t *events,
+                                       const uint64_t *values, int64_t n_values, sentinel_verdict_t *verdicts,
+                                       void *stream);
+int  sentinel_submit_param_multi_batch_host(sentinel_engine_t *eng, int64_t n, const sentinel_param_multi_event_t *events,
+                                            const uint64_t *values, int64_t n_values, sentinel_verdict_t *verdicts);
+
+/* Counter mode of the cluster param path (BASELINE config 4).  COUNT_MIN keeps, per rule, a
+ * depth x width sketch of window counters instead of exact per-value counters: memory is bounded
+ * whatever the number of values, estimates never undercount a value's own passes, so a request may
+ * be blocked that exact counters would pass but never the reverse; with probability >= 1 -
+ * exp(-depth) an estimate exceeds the true window count by at most (e / width) x (the rule's total
+ * window count).  Switching modes clears the param counters. */
+#define SENTINEL_PARAM_EXACT      0
+#define SENTINEL_PARAM_COUNT_MIN  1
+int  sentinel_set_param_mode(sentinel_engine_t *eng, int32_t mode, int32_t depth, int32_t width);
+
+/* Local hot-parameter rule (ParamFlowRule, QPS grade, default control behaviour) as
+ * ParamFlowChecker.passDefaultLocalCheck reads it (ParamFlowChecker.java:127-202).  Rule index =
+ * position in the loaded array; rules failing ParamFlowRuleUtil.isValidRule
+ * (ParamFlowRuleUtil.java:46-52) answer NO_RULE_EXISTS.  32 bytes. */
+typedef struct {
+    double  count;             /* ParamFlowRule.count: tokenCount = (long) count */
+    int64_t burst_count;       /* ParamFlowRule.burstCount */
+    int64_t duration_in_sec;   /* ParamFlowRule.durationInSec */
+    int32_t hot_begin;         /* [hot_begin, hot_begin + hot_n) into the hot-item arrays */
+    int32_t hot_n;
+} sentinel_local_param_rule_t;
+
+/* Loads the local rules; every token bucket restarts (ParameterMetric counters). */
+int  sentinel_load_local_param_rules(sentinel_engine_t *eng, const sentinel_local_param_rule_t *rules, int32_t n,
+                                     const uint64_t *hot_keys, const int32_t *hot_counts, int32_t n_hot);
+/* passLocalCheck per event: OK (pass) or BLOCKED; an empty value list passes. */
+int  sentinel_submit_local_param_batch(sentinel_engine_t *eng, int64_t n, const sentinel_param_multi_event_t *events,
+                                       const uint64_t *values, int64_t n_values, sentinel_verdict_t *verdicts,
+                                       void *stream);
+int  sentinel_submit_local_param_batch_host(sentinel_engine_t *eng, int64_t n, const sentinel_param_multi_event_t *events,
+                                            const uint64_t *values, int64_t n_values, sentinel_verdict_t *verdicts);
+/* Token bucket of one value: {lastAddTokenTime, tokens} (-1 when absent); returns 1 if present. */
+int  sentinel_local_param_state(sentinel_engine_t *eng, uint64_t param_key, int64_t *last_add_ms, int64_t *tokens);
+
 /* ---- per-call TokenService mirror (one event, synchronous) ---- */
 int  sentinel_request_token(sentinel_engine_t *eng, int64_t flow_id, int32_t acquire_count,
                             int32_t prioritized, int64_t ts, sentinel_token_result_t *out);

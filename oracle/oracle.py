@@ -113,6 +113,12 @@ def lib():
         "orc_pbucket_new": (vp, []),
         "orc_pbucket_free": (None, [vp]),
         "orc_pbucket_pass_default": (C.c_int, [vp, u64, i64, i64, i64, C.c_int, i64]),
+        "orc_param_multi_replay": (None, [vp, i64, vp, vp, vp, vp, vp, vp, i64, vp, vp]),
+        "orc_param_cm_audit": (None, [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "orc_lparam_new": (vp, [vp, C.c_int, vp, vp, C.c_int]),
+        "orc_lparam_free": (None, [vp]),
+        "orc_lparam_replay": (None, [vp, i64, vp, vp, vp, vp, vp, vp, i64, vp]),
+        "orc_lparam_state": (C.c_int, [vp, i32, u64, vp, vp]),
         "orc_java_d2i": (i32, [dbl]),
         "orc_java_string_hash": (i32, [vp, i64]),
     }
@@ -234,6 +240,50 @@ class ParamTokenBucket:
 
     def pass_default(self, key, token_count, burst, duration_sec, acquire, t):
         return lib().orc_pbucket_pass_default(self.h, key, token_count, burst, duration_sec, acquire, t)
+
+
+class LocalParamRule(C.Structure):
+    _fields_ = [("count", C.c_double), ("burst_count", C.c_int64), ("duration_in_sec", C.c_int64),
+                ("hot_begin", C.c_int32), ("hot_n", C.c_int32)]
+
+
+def _multi_args(rule_idx, acquire, ts, vbegin, vcount, values):
+    return (np.ascontiguousarray(rule_idx, dtype=np.int32), np.ascontiguousarray(acquire, dtype=np.int32),
+            np.ascontiguousarray(ts, dtype=np.int64), np.ascontiguousarray(vbegin, dtype=np.int32),
+            np.ascontiguousarray(vcount, dtype=np.int32), np.ascontiguousarray(values, dtype=np.uint64))
+
+
+class LocalParamOracle:
+    """ParamFlowChecker.passLocalCheck replay, one ParameterMetric per rule (ParamFlowChecker.java:78-202).
+    rules: [(count, burst_count, duration_in_sec, {key: hot_count})]; rule index = position."""
+
+    def __init__(self, rules):
+        arr = (LocalParamRule * max(len(rules), 1))()
+        keys, counts = [], []
+        for i, (count, burst, dur, hot) in enumerate(rules):
+            arr[i] = LocalParamRule(float(count), int(burst), int(dur), len(keys), len(hot))
+            for k, c in hot.items():
+                keys.append(k)
+                counts.append(c)
+        hk = np.array(keys or [0], dtype=np.uint64)
+        hc = np.array(counts or [0], dtype=np.int32)
+        self.h = lib().orc_lparam_new(arr, len(rules), _p(hk), _p(hc), len(keys))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_lparam_free(self.h)
+
+    def replay(self, rule_idx, acquire, ts, vbegin, vcount, values) -> np.ndarray:
+        r, a, t, b, c, v = _multi_args(rule_idx, acquire, ts, vbegin, vcount, values)
+        status = np.zeros(len(t), dtype=np.int8)
+        lib().orc_lparam_replay(self.h, len(t), _p(r), _p(a), _p(t), _p(b), _p(c), _p(v) if len(v) else None,
+                                len(v), _p(status))
+        return status
+
+    def state(self, rule_idx, key):
+        last, tok = C.c_int64(), C.c_int64()
+        lib().orc_lparam_state(self.h, int(rule_idx), int(key), C.byref(last), C.byref(tok))
+        return last.value, tok.value
 
 
 def default_controller_check(node_value, count, grade, acquire) -> bool:
@@ -367,6 +417,23 @@ class TokenServiceOracle:
         remaining = np.zeros(n, dtype=np.int32)
         lib().orc_param_replay(self.h, n, _p(rule_idx), _p(acquire), _p(keys), _p(ts), _p(status), _p(remaining))
         return status, remaining
+
+    def param_multi_replay(self, rule_idx, acquire, ts, vbegin, vcount, values):
+        r, a, t, b, c, v = _multi_args(rule_idx, acquire, ts, vbegin, vcount, values)
+        status = np.zeros(len(t), dtype=np.int8)
+        remaining = np.zeros(len(t), dtype=np.int32)
+        lib().orc_param_multi_replay(self.h, len(t), _p(r), _p(a), _p(t), _p(b), _p(c), _p(v) if len(v) else None,
+                                     len(v), _p(status), _p(remaining))
+        return status, remaining
+
+    def param_cm_audit(self, rule_idx, acquire, ts, vbegin, vcount, values, status_cm):
+        """(violations, false_blocks, decided) of count-min verdicts replayed on exact counters."""
+        r, a, t, b, c, v = _multi_args(rule_idx, acquire, ts, vbegin, vcount, values)
+        st = np.ascontiguousarray(status_cm, dtype=np.int8)
+        viol, fb, dec = C.c_int64(), C.c_int64(), C.c_int64()
+        lib().orc_param_cm_audit(self.h, len(t), _p(r), _p(a), _p(t), _p(b), _p(c), _p(v), _p(st),
+                                 C.byref(viol), C.byref(fb), C.byref(dec))
+        return viol.value, fb.value, dec.value
 
     def param_sum(self, rule_idx, t, key):
         return lib().orc_engine_param_sum(self.h, rule_idx, t, key)

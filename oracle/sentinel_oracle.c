@@ -894,3 +894,122 @@ int orc_pbucket_pass_default(orc_param_bucket *b, uint64_t key, int64_t token_co
     }
     return -1;   /* time counter present, token counter absent: only after LRU eviction (unpinned) */
 }
+
+/* ------------------------------------------------------------------ multi-value cluster params */
+/* A batch of requestParamToken calls with value lists, in arrival order (CPFC:42-87 per call). */
+void orc_param_multi_replay(orc_engine *e, int64_t n, const int32_t *rule_idx, const int32_t *acquire,
+                            const int64_t *ts, const int32_t *vbegin, const int32_t *vcount,
+                            const uint64_t *values, int64_t n_values, int8_t *status, int32_t *remaining) {
+    for (int64_t i = 0; i < n; i++) {
+        const int32_t b = vbegin[i], c = vcount[i];
+        if (c < 0 || b < 0 || (int64_t)b + c > n_values) { status[i] = ORC_BAD_REQUEST; remaining[i] = 0; continue; }
+        orc_request_param_token(e, rule_idx[i], acquire[i], ts[i], values + b, c, &status[i], &remaining[i]);
+    }
+}
+
+/* Audit of count-min verdicts against exact counters on the same history: replays the sequence
+ * of decisions the sketch made (passes add to the exact ClusterParamMetric, blocks do not) and
+ * counts (a) passes the exact checker would have blocked -- must be 0 for a one-sided sketch --
+ * and (b) blocks the exact checker would have passed (false blocks). */
+void orc_param_cm_audit(orc_engine *e, int64_t n, const int32_t *rule_idx, const int32_t *acquire,
+                        const int64_t *ts, const int32_t *vbegin, const int32_t *vcount, const uint64_t *values,
+                        const int8_t *status_cm, int64_t *violations, int64_t *false_blocks, int64_t *decided) {
+    *violations = *false_blocks = *decided = 0;
+    for (int64_t i = 0; i < n; i++) {
+        if (status_cm[i] != ORC_OK && status_cm[i] != ORC_BLOCKED) continue;
+        const int32_t idx = rule_idx[i];
+        if (idx < 0 || idx >= e->n_prules || !e->prules[idx].pm) continue;
+        const orc_param_rule *r = &e->prules[idx].r;
+        orc_param_metric *m = e->prules[idx].pm;
+        const uint64_t *v = values + vbegin[i];
+        int exact_pass = 1;
+        for (int j = 0; j < vcount[i]; j++) {
+            double next = (param_threshold(e, r, v[j]) - orc_pm_get_avg(m, ts[i], v[j])) - (double)acquire[i];
+            if (next < 0) { exact_pass = 0; break; }
+        }
+        (*decided)++;
+        if (status_cm[i] == ORC_OK) {
+            if (!exact_pass) (*violations)++;
+            for (int j = 0; j < vcount[i]; j++) orc_pm_add_value(m, ts[i], v[j], acquire[i]);
+        } else if (exact_pass) {
+            (*false_blocks)++;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ local param engine */
+/* ParamFlowChecker.passLocalCheck (PFC:78-103) with one ParameterMetric token/time counter pair
+ * per rule (ParameterMetric.java:95-118); rules failing ParamFlowRuleUtil.isValidRule
+ * (ParamFlowRuleUtil.java:46-52) are not loaded. */
+typedef struct {
+    orc_local_param_rule r;
+    int valid;
+    int64_t token_count;      /* (long) rule.count (PFC:139) */
+    orc_param_bucket *b;
+    kvmap hot;                /* param key -> hot-item count (PFC:138-142) */
+} local_entry;
+
+struct orc_local_engine {
+    local_entry *rules;
+    int n;
+};
+
+orc_local_engine *orc_lparam_new(const orc_local_param_rule *rules, int n, const uint64_t *hot_keys,
+                                const int32_t *hot_counts, int n_hot) {
+    orc_local_engine *e = (orc_local_engine *)calloc(1, sizeof(*e));
+    e->n = n;
+    e->rules = (local_entry *)calloc((size_t)(n > 0 ? n : 1), sizeof(local_entry));
+    for (int i = 0; i < n; i++) {
+        local_entry *le = &e->rules[i];
+        le->r = rules[i];
+        le->valid = rules[i].count >= 0 && rules[i].burst_count >= 0 && rules[i].duration_in_sec > 0;
+        le->token_count = orc_java_d2l(rules[i].count);
+        le->b = orc_pbucket_new();
+        kv_init(&le->hot);
+        for (int h = 0; h < rules[i].hot_n; h++) {
+            const int j = rules[i].hot_begin + h;
+            if (j >= 0 && j < n_hot) *kv_insert(&le->hot, hot_keys[j], 0) = hot_counts[j];
+        }
+    }
+    return e;
+}
+
+void orc_lparam_free(orc_local_engine *e) {
+    if (!e) return;
+    for (int i = 0; i < e->n; i++) { orc_pbucket_free(e->rules[i].b); kv_free(&e->rules[i].hot); }
+    free(e->rules);
+    free(e);
+}
+
+void orc_lparam_replay(orc_local_engine *e, int64_t n, const int32_t *rule_idx, const int32_t *acquire,
+                      const int64_t *ts, const int32_t *vbegin, const int32_t *vcount, const uint64_t *values,
+                      int64_t n_values, int8_t *status) {
+    for (int64_t i = 0; i < n; i++) {
+        const int32_t b = vbegin[i], c = vcount[i];
+        if (c < 0 || b < 0 || (int64_t)b + c > n_values) { status[i] = ORC_BAD_REQUEST; continue; }
+        const int32_t idx = rule_idx[i];
+        if (idx < 0 || idx >= e->n || !e->rules[idx].valid) { status[i] = ORC_NO_RULE_EXISTS; continue; }
+        local_entry *le = &e->rules[idx];
+        int st = ORC_OK;
+        for (int j = 0; j < c; j++) {      /* every element must pass, no rollback (PFC:81-94) */
+            const uint64_t key = values[b + j];
+            const int64_t *hv = kv_find(&le->hot, key);
+            const int64_t tok = hv ? *hv : le->token_count;
+            const int r = orc_pbucket_pass_default(le->b, key, tok, le->r.burst_count, le->r.duration_in_sec,
+                                                   acquire[i], ts[i]);
+            if (r == 0) { st = ORC_BLOCKED; break; }
+            if (r < 0) { st = ORC_FAIL; break; }
+        }
+        status[i] = (int8_t)st;
+    }
+}
+
+int orc_lparam_state(orc_local_engine *e, int32_t idx, uint64_t key, int64_t *last, int64_t *tokens) {
+    *last = *tokens = -1;
+    if (idx < 0 || idx >= e->n) return 0;
+    int64_t *l = kv_find(&e->rules[idx].b->time_ctr, key);
+    int64_t *t = kv_find(&e->rules[idx].b->token_ctr, key);
+    if (l) *last = *l;
+    if (t) *tokens = *t;
+    return l != NULL;
+}

@@ -174,6 +174,32 @@ void orc_pbucket_free(orc_param_bucket *b);
 int  orc_pbucket_pass_default(orc_param_bucket *b, uint64_t key, int64_t token_count, int64_t burst,
                               int64_t duration_sec, int acquire, int64_t t);
 
+/* ---------------- multi-value cluster params, count-min audit, local param engine ---------------- */
+void orc_param_multi_replay(orc_engine *e, int64_t n, const int32_t *rule_idx, const int32_t *acquire,
+                            const int64_t *ts, const int32_t *vbegin, const int32_t *vcount,
+                            const uint64_t *values, int64_t n_values, int8_t *status, int32_t *remaining);
+void orc_param_cm_audit(orc_engine *e, int64_t n, const int32_t *rule_idx, const int32_t *acquire,
+                        const int64_t *ts, const int32_t *vbegin, const int32_t *vcount, const uint64_t *values,
+                        const int8_t *status_cm, int64_t *violations, int64_t *false_blocks, int64_t *decided);
+
+/* Mirrors include/sentinel_amd.h's sentinel_local_param_rule_t. */
+typedef struct {
+    double  count;
+    int64_t burst_count;
+    int64_t duration_in_sec;
+    int32_t hot_begin;
+    int32_t hot_n;
+} orc_local_param_rule;
+
+typedef struct orc_local_engine orc_local_engine;
+orc_local_engine *orc_lparam_new(const orc_local_param_rule *rules, int n, const uint64_t *hot_keys,
+                                const int32_t *hot_counts, int n_hot);
+void orc_lparam_free(orc_local_engine *e);
+void orc_lparam_replay(orc_local_engine *e, int64_t n, const int32_t *rule_idx, const int32_t *acquire,
+                      const int64_t *ts, const int32_t *vbegin, const int32_t *vcount, const uint64_t *values,
+                      int64_t n_values, int8_t *status);
+int  orc_lparam_state(orc_local_engine *e, int32_t idx, uint64_t key, int64_t *last, int64_t *tokens);
+
 /* ---------------- Java numerics ---------------- */
 int32_t orc_java_d2i(double d);
 int64_t orc_java_d2l(double d);

@@ -1,0 +1,28 @@
+# Full GPU round check on one MI355X: parity tests, bench, rocprofv3 kernel stats, and the two
+# PMC passes (FETCH_SIZE, WRITE_SIZE: separate runs, as MI355X_MICROARCH.md prescribes).
+# Every GPU step has its own time limit; the chain stops at the first failure.
+# Usage (from gpurun): bash scripts/gpu_round.sh [TAG]   -> results under gpurun_out/$TAG
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+TAG=${1:-round}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+echo "== tests"
+timeout -k 10 480 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $O/gpu_tests.log 2>&1
+rc=$?
+tail -3 $O/gpu_tests.log
+[ $rc -eq 0 ] || { grep -E "Error|assert|FAIL" $O/gpu_tests.log | head -20; exit $rc; }
+echo "== bench"
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+cat $O/bench.json
+echo "== rocprof stats"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/bench_prof.json 2> $O/prof.err || { tail -20 $O/prof.err; exit 1; }
+echo "== pmc FETCH_SIZE"
+timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile > /dev/null 2> $O/pmc_fetch.err || { tail -20 $O/pmc_fetch.err; exit 1; }
+echo "== pmc WRITE_SIZE"
+timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile > /dev/null 2> $O/pmc_write.err || { tail -20 $O/pmc_write.err; exit 1; }
+cd $R
+python scripts/pmc_summary.py $O > $O/pmc_summary.json && cat $O/pmc_summary.json
+echo "ROUND OK"

@@ -3,7 +3,7 @@ flow-control hot path (LeapArray/ClusterMetric + ClusterFlowChecker/ClusterParam
 the TokenService SPI).  See DESIGN.md."""
 from ._lib import SentinelError, load as load_library  # noqa: F401
 from .token_service import (ClusterFlowConfig, ClusterRuleConstant, FlowRule, GpuTokenService,  # noqa: F401
-                            ParamFlowRule, ServerNamespace, TokenResult, TokenResultStatus)
+                            LocalParamRule, ParamFlowRule, ServerNamespace, TokenResult, TokenResultStatus)
 
-__all__ = ["GpuTokenService", "FlowRule", "ParamFlowRule", "ClusterFlowConfig", "ClusterRuleConstant",
+__all__ = ["GpuTokenService", "FlowRule", "ParamFlowRule", "LocalParamRule", "ClusterFlowConfig", "ClusterRuleConstant",
            "ServerNamespace", "TokenResult", "TokenResultStatus", "SentinelError", "load_library"]

@@ -43,7 +43,13 @@ EXPORTS = [
     "sentinel_snapshot", "sentinel_snapshot_device", "sentinel_engine_stream",
     "sentinel_profile_enable", "sentinel_profile_read",
     "sentinel_batcher_create", "sentinel_batcher_destroy", "sentinel_batcher_request_token", "sentinel_batcher_stats",
+    "sentinel_submit_param_multi_batch", "sentinel_submit_param_multi_batch_host", "sentinel_set_param_mode",
+    "sentinel_load_local_param_rules", "sentinel_submit_local_param_batch", "sentinel_submit_local_param_batch_host",
+    "sentinel_local_param_state",
 ]
+
+PARAM_EXACT = 0
+PARAM_COUNT_MIN = 1
 
 
 class ServerConfig(C.Structure):
@@ -66,6 +72,11 @@ class ParamRuleC(C.Structure):
                 ("namespace_idx", C.c_int32), ("hot_begin", C.c_int32), ("hot_n", C.c_int32)]
 
 
+class LocalParamRuleC(C.Structure):
+    _fields_ = [("count", C.c_double), ("burst_count", C.c_int64), ("duration_in_sec", C.c_int64),
+                ("hot_begin", C.c_int32), ("hot_n", C.c_int32)]
+
+
 class TokenResultC(C.Structure):
     _fields_ = [("status", C.c_int32), ("remaining", C.c_int32), ("wait_in_ms", C.c_int32), ("reserved", C.c_int32)]
 
@@ -77,6 +88,8 @@ class FlowSnapshotC(C.Structure):
 # AoS records of include/sentinel_amd.h
 EVENT_DTYPE = np.dtype([("flow_idx", "<i4"), ("acquire", "<i4"), ("ts", "<i8")])
 PARAM_EVENT_DTYPE = np.dtype([("rule_idx", "<i4"), ("acquire", "<i4"), ("ts", "<i8"), ("param_key", "<u8")])
+MULTI_EVENT_DTYPE = np.dtype([("rule_idx", "<i4"), ("acquire", "<i4"), ("ts", "<i8"), ("value_begin", "<i4"),
+                              ("value_count", "<i4")])
 VERDICT_DTYPE = np.dtype([("remaining", "<i4"), ("status", "<i2"), ("wait_in_ms", "<u2")])
 
 
@@ -131,6 +144,13 @@ def load():
         "sentinel_batcher_destroy": (C.c_int, [vp]),
         "sentinel_batcher_request_token": (C.c_int, [vp, i64, i32, i32, i64, vp]),
         "sentinel_batcher_stats": (C.c_int, [vp, vp, vp]),
+        "sentinel_submit_param_multi_batch": (C.c_int, [vp, i64, vp, vp, i64, vp, vp]),
+        "sentinel_submit_param_multi_batch_host": (C.c_int, [vp, i64, vp, vp, i64, vp]),
+        "sentinel_set_param_mode": (C.c_int, [vp, i32, i32, i32]),
+        "sentinel_load_local_param_rules": (C.c_int, [vp, vp, i32, vp, vp, i32]),
+        "sentinel_submit_local_param_batch": (C.c_int, [vp, i64, vp, vp, i64, vp, vp]),
+        "sentinel_submit_local_param_batch_host": (C.c_int, [vp, i64, vp, vp, i64, vp]),
+        "sentinel_local_param_state": (C.c_int, [vp, u64, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

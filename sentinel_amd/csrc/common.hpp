@@ -22,7 +22,13 @@ enum : int8_t { ST_BAD_REQUEST = -4, ST_TOO_MANY_REQUEST = -2, ST_FAIL = -1, ST_
 enum : uint8_t { KIND_CLUSTER = 0,   // ClusterFlowChecker (srv/flow/ClusterFlowChecker.java:55-112)
                  KIND_SIMPLE = 1,    // SimpleClusterFlowChecker (rls/flow/SimpleClusterFlowChecker.java:33-65)
                  KIND_LIMITER = 2,   // RequestLimiter.tryPass (srv/flow/statistic/limit/RequestLimiter.java:72-87)
-                 KIND_PARAM = 3 };   // ClusterParamFlowChecker single value (srv/flow/ClusterParamFlowChecker.java:42-87)
+                 KIND_PARAM = 3,     // ClusterParamFlowChecker single value (srv/flow/ClusterParamFlowChecker.java:42-87)
+                 KIND_LOCAL_PARAM = 4 };   // ParamFlowChecker.passLocalCheck (pfc/.../ParamFlowChecker.java:78-202)
+
+// Namespace routing of a rule (ClusterFlowChecker.allowProceed, CFC:50-53; GlobalRequestLimiter.tryPass,
+// GRL:46-55): >= 0 is the namespace's limiter key.
+constexpr int32_t ROUTE_TOO_MANY = -1;   // namespace == null -> TOO_MANY_REQUEST (GRL:47-49)
+constexpr int32_t ROUTE_PLAIN = -2;      // no limiter for the namespace (GRL:51-53)
 
 // JLS 5.1.3 double -> int: NaN -> 0, saturating.
 __host__ __device__ inline int32_t java_d2i(double d) {
@@ -48,6 +54,46 @@ __device__ inline int64_t epoch_of(int64_t t, int32_t w, double rcp_w) {
     if (r < 0) e -= 1;
     else if (r >= (int64_t)w) e += 1;
     return e;
+}
+
+// 64-bit finaliser (murmur3 fmix64): open-addressing slots and count-min columns.
+__host__ __device__ inline uint64_t mix64(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+    return x;
+}
+
+// JLS 5.1.3 double -> long: NaN -> 0, saturating.
+__host__ __device__ inline int64_t java_d2l(double d) {
+    if (d != d) return 0;
+    if (d >= 9223372036854775807.0) return INT64_MAX;
+    if (d <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)d;
+}
+
+constexpr uint64_t PKEY_EMPTY = 0xFFFFFFFFFFFFFFFFull;   // reserved param key (empty table slot)
+
+// Find or insert `key` in an open-addressing table of 2^k slots; returns the slot or -1 (full).
+__device__ inline int64_t slot_insert(unsigned long long *table, uint64_t mask, uint64_t key) {
+    uint64_t h = mix64(key) & mask;
+    for (uint64_t probes = 0; probes <= mask; ++probes) {
+        const unsigned long long prev = atomicCAS(&table[h], (unsigned long long)PKEY_EMPTY, (unsigned long long)key);
+        if (prev == PKEY_EMPTY || prev == key) return (int64_t)h;
+        h = (h + 1) & mask;
+    }
+    return -1;
+}
+
+// Read-only lookup; returns the slot or -1.
+__device__ inline int64_t slot_find(const unsigned long long *table, uint64_t mask, uint64_t key) {
+    if (!table) return -1;
+    uint64_t h = mix64(key) & mask;
+    for (uint64_t probes = 0; probes <= mask; ++probes) {
+        const unsigned long long x = table[h];
+        if (x == PKEY_EMPTY) return -1;
+        if (x == key) return (int64_t)h;
+        h = (h + 1) & mask;
+    }
+    return -1;
 }
 
 __device__ inline uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }

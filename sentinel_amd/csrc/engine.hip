@@ -29,6 +29,7 @@
 #include "../../include/sentinel_amd.h"
 #include "admission.hpp"
 #include "common.hpp"
+#include "param_rules.hpp"
 #include "scan_sort.hpp"
 
 using namespace sentinel;
@@ -97,15 +98,7 @@ struct TableBufs {
     }
 };
 
-constexpr int32_t ROUTE_TOO_MANY = -1;   // CLUSTER rule whose namespace is null (GRL:47-49)
-constexpr int32_t ROUTE_PLAIN = -2;      // no limiter for the namespace (GRL:51-53)
 
-__device__ inline uint64_t mix64(uint64_t x) {
-    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
-    return x;
-}
-
-constexpr uint64_t PKEY_EMPTY = 0xFFFFFFFFFFFFFFFFull;
 
 // ------------------------------------------------------------------ prep kernels
 
@@ -186,16 +179,9 @@ __global__ __launch_bounds__(SORT_THREADS) void k_param_prep(
             if (r == ROUTE_TOO_MANY) st = ST_TOO_MANY_REQUEST;
             else if (e.ts < 0) st = ST_FAIL;
             else {
-                const unsigned long long key = (unsigned long long)e.key;
-                uint64_t h = mix64(key) & cap_mask;
-                uint64_t probes = 0;
-                for (;;) {
-                    const unsigned long long prev = atomicCAS(&table[h], (unsigned long long)PKEY_EMPTY, key);
-                    if (prev == PKEY_EMPTY || prev == key) break;
-                    h = (h + 1) & cap_mask;
-                    if (++probes > cap_mask) { st = ST_FAIL; break; }    // table full
-                }
-                if (st == 127) {
+                const int64_t h = slot_insert(table, cap_mask, e.key);
+                if (h < 0) st = ST_FAIL;                                   // table full
+                else {
                     k = (uint32_t)h;
                     slot_rule[h] = e.idx;    // identical value from every writer of this slot
                     if (r >= 0) l = (uint32_t)r;
@@ -232,16 +218,8 @@ __global__ __launch_bounds__(256) void k_param_meta(int64_t n, const uint32_t *_
     if (s == finvalid) return;
     const int32_t r = slot_rule[s];
     double thr = rule_thr[r];
-    if (hot_table) {   // ClusterParamFlowChecker.getRawThreshold (CPFC:113-120)
-        const unsigned long long key = (unsigned long long)ev[i].key;
-        uint64_t h = mix64(key) & hot_mask;
-        for (uint64_t p = 0; p <= hot_mask; ++p) {
-            const unsigned long long x = hot_table[h];
-            if (x == PKEY_EMPTY) break;
-            if (x == key) { thr = hot_thr[h]; break; }
-            h = (h + 1) & hot_mask;
-        }
-    }
+    const int64_t h = slot_find(hot_table, hot_mask, ev[i].key);   // ClusterParamFlowChecker.getRawThreshold (CPFC:113-120)
+    if (h >= 0) thr = hot_thr[h];
     slot_n[s] = rule_n[r];
     slot_w[s] = rule_w[r];
     slot_rcp[s] = rule_rcp[r];
@@ -324,6 +302,19 @@ struct sentinel_engine {
     int32_t pmax_n = 1;
     uint64_t hot_mask = 0;
     bool has_hot = false;
+    DevBuf d_prule_kind;               // KIND_PARAM per rule (segment kernel of the per-rule path)
+    int32_t pmode = SENTINEL_PARAM_EXACT;
+    int32_t cm_depth = 4;
+    uint32_t cm_width = 1024;
+    DevBuf d_cm;                       // count-min cells (SENTINEL_PARAM_COUNT_MIN)
+
+    // local param rules (ParamFlowChecker.passLocalCheck); rule index = load position
+    int32_t nlrules = 0;
+    DevBuf d_lrule_valid, d_lrule_tok, d_lrule_burst, d_lrule_dur, d_lrule_w, d_lrule_rcp, d_lrule_kind;
+    DevBuf d_lhot_keys, d_lhot_tok, d_ltable, d_lstate;
+    uint64_t lhot_mask = 0;
+    bool lhas_hot = false;
+    uint64_t lcap = (uint64_t)1 << 22;
 
     // per-kernel profiling (HIP events on the launch stream)
     struct ProfRec { const char *name; hipEvent_t a, b; int64_t units; };
@@ -369,7 +360,8 @@ struct sentinel_engine {
     // batch workspace
     DevBuf w_fkey, w_lkey, w_skey, w_sval, w_ktmp, w_vtmp, w_fhist, w_lhist, w_parts, w_segid, w_bad, w_hep,
         w_hacq, w_segstart, w_segkey, w_segep, w_segacq, w_het, w_done, w_s0, w_k, w_counters;
-    DevBuf io_ev, io_fl, io_out;
+    DevBuf w_vslot;                    // slot of every value of a param batch
+    DevBuf io_ev, io_fl, io_out, io_vals;
     int64_t ws_cap = 0;
 
     int ensure_ws(int64_t n) {
@@ -427,6 +419,44 @@ struct sentinel_engine {
         T.ncounters = ncounters;
         T.max_occupy_ratio = cfg.max_occupy_ratio;
         return T;
+    }
+
+    // Rule tables read by the segment kernel of the per-rule param path.
+    KeyTable param_rule_table() {
+        KeyTable T{};
+        T.n = d_prule_n.as<int32_t>();
+        T.w = d_prule_w.as<int32_t>();
+        T.rcp_w = d_prule_rcp.as<double>();
+        T.I_s = d_prule_Is.as<double>();
+        T.thr = d_prule_thr.as<double>();
+        T.kind = d_prule_kind.as<uint8_t>();
+        T.ncounters = 1;
+        return T;
+    }
+    KeyTable local_rule_table() {
+        KeyTable T{};
+        T.w = d_lrule_w.as<int32_t>();
+        T.rcp_w = d_lrule_rcp.as<double>();
+        T.kind = d_lrule_kind.as<uint8_t>();
+        T.ncounters = 1;
+        return T;
+    }
+    ParamCtx param_ctx() {
+        ParamCtx C{};
+        C.R = ParamRules{d_prule_n.as<int32_t>(), d_prule_w.as<int32_t>(), d_prule_rcp.as<double>(),
+                         d_prule_Is.as<double>(), d_prule_thr.as<double>(),
+                         has_hot ? d_hot_table.as<unsigned long long>() : nullptr, hot_mask, d_hot_thr.as<double>()};
+        C.PT = table(pt, 1, header_words(pmax_n));
+        C.CM = CountMin{d_cm.as<uint64_t>(), cm_depth, cm_width, pmax_n};
+        C.L = LocalRules{d_lrule_valid.as<uint8_t>(), d_lrule_tok.as<int64_t>(), d_lrule_burst.as<int64_t>(),
+                         d_lrule_dur.as<int64_t>(), lhas_hot ? d_lhot_keys.as<unsigned long long>() : nullptr,
+                         lhot_mask, d_lhot_tok.as<int64_t>(), d_lstate.as<int64_t>()};
+        C.vslot = w_vslot.as<uint32_t>();
+        return C;
+    }
+    SlotMeta slot_meta() {
+        return SlotMeta{pt.n.as<int32_t>(), pt.w.as<int32_t>(), pt.rcp.as<double>(), pt.Is.as<double>(),
+                        pt.thr.as<double>(), pt.kind.as<uint8_t>()};
     }
 
     void scan(uint32_t *buf, int64_t n, bool exclusive, hipStream_t s) {
@@ -500,9 +530,9 @@ struct sentinel_engine {
         });
     }
 
-    // The generic pipeline: sort by key, segment, decide, scatter.
-    void run_pipeline(const KeyTable &T, const uint32_t *keys, uint32_t *hist, int64_t n, int bits,
-                      const EventSrc &src, const Verdicts &V, hipStream_t s, int max_n, bool limiter) {
+    // K2 sort by key + (key, epoch) segment records (W.seg_*).
+    void sort_segments(const KeyTable &T, const uint32_t *keys, uint32_t *hist, int64_t n, int bits,
+                       const EventSrc &src, hipStream_t s) {
         BatchWork W = work();
         const uint32_t invalid = ((uint32_t)1 << bits) - 1;
         sort(keys, n, bits, hist, src, s);
@@ -521,6 +551,14 @@ struct sentinel_engine {
             scan(W.segid, n, false, s);
             launch("seg_mark", n, s, [&] { k_seg_mark<<<g, 256, 0, s>>>(W, n); });
         }
+    }
+
+    // The generic pipeline: sort by key, segment, decide, scatter.
+    void run_pipeline(const KeyTable &T, const uint32_t *keys, uint32_t *hist, int64_t n, int bits,
+                      const EventSrc &src, const Verdicts &V, hipStream_t s, int max_n, bool limiter) {
+        sort_segments(T, keys, hist, n, bits, src, s);
+        BatchWork W = work();
+        const unsigned g = grid_for(n);
         if (max_n <= PROC_G * PROC_SLOTS_PER_LANE && process_impl == 1)
             launch("process", n, s, [&] {
                 k_process_grp<<<std::min<unsigned>(grid_for(n * PROC_G), 8192), 256, 0, s>>>(T, W, src, V, n);
@@ -544,7 +582,34 @@ struct sentinel_engine {
     int rebuild_flow_thresholds();
     int rebuild_limiters();
     int rebuild_routes();
+    int clear_param_slots();
+    int rebuild_cm();
 };
+
+// Exact param counters restart: every slot free, every window absent (stream synchronised).
+int sentinel_engine::clear_param_slots() {
+    if (!d_ptable.p) return 0;
+    const uint64_t P = pcap;
+    const int64_t stride = header_words(pmax_n);
+    HIP_OK(hipMemsetAsync(d_ptable.p, 0xFF, P * 8, stream));
+    k_init_state<<<grid_for((int64_t)P), 256, 0, stream>>>(pt.state.as<int64_t>(), nullptr, stride, nullptr, pmax_n,
+                                                           stride, (int64_t)P);
+    HIP_OK(hipStreamSynchronize(stream));
+    return 0;
+}
+
+// Count-min cells for every param rule, zeroed (count 0 = nothing counted).
+int sentinel_engine::rebuild_cm() {
+    if (pmode != SENTINEL_PARAM_COUNT_MIN) return 0;
+    const size_t R = std::max<size_t>(prules.size(), 1);
+    const size_t bytes = R * (size_t)cm_depth * (size_t)cm_width * (size_t)pmax_n * 8;
+    if (bytes > ((size_t)96 << 30)) return fail(SENTINEL_E_NOMEM, "count-min sketch would exceed 96 GiB");
+    int rc = d_cm.ensure(bytes);
+    if (rc) return rc;
+    HIP_OK(hipMemsetAsync(d_cm.p, 0, bytes, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    return 0;
+}
 
 // Host mirror of ClusterFlowChecker.calcGlobalThreshold * exceedCount (CFC:38-48, 68) and
 // SimpleClusterFlowChecker (SCFC:42), evaluated in double exactly as Java does.
@@ -669,7 +734,11 @@ static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const u
     return 0;
 }
 
+static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamEvent *pev, const MultiEvent *mev,
+                         const uint64_t *values, int64_t n_values, uint64_t *out, hipStream_t s);
+
 static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, uint64_t *out, hipStream_t s) {
+    if (e->pmode == SENTINEL_PARAM_COUNT_MIN) return submit_prules(e, PMODE_CM, n, ev, nullptr, nullptr, 0, out, s);
     if (n <= 0) return 0;
     if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
     int rc = e->ensure_ws(n);
@@ -720,9 +789,91 @@ static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, u
     return 0;
 }
 
-static uint64_t host_mix64(uint64_t x) {
-    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
-    return x;
+// Hot-parameter requests decided per rule (param_rules.hpp): multi-value cluster requests (exact or
+// count-min counters) and the local token bucket.  Events are single-value (pev) or multi-value
+// (mev + values[0, n_values)).
+static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamEvent *pev, const MultiEvent *mev,
+                         const uint64_t *values, int64_t n_values, uint64_t *out, hipStream_t s) {
+    if (n <= 0) return 0;
+    if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
+    int rc = e->ensure_ws(n);
+    if (rc) return rc;
+    const bool local = mode == PMODE_LOCAL;
+    const int64_t nv = pev ? n : n_values;
+    if (nv > ((int64_t)1 << 31) - 1) return fail(SENTINEL_E_INVALID, "too many values (max 2^31 - 1)");
+    rc = e->w_vslot.ensure((size_t)std::max<int64_t>(nv, 1) * 4);
+    if (rc) return rc;
+    const int32_t R = local ? e->nlrules : (int32_t)e->prules.size();
+    const int rbits = bits_for(R);
+    const uint32_t rinvalid = ((uint32_t)1 << rbits) - 1;
+    const bool lim = !local && e->nlimiters > 0 && !e->param_plain && R > 0;
+    const int lbits = bits_for(e->nlimiters);
+    const uint32_t linvalid = ((uint32_t)1 << lbits) - 1;
+    uint32_t *fkey = e->w_fkey.as<uint32_t>();
+    uint32_t *lkey = lim ? e->w_lkey.as<uint32_t>() : nullptr;
+    const int64_t nb = sort_blocks(n);
+    const ParamEvent *evp = pev ? pev : (const ParamEvent *)mev;
+    const ValueSrc vs{pev, mev, values, nv};
+    const ParamCtx C = e->param_ctx();
+    unsigned long long *table = nullptr;
+    uint64_t mask = 0;
+    if (mode == PMODE_EXACT && R > 0) { table = e->d_ptable.as<unsigned long long>(); mask = e->pcap - 1; }
+    if (local && R > 0) { table = e->d_ltable.as<unsigned long long>(); mask = e->lcap - 1; }
+    HIP_OK(hipMemsetAsync(e->w_counters.p, 0, 16, s));
+    e->launch("prule_prep", n, s, [&] {
+        if (local)
+            k_prule_prep<true><<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
+                n, evp, vs, R, e->d_lrule_valid.as<uint8_t>(), nullptr, C.R, table, mask, SlotMeta{}, e->w_vslot.as<uint32_t>(), out,
+                fkey, rinvalid, e->w_fhist.as<uint32_t>(), nullptr, linvalid, e->w_lhist.as<uint32_t>(), nb);
+        else
+            k_prule_prep<false><<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
+                n, evp, vs, R, nullptr, e->param_plain ? nullptr : e->d_prule_route.as<int32_t>(), C.R, table, mask,
+                e->slot_meta(), e->w_vslot.as<uint32_t>(), out, fkey, rinvalid, e->w_fhist.as<uint32_t>(), lkey, linvalid,
+                e->w_lhist.as<uint32_t>(), nb);
+    });
+    if (R == 0) {
+        HIP_OK(hipGetLastError());
+        return 0;
+    }
+    if (lim) {   // ClusterParamFlowChecker.allowProceed: one limiter pass per request (CPFC:45-47)
+        Verdicts V{out, fkey, rinvalid};
+        KeyTable LT = e->table(e->lt, 1, e->lim_stride);
+        EventSrc lsrc{nullptr, evp, nullptr, true};
+        e->run_pipeline(LT, lkey, e->w_lhist.as<uint32_t>(), n, lbits, lsrc, V, s, 10, true);
+        e->hist_pass0(fkey, n, e->w_fhist.as<uint32_t>(), s);
+    }
+    const KeyTable RT = local ? e->local_rule_table() : e->param_rule_table();
+    const EventSrc src{nullptr, evp, nullptr, false};
+    e->sort_segments(RT, fkey, e->w_fhist.as<uint32_t>(), n, rbits, src, s);
+    const BatchWork W = e->work();
+    const unsigned g = grid_for(n);
+    e->launch("prule_process", n, s, [&] {
+        if (mode == PMODE_LOCAL) k_prule_process<PMODE_LOCAL><<<g, 256, 0, s>>>(C, W, evp, vs, out, n);
+        else if (mode == PMODE_CM) k_prule_process<PMODE_CM><<<g, 256, 0, s>>>(C, W, evp, vs, out, n);
+        else k_prule_process<PMODE_EXACT><<<g, 256, 0, s>>>(C, W, evp, vs, out, n);
+    });
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+// Host-pointer variant of the per-rule param path: H2D, decide, D2H, synchronous.
+static int submit_prules_host(sentinel_engine_t *e, int mode, int64_t n, const sentinel_param_multi_event_t *ev,
+                              const uint64_t *values, int64_t n_values, sentinel_verdict_t *out) {
+    if (n == 0) return 0;
+    hipStream_t s = e->stream;
+    int rc = 0;
+    rc |= e->io_ev.ensure(n * sizeof(MultiEvent));
+    rc |= e->io_vals.ensure(std::max<int64_t>(n_values, 1) * 8);
+    rc |= e->io_out.ensure(n * 8);
+    if (rc) return SENTINEL_E_NOMEM;
+    HIP_OK(hipMemcpyAsync(e->io_ev.p, ev, n * sizeof(MultiEvent), hipMemcpyHostToDevice, s));
+    if (n_values > 0) HIP_OK(hipMemcpyAsync(e->io_vals.p, values, n_values * 8, hipMemcpyHostToDevice, s));
+    rc = submit_prules(e, mode, n, nullptr, e->io_ev.as<MultiEvent>(), e->io_vals.as<uint64_t>(), n_values,
+                       e->io_out.as<uint64_t>(), s);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 8, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    return 0;
 }
 
 static bool valid_window(int32_t n, int32_t interval) {  // FlowRuleUtil.isWindowConfigValid (FlowRuleUtil.java:229-231)
@@ -793,7 +944,10 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
                       &e->d_hot_table, &e->d_hot_thr, &e->w_fkey, &e->w_lkey, &e->w_skey, &e->w_sval, &e->w_ktmp,
                       &e->w_vtmp, &e->w_fhist, &e->w_lhist, &e->w_parts, &e->w_segid, &e->w_bad, &e->w_hep,
                       &e->w_hacq, &e->w_segstart, &e->w_segkey, &e->w_segep, &e->w_segacq, &e->w_het, &e->w_done,
-                      &e->w_s0, &e->w_k, &e->w_counters, &e->io_ev, &e->io_fl, &e->io_out})
+                      &e->w_s0, &e->w_k, &e->w_counters, &e->io_ev, &e->io_fl, &e->io_out, &e->io_vals, &e->w_vslot,
+                      &e->d_prule_kind, &e->d_cm, &e->d_lrule_valid, &e->d_lrule_tok, &e->d_lrule_burst,
+                      &e->d_lrule_dur, &e->d_lrule_w, &e->d_lrule_rcp, &e->d_lrule_kind, &e->d_lhot_keys,
+                      &e->d_lhot_tok, &e->d_ltable, &e->d_lstate})
         b->release();
     (void)hipStreamDestroy(e->stream);
     delete e;
@@ -1021,7 +1175,7 @@ int sentinel_load_param_rules(sentinel_engine_t *e, const sentinel_param_rule_t 
     std::vector<uint64_t> hk(hcap, PKEY_EMPTY);
     std::vector<double> hv(hcap, 0.0);
     for (auto &kv : hot) {
-        uint64_t h = host_mix64(kv.first) & (hcap - 1);
+        uint64_t h = mix64(kv.first) & (hcap - 1);
         while (hk[h] != PKEY_EMPTY && hk[h] != kv.first) h = (h + 1) & (hcap - 1);
         hk[h] = kv.first;
         hv[h] = kv.second;
@@ -1043,10 +1197,12 @@ int sentinel_load_param_rules(sentinel_engine_t *e, const sentinel_param_rule_t 
     const int64_t stride = header_words(maxn);
     rc |= e->pt.state.ensure(P * stride * 8);
     if (rc) return SENTINEL_E_NOMEM;
-    HIP_OK(hipMemsetAsync(e->d_ptable.p, 0xFF, P * 8, e->stream));
-    k_init_state<<<grid_for((int64_t)P), 256, 0, e->stream>>>(e->pt.state.as<int64_t>(), nullptr, stride, nullptr, maxn,
-                                                              stride, (int64_t)P);
-    HIP_OK(hipStreamSynchronize(e->stream));
+    rc = upload(e->d_prule_kind, std::vector<uint8_t>(nn.size(), KIND_PARAM));
+    if (rc) return rc;
+    rc = e->clear_param_slots();
+    if (rc) return rc;
+    rc = e->rebuild_cm();
+    if (rc) return rc;
     return e->rebuild_routes();
 }
 
@@ -1104,6 +1260,154 @@ int sentinel_submit_param_batch_host(sentinel_engine_t *e, int64_t n, const sent
     HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     return 0;
+}
+
+int sentinel_submit_param_multi_batch(sentinel_engine_t *e, int64_t n, const sentinel_param_multi_event_t *ev,
+                                      const uint64_t *values, int64_t n_values, sentinel_verdict_t *out, void *stream) {
+    if (!e || n < 0 || n_values < 0 || (n > 0 && (!ev || !out)) || (n_values > 0 && !values))
+        return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    return submit_prules(e, e->pmode == SENTINEL_PARAM_COUNT_MIN ? PMODE_CM : PMODE_EXACT, n, nullptr,
+                         (const MultiEvent *)ev, values, n_values, (uint64_t *)out, stream ? (hipStream_t)stream : e->stream);
+}
+
+int sentinel_submit_param_multi_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_param_multi_event_t *ev,
+                                           const uint64_t *values, int64_t n_values, sentinel_verdict_t *out) {
+    if (!e || n < 0 || n_values < 0 || (n > 0 && (!ev || !out)) || (n_values > 0 && !values))
+        return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    return submit_prules_host(e, e->pmode == SENTINEL_PARAM_COUNT_MIN ? PMODE_CM : PMODE_EXACT, n, ev, values,
+                              n_values, out);
+}
+
+int sentinel_set_param_mode(sentinel_engine_t *e, int32_t mode, int32_t depth, int32_t width) {
+    if (!e || (mode != SENTINEL_PARAM_EXACT && mode != SENTINEL_PARAM_COUNT_MIN)) return fail(SENTINEL_E_INVALID, "bad param mode");
+    if (mode == SENTINEL_PARAM_COUNT_MIN && (depth < 1 || depth > 16 || width < 16 || (width & (width - 1)) != 0))
+        return fail(SENTINEL_E_INVALID, "count-min needs 1 <= depth <= 16 and a power-of-two width >= 16");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    e->pmode = mode;
+    if (mode == SENTINEL_PARAM_COUNT_MIN) {
+        e->cm_depth = depth;
+        e->cm_width = (uint32_t)width;
+    }
+    int rc = e->clear_param_slots();
+    if (rc) return rc;
+    return e->rebuild_cm();
+}
+
+int sentinel_load_local_param_rules(sentinel_engine_t *e, const sentinel_local_param_rule_t *rules, int32_t n,
+                                    const uint64_t *hot_keys, const int32_t *hot_counts, int32_t n_hot) {
+    if (!e || n < 0 || (n > 0 && !rules) || n_hot < 0 || (n_hot > 0 && (!hot_keys || !hot_counts)))
+        return fail(SENTINEL_E_INVALID, "bad local param rules");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    const size_t N = (size_t)std::max(n, 1);
+    std::vector<uint8_t> valid(N, 0), kind(N, KIND_LOCAL_PARAM);
+    std::vector<int64_t> tok(N, 0), burst(N, 0), dur(N, 1);
+    std::vector<int32_t> w(N, 1 << 30);
+    std::vector<double> rcp(N, 1.0 / (double)(1 << 30));
+    std::vector<std::pair<uint64_t, int64_t>> hot;
+    for (int32_t i = 0; i < n; ++i) {
+        const sentinel_local_param_rule_t &r = rules[i];
+        // ParamFlowRuleUtil.isValidRule (ParamFlowRuleUtil.java:46-52): count >= 0, burstCount >= 0,
+        // durationInSec > 0 (QPS grade, default control behaviour)
+        if (!(r.count >= 0) || r.burst_count < 0 || r.duration_in_sec <= 0) continue;
+        valid[i] = 1;
+        tok[i] = java_d2l(r.count);                          // (long) rule.getCount()  (PFC:139)
+        burst[i] = r.burst_count;
+        dur[i] = wrap_mul(r.duration_in_sec, 1000);          // rule.getDurationInSec() * 1000
+        for (int32_t h = 0; h < r.hot_n; ++h) {
+            const int32_t j = r.hot_begin + h;
+            if (j < 0 || j >= n_hot) return fail(SENTINEL_E_INVALID, "hot item range out of bounds");
+            hot.emplace_back(hot_keys[j], (int64_t)hot_counts[j]);
+        }
+    }
+    uint64_t hcap = 16;
+    while (hcap < 2 * hot.size() + 2) hcap <<= 1;
+    std::vector<uint64_t> hk(hcap, PKEY_EMPTY);
+    std::vector<int64_t> hv(hcap, 0);
+    for (auto &kv : hot) {
+        uint64_t h = mix64(kv.first) & (hcap - 1);
+        while (hk[h] != PKEY_EMPTY && hk[h] != kv.first) h = (h + 1) & (hcap - 1);
+        hk[h] = kv.first;
+        hv[h] = kv.second;
+    }
+    int rc = 0;
+    rc |= upload(e->d_lrule_valid, valid);
+    rc |= upload(e->d_lrule_tok, tok);
+    rc |= upload(e->d_lrule_burst, burst);
+    rc |= upload(e->d_lrule_dur, dur);
+    rc |= upload(e->d_lrule_w, w);
+    rc |= upload(e->d_lrule_rcp, rcp);
+    rc |= upload(e->d_lrule_kind, kind);
+    rc |= upload(e->d_lhot_keys, hk);
+    rc |= upload(e->d_lhot_tok, hv);
+    if (const char *c = getenv("SENTINEL_LOCAL_PARAM_CAPACITY")) {
+        uint64_t v = strtoull(c, nullptr, 10), p = 1024;
+        while (p < v) p <<= 1;
+        e->lcap = p;
+    }
+    rc |= e->d_ltable.ensure(e->lcap * 8);
+    rc |= e->d_lstate.ensure(e->lcap * 16);
+    if (rc) return rc < 0 ? rc : SENTINEL_E_NOMEM;
+    e->lhot_mask = hcap - 1;
+    e->lhas_hot = !hot.empty();
+    // ParameterMetric token/time counters restart with the rules (every slot free, every bucket absent)
+    HIP_OK(hipMemsetAsync(e->d_ltable.p, 0xFF, e->lcap * 8, e->stream));
+    k_fill_i64<<<grid_for((int64_t)(2 * e->lcap)), 256, 0, e->stream>>>(e->d_lstate.as<int64_t>(), (int64_t)(2 * e->lcap),
+                                                                       LOCAL_ABSENT);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(e->stream));
+    e->nlrules = n;
+    return 0;
+}
+
+int sentinel_submit_local_param_batch(sentinel_engine_t *e, int64_t n, const sentinel_param_multi_event_t *ev,
+                                      const uint64_t *values, int64_t n_values, sentinel_verdict_t *out, void *stream) {
+    if (!e || n < 0 || n_values < 0 || (n > 0 && (!ev || !out)) || (n_values > 0 && !values))
+        return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    return submit_prules(e, PMODE_LOCAL, n, nullptr, (const MultiEvent *)ev, values, n_values, (uint64_t *)out,
+                         stream ? (hipStream_t)stream : e->stream);
+}
+
+int sentinel_submit_local_param_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_param_multi_event_t *ev,
+                                           const uint64_t *values, int64_t n_values, sentinel_verdict_t *out) {
+    if (!e || n < 0 || n_values < 0 || (n > 0 && (!ev || !out)) || (n_values > 0 && !values))
+        return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    return submit_prules_host(e, PMODE_LOCAL, n, ev, values, n_values, out);
+}
+
+int sentinel_local_param_state(sentinel_engine_t *e, uint64_t key, int64_t *last_add_ms, int64_t *tokens) {
+    if (!e || !last_add_ms || !tokens) return fail(SENTINEL_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(e->mu);
+    *last_add_ms = -1;
+    *tokens = -1;
+    if (!e->d_ltable.p) return 0;
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    std::vector<uint64_t> table(e->lcap);
+    HIP_OK(hipMemcpy(table.data(), e->d_ltable.p, e->lcap * 8, hipMemcpyDeviceToHost));
+    uint64_t h = mix64(key) & (e->lcap - 1);
+    for (uint64_t p = 0; p < e->lcap; ++p) {
+        if (table[h] == PKEY_EMPTY) return 0;
+        if (table[h] == key) break;
+        h = (h + 1) & (e->lcap - 1);
+    }
+    if (table[h] != key) return 0;
+    int64_t st[2];
+    HIP_OK(hipMemcpy(st, e->d_lstate.as<int64_t>() + 2 * h, 16, hipMemcpyDeviceToHost));
+    *last_add_ms = st[0] == LOCAL_ABSENT ? -1 : st[0];
+    *tokens = st[1] == LOCAL_ABSENT ? -1 : st[1];
+    return 1;
 }
 
 int sentinel_request_token(sentinel_engine_t *e, int64_t flow_id, int32_t acquire, int32_t prio, int64_t ts,
@@ -1186,10 +1490,24 @@ int sentinel_param_sum(sentinel_engine_t *e, int32_t ridx, uint64_t pkey, int64_
     HIP_OK(hipSetDevice(e->device));
     HIP_OK(hipStreamSynchronize(e->stream));
     *out = 0;
+    if (e->pmode == SENTINEL_PARAM_COUNT_MIN) {   // the sketch estimate (min over rows of the window sum)
+        const sentinel_param_rule_t &r = e->prules[ridx];
+        const int n = r.sample_count;
+        const int64_t E = ts / (r.window_interval_ms / n);
+        const CountMin C{e->d_cm.as<uint64_t>(), e->cm_depth, e->cm_width, e->pmax_n};
+        int64_t est = INT64_MAX;
+        std::vector<uint64_t> cell(e->pmax_n);
+        for (int d = 0; d < e->cm_depth; ++d) {
+            HIP_OK(hipMemcpy(cell.data(), cm_cell(C, (uint32_t)ridx, d, pkey), cell.size() * 8, hipMemcpyDeviceToHost));
+            est = std::min(est, cm_cell_sum(cell.data(), n, E));
+        }
+        *out = est;
+        return 0;
+    }
     const uint64_t P = e->pcap;
     std::vector<uint64_t> table(P);
     HIP_OK(hipMemcpy(table.data(), e->d_ptable.p, P * 8, hipMemcpyDeviceToHost));
-    uint64_t h = host_mix64(pkey) & (P - 1);
+    uint64_t h = mix64(pkey) & (P - 1);
     for (uint64_t p = 0; p < P; ++p) {
         if (table[h] == PKEY_EMPTY) return 0;
         if (table[h] == pkey) break;

@@ -1,0 +1,363 @@
+// param_rules.hpp -- hot-parameter requests decided one rule at a time (gfx950).
+//
+// Three checkers share one pipeline: events are grouped by rule (K2 radix sort, arrival order
+// kept), and one lane walks each rule's events in order:
+//
+//   PMODE_EXACT  ClusterParamFlowChecker.acquireClusterToken over any number of values
+//                (srv/flow/ClusterParamFlowChecker.java:42-87): every value is checked in order,
+//                the first negative remaining blocks the request with no counter touched, else
+//                every value's window counter is incremented (duplicates twice).  Per-value
+//                state is the exact open-addressing slot of admission.hpp (KIND_PARAM keys).
+//   PMODE_CM     the same checker over a count-min sketch of window counters (opt-in): every
+//                rule owns depth x width cells of n slots {tag = epoch mod 2^24, count}; the
+//                estimate is the minimum over rows of the cell's window sum, so it never
+//                undercounts the value's own passes (the sketch only adds) and a request can be
+//                blocked that exact counters would pass, never the reverse.
+//   PMODE_LOCAL  ParamFlowChecker.passLocalCheck / passDefaultLocalCheck
+//                (pfc/slots/block/flow/param/ParamFlowChecker.java:78-202): a token bucket
+//                {lastAddTokenTime, tokens} per (rule, value), every element of a collection
+//                must pass, earlier elements keep their consumed tokens.
+//
+// A value list couples several counters of one rule, so a rule's events cannot be split into
+// independent per-key segments: the per-rule lane is the "wave-per-segment fallback" of the
+// north star applied at rule granularity.  Single-value cluster requests in exact mode keep the
+// closed-form per-key path of admission.hpp.
+#pragma once
+
+#include "admission.hpp"
+
+namespace sentinel {
+
+// sentinel_param_multi_event_t.  Its first 16 bytes are those of Event / ParamEvent, so the sort,
+// segment and limiter kernels read it through a ParamEvent pointer.
+struct MultiEvent {
+    int32_t idx;
+    int32_t acquire;
+    int64_t ts;
+    int32_t begin;
+    int32_t count;
+};
+static_assert(sizeof(MultiEvent) == sizeof(ParamEvent), "multi events share the ParamEvent stride");
+
+// Value list of event s: single-value events carry their value (param key) in the event.
+struct ValueSrc {
+    const ParamEvent *pev;
+    const MultiEvent *mev;
+    const uint64_t *values;
+    int64_t n_values;
+    __device__ inline int32_t begin(uint32_t s) const { return pev ? (int32_t)s : mev[s].begin; }
+    __device__ inline int32_t count(uint32_t s) const { return pev ? 1 : mev[s].count; }
+    __device__ inline uint64_t value(int64_t j) const { return pev ? pev[j].key : values[j]; }
+};
+
+// Cluster param rule table (dense rule index) + hot items keyed by param key.
+struct ParamRules {
+    const int32_t *n;
+    const int32_t *w;
+    const double *rcp_w;
+    const double *I_s;
+    const double *thr;                    // count, x connectedCount for AVG_LOCAL (CPFC:101-111)
+    const unsigned long long *hot_keys;   // null: no hot items
+    uint64_t hot_mask;
+    const double *hot_thr;
+};
+
+// Per-slot window parameters written by the prep kernel (exact mode).
+struct SlotMeta {
+    int32_t *n;
+    int32_t *w;
+    double *rcp;
+    double *Is;
+    double *thr;
+    uint8_t *kind;
+};
+
+// Count-min sketch: rule-major [rule][depth][width][nmax] packed cells.
+struct CountMin {
+    uint64_t *cells;
+    int32_t depth;
+    uint32_t width;       // power of two
+    int32_t nmax;
+};
+
+constexpr int64_t LOCAL_ABSENT = INT64_MIN;   // CacheMap entry absent
+
+// Local param rules (position = rule index) + hot items + token-bucket state per slot.
+struct LocalRules {
+    const uint8_t *valid;
+    const int64_t *tokens;    // (long) rule.count  (PFC:139)
+    const int64_t *burst;     // rule.burstCount    (PFC:148)
+    const int64_t *dur_ms;    // rule.durationInSec * 1000 (PFC:166)
+    const unsigned long long *hot_keys;
+    uint64_t hot_mask;
+    const int64_t *hot_tokens;
+    int64_t *state;           // per slot {lastAddTokenTime, tokens}
+};
+
+struct ParamCtx {
+    ParamRules R;
+    KeyTable PT;              // exact-mode slot state
+    CountMin CM;
+    LocalRules L;
+    const uint32_t *vslot;    // slot of each value (exact / local)
+};
+
+constexpr int PMODE_EXACT = 0;
+constexpr int PMODE_CM = 1;
+constexpr int PMODE_LOCAL = 2;
+
+// ClusterParamFlowChecker.getRawThreshold (CPFC:113-120): hot-item count, else rule count.
+__device__ inline double value_threshold(const ParamRules &R, uint32_t rule, uint64_t key) {
+    const int64_t h = slot_find(R.hot_keys, R.hot_mask, key);
+    return h >= 0 ? R.hot_thr[h] : R.thr[rule];
+}
+
+// ------------------------------------------------------------------ prep
+
+// Validation + routing of single- or multi-value events, slot of every value, sort keys (rule
+// index) and the pass-0 digit histograms.  Cluster: DefaultTokenService.requestParamToken
+// (DTS:51-62: null id, acquire <= 0, empty params -> BAD_REQUEST; unknown rule -> NO_RULE_EXISTS)
+// and ClusterParamFlowChecker.allowProceed (CPFC:37-47).  Local: ParamFlowChecker.passCheck
+// reaches passLocalCheck with no request validation; an empty collection passes (PFC:81-102).
+template <bool LOCAL>
+__global__ __launch_bounds__(SORT_THREADS) void k_prule_prep(
+    int64_t n, const ParamEvent *__restrict__ ev, ValueSrc vs, int32_t nrules, const uint8_t *__restrict__ rule_valid,
+    const int32_t *__restrict__ route, ParamRules R, unsigned long long *table, uint64_t cap_mask, SlotMeta M,
+    uint32_t *__restrict__ vslot, uint64_t *__restrict__ out, uint32_t *__restrict__ fkey, uint32_t finvalid,
+    uint32_t *__restrict__ fhist, uint32_t *__restrict__ lkey, uint32_t linvalid, uint32_t *__restrict__ lhist,
+    int64_t nblocks) {
+    __shared__ uint32_t hf[MAX_PASSES][RADIX];
+    __shared__ uint32_t hl[MAX_PASSES][RADIX];
+    for (int d = threadIdx.x; d < MAX_PASSES * RADIX; d += SORT_THREADS) {
+        (&hf[0][0])[d] = 0;
+        (&hl[0][0])[d] = 0;
+    }
+    __syncthreads();
+    const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
+        if (i >= n) break;
+        const ParamEvent e = ev[i];
+        const int32_t cnt = vs.count((uint32_t)i);
+        const int32_t b = vs.begin((uint32_t)i);
+        const bool bad_range = cnt < 0 || b < 0 || (int64_t)b + cnt > vs.n_values;
+        int st = 127;
+        uint32_t l = linvalid;
+        if (LOCAL) {
+            if (bad_range) st = ST_BAD_REQUEST;
+            else if (e.idx < 0 || e.idx >= nrules || (rule_valid && !rule_valid[e.idx])) st = ST_NO_RULE_EXISTS;
+            else if (cnt == 0) st = ST_OK;
+        } else {
+            if (e.idx == SENTINEL_IDX_BAD_ID || e.acquire <= 0 || cnt <= 0) st = ST_BAD_REQUEST;
+            else if (bad_range) st = ST_BAD_REQUEST;
+            else if (e.idx < 0 || e.idx >= nrules) st = ST_NO_RULE_EXISTS;
+            else {
+                const int32_t r = route ? route[e.idx] : ROUTE_PLAIN;
+                if (r == ROUTE_TOO_MANY) st = ST_TOO_MANY_REQUEST;   // namespace == null
+                else if (e.ts < 0) st = ST_FAIL;                       // reference: NPE in LeapArray
+                else if (r >= 0) l = (uint32_t)r;
+            }
+        }
+        if (st == 127 && table) {
+            for (int32_t q = 0; q < cnt; ++q) {
+                const uint64_t key = vs.value((int64_t)b + q);
+                const int64_t h = slot_insert(table, cap_mask, key);
+                if (h < 0) { st = ST_FAIL; break; }                    // table full
+                vslot[b + q] = (uint32_t)h;
+                if (!LOCAL) {   // identical values from every writer of this slot
+                    M.n[h] = R.n[e.idx];
+                    M.w[h] = R.w[e.idx];
+                    M.rcp[h] = R.rcp_w[e.idx];
+                    M.Is[h] = R.I_s[e.idx];
+                    M.thr[h] = value_threshold(R, (uint32_t)e.idx, key);
+                    M.kind[h] = KIND_PARAM;
+                }
+            }
+        }
+        const uint32_t k = st == 127 ? (uint32_t)e.idx : finvalid;
+        if (st != 127) l = linvalid;
+        fkey[i] = k;
+        tile_hist_accumulate(hf, k, 1);
+        if (lkey) {
+            lkey[i] = l;
+            tile_hist_accumulate(hl, l, 1);
+        }
+        if (st != 127) put_verdict(out, (uint32_t)i, st, 0, 0);
+    }
+    __syncthreads();
+    tile_hist_store(hf, fhist, 1, nblocks);
+    if (lkey) tile_hist_store(hl, lhist, 1, nblocks);
+}
+
+// ------------------------------------------------------------------ checkers
+
+// Exact counters: ClusterParamFlowChecker.acquireClusterToken (CPFC:58-86).  getAvg(value) rolls the
+// value's window first (ClusterParamMetric.java:46-82 -> LeapArray.currentWindow).
+__device__ inline uint64_t exact_check(const ParamCtx &C, int64_t E, int32_t a, int32_t b, int32_t cnt) {
+    double remaining = -1.0;
+    for (int32_t q = 0; q < cnt; ++q) {
+        const uint32_t s = C.vslot[b + q];
+        const KeyState ks = key_state(C.PT, s);
+        roll(C.PT, s, ks, E);
+        const int64_t sum = window_sum(ks, E, EV_PASS);
+        const double next = remaining_of(C.PT.thr[s], C.PT.I_s[s], sum, a);
+        remaining = next;
+        if (next < 0.0) return pack_verdict(ST_BLOCKED, 0, 0);    // CPFC:66-70, no counter touched
+    }
+    for (int32_t q = 0; q < cnt; ++q) {                            // CPFC:73-76
+        const uint32_t s = C.vslot[b + q];
+        const KeyState ks = key_state(C.PT, s);
+        add_counter(C.PT, s, ks, E, EV_PASS, a);
+    }
+    if (cnt > 1) remaining = -1.0;                                 // CPFC:81-84
+    return pack_verdict(ST_OK, java_d2i(remaining), 0);
+}
+
+// Count-min cells: {tag = epoch mod 2^24 : 24 | count : 40}.
+constexpr int CM_COUNT_BITS = 40;
+constexpr uint64_t CM_COUNT_MAX = (1ull << CM_COUNT_BITS) - 1;
+constexpr uint32_t CM_TAG_MASK = (1u << 24) - 1;
+
+__host__ __device__ inline uint64_t *cm_cell(const CountMin &C, uint32_t rule, int d, uint64_t key) {
+    const uint64_t col = mix64(key + 0x9E3779B97F4A7C15ull * (uint64_t)(d + 1)) & (uint64_t)(C.width - 1);
+    return C.cells + (((uint64_t)rule * (uint64_t)C.depth + (uint64_t)d) * C.width + col) * (uint64_t)C.nmax;
+}
+
+// Window sum of one cell at epoch E: slots tagged with one of the epochs (E-n, E] (a tag 2^24
+// epochs stale aliases into the window: it can only add, never remove, count).
+__host__ __device__ inline int64_t cm_cell_sum(const uint64_t *c, int nsc, int64_t E) {
+    int64_t s = 0;
+    for (int j = 0; j < nsc; ++j) {
+        const uint64_t x = c[j];
+        const uint32_t tag = (uint32_t)(x >> CM_COUNT_BITS);
+        if ((((uint32_t)E - tag) & CM_TAG_MASK) < (uint32_t)nsc) s += (int64_t)(x & CM_COUNT_MAX);
+    }
+    return s;
+}
+
+__device__ inline int64_t cm_estimate(const CountMin &C, uint32_t rule, uint64_t key, int nsc, int64_t E) {
+    int64_t est = INT64_MAX;
+    for (int d = 0; d < C.depth; ++d) {
+        const int64_t s = cm_cell_sum(cm_cell(C, rule, d, key), nsc, E);
+        est = s < est ? s : est;
+    }
+    return est;
+}
+
+// Add a to the value's slot E mod n in every row; a slot tagged with another epoch restarts at
+// zero (the LeapArray reset); counts saturate instead of wrapping (never undercount).
+__device__ inline void cm_add(const CountMin &C, uint32_t rule, uint64_t key, int nsc, int64_t E, int32_t a) {
+    const int j = (int)(E % nsc);
+    const uint64_t tag = (uint64_t)((uint32_t)E & CM_TAG_MASK) << CM_COUNT_BITS;
+    for (int d = 0; d < C.depth; ++d) {
+        uint64_t *c = cm_cell(C, rule, d, key) + j;
+        const uint64_t x = *c;
+        uint64_t cnt = ((x & ~CM_COUNT_MAX) == tag) ? (x & CM_COUNT_MAX) : 0;
+        cnt += (uint64_t)(uint32_t)a;
+        if (cnt > CM_COUNT_MAX) cnt = CM_COUNT_MAX;
+        *c = tag | cnt;
+    }
+}
+
+__device__ inline uint64_t cm_check(const ParamCtx &C, uint32_t rule, int64_t E, int32_t a, const ValueSrc &vs,
+                                    int32_t b, int32_t cnt) {
+    const int nsc = C.R.n[rule];
+    const double I_s = C.R.I_s[rule];
+    double remaining = -1.0;
+    for (int32_t q = 0; q < cnt; ++q) {
+        const uint64_t key = vs.value((int64_t)b + q);
+        const int64_t est = cm_estimate(C.CM, rule, key, nsc, E);
+        const double next = remaining_of(value_threshold(C.R, rule, key), I_s, est, a);
+        remaining = next;
+        if (next < 0.0) return pack_verdict(ST_BLOCKED, 0, 0);
+    }
+    for (int32_t q = 0; q < cnt; ++q) cm_add(C.CM, rule, vs.value((int64_t)b + q), nsc, E, a);
+    if (cnt > 1) remaining = -1.0;
+    return pack_verdict(ST_OK, java_d2i(remaining), 0);
+}
+
+// ParamFlowChecker.passDefaultLocalCheck (PFC:127-202) on one (rule, value) bucket, single-threaded
+// (every CAS of the reference succeeds).  Returns 1 pass, 0 block, -1 when the time counter exists
+// without a token counter (only after an LRU eviction; the reference spins there).
+__device__ inline int bucket_pass(int64_t *st, int64_t token_count, int64_t burst, int64_t dur_ms, int32_t a, int64_t t) {
+    if (token_count == 0) return 0;                                          // PFC:144-146
+    const int64_t max_count = wrap_add(token_count, burst);                  // PFC:148
+    if ((int64_t)a > max_count) return 0;                                    // PFC:149-151
+    const int64_t last = st[0];
+    if (last == LOCAL_ABSENT) {                                              // PFC:156-161
+        st[0] = t;
+        if (st[1] == LOCAL_ABSENT) st[1] = wrap_add(max_count, -(int64_t)a);
+        return 1;
+    }
+    const int64_t pass_time = wrap_add(t, -last);                            // PFC:164
+    const int64_t rest = st[1];
+    if (pass_time > dur_ms) {                                                // PFC:166
+        if (rest == LOCAL_ABSENT) {                                          // PFC:167-171
+            st[1] = wrap_add(max_count, -(int64_t)a);
+            st[0] = t;
+            return 1;
+        }
+        const int64_t to_add = wrap_mul(pass_time, token_count) / dur_ms;    // PFC:174, long division
+        const int64_t new_qps = wrap_add(to_add, rest) > max_count ? wrap_add(max_count, -(int64_t)a)
+                                                                   : wrap_add(wrap_add(rest, to_add), -(int64_t)a);
+        if (new_qps < 0) return 0;                                           // PFC:178-180
+        st[1] = new_qps;                                                     // PFC:181-184
+        st[0] = t;
+        return 1;
+    }
+    if (rest == LOCAL_ABSENT) return -1;                                     // PFC:188-199
+    if (wrap_add(rest, -(int64_t)a) >= 0) {
+        st[1] = wrap_add(rest, -(int64_t)a);
+        return 1;
+    }
+    return 0;
+}
+
+// ParamFlowChecker.passLocalCheck (PFC:78-103): every element must pass, in order; no rollback.
+__device__ inline uint64_t local_check(const ParamCtx &C, uint32_t rule, int64_t t, int32_t a, const ValueSrc &vs,
+                                       int32_t b, int32_t cnt) {
+    for (int32_t q = 0; q < cnt; ++q) {
+        const uint64_t key = vs.value((int64_t)b + q);
+        const uint32_t s = C.vslot[b + q];
+        const int64_t h = slot_find(C.L.hot_keys, C.L.hot_mask, key);       // PFC:138-142
+        const int64_t tok = h >= 0 ? C.L.hot_tokens[h] : C.L.tokens[rule];
+        const int r = bucket_pass(C.L.state + 2 * (int64_t)s, tok, C.L.burst[rule], C.L.dur_ms[rule], a, t);
+        if (r == 0) return pack_verdict(ST_BLOCKED, 0, 0);
+        if (r < 0) return pack_verdict(ST_FAIL, 0, 0);
+    }
+    return pack_verdict(ST_OK, 0, 0);
+}
+
+// One lane per rule: walks the rule's sorted (arrival-ordered) events through its segments.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_prule_process(ParamCtx C, BatchWork W, const ParamEvent *__restrict__ ev,
+                                                       ValueSrc vs, uint64_t *__restrict__ out, int64_t n) {
+    const int64_t g0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t S = (int64_t)*W.nseg;
+    if (g0 >= S || (int64_t)*W.nvalid == 0) return;
+    const uint32_t rule = W.seg_key[g0];
+    if (g0 > 0 && W.seg_key[g0 - 1] == rule) return;    // not the first segment of its rule
+    for (int64_t g = g0; g < S; ++g) {
+        if (g > g0 && W.seg_key[g] != rule) break;
+        const int64_t E = W.seg_epoch[g];
+        const uint32_t end = W.seg_start[g + 1];
+        for (uint32_t i = W.seg_start[g]; i < end; ++i) {
+            const uint32_t seq = (uint32_t)W.sval[i] & SEQ_MASK;
+            const ParamEvent e = ev[seq];
+            const int32_t b = vs.begin(seq);
+            const int32_t cnt = vs.count(seq);
+            uint64_t v;
+            if (MODE == PMODE_LOCAL) v = local_check(C, rule, e.ts, e.acquire, vs, b, cnt);
+            else if (MODE == PMODE_CM) v = cm_check(C, rule, E, e.acquire, vs, b, cnt);
+            else v = exact_check(C, E, e.acquire, b, cnt);
+            out[seq] = v;
+        }
+    }
+}
+
+__global__ void k_fill_i64(int64_t *p, int64_t n, int64_t v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+}  // namespace sentinel

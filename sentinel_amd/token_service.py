@@ -82,6 +82,15 @@ class ParamFlowRule:
 
 
 @dataclass
+class LocalParamRule:
+    """Local ParamFlowRule as passDefaultLocalCheck reads it (QPS grade, default behaviour)."""
+    count: float = 0.0
+    burst_count: int = 0
+    duration_in_sec: int = 1
+    hot_items: dict = field(default_factory=dict)   # param key -> int count
+
+
+@dataclass
 class ServerNamespace:
     connected_count: int = 0
     has_limiter: bool = False
@@ -220,8 +229,13 @@ class GpuTokenService:
         params = list(params) if params is not None else []
         if rule_id is None or int(rule_id) <= 0 or acquire_count <= 0 or not params:
             return TokenResult(TokenResultStatus.BAD_REQUEST)       # DefaultTokenService.java:53-55
-        if len(params) != 1:
-            raise NotImplementedError("multi-value param requests: round-2 item (sequential all-or-nothing path)")
+        if len(params) != 1:   # ClusterParamFlowChecker over the whole value list (CPFC:58-86)
+            idx = int(self.lookup_param_idx([int(rule_id)])[0])
+            st, rem = self.submit_param_multi_batch_host(
+                np.array([idx], np.int32), np.array([acquire_count], np.int32),
+                np.array([_now_ms() if ts is None else int(ts)], np.int64), np.array([0], np.int32),
+                np.array([len(params)], np.int32), np.array(params, dtype=np.uint64))
+            return TokenResult(int(st[0]), int(rem[0]), 0)
         out = _lib.TokenResultC()
         check(self._L.sentinel_request_param_token(self._h, int(rule_id), int(acquire_count), int(params[0]),
                                                    _now_ms() if ts is None else int(ts), C.byref(out)),
@@ -294,6 +308,72 @@ class GpuTokenService:
         out = np.empty(len(ev), dtype=_lib.VERDICT_DTYPE)
         check(self._L.sentinel_submit_param_batch_host(self._h, len(ev), _p(ev), _p(out)), "submit_param_batch_host")
         return out["status"].astype(np.int8), out["remaining"].copy()
+
+    @staticmethod
+    def pack_multi_events(rule_idx, acquire, ts, value_begin, value_count) -> np.ndarray:
+        ev = np.empty(len(ts), dtype=_lib.MULTI_EVENT_DTYPE)
+        ev["rule_idx"] = rule_idx
+        ev["acquire"] = acquire
+        ev["ts"] = ts
+        ev["value_begin"] = value_begin
+        ev["value_count"] = value_count
+        return ev
+
+    def submit_param_multi_batch_host(self, rule_idx, acquire, ts, value_begin, value_count, values):
+        """requestParamToken with value lists (host arrays in, (status, remaining) out)."""
+        ev = self.pack_multi_events(rule_idx, acquire, ts, value_begin, value_count)
+        vals = np.ascontiguousarray(values, dtype=np.uint64)
+        out = np.empty(len(ev), dtype=_lib.VERDICT_DTYPE)
+        check(self._L.sentinel_submit_param_multi_batch_host(self._h, len(ev), _p(ev), _p(vals) if len(vals) else None,
+                                                             len(vals), _p(out)), "submit_param_multi_batch_host")
+        return out["status"].astype(np.int8), out["remaining"].copy()
+
+    def submit_param_multi_batch(self, events, values, verdicts=None, stream=None):
+        """Device tensors: events int64 (n, 3) of sentinel_param_multi_event_t, values uint64/int64 (m,)."""
+        import torch
+        n = int(events.shape[0])
+        if verdicts is None:
+            verdicts = torch.empty(n, dtype=torch.int64, device=events.device)
+        s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        check(self._L.sentinel_submit_param_multi_batch(self._h, n, C.c_void_p(events.data_ptr()),
+                                                        C.c_void_p(values.data_ptr()), int(values.shape[0]),
+                                                        C.c_void_p(verdicts.data_ptr()), None if s is None else C.c_void_p(s)),
+              "submit_param_multi_batch")
+        return verdicts
+
+    def set_param_mode(self, mode: int, depth: int = 4, width: int = 1024):
+        """SENTINEL_PARAM_EXACT (0) or SENTINEL_PARAM_COUNT_MIN (1); clears the param counters."""
+        check(self._L.sentinel_set_param_mode(self._h, int(mode), int(depth), int(width)), "set_param_mode")
+
+    def load_local_param_rules(self, rules: Sequence[LocalParamRule]):
+        """Local ParamFlowRules (index = position); every token bucket restarts."""
+        arr = (_lib.LocalParamRuleC * max(len(rules), 1))()
+        keys, counts = [], []
+        for i, r in enumerate(rules):
+            arr[i] = _lib.LocalParamRuleC(float(r.count), int(r.burst_count), int(r.duration_in_sec), len(keys),
+                                          len(r.hot_items))
+            for k, c in r.hot_items.items():
+                keys.append(k)
+                counts.append(c)
+        hk = np.array(keys or [0], dtype=np.uint64)
+        hc = np.array(counts or [0], dtype=np.int32)
+        check(self._L.sentinel_load_local_param_rules(self._h, arr, len(rules), _p(hk), _p(hc), len(keys)),
+              "load_local_param_rules")
+
+    def submit_local_param_batch_host(self, rule_idx, acquire, ts, value_begin, value_count, values):
+        """ParamFlowChecker.passLocalCheck per event; returns the status array (OK / BLOCKED / ...)."""
+        ev = self.pack_multi_events(rule_idx, acquire, ts, value_begin, value_count)
+        vals = np.ascontiguousarray(values, dtype=np.uint64)
+        out = np.empty(len(ev), dtype=_lib.VERDICT_DTYPE)
+        check(self._L.sentinel_submit_local_param_batch_host(self._h, len(ev), _p(ev), _p(vals) if len(vals) else None,
+                                                             len(vals), _p(out)), "submit_local_param_batch_host")
+        return out["status"].astype(np.int8)
+
+    def local_param_state(self, key: int):
+        last, tok = C.c_int64(), C.c_int64()
+        rc = self._L.sentinel_local_param_state(self._h, int(key), C.byref(last), C.byref(tok))
+        check(rc, "local_param_state")
+        return last.value, tok.value
 
     def synchronize(self):
         check(self._L.sentinel_synchronize(self._h), "synchronize")

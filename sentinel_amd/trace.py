@@ -151,3 +151,18 @@ def config4(n_events: int, seed: int = 4, n_rules: int = 100_000, universe: int 
     rate = offered_ratio * float(count.sum()) * 0.05
     ts = timestamps(n_events, rate, t0)
     return count, hot, rule_idx, vals, keys, ts
+
+
+def param_value_lists(rule_idx: np.ndarray, rng: np.random.Generator, universe: int = 300, zipf_s: float = 1.2,
+                      max_values: int = 4):
+    """Value lists for multi-value param requests (1..max_values values each, Zipf over a per-rule
+    universe, repeats allowed).  Returns (value_begin, value_count, keys) with key = (rule << 20) | value."""
+    n = len(rule_idx)
+    counts = rng.integers(1, max_values + 1, size=n).astype(np.int32)
+    begin = np.zeros(n, dtype=np.int32)
+    if n:
+        begin[1:] = np.cumsum(counts)[:-1]
+    vals = zipf_indices(universe, zipf_s, int(counts.sum()), rng, permute=False)
+    owner = np.repeat(np.asarray(rule_idx, dtype=np.int64), counts)
+    keys = (owner.astype(np.uint64) << np.uint64(20)) | vals.astype(np.uint64)
+    return begin, counts, keys

@@ -1,0 +1,197 @@
+"""GPU parity of the per-rule hot-parameter paths (param_rules.hpp) against the CPU oracle:
+multi-value cluster requests (bit-exact), count-min mode (one-sided: audited on exact counters),
+and the local ParamFlowChecker token bucket (bit-exact, including the reference's KAT sequences)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from sentinel_amd import trace as T
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _cluster_pair(oracle_mod, count, hot, sample_count=lambda r: 2 if r % 2 else 5, namespaces=None):
+    import sentinel_amd as sa
+    from sentinel_amd.token_service import ServerNamespace
+    R = len(count)
+    prules = [sa.ParamFlowRule(count=float(count[r]), cluster_config=sa.ClusterFlowConfig(
+        flow_id=r + 1, threshold_type=1, sample_count=sample_count(r), window_interval_ms=1000),
+        hot_items=hot.get(r, {}), namespace=(r % len(namespaces)) if namespaces else 0) for r in range(R)]
+    svc = sa.GpuTokenService(0)
+    ns = namespaces or [dict()]
+    svc.set_namespaces([ServerNamespace(**n) for n in ns])
+    svc.load_param_rules(prules)
+    orc = oracle_mod.TokenServiceOracle(
+        [], namespaces=[dict(connected_count=n.get("connected_count", 0), has_limiter=n.get("has_limiter", 0),
+                             max_allowed_qps=n.get("max_allowed_qps", 30000.0)) for n in ns],
+        param_rules=[dict(flow_id=r + 1, count=float(count[r]), threshold_type=1, sample_count=sample_count(r),
+                          window_interval_ms=1000, namespace_idx=(r % len(namespaces)) if namespaces else 0)
+                     for r in range(R)],
+        hot_items={r: list(hot[r].items()) for r in hot})
+    return svc, orc
+
+
+def _slice_lists(b, c, k, lo, hi):
+    bb = b[lo:hi]
+    start = int(bb[0]) if len(bb) else 0
+    end = int(bb[-1] + c[hi - 1]) if len(bb) else 0
+    return (bb - start).astype(np.int32), c[lo:hi], k[start:end]
+
+
+def test_multi_value_exact_bitexact(oracle_mod):
+    count, hot, rule_idx, vals, keys, ts = T.config4(80_000, seed=44, n_rules=150, universe=250)
+    rng = np.random.default_rng(44)
+    b, c, k = T.param_value_lists(rule_idx, rng, universe=250)
+    acq = np.where(np.arange(len(ts)) % 5 == 0, 2, 1).astype(np.int32)
+    svc, orc = _cluster_pair(oracle_mod, count, hot)
+    for lo, hi in [(0, 30_000), (30_000, 80_000)]:
+        bb, cc, kk = _slice_lists(b, c, k, lo, hi)
+        sg, rg = svc.submit_param_multi_batch_host(rule_idx[lo:hi], acq[lo:hi], ts[lo:hi], bb, cc, kk)
+        so, ro = orc.param_multi_replay(rule_idx[lo:hi], acq[lo:hi], ts[lo:hi], bb, cc, kk)
+        bad = np.nonzero((sg != so) | (rg != ro))[0]
+        assert len(bad) == 0, (len(bad), bad[:5], sg[bad[:5]], so[bad[:5]], rg[bad[:5]], ro[bad[:5]])
+    assert set(np.unique(so)) <= {0, 1} and (so == 1).any() and (so == 0).any()
+    t = int(ts[-1])
+    for j in range(0, len(k), 331):
+        r = int(k[j] >> np.uint64(20))
+        assert svc.param_sum(r, int(k[j]), t) == orc.param_sum(r, t, int(k[j]))
+
+
+def test_single_and_multi_batches_share_exact_counters(oracle_mod):
+    """Single-value fast path (per key) and the per-rule path interleave on one set of counters."""
+    count, hot, rule_idx, vals, keys, ts = T.config4(60_000, seed=45, n_rules=80, universe=120)
+    rng = np.random.default_rng(45)
+    b, c, k = T.param_value_lists(rule_idx, rng, universe=120, max_values=3)
+    acq = np.ones(len(ts), np.int32)
+    svc, orc = _cluster_pair(oracle_mod, count, hot)
+    cuts = [0, 15_000, 30_000, 45_000, 60_000]
+    for i in range(4):
+        lo, hi = cuts[i], cuts[i + 1]
+        if i % 2 == 0:
+            sg, rg = svc.submit_param_batch_host(rule_idx[lo:hi], acq[lo:hi], keys[lo:hi], ts[lo:hi])
+            so, ro = orc.param_replay(rule_idx[lo:hi], acq[lo:hi], keys[lo:hi], ts[lo:hi])
+        else:
+            bb, cc, kk = _slice_lists(b, c, k, lo, hi)
+            sg, rg = svc.submit_param_multi_batch_host(rule_idx[lo:hi], acq[lo:hi], ts[lo:hi], bb, cc, kk)
+            so, ro = orc.param_multi_replay(rule_idx[lo:hi], acq[lo:hi], ts[lo:hi], bb, cc, kk)
+        assert np.array_equal(sg, so) and np.array_equal(rg, ro), i
+
+
+def test_multi_value_edge_cases_and_limiter(oracle_mod):
+    rng = np.random.default_rng(46)
+    count = rng.integers(3, 30, size=60).astype(np.float64)
+    ns = [dict(connected_count=1, has_limiter=1, max_allowed_qps=900.0), dict(connected_count=2)]
+    svc, orc = _cluster_pair(oracle_mod, count, {}, namespaces=ns)
+    n = 20_000
+    ridx = rng.integers(-3, 63, size=n).astype(np.int32)
+    ridx[ridx == -3] = -2                                  # BAD id
+    acq = rng.integers(-1, 3, size=n).astype(np.int32)
+    b, c, k = T.param_value_lists(np.clip(ridx, 0, 59), rng, universe=40, max_values=4)
+    c = c.copy()
+    c[::97] = 0                                            # empty params -> BAD_REQUEST
+    ts = T.timestamps(n, 4000.0, T.T0_ALIGNED + 77)
+    sg, rg = svc.submit_param_multi_batch_host(ridx, acq, ts, b, c, k)
+    so, ro = orc.param_multi_replay(ridx, acq, ts, b, c, k)
+    bad = np.nonzero((sg != so) | (rg != ro))[0]
+    assert len(bad) == 0, (len(bad), bad[:5], sg[bad[:5]], so[bad[:5]])
+    assert {-4, -2, 0, 1, 3} <= set(np.unique(so).tolist())
+
+
+def test_count_min_is_one_sided(oracle_mod):
+    """Narrow sketch (width 64): collisions happen; every pass must still be admissible on exact
+    counters replaying the sketch's own decisions.  Wide sketch: false blocks vanish."""
+    import sentinel_amd as sa
+    count, hot, rule_idx, vals, keys, ts = T.config4(60_000, seed=47, n_rules=60, universe=400, offered_ratio=40.0)
+    rng = np.random.default_rng(47)
+    b, c, k = T.param_value_lists(rule_idx, rng, universe=400, max_values=3)
+    acq = np.ones(len(ts), np.int32)
+    rates = {}
+    for width in (64, 8192):
+        svc, orc = _cluster_pair(oracle_mod, count, hot)
+        svc.set_param_mode(sa._lib.PARAM_COUNT_MIN, depth=4, width=width)
+        sg, _ = svc.submit_param_multi_batch_host(rule_idx, acq, ts, b, c, k)
+        viol, fb, dec = orc.param_cm_audit(rule_idx, acq, ts, b, c, k, sg)
+        assert viol == 0, (width, viol)
+        assert dec == len(ts)
+        rates[width] = fb / dec
+        # estimates never undercount the value's own (sketch-admitted) window count
+        t = int(ts[-1])
+        for j in range(0, len(k), 997):
+            r = int(k[j] >> np.uint64(20))
+            assert svc.param_sum(r, int(k[j]), t) >= orc.param_sum(r, t, int(k[j]))
+    assert rates[64] > rates[8192]
+    assert rates[8192] < 1e-3, rates
+    # single-value batches go through the sketch too in count-min mode
+    svc, orc = _cluster_pair(oracle_mod, count, hot)
+    svc.set_param_mode(sa._lib.PARAM_COUNT_MIN, depth=2, width=32)
+    sg, _ = svc.submit_param_batch_host(rule_idx[:20_000], acq[:20_000], keys[:20_000], ts[:20_000])
+    n1 = np.ones(20_000, np.int32)
+    viol, fb, dec = orc.param_cm_audit(rule_idx[:20_000], acq[:20_000], ts[:20_000], np.arange(20_000), n1,
+                                       keys[:20_000], sg)
+    assert viol == 0 and dec == 20_000
+
+
+def _local_pair(oracle_mod, rules):
+    import sentinel_amd as sa
+    svc = sa.GpuTokenService(0)
+    svc.load_local_param_rules([sa.LocalParamRule(count=r[0], burst_count=r[1], duration_in_sec=r[2],
+                                                  hot_items=r[3]) for r in rules])
+    return svc, oracle_mod.LocalParamOracle(rules)
+
+
+def test_local_param_kat_sequences(oracle_mod):
+    kat = json.load(open(os.path.join(GOLDEN, "kat_param_default_checker.json")))
+    for case in kat["cases"]:
+        for t0 in kat["t0"]:
+            svc, _ = _local_pair(oracle_mod, [(case["token_count"], case["burst"], case["duration"], {})])
+            t, ts = t0, []
+            for dt, _x in case["steps"]:
+                t += dt
+                ts.append(t)
+            n = len(ts)
+            # one batch per step: the sequence crosses batches like the reference's calls cross time
+            got = [int(svc.submit_local_param_batch_host([0], [1], [ts[i]], [0], [1], [7])[0]) for i in range(n)]
+            assert got == [0 if x else 1 for _, x in case["steps"]], case["name"]
+            # and the whole sequence as ONE batch gives the same answers (sequential per key)
+            svc2, _ = _local_pair(oracle_mod, [(case["token_count"], case["burst"], case["duration"], {})])
+            st = svc2.submit_local_param_batch_host(np.zeros(n), np.ones(n), ts, np.arange(n), np.ones(n), np.full(n, 7))
+            assert list(st) == got, case["name"]
+
+
+def test_local_param_bitexact(oracle_mod):
+    rng = np.random.default_rng(48)
+    R = 300
+    rules = []
+    for r in range(R):
+        hot = {}
+        if r % 7 == 0:
+            for v in range(3):
+                hot[int((r << 20) | v)] = int(rng.integers(0, 6))
+        rules.append((float(rng.integers(0, 40)) + (0.5 if r % 5 == 0 else 0.0), int(rng.integers(0, 4)),
+                      int(rng.choice([1, 1, 2, 5])), hot))
+    rules[3] = (-1.0, 0, 1, {})                 # invalid rule -> NO_RULE_EXISTS
+    svc, orc = _local_pair(oracle_mod, rules)
+    n = 120_000
+    ridx = T.zipf_indices(R, 1.05, n, rng)
+    ridx[::501] = R + 3                         # unknown rule
+    acq = rng.integers(1, 4, size=n).astype(np.int32)
+    b, c, k = T.param_value_lists(np.minimum(ridx, R - 1), rng, universe=60, max_values=3)
+    c = c.copy()
+    c[::613] = 0                                # empty collection passes
+    ts = T.timestamps(n, 20_000.0, T.T0_ALIGNED + 13)
+    for lo, hi in [(0, 40_000), (40_000, 120_000)]:
+        bb, cc, kk = _slice_lists(b, c, k, lo, hi)
+        sg = svc.submit_local_param_batch_host(ridx[lo:hi], acq[lo:hi], ts[lo:hi], bb, cc, kk)
+        so = orc.replay(ridx[lo:hi], acq[lo:hi], ts[lo:hi], bb, cc, kk)
+        bad = np.nonzero(sg != so)[0]
+        assert len(bad) == 0, (len(bad), bad[:5], sg[bad[:5]], so[bad[:5]])
+    assert {0, 1, 3} <= set(np.unique(so).tolist())
+    for j in range(0, len(k), 401):
+        r = int(k[j] >> np.uint64(20))
+        lo_, to_ = orc.state(r, int(k[j]))
+        lg, tg = svc.local_param_state(int(k[j]))
+        assert (lg, tg) == (lo_, to_), (j, lg, tg, lo_, to_)
