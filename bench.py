@@ -40,6 +40,32 @@ KERNEL_BYTES_PER_EVENT = {
 }
 
 
+# rocprofv3 kernel symbols behind each engine profile name (for the PMC traffic of the roofline).
+KERNEL_SYMBOLS = {
+    "flow_prep": ("k_flow_prep",), "radix_hist": ("k_radix_hist_pass",), "radix_scatter": ("k_radix_scatter_p",),
+    "scan": ("k_scan_lookback",), "segments": ("k_segments",), "process": ("k_process",), "verdict": ("k_verdict",),
+    "part_scatter": ("k_part_scatter",), "part_process": ("k_part_process",),
+}
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this workload
+    (scripts/gpu_round.sh: separate FETCH_SIZE / WRITE_SIZE passes, FETCH doubled on gfx950)."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            summ = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    pats = KERNEL_SYMBOLS.get(kernel, ())
+    tot = disp = 0.0
+    for name, v in summ.items():
+        if any(name.startswith(p) for p in pats) and v.get("traffic_bytes_avg"):
+            tot += v["traffic_bytes_avg"] * v["dispatches"]
+            disp += v["dispatches"]
+    return round(tot / disp, 1) if disp else None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -183,7 +209,9 @@ def main():
             bpe = (32.0 + 24.0 * (passes - 1)) / passes
         ach = (bpe or 0.0) * d["units_per_call"] / (d["avg_us"] * 1e-6) / 1e9
         roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom),
+                "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_latest.json)",
+                "algorithmic_bytes_per_launch": round((bpe or 0.0) * d["units_per_call"], 1),
                 "bytes_per_event": bpe, "avg_us": round(d["avg_us"], 2)}
 
     # ---- CPU baseline: the oracle ("port") on bounded samples of the same workload, rank 0, N=1.

@@ -1,7 +1,10 @@
+# GPU parity tests only (optionally a subset: bash scripts/gpu_tests_only.sh TAG tests/a.py tests/b.py)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out/param1
-timeout -k 10 400 python -u -m pytest tests/test_param_rules_gpu.py tests/test_gpu_parity.py -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/param1/tests.log 2>&1
+TAG=${1:-tests}
+shift
+mkdir -p gpurun_out/$TAG
+timeout -k 10 500 python -u -m pytest ${@:-tests} -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/$TAG/tests.log 2>&1
 rc=$?
-tail -25 gpurun_out/param1/tests.log
+tail -30 gpurun_out/$TAG/tests.log
 exit $rc
