@@ -246,6 +246,48 @@ int  sentinel_submit_local_param_batch_host(sentinel_engine_t *eng, int64_t n, c
 /* Token bucket of one value: {lastAddTokenTime, tokens} (-1 when absent); returns 1 if present. */
 int  sentinel_local_param_state(sentinel_engine_t *eng, uint64_t param_key, int64_t *last_add_ms, int64_t *tokens);
 
+/* ---- cluster concurrency tokens (thread grade): TokenService.requestConcurrentToken /
+ *      releaseConcurrentToken (TokenService.java:56,62) -> ConcurrentClusterFlowChecker
+ *      (sentinel-cluster/.../cluster/flow/ConcurrentClusterFlowChecker.java:48-101) ---- */
+#define SENTINEL_STATUS_RELEASE_OK       6    /* TokenResultStatus.RELEASE_OK */
+#define SENTINEL_STATUS_ALREADY_RELEASE  7    /* TokenResultStatus.ALREADY_RELEASE */
+#define SENTINEL_CONCURRENT_ACQUIRE  0
+#define SENTINEL_CONCURRENT_RELEASE  1
+#define SENTINEL_CONCURRENT_HAS_ADDRESS 1u    /* flags: clientAddress non-null and non-empty (DTS:89-91) */
+
+/* One acquire (flow_idx from sentinel_lookup_flow_idx, acquire count, flags) or release (token_id).
+ * 24 bytes. */
+typedef struct {
+    int32_t flow_idx;
+    int32_t acquire;
+    int64_t token_id;
+    int32_t kind;
+    uint32_t flags;
+} sentinel_concurrent_event_t;
+
+/* TokenResult of a concurrent call: status OK with a fresh token id, BLOCKED, BAD_REQUEST,
+ * NO_RULE_EXISTS, FAIL (token cache full), RELEASE_OK or ALREADY_RELEASE.  16 bytes. */
+typedef struct {
+    int64_t token_id;
+    int32_t status;
+    int32_t reserved;
+} sentinel_concurrent_result_t;
+
+/* A batch of acquires / releases in arrival order; each flow's events are decided in order (HOST
+ * pointers, synchronous).  Token ids are engine-generated opaque 64-bit values (the reference draws
+ * them from UUID.randomUUID(), TokenCacheNode.java:63). */
+int  sentinel_submit_concurrent_batch_host(sentinel_engine_t *eng, int64_t n, const sentinel_concurrent_event_t *events,
+                                           sentinel_concurrent_result_t *results);
+/* CurrentConcurrencyManager.get(flowId) of a loaded flow. */
+int  sentinel_concurrent_now_calls(sentinel_engine_t *eng, int32_t flow_idx, int32_t *now_calls);
+/* TokenCacheNodeManager.getSize(). */
+int  sentinel_concurrent_token_count(sentinel_engine_t *eng, int64_t *count);
+/* One RegularExpireStrategy sweep (RegularExpireStrategy.java:94-124): removes up to max_tokens
+ * cached tokens (the reference: executeCount = 1000 per 1 s tick) and returns their counts to
+ * nowCalls.  Which tokens go first when more than max_tokens are cached is unspecified (the
+ * reference follows ConcurrentLinkedHashMap key order). */
+int  sentinel_concurrent_expire(sentinel_engine_t *eng, int64_t max_tokens, int64_t *removed);
+
 /* ---- per-call TokenService mirror (one event, synchronous) ---- */
 int  sentinel_request_token(sentinel_engine_t *eng, int64_t flow_id, int32_t acquire_count,
                             int32_t prioritized, int64_t ts, sentinel_token_result_t *out);

@@ -119,6 +119,10 @@ def lib():
         "orc_lparam_free": (None, [vp]),
         "orc_lparam_replay": (None, [vp, i64, vp, vp, vp, vp, vp, vp, i64, vp]),
         "orc_lparam_state": (C.c_int, [vp, i32, u64, vp, vp]),
+        "orc_concurrent_replay": (None, [vp, i64, vp, vp, vp, vp]),
+        "orc_concurrent_now_calls": (i32, [vp, i32]),
+        "orc_concurrent_token_count": (i64, [vp]),
+        "orc_concurrent_expire_all": (i64, [vp]),
         "orc_java_d2i": (i32, [dbl]),
         "orc_java_string_hash": (i32, [vp, i64]),
     }
@@ -448,6 +452,28 @@ class TokenServiceOracle:
         if w < 0:
             raise ValueError("no metric for flow index %d" % idx)
         return out
+
+    def reload_flow_rules(self, rules):
+        """ClusterFlowRuleManager.loadRules again (nowCalls of surviving flowIds carried over)."""
+        self.rules = list(rules)
+        self._rules_c = rules_array(self.rules)
+        lib().orc_engine_load_flow_rules(self.h, self._rules_c, len(self.rules))
+
+    CONC_EVENT = np.dtype([("flow_idx", "<i4"), ("acquire", "<i4"), ("token_id", "<i8"), ("kind", "<i4"),
+                           ("flags", "<u4")])
+
+    def concurrent_replay(self, events: np.ndarray, new_ids):
+        """ConcurrentClusterFlowChecker replay; events in CONC_EVENT layout; returns (status, token_id)."""
+        ev = np.ascontiguousarray(events, dtype=self.CONC_EVENT)
+        ids = np.ascontiguousarray(new_ids, dtype=np.int64)
+        st = np.zeros(len(ev), dtype=np.int8)
+        tok = np.zeros(len(ev), dtype=np.int64)
+        lib().orc_concurrent_replay(self.h, len(ev), _p(ev), _p(ids), _p(st), _p(tok))
+        return st, tok
+
+    def concurrent_now_calls(self, idx): return lib().orc_concurrent_now_calls(self.h, idx)
+    def concurrent_token_count(self): return lib().orc_concurrent_token_count(self.h)
+    def concurrent_expire_all(self): return lib().orc_concurrent_expire_all(self.h)
 
     def limiter_sum(self, ns, t):
         return lib().orc_engine_limiter_sum(self.h, ns, t)

@@ -476,6 +476,14 @@ struct orc_engine {
     uint64_t *hot_keys;
     int32_t *hot_counts;
     int n_hot;
+    /* concurrency tokens (ConcurrentClusterFlowChecker) */
+    kvmap now_calls;          /* flowId -> nowCalls (CurrentConcurrencyManager) */
+    kvmap rule_by_fid;        /* flowId -> rule index (ClusterFlowRuleManager.getFlowRuleById) */
+    kvmap tok_index;          /* tokenId -> record (TokenCacheNodeManager) */
+    int64_t *tok_fid;
+    int32_t *tok_acq;
+    uint8_t *tok_alive;
+    int64_t tok_n, tok_cap, tok_live;
 };
 
 orc_engine *orc_engine_new(const orc_server_config *cfg, const orc_namespace *ns, int n_ns) {
@@ -499,6 +507,8 @@ void orc_engine_free(orc_engine *e) {
     for (int i = 0; i < e->n_prules; i++) orc_pm_free(e->prules[i].pm);
     free(e->ns); free(e->lim); free(e->rules); free(e->cm); free(e->prules);
     free(e->hot_keys); free(e->hot_counts);
+    kv_free(&e->now_calls); kv_free(&e->rule_by_fid); kv_free(&e->tok_index);
+    free(e->tok_fid); free(e->tok_acq); free(e->tok_alive);
     free(e);
 }
 
@@ -510,10 +520,20 @@ int orc_engine_load_flow_rules(orc_engine *e, const orc_flow_rule *rules, int n)
     e->rules = (orc_flow_rule *)calloc((size_t)(n > 0 ? n : 1), sizeof(orc_flow_rule));
     e->cm = (orc_cluster_metric **)calloc((size_t)(n > 0 ? n : 1), sizeof(orc_cluster_metric *));
     e->n_rules = n;
+    kvmap now;
+    kv_init(&now);
+    kv_free(&e->rule_by_fid);
     for (int i = 0; i < n; i++) {
         e->rules[i] = rules[i];
         e->cm[i] = orc_cm_new(rules[i].sample_count, rules[i].window_interval_ms);  /* NULL => FAIL */
+        if (!e->cm[i] || rules[i].flow_id <= 0) continue;
+        *kv_insert(&e->rule_by_fid, (uint64_t)rules[i].flow_id, 0) = i;           /* ruleMap.put: last wins */
+        /* CFRM:356-358: nowCalls survives for flowIds still present, new flowIds start at 0 */
+        const int64_t *old = kv_find(&e->now_calls, (uint64_t)rules[i].flow_id);
+        *kv_insert(&now, (uint64_t)rules[i].flow_id, 0) = old ? *old : 0;
     }
+    kv_free(&e->now_calls);
+    e->now_calls = now;
     return 0;
 }
 
@@ -1012,4 +1032,78 @@ int orc_lparam_state(orc_local_engine *e, int32_t idx, uint64_t key, int64_t *la
     if (l) *last = *l;
     if (t) *tokens = *t;
     return l != NULL;
+}
+
+/* ------------------------------------------------------------------ concurrency tokens */
+/* ConcurrentClusterFlowChecker (CCFC:35-101) replayed sequentially.  new_ids[i] is the token id an
+ * acquire receives when it passes (the reference draws it from UUID.randomUUID()). */
+static double conc_threshold(const orc_engine *e, const orc_flow_rule *r) {     /* CCFC:35-46 */
+    if (r->threshold_type == 1) return r->count;
+    const int cc = (r->namespace_idx >= 0 && r->namespace_idx < e->n_ns) ? e->ns[r->namespace_idx].connected_count : 0;
+    return r->count * (double)cc;
+}
+
+void orc_concurrent_replay(orc_engine *e, int64_t n, const orc_concurrent_event *ev, const int64_t *new_ids,
+                           int8_t *status, int64_t *token_out) {
+    for (int64_t i = 0; i < n; i++) {
+        const orc_concurrent_event *x = &ev[i];
+        token_out[i] = 0;
+        if (x->kind == 0) {
+            if (!(x->flags & 1u) || x->flow_idx == -2 || x->acquire <= 0) { status[i] = ORC_BAD_REQUEST; continue; }
+            if (x->flow_idx < 0 || x->flow_idx >= e->n_rules || !e->cm[x->flow_idx]) { status[i] = ORC_NO_RULE_EXISTS; continue; }
+            const orc_flow_rule *r = &e->rules[x->flow_idx];
+            int64_t *now = kv_find(&e->now_calls, (uint64_t)r->flow_id);
+            if (!now) { status[i] = ORC_FAIL; continue; }                          /* CCFC:51-54 */
+            const int32_t sum = (int32_t)((uint32_t)(int32_t)*now + (uint32_t)x->acquire);
+            if ((double)sum > conc_threshold(e, r)) { status[i] = ORC_BLOCKED; continue; }   /* CCFC:57-69 */
+            *now = (int32_t)((uint32_t)(int32_t)*now + (uint32_t)x->acquire);     /* CCFC:70 */
+            if (e->tok_n == e->tok_cap) {
+                e->tok_cap = e->tok_cap ? 2 * e->tok_cap : 1024;
+                e->tok_fid = (int64_t *)realloc(e->tok_fid, (size_t)e->tok_cap * sizeof(int64_t));
+                e->tok_acq = (int32_t *)realloc(e->tok_acq, (size_t)e->tok_cap * sizeof(int32_t));
+                e->tok_alive = (uint8_t *)realloc(e->tok_alive, (size_t)e->tok_cap);
+            }
+            e->tok_fid[e->tok_n] = r->flow_id;
+            e->tok_acq[e->tok_n] = x->acquire;
+            e->tok_alive[e->tok_n] = 1;
+            *kv_insert(&e->tok_index, (uint64_t)new_ids[i], 0) = e->tok_n++;
+            e->tok_live++;
+            status[i] = ORC_OK;
+            token_out[i] = new_ids[i];
+        } else if (x->kind == 1) {
+            const int64_t *rec = kv_find(&e->tok_index, (uint64_t)x->token_id);     /* CCFC:82-86 */
+            if (!rec || !e->tok_alive[*rec]) { status[i] = 7; continue; }           /* ALREADY_RELEASE */
+            if (!kv_find(&e->rule_by_fid, (uint64_t)e->tok_fid[*rec])) { status[i] = ORC_NO_RULE_EXISTS; continue; }
+            e->tok_alive[*rec] = 0;                                                 /* CCFC:92-98 */
+            e->tok_live--;
+            int64_t *now = kv_find(&e->now_calls, (uint64_t)e->tok_fid[*rec]);
+            *now = (int32_t)((uint32_t)(int32_t)*now - (uint32_t)e->tok_acq[*rec]);
+            status[i] = 6;                                                          /* RELEASE_OK */
+        } else {
+            status[i] = ORC_BAD_REQUEST;
+        }
+    }
+}
+
+int32_t orc_concurrent_now_calls(orc_engine *e, int32_t flow_idx) {
+    if (flow_idx < 0 || flow_idx >= e->n_rules) return 0;
+    const int64_t *now = kv_find(&e->now_calls, (uint64_t)e->rules[flow_idx].flow_id);
+    return now ? (int32_t)*now : 0;
+}
+
+int64_t orc_concurrent_token_count(orc_engine *e) { return e->tok_live; }
+
+/* RegularExpireStrategy.clearToken with <= executeCount cached tokens: every token qualifies and
+ * leaves the cache; nowCalls of a still-present flowId gets the count back (RES:94-136). */
+int64_t orc_concurrent_expire_all(orc_engine *e) {
+    int64_t removed = 0;
+    for (int64_t t = 0; t < e->tok_n; t++) {
+        if (!e->tok_alive[t]) continue;
+        e->tok_alive[t] = 0;
+        e->tok_live--;
+        removed++;
+        int64_t *now = kv_find(&e->now_calls, (uint64_t)e->tok_fid[t]);
+        if (now) *now = (int32_t)((uint32_t)(int32_t)*now - (uint32_t)e->tok_acq[t]);
+    }
+    return removed;
 }

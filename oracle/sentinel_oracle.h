@@ -200,6 +200,22 @@ void orc_lparam_replay(orc_local_engine *e, int64_t n, const int32_t *rule_idx, 
                       int64_t n_values, int8_t *status);
 int  orc_lparam_state(orc_local_engine *e, int32_t idx, uint64_t key, int64_t *last, int64_t *tokens);
 
+/* ---------------- concurrency tokens (ConcurrentClusterFlowChecker) ---------------- */
+/* Mirrors include/sentinel_amd.h's sentinel_concurrent_event_t (kind 0 acquire, 1 release). */
+typedef struct {
+    int32_t flow_idx;
+    int32_t acquire;
+    int64_t token_id;
+    int32_t kind;
+    uint32_t flags;        /* bit0: clientAddress non-empty */
+} orc_concurrent_event;
+
+void orc_concurrent_replay(orc_engine *e, int64_t n, const orc_concurrent_event *ev, const int64_t *new_ids,
+                           int8_t *status, int64_t *token_out);
+int32_t orc_concurrent_now_calls(orc_engine *e, int32_t flow_idx);
+int64_t orc_concurrent_token_count(orc_engine *e);
+int64_t orc_concurrent_expire_all(orc_engine *e);
+
 /* ---------------- Java numerics ---------------- */
 int32_t orc_java_d2i(double d);
 int64_t orc_java_d2l(double d);

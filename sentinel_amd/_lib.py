@@ -46,7 +46,14 @@ EXPORTS = [
     "sentinel_submit_param_multi_batch", "sentinel_submit_param_multi_batch_host", "sentinel_set_param_mode",
     "sentinel_load_local_param_rules", "sentinel_submit_local_param_batch", "sentinel_submit_local_param_batch_host",
     "sentinel_local_param_state",
+    "sentinel_submit_concurrent_batch_host", "sentinel_concurrent_now_calls", "sentinel_concurrent_token_count",
+    "sentinel_concurrent_expire",
 ]
+
+STATUS_RELEASE_OK = 6
+STATUS_ALREADY_RELEASE = 7
+CONCURRENT_ACQUIRE = 0
+CONCURRENT_RELEASE = 1
 
 PARAM_EXACT = 0
 PARAM_COUNT_MIN = 1
@@ -90,6 +97,9 @@ EVENT_DTYPE = np.dtype([("flow_idx", "<i4"), ("acquire", "<i4"), ("ts", "<i8")])
 PARAM_EVENT_DTYPE = np.dtype([("rule_idx", "<i4"), ("acquire", "<i4"), ("ts", "<i8"), ("param_key", "<u8")])
 MULTI_EVENT_DTYPE = np.dtype([("rule_idx", "<i4"), ("acquire", "<i4"), ("ts", "<i8"), ("value_begin", "<i4"),
                               ("value_count", "<i4")])
+CONC_EVENT_DTYPE = np.dtype([("flow_idx", "<i4"), ("acquire", "<i4"), ("token_id", "<i8"), ("kind", "<i4"),
+                             ("flags", "<u4")])
+CONC_RESULT_DTYPE = np.dtype([("token_id", "<i8"), ("status", "<i4"), ("reserved", "<i4")])
 VERDICT_DTYPE = np.dtype([("remaining", "<i4"), ("status", "<i2"), ("wait_in_ms", "<u2")])
 
 
@@ -151,6 +161,10 @@ def load():
         "sentinel_submit_local_param_batch": (C.c_int, [vp, i64, vp, vp, i64, vp, vp]),
         "sentinel_submit_local_param_batch_host": (C.c_int, [vp, i64, vp, vp, i64, vp]),
         "sentinel_local_param_state": (C.c_int, [vp, u64, vp, vp]),
+        "sentinel_submit_concurrent_batch_host": (C.c_int, [vp, i64, vp, vp]),
+        "sentinel_concurrent_now_calls": (C.c_int, [vp, i32, vp]),
+        "sentinel_concurrent_token_count": (C.c_int, [vp, vp]),
+        "sentinel_concurrent_expire": (C.c_int, [vp, i64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

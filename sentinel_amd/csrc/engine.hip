@@ -29,7 +29,9 @@
 #include "../../include/sentinel_amd.h"
 #include "admission.hpp"
 #include "common.hpp"
+#include "concurrent.hpp"
 #include "param_rules.hpp"
+#include <random>
 #include "scan_sort.hpp"
 
 using namespace sentinel;
@@ -316,6 +318,12 @@ struct sentinel_engine {
     bool lhas_hot = false;
     uint64_t lcap = (uint64_t)1 << 22;
 
+    // concurrency tokens (ConcurrentClusterFlowChecker): nowCalls per flow, token cache in HBM
+    DevBuf d_now, d_conc_thr, d_seg1_w, d_seg1_rcp, d_seg1_kind;
+    DevBuf d_tok_keys, d_tok_fid, d_tok_fidx, d_tok_acq, d_tok_counts, d_tok_ticket;
+    uint64_t tcap = (uint64_t)1 << 22;
+    uint64_t tok_salt = 0, tok_counter = 1;
+
     // per-kernel profiling (HIP events on the launch stream)
     struct ProfRec { const char *name; hipEvent_t a, b; int64_t units; };
     struct ProfAcc { double ms = 0; int64_t calls = 0; int64_t units = 0; };
@@ -584,7 +592,79 @@ struct sentinel_engine {
     int rebuild_routes();
     int clear_param_slots();
     int rebuild_cm();
+    int ensure_tokens();
+    int rewrite_tokens(bool compact);
+    TokenTable token_table() {
+        return TokenTable{d_tok_keys.as<unsigned long long>(), d_tok_fid.as<int64_t>(), d_tok_fidx.as<int32_t>(),
+                          d_tok_acq.as<int32_t>(), tcap - 1, d_tok_counts.as<unsigned long long>()};
+    }
 };
+
+// Token cache: allocated on first use (SENTINEL_TOKEN_CAPACITY slots, default 4M).
+int sentinel_engine::ensure_tokens() {
+    if (d_tok_keys.p) return 0;
+    if (const char *c = getenv("SENTINEL_TOKEN_CAPACITY")) {
+        uint64_t v = strtoull(c, nullptr, 10), p = 1024;
+        while (p < v) p <<= 1;
+        tcap = p;
+    }
+    int rc = 0;
+    rc |= d_tok_keys.ensure(tcap * 8);
+    rc |= d_tok_fid.ensure(tcap * 8);
+    rc |= d_tok_fidx.ensure(tcap * 4);
+    rc |= d_tok_acq.ensure(tcap * 4);
+    rc |= d_tok_counts.ensure(16);
+    rc |= d_tok_ticket.ensure(8);
+    if (rc) return SENTINEL_E_NOMEM;
+    HIP_OK(hipMemsetAsync(d_tok_keys.p, 0xFF, tcap * 8, stream));
+    HIP_OK(hipMemsetAsync(d_tok_counts.p, 0, 16, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    std::random_device rd;                 // token ids: {salt:23 | counter:40}, opaque to clients like UUID bits
+    tok_salt = ((uint64_t)rd() ^ ((uint64_t)rd() << 11)) & ((1ull << 23) - 1);
+    return 0;
+}
+
+// Host rewrite of the token cache: remap every live token's flow index from its flowId (after a
+// rule load: tokens of removed flows answer NO_RULE_EXISTS until the flowId comes back), and
+// optionally drop tombstones by re-inserting the live tokens into a fresh table.
+int sentinel_engine::rewrite_tokens(bool compact) {
+    if (!d_tok_keys.p) return 0;
+    std::vector<uint64_t> keys(tcap);
+    std::vector<int64_t> fid(tcap);
+    std::vector<int32_t> acq(tcap);
+    HIP_OK(hipMemcpy(keys.data(), d_tok_keys.p, tcap * 8, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(fid.data(), d_tok_fid.p, tcap * 8, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(acq.data(), d_tok_acq.p, tcap * 4, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> nk(tcap, PKEY_EMPTY);
+    std::vector<int64_t> nf(tcap, 0);
+    std::vector<int32_t> nx(tcap, -1), na(tcap, 0);
+    uint64_t live = 0, dead = 0;
+    for (uint64_t h = 0; h < tcap; ++h) {
+        if (keys[h] == PKEY_EMPTY) continue;
+        if (keys[h] == TOKEN_TOMB) {
+            if (!compact) { nk[h] = TOKEN_TOMB; ++dead; }
+            continue;
+        }
+        uint64_t d = h;
+        if (compact) {
+            d = mix64(keys[h]) & (tcap - 1);
+            while (nk[d] != PKEY_EMPTY) d = (d + 1) & (tcap - 1);
+        }
+        auto it = flow_index.find(fid[h]);
+        nk[d] = keys[h];
+        nf[d] = fid[h];
+        nx[d] = it == flow_index.end() ? -1 : it->second;
+        na[d] = acq[h];
+        ++live;
+    }
+    const unsigned long long counts[2] = {live, dead};
+    HIP_OK(hipMemcpy(d_tok_keys.p, nk.data(), tcap * 8, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_tok_fid.p, nf.data(), tcap * 8, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_tok_fidx.p, nx.data(), tcap * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_tok_acq.p, na.data(), tcap * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_tok_counts.p, counts, 16, hipMemcpyHostToDevice));
+    return 0;
+}
 
 // Exact param counters restart: every slot free, every window absent (stream synchronised).
 int sentinel_engine::clear_param_slots() {
@@ -629,7 +709,16 @@ int sentinel_engine::rebuild_flow_thresholds() {
             thr[i] = g * cfg.exceed_count;
         }
     }
-    return upload(ft.thr, thr);
+    int rc = upload(ft.thr, thr);
+    if (rc) return rc;
+    // ConcurrentClusterFlowChecker.calcGlobalThreshold (CCFC:35-46): no exceedCount
+    std::vector<double> cthr(std::max<size_t>(rules.size(), 1), 0.0);
+    for (size_t i = 0; i < rules.size(); ++i) {
+        const sentinel_flow_rule_t &r = rules[i];
+        const int32_t c = (r.namespace_idx >= 0 && r.namespace_idx < (int32_t)ns.size()) ? ns[r.namespace_idx].connected_count : 0;
+        cthr[i] = r.threshold_type == SENTINEL_THRESHOLD_GLOBAL ? r.count : r.count * (double)c;
+    }
+    return upload(d_conc_thr, cthr);
 }
 
 // Per-rule routing: TOO_MANY_REQUEST for a null namespace, limiter id, or plain.
@@ -947,7 +1036,9 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
                       &e->w_s0, &e->w_k, &e->w_counters, &e->io_ev, &e->io_fl, &e->io_out, &e->io_vals, &e->w_vslot,
                       &e->d_prule_kind, &e->d_cm, &e->d_lrule_valid, &e->d_lrule_tok, &e->d_lrule_burst,
                       &e->d_lrule_dur, &e->d_lrule_w, &e->d_lrule_rcp, &e->d_lrule_kind, &e->d_lhot_keys,
-                      &e->d_lhot_tok, &e->d_ltable, &e->d_lstate})
+                      &e->d_lhot_tok, &e->d_ltable, &e->d_lstate, &e->d_now, &e->d_conc_thr, &e->d_seg1_w,
+                      &e->d_seg1_rcp, &e->d_seg1_kind, &e->d_tok_keys, &e->d_tok_fid, &e->d_tok_fidx,
+                      &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket})
         b->release();
     (void)hipStreamDestroy(e->stream);
     delete e;
@@ -1029,6 +1120,9 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
         old_state.resize(e->flow_state_words);
         HIP_OK(hipMemcpy(old_state.data(), e->ft.state.p, old_state.size() * 8, hipMemcpyDeviceToHost));
     }
+    std::vector<int32_t> old_now(old_index.size(), 0);
+    if (!old_index.empty() && e->d_now.p)
+        HIP_OK(hipMemcpy(old_now.data(), e->d_now.p, old_now.size() * 4, hipMemcpyDeviceToHost));
     std::vector<int64_t> old_occ(2 * old_index.size());
     std::vector<uint8_t> old_hocc(old_index.size());
     if (!old_index.empty()) {
@@ -1068,11 +1162,13 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
     std::vector<int64_t> st(std::max<int64_t>(words, 1), 0);
     std::vector<int64_t> occ(2 * std::max<size_t>(F, 1), 0);
     std::vector<uint8_t> hocc(std::max<size_t>(F, 1), 0);
+    std::vector<int32_t> now(std::max<size_t>(F, 1), 0);
     for (size_t i = 0; i < F; ++i) {
         for (int j = 0; j < nn[i]; ++j) st[off[i] + 2 * j] = EPOCH_ABSENT;
         auto it = old_index.find(ids[i]);
         if (it == old_index.end()) continue;
         const int32_t o = it->second;
+        now[i] = old_now[o];       // CurrentConcurrencyManager keeps nowCalls of surviving flowIds (CFRM:356-358)
         // ClusterMetric is kept as constructed with the OLD (n, interval): only carry when equal
         if (old_n[o] != nn[i] || old_w[o] != ww[i]) continue;
         std::copy(old_state.begin() + old_off[o], old_state.begin() + old_off[o] + flow_record_words(nn[i]),
@@ -1092,12 +1188,18 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
     rc |= upload(e->ft.occ, occ);
     rc |= upload(e->ft.has_occ, hocc);
     rc |= upload(e->d_flow_ids, ids);
+    rc |= upload(e->d_now, now);
+    rc |= upload(e->d_seg1_w, std::vector<int32_t>(std::max<size_t>(F, 1), 1 << 30));
+    rc |= upload(e->d_seg1_rcp, std::vector<double>(std::max<size_t>(F, 1), 1.0 / (double)(1 << 30)));
+    rc |= upload(e->d_seg1_kind, std::vector<uint8_t>(std::max<size_t>(F, 1), KIND_LOCAL_PARAM));
     if (rc) return rc;
     e->h_flow_off = off;
     e->h_flow_n = nn;
     e->h_flow_w = ww;
     e->flow_state_words = words;
     e->flow_max_n = nn.empty() ? 1 : *std::max_element(nn.begin(), nn.end());
+    rc = e->rewrite_tokens(false);
+    if (rc) return rc;
     rc = e->rebuild_routes();
     if (rc) return rc;
     return e->rebuild_flow_thresholds();
@@ -1408,6 +1510,103 @@ int sentinel_local_param_state(sentinel_engine_t *e, uint64_t key, int64_t *last
     *last_add_ms = st[0] == LOCAL_ABSENT ? -1 : st[0];
     *tokens = st[1] == LOCAL_ABSENT ? -1 : st[1];
     return 1;
+}
+
+int sentinel_submit_concurrent_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_concurrent_event_t *ev,
+                                          sentinel_concurrent_result_t *out) {
+    if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    if (n == 0) return 0;
+    if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    int rc = e->ensure_tokens();
+    if (rc) return rc;
+    hipStream_t s = e->stream;
+    unsigned long long counts[2];
+    HIP_OK(hipMemcpy(counts, e->d_tok_counts.p, 16, hipMemcpyDeviceToHost));
+    if ((double)(counts[0] + counts[1] + (uint64_t)n) > 0.75 * (double)e->tcap && counts[1] > 0) {
+        rc = e->rewrite_tokens(true);        // drop tombstones before the table clogs
+        if (rc) return rc;
+    }
+    rc = e->ensure_ws(n);
+    rc |= e->io_ev.ensure(n * sizeof(ConcEvent));
+    rc |= e->io_out.ensure(n * 16);
+    if (rc) return SENTINEL_E_NOMEM;
+    HIP_OK(hipMemcpyAsync(e->io_ev.p, ev, n * sizeof(ConcEvent), hipMemcpyHostToDevice, s));
+    const ConcEvent *dev = e->io_ev.as<ConcEvent>();
+    uint64_t *dout = e->io_out.as<uint64_t>();
+    const int32_t F = (int32_t)e->rules.size();
+    const int fbits = bits_for(F);
+    const uint32_t finvalid = ((uint32_t)1 << fbits) - 1;
+    uint32_t *fkey = e->w_fkey.as<uint32_t>();
+    const int64_t nb = sort_blocks(n);
+    const TokenTable TT = e->token_table();
+    HIP_OK(hipMemsetAsync(e->w_counters.p, 0, 16, s));
+    e->launch("conc_prep", n, s, [&] {
+        k_conc_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(n, dev, F, TT, dout, fkey, finvalid,
+                                                                      e->w_fhist.as<uint32_t>(), nb);
+    });
+    if (F > 0) {
+        KeyTable T1{};
+        T1.w = e->d_seg1_w.as<int32_t>();
+        T1.rcp_w = e->d_seg1_rcp.as<double>();
+        T1.kind = e->d_seg1_kind.as<uint8_t>();
+        T1.ncounters = 1;
+        const EventSrc src{nullptr, (const ParamEvent *)dev, nullptr, false};
+        e->sort_segments(T1, fkey, e->w_fhist.as<uint32_t>(), n, fbits, src, s);
+        const BatchWork W = e->work();
+        const uint64_t id_base = (e->tok_salt << 40) | e->tok_counter;
+        e->launch("conc_process", n, s, [&] {
+            k_conc_process<<<grid_for(n), 256, 0, s>>>(W, dev, e->d_now.as<int32_t>(), e->d_conc_thr.as<double>(),
+                                                       e->d_flow_ids.as<int64_t>(), TT, id_base, dout);
+        });
+        e->tok_counter += (uint64_t)n;
+    }
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(out, dout, n * 16, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    return 0;
+}
+
+int sentinel_concurrent_now_calls(sentinel_engine_t *e, int32_t flow_idx, int32_t *now_calls) {
+    if (!e || !now_calls) return fail(SENTINEL_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(e->mu);
+    if (flow_idx < 0 || flow_idx >= (int32_t)e->rules.size()) return fail(SENTINEL_E_INVALID, "bad flow index");
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    HIP_OK(hipMemcpy(now_calls, e->d_now.as<int32_t>() + flow_idx, 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int sentinel_concurrent_token_count(sentinel_engine_t *e, int64_t *count) {
+    if (!e || !count) return fail(SENTINEL_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(e->mu);
+    *count = 0;
+    if (!e->d_tok_counts.p) return 0;
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    unsigned long long c[2];
+    HIP_OK(hipMemcpy(c, e->d_tok_counts.p, 16, hipMemcpyDeviceToHost));
+    *count = (int64_t)c[0];
+    return 0;
+}
+
+int sentinel_concurrent_expire(sentinel_engine_t *e, int64_t max_tokens, int64_t *removed) {
+    if (!e || !removed || max_tokens < 0) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    *removed = 0;
+    if (!e->d_tok_keys.p || max_tokens == 0) return 0;
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipMemsetAsync(e->d_tok_ticket.p, 0, 8, e->stream));
+    k_conc_expire<<<grid_for((int64_t)e->tcap), 256, 0, e->stream>>>(e->token_table(), e->d_now.as<int32_t>(),
+                                                                    (unsigned long long)max_tokens,
+                                                                    e->d_tok_ticket.as<unsigned long long>());
+    HIP_OK(hipGetLastError());
+    unsigned long long t = 0;
+    HIP_OK(hipMemcpyAsync(&t, e->d_tok_ticket.p, 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    *removed = (int64_t)std::min<unsigned long long>(t, (unsigned long long)max_tokens);
+    return 0;
 }
 
 int sentinel_request_token(sentinel_engine_t *e, int64_t flow_id, int32_t acquire, int32_t prio, int64_t ts,

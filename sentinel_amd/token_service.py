@@ -242,11 +242,47 @@ class GpuTokenService:
               "request_param_token")
         return TokenResult(out.status, out.remaining, out.wait_in_ms)
 
-    def request_concurrent_token(self, client_address, rule_id, acquire_count):
-        raise NotImplementedError("concurrent (thread-grade) cluster tokens are a SURVEY §8(f) 'next' row")
+    def request_concurrent_token(self, client_address: Optional[str], rule_id: Optional[int],
+                                 acquire_count: int) -> TokenResult:
+        """TokenService.requestConcurrentToken (TokenService.java:56): OK carries the token id."""
+        fid = 0 if rule_id is None else int(rule_id)
+        idx = int(self.lookup_flow_idx([fid])[0])
+        st, tok = self.submit_concurrent_batch_host([idx], [acquire_count], [0], [_lib.CONCURRENT_ACQUIRE],
+                                                    [1 if client_address else 0])
+        return TokenResult(int(st[0]), token_id=int(tok[0]))
 
-    def release_concurrent_token(self, token_id):
-        raise NotImplementedError("concurrent (thread-grade) cluster tokens are a SURVEY §8(f) 'next' row")
+    def release_concurrent_token(self, token_id: Optional[int]) -> Optional[TokenResult]:
+        """TokenService.releaseConcurrentToken (TokenService.java:62); returns the checker's status
+        (RELEASE_OK / ALREADY_RELEASE / NO_RULE_EXISTS), None for a null token like the reference."""
+        if token_id is None:
+            return None
+        st, _ = self.submit_concurrent_batch_host([0], [0], [int(token_id)], [_lib.CONCURRENT_RELEASE], [0])
+        return TokenResult(int(st[0]))
+
+    def submit_concurrent_batch_host(self, flow_idx, acquire, token_id, kind, flags):
+        """A batch of concurrent acquires / releases in arrival order -> (status, token_id) arrays."""
+        ev = np.empty(len(kind), dtype=_lib.CONC_EVENT_DTYPE)
+        ev["flow_idx"], ev["acquire"], ev["token_id"], ev["kind"], ev["flags"] = flow_idx, acquire, token_id, kind, flags
+        out = np.empty(len(ev), dtype=_lib.CONC_RESULT_DTYPE)
+        check(self._L.sentinel_submit_concurrent_batch_host(self._h, len(ev), _p(ev), _p(out)),
+              "submit_concurrent_batch_host")
+        return out["status"].astype(np.int8), out["token_id"].copy()
+
+    def concurrent_now_calls(self, flow_idx: int) -> int:
+        v = C.c_int32()
+        check(self._L.sentinel_concurrent_now_calls(self._h, int(flow_idx), C.byref(v)), "concurrent_now_calls")
+        return v.value
+
+    def concurrent_token_count(self) -> int:
+        v = C.c_int64()
+        check(self._L.sentinel_concurrent_token_count(self._h, C.byref(v)), "concurrent_token_count")
+        return v.value
+
+    def concurrent_expire(self, max_tokens: int = 1000) -> int:
+        """One RegularExpireStrategy sweep (executeCount 1000 by default)."""
+        v = C.c_int64()
+        check(self._L.sentinel_concurrent_expire(self._h, int(max_tokens), C.byref(v)), "concurrent_expire")
+        return v.value
 
     # ---------------------------------------------------------------- batched hot path
     @staticmethod

@@ -1,0 +1,121 @@
+"""Cluster concurrency tokens (ConcurrentClusterFlowChecker): the oracle pinned by the reference's
+ConcurrentClusterFlowCheckerTest (CPU), and the GPU engine against the oracle over batches of
+interleaved acquires / releases, rule reloads and expiry sweeps (GPU)."""
+import numpy as np
+import pytest
+
+from sentinel_amd import trace as T
+
+
+def _rule(flow_id=111, count=10.0, threshold_type=1):
+    return dict(flow_id=flow_id, count=count, threshold_type=threshold_type, sample_count=10, window_interval_ms=1000,
+                namespace_idx=0, checker=0)
+
+
+def _events(oracle_mod, kinds, flow_idx=0, acquire=1, tokens=None, flags=1):
+    n = len(kinds)
+    ev = np.zeros(n, dtype=oracle_mod.TokenServiceOracle.CONC_EVENT)
+    ev["kind"] = kinds
+    ev["flow_idx"] = flow_idx
+    ev["acquire"] = acquire
+    ev["flags"] = flags
+    if tokens is not None:
+        ev["token_id"] = tokens
+    return ev
+
+
+def test_oracle_matches_reference_concurrent_test(oracle_mod):
+    """ConcurrentClusterFlowCheckerTest.java:61-84 (testEasyAcquireAndRelease) and :115-124 (expiry)."""
+    o = oracle_mod.TokenServiceOracle([_rule()])
+    st, tok = o.concurrent_replay(_events(oracle_mod, [0] * 20), np.arange(1, 21))
+    assert list(st[:10]) == [0] * 10 and (tok[:10] != 0).all()
+    assert list(st[10:]) == [1] * 10                       # BLOCKED once nowCalls == count
+    st, _ = o.concurrent_replay(_events(oracle_mod, [1] * 10, tokens=tok[:10]), np.zeros(10))
+    assert list(st) == [6] * 10                            # RELEASE_OK
+    assert o.concurrent_now_calls(0) == 0 and o.concurrent_token_count() == 0
+    st, _ = o.concurrent_replay(_events(oracle_mod, [1], tokens=tok[:1]), np.zeros(1))
+    assert list(st) == [7]                                 # ALREADY_RELEASE
+    o.concurrent_replay(_events(oracle_mod, [0] * 10), np.arange(100, 110))
+    assert o.concurrent_expire_all() == 10
+    assert o.concurrent_now_calls(0) == 0 and o.concurrent_token_count() == 0
+    # validation (DefaultTokenService.java:64-75, 89-91): no address, bad id, count <= 0, unknown rule
+    st, _ = o.concurrent_replay(np.concatenate([_events(oracle_mod, [0], flags=0), _events(oracle_mod, [0], flow_idx=-2),
+                                                _events(oracle_mod, [0], acquire=0), _events(oracle_mod, [0], flow_idx=-1)]),
+                                np.arange(4))
+    assert list(st) == [-4, -4, -4, 3]
+
+
+@pytest.mark.gpu
+def test_gpu_reference_sequence():
+    import sentinel_amd as sa
+    svc = sa.GpuTokenService(0)
+    svc.load_flow_rules([sa.FlowRule(count=10, cluster_config=sa.ClusterFlowConfig(flow_id=111, threshold_type=1))])
+    res = [svc.request_concurrent_token("127.0.0.1", 111, 1) for _ in range(20)]
+    assert all(r.status == 0 and r.token_id != 0 for r in res[:10])
+    assert all(r.status == 1 for r in res[10:])
+    assert len({r.token_id for r in res[:10]}) == 10
+    assert all(svc.release_concurrent_token(r.token_id).status == 6 for r in res[:10])
+    assert svc.concurrent_now_calls(0) == 0 and svc.concurrent_token_count() == 0
+    assert svc.release_concurrent_token(res[0].token_id).status == 7
+    assert svc.release_concurrent_token(None) is None
+    for _ in range(10):
+        svc.request_concurrent_token("127.0.0.1", 111, 1)
+    assert svc.concurrent_expire(1000) == 10
+    assert svc.concurrent_now_calls(0) == 0 and svc.concurrent_token_count() == 0
+    assert svc.request_concurrent_token("", 111, 1).status == -4
+    assert svc.request_concurrent_token("a", 999, 1).status == 3
+
+
+@pytest.mark.gpu
+def test_gpu_concurrent_batches_match_oracle(oracle_mod):
+    import sentinel_amd as sa
+    from sentinel_amd.token_service import ServerNamespace
+    rng = np.random.default_rng(71)
+    F = 400
+
+    def make_rules(ids):
+        return [_rule(int(f), float(rng.integers(1, 12)), int(rng.integers(0, 2))) for f in ids]
+    rules = make_rules(np.arange(1, F + 1))
+    svc = sa.GpuTokenService(0)
+    svc.set_namespaces([ServerNamespace(connected_count=3)])
+    svc.load_flow_rules([sa.FlowRule(count=r["count"], cluster_config=sa.ClusterFlowConfig(
+        flow_id=r["flow_id"], threshold_type=r["threshold_type"])) for r in rules])
+    orc = oracle_mod.TokenServiceOracle(rules, namespaces=[dict(connected_count=3)])
+    outstanding = []
+    for b in range(12):
+        if b == 6:   # reload: flows 1..100 removed, 401..450 added, the rest kept (nowCalls carried)
+            rules = rules[100:] + make_rules(np.arange(F + 1, F + 51))
+            svc.load_flow_rules([sa.FlowRule(count=r["count"], cluster_config=sa.ClusterFlowConfig(
+                flow_id=r["flow_id"], threshold_type=r["threshold_type"])) for r in rules])
+            orc.reload_flow_rules(rules)
+        n = int(rng.integers(2000, 6000))
+        kind = (rng.random(n) < 0.35).astype(np.int32)
+        if not outstanding:
+            kind[:] = 0
+        fidx = T.zipf_indices(len(rules), 1.1, n, rng)
+        acq = rng.integers(1, 4, size=n).astype(np.int32)
+        flags = (rng.random(n) > 0.01).astype(np.uint32)
+        tok = np.zeros(n, np.int64)
+        rel = np.nonzero(kind == 1)[0]
+        if len(rel):
+            pick = rng.integers(0, len(outstanding), size=len(rel))
+            tok[rel] = np.array(outstanding, np.int64)[pick]     # repeats -> ALREADY_RELEASE
+            tok[rel[::53]] = 12345                               # never issued
+        fidx[::211] = -1                                         # unknown rule
+        st_g, tok_g = svc.submit_concurrent_batch_host(fidx, acq, tok, kind, flags)
+        ev = np.zeros(n, dtype=orc.CONC_EVENT)
+        ev["flow_idx"], ev["acquire"], ev["token_id"], ev["kind"], ev["flags"] = fidx, acq, tok, kind, flags
+        st_o, tok_o = orc.concurrent_replay(ev, tok_g)
+        bad = np.nonzero(st_g != st_o)[0]
+        assert len(bad) == 0, (b, len(bad), bad[:5], st_g[bad[:5]], st_o[bad[:5]], kind[bad[:5]])
+        ok = st_g == 0
+        assert (tok_g[ok] != 0).all() and len(np.unique(tok_g[ok])) == int(ok.sum())
+        released = set(tok[(kind == 1) & (st_g == 6)].tolist())
+        outstanding = [t for t in outstanding if t not in released] + tok_g[ok].tolist()
+        for f in range(0, len(rules), 7):
+            assert svc.concurrent_now_calls(f) == orc.concurrent_now_calls(f), (b, f)
+        assert svc.concurrent_token_count() == orc.concurrent_token_count()
+        if b in (3, 9) and svc.concurrent_token_count() <= 1000:
+            assert svc.concurrent_expire(1000) == orc.concurrent_expire_all()
+            outstanding = []
+    assert {0, 1, 3, 6, 7, -4} <= set(np.unique(st_o).tolist()) | {6, 7}
