@@ -31,6 +31,7 @@
 #include "common.hpp"
 #include "concurrent.hpp"
 #include "param_rules.hpp"
+#include "partition.hpp"
 #include <random>
 #include "scan_sort.hpp"
 
@@ -284,6 +285,7 @@ struct sentinel_engine {
     bool verdict_nt = false;   // SENTINEL_VERDICT_NT=1: non-temporal verdict stores
     bool use_lookback = true;  // SENTINEL_SCAN=3pass selects the three-kernel scan
     bool fused_segments = true; // SENTINEL_SEGMENTS=split selects heads -> scan -> mark
+    int flow_path = 0;         // SENTINEL_FLOW_PATH: 0 auto, 1 sorted (global radix sort), 2 partition-local
     bool diag_linear = false;  // SENTINEL_DIAG_LINEAR=1: verdicts in sorted order (cost diagnostic, wrong output)   // SENTINEL_PROCESS: 0 reg (default), 1 group, 2 thread-in-memory
     int64_t flow_state_words = 0;
 
@@ -369,6 +371,8 @@ struct sentinel_engine {
     DevBuf w_fkey, w_lkey, w_skey, w_sval, w_ktmp, w_vtmp, w_fhist, w_lhist, w_parts, w_segid, w_bad, w_hep,
         w_hacq, w_segstart, w_segkey, w_segep, w_segacq, w_het, w_done, w_s0, w_k, w_counters;
     DevBuf w_vslot;                    // slot of every value of a param batch
+    DevBuf w_pkey;                     // partition path: 16-bit local flow keys in range order
+    DevBuf w_runs;                     // partition path: run starts, run flows, runs per range
     DevBuf io_ev, io_fl, io_out, io_vals;
     int64_t ws_cap = 0;
 
@@ -380,7 +384,8 @@ struct sentinel_engine {
             rc |= b->ensure(c * 4);
         for (DevBuf *b : {&w_hep, &w_segep, &w_s0, &w_sval, &w_vtmp}) rc |= b->ensure(c * 8);
         for (DevBuf *b : {&w_bad, &w_het, &w_done}) rc |= b->ensure(c);
-        rc |= w_fhist.ensure((size_t)hist_words(c, MAX_PASSES) * 4);
+        rc |= w_fhist.ensure((size_t)(hist_words(c, MAX_PASSES) + 64) * 4);
+        rc |= w_pkey.ensure((size_t)c * 2);
         rc |= w_lhist.ensure((size_t)hist_words(c, MAX_PASSES) * 4);
         rc |= w_parts.ensure((size_t)(scan_parts(std::max<int64_t>(c, hist_words(c, MAX_PASSES))) + 16) * 8);
         rc |= w_segstart.ensure((c + 1) * 4);
@@ -786,6 +791,63 @@ int sentinel_engine::rebuild_limiters() {
     return rebuild_routes();
 }
 
+// Partition-local flow path (partition.hpp): prep + range histogram, scan, one multi-split pass,
+// one fused decide pass per flow range.
+template <int NMAX>
+static void launch_part_runs(sentinel_engine_t *e, unsigned nparts, const KeyTable &FT, const uint32_t *offsets,
+                             int64_t nb, int lb, const EventSrc &src, const Verdicts &V, int64_t n, hipStream_t s) {
+    const dim3 grid(nparts, (unsigned)(((1u << lb) + 255) / 256));
+    e->launch("part_runs", n, s, [&] {
+        k_part_runs<NMAX><<<grid, 256, 0, s>>>(FT, e->w_vtmp.as<uint64_t>(), offsets, nb, lb, e->w_runs.as<uint32_t>(),
+                                               e->w_runs.as<uint32_t>() + ((size_t)nparts << lb),
+                                               e->w_runs.as<uint32_t>() + ((size_t)nparts << (lb + 1)), src, V);
+    });
+}
+
+static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
+                            hipStream_t s) {
+    const int32_t F = (int32_t)e->rules.size();
+    const int fbits = bits_for(F);
+    const uint32_t finvalid = ((uint32_t)1 << fbits) - 1;
+    const int lb = std::max(0, fbits - PART_MAX_BITS);
+    const int32_t nparts = (int32_t)(((int64_t)F + (1 << lb) - 1) >> lb);
+    const int pbits = bits_for(nparts - 1 > 0 ? nparts - 1 : 1);
+    const int64_t nb = sort_blocks(n);
+    uint32_t *fkey = e->w_fkey.as<uint32_t>();
+    uint32_t *hist = e->w_fhist.as<uint32_t>();
+    const int64_t hn = (int64_t)nparts * nb + 1;           // digit-major histograms + the total
+    HIP_OK(hipMemsetAsync(hist + hn - 1, 0, 4, s));
+    e->launch("part_prep", n, s, [&] {
+        k_part_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
+            n, ev, F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, fkey, finvalid, lb, hist, nb, nparts);
+    });
+    e->scan(hist, hn, true, s);
+    const EventSrc src{ev, nullptr, fl, false};
+    e->launch("part_scatter", n, s, [&] {
+        k_part_scatter<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(fkey, src, e->w_pkey.as<uint16_t>(),
+                                                                         e->w_sval.as<uint64_t>(), n, finvalid, lb, pbits,
+                                                                         hist, nb, nparts);
+    });
+    int rc = e->w_runs.ensure((((size_t)nparts << (lb + 1)) + (size_t)nparts) * 4);
+    if (rc) return rc;
+    uint32_t *runs = e->w_runs.as<uint32_t>();
+    e->launch("part_sort", n, s, [&] {
+        k_part_sort<<<(unsigned)nparts, PSORT_THREADS, 0, s>>>(e->w_pkey.as<uint16_t>(), e->w_sval.as<uint64_t>(),
+                                                               e->w_vtmp.as<uint64_t>(), hist, nb, lb, runs,
+                                                               runs + ((size_t)nparts << lb),
+                                                               runs + ((size_t)nparts << (lb + 1)));
+    });
+    const KeyTable FT = e->table(e->ft, NEV, 0);
+    const Verdicts V{out, fkey, finvalid};
+    const int mx = e->flow_max_n;
+    if (mx <= 2) launch_part_runs<2>(e, (unsigned)nparts, FT, hist, nb, lb, src, V, n, s);
+    else if (mx <= 4) launch_part_runs<4>(e, (unsigned)nparts, FT, hist, nb, lb, src, V, n, s);
+    else if (mx <= 10) launch_part_runs<10>(e, (unsigned)nparts, FT, hist, nb, lb, src, V, n, s);
+    else launch_part_runs<16>(e, (unsigned)nparts, FT, hist, nb, lb, src, V, n, s);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
 static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
                        hipStream_t s) {
     if (n <= 0) return 0;
@@ -796,6 +858,11 @@ static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const u
     const int fbits = bits_for(F);
     const uint32_t finvalid = ((uint32_t)1 << fbits) - 1;
     const bool lim = e->nlimiters > 0 && !e->flow_plain;
+    // partition-local path: no namespace limiter (a limiter couples flows), windows of <= 16 buckets,
+    // <= 2^20 flows; auto picks it for large flow tables (a hot flow serialises its range's workgroup)
+    const bool part = !lim && F > 0 && e->flow_max_n <= 16 && bits_for(F) <= 2 * PART_MAX_BITS &&
+                      (e->flow_path == 2 || (e->flow_path == 0 && F >= 32768));
+    if (part) return submit_flow_part(e, n, ev, fl, out, s);
     const int lbits = bits_for(e->nlimiters);
     const uint32_t linvalid = ((uint32_t)1 << lbits) - 1;
     uint32_t *fkey = e->w_fkey.as<uint32_t>();
@@ -1001,6 +1068,10 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
     if (const char *c = getenv("SENTINEL_VERDICT_NT")) e->verdict_nt = std::string(c) == "1";
     if (const char *c = getenv("SENTINEL_SCAN")) e->use_lookback = std::string(c) != "3pass";
     if (const char *c = getenv("SENTINEL_DIAG_LINEAR")) e->diag_linear = std::string(c) == "1";
+    if (const char *c = getenv("SENTINEL_FLOW_PATH")) {
+        const std::string v(c);
+        e->flow_path = v == "sorted" ? 1 : v == "partition" ? 2 : 0;
+    }
     if (const char *c = getenv("SENTINEL_SEGMENTS")) e->fused_segments = std::string(c) != "split";
     if (const char *c = getenv("SENTINEL_PARAM_CAPACITY")) {
         uint64_t v = strtoull(c, nullptr, 10);
@@ -1038,7 +1109,7 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
                       &e->d_lrule_dur, &e->d_lrule_w, &e->d_lrule_rcp, &e->d_lrule_kind, &e->d_lhot_keys,
                       &e->d_lhot_tok, &e->d_ltable, &e->d_lstate, &e->d_now, &e->d_conc_thr, &e->d_seg1_w,
                       &e->d_seg1_rcp, &e->d_seg1_kind, &e->d_tok_keys, &e->d_tok_fid, &e->d_tok_fidx,
-                      &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket})
+                      &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->w_pkey, &e->w_runs})
         b->release();
     (void)hipStreamDestroy(e->stream);
     delete e;

@@ -1,0 +1,404 @@
+// partition.hpp -- the partition-local flow path (gfx950): one scatter pass + one fused
+// decide pass, instead of a full 3-pass radix sort followed by segment / process / verdict kernels.
+//
+// A flow's events only interact with each other (ClusterFlowChecker reads and writes one flow's
+// ClusterMetric), so the batch only needs to be grouped by flow, in arrival order, not globally
+// sorted.  The flow index space is cut into P <= 1024 contiguous ranges of 2^lb flows:
+//
+//   k_part_prep     validation + routing (as k_flow_prep) and per-tile histograms of the range
+//                   digit d = flow >> lb (invalid events are decided here and leave the pipeline)
+//   scan            exclusive scan of the digit-major histograms -> every tile's output offsets
+//   k_part_scatter  stable multi-split of the events into their ranges (one pass, LDS-staged
+//                   contiguous runs); writes the 16-bit local flow key and the 64-bit sorted value
+//   k_part_sort     one workgroup per range: stable counting sort of the range by local flow key
+//                   (any range size: chunks of 4096 ranked with ballots, running bin offsets) and
+//                   the run record {start, flow} of every flow present
+//   k_part_runs     one lane per flow run, decided exactly like k_process_reg (window header in
+//                   VGPRs, closed-form epoch segments, sequential fallback); the lane writes its
+//                   run's verdicts straight to their arrival positions
+//
+// Global order after k_part_sort = (range, local key, arrival) = the order the 3-pass radix sort
+// produces, in 1 scatter pass + 1 in-range pass.  A hot flow makes one lane long (it walks its
+// events), which is why the engine uses this path for large flow tables (engine.hip, flow_path).
+#pragma once
+
+#include "admission.hpp"
+
+namespace sentinel {
+
+constexpr int PART_MAX_BITS = 10;                  // <= 1024 ranges, <= 1024 flows per range
+constexpr int PART_BINS = 1 << PART_MAX_BITS;
+
+// Validation + routing as k_flow_prep; histogram of the range digit of valid events only.
+__global__ __launch_bounds__(SORT_THREADS) void k_part_prep(int64_t n, const Event *__restrict__ ev, int32_t nflows,
+                                                            const int32_t *__restrict__ route,
+                                                            uint64_t *__restrict__ out, uint32_t *__restrict__ fkey,
+                                                            uint32_t finvalid, int lb, uint32_t *__restrict__ hist,
+                                                            int64_t nblocks, int32_t nparts) {
+    __shared__ uint32_t h[PART_BINS];
+    for (int d = threadIdx.x; d < PART_BINS; d += SORT_THREADS) h[d] = 0;
+    __syncthreads();
+    const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
+#pragma unroll 4
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
+        if (i >= n) break;
+        const Event e = ev[i];
+        int st = 127;
+        uint32_t k = finvalid;
+        if (e.idx == SENTINEL_IDX_BAD_ID || e.acquire <= 0) st = ST_BAD_REQUEST;      // DTS:38-40
+        else if (e.idx < 0 || e.idx >= nflows) st = ST_NO_RULE_EXISTS;               // DTS:42-45
+        else if (route && route[e.idx] == ROUTE_TOO_MANY) st = ST_TOO_MANY_REQUEST;  // namespace == null (CFC:50-53)
+        else if (e.ts < 0) st = ST_FAIL;                                              // reference: NPE in LeapArray
+        else k = (uint32_t)e.idx;
+        fkey[i] = k;
+        if (st == 127) atomicAdd(&h[k >> lb], 1u);
+        else put_verdict(out, (uint32_t)i, st, 0, 0);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < nparts; d += SORT_THREADS) hist[(int64_t)d * nblocks + blockIdx.x] = h[d];
+}
+
+// Stable multi-split of the valid events by range digit (one pass).  Same tiling as k_part_prep;
+// ranking with one 64-bit ballot per digit bit and wave-private LDS counters; the tile is staged
+// in LDS in digit order and written out as contiguous per-range runs.
+__global__ __launch_bounds__(SORT_THREADS) void k_part_scatter(const uint32_t *__restrict__ keys_in, EventSrc src,
+                                                               uint16_t *__restrict__ keys_out,
+                                                               uint64_t *__restrict__ vals_out, int64_t n,
+                                                               uint32_t finvalid, int lb, int pbits,
+                                                               const uint32_t *__restrict__ offsets, int64_t nblocks,
+                                                               int32_t nparts) {
+    __shared__ uint16_t cnt[SORT_WAVES][PART_BINS];
+    __shared__ uint32_t goff[PART_BINS];
+    __shared__ uint32_t loff[PART_BINS];
+    __shared__ uint32_t waves_tot[SORT_WAVES];
+    __shared__ uint16_t skeys[SORT_TILE];
+    __shared__ uint16_t sdig[SORT_TILE];
+    __shared__ uint64_t svals[SORT_TILE];
+    const int wave = threadIdx.x / WAVE;
+    const uint32_t lane = lane_id();
+    for (int d = threadIdx.x; d < PART_BINS; d += SORT_THREADS) {
+#pragma unroll
+        for (int w = 0; w < SORT_WAVES; ++w) cnt[w][d] = 0;
+        goff[d] = d < nparts ? offsets[(int64_t)d * nblocks + blockIdx.x] : 0u;
+    }
+    __syncthreads();
+    const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
+    const int64_t base = tile0 + (int64_t)wave * (SORT_ITEMS * WAVE);
+    const int64_t T0 = src.t0();
+    uint32_t key[SORT_ITEMS], rank[SORT_ITEMS];
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const int64_t i = base + j * WAVE + lane;
+        key[j] = i < n ? keys_in[i] : finvalid;
+    }
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const bool valid = key[j] != finvalid;
+        const uint32_t d = valid ? key[j] >> lb : 0u;
+        uint64_t peers = __ballot(valid);
+        for (int b = 0; b < pbits; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bal = __ballot(valid && bit);
+            peers &= bit ? bal : ~bal;
+        }
+        uint32_t r = 0;
+        if (valid) r = cnt[wave][d] + mask_rank(peers);
+        __builtin_amdgcn_wave_barrier();
+        if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane) cnt[wave][d] += (uint16_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        rank[j] = valid ? r : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    // per digit: exclusive over waves (in place), then an exclusive scan over digits -> loff
+    constexpr int DPT = PART_BINS / SORT_THREADS;   // digits per thread
+    uint32_t dtot[DPT > 0 ? DPT : 1];
+    uint32_t mine = 0;
+#pragma unroll
+    for (int q = 0; q < DPT; ++q) {
+        const int d = threadIdx.x * DPT + q;
+        uint32_t run = 0;
+#pragma unroll
+        for (int w = 0; w < SORT_WAVES; ++w) {
+            const uint32_t c = cnt[w][d];
+            cnt[w][d] = (uint16_t)run;
+            run += c;
+        }
+        dtot[q] = run;
+        mine += run;
+    }
+    uint32_t total;
+    uint32_t pre = block_exclusive_scan(mine, waves_tot, &total);
+#pragma unroll
+    for (int q = 0; q < DPT; ++q) {
+        loff[threadIdx.x * DPT + q] = pre;
+        pre += dtot[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        if (rank[j] == 0xFFFFFFFFu) continue;
+        const int64_t i = base + j * WAVE + lane;
+        const uint32_t d = key[j] >> lb;
+        const uint32_t p = loff[d] + cnt[wave][d] + rank[j];
+        skeys[p] = (uint16_t)(key[j] & ((1u << lb) - 1));
+        sdig[p] = (uint16_t)d;
+        svals[p] = src.pack((uint32_t)i, T0);
+    }
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < total; p += SORT_THREADS) {
+        const uint32_t d = sdig[p];
+        const uint32_t dst = goff[d] + p - loff[d];
+        if (dst >= (uint64_t)n) continue;          // guard: a corrupt offset must never write out of bounds
+        keys_out[dst] = skeys[p];
+        vals_out[dst] = svals[p];
+    }
+}
+
+// One flow's run of sorted events [q0, q1) (arrival order): closed-form segments with the window
+// header in VGPRs, sequential fallback on global memory (as k_process_reg), verdicts written to
+// the arrival positions.
+template <int NMAX>
+__device__ inline void part_run(const KeyTable &T, uint32_t key, const uint64_t *s_val, uint32_t q0, uint32_t q1,
+                                const EventSrc &src, const Verdicts &V, int64_t T0) {
+    const KeyState ks = key_state(T, key);
+    const int nsc = ks.n;
+    const uint8_t kind = T.kind[key];
+    const double thr = T.thr[key];
+    const double I_s = T.I_s[key];
+    const int32_t w = T.w[key];
+    const double rcp = T.rcp_w[key];
+    int64_t ep[NMAX], ps[NMAX];
+    uint32_t dirty = 0;
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+        if (j < nsc) {
+            const longlong2 v = *reinterpret_cast<const longlong2 *>(ks.base + 2 * j);
+            ep[j] = v.x;
+            ps[j] = v.y;
+        } else {
+            ep[j] = EPOCH_ABSENT;
+            ps[j] = 0;
+        }
+    }
+    bool occ_pending = ks.seven && kind == KIND_CLUSTER && T.has_occ[key];
+    uint32_t q = q0;
+    while (q < q1) {
+        int64_t t;
+        int32_t a;
+        bool prio;
+        src.unpack(s_val[q], T0, t, a, prio);
+        const int64_t E = epoch_of(t, w, rcp);
+        bool het = prio && kind == KIND_CLUSTER;
+        uint32_t q2 = q + 1;
+        for (; q2 < q1; ++q2) {                       // the segment: same epoch
+            int64_t t2;
+            int32_t a2;
+            bool p2;
+            src.unpack(s_val[q2], T0, t2, a2, p2);
+            if (epoch_of(t2, w, rcp) != E) break;
+            het |= a2 != a || (p2 && kind == KIND_CLUSTER);
+        }
+        bool slow = het || occ_pending;
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j) slow |= (ep[j] != EPOCH_ABSENT && ep[j] > E);
+        if (slow) {
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j)
+                if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.base + 2 * j) = longlong2{ep[j], ps[j]};
+            dirty = 0;
+            for (uint32_t i = q; i < q2; ++i) {
+                const uint32_t seq = (uint32_t)s_val[i] & SEQ_MASK;
+                int64_t tt;
+                int32_t aa;
+                uint8_t fl;
+                src.load(seq, tt, aa, fl);
+                seq_event(T, key, ks, E, aa, fl, seq, V);
+            }
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j)
+                if (j < nsc) { ep[j] = ks.ep(j); ps[j] = ks.cnt(EV_PASS, j); }
+            occ_pending = ks.seven && kind == KIND_CLUSTER && T.has_occ[key];
+            q = q2;
+            continue;
+        }
+        const uint32_t len = q2 - q;
+        const int slot = (int)(E % nsc);
+        bool fresh = false;
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j)
+            if (j == slot && ep[j] != E) { fresh = true; ep[j] = E; ps[j] = 0; }
+        int64_t s0 = 0;
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j)
+            if (ep[j] != EPOCH_ABSENT && ep[j] > E - nsc) s0 = wrap_add(s0, ps[j]);
+        uint32_t lo = 0, hi = len;                      // K = first p with !admits(S0 + p*a)
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            if (admits(kind, thr, I_s, wrap_add(s0, wrap_mul((int64_t)mid, a)), a)) lo = mid + 1;
+            else hi = mid;
+        }
+        const uint32_t K = lo;
+        const int64_t nb = (int64_t)(len - K);
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j)
+            if (j == slot) { ps[j] = wrap_add(ps[j], wrap_mul((int64_t)K, a)); dirty |= 1u << j; }
+        if (ks.seven) {
+            int64_t *r = ks.rest(slot);
+            int64_t blk = 0, preq = 0, breq = 0;
+            if (!fresh) { blk = r[0]; preq = r[1]; breq = r[2]; }
+            *reinterpret_cast<longlong2 *>(r) = longlong2{wrap_add(blk, wrap_mul(nb, a)), wrap_add(preq, (int64_t)K)};
+            r[2] = wrap_add(breq, nb);
+            if (fresh) {
+                *reinterpret_cast<longlong2 *>(r + 3) = longlong2{0, 0};
+                *reinterpret_cast<longlong2 *>(r + 5) = longlong2{0, 0};
+            }
+        }
+        for (uint32_t k = 0; k < len; ++k) {
+            const uint32_t seq = (uint32_t)s_val[q + k] & SEQ_MASK;
+            uint64_t v;
+            if (k < K) v = pack_verdict(ST_OK, java_d2i(remaining_of(thr, I_s, wrap_add(s0, wrap_mul((int64_t)k, a)), a)), 0);
+            else v = pack_verdict(ST_BLOCKED, 0, 0);
+            V.out[seq] = v;
+        }
+        q = q2;
+    }
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j)
+        if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.base + 2 * j) = longlong2{ep[j], ps[j]};
+}
+
+// One workgroup per flow range: a stable counting sort of the range's events by local flow key
+// (histogram -> bin offsets -> chunks of 4096 ranked with ballots in arrival order, each event
+// written to its final slot inside the range; the range's ~100 KB stay L2-resident) and the run
+// records {start, flow} of every flow present.  Any range size works: chunks only carry running
+// per-bin offsets, nothing has to fit in LDS.
+constexpr int PSORT_THREADS = 512;
+constexpr int PSORT_WAVES = PSORT_THREADS / WAVE;
+constexpr int PSORT_ITEMS = 8;
+constexpr int PSORT_CHUNK = PSORT_THREADS * PSORT_ITEMS;
+
+__global__ __launch_bounds__(PSORT_THREADS) void k_part_sort(const uint16_t *__restrict__ pkey,
+                                                             const uint64_t *__restrict__ pval,
+                                                             uint64_t *__restrict__ sval,
+                                                             const uint32_t *__restrict__ offsets, int64_t nblocks,
+                                                             int lb, uint32_t *__restrict__ run_start,
+                                                             uint32_t *__restrict__ run_flow,
+                                                             uint32_t *__restrict__ nruns) {
+    __shared__ uint32_t base[PART_BINS];                 // per-bin counts, then running slot offsets
+    __shared__ uint16_t cnt[PSORT_WAVES][PART_BINS];
+    __shared__ uint32_t waves_tot[PSORT_WAVES];
+    const int p = blockIdx.x;
+    const uint32_t pstart = offsets[(int64_t)p * nblocks];
+    const uint32_t pend = offsets[(int64_t)(p + 1) * nblocks];
+    const int wave = threadIdx.x / WAVE;
+    const uint32_t lane = lane_id();
+    const uint32_t R = 1u << lb;
+    for (int d = threadIdx.x; d < PART_BINS; d += PSORT_THREADS) base[d] = 0;
+    __syncthreads();
+    for (uint32_t q = pstart + threadIdx.x; q < pend; q += PSORT_THREADS) atomicAdd(&base[pkey[q]], 1u);
+    __syncthreads();
+    constexpr int BPT = PART_BINS / PSORT_THREADS;
+    uint32_t c[BPT], tot = 0, nz = 0;
+#pragma unroll
+    for (int k = 0; k < BPT; ++k) {
+        c[k] = base[threadIdx.x * BPT + k];
+        tot += c[k];
+        nz += c[k] != 0;
+    }
+    uint32_t all, nall;
+    uint32_t at = block_exclusive_scan(tot, waves_tot, &all);
+    uint32_t rn = block_exclusive_scan(nz, waves_tot, &nall);
+#pragma unroll
+    for (int k = 0; k < BPT; ++k) {
+        const uint32_t d = threadIdx.x * BPT + k;
+        base[d] = pstart + at;
+        if (c[k]) {
+            run_start[(uint64_t)p * R + rn] = pstart + at;
+            run_flow[(uint64_t)p * R + rn] = ((uint32_t)p << lb) | d;
+            ++rn;
+        }
+        at += c[k];
+    }
+    if (threadIdx.x == 0) nruns[p] = nall;
+    __syncthreads();
+    for (uint32_t c0 = pstart; c0 < pend; c0 += PSORT_CHUNK) {
+        const uint32_t cn = min((uint32_t)PSORT_CHUNK, pend - c0);
+        for (int d = threadIdx.x; d < PSORT_WAVES * PART_BINS; d += PSORT_THREADS) (&cnt[0][0])[d] = 0;
+        __syncthreads();
+        uint32_t key[PSORT_ITEMS], rank[PSORT_ITEMS];
+        uint64_t val[PSORT_ITEMS];
+        const uint32_t b0 = (uint32_t)wave * (PSORT_ITEMS * WAVE);
+#pragma unroll
+        for (int j = 0; j < PSORT_ITEMS; ++j) {
+            const uint32_t qq = b0 + j * WAVE + lane;
+            const bool valid = qq < cn;
+            key[j] = valid ? pkey[c0 + qq] : 0u;
+            val[j] = valid ? pval[c0 + qq] : 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < PSORT_ITEMS; ++j) {
+            const bool valid = b0 + j * WAVE + lane < cn;
+            const uint32_t d = key[j];
+            uint64_t peers = __ballot(valid);
+            for (int b = 0; b < lb; ++b) {
+                const bool bit = (d >> b) & 1u;
+                const uint64_t bal = __ballot(valid && bit);
+                peers &= bit ? bal : ~bal;
+            }
+            uint32_t r = 0;
+            if (valid) r = cnt[wave][d] + mask_rank(peers);
+            __builtin_amdgcn_wave_barrier();
+            if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane) cnt[wave][d] += (uint16_t)__popcll(peers);
+            __builtin_amdgcn_wave_barrier();
+            rank[j] = valid ? r : 0xFFFFFFFFu;
+        }
+        __syncthreads();
+        uint32_t dt[BPT];
+#pragma unroll
+        for (int k = 0; k < BPT; ++k) {
+            const int d = threadIdx.x * BPT + k;
+            uint32_t run = 0;
+            if (d < (int)R) {
+#pragma unroll
+                for (int w = 0; w < PSORT_WAVES; ++w) {
+                    const uint32_t x = cnt[w][d];
+                    cnt[w][d] = (uint16_t)run;
+                    run += x;
+                }
+            }
+            dt[k] = run;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PSORT_ITEMS; ++j) {
+            if (rank[j] == 0xFFFFFFFFu) continue;
+            const uint32_t d = key[j];
+            sval[base[d] + cnt[wave][d] + rank[j]] = val[j];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < BPT; ++k) base[threadIdx.x * BPT + k] += dt[k];
+        __syncthreads();
+    }
+}
+
+// One lane per flow run (grid: ranges x ceil(2^lb / 256)): the run's events are contiguous in
+// arrival order in `sval`.
+template <int NMAX>
+__global__ __launch_bounds__(256) void k_part_runs(KeyTable T, const uint64_t *__restrict__ sval,
+                                                   const uint32_t *__restrict__ offsets, int64_t nblocks, int lb,
+                                                   const uint32_t *__restrict__ run_start,
+                                                   const uint32_t *__restrict__ run_flow,
+                                                   const uint32_t *__restrict__ nruns, EventSrc src, Verdicts V) {
+    const int p = blockIdx.x;
+    const uint32_t r = blockIdx.y * blockDim.x + threadIdx.x;
+    const uint32_t nr = nruns[p];
+    if (r >= nr) return;
+    const uint64_t i = ((uint64_t)p << lb) + r;
+    const uint32_t q0 = run_start[i];
+    const uint32_t q1 = r + 1 < nr ? run_start[i + 1] : offsets[(int64_t)(p + 1) * nblocks];
+    part_run<NMAX>(T, run_flow[i], sval, q0, q1, src, V, src.t0());
+}
+
+}  // namespace sentinel

@@ -12,6 +12,14 @@ from sentinel_amd import trace as T
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["sorted", "partition"])
+def flow_path(request, monkeypatch):
+    """Every flow parity case runs on both flow pipelines: the global radix sort and the
+    partition-local path (SENTINEL_FLOW_PATH is read when an engine is created)."""
+    monkeypatch.setenv("SENTINEL_FLOW_PATH", request.param)
+    return request.param
+
+
 def _engine(rules, namespaces=None, exceed=1.0, occ=1.0):
     import sentinel_amd as sa
     from sentinel_amd.token_service import ServerNamespace
