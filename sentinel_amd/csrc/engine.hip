@@ -286,6 +286,11 @@ struct sentinel_engine {
     bool use_lookback = true;  // SENTINEL_SCAN=3pass selects the three-kernel scan
     bool fused_segments = true; // SENTINEL_SEGMENTS=split selects heads -> scan -> mark
     int flow_path = 0;         // SENTINEL_FLOW_PATH: 0 auto, 1 sorted (global radix sort), 2 partition-local
+    // auto policy: the partition path unless the last partition batch was skewed (its largest flow
+    // range > 8x the mean): then the sorted path for the next 1024 batches, then one probe again
+    DevBuf d_part_stat;
+    unsigned long long *h_part_stat = nullptr;   // pinned mirror, written asynchronously after each batch
+    int64_t flow_batches = 0, sorted_until = -1;
     bool diag_linear = false;  // SENTINEL_DIAG_LINEAR=1: verdicts in sorted order (cost diagnostic, wrong output)   // SENTINEL_PROCESS: 0 reg (default), 1 group, 2 thread-in-memory
     int64_t flow_state_words = 0;
 
@@ -797,10 +802,17 @@ template <int NMAX>
 static void launch_part_runs(sentinel_engine_t *e, unsigned nparts, const KeyTable &FT, const uint32_t *offsets,
                              int64_t nb, int lb, const EventSrc &src, const Verdicts &V, int64_t n, hipStream_t s) {
     const dim3 grid(nparts, (unsigned)(((1u << lb) + 255) / 256));
+    uint32_t *runs = e->w_runs.as<uint32_t>();
+    uint32_t *nlong = runs + ((size_t)nparts << (lb + 1)) + nparts;
+    uint32_t *long_runs = nlong + 1;
+    (void)hipMemsetAsync(nlong, 0, 4, s);
     e->launch("part_runs", n, s, [&] {
-        k_part_runs<NMAX><<<grid, 256, 0, s>>>(FT, e->w_vtmp.as<uint64_t>(), offsets, nb, lb, e->w_runs.as<uint32_t>(),
-                                               e->w_runs.as<uint32_t>() + ((size_t)nparts << lb),
-                                               e->w_runs.as<uint32_t>() + ((size_t)nparts << (lb + 1)), src, V);
+        k_part_runs<NMAX><<<grid, 256, 0, s>>>(FT, e->w_vtmp.as<uint64_t>(), offsets, nb, lb, runs,
+                                               runs + ((size_t)nparts << lb), runs + ((size_t)nparts << (lb + 1)), src,
+                                               V, long_runs, nlong);
+    });
+    e->launch("part_long", n, s, [&] {   // hot flows (runs > LONG_RUN events): a workgroup each
+        k_part_long<NMAX><<<256, PL_THREADS, 0, s>>>(FT, e->w_vtmp.as<uint64_t>(), long_runs, nlong, src, V);
     });
 }
 
@@ -828,15 +840,25 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
                                                                          e->w_sval.as<uint64_t>(), n, finvalid, lb, pbits,
                                                                          hist, nb, nparts);
     });
-    int rc = e->w_runs.ensure((((size_t)nparts << (lb + 1)) + (size_t)nparts) * 4);
+    // run starts + run flows (2^lb per range), runs per range, long-run count + {q0, q1, flow} records
+    int rc = e->w_runs.ensure((((size_t)nparts << (lb + 1)) + (size_t)nparts + 1 + 3 * ((size_t)n / LONG_RUN + 2)) * 4);
     if (rc) return rc;
     uint32_t *runs = e->w_runs.as<uint32_t>();
+    if (!e->d_part_stat.p) {
+        rc = e->d_part_stat.ensure(8);
+        if (rc) return rc;
+        HIP_OK(hipHostMalloc((void **)&e->h_part_stat, 8, 0));
+        *e->h_part_stat = 0;
+    }
+    unsigned long long *stat = e->d_part_stat.as<unsigned long long>();
+    HIP_OK(hipMemsetAsync(stat, 0, 8, s));
     e->launch("part_sort", n, s, [&] {
         k_part_sort<<<(unsigned)nparts, PSORT_THREADS, 0, s>>>(e->w_pkey.as<uint16_t>(), e->w_sval.as<uint64_t>(),
                                                                e->w_vtmp.as<uint64_t>(), hist, nb, lb, runs,
                                                                runs + ((size_t)nparts << lb),
-                                                               runs + ((size_t)nparts << (lb + 1)));
+                                                               runs + ((size_t)nparts << (lb + 1)), stat);
     });
+    HIP_OK(hipMemcpyAsync(e->h_part_stat, stat, 8, hipMemcpyDeviceToHost, s));
     const KeyTable FT = e->table(e->ft, NEV, 0);
     const Verdicts V{out, fkey, finvalid};
     const int mx = e->flow_max_n;
@@ -860,8 +882,23 @@ static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const u
     const bool lim = e->nlimiters > 0 && !e->flow_plain;
     // partition-local path: no namespace limiter (a limiter couples flows), windows of <= 16 buckets,
     // <= 2^20 flows; auto picks it for large flow tables (a hot flow serialises its range's workgroup)
-    const bool part = !lim && F > 0 && e->flow_max_n <= 16 && bits_for(F) <= 2 * PART_MAX_BITS &&
-                      (e->flow_path == 2 || (e->flow_path == 0 && F >= 32768));
+    bool part = !lim && F > 0 && e->flow_max_n <= 16 && bits_for(F) <= 2 * PART_MAX_BITS &&
+                (e->flow_path == 2 || (e->flow_path == 0 && F >= 32768));
+    const int64_t batch = e->flow_batches++;
+    if (part && e->flow_path == 0) {
+        if (batch < e->sorted_until) {
+            part = false;
+        } else if (e->h_part_stat) {
+            const int lb = std::max(0, bits_for(F) - PART_MAX_BITS);
+            const int64_t nparts = ((int64_t)F + (1 << lb) - 1) >> lb;
+            const uint64_t seen = *(volatile unsigned long long *)e->h_part_stat;
+            if ((double)seen > 8.0 * (double)n / (double)nparts + 4096.0) {
+                e->sorted_until = batch + 1024;
+                *(volatile unsigned long long *)e->h_part_stat = 0;
+                part = false;
+            }
+        }
+    }
     if (part) return submit_flow_part(e, n, ev, fl, out, s);
     const int lbits = bits_for(e->nlimiters);
     const uint32_t linvalid = ((uint32_t)1 << lbits) - 1;
@@ -1111,6 +1148,8 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
                       &e->d_seg1_rcp, &e->d_seg1_kind, &e->d_tok_keys, &e->d_tok_fid, &e->d_tok_fidx,
                       &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->w_pkey, &e->w_runs})
         b->release();
+    if (e->h_part_stat) (void)hipHostFree(e->h_part_stat);
+    e->d_part_stat.release();
     (void)hipStreamDestroy(e->stream);
     delete e;
     return 0;

@@ -155,80 +155,85 @@ __global__ __launch_bounds__(SORT_THREADS) void k_part_scatter(const uint32_t *_
     }
 }
 
-// One flow's run of sorted events [q0, q1) (arrival order): closed-form segments with the window
-// header in VGPRs, sequential fallback on global memory (as k_process_reg), verdicts written to
-// the arrival positions.
+// A flow's window header {epoch, PASS} x n held in VGPRs while its events are decided in arrival
+// order (the k_process_reg scheme): closed-form homogeneous segments, the reference state machine
+// (seq_event on global memory) for everything else, only dirty pairs written back.
 template <int NMAX>
-__device__ inline void part_run(const KeyTable &T, uint32_t key, const uint64_t *s_val, uint32_t q0, uint32_t q1,
-                                const EventSrc &src, const Verdicts &V, int64_t T0) {
-    const KeyState ks = key_state(T, key);
-    const int nsc = ks.n;
-    const uint8_t kind = T.kind[key];
-    const double thr = T.thr[key];
-    const double I_s = T.I_s[key];
-    const int32_t w = T.w[key];
-    const double rcp = T.rcp_w[key];
+struct FlowWindow {
+    KeyState ks;
+    int nsc;
+    uint8_t kind;
+    double thr, I_s, rcp;
+    int32_t w;
     int64_t ep[NMAX], ps[NMAX];
-    uint32_t dirty = 0;
+    uint32_t dirty;
+    bool occ_pending;
+
+    __device__ inline void load(const KeyTable &T, uint32_t key) {
+        ks = key_state(T, key);
+        nsc = ks.n;
+        kind = T.kind[key];
+        thr = T.thr[key];
+        I_s = T.I_s[key];
+        w = T.w[key];
+        rcp = T.rcp_w[key];
+        dirty = 0;
 #pragma unroll
-    for (int j = 0; j < NMAX; ++j) {
-        if (j < nsc) {
-            const longlong2 v = *reinterpret_cast<const longlong2 *>(ks.base + 2 * j);
-            ep[j] = v.x;
-            ps[j] = v.y;
-        } else {
-            ep[j] = EPOCH_ABSENT;
-            ps[j] = 0;
-        }
-    }
-    bool occ_pending = ks.seven && kind == KIND_CLUSTER && T.has_occ[key];
-    uint32_t q = q0;
-    while (q < q1) {
-        int64_t t;
-        int32_t a;
-        bool prio;
-        src.unpack(s_val[q], T0, t, a, prio);
-        const int64_t E = epoch_of(t, w, rcp);
-        bool het = prio && kind == KIND_CLUSTER;
-        uint32_t q2 = q + 1;
-        for (; q2 < q1; ++q2) {                       // the segment: same epoch
-            int64_t t2;
-            int32_t a2;
-            bool p2;
-            src.unpack(s_val[q2], T0, t2, a2, p2);
-            if (epoch_of(t2, w, rcp) != E) break;
-            het |= a2 != a || (p2 && kind == KIND_CLUSTER);
-        }
-        bool slow = het || occ_pending;
-#pragma unroll
-        for (int j = 0; j < NMAX; ++j) slow |= (ep[j] != EPOCH_ABSENT && ep[j] > E);
-        if (slow) {
-#pragma unroll
-            for (int j = 0; j < NMAX; ++j)
-                if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.base + 2 * j) = longlong2{ep[j], ps[j]};
-            dirty = 0;
-            for (uint32_t i = q; i < q2; ++i) {
-                const uint32_t seq = (uint32_t)s_val[i] & SEQ_MASK;
-                int64_t tt;
-                int32_t aa;
-                uint8_t fl;
-                src.load(seq, tt, aa, fl);
-                seq_event(T, key, ks, E, aa, fl, seq, V);
+        for (int j = 0; j < NMAX; ++j) {
+            if (j < nsc) {
+                const longlong2 v = *reinterpret_cast<const longlong2 *>(ks.base + 2 * j);
+                ep[j] = v.x;
+                ps[j] = v.y;
+            } else {
+                ep[j] = EPOCH_ABSENT;
+                ps[j] = 0;
             }
-#pragma unroll
-            for (int j = 0; j < NMAX; ++j)
-                if (j < nsc) { ep[j] = ks.ep(j); ps[j] = ks.cnt(EV_PASS, j); }
-            occ_pending = ks.seven && kind == KIND_CLUSTER && T.has_occ[key];
-            q = q2;
-            continue;
         }
-        const uint32_t len = q2 - q;
+        occ_pending = ks.seven && kind == KIND_CLUSTER && T.has_occ[key];
+    }
+
+    __device__ inline void flush() {
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j)
+            if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.base + 2 * j) = longlong2{ep[j], ps[j]};
+        dirty = 0;
+    }
+
+    // a segment at epoch E needs the sequential path (heterogeneous / prioritized, pending occupy
+    // transfer, or a slot newer than E: the clock went backwards for this flow)
+    __device__ inline bool slow(int64_t E, bool het) const {
+        bool s = het || occ_pending;
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j) s |= (ep[j] != EPOCH_ABSENT && ep[j] > E);
+        return s;
+    }
+
+    // the sequential path over sorted positions [q, q2) of `vals`
+    __device__ inline void sequential(const KeyTable &T, uint32_t key, int64_t E, const uint64_t *vals, uint32_t q,
+                                      uint32_t q2, const EventSrc &src, const Verdicts &V) {
+        flush();
+        for (uint32_t i = q; i < q2; ++i) {
+            const uint32_t seq = (uint32_t)vals[i] & SEQ_MASK;
+            int64_t tt;
+            int32_t aa;
+            uint8_t fl;
+            src.load(seq, tt, aa, fl);
+            seq_event(T, key, ks, E, aa, fl, seq, V);
+        }
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j)
+            if (j < nsc) { ep[j] = ks.ep(j); ps[j] = ks.cnt(EV_PASS, j); }
+        occ_pending = ks.seven && kind == KIND_CLUSTER && T.has_occ[key];
+    }
+
+    // closed form for a homogeneous segment of `len` events with acquire a: roll, S0, K, counters
+    __device__ inline void fast(int64_t E, int32_t a, uint32_t len, int64_t &s0, uint32_t &K) {
         const int slot = (int)(E % nsc);
         bool fresh = false;
 #pragma unroll
         for (int j = 0; j < NMAX; ++j)
             if (j == slot && ep[j] != E) { fresh = true; ep[j] = E; ps[j] = 0; }
-        int64_t s0 = 0;
+        s0 = 0;
 #pragma unroll
         for (int j = 0; j < NMAX; ++j)
             if (ep[j] != EPOCH_ABSENT && ep[j] > E - nsc) s0 = wrap_add(s0, ps[j]);
@@ -238,7 +243,7 @@ __device__ inline void part_run(const KeyTable &T, uint32_t key, const uint64_t 
             if (admits(kind, thr, I_s, wrap_add(s0, wrap_mul((int64_t)mid, a)), a)) lo = mid + 1;
             else hi = mid;
         }
-        const uint32_t K = lo;
+        K = lo;
         const int64_t nb = (int64_t)(len - K);
 #pragma unroll
         for (int j = 0; j < NMAX; ++j)
@@ -254,18 +259,181 @@ __device__ inline void part_run(const KeyTable &T, uint32_t key, const uint64_t 
                 *reinterpret_cast<longlong2 *>(r + 5) = longlong2{0, 0};
             }
         }
-        for (uint32_t k = 0; k < len; ++k) {
-            const uint32_t seq = (uint32_t)s_val[q + k] & SEQ_MASK;
-            uint64_t v;
-            if (k < K) v = pack_verdict(ST_OK, java_d2i(remaining_of(thr, I_s, wrap_add(s0, wrap_mul((int64_t)k, a)), a)), 0);
-            else v = pack_verdict(ST_BLOCKED, 0, 0);
-            V.out[seq] = v;
+    }
+
+    __device__ inline uint64_t verdict(int64_t s0, int32_t a, uint32_t K, uint32_t k) const {
+        if (k < K) return pack_verdict(ST_OK, java_d2i(remaining_of(thr, I_s, wrap_add(s0, wrap_mul((int64_t)k, a)), a)), 0);
+        return pack_verdict(ST_BLOCKED, 0, 0);
+    }
+};
+
+// One flow's run of sorted events [q0, q1) (arrival order), decided by one lane; verdicts written
+// to the arrival positions.
+template <int NMAX>
+__device__ inline void part_run(const KeyTable &T, uint32_t key, const uint64_t *s_val, uint32_t q0, uint32_t q1,
+                                const EventSrc &src, const Verdicts &V, int64_t T0) {
+    FlowWindow<NMAX> fw;
+    fw.load(T, key);
+    uint32_t q = q0;
+    while (q < q1) {
+        int64_t t;
+        int32_t a;
+        bool prio;
+        src.unpack(s_val[q], T0, t, a, prio);
+        const int64_t E = epoch_of(t, fw.w, fw.rcp);
+        bool het = prio && fw.kind == KIND_CLUSTER;
+        uint32_t q2 = q + 1;
+        for (; q2 < q1; ++q2) {                       // the segment: same epoch
+            int64_t t2;
+            int32_t a2;
+            bool p2;
+            src.unpack(s_val[q2], T0, t2, a2, p2);
+            if (epoch_of(t2, fw.w, fw.rcp) != E) break;
+            het |= a2 != a || (p2 && fw.kind == KIND_CLUSTER);
+        }
+        if (fw.slow(E, het)) {
+            fw.sequential(T, key, E, s_val, q, q2, src, V);
+        } else {
+            int64_t s0;
+            uint32_t K;
+            fw.fast(E, a, q2 - q, s0, K);
+            for (uint32_t k = 0; k < q2 - q; ++k) V.out[(uint32_t)s_val[q + k] & SEQ_MASK] = fw.verdict(s0, a, K, k);
         }
         q = q2;
     }
+    fw.flush();
+}
+
+// Runs longer than this are decided by a whole workgroup (k_part_long): one lane walking a hot
+// flow's events would serialise the batch.
+constexpr uint32_t LONG_RUN = 2048;
+constexpr int PL_THREADS = 512;
+constexpr int PL_ITEMS = 8;
+constexpr int PL_CHUNK = PL_THREADS * PL_ITEMS;
+
+// One workgroup per long run (grid-stride over the deferred list): chunks of 4096 events; per
+// chunk every lane computes the epochs of its 8 contiguous events, segment heads come from a block
+// scan, lane 0 walks the chunk's segments with the window in its VGPRs (closed form or sequential),
+// then all lanes write the verdicts.  A chunk boundary only splits a segment in two consecutive
+// segments of the same epoch, which the window algebra treats identically.
+template <int NMAX>
+__global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint64_t *__restrict__ sval,
+                                                          const uint32_t *__restrict__ long_runs,
+                                                          const uint32_t *__restrict__ nlong, EventSrc src, Verdicts V) {
+    __shared__ uint16_t seg_start[PL_CHUNK + 1];
+    __shared__ int64_t seg_E[PL_CHUNK];
+    __shared__ int32_t seg_a[PL_CHUNK];
+    __shared__ int64_t seg_s0[PL_CHUNK];
+    __shared__ uint32_t seg_K[PL_CHUNK];
+    __shared__ uint32_t seg_flag[PL_CHUNK];      // bit0 heterogeneous, bit1 decided sequentially
+    __shared__ int64_t l_E[PL_THREADS];
+    __shared__ int32_t l_a[PL_THREADS];
+    __shared__ uint32_t waves_tot[PL_THREADS / WAVE];
+    __shared__ uint32_t s_nseg;
+    const uint32_t total = *nlong;
+    const int64_t T0 = src.t0();
+    for (uint32_t r = blockIdx.x; r < total; r += gridDim.x) {
+        const uint32_t q0 = long_runs[3 * (uint64_t)r], q1 = long_runs[3 * (uint64_t)r + 1];
+        const uint32_t key = long_runs[3 * (uint64_t)r + 2];
+        FlowWindow<NMAX> fw;                      // meaningful in lane 0 only
+        if (threadIdx.x == 0) fw.load(T, key);
+        const int32_t w = T.w[key];
+        const double rcp = T.rcp_w[key];
+        const bool cluster = T.kind[key] == KIND_CLUSTER;
+        for (uint32_t c0 = q0; c0 < q1; c0 += PL_CHUNK) {
+            const uint32_t cn = min((uint32_t)PL_CHUNK, q1 - c0);
+            int64_t E[PL_ITEMS];
+            int32_t a[PL_ITEMS];
+            uint32_t heads = 0, bad = 0;
 #pragma unroll
-    for (int j = 0; j < NMAX; ++j)
-        if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.base + 2 * j) = longlong2{ep[j], ps[j]};
+            for (int k = 0; k < PL_ITEMS; ++k) {
+                const uint32_t qq = threadIdx.x * PL_ITEMS + k;
+                E[k] = 0;
+                a[k] = 0;
+                if (qq < cn) {
+                    int64_t t;
+                    bool prio;
+                    src.unpack(sval[c0 + qq], T0, t, a[k], prio);
+                    E[k] = epoch_of(t, w, rcp);
+                    if (prio && cluster) bad |= 1u << k;
+                }
+            }
+            l_E[threadIdx.x] = E[PL_ITEMS - 1];
+            l_a[threadIdx.x] = a[PL_ITEMS - 1];
+            for (uint32_t g = threadIdx.x; g < PL_CHUNK; g += PL_THREADS) seg_flag[g] = 0;
+            __syncthreads();
+            int64_t pe = threadIdx.x ? l_E[threadIdx.x - 1] : 0;
+            int32_t pa = threadIdx.x ? l_a[threadIdx.x - 1] : 0;
+#pragma unroll
+            for (int k = 0; k < PL_ITEMS; ++k) {
+                const uint32_t qq = threadIdx.x * PL_ITEMS + k;
+                if (qq < cn) {
+                    if (qq == 0 || E[k] != pe) heads |= 1u << k;
+                    else if (a[k] != pa) bad |= 1u << k;
+                }
+                pe = E[k];
+                pa = a[k];
+            }
+            uint32_t nseg;
+            uint32_t g = block_exclusive_scan((uint32_t)__popc(heads), waves_tot, &nseg);
+            uint32_t gid[PL_ITEMS];
+#pragma unroll
+            for (int k = 0; k < PL_ITEMS; ++k) {
+                const uint32_t qq = threadIdx.x * PL_ITEMS + k;
+                if (heads & (1u << k)) {
+                    seg_start[g] = (uint16_t)qq;
+                    seg_E[g] = E[k];
+                    seg_a[g] = a[k];
+                    ++g;
+                }
+                gid[k] = g - 1;
+            }
+            if (threadIdx.x == 0) s_nseg = nseg;
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < PL_ITEMS; ++k)
+                if ((bad & (1u << k)) && threadIdx.x * PL_ITEMS + k < cn) atomicOr(&seg_flag[gid[k]], 1u);
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const uint32_t ns = s_nseg;
+                for (uint32_t sgi = 0; sgi < ns; ++sgi) {
+                    const uint32_t st = seg_start[sgi];
+                    const uint32_t en = sgi + 1 < ns ? seg_start[sgi + 1] : cn;
+                    const int64_t Es = seg_E[sgi];
+                    if (fw.slow(Es, seg_flag[sgi] & 1u)) {
+                        fw.sequential(T, key, Es, sval, c0 + st, c0 + en, src, V);
+                        seg_flag[sgi] |= 2u;
+                    } else {
+                        int64_t s0;
+                        uint32_t K;
+                        fw.fast(Es, seg_a[sgi], en - st, s0, K);
+                        seg_s0[sgi] = s0;
+                        seg_K[sgi] = K;
+                    }
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < PL_ITEMS; ++k) {
+                const uint32_t qq = threadIdx.x * PL_ITEMS + k;
+                if (qq >= cn) continue;
+                const uint32_t sg = gid[k];
+                if (seg_flag[sg] & 2u) continue;
+                const uint32_t seq = (uint32_t)sval[c0 + qq] & SEQ_MASK;
+                uint64_t v;
+                if (qq - seg_start[sg] < seg_K[sg])
+                    v = pack_verdict(ST_OK, java_d2i(remaining_of(T.thr[key], T.I_s[key],
+                                                                  wrap_add(seg_s0[sg], wrap_mul((int64_t)(qq - seg_start[sg]), seg_a[sg])),
+                                                                  seg_a[sg])), 0);
+                else
+                    v = pack_verdict(ST_BLOCKED, 0, 0);
+                V.out[seq] = v;
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) fw.flush();
+        __syncthreads();
+    }
 }
 
 // One workgroup per flow range: a stable counting sort of the range's events by local flow key
@@ -284,7 +452,8 @@ __global__ __launch_bounds__(PSORT_THREADS) void k_part_sort(const uint16_t *__r
                                                              const uint32_t *__restrict__ offsets, int64_t nblocks,
                                                              int lb, uint32_t *__restrict__ run_start,
                                                              uint32_t *__restrict__ run_flow,
-                                                             uint32_t *__restrict__ nruns) {
+                                                             uint32_t *__restrict__ nruns,
+                                                             unsigned long long *__restrict__ max_range) {
     __shared__ uint32_t base[PART_BINS];                 // per-bin counts, then running slot offsets
     __shared__ uint16_t cnt[PSORT_WAVES][PART_BINS];
     __shared__ uint32_t waves_tot[PSORT_WAVES];
@@ -294,6 +463,7 @@ __global__ __launch_bounds__(PSORT_THREADS) void k_part_sort(const uint16_t *__r
     const int wave = threadIdx.x / WAVE;
     const uint32_t lane = lane_id();
     const uint32_t R = 1u << lb;
+    if (threadIdx.x == 0 && max_range) atomicMax(max_range, (unsigned long long)(pend - pstart));   // skew statistic
     for (int d = threadIdx.x; d < PART_BINS; d += PSORT_THREADS) base[d] = 0;
     __syncthreads();
     for (uint32_t q = pstart + threadIdx.x; q < pend; q += PSORT_THREADS) atomicAdd(&base[pkey[q]], 1u);
@@ -390,7 +560,8 @@ __global__ __launch_bounds__(256) void k_part_runs(KeyTable T, const uint64_t *_
                                                    const uint32_t *__restrict__ offsets, int64_t nblocks, int lb,
                                                    const uint32_t *__restrict__ run_start,
                                                    const uint32_t *__restrict__ run_flow,
-                                                   const uint32_t *__restrict__ nruns, EventSrc src, Verdicts V) {
+                                                   const uint32_t *__restrict__ nruns, EventSrc src, Verdicts V,
+                                                   uint32_t *__restrict__ long_runs, uint32_t *__restrict__ nlong) {
     const int p = blockIdx.x;
     const uint32_t r = blockIdx.y * blockDim.x + threadIdx.x;
     const uint32_t nr = nruns[p];
@@ -398,6 +569,13 @@ __global__ __launch_bounds__(256) void k_part_runs(KeyTable T, const uint64_t *_
     const uint64_t i = ((uint64_t)p << lb) + r;
     const uint32_t q0 = run_start[i];
     const uint32_t q1 = r + 1 < nr ? run_start[i + 1] : offsets[(int64_t)(p + 1) * nblocks];
+    if (q1 - q0 > LONG_RUN) {                     // hot flow: a whole workgroup takes it (k_part_long)
+        const uint32_t k = atomicAdd(nlong, 1u);
+        long_runs[3 * (uint64_t)k] = q0;
+        long_runs[3 * (uint64_t)k + 1] = q1;
+        long_runs[3 * (uint64_t)k + 2] = run_flow[i];
+        return;
+    }
     part_run<NMAX>(T, run_flow[i], sval, q0, q1, src, V, src.t0());
 }
 

@@ -313,3 +313,21 @@ def test_batcher_concurrent_threads():
     assert nr == 400 and 1 <= nb <= 400
     assert b.request_token(None, 1, False, ts=t).status == sa.TokenResultStatus.BAD_REQUEST
     b.close()
+
+
+def test_hot_flow_long_runs(oracle_mod):
+    """One flow takes most of the batch (runs far longer than one lane should walk): the partition
+    path hands it to a whole workgroup; heterogeneous acquires, prioritized events and a clock
+    that steps back put sequential segments inside the long run."""
+    rng = np.random.default_rng(41)
+    rules = T.make_rules(100, rng, count_lo=50, count_hi=4000, sample_count=4, window_interval_ms=400)
+    n = 90_000
+    idx = rng.integers(0, 100, size=n).astype(np.int32)
+    idx[rng.random(n) < 0.6] = 7
+    acq = np.ones(n, np.int32)
+    acq[rng.random(n) < 0.03] = 2
+    ts = T.timestamps(n, 30_000.0, T.T0_ALIGNED + 11)
+    ts = ts + np.where(rng.random(n) < 0.002, -rng.integers(0, 300, size=n), 0)
+    flags = (rng.random(n) < 0.01).astype(np.uint8)
+    ev = T.Events(idx, acq, ts.astype(np.int64), flags)
+    _compare(_engine(rules, occ=0.9), _oracle(oracle_mod, rules, occ=0.9), rules, ev, batches=3)
