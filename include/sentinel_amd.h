@@ -246,6 +246,32 @@ int  sentinel_submit_local_param_batch_host(sentinel_engine_t *eng, int64_t n, c
 /* Token bucket of one value: {lastAddTokenTime, tokens} (-1 when absent); returns 1 if present. */
 int  sentinel_local_param_state(sentinel_engine_t *eng, uint64_t param_key, int64_t *last_add_ms, int64_t *tokens);
 
+/* ---- local SphU.entry admission: DefaultController over a resource's ClusterNode ----
+ * FlowSlot -> FlowRuleChecker.passLocalCheck -> DefaultController.canPass (QPS grade, limitApp
+ * "default", strategy DIRECT: sentinel-core/.../slots/block/flow/FlowRuleChecker.java:44-132,
+ * controller/DefaultController.java:49-76) and StatisticSlot's booking into the StatisticNode's
+ * second window (SampleCountProperty x IntervalProperty) and minute window (60 x 1 s)
+ * (sentinel-core/.../slots/statistic/StatisticSlot.java:55-116, node/StatisticNode.java:96-264). */
+typedef struct {
+    double  count;       /* the smallest count of the resource's QPS FlowRules (every rule must pass) */
+    int32_t has_rule;    /* 0: no flow rule -> every entry passes (and is counted) */
+    int32_t reserved;
+} sentinel_local_resource_t;
+
+/* Loads the resources (index = position) with the node window config (defaults 2, 1000); every
+ * node starts empty.  Preconditions (documented): <= 6000 resources (CtSph MAX_SLOT_CHAIN_SIZE), no
+ * prioritized entries. */
+int  sentinel_load_local_resources(sentinel_engine_t *eng, const sentinel_local_resource_t *res, int32_t n,
+                                   int32_t sample_count, int32_t interval_ms);
+/* Events {resource index, acquireCount, ts}: OK (entry) or BLOCKED (FlowException); an unknown
+ * resource answers NO_RULE_EXISTS. */
+int  sentinel_submit_local_entry_batch(sentinel_engine_t *eng, int64_t n, const sentinel_event_t *events,
+                                       sentinel_verdict_t *verdicts, void *stream);
+int  sentinel_submit_local_entry_batch_host(sentinel_engine_t *eng, int64_t n, const sentinel_event_t *events,
+                                            sentinel_verdict_t *verdicts);
+/* {second-window PASS, BLOCK, minute-window PASS, BLOCK} sums of a resource's node at ts (read-only). */
+int  sentinel_local_node_stats(sentinel_engine_t *eng, int32_t resource_idx, int64_t ts, int64_t *out4);
+
 /* ---- cluster concurrency tokens (thread grade): TokenService.requestConcurrentToken /
  *      releaseConcurrentToken (TokenService.java:56,62) -> ConcurrentClusterFlowChecker
  *      (sentinel-cluster/.../cluster/flow/ConcurrentClusterFlowChecker.java:48-101) ---- */

@@ -105,6 +105,7 @@ def lib():
         "orc_node_pass_sum": (i64, [vp, i64]),
         "orc_node_block_sum": (i64, [vp, i64]),
         "orc_node_total_pass": (i64, [vp, i64]),
+        "orc_node_minute_block": (i64, [vp, i64]),
         "orc_node_add_pass_request": (None, [vp, i64, C.c_int]),
         "orc_node_increase_block_qps": (None, [vp, i64, C.c_int]),
         "orc_default_controller_can_pass": (C.c_int, [vp, dbl, C.c_int, C.c_int, i32, i64]),
@@ -218,6 +219,7 @@ class StatisticNode:
     def pass_sum(self, t): return lib().orc_node_pass_sum(self.h, t)
     def block_sum(self, t): return lib().orc_node_block_sum(self.h, t)
     def total_pass(self, t): return lib().orc_node_total_pass(self.h, t)
+    def minute_block(self, t): return lib().orc_node_minute_block(self.h, t)
     def add_pass_request(self, t, c): lib().orc_node_add_pass_request(self.h, t, c)
     def increase_block_qps(self, t, c): lib().orc_node_increase_block_qps(self.h, t, c)
 

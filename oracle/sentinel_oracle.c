@@ -816,6 +816,7 @@ void orc_node_free(orc_stat_node *nd) {
 int64_t orc_node_pass_sum(orc_stat_node *nd, int64_t t) { return ba_sum(&nd->sec, t, ORC_M_PASS); }
 int64_t orc_node_block_sum(orc_stat_node *nd, int64_t t) { return ba_sum(&nd->sec, t, ORC_M_BLOCK); }
 int64_t orc_node_total_pass(orc_stat_node *nd, int64_t t) { return ba_sum(&nd->min, t, ORC_M_PASS); }
+int64_t orc_node_minute_block(orc_stat_node *nd, int64_t t) { return ba_sum(&nd->min, t, ORC_M_BLOCK); }
 
 double orc_node_pass_qps(orc_stat_node *nd, int64_t t) {          /* SN:200-202 */
     return (double)orc_node_pass_sum(nd, t) / nd->sec.la.interval_sec;

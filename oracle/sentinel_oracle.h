@@ -154,6 +154,7 @@ double orc_node_pass_qps(orc_stat_node *nd, int64_t t);
 int64_t orc_node_pass_sum(orc_stat_node *nd, int64_t t);       /* rollingCounterInSecond.pass() */
 int64_t orc_node_block_sum(orc_stat_node *nd, int64_t t);
 int64_t orc_node_total_pass(orc_stat_node *nd, int64_t t);     /* rollingCounterInMinute.pass() */
+int64_t orc_node_minute_block(orc_stat_node *nd, int64_t t);   /* rollingCounterInMinute.block() */
 void   orc_node_add_pass_request(orc_stat_node *nd, int64_t t, int count);
 void   orc_node_increase_block_qps(orc_stat_node *nd, int64_t t, int count);
 /* DefaultController.canPass(node, acquire) for QPS grade (grade=1) or THREAD grade (0). */

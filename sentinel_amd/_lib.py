@@ -48,6 +48,8 @@ EXPORTS = [
     "sentinel_local_param_state",
     "sentinel_submit_concurrent_batch_host", "sentinel_concurrent_now_calls", "sentinel_concurrent_token_count",
     "sentinel_concurrent_expire",
+    "sentinel_load_local_resources", "sentinel_submit_local_entry_batch", "sentinel_submit_local_entry_batch_host",
+    "sentinel_local_node_stats",
 ]
 
 STATUS_RELEASE_OK = 6
@@ -82,6 +84,10 @@ class ParamRuleC(C.Structure):
 class LocalParamRuleC(C.Structure):
     _fields_ = [("count", C.c_double), ("burst_count", C.c_int64), ("duration_in_sec", C.c_int64),
                 ("hot_begin", C.c_int32), ("hot_n", C.c_int32)]
+
+
+class LocalResourceC(C.Structure):
+    _fields_ = [("count", C.c_double), ("has_rule", C.c_int32), ("reserved", C.c_int32)]
 
 
 class TokenResultC(C.Structure):
@@ -165,6 +171,10 @@ def load():
         "sentinel_concurrent_now_calls": (C.c_int, [vp, i32, vp]),
         "sentinel_concurrent_token_count": (C.c_int, [vp, vp]),
         "sentinel_concurrent_expire": (C.c_int, [vp, i64, vp]),
+        "sentinel_load_local_resources": (C.c_int, [vp, vp, i32, i32, i32]),
+        "sentinel_submit_local_entry_batch": (C.c_int, [vp, i64, vp, vp, vp]),
+        "sentinel_submit_local_entry_batch_host": (C.c_int, [vp, i64, vp, vp]),
+        "sentinel_local_node_stats": (C.c_int, [vp, i32, i64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -32,6 +32,7 @@
 #include "concurrent.hpp"
 #include "param_rules.hpp"
 #include "partition.hpp"
+#include "local_entry.hpp"
 #include <random>
 #include "scan_sort.hpp"
 
@@ -324,6 +325,11 @@ struct sentinel_engine {
     uint64_t lhot_mask = 0;
     bool lhas_hot = false;
     uint64_t lcap = (uint64_t)1 << 22;
+
+    // local resources (SphU.entry: DefaultController over the ClusterNode's StatisticNode)
+    int32_t nlres = 0, lres_n = 2, lres_w = 500, lres_g = 500;
+    double lres_Is = 1.0;
+    DevBuf d_lres_state, d_lres_count, d_lres_w, d_lres_rcp, d_lres_kind;
 
     // concurrency tokens (ConcurrentClusterFlowChecker): nowCalls per flow, token cache in HBM
     DevBuf d_now, d_conc_thr, d_seg1_w, d_seg1_rcp, d_seg1_kind;
@@ -1069,6 +1075,42 @@ static int submit_prules_host(sentinel_engine_t *e, int mode, int64_t n, const s
     return 0;
 }
 
+// Local SphU.entry batches (local_entry.hpp): validation, sort by resource, (resource, epoch of
+// gcd(second bucket, 1000 ms)) segments, one lane per resource, parallel verdicts.
+static int submit_local_entry(sentinel_engine_t *e, int64_t n, const Event *ev, uint64_t *out, hipStream_t s) {
+    if (n <= 0) return 0;
+    if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
+    int rc = e->ensure_ws(n);
+    if (rc) return rc;
+    const int32_t R = e->nlres;
+    const int rbits = bits_for(R);
+    const uint32_t rinvalid = ((uint32_t)1 << rbits) - 1;
+    uint32_t *fkey = e->w_fkey.as<uint32_t>();
+    const int64_t nb = sort_blocks(n);
+    HIP_OK(hipMemsetAsync(e->w_counters.p, 0, 16, s));
+    e->launch("lentry_prep", n, s, [&] {
+        k_lentry_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(n, ev, R, out, fkey, rinvalid,
+                                                                        e->w_fhist.as<uint32_t>(), nb);
+    });
+    if (R == 0) {
+        HIP_OK(hipGetLastError());
+        return 0;
+    }
+    KeyTable RT{};
+    RT.w = e->d_lres_w.as<int32_t>();
+    RT.rcp_w = e->d_lres_rcp.as<double>();
+    RT.kind = e->d_lres_kind.as<uint8_t>();
+    RT.ncounters = 1;
+    const EventSrc src{ev, nullptr, nullptr, false};
+    e->sort_segments(RT, fkey, e->w_fhist.as<uint32_t>(), n, rbits, src, s);
+    const BatchWork W = e->work();
+    const LocalNodes L{e->d_lres_state.as<int64_t>(), e->d_lres_count.as<double>(), e->lres_n, e->lres_w, e->lres_Is};
+    e->launch("lentry_process", n, s, [&] { k_lentry_process<<<grid_for(n), 256, 0, s>>>(L, W, src, out); });
+    e->launch("lentry_verdict", n, s, [&] { k_lentry_verdict<<<grid_for(n), 256, 0, s>>>(W, out, n); });
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
 static bool valid_window(int32_t n, int32_t interval) {  // FlowRuleUtil.isWindowConfigValid (FlowRuleUtil.java:229-231)
     return n > 0 && interval > 0 && interval % n == 0;
 }
@@ -1146,7 +1188,8 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
                       &e->d_lrule_dur, &e->d_lrule_w, &e->d_lrule_rcp, &e->d_lrule_kind, &e->d_lhot_keys,
                       &e->d_lhot_tok, &e->d_ltable, &e->d_lstate, &e->d_now, &e->d_conc_thr, &e->d_seg1_w,
                       &e->d_seg1_rcp, &e->d_seg1_kind, &e->d_tok_keys, &e->d_tok_fid, &e->d_tok_fidx,
-                      &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->w_pkey, &e->w_runs})
+                      &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->w_pkey, &e->w_runs, &e->d_lres_state,
+                      &e->d_lres_count, &e->d_lres_w, &e->d_lres_rcp, &e->d_lres_kind})
         b->release();
     if (e->h_part_stat) (void)hipHostFree(e->h_part_stat);
     e->d_part_stat.release();
@@ -1620,6 +1663,92 @@ int sentinel_local_param_state(sentinel_engine_t *e, uint64_t key, int64_t *last
     *last_add_ms = st[0] == LOCAL_ABSENT ? -1 : st[0];
     *tokens = st[1] == LOCAL_ABSENT ? -1 : st[1];
     return 1;
+}
+
+int sentinel_load_local_resources(sentinel_engine_t *e, const sentinel_local_resource_t *res, int32_t n,
+                                  int32_t sample_count, int32_t interval_ms) {
+    if (!e || n < 0 || (n > 0 && !res)) return fail(SENTINEL_E_INVALID, "bad local resources");
+    // SampleCountProperty / IntervalProperty validity: positive, INTERVAL % SAMPLE_COUNT == 0
+    if (sample_count < 1 || sample_count > LOCAL_NMAX || interval_ms <= 0 || interval_ms % sample_count != 0)
+        return fail(SENTINEL_E_INVALID, "sample_count must be 1..8 and divide interval_ms");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    const size_t N = (size_t)std::max(n, 1);
+    int32_t w = interval_ms / sample_count, a = w, b = 1000;
+    while (b) { const int32_t t = a % b; a = b; b = t; }            // segment length gcd(w, 1000)
+    std::vector<double> count(N, HUGE_VAL);
+    for (int32_t i = 0; i < n; ++i)
+        if (res[i].has_rule && res[i].count >= 0) count[i] = res[i].count;   // invalid rules (count < 0) are dropped
+    std::vector<int64_t> st(N * LOCAL_WORDS, 0);
+    for (size_t i = 0; i < N; ++i)
+        for (int j = 0; j < LOCAL_NMAX + LOCAL_MIN_SLOTS; ++j) st[i * LOCAL_WORDS + 3 * j] = EPOCH_ABSENT;
+    int rc = 0;
+    rc |= upload(e->d_lres_state, st);
+    rc |= upload(e->d_lres_count, count);
+    rc |= upload(e->d_lres_w, std::vector<int32_t>(N, a));
+    rc |= upload(e->d_lres_rcp, std::vector<double>(N, 1.0 / (double)a));
+    rc |= upload(e->d_lres_kind, std::vector<uint8_t>(N, KIND_LOCAL_PARAM));
+    if (rc) return rc;
+    e->nlres = n;
+    e->lres_n = sample_count;
+    e->lres_w = w;
+    e->lres_g = a;
+    e->lres_Is = interval_ms / 1000.0;                                 // LeapArray.intervalInSecond
+    return 0;
+}
+
+int sentinel_submit_local_entry_batch(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev,
+                                      sentinel_verdict_t *out, void *stream) {
+    if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    return submit_local_entry(e, n, (const Event *)ev, (uint64_t *)out, stream ? (hipStream_t)stream : e->stream);
+}
+
+int sentinel_submit_local_entry_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev,
+                                           sentinel_verdict_t *out) {
+    if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    hipStream_t s = e->stream;
+    int rc = 0;
+    rc |= e->io_ev.ensure(n * sizeof(Event));
+    rc |= e->io_out.ensure(n * 8);
+    if (rc) return SENTINEL_E_NOMEM;
+    HIP_OK(hipMemcpyAsync(e->io_ev.p, ev, n * sizeof(Event), hipMemcpyHostToDevice, s));
+    rc = submit_local_entry(e, n, e->io_ev.as<Event>(), e->io_out.as<uint64_t>(), s);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 8, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    return 0;
+}
+
+int sentinel_local_node_stats(sentinel_engine_t *e, int32_t idx, int64_t ts, int64_t *out) {
+    if (!e || !out || ts < 0) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    if (idx < 0 || idx >= e->nlres) return fail(SENTINEL_E_INVALID, "bad resource index");
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    std::vector<int64_t> st(LOCAL_WORDS);
+    HIP_OK(hipMemcpy(st.data(), e->d_lres_state.as<int64_t>() + (int64_t)idx * LOCAL_WORDS, LOCAL_WORDS * 8,
+                     hipMemcpyDeviceToHost));
+    const int64_t E = ts / e->lres_w, E1 = ts / 1000;   // read-only view: valid epochs (E - n, E]
+    for (int k = 0; k < 4; ++k) out[k] = 0;
+    for (int j = 0; j < e->lres_n; ++j)
+        if (st[3 * j] != EPOCH_ABSENT && st[3 * j] > E - e->lres_n && st[3 * j] <= E) {
+            out[0] += st[3 * j + 1];
+            out[1] += st[3 * j + 2];
+        }
+    for (int j = 0; j < LOCAL_MIN_SLOTS; ++j) {
+        const int64_t *m = st.data() + 3 * (LOCAL_NMAX + j);
+        if (m[0] != EPOCH_ABSENT && m[0] > E1 - LOCAL_MIN_SLOTS && m[0] <= E1) {
+            out[2] += m[1];
+            out[3] += m[2];
+        }
+    }
+    return 0;
 }
 
 int sentinel_submit_concurrent_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_concurrent_event_t *ev,

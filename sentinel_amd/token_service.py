@@ -411,6 +411,31 @@ class GpuTokenService:
         check(rc, "local_param_state")
         return last.value, tok.value
 
+    # ---------------------------------------------------------------- local SphU.entry (DefaultController)
+    def load_local_resources(self, counts, sample_count: int = 2, interval_ms: int = 1000):
+        """Local resources (index = position): the smallest QPS rule count per resource, or None for
+        a resource without flow rules; the StatisticNode window config (SampleCountProperty,
+        IntervalProperty)."""
+        arr = (_lib.LocalResourceC * max(len(counts), 1))()
+        for i, c in enumerate(counts):
+            arr[i] = _lib.LocalResourceC(0.0 if c is None else float(c), 0 if c is None else 1, 0)
+        check(self._L.sentinel_load_local_resources(self._h, arr, len(counts), int(sample_count), int(interval_ms)),
+              "load_local_resources")
+
+    def submit_local_entry_batch_host(self, resource_idx, acquire, ts):
+        """SphU.entry for a batch -> status array (OK = entry, BLOCKED = FlowException)."""
+        ev = self.pack_events(resource_idx, acquire, ts)
+        out = np.empty(len(ev), dtype=_lib.VERDICT_DTYPE)
+        check(self._L.sentinel_submit_local_entry_batch_host(self._h, len(ev), _p(ev), _p(out)),
+              "submit_local_entry_batch_host")
+        return out["status"].astype(np.int8)
+
+    def local_node_stats(self, resource_idx: int, ts: int) -> np.ndarray:
+        """{second PASS, second BLOCK, minute PASS, minute BLOCK} of the resource's node at ts."""
+        out = np.zeros(4, dtype=np.int64)
+        check(self._L.sentinel_local_node_stats(self._h, int(resource_idx), int(ts), _p(out)), "local_node_stats")
+        return out
+
     def synchronize(self):
         check(self._L.sentinel_synchronize(self._h), "synchronize")
 

@@ -166,3 +166,22 @@ def param_value_lists(rule_idx: np.ndarray, rng: np.random.Generator, universe: 
     owner = np.repeat(np.asarray(rule_idx, dtype=np.int64), counts)
     keys = (owner.astype(np.uint64) << np.uint64(20)) | vals.astype(np.uint64)
     return begin, counts, keys
+
+
+def config1(seed: int = 1, t0: int = T0_ALIGNED, duration_ms: int = 100_000, threads: int = 32):
+    """FlowQpsDemo traffic (FlowQpsDemo.java:132-157): `threads` workers loop SphU.entry("abc")
+    then sleep U[0, 50) ms, for `duration_ms`.  Returns the merged entry timestamps (arrival order:
+    time, then worker) -- one resource, acquire 1."""
+    rng = np.random.default_rng(seed)
+    ts = []
+    for w in range(threads):
+        t = t0
+        out = []
+        while t < t0 + duration_ms:
+            out.append(t)
+            t += int(rng.integers(0, 50))
+        ts.append(np.array(out, dtype=np.int64))
+    allt = np.concatenate(ts)
+    worker = np.concatenate([np.full(len(x), i) for i, x in enumerate(ts)])
+    order = np.lexsort((worker, allt))
+    return allt[order]
