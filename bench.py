@@ -195,6 +195,25 @@ def main():
         torch.cuda.synchronize()
     snap_ms = (time.perf_counter() - ts0) * 1000.0
 
+    # PCIe-inclusive host path: 1M-event batches from pinned host memory through the C ABI
+    # (H2D, decide, D2H, synchronous) -- reported beside `value`, never as it.
+    host_path = None
+    if rank == 0:
+        import ctypes as C
+        m = min(N, 1 << 20)
+        hev = torch.empty((m, 2), dtype=torch.int64, pin_memory=True)
+        hev.copy_(ev_b[-1][:m])
+        hout = torch.empty(m, dtype=torch.int64, pin_memory=True)
+        reps = 5
+        h0 = time.perf_counter()
+        for _ in range(reps):
+            rc = svc._L.sentinel_submit_flow_batch_host(svc.handle, m, C.c_void_p(hev.data_ptr()), None,
+                                                        C.c_void_p(hout.data_ptr()))
+            assert rc == 0
+        hdt = (time.perf_counter() - h0) / reps
+        host_path = {"decisions_per_s": round(m / hdt, 1), "batch": m, "ms_per_batch": round(hdt * 1000.0, 3),
+                     "note": "pinned host events -> H2D -> decide -> D2H, synchronous per batch"}
+
     total_events = float(N) * args.steps * world
     value = total_events / elapsed
 
@@ -280,6 +299,7 @@ def main():
         "p99_batch_ms": round(p99, 4),
         "median_batch_ms": round(lat[len(lat) // 2], 4),
         "snapshot_allgather_ms": round(snap_ms, 3),
+        "host_path": host_path,
         "pipeline_bytes_per_decision": round(pipeline_bytes, 2),
         "pipeline_hbm_frac": round(value / world * pipeline_bytes / (HBM_PEAK_GBS * 1e9), 4),
         "roofline": roof,
