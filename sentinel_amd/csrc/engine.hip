@@ -807,13 +807,13 @@ int sentinel_engine::rebuild_limiters() {
 template <int NMAX>
 static void launch_part_runs(sentinel_engine_t *e, unsigned nparts, const KeyTable &FT, const uint32_t *offsets,
                              int64_t nb, int lb, const EventSrc &src, const Verdicts &V, int64_t n, hipStream_t s) {
-    const dim3 grid(nparts, (unsigned)(((1u << lb) + 255) / 256));
+    const dim3 grid(nparts, (unsigned)(((1u << lb) + PR_THREADS - 1) / PR_THREADS));
     uint32_t *runs = e->w_runs.as<uint32_t>();
     uint32_t *nlong = runs + ((size_t)nparts << (lb + 1)) + nparts;
     uint32_t *long_runs = nlong + 1;
     (void)hipMemsetAsync(nlong, 0, 4, s);
     e->launch("part_runs", n, s, [&] {
-        k_part_runs<NMAX><<<grid, 256, 0, s>>>(FT, e->w_vtmp.as<uint64_t>(), offsets, nb, lb, runs,
+        k_part_runs<NMAX><<<grid, PR_THREADS, 0, s>>>(FT, e->w_vtmp.as<uint64_t>(), offsets, nb, lb, runs,
                                                runs + ((size_t)nparts << lb), runs + ((size_t)nparts << (lb + 1)), src,
                                                V, long_runs, nlong);
     });

@@ -553,22 +553,39 @@ __global__ __launch_bounds__(PSORT_THREADS) void k_part_sort(const uint16_t *__r
     }
 }
 
-// One lane per flow run (grid: ranges x ceil(2^lb / 256)): the run's events are contiguous in
-// arrival order in `sval`.
+// One lane per flow run (grid: ranges x ceil(2^lb / 256)).  The block's 256 runs are contiguous in
+// `sval`; when their events fit (the common case: ~256 x mean run length) the block stages them in
+// LDS with coalesced loads, so each lane walks its run at LDS latency instead of a chain of
+// dependent global loads.
+constexpr int PR_THREADS = 256;
+constexpr uint32_t PR_STAGE = 4096;               // events staged per block (32 KB)
+
 template <int NMAX>
-__global__ __launch_bounds__(256) void k_part_runs(KeyTable T, const uint64_t *__restrict__ sval,
-                                                   const uint32_t *__restrict__ offsets, int64_t nblocks, int lb,
-                                                   const uint32_t *__restrict__ run_start,
-                                                   const uint32_t *__restrict__ run_flow,
-                                                   const uint32_t *__restrict__ nruns, EventSrc src, Verdicts V,
-                                                   uint32_t *__restrict__ long_runs, uint32_t *__restrict__ nlong) {
+__global__ __launch_bounds__(PR_THREADS) void k_part_runs(KeyTable T, const uint64_t *__restrict__ sval,
+                                                          const uint32_t *__restrict__ offsets, int64_t nblocks,
+                                                          int lb, const uint32_t *__restrict__ run_start,
+                                                          const uint32_t *__restrict__ run_flow,
+                                                          const uint32_t *__restrict__ nruns, EventSrc src, Verdicts V,
+                                                          uint32_t *__restrict__ long_runs, uint32_t *__restrict__ nlong) {
+    __shared__ uint64_t lv[PR_STAGE];
     const int p = blockIdx.x;
-    const uint32_t r = blockIdx.y * blockDim.x + threadIdx.x;
     const uint32_t nr = nruns[p];
+    const uint32_t r0 = blockIdx.y * PR_THREADS;
+    if (r0 >= nr) return;                         // block-uniform
+    const uint64_t ib = (uint64_t)p << lb;
+    const uint32_t pend = offsets[(int64_t)(p + 1) * nblocks];
+    const uint32_t rend = min(r0 + (uint32_t)PR_THREADS, nr);
+    const uint32_t s0 = run_start[ib + r0];
+    const uint32_t s1 = rend < nr ? run_start[ib + rend] : pend;
+    const bool staged = s1 - s0 <= PR_STAGE;
+    if (staged)
+        for (uint32_t q = threadIdx.x; q < s1 - s0; q += PR_THREADS) lv[q] = sval[s0 + q];
+    __syncthreads();
+    const uint32_t r = r0 + threadIdx.x;
     if (r >= nr) return;
-    const uint64_t i = ((uint64_t)p << lb) + r;
+    const uint64_t i = ib + r;
     const uint32_t q0 = run_start[i];
-    const uint32_t q1 = r + 1 < nr ? run_start[i + 1] : offsets[(int64_t)(p + 1) * nblocks];
+    const uint32_t q1 = r + 1 < nr ? run_start[i + 1] : pend;
     if (q1 - q0 > LONG_RUN) {                     // hot flow: a whole workgroup takes it (k_part_long)
         const uint32_t k = atomicAdd(nlong, 1u);
         long_runs[3 * (uint64_t)k] = q0;
@@ -576,7 +593,8 @@ __global__ __launch_bounds__(256) void k_part_runs(KeyTable T, const uint64_t *_
         long_runs[3 * (uint64_t)k + 2] = run_flow[i];
         return;
     }
-    part_run<NMAX>(T, run_flow[i], sval, q0, q1, src, V, src.t0());
+    if (staged) part_run<NMAX>(T, run_flow[i], lv, q0 - s0, q1 - s0, src, V, src.t0());
+    else part_run<NMAX>(T, run_flow[i], sval, q0, q1, src, V, src.t0());
 }
 
 }  // namespace sentinel
