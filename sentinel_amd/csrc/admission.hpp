@@ -41,6 +41,7 @@ struct ParamEvent {
 };
 
 __host__ __device__ inline int64_t header_words(int n) { return ((2 * (int64_t)n) + 7) & ~(int64_t)7; }
+constexpr int HB_KEYS = 64;    // flows per block of the blocked header region (one wave)
 __host__ __device__ inline int64_t flow_record_words(int n) { return header_words(n) + 8 * (int64_t)n; }
 
 // Per-key tables (device pointers).
@@ -57,6 +58,8 @@ struct KeyTable {
     int64_t *occ;            // CLUSTER only: [2*k] occupy PASS, [2*k+1] occupy PASS_REQUEST (CMLA:129)
     uint8_t *has_occ;        // CMLA:130
     int32_t ncounters;       // 7 (flows) or 1 (limiter / param)
+    int32_t hblock;          // > 0: headers in the blocked slot-major region (slots per block);
+                             // state_off then locates the rest lines only
     double max_occupy_ratio; // ServerFlowConfig.maxOccupyRatio
 };
 
@@ -149,24 +152,49 @@ struct Verdicts {
     uint32_t flow_key_invalid;
 };
 
+// A key's state: header pair j {epoch, PASS} at base + hs*j (hs = 2: contiguous record;
+// hs = 2*HB_KEYS: the flow table's blocked slot-major header region), rest lines at rbase.
 struct KeyState {
     int64_t *base;
+    int64_t *rbase;
+    int hs;
     int n;
     bool seven;   // 7-counter flow layout
-    __device__ inline int64_t &ep(int slot) const { return base[2 * slot]; }
+    __device__ inline int64_t *pair(int slot) const { return base + (int64_t)hs * slot; }
+    __device__ inline int64_t &ep(int slot) const { return pair(slot)[0]; }
     __device__ inline int64_t &cnt(int ev, int slot) const {
-        if (ev == EV_PASS || !seven) return base[2 * slot + 1];
+        if (ev == EV_PASS || !seven) return pair(slot)[1];
         return rest(slot)[ev - 1];
     }
-    __device__ inline int64_t *rest(int slot) const { return base + header_words(n) + 8 * (int64_t)slot; }
+    __device__ inline int64_t *rest(int slot) const { return rbase + 8 * (int64_t)slot; }
 };
+
+// Slots per block of the flow header region: the kernel template bucket of the largest n, so a
+// kernel instantiated for NMAX slots may load all NMAX pairs of any flow without bounds checks.
+__host__ __device__ inline int32_t header_block_slots(int32_t maxn) {
+    return maxn <= 2 ? 2 : maxn <= 4 ? 4 : maxn <= 10 ? 10 : maxn <= 16 ? 16 : maxn;
+}
+
+// Flow-table header region: blocks of HB_KEYS flows, slot-major inside a block, so the 64 lanes
+// of a wave that read slot j of 64 consecutive flows read 1 KB of contiguous memory.
+__host__ __device__ inline int64_t blocked_pair_word(int64_t key, int hblock, int slot) {
+    return 2 * ((((key / HB_KEYS) * hblock + slot) * HB_KEYS) + key % HB_KEYS);
+}
 
 __device__ inline KeyState key_state(const KeyTable &T, uint32_t key) {
     KeyState k;
     const int64_t off = T.state_off ? T.state_off[key] : (int64_t)key * T.state_stride;
-    k.base = T.state + off;
     k.n = T.n[key];
     k.seven = T.ncounters == NEV;
+    if (T.hblock) {
+        k.base = T.state + blocked_pair_word(key, T.hblock, 0);
+        k.hs = 2 * HB_KEYS;
+        k.rbase = T.state + off;
+    } else {
+        k.base = T.state + off;
+        k.hs = 2;
+        k.rbase = k.base + header_words(k.n);
+    }
     return k;
 }
 
@@ -213,8 +241,19 @@ __device__ inline void add_counter(const KeyTable &T, uint32_t key, const KeySta
 }
 
 // The monotone admission predicate of each checker, evaluated in Java operation order.
+// x / I_s as Java evaluates it (one correctly rounded IEEE division).  When I_s is a normal power
+// of two (1.0 for every 1000 ms interval) the quotient is x * 2^-k, which v_ldexp_f64 produces
+// exactly with the same rounding -- one instruction instead of the div_scale/rcp/fma/fixup chain.
+__device__ inline double div_interval(double x, double I_s) {
+    const uint64_t b = (uint64_t)__double_as_longlong(I_s);
+    const uint32_t ex = (uint32_t)(b >> 52) & 0x7FFu;
+    if ((b & 0x000FFFFFFFFFFFFFull) == 0 && ex != 0 && ex != 0x7FFu && !(b >> 63))
+        return ldexp(x, 1023 - (int)ex);
+    return x / I_s;
+}
+
 __device__ inline bool admits(uint8_t kind, double thr, double I_s, int64_t x, int32_t a) {
-    const double avg = (double)x / I_s;
+    const double avg = div_interval((double)x, I_s);
     switch (kind) {
         case KIND_LIMITER: return avg + 1.0 <= thr;                      // RequestLimiter.java:72-74
         case KIND_PARAM: return !(((thr - avg) - (double)a) < 0.0);       // ClusterParamFlowChecker.java:64-66
@@ -223,7 +262,7 @@ __device__ inline bool admits(uint8_t kind, double thr, double I_s, int64_t x, i
 }
 
 __device__ inline double remaining_of(double thr, double I_s, int64_t x, int32_t a) {
-    return (thr - (double)x / I_s) - (double)a;
+    return (thr - div_interval((double)x, I_s)) - (double)a;
 }
 
 __device__ inline void reject_limited(const Verdicts &V, uint32_t seq) {
@@ -669,7 +708,7 @@ __global__ __launch_bounds__(256) void k_process_reg(KeyTable T, BatchWork W, Ev
 #pragma unroll
     for (int j = 0; j < NMAX; ++j) {
         if (j < nsc) {
-            const longlong2 v = *reinterpret_cast<const longlong2 *>(ks.base + 2 * j);
+            const longlong2 v = *reinterpret_cast<const longlong2 *>(ks.pair(j));
             ep[j] = v.x;
             ps[j] = v.y;
         } else {
@@ -689,7 +728,7 @@ __global__ __launch_bounds__(256) void k_process_reg(KeyTable T, BatchWork W, Ev
         if (slow) {
 #pragma unroll
             for (int j = 0; j < NMAX; ++j)
-                if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.base + 2 * j) = longlong2{ep[j], ps[j]};
+                if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.pair(j)) = longlong2{ep[j], ps[j]};
             dirty = 0;
             for (uint32_t i = st; i < st + len; ++i) {
                 const uint32_t seq = (uint32_t)W.sval[i] & SEQ_MASK;
@@ -745,7 +784,7 @@ __global__ __launch_bounds__(256) void k_process_reg(KeyTable T, BatchWork W, Ev
     }
 #pragma unroll
     for (int j = 0; j < NMAX; ++j)
-        if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.base + 2 * j) = longlong2{ep[j], ps[j]};
+        if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.pair(j)) = longlong2{ep[j], ps[j]};
 }
 
 // K1+K3 with a lane group per key (G lanes, up to PROC_SLOTS_PER_LANE slots per lane, so

@@ -282,6 +282,7 @@ struct sentinel_engine {
     DevBuf d_flow_route, d_flow_ids;
     bool flow_plain = true;          // no flow needs a limiter or namespace check
     int32_t flow_max_n = 1;
+    int32_t flow_hblock = 2;        // slots per block of the flow header region (>= every flow's n)
     int process_impl = 0;
     bool verdict_nt = false;   // SENTINEL_VERDICT_NT=1: non-temporal verdict stores
     bool use_lookback = true;  // SENTINEL_SCAN=3pass selects the three-kernel scan
@@ -440,6 +441,7 @@ struct sentinel_engine {
         T.state = b.state.as<int64_t>();
         T.occ = b.occ.as<int64_t>();
         T.has_occ = b.has_occ.as<uint8_t>();
+        T.hblock = &b == &ft ? flow_hblock : 0;
         T.ncounters = ncounters;
         T.max_occupy_ratio = cfg.max_occupy_ratio;
         return T;
@@ -803,22 +805,34 @@ int sentinel_engine::rebuild_limiters() {
 }
 
 // Partition-local flow path (partition.hpp): prep + range histogram, scan, one multi-split pass,
-// one fused decide pass per flow range.
+// one fused sort + decide pass per flow range (LDS), oversized ranges redone from HBM, hot flows.
 template <int NMAX>
-static void launch_part_runs(sentinel_engine_t *e, unsigned nparts, const KeyTable &FT, const uint32_t *offsets,
-                             int64_t nb, int lb, const EventSrc &src, const Verdicts &V, int64_t n, hipStream_t s) {
-    const dim3 grid(nparts, (unsigned)(((1u << lb) + PR_THREADS - 1) / PR_THREADS));
-    uint32_t *runs = e->w_runs.as<uint32_t>();
-    uint32_t *nlong = runs + ((size_t)nparts << (lb + 1)) + nparts;
-    uint32_t *long_runs = nlong + 1;
-    (void)hipMemsetAsync(nlong, 0, 4, s);
-    e->launch("part_runs", n, s, [&] {
-        k_part_runs<NMAX><<<grid, PR_THREADS, 0, s>>>(FT, e->w_vtmp.as<uint64_t>(), offsets, nb, lb, runs,
-                                               runs + ((size_t)nparts << lb), runs + ((size_t)nparts << (lb + 1)), src,
-                                               V, long_runs, nlong);
+static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTable &FT, const uint32_t *offsets,
+                               int64_t nb, int lb, const EventSrc &src, const Verdicts &V, int64_t n, hipStream_t s,
+                               uint32_t *ctl, unsigned long long *stat) {
+    // ctl: [0] long-run count, [1] oversized-half count, [2, 2 + 2 nparts) oversized halves, then long runs
+    uint32_t *nlong = ctl, *nbig = ctl + 1, *big = ctl + 2;
+    uint32_t *long_runs = big + 2 * (size_t)nparts;
+    uint16_t *pkey = e->w_pkey.as<uint16_t>();
+    const uint64_t *pval = e->w_sval.as<uint64_t>();
+    uint64_t *gsval = e->w_vtmp.as<uint64_t>();
+    (void)hipMemsetAsync(ctl, 0, 8, s);
+    // a batch whose mean range does not fit goes straight to the HBM-sorting kernel
+    const bool all_big = n > (int64_t)nparts * (int64_t)(PH_KEYS * 3 / 4);
+    if (!all_big) {
+        e->launch("part_fused", n, s, [&] {
+            k_part_half<NMAX><<<16u * (unsigned)((nparts + 7) / 8), PH_THREADS, 0, s>>>(
+                FT, pkey, pval, gsval, offsets, nb, lb, nparts, (int32_t)e->rules.size(), src, V, long_runs, nlong, big,
+                nbig, stat);
+        });
+    }
+    e->launch("part_big", n, s, [&] {
+        k_part_big<NMAX><<<all_big ? 2u * (unsigned)nparts : (unsigned)std::min<int32_t>(2 * nparts, 256), PH_THREADS, 0, s>>>(
+            FT, pkey, pval, gsval, offsets, nb, lb, nparts, src, V, long_runs, nlong, all_big ? nullptr : big, nbig,
+            stat);
     });
     e->launch("part_long", n, s, [&] {   // hot flows (runs > LONG_RUN events): a workgroup each
-        k_part_long<NMAX><<<256, PL_THREADS, 0, s>>>(FT, e->w_vtmp.as<uint64_t>(), long_runs, nlong, src, V);
+        k_part_long<NMAX><<<256, PL_THREADS, 0, s>>>(FT, gsval, long_runs, nlong, src, V);
     });
 }
 
@@ -846,10 +860,8 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
                                                                          e->w_sval.as<uint64_t>(), n, finvalid, lb, pbits,
                                                                          hist, nb, nparts);
     });
-    // run starts + run flows (2^lb per range), runs per range, long-run count + {q0, q1, flow} records
-    int rc = e->w_runs.ensure((((size_t)nparts << (lb + 1)) + (size_t)nparts + 1 + 3 * ((size_t)n / LONG_RUN + 2)) * 4);
+    int rc = e->w_runs.ensure((2 + 2 * (size_t)nparts + 3 * ((size_t)n / LONG_RUN + 2)) * 4);
     if (rc) return rc;
-    uint32_t *runs = e->w_runs.as<uint32_t>();
     if (!e->d_part_stat.p) {
         rc = e->d_part_stat.ensure(8);
         if (rc) return rc;
@@ -858,20 +870,15 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
     }
     unsigned long long *stat = e->d_part_stat.as<unsigned long long>();
     HIP_OK(hipMemsetAsync(stat, 0, 8, s));
-    e->launch("part_sort", n, s, [&] {
-        k_part_sort<<<(unsigned)nparts, PSORT_THREADS, 0, s>>>(e->w_pkey.as<uint16_t>(), e->w_sval.as<uint64_t>(),
-                                                               e->w_vtmp.as<uint64_t>(), hist, nb, lb, runs,
-                                                               runs + ((size_t)nparts << lb),
-                                                               runs + ((size_t)nparts << (lb + 1)), stat);
-    });
-    HIP_OK(hipMemcpyAsync(e->h_part_stat, stat, 8, hipMemcpyDeviceToHost, s));
     const KeyTable FT = e->table(e->ft, NEV, 0);
     const Verdicts V{out, fkey, finvalid};
+    uint32_t *ctl = e->w_runs.as<uint32_t>();
     const int mx = e->flow_max_n;
-    if (mx <= 2) launch_part_runs<2>(e, (unsigned)nparts, FT, hist, nb, lb, src, V, n, s);
-    else if (mx <= 4) launch_part_runs<4>(e, (unsigned)nparts, FT, hist, nb, lb, src, V, n, s);
-    else if (mx <= 10) launch_part_runs<10>(e, (unsigned)nparts, FT, hist, nb, lb, src, V, n, s);
-    else launch_part_runs<16>(e, (unsigned)nparts, FT, hist, nb, lb, src, V, n, s);
+    if (mx <= 2) launch_part_decide<2>(e, nparts, FT, hist, nb, lb, src, V, n, s, ctl, stat);
+    else if (mx <= 4) launch_part_decide<4>(e, nparts, FT, hist, nb, lb, src, V, n, s, ctl, stat);
+    else if (mx <= 10) launch_part_decide<10>(e, nparts, FT, hist, nb, lb, src, V, n, s, ctl, stat);
+    else launch_part_decide<16>(e, nparts, FT, hist, nb, lb, src, V, n, s, ctl, stat);
+    HIP_OK(hipMemcpyAsync(e->h_part_stat, stat, 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipGetLastError());
     return 0;
 }
@@ -1210,6 +1217,12 @@ int sentinel_profile_enable(sentinel_engine_t *e, int enable) {
     return 0;
 }
 
+#ifdef SENTINEL_DIAG_PHASES
+int sentinel_diag_phases(unsigned long long *out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), (size_t)n * 5 * 8) == hipSuccess ? 0 : -1;
+}
+#endif
+
 int sentinel_profile_read(sentinel_engine_t *e, int max, char *names32, double *total_ms, int64_t *calls,
                           int64_t *units) {
     if (!e || max < 0 || (max > 0 && (!names32 || !total_ms || !calls || !units))) return fail(SENTINEL_E_INVALID, "bad arguments");
@@ -1299,7 +1312,13 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
     std::vector<int32_t> nn(F), ww(F);
     std::vector<double> rcp(F), Is(F);
     std::vector<uint8_t> kind(F);
-    int64_t words = 0;
+    // layout: blocked slot-major header region (HB_KEYS flows x hblock slots per block), then the
+    // rest lines of every flow at off[i]
+    int32_t maxn = 1;
+    for (size_t i = 0; i < F; ++i) maxn = std::max(maxn, e->rules[i].sample_count);
+    const int32_t hblock = header_block_slots(maxn);
+    const int64_t hwords = (((int64_t)F + HB_KEYS - 1) / HB_KEYS) * hblock * HB_KEYS * 2;
+    int64_t words = hwords;
     for (size_t i = 0; i < F; ++i) {
         const sentinel_flow_rule_t &r = e->rules[i];
         off[i] = words;
@@ -1309,22 +1328,28 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
         Is[i] = r.window_interval_ms / 1000.0;   // LeapArray.java:74
         kind[i] = r.checker == SENTINEL_CHECKER_SIMPLE ? KIND_SIMPLE : KIND_CLUSTER;
         ids[i] = r.flow_id;
-        words += flow_record_words(r.sample_count);
+        words += 8 * (int64_t)r.sample_count;
     }
     // new state image: fresh, then carry surviving flows whose window shape is unchanged
     std::vector<int64_t> st(std::max<int64_t>(words, 1), 0);
     std::vector<int64_t> occ(2 * std::max<size_t>(F, 1), 0);
     std::vector<uint8_t> hocc(std::max<size_t>(F, 1), 0);
     std::vector<int32_t> now(std::max<size_t>(F, 1), 0);
+    const int32_t old_hblock = e->flow_hblock;
     for (size_t i = 0; i < F; ++i) {
-        for (int j = 0; j < nn[i]; ++j) st[off[i] + 2 * j] = EPOCH_ABSENT;
+        for (int j = 0; j < nn[i]; ++j) st[blocked_pair_word((int64_t)i, hblock, j)] = EPOCH_ABSENT;
         auto it = old_index.find(ids[i]);
         if (it == old_index.end()) continue;
         const int32_t o = it->second;
         now[i] = old_now[o];       // CurrentConcurrencyManager keeps nowCalls of surviving flowIds (CFRM:356-358)
         // ClusterMetric is kept as constructed with the OLD (n, interval): only carry when equal
         if (old_n[o] != nn[i] || old_w[o] != ww[i]) continue;
-        std::copy(old_state.begin() + old_off[o], old_state.begin() + old_off[o] + flow_record_words(nn[i]),
+        for (int j = 0; j < nn[i]; ++j) {
+            const int64_t a = blocked_pair_word((int64_t)o, old_hblock, j), b = blocked_pair_word((int64_t)i, hblock, j);
+            st[b] = old_state[a];
+            st[b + 1] = old_state[a + 1];
+        }
+        std::copy(old_state.begin() + old_off[o], old_state.begin() + old_off[o] + 8 * (int64_t)nn[i],
                   st.begin() + off[i]);
         occ[2 * i] = old_occ[2 * o];
         occ[2 * i + 1] = old_occ[2 * o + 1];
@@ -1350,6 +1375,7 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
     e->h_flow_n = nn;
     e->h_flow_w = ww;
     e->flow_state_words = words;
+    e->flow_hblock = hblock;
     e->flow_max_n = nn.empty() ? 1 : *std::max_element(nn.begin(), nn.end());
     rc = e->rewrite_tokens(false);
     if (rc) return rc;
@@ -1898,20 +1924,22 @@ int sentinel_dump_flow(sentinel_engine_t *e, int32_t idx, int64_t *out, int32_t 
     if (out_len < need) return fail(SENTINEL_E_INVALID, "output too small");
     HIP_OK(hipSetDevice(e->device));
     HIP_OK(hipStreamSynchronize(e->stream));
-    std::vector<int64_t> st(flow_record_words(n));
-    HIP_OK(hipMemcpy(st.data(), e->ft.state.as<int64_t>() + e->h_flow_off[idx], st.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<int64_t> hdr(2 * (size_t)n), rest(8 * (size_t)n);
+    for (int j = 0; j < n; ++j)
+        HIP_OK(hipMemcpy(hdr.data() + 2 * j, e->ft.state.as<int64_t>() + blocked_pair_word(idx, e->flow_hblock, j), 16,
+                         hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(rest.data(), e->ft.state.as<int64_t>() + e->h_flow_off[idx], rest.size() * 8, hipMemcpyDeviceToHost));
     int64_t occ[2];
     uint8_t hocc;
     HIP_OK(hipMemcpy(occ, e->ft.occ.as<int64_t>() + 2 * idx, 16, hipMemcpyDeviceToHost));
     HIP_OK(hipMemcpy(&hocc, e->ft.has_occ.as<uint8_t>() + idx, 1, hipMemcpyDeviceToHost));
     const int64_t w = e->h_flow_w[idx];
-    const int64_t hw = header_words(n);
     for (int j = 0; j < n; ++j) {
         int64_t *o = out + j * (1 + NEV);
-        const bool present = st[2 * j] != EPOCH_ABSENT;
-        o[0] = present ? st[2 * j] * w : -1;
-        o[1 + EV_PASS] = present ? st[2 * j + 1] : 0;
-        for (int c = 1; c < NEV; ++c) o[1 + c] = present ? st[hw + 8 * j + (c - 1)] : 0;
+        const bool present = hdr[2 * j] != EPOCH_ABSENT;
+        o[0] = present ? hdr[2 * j] * w : -1;
+        o[1 + EV_PASS] = present ? hdr[2 * j + 1] : 0;
+        for (int c = 1; c < NEV; ++c) o[1 + c] = present ? rest[8 * j + (c - 1)] : 0;
     }
     int64_t *o = out + n * (1 + NEV);
     for (int c = 0; c < NEV; ++c) o[c] = 0;

@@ -168,8 +168,14 @@ struct FlowWindow {
     int64_t ep[NMAX], ps[NMAX];
     uint32_t dirty;
     bool occ_pending;
+    // batch clock: epoch of T0 and T0 mod w, so an event's epoch is E0 + floor((r0 + dt) / w) in
+    // 32-bit arithmetic (dt = ts - T0 from the packed value, |dt| < 2^23)
+    int64_t E0;
+    int32_t r0;
+    float rcpf;
 
-    __device__ inline void load(const KeyTable &T, uint32_t key) {
+    // the rule part: independent loads only (may be issued long before the header is needed)
+    __device__ inline void load_rule(const KeyTable &T, uint32_t key) {
         ks = key_state(T, key);
         nsc = ks.n;
         kind = T.kind[key];
@@ -177,25 +183,72 @@ struct FlowWindow {
         I_s = T.I_s[key];
         w = T.w[key];
         rcp = T.rcp_w[key];
+        occ_pending = T.has_occ[key] != 0;
+    }
+
+    __device__ inline void load_header(int64_t T0) {
+        occ_pending = occ_pending && ks.seven && kind == KIND_CLUSTER;
         dirty = 0;
+        if (ks.hs != 2) {
+            // blocked header region with NMAX slots per block: every pair load is in bounds, so
+            // they are all issued without waiting for n
 #pragma unroll
-        for (int j = 0; j < NMAX; ++j) {
-            if (j < nsc) {
-                const longlong2 v = *reinterpret_cast<const longlong2 *>(ks.base + 2 * j);
-                ep[j] = v.x;
-                ps[j] = v.y;
-            } else {
-                ep[j] = EPOCH_ABSENT;
-                ps[j] = 0;
+            for (int j = 0; j < NMAX; ++j) {
+                const longlong2 v = *reinterpret_cast<const longlong2 *>(ks.pair(j));
+                ep[j] = j < nsc ? v.x : EPOCH_ABSENT;
+                ps[j] = j < nsc ? v.y : 0;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j) {
+                if (j < nsc) {
+                    const longlong2 v = *reinterpret_cast<const longlong2 *>(ks.pair(j));
+                    ep[j] = v.x;
+                    ps[j] = v.y;
+                } else {
+                    ep[j] = EPOCH_ABSENT;
+                    ps[j] = 0;
+                }
             }
         }
-        occ_pending = ks.seven && kind == KIND_CLUSTER && T.has_occ[key];
+        E0 = epoch_of(T0, w, rcp);
+        r0 = (int32_t)(T0 - E0 * (int64_t)w);
+        rcpf = 1.0f / (float)w;
+    }
+
+    __device__ inline void load(const KeyTable &T, uint32_t key, int64_t T0) {
+        load_rule(T, key);
+        load_header(T0);
+    }
+
+    // Epoch, acquire and prioritized flag of a packed value.  Exact: q is within one of
+    // floor(x / w) (x < 2^24 is exact in float, the product is off by at most one ulp) and the
+    // remainder test fixes it; escaped values take the 64-bit path.
+    __device__ inline int64_t event(uint64_t v, const EventSrc &src, int64_t T0, int32_t &a, bool &prio) const {
+        const uint32_t dtf = (uint32_t)(v >> VAL_DT_SHIFT) & VAL_DT_ESC;
+        const uint32_t af = (uint32_t)(v >> VAL_ACQ_SHIFT) & VAL_ACQ_ESC;
+        prio = (v & VAL_PRIO) != 0;
+        if (dtf == VAL_DT_ESC || af == VAL_ACQ_ESC || w >= (1 << 30)) {
+            int64_t t;
+            src.unpack(v, T0, t, a, prio);
+            return epoch_of(t, w, rcp);
+        }
+        a = src.unit_acquire ? 1 : (int32_t)af;
+        const int32_t x = r0 + ((int32_t)(dtf << 8) >> 8);
+        int32_t q = (int32_t)floorf((float)x * rcpf);
+        const int32_t rem = x - q * w;
+        if (rem < 0) --q;
+        else if (rem >= w) ++q;
+        return E0 + q;
     }
 
     __device__ inline void flush() {
+#ifdef SENTINEL_DIAG_NOFLUSH    // cost diagnostic only (wrong state)
+        return;
+#endif
 #pragma unroll
         for (int j = 0; j < NMAX; ++j)
-            if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.base + 2 * j) = longlong2{ep[j], ps[j]};
+            if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.pair(j)) = longlong2{ep[j], ps[j]};
         dirty = 0;
     }
 
@@ -248,7 +301,11 @@ struct FlowWindow {
 #pragma unroll
         for (int j = 0; j < NMAX; ++j)
             if (j == slot) { ps[j] = wrap_add(ps[j], wrap_mul((int64_t)K, a)); dirty |= 1u << j; }
+#ifdef SENTINEL_DIAG_NOREST     // cost diagnostic only (wrong counters)
+        if (false) {
+#else
         if (ks.seven) {
+#endif
             int64_t *r = ks.rest(slot);
             int64_t blk = 0, preq = 0, breq = 0;
             if (!fresh) { blk = r[0]; preq = r[1]; breq = r[2]; }
@@ -261,34 +318,31 @@ struct FlowWindow {
         }
     }
 
-    __device__ inline uint64_t verdict(int64_t s0, int32_t a, uint32_t K, uint32_t k) const {
-        if (k < K) return pack_verdict(ST_OK, java_d2i(remaining_of(thr, I_s, wrap_add(s0, wrap_mul((int64_t)k, a)), a)), 0);
-        return pack_verdict(ST_BLOCKED, 0, 0);
+    // `small`: every S0 + k*a of the segment fits in int32, so the int64 -> double conversion is one
+    // v_cvt_f64_i32 (same value)
+    __device__ inline uint64_t verdict(int64_t s0, int32_t a, uint32_t K, uint32_t k, bool small) const {
+        if (k >= K) return pack_verdict(ST_BLOCKED, 0, 0);
+        const double x = small ? (double)((int32_t)s0 + (int32_t)k * a) : (double)wrap_add(s0, wrap_mul((int64_t)k, a));
+        return pack_verdict(ST_OK, java_d2i((thr - div_interval(x, I_s)) - (double)a), 0);
     }
 };
 
 // One flow's run of sorted events [q0, q1) (arrival order), decided by one lane; verdicts written
 // to the arrival positions.
 template <int NMAX>
-__device__ inline void part_run(const KeyTable &T, uint32_t key, const uint64_t *s_val, uint32_t q0, uint32_t q1,
-                                const EventSrc &src, const Verdicts &V, int64_t T0) {
-    FlowWindow<NMAX> fw;
-    fw.load(T, key);
+__device__ inline void part_run_w(FlowWindow<NMAX> &fw, const KeyTable &T, uint32_t key, const uint64_t *s_val,
+                                  uint32_t q0, uint32_t q1, const EventSrc &src, const Verdicts &V, int64_t T0) {
     uint32_t q = q0;
     while (q < q1) {
-        int64_t t;
         int32_t a;
         bool prio;
-        src.unpack(s_val[q], T0, t, a, prio);
-        const int64_t E = epoch_of(t, fw.w, fw.rcp);
+        const int64_t E = fw.event(s_val[q], src, T0, a, prio);
         bool het = prio && fw.kind == KIND_CLUSTER;
         uint32_t q2 = q + 1;
         for (; q2 < q1; ++q2) {                       // the segment: same epoch
-            int64_t t2;
             int32_t a2;
             bool p2;
-            src.unpack(s_val[q2], T0, t2, a2, p2);
-            if (epoch_of(t2, fw.w, fw.rcp) != E) break;
+            if (fw.event(s_val[q2], src, T0, a2, p2) != E) break;
             het |= a2 != a || (p2 && fw.kind == KIND_CLUSTER);
         }
         if (fw.slow(E, het)) {
@@ -296,12 +350,34 @@ __device__ inline void part_run(const KeyTable &T, uint32_t key, const uint64_t 
         } else {
             int64_t s0;
             uint32_t K;
-            fw.fast(E, a, q2 - q, s0, K);
-            for (uint32_t k = 0; k < q2 - q; ++k) V.out[(uint32_t)s_val[q + k] & SEQ_MASK] = fw.verdict(s0, a, K, k);
+            const uint32_t len = q2 - q;
+            fw.fast(E, a, len, s0, K);
+            const bool small = s0 >= 0 && s0 + (int64_t)len * a < (int64_t)INT32_MAX;
+#ifdef SENTINEL_DIAG_VLINEAR   // cost diagnostic only (wrong output): one 64-byte line per flow
+            for (uint32_t k = 0; k < len; ++k) V.out[key * 8 + (k & 7)] = fw.verdict(s0, a, K, k, small);
+#else
+#ifdef SENTINEL_DIAG_NOVERDICT  // cost diagnostic only (no output)
+            {
+                uint64_t acc = 0;
+                for (uint32_t k = 0; k < len; ++k) acc ^= fw.verdict(s0, a, K, k, small) ^ s_val[q + k];
+                if (acc == 0x123456789ull) V.out[0] = acc;
+            }
+#else
+            for (uint32_t k = 0; k < len; ++k) V.out[(uint32_t)s_val[q + k] & SEQ_MASK] = fw.verdict(s0, a, K, k, small);
+#endif
+#endif
         }
         q = q2;
     }
     fw.flush();
+}
+
+template <int NMAX>
+__device__ inline void part_run(const KeyTable &T, uint32_t key, const uint64_t *s_val, uint32_t q0, uint32_t q1,
+                                const EventSrc &src, const Verdicts &V, int64_t T0) {
+    FlowWindow<NMAX> fw;
+    fw.load(T, key, T0);
+    part_run_w<NMAX>(fw, T, key, s_val, q0, q1, src, V, T0);
 }
 
 // Runs longer than this are decided by a whole workgroup (k_part_long): one lane walking a hot
@@ -336,7 +412,7 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
         const uint32_t q0 = long_runs[3 * (uint64_t)r], q1 = long_runs[3 * (uint64_t)r + 1];
         const uint32_t key = long_runs[3 * (uint64_t)r + 2];
         FlowWindow<NMAX> fw;                      // meaningful in lane 0 only
-        if (threadIdx.x == 0) fw.load(T, key);
+        if (threadIdx.x == 0) fw.load(T, key, T0);
         const int32_t w = T.w[key];
         const double rcp = T.rcp_w[key];
         const bool cluster = T.kind[key] == KIND_CLUSTER;
@@ -595,6 +671,315 @@ __global__ __launch_bounds__(PR_THREADS) void k_part_runs(KeyTable T, const uint
     }
     if (staged) part_run<NMAX>(T, run_flow[i], lv, q0 - s0, q1 - s0, src, V, src.t0());
     else part_run<NMAX>(T, run_flow[i], sval, q0, q1, src, V, src.t0());
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused per-range sort + decide (the default partition kernels).  A flow range of 2^lb flows is
+// split in two halves of 2^hb flows (hb = lb - 1), one 512-thread workgroup per half, so that two
+// workgroups fit per CU (LDS ~58 KB, <= 128 VGPRs) and one's HBM round trips overlap the other's
+// work.  The two halves of a range run on the same XCD (blocks b and b + 8), so the range's keys
+// and values come from HBM once and from that XCD's L2 the second time.  Per half:
+//   1. all of the range's keys are loaded at once (24 per thread) and the half's events are
+//      ranked with ballots (stable: arrival order kept) -> per-flow counts -> flow starts;
+//   2. the half's values are gathered straight into their sorted slots in LDS;
+//   3. thread t decides local flow t from LDS (closed-form epoch segments / sequential fallback)
+//      and writes the verdicts to their arrival positions.
+// A range of more than PH_KEYS events, or a half of more than PH_CAP, is appended to `big` and
+// decided by k_part_big, which sorts into HBM; runs longer than LONG_RUN go to k_part_long.
+constexpr int PH_THREADS = 512;
+constexpr int PH_WAVES = PH_THREADS / WAVE;
+constexpr uint32_t PH_KEYS = 12288;                // range events scanned by a half's workgroup
+constexpr int PH_ITEMS = PH_KEYS / PH_THREADS;     // 24 keys per thread
+constexpr uint32_t PH_CAP = 6144;                  // events of one half sorted in LDS (48 KB)
+constexpr int PH_BINS = PART_BINS / 2;             // flows per half
+constexpr int PH_MAX_LONG = PH_CAP / (LONG_RUN + 1) + 1;
+constexpr uint32_t PH_SMALL_RUN = 32;              // longest run sorted by its own thread
+static_assert(PH_BINS == PH_THREADS, "one flow per thread");
+
+// Lanes of the wave holding the same key d (valid lanes only): one ballot per key bit, each
+// narrowing the candidate set to the lanes that agree on that bit.
+__device__ inline uint64_t match_peers(uint32_t d, bool valid, int nbits) {
+    uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
+#pragma unroll
+    for (int b = 0; b < PART_MAX_BITS; ++b) {
+        if (b < nbits) {
+            const uint64_t bal = __builtin_amdgcn_ballot_w64((d >> b) & 1u);
+            const uint64_t flip = ((d >> b) & 1u) ? 0ull : ~0ull;
+            peers &= bal ^ flip;
+        }
+    }
+    return peers;
+}
+
+// block b -> (range, half): both halves of a range on the XCD b mod 8
+__device__ inline void half_of_block(uint32_t b, uint32_t &p, uint32_t &h) {
+    p = (b & 7u) | ((b >> 4) << 3);
+    h = (b >> 3) & 1u;
+}
+
+#ifdef SENTINEL_DIAG_PHASES     // cost diagnostic: wall-clock stamps per workgroup and phase
+__device__ unsigned long long g_phase[4096][5];
+#define PF_STAMP(i) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_phase[blockIdx.x][i] = wall_clock64(); } while (0)
+#else
+#define PF_STAMP(i) do { } while (0)
+#endif
+
+// The part of a flow's window decision that follows the sort: hot runs are handed to k_part_long
+// (their events copied to HBM first when they sit in LDS), the others decided here.
+template <int NMAX>
+__device__ inline void part_decide_flow(const KeyTable &T, uint32_t key, const uint64_t *vals, uint32_t st,
+                                        uint32_t c, const EventSrc &src, const Verdicts &V, int64_t T0) {
+    if (c > 0 && c <= LONG_RUN) part_run<NMAX>(T, key, vals, st, st + c, src, V, T0);
+}
+
+template <int NMAX>
+__global__ __launch_bounds__(PH_THREADS, NMAX > 10 ? 2 : 4) void k_part_half(
+    KeyTable T, const uint16_t *__restrict__ pkey, const uint64_t *__restrict__ pval, uint64_t *__restrict__ gsval,
+    const uint32_t *__restrict__ offsets, int64_t nblocks, int lb, int32_t nranges, int32_t nflows, EventSrc src, Verdicts V,
+    uint32_t *__restrict__ long_runs, uint32_t *__restrict__ nlong, uint32_t *__restrict__ big,
+    uint32_t *__restrict__ nbig, unsigned long long *__restrict__ max_range) {
+    __shared__ uint64_t sv[PH_CAP];
+    __shared__ uint16_t cnt[PH_WAVES][PH_BINS];
+    __shared__ uint32_t base[PH_BINS];
+    __shared__ uint32_t waves_tot[PH_WAVES];
+    __shared__ uint32_t s_nlong, s_cmax;
+    __shared__ uint32_t s_long[PH_MAX_LONG][2];
+    uint32_t p, h;
+    half_of_block(blockIdx.x, p, h);
+    const int hb = lb > 0 ? lb - 1 : 0;
+    if ((int32_t)p >= nranges || (lb == 0 && h == 1)) return;
+    const int wave = threadIdx.x / WAVE;
+    const uint32_t lane = lane_id();
+    const uint32_t t = threadIdx.x;
+    const int64_t T0 = src.t0();
+    const uint32_t pstart = offsets[(int64_t)p * nblocks];
+    const uint32_t pend = offsets[(int64_t)(p + 1) * nblocks];
+    const uint32_t size = pend - pstart;
+    if (t == 0 && h == 0 && max_range) atomicMax(max_range, (unsigned long long)size);   // skew statistic
+    if (size > PH_KEYS) {                                 // block-uniform
+        if (t == 0) big[atomicAdd(nbig, 1u)] = (p << 1) | h;
+        return;
+    }
+    PF_STAMP(0);
+    // 1. keys (all at once) -> per-flow counts (LDS atomics) -> flow starts
+    const uint32_t b0 = (uint32_t)wave * (PH_ITEMS * WAVE);
+    const uint32_t hmask = (1u << hb) - 1u;
+    uint32_t kk[PH_ITEMS];                                // local flow, or 0xFFFFFFFF: not this half's
+#pragma unroll
+    for (int j = 0; j < PH_ITEMS; ++j) {
+        const uint32_t q = b0 + j * WAVE + lane;
+        const uint32_t k = q < size ? (uint32_t)pkey[pstart + q] : 0xFFFFFFFFu;
+        kk[j] = (k != 0xFFFFFFFFu && (k >> hb) == h) ? (k & hmask) : 0xFFFFFFFFu;
+    }
+    base[t] = 0;
+    if (t == 0) { s_nlong = 0; s_cmax = 0; }
+    __syncthreads();
+    const uint32_t key = (p << lb) | (h << hb) | t;
+    FlowWindow<NMAX> fw;                                  // rule fields in flight during the sort
+    if (t <= hmask && key < (uint32_t)nflows) fw.load_rule(T, key);
+#pragma unroll
+    for (int j = 0; j < PH_ITEMS; ++j)
+        if (kk[j] != 0xFFFFFFFFu) atomicAdd(&base[kk[j]], 1u);
+    __syncthreads();
+    const uint32_t c = base[t];                           // this thread's flow: events in the half
+    uint32_t total;
+    const uint32_t start = block_exclusive_scan(c, waves_tot, &total);
+    if (total > PH_CAP) {                                 // block-uniform: the half does not fit in LDS
+        if (t == 0) big[atomicAdd(nbig, 1u)] = (p << 1) | h;
+        return;
+    }
+    if (c) atomicMax(&s_cmax, c);
+    base[t] = start;
+    uint64_t val[PH_ITEMS];                               // all value loads in flight together
+#pragma unroll
+    for (int j = 0; j < PH_ITEMS; ++j)
+        val[j] = kk[j] != 0xFFFFFFFFu ? pval[pstart + b0 + j * WAVE + lane] : 0ull;
+    __syncthreads();
+    PF_STAMP(1);
+    // 2. values into their flow's slots, in arrival order
+    if (s_cmax <= PH_SMALL_RUN) {
+        // short runs (the common case): unordered slots by LDS atomics, then each thread
+        // insertion-sorts its own run by arrival position (the low bits of the value)
+#pragma unroll
+        for (int j = 0; j < PH_ITEMS; ++j)
+            if (kk[j] != 0xFFFFFFFFu) sv[atomicAdd(&base[kk[j]], 1u)] = val[j];
+        __syncthreads();
+        for (uint32_t i = start + 1; i < start + c; ++i) {
+            const uint64_t v = sv[i];
+            const uint32_t sq = (uint32_t)v & SEQ_MASK;
+            uint32_t j = i;
+            for (; j > start; --j) {
+                const uint64_t u = sv[j - 1];
+                if (((uint32_t)u & SEQ_MASK) < sq) break;
+                sv[j] = u;
+            }
+            sv[j] = v;
+        }
+    } else {
+        // a long run somewhere: stable ranking with ballots (arrival order kept by construction)
+        {
+            uint32_t *z = reinterpret_cast<uint32_t *>(&cnt[0][0]);
+            for (int d = t; d < PH_WAVES * PH_BINS / 2; d += PH_THREADS) z[d] = 0;
+        }
+        __syncthreads();
+        uint32_t rank[PH_ITEMS];
+#pragma unroll
+        for (int j = 0; j < PH_ITEMS; ++j) {
+            const bool valid = kk[j] != 0xFFFFFFFFu;
+            const uint32_t d = kk[j] & hmask;
+            const uint64_t peers = match_peers(d, valid, hb);
+            uint32_t r = 0;
+            if (valid) r = cnt[wave][d] + mask_rank(peers);
+            __builtin_amdgcn_wave_barrier();
+            if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane) cnt[wave][d] += (uint16_t)__popcll(peers);
+            __builtin_amdgcn_wave_barrier();
+            rank[j] = r;
+        }
+        __syncthreads();
+        uint32_t run = 0;
+#pragma unroll
+        for (int w = 0; w < PH_WAVES; ++w) {
+            const uint32_t x = cnt[w][t];
+            cnt[w][t] = (uint16_t)run;
+            run += x;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PH_ITEMS; ++j) {
+            if (kk[j] == 0xFFFFFFFFu) continue;
+            sv[base[kk[j]] + cnt[wave][kk[j]] + rank[j]] = val[j];
+        }
+    }
+    __syncthreads();
+    PF_STAMP(2);
+    // 3. decide.  Hot runs go to k_part_long from HBM: the half's region of gsval is its own
+    // (half 0 at the range start, half 1 at its end).
+    const uint32_t goff = pstart + (h ? size - total : 0u);
+    if (c > LONG_RUN) {
+        const uint32_t j = atomicAdd(nlong, 1u);
+        long_runs[3 * (uint64_t)j] = goff + start;
+        long_runs[3 * (uint64_t)j + 1] = goff + start + c;
+        long_runs[3 * (uint64_t)j + 2] = key;
+        const uint32_t l = atomicAdd(&s_nlong, 1u);
+        s_long[l][0] = start;
+        s_long[l][1] = c;
+    }
+    __syncthreads();
+    for (uint32_t l = 0; l < s_nlong; ++l)
+        for (uint32_t q = t; q < s_long[l][1]; q += PH_THREADS) gsval[goff + s_long[l][0] + q] = sv[s_long[l][0] + q];
+    if (c > 0 && c <= LONG_RUN) {
+        fw.load_header(T0);
+        part_run_w<NMAX>(fw, T, key, sv, start, start + c, src, V, T0);
+    }
+#ifdef SENTINEL_DIAG_PHASES
+    __syncthreads();
+    PF_STAMP(3);
+#endif
+}
+
+// Oversized halves (or every half, `big == nullptr`): the same decision with the half sorted into
+// HBM in chunks (any size).  Entry = (range << 1) | half.
+constexpr int PB_ITEMS = 8;
+constexpr int PB_CHUNK = PH_THREADS * PB_ITEMS;
+
+template <int NMAX>
+__global__ __launch_bounds__(PH_THREADS) void k_part_big(
+    KeyTable T, const uint16_t *__restrict__ pkey, const uint64_t *__restrict__ pval, uint64_t *__restrict__ gsval,
+    const uint32_t *__restrict__ offsets, int64_t nblocks, int lb, int32_t nranges, EventSrc src, Verdicts V,
+    uint32_t *__restrict__ long_runs, uint32_t *__restrict__ nlong, const uint32_t *__restrict__ big,
+    const uint32_t *__restrict__ nbig, unsigned long long *__restrict__ max_range) {
+    __shared__ uint16_t cnt[PH_WAVES][PH_BINS];
+    __shared__ uint32_t base[PH_BINS];
+    __shared__ uint32_t waves_tot[PH_WAVES];
+    const int wave = threadIdx.x / WAVE;
+    const uint32_t lane = lane_id();
+    const uint32_t t = threadIdx.x;
+    const int64_t T0 = src.t0();
+    const int hb = lb > 0 ? lb - 1 : 0;
+    const uint32_t hmask = (1u << hb) - 1u;
+    const uint32_t nwork = big ? *nbig : 2u * (uint32_t)nranges;
+    for (uint32_t wi = blockIdx.x; wi < nwork; wi += gridDim.x) {
+        const uint32_t e = big ? big[wi] : wi;
+        const uint32_t p = e >> 1, h = e & 1u;
+        if (lb == 0 && h == 1) continue;                  // block-uniform
+        const uint32_t pstart = offsets[(int64_t)p * nblocks];
+        const uint32_t pend = offsets[(int64_t)(p + 1) * nblocks];
+        const uint32_t size = pend - pstart;
+        if (!big && h == 0 && t == 0 && max_range) atomicMax(max_range, (unsigned long long)size);
+        base[t] = 0;
+        __syncthreads();
+        for (uint32_t q = pstart + t; q < pend; q += PH_THREADS) {
+            const uint32_t k = pkey[q];
+            if ((k >> hb) == h) atomicAdd(&base[k & hmask], 1u);
+        }
+        __syncthreads();
+        const uint32_t c = base[t];
+        uint32_t total;
+        const uint32_t start = block_exclusive_scan(c, waves_tot, &total);
+        const uint32_t goff = pstart + (h ? size - total : 0u);
+        base[t] = start;
+        uint64_t *dst = gsval + goff;
+        for (uint32_t c0 = pstart; c0 < pend; c0 += PB_CHUNK) {
+            const uint32_t cn = min((uint32_t)PB_CHUNK, pend - c0);
+            {
+                uint32_t *z = reinterpret_cast<uint32_t *>(&cnt[0][0]);
+                for (int d = t; d < PH_WAVES * PH_BINS / 2; d += PH_THREADS) z[d] = 0;
+            }
+            __syncthreads();
+            uint32_t kk[PB_ITEMS], rank[PB_ITEMS];
+            uint64_t val[PB_ITEMS];
+            const uint32_t b0 = (uint32_t)wave * (PB_ITEMS * WAVE);
+#pragma unroll
+            for (int j = 0; j < PB_ITEMS; ++j) {
+                const uint32_t qq = b0 + j * WAVE + lane;
+                kk[j] = qq < cn ? (uint32_t)pkey[c0 + qq] : 0xFFFFFFFFu;
+                val[j] = qq < cn ? pval[c0 + qq] : 0ull;
+            }
+#pragma unroll
+            for (int j = 0; j < PB_ITEMS; ++j) {
+                const bool valid = kk[j] != 0xFFFFFFFFu && (kk[j] >> hb) == h;
+                const uint32_t d = kk[j] & hmask;
+                uint64_t peers = __ballot(valid);
+                for (int bb = 0; bb < hb; ++bb) {
+                    const bool bit = (d >> bb) & 1u;
+                    const uint64_t bal = __ballot(valid && bit);
+                    peers &= bit ? bal : ~bal;
+                }
+                uint32_t r = 0;
+                if (valid) r = cnt[wave][d] + mask_rank(peers);
+                __builtin_amdgcn_wave_barrier();
+                if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane) cnt[wave][d] += (uint16_t)__popcll(peers);
+                __builtin_amdgcn_wave_barrier();
+                rank[j] = valid ? r : 0xFFFFFFFFu;
+            }
+            __syncthreads();
+            uint32_t run = 0;
+#pragma unroll
+            for (int w = 0; w < PH_WAVES; ++w) {
+                const uint32_t x = cnt[w][t];
+                cnt[w][t] = (uint16_t)run;
+                run += x;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < PB_ITEMS; ++j) {
+                if (rank[j] == 0xFFFFFFFFu) continue;
+                const uint32_t d = kk[j] & hmask;
+                dst[base[d] + cnt[wave][d] + rank[j]] = val[j];
+            }
+            __syncthreads();
+            base[t] += run;
+        }
+        const uint32_t key = (p << lb) | (h << hb) | t;
+        if (c > LONG_RUN) {
+            const uint32_t j = atomicAdd(nlong, 1u);
+            long_runs[3 * (uint64_t)j] = goff + start;
+            long_runs[3 * (uint64_t)j + 1] = goff + start + c;
+            long_runs[3 * (uint64_t)j + 2] = key;
+        }
+        if (t <= hmask) part_decide_flow<NMAX>(T, key, dst, start, c, src, V, T0);
+        __syncthreads();                                  // LDS reuse by the next entry
+    }
 }
 
 }  // namespace sentinel
