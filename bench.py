@@ -39,7 +39,6 @@ KERNEL_BYTES_PER_EVENT = {
     "verdict": 20.0,          # read segid 4 + value 8, write the 8-B verdict
     "part_prep": 20.0,        # read the 16-B event, write the 4-B key (range histogram in LDS)
     "part_scatter": 30.0,     # read key 4 + event 16, write local key 2 + value 8
-    "part_sort": 22.0,        # read local key twice 4 + value 8, write value 8 (range-local, L2-resident), run records
 }
 
 
@@ -47,8 +46,8 @@ KERNEL_BYTES_PER_EVENT = {
 KERNEL_SYMBOLS = {
     "flow_prep": ("k_flow_prep",), "radix_hist": ("k_radix_hist_pass",), "radix_scatter": ("k_radix_scatter_p",),
     "scan": ("k_scan_lookback",), "segments": ("k_segments",), "process": ("k_process",), "verdict": ("k_verdict",),
-    "part_prep": ("k_part_prep",), "part_scatter": ("k_part_scatter",), "part_sort": ("k_part_sort",),
-    "part_runs": ("k_part_runs",),
+    "part_prep": ("k_part_prep",), "part_scatter": ("k_part_scatter",),
+    "part_fused": ("k_part_half",), "part_big": ("k_part_big",), "part_long": ("k_part_long",),
 }
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
 
@@ -227,11 +226,12 @@ def main():
             # per touched flow: read n epochs + n PASS, write epoch + 4 counters; per event: segment record
             e_f = N / max(1, F)
             bpe = (args.sample_count * 16 + 40 + 24) / max(1.0, min(e_f, 1e9)) if F else 0.0
-        if dom == "part_runs":
-            # per event: read local key 2 + value 8, write the 8-B verdict; per touched flow: the
-            # window header (16 B per bucket) read + written back, one 64-B counter line read + written
+        if dom == "part_fused":
+            # per event: read local key 2 + value 8, write the 8-B verdict; per touched flow: read
+            # the window header (16 B per bucket) and the 42 B of rule fields, write back the rolled
+            # bucket's 16-B pair, read + write its 64-B counter line
             e_f = N / max(1, F)
-            bpe = 18.0 + (args.sample_count * 16 * 2 + 128) / max(1.0, e_f)
+            bpe = 18.0 + (args.sample_count * 16 + 42 + 16 + 128) / max(1.0, e_f)
         if dom == "radix_scatter":
             passes = max(1, round(d["calls"] / max(1, args.steps)))
             bpe = (32.0 + 24.0 * (passes - 1)) / passes

@@ -376,13 +376,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter_p(
         const int64_t i = base + j * WAVE + lane;
         const bool valid = i < n;
         const uint32_t d = (key[j] >> shift) & (RADIX - 1);
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < RADIX_BITS; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t bal = __ballot(valid && bit);
-            peers &= bit ? bal : ~bal;
-        }
+        const uint64_t peers = match_peers<RADIX_BITS>(d, valid, RADIX_BITS);
         uint32_t r = 0;
         if (valid) r = cnt[wave][d] + mask_rank(peers);
         __builtin_amdgcn_wave_barrier();

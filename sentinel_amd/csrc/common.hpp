@@ -99,6 +99,22 @@ __device__ inline int64_t slot_find(const unsigned long long *table, uint64_t ma
 __device__ inline uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 // popcount(mask & lanes-below-me)
+// Lanes of the wave holding the same key d (valid lanes only): one ballot per key bit, each
+// narrowing the candidate set to the lanes that agree on that bit (nbits <= MAXB).
+template <int MAXB>
+__device__ inline uint64_t match_peers(uint32_t d, bool valid, int nbits) {
+    uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
+#pragma unroll
+    for (int b = 0; b < MAXB; ++b) {
+        if (b < nbits) {
+            const uint64_t bal = __builtin_amdgcn_ballot_w64((d >> b) & 1u);
+            const uint64_t flip = ((d >> b) & 1u) ? 0ull : ~0ull;
+            peers &= bal ^ flip;
+        }
+    }
+    return peers;
+}
+
 __device__ inline uint32_t mask_rank(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }

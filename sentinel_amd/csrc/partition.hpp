@@ -10,15 +10,15 @@
 //   scan            exclusive scan of the digit-major histograms -> every tile's output offsets
 //   k_part_scatter  stable multi-split of the events into their ranges (one pass, LDS-staged
 //                   contiguous runs); writes the 16-bit local flow key and the 64-bit sorted value
-//   k_part_sort     one workgroup per range: stable counting sort of the range by local flow key
-//                   (any range size: chunks of 4096 ranked with ballots, running bin offsets) and
-//                   the run record {start, flow} of every flow present
-//   k_part_runs     one lane per flow run, decided exactly like k_process_reg (window header in
-//                   VGPRs, closed-form epoch segments, sequential fallback); the lane writes its
-//                   run's verdicts straight to their arrival positions
+//   k_part_half     one workgroup per half range (512 flows): the half's events counted and placed
+//                   in LDS in (flow, arrival) order, then one lane per flow decides its run
+//                   (window header in VGPRs, closed-form epoch segments, sequential fallback) and
+//                   writes the verdicts straight to their arrival positions
+//   k_part_big      the same for halves too large for LDS, sorted through HBM
+//   k_part_long     runs longer than LONG_RUN: a workgroup per hot flow
 //
-// Global order after k_part_sort = (range, local key, arrival) = the order the 3-pass radix sort
-// produces, in 1 scatter pass + 1 in-range pass.  A hot flow makes one lane long (it walks its
+// Order inside a half after placement = (local flow, arrival) = the order the 3-pass radix sort
+// produces, in 1 scatter pass + 1 in-LDS pass.  A hot flow makes one lane long (it walks its
 // events), which is why the engine uses this path for large flow tables (engine.hip, flow_path).
 #pragma once
 
@@ -39,11 +39,17 @@ __global__ __launch_bounds__(SORT_THREADS) void k_part_prep(int64_t n, const Eve
     for (int d = threadIdx.x; d < PART_BINS; d += SORT_THREADS) h[d] = 0;
     __syncthreads();
     const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
-#pragma unroll 4
+    Event evs[SORT_ITEMS];                          // every event load of the tile in flight at once
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
+        if (i < n) evs[j] = ev[i];
+    }
+#pragma unroll
     for (int j = 0; j < SORT_ITEMS; ++j) {
         const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
         if (i >= n) break;
-        const Event e = ev[i];
+        const Event e = evs[j];
         int st = 127;
         uint32_t k = finvalid;
         if (e.idx == SENTINEL_IDX_BAD_ID || e.acquire <= 0) st = ST_BAD_REQUEST;      // DTS:38-40
@@ -96,12 +102,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_part_scatter(const uint32_t *_
     for (int j = 0; j < SORT_ITEMS; ++j) {
         const bool valid = key[j] != finvalid;
         const uint32_t d = valid ? key[j] >> lb : 0u;
-        uint64_t peers = __ballot(valid);
-        for (int b = 0; b < pbits; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t bal = __ballot(valid && bit);
-            peers &= bit ? bal : ~bal;
-        }
+        const uint64_t peers = match_peers<PART_MAX_BITS>(d, valid, pbits);
         uint32_t r = 0;
         if (valid) r = cnt[wave][d] + mask_rank(peers);
         __builtin_amdgcn_wave_barrier();
@@ -138,12 +139,11 @@ __global__ __launch_bounds__(SORT_THREADS) void k_part_scatter(const uint32_t *_
 #pragma unroll
     for (int j = 0; j < SORT_ITEMS; ++j) {
         if (rank[j] == 0xFFFFFFFFu) continue;
-        const int64_t i = base + j * WAVE + lane;
         const uint32_t d = key[j] >> lb;
         const uint32_t p = loff[d] + cnt[wave][d] + rank[j];
         skeys[p] = (uint16_t)(key[j] & ((1u << lb) - 1));
         sdig[p] = (uint16_t)d;
-        svals[p] = src.pack((uint32_t)i, T0);
+        svals[p] = src.pack((uint32_t)(base + j * WAVE + lane), T0);
     }
     __syncthreads();
     for (uint32_t p = threadIdx.x; p < total; p += SORT_THREADS) {
@@ -512,167 +512,6 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
     }
 }
 
-// One workgroup per flow range: a stable counting sort of the range's events by local flow key
-// (histogram -> bin offsets -> chunks of 4096 ranked with ballots in arrival order, each event
-// written to its final slot inside the range; the range's ~100 KB stay L2-resident) and the run
-// records {start, flow} of every flow present.  Any range size works: chunks only carry running
-// per-bin offsets, nothing has to fit in LDS.
-constexpr int PSORT_THREADS = 512;
-constexpr int PSORT_WAVES = PSORT_THREADS / WAVE;
-constexpr int PSORT_ITEMS = 8;
-constexpr int PSORT_CHUNK = PSORT_THREADS * PSORT_ITEMS;
-
-__global__ __launch_bounds__(PSORT_THREADS) void k_part_sort(const uint16_t *__restrict__ pkey,
-                                                             const uint64_t *__restrict__ pval,
-                                                             uint64_t *__restrict__ sval,
-                                                             const uint32_t *__restrict__ offsets, int64_t nblocks,
-                                                             int lb, uint32_t *__restrict__ run_start,
-                                                             uint32_t *__restrict__ run_flow,
-                                                             uint32_t *__restrict__ nruns,
-                                                             unsigned long long *__restrict__ max_range) {
-    __shared__ uint32_t base[PART_BINS];                 // per-bin counts, then running slot offsets
-    __shared__ uint16_t cnt[PSORT_WAVES][PART_BINS];
-    __shared__ uint32_t waves_tot[PSORT_WAVES];
-    const int p = blockIdx.x;
-    const uint32_t pstart = offsets[(int64_t)p * nblocks];
-    const uint32_t pend = offsets[(int64_t)(p + 1) * nblocks];
-    const int wave = threadIdx.x / WAVE;
-    const uint32_t lane = lane_id();
-    const uint32_t R = 1u << lb;
-    if (threadIdx.x == 0 && max_range) atomicMax(max_range, (unsigned long long)(pend - pstart));   // skew statistic
-    for (int d = threadIdx.x; d < PART_BINS; d += PSORT_THREADS) base[d] = 0;
-    __syncthreads();
-    for (uint32_t q = pstart + threadIdx.x; q < pend; q += PSORT_THREADS) atomicAdd(&base[pkey[q]], 1u);
-    __syncthreads();
-    constexpr int BPT = PART_BINS / PSORT_THREADS;
-    uint32_t c[BPT], tot = 0, nz = 0;
-#pragma unroll
-    for (int k = 0; k < BPT; ++k) {
-        c[k] = base[threadIdx.x * BPT + k];
-        tot += c[k];
-        nz += c[k] != 0;
-    }
-    uint32_t all, nall;
-    uint32_t at = block_exclusive_scan(tot, waves_tot, &all);
-    uint32_t rn = block_exclusive_scan(nz, waves_tot, &nall);
-#pragma unroll
-    for (int k = 0; k < BPT; ++k) {
-        const uint32_t d = threadIdx.x * BPT + k;
-        base[d] = pstart + at;
-        if (c[k]) {
-            run_start[(uint64_t)p * R + rn] = pstart + at;
-            run_flow[(uint64_t)p * R + rn] = ((uint32_t)p << lb) | d;
-            ++rn;
-        }
-        at += c[k];
-    }
-    if (threadIdx.x == 0) nruns[p] = nall;
-    __syncthreads();
-    for (uint32_t c0 = pstart; c0 < pend; c0 += PSORT_CHUNK) {
-        const uint32_t cn = min((uint32_t)PSORT_CHUNK, pend - c0);
-        for (int d = threadIdx.x; d < PSORT_WAVES * PART_BINS; d += PSORT_THREADS) (&cnt[0][0])[d] = 0;
-        __syncthreads();
-        uint32_t key[PSORT_ITEMS], rank[PSORT_ITEMS];
-        uint64_t val[PSORT_ITEMS];
-        const uint32_t b0 = (uint32_t)wave * (PSORT_ITEMS * WAVE);
-#pragma unroll
-        for (int j = 0; j < PSORT_ITEMS; ++j) {
-            const uint32_t qq = b0 + j * WAVE + lane;
-            const bool valid = qq < cn;
-            key[j] = valid ? pkey[c0 + qq] : 0u;
-            val[j] = valid ? pval[c0 + qq] : 0ull;
-        }
-#pragma unroll
-        for (int j = 0; j < PSORT_ITEMS; ++j) {
-            const bool valid = b0 + j * WAVE + lane < cn;
-            const uint32_t d = key[j];
-            uint64_t peers = __ballot(valid);
-            for (int b = 0; b < lb; ++b) {
-                const bool bit = (d >> b) & 1u;
-                const uint64_t bal = __ballot(valid && bit);
-                peers &= bit ? bal : ~bal;
-            }
-            uint32_t r = 0;
-            if (valid) r = cnt[wave][d] + mask_rank(peers);
-            __builtin_amdgcn_wave_barrier();
-            if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane) cnt[wave][d] += (uint16_t)__popcll(peers);
-            __builtin_amdgcn_wave_barrier();
-            rank[j] = valid ? r : 0xFFFFFFFFu;
-        }
-        __syncthreads();
-        uint32_t dt[BPT];
-#pragma unroll
-        for (int k = 0; k < BPT; ++k) {
-            const int d = threadIdx.x * BPT + k;
-            uint32_t run = 0;
-            if (d < (int)R) {
-#pragma unroll
-                for (int w = 0; w < PSORT_WAVES; ++w) {
-                    const uint32_t x = cnt[w][d];
-                    cnt[w][d] = (uint16_t)run;
-                    run += x;
-                }
-            }
-            dt[k] = run;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < PSORT_ITEMS; ++j) {
-            if (rank[j] == 0xFFFFFFFFu) continue;
-            const uint32_t d = key[j];
-            sval[base[d] + cnt[wave][d] + rank[j]] = val[j];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < BPT; ++k) base[threadIdx.x * BPT + k] += dt[k];
-        __syncthreads();
-    }
-}
-
-// One lane per flow run (grid: ranges x ceil(2^lb / 256)).  The block's 256 runs are contiguous in
-// `sval`; when their events fit (the common case: ~256 x mean run length) the block stages them in
-// LDS with coalesced loads, so each lane walks its run at LDS latency instead of a chain of
-// dependent global loads.
-constexpr int PR_THREADS = 256;
-constexpr uint32_t PR_STAGE = 4096;               // events staged per block (32 KB)
-
-template <int NMAX>
-__global__ __launch_bounds__(PR_THREADS) void k_part_runs(KeyTable T, const uint64_t *__restrict__ sval,
-                                                          const uint32_t *__restrict__ offsets, int64_t nblocks,
-                                                          int lb, const uint32_t *__restrict__ run_start,
-                                                          const uint32_t *__restrict__ run_flow,
-                                                          const uint32_t *__restrict__ nruns, EventSrc src, Verdicts V,
-                                                          uint32_t *__restrict__ long_runs, uint32_t *__restrict__ nlong) {
-    __shared__ uint64_t lv[PR_STAGE];
-    const int p = blockIdx.x;
-    const uint32_t nr = nruns[p];
-    const uint32_t r0 = blockIdx.y * PR_THREADS;
-    if (r0 >= nr) return;                         // block-uniform
-    const uint64_t ib = (uint64_t)p << lb;
-    const uint32_t pend = offsets[(int64_t)(p + 1) * nblocks];
-    const uint32_t rend = min(r0 + (uint32_t)PR_THREADS, nr);
-    const uint32_t s0 = run_start[ib + r0];
-    const uint32_t s1 = rend < nr ? run_start[ib + rend] : pend;
-    const bool staged = s1 - s0 <= PR_STAGE;
-    if (staged)
-        for (uint32_t q = threadIdx.x; q < s1 - s0; q += PR_THREADS) lv[q] = sval[s0 + q];
-    __syncthreads();
-    const uint32_t r = r0 + threadIdx.x;
-    if (r >= nr) return;
-    const uint64_t i = ib + r;
-    const uint32_t q0 = run_start[i];
-    const uint32_t q1 = r + 1 < nr ? run_start[i + 1] : pend;
-    if (q1 - q0 > LONG_RUN) {                     // hot flow: a whole workgroup takes it (k_part_long)
-        const uint32_t k = atomicAdd(nlong, 1u);
-        long_runs[3 * (uint64_t)k] = q0;
-        long_runs[3 * (uint64_t)k + 1] = q1;
-        long_runs[3 * (uint64_t)k + 2] = run_flow[i];
-        return;
-    }
-    if (staged) part_run<NMAX>(T, run_flow[i], lv, q0 - s0, q1 - s0, src, V, src.t0());
-    else part_run<NMAX>(T, run_flow[i], sval, q0, q1, src, V, src.t0());
-}
-
 // ---------------------------------------------------------------------------------------------
 // Fused per-range sort + decide (the default partition kernels).  A flow range of 2^lb flows is
 // split in two halves of 2^hb flows (hb = lb - 1), one 512-thread workgroup per half, so that two
@@ -696,21 +535,6 @@ constexpr int PH_MAX_LONG = PH_CAP / (LONG_RUN + 1) + 1;
 constexpr uint32_t PH_SMALL_RUN = 32;              // longest run sorted by its own thread
 static_assert(PH_BINS == PH_THREADS, "one flow per thread");
 
-// Lanes of the wave holding the same key d (valid lanes only): one ballot per key bit, each
-// narrowing the candidate set to the lanes that agree on that bit.
-__device__ inline uint64_t match_peers(uint32_t d, bool valid, int nbits) {
-    uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
-#pragma unroll
-    for (int b = 0; b < PART_MAX_BITS; ++b) {
-        if (b < nbits) {
-            const uint64_t bal = __builtin_amdgcn_ballot_w64((d >> b) & 1u);
-            const uint64_t flip = ((d >> b) & 1u) ? 0ull : ~0ull;
-            peers &= bal ^ flip;
-        }
-    }
-    return peers;
-}
-
 // block b -> (range, half): both halves of a range on the XCD b mod 8
 __device__ inline void half_of_block(uint32_t b, uint32_t &p, uint32_t &h) {
     p = (b & 7u) | ((b >> 4) << 3);
@@ -723,14 +547,6 @@ __device__ unsigned long long g_phase[4096][5];
 #else
 #define PF_STAMP(i) do { } while (0)
 #endif
-
-// The part of a flow's window decision that follows the sort: hot runs are handed to k_part_long
-// (their events copied to HBM first when they sit in LDS), the others decided here.
-template <int NMAX>
-__device__ inline void part_decide_flow(const KeyTable &T, uint32_t key, const uint64_t *vals, uint32_t st,
-                                        uint32_t c, const EventSrc &src, const Verdicts &V, int64_t T0) {
-    if (c > 0 && c <= LONG_RUN) part_run<NMAX>(T, key, vals, st, st + c, src, V, T0);
-}
 
 template <int NMAX>
 __global__ __launch_bounds__(PH_THREADS, NMAX > 10 ? 2 : 4) void k_part_half(
@@ -827,7 +643,7 @@ __global__ __launch_bounds__(PH_THREADS, NMAX > 10 ? 2 : 4) void k_part_half(
         for (int j = 0; j < PH_ITEMS; ++j) {
             const bool valid = kk[j] != 0xFFFFFFFFu;
             const uint32_t d = kk[j] & hmask;
-            const uint64_t peers = match_peers(d, valid, hb);
+            const uint64_t peers = match_peers<PART_MAX_BITS>(d, valid, hb);
             uint32_t r = 0;
             if (valid) r = cnt[wave][d] + mask_rank(peers);
             __builtin_amdgcn_wave_barrier();
@@ -939,12 +755,7 @@ __global__ __launch_bounds__(PH_THREADS) void k_part_big(
             for (int j = 0; j < PB_ITEMS; ++j) {
                 const bool valid = kk[j] != 0xFFFFFFFFu && (kk[j] >> hb) == h;
                 const uint32_t d = kk[j] & hmask;
-                uint64_t peers = __ballot(valid);
-                for (int bb = 0; bb < hb; ++bb) {
-                    const bool bit = (d >> bb) & 1u;
-                    const uint64_t bal = __ballot(valid && bit);
-                    peers &= bit ? bal : ~bal;
-                }
+                const uint64_t peers = match_peers<PART_MAX_BITS>(d, valid, hb);
                 uint32_t r = 0;
                 if (valid) r = cnt[wave][d] + mask_rank(peers);
                 __builtin_amdgcn_wave_barrier();
@@ -977,7 +788,7 @@ __global__ __launch_bounds__(PH_THREADS) void k_part_big(
             long_runs[3 * (uint64_t)j + 1] = goff + start + c;
             long_runs[3 * (uint64_t)j + 2] = key;
         }
-        if (t <= hmask) part_decide_flow<NMAX>(T, key, dst, start, c, src, V, T0);
+        if (c > 0 && c <= LONG_RUN) part_run<NMAX>(T, key, dst, start, start + c, src, V, T0);
         __syncthreads();                                  // LDS reuse by the next entry
     }
 }
