@@ -384,7 +384,8 @@ struct sentinel_engine {
         w_hacq, w_segstart, w_segkey, w_segep, w_segacq, w_het, w_done, w_s0, w_k, w_counters;
     DevBuf w_vslot;                    // slot of every value of a param batch
     DevBuf w_pkey;                     // partition path: 16-bit local flow keys in range order
-    DevBuf w_runs;                     // partition path: run starts, run flows, runs per range
+    DevBuf w_runs;                     // partition path: long-run / oversized-half work lists
+    DevBuf w_pscan;                    // partition path: per-group range sums + range starts
     DevBuf io_ev, io_fl, io_out, io_vals;
     int64_t ws_cap = 0;
 
@@ -807,8 +808,8 @@ int sentinel_engine::rebuild_limiters() {
 // Partition-local flow path (partition.hpp): prep + range histogram, scan, one multi-split pass,
 // one fused sort + decide pass per flow range (LDS), oversized ranges redone from HBM, hot flows.
 template <int NMAX>
-static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTable &FT, const uint32_t *offsets,
-                               int64_t nb, int lb, const EventSrc &src, const Verdicts &V, int64_t n, hipStream_t s,
+static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTable &FT, const uint32_t *rstart,
+                               int lb, const EventSrc &src, const Verdicts &V, int64_t n, hipStream_t s,
                                uint32_t *ctl, unsigned long long *stat) {
     // ctl: [0] long-run count, [1] oversized-half count, [2, 2 + 2 nparts) oversized halves, then long runs
     uint32_t *nlong = ctl, *nbig = ctl + 1, *big = ctl + 2;
@@ -822,13 +823,13 @@ static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTa
     if (!all_big) {
         e->launch("part_fused", n, s, [&] {
             k_part_half<NMAX><<<16u * (unsigned)((nparts + 7) / 8), PH_THREADS, 0, s>>>(
-                FT, pkey, pval, gsval, offsets, nb, lb, nparts, (int32_t)e->rules.size(), src, V, long_runs, nlong, big,
+                FT, pkey, pval, gsval, rstart, lb, nparts, (int32_t)e->rules.size(), src, V, long_runs, nlong, big,
                 nbig, stat);
         });
     }
     e->launch("part_big", n, s, [&] {
         k_part_big<NMAX><<<all_big ? 2u * (unsigned)nparts : (unsigned)std::min<int32_t>(2 * nparts, 256), PH_THREADS, 0, s>>>(
-            FT, pkey, pval, gsval, offsets, nb, lb, nparts, src, V, long_runs, nlong, all_big ? nullptr : big, nbig,
+            FT, pkey, pval, gsval, rstart, lb, nparts, src, V, long_runs, nlong, all_big ? nullptr : big, nbig,
             stat);
     });
     e->launch("part_long", n, s, [&] {   // hot flows (runs > LONG_RUN events): a workgroup each
@@ -846,21 +847,29 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
     const int pbits = bits_for(nparts - 1 > 0 ? nparts - 1 : 1);
     const int64_t nb = sort_blocks(n);
     uint32_t *fkey = e->w_fkey.as<uint32_t>();
-    uint32_t *hist = e->w_fhist.as<uint32_t>();
-    const int64_t hn = (int64_t)nparts * nb + 1;           // digit-major histograms + the total
-    HIP_OK(hipMemsetAsync(hist + hn - 1, 0, 4, s));
+    uint32_t *hist = e->w_fhist.as<uint32_t>();             // tile-major range histograms -> offsets
+    const int64_t ng = (nb + PS_GROUP - 1) / PS_GROUP;
+    int rc = e->w_pscan.ensure(((size_t)ng * nparts + nparts + 1) * 4);
+    if (rc) return rc;
+    uint32_t *gsum = e->w_pscan.as<uint32_t>();
+    uint32_t *rstart = gsum + (size_t)ng * nparts;
     e->launch("part_prep", n, s, [&] {
         k_part_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
             n, ev, F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, fkey, finvalid, lb, hist, nb, nparts);
     });
-    e->scan(hist, hn, true, s);
+    e->launch("scan", n, s, [&] {
+        const dim3 g2((unsigned)ng, (unsigned)((nparts + PS_THREADS - 1) / PS_THREADS));
+        k_part_colsum<<<g2, PS_THREADS, 0, s>>>(hist, nb, nparts, gsum);
+        k_part_ranges<<<1, PART_BINS, 0, s>>>(gsum, ng, nparts, rstart);
+        k_part_offsets<<<g2, PS_THREADS, 0, s>>>(hist, nb, nparts, gsum, rstart);
+    });
     const EventSrc src{ev, nullptr, fl, false};
     e->launch("part_scatter", n, s, [&] {
         k_part_scatter<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(fkey, src, e->w_pkey.as<uint16_t>(),
                                                                          e->w_sval.as<uint64_t>(), n, finvalid, lb, pbits,
                                                                          hist, nb, nparts);
     });
-    int rc = e->w_runs.ensure((2 + 2 * (size_t)nparts + 3 * ((size_t)n / LONG_RUN + 2)) * 4);
+    rc = e->w_runs.ensure((2 + 2 * (size_t)nparts + 3 * ((size_t)n / LONG_RUN + 2)) * 4);
     if (rc) return rc;
     if (!e->d_part_stat.p) {
         rc = e->d_part_stat.ensure(8);
@@ -874,10 +883,10 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
     const Verdicts V{out, fkey, finvalid};
     uint32_t *ctl = e->w_runs.as<uint32_t>();
     const int mx = e->flow_max_n;
-    if (mx <= 2) launch_part_decide<2>(e, nparts, FT, hist, nb, lb, src, V, n, s, ctl, stat);
-    else if (mx <= 4) launch_part_decide<4>(e, nparts, FT, hist, nb, lb, src, V, n, s, ctl, stat);
-    else if (mx <= 10) launch_part_decide<10>(e, nparts, FT, hist, nb, lb, src, V, n, s, ctl, stat);
-    else launch_part_decide<16>(e, nparts, FT, hist, nb, lb, src, V, n, s, ctl, stat);
+    if (mx <= 2) launch_part_decide<2>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
+    else if (mx <= 4) launch_part_decide<4>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
+    else if (mx <= 10) launch_part_decide<10>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
+    else launch_part_decide<16>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
     HIP_OK(hipMemcpyAsync(e->h_part_stat, stat, 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipGetLastError());
     return 0;
@@ -1195,7 +1204,7 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
                       &e->d_lrule_dur, &e->d_lrule_w, &e->d_lrule_rcp, &e->d_lrule_kind, &e->d_lhot_keys,
                       &e->d_lhot_tok, &e->d_ltable, &e->d_lstate, &e->d_now, &e->d_conc_thr, &e->d_seg1_w,
                       &e->d_seg1_rcp, &e->d_seg1_kind, &e->d_tok_keys, &e->d_tok_fid, &e->d_tok_fidx,
-                      &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->w_pkey, &e->w_runs, &e->d_lres_state,
+                      &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->w_pkey, &e->w_runs, &e->w_pscan, &e->d_lres_state,
                       &e->d_lres_count, &e->d_lres_w, &e->d_lres_rcp, &e->d_lres_kind})
         b->release();
     if (e->h_part_stat) (void)hipHostFree(e->h_part_stat);

@@ -62,7 +62,63 @@ __global__ __launch_bounds__(SORT_THREADS) void k_part_prep(int64_t n, const Eve
         else put_verdict(out, (uint32_t)i, st, 0, 0);
     }
     __syncthreads();
-    for (int d = threadIdx.x; d < nparts; d += SORT_THREADS) hist[(int64_t)d * nblocks + blockIdx.x] = h[d];
+    // tile-major: this tile's 4 KB row is one contiguous store
+    for (int d = threadIdx.x; d < nparts; d += SORT_THREADS) hist[(int64_t)blockIdx.x * nparts + d] = h[d];
+}
+
+// Offsets of the multi-split from the tile-major histograms h[b][d] (b = tile, d = range):
+// off[b][d] = start(d) + sum_{b' < b} h[b'][d], start(d) = sum_{d' < d} total(d').  Three small
+// passes over groups of PS_GROUP tiles, every access a coalesced row: column sums per group,
+// one workgroup scanning groups and ranges, then the running offsets written in place.
+constexpr int PS_GROUP = 32;
+constexpr int PS_THREADS = 256;
+
+__global__ __launch_bounds__(PS_THREADS) void k_part_colsum(const uint32_t *__restrict__ hist, int64_t nb, int32_t P,
+                                                            uint32_t *__restrict__ gsum) {
+    const int64_t g = blockIdx.x;
+    const int d = blockIdx.y * PS_THREADS + threadIdx.x;
+    if (d >= P) return;
+    const int64_t b0 = g * PS_GROUP, b1 = min(b0 + PS_GROUP, nb);
+    uint32_t s = 0;
+#pragma unroll 8
+    for (int64_t b = b0; b < b1; ++b) s += hist[b * P + d];
+    gsum[g * P + d] = s;
+}
+
+// One workgroup of PART_BINS threads: per range, exclusive scan of its group sums (in place); then
+// the exclusive scan of the range totals -> rstart[0..P] (rstart[P] = valid events).
+__global__ __launch_bounds__(PART_BINS) void k_part_ranges(uint32_t *__restrict__ gsum, int64_t ng, int32_t P,
+                                                           uint32_t *__restrict__ rstart) {
+    __shared__ uint32_t waves_tot[PART_BINS / WAVE];
+    const int d = threadIdx.x;
+    uint32_t run = 0;
+    if (d < P) {
+        for (int64_t g = 0; g < ng; ++g) {
+            const uint32_t x = gsum[g * P + d];
+            gsum[g * P + d] = run;
+            run += x;
+        }
+    }
+    uint32_t total;
+    const uint32_t st = block_exclusive_scan(run, waves_tot, &total);
+    if (d < P) rstart[d] = st;
+    if (d == 0) rstart[P] = total;
+}
+
+__global__ __launch_bounds__(PS_THREADS) void k_part_offsets(uint32_t *__restrict__ hist, int64_t nb, int32_t P,
+                                                             const uint32_t *__restrict__ gsum,
+                                                             const uint32_t *__restrict__ rstart) {
+    const int64_t g = blockIdx.x;
+    const int d = blockIdx.y * PS_THREADS + threadIdx.x;
+    if (d >= P) return;
+    const int64_t b0 = g * PS_GROUP, b1 = min(b0 + PS_GROUP, nb);
+    uint32_t run = rstart[d] + gsum[g * P + d];
+#pragma unroll 8
+    for (int64_t b = b0; b < b1; ++b) {
+        const uint32_t x = hist[b * P + d];
+        hist[b * P + d] = run;
+        run += x;
+    }
 }
 
 // Stable multi-split of the valid events by range digit (one pass).  Same tiling as k_part_prep;
@@ -86,7 +142,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_part_scatter(const uint32_t *_
     for (int d = threadIdx.x; d < PART_BINS; d += SORT_THREADS) {
 #pragma unroll
         for (int w = 0; w < SORT_WAVES; ++w) cnt[w][d] = 0;
-        goff[d] = d < nparts ? offsets[(int64_t)d * nblocks + blockIdx.x] : 0u;
+        goff[d] = d < nparts ? offsets[(int64_t)blockIdx.x * nparts + d] : 0u;   // tile-major row
     }
     __syncthreads();
     const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
@@ -551,7 +607,7 @@ __device__ unsigned long long g_phase[4096][5];
 template <int NMAX>
 __global__ __launch_bounds__(PH_THREADS, NMAX > 10 ? 2 : 4) void k_part_half(
     KeyTable T, const uint16_t *__restrict__ pkey, const uint64_t *__restrict__ pval, uint64_t *__restrict__ gsval,
-    const uint32_t *__restrict__ offsets, int64_t nblocks, int lb, int32_t nranges, int32_t nflows, EventSrc src, Verdicts V,
+    const uint32_t *__restrict__ rstart, int lb, int32_t nranges, int32_t nflows, EventSrc src, Verdicts V,
     uint32_t *__restrict__ long_runs, uint32_t *__restrict__ nlong, uint32_t *__restrict__ big,
     uint32_t *__restrict__ nbig, unsigned long long *__restrict__ max_range) {
     __shared__ uint64_t sv[PH_CAP];
@@ -568,8 +624,8 @@ __global__ __launch_bounds__(PH_THREADS, NMAX > 10 ? 2 : 4) void k_part_half(
     const uint32_t lane = lane_id();
     const uint32_t t = threadIdx.x;
     const int64_t T0 = src.t0();
-    const uint32_t pstart = offsets[(int64_t)p * nblocks];
-    const uint32_t pend = offsets[(int64_t)(p + 1) * nblocks];
+    const uint32_t pstart = rstart[p];
+    const uint32_t pend = rstart[p + 1];
     const uint32_t size = pend - pstart;
     if (t == 0 && h == 0 && max_range) atomicMax(max_range, (unsigned long long)size);   // skew statistic
     if (size > PH_KEYS) {                                 // block-uniform
@@ -701,7 +757,7 @@ constexpr int PB_CHUNK = PH_THREADS * PB_ITEMS;
 template <int NMAX>
 __global__ __launch_bounds__(PH_THREADS) void k_part_big(
     KeyTable T, const uint16_t *__restrict__ pkey, const uint64_t *__restrict__ pval, uint64_t *__restrict__ gsval,
-    const uint32_t *__restrict__ offsets, int64_t nblocks, int lb, int32_t nranges, EventSrc src, Verdicts V,
+    const uint32_t *__restrict__ rstart, int lb, int32_t nranges, EventSrc src, Verdicts V,
     uint32_t *__restrict__ long_runs, uint32_t *__restrict__ nlong, const uint32_t *__restrict__ big,
     const uint32_t *__restrict__ nbig, unsigned long long *__restrict__ max_range) {
     __shared__ uint16_t cnt[PH_WAVES][PH_BINS];
@@ -718,8 +774,8 @@ __global__ __launch_bounds__(PH_THREADS) void k_part_big(
         const uint32_t e = big ? big[wi] : wi;
         const uint32_t p = e >> 1, h = e & 1u;
         if (lb == 0 && h == 1) continue;                  // block-uniform
-        const uint32_t pstart = offsets[(int64_t)p * nblocks];
-        const uint32_t pend = offsets[(int64_t)(p + 1) * nblocks];
+        const uint32_t pstart = rstart[p];
+        const uint32_t pend = rstart[p + 1];
         const uint32_t size = pend - pstart;
         if (!big && h == 0 && t == 0 && max_range) atomicMax(max_range, (unsigned long long)size);
         base[t] = 0;
