@@ -64,14 +64,21 @@ struct KeyTable {
 };
 
 // The sorted 64-bit value of an event: [0,28) arrival position, [28] prioritized flag,
-// [29,53) ts - T0 (signed 24 bits), [53,64) acquire (11 bits).  Out-of-range ts deltas or
-// acquire counts use the all-ones escape and are read back from the event itself.
+// [29,45) ts - T0 (signed 16 bits), [45,54) acquire (9 bits), [54,64) the partition path's local
+// flow key (10 bits; 0 elsewhere).  Out-of-range ts deltas or acquire counts use the all-ones
+// escape and are read back from the event itself.
 constexpr uint32_t SEQ_MASK = 0x0FFFFFFFu;
 constexpr uint64_t VAL_PRIO = 1ull << 28;
 constexpr int VAL_DT_SHIFT = 29;
-constexpr uint32_t VAL_DT_ESC = 0xFFFFFFu;      // 24 bits
-constexpr int VAL_ACQ_SHIFT = 53;
-constexpr uint32_t VAL_ACQ_ESC = 0x7FFu;        // 11 bits
+constexpr int VAL_DT_BITS = 16;
+constexpr uint32_t VAL_DT_ESC = 0xFFFFu;
+constexpr int VAL_ACQ_SHIFT = 45;
+constexpr uint32_t VAL_ACQ_ESC = 0x1FFu;        // 9 bits
+constexpr int VAL_KEY_SHIFT = 54;
+
+__host__ __device__ inline int32_t val_dt(uint32_t dtf) {
+    return (int32_t)(dtf << (32 - VAL_DT_BITS)) >> (32 - VAL_DT_BITS);
+}
 
 // Where the events of a pipeline run come from (one of the two is non-null).
 struct EventSrc {
@@ -96,7 +103,8 @@ struct EventSrc {
         uint8_t fl;
         load(s, t, a, fl);
         const int64_t dt = t - T0;
-        const uint32_t dtf = (dt > -(1 << 23) && dt < (1 << 23) - 1) ? ((uint32_t)dt & VAL_DT_ESC) : VAL_DT_ESC;
+        const uint32_t dtf = (dt > -(1 << (VAL_DT_BITS - 1)) && dt < (1 << (VAL_DT_BITS - 1)) - 1)
+                                 ? ((uint32_t)dt & VAL_DT_ESC) : VAL_DT_ESC;
         const uint32_t af = (a > 0 && a < (int32_t)VAL_ACQ_ESC) ? (uint32_t)a : VAL_ACQ_ESC;
         return (uint64_t)s | ((fl & 1u) ? VAL_PRIO : 0ull) | ((uint64_t)dtf << VAL_DT_SHIFT) | ((uint64_t)af << VAL_ACQ_SHIFT);
     }
@@ -111,7 +119,7 @@ struct EventSrc {
             load((uint32_t)v & SEQ_MASK, t, a, fl);
             return;
         }
-        t = T0 + (int64_t)((int32_t)(dtf << 8) >> 8);
+        t = T0 + (int64_t)val_dt(dtf);
         a = unit_acquire ? 1 : (int32_t)af;
     }
 };

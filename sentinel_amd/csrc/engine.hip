@@ -383,7 +383,6 @@ struct sentinel_engine {
     DevBuf w_fkey, w_lkey, w_skey, w_sval, w_ktmp, w_vtmp, w_fhist, w_lhist, w_parts, w_segid, w_bad, w_hep,
         w_hacq, w_segstart, w_segkey, w_segep, w_segacq, w_het, w_done, w_s0, w_k, w_counters;
     DevBuf w_vslot;                    // slot of every value of a param batch
-    DevBuf w_pkey;                     // partition path: 16-bit local flow keys in range order
     DevBuf w_runs;                     // partition path: long-run / oversized-half work lists
     DevBuf w_pscan;                    // partition path: per-group range sums + range starts
     DevBuf io_ev, io_fl, io_out, io_vals;
@@ -398,7 +397,6 @@ struct sentinel_engine {
         for (DevBuf *b : {&w_hep, &w_segep, &w_s0, &w_sval, &w_vtmp}) rc |= b->ensure(c * 8);
         for (DevBuf *b : {&w_bad, &w_het, &w_done}) rc |= b->ensure(c);
         rc |= w_fhist.ensure((size_t)(hist_words(c, MAX_PASSES) + 64) * 4);
-        rc |= w_pkey.ensure((size_t)c * 2);
         rc |= w_lhist.ensure((size_t)hist_words(c, MAX_PASSES) * 4);
         rc |= w_parts.ensure((size_t)(scan_parts(std::max<int64_t>(c, hist_words(c, MAX_PASSES))) + 16) * 8);
         rc |= w_segstart.ensure((c + 1) * 4);
@@ -814,7 +812,6 @@ static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTa
     // ctl: [0] long-run count, [1] oversized-half count, [2, 2 + 2 nparts) oversized halves, then long runs
     uint32_t *nlong = ctl, *nbig = ctl + 1, *big = ctl + 2;
     uint32_t *long_runs = big + 2 * (size_t)nparts;
-    uint16_t *pkey = e->w_pkey.as<uint16_t>();
     const uint64_t *pval = e->w_sval.as<uint64_t>();
     uint64_t *gsval = e->w_vtmp.as<uint64_t>();
     (void)hipMemsetAsync(ctl, 0, 8, s);
@@ -823,13 +820,13 @@ static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTa
     if (!all_big) {
         e->launch("part_fused", n, s, [&] {
             k_part_half<NMAX><<<16u * (unsigned)((nparts + 7) / 8), PH_THREADS, 0, s>>>(
-                FT, pkey, pval, gsval, rstart, lb, nparts, (int32_t)e->rules.size(), src, V, long_runs, nlong, big,
+                FT, pval, gsval, rstart, lb, nparts, (int32_t)e->rules.size(), src, V, long_runs, nlong, big,
                 nbig, stat);
         });
     }
     e->launch("part_big", n, s, [&] {
         k_part_big<NMAX><<<all_big ? 2u * (unsigned)nparts : (unsigned)std::min<int32_t>(2 * nparts, 256), PH_THREADS, 0, s>>>(
-            FT, pkey, pval, gsval, rstart, lb, nparts, src, V, long_runs, nlong, all_big ? nullptr : big, nbig,
+            FT, pval, gsval, rstart, lb, nparts, src, V, long_runs, nlong, all_big ? nullptr : big, nbig,
             stat);
     });
     e->launch("part_long", n, s, [&] {   // hot flows (runs > LONG_RUN events): a workgroup each
@@ -865,8 +862,8 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
     });
     const EventSrc src{ev, nullptr, fl, false};
     e->launch("part_scatter", n, s, [&] {
-        k_part_scatter<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(fkey, src, e->w_pkey.as<uint16_t>(),
-                                                                         e->w_sval.as<uint64_t>(), n, finvalid, lb, pbits,
+        k_part_scatter<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(fkey, src, e->w_sval.as<uint64_t>(), n,
+                                                                         finvalid, lb, pbits,
                                                                          hist, nb, nparts);
     });
     rc = e->w_runs.ensure((2 + 2 * (size_t)nparts + 3 * ((size_t)n / LONG_RUN + 2)) * 4);
@@ -1204,7 +1201,7 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
                       &e->d_lrule_dur, &e->d_lrule_w, &e->d_lrule_rcp, &e->d_lrule_kind, &e->d_lhot_keys,
                       &e->d_lhot_tok, &e->d_ltable, &e->d_lstate, &e->d_now, &e->d_conc_thr, &e->d_seg1_w,
                       &e->d_seg1_rcp, &e->d_seg1_kind, &e->d_tok_keys, &e->d_tok_fid, &e->d_tok_fidx,
-                      &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->w_pkey, &e->w_runs, &e->w_pscan, &e->d_lres_state,
+                      &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->w_runs, &e->w_pscan, &e->d_lres_state,
                       &e->d_lres_count, &e->d_lres_w, &e->d_lres_rcp, &e->d_lres_kind})
         b->release();
     if (e->h_part_stat) (void)hipHostFree(e->h_part_stat);

@@ -125,7 +125,6 @@ __global__ __launch_bounds__(PS_THREADS) void k_part_offsets(uint32_t *__restric
 // ranking with one 64-bit ballot per digit bit and wave-private LDS counters; the tile is staged
 // in LDS in digit order and written out as contiguous per-range runs.
 __global__ __launch_bounds__(SORT_THREADS) void k_part_scatter(const uint32_t *__restrict__ keys_in, EventSrc src,
-                                                               uint16_t *__restrict__ keys_out,
                                                                uint64_t *__restrict__ vals_out, int64_t n,
                                                                uint32_t finvalid, int lb, int pbits,
                                                                const uint32_t *__restrict__ offsets, int64_t nblocks,
@@ -134,7 +133,6 @@ __global__ __launch_bounds__(SORT_THREADS) void k_part_scatter(const uint32_t *_
     __shared__ uint32_t goff[PART_BINS];
     __shared__ uint32_t loff[PART_BINS];
     __shared__ uint32_t waves_tot[SORT_WAVES];
-    __shared__ uint16_t skeys[SORT_TILE];
     __shared__ uint16_t sdig[SORT_TILE];
     __shared__ uint64_t svals[SORT_TILE];
     const int wave = threadIdx.x / WAVE;
@@ -197,16 +195,15 @@ __global__ __launch_bounds__(SORT_THREADS) void k_part_scatter(const uint32_t *_
         if (rank[j] == 0xFFFFFFFFu) continue;
         const uint32_t d = key[j] >> lb;
         const uint32_t p = loff[d] + cnt[wave][d] + rank[j];
-        skeys[p] = (uint16_t)(key[j] & ((1u << lb) - 1));
         sdig[p] = (uint16_t)d;
-        svals[p] = src.pack((uint32_t)(base + j * WAVE + lane), T0);
+        svals[p] = src.pack((uint32_t)(base + j * WAVE + lane), T0) |
+                   ((uint64_t)(key[j] & ((1u << lb) - 1)) << VAL_KEY_SHIFT);
     }
     __syncthreads();
     for (uint32_t p = threadIdx.x; p < total; p += SORT_THREADS) {
         const uint32_t d = sdig[p];
         const uint32_t dst = goff[d] + p - loff[d];
         if (dst >= (uint64_t)n) continue;          // guard: a corrupt offset must never write out of bounds
-        keys_out[dst] = skeys[p];
         vals_out[dst] = svals[p];
     }
 }
@@ -290,7 +287,7 @@ struct FlowWindow {
             return epoch_of(t, w, rcp);
         }
         a = src.unit_acquire ? 1 : (int32_t)af;
-        const int32_t x = r0 + ((int32_t)(dtf << 8) >> 8);
+        const int32_t x = r0 + val_dt(dtf);
         int32_t q = (int32_t)floorf((float)x * rcpf);
         const int32_t rem = x - q * w;
         if (rem < 0) --q;
@@ -606,7 +603,7 @@ __device__ unsigned long long g_phase[4096][5];
 
 template <int NMAX>
 __global__ __launch_bounds__(PH_THREADS, NMAX > 10 ? 2 : 4) void k_part_half(
-    KeyTable T, const uint16_t *__restrict__ pkey, const uint64_t *__restrict__ pval, uint64_t *__restrict__ gsval,
+    KeyTable T, const uint64_t *__restrict__ pval, uint64_t *__restrict__ gsval,
     const uint32_t *__restrict__ rstart, int lb, int32_t nranges, int32_t nflows, EventSrc src, Verdicts V,
     uint32_t *__restrict__ long_runs, uint32_t *__restrict__ nlong, uint32_t *__restrict__ big,
     uint32_t *__restrict__ nbig, unsigned long long *__restrict__ max_range) {
@@ -636,12 +633,17 @@ __global__ __launch_bounds__(PH_THREADS, NMAX > 10 ? 2 : 4) void k_part_half(
     // 1. keys (all at once) -> per-flow counts (LDS atomics) -> flow starts
     const uint32_t b0 = (uint32_t)wave * (PH_ITEMS * WAVE);
     const uint32_t hmask = (1u << hb) - 1u;
+    uint64_t val[PH_ITEMS];                               // every value load in flight at once
     uint32_t kk[PH_ITEMS];                                // local flow, or 0xFFFFFFFF: not this half's
 #pragma unroll
     for (int j = 0; j < PH_ITEMS; ++j) {
         const uint32_t q = b0 + j * WAVE + lane;
-        const uint32_t k = q < size ? (uint32_t)pkey[pstart + q] : 0xFFFFFFFFu;
-        kk[j] = (k != 0xFFFFFFFFu && (k >> hb) == h) ? (k & hmask) : 0xFFFFFFFFu;
+        val[j] = q < size ? pval[pstart + q] : ~0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < PH_ITEMS; ++j) {
+        const uint32_t k = (uint32_t)(val[j] >> VAL_KEY_SHIFT);
+        kk[j] = (val[j] != ~0ull && (k >> hb) == h) ? (k & hmask) : 0xFFFFFFFFu;
     }
     base[t] = 0;
     if (t == 0) { s_nlong = 0; s_cmax = 0; }
@@ -662,10 +664,6 @@ __global__ __launch_bounds__(PH_THREADS, NMAX > 10 ? 2 : 4) void k_part_half(
     }
     if (c) atomicMax(&s_cmax, c);
     base[t] = start;
-    uint64_t val[PH_ITEMS];                               // all value loads in flight together
-#pragma unroll
-    for (int j = 0; j < PH_ITEMS; ++j)
-        val[j] = kk[j] != 0xFFFFFFFFu ? pval[pstart + b0 + j * WAVE + lane] : 0ull;
     __syncthreads();
     PF_STAMP(1);
     // 2. values into their flow's slots, in arrival order
@@ -756,7 +754,7 @@ constexpr int PB_CHUNK = PH_THREADS * PB_ITEMS;
 
 template <int NMAX>
 __global__ __launch_bounds__(PH_THREADS) void k_part_big(
-    KeyTable T, const uint16_t *__restrict__ pkey, const uint64_t *__restrict__ pval, uint64_t *__restrict__ gsval,
+    KeyTable T, const uint64_t *__restrict__ pval, uint64_t *__restrict__ gsval,
     const uint32_t *__restrict__ rstart, int lb, int32_t nranges, EventSrc src, Verdicts V,
     uint32_t *__restrict__ long_runs, uint32_t *__restrict__ nlong, const uint32_t *__restrict__ big,
     const uint32_t *__restrict__ nbig, unsigned long long *__restrict__ max_range) {
@@ -781,7 +779,7 @@ __global__ __launch_bounds__(PH_THREADS) void k_part_big(
         base[t] = 0;
         __syncthreads();
         for (uint32_t q = pstart + t; q < pend; q += PH_THREADS) {
-            const uint32_t k = pkey[q];
+            const uint32_t k = (uint32_t)(pval[q] >> VAL_KEY_SHIFT);
             if ((k >> hb) == h) atomicAdd(&base[k & hmask], 1u);
         }
         __syncthreads();
@@ -804,8 +802,8 @@ __global__ __launch_bounds__(PH_THREADS) void k_part_big(
 #pragma unroll
             for (int j = 0; j < PB_ITEMS; ++j) {
                 const uint32_t qq = b0 + j * WAVE + lane;
-                kk[j] = qq < cn ? (uint32_t)pkey[c0 + qq] : 0xFFFFFFFFu;
                 val[j] = qq < cn ? pval[c0 + qq] : 0ull;
+                kk[j] = qq < cn ? (uint32_t)(val[j] >> VAL_KEY_SHIFT) : 0xFFFFFFFFu;
             }
 #pragma unroll
             for (int j = 0; j < PB_ITEMS; ++j) {
