@@ -814,7 +814,6 @@ static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTa
     uint32_t *long_runs = big + 2 * (size_t)nparts;
     const uint64_t *pval = e->w_sval.as<uint64_t>();
     uint64_t *gsval = e->w_vtmp.as<uint64_t>();
-    (void)hipMemsetAsync(ctl, 0, 8, s);
     // a batch whose mean range does not fit goes straight to the HBM-sorting kernel
     const bool all_big = n > (int64_t)nparts * (int64_t)(PH_KEYS * 3 / 4);
     if (!all_big) {
@@ -830,7 +829,7 @@ static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTa
             stat);
     });
     e->launch("part_long", n, s, [&] {   // hot flows (runs > LONG_RUN events): a workgroup each
-        k_part_long<NMAX><<<256, PL_THREADS, 0, s>>>(FT, gsval, long_runs, nlong, src, V);
+        k_part_long<NMAX><<<256, PL_THREADS, 0, s>>>(FT, gsval, long_runs, nlong, src, V, stat, e->h_part_stat);
     });
 }
 
@@ -850,9 +849,20 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
     if (rc) return rc;
     uint32_t *gsum = e->w_pscan.as<uint32_t>();
     uint32_t *rstart = gsum + (size_t)ng * nparts;
+    rc = e->w_runs.ensure((2 + 2 * (size_t)nparts + 3 * ((size_t)n / LONG_RUN + 2)) * 4);
+    if (rc) return rc;
+    if (!e->d_part_stat.p) {
+        rc = e->d_part_stat.ensure(8);
+        if (rc) return rc;
+        HIP_OK(hipHostMalloc((void **)&e->h_part_stat, 8, 0));
+        *e->h_part_stat = 0;
+    }
+    unsigned long long *stat = e->d_part_stat.as<unsigned long long>();
+    uint32_t *ctl = e->w_runs.as<uint32_t>();
     e->launch("part_prep", n, s, [&] {
         k_part_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
-            n, ev, F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, fkey, finvalid, lb, hist, nb, nparts);
+            n, ev, F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, fkey, finvalid, lb, hist, nb, nparts,
+            ctl, stat);
     });
     e->launch("scan", n, s, [&] {
         const dim3 g2((unsigned)ng, (unsigned)((nparts + PS_THREADS - 1) / PS_THREADS));
@@ -866,25 +876,13 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
                                                                          finvalid, lb, pbits,
                                                                          hist, nb, nparts);
     });
-    rc = e->w_runs.ensure((2 + 2 * (size_t)nparts + 3 * ((size_t)n / LONG_RUN + 2)) * 4);
-    if (rc) return rc;
-    if (!e->d_part_stat.p) {
-        rc = e->d_part_stat.ensure(8);
-        if (rc) return rc;
-        HIP_OK(hipHostMalloc((void **)&e->h_part_stat, 8, 0));
-        *e->h_part_stat = 0;
-    }
-    unsigned long long *stat = e->d_part_stat.as<unsigned long long>();
-    HIP_OK(hipMemsetAsync(stat, 0, 8, s));
     const KeyTable FT = e->table(e->ft, NEV, 0);
     const Verdicts V{out, fkey, finvalid};
-    uint32_t *ctl = e->w_runs.as<uint32_t>();
     const int mx = e->flow_max_n;
     if (mx <= 2) launch_part_decide<2>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
     else if (mx <= 4) launch_part_decide<4>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
     else if (mx <= 10) launch_part_decide<10>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
     else launch_part_decide<16>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
-    HIP_OK(hipMemcpyAsync(e->h_part_stat, stat, 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipGetLastError());
     return 0;
 }

@@ -34,7 +34,13 @@ __global__ __launch_bounds__(SORT_THREADS) void k_part_prep(int64_t n, const Eve
                                                             const int32_t *__restrict__ route,
                                                             uint64_t *__restrict__ out, uint32_t *__restrict__ fkey,
                                                             uint32_t finvalid, int lb, uint32_t *__restrict__ hist,
-                                                            int64_t nblocks, int32_t nparts) {
+                                                            int64_t nblocks, int32_t nparts,
+                                                            uint32_t *__restrict__ ctl_zero,
+                                                            unsigned long long *__restrict__ stat_zero) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {        // the batch's work-list counters and skew statistic
+        if (ctl_zero) { ctl_zero[0] = 0; ctl_zero[1] = 0; }
+        if (stat_zero) *stat_zero = 0;
+    }
     __shared__ uint32_t h[PART_BINS];
     for (int d = threadIdx.x; d < PART_BINS; d += SORT_THREADS) h[d] = 0;
     __syncthreads();
@@ -80,8 +86,8 @@ __global__ __launch_bounds__(PS_THREADS) void k_part_colsum(const uint32_t *__re
     if (d >= P) return;
     const int64_t b0 = g * PS_GROUP, b1 = min(b0 + PS_GROUP, nb);
     uint32_t s = 0;
-#pragma unroll 8
-    for (int64_t b = b0; b < b1; ++b) s += hist[b * P + d];
+#pragma unroll
+    for (int k = 0; k < PS_GROUP; ++k) s += b0 + k < b1 ? hist[(b0 + k) * P + d] : 0u;
     gsum[g * P + d] = s;
 }
 
@@ -93,10 +99,15 @@ __global__ __launch_bounds__(PART_BINS) void k_part_ranges(uint32_t *__restrict_
     const int d = threadIdx.x;
     uint32_t run = 0;
     if (d < P) {
-        for (int64_t g = 0; g < ng; ++g) {
-            const uint32_t x = gsum[g * P + d];
-            gsum[g * P + d] = run;
-            run += x;
+        for (int64_t g0 = 0; g0 < ng; g0 += 16) {          // 16 loads in flight, then the stores
+            uint32_t x[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) x[k] = g0 + k < ng ? gsum[(g0 + k) * P + d] : 0u;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                if (g0 + k < ng) gsum[(g0 + k) * P + d] = run;
+                run += x[k];
+            }
         }
     }
     uint32_t total;
@@ -113,11 +124,13 @@ __global__ __launch_bounds__(PS_THREADS) void k_part_offsets(uint32_t *__restric
     if (d >= P) return;
     const int64_t b0 = g * PS_GROUP, b1 = min(b0 + PS_GROUP, nb);
     uint32_t run = rstart[d] + gsum[g * P + d];
-#pragma unroll 8
-    for (int64_t b = b0; b < b1; ++b) {
-        const uint32_t x = hist[b * P + d];
-        hist[b * P + d] = run;
-        run += x;
+    uint32_t x[PS_GROUP];                                 // the group's column in flight at once
+#pragma unroll
+    for (int k = 0; k < PS_GROUP; ++k) x[k] = b0 + k < b1 ? hist[(b0 + k) * P + d] : 0u;
+#pragma unroll
+    for (int k = 0; k < PS_GROUP; ++k) {
+        if (b0 + k < b1) hist[(b0 + k) * P + d] = run;
+        run += x[k];
     }
 }
 
@@ -448,7 +461,12 @@ constexpr int PL_CHUNK = PL_THREADS * PL_ITEMS;
 template <int NMAX>
 __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint64_t *__restrict__ sval,
                                                           const uint32_t *__restrict__ long_runs,
-                                                          const uint32_t *__restrict__ nlong, EventSrc src, Verdicts V) {
+                                                          const uint32_t *__restrict__ nlong, EventSrc src, Verdicts V,
+                                                          const unsigned long long *__restrict__ stat,
+                                                          unsigned long long *__restrict__ host_stat) {
+    // the last kernel of a partition batch publishes the skew statistic to pinned host memory
+    if (host_stat && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(host_stat, *stat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __shared__ uint16_t seg_start[PL_CHUNK + 1];
     __shared__ int64_t seg_E[PL_CHUNK];
     __shared__ int32_t seg_a[PL_CHUNK];
