@@ -38,7 +38,7 @@ KERNEL_BYTES_PER_EVENT = {
     "seg_mark": 5.0,          # read segid 4 + flag 1 (segment records are per segment)
     "verdict": 20.0,          # read segid 4 + value 8, write the 8-B verdict
     "part_prep": 20.0,        # read the 16-B event, write the 4-B key (range histogram in LDS)
-    "part_scatter": 30.0,     # read key 4 + event 16, write local key 2 + value 8
+    "part_scatter": 28.0,     # read key 4 + event 16, write the 8-B packed value (local key inside)
 }
 
 
@@ -227,11 +227,11 @@ def main():
             e_f = N / max(1, F)
             bpe = (args.sample_count * 16 + 40 + 24) / max(1.0, min(e_f, 1e9)) if F else 0.0
         if dom == "part_fused":
-            # per event: read local key 2 + value 8, write the 8-B verdict; per touched flow: read
-            # the window header (16 B per bucket) and the 42 B of rule fields, write back the rolled
-            # bucket's 16-B pair, read + write its 64-B counter line
+            # per event: read the 8-B packed value (local key inside), write the 8-B verdict; per
+            # touched flow: read the window header (16 B per bucket) and the 42 B of rule fields,
+            # write back the rolled bucket's 16-B pair, read + write its 64-B counter line
             e_f = N / max(1, F)
-            bpe = 18.0 + (args.sample_count * 16 + 42 + 16 + 128) / max(1.0, e_f)
+            bpe = 16.0 + (args.sample_count * 16 + 42 + 16 + 128) / max(1.0, e_f)
         if dom == "radix_scatter":
             passes = max(1, round(d["calls"] / max(1, args.steps)))
             bpe = (32.0 + 24.0 * (passes - 1)) / passes
