@@ -259,18 +259,25 @@ typedef struct {
 } sentinel_local_resource_t;
 
 /* Loads the resources (index = position) with the node window config (defaults 2, 1000); every
- * node starts empty.  Preconditions (documented): <= 6000 resources (CtSph MAX_SLOT_CHAIN_SIZE), no
- * prioritized entries. */
+ * node starts empty.  Precondition (documented): <= 6000 resources (CtSph MAX_SLOT_CHAIN_SIZE). */
 int  sentinel_load_local_resources(sentinel_engine_t *eng, const sentinel_local_resource_t *res, int32_t n,
                                    int32_t sample_count, int32_t interval_ms);
-/* Events {resource index, acquireCount, ts}: OK (entry) or BLOCKED (FlowException); an unknown
- * resource answers NO_RULE_EXISTS. */
+/* Events {resource index, acquireCount, ts} + optional prioritized flags (SphU.entryWithPriority,
+ * bit 0): OK (entry) or BLOCKED (FlowException); an unknown resource answers NO_RULE_EXISTS.  A
+ * prioritized entry over the limit that StatisticNode.tryOccupyNext can place in a future window
+ * (DefaultController.java:52-64) answers OK with waitInMs = the wait (PriorityWaitException: the
+ * caller sleeps, then the entry passes).  Replaces SphU.entry(...) -> ... -> FlowSlot ->
+ * DefaultController.canPass and StatisticSlot.entry's booking (StatisticSlot.java:55-116). */
 int  sentinel_submit_local_entry_batch(sentinel_engine_t *eng, int64_t n, const sentinel_event_t *events,
-                                       sentinel_verdict_t *verdicts, void *stream);
+                                       const uint8_t *prioritized, sentinel_verdict_t *verdicts, void *stream);
 int  sentinel_submit_local_entry_batch_host(sentinel_engine_t *eng, int64_t n, const sentinel_event_t *events,
-                                            sentinel_verdict_t *verdicts);
-/* {second-window PASS, BLOCK, minute-window PASS, BLOCK} sums of a resource's node at ts (read-only). */
-int  sentinel_local_node_stats(sentinel_engine_t *eng, int32_t resource_idx, int64_t ts, int64_t *out4);
+                                            const uint8_t *prioritized, sentinel_verdict_t *verdicts);
+/* {second-window PASS, BLOCK, minute-window PASS, BLOCK, minute OCCUPIED_PASS, waiting()} of a
+ * resource's node at ts (read-only view, no roll). */
+int  sentinel_local_node_stats(sentinel_engine_t *eng, int32_t resource_idx, int64_t ts, int64_t *out6);
+/* OccupyTimeoutProperty.updateTimeout (OccupyTimeoutProperty.java:64-78): values < 0 or above the
+ * node interval are ignored (default 500 ms). */
+int  sentinel_set_occupy_timeout(sentinel_engine_t *eng, int32_t timeout_ms);
 
 /* ---- cluster concurrency tokens (thread grade): TokenService.requestConcurrentToken /
  *      releaseConcurrentToken (TokenService.java:56,62) -> ConcurrentClusterFlowChecker

@@ -111,6 +111,17 @@ def lib():
         "orc_default_controller_can_pass": (C.c_int, [vp, dbl, C.c_int, C.c_int, i32, i64]),
         "orc_default_controller_check": (C.c_int, [dbl, dbl, C.c_int, C.c_int]),
         "orc_local_replay": (None, [vp, dbl, i64, vp, vp, vp]),
+        "orc_local_replay_prio": (None, [vp, dbl, i64, vp, vp, vp, vp, vp]),
+        "orc_local_entry": (C.c_int, [vp, dbl, C.c_int, C.c_int, i64, vp]),
+        "orc_node_set_occupy_timeout": (None, [vp, C.c_int]),
+        "orc_node_waiting": (i64, [vp, i64]),
+        "orc_node_minute_occupied": (i64, [vp, i64]),
+        "orc_node_try_occupy_next": (i64, [vp, i64, C.c_int, dbl]),
+        "orc_node_add_waiting": (None, [vp, i64, C.c_int]),
+        "orc_node_add_occupied_pass": (None, [vp, i64, C.c_int]),
+        "orc_node_sec_window_pass": (i64, [vp, i64]),
+        "orc_node_sec_window_add_pass": (None, [vp, i64, C.c_int]),
+        "orc_node_sec_values": (i64, [vp, i64, vp]),
         "orc_pbucket_new": (vp, []),
         "orc_pbucket_free": (None, [vp]),
         "orc_pbucket_pass_default": (C.c_int, [vp, u64, i64, i64, i64, C.c_int, i64]),
@@ -232,6 +243,36 @@ class StatisticNode:
         out = np.zeros(len(ts), dtype=np.uint8)
         lib().orc_local_replay(self.h, count, len(ts), _p(acquire), _p(ts), _p(out))
         return out
+
+    def replay_prio(self, count, acquire: np.ndarray, ts: np.ndarray, prio: np.ndarray):
+        """(passed u8, waitInMs i64) per entry, prioritized entries included."""
+        acquire = np.ascontiguousarray(acquire, dtype=np.int32)
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        prio = np.ascontiguousarray(prio, dtype=np.uint8)
+        out = np.zeros(len(ts), dtype=np.uint8)
+        wait = np.zeros(len(ts), dtype=np.int64)
+        lib().orc_local_replay_prio(self.h, count, len(ts), _p(acquire), _p(ts), _p(prio), _p(out), _p(wait))
+        return out, wait
+
+    def entry(self, count, acquire, t, prioritized=False):
+        w = C.c_int64(0)
+        ok = lib().orc_local_entry(self.h, count, acquire, int(prioritized), t, C.byref(w))
+        return bool(ok), int(w.value)
+
+    def set_occupy_timeout(self, ms): lib().orc_node_set_occupy_timeout(self.h, ms)
+    def waiting(self, t): return lib().orc_node_waiting(self.h, t)
+    def minute_occupied(self, t): return lib().orc_node_minute_occupied(self.h, t)
+    def try_occupy_next(self, t, acquire, threshold): return lib().orc_node_try_occupy_next(self.h, t, acquire, threshold)
+    def add_waiting(self, future_t, c): lib().orc_node_add_waiting(self.h, future_t, c)
+    def add_occupied_pass(self, t, c): lib().orc_node_add_occupied_pass(self.h, t, c)
+    # OccupiableBucketLeapArray surface (rollingCounterInSecond's array) for the reference's own tests
+    def window_pass(self, t): return lib().orc_node_sec_window_pass(self.h, t)
+    def window_add_pass(self, t, c): lib().orc_node_sec_window_add_pass(self.h, t, c)
+
+    def values(self, t):
+        s = C.c_int64(0)
+        k = lib().orc_node_sec_values(self.h, t, C.byref(s))
+        return int(k), int(s.value)
 
 
 class ParamTokenBucket:

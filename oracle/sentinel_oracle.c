@@ -757,23 +757,42 @@ int orc_engine_param_overflowed(const orc_engine *e) {
 }
 
 /* ------------------------------------------------------------------ local StatisticNode */
-/* SN:96-103: rollingCounterInSecond = ArrayMetric(SAMPLE_COUNT=2, INTERVAL=1000) with occupy
- * (OccupiableBucketLeapArray), rollingCounterInMinute = ArrayMetric(60, 60000, false).
- * Only the non-prioritized path is restated: the borrow array (FutureBucketLeapArray) is only
- * written by addWaiting (prioritized occupy), so newEmptyBucket/resetWindowTo never borrow here. */
+/* SN:96-103: rollingCounterInSecond = ArrayMetric(SAMPLE_COUNT, INTERVAL) over an
+ * OccupiableBucketLeapArray (occupy/OccupiableBucketLeapArray.java:29-101) whose borrowArray is a
+ * FutureBucketLeapArray (occupy/FutureBucketLeapArray.java:28-53); rollingCounterInMinute =
+ * ArrayMetric(60, 60000, false) over a plain BucketLeapArray. */
 typedef struct {
     leap la;
     int64_t *c;          /* n x 6 MetricBucket counters */
     int64_t scratch[ORC_M_NEVENTS];
+    int occupiable;      /* seed new / reset buckets from `borrow` (OBLA:40-64) */
+    void *borrow;        /* bucket_array * (FutureBucketLeapArray) */
+    int future;          /* FutureBucketLeapArray: deprecated iff time >= windowStart (FBLA:49-52) */
 } bucket_array;
 
 struct orc_stat_node {
-    bucket_array sec, min;
+    bucket_array sec, min, borrow;
+    int occupy_timeout;  /* OccupyTimeoutProperty.occupyTimeout (default 500) */
 };
 
 static void ba_init(bucket_array *a, int n, int interval) {
+    memset(a, 0, sizeof(*a));
     leap_init(&a->la, n, interval);
     a->c = (int64_t *)calloc((size_t)n * ORC_M_NEVENTS, sizeof(int64_t));
+}
+
+static int ba_deprecated(const bucket_array *a, int64_t t, int i) {
+    return a->future ? t >= a->la.start[i] : leap_deprecated(&a->la, t, i);
+}
+
+/* LA:290-303 getWindowValue(time): no roll; the bucket only if start <= time < start + win. */
+static int64_t *ba_window_value(bucket_array *a, int64_t t) {
+    if (t < 0) return NULL;
+    int i = leap_idx(&a->la, t);
+    if (!a->la.present[i]) return NULL;
+    int64_t st = a->la.start[i];
+    if (!(st <= t && t < st + a->la.win)) return NULL;   /* WindowWrap.isTimeInWindow (WW:93-95) */
+    return a->c + (size_t)i * ORC_M_NEVENTS;
 }
 
 static int64_t *ba_current(bucket_array *a, int64_t t) {
@@ -782,7 +801,19 @@ static int64_t *ba_current(bucket_array *a, int64_t t) {
     if (act == LA_NULL) return NULL;
     if (act == LA_DETACHED) { memset(a->scratch, 0, sizeof(a->scratch)); return a->scratch; }
     int64_t *b = a->c + (size_t)i * ORC_M_NEVENTS;
-    if (act != LA_SAME) memset(b, 0, sizeof(int64_t) * ORC_M_NEVENTS);   /* MetricBucket.reset() */
+    if (act == LA_NEW) {
+        memset(b, 0, sizeof(int64_t) * ORC_M_NEVENTS);
+        if (a->occupiable) {                   /* OBLA:40-49 newEmptyBucket(time): reset(borrowBucket) */
+            const int64_t *bb = ba_window_value((bucket_array *)a->borrow, t);
+            if (bb) memcpy(b, bb, sizeof(int64_t) * ORC_M_NEVENTS);
+        }
+    } else if (act == LA_RESET) {
+        memset(b, 0, sizeof(int64_t) * ORC_M_NEVENTS);
+        if (a->occupiable) {                   /* OBLA:52-64 resetWindowTo: addPass((int) borrow.pass()) */
+            const int64_t *bb = ba_window_value((bucket_array *)a->borrow, a->la.start[i]);
+            if (bb) b[ORC_M_PASS] = (int32_t)bb[ORC_M_PASS];
+        }
+    }
     return b;
 }
 
@@ -790,7 +821,7 @@ static int64_t ba_sum(bucket_array *a, int64_t t, int ev) {   /* ArrayMetric.pas
     ba_current(a, t);
     int64_t s = 0;
     for (int i = 0; i < a->la.n; i++)
-        if (a->la.present[i] && !leap_deprecated(&a->la, t, i)) s = wrap_add64(s, a->c[(size_t)i * ORC_M_NEVENTS + ev]);
+        if (a->la.present[i] && !ba_deprecated(a, t, i)) s = wrap_add64(s, a->c[(size_t)i * ORC_M_NEVENTS + ev]);
     return s;
 }
 
@@ -802,21 +833,37 @@ static void ba_add(bucket_array *a, int64_t t, int ev, int64_t x) {
 orc_stat_node *orc_node_new(int sample_count, int interval_ms) {
     orc_stat_node *nd = (orc_stat_node *)calloc(1, sizeof(*nd));
     ba_init(&nd->sec, sample_count, interval_ms);
+    ba_init(&nd->borrow, sample_count, interval_ms);     /* OBLA:36 */
+    nd->borrow.future = 1;
+    nd->sec.occupiable = 1;
+    nd->sec.borrow = &nd->borrow;
     ba_init(&nd->min, 60, 60 * 1000);
+    nd->occupy_timeout = 500;                            /* OccupyTimeoutProperty.java:40 */
     return nd;
 }
 
 void orc_node_free(orc_stat_node *nd) {
     if (!nd) return;
     leap_free(&nd->sec.la); free(nd->sec.c);
+    leap_free(&nd->borrow.la); free(nd->borrow.c);
     leap_free(&nd->min.la); free(nd->min.c);
     free(nd);
+}
+
+/* OccupyTimeoutProperty.updateTimeout (OTP:64-78): ignored when < 0 or > INTERVAL. */
+void orc_node_set_occupy_timeout(orc_stat_node *nd, int ms) {
+    if (ms < 0 || ms > nd->sec.la.interval) return;
+    nd->occupy_timeout = ms;
 }
 
 int64_t orc_node_pass_sum(orc_stat_node *nd, int64_t t) { return ba_sum(&nd->sec, t, ORC_M_PASS); }
 int64_t orc_node_block_sum(orc_stat_node *nd, int64_t t) { return ba_sum(&nd->sec, t, ORC_M_BLOCK); }
 int64_t orc_node_total_pass(orc_stat_node *nd, int64_t t) { return ba_sum(&nd->min, t, ORC_M_PASS); }
 int64_t orc_node_minute_block(orc_stat_node *nd, int64_t t) { return ba_sum(&nd->min, t, ORC_M_BLOCK); }
+int64_t orc_node_minute_occupied(orc_stat_node *nd, int64_t t) { return ba_sum(&nd->min, t, ORC_M_OCCUPIED_PASS); }
+
+/* ArrayMetric.waiting -> OBLA.currentWaiting (OBLA:66-76): roll the borrow array, sum the future buckets. */
+int64_t orc_node_waiting(orc_stat_node *nd, int64_t t) { return ba_sum(&nd->borrow, t, ORC_M_PASS); }
 
 double orc_node_pass_qps(orc_stat_node *nd, int64_t t) {          /* SN:200-202 */
     return (double)orc_node_pass_sum(nd, t) / nd->sec.la.interval_sec;
@@ -830,6 +877,42 @@ void orc_node_add_pass_request(orc_stat_node *nd, int64_t t, int count) {   /* S
 void orc_node_increase_block_qps(orc_stat_node *nd, int64_t t, int count) { /* SN:261-264 */
     ba_add(&nd->sec, t, ORC_M_BLOCK, count);
     ba_add(&nd->min, t, ORC_M_BLOCK, count);
+}
+
+/* OBLA:78-82 addWaiting(time, n): borrowArray.currentWindow(time).add(PASS, n) */
+void orc_node_add_waiting(orc_stat_node *nd, int64_t future_time, int count) {
+    ba_add(&nd->borrow, future_time, ORC_M_PASS, count);
+}
+
+/* SN:333-336 addOccupiedPass: the MINUTE counter's OCCUPIED_PASS and PASS */
+void orc_node_add_occupied_pass(orc_stat_node *nd, int64_t t, int count) {
+    ba_add(&nd->min, t, ORC_M_OCCUPIED_PASS, count);
+    ba_add(&nd->min, t, ORC_M_PASS, count);
+}
+
+/* SN:288-320 tryOccupyNext(currentTime, acquireCount, threshold); INTERVAL / SAMPLE_COUNT are the
+ * node's own second-window configuration. */
+int64_t orc_node_try_occupy_next(orc_stat_node *nd, int64_t t, int acquire, double threshold) {
+    const int interval = nd->sec.la.interval;
+    const double max_count = threshold * (double)interval / 1000;
+    const int64_t current_borrow = orc_node_waiting(nd, t);
+    if ((double)current_borrow >= max_count) return nd->occupy_timeout;
+    const int wl = interval / nd->sec.la.n;
+    int64_t earliest = t - t % wl + wl - interval;
+    int idx = 0;
+    int64_t current_pass = orc_node_pass_sum(nd, t);
+    while (earliest < t) {
+        const int64_t wait = (int64_t)idx * wl + wl - t % wl;
+        if (wait >= nd->occupy_timeout) break;
+        const int64_t *b = ba_window_value(&nd->sec, earliest);       /* ArrayMetric.getWindowPass */
+        const int64_t window_pass = b ? b[ORC_M_PASS] : 0;
+        const int64_t lhs = wrap_add64(wrap_add64(wrap_add64(current_pass, current_borrow), acquire), -window_pass);
+        if ((double)lhs <= max_count) return wait;
+        earliest += wl;
+        current_pass = wrap_add64(current_pass, -window_pass);
+        idx++;
+    }
+    return nd->occupy_timeout;
 }
 
 /* DC:49-76 (non-prioritized): curCount + acquireCount > count  -> block. int + int wraps. */
@@ -846,14 +929,55 @@ int orc_default_controller_check(double node_value, double count, int grade, int
     return !((double)sum > count);
 }
 
+/* One SphU.entry of a QPS-grade resource: DC:49-69 then StatisticSlot's booking (SS:55-116).
+ * Returns 1 pass, 0 block; *wait = waitInMs of a prioritized pass (PriorityWaitException: the
+ * entry passes after sleeping, only the thread count and the occupied / waiting counters move). */
+int orc_local_entry(orc_stat_node *nd, double count, int acquire, int prioritized, int64_t t, int64_t *wait) {
+    *wait = 0;
+    if (orc_default_controller_can_pass(nd, count, 1, acquire, 0, t)) {
+        orc_node_add_pass_request(nd, t, acquire);                    /* SS:62-63 */
+        return 1;
+    }
+    if (prioritized) {                                               /* DC:52-64 */
+        const int64_t w = orc_node_try_occupy_next(nd, t, acquire, count);
+        if (w < nd->occupy_timeout) {
+            orc_node_add_waiting(nd, t + w, acquire);
+            orc_node_add_occupied_pass(nd, t, acquire);
+            *wait = w;                                               /* SS:81-95 */
+            return 1;
+        }
+    }
+    orc_node_increase_block_qps(nd, t, acquire);                     /* SS:96-104 */
+    return 0;
+}
+
 void orc_local_replay(orc_stat_node *nd, double count, int64_t n, const int32_t *acquire,
                       const int64_t *ts, uint8_t *out_pass) {
     for (int64_t i = 0; i < n; i++) {
-        int ok = orc_default_controller_can_pass(nd, count, 1, acquire[i], 0, ts[i]);
-        if (ok) orc_node_add_pass_request(nd, ts[i], acquire[i]);     /* StatisticSlot.java:64-70 */
-        else orc_node_increase_block_qps(nd, ts[i], acquire[i]);      /* StatisticSlot.java:96-104 */
-        out_pass[i] = (uint8_t)ok;
+        int64_t w;
+        out_pass[i] = (uint8_t)orc_local_entry(nd, count, acquire[i], 0, ts[i], &w);
     }
+}
+
+void orc_local_replay_prio(orc_stat_node *nd, double count, int64_t n, const int32_t *acquire, const int64_t *ts,
+                           const uint8_t *prio, uint8_t *out_pass, int64_t *out_wait) {
+    for (int64_t i = 0; i < n; i++)
+        out_pass[i] = (uint8_t)orc_local_entry(nd, count, acquire[i], prio ? (prio[i] & 1) : 0, ts[i], &out_wait[i]);
+}
+
+/* OccupiableBucketLeapArray surface for the reference's own tests (OccupiableBucketLeapArrayTest). */
+int64_t orc_node_sec_window_pass(orc_stat_node *nd, int64_t t) {     /* currentWindow(t).value().pass() */
+    int64_t *b = ba_current(&nd->sec, t);
+    return b ? b[ORC_M_PASS] : 0;
+}
+void orc_node_sec_window_add_pass(orc_stat_node *nd, int64_t t, int n) { ba_add(&nd->sec, t, ORC_M_PASS, n); }
+/* values(t) without a roll: {count of buckets, sum of PASS} */
+int64_t orc_node_sec_values(orc_stat_node *nd, int64_t t, int64_t *sum) {
+    int64_t k = 0, s = 0;
+    for (int i = 0; i < nd->sec.la.n; i++)
+        if (nd->sec.la.present[i] && !ba_deprecated(&nd->sec, t, i)) { k++; s = wrap_add64(s, nd->sec.c[(size_t)i * ORC_M_NEVENTS]); }
+    *sum = s;
+    return k;
 }
 
 /* ------------------------------------------------------------------ local param token bucket */

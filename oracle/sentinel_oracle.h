@@ -166,6 +166,20 @@ int    orc_default_controller_can_pass(orc_stat_node *nd, double count, int grad
 int    orc_default_controller_check(double node_value, double count, int grade, int acquire);
 void   orc_local_replay(orc_stat_node *nd, double count, int64_t n, const int32_t *acquire,
                         const int64_t *ts, uint8_t *out_pass);
+/* Prioritized entries too (DefaultController.java:52-64 + StatisticNode.tryOccupyNext): out_wait =
+ * waitInMs of an occupied pass (0 otherwise). */
+void   orc_local_replay_prio(orc_stat_node *nd, double count, int64_t n, const int32_t *acquire,
+                             const int64_t *ts, const uint8_t *prio, uint8_t *out_pass, int64_t *out_wait);
+int    orc_local_entry(orc_stat_node *nd, double count, int acquire, int prioritized, int64_t t, int64_t *wait);
+void   orc_node_set_occupy_timeout(orc_stat_node *nd, int ms);
+int64_t orc_node_waiting(orc_stat_node *nd, int64_t t);                 /* rollingCounterInSecond.waiting() */
+int64_t orc_node_minute_occupied(orc_stat_node *nd, int64_t t);         /* rollingCounterInMinute.occupiedPass() */
+int64_t orc_node_try_occupy_next(orc_stat_node *nd, int64_t t, int acquire, double threshold);
+void   orc_node_add_waiting(orc_stat_node *nd, int64_t future_time, int count);
+void   orc_node_add_occupied_pass(orc_stat_node *nd, int64_t t, int count);
+int64_t orc_node_sec_window_pass(orc_stat_node *nd, int64_t t);
+void   orc_node_sec_window_add_pass(orc_stat_node *nd, int64_t t, int n);
+int64_t orc_node_sec_values(orc_stat_node *nd, int64_t t, int64_t *sum);
 
 /* ---------------- Local param token bucket (ParamFlowChecker.passDefaultLocalCheck) ----------- */
 typedef struct orc_param_bucket orc_param_bucket;

@@ -330,6 +330,8 @@ struct sentinel_engine {
     // local resources (SphU.entry: DefaultController over the ClusterNode's StatisticNode)
     int32_t nlres = 0, lres_n = 2, lres_w = 500, lres_g = 500;
     double lres_Is = 1.0;
+    int32_t lres_interval = 1000;      // IntervalProperty.INTERVAL of the local nodes
+    int32_t occupy_timeout = 500;      // OccupyTimeoutProperty.occupyTimeout (OccupyTimeoutProperty.java:40)
     DevBuf d_lres_state, d_lres_count, d_lres_w, d_lres_rcp, d_lres_kind;
 
     // concurrency tokens (ConcurrentClusterFlowChecker): nowCalls per flow, token cache in HBM
@@ -1088,7 +1090,8 @@ static int submit_prules_host(sentinel_engine_t *e, int mode, int64_t n, const s
 
 // Local SphU.entry batches (local_entry.hpp): validation, sort by resource, (resource, epoch of
 // gcd(second bucket, 1000 ms)) segments, one lane per resource, parallel verdicts.
-static int submit_local_entry(sentinel_engine_t *e, int64_t n, const Event *ev, uint64_t *out, hipStream_t s) {
+static int submit_local_entry(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
+                              hipStream_t s) {
     if (n <= 0) return 0;
     if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
     int rc = e->ensure_ws(n);
@@ -1112,10 +1115,11 @@ static int submit_local_entry(sentinel_engine_t *e, int64_t n, const Event *ev, 
     RT.rcp_w = e->d_lres_rcp.as<double>();
     RT.kind = e->d_lres_kind.as<uint8_t>();
     RT.ncounters = 1;
-    const EventSrc src{ev, nullptr, nullptr, false};
+    const EventSrc src{ev, nullptr, fl, false};
     e->sort_segments(RT, fkey, e->w_fhist.as<uint32_t>(), n, rbits, src, s);
     const BatchWork W = e->work();
-    const LocalNodes L{e->d_lres_state.as<int64_t>(), e->d_lres_count.as<double>(), e->lres_n, e->lres_w, e->lres_Is};
+    const LocalNodes L{e->d_lres_state.as<int64_t>(), e->d_lres_count.as<double>(), e->lres_n, e->lres_w, e->lres_Is,
+                       e->lres_interval, e->occupy_timeout};
     e->launch("lentry_process", n, s, [&] { k_lentry_process<<<grid_for(n), 256, 0, s>>>(L, W, src, out); });
     e->launch("lentry_verdict", n, s, [&] { k_lentry_verdict<<<grid_for(n), 256, 0, s>>>(W, out, n); });
     HIP_OK(hipGetLastError());
@@ -1711,33 +1715,40 @@ int sentinel_load_local_resources(sentinel_engine_t *e, const sentinel_local_res
     for (int32_t i = 0; i < n; ++i)
         if (res[i].has_rule && res[i].count >= 0) count[i] = res[i].count;   // invalid rules (count < 0) are dropped
     std::vector<int64_t> st(N * LOCAL_WORDS, 0);
-    for (size_t i = 0; i < N; ++i)
-        for (int j = 0; j < LOCAL_NMAX + LOCAL_MIN_SLOTS; ++j) st[i * LOCAL_WORDS + 3 * j] = EPOCH_ABSENT;
+    for (size_t i = 0; i < N; ++i) {
+        int64_t *r = st.data() + i * LOCAL_WORDS;
+        for (int j = 0; j < LOCAL_NMAX; ++j) r[LOCAL_SEC_W * j] = r[LOCAL_BOR_OFF + LOCAL_BOR_W * j] = EPOCH_ABSENT;
+        for (int j = 0; j < LOCAL_MIN_SLOTS; ++j) r[LOCAL_MIN_OFF + LOCAL_MIN_W * j] = EPOCH_ABSENT;
+    }
     int rc = 0;
     rc |= upload(e->d_lres_state, st);
     rc |= upload(e->d_lres_count, count);
     rc |= upload(e->d_lres_w, std::vector<int32_t>(N, a));
     rc |= upload(e->d_lres_rcp, std::vector<double>(N, 1.0 / (double)a));
-    rc |= upload(e->d_lres_kind, std::vector<uint8_t>(N, KIND_LOCAL_PARAM));
+    // KIND_CLUSTER: a prioritized event makes its segment heterogeneous (sequential path)
+    rc |= upload(e->d_lres_kind, std::vector<uint8_t>(N, KIND_CLUSTER));
     if (rc) return rc;
     e->nlres = n;
     e->lres_n = sample_count;
     e->lres_w = w;
     e->lres_g = a;
     e->lres_Is = interval_ms / 1000.0;                                 // LeapArray.intervalInSecond
+    e->lres_interval = interval_ms;
+    if (e->occupy_timeout > interval_ms) e->occupy_timeout = interval_ms;
     return 0;
 }
 
 int sentinel_submit_local_entry_batch(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev,
-                                      sentinel_verdict_t *out, void *stream) {
+                                      const uint8_t *prioritized, sentinel_verdict_t *out, void *stream) {
     if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
-    return submit_local_entry(e, n, (const Event *)ev, (uint64_t *)out, stream ? (hipStream_t)stream : e->stream);
+    return submit_local_entry(e, n, (const Event *)ev, prioritized, (uint64_t *)out,
+                              stream ? (hipStream_t)stream : e->stream);
 }
 
 int sentinel_submit_local_entry_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev,
-                                           sentinel_verdict_t *out) {
+                                           const uint8_t *prioritized, sentinel_verdict_t *out) {
     if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
     if (n == 0) return 0;
     std::lock_guard<std::mutex> g(e->mu);
@@ -1747,8 +1758,12 @@ int sentinel_submit_local_entry_batch_host(sentinel_engine_t *e, int64_t n, cons
     rc |= e->io_ev.ensure(n * sizeof(Event));
     rc |= e->io_out.ensure(n * 8);
     if (rc) return SENTINEL_E_NOMEM;
+    if (prioritized) rc |= e->io_fl.ensure(n);
+    if (rc) return SENTINEL_E_NOMEM;
     HIP_OK(hipMemcpyAsync(e->io_ev.p, ev, n * sizeof(Event), hipMemcpyHostToDevice, s));
-    rc = submit_local_entry(e, n, e->io_ev.as<Event>(), e->io_out.as<uint64_t>(), s);
+    if (prioritized) HIP_OK(hipMemcpyAsync(e->io_fl.p, prioritized, n, hipMemcpyHostToDevice, s));
+    rc = submit_local_entry(e, n, e->io_ev.as<Event>(), prioritized ? e->io_fl.as<uint8_t>() : nullptr,
+                            e->io_out.as<uint64_t>(), s);
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
@@ -1765,19 +1780,33 @@ int sentinel_local_node_stats(sentinel_engine_t *e, int32_t idx, int64_t ts, int
     HIP_OK(hipMemcpy(st.data(), e->d_lres_state.as<int64_t>() + (int64_t)idx * LOCAL_WORDS, LOCAL_WORDS * 8,
                      hipMemcpyDeviceToHost));
     const int64_t E = ts / e->lres_w, E1 = ts / 1000;   // read-only view: valid epochs (E - n, E]
-    for (int k = 0; k < 4; ++k) out[k] = 0;
-    for (int j = 0; j < e->lres_n; ++j)
-        if (st[3 * j] != EPOCH_ABSENT && st[3 * j] > E - e->lres_n && st[3 * j] <= E) {
-            out[0] += st[3 * j + 1];
-            out[1] += st[3 * j + 2];
+    for (int k = 0; k < 6; ++k) out[k] = 0;
+    for (int j = 0; j < e->lres_n; ++j) {
+        const int64_t *s = st.data() + LOCAL_SEC_W * j;
+        if (s[0] != EPOCH_ABSENT && s[0] > E - e->lres_n && s[0] <= E) {
+            out[0] += s[1];
+            out[1] += s[2];
         }
+        const int64_t *b = st.data() + LOCAL_BOR_OFF + LOCAL_BOR_W * j;
+        if (b[0] != EPOCH_ABSENT && b[0] * e->lres_w > ts) out[5] += b[1];   // waiting(): future borrows
+    }
     for (int j = 0; j < LOCAL_MIN_SLOTS; ++j) {
-        const int64_t *m = st.data() + 3 * (LOCAL_NMAX + j);
+        const int64_t *m = st.data() + LOCAL_MIN_OFF + LOCAL_MIN_W * j;
         if (m[0] != EPOCH_ABSENT && m[0] > E1 - LOCAL_MIN_SLOTS && m[0] <= E1) {
             out[2] += m[1];
             out[3] += m[2];
+            out[4] += m[3];
         }
     }
+    return 0;
+}
+
+int sentinel_set_occupy_timeout(sentinel_engine_t *e, int32_t timeout_ms) {
+    if (!e) return fail(SENTINEL_E_INVALID, "null engine");
+    std::lock_guard<std::mutex> g(e->mu);
+    // OccupyTimeoutProperty.updateTimeout (OccupyTimeoutProperty.java:64-78): < 0 or > INTERVAL ignored
+    if (timeout_ms < 0 || timeout_ms > e->lres_interval) return 0;
+    e->occupy_timeout = timeout_ms;
     return 0;
 }
 

@@ -422,17 +422,26 @@ class GpuTokenService:
         check(self._L.sentinel_load_local_resources(self._h, arr, len(counts), int(sample_count), int(interval_ms)),
               "load_local_resources")
 
-    def submit_local_entry_batch_host(self, resource_idx, acquire, ts):
-        """SphU.entry for a batch -> status array (OK = entry, BLOCKED = FlowException)."""
+    def submit_local_entry_batch_host(self, resource_idx, acquire, ts, prioritized=None, with_wait=False):
+        """SphU.entry (SphU.entryWithPriority where `prioritized`) for a batch -> status array (OK =
+        entry, BLOCKED = FlowException); with_wait also returns waitInMs (> 0: an occupied pass,
+        the PriorityWaitException wait)."""
         ev = self.pack_events(resource_idx, acquire, ts)
+        pr = None if prioritized is None else np.ascontiguousarray(prioritized, dtype=np.uint8)
         out = np.empty(len(ev), dtype=_lib.VERDICT_DTYPE)
-        check(self._L.sentinel_submit_local_entry_batch_host(self._h, len(ev), _p(ev), _p(out)),
+        check(self._L.sentinel_submit_local_entry_batch_host(self._h, len(ev), _p(ev), _p(pr), _p(out)),
               "submit_local_entry_batch_host")
-        return out["status"].astype(np.int8)
+        st = out["status"].astype(np.int8)
+        return (st, out["wait_in_ms"].astype(np.int64)) if with_wait else st
+
+    def set_occupy_timeout(self, ms: int):
+        """OccupyTimeoutProperty.updateTimeout (ignored when < 0 or above the node interval)."""
+        check(self._L.sentinel_set_occupy_timeout(self._h, int(ms)), "set_occupy_timeout")
 
     def local_node_stats(self, resource_idx: int, ts: int) -> np.ndarray:
-        """{second PASS, second BLOCK, minute PASS, minute BLOCK} of the resource's node at ts."""
-        out = np.zeros(4, dtype=np.int64)
+        """{second PASS, second BLOCK, minute PASS, minute BLOCK, minute OCCUPIED_PASS, waiting} of
+        the resource's node at ts (read-only)."""
+        out = np.zeros(6, dtype=np.int64)
         check(self._L.sentinel_local_node_stats(self._h, int(resource_idx), int(ts), _p(out)), "local_node_stats")
         return out
 

@@ -102,6 +102,41 @@ def test_kat_cases(oracle_mod, fixture):
             run_ops(oracle_mod, case["ops"], t0)
 
 
+def _occ_ops(node, ops, t0):
+    for op in ops:
+        k, t = op["op"], t0 + op.get("dt", 0)
+        if k == "add_pass":
+            node.window_add_pass(t, op["n"])
+        elif k == "window_pass":
+            assert node.window_pass(t) == op["expect"], op
+        elif k == "add_waiting":
+            node.add_waiting(t, op["n"])
+        elif k == "waiting":
+            assert node.waiting(t0) == op["expect"], op          # currentWaiting() at the mocked clock
+        elif k == "touch":
+            node.window_pass(t)                                   # leapArray.currentWindow(t)
+        elif k == "values":
+            assert node.values(t) == (op["expect_size"], op["expect_sum"]), op
+        elif k == "values_aligned":
+            assert node.values(t0 - t0 % 200 + 2000) == (op["expect_size"], op["expect_sum"]), op
+        else:
+            raise KeyError(k)
+
+
+def test_kat_occupiable_bucket_leap_array(oracle_mod):
+    kat = load("kat_occupiable_bucket_leap_array.json")
+    w = kat["window"]
+    for case in kat["cases"]:
+        for t0 in kat["t0"]:
+            node = oracle_mod.StatisticNode(kat["n"], kat["interval"])
+            for _ in range(case.get("repeat", 1)):
+                _occ_ops(node, case["ops"], t0)
+            for i in range(case.get("steps", 0)):                 # testWindowAfterOneInterval's loop
+                node.window_add_pass(t0 + i * w, 1)
+                node.add_waiting(t0 + (i + 1) * w, 1)
+            _occ_ops(node, case.get("after", []), t0)
+
+
 def test_kat_default_controller(oracle_mod):
     kat = load("kat_default_controller.json")
     for case in kat["mocked"]:
