@@ -356,6 +356,9 @@ void *sentinel_engine_stream(sentinel_engine_t *eng);
  * `max` entries: names (32 chars each), total milliseconds, launch count and events processed
  * (summed over launches); returns the number of entries. */
 int  sentinel_profile_enable(sentinel_engine_t *eng, int enable);
+/* Time only the named kernel (NULL or "": every kernel): two events per launch of it instead of two
+ * per launch of every kernel, so a timed run keeps its dominant kernel's live duration cheaply. */
+int  sentinel_profile_select(sentinel_engine_t *eng, const char *kernel);
 int  sentinel_profile_read(sentinel_engine_t *eng, int max, char *names32, double *total_ms,
                            int64_t *calls, int64_t *units);
 

@@ -344,6 +344,7 @@ struct sentinel_engine {
     struct ProfRec { const char *name; hipEvent_t a, b; int64_t units; };
     struct ProfAcc { double ms = 0; int64_t calls = 0; int64_t units = 0; };
     bool prof = false;
+    std::string prof_only;                 // non-empty: only this kernel is timed
     std::vector<ProfRec> prof_pending;
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<std::string, ProfAcc>> prof_acc;
@@ -357,7 +358,7 @@ struct sentinel_engine {
 
     template <class F>
     void launch(const char *name, int64_t units, hipStream_t s, F &&f) {
-        if (!prof) { f(); return; }
+        if (!prof || (!prof_only.empty() && prof_only != name)) { f(); return; }
         hipEvent_t a = get_ev(), b = get_ev();
         (void)hipEventRecord(a, s);
         f();
@@ -1222,6 +1223,13 @@ int sentinel_profile_enable(sentinel_engine_t *e, int enable) {
     e->prof_collect();
     e->prof_acc.clear();
     e->prof = enable != 0;
+    return 0;
+}
+
+int sentinel_profile_select(sentinel_engine_t *e, const char *kernel) {
+    if (!e) return fail(SENTINEL_E_INVALID, "null engine");
+    std::lock_guard<std::mutex> g(e->mu);
+    e->prof_only = kernel ? kernel : "";
     return 0;
 }
 
