@@ -331,3 +331,33 @@ def test_hot_flow_long_runs(oracle_mod):
     flags = (rng.random(n) < 0.01).astype(np.uint8)
     ev = T.Events(idx, acq, ts.astype(np.int64), flags)
     _compare(_engine(rules, occ=0.9), _oracle(oracle_mod, rules, occ=0.9), rules, ev, batches=3)
+
+
+def test_partition_ballot_ranking_split_halves(oracle_mod):
+    """4096 flows (4 per range, 2 per half) with ~50 events per flow per batch: every half of the
+    partition path takes the stable ballot ranking (runs longer than the per-run insertion sort)."""
+    rng = np.random.default_rng(43)
+    rules = T.make_rules(4096, rng, count_lo=5, count_hi=200, sample_count=2, window_interval_ms=1000)
+    n = 400_000
+    idx = rng.integers(0, 4096, size=n).astype(np.int32)
+    acq = np.ones(n, np.int32)
+    acq[rng.random(n) < 0.02] = 3
+    ts = T.timestamps(n, 150_000.0, T.T0_ALIGNED + 5)
+    ev = T.Events(idx, acq, ts.astype(np.int64), None)
+    _compare(_engine(rules), _oracle(oracle_mod, rules), rules, ev, batches=2)
+
+
+def test_partition_oversized_half(oracle_mod):
+    """65536 flows (64 per range): one half of one range gets ~7000 events (more than fit in LDS)
+    while its range stays under the key capacity, so that half goes through k_part_big and the
+    other half through k_part_half, both writing the same range."""
+    rng = np.random.default_rng(47)
+    F = 65536
+    rules = T.make_rules(F, rng, count_lo=5, count_hi=500, sample_count=10, window_interval_ms=1000)
+    n = 300_000
+    idx = rng.integers(0, F, size=n).astype(np.int32)
+    hot = rng.random(n) < 0.024                    # ~7200 events into flows 352..383 (range 5, half 1)
+    idx[hot] = 352 + rng.integers(0, 32, size=int(hot.sum()))
+    ts = T.timestamps(n, 400_000.0, T.T0_ALIGNED + 3)
+    ev = T.Events(idx, np.ones(n, np.int32), ts.astype(np.int64), None)
+    _compare(_engine(rules), _oracle(oracle_mod, rules), rules, ev, batches=1)
