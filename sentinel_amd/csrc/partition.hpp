@@ -648,14 +648,16 @@ __global__ __launch_bounds__(PH_THREADS, NMAX > 10 ? 2 : 4) void k_part_half(
         return;
     }
     PF_STAMP(0);
-    // 1. keys (all at once) -> per-flow counts (LDS atomics) -> flow starts
+    // 1. keys (all at once) -> per-flow counts (LDS atomics) -> flow starts.  Item j of thread t is
+    // range position j * PH_THREADS + t: the workgroup sweeps the range in arrival order, so the
+    // slots handed out below come out nearly in arrival order and the per-run sort has little to do.
     const uint32_t b0 = (uint32_t)wave * (PH_ITEMS * WAVE);
     const uint32_t hmask = (1u << hb) - 1u;
     uint64_t val[PH_ITEMS];                               // every value load in flight at once
     uint32_t kk[PH_ITEMS];                                // local flow, or 0xFFFFFFFF: not this half's
 #pragma unroll
     for (int j = 0; j < PH_ITEMS; ++j) {
-        const uint32_t q = b0 + j * WAVE + lane;
+        const uint32_t q = j * PH_THREADS + t;
         val[j] = q < size ? pval[pstart + q] : ~0ull;
     }
 #pragma unroll
@@ -704,7 +706,15 @@ __global__ __launch_bounds__(PH_THREADS, NMAX > 10 ? 2 : 4) void k_part_half(
             sv[j] = v;
         }
     } else {
-        // a long run somewhere: stable ranking with ballots (arrival order kept by construction)
+        // a long run somewhere: stable ranking with ballots (arrival order kept by construction),
+        // over wave-contiguous blocks of the range (item j of a lane = position b0 + j * 64 + lane)
+#pragma unroll
+        for (int j = 0; j < PH_ITEMS; ++j) {
+            const uint32_t q = b0 + j * WAVE + lane;
+            val[j] = q < size ? pval[pstart + q] : ~0ull;
+            const uint32_t k = (uint32_t)(val[j] >> VAL_KEY_SHIFT);
+            kk[j] = (val[j] != ~0ull && (k >> hb) == h) ? (k & hmask) : 0xFFFFFFFFu;
+        }
         {
             uint32_t *z = reinterpret_cast<uint32_t *>(&cnt[0][0]);
             for (int d = t; d < PH_WAVES * PH_BINS / 2; d += PH_THREADS) z[d] = 0;
