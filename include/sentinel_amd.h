@@ -178,6 +178,14 @@ int  sentinel_submit_flow_batch(sentinel_engine_t *eng, int64_t n, const sentine
 /* Same with HOST pointers (pinned or pageable): H2D, decide, D2H, synchronous. */
 int  sentinel_submit_flow_batch_host(sentinel_engine_t *eng, int64_t n, const sentinel_event_t *events,
                                      const uint8_t *flags, sentinel_verdict_t *verdicts);
+/* Host-fed stream (the north star's pinned host ring + hipMemcpyAsync double-buffering on side
+ * streams): decides n HOST events as consecutive batches of `batch` events, batch i+1's H2D and
+ * batch i-1's D2H overlapping batch i's decide.  Verdicts equal one sequential replay of all n events
+ * (= sentinel_submit_flow_batch_host over all n).  `batch_ms` (optional, ceil(n / batch) floats):
+ * per-batch latency, H2D start -> verdicts in host memory.  Pass pinned memory for overlap. */
+int  sentinel_submit_flow_stream_host(sentinel_engine_t *eng, int64_t n, const sentinel_event_t *events,
+                                      const uint8_t *flags, sentinel_verdict_t *verdicts, int64_t batch,
+                                      float *batch_ms);
 int  sentinel_submit_param_batch(sentinel_engine_t *eng, int64_t n, const sentinel_param_event_t *events,
                                  sentinel_verdict_t *verdicts, void *stream);
 int  sentinel_submit_param_batch_host(sentinel_engine_t *eng, int64_t n, const sentinel_param_event_t *events,

@@ -18,11 +18,13 @@ timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 > $O/bench.json 2> $O
 cat $O/bench.json
 echo "== rocprof stats"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/bench_prof.json 2> $O/prof.err || { tail -20 $O/prof.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-path > $O/bench_prof.json 2> $O/prof.err || { tail -20 $O/prof.err; exit 1; }
 echo "== pmc FETCH_SIZE"
-timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile > /dev/null 2> $O/pmc_fetch.err || { tail -20 $O/pmc_fetch.err; exit 1; }
+timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-host-path > /dev/null 2> $O/pmc_fetch.err || { tail -20 $O/pmc_fetch.err; exit 1; }
 echo "== pmc WRITE_SIZE"
-timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile > /dev/null 2> $O/pmc_write.err || { tail -20 $O/pmc_write.err; exit 1; }
+timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-host-path > /dev/null 2> $O/pmc_write.err || { tail -20 $O/pmc_write.err; exit 1; }
 cd $R
 python scripts/pmc_summary.py $O > $O/pmc_summary.json && cat $O/pmc_summary.json
+# rocprof launches of each kernel split into the bench phases (the host-path batches share the kernels)
+python scripts/trace_summary.py $O/prof/run_kernel_trace.csv warmup:2,profile:3,timed:10 > $O/kernel_trace_summary.json
 echo "ROUND OK"

@@ -389,6 +389,10 @@ struct sentinel_engine {
     DevBuf w_runs;                     // partition path: long-run / oversized-half work lists
     DevBuf w_pscan;                    // partition path: per-group range sums + range starts
     DevBuf io_ev, io_fl, io_out, io_vals;
+    // streamed host path (sentinel_submit_flow_stream_host): copy streams + two staging slots
+    hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+    hipEvent_t x_h2d[2] = {}, x_comp[2] = {};
+    DevBuf st_ev[2], st_fl[2], st_out[2];
     int64_t ws_cap = 0;
 
     int ensure_ws(int64_t n) {
@@ -1207,6 +1211,15 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
                       &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->w_runs, &e->w_pscan, &e->d_lres_state,
                       &e->d_lres_count, &e->d_lres_w, &e->d_lres_rcp, &e->d_lres_kind})
         b->release();
+    for (int k = 0; k < 2; ++k) {
+        e->st_ev[k].release();
+        e->st_fl[k].release();
+        e->st_out[k].release();
+        if (e->x_h2d[k]) (void)hipEventDestroy(e->x_h2d[k]);
+        if (e->x_comp[k]) (void)hipEventDestroy(e->x_comp[k]);
+    }
+    if (e->s_h2d) (void)hipStreamDestroy(e->s_h2d);
+    if (e->s_d2h) (void)hipStreamDestroy(e->s_d2h);
     if (e->h_part_stat) (void)hipHostFree(e->h_part_stat);
     e->d_part_stat.release();
     (void)hipStreamDestroy(e->stream);
@@ -1530,6 +1543,79 @@ int sentinel_submit_flow_batch_host(sentinel_engine_t *e, int64_t n, const senti
     HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     return 0;
+}
+
+// Host-fed stream: consecutive batches pipelined over three HIP streams.  Batch i's H2D (s_h2d),
+// decide (engine stream) and D2H (s_d2h) overlap batch i-1's D2H and batch i+1's H2D; device staging
+// is double-buffered (slot i & 1), a slot is refilled only after the decide that read it finished and
+// its verdicts left.  Batches are decided in order on one stream, so the verdicts equal one
+// sequential replay of all n events (what sentinel_submit_flow_batch_host over all n returns).
+int sentinel_submit_flow_stream_host(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev,
+                                     const uint8_t *flags, sentinel_verdict_t *out, int64_t batch,
+                                     float *batch_ms) {
+    if (!e || n < 0 || batch <= 0 || batch > MAX_BATCH || (n > 0 && (!ev || !out)))
+        return fail(SENTINEL_E_INVALID, "bad arguments");
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    if (!e->s_h2d) {
+        HIP_OK(hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking));
+        HIP_OK(hipStreamCreateWithFlags(&e->s_d2h, hipStreamNonBlocking));
+        for (int k = 0; k < 2; ++k) {
+            HIP_OK(hipEventCreateWithFlags(&e->x_h2d[k], hipEventDisableTiming));
+            HIP_OK(hipEventCreateWithFlags(&e->x_comp[k], hipEventDisableTiming));
+        }
+    }
+    const int64_t b = std::min(batch, n);
+    int rc = 0;
+    for (int k = 0; k < 2; ++k) {
+        rc |= e->st_ev[k].ensure(b * sizeof(Event));
+        rc |= e->st_out[k].ensure(b * 8);
+        if (flags) rc |= e->st_fl[k].ensure(b);
+    }
+    if (rc) return SENTINEL_E_NOMEM;
+    const int64_t nb = (n + b - 1) / b;
+    std::vector<hipEvent_t> t0, t1;
+    if (batch_ms) {
+        t0.resize(nb);
+        t1.resize(nb);
+        for (int64_t i = 0; i < nb; ++i) {
+            t0[i] = e->get_ev();
+            t1[i] = e->get_ev();
+        }
+    }
+    for (int64_t i = 0; i < nb; ++i) {
+        const int k = (int)(i & 1);
+        const int64_t off = i * b, m = std::min(b, n - off);
+        // the slot's events were read by batch i-2's decide, its verdicts copied out by batch i-2's D2H
+        if (i >= 2) HIP_OK(hipStreamWaitEvent(e->s_h2d, e->x_comp[k], 0));
+        if (batch_ms) HIP_OK(hipEventRecord(t0[i], e->s_h2d));
+        HIP_OK(hipMemcpyAsync(e->st_ev[k].p, ev + off, m * sizeof(Event), hipMemcpyHostToDevice, e->s_h2d));
+        if (flags) HIP_OK(hipMemcpyAsync(e->st_fl[k].p, flags + off, m, hipMemcpyHostToDevice, e->s_h2d));
+        HIP_OK(hipEventRecord(e->x_h2d[k], e->s_h2d));
+        HIP_OK(hipStreamWaitEvent(e->stream, e->x_h2d[k], 0));
+        if (i >= 2) HIP_OK(hipStreamWaitEvent(e->stream, t1.empty() ? e->x_comp[k] : t1[i - 2], 0));
+        rc = submit_flow(e, m, e->st_ev[k].as<Event>(), flags ? e->st_fl[k].as<uint8_t>() : nullptr,
+                         e->st_out[k].as<uint64_t>(), e->stream);
+        if (rc) break;
+        HIP_OK(hipEventRecord(e->x_comp[k], e->stream));
+        HIP_OK(hipStreamWaitEvent(e->s_d2h, e->x_comp[k], 0));
+        HIP_OK(hipMemcpyAsync(out + off, e->st_out[k].p, m * 8, hipMemcpyDeviceToHost, e->s_d2h));
+        if (batch_ms) HIP_OK(hipEventRecord(t1[i], e->s_d2h));
+        else HIP_OK(hipEventRecord(e->x_comp[k], e->s_d2h));   // D2H done: the slot is free again
+    }
+    HIP_OK(hipStreamSynchronize(e->s_d2h));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    if (batch_ms) {
+        for (int64_t i = 0; i < nb; ++i) {
+            float ms = 0;
+            if (rc == 0) HIP_OK(hipEventElapsedTime(&ms, t0[i], t1[i]));
+            batch_ms[i] = ms;
+            e->ev_pool.push_back(t0[i]);
+            e->ev_pool.push_back(t1[i]);
+        }
+    }
+    return rc;
 }
 
 int sentinel_submit_param_batch(sentinel_engine_t *e, int64_t n, const sentinel_param_event_t *ev,

@@ -327,6 +327,17 @@ class GpuTokenService:
               "submit_flow_batch_host")
         return out["status"].astype(np.int8), out["remaining"].copy(), out["wait_in_ms"].astype(np.int32)
 
+    def submit_flow_stream_host(self, flow_idx, acquire, ts, flags=None, batch=1 << 20):
+        """Like submit_flow_batch_host, pipelined in batches of `batch` events over side streams
+        (H2D / decide / D2H overlap).  Returns (status, remaining, wait_in_ms, batch_ms)."""
+        ev = self.pack_events(flow_idx, acquire, ts)
+        flags = None if flags is None else np.ascontiguousarray(flags, dtype=np.uint8)
+        out = np.empty(len(ev), dtype=_lib.VERDICT_DTYPE)
+        ms = np.zeros(max(1, -(-len(ev) // batch)), dtype=np.float32)
+        check(self._L.sentinel_submit_flow_stream_host(self._h, len(ev), _p(ev), _p(flags), _p(out), batch, _p(ms)),
+              "submit_flow_stream_host")
+        return out["status"].astype(np.int8), out["remaining"].copy(), out["wait_in_ms"].astype(np.int32), ms
+
     def submit_param_batch(self, events, verdicts=None, stream=None):
         """events: torch int64 tensor (n, 3) of sentinel_param_event_t records."""
         import torch

@@ -361,3 +361,16 @@ def test_partition_oversized_half(oracle_mod):
     ts = T.timestamps(n, 400_000.0, T.T0_ALIGNED + 3)
     ev = T.Events(idx, np.ones(n, np.int32), ts.astype(np.int64), None)
     _compare(_engine(rules), _oracle(oracle_mod, rules), rules, ev, batches=1)
+
+
+def test_stream_host_pipelined_bitexact(oracle_mod):
+    """sentinel_submit_flow_stream_host: the trace in uneven consecutive batches pipelined over the
+    copy streams (odd tail batch, both staging slots reused several times, prioritized flags) equals
+    the oracle's sequential replay of the whole trace, and every batch reports a latency."""
+    rules, ev = T.config2(250_000, seed=21, n_flows=3000)
+    flags = (np.random.default_rng(5).random(len(ev.ts)) < 0.01).astype(np.uint8)
+    svc = _engine(rules)
+    st_g, rem_g, w_g, ms = svc.submit_flow_stream_host(ev.flow_idx, ev.acquire, ev.ts, flags, batch=37_000)
+    st_o, rem_o, w_o = _oracle(oracle_mod, rules).replay(ev.flow_idx, ev.acquire, ev.ts, flags)
+    assert np.array_equal(st_g, st_o) and np.array_equal(rem_g, rem_o) and np.array_equal(w_g, w_o)
+    assert len(ms) == 7 and (ms > 0).all()
