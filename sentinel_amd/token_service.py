@@ -13,8 +13,10 @@ meaning and error convention (status codes, never exceptions for bad input).  Th
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import time
+import weakref
 from dataclasses import dataclass, field
 from typing import Iterable, Optional, Sequence
 
@@ -97,6 +99,22 @@ class ServerNamespace:
     max_allowed_qps: float = 30000.0   # ServerFlowConfig.DEFAULT_MAX_ALLOWED_QPS
 
 
+# Engines and batchers still alive at interpreter exit are closed by an atexit hook (batchers
+# first), while the HIP runtime is still up; finalizers of module globals would run too late.
+_LIVE_BATCHERS: "weakref.WeakSet" = weakref.WeakSet()
+_LIVE_ENGINES: "weakref.WeakSet" = weakref.WeakSet()
+
+
+@atexit.register
+def _close_all():
+    for group in (_LIVE_BATCHERS, _LIVE_ENGINES):
+        for obj in list(group):
+            try:
+                obj.close()
+            except Exception:
+                pass
+
+
 def _p(a):
     return None if a is None else C.c_void_p(a.ctypes.data)
 
@@ -114,6 +132,7 @@ class GpuTokenService:
         self._h = C.c_void_p()
         cfg = _lib.ServerConfig(exceed_count, max_occupy_ratio)
         check(self._L.sentinel_engine_create(device, C.byref(cfg), C.byref(self._h)), "sentinel_engine_create")
+        _LIVE_ENGINES.add(self)
         self.device = device
         self.sample_counts = {}
         self._flow_rules = []
@@ -493,6 +512,7 @@ class TokenBatcher:
         self._L = svc._L
         self._b = C.c_void_p()
         check(self._L.sentinel_batcher_create(svc.handle, max_batch, max_wait_us, C.byref(self._b)), "batcher_create")
+        _LIVE_BATCHERS.add(self)
 
     def request_token(self, rule_id, acquire_count, prioritized=False, ts=None) -> TokenResult:
         out = _lib.TokenResultC()
