@@ -438,6 +438,83 @@ __device__ inline void part_run_w(FlowWindow<NMAX> &fw, const KeyTable &T, uint3
     fw.flush();
 }
 
+// The common case of a run: every event of the flow in the batch falls in one epoch E with one
+// acquire count and no prioritized cluster request (a flow sees ~8 events per batch over a few ms,
+// windows are >= 100 ms).  Then the whole run is one closed-form segment (FlowWindow::fast), and the
+// window header, folded as it arrives, is only needed as {PASS sum of the valid slots, the rolled
+// slot's pair, "a slot is newer than E"}.  The rolled slot's rest line does not depend on the header,
+// so its load is issued together with the header loads: one memory round trip instead of two.
+// Returns false, having written nothing, when the run needs the general walk (part_run_w).
+template <int NMAX>
+__device__ inline bool part_run_single(FlowWindow<NMAX> &fw, const uint64_t *s_val, uint32_t q0, uint32_t q1,
+                                       const EventSrc &src, const Verdicts &V, int64_t T0) {
+    if (fw.ks.hs == 2) return false;
+    fw.E0 = epoch_of(T0, fw.w, fw.rcp);
+    fw.r0 = (int32_t)(T0 - fw.E0 * (int64_t)fw.w);
+    fw.rcpf = 1.0f / (float)fw.w;
+    int32_t a;
+    bool prio;
+    const int64_t E = fw.event(s_val[q0], src, T0, a, prio);
+    bool ok = !(prio && fw.kind == KIND_CLUSTER) && !(fw.occ_pending && fw.ks.seven && fw.kind == KIND_CLUSTER);
+    for (uint32_t q = q0 + 1; q < q1 && ok; ++q) {
+        int32_t a2;
+        bool p2;
+        ok = fw.event(s_val[q], src, T0, a2, p2) == E && a2 == a && !(p2 && fw.kind == KIND_CLUSTER);
+    }
+    if (!ok) return false;
+    const int nsc = fw.nsc;
+    const int slot = (int)(E % nsc);
+    // header pairs (every slot of the block: in bounds) and the rolled slot's rest line, in flight together
+    longlong2 hp[NMAX];
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) hp[j] = *reinterpret_cast<const longlong2 *>(fw.ks.pair(j));
+    int64_t *r = fw.ks.rest(slot);
+    int64_t blk = 0, preq = 0, breq = 0;
+    if (fw.ks.seven) {
+        const longlong2 r01 = *reinterpret_cast<const longlong2 *>(r);
+        blk = r01.x;
+        preq = r01.y;
+        breq = r[2];
+    }
+    int64_t s_other = 0, ep_s = EPOCH_ABSENT, ps_s = 0;
+    bool newer = false;
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+        if (j >= nsc) continue;
+        const int64_t e = hp[j].x;
+        if (j == slot) { ep_s = e; ps_s = hp[j].y; }
+        else if (e != EPOCH_ABSENT && e > E - nsc) s_other = wrap_add(s_other, hp[j].y);
+        newer |= e != EPOCH_ABSENT && e > E;
+    }
+    if (newer) return false;                              // clock went backwards: detached windows
+    const bool fresh = ep_s != E;
+    const int64_t base = fresh ? 0 : ps_s;
+    const int64_t s0 = wrap_add(s_other, base);
+    const uint32_t len = q1 - q0;
+    uint32_t lo = 0, hi = len;                            // K = first p with !admits(S0 + p*a)
+    while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo) / 2;
+        if (admits(fw.kind, fw.thr, fw.I_s, wrap_add(s0, wrap_mul((int64_t)mid, a)), a)) lo = mid + 1;
+        else hi = mid;
+    }
+    const uint32_t K = lo;
+    const int64_t nb = (int64_t)(len - K);
+    *reinterpret_cast<longlong2 *>(fw.ks.pair(slot)) = longlong2{E, wrap_add(base, wrap_mul((int64_t)K, a))};
+    if (fw.ks.seven) {
+        if (fresh) { blk = 0; preq = 0; breq = 0; }
+        *reinterpret_cast<longlong2 *>(r) = longlong2{wrap_add(blk, wrap_mul(nb, a)), wrap_add(preq, (int64_t)K)};
+        r[2] = wrap_add(breq, nb);
+        if (fresh) {
+            *reinterpret_cast<longlong2 *>(r + 3) = longlong2{0, 0};
+            *reinterpret_cast<longlong2 *>(r + 5) = longlong2{0, 0};
+        }
+    }
+    const bool small = s0 >= 0 && s0 + (int64_t)len * a < (int64_t)INT32_MAX;
+    for (uint32_t k = 0; k < len; ++k)
+        V.out[(uint32_t)s_val[q0 + k] & SEQ_MASK] = fw.verdict(s0, a, K, k, small);
+    return true;
+}
+
 template <int NMAX>
 __device__ inline void part_run(const KeyTable &T, uint32_t key, const uint64_t *s_val, uint32_t q0, uint32_t q1,
                                 const EventSrc &src, const Verdicts &V, int64_t T0) {
@@ -765,7 +842,7 @@ __global__ __launch_bounds__(PH_THREADS, NMAX > 10 ? 2 : 4) void k_part_half(
     __syncthreads();
     for (uint32_t l = 0; l < s_nlong; ++l)
         for (uint32_t q = t; q < s_long[l][1]; q += PH_THREADS) gsval[goff + s_long[l][0] + q] = sv[s_long[l][0] + q];
-    if (c > 0 && c <= LONG_RUN) {
+    if (c > 0 && c <= LONG_RUN && !part_run_single<NMAX>(fw, sv, start, start + c, src, V, T0)) {
         fw.load_header(T0);
         part_run_w<NMAX>(fw, T, key, sv, start, start + c, src, V, T0);
     }
