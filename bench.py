@@ -280,9 +280,10 @@ def main():
         if dom == "part_fused":
             # per event: read the 8-B packed value (local key inside), write the 8-B verdict; per
             # touched flow: read the window header (16 B per bucket) and the 42 B of rule fields,
-            # write back the rolled bucket's 16-B pair, read + write its 64-B counter line
+            # write back the rolled bucket's 16-B pair, read + write its BLOCK / PASS_REQUEST /
+            # BLOCK_REQUEST counters (3 x 8 B each way, blocked counter rows)
             e_f = N / max(1, F)
-            bpe = 16.0 + (args.sample_count * 16 + 42 + 16 + 128) / max(1.0, e_f)
+            bpe = 16.0 + (args.sample_count * 16 + 42 + 16 + 48) / max(1.0, e_f)
         if dom == "radix_scatter":
             passes = max(1, round(d["calls"] / max(1, args.steps)))
             bpe = (32.0 + 24.0 * (passes - 1)) / passes

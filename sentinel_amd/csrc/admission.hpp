@@ -161,20 +161,37 @@ struct Verdicts {
 };
 
 // A key's state: header pair j {epoch, PASS} at base + hs*j (hs = 2: contiguous record;
-// hs = 2*HB_KEYS: the flow table's blocked slot-major header region), rest lines at rbase.
+// hs = 2*HB_KEYS: the flow table's blocked slot-major header region); the other six counters of
+// slot j (BLOCK .. WAITING) at rbase + rs*j + rcs*c (rs = 8, rcs = 1: a contiguous rest line;
+// rs = 6*HB_KEYS, rcs = HB_KEYS: the flow table's blocked rest region, counter-major per slot, so
+// the 64 lanes of a wave touching counter c of slot j of 64 consecutive flows touch 512 B).
 struct KeyState {
     int64_t *base;
     int64_t *rbase;
     int hs;
     int n;
+    int rs, rcs;
     bool seven;   // 7-counter flow layout
     __device__ inline int64_t *pair(int slot) const { return base + (int64_t)hs * slot; }
     __device__ inline int64_t &ep(int slot) const { return pair(slot)[0]; }
     __device__ inline int64_t &cnt(int ev, int slot) const {
         if (ev == EV_PASS || !seven) return pair(slot)[1];
-        return rest(slot)[ev - 1];
+        return rc(slot, ev - 1);
     }
-    __device__ inline int64_t *rest(int slot) const { return rbase + 8 * (int64_t)slot; }
+    __device__ inline int64_t &rc(int slot, int c) const { return rbase[(int64_t)rs * slot + (int64_t)rcs * c]; }
+    // ClusterMetric.add of a decided homogeneous segment on slot `slot` (CFC:76-77,100-101):
+    // BLOCK += nb*a, PASS_REQUEST += K, BLOCK_REQUEST += nb, from the slot's previous values
+    // (zero for a fresh bucket, whose other counters are cleared: LeapArray.resetWindowTo)
+    __device__ inline void book_rest(int slot, bool fresh, int64_t blk, int64_t preq, int64_t breq, int64_t nb,
+                                     int32_t a, uint32_t K) const {
+        if (fresh) { blk = 0; preq = 0; breq = 0; }
+        rc(slot, EV_BLOCK - 1) = wrap_add(blk, wrap_mul(nb, a));
+        rc(slot, EV_PASS_REQUEST - 1) = wrap_add(preq, (int64_t)K);
+        rc(slot, EV_BLOCK_REQUEST - 1) = wrap_add(breq, nb);
+        if (fresh)
+#pragma unroll
+            for (int c = 3; c < 6; ++c) rc(slot, c) = 0;
+    }
 };
 
 // Slots per block of the flow header region: the kernel template bucket of the largest n, so a
@@ -189,6 +206,12 @@ __host__ __device__ inline int64_t blocked_pair_word(int64_t key, int hblock, in
     return 2 * ((((key / HB_KEYS) * hblock + slot) * HB_KEYS) + key % HB_KEYS);
 }
 
+// Flow-table rest region (after the header region): blocks of HB_KEYS flows, per slot six
+// counter rows of HB_KEYS words.  Word of counter c of slot j of flow `key`, from the region start.
+__host__ __device__ inline int64_t blocked_rest_word(int64_t key, int hblock, int slot, int c) {
+    return (((key / HB_KEYS) * hblock + slot) * 6 + c) * HB_KEYS + key % HB_KEYS;
+}
+
 __device__ inline KeyState key_state(const KeyTable &T, uint32_t key) {
     KeyState k;
     const int64_t off = T.state_off ? T.state_off[key] : (int64_t)key * T.state_stride;
@@ -197,11 +220,15 @@ __device__ inline KeyState key_state(const KeyTable &T, uint32_t key) {
     if (T.hblock) {
         k.base = T.state + blocked_pair_word(key, T.hblock, 0);
         k.hs = 2 * HB_KEYS;
-        k.rbase = T.state + off;
+        k.rbase = T.state + off;                 // blocked_rest_word(key, hblock, 0, 0) + region start
+        k.rs = 6 * HB_KEYS;
+        k.rcs = HB_KEYS;
     } else {
         k.base = T.state + off;
         k.hs = 2;
         k.rbase = k.base + header_words(k.n);
+        k.rs = 8;
+        k.rcs = 1;
     }
     return k;
 }
@@ -217,9 +244,8 @@ __device__ inline int roll(const KeyTable &T, uint32_t key, const KeyState &S, i
     S.ep(slot) = E;
     S.cnt(EV_PASS, slot) = 0;
     if (S.seven) {
-        int64_t *r = &S.cnt(EV_BLOCK, slot);
 #pragma unroll
-        for (int c = 0; c < 6; ++c) r[c] = 0;
+        for (int c = 0; c < 6; ++c) S.rc(slot, c) = 0;
         if (reset && T.kind[key] == KIND_CLUSTER && T.has_occ[key]) {
             // ClusterMetricLeapArray.transferOccupyToBucket (ClusterMetricLeapArray.java:154-169)
             int64_t *o = T.occ + 2 * (int64_t)key;
@@ -770,15 +796,9 @@ __global__ __launch_bounds__(256) void k_process_reg(KeyTable T, BatchWork W, Ev
         for (int j = 0; j < NMAX; ++j)
             if (j == slot) { ps[j] = wrap_add(ps[j], wrap_mul((int64_t)K, a)); dirty |= 1u << j; }
         if (ks.seven) {
-            int64_t *r = ks.rest(slot);
             int64_t blk = 0, preq = 0, breq = 0;
-            if (!fresh) { blk = r[0]; preq = r[1]; breq = r[2]; }
-            *reinterpret_cast<longlong2 *>(r) = longlong2{wrap_add(blk, wrap_mul(nb, a)), wrap_add(preq, (int64_t)K)};
-            r[2] = wrap_add(breq, nb);
-            if (fresh) {
-                *reinterpret_cast<longlong2 *>(r + 3) = longlong2{0, 0};
-                *reinterpret_cast<longlong2 *>(r + 5) = longlong2{0, 0};
-            }
+            if (!fresh) { blk = ks.rc(slot, 0); preq = ks.rc(slot, 1); breq = ks.rc(slot, 2); }
+            ks.book_rest(slot, fresh, blk, preq, breq, nb, a, K);
         }
         W.seg_s0[g] = s0;
         W.seg_k[g] = K;
@@ -881,7 +901,7 @@ __device__ inline void process_key_group(const KeyTable &T, const BatchWork &W, 
 #pragma unroll
                 for (int q = 0; q < PROC_SLOTS_PER_LANE; ++q) if (q == qs) { ep[q] = E; ps[q] = 0; dirty[q] = true; }
             }
-            if (ks.seven && lg < 6) ks.rest(slot)[lg] = 0;
+            if (ks.seven && lg < 6) ks.rc(slot, lg) = 0;
         }
         int64_t part = 0;
 #pragma unroll
@@ -902,10 +922,9 @@ __device__ inline void process_key_group(const KeyTable &T, const BatchWork &W, 
                 if (q == qs) { ps[q] = wrap_add(ps[q], wrap_mul((int64_t)K, a)); dirty[q] = true; }
         }
         if (ks.seven) {
-            int64_t *r = ks.rest(slot);
-            if (lg == EV_PASS_REQUEST - 1) r[lg] = wrap_add(r[lg], (int64_t)K);
-            else if (lg == EV_BLOCK - 1) r[lg] = wrap_add(r[lg], wrap_mul(nb, a));
-            else if (lg == EV_BLOCK_REQUEST - 1) r[lg] = wrap_add(r[lg], nb);
+            if (lg == EV_PASS_REQUEST - 1) ks.rc(slot, lg) = wrap_add(ks.rc(slot, lg), (int64_t)K);
+            else if (lg == EV_BLOCK - 1) ks.rc(slot, lg) = wrap_add(ks.rc(slot, lg), wrap_mul(nb, a));
+            else if (lg == EV_BLOCK_REQUEST - 1) ks.rc(slot, lg) = wrap_add(ks.rc(slot, lg), nb);
         }
         if (lg == 0) {
             W.seg_s0[g] = s0;

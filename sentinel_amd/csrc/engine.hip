@@ -1342,22 +1342,23 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
     std::vector<double> rcp(F), Is(F);
     std::vector<uint8_t> kind(F);
     // layout: blocked slot-major header region (HB_KEYS flows x hblock slots per block), then the
-    // rest lines of every flow at off[i]
+    // blocked rest region (per block and slot, six counter rows of HB_KEYS flows); off[i] = flow i's
+    // counter-0 slot-0 word of the rest region
     int32_t maxn = 1;
     for (size_t i = 0; i < F; ++i) maxn = std::max(maxn, e->rules[i].sample_count);
     const int32_t hblock = header_block_slots(maxn);
-    const int64_t hwords = (((int64_t)F + HB_KEYS - 1) / HB_KEYS) * hblock * HB_KEYS * 2;
-    int64_t words = hwords;
+    const int64_t nblk = ((int64_t)F + HB_KEYS - 1) / HB_KEYS;
+    const int64_t hwords = nblk * hblock * HB_KEYS * 2;
+    const int64_t words = hwords + nblk * hblock * 6 * HB_KEYS;
     for (size_t i = 0; i < F; ++i) {
         const sentinel_flow_rule_t &r = e->rules[i];
-        off[i] = words;
+        off[i] = hwords + blocked_rest_word((int64_t)i, hblock, 0, 0);
         nn[i] = r.sample_count;
         ww[i] = r.window_interval_ms / r.sample_count;
         rcp[i] = 1.0 / (double)ww[i];
         Is[i] = r.window_interval_ms / 1000.0;   // LeapArray.java:74
         kind[i] = r.checker == SENTINEL_CHECKER_SIMPLE ? KIND_SIMPLE : KIND_CLUSTER;
         ids[i] = r.flow_id;
-        words += 8 * (int64_t)r.sample_count;
     }
     // new state image: fresh, then carry surviving flows whose window shape is unchanged
     std::vector<int64_t> st(std::max<int64_t>(words, 1), 0);
@@ -1378,8 +1379,9 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
             st[b] = old_state[a];
             st[b + 1] = old_state[a + 1];
         }
-        std::copy(old_state.begin() + old_off[o], old_state.begin() + old_off[o] + 8 * (int64_t)nn[i],
-                  st.begin() + off[i]);
+        for (int j = 0; j < nn[i]; ++j)
+            for (int c = 0; c < 6; ++c)
+                st[off[i] + (int64_t)j * 6 * HB_KEYS + c * HB_KEYS] = old_state[old_off[o] + (int64_t)j * 6 * HB_KEYS + c * HB_KEYS];
         occ[2 * i] = old_occ[2 * o];
         occ[2 * i + 1] = old_occ[2 * o + 1];
         hocc[i] = old_hocc[o];
@@ -2051,11 +2053,15 @@ int sentinel_dump_flow(sentinel_engine_t *e, int32_t idx, int64_t *out, int32_t 
     if (out_len < need) return fail(SENTINEL_E_INVALID, "output too small");
     HIP_OK(hipSetDevice(e->device));
     HIP_OK(hipStreamSynchronize(e->stream));
-    std::vector<int64_t> hdr(2 * (size_t)n), rest(8 * (size_t)n);
+    // the flow's words of the blocked rest region span (n - 1) slot rows + 6 counter rows
+    const int64_t rspan = (int64_t)(n - 1) * 6 * HB_KEYS + 5 * HB_KEYS + 1;
+    std::vector<int64_t> hdr(2 * (size_t)n), rspan_w((size_t)rspan), rest(8 * (size_t)n);
     for (int j = 0; j < n; ++j)
         HIP_OK(hipMemcpy(hdr.data() + 2 * j, e->ft.state.as<int64_t>() + blocked_pair_word(idx, e->flow_hblock, j), 16,
                          hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(rest.data(), e->ft.state.as<int64_t>() + e->h_flow_off[idx], rest.size() * 8, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(rspan_w.data(), e->ft.state.as<int64_t>() + e->h_flow_off[idx], rspan * 8, hipMemcpyDeviceToHost));
+    for (int j = 0; j < n; ++j)
+        for (int c = 0; c < 6; ++c) rest[8 * j + c] = rspan_w[(size_t)j * 6 * HB_KEYS + c * HB_KEYS];
     int64_t occ[2];
     uint8_t hocc;
     HIP_OK(hipMemcpy(occ, e->ft.occ.as<int64_t>() + 2 * idx, 16, hipMemcpyDeviceToHost));

@@ -372,15 +372,9 @@ struct FlowWindow {
 #else
         if (ks.seven) {
 #endif
-            int64_t *r = ks.rest(slot);
             int64_t blk = 0, preq = 0, breq = 0;
-            if (!fresh) { blk = r[0]; preq = r[1]; breq = r[2]; }
-            *reinterpret_cast<longlong2 *>(r) = longlong2{wrap_add(blk, wrap_mul(nb, a)), wrap_add(preq, (int64_t)K)};
-            r[2] = wrap_add(breq, nb);
-            if (fresh) {
-                *reinterpret_cast<longlong2 *>(r + 3) = longlong2{0, 0};
-                *reinterpret_cast<longlong2 *>(r + 5) = longlong2{0, 0};
-            }
+            if (!fresh) { blk = ks.rc(slot, 0); preq = ks.rc(slot, 1); breq = ks.rc(slot, 2); }
+            ks.book_rest(slot, fresh, blk, preq, breq, nb, a, K);
         }
     }
 
@@ -466,16 +460,21 @@ __device__ inline bool part_run_single(FlowWindow<NMAX> &fw, const uint64_t *s_v
     const int slot = (int)(E % nsc);
     // header pairs (every slot of the block: in bounds) and the rolled slot's rest line, in flight together
     longlong2 hp[NMAX];
+#ifdef SENTINEL_DIAG_HDR1       // cost diagnostic only (wrong sums): the rolled slot's pair alone
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) hp[j] = longlong2{EPOCH_ABSENT, 0};
+    hp[0] = *reinterpret_cast<const longlong2 *>(fw.ks.pair(slot));
+#else
 #pragma unroll
     for (int j = 0; j < NMAX; ++j) hp[j] = *reinterpret_cast<const longlong2 *>(fw.ks.pair(j));
-    int64_t *r = fw.ks.rest(slot);
+#endif
+#ifdef SENTINEL_DIAG_NOREST     // cost diagnostic only (wrong counters)
+    const bool seven = false;
+#else
+    const bool seven = fw.ks.seven;
+#endif
     int64_t blk = 0, preq = 0, breq = 0;
-    if (fw.ks.seven) {
-        const longlong2 r01 = *reinterpret_cast<const longlong2 *>(r);
-        blk = r01.x;
-        preq = r01.y;
-        breq = r[2];
-    }
+    if (seven) { blk = fw.ks.rc(slot, 0); preq = fw.ks.rc(slot, 1); breq = fw.ks.rc(slot, 2); }
     int64_t s_other = 0, ep_s = EPOCH_ABSENT, ps_s = 0;
     bool newer = false;
 #pragma unroll
@@ -500,18 +499,18 @@ __device__ inline bool part_run_single(FlowWindow<NMAX> &fw, const uint64_t *s_v
     const uint32_t K = lo;
     const int64_t nb = (int64_t)(len - K);
     *reinterpret_cast<longlong2 *>(fw.ks.pair(slot)) = longlong2{E, wrap_add(base, wrap_mul((int64_t)K, a))};
-    if (fw.ks.seven) {
-        if (fresh) { blk = 0; preq = 0; breq = 0; }
-        *reinterpret_cast<longlong2 *>(r) = longlong2{wrap_add(blk, wrap_mul(nb, a)), wrap_add(preq, (int64_t)K)};
-        r[2] = wrap_add(breq, nb);
-        if (fresh) {
-            *reinterpret_cast<longlong2 *>(r + 3) = longlong2{0, 0};
-            *reinterpret_cast<longlong2 *>(r + 5) = longlong2{0, 0};
-        }
-    }
+    if (seven) fw.ks.book_rest(slot, fresh, blk, preq, breq, nb, a, K);
     const bool small = s0 >= 0 && s0 + (int64_t)len * a < (int64_t)INT32_MAX;
+#if defined(SENTINEL_DIAG_NOVERDICT)     // cost diagnostic only (no output)
+    uint64_t acc = 0;
+    for (uint32_t k = 0; k < len; ++k) acc ^= fw.verdict(s0, a, K, k, small) ^ s_val[q0 + k];
+    if (acc == 0x123456789ull) V.out[0] = acc;
+#elif defined(SENTINEL_DIAG_VLINEAR)     // cost diagnostic only (wrong output): flow-contiguous stores
+    for (uint32_t k = 0; k < len; ++k) V.out[(blockIdx.x * blockDim.x + threadIdx.x) * 8 + (k & 7)] = fw.verdict(s0, a, K, k, small);
+#else
     for (uint32_t k = 0; k < len; ++k)
         V.out[(uint32_t)s_val[q0 + k] & SEQ_MASK] = fw.verdict(s0, a, K, k, small);
+#endif
     return true;
 }
 
