@@ -37,8 +37,8 @@ KERNEL_BYTES_PER_EVENT = {
     "seg_heads": 17.0,        # read key 4 + value 8, write head 4 + homogeneity flag 1
     "seg_mark": 5.0,          # read segid 4 + flag 1 (segment records are per segment)
     "verdict": 20.0,          # read segid 4 + value 8, write the 8-B verdict
-    "part_prep": 20.0,        # read the 16-B event, write the 4-B key (range histogram in LDS)
-    "part_scatter": 28.0,     # read key 4 + event 16, write the 8-B packed value (local key inside)
+    "part_prep": 16.0,        # read the 16-B event (range histogram in LDS; no key array without namespace routes)
+    "part_scatter": 24.0,     # read the 16-B event (key re-derived), write the 8-B packed value (local key inside)
 }
 
 

@@ -102,6 +102,13 @@ struct EventSrc {
         int32_t a;
         uint8_t fl;
         load(s, t, a, fl);
+        return pack_fields(s, t, a, fl, T0);
+    }
+    // ... of an event already loaded (flow events)
+    __device__ inline uint64_t pack_event(uint32_t s, const Event &e, uint8_t fl, int64_t T0) const {
+        return pack_fields(s, e.ts, unit_acquire ? 1 : e.acquire, fl, T0);
+    }
+    __device__ inline uint64_t pack_fields(uint32_t s, int64_t t, int32_t a, uint8_t fl, int64_t T0) const {
         const int64_t dt = t - T0;
         const uint32_t dtf = (dt > -(1 << (VAL_DT_BITS - 1)) && dt < (1 << (VAL_DT_BITS - 1)) - 1)
                                  ? ((uint32_t)dt & VAL_DT_ESC) : VAL_DT_ESC;

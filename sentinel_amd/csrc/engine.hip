@@ -868,7 +868,8 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
     uint32_t *ctl = e->w_runs.as<uint32_t>();
     e->launch("part_prep", n, s, [&] {
         k_part_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
-            n, ev, F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, fkey, finvalid, lb, hist, nb, nparts,
+            n, ev, F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, e->flow_plain ? nullptr : fkey,
+            finvalid, lb, hist, nb, nparts,
             ctl, stat);
     });
     e->launch("scan", n, s, [&] {
@@ -879,9 +880,9 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
     });
     const EventSrc src{ev, nullptr, fl, false};
     e->launch("part_scatter", n, s, [&] {
-        k_part_scatter<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(fkey, src, e->w_sval.as<uint64_t>(), n,
-                                                                         finvalid, lb, pbits,
-                                                                         hist, nb, nparts);
+        k_part_scatter<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(e->flow_plain ? nullptr : fkey, src,
+                                                                         e->w_sval.as<uint64_t>(), n, finvalid, lb,
+                                                                         pbits, hist, nb, nparts, F);
     });
     const KeyTable FT = e->table(e->ft, NEV, 0);
     const Verdicts V{out, fkey, finvalid};

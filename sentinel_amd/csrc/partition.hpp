@@ -63,7 +63,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_part_prep(int64_t n, const Eve
         else if (route && route[e.idx] == ROUTE_TOO_MANY) st = ST_TOO_MANY_REQUEST;  // namespace == null (CFC:50-53)
         else if (e.ts < 0) st = ST_FAIL;                                              // reference: NPE in LeapArray
         else k = (uint32_t)e.idx;
-        fkey[i] = k;
+        if (fkey) fkey[i] = k;
         if (st == 127) atomicAdd(&h[k >> lb], 1u);
         else put_verdict(out, (uint32_t)i, st, 0, 0);
     }
@@ -136,12 +136,14 @@ __global__ __launch_bounds__(PS_THREADS) void k_part_offsets(uint32_t *__restric
 
 // Stable multi-split of the valid events by range digit (one pass).  Same tiling as k_part_prep;
 // ranking with one 64-bit ballot per digit bit and wave-private LDS counters; the tile is staged
-// in LDS in digit order and written out as contiguous per-range runs.
+// in LDS in digit order and written out as contiguous per-range runs.  keys_in == null (no
+// namespace routes, the common case): the flow key and validity are re-derived from the event the
+// value is packed from anyway, so k_part_prep writes no key array and nothing reads one.
 __global__ __launch_bounds__(SORT_THREADS) void k_part_scatter(const uint32_t *__restrict__ keys_in, EventSrc src,
                                                                uint64_t *__restrict__ vals_out, int64_t n,
                                                                uint32_t finvalid, int lb, int pbits,
                                                                const uint32_t *__restrict__ offsets, int64_t nblocks,
-                                                               int32_t nparts) {
+                                                               int32_t nparts, int32_t nflows) {
     __shared__ uint16_t cnt[SORT_WAVES][PART_BINS];
     __shared__ uint32_t goff[PART_BINS];
     __shared__ uint32_t loff[PART_BINS];
@@ -160,10 +162,31 @@ __global__ __launch_bounds__(SORT_THREADS) void k_part_scatter(const uint32_t *_
     const int64_t base = tile0 + (int64_t)wave * (SORT_ITEMS * WAVE);
     const int64_t T0 = src.t0();
     uint32_t key[SORT_ITEMS], rank[SORT_ITEMS];
+    uint64_t pk[SORT_ITEMS];                       // packed values (keys_in == null: from the events loaded here)
+    if (keys_in) {
 #pragma unroll
-    for (int j = 0; j < SORT_ITEMS; ++j) {
-        const int64_t i = base + j * WAVE + lane;
-        key[j] = i < n ? keys_in[i] : finvalid;
+        for (int j = 0; j < SORT_ITEMS; ++j) {
+            const int64_t i = base + j * WAVE + lane;
+            key[j] = i < n ? keys_in[i] : finvalid;
+        }
+    } else {
+        Event evs[SORT_ITEMS];
+        uint8_t fls[SORT_ITEMS];
+#pragma unroll
+        for (int j = 0; j < SORT_ITEMS; ++j) {
+            const int64_t i = base + j * WAVE + lane;
+            if (i < n) { evs[j] = src.ev[i]; fls[j] = src.flags ? src.flags[i] : 0; }
+        }
+#pragma unroll
+        for (int j = 0; j < SORT_ITEMS; ++j) {
+            const int64_t i = base + j * WAVE + lane;
+            const Event e = evs[j];
+            // k_part_prep's validation without the route check (keys_in is only null without routes)
+            const bool ok = i < n && e.idx != SENTINEL_IDX_BAD_ID && e.acquire > 0 && e.idx >= 0 && e.idx < nflows &&
+                            e.ts >= 0;
+            key[j] = ok ? (uint32_t)e.idx : finvalid;
+            pk[j] = ok ? src.pack_event((uint32_t)i, e, fls[j], T0) : 0ull;
+        }
     }
 #pragma unroll
     for (int j = 0; j < SORT_ITEMS; ++j) {
@@ -209,7 +232,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_part_scatter(const uint32_t *_
         const uint32_t d = key[j] >> lb;
         const uint32_t p = loff[d] + cnt[wave][d] + rank[j];
         sdig[p] = (uint16_t)d;
-        svals[p] = src.pack((uint32_t)(base + j * WAVE + lane), T0) |
+        svals[p] = (keys_in ? src.pack((uint32_t)(base + j * WAVE + lane), T0) : pk[j]) |
                    ((uint64_t)(key[j] & ((1u << lb) - 1)) << VAL_KEY_SHIFT);
     }
     __syncthreads();
