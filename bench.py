@@ -84,6 +84,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3)
+    ap.add_argument("--kernel-every", type=int, default=2,
+                    help="time the dominant kernel with HIP events on every k-th timed step")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-fed legs")
     ap.add_argument("--host-reps", type=int, default=20)
     return ap.parse_args()
@@ -169,17 +171,21 @@ def main():
         dom = max(breakdown, key=lambda k: breakdown[k]["total_ms"])
         svc._L.sentinel_profile_select(svc.handle, dom.encode())
         svc._L.sentinel_profile_enable(svc.handle, 1)
-    tev_a = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    tev_b = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    # batch boundaries: one event between consecutive batches (batch k = tev[k] -> tev[k + 1]);
+    # the dominant kernel is bracketed by the engine's HIP events on every `kernel_every`-th timed
+    # step (each event record idles the queue ~5 us)
+    tev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for k in range(args.steps):
         s = args.warmup + pstep + k
-        tev_a[k].record(ext)
+        if not args.no_profile:
+            svc._L.sentinel_profile_gate(svc.handle, 1 if k % args.kernel_every == 0 else 0)
+        tev[k].record(ext)
         svc.submit_flow_batch(ev_b[s], verdicts=verdicts)
-        tev_b[k].record(ext)
+    tev[args.steps].record(ext)
     svc.synchronize()
     torch.cuda.synchronize()
     if world > 1:
@@ -189,7 +195,7 @@ def main():
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
-    lat = sorted(tev_a[k].elapsed_time(tev_b[k]) for k in range(args.steps))
+    lat = sorted(tev[k].elapsed_time(tev[k + 1]) for k in range(args.steps))
     p99 = lat[min(len(lat) - 1, int(np.ceil(0.99 * len(lat))) - 1)]
 
     # ---- the dominant kernel's live duration over the timed region (HIP events on the engine stream)

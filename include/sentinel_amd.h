@@ -367,6 +367,9 @@ int  sentinel_profile_enable(sentinel_engine_t *eng, int enable);
 /* Time only the named kernel (NULL or "": every kernel): two events per launch of it instead of two
  * per launch of every kernel, so a timed run keeps its dominant kernel's live duration cheaply. */
 int  sentinel_profile_select(sentinel_engine_t *eng, const char *kernel);
+/* Gate the timing of following launches on (1) or off (0) without collecting or clearing what was
+ * timed so far (no host synchronisation: callable between the batches of a timed loop). */
+int  sentinel_profile_gate(sentinel_engine_t *eng, int on);
 int  sentinel_profile_read(sentinel_engine_t *eng, int max, char *names32, double *total_ms,
                            int64_t *calls, int64_t *units);
 

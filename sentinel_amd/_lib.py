@@ -49,7 +49,7 @@ EXPORTS = [
     "sentinel_submit_concurrent_batch_host", "sentinel_concurrent_now_calls", "sentinel_concurrent_token_count",
     "sentinel_concurrent_expire",
     "sentinel_load_local_resources", "sentinel_submit_local_entry_batch", "sentinel_submit_local_entry_batch_host",
-    "sentinel_local_node_stats", "sentinel_set_occupy_timeout", "sentinel_profile_select",
+    "sentinel_local_node_stats", "sentinel_set_occupy_timeout", "sentinel_profile_select", "sentinel_profile_gate",
 ]
 
 STATUS_RELEASE_OK = 6
@@ -178,6 +178,7 @@ def load():
         "sentinel_local_node_stats": (C.c_int, [vp, i32, i64, vp]),
         "sentinel_set_occupy_timeout": (C.c_int, [vp, i32]),
         "sentinel_profile_select": (C.c_int, [vp, C.c_char_p]),
+        "sentinel_profile_gate": (C.c_int, [vp, C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
