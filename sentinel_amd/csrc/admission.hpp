@@ -58,8 +58,9 @@ struct KeyTable {
     int64_t *occ;            // CLUSTER only: [2*k] occupy PASS, [2*k+1] occupy PASS_REQUEST (CMLA:129)
     uint8_t *has_occ;        // CMLA:130
     int32_t ncounters;       // 7 (flows) or 1 (limiter / param)
-    int32_t hblock;          // > 0: headers in the blocked slot-major region (slots per block);
-                             // state_off then locates the rest lines only
+    int32_t hblock;          // > 0: headers in the blocked slot-major region (slots per block),
+                             // rest counters in the blocked rest region at word rest_base
+    int64_t rest_base;
     double max_occupy_ratio; // ServerFlowConfig.maxOccupyRatio
 };
 
@@ -221,16 +222,16 @@ __host__ __device__ inline int64_t blocked_rest_word(int64_t key, int hblock, in
 
 __device__ inline KeyState key_state(const KeyTable &T, uint32_t key) {
     KeyState k;
-    const int64_t off = T.state_off ? T.state_off[key] : (int64_t)key * T.state_stride;
     k.n = T.n[key];
     k.seven = T.ncounters == NEV;
-    if (T.hblock) {
+    if (T.hblock) {                              // pure address arithmetic: no dependent load
         k.base = T.state + blocked_pair_word(key, T.hblock, 0);
         k.hs = 2 * HB_KEYS;
-        k.rbase = T.state + off;                 // blocked_rest_word(key, hblock, 0, 0) + region start
+        k.rbase = T.state + T.rest_base + blocked_rest_word(key, T.hblock, 0, 0);
         k.rs = 6 * HB_KEYS;
         k.rcs = HB_KEYS;
     } else {
+        const int64_t off = T.state_off ? T.state_off[key] : (int64_t)key * T.state_stride;
         k.base = T.state + off;
         k.hs = 2;
         k.rbase = k.base + header_words(k.n);

@@ -283,6 +283,7 @@ struct sentinel_engine {
     bool flow_plain = true;          // no flow needs a limiter or namespace check
     int32_t flow_max_n = 1;
     int32_t flow_hblock = 2;        // slots per block of the flow header region (>= every flow's n)
+    int64_t flow_rest_base = 0;     // word offset of the flow table's blocked rest region
     int process_impl = 0;
     bool verdict_nt = false;   // SENTINEL_VERDICT_NT=1: non-temporal verdict stores
     bool use_lookback = true;  // SENTINEL_SCAN=3pass selects the three-kernel scan
@@ -450,6 +451,7 @@ struct sentinel_engine {
         T.occ = b.occ.as<int64_t>();
         T.has_occ = b.has_occ.as<uint8_t>();
         T.hblock = &b == &ft ? flow_hblock : 0;
+        T.rest_base = &b == &ft ? flow_rest_base : 0;
         T.ncounters = ncounters;
         T.max_occupy_ratio = cfg.max_occupy_ratio;
         return T;
@@ -1417,6 +1419,7 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
     e->h_flow_w = ww;
     e->flow_state_words = words;
     e->flow_hblock = hblock;
+    e->flow_rest_base = hwords;
     e->flow_max_n = nn.empty() ? 1 : *std::max_element(nn.begin(), nn.end());
     rc = e->rewrite_tokens(false);
     if (rc) return rc;

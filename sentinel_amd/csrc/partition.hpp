@@ -257,6 +257,7 @@ struct FlowWindow {
     int64_t ep[NMAX], ps[NMAX];
     uint32_t dirty;
     bool occ_pending;
+    uint8_t occ_raw;         // T.has_occ[key] as loaded (compared only where used: no early wait)
     // batch clock: epoch of T0 and T0 mod w, so an event's epoch is E0 + floor((r0 + dt) / w) in
     // 32-bit arithmetic (dt = ts - T0 from the packed value, |dt| < 2^23)
     int64_t E0;
@@ -272,11 +273,11 @@ struct FlowWindow {
         I_s = T.I_s[key];
         w = T.w[key];
         rcp = T.rcp_w[key];
-        occ_pending = T.has_occ[key] != 0;
+        occ_raw = T.has_occ[key];
     }
 
     __device__ inline void load_header(int64_t T0) {
-        occ_pending = occ_pending && ks.seven && kind == KIND_CLUSTER;
+        occ_pending = occ_raw != 0 && ks.seven && kind == KIND_CLUSTER;
         dirty = 0;
         if (ks.hs != 2) {
             // blocked header region with NMAX slots per block: every pair load is in bounds, so
@@ -472,7 +473,7 @@ __device__ inline bool part_run_single(FlowWindow<NMAX> &fw, const uint64_t *s_v
     int32_t a;
     bool prio;
     const int64_t E = fw.event(s_val[q0], src, T0, a, prio);
-    bool ok = !(prio && fw.kind == KIND_CLUSTER) && !(fw.occ_pending && fw.ks.seven && fw.kind == KIND_CLUSTER);
+    bool ok = !(prio && fw.kind == KIND_CLUSTER) && !(fw.occ_raw != 0 && fw.ks.seven && fw.kind == KIND_CLUSTER);
     for (uint32_t q = q0 + 1; q < q1 && ok; ++q) {
         int32_t a2;
         bool p2;
@@ -696,6 +697,11 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
 // A range of more than PH_KEYS events, or a half of more than PH_CAP, is appended to `big` and
 // decided by k_part_big, which sorts into HBM; runs longer than LONG_RUN go to k_part_long.
 constexpr int PH_THREADS = 512;
+#ifndef SENTINEL_PH_MINB
+// 4 waves per SIMD = the 2 workgroups per CU the LDS (~59 KB) admits: 128 VGPRs, a few spills.
+// Measured: 2 waves per SIMD (no spills, 1 workgroup per CU) is 16% slower.
+#define SENTINEL_PH_MINB 4
+#endif
 constexpr int PH_WAVES = PH_THREADS / WAVE;
 constexpr uint32_t PH_KEYS = 12288;                // range events scanned by a half's workgroup
 constexpr int PH_ITEMS = PH_KEYS / PH_THREADS;     // 24 keys per thread
@@ -719,7 +725,7 @@ __device__ unsigned long long g_phase[4096][5];
 #endif
 
 template <int NMAX>
-__global__ __launch_bounds__(PH_THREADS, NMAX > 10 ? 2 : 4) void k_part_half(
+__global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     KeyTable T, const uint64_t *__restrict__ pval, uint64_t *__restrict__ gsval,
     const uint32_t *__restrict__ rstart, int lb, int32_t nranges, int32_t nflows, EventSrc src, Verdicts V,
     uint32_t *__restrict__ long_runs, uint32_t *__restrict__ nlong, uint32_t *__restrict__ big,
@@ -753,26 +759,29 @@ __global__ __launch_bounds__(PH_THREADS, NMAX > 10 ? 2 : 4) void k_part_half(
     const uint32_t b0 = (uint32_t)wave * (PH_ITEMS * WAVE);
     const uint32_t hmask = (1u << hb) - 1u;
     uint64_t val[PH_ITEMS];                               // every value load in flight at once
-    uint32_t kk[PH_ITEMS];                                // local flow, or 0xFFFFFFFF: not this half's
+    // local flow of a value, or 0xFFFFFFFF: not this half's (recomputed where used: no registers)
+    auto local = [&](uint64_t v) -> uint32_t {
+        const uint32_t k = (uint32_t)(v >> VAL_KEY_SHIFT);
+        return (v != ~0ull && (k >> hb) == h) ? (k & hmask) : 0xFFFFFFFFu;
+    };
 #pragma unroll
     for (int j = 0; j < PH_ITEMS; ++j) {
         const uint32_t q = j * PH_THREADS + t;
         val[j] = q < size ? pval[pstart + q] : ~0ull;
     }
-#pragma unroll
-    for (int j = 0; j < PH_ITEMS; ++j) {
-        const uint32_t k = (uint32_t)(val[j] >> VAL_KEY_SHIFT);
-        kk[j] = (val[j] != ~0ull && (k >> hb) == h) ? (k & hmask) : 0xFFFFFFFFu;
-    }
     base[t] = 0;
     if (t == 0) { s_nlong = 0; s_cmax = 0; }
     __syncthreads();
     const uint32_t key = (p << lb) | (h << hb) | t;
-    FlowWindow<NMAX> fw;                                  // rule fields in flight during the sort
-    if (t <= hmask && key < (uint32_t)nflows) fw.load_rule(T, key);
+    // rule fields in flight during the sort: loaded unconditionally (a clamped key for lanes without a
+    // flow, never used) so no branch join makes the compiler wait for them before the count phase
+    FlowWindow<NMAX> fw;
+    fw.load_rule(T, min(key, (uint32_t)nflows - 1u));
 #pragma unroll
-    for (int j = 0; j < PH_ITEMS; ++j)
-        if (kk[j] != 0xFFFFFFFFu) atomicAdd(&base[kk[j]], 1u);
+    for (int j = 0; j < PH_ITEMS; ++j) {
+        const uint32_t kj = local(val[j]);
+        if (kj != 0xFFFFFFFFu) atomicAdd(&base[kj], 1u);
+    }
     __syncthreads();
     const uint32_t c = base[t];                           // this thread's flow: events in the half
     uint32_t total;
@@ -790,8 +799,10 @@ __global__ __launch_bounds__(PH_THREADS, NMAX > 10 ? 2 : 4) void k_part_half(
         // short runs (the common case): unordered slots by LDS atomics, then each thread
         // insertion-sorts its own run by arrival position (the low bits of the value)
 #pragma unroll
-        for (int j = 0; j < PH_ITEMS; ++j)
-            if (kk[j] != 0xFFFFFFFFu) sv[atomicAdd(&base[kk[j]], 1u)] = val[j];
+        for (int j = 0; j < PH_ITEMS; ++j) {
+            const uint32_t kj = local(val[j]);
+            if (kj != 0xFFFFFFFFu) sv[atomicAdd(&base[kj], 1u)] = val[j];
+        }
         __syncthreads();
         for (uint32_t i = start + 1; i < start + c; ++i) {
             const uint64_t v = sv[i];
@@ -811,8 +822,6 @@ __global__ __launch_bounds__(PH_THREADS, NMAX > 10 ? 2 : 4) void k_part_half(
         for (int j = 0; j < PH_ITEMS; ++j) {
             const uint32_t q = b0 + j * WAVE + lane;
             val[j] = q < size ? pval[pstart + q] : ~0ull;
-            const uint32_t k = (uint32_t)(val[j] >> VAL_KEY_SHIFT);
-            kk[j] = (val[j] != ~0ull && (k >> hb) == h) ? (k & hmask) : 0xFFFFFFFFu;
         }
         {
             uint32_t *z = reinterpret_cast<uint32_t *>(&cnt[0][0]);
@@ -822,8 +831,9 @@ __global__ __launch_bounds__(PH_THREADS, NMAX > 10 ? 2 : 4) void k_part_half(
         uint32_t rank[PH_ITEMS];
 #pragma unroll
         for (int j = 0; j < PH_ITEMS; ++j) {
-            const bool valid = kk[j] != 0xFFFFFFFFu;
-            const uint32_t d = kk[j] & hmask;
+            const uint32_t kj = local(val[j]);
+            const bool valid = kj != 0xFFFFFFFFu;
+            const uint32_t d = kj & hmask;
             const uint64_t peers = match_peers<PART_MAX_BITS>(d, valid, hb);
             uint32_t r = 0;
             if (valid) r = cnt[wave][d] + mask_rank(peers);
@@ -843,8 +853,9 @@ __global__ __launch_bounds__(PH_THREADS, NMAX > 10 ? 2 : 4) void k_part_half(
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < PH_ITEMS; ++j) {
-            if (kk[j] == 0xFFFFFFFFu) continue;
-            sv[base[kk[j]] + cnt[wave][kk[j]] + rank[j]] = val[j];
+            const uint32_t kj = local(val[j]);
+            if (kj == 0xFFFFFFFFu) continue;
+            sv[base[kj] + cnt[wave][kj] + rank[j]] = val[j];
         }
     }
     __syncthreads();
