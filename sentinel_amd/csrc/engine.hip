@@ -871,7 +871,7 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
     unsigned long long *stat = e->d_part_stat.as<unsigned long long>();
     uint32_t *ctl = e->w_runs.as<uint32_t>();
     e->launch("part_prep", n, s, [&] {
-        k_part_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
+        k_part_prep<<<dim3((unsigned)nb), dim3(PP_THREADS), 0, s>>>(
             n, ev, F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, e->flow_plain ? nullptr : fkey,
             finvalid, lb, hist, nb, nparts,
             ctl, stat);
