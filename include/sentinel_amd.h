@@ -367,6 +367,10 @@ int  sentinel_profile_enable(sentinel_engine_t *eng, int enable);
 /* Time only the named kernel (NULL or "": every kernel): two events per launch of it instead of two
  * per launch of every kernel, so a timed run keeps its dominant kernel's live duration cheaply. */
 int  sentinel_profile_select(sentinel_engine_t *eng, const char *kernel);
+/* Flow pipeline of the following batches: 0 auto (partition-local for >= 32768 flows, radix sort
+ * after a skewed batch), 1 the global radix sort, 2 the partition-local path (where it applies:
+ * no namespace limiter, <= 16 buckets).  Verdicts are identical on every path. */
+int  sentinel_set_flow_path(sentinel_engine_t *eng, int path);
 /* Gate the timing of following launches on (1) or off (0) without collecting or clearing what was
  * timed so far (no host synchronisation: callable between the batches of a timed loop). */
 int  sentinel_profile_gate(sentinel_engine_t *eng, int on);

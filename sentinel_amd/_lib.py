@@ -49,7 +49,7 @@ EXPORTS = [
     "sentinel_submit_concurrent_batch_host", "sentinel_concurrent_now_calls", "sentinel_concurrent_token_count",
     "sentinel_concurrent_expire",
     "sentinel_load_local_resources", "sentinel_submit_local_entry_batch", "sentinel_submit_local_entry_batch_host",
-    "sentinel_local_node_stats", "sentinel_set_occupy_timeout", "sentinel_profile_select", "sentinel_profile_gate",
+    "sentinel_local_node_stats", "sentinel_set_occupy_timeout", "sentinel_profile_select", "sentinel_profile_gate", "sentinel_set_flow_path",
 ]
 
 STATUS_RELEASE_OK = 6
@@ -179,6 +179,7 @@ def load():
         "sentinel_set_occupy_timeout": (C.c_int, [vp, i32]),
         "sentinel_profile_select": (C.c_int, [vp, C.c_char_p]),
         "sentinel_profile_gate": (C.c_int, [vp, C.c_int]),
+        "sentinel_set_flow_path": (C.c_int, [vp, C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

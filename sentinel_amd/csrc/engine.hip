@@ -1244,6 +1244,13 @@ int sentinel_profile_enable(sentinel_engine_t *e, int enable) {
     return 0;
 }
 
+int sentinel_set_flow_path(sentinel_engine_t *e, int path) {
+    if (!e || path < 0 || path > 2) return fail(SENTINEL_E_INVALID, "bad flow path");
+    std::lock_guard<std::mutex> g(e->mu);
+    e->flow_path = path;
+    return 0;
+}
+
 int sentinel_profile_gate(sentinel_engine_t *e, int on) {
     if (!e) return fail(SENTINEL_E_INVALID, "null engine");
     std::lock_guard<std::mutex> g(e->mu);

@@ -337,6 +337,12 @@ class GpuTokenService:
         check(rc, "submit_flow_batch")
         return verdicts
 
+    def set_flow_path(self, path: str):
+        """Flow pipeline of the following batches: "auto", "sorted" (global radix sort) or
+        "partition" (partition-local); verdicts are identical on every path."""
+        check(self._L.sentinel_set_flow_path(self._h, {"auto": 0, "sorted": 1, "partition": 2}[path]),
+              "sentinel_set_flow_path")
+
     def submit_flow_batch_host(self, flow_idx, acquire, ts, flags=None):
         """Host arrays in, (status, remaining, wait_in_ms) numpy arrays out (synchronous)."""
         ev = self.pack_events(flow_idx, acquire, ts)

@@ -374,3 +374,53 @@ def test_stream_host_pipelined_bitexact(oracle_mod):
     st_o, rem_o, w_o = _oracle(oracle_mod, rules).replay(ev.flow_idx, ev.acquire, ev.ts, flags)
     assert np.array_equal(st_g, st_o) and np.array_equal(rem_g, rem_o) and np.array_equal(w_g, w_o)
     assert len(ms) == 7 and (ms > 0).all()
+
+
+def _norm_dump(d, n):
+    """Window dump with absent slots and present all-zero slots made equal (a snapshot's roll of a
+    stale slot leaves it present and empty; the next event's own roll would produce the same)."""
+    d = np.array(d, dtype=np.int64).reshape(-1)
+    w = d[: n * 8].reshape(n, 8).copy()
+    w[(w[:, 1:] == 0).all(axis=1), 0] = -1
+    return w, d[n * 8:]
+
+
+def test_path_switches_snapshots_and_epoch_gaps(oracle_mod):
+    """One engine, one flow table written by both pipelines in turn (sentinel_set_flow_path) and by
+    snapshots (which roll windows) between batches; batches advance by 0, 1, 2..n-1 and >= n epochs,
+    some with heterogeneous acquire counts (the general walk).  Every verdict must equal the
+    oracle's, and the final windows too (absent == present-and-empty)."""
+    rng = np.random.default_rng(41)
+    F = 3000
+    rules = T.make_rules(F, rng, count_lo=5, count_hi=60)
+    ns = np.array([2, 4, 10])[np.arange(F) % 3].astype(np.int32)
+    rules.sample_count[:] = ns
+    rules.window_interval_ms[:] = ns * 100                   # w = 100 ms for every flow
+    svc, orc = _engine(rules), _oracle(oracle_mod, rules)
+    t = T.T0_ALIGNED + 37
+    # (epochs advanced before the batch, pipeline, snapshot before the batch)
+    plan = [(0, "partition", False), (0, "partition", False), (1, "partition", False), (1, "sorted", False),
+            (0, "partition", False), (1, "partition", True), (0, "partition", False), (2, "partition", False),
+            (3, "partition", False), (12, "partition", False), (1, "partition", False), (0, "sorted", False),
+            (1, "partition", False), (1, "partition", True), (0, "partition", False), (25, "partition", False)]
+    for b, (adv, path, snap) in enumerate(plan):
+        t += adv * 100
+        if snap:
+            svc.snapshot(t)
+        svc.set_flow_path(path)
+        m = 20_000
+        idx = rng.integers(0, F, size=m).astype(np.int32)
+        ts = np.sort(t + rng.integers(0, 40, size=m)).astype(np.int64)   # mostly one epoch per flow
+        acq = np.ones(m, np.int32)
+        if b in (4, 12):
+            acq = rng.integers(1, 3, size=m).astype(np.int32)   # heterogeneous runs: the general walk
+        st_g, rem_g, w_g = svc.submit_flow_batch_host(idx, acq, ts)
+        st_o, rem_o, w_o = orc.replay(idx, acq, ts)
+        bad = np.nonzero((st_g != st_o) | (rem_g != rem_o) | (w_g != w_o))[0]
+        assert len(bad) == 0, (b, path, len(bad), bad[:5], st_g[bad[:5]], st_o[bad[:5]], rem_g[bad[:5]], rem_o[bad[:5]])
+        t = int(ts[-1])
+    for f in range(0, F, 11):
+        n = int(ns[f])
+        g, go = _norm_dump(svc.dump_flow(f, n), n)
+        o, oo = _norm_dump(orc.dump_flow(f), n)
+        assert np.array_equal(g, o) and np.array_equal(go, oo), (f, g, o)
