@@ -852,7 +852,7 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
     const int lb = std::max(0, fbits - PART_MAX_BITS);
     const int32_t nparts = (int32_t)(((int64_t)F + (1 << lb) - 1) >> lb);
     const int pbits = bits_for(nparts - 1 > 0 ? nparts - 1 : 1);
-    const int64_t nb = sort_blocks(n);
+    const int64_t nb = part_blocks(n);
     uint32_t *fkey = e->w_fkey.as<uint32_t>();
     uint32_t *hist = e->w_fhist.as<uint32_t>();             // tile-major range histograms -> offsets
     const int64_t ng = (nb + PS_GROUP - 1) / PS_GROUP;
@@ -884,7 +884,7 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
     });
     const EventSrc src{ev, nullptr, fl, false};
     e->launch("part_scatter", n, s, [&] {
-        k_part_scatter<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(e->flow_plain ? nullptr : fkey, src,
+        k_part_scatter<<<dim3((unsigned)nb), dim3(PT_THREADS), 0, s>>>(e->flow_plain ? nullptr : fkey, src,
                                                                          e->w_sval.as<uint64_t>(), n, finvalid, lb,
                                                                          pbits, hist, nb, nparts, F);
     });

@@ -29,12 +29,26 @@ namespace sentinel {
 constexpr int PART_MAX_BITS = 10;                  // <= 1024 ranges, <= 1024 flows per range
 constexpr int PART_BINS = 1 << PART_MAX_BITS;
 
+// Partition tile (k_part_prep histogram rows and k_part_scatter blocks): PT_TILE events.
+#ifndef SENTINEL_PT_THREADS
+#define SENTINEL_PT_THREADS 512
+#endif
+#ifndef SENTINEL_PT_ITEMS
+#define SENTINEL_PT_ITEMS 8
+#endif
+constexpr int PT_THREADS = SENTINEL_PT_THREADS;
+constexpr int PT_WAVES = PT_THREADS / WAVE;
+constexpr int PT_ITEMS = SENTINEL_PT_ITEMS;
+constexpr int PT_TILE = PT_THREADS * PT_ITEMS;
+static_assert(PT_THREADS >= 256 && PT_THREADS <= PART_BINS && PT_TILE <= 65535, "partition tile");
+inline int64_t part_blocks(int64_t n) { return (n + PT_TILE - 1) / PT_TILE; }
+
 // Validation + routing as k_flow_prep; histogram of the range digit of valid events only.
 #ifndef SENTINEL_PREP_THREADS
 #define SENTINEL_PREP_THREADS 1024    // 4 events per thread: measured 38 us vs 40 (512) and 47 (256)
 #endif
 constexpr int PP_THREADS = SENTINEL_PREP_THREADS;
-constexpr int PP_ITEMS = SORT_TILE / PP_THREADS;
+constexpr int PP_ITEMS = PT_TILE / PP_THREADS;
 __global__ __launch_bounds__(PP_THREADS) void k_part_prep(int64_t n, const Event *__restrict__ ev, int32_t nflows,
                                                             const int32_t *__restrict__ route,
                                                             uint64_t *__restrict__ out, uint32_t *__restrict__ fkey,
@@ -47,7 +61,7 @@ __global__ __launch_bounds__(PP_THREADS) void k_part_prep(int64_t n, const Event
         if (stat_zero) *stat_zero = 0;
     }
     __shared__ uint32_t h[PART_BINS];
-    const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
+    const int64_t tile0 = (int64_t)blockIdx.x * PT_TILE;
     Event evs[PP_ITEMS];                            // every event load of the tile in flight at once
 #pragma unroll
     for (int j = 0; j < PP_ITEMS; ++j) {
@@ -104,12 +118,12 @@ __global__ __launch_bounds__(PART_BINS) void k_part_ranges(uint32_t *__restrict_
     const int d = threadIdx.x;
     uint32_t run = 0;
     if (d < P) {
-        for (int64_t g0 = 0; g0 < ng; g0 += 16) {          // 16 loads in flight, then the stores
-            uint32_t x[16];
+        for (int64_t g0 = 0; g0 < ng; g0 += 32) {          // 32 loads in flight (two round trips for
+            uint32_t x[32];                                 // an 8M-event batch), then the stores
 #pragma unroll
-            for (int k = 0; k < 16; ++k) x[k] = g0 + k < ng ? gsum[(g0 + k) * P + d] : 0u;
+            for (int k = 0; k < 32; ++k) x[k] = g0 + k < ng ? gsum[(g0 + k) * P + d] : 0u;
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
+            for (int k = 0; k < 32; ++k) {
                 if (g0 + k < ng) gsum[(g0 + k) * P + d] = run;
                 run += x[k];
             }
@@ -144,46 +158,46 @@ __global__ __launch_bounds__(PS_THREADS) void k_part_offsets(uint32_t *__restric
 // in LDS in digit order and written out as contiguous per-range runs.  keys_in == null (no
 // namespace routes, the common case): the flow key and validity are re-derived from the event the
 // value is packed from anyway, so k_part_prep writes no key array and nothing reads one.
-__global__ __launch_bounds__(SORT_THREADS) void k_part_scatter(const uint32_t *__restrict__ keys_in, EventSrc src,
+__global__ __launch_bounds__(PT_THREADS) void k_part_scatter(const uint32_t *__restrict__ keys_in, EventSrc src,
                                                                uint64_t *__restrict__ vals_out, int64_t n,
                                                                uint32_t finvalid, int lb, int pbits,
                                                                const uint32_t *__restrict__ offsets, int64_t nblocks,
                                                                int32_t nparts, int32_t nflows) {
-    __shared__ uint16_t cnt[SORT_WAVES][PART_BINS];
+    __shared__ uint16_t cnt[PT_WAVES][PART_BINS];
     __shared__ uint32_t goff[PART_BINS];
     __shared__ uint32_t loff[PART_BINS];
-    __shared__ uint32_t waves_tot[SORT_WAVES];
-    __shared__ uint16_t sdig[SORT_TILE];
-    __shared__ uint64_t svals[SORT_TILE];
+    __shared__ uint32_t waves_tot[PT_WAVES];
+    __shared__ uint16_t sdig[PT_TILE];
+    __shared__ uint64_t svals[PT_TILE];
     const int wave = threadIdx.x / WAVE;
     const uint32_t lane = lane_id();
-    for (int d = threadIdx.x; d < PART_BINS; d += SORT_THREADS) {
+    for (int d = threadIdx.x; d < PART_BINS; d += PT_THREADS) {
 #pragma unroll
-        for (int w = 0; w < SORT_WAVES; ++w) cnt[w][d] = 0;
+        for (int w = 0; w < PT_WAVES; ++w) cnt[w][d] = 0;
         goff[d] = d < nparts ? offsets[(int64_t)blockIdx.x * nparts + d] : 0u;   // tile-major row
     }
     __syncthreads();
-    const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
-    const int64_t base = tile0 + (int64_t)wave * (SORT_ITEMS * WAVE);
+    const int64_t tile0 = (int64_t)blockIdx.x * PT_TILE;
+    const int64_t base = tile0 + (int64_t)wave * (PT_ITEMS * WAVE);
     const int64_t T0 = src.t0();
-    uint32_t key[SORT_ITEMS], rank[SORT_ITEMS];
-    uint64_t pk[SORT_ITEMS];                       // packed values (keys_in == null: from the events loaded here)
+    uint32_t key[PT_ITEMS], rank[PT_ITEMS];
+    uint64_t pk[PT_ITEMS];                       // packed values (keys_in == null: from the events loaded here)
     if (keys_in) {
 #pragma unroll
-        for (int j = 0; j < SORT_ITEMS; ++j) {
+        for (int j = 0; j < PT_ITEMS; ++j) {
             const int64_t i = base + j * WAVE + lane;
             key[j] = i < n ? keys_in[i] : finvalid;
         }
     } else {
-        Event evs[SORT_ITEMS];
-        uint8_t fls[SORT_ITEMS];
+        Event evs[PT_ITEMS];
+        uint8_t fls[PT_ITEMS];
 #pragma unroll
-        for (int j = 0; j < SORT_ITEMS; ++j) {
+        for (int j = 0; j < PT_ITEMS; ++j) {
             const int64_t i = base + j * WAVE + lane;
             if (i < n) { evs[j] = src.ev[i]; fls[j] = src.flags ? src.flags[i] : 0; }
         }
 #pragma unroll
-        for (int j = 0; j < SORT_ITEMS; ++j) {
+        for (int j = 0; j < PT_ITEMS; ++j) {
             const int64_t i = base + j * WAVE + lane;
             const Event e = evs[j];
             // k_part_prep's validation without the route check (keys_in is only null without routes)
@@ -194,7 +208,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_part_scatter(const uint32_t *_
         }
     }
 #pragma unroll
-    for (int j = 0; j < SORT_ITEMS; ++j) {
+    for (int j = 0; j < PT_ITEMS; ++j) {
         const bool valid = key[j] != finvalid;
         const uint32_t d = valid ? key[j] >> lb : 0u;
         const uint64_t peers = match_peers<PART_MAX_BITS>(d, valid, pbits);
@@ -207,7 +221,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_part_scatter(const uint32_t *_
     }
     __syncthreads();
     // per digit: exclusive over waves (in place), then an exclusive scan over digits -> loff
-    constexpr int DPT = PART_BINS / SORT_THREADS;   // digits per thread
+    constexpr int DPT = PART_BINS / PT_THREADS;   // digits per thread
     uint32_t dtot[DPT > 0 ? DPT : 1];
     uint32_t mine = 0;
 #pragma unroll
@@ -215,7 +229,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_part_scatter(const uint32_t *_
         const int d = threadIdx.x * DPT + q;
         uint32_t run = 0;
 #pragma unroll
-        for (int w = 0; w < SORT_WAVES; ++w) {
+        for (int w = 0; w < PT_WAVES; ++w) {
             const uint32_t c = cnt[w][d];
             cnt[w][d] = (uint16_t)run;
             run += c;
@@ -232,7 +246,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_part_scatter(const uint32_t *_
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < SORT_ITEMS; ++j) {
+    for (int j = 0; j < PT_ITEMS; ++j) {
         if (rank[j] == 0xFFFFFFFFu) continue;
         const uint32_t d = key[j] >> lb;
         const uint32_t p = loff[d] + cnt[wave][d] + rank[j];
@@ -241,7 +255,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_part_scatter(const uint32_t *_
                    ((uint64_t)(key[j] & ((1u << lb) - 1)) << VAL_KEY_SHIFT);
     }
     __syncthreads();
-    for (uint32_t p = threadIdx.x; p < total; p += SORT_THREADS) {
+    for (uint32_t p = threadIdx.x; p < total; p += PT_THREADS) {
         const uint32_t d = sdig[p];
         const uint32_t dst = goff[d] + p - loff[d];
         if (dst >= (uint64_t)n) continue;          // guard: a corrupt offset must never write out of bounds
