@@ -826,7 +826,10 @@ static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTa
     const uint64_t *pval = e->w_sval.as<uint64_t>();
     uint64_t *gsval = e->w_vtmp.as<uint64_t>();
     // a batch whose mean range does not fit goes straight to the HBM-sorting kernel
-    const bool all_big = n > (int64_t)nparts * (int64_t)(PH_KEYS * 3 / 4);
+#ifndef SENTINEL_ALLBIG_PCT
+#define SENTINEL_ALLBIG_PCT 90
+#endif
+    const bool all_big = n > (int64_t)nparts * (int64_t)(PH_KEYS * SENTINEL_ALLBIG_PCT / 100);
     if (!all_big) {
         e->launch("part_fused", n, s, [&] {
             k_part_half<NMAX><<<16u * (unsigned)((nparts + 7) / 8), PH_THREADS, 0, s>>>(

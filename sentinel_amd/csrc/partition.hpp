@@ -722,9 +722,19 @@ constexpr int PH_THREADS = 512;
 #define SENTINEL_PH_MINB 4
 #endif
 constexpr int PH_WAVES = PH_THREADS / WAVE;
-constexpr uint32_t PH_KEYS = 12288;                // range events scanned by a half's workgroup
-constexpr int PH_ITEMS = PH_KEYS / PH_THREADS;     // 24 keys per thread
-constexpr uint32_t PH_CAP = 6144;                  // events of one half sorted in LDS (48 KB)
+// A half's workgroup scans up to PH_KEYS range events (20 per thread) and sorts up to PH_CAP of
+// them in LDS; batches whose mean range exceeds 90% of PH_KEYS go to k_part_big whole (engine.hip).
+// Measured on config 3 (mean range 8590): 10240 / 5120 is 2.5% faster than 12288 / 6144 (fewer
+// value registers, fewer spills); 3 workgroups per CU (80 VGPRs) is 45% slower.
+#ifndef SENTINEL_PH_KEYS
+#define SENTINEL_PH_KEYS 10240
+#endif
+#ifndef SENTINEL_PH_CAP
+#define SENTINEL_PH_CAP 5120
+#endif
+constexpr uint32_t PH_KEYS = SENTINEL_PH_KEYS;     // range events scanned by a half's workgroup
+constexpr int PH_ITEMS = PH_KEYS / PH_THREADS;     // 20 keys per thread
+constexpr uint32_t PH_CAP = SENTINEL_PH_CAP;       // events of one half sorted in LDS (40 KB)
 constexpr int PH_BINS = PART_BINS / 2;             // flows per half
 constexpr int PH_MAX_LONG = PH_CAP / (LONG_RUN + 1) + 1;
 constexpr uint32_t PH_SMALL_RUN = 32;              // longest run sorted by its own thread
