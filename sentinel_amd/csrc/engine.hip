@@ -859,10 +859,11 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
     uint32_t *fkey = e->w_fkey.as<uint32_t>();
     uint32_t *hist = e->w_fhist.as<uint32_t>();             // tile-major range histograms -> offsets
     const int64_t ng = (nb + PS_GROUP - 1) / PS_GROUP;
-    int rc = e->w_pscan.ensure(((size_t)ng * nparts + nparts + 1) * 4);
+    int rc = e->w_pscan.ensure(((size_t)ng * nparts + 2 * (size_t)nparts + 1) * 4);
     if (rc) return rc;
     uint32_t *gsum = e->w_pscan.as<uint32_t>();
     uint32_t *rstart = gsum + (size_t)ng * nparts;
+    uint32_t *rtot = rstart + nparts + 1;
     rc = e->w_runs.ensure((2 + 2 * (size_t)nparts + 3 * ((size_t)n / LONG_RUN + 2)) * 4);
     if (rc) return rc;
     if (!e->d_part_stat.p) {
@@ -882,8 +883,9 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
     e->launch("scan", n, s, [&] {
         const dim3 g2((unsigned)ng, (unsigned)((nparts + PS_THREADS - 1) / PS_THREADS));
         k_part_colsum<<<g2, PS_THREADS, 0, s>>>(hist, nb, nparts, gsum);
-        k_part_ranges<<<1, PART_BINS, 0, s>>>(gsum, ng, nparts, rstart);
-        k_part_offsets<<<g2, PS_THREADS, 0, s>>>(hist, nb, nparts, gsum, rstart);
+        k_part_colscan<<<(unsigned)((nparts + PC_THREADS / WAVE - 1) / (PC_THREADS / WAVE)), PC_THREADS, 0, s>>>(
+            gsum, ng, nparts, rtot);
+        k_part_offsets<<<g2, PS_THREADS, 0, s>>>(hist, nb, nparts, gsum, rtot, rstart);
     });
     const EventSrc src{ev, nullptr, fl, false};
     e->launch("part_scatter", n, s, [&] {

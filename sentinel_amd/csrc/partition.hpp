@@ -110,39 +110,57 @@ __global__ __launch_bounds__(PS_THREADS) void k_part_colsum(const uint32_t *__re
     gsum[g * P + d] = s;
 }
 
-// One workgroup of PART_BINS threads: per range, exclusive scan of its group sums (in place); then
-// the exclusive scan of the range totals -> rstart[0..P] (rstart[P] = valid events).
-__global__ __launch_bounds__(PART_BINS) void k_part_ranges(uint32_t *__restrict__ gsum, int64_t ng, int32_t P,
-                                                           uint32_t *__restrict__ rstart) {
-    __shared__ uint32_t waves_tot[PART_BINS / WAVE];
-    const int d = threadIdx.x;
-    uint32_t run = 0;
-    if (d < P) {
-        for (int64_t g0 = 0; g0 < ng; g0 += 32) {          // 32 loads in flight (two round trips for
-            uint32_t x[32];                                 // an 8M-event batch), then the stores
-#pragma unroll
-            for (int k = 0; k < 32; ++k) x[k] = g0 + k < ng ? gsum[(g0 + k) * P + d] : 0u;
-#pragma unroll
-            for (int k = 0; k < 32; ++k) {
-                if (g0 + k < ng) gsum[(g0 + k) * P + d] = run;
-                run += x[k];
-            }
-        }
+// One wave per range: exclusive scan of the range's group sums (in place, 64 groups per step, one
+// load per lane) and the range total -> tot[d].  Every CU takes a few ranges (the previous single
+// 1024-thread workgroup left 255 CUs idle for 8 us).
+constexpr int PC_THREADS = 256;
+__global__ __launch_bounds__(PC_THREADS) void k_part_colscan(uint32_t *__restrict__ gsum, int64_t ng, int32_t P,
+                                                             uint32_t *__restrict__ tot) {
+    const int d = blockIdx.x * (PC_THREADS / WAVE) + threadIdx.x / WAVE;
+    if (d >= P) return;                                   // wave-uniform
+    const uint32_t lane = lane_id();
+    uint32_t carry = 0;
+    for (int64_t g0 = 0; g0 < ng; g0 += WAVE) {
+        const int64_t g = g0 + lane;
+        const uint32_t x = g < ng ? gsum[g * P + d] : 0u;
+        const uint32_t inc = wave_inclusive_scan(x);
+        if (g < ng) gsum[g * P + d] = carry + inc - x;
+        carry += __shfl(inc, WAVE - 1, WAVE);
     }
-    uint32_t total;
-    const uint32_t st = block_exclusive_scan(run, waves_tot, &total);
-    if (d < P) rstart[d] = st;
-    if (d == 0) rstart[P] = total;
+    if (lane == 0) tot[d] = carry;
+}
+
+// Range starts: rstart[d] = sum of tot[d'] for d' < d, rstart[P] = valid events.  Computed by every
+// k_part_offsets workgroup for its own 256 ranges (the totals are 4 KB, read from L2).
+__device__ inline uint32_t part_range_start(const uint32_t *__restrict__ tot, int32_t P, int d0, int d,
+                                            uint32_t *lds_waves, uint32_t *grand) {
+    uint32_t before = 0;                                  // this lane's share of tot[0, d0)
+    for (int k = threadIdx.x; k < d0; k += PS_THREADS) before += tot[k];
+    uint32_t b_total;
+    (void)block_exclusive_scan(before, lds_waves, &b_total);
+    uint32_t chunk_total;
+    const uint32_t ex = block_exclusive_scan(d < P ? tot[d] : 0u, lds_waves, &chunk_total);
+    *grand = b_total + chunk_total;
+    return b_total + ex;
 }
 
 __global__ __launch_bounds__(PS_THREADS) void k_part_offsets(uint32_t *__restrict__ hist, int64_t nb, int32_t P,
                                                              const uint32_t *__restrict__ gsum,
-                                                             const uint32_t *__restrict__ rstart) {
+                                                             const uint32_t *__restrict__ tot,
+                                                             uint32_t *__restrict__ rstart) {
+    __shared__ uint32_t waves_tot[PS_THREADS / WAVE];
     const int64_t g = blockIdx.x;
-    const int d = blockIdx.y * PS_THREADS + threadIdx.x;
+    const int d0 = blockIdx.y * PS_THREADS;
+    const int d = d0 + threadIdx.x;
+    uint32_t grand;
+    const uint32_t rs = part_range_start(tot, P, d0, d, waves_tot, &grand);
     if (d >= P) return;
+    if (g == 0) {
+        rstart[d] = rs;
+        if (d == P - 1) rstart[P] = grand;
+    }
     const int64_t b0 = g * PS_GROUP, b1 = min(b0 + PS_GROUP, nb);
-    uint32_t run = rstart[d] + gsum[g * P + d];
+    uint32_t run = rs + gsum[g * P + d];
     uint32_t x[PS_GROUP];                                 // the group's column in flight at once
 #pragma unroll
     for (int k = 0; k < PS_GROUP; ++k) x[k] = b0 + k < b1 ? hist[(b0 + k) * P + d] : 0u;
