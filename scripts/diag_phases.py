@@ -13,7 +13,7 @@ import sentinel_amd as sa  # noqa: E402
 from sentinel_amd import trace as T  # noqa: E402
 from sentinel_amd.token_service import device_events  # noqa: E402
 
-F, N = 1_000_000, 8 * 1024 * 1024
+F, N = int(os.environ.get("DIAG_FLOWS", "1000000")), 8 * 1024 * 1024   # 977 ranges for 125k..1M flows
 rng = np.random.default_rng(3)
 rules = T.make_rules(F, rng, sample_count=10, window_interval_ms=1000)
 svc = sa.GpuTokenService(0)

@@ -832,9 +832,15 @@ static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTa
     const bool all_big = n > (int64_t)nparts * (int64_t)(PH_KEYS * SENTINEL_ALLBIG_PCT / 100);
     if (!all_big) {
         e->launch("part_fused", n, s, [&] {
-            k_part_half<NMAX><<<16u * (unsigned)((nparts + 7) / 8), PH_THREADS, 0, s>>>(
-                FT, pval, gsval, rstart, lb, nparts, (int32_t)e->rules.size(), src, V, long_runs, nlong, big,
-                nbig, stat);
+            const dim3 g(16u * (unsigned)((nparts + 7) / 8));
+            if (part_coop(lb))      // <= 256 flows per half: cooperative verdict sweep
+                k_part_half<NMAX, true><<<g, PH_THREADS, 0, s>>>(FT, pval, gsval, rstart, lb, nparts,
+                                                                 (int32_t)e->rules.size(), src, V, long_runs,
+                                                                 nlong, big, nbig, stat);
+            else
+                k_part_half<NMAX, false><<<g, PH_THREADS, 0, s>>>(FT, pval, gsval, rstart, lb, nparts,
+                                                                  (int32_t)e->rules.size(), src, V, long_runs,
+                                                                  nlong, big, nbig, stat);
         });
     }
     e->launch("part_big", n, s, [&] {

@@ -284,6 +284,15 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(const uint32_t *__r
 // A flow's window header {epoch, PASS} x n held in VGPRs while its events are decided in arrival
 // order (the k_process_reg scheme): closed-form homogeneous segments, the reference state machine
 // (seq_event on global memory) for everything else, only dirty pairs written back.
+// Verdict of the k-th event of a closed-form segment (ClusterFlowChecker.java:72-82): the first K
+// pass with remaining = (int)((G - (S0 + k*a) / I_s) - a), the rest are BLOCKED.  `small`: every
+// S0 + k*a of the segment fits in int32, so the int64 -> double conversion is one v_cvt_f64_i32.
+__device__ inline uint64_t run_verdict(double thr, double I_s, int64_t s0, int32_t a, uint32_t K, uint32_t k, bool small) {
+    if (k >= K) return pack_verdict(ST_BLOCKED, 0, 0);
+    const double x = small ? (double)((int32_t)s0 + (int32_t)k * a) : (double)wrap_add(s0, wrap_mul((int64_t)k, a));
+    return pack_verdict(ST_OK, java_d2i((thr - div_interval(x, I_s)) - (double)a), 0);
+}
+
 template <int NMAX>
 struct FlowWindow {
     KeyState ks;
@@ -442,9 +451,7 @@ struct FlowWindow {
     // `small`: every S0 + k*a of the segment fits in int32, so the int64 -> double conversion is one
     // v_cvt_f64_i32 (same value)
     __device__ inline uint64_t verdict(int64_t s0, int32_t a, uint32_t K, uint32_t k, bool small) const {
-        if (k >= K) return pack_verdict(ST_BLOCKED, 0, 0);
-        const double x = small ? (double)((int32_t)s0 + (int32_t)k * a) : (double)wrap_add(s0, wrap_mul((int64_t)k, a));
-        return pack_verdict(ST_OK, java_d2i((thr - div_interval(x, I_s)) - (double)a), 0);
+        return run_verdict(thr, I_s, s0, a, K, k, small);
     }
 };
 
@@ -500,9 +507,12 @@ __device__ inline void part_run_w(FlowWindow<NMAX> &fw, const KeyTable &T, uint3
 // slot's pair, "a slot is newer than E"}.  The rolled slot's rest line does not depend on the header,
 // so its load is issued together with the header loads: one memory round trip instead of two.
 // Returns false, having written nothing, when the run needs the general walk (part_run_w).
-template <int NMAX>
+// DEFER: the verdicts are not written here; the segment's {s0, K, a, small} come back to the caller
+// (k_part_half's cooperative verdict sweep writes them with every lane of the workgroup).
+template <int NMAX, bool DEFER = false>
 __device__ inline bool part_run_single(FlowWindow<NMAX> &fw, const uint64_t *s_val, uint32_t q0, uint32_t q1,
-                                       const EventSrc &src, const Verdicts &V, int64_t T0) {
+                                       const EventSrc &src, const Verdicts &V, int64_t T0, int64_t *d_s0 = nullptr,
+                                       uint32_t *d_K = nullptr, int32_t *d_a = nullptr, bool *d_small = nullptr) {
     if (fw.ks.hs == 2) return false;
     fw.E0 = epoch_of(T0, fw.w, fw.rcp);
     fw.r0 = (int32_t)(T0 - fw.E0 * (int64_t)fw.w);
@@ -562,6 +572,13 @@ __device__ inline bool part_run_single(FlowWindow<NMAX> &fw, const uint64_t *s_v
     *reinterpret_cast<longlong2 *>(fw.ks.pair(slot)) = longlong2{E, wrap_add(base, wrap_mul((int64_t)K, a))};
     if (seven) fw.ks.book_rest(slot, fresh, blk, preq, breq, nb, a, K);
     const bool small = s0 >= 0 && s0 + (int64_t)len * a < (int64_t)INT32_MAX;
+    if (DEFER) {
+        *d_s0 = s0;
+        *d_K = K;
+        *d_a = a;
+        *d_small = small;
+        return true;
+    }
 #if defined(SENTINEL_DIAG_NOVERDICT)     // cost diagnostic only (no output)
     uint64_t acc = 0;
     for (uint32_t k = 0; k < len; ++k) acc ^= fw.verdict(s0, a, K, k, small) ^ s_val[q0 + k];
@@ -573,6 +590,57 @@ __device__ inline bool part_run_single(FlowWindow<NMAX> &fw, const uint64_t *s_v
         V.out[(uint32_t)s_val[q0 + k] & SEQ_MASK] = fw.verdict(s0, a, K, k, small);
 #endif
     return true;
+}
+
+// cooperative verdict record flags (k_part_half<NMAX, true>): K in the low bits
+constexpr uint32_t COOP_SKIP = 1u << 31, COOP_SMALL = 1u << 30;
+
+// part_run_w for the cooperative sweep: the run's first two segments, when decided in closed form,
+// are returned as records {s0, K | small, a} instead of written (the workgroup writes them from
+// LDS); sequential segments and any third segment write their verdicts here.  len1 / len12 = end of
+// the first / second segment relative to q0.
+template <int NMAX>
+__device__ inline void part_run_defer(FlowWindow<NMAX> &fw, const KeyTable &T, uint32_t key, const uint64_t *s_val,
+                                      uint32_t q0, uint32_t q1, const EventSrc &src, const Verdicts &V, int64_t T0,
+                                      int64_t *s0o, uint32_t *reco, int32_t *ao, uint32_t &len1, uint32_t &len12) {
+    reco[0] = reco[1] = COOP_SKIP;
+    len1 = len12 = 0;
+    uint32_t q = q0;
+    int si = 0;
+    while (q < q1) {
+        int32_t a;
+        bool prio;
+        const int64_t E = fw.event(s_val[q], src, T0, a, prio);
+        bool het = prio && fw.kind == KIND_CLUSTER;
+        uint32_t q2 = q + 1;
+        for (; q2 < q1; ++q2) {
+            int32_t a2;
+            bool p2;
+            if (fw.event(s_val[q2], src, T0, a2, p2) != E) break;
+            het |= a2 != a || (p2 && fw.kind == KIND_CLUSTER);
+        }
+        if (fw.slow(E, het)) {
+            fw.sequential(T, key, E, s_val, q, q2, src, V);
+        } else {
+            int64_t s0;
+            uint32_t K;
+            const uint32_t len = q2 - q;
+            fw.fast(E, a, len, s0, K);
+            const bool small = s0 >= 0 && s0 + (int64_t)len * a < (int64_t)INT32_MAX;
+            if (si < 2) {
+                s0o[si] = s0;
+                reco[si] = K | (small ? COOP_SMALL : 0u);
+                ao[si] = a;
+            } else {
+                for (uint32_t k = 0; k < len; ++k) V.out[(uint32_t)s_val[q + k] & SEQ_MASK] = fw.verdict(s0, a, K, k, small);
+            }
+        }
+        if (si == 0) len1 = q2 - q0;
+        if (si <= 1) len12 = q2 - q0;
+        ++si;
+        q = q2;
+    }
+    fw.flush();
 }
 
 template <int NMAX>
@@ -755,7 +823,26 @@ constexpr int PH_ITEMS = PH_KEYS / PH_THREADS;     // 20 keys per thread
 constexpr uint32_t PH_CAP = SENTINEL_PH_CAP;       // events of one half sorted in LDS (40 KB)
 constexpr int PH_BINS = PART_BINS / 2;             // flows per half
 constexpr int PH_MAX_LONG = PH_CAP / (LONG_RUN + 1) + 1;
-constexpr uint32_t PH_SMALL_RUN = 32;              // longest run sorted by its own thread
+#ifndef SENTINEL_PH_SMALL_RUN
+#define SENTINEL_PH_SMALL_RUN 64
+#endif
+constexpr uint32_t PH_SMALL_RUN = SENTINEL_PH_SMALL_RUN;   // longest run sorted by its own thread
+// Cooperative verdicts: with at most 2^PH_COOP_HB flows per half (flow tables below 2^19 flows, e.g.
+// a rank's shard of 1M flowIds at N >= 2), lanes own several events each; the owner lane of a
+// single-segment run only computes {S0, K} and all 512 lanes then write the half's verdicts from LDS,
+// instead of 2^hb lanes walking runs of 16..70 events while the other waves idle.
+#ifndef SENTINEL_PH_COOP_HB
+#define SENTINEL_PH_COOP_HB 8
+#endif
+#ifndef SENTINEL_PH_COOP_MINHB
+#define SENTINEL_PH_COOP_MINHB 0
+#endif
+constexpr int PH_COOP_HB = SENTINEL_PH_COOP_HB;
+constexpr int PH_COOP_FLOWS = 1 << (PH_COOP_HB > 0 ? PH_COOP_HB : 0);
+inline bool part_coop(int lb) {
+    const int hb = lb > 0 ? lb - 1 : 0;
+    return PH_COOP_HB > 0 && hb <= PH_COOP_HB && hb >= SENTINEL_PH_COOP_MINHB;
+}
 static_assert(PH_BINS == PH_THREADS, "one flow per thread");
 
 // block b -> (range, half): both halves of a range on the XCD b mod 8
@@ -771,14 +858,26 @@ __device__ unsigned long long g_phase[4096][5];
 #define PF_STAMP(i) do { } while (0)
 #endif
 
-template <int NMAX>
+template <int NMAX, bool COOP>
 __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     KeyTable T, const uint64_t *__restrict__ pval, uint64_t *__restrict__ gsval,
     const uint32_t *__restrict__ rstart, int lb, int32_t nranges, int32_t nflows, EventSrc src, Verdicts V,
     uint32_t *__restrict__ long_runs, uint32_t *__restrict__ nlong, uint32_t *__restrict__ big,
     uint32_t *__restrict__ nbig, unsigned long long *__restrict__ max_range) {
     __shared__ uint64_t sv[PH_CAP];
-    __shared__ uint16_t cnt[PH_WAVES][PH_BINS];
+    // the ballot ranking's per-wave counters and (after the sort) the cooperative verdict records,
+    // one per flow of the half, share one LDS buffer
+    constexpr int CF = COOP ? PH_COOP_FLOWS : 1;
+    constexpr int CNT_BYTES = PH_WAVES * PH_BINS * 2;
+    constexpr int COOP_BYTES = COOP ? CF * 56 : 0;
+    __shared__ uint64_t ubuf[((CNT_BYTES > COOP_BYTES ? CNT_BYTES : COOP_BYTES) + 7) / 8];
+    uint16_t(*cnt)[PH_BINS] = reinterpret_cast<uint16_t(*)[PH_BINS]>(ubuf);
+    double *c_thr = reinterpret_cast<double *>(ubuf);                 // [CF]
+    double *c_is = c_thr + CF;                                         // [CF]
+    int64_t *c_s0 = reinterpret_cast<int64_t *>(c_is + CF);            // [2][CF]
+    uint64_t *c_pos = reinterpret_cast<uint64_t *>(c_s0 + 2 * CF);     // [CF] start | len1 << 16 | len12 << 32
+    uint32_t *c_K = reinterpret_cast<uint32_t *>(c_pos + CF);          // [2][CF]
+    int32_t *c_a = reinterpret_cast<int32_t *>(c_K + 2 * CF);          // [2][CF]
     __shared__ uint32_t base[PH_BINS];
     __shared__ uint32_t waves_tot[PH_WAVES];
     __shared__ uint32_t s_nlong, s_cmax;
@@ -922,7 +1021,49 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     __syncthreads();
     for (uint32_t l = 0; l < s_nlong; ++l)
         for (uint32_t q = t; q < s_long[l][1]; q += PH_THREADS) gsval[goff + s_long[l][0] + q] = sv[s_long[l][0] + q];
-    if (c > 0 && c <= LONG_RUN && !part_run_single<NMAX>(fw, sv, start, start + c, src, V, T0)) {
+    if (COOP) {                                           // launched only when 2^hb <= PH_COOP_FLOWS
+        if (t < (1u << hb)) {
+            int64_t s0[2] = {0, 0};
+            uint32_t rec[2] = {COOP_SKIP, COOP_SKIP};
+            int32_t a[2] = {0, 0};
+            uint32_t len1 = 0, len12 = 0;
+            if (c > 0 && c <= LONG_RUN) {
+                bool small;
+                if (part_run_single<NMAX, true>(fw, sv, start, start + c, src, V, T0, &s0[0], &rec[0], &a[0], &small)) {
+                    rec[0] |= small ? COOP_SMALL : 0u;
+                    len1 = len12 = c;
+                } else {
+                    fw.load_header(T0);
+                    part_run_defer<NMAX>(fw, T, key, sv, start, start + c, src, V, T0, s0, rec, a, len1, len12);
+                }
+                c_thr[t] = fw.thr;
+                c_is[t] = fw.I_s;
+            }
+            c_s0[t] = s0[0];
+            c_s0[CF + t] = s0[1];
+            c_K[t] = rec[0];
+            c_K[CF + t] = rec[1];
+            c_a[t] = a[0];
+            c_a[CF + t] = a[1];
+            c_pos[t] = (uint64_t)start | ((uint64_t)len1 << 16) | ((uint64_t)len12 << 32);
+        }
+        __syncthreads();
+        // every lane: positions t, t + 512, ... of the half's sorted events (flow key in the value)
+        for (uint32_t i = t; i < total; i += PH_THREADS) {
+            const uint64_t v = sv[i];
+            const uint32_t kj = (uint32_t)(v >> VAL_KEY_SHIFT) & hmask;
+            const uint64_t pos = c_pos[kj];
+            const uint32_t k = i - (uint32_t)(pos & 0xFFFFu);
+            const uint32_t l1 = (uint32_t)(pos >> 16) & 0xFFFFu, l12 = (uint32_t)(pos >> 32) & 0xFFFFu;
+            if (k >= l12) continue;                               // third segment on: written by the walk
+            const uint32_t sg = k < l1 ? 0u : 1u;
+            const uint32_t rec = c_K[sg * CF + kj];
+            if (rec & COOP_SKIP) continue;                        // sequential segment: written by the walk
+            V.out[(uint32_t)v & SEQ_MASK] = run_verdict(c_thr[kj], c_is[kj], c_s0[sg * CF + kj], c_a[sg * CF + kj],
+                                                        rec & (COOP_SMALL - 1u), sg ? k - l1 : k,
+                                                        (rec & COOP_SMALL) != 0);
+        }
+    } else if (c > 0 && c <= LONG_RUN && !part_run_single<NMAX>(fw, sv, start, start + c, src, V, T0)) {
         fw.load_header(T0);
         part_run_w<NMAX>(fw, T, key, sv, start, start + c, src, V, T0);
     }

@@ -280,6 +280,40 @@ def test_full_size_properties_config3():
     assert torch.equal(v, v2)
 
 
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_bench_rank_shapes_bitexact(oracle_mod, world):
+    """Bit-exact at the exact per-rank shapes of the bench (`bench.py --gpus N`): rank 0's shard
+    (splitmix64(flowId) mod N) of the 1M-flowId config-3 universe, 8M-event batches, two batches
+    so the second rolls windows written by the first; oracle = the flow-sharded replay."""
+    import torch
+    from sentinel_amd.token_service import decode_verdicts, device_events
+    rng = np.random.default_rng(3)
+    rules = T.make_rules(1_000_000, rng, sample_count=10, window_interval_ms=1000)
+    if world > 1:
+        rules = rules.subset(np.nonzero(T.shard_of(rules.flow_id, world) == 0)[0])
+    F = len(rules)
+    svc = _engine(rules)
+    orc = oracle_mod.TokenServiceOracle.from_arrays(rules.flow_id, rules.count, rules.threshold_type,
+                                                    rules.sample_count, rules.window_interval_ms,
+                                                    rules.namespace, rules.checker)
+    n = 8 * 1024 * 1024
+    ms_per_event = 1000.0 / (2.0 * float(rules.count.sum()))
+    erng = np.random.default_rng(100 + world)
+    for b in range(2):
+        idx = erng.integers(0, F, n, dtype=np.int32)
+        ts = (T.T0_ALIGNED + np.floor(np.arange(b * n, (b + 1) * n, dtype=np.float64) * ms_per_event)).astype(np.int64)
+        acq = np.ones(n, np.int32)
+        v = svc.submit_flow_batch(device_events(torch.from_numpy(idx).cuda(), torch.from_numpy(acq).cuda(),
+                                                torch.from_numpy(ts).cuda()))
+        svc.synchronize()
+        st_g, rem_g, _ = decode_verdicts(v)
+        st_o, rem_o, _, _ = orc.replay_mt(idx, acq, ts, 16)
+        bad = np.nonzero((st_g != st_o) | (rem_g != rem_o))[0]
+        assert len(bad) == 0, (world, b, len(bad), bad[:5], st_g[bad[:5]], st_o[bad[:5]])
+    for f in np.random.default_rng(1).choice(F, 300, replace=False):
+        assert np.array_equal(svc.dump_flow(int(f), 10), orc.dump_flow(int(f))), f
+
+
 def test_batcher_concurrent_threads():
     """Many threads calling the per-call API concurrently: batched on the GPU, and the result set
     equals a sequential replay in some arrival order (homogeneous acquire => order-free counts)."""
