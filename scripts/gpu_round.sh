@@ -16,6 +16,11 @@ tail -3 $O/gpu_tests.log
 echo "== bench"
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
+echo "== per-rank shapes of the scaling bench (1M / N flows per rank, 8M events)"
+for F in 500000 250000 125000; do
+  timeout -k 10 180 python -u bench.py --flows $F --steps 20 --warmup 3 --no-cpu-baseline --no-host-path > $O/bench_flows_$F.json 2> $O/bench_flows_$F.err || { tail -20 $O/bench_flows_$F.err; exit 1; }
+done
+python -c "import json; print(json.dumps({F: {k: json.load(open('$O/bench_flows_%d.json' % F))[k] for k in ('value', 'p99_batch_ms', 'kernels')} for F in (500000, 250000, 125000)}))" > $O/rank_shapes.json && cat $O/rank_shapes.json
 echo "== rocprof stats"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-path > $O/bench_prof.json 2> $O/prof.err || { tail -20 $O/prof.err; exit 1; }
