@@ -602,7 +602,8 @@ constexpr uint32_t COOP_SKIP = 1u << 31, COOP_SMALL = 1u << 30;
 template <int NMAX>
 __device__ inline void part_run_defer(FlowWindow<NMAX> &fw, const KeyTable &T, uint32_t key, const uint64_t *s_val,
                                       uint32_t q0, uint32_t q1, const EventSrc &src, const Verdicts &V, int64_t T0,
-                                      int64_t *s0o, uint32_t *reco, int32_t *ao, uint32_t &len1, uint32_t &len12) {
+                                      int64_t *s0o, uint32_t *reco, int32_t *ao, uint32_t &len1, uint32_t &len12,
+                                      const uint32_t *segb = nullptr, const uint32_t *hetb = nullptr) {
     reco[0] = reco[1] = COOP_SKIP;
     len1 = len12 = 0;
     uint32_t q = q0;
@@ -613,11 +614,25 @@ __device__ inline void part_run_defer(FlowWindow<NMAX> &fw, const KeyTable &T, u
         const int64_t E = fw.event(s_val[q], src, T0, a, prio);
         bool het = prio && fw.kind == KIND_CLUSTER;
         uint32_t q2 = q + 1;
-        for (; q2 < q1; ++q2) {
-            int32_t a2;
-            bool p2;
-            if (fw.event(s_val[q2], src, T0, a2, p2) != E) break;
-            het |= a2 != a || (p2 && fw.kind == KIND_CLUSTER);
+        if (segb) {
+            // segment starts / heterogeneous positions marked by the whole workgroup (k_part_half)
+            uint32_t wi = q2 >> 5;
+            uint32_t m = q2 < q1 ? segb[wi] & (~0u << (q2 & 31)) : 0u;
+            while (!m && (wi + 1) * 32 < q1) m = segb[++wi];
+            q2 = m ? min(q1, wi * 32 + (uint32_t)__ffs(m) - 1) : q1;
+            for (uint32_t hw = q >> 5; hw <= (q2 - 1) >> 5; ++hw) {
+                uint32_t hm = hetb[hw];
+                if (hw == q >> 5) hm &= ~0u << (q & 31);
+                if (hw == (q2 - 1) >> 5 && ((q2 & 31) != 0)) hm &= (1u << (q2 & 31)) - 1u;
+                het |= hm != 0;
+            }
+        } else {
+            for (; q2 < q1; ++q2) {
+                int32_t a2;
+                bool p2;
+                if (fw.event(s_val[q2], src, T0, a2, p2) != E) break;
+                het |= a2 != a || (p2 && fw.kind == KIND_CLUSTER);
+            }
         }
         if (fw.slow(E, het)) {
             fw.sequential(T, key, E, s_val, q, q2, src, V);
@@ -883,6 +898,19 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     __shared__ uint32_t waves_tot[PH_WAVES];
     __shared__ uint32_t s_nlong, s_cmax;
     __shared__ uint32_t s_long[PH_MAX_LONG][2];
+#ifndef SENTINEL_NO_COOP_BITS
+    // parallel segment marking for halves of <= 128 flows: per-flow epoch parameters, then one bit per
+    // sorted event for "segment start" and "heterogeneous" (acquire differs from its predecessor's or
+    // a prioritized cluster request)
+    constexpr int CB = COOP ? PH_COOP_FLOWS / 2 : 1;
+    constexpr int MW = COOP ? (int)(PH_CAP + 31) / 32 : 1;
+    __shared__ int64_t p_E0[CB];
+    __shared__ double p_rcp[CB];
+    __shared__ int32_t p_r0[CB], p_w[CB];
+    __shared__ float p_rcpf[CB];
+    __shared__ uint32_t p_start[CB], p_cl[CB];
+    __shared__ uint32_t segb[MW], hetb[MW];
+#endif
     uint32_t p, h;
     half_of_block(blockIdx.x, p, h);
     const int hb = lb > 0 ? lb - 1 : 0;
@@ -1023,6 +1051,50 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     for (uint32_t l = 0; l < s_nlong; ++l)
         for (uint32_t q = t; q < s_long[l][1]; q += PH_THREADS) gsval[goff + s_long[l][0] + q] = sv[s_long[l][0] + q];
     if (COOP) {                                           // launched only when 2^hb <= PH_COOP_FLOWS
+#ifndef SENTINEL_NO_COOP_BITS
+        const bool bits = hb < PH_COOP_SINGLE_HB;         // block-uniform
+        if (bits) {
+            for (uint32_t j = t; j < (uint32_t)MW; j += PH_THREADS) { segb[j] = 0; hetb[j] = 0; }
+            if (t < (1u << hb) && c > 0) {
+                p_E0[t] = epoch_of(T0, fw.w, fw.rcp);
+                p_r0[t] = (int32_t)(T0 - p_E0[t] * (int64_t)fw.w);
+                p_rcpf[t] = 1.0f / (float)fw.w;
+                p_w[t] = fw.w;
+                p_rcp[t] = fw.rcp;
+                p_start[t] = start;
+                p_cl[t] = fw.kind == KIND_CLUSTER;
+            }
+            __syncthreads();
+            for (uint32_t i = t; i < total; i += PH_THREADS) {
+                const uint64_t v = sv[i];
+                const uint32_t kj = (uint32_t)(v >> VAL_KEY_SHIFT) & hmask;
+                FlowWindow<NMAX> lw;                      // epoch parameters only
+                lw.w = p_w[kj];
+                lw.rcp = p_rcp[kj];
+                lw.E0 = p_E0[kj];
+                lw.r0 = p_r0[kj];
+                lw.rcpf = p_rcpf[kj];
+                int32_t ai;
+                bool pi;
+                const int64_t Ei = lw.event(v, src, T0, ai, pi);
+                bool st = i == p_start[kj];
+                bool het = pi && p_cl[kj];
+                if (!st) {
+                    int32_t ap;
+                    bool pp;
+                    const int64_t Ep = lw.event(sv[i - 1], src, T0, ap, pp);
+                    st = Ep != Ei;
+                    if (!st) het |= ai != ap;
+                }
+                if (st) atomicOr(&segb[i >> 5], 1u << (i & 31));
+                if (het) atomicOr(&hetb[i >> 5], 1u << (i & 31));
+            }
+            __syncthreads();
+        }
+#else
+        const bool bits = false;
+        const uint32_t *segb = nullptr, *hetb = nullptr;
+#endif
         if (t < (1u << hb)) {
             int64_t s0[2] = {0, 0};
             uint32_t rec[2] = {COOP_SKIP, COOP_SKIP};
@@ -1039,7 +1111,8 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
                     len1 = len12 = c;
                 } else {
                     fw.load_header(T0);
-                    part_run_defer<NMAX>(fw, T, key, sv, start, start + c, src, V, T0, s0, rec, a, len1, len12);
+                    part_run_defer<NMAX>(fw, T, key, sv, start, start + c, src, V, T0, s0, rec, a, len1, len12,
+                                         bits ? segb : nullptr, bits ? hetb : nullptr);
                 }
                 c_thr[t] = fw.thr;
                 c_is[t] = fw.I_s;
