@@ -131,14 +131,20 @@ int  sentinel_device_count(void);
 int  sentinel_set_server_config(sentinel_engine_t *eng, const sentinel_server_config_t *cfg);
 int  sentinel_set_namespaces(sentinel_engine_t *eng, const sentinel_namespace_t *ns, int32_t n);
 int  sentinel_set_connected_count(sentinel_engine_t *eng, int32_t namespace_idx, int32_t connected);
-/* Loads the flow rule table.  Invalid rules (FlowRuleUtil.isValidRule: flowId <= 0, count < 0,
- * bad window config) are dropped exactly like ClusterFlowRuleManager does; their index maps to
- * SENTINEL_IDX_NO_RULE.  Metrics of flowIds present before and after the load are kept
- * (ClusterMetricStatistics.putMetricIfAbsent); new flowIds start empty. */
+/* Loads the flow rule table: ClusterFlowRuleManager.applyClusterFlowRule (ClusterFlowRuleManager.java:
+ * 325-372) over every namespace at once.  Invalid rules (FlowRuleUtil.isValidRule: flowId <= 0,
+ * count < 0, bad window config) are dropped; a repeated flowId keeps its first position and its
+ * last rule.  ClusterMetricStatistics.putMetricIfAbsent: a flowId present before and after keeps
+ * its metric -- its OLD window and counters -- and its nowCalls; a new flowId gets the window of
+ * its first occurrence; a flowId that left loses its metric, unless its namespace's list (raw
+ * rules of that namespace_idx, valid or not) is empty: then the metric is kept aside (clearAndResetRulesFor
+ * leaves METRIC_MAP alone) and comes back if the flowId is loaded again.  The window state moves on
+ * the device; the previous table stays in place if anything fails.  Param rules: the same. */
 int  sentinel_load_flow_rules(sentinel_engine_t *eng, const sentinel_flow_rule_t *rules, int32_t n);
 int  sentinel_load_param_rules(sentinel_engine_t *eng, const sentinel_param_rule_t *rules, int32_t n,
                                const uint64_t *hot_keys, const int32_t *hot_counts, int32_t n_hot);
 int32_t sentinel_flow_count(sentinel_engine_t *eng);
+int32_t sentinel_param_count(sentinel_engine_t *eng);   /* dense param rules (valid, one per flowId) */
 /* flowId -> dense index (or SENTINEL_IDX_NO_RULE / SENTINEL_IDX_BAD_ID), host side. */
 int  sentinel_lookup_flow_idx(sentinel_engine_t *eng, int64_t n, const int64_t *flow_ids, int32_t *idx_out);
 int  sentinel_lookup_param_idx(sentinel_engine_t *eng, int64_t n, const int64_t *flow_ids, int32_t *idx_out);
@@ -357,6 +363,40 @@ int  sentinel_param_sum(sentinel_engine_t *eng, int32_t rule_idx, uint64_t param
 int  sentinel_snapshot(sentinel_engine_t *eng, int64_t ts, sentinel_flow_snapshot_t *out);
 /* Device-pointer variant (for the RCCL all-gather), asynchronous on `stream`. */
 int  sentinel_snapshot_device(sentinel_engine_t *eng, int64_t ts, sentinel_flow_snapshot_t *d_out, void *stream);
+
+/* getTopValues(number) of every loaded param rule at ts (ClusterParamMetric.getTopValues,
+ * sentinel-cluster/.../cluster/flow/statistic/metric/ClusterParamMetric.java:84-127): per rule up to
+ * `number` (param key, avg = sum / intervalInSecond) with a non-zero window count, by (int) count
+ * descending, equal (int) counts by key ascending (the reference leaves their order to HashMap
+ * iteration).  count[r] entries for rule r; keys / avgs are rule-major [rules][number].  Exact mode
+ * only (the count-min sketch keeps no keys: every count is 0).  Host pointers, synchronous. */
+int  sentinel_param_top_values(sentinel_engine_t *eng, int64_t ts, int32_t number, int32_t *count,
+                               uint64_t *keys, double *avgs);
+/* ClusterMetricNodeGenerator.paramToMetricNode (ClusterMetricNodeGenerator.java:88-105) per param rule:
+ * flowId + topParams = getTopValues(5), for the RCCL all-gather of the snapshot.  DEVICE pointer with
+ * one record per loaded param rule; synchronous on `stream`. */
+#define SENTINEL_TOP_PARAMS 5
+typedef struct {
+    int64_t  flow_id;
+    int32_t  n_top;
+    int32_t  reserved;
+    uint64_t key[SENTINEL_TOP_PARAMS];
+    double   avg[SENTINEL_TOP_PARAMS];
+} sentinel_param_snapshot_t;
+int  sentinel_param_snapshot_device(sentinel_engine_t *eng, int64_t ts, sentinel_param_snapshot_t *d_out, void *stream);
+
+/* ---- metric registry (ClusterMetricStatistics / ClusterParamMetricStatistics) ---- */
+/* The window {sampleCount, intervalMs} of the METRIC behind a flow: a reload keeps a surviving flowId's
+ * metric as it was built (ClusterFlowRuleManager.java:361-362), so it can differ from its rule's. */
+int  sentinel_flow_window(sentinel_engine_t *eng, int32_t flow_idx, int32_t *sample_count, int32_t *interval_ms);
+/* ClusterMetricStatistics.METRIC_MAP.size(): flow metrics held, orphaned ones included. */
+int64_t sentinel_metric_count(sentinel_engine_t *eng);
+/* Server window change (ServerFlowConfig sampleCount / intervalMs; ClusterServerConfigManager.java:333-343):
+ * ClusterMetricStatistics.resetFlowMetrics + ClusterParamMetricStatistics.resetFlowMetrics -- every flow and
+ * param metric, orphans included, restarts empty with this window.  An invalid window is ignored. */
+int  sentinel_reset_metrics(sentinel_engine_t *eng, int32_t sample_count, int32_t interval_ms);
+/* Param slot table statistics: {capacity, live slots after the last rebuild, rebuilds so far}. */
+int  sentinel_param_table_stats(sentinel_engine_t *eng, int64_t *out3);
 /* The engine's own stream (hipStream_t). */
 void *sentinel_engine_stream(sentinel_engine_t *eng);
 /* Per-kernel timing with HIP events recorded on the launch stream (for roofline reporting).

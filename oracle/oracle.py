@@ -93,6 +93,11 @@ def lib():
         "orc_flow_replay": (None, [vp, i64, vp, vp, vp, vp, vp, vp, vp]),
         "orc_flow_replay_mt": (C.c_int, [vp, i64, vp, vp, vp, vp, vp, vp, vp, C.c_int]),
         "orc_engine_dump_flow": (C.c_int, [vp, i32, vp]),
+        "orc_engine_reset_metrics": (C.c_int, [vp, C.c_int, C.c_int]),
+        "orc_engine_flow_window": (C.c_int, [vp, i32, vp]),
+        "orc_engine_metric_count": (i64, [vp]),
+        "orc_engine_param_top_values": (C.c_int, [vp, i32, i64, C.c_int, vp, vp]),
+        "orc_engine_param_window": (C.c_int, [vp, i32, vp]),
         "orc_engine_limiter_sum": (i64, [vp, i32, i64]),
         "orc_engine_load_param_rules": (C.c_int, [vp, vp, C.c_int, vp, vp, C.c_int]),
         "orc_request_param_token": (None, [vp, i32, i32, i64, vp, C.c_int, vp, vp]),
@@ -488,8 +493,16 @@ class TokenServiceOracle:
     def param_overflowed(self):
         return bool(lib().orc_engine_param_overflowed(self.h))
 
+    def flow_window(self, idx):
+        """(sampleCount, intervalMs) of the metric behind dense flow index idx (its window, which a
+        reload keeps even when the rule's window changed)."""
+        w = np.zeros(2, dtype=np.int32)
+        if lib().orc_engine_flow_window(self.h, int(idx), _p(w)) < 0:
+            raise ValueError("no metric for flow index %d" % idx)
+        return int(w[0]), int(w[1])
+
     def dump_flow(self, idx) -> np.ndarray:
-        n = int(self.rules[idx].get("sample_count", 10)) if self.rules is not None else int(self._rec["sample_count"][idx])
+        n = self.flow_window(idx)[0]
         out = np.zeros(n * 8 + 8, dtype=np.int64)
         w = lib().orc_engine_dump_flow(self.h, idx, _p(out))
         if w < 0:
@@ -497,10 +510,30 @@ class TokenServiceOracle:
         return out
 
     def reload_flow_rules(self, rules):
-        """ClusterFlowRuleManager.loadRules again (nowCalls of surviving flowIds carried over)."""
-        self.rules = list(rules)
-        self._rules_c = rules_array(self.rules)
-        lib().orc_engine_load_flow_rules(self.h, self._rules_c, len(self.rules))
+        """ClusterFlowRuleManager.loadRules again: surviving flowIds keep their ClusterMetric (old
+        window and counters) and nowCalls; returns the number of dense flows."""
+        self.rules = None
+        self._rules_c = rules_array(list(rules))
+        return lib().orc_engine_load_flow_rules(self.h, self._rules_c, len(rules))
+
+    def reset_metrics(self, sample_count, interval_ms):
+        """Server window change (ClusterServerConfigManager.java:333-343): every metric restarts."""
+        return lib().orc_engine_reset_metrics(self.h, int(sample_count), int(interval_ms))
+
+    def metric_count(self):
+        return lib().orc_engine_metric_count(self.h)
+
+    def param_top_values(self, rule_idx, t, number=5):
+        keys = np.zeros(max(number, 1), dtype=np.uint64)
+        avgs = np.zeros(max(number, 1), dtype=np.float64)
+        k = lib().orc_engine_param_top_values(self.h, int(rule_idx), int(t), int(number), _p(keys), _p(avgs))
+        return [(int(keys[i]), float(avgs[i])) for i in range(k)]
+
+    def param_window(self, idx):
+        w = np.zeros(2, dtype=np.int32)
+        if lib().orc_engine_param_window(self.h, int(idx), _p(w)) < 0:
+            raise ValueError("no param metric for rule index %d" % idx)
+        return int(w[0]), int(w[1])
 
     CONC_EVENT = np.dtype([("flow_idx", "<i4"), ("acquire", "<i4"), ("token_id", "<i8"), ("kind", "<i4"),
                            ("flags", "<u4")])

@@ -468,11 +468,13 @@ struct orc_engine {
     orc_namespace *ns;
     orc_limiter **lim;
     int n_ns;
-    orc_flow_rule *rules;
-    orc_cluster_metric **cm;
+    orc_flow_rule *rules;       /* dense table: valid rules, one per flowId (first position, last content) */
+    orc_cluster_metric **cm;    /* cm[i] = METRIC_MAP.get(rules[i].flowId) (owned by metric_map) */
     int n_rules;
-    param_entry *prules;
+    kvmap metric_map;           /* ClusterMetricStatistics.METRIC_MAP: flowId -> orc_cluster_metric* */
+    param_entry *prules;        /* dense table of valid param rules; pm owned by param_metric_map */
     int n_prules;
+    kvmap param_metric_map;     /* ClusterParamMetricStatistics.METRIC_MAP: flowId -> orc_param_metric* */
     uint64_t *hot_keys;
     int32_t *hot_counts;
     int n_hot;
@@ -503,8 +505,11 @@ orc_engine *orc_engine_new(const orc_server_config *cfg, const orc_namespace *ns
 void orc_engine_free(orc_engine *e) {
     if (!e) return;
     for (int i = 0; i < e->n_ns; i++) orc_limiter_free(e->lim[i]);
-    for (int i = 0; i < e->n_rules; i++) orc_cm_free(e->cm[i]);
-    for (int i = 0; i < e->n_prules; i++) orc_pm_free(e->prules[i].pm);
+    for (int64_t j = 0; j < e->metric_map.cap; j++)
+        if (e->metric_map.used[j]) orc_cm_free((orc_cluster_metric *)(intptr_t)e->metric_map.v[j]);
+    for (int64_t j = 0; j < e->param_metric_map.cap; j++)
+        if (e->param_metric_map.used[j]) orc_pm_free((orc_param_metric *)(intptr_t)e->param_metric_map.v[j]);
+    kv_free(&e->metric_map); kv_free(&e->param_metric_map);
     free(e->ns); free(e->lim); free(e->rules); free(e->cm); free(e->prules);
     free(e->hot_keys); free(e->hot_counts);
     kv_free(&e->now_calls); kv_free(&e->rule_by_fid); kv_free(&e->tok_index);
@@ -512,30 +517,127 @@ void orc_engine_free(orc_engine *e) {
     free(e);
 }
 
-/* ClusterFlowRuleManager.applyClusterFlowRule (ClusterFlowRuleManager.java:325-372): one
- * ClusterMetric per flowId with the rule's (sampleCount, windowIntervalMs). */
+/* Remove `key` from a kvmap (backward-shift deletion keeps linear-probe chains intact). */
+static void kv_erase(kvmap *m, uint64_t key) {
+    if (!m->cap) return;
+    const uint64_t mask = (uint64_t)(m->cap - 1);
+    uint64_t h = mix64(key) & mask;
+    while (m->used[h] && m->k[h] != key) h = (h + 1) & mask;
+    if (!m->used[h]) return;
+    m->used[h] = 0;
+    m->size--;
+    uint64_t j = h;
+    for (;;) {
+        j = (j + 1) & mask;
+        if (!m->used[j]) return;
+        const uint64_t home = mix64(m->k[j]) & mask;
+        /* move j back to the hole h unless its home lies cyclically in (h, j] */
+        const int keep = (h <= j) ? (home > h && home <= j) : (home > h || home <= j);
+        if (keep) continue;
+        m->used[h] = 1; m->k[h] = m->k[j]; m->v[h] = m->v[j];
+        m->used[j] = 0;
+        h = j;
+    }
+}
+
+static int valid_window(int n, int interval) { return n > 0 && interval > 0 && interval % n == 0; }
+
+/* Per-namespace raw list sizes of a whole-table load (namespace_idx -1 and out-of-range indices
+ * each form their own group). */
+static int64_t ns_group(int32_t ns_idx, int n_ns) { return (ns_idx >= 0 && ns_idx < n_ns) ? ns_idx : -1; }
+
+/* ClusterFlowRuleManager.applyClusterFlowRule (ClusterFlowRuleManager.java:325-372) applied to every
+ * namespace at once.  Valid rules (FlowRuleUtil.isValidRule: flowId > 0, count >= 0, window config)
+ * are deduplicated by flowId: ruleMap.put keeps the last rule, the dense index is the first
+ * position.  ClusterMetricStatistics.putMetricIfAbsent (CFRM:361-362) runs in list order, so a
+ * flowId that already has a metric keeps it -- with its OLD sampleCount / windowIntervalMs and its
+ * counters -- and a new flowId gets the window of its first occurrence.  A flowId that left the
+ * table loses its metric (clearAndResetRulesConditional -> removeMetric, CFRM:285-301) unless its
+ * namespace's new list is empty: clearAndResetRulesFor (CFRM:268-283) leaves METRIC_MAP alone, so
+ * the metric stays, unreachable, and is picked up again if the flowId comes back.  nowCalls
+ * (CurrentConcurrencyManager) survives only for flowIds present before and after (CFRM:356-358). */
 int orc_engine_load_flow_rules(orc_engine *e, const orc_flow_rule *rules, int n) {
-    for (int i = 0; i < e->n_rules; i++) orc_cm_free(e->cm[i]);
+    /* raw list size per namespace group */
+    int64_t *raw = (int64_t *)calloc((size_t)e->n_ns + 1, sizeof(int64_t));
+    for (int i = 0; i < n; i++) raw[ns_group(rules[i].namespace_idx, e->n_ns) + 1]++;
+    /* dense table */
+    orc_flow_rule *nr = (orc_flow_rule *)calloc((size_t)(n > 0 ? n : 1), sizeof(orc_flow_rule));
+    kvmap nidx;
+    kv_init(&nidx);
+    int nn = 0;
+    for (int i = 0; i < n; i++) {
+        const orc_flow_rule *r = &rules[i];
+        if (r->flow_id <= 0 || !(r->count >= 0) || !valid_window(r->sample_count, r->window_interval_ms)) continue;
+        int64_t *p = kv_find(&nidx, (uint64_t)r->flow_id);
+        if (p) { nr[*p] = *r; continue; }
+        *kv_insert(&nidx, (uint64_t)r->flow_id, 0) = nn;
+        nr[nn++] = *r;
+        /* putMetricIfAbsent with the first occurrence's window */
+        if (!kv_find(&e->metric_map, (uint64_t)r->flow_id))
+            *kv_insert(&e->metric_map, (uint64_t)r->flow_id, 0) =
+                (int64_t)(intptr_t)orc_cm_new(r->sample_count, r->window_interval_ms);
+    }
+    /* flowIds that left: drop the metric unless their namespace's list is empty */
+    for (int i = 0; i < e->n_rules; i++) {
+        const orc_flow_rule *o = &e->rules[i];
+        if (kv_find(&nidx, (uint64_t)o->flow_id)) continue;
+        if (raw[ns_group(o->namespace_idx, e->n_ns) + 1] == 0) continue;          /* orphaned, kept */
+        int64_t *m = kv_find(&e->metric_map, (uint64_t)o->flow_id);
+        if (m) orc_cm_free((orc_cluster_metric *)(intptr_t)*m);
+        kv_erase(&e->metric_map, (uint64_t)o->flow_id);
+    }
     free(e->rules); free(e->cm);
-    e->rules = (orc_flow_rule *)calloc((size_t)(n > 0 ? n : 1), sizeof(orc_flow_rule));
-    e->cm = (orc_cluster_metric **)calloc((size_t)(n > 0 ? n : 1), sizeof(orc_cluster_metric *));
-    e->n_rules = n;
+    e->rules = nr;
+    e->n_rules = nn;
+    e->cm = (orc_cluster_metric **)calloc((size_t)(nn > 0 ? nn : 1), sizeof(orc_cluster_metric *));
     kvmap now;
     kv_init(&now);
-    kv_free(&e->rule_by_fid);
-    for (int i = 0; i < n; i++) {
-        e->rules[i] = rules[i];
-        e->cm[i] = orc_cm_new(rules[i].sample_count, rules[i].window_interval_ms);  /* NULL => FAIL */
-        if (!e->cm[i] || rules[i].flow_id <= 0) continue;
-        *kv_insert(&e->rule_by_fid, (uint64_t)rules[i].flow_id, 0) = i;           /* ruleMap.put: last wins */
-        /* CFRM:356-358: nowCalls survives for flowIds still present, new flowIds start at 0 */
-        const int64_t *old = kv_find(&e->now_calls, (uint64_t)rules[i].flow_id);
-        *kv_insert(&now, (uint64_t)rules[i].flow_id, 0) = old ? *old : 0;
+    for (int i = 0; i < nn; i++) {
+        e->cm[i] = (orc_cluster_metric *)(intptr_t)*kv_find(&e->metric_map, (uint64_t)nr[i].flow_id);
+        const int64_t *old = kv_find(&e->now_calls, (uint64_t)nr[i].flow_id);
+        *kv_insert(&now, (uint64_t)nr[i].flow_id, 0) = old ? *old : 0;
     }
     kv_free(&e->now_calls);
     e->now_calls = now;
+    kv_free(&e->rule_by_fid);
+    e->rule_by_fid = nidx;
+    free(raw);
+    return nn;
+}
+
+/* ClusterServerConfigManager.applyGlobalFlowConfig with a new (sampleCount, intervalMs)
+ * (ClusterServerConfigManager.java:333-343): ClusterMetricStatistics.resetFlowMetrics and
+ * ClusterParamMetricStatistics.resetFlowMetrics replace EVERY metric -- orphans included -- with a
+ * fresh one of the server window. */
+int orc_engine_reset_metrics(orc_engine *e, int sample_count, int interval_ms) {
+    if (!valid_window(sample_count, interval_ms)) return -1;
+    for (int64_t j = 0; j < e->metric_map.cap; j++) {
+        if (!e->metric_map.used[j]) continue;
+        orc_cm_free((orc_cluster_metric *)(intptr_t)e->metric_map.v[j]);
+        e->metric_map.v[j] = (int64_t)(intptr_t)orc_cm_new(sample_count, interval_ms);
+    }
+    for (int i = 0; i < e->n_rules; i++)
+        e->cm[i] = (orc_cluster_metric *)(intptr_t)*kv_find(&e->metric_map, (uint64_t)e->rules[i].flow_id);
+    for (int64_t j = 0; j < e->param_metric_map.cap; j++) {
+        if (!e->param_metric_map.used[j]) continue;
+        orc_pm_free((orc_param_metric *)(intptr_t)e->param_metric_map.v[j]);
+        e->param_metric_map.v[j] = (int64_t)(intptr_t)orc_pm_new(sample_count, interval_ms, 4000);
+    }
+    for (int i = 0; i < e->n_prules; i++)
+        e->prules[i].pm = (orc_param_metric *)(intptr_t)*kv_find(&e->param_metric_map, (uint64_t)e->prules[i].r.flow_id);
     return 0;
 }
+
+/* Window of the metric behind dense flow index idx: {sampleCount, intervalMs}; -1 if none. */
+int orc_engine_flow_window(const orc_engine *e, int32_t idx, int32_t *out2) {
+    if (idx < 0 || idx >= e->n_rules || !e->cm[idx]) return -1;
+    out2[0] = e->cm[idx]->la.n;
+    out2[1] = e->cm[idx]->la.interval;
+    return 0;
+}
+
+/* Number of metrics held (reachable + orphaned): METRIC_MAP.size(). */
+int64_t orc_engine_metric_count(const orc_engine *e) { return e->metric_map.size; }
 
 /* GRL:46-55 tryPass(namespace) */
 static int engine_allow_proceed(orc_engine *e, int32_t ns, int64_t t) {
@@ -683,17 +785,46 @@ int64_t orc_engine_limiter_sum(orc_engine *e, int32_t ns, int64_t t) {
 }
 
 /* ---- cluster hot-parameter path ---- */
+/* ClusterParamFlowRuleManager.applyClusterParamRules (ClusterParamFlowRuleManager.java:318-360) for
+ * every namespace at once, with the flow table's semantics: valid rules (ParamFlowRuleUtil.isValidRule:
+ * count >= 0, window config, flowId > 0) deduplicated by flowId (last rule wins, first position keeps
+ * the dense index); ClusterParamMetricStatistics.putMetricIfAbsent (:355-356) keeps the metric -- old
+ * window and counters -- of a flowId present before and after; a flowId that left loses its metric
+ * unless its namespace's list is empty (clearAndResetRulesFor keeps METRIC_MAP entries). */
 int orc_engine_load_param_rules(orc_engine *e, const orc_param_rule *rules, int n,
                                 const uint64_t *hot_keys, const int32_t *hot_counts, int n_hot) {
-    for (int i = 0; i < e->n_prules; i++) orc_pm_free(e->prules[i].pm);
-    free(e->prules); free(e->hot_keys); free(e->hot_counts);
-    e->prules = (param_entry *)calloc((size_t)(n > 0 ? n : 1), sizeof(param_entry));
-    e->n_prules = n;
+    int64_t *raw = (int64_t *)calloc((size_t)e->n_ns + 1, sizeof(int64_t));
+    for (int i = 0; i < n; i++) raw[ns_group(rules[i].namespace_idx, e->n_ns) + 1]++;
+    param_entry *np = (param_entry *)calloc((size_t)(n > 0 ? n : 1), sizeof(param_entry));
+    kvmap nidx;
+    kv_init(&nidx);
+    int nn = 0;
     for (int i = 0; i < n; i++) {
-        e->prules[i].r = rules[i];
-        /* ClusterParamFlowRuleManager.java:355 -> ClusterParamMetric(sampleCount, windowIntervalMs), cap 4000 */
-        e->prules[i].pm = orc_pm_new(rules[i].sample_count, rules[i].window_interval_ms, 4000);
+        const orc_param_rule *r = &rules[i];
+        if (r->flow_id <= 0 || !(r->count >= 0) || !valid_window(r->sample_count, r->window_interval_ms)) continue;
+        int64_t *p = kv_find(&nidx, (uint64_t)r->flow_id);
+        if (p) { np[*p].r = *r; continue; }
+        *kv_insert(&nidx, (uint64_t)r->flow_id, 0) = nn;
+        np[nn++].r = *r;
+        if (!kv_find(&e->param_metric_map, (uint64_t)r->flow_id))
+            *kv_insert(&e->param_metric_map, (uint64_t)r->flow_id, 0) =
+                (int64_t)(intptr_t)orc_pm_new(r->sample_count, r->window_interval_ms, 4000);
     }
+    for (int i = 0; i < e->n_prules; i++) {
+        const orc_param_rule *o = &e->prules[i].r;
+        if (kv_find(&nidx, (uint64_t)o->flow_id)) continue;
+        if (raw[ns_group(o->namespace_idx, e->n_ns) + 1] == 0) continue;
+        int64_t *m = kv_find(&e->param_metric_map, (uint64_t)o->flow_id);
+        if (m) orc_pm_free((orc_param_metric *)(intptr_t)*m);
+        kv_erase(&e->param_metric_map, (uint64_t)o->flow_id);
+    }
+    for (int i = 0; i < nn; i++)
+        np[i].pm = (orc_param_metric *)(intptr_t)*kv_find(&e->param_metric_map, (uint64_t)np[i].r.flow_id);
+    free(e->prules); free(e->hot_keys); free(e->hot_counts);
+    e->prules = np;
+    e->n_prules = nn;
+    kv_free(&nidx);
+    free(raw);
     e->n_hot = n_hot;
     e->hot_keys = (uint64_t *)calloc((size_t)(n_hot > 0 ? n_hot : 1), sizeof(uint64_t));
     e->hot_counts = (int32_t *)calloc((size_t)(n_hot > 0 ? n_hot : 1), sizeof(int32_t));
@@ -701,6 +832,19 @@ int orc_engine_load_param_rules(orc_engine *e, const orc_param_rule *rules, int 
         memcpy(e->hot_keys, hot_keys, sizeof(uint64_t) * (size_t)n_hot);
         memcpy(e->hot_counts, hot_counts, sizeof(int32_t) * (size_t)n_hot);
     }
+    return nn;
+}
+
+/* getTopValues(number) of the param metric behind dense rule idx (ClusterParamMetric.java:84-127). */
+int orc_engine_param_top_values(orc_engine *e, int32_t idx, int64_t t, int number, uint64_t *keys, double *avgs) {
+    if (idx < 0 || idx >= e->n_prules || !e->prules[idx].pm) return 0;
+    return orc_pm_top_values(e->prules[idx].pm, t, number, keys, avgs);
+}
+
+int orc_engine_param_window(const orc_engine *e, int32_t idx, int32_t *out2) {
+    if (idx < 0 || idx >= e->n_prules || !e->prules[idx].pm) return -1;
+    out2[0] = e->prules[idx].pm->la.n;
+    out2[1] = e->prules[idx].pm->la.interval;
     return 0;
 }
 

@@ -99,7 +99,12 @@ typedef struct {
 typedef struct orc_engine orc_engine;
 orc_engine *orc_engine_new(const orc_server_config *cfg, const orc_namespace *ns, int n_ns);
 void orc_engine_free(orc_engine *e);
+/* Returns the number of dense flows (valid rules, one per flowId).  Reload semantics in the .c. */
 int  orc_engine_load_flow_rules(orc_engine *e, const orc_flow_rule *rules, int n);
+/* Server window change: every metric (flow and param, orphans included) restarts with it. */
+int  orc_engine_reset_metrics(orc_engine *e, int sample_count, int interval_ms);
+int  orc_engine_flow_window(const orc_engine *e, int32_t flow_idx, int32_t *out2);
+int64_t orc_engine_metric_count(const orc_engine *e);
 
 /* Token-result status codes (core/cluster/TokenResultStatus.java:27-69). */
 enum {
@@ -144,6 +149,8 @@ void orc_request_param_token(orc_engine *e, int32_t rule_idx, int32_t acquire, i
 void orc_param_replay(orc_engine *e, int64_t n, const int32_t *rule_idx, const int32_t *acquire,
                       const uint64_t *param_key, const int64_t *ts, int8_t *status, int32_t *remaining);
 int64_t orc_engine_param_sum(orc_engine *e, int32_t rule_idx, int64_t t, uint64_t key);
+int  orc_engine_param_top_values(orc_engine *e, int32_t rule_idx, int64_t t, int number, uint64_t *keys, double *avgs);
+int  orc_engine_param_window(const orc_engine *e, int32_t rule_idx, int32_t *out2);
 int  orc_engine_param_overflowed(const orc_engine *e);
 
 /* ---------------- Local path: StatisticNode + DefaultController (config 1) ---------------- */

@@ -50,6 +50,8 @@ EXPORTS = [
     "sentinel_concurrent_expire",
     "sentinel_load_local_resources", "sentinel_submit_local_entry_batch", "sentinel_submit_local_entry_batch_host",
     "sentinel_local_node_stats", "sentinel_set_occupy_timeout", "sentinel_profile_select", "sentinel_profile_gate", "sentinel_set_flow_path",
+    "sentinel_param_top_values", "sentinel_param_snapshot_device", "sentinel_flow_window", "sentinel_metric_count",
+    "sentinel_reset_metrics", "sentinel_param_table_stats", "sentinel_param_count",
 ]
 
 STATUS_RELEASE_OK = 6
@@ -107,6 +109,9 @@ CONC_EVENT_DTYPE = np.dtype([("flow_idx", "<i4"), ("acquire", "<i4"), ("token_id
                              ("flags", "<u4")])
 CONC_RESULT_DTYPE = np.dtype([("token_id", "<i8"), ("status", "<i4"), ("reserved", "<i4")])
 VERDICT_DTYPE = np.dtype([("remaining", "<i4"), ("status", "<i2"), ("wait_in_ms", "<u2")])
+TOP_PARAMS = 5
+PARAM_SNAPSHOT_DTYPE = np.dtype([("flow_id", "<i8"), ("n_top", "<i4"), ("reserved", "<i4"),
+                                 ("key", "<u8", (TOP_PARAMS,)), ("avg", "<f8", (TOP_PARAMS,))])
 
 
 class SentinelError(RuntimeError):
@@ -180,6 +185,13 @@ def load():
         "sentinel_profile_select": (C.c_int, [vp, C.c_char_p]),
         "sentinel_profile_gate": (C.c_int, [vp, C.c_int]),
         "sentinel_set_flow_path": (C.c_int, [vp, C.c_int]),
+        "sentinel_param_top_values": (C.c_int, [vp, i64, i32, vp, vp, vp]),
+        "sentinel_param_snapshot_device": (C.c_int, [vp, i64, vp, vp]),
+        "sentinel_flow_window": (C.c_int, [vp, i32, vp, vp]),
+        "sentinel_metric_count": (i64, [vp]),
+        "sentinel_reset_metrics": (C.c_int, [vp, i32, i32]),
+        "sentinel_param_table_stats": (C.c_int, [vp, vp]),
+        "sentinel_param_count": (i32, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

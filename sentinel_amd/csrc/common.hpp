@@ -73,11 +73,17 @@ __host__ __device__ inline int64_t java_d2l(double d) {
 constexpr uint64_t PKEY_EMPTY = 0xFFFFFFFFFFFFFFFFull;   // reserved param key (empty table slot)
 
 // Find or insert `key` in an open-addressing table of 2^k slots; returns the slot or -1 (full).
-__device__ inline int64_t slot_insert(unsigned long long *table, uint64_t mask, uint64_t key) {
+// `fresh` (optional) counts the keys this call inserted.
+__device__ inline int64_t slot_insert(unsigned long long *table, uint64_t mask, uint64_t key,
+                                      unsigned long long *fresh = nullptr) {
     uint64_t h = mix64(key) & mask;
     for (uint64_t probes = 0; probes <= mask; ++probes) {
         const unsigned long long prev = atomicCAS(&table[h], (unsigned long long)PKEY_EMPTY, (unsigned long long)key);
-        if (prev == PKEY_EMPTY || prev == key) return (int64_t)h;
+        if (prev == PKEY_EMPTY) {
+            if (fresh) atomicAdd(fresh, 1ull);
+            return (int64_t)h;
+        }
+        if (prev == key) return (int64_t)h;
         h = (h + 1) & mask;
     }
     return -1;

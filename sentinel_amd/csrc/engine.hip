@@ -31,6 +31,7 @@
 #include "common.hpp"
 #include "concurrent.hpp"
 #include "param_rules.hpp"
+#include "param_table.hpp"
 #include "partition.hpp"
 #include "local_entry.hpp"
 #include <random>
@@ -159,8 +160,8 @@ __global__ __launch_bounds__(SORT_THREADS) void k_flow_prep(
 // (rule, value): the host's injective encoding of the Java typed value.
 __global__ __launch_bounds__(SORT_THREADS) void k_param_prep(
     int64_t n, const ParamEvent *__restrict__ ev, int32_t nrules, const int32_t *__restrict__ route,
-    unsigned long long *table, uint64_t cap_mask, int32_t *slot_rule, uint64_t *__restrict__ out,
-    uint32_t *__restrict__ fkey, uint32_t finvalid, int fpasses, uint32_t *__restrict__ fhist,
+    unsigned long long *table, uint64_t cap_mask, int32_t *slot_rule, unsigned long long *fresh,
+    uint64_t *__restrict__ out, uint32_t *__restrict__ fkey, uint32_t finvalid, int fpasses, uint32_t *__restrict__ fhist,
     uint32_t *__restrict__ lkey, uint32_t linvalid, int lpasses, uint32_t *__restrict__ lhist, int64_t nblocks) {
     __shared__ uint32_t hf[MAX_PASSES][RADIX];
     __shared__ uint32_t hl[MAX_PASSES][RADIX];
@@ -183,8 +184,8 @@ __global__ __launch_bounds__(SORT_THREADS) void k_param_prep(
             if (r == ROUTE_TOO_MANY) st = ST_TOO_MANY_REQUEST;
             else if (e.ts < 0) st = ST_FAIL;
             else {
-                const int64_t h = slot_insert(table, cap_mask, e.key);
-                if (h < 0) st = ST_FAIL;                                   // table full
+                const int64_t h = slot_insert(table, cap_mask, e.key, fresh);
+                if (h < 0) st = ST_FAIL;          // table full: the host's param_reserve prevents it
                 else {
                     k = (uint32_t)h;
                     slot_rule[h] = e.idx;    // identical value from every writer of this slot
@@ -232,6 +233,11 @@ __global__ __launch_bounds__(256) void k_param_meta(int64_t n, const uint32_t *_
     slot_kind[s] = KIND_PARAM;
 }
 
+// One key's slot (or -1) for the host's read-only queries.
+__global__ void k_slot_find_one(const unsigned long long *table, uint64_t mask, uint64_t key, int64_t *out) {
+    *out = slot_find(table, mask, key);
+}
+
 // Snapshot of one flow: getAvg(BLOCK) then getAvg(PASS) at ts (ClusterMetricNodeGenerator.java:79-84).
 __global__ __launch_bounds__(256) void k_snapshot(KeyTable T, int32_t nflows, int64_t ts,
                                                   const int64_t *__restrict__ flow_ids,
@@ -261,6 +267,79 @@ __global__ void k_init_state(int64_t *state, const int64_t *__restrict__ off, in
     for (int64_t j = 0; j < words; ++j) state[o + j] = (j < 2 * n && (j & 1) == 0) ? EPOCH_ABSENT : 0;
 }
 
+// Flow-table remap of a rule reload (ClusterMetricStatistics.putMetricIfAbsent, CFRM:361-362):
+// new flow i takes the window state of old flow src[i] >= 0 (with the old window, which the host
+// kept in nn[i]), of the staged record stg[stg_off[i]] when src[i] == -2 (an orphaned metric coming
+// back), or starts empty (-1).  Blocked header / rest layouts of the old and new tables may differ
+// (slots per block = header_block_slots of each table's largest n).  Staged record: 2n pair words,
+// 6n rest words (slot-major, counters BLOCK .. WAITING), occupy PASS, occupy PASS_REQUEST, has_occ.
+// The new state must be zeroed beforehand.  nowCalls (CurrentConcurrencyManager) moves with src >= 0.
+__global__ __launch_bounds__(256) void k_flow_remap(
+    int64_t *__restrict__ nst, int32_t nhb, int64_t nrb, const int32_t *__restrict__ nn,
+    const int64_t *__restrict__ ost, int32_t ohb, int64_t orb, const int32_t *__restrict__ src,
+    const int64_t *__restrict__ stg, const int64_t *__restrict__ stg_off, int64_t *__restrict__ nocc,
+    uint8_t *__restrict__ nhocc, int32_t *__restrict__ nnow, const int64_t *__restrict__ oocc,
+    const uint8_t *__restrict__ ohocc, const int32_t *__restrict__ onow, int32_t F) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= F) return;
+    const int n = nn[i];
+    const int32_t s = src[i];
+    const int64_t *r = s == -2 ? stg + stg_off[i] : nullptr;
+    for (int j = 0; j < n; ++j) {
+        const int64_t d = blocked_pair_word(i, nhb, j);
+        int64_t ep = EPOCH_ABSENT, ps = 0;
+        if (s >= 0) {
+            const int64_t o = blocked_pair_word(s, ohb, j);
+            ep = ost[o];
+            ps = ost[o + 1];
+        } else if (r) {
+            ep = r[2 * j];
+            ps = r[2 * j + 1];
+        }
+        nst[d] = ep;
+        nst[d + 1] = ps;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            int64_t v = 0;
+            if (s >= 0) v = ost[orb + blocked_rest_word(s, ohb, j, c)];
+            else if (r) v = r[2 * n + 6 * j + c];
+            nst[nrb + blocked_rest_word(i, nhb, j, c)] = v;
+        }
+    }
+    int64_t o0 = 0, o1 = 0;
+    uint8_t h = 0;
+    int32_t now = 0;
+    if (s >= 0) { o0 = oocc[2 * s]; o1 = oocc[2 * s + 1]; h = ohocc[s]; now = onow ? onow[s] : 0; }
+    else if (r) { o0 = r[8 * n]; o1 = r[8 * n + 1]; h = (uint8_t)r[8 * n + 2]; }
+    nocc[2 * i] = o0;
+    nocc[2 * i + 1] = o1;
+    nhocc[i] = h;
+    nnow[i] = now;
+}
+
+// Staged records (k_flow_remap's format) of the old flows idx[k] whose metric outlives their rule
+// (an emptied namespace list: clearAndResetRulesFor keeps METRIC_MAP, CFRM:268-283).
+__global__ __launch_bounds__(256) void k_flow_gather(const int64_t *__restrict__ ost, int32_t ohb, int64_t orb,
+                                                     const int32_t *__restrict__ idx, const int32_t *__restrict__ nn,
+                                                     const int64_t *__restrict__ off, int32_t K,
+                                                     const int64_t *__restrict__ oocc,
+                                                     const uint8_t *__restrict__ ohocc, int64_t *__restrict__ out) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= K) return;
+    const int32_t o = idx[k];
+    const int n = nn[k];
+    int64_t *r = out + off[k];
+    for (int j = 0; j < n; ++j) {
+        const int64_t p = blocked_pair_word(o, ohb, j);
+        r[2 * j] = ost[p];
+        r[2 * j + 1] = ost[p + 1];
+        for (int c = 0; c < 6; ++c) r[2 * n + 6 * j + c] = ost[orb + blocked_rest_word(o, ohb, j, c)];
+    }
+    r[8 * n] = oocc[2 * o];
+    r[8 * n + 1] = oocc[2 * o + 1];
+    r[8 * n + 2] = ohocc[o];
+}
+
 inline unsigned grid_for(int64_t n, int threads = 256) { return (unsigned)std::max<int64_t>(1, (n + threads - 1) / threads); }
 
 }  // namespace
@@ -276,8 +355,13 @@ struct sentinel_engine {
     // flows
     std::vector<sentinel_flow_rule_t> rules;
     std::unordered_map<int64_t, int32_t> flow_index;
-    std::vector<int32_t> h_flow_n, h_flow_w;
+    std::vector<int32_t> h_flow_n, h_flow_w, h_flow_interval;   // the window of each flow's METRIC
     std::vector<int64_t> h_flow_off;
+    // metrics that outlived their rule (a namespace whose rule list became empty keeps METRIC_MAP
+    // entries: ClusterFlowRuleManager.clearAndResetRulesFor, CFRM:268-283), by flowId: window +
+    // staged record (k_flow_remap format); revived if the flowId is loaded again
+    struct Orphan { int32_t n, interval; std::vector<int64_t> rec; };
+    std::unordered_map<int64_t, Orphan> orphans;
     TableBufs ft;
     DevBuf d_flow_route, d_flow_ids;
     bool flow_plain = true;          // no flow needs a limiter or namespace check
@@ -310,11 +394,20 @@ struct sentinel_engine {
     DevBuf d_ptable, d_slot_rule, d_hot_table, d_hot_thr;
     bool param_plain = true;
     TableBufs pt;
-    uint64_t pcap = (uint64_t)1 << 22;
+    uint64_t pcap = (uint64_t)1 << 20;     // initial param slots; grows on demand (param_reserve)
     int32_t pmax_n = 1;
     uint64_t hot_mask = 0;
     bool has_hot = false;
     DevBuf d_prule_kind;               // KIND_PARAM per rule (segment kernel of the per-rule path)
+    std::vector<int32_t> h_prule_n, h_prule_interval;   // the window of each param rule's METRIC
+    // param metrics that outlived their rule (emptied namespace list), by flowId: window + exported
+    // slots ((2 + 2n) words each: key, -, n {epoch, count} pairs)
+    struct POrphan { int32_t n, interval; std::vector<int64_t> recs; };
+    std::unordered_map<int64_t, POrphan> porphans;
+    uint64_t p_live = 0;               // live slots after the last rebuild
+    uint64_t p_ub = 0;                 // values submitted since (an upper bound of the fresh inserts)
+    DevBuf d_pfresh;                   // device: fresh inserts since the last rebuild
+    uint64_t p_rebuilds = 0;
     int32_t pmode = SENTINEL_PARAM_EXACT;
     int32_t cm_depth = 4;
     uint32_t cm_width = 1024;
@@ -616,9 +709,20 @@ struct sentinel_engine {
     }
 
     int rebuild_flow_thresholds();
+    void flow_thresholds(const std::vector<sentinel_flow_rule_t> &rules, std::vector<double> &thr,
+                         std::vector<double> &cthr) const;
+    bool flow_routes(const std::vector<sentinel_flow_rule_t> &rules, std::vector<int32_t> &route) const;
     int rebuild_limiters();
     int rebuild_routes();
+    int install_flows(std::vector<sentinel_flow_rule_t> &&nr, std::unordered_map<int64_t, int32_t> &&nidx,
+                      std::vector<int32_t> &&gn, std::vector<int32_t> &&gint, std::vector<int32_t> &&src,
+                      std::vector<int64_t> &&stg, std::vector<int64_t> &&stg_off, const std::vector<int32_t> &orphan_old);
     int clear_param_slots();
+    int param_rebuild(uint64_t new_cap, const std::vector<int32_t> &rmap, int32_t new_maxn,
+                      const std::vector<int32_t> &new_rn, const std::vector<int64_t> &imp, int64_t imp_stride,
+                      const std::vector<int32_t> &imp_rule, std::vector<std::pair<int32_t, std::vector<int64_t>>> *exported);
+    int param_reserve(int64_t nv);
+    int reset_param_metrics(int32_t sample_count, int32_t interval_ms);
     int rebuild_cm();
     int ensure_tokens();
     int rewrite_tokens(bool compact);
@@ -700,10 +804,178 @@ int sentinel_engine::clear_param_slots() {
     const uint64_t P = pcap;
     const int64_t stride = header_words(pmax_n);
     HIP_OK(hipMemsetAsync(d_ptable.p, 0xFF, P * 8, stream));
+    HIP_OK(hipMemsetAsync(d_pfresh.p, 0, 8, stream));
     k_init_state<<<grid_for((int64_t)P), 256, 0, stream>>>(pt.state.as<int64_t>(), nullptr, stride, nullptr, pmax_n,
                                                            stride, (int64_t)P);
     HIP_OK(hipStreamSynchronize(stream));
+    p_live = p_ub = 0;
     return 0;
+}
+
+// Rebuild of the exact param table into a fresh one of new_cap slots (param_table.hpp): live slots of
+// rules with rmap[old rule] >= 0 move under the new index unless dead, rmap == -2 exports the rule's
+// slots to `exported` (old rule, records), -1 drops them; `imp` (imp_stride words per record, rule
+// imp_rule[k]) is inserted afterwards.  new_rn: the new rules' windows (n).  On failure the old table
+// stays in place.
+int sentinel_engine::param_rebuild(uint64_t new_cap, const std::vector<int32_t> &rmap, int32_t new_maxn,
+                                   const std::vector<int32_t> &new_rn, const std::vector<int64_t> &imp,
+                                   int64_t imp_stride, const std::vector<int32_t> &imp_rule,
+                                   std::vector<std::pair<int32_t, std::vector<int64_t>>> *exported) {
+    const int64_t nstride = header_words(new_maxn);
+    const int64_t ostride = header_words(pmax_n);
+    DevBuf nkeys, nrule, nstate, nn, nw, nrcp, nIs, nthr, nkind, dmap, dnewest, dcount, dxout, dimp, dimprule, dnrn;
+    auto cleanup = [&] {
+        for (DevBuf *b : {&nkeys, &nrule, &nstate, &nn, &nw, &nrcp, &nIs, &nthr, &nkind, &dmap, &dnewest, &dcount, &dxout,
+                          &dimp, &dimprule, &dnrn})
+            b->release();
+    };
+    int rc = 0;
+    rc |= nkeys.ensure(new_cap * 8);
+    rc |= nrule.ensure(new_cap * 4);
+    rc |= nstate.ensure(new_cap * (uint64_t)nstride * 8);
+    rc |= nn.ensure(new_cap * 4);
+    rc |= nw.ensure(new_cap * 4);
+    rc |= nrcp.ensure(new_cap * 8);
+    rc |= nIs.ensure(new_cap * 8);
+    rc |= nthr.ensure(new_cap * 8);
+    rc |= nkind.ensure(new_cap);
+    rc |= dcount.ensure(16);
+    if (rc) { cleanup(); return SENTINEL_E_NOMEM; }
+    const int32_t OR = (int32_t)rmap.size();
+    bool any_export = false;
+    for (int32_t m : rmap) any_export |= m == -2;
+    const bool have_old = d_ptable.p != nullptr && OR > 0;
+    if (hipMemsetAsync(nkeys.p, 0xFF, new_cap * 8, stream) != hipSuccess || hipMemsetAsync(dcount.p, 0, 16, stream) != hipSuccess) {
+        cleanup();
+        return fail(SENTINEL_E_DEVICE, "memset failed");
+    }
+    k_init_state<<<grid_for((int64_t)new_cap), 256, 0, stream>>>(nstate.as<int64_t>(), nullptr, nstride, nullptr, new_maxn,
+                                                                 nstride, (int64_t)new_cap);
+    const PSlots N{nkeys.as<unsigned long long>(), nrule.as<int32_t>(), nstate.as<int64_t>(), nstride, new_cap - 1};
+    const PSlots O{d_ptable.as<unsigned long long>(), d_slot_rule.as<int32_t>(), pt.state.as<int64_t>(), ostride, pcap - 1};
+    unsigned long long *live = dcount.as<unsigned long long>();
+    unsigned long long *xcount = live + 1;
+    uint64_t xcap = 0;
+    const int64_t xstride = 2 + 2 * (int64_t)pmax_n;
+    if (have_old) {
+        rc |= upload(dmap, rmap);
+        rc |= dnewest.ensure((size_t)OR * 8);
+        if (any_export) {
+            xcap = pcap;   // every slot could belong to an exported rule
+            rc |= dxout.ensure(xcap * (uint64_t)xstride * 8);
+        }
+        if (rc) { cleanup(); return SENTINEL_E_NOMEM; }
+        (void)hipMemsetAsync(dnewest.p, 0, (size_t)OR * 8, stream);
+        k_ptable_rule_newest<<<grid_for((int64_t)pcap), 256, 0, stream>>>(O, pcap, d_prule_n.as<int32_t>(),
+                                                                         dnewest.as<unsigned long long>());
+        k_ptable_rebuild<<<grid_for((int64_t)pcap), 256, 0, stream>>>(O, pcap, dmap.as<int32_t>(), d_prule_n.as<int32_t>(),
+                                                                     dnewest.as<unsigned long long>(), N, live,
+                                                                     dxout.as<int64_t>(), xstride, xcount, xcap);
+    }
+    const int64_t K = imp_stride > 0 ? (int64_t)imp.size() / imp_stride : 0;
+    if (K > 0) {
+        rc |= upload(dimp, imp);
+        rc |= upload(dimprule, imp_rule);
+        rc |= upload(dnrn, new_rn);
+        if (rc) { cleanup(); return SENTINEL_E_NOMEM; }
+        k_ptable_import<<<grid_for(K), 256, 0, stream>>>(dimp.as<int64_t>(), imp_stride, K, dimprule.as<int32_t>(),
+                                                        dnrn.as<int32_t>(), N, live);
+    }
+    unsigned long long cnt[2] = {0, 0};
+    if (hipGetLastError() != hipSuccess || hipMemcpyAsync(cnt, dcount.p, 16, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess) {
+        cleanup();
+        return fail(SENTINEL_E_DEVICE, "param table rebuild failed");
+    }
+    if (exported && any_export && cnt[1] > 0) {
+        const uint64_t nx = std::min<uint64_t>(cnt[1], xcap);
+        std::vector<int64_t> x(nx * xstride);
+        if (hipMemcpy(x.data(), dxout.p, x.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) {
+            cleanup();
+            return fail(SENTINEL_E_DEVICE, "param export failed");
+        }
+        for (uint64_t k = 0; k < nx; ++k) {
+            const int64_t *r = x.data() + k * xstride;
+            const int32_t orule = (int32_t)r[1];
+            const int n = h_prule_n[orule];
+            auto it = std::find_if(exported->begin(), exported->end(), [&](auto &p) { return p.first == orule; });
+            if (it == exported->end()) { exported->emplace_back(orule, std::vector<int64_t>()); it = exported->end() - 1; }
+            it->second.insert(it->second.end(), r, r + 2 + 2 * n);
+        }
+    }
+    std::swap(d_ptable, nkeys);
+    std::swap(d_slot_rule, nrule);
+    std::swap(pt.state, nstate);
+    std::swap(pt.n, nn);
+    std::swap(pt.w, nw);
+    std::swap(pt.rcp, nrcp);
+    std::swap(pt.Is, nIs);
+    std::swap(pt.thr, nthr);
+    std::swap(pt.kind, nkind);
+    cleanup();
+    if (!d_pfresh.p && d_pfresh.ensure(8)) return SENTINEL_E_NOMEM;
+    HIP_OK(hipMemsetAsync(d_pfresh.p, 0, 8, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    pcap = new_cap;
+    pmax_n = new_maxn;
+    p_live = cnt[0];
+    p_ub = 0;
+    ++p_rebuilds;
+    return 0;
+}
+
+// Room for nv more values before a batch: the table never holds more than 3/4 of its slots, so a
+// slot insert cannot fail.  The bound is tracked without a device read (values submitted since the
+// last rebuild); only when it could be crossed the exact count is read, dead slots are reclaimed, and
+// the table grows if the live slots still leave too little room.
+int sentinel_engine::param_reserve(int64_t nv) {
+    if (!d_ptable.p) return 0;
+    const uint64_t lim = pcap / 4 * 3;
+    if (p_live + p_ub + (uint64_t)nv <= lim) { p_ub += (uint64_t)nv; return 0; }
+    unsigned long long fresh = 0;
+    HIP_OK(hipMemcpyAsync(&fresh, d_pfresh.p, 8, hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    if (p_live + fresh + (uint64_t)nv <= lim) { p_live += fresh; p_ub = (uint64_t)nv; HIP_OK(hipMemsetAsync(d_pfresh.p, 0, 8, stream)); return 0; }
+    std::vector<int32_t> ident(prules.size());
+    for (size_t i = 0; i < ident.size(); ++i) ident[i] = (int32_t)i;
+    int rc = param_rebuild(pcap, ident, pmax_n, h_prule_n, {}, 0, {}, nullptr);        // reclaim dead slots
+    if (rc) return rc;
+    uint64_t cap = pcap;
+    while (p_live + (uint64_t)nv > cap / 4 * 3) cap <<= 1;
+    if (cap != pcap) {
+        rc = param_rebuild(cap, ident, pmax_n, h_prule_n, {}, 0, {}, nullptr);         // grow
+        if (rc) return rc;
+    }
+    p_ub = (uint64_t)nv;
+    return 0;
+}
+
+// Server window change: every param metric (orphans included) restarts with the server window
+// (ClusterParamMetricStatistics.resetFlowMetrics, ClusterParamMetricStatistics.java:60-66).
+int sentinel_engine::reset_param_metrics(int32_t sample_count, int32_t interval_ms) {
+    for (auto &kv : porphans) {
+        kv.second.n = sample_count;
+        kv.second.interval = interval_ms;
+        kv.second.recs.clear();
+    }
+    const size_t R = prules.size();
+    if (R == 0) return 0;
+    h_prule_n.assign(R, sample_count);
+    h_prule_interval.assign(R, interval_ms);
+    std::vector<int32_t> ww(R, interval_ms / sample_count);
+    std::vector<double> rcp(R, 1.0 / (double)(interval_ms / sample_count)), Is(R, interval_ms / 1000.0);
+    int rc = 0;
+    rc |= upload(d_prule_n, h_prule_n);
+    rc |= upload(d_prule_w, ww);
+    rc |= upload(d_prule_rcp, rcp);
+    rc |= upload(d_prule_Is, Is);
+    if (rc) return rc;
+    pmax_n = sample_count;
+    if (d_ptable.p) {
+        rc = param_rebuild(pcap, std::vector<int32_t>(R, -1), pmax_n, h_prule_n, {}, 0, {}, nullptr);
+        if (rc) return rc;
+    }
+    return rebuild_cm();
 }
 
 // Count-min cells for every param rule, zeroed (count 0 = nothing counted).
@@ -722,7 +994,16 @@ int sentinel_engine::rebuild_cm() {
 // Host mirror of ClusterFlowChecker.calcGlobalThreshold * exceedCount (CFC:38-48, 68) and
 // SimpleClusterFlowChecker (SCFC:42), evaluated in double exactly as Java does.
 int sentinel_engine::rebuild_flow_thresholds() {
-    std::vector<double> thr(rules.size());
+    std::vector<double> thr, cthr;
+    flow_thresholds(rules, thr, cthr);
+    int rc = upload(ft.thr, thr);
+    if (rc) return rc;
+    return upload(d_conc_thr, cthr);
+}
+
+void sentinel_engine::flow_thresholds(const std::vector<sentinel_flow_rule_t> &rules, std::vector<double> &thr,
+                                      std::vector<double> &cthr) const {
+    thr.assign(rules.size(), 0.0);
     for (size_t i = 0; i < rules.size(); ++i) {
         const sentinel_flow_rule_t &r = rules[i];
         if (r.checker == SENTINEL_CHECKER_SIMPLE) {
@@ -737,22 +1018,21 @@ int sentinel_engine::rebuild_flow_thresholds() {
             thr[i] = g * cfg.exceed_count;
         }
     }
-    int rc = upload(ft.thr, thr);
-    if (rc) return rc;
     // ConcurrentClusterFlowChecker.calcGlobalThreshold (CCFC:35-46): no exceedCount
-    std::vector<double> cthr(std::max<size_t>(rules.size(), 1), 0.0);
+    cthr.assign(std::max<size_t>(rules.size(), 1), 0.0);
     for (size_t i = 0; i < rules.size(); ++i) {
         const sentinel_flow_rule_t &r = rules[i];
         const int32_t c = (r.namespace_idx >= 0 && r.namespace_idx < (int32_t)ns.size()) ? ns[r.namespace_idx].connected_count : 0;
         cthr[i] = r.threshold_type == SENTINEL_THRESHOLD_GLOBAL ? r.count : r.count * (double)c;
     }
-    return upload(d_conc_thr, cthr);
 }
 
 // Per-rule routing: TOO_MANY_REQUEST for a null namespace, limiter id, or plain.
-int sentinel_engine::rebuild_routes() {
-    std::vector<int32_t> route(rules.size());
-    flow_plain = true;
+// Per-rule routing of a flow table (namespace null -> TOO_MANY_REQUEST, limiter key, or plain);
+// returns whether every flow is plain.
+bool sentinel_engine::flow_routes(const std::vector<sentinel_flow_rule_t> &rules, std::vector<int32_t> &route) const {
+    route.assign(rules.size(), ROUTE_PLAIN);
+    bool plain = true;
     for (size_t i = 0; i < rules.size(); ++i) {
         const sentinel_flow_rule_t &r = rules[i];
         int32_t v = ROUTE_PLAIN;
@@ -761,8 +1041,14 @@ int sentinel_engine::rebuild_routes() {
             else if (h_ns_limiter[r.namespace_idx] >= 0) v = h_ns_limiter[r.namespace_idx];
         }
         route[i] = v;
-        if (v != ROUTE_PLAIN) flow_plain = false;
+        if (v != ROUTE_PLAIN) plain = false;
     }
+    return plain;
+}
+
+int sentinel_engine::rebuild_routes() {
+    std::vector<int32_t> route;
+    flow_plain = flow_routes(rules, route);
     int rc = upload(d_flow_route, route);
     if (rc) return rc;
     std::vector<int32_t> proute(prules.size());
@@ -977,6 +1263,11 @@ static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, u
     int rc = e->ensure_ws(n);
     if (rc) return rc;
     const int32_t R = (int32_t)e->prules.size();
+    if (R > 0 && e->d_ptable.p) {
+        if (s != e->stream) HIP_OK(hipStreamSynchronize(s));
+        rc = e->param_reserve(n);             // room for every value of the batch: never FAIL
+        if (rc) return rc;
+    }
     const uint64_t P = e->pcap;
     const int pbits = bits_for((int64_t)P);
     const uint32_t pinvalid = ((uint32_t)1 << pbits) - 1;
@@ -991,7 +1282,8 @@ static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, u
     e->launch("param_prep", n, s, [&] {
         k_param_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
             n, ev, have ? R : 0, e->param_plain ? nullptr : e->d_prule_route.as<int32_t>(),
-            e->d_ptable.as<unsigned long long>(), P - 1, e->d_slot_rule.as<int32_t>(), out, fkey, pinvalid,
+            e->d_ptable.as<unsigned long long>(), P - 1, e->d_slot_rule.as<int32_t>(),
+            e->d_pfresh.as<unsigned long long>(), out, fkey, pinvalid,
             1, e->w_fhist.as<uint32_t>(), lkey, linvalid, 1, e->w_lhist.as<uint32_t>(), nb);
     });
     if (!have) {
@@ -1047,6 +1339,11 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
     const int64_t nb = sort_blocks(n);
     const ParamEvent *evp = pev ? pev : (const ParamEvent *)mev;
     const ValueSrc vs{pev, mev, values, nv};
+    if (mode == PMODE_EXACT && R > 0) {
+        if (s != e->stream) HIP_OK(hipStreamSynchronize(s));
+        rc = e->param_reserve(nv);            // room for every value of the batch: never FAIL
+        if (rc) return rc;
+    }
     const ParamCtx C = e->param_ctx();
     unsigned long long *table = nullptr;
     uint64_t mask = 0;
@@ -1056,12 +1353,13 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
     e->launch("prule_prep", n, s, [&] {
         if (local)
             k_prule_prep<true><<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
-                n, evp, vs, R, e->d_lrule_valid.as<uint8_t>(), nullptr, C.R, table, mask, SlotMeta{}, e->w_vslot.as<uint32_t>(), out,
+                n, evp, vs, R, e->d_lrule_valid.as<uint8_t>(), nullptr, C.R, table, mask, nullptr, SlotMeta{},
+                e->w_vslot.as<uint32_t>(), out,
                 fkey, rinvalid, e->w_fhist.as<uint32_t>(), nullptr, linvalid, e->w_lhist.as<uint32_t>(), nb);
         else
             k_prule_prep<false><<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
                 n, evp, vs, R, nullptr, e->param_plain ? nullptr : e->d_prule_route.as<int32_t>(), C.R, table, mask,
-                e->slot_meta(), e->w_vslot.as<uint32_t>(), out, fkey, rinvalid, e->w_fhist.as<uint32_t>(), lkey, linvalid,
+                e->d_pfresh.as<unsigned long long>(), e->slot_meta(), e->w_vslot.as<uint32_t>(), out, fkey, rinvalid, e->w_fhist.as<uint32_t>(), lkey, linvalid,
                 e->w_lhist.as<uint32_t>(), nb);
     });
     if (R == 0) {
@@ -1336,117 +1634,253 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
     HIP_OK(hipStreamSynchronize(e->stream));
-    // keep the old state to carry metrics of surviving flowIds (putMetricIfAbsent, CFRM:361)
-    std::unordered_map<int64_t, int32_t> old_index = e->flow_index;
-    std::vector<int64_t> old_off = e->h_flow_off;
-    std::vector<int32_t> old_n = e->h_flow_n, old_w = e->h_flow_w;
-    std::vector<int64_t> old_state;
-    if (e->flow_state_words > 0 && !old_index.empty()) {
-        old_state.resize(e->flow_state_words);
-        HIP_OK(hipMemcpy(old_state.data(), e->ft.state.p, old_state.size() * 8, hipMemcpyDeviceToHost));
-    }
-    std::vector<int32_t> old_now(old_index.size(), 0);
-    if (!old_index.empty() && e->d_now.p)
-        HIP_OK(hipMemcpy(old_now.data(), e->d_now.p, old_now.size() * 4, hipMemcpyDeviceToHost));
-    std::vector<int64_t> old_occ(2 * old_index.size());
-    std::vector<uint8_t> old_hocc(old_index.size());
-    if (!old_index.empty()) {
-        HIP_OK(hipMemcpy(old_occ.data(), e->ft.occ.p, old_occ.size() * 8, hipMemcpyDeviceToHost));
-        HIP_OK(hipMemcpy(old_hocc.data(), e->ft.has_occ.p, old_hocc.size(), hipMemcpyDeviceToHost));
-    }
-
-    e->rules.clear();
-    e->flow_index.clear();
+    // ClusterFlowRuleManager.applyClusterFlowRule (CFRM:325-372) over every namespace at once.
+    // Raw list size per namespace group: an emptied list keeps its flows' metrics (CFRM:268-283).
+    std::unordered_map<int32_t, int64_t> raw_ns;
+    auto group = [&](int32_t nsi) { return (nsi >= 0 && nsi < (int32_t)e->ns.size()) ? nsi : -1; };
+    for (int32_t i = 0; i < n; ++i) raw_ns[group(rules[i].namespace_idx)]++;
+    // valid rules (FlowRuleUtil.isValidRule, FlowRuleUtil.java:184-231) deduplicated by flowId:
+    // ruleMap.put keeps the last rule, the dense index is the first position; putMetricIfAbsent
+    // (CFRM:361-362) runs in list order, so a new flowId gets its first occurrence's window
+    std::vector<sentinel_flow_rule_t> nr;
+    std::unordered_map<int64_t, int32_t> nidx;
+    std::vector<int32_t> gn, gint;
     for (int32_t i = 0; i < n; ++i) {
         const sentinel_flow_rule_t &r = rules[i];
-        // FlowRuleUtil.isValidRule / checkClusterField (FlowRuleUtil.java:184-227)
         if (r.flow_id <= 0 || !(r.count >= 0) || !valid_window(r.sample_count, r.window_interval_ms)) continue;
-        auto it = e->flow_index.find(r.flow_id);
-        if (it != e->flow_index.end()) { e->rules[it->second] = r; continue; }   // ruleMap.put: last wins
-        e->flow_index.emplace(r.flow_id, (int32_t)e->rules.size());
-        e->rules.push_back(r);
+        auto it = nidx.find(r.flow_id);
+        if (it != nidx.end()) { nr[it->second] = r; continue; }
+        nidx.emplace(r.flow_id, (int32_t)nr.size());
+        nr.push_back(r);
+        gn.push_back(r.sample_count);
+        gint.push_back(r.window_interval_ms);
     }
-    const size_t F = e->rules.size();
-    std::vector<int64_t> off(F), ids(F);
-    std::vector<int32_t> nn(F), ww(F);
-    std::vector<double> rcp(F), Is(F);
-    std::vector<uint8_t> kind(F);
-    // layout: blocked slot-major header region (HB_KEYS flows x hblock slots per block), then the
-    // blocked rest region (per block and slot, six counter rows of HB_KEYS flows); off[i] = flow i's
-    // counter-0 slot-0 word of the rest region
+    const size_t F = nr.size();
+    if (F > (size_t)INT32_MAX / 2) return fail(SENTINEL_E_INVALID, "too many flow rules");
+    // where each flow's metric comes from: an existing flow (old window and counters), an orphaned
+    // metric of the same flowId, or a fresh one
+    std::vector<int32_t> src(F, -1);
+    std::vector<int64_t> stg, stg_off(F, -1);
+    for (size_t i = 0; i < F; ++i) {
+        const int64_t fid = nr[i].flow_id;
+        auto it = e->flow_index.find(fid);
+        if (it != e->flow_index.end()) {
+            src[i] = it->second;
+            gn[i] = e->h_flow_n[it->second];
+            gint[i] = e->h_flow_interval[it->second];
+            continue;
+        }
+        auto o = e->orphans.find(fid);
+        if (o != e->orphans.end()) {
+            src[i] = -2;
+            gn[i] = o->second.n;
+            gint[i] = o->second.interval;
+            stg_off[i] = (int64_t)stg.size();
+            stg.insert(stg.end(), o->second.rec.begin(), o->second.rec.end());
+        }
+    }
+    // flows that leave: their metric goes away (clearAndResetRulesConditional -> removeMetric,
+    // CFRM:285-301) unless their namespace's list is empty
+    std::vector<int32_t> orphan_old;
+    for (size_t o = 0; o < e->rules.size(); ++o) {
+        const sentinel_flow_rule_t &r = e->rules[o];
+        if (nidx.count(r.flow_id)) continue;
+        auto c = raw_ns.find(group(r.namespace_idx));
+        if (c == raw_ns.end() || c->second == 0) orphan_old.push_back((int32_t)o);
+    }
+    return e->install_flows(std::move(nr), std::move(nidx), std::move(gn), std::move(gint), std::move(src),
+                            std::move(stg), std::move(stg_off), orphan_old);
+}
+
+// Builds the new flow table on the device (every buffer fresh), remaps the window state of the old
+// one, then swaps it in: on any failure the engine keeps its previous table untouched.
+int sentinel_engine::install_flows(std::vector<sentinel_flow_rule_t> &&nr, std::unordered_map<int64_t, int32_t> &&nidx,
+                                   std::vector<int32_t> &&gn, std::vector<int32_t> &&gint, std::vector<int32_t> &&src,
+                                   std::vector<int64_t> &&stg, std::vector<int64_t> &&stg_off,
+                                   const std::vector<int32_t> &orphan_old) {
+    const size_t F = nr.size();
+    const size_t F1 = std::max<size_t>(F, 1);
+    std::vector<int64_t> off(F1, 0), ids(F1, 0);
+    std::vector<int32_t> ww(F1, 1);
+    std::vector<double> rcp(F1, 1.0), Is(F1, 1.0);
+    std::vector<uint8_t> kind(F1, KIND_CLUSTER);
     int32_t maxn = 1;
-    for (size_t i = 0; i < F; ++i) maxn = std::max(maxn, e->rules[i].sample_count);
+    for (size_t i = 0; i < F; ++i) maxn = std::max(maxn, gn[i]);
+    // layout: blocked slot-major header region (HB_KEYS flows x hblock slots per block), then the
+    // blocked rest region (per block and slot, six counter rows of HB_KEYS flows)
     const int32_t hblock = header_block_slots(maxn);
     const int64_t nblk = ((int64_t)F + HB_KEYS - 1) / HB_KEYS;
     const int64_t hwords = nblk * hblock * HB_KEYS * 2;
-    const int64_t words = hwords + nblk * hblock * 6 * HB_KEYS;
+    const int64_t words = std::max<int64_t>(hwords + nblk * hblock * 6 * HB_KEYS, 1);
     for (size_t i = 0; i < F; ++i) {
-        const sentinel_flow_rule_t &r = e->rules[i];
         off[i] = hwords + blocked_rest_word((int64_t)i, hblock, 0, 0);
-        nn[i] = r.sample_count;
-        ww[i] = r.window_interval_ms / r.sample_count;
+        ww[i] = gint[i] / gn[i];
         rcp[i] = 1.0 / (double)ww[i];
-        Is[i] = r.window_interval_ms / 1000.0;   // LeapArray.java:74
-        kind[i] = r.checker == SENTINEL_CHECKER_SIMPLE ? KIND_SIMPLE : KIND_CLUSTER;
-        ids[i] = r.flow_id;
+        Is[i] = gint[i] / 1000.0;                       // LeapArray.intervalInSecond (LeapArray.java:74)
+        kind[i] = nr[i].checker == SENTINEL_CHECKER_SIMPLE ? KIND_SIMPLE : KIND_CLUSTER;
+        ids[i] = nr[i].flow_id;
     }
-    // new state image: fresh, then carry surviving flows whose window shape is unchanged
-    std::vector<int64_t> st(std::max<int64_t>(words, 1), 0);
-    std::vector<int64_t> occ(2 * std::max<size_t>(F, 1), 0);
-    std::vector<uint8_t> hocc(std::max<size_t>(F, 1), 0);
-    std::vector<int32_t> now(std::max<size_t>(F, 1), 0);
-    const int32_t old_hblock = e->flow_hblock;
-    for (size_t i = 0; i < F; ++i) {
-        for (int j = 0; j < nn[i]; ++j) st[blocked_pair_word((int64_t)i, hblock, j)] = EPOCH_ABSENT;
-        auto it = old_index.find(ids[i]);
-        if (it == old_index.end()) continue;
-        const int32_t o = it->second;
-        now[i] = old_now[o];       // CurrentConcurrencyManager keeps nowCalls of surviving flowIds (CFRM:356-358)
-        // ClusterMetric is kept as constructed with the OLD (n, interval): only carry when equal
-        if (old_n[o] != nn[i] || old_w[o] != ww[i]) continue;
-        for (int j = 0; j < nn[i]; ++j) {
-            const int64_t a = blocked_pair_word((int64_t)o, old_hblock, j), b = blocked_pair_word((int64_t)i, hblock, j);
-            st[b] = old_state[a];
-            st[b + 1] = old_state[a + 1];
-        }
-        for (int j = 0; j < nn[i]; ++j)
-            for (int c = 0; c < 6; ++c)
-                st[off[i] + (int64_t)j * 6 * HB_KEYS + c * HB_KEYS] = old_state[old_off[o] + (int64_t)j * 6 * HB_KEYS + c * HB_KEYS];
-        occ[2 * i] = old_occ[2 * o];
-        occ[2 * i + 1] = old_occ[2 * o + 1];
-        hocc[i] = old_hocc[o];
-    }
+    std::vector<double> thr, cthr;
+    flow_thresholds(nr, thr, cthr);
+    thr.resize(F1, 0.0);
+    std::vector<int32_t> route;
+    const bool plain = flow_routes(nr, route);
+    route.resize(F1, ROUTE_PLAIN);
+    std::vector<int32_t> nnv(gn);
+    nnv.resize(F1, 1);
+    // new device buffers
+    TableBufs nft;
+    DevBuf nroute, nids, nnow, ncthr, s1w, s1r, s1k, dsrc, dstg, dstgoff;
+    auto cleanup = [&] {
+        nft.release();
+        for (DevBuf *b : {&nroute, &nids, &nnow, &ncthr, &s1w, &s1r, &s1k, &dsrc, &dstg, &dstgoff}) b->release();
+    };
     int rc = 0;
-    rc |= upload(e->ft.off, off);
-    rc |= upload(e->ft.n, nn);
-    rc |= upload(e->ft.w, ww);
-    rc |= upload(e->ft.rcp, rcp);
-    rc |= upload(e->ft.Is, Is);
-    rc |= upload(e->ft.kind, kind);
-    rc |= upload(e->ft.state, st);
-    rc |= upload(e->ft.occ, occ);
-    rc |= upload(e->ft.has_occ, hocc);
-    rc |= upload(e->d_flow_ids, ids);
-    rc |= upload(e->d_now, now);
-    rc |= upload(e->d_seg1_w, std::vector<int32_t>(std::max<size_t>(F, 1), 1 << 30));
-    rc |= upload(e->d_seg1_rcp, std::vector<double>(std::max<size_t>(F, 1), 1.0 / (double)(1 << 30)));
-    rc |= upload(e->d_seg1_kind, std::vector<uint8_t>(std::max<size_t>(F, 1), KIND_LOCAL_PARAM));
+    rc |= upload(nft.off, off);
+    rc |= upload(nft.n, nnv);
+    rc |= upload(nft.w, ww);
+    rc |= upload(nft.rcp, rcp);
+    rc |= upload(nft.Is, Is);
+    rc |= upload(nft.kind, kind);
+    rc |= upload(nft.thr, thr);
+    rc |= upload(nroute, route);
+    rc |= upload(nids, ids);
+    rc |= upload(ncthr, cthr);
+    rc |= upload(s1w, std::vector<int32_t>(F1, 1 << 30));
+    rc |= upload(s1r, std::vector<double>(F1, 1.0 / (double)(1 << 30)));
+    rc |= upload(s1k, std::vector<uint8_t>(F1, KIND_LOCAL_PARAM));
+    src.resize(F1, -1);
+    stg_off.resize(F1, -1);
+    if (stg.empty()) stg.push_back(0);
+    rc |= upload(dsrc, src);
+    rc |= upload(dstg, stg);
+    rc |= upload(dstgoff, stg_off);
+    rc |= nft.state.ensure((size_t)words * 8);
+    rc |= nft.occ.ensure(F1 * 16);
+    rc |= nft.has_occ.ensure(F1);
+    rc |= nnow.ensure(F1 * 4);
+    if (rc) { cleanup(); return rc < 0 ? rc : SENTINEL_E_NOMEM; }
+    // orphans of this load: their old records, staged to the host before the old table goes
+    std::vector<Orphan> new_orphans;
+    if (!orphan_old.empty() && ft.state.p) {
+        const int32_t K = (int32_t)orphan_old.size();
+        std::vector<int32_t> on(K);
+        std::vector<int64_t> ooff(K);
+        int64_t tot = 0;
+        for (int32_t k = 0; k < K; ++k) { on[k] = h_flow_n[orphan_old[k]]; ooff[k] = tot; tot += 8 * (int64_t)on[k] + 3; }
+        DevBuf di, dn, doff, dout;
+        rc |= upload(di, orphan_old);
+        rc |= upload(dn, on);
+        rc |= upload(doff, ooff);
+        rc |= dout.ensure((size_t)tot * 8);
+        std::vector<int64_t> recs(tot);
+        if (!rc) {
+            k_flow_gather<<<grid_for(K), 256, 0, stream>>>(ft.state.as<int64_t>(), flow_hblock, flow_rest_base,
+                                                          di.as<int32_t>(), dn.as<int32_t>(), doff.as<int64_t>(), K,
+                                                          ft.occ.as<int64_t>(), ft.has_occ.as<uint8_t>(), dout.as<int64_t>());
+            if (hipGetLastError() != hipSuccess ||
+                hipMemcpyAsync(recs.data(), dout.p, (size_t)tot * 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+                hipStreamSynchronize(stream) != hipSuccess)
+                rc = fail(SENTINEL_E_DEVICE, "orphan gather failed");
+        }
+        for (DevBuf *b : {&di, &dn, &doff, &dout}) b->release();
+        if (rc) { cleanup(); return rc < 0 ? rc : SENTINEL_E_NOMEM; }
+        for (int32_t k = 0; k < K; ++k)
+            new_orphans.push_back(Orphan{on[k], h_flow_interval[orphan_old[k]],
+                                         std::vector<int64_t>(recs.begin() + ooff[k], recs.begin() + ooff[k] + 8 * on[k] + 3)});
+    }
+    if (hipMemsetAsync(nft.state.p, 0, (size_t)words * 8, stream) != hipSuccess) { cleanup(); return fail(SENTINEL_E_DEVICE, "memset failed"); }
+    if (F > 0) {
+        const bool have_old = ft.state.p != nullptr && !rules.empty();
+        k_flow_remap<<<grid_for((int64_t)F), 256, 0, stream>>>(
+            nft.state.as<int64_t>(), hblock, hwords, nft.n.as<int32_t>(), have_old ? ft.state.as<int64_t>() : nullptr,
+            flow_hblock, flow_rest_base, dsrc.as<int32_t>(), dstg.as<int64_t>(), dstgoff.as<int64_t>(),
+            nft.occ.as<int64_t>(), nft.has_occ.as<uint8_t>(), nnow.as<int32_t>(), have_old ? ft.occ.as<int64_t>() : nullptr,
+            have_old ? ft.has_occ.as<uint8_t>() : nullptr, have_old ? d_now.as<int32_t>() : nullptr, (int32_t)F);
+    }
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(stream) != hipSuccess) {
+        cleanup();
+        return fail(SENTINEL_E_DEVICE, "flow remap failed");
+    }
+    // swap the new table in (nothing below can fail), then release the old buffers
+    for (auto &kv : nidx) orphans.erase(kv.first);   // revived orphans left the registry
+    for (size_t k = 0; k < orphan_old.size(); ++k) orphans[rules[orphan_old[k]].flow_id] = std::move(new_orphans[k]);
+    std::swap(ft, nft);
+    std::swap(d_flow_route, nroute);
+    std::swap(d_flow_ids, nids);
+    std::swap(d_now, nnow);
+    std::swap(d_conc_thr, ncthr);
+    std::swap(d_seg1_w, s1w);
+    std::swap(d_seg1_rcp, s1r);
+    std::swap(d_seg1_kind, s1k);
+    cleanup();
+    rules = std::move(nr);
+    flow_index = std::move(nidx);
+    off.resize(F);
+    h_flow_off = std::move(off);
+    h_flow_n = std::move(gn);
+    ww.resize(F);
+    h_flow_w = std::move(ww);
+    h_flow_interval = std::move(gint);
+    flow_state_words = words;
+    flow_hblock = hblock;
+    flow_rest_base = hwords;
+    flow_max_n = maxn;
+    flow_plain = plain;
+    return rewrite_tokens(false);
+}
+
+// ClusterServerConfigManager.applyGlobalFlowConfig with a new server window (ClusterServerConfigManager.java:
+// 333-343): ClusterMetricStatistics.resetFlowMetrics / ClusterParamMetricStatistics.resetFlowMetrics
+// replace every metric -- orphaned ones included -- with a fresh one of the server's window.
+int sentinel_reset_metrics(sentinel_engine_t *e, int32_t sample_count, int32_t interval_ms) {
+    if (!e) return fail(SENTINEL_E_INVALID, "null engine");
+    if (!valid_window(sample_count, interval_ms)) return 0;   // invalid window: ignored (CSCM:335-336)
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    for (auto &kv : e->orphans) {
+        sentinel_engine::Orphan &o = kv.second;
+        o.n = sample_count;
+        o.interval = interval_ms;
+        o.rec.assign(8 * (size_t)sample_count + 3, 0);
+        for (int j = 0; j < sample_count; ++j) o.rec[2 * j] = EPOCH_ABSENT;
+    }
+    const size_t F = e->rules.size();
+    std::vector<sentinel_flow_rule_t> nr = e->rules;
+    std::unordered_map<int64_t, int32_t> nidx = e->flow_index;
+    int rc = e->install_flows(std::move(nr), std::move(nidx), std::vector<int32_t>(F, sample_count),
+                              std::vector<int32_t>(F, interval_ms), std::vector<int32_t>(F, -1), {}, {}, {});
     if (rc) return rc;
-    e->h_flow_off = off;
-    e->h_flow_n = nn;
-    e->h_flow_w = ww;
-    e->flow_state_words = words;
-    e->flow_hblock = hblock;
-    e->flow_rest_base = hwords;
-    e->flow_max_n = nn.empty() ? 1 : *std::max_element(nn.begin(), nn.end());
-    rc = e->rewrite_tokens(false);
-    if (rc) return rc;
-    rc = e->rebuild_routes();
-    if (rc) return rc;
-    return e->rebuild_flow_thresholds();
+    return e->reset_param_metrics(sample_count, interval_ms);
+}
+
+int sentinel_flow_window(sentinel_engine_t *e, int32_t idx, int32_t *sample_count, int32_t *interval_ms) {
+    if (!e || !sample_count || !interval_ms) return fail(SENTINEL_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(e->mu);
+    if (idx < 0 || idx >= (int32_t)e->rules.size()) return fail(SENTINEL_E_INVALID, "bad flow index");
+    *sample_count = e->h_flow_n[idx];
+    *interval_ms = e->h_flow_interval[idx];
+    return 0;
+}
+
+int sentinel_param_table_stats(sentinel_engine_t *e, int64_t *out3) {
+    if (!e || !out3) return fail(SENTINEL_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(e->mu);
+    out3[0] = e->d_ptable.p ? (int64_t)e->pcap : 0;
+    out3[1] = (int64_t)e->p_live;
+    out3[2] = (int64_t)e->p_rebuilds;
+    return 0;
+}
+
+int64_t sentinel_metric_count(sentinel_engine_t *e) {
+    if (!e) return fail(SENTINEL_E_INVALID, "null engine");
+    std::lock_guard<std::mutex> g(e->mu);
+    return (int64_t)e->rules.size() + (int64_t)e->orphans.size();
 }
 
 int32_t sentinel_flow_count(sentinel_engine_t *e) { return e ? (int32_t)e->rules.size() : 0; }
+int32_t sentinel_param_count(sentinel_engine_t *e) { return e ? (int32_t)e->prules.size() : 0; }
 
 int sentinel_lookup_flow_idx(sentinel_engine_t *e, int64_t n, const int64_t *ids, int32_t *out) {
     if (!e || n < 0 || (n > 0 && (!ids || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
@@ -1468,6 +1902,12 @@ int sentinel_lookup_param_idx(sentinel_engine_t *e, int64_t n, const int64_t *id
     return 0;
 }
 
+// ClusterParamFlowRuleManager.applyClusterParamRules (ClusterParamFlowRuleManager.java:318-360) over every
+// namespace at once, with the flow table's reload semantics: valid rules deduplicated by flowId (the
+// last rule wins, the first position keeps the dense index); putMetricIfAbsent (:355-356) keeps the
+// metric -- window, per-value counters -- of a flowId present before and after; a flowId that left
+// loses its metric unless its namespace's list is empty (the metric is kept aside and comes back with
+// the flowId).
 int sentinel_load_param_rules(sentinel_engine_t *e, const sentinel_param_rule_t *rules, int32_t n,
                               const uint64_t *hot_keys, const int32_t *hot_counts, int32_t n_hot) {
     if (!e || n < 0 || (n > 0 && !rules) || n_hot < 0 || (n_hot > 0 && (!hot_keys || !hot_counts)))
@@ -1475,39 +1915,103 @@ int sentinel_load_param_rules(sentinel_engine_t *e, const sentinel_param_rule_t 
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
     HIP_OK(hipStreamSynchronize(e->stream));
-    e->prules.clear();
-    e->param_index.clear();
-    std::vector<int32_t> nn, ww;
-    std::vector<double> rcp, Is, thr;
-    std::vector<std::pair<uint64_t, double>> hot;
-    int32_t maxn = 1;
+    for (int32_t i = 0; i < n; ++i)
+        if (rules[i].hot_n < 0 || (rules[i].hot_n > 0 && (rules[i].hot_begin < 0 || rules[i].hot_begin + rules[i].hot_n > n_hot)))
+            return fail(SENTINEL_E_INVALID, "hot item range out of bounds");
+    std::unordered_map<int32_t, int64_t> raw_ns;
+    auto group = [&](int32_t nsi) { return (nsi >= 0 && nsi < (int32_t)e->ns.size()) ? nsi : -1; };
+    for (int32_t i = 0; i < n; ++i) raw_ns[group(rules[i].namespace_idx)]++;
+    std::vector<sentinel_param_rule_t> nr;
+    std::unordered_map<int64_t, int32_t> nidx;
+    std::vector<int32_t> gn, gint;
     for (int32_t i = 0; i < n; ++i) {
         const sentinel_param_rule_t &r = rules[i];
+        // ParamFlowRuleUtil.isValidRule (ParamFlowRuleUtil.java:46-67): count >= 0, window, flowId > 0
         if (r.flow_id <= 0 || !(r.count >= 0) || !valid_window(r.sample_count, r.window_interval_ms)) continue;
-        if (e->param_index.count(r.flow_id)) continue;
-        e->param_index.emplace(r.flow_id, (int32_t)e->prules.size());
-        e->prules.push_back(r);
-        nn.push_back(r.sample_count);
-        ww.push_back(r.window_interval_ms / r.sample_count);
-        rcp.push_back(1.0 / (double)ww.back());
-        Is.push_back(r.window_interval_ms / 1000.0);
+        auto it = nidx.find(r.flow_id);
+        if (it != nidx.end()) { nr[it->second] = r; continue; }
+        nidx.emplace(r.flow_id, (int32_t)nr.size());
+        nr.push_back(r);
+        gn.push_back(r.sample_count);
+        gint.push_back(r.window_interval_ms);
+    }
+    const size_t R = nr.size();
+    // old rule -> new rule (>= 0), dropped (-1) or orphaned (-2); orphans coming back are imported
+    std::vector<int32_t> rmap(e->prules.size(), -1);
+    for (size_t o = 0; o < e->prules.size(); ++o) {
+        const sentinel_param_rule_t &r = e->prules[o];
+        auto it = nidx.find(r.flow_id);
+        if (it != nidx.end()) {
+            rmap[o] = it->second;
+            gn[it->second] = e->h_prule_n[o];
+            gint[it->second] = e->h_prule_interval[o];
+            continue;
+        }
+        auto c = raw_ns.find(group(r.namespace_idx));
+        if (c == raw_ns.end() || c->second == 0) rmap[o] = -2;
+    }
+    std::vector<int64_t> imp;
+    std::vector<int32_t> imp_rule;
+    std::vector<int64_t> revived;
+    int32_t maxn = 1;
+    for (size_t i = 0; i < R; ++i) {
+        auto o = e->porphans.find(nr[i].flow_id);
+        if (o != e->porphans.end() && !std::any_of(rmap.begin(), rmap.end(), [&](int32_t m) { return m == (int32_t)i; })) {
+            gn[i] = o->second.n;
+            gint[i] = o->second.interval;
+            revived.push_back(nr[i].flow_id);
+        }
+        maxn = std::max(maxn, gn[i]);
+    }
+    // imported records are re-strided to the new table: (2 + 2 maxn) words each
+    const int64_t istride = 2 + 2 * (int64_t)maxn;
+    for (int64_t fid : revived) {
+        const sentinel_engine::POrphan &o = e->porphans[fid];
+        const int64_t rs = 2 + 2 * (int64_t)o.n;
+        for (size_t k = 0; k + rs <= o.recs.size(); k += rs) {
+            imp.insert(imp.end(), o.recs.begin() + k, o.recs.begin() + k + rs);
+            imp.resize(imp.size() + (istride - rs), 0);
+            imp_rule.push_back(nidx[fid]);
+        }
+    }
+    std::vector<int32_t> ww(std::max<size_t>(R, 1), 1);
+    std::vector<double> rcp(std::max<size_t>(R, 1), 1.0), Is(std::max<size_t>(R, 1), 1.0), thr(std::max<size_t>(R, 1), 0.0);
+    std::vector<std::pair<uint64_t, double>> hot;
+    for (size_t i = 0; i < R; ++i) {
+        const sentinel_param_rule_t &r = nr[i];
+        ww[i] = gint[i] / gn[i];
+        rcp[i] = 1.0 / (double)ww[i];
+        Is[i] = gint[i] / 1000.0;
         // calcGlobalThreshold(rule, value) without hot item: count or count*connectedCount (CPFC:101-111)
         const int32_t cc = (r.namespace_idx >= 0 && r.namespace_idx < (int32_t)e->ns.size()) ? e->ns[r.namespace_idx].connected_count : 0;
         double c = r.count;
         if (r.threshold_type != SENTINEL_THRESHOLD_GLOBAL) c = c * (double)cc;
-        thr.push_back(c);
-        maxn = std::max(maxn, r.sample_count);
+        thr[i] = c;
         for (int32_t h = 0; h < r.hot_n; ++h) {
             const int32_t j = r.hot_begin + h;
-            if (j < 0 || j >= n_hot) return fail(SENTINEL_E_INVALID, "hot item range out of bounds");
             double hc = (double)hot_counts[j];
             if (r.threshold_type != SENTINEL_THRESHOLD_GLOBAL) hc = hc * (double)cc;
             hot.emplace_back(hot_keys[j], hc);
         }
     }
-    e->pmax_n = maxn;
     int rc = 0;
-    rc |= upload(e->d_prule_n, nn);
+    if (!e->d_pfresh.p) rc |= e->d_pfresh.ensure(8);
+    if (rc) return SENTINEL_E_NOMEM;
+    // the slot table: survivors move to their new index, orphans leave for the host, revived ones return
+    std::vector<std::pair<int32_t, std::vector<int64_t>>> exported;
+    std::vector<int32_t> nn_up(gn);
+    nn_up.resize(std::max<size_t>(R, 1), 1);
+    rc = e->param_rebuild(e->pcap, rmap, maxn, nn_up, imp, istride, imp_rule, &exported);
+    if (rc) return rc;
+    for (int64_t fid : revived) e->porphans.erase(fid);
+    for (size_t o = 0; o < rmap.size(); ++o)
+        if (rmap[o] == -2) e->porphans[e->prules[o].flow_id] = sentinel_engine::POrphan{e->h_prule_n[o], e->h_prule_interval[o], {}};
+    for (auto &x : exported) e->porphans[e->prules[x.first].flow_id].recs = std::move(x.second);
+    e->prules = std::move(nr);
+    e->param_index = std::move(nidx);
+    e->h_prule_n = gn;
+    e->h_prule_interval = gint;
+    rc |= upload(e->d_prule_n, nn_up);
     rc |= upload(e->d_prule_w, ww);
     rc |= upload(e->d_prule_rcp, rcp);
     rc |= upload(e->d_prule_Is, Is);
@@ -1527,22 +2031,7 @@ int sentinel_load_param_rules(sentinel_engine_t *e, const sentinel_param_rule_t 
     e->has_hot = !hot.empty();
     rc |= upload(e->d_hot_table, hk);
     rc |= upload(e->d_hot_thr, hv);
-    // slot table + per-slot state (fresh on every load)
-    const uint64_t P = e->pcap;
-    rc |= e->d_ptable.ensure(P * 8);
-    rc |= e->d_slot_rule.ensure(P * 4);
-    rc |= e->pt.n.ensure(P * 4);
-    rc |= e->pt.w.ensure(P * 4);
-    rc |= e->pt.rcp.ensure(P * 8);
-    rc |= e->pt.Is.ensure(P * 8);
-    rc |= e->pt.thr.ensure(P * 8);
-    rc |= e->pt.kind.ensure(P);
-    const int64_t stride = header_words(maxn);
-    rc |= e->pt.state.ensure(P * stride * 8);
-    if (rc) return SENTINEL_E_NOMEM;
-    rc = upload(e->d_prule_kind, std::vector<uint8_t>(nn.size(), KIND_PARAM));
-    if (rc) return rc;
-    rc = e->clear_param_slots();
+    rc |= upload(e->d_prule_kind, std::vector<uint8_t>(std::max<size_t>(R, 1), KIND_PARAM));
     if (rc) return rc;
     rc = e->rebuild_cm();
     if (rc) return rc;
@@ -2121,9 +2610,8 @@ int sentinel_param_sum(sentinel_engine_t *e, int32_t ridx, uint64_t pkey, int64_
     HIP_OK(hipStreamSynchronize(e->stream));
     *out = 0;
     if (e->pmode == SENTINEL_PARAM_COUNT_MIN) {   // the sketch estimate (min over rows of the window sum)
-        const sentinel_param_rule_t &r = e->prules[ridx];
-        const int n = r.sample_count;
-        const int64_t E = ts / (r.window_interval_ms / n);
+        const int n = e->h_prule_n[ridx];
+        const int64_t E = ts / (e->h_prule_interval[ridx] / n);
         const CountMin C{e->d_cm.as<uint64_t>(), e->cm_depth, e->cm_width, e->pmax_n};
         int64_t est = INT64_MAX;
         std::vector<uint64_t> cell(e->pmax_n);
@@ -2134,18 +2622,17 @@ int sentinel_param_sum(sentinel_engine_t *e, int32_t ridx, uint64_t pkey, int64_
         *out = est;
         return 0;
     }
-    const uint64_t P = e->pcap;
-    std::vector<uint64_t> table(P);
-    HIP_OK(hipMemcpy(table.data(), e->d_ptable.p, P * 8, hipMemcpyDeviceToHost));
-    uint64_t h = mix64(pkey) & (P - 1);
-    for (uint64_t p = 0; p < P; ++p) {
-        if (table[h] == PKEY_EMPTY) return 0;
-        if (table[h] == pkey) break;
-        h = (h + 1) & (P - 1);
-    }
-    const sentinel_param_rule_t &r = e->prules[ridx];
-    const int n = r.sample_count;
-    const int64_t w = r.window_interval_ms / n;
+    if (!e->d_ptable.p) return 0;
+    DevBuf d;
+    if (d.ensure(8)) return SENTINEL_E_NOMEM;
+    k_slot_find_one<<<1, 1, 0, e->stream>>>(e->d_ptable.as<unsigned long long>(), e->pcap - 1, pkey, d.as<int64_t>());
+    int64_t h = -1;
+    HIP_OK(hipMemcpyAsync(&h, d.p, 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    d.release();
+    if (h < 0) return 0;
+    const int n = e->h_prule_n[ridx];                                     // the metric's window
+    const int64_t w = e->h_prule_interval[ridx] / n;
     const int64_t stride = header_words(e->pmax_n);
     std::vector<int64_t> st(2 * n);
     HIP_OK(hipMemcpy(st.data(), e->pt.state.as<int64_t>() + h * stride, st.size() * 8, hipMemcpyDeviceToHost));
@@ -2154,6 +2641,117 @@ int sentinel_param_sum(sentinel_engine_t *e, int32_t ridx, uint64_t pkey, int64_
     for (int j = 0; j < n; ++j)
         if (st[2 * j] != EPOCH_ABSENT && st[2 * j] > E - n && st[2 * j] <= E) s += st[2 * j + 1];
     *out = s;
+    return 0;
+}
+
+// getTopValues(number) of every param rule at ts into device arrays count[R], key[R][number], sum[R][number]
+// (param_table.hpp, k_ptop_*): number rounds of a per-rule selection over the live slots.
+static int param_top(sentinel_engine_t *e, int64_t ts, int32_t number, hipStream_t s, DevBuf &dcount, DevBuf &dkey,
+                     DevBuf &dsum) {
+    const int32_t R = (int32_t)e->prules.size();
+    int rc = 0;
+    rc |= dcount.ensure((size_t)std::max(R, 1) * 4);
+    rc |= dkey.ensure((size_t)std::max(R, 1) * number * 8);
+    rc |= dsum.ensure((size_t)std::max(R, 1) * number * 8);
+    if (rc) return SENTINEL_E_NOMEM;
+    HIP_OK(hipMemsetAsync(dcount.p, 0, (size_t)std::max(R, 1) * 4, s));
+    if (R == 0 || !e->d_ptable.p || e->pmode != SENTINEL_PARAM_EXACT) return 0;
+    const uint64_t cap = e->pcap;
+    DevBuf sums, pr, pk, cr, ck;
+    rc |= sums.ensure(cap * 8);
+    for (DevBuf *b : {&pr, &pk, &cr, &ck}) rc |= b->ensure((size_t)R * 8);
+    if (rc) return SENTINEL_E_NOMEM;
+    const PSlots T{e->d_ptable.as<unsigned long long>(), e->d_slot_rule.as<int32_t>(), e->pt.state.as<int64_t>(),
+                   header_words(e->pmax_n), cap - 1};
+    const unsigned g = grid_for((int64_t)cap);
+    k_ptop_sums<<<g, 256, 0, s>>>(T, cap, e->d_prule_n.as<int32_t>(), e->d_prule_w.as<int32_t>(),
+                                  e->d_prule_rcp.as<double>(), ts, sums.as<int64_t>());
+    HIP_OK(hipMemsetAsync(pr.p, 0, (size_t)R * 8, s));
+    HIP_OK(hipMemsetAsync(pk.p, 0, (size_t)R * 8, s));
+    HIP_OK(hipMemsetAsync(cr.p, 0, (size_t)R * 8, s));
+    HIP_OK(hipMemsetAsync(ck.p, 0xFF, (size_t)R * 8, s));
+    for (int k = 0; k < number; ++k) {
+        k_ptop_best_sum<<<g, 256, 0, s>>>(T, cap, sums.as<int64_t>(), pr.as<unsigned long long>(), pk.as<unsigned long long>(),
+                                         cr.as<unsigned long long>());
+        k_ptop_best_key<<<g, 256, 0, s>>>(T, cap, sums.as<int64_t>(), pr.as<unsigned long long>(), pk.as<unsigned long long>(),
+                                         cr.as<unsigned long long>(), ck.as<unsigned long long>());
+        k_ptop_take<<<g, 256, 0, s>>>(T, cap, sums.as<int64_t>(), cr.as<unsigned long long>(), ck.as<unsigned long long>(), k,
+                                     number, dkey.as<uint64_t>(), dsum.as<int64_t>());
+        k_ptop_advance<<<grid_for(R), 256, 0, s>>>(R, pr.as<unsigned long long>(), pk.as<unsigned long long>(),
+                                                  cr.as<unsigned long long>(), ck.as<unsigned long long>(), dcount.as<int32_t>());
+    }
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(s));        // the temporaries are freed below
+    for (DevBuf *b : {&sums, &pr, &pk, &cr, &ck}) b->release();
+    return 0;
+}
+
+int sentinel_param_top_values(sentinel_engine_t *e, int64_t ts, int32_t number, int32_t *count, uint64_t *keys,
+                              double *avgs) {
+    if (!e || number <= 0 || !count || !keys || !avgs) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    const int32_t R = (int32_t)e->prules.size();
+    DevBuf dc, dk, ds;
+    int rc = param_top(e, ts, number, e->stream, dc, dk, ds);
+    if (rc) return rc;
+    std::vector<int64_t> sum((size_t)R * number);
+    if (R > 0) {
+        HIP_OK(hipMemcpy(count, dc.p, (size_t)R * 4, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(keys, dk.p, (size_t)R * number * 8, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(sum.data(), ds.p, (size_t)R * number * 8, hipMemcpyDeviceToHost));
+    }
+    for (int32_t r = 0; r < R; ++r) {
+        const double I_s = e->h_prule_interval[r] / 1000.0;
+        for (int32_t k = 0; k < number; ++k) {
+            const size_t i = (size_t)r * number + k;
+            avgs[i] = k < count[r] ? (double)sum[i] / I_s : 0.0;     // (double) sum / intervalInSecond
+            if (k >= count[r]) keys[i] = 0;
+        }
+    }
+    return 0;
+}
+
+// ClusterMetricNodeGenerator.paramToMetricNode (ClusterMetricNodeGenerator.java:88-105) for every param rule:
+// {flowId, topParams = getTopValues(5)} records in device memory (the param leg of the RCCL snapshot).
+__global__ __launch_bounds__(256) void k_ptop_records(int32_t R, const int64_t *__restrict__ ids,
+                                                      const int32_t *__restrict__ count, const uint64_t *__restrict__ key,
+                                                      const int64_t *__restrict__ sum, const double *__restrict__ Is,
+                                                      sentinel_param_snapshot_t *__restrict__ out) {
+    const int32_t r = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (r >= R) return;
+    sentinel_param_snapshot_t o;
+    o.flow_id = ids[r];
+    o.n_top = count[r];
+    o.reserved = 0;
+    for (int k = 0; k < SENTINEL_TOP_PARAMS; ++k) {
+        const bool v = k < count[r];
+        o.key[k] = v ? key[(int64_t)r * SENTINEL_TOP_PARAMS + k] : 0;
+        o.avg[k] = v ? (double)sum[(int64_t)r * SENTINEL_TOP_PARAMS + k] / Is[r] : 0.0;
+    }
+    out[r] = o;
+}
+
+int sentinel_param_snapshot_device(sentinel_engine_t *e, int64_t ts, sentinel_param_snapshot_t *d_out, void *stream) {
+    if (!e || !d_out) return fail(SENTINEL_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    const int32_t R = (int32_t)e->prules.size();
+    if (R == 0) return 0;
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    if (s != e->stream) HIP_OK(hipStreamSynchronize(e->stream));
+    DevBuf dc, dk, ds, ids;
+    int rc = param_top(e, ts, SENTINEL_TOP_PARAMS, s, dc, dk, ds);
+    if (rc) return rc;
+    std::vector<int64_t> fid(R);
+    for (int32_t r = 0; r < R; ++r) fid[r] = e->prules[r].flow_id;
+    rc = upload(ids, fid);
+    if (rc) return rc;
+    k_ptop_records<<<grid_for(R), 256, 0, s>>>(R, ids.as<int64_t>(), dc.as<int32_t>(), dk.as<uint64_t>(), ds.as<int64_t>(),
+                                              e->d_prule_Is.as<double>(), d_out);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(s));
     return 0;
 }
 

@@ -122,7 +122,8 @@ __device__ inline double value_threshold(const ParamRules &R, uint32_t rule, uin
 template <bool LOCAL>
 __global__ __launch_bounds__(SORT_THREADS) void k_prule_prep(
     int64_t n, const ParamEvent *__restrict__ ev, ValueSrc vs, int32_t nrules, const uint8_t *__restrict__ rule_valid,
-    const int32_t *__restrict__ route, ParamRules R, unsigned long long *table, uint64_t cap_mask, SlotMeta M,
+    const int32_t *__restrict__ route, ParamRules R, unsigned long long *table, uint64_t cap_mask,
+    unsigned long long *fresh, SlotMeta M,
     uint32_t *__restrict__ vslot, uint64_t *__restrict__ out, uint32_t *__restrict__ fkey, uint32_t finvalid,
     uint32_t *__restrict__ fhist, uint32_t *__restrict__ lkey, uint32_t linvalid, uint32_t *__restrict__ lhist,
     int64_t nblocks) {
@@ -161,7 +162,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_prule_prep(
         if (st == 127 && table) {
             for (int32_t q = 0; q < cnt; ++q) {
                 const uint64_t key = vs.value((int64_t)b + q);
-                const int64_t h = slot_insert(table, cap_mask, key);
+                const int64_t h = slot_insert(table, cap_mask, key, fresh);
                 if (h < 0) { st = ST_FAIL; break; }                    // table full
                 vslot[b + q] = (uint32_t)h;
                 if (!LOCAL) {   // identical values from every writer of this slot

@@ -1,0 +1,234 @@
+// param_table.hpp -- the exact hot-parameter slot table, kept bounded (gfx950).
+//
+// One open-addressing slot per (rule, value) key holds the value's window {epoch, count} x n: the
+// value's entries in the buckets of ClusterParamMetric's leap array (ClusterParamMetric.java:46-82,
+// ClusterParameterLeapArray.java:33-49; one CacheMap<value, LongAdder> per bucket).  The host never
+// lets the table fill up: before a batch whose values could exceed 3/4 of the capacity it rebuilds
+// the table (engine.hip, sentinel_engine::param_reserve), which
+//   * drops dead slots: a slot none of whose buckets can be valid again -- every epoch <= E_r - n,
+//     E_r = the newest epoch of any slot of its rule (every request of rule r rolls its values'
+//     slots to the request's epoch, so E_r = epoch of the rule's latest timestamp) -- reads exactly
+//     like a value with no CacheMap entry (the reference's bucket reset clears the whole map,
+//     CPLA:40-49), given per-rule non-decreasing timestamps (the documented precondition of exact
+//     param parity);
+//   * grows the table when the live slots alone would still exceed the bound;
+//   * carries a rule reload (ClusterParamMetricStatistics.putMetricIfAbsent, ClusterParamFlowRuleManager
+//     .java:355-356): slots of surviving rules move to the rule's new index, slots of removed rules
+//     go, slots of orphaned rules (emptied namespace list) are exported to the host and imported back
+//     if the flowId returns.
+// getTopValues (ClusterParamMetric.java:84-127) for the ClusterMetricNode snapshot is a selection
+// over the live slots of each rule (k_ptop_*).
+#pragma once
+
+#include "admission.hpp"
+
+namespace sentinel {
+
+struct PSlots {
+    unsigned long long *keys;   // PKEY_EMPTY = free
+    int32_t *rule;              // dense param rule index of the slot
+    int64_t *state;             // stride words per slot: {epoch, count} x n
+    int64_t stride;
+    uint64_t mask;              // capacity - 1
+};
+
+// Insert a key known to be absent (a rebuild re-inserts unique keys): linear probing.
+__device__ inline int64_t slot_place(unsigned long long *keys, uint64_t mask, uint64_t key) {
+    uint64_t h = mix64(key) & mask;
+    for (uint64_t probes = 0; probes <= mask; ++probes) {
+        if (atomicCAS(&keys[h], (unsigned long long)PKEY_EMPTY, (unsigned long long)key) == PKEY_EMPTY) return (int64_t)h;
+        h = (h + 1) & mask;
+    }
+    return -1;
+}
+
+__device__ inline int64_t slot_newest(const int64_t *st, int n) {
+    int64_t m = EPOCH_ABSENT;
+    for (int j = 0; j < n; ++j) m = st[2 * j] > m ? st[2 * j] : m;
+    return m;
+}
+
+// Per rule: the newest epoch over its live slots (wave-aggregated when a wave's slots share a rule).
+__global__ __launch_bounds__(256) void k_ptable_rule_newest(PSlots T, uint64_t cap, const int32_t *__restrict__ rn,
+                                                            unsigned long long *__restrict__ newest) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool live = false;
+    int32_t r = 0;
+    int64_t e = EPOCH_ABSENT;
+    if (s < cap && T.keys[s] != PKEY_EMPTY) {
+        r = T.rule[s];
+        e = slot_newest(T.state + (int64_t)s * T.stride, rn[r]);
+        live = e != EPOCH_ABSENT;
+    }
+    const uint64_t act = __builtin_amdgcn_ballot_w64(live);
+    if (!act) return;
+    const int first = __ffsll((unsigned long long)act) - 1;
+    const int32_t r0 = __shfl(r, first, WAVE);
+    const uint64_t same = __builtin_amdgcn_ballot_w64(live && r == r0);
+    if (same == act) {                                    // one rule in the wave: reduce, one atomic
+        int64_t m = live ? e : EPOCH_ABSENT;
+#pragma unroll
+        for (int o = WAVE / 2; o >= 1; o >>= 1) {
+            const int64_t x = __shfl_xor(m, o, WAVE);
+            m = x > m ? x : m;
+        }
+        if ((int)lane_id() == first) atomicMax(&newest[r0], (unsigned long long)(m + 1));
+    } else if (live) {
+        atomicMax(&newest[r], (unsigned long long)(e + 1));
+    }
+}
+
+// Rebuild: every live slot of the old table whose rule survives (rmap[r] >= 0) and which is not dead
+// moves to the new table (pre-initialised: keys free, state absent) under rule rmap[r]; rmap[r] == -2
+// exports the slot (key, old rule, 2n state words) to `xout` (xcount counts them); -1 drops it.
+// newest[r] - 1 = the rule's newest epoch (0: never seen -> nothing is dead).
+__global__ __launch_bounds__(256) void k_ptable_rebuild(PSlots O, uint64_t ocap, const int32_t *__restrict__ rmap,
+                                                        const int32_t *__restrict__ orn,
+                                                        const unsigned long long *__restrict__ newest, PSlots N,
+                                                        unsigned long long *__restrict__ live,
+                                                        int64_t *__restrict__ xout, int64_t xstride,
+                                                        unsigned long long *__restrict__ xcount, uint64_t xcap) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ocap) return;
+    const unsigned long long key = O.keys[s];
+    if (key == PKEY_EMPTY) return;
+    const int32_t r = O.rule[s];
+    const int32_t m = rmap[r];
+    if (m == -1) return;
+    const int n = orn[r];
+    const int64_t *st = O.state + (int64_t)s * O.stride;
+    if (m == -2) {
+        const unsigned long long k = atomicAdd(xcount, 1ull);
+        if (k >= xcap) return;
+        int64_t *x = xout + (int64_t)k * xstride;
+        x[0] = (int64_t)key;
+        x[1] = r;
+        for (int j = 0; j < 2 * n; ++j) x[2 + j] = st[j];
+        return;
+    }
+    const int64_t E = (int64_t)newest[r] - 1;
+    if (newest[r] != 0) {
+        bool valid = false;
+        for (int j = 0; j < n; ++j) valid |= st[2 * j] != EPOCH_ABSENT && st[2 * j] > E - n;
+        if (!valid) return;                               // dead: reads like an absent value
+    }
+    const int64_t h = slot_place(N.keys, N.mask, key);
+    if (h < 0) return;                                    // cannot happen: the new table has room
+    int64_t *d = N.state + h * N.stride;
+    for (int j = 0; j < 2 * n; ++j) d[j] = st[j];
+    N.rule[h] = m;
+    atomicAdd(live, 1ull);
+}
+
+// Import exported slots (k_ptable_rebuild's record format) under rule rule_of[k].
+__global__ __launch_bounds__(256) void k_ptable_import(const int64_t *__restrict__ x, int64_t xstride, int64_t K,
+                                                       const int32_t *__restrict__ rule_of, const int32_t *__restrict__ nn,
+                                                       PSlots N, unsigned long long *__restrict__ live) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= K) return;
+    const int64_t *r = x + k * xstride;
+    const int32_t rule = rule_of[k];
+    const int64_t h = slot_place(N.keys, N.mask, (uint64_t)r[0]);
+    if (h < 0) return;
+    const int n = nn[rule];
+    int64_t *d = N.state + h * N.stride;
+    for (int j = 0; j < 2 * n; ++j) d[j] = r[2 + j];
+    N.rule[h] = rule;
+    atomicAdd(live, 1ull);
+}
+
+// ---------------------------------------------------------------- getTopValues (snapshot)
+// Per live slot at time ts: the value's window sum over its valid buckets (a read-only view equals
+// the sum after currentWindow(): the roll only empties an invalid bucket), and (int) of it, the
+// reference's sort key ((int) b - (int) a, ClusterParamMetric.java:107-113).  Values with no count
+// have no CacheMap entry in the reference and are not candidates.
+__global__ __launch_bounds__(256) void k_ptop_sums(PSlots T, uint64_t cap, const int32_t *__restrict__ rn,
+                                                   const int32_t *__restrict__ rw, const double *__restrict__ rrcp,
+                                                   int64_t ts, int64_t *__restrict__ sum) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= cap) return;
+    int64_t v = 0;
+    if (T.keys[s] != PKEY_EMPTY) {
+        const int32_t r = T.rule[s];
+        const int n = rn[r];
+        const int64_t E = epoch_of(ts, rw[r], rrcp[r]);
+        const int64_t *st = T.state + (int64_t)s * T.stride;
+        for (int j = 0; j < n; ++j)
+            if (st[2 * j] != EPOCH_ABSENT && st[2 * j] > E - n) v = wrap_add(v, st[2 * j + 1]);
+    }
+    sum[s] = v;
+}
+
+// Order (int) sum descending, key ascending; `prev` = the rule's previous pick (none in round 0).
+__device__ inline uint64_t top_rank(int64_t v) { return ((uint64_t)1 << 32) | ((uint32_t)(int32_t)v ^ 0x80000000u); }
+
+__device__ inline bool top_after(uint64_t rk, uint64_t key, uint64_t prk, uint64_t pkey) {
+    return prk == 0 || rk < prk || (rk == prk && key > pkey);
+}
+
+// Round phase A: best (int) sum among the candidates after the previous pick.
+__global__ __launch_bounds__(256) void k_ptop_best_sum(PSlots T, uint64_t cap, const int64_t *__restrict__ sum,
+                                                       const unsigned long long *__restrict__ prev_rank,
+                                                       const unsigned long long *__restrict__ prev_key,
+                                                       unsigned long long *__restrict__ cand_rank) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= cap) return;
+    const unsigned long long key = T.keys[s];
+    if (key == PKEY_EMPTY || sum[s] == 0) return;
+    const int32_t r = T.rule[s];
+    const uint64_t rk = top_rank(sum[s]);
+    if (top_after(rk, key, prev_rank[r], prev_key[r])) atomicMax(&cand_rank[r], (unsigned long long)rk);
+}
+
+// Round phase B: smallest key with that (int) sum (after the previous pick).
+__global__ __launch_bounds__(256) void k_ptop_best_key(PSlots T, uint64_t cap, const int64_t *__restrict__ sum,
+                                                       const unsigned long long *__restrict__ prev_rank,
+                                                       const unsigned long long *__restrict__ prev_key,
+                                                       const unsigned long long *__restrict__ cand_rank,
+                                                       unsigned long long *__restrict__ cand_key) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= cap) return;
+    const unsigned long long key = T.keys[s];
+    if (key == PKEY_EMPTY || sum[s] == 0) return;
+    const int32_t r = T.rule[s];
+    const uint64_t rk = top_rank(sum[s]);
+    if (rk == cand_rank[r] && top_after(rk, key, prev_rank[r], prev_key[r])) atomicMin(&cand_key[r], key);
+}
+
+// Round phase C: the pick's long sum (keys are unique) -> the rule's k-th entry.
+__global__ __launch_bounds__(256) void k_ptop_take(PSlots T, uint64_t cap, const int64_t *__restrict__ sum,
+                                                   const unsigned long long *__restrict__ cand_rank,
+                                                   const unsigned long long *__restrict__ cand_key, int k, int number,
+                                                   uint64_t *__restrict__ out_key, int64_t *__restrict__ out_sum) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= cap) return;
+    const unsigned long long key = T.keys[s];
+    if (key == PKEY_EMPTY || sum[s] == 0) return;
+    const int32_t r = T.rule[s];
+    if (cand_rank[r] != 0 && key == cand_key[r]) {
+        out_key[(int64_t)r * number + k] = key;
+        out_sum[(int64_t)r * number + k] = sum[s];
+    }
+}
+
+// Per rule: advance prev <- cand, reset cand, count the entries found.
+__global__ __launch_bounds__(256) void k_ptop_advance(int32_t R, unsigned long long *__restrict__ prev_rank,
+                                                      unsigned long long *__restrict__ prev_key,
+                                                      unsigned long long *__restrict__ cand_rank,
+                                                      unsigned long long *__restrict__ cand_key,
+                                                      int32_t *__restrict__ count) {
+    const int32_t r = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (r >= R) return;
+    if (cand_rank[r] != 0) {
+        prev_rank[r] = cand_rank[r];
+        prev_key[r] = cand_key[r];
+        count[r] += 1;
+    } else {
+        prev_rank[r] = 1;                                 // exhausted: nothing ranks after this
+        prev_key[r] = ~0ull;
+    }
+    cand_rank[r] = 0;
+    cand_key[r] = ~0ull;
+}
+
+}  // namespace sentinel

@@ -215,8 +215,13 @@ class GpuTokenService:
         check(self._L.sentinel_load_param_rules(self._h, arr, len(rules), _p(hk), _p(hc), len(keys)),
               "load_param_rules")
 
+
     def flow_count(self) -> int:
         return int(self._L.sentinel_flow_count(self._h))
+
+    def param_count(self) -> int:
+        """Dense param rules loaded (valid, one per flowId)."""
+        return int(self._L.sentinel_param_count(self._h))
 
     def lookup_flow_idx(self, flow_ids) -> np.ndarray:
         ids = np.ascontiguousarray(flow_ids, dtype=np.int64)
@@ -485,7 +490,50 @@ class GpuTokenService:
         check(self._L.sentinel_synchronize(self._h), "synchronize")
 
     # ---------------------------------------------------------------- observability
-    def dump_flow(self, idx: int, sample_count: int) -> np.ndarray:
+    def flow_window(self, idx: int):
+        """(sampleCount, intervalMs) of the metric behind flow idx (a reload keeps a surviving flowId's
+        metric, so this can differ from its current rule's window)."""
+        n, iv = C.c_int32(), C.c_int32()
+        check(self._L.sentinel_flow_window(self._h, int(idx), C.byref(n), C.byref(iv)), "flow_window")
+        return n.value, iv.value
+
+    def metric_count(self) -> int:
+        """ClusterMetricStatistics.METRIC_MAP.size() (orphaned metrics included)."""
+        return int(self._L.sentinel_metric_count(self._h))
+
+    def reset_metrics(self, sample_count: int, interval_ms: int):
+        """Server window change: every flow / param metric restarts with this window
+        (ClusterServerConfigManager.java:333-343)."""
+        check(self._L.sentinel_reset_metrics(self._h, int(sample_count), int(interval_ms)), "reset_metrics")
+
+    def param_table_stats(self):
+        """{capacity, live slots after the last rebuild, rebuilds} of the exact param slot table."""
+        out = np.zeros(3, dtype=np.int64)
+        check(self._L.sentinel_param_table_stats(self._h, _p(out)), "param_table_stats")
+        return dict(capacity=int(out[0]), live=int(out[1]), rebuilds=int(out[2]))
+
+    def param_top_values(self, ts: int, number: int = _lib.TOP_PARAMS):
+        """getTopValues(number) of every param rule at ts -> list (per rule index) of [(key, avg)]."""
+        n_rules = self.param_count()
+        cnt = np.zeros(max(n_rules, 1), dtype=np.int32)
+        keys = np.zeros(max(n_rules, 1) * number, dtype=np.uint64)
+        avgs = np.zeros(max(n_rules, 1) * number, dtype=np.float64)
+        check(self._L.sentinel_param_top_values(self._h, int(ts), int(number), _p(cnt), _p(keys), _p(avgs)),
+              "param_top_values")
+        return [[(int(keys[r * number + k]), float(avgs[r * number + k])) for k in range(int(cnt[r]))]
+                for r in range(n_rules)]
+
+    def param_snapshot_device(self, ts: int, out_tensor, stream=None):
+        """paramToMetricNode records (flowId, top-5 params) of every param rule into a device tensor
+        of len(rules) * 96 bytes (PARAM_SNAPSHOT_DTYPE layout)."""
+        s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        check(self._L.sentinel_param_snapshot_device(self._h, int(ts), C.c_void_p(out_tensor.data_ptr()),
+                                                     None if s is None else C.c_void_p(s)), "param_snapshot_device")
+        return out_tensor
+
+    def dump_flow(self, idx: int, sample_count: Optional[int] = None) -> np.ndarray:
+        """Window dump of flow idx (oracle layout); the window is the metric's (flow_window)."""
+        sample_count = self.flow_window(idx)[0]
         out = np.zeros(sample_count * 8 + 8, dtype=np.int64)
         check(self._L.sentinel_dump_flow(self._h, int(idx), _p(out), len(out)), "dump_flow")
         return out

@@ -458,3 +458,12 @@ def test_path_switches_snapshots_and_epoch_gaps(oracle_mod):
         g, go = _norm_dump(svc.dump_flow(f, n), n)
         o, oo = _norm_dump(orc.dump_flow(f), n)
         assert np.array_equal(g, o) and np.array_equal(go, oo), (f, g, o)
+
+
+@pytest.mark.parametrize("batch", [1 << 20, 1 << 22])
+def test_config2_full_size_bitexact(oracle_mod, batch):
+    """BASELINE config 2 at its stated size: 10k flowIds, QPS grade, 1 s / 2-bucket windows, Zipf(1.1)
+    requests at 2x the summed thresholds, acquire 1, batches of 1M and 4M events (two batches, so the
+    second rolls windows the first wrote); bit-exact verdicts and windows on both flow pipelines."""
+    rules, ev = T.config2(2 * batch, seed=2, n_flows=10_000)
+    _compare(_engine(rules), _oracle(oracle_mod, rules), rules, ev, batches=2)
