@@ -1,7 +1,7 @@
-"""bench.py -- token decisions/sec of the MI355X engine on BASELINE config 3.
+"""bench.py -- token decisions/sec of the MI355X engine (BASELINE.json metric and configs).
 
-Workload (BASELINE.json configs[2], the config the headline metric is quoted on): a universe of
-1M flowIds (cluster FlowRules, GLOBAL threshold count ~ U{10..1000}, default cluster window
+Default workload (BASELINE.json configs[2], the config the headline metric is quoted on): a universe
+of 1M flowIds (cluster FlowRules, GLOBAL threshold count ~ U{10..1000}, default cluster window
 sampleCount=10 / windowIntervalMs=1000 -> 10 x 100 ms buckets), hash-sharded over the ranks by
 splitmix64(flowId) mod N.  Every rank decides a fixed 8M-event batch per step over its own flows
 (uniform, acquire 1, monotone timestamps at 2x the shard's summed thresholds): weak scaling, no
@@ -9,8 +9,19 @@ collective on the decision path.  A step = one batch through DefaultTokenService
 semantics (validation, window roll, ClusterFlowChecker admission, verdict write-back), inputs
 already resident in HBM.
 
-Prints ONE JSON line (rank 0).  Extra fields: p99 device batch latency, per-kernel profile,
-the roofline of the dominant kernel, and the CPU oracle ("port") timed on a bounded sample.
+--config selects the other BASELINE configs (their JSON lines go under profiles/, never to the driver):
+  2     10k flowIds, n=2 / 1000 ms, Zipf(1.1) requests, 4M-event batches (configs[1])
+  4     hot-parameter cluster rules: 100k resources x Zipf(1.2) over 1000 Long values, exact counters
+  4cm   the same on the shared count-min sketch (w=2^20, d=4) + the measured false-block rate vs e*N/w
+  5     Envoy RLS rules (SimpleClusterFlowChecker, n=1 / 1000 ms), hitsAddend ~ geometric(0.3) capped at
+        64: heterogeneous acquire -> the sequential per-segment path; plus concurrency-token acquire /
+        release throughput (the thread-grade rules of the config)
+  3lim  config 3 with the namespace GlobalRequestLimiter on (the reference creates one per namespace
+        after any namespace-set change): the radix-sort path
+
+Prints ONE JSON line (rank 0).  Extra fields: p99 batch latency from >= 200 batches of an untimed
+latency loop (device events, and host clock with a synchronize per batch), per-kernel profile, the
+roofline of the dominant kernel, and the CPU oracle ("port") timed on a bounded sample.
 """
 from __future__ import annotations
 
@@ -27,7 +38,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
-# Algorithmic bytes per processed event for each kernel of the pipeline (DESIGN.md "Kernels").
+# Algorithmic bytes per processed event for each kernel of the pipelines (DESIGN.md "Kernels").
 KERNEL_BYTES_PER_EVENT = {
     "flow_prep": 20.0,        # read the 16-B event, write the 4-B sort key (histograms stay in LDS)
     "radix_hist": 4.0,        # read key
@@ -35,12 +46,15 @@ KERNEL_BYTES_PER_EVENT = {
     "scan_tiles": 8.0,
     "scan_add": 8.0,
     "seg_heads": 17.0,        # read key 4 + value 8, write head 4 + homogeneity flag 1
+    "segments": 17.0,         # read key 4 + value 8, write segment id 4 + flag 1 (records are per segment)
     "seg_mark": 5.0,          # read segid 4 + flag 1 (segment records are per segment)
     "verdict": 20.0,          # read segid 4 + value 8, write the 8-B verdict
     "part_prep": 16.0,        # read the 16-B event (range histogram in LDS; no key array without namespace routes)
     "part_scatter": 24.0,     # read the 16-B event (key re-derived), write the 8-B packed value (local key inside)
+    "param_prep": 48.0,       # read the 24-B event, write key 4 + slot rule 4, slot insert (8-B CAS), verdict slot 8
+    "param_meta": 48.0,       # read key 4 + event key 8, rule fields ~16, write the slot's 5 fields (~20 B)
+    "prule_prep": 36.0,       # read the 24-B event + value 8, write key 4
 }
-
 
 # rocprofv3 kernel symbols behind each engine profile name (for the PMC traffic of the roofline).
 KERNEL_SYMBOLS = {
@@ -48,25 +62,59 @@ KERNEL_SYMBOLS = {
     "scan": ("k_scan_lookback",), "segments": ("k_segments",), "process": ("k_process",), "verdict": ("k_verdict",),
     "part_prep": ("k_part_prep",), "part_scatter": ("k_part_scatter",),
     "part_fused": ("k_part_half",), "part_big": ("k_part_big",), "part_long": ("k_part_long",),
+    "param_prep": ("k_param_prep",), "param_meta": ("k_param_meta",), "prule_prep": ("k_prule_prep",),
+    "prule_process": ("k_prule_process",), "part_unsplit": ("k_part_unsplit",),
 }
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
+PMC_DIR = os.path.join(ROOT, "profiles", "pmc")
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this workload
-    (scripts/gpu_round.sh: separate FETCH_SIZE / WRITE_SIZE passes, FETCH doubled on gfx950)."""
+def pmc_traffic(kernel: str, shape: dict):
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary of THIS workload shape
+    (profiles/pmc/*.json written by scripts/pmc_summary.py: separate FETCH_SIZE / WRITE_SIZE passes,
+    FETCH doubled on gfx950); None when no PMC run of this shape exists."""
     try:
-        with open(PMC_SUMMARY) as f:
-            summ = json.load(f)["kernels"]
-    except (OSError, ValueError, KeyError):
-        return None
-    pats = KERNEL_SYMBOLS.get(kernel, ())
-    tot = disp = 0.0
-    for name, v in summ.items():
-        if any(name.startswith(p) for p in pats) and v.get("traffic_bytes_avg"):
-            tot += v["traffic_bytes_avg"] * v["dispatches"]
-            disp += v["dispatches"]
-    return round(tot / disp, 1) if disp else None
+        files = sorted(os.listdir(PMC_DIR))
+    except OSError:
+        return None, None
+    for fn in reversed(files):
+        try:
+            with open(os.path.join(PMC_DIR, fn)) as f:
+                summ = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if summ.get("shape") != shape:
+            continue
+        pats = KERNEL_SYMBOLS.get(kernel, ())
+        tot = disp = 0.0
+        for name, v in summ.get("kernels", {}).items():
+            if any(name.startswith(p) for p in pats) and v.get("traffic_bytes_avg"):
+                tot += v["traffic_bytes_avg"] * v["dispatches"]
+                disp += v["dispatches"]
+        if disp:
+            return round(tot / disp, 1), f"profiles/pmc/{fn}"
+    return None, None
+
+
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count()
+    return model, os.cpu_count(), avail
+
+
+def log(msg):
+    """Progress on stderr (long GPU runs must keep writing)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 def parse():
@@ -74,9 +122,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--events-per-gpu", type=int, default=8 * 1024 * 1024)
-    ap.add_argument("--flows", type=int, default=1_000_000)
-    ap.add_argument("--sample-count", type=int, default=10)
+    ap.add_argument("--config", default="3", choices=["3", "2", "4", "4cm", "5", "3lim"])
+    ap.add_argument("--events-per-gpu", type=int, default=None)
+    ap.add_argument("--flows", type=int, default=None)
+    ap.add_argument("--sample-count", type=int, default=None)
     ap.add_argument("--interval-ms", type=int, default=1000)
     ap.add_argument("--cpu-steps-1core", type=int, default=2)
     ap.add_argument("--cpu-steps-mt", type=int, default=12)
@@ -86,9 +135,256 @@ def parse():
     ap.add_argument("--profile-steps", type=int, default=3)
     ap.add_argument("--kernel-every", type=int, default=2,
                     help="time the dominant kernel with HIP events on every k-th timed step")
+    ap.add_argument("--latency-batches", type=int, default=200,
+                    help="batches of the untimed latency loop (p99 from these, not from the timed steps)")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-fed legs")
-    ap.add_argument("--host-reps", type=int, default=20)
+    ap.add_argument("--host-reps", type=int, default=200)
     return ap.parse_args()
+
+
+class FlowWorkload:
+    """Flow events (sentinel_event_t) of configs 2, 3, 5 and 3lim, generated on the device."""
+
+    def __init__(self, args, world, rank, dev):
+        import torch
+        from sentinel_amd import trace as T
+        import sentinel_amd as sa
+        from sentinel_amd.token_service import ServerNamespace
+        self.T, self.torch, self.dev, self.args = T, torch, dev, args
+        cfg = args.config
+        rng = np.random.default_rng({"3": 3, "3lim": 3, "2": 2, "5": 5}[cfg])
+        if cfg in ("3", "3lim"):
+            flows = args.flows or 1_000_000
+            n = args.sample_count or 10
+            rules = T.make_rules(flows, rng, sample_count=n, window_interval_ms=args.interval_ms)
+            self.N = args.events_per_gpu or 8 * 1024 * 1024
+            self.dist, self.acq_kind, self.workload = "uniform", "ones", (
+                f"config3: {flows} flowIds hash-sharded (splitmix64 mod N), cluster GLOBAL rules count~U{{10..1000}}, "
+                f"n={n} w={args.interval_ms // n}ms, uniform flows, acquire=1, 2x offered load"
+                + (", namespace GlobalRequestLimiter on (cap 1e15/s)" if cfg == "3lim" else ""))
+        elif cfg == "2":
+            flows = args.flows or 10_000
+            n = args.sample_count or 2
+            rules = T.make_rules(flows, rng, sample_count=n, window_interval_ms=args.interval_ms)
+            self.N = args.events_per_gpu or 4 * 1024 * 1024
+            self.dist, self.acq_kind, self.workload = "zipf1.1", "ones", (
+                f"config2: {flows} flowIds, cluster GLOBAL rules count~U{{10..1000}}, n={n} w={args.interval_ms // n}ms, "
+                f"Zipf(1.1) requests, acquire=1, 2x offered load, {self.N}-event batches")
+        else:
+            flows = args.flows or 20_000
+            rules = T.make_rules(flows, rng, count_lo=50, count_hi=5000, sample_count=1, window_interval_ms=1000, checker=1)
+            self.N = args.events_per_gpu or 4 * 1024 * 1024
+            self.dist, self.acq_kind, self.workload = "zipf1.1", "geometric", (
+                f"config5: {flows} Envoy RLS rules (SimpleClusterFlowChecker, n=1 w=1000ms, GLOBAL), Zipf(1.1) "
+                f"descriptors, hitsAddend~geometric(0.3) capped at 64 (heterogeneous acquire: sequential path), "
+                f"2x offered load")
+        mine = np.nonzero(T.shard_of(rules.flow_id, world) == rank)[0] if world > 1 else np.arange(len(rules))
+        self.rules = rules.subset(mine)
+        self.F = len(self.rules)
+        self.namespaces = [dict(connected_count=1, has_limiter=1, max_allowed_qps=1e15)] if cfg == "3lim" else None
+        self.svc = sa.GpuTokenService(dev.index or 0)
+        if self.namespaces:
+            self.svc.set_namespaces([ServerNamespace(**x) for x in self.namespaces])
+        r = self.rules
+        self.svc.load_rules_array(r.flow_id, r.count, r.threshold_type, r.sample_count, r.window_interval_ms,
+                                  r.namespace, r.checker)
+        mean_acq = 1.0 if self.acq_kind == "ones" else 2.81
+        self.rate = 2.0 * float(r.count.sum()) / mean_acq          # offered events per second
+        self.ms_per_event = 1000.0 / self.rate
+        self.gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+        if self.dist.startswith("zipf"):
+            w = 1.0 / np.power(np.arange(1, self.F + 1, dtype=np.float64), 1.1)
+            perm = np.random.default_rng(7 + rank).permutation(self.F)
+            self.zipf_cdf = torch.from_numpy(np.cumsum(w) / w.sum()).to(dev)
+            self.zipf_perm = torch.from_numpy(perm.astype(np.int32)).to(dev)
+        self.verdicts = torch.empty(self.N, dtype=torch.int64, device=dev)
+
+    def batch(self, s):
+        """Step s's events (device tensor (N, 2) int64): consecutive in time across steps."""
+        torch, N = self.torch, self.N
+        if self.dist == "uniform":
+            idx = torch.randint(0, self.F, (N,), dtype=torch.int32, device=self.dev, generator=self.gen)
+        else:
+            u = torch.rand(N, dtype=torch.float64, device=self.dev, generator=self.gen)
+            idx = self.zipf_perm[torch.clamp(torch.searchsorted(self.zipf_cdf, u, right=True), max=self.F - 1)]
+        if self.acq_kind == "ones":
+            acq = torch.ones(N, dtype=torch.int32, device=self.dev)
+        else:   # geometric(0.3) capped at 64: floor(log(U) / log(0.7)) + 1
+            u = torch.rand(N, dtype=torch.float64, device=self.dev, generator=self.gen)
+            acq = torch.clamp(torch.floor(torch.log1p(-u) / np.log(0.7)) + 1, max=64).to(torch.int32)
+        base = torch.arange(s * N, (s + 1) * N, device=self.dev, dtype=torch.float64)
+        ts = (self.T.T0_ALIGNED + torch.floor(base * self.ms_per_event)).to(torch.int64)
+        from sentinel_amd.token_service import device_events
+        return device_events(idx, acq, ts)
+
+    def span_ms(self):
+        return int(np.ceil(self.N * self.ms_per_event)) + 1
+
+    def submit(self, b):
+        self.svc.submit_flow_batch(b, verdicts=self.verdicts)
+
+    def cpu_baseline(self, batches, k1, kmt, threads):
+        from oracle import oracle as O
+        r = self.rules
+
+        def host_steps(k):
+            e = self.torch.cat(batches[:k]).cpu().numpy()
+            return (e[:, 0] & 0xFFFFFFFF).astype(np.int32), (e[:, 0] >> 32).astype(np.int32), e[:, 1].copy()
+
+        def fresh():
+            return O.TokenServiceOracle.from_arrays(r.flow_id, r.count, r.threshold_type, r.sample_count,
+                                                    r.window_interval_ms, r.namespace, r.checker,
+                                                    namespaces=self.namespaces)
+        idx, acq, ts = host_steps(k1)
+        orc = fresh()
+        c0 = time.perf_counter()
+        orc.replay(idx, acq, ts)
+        cdt = time.perf_counter() - c0
+        one = (len(ts), cdt, 1, "sequential oracle replay")
+        if self.namespaces:          # a namespace limiter couples every flow: no sharded replay
+            return one, None
+        idx, acq, ts = host_steps(kmt)
+        orc = fresh()
+        c0 = time.perf_counter()
+        used = orc.replay_mt(idx, acq, ts, threads)[3]
+        cdt = time.perf_counter() - c0
+        mt = (len(ts), cdt, int(used), f"oracle replay sharded by flow over {used} pthreads")
+        return one, mt
+
+    def bytes_of(self, dom, d, steps):
+        """Algorithmic bytes per processed event of the dominant kernel."""
+        n = int(self.rules.sample_count.max())
+        e_f = self.N / max(1, self.F)
+        if dom == "process":
+            # per touched flow: read n epochs + n PASS, write epoch + 4 counters; per event: segment record
+            return (n * 16 + 40 + 24) / max(1.0, e_f)
+        if dom == "part_fused":
+            # per event: read the 8-B packed value (local key inside), write the 8-B verdict; per
+            # touched flow: read the window header (16 B per bucket) and the rule fields, write back
+            # the rolled bucket's 16-B pair, read + write its BLOCK / PASS_REQUEST / BLOCK_REQUEST
+            # counters (3 x 8 B each way, blocked counter rows)
+            return 16.0 + (n * 16 + 42 + 16 + 48) / max(1.0, e_f)
+        if dom == "radix_scatter":
+            passes = max(1, round(d["calls"] / max(1, steps)))
+            return (32.0 + 24.0 * (passes - 1)) / passes
+        return KERNEL_BYTES_PER_EVENT.get(dom)
+
+    def pipeline_bytes(self):
+        n = int(self.rules.sample_count.max())
+        return 21.0 + (n * 64 + 64 + 16) / max(1.0, self.N / max(1, self.F))
+
+    def shape(self):
+        return {"config": self.args.config, "flows": self.F, "events": self.N,
+                "sample_count": int(self.rules.sample_count.max())}
+
+
+class ParamWorkload:
+    """Cluster hot-parameter requests (sentinel_param_event_t) of config 4, exact or count-min."""
+
+    def __init__(self, args, world, rank, dev):
+        import torch
+        import sentinel_amd as sa
+        from sentinel_amd import trace as T
+        from sentinel_amd.token_service import ServerNamespace
+        self.T, self.torch, self.dev, self.args = T, torch, dev, args
+        self.R_total = args.flows or 100_000
+        self.universe = 1000
+        self.N = args.events_per_gpu or 4 * 1024 * 1024
+        n = args.sample_count or 10
+        rng = np.random.default_rng(4)
+        count = rng.integers(5, 101, size=self.R_total).astype(np.float64)
+        flow_id = np.arange(1, self.R_total + 1, dtype=np.int64)
+        mine = np.nonzero(T.shard_of(flow_id, world) == rank)[0] if world > 1 else np.arange(self.R_total)
+        self.flow_id, self.count = flow_id[mine], count[mine]
+        self.R = len(mine)
+        self.hot = {}
+        for r in range(min(self.R, 1000)):                # ~1% of values are hot items on the first rules
+            for v in range(10):
+                self.hot.setdefault(r, {})[int((np.uint64(self.flow_id[r]) << np.uint64(20)) | np.uint64(v))] = \
+                    int(rng.integers(1, 20))
+        self.n, self.interval = n, args.interval_ms
+        self.prules = [dict(flow_id=int(self.flow_id[r]), count=float(self.count[r]), threshold_type=1, sample_count=n,
+                            window_interval_ms=self.interval) for r in range(self.R)]
+        self.svc = sa.GpuTokenService(dev.index or 0)
+        self.svc.set_namespaces([ServerNamespace()])
+        self.svc.load_param_rules([sa.ParamFlowRule(count=p["count"], cluster_config=sa.ClusterFlowConfig(
+            flow_id=p["flow_id"], threshold_type=1, sample_count=n, window_interval_ms=self.interval),
+            hot_items=self.hot.get(r, {})) for r, p in enumerate(self.prules)])
+        self.cm = args.config == "4cm"
+        self.cm_width, self.cm_depth = 1 << 20, 4
+        if self.cm:
+            from sentinel_amd import _lib
+            self.svc.set_param_mode(_lib.PARAM_COUNT_MIN_SHARED, self.cm_depth, self.cm_width)
+        self.rate = 2.0 * float(self.count.sum()) * 0.05     # offered requests per second (BASELINE.md config 4)
+        self.ms_per_event = 1000.0 / self.rate
+        self.gen = torch.Generator(device=dev).manual_seed(2000 + rank)
+        w = 1.0 / np.power(np.arange(1, self.universe + 1, dtype=np.float64), 1.2)
+        self.zipf_cdf = torch.from_numpy(np.cumsum(w) / w.sum()).to(dev)
+        self.fid_dev = torch.from_numpy(self.flow_id.astype(np.int64)).to(dev)
+        self.verdicts = torch.empty(self.N, dtype=torch.int64, device=dev)
+        self.workload = (f"config4: {self.R_total} hot-parameter cluster rules (count~U{{5..100}}, hot items), values "
+                         f"Zipf(1.2) over 1000 Long keys per resource, n={n} w={self.interval // n}ms, acquire 1, "
+                         f"{self.N}-event batches, " + (f"shared count-min sketch d={self.cm_depth} w=2^20"
+                                                        if self.cm else "exact per-value counters"))
+
+    def batch(self, s):
+        torch, N = self.torch, self.N
+        ridx = torch.randint(0, self.R, (N,), dtype=torch.int32, device=self.dev, generator=self.gen)
+        u = torch.rand(N, dtype=torch.float64, device=self.dev, generator=self.gen)
+        vals = torch.clamp(torch.searchsorted(self.zipf_cdf, u, right=True), max=self.universe - 1).to(torch.int64)
+        keys = (self.fid_dev[ridx.long()] << 20) | vals       # injective per (rule flowId, value)
+        base = torch.arange(s * N, (s + 1) * N, device=self.dev, dtype=torch.float64)
+        ts = (self.T.T0_ALIGNED + torch.floor(base * self.ms_per_event)).to(torch.int64)
+        w0 = (torch.ones(N, dtype=torch.int64, device=self.dev) << 32) | (ridx.to(torch.int64) & 0xFFFFFFFF)
+        return torch.stack([w0, ts, keys], dim=1).contiguous()
+
+    def span_ms(self):
+        return int(np.ceil(self.N * self.ms_per_event)) + 1
+
+    def submit(self, b):
+        self.svc.submit_param_batch(b, verdicts=self.verdicts)
+
+    def _host(self, batches, k):
+        e = self.torch.cat(batches[:k]).cpu().numpy()
+        return (e[:, 0] & 0xFFFFFFFF).astype(np.int32), (e[:, 0] >> 32).astype(np.int32), e[:, 2].astype(np.uint64), e[:, 1].copy()
+
+    def _oracle(self):
+        from oracle import oracle as O
+        return O.TokenServiceOracle([], param_rules=self.prules, hot_items={r: list(h.items()) for r, h in self.hot.items()})
+
+    def cpu_baseline(self, batches, k1, kmt, threads):
+        ridx, acq, keys, ts = self._host(batches, k1)
+        orc = self._oracle()
+        c0 = time.perf_counter()
+        orc.param_replay(ridx, acq, keys, ts)
+        cdt = time.perf_counter() - c0
+        return (len(ts), cdt, 1, "sequential oracle replay (ClusterParamFlowChecker, exact counters)"), None
+
+    def false_blocks(self, batches, k, svc_verdicts):
+        """Count-min audit: the sketch's verdicts replayed on exact counters (same admitted history):
+        violations (sketch passed, exact would block) must be 0; false blocks are the price of the sketch."""
+        ridx, acq, keys, ts = self._host(batches, k)
+        from sentinel_amd.token_service import decode_verdicts
+        st = np.concatenate([decode_verdicts(v)[0] for v in svc_verdicts]).astype(np.int8)
+        orc = self._oracle()
+        ones = np.ones(len(ts), np.int32)
+        viol, fb, dec = orc.param_cm_audit(ridx, acq, ts, np.arange(len(ts), dtype=np.int32), ones, keys, st)
+        return viol, fb, dec
+
+    def bytes_of(self, dom, d, steps):
+        if dom == "radix_scatter":
+            passes = max(1, round(d["calls"] / max(1, steps)))
+            return (32.0 + 24.0 * (passes - 1)) / passes
+        if dom == "process":
+            # per touched (rule, value) slot: read n {epoch, count} pairs, write one; per event: segment record
+            return 24.0 + (self.n * 16 + 16) / 4.0
+        return KERNEL_BYTES_PER_EVENT.get(dom)
+
+    def pipeline_bytes(self):
+        return 24.0 + 8.0 + (self.n * 16 * 2 + 16) / 4.0
+
+    def shape(self):
+        return {"config": self.args.config, "rules": self.R, "events": self.N, "sample_count": self.n}
 
 
 def main():
@@ -104,44 +400,22 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    import sentinel_amd as sa
-    from sentinel_amd import trace as T
-
-    # ---- rule universe (identical on every rank), then this rank's shard
-    rng = np.random.default_rng(3)
-    rules = T.make_rules(args.flows, rng, sample_count=args.sample_count, window_interval_ms=args.interval_ms)
-    mine = np.nonzero(T.shard_of(rules.flow_id, world) == rank)[0] if world > 1 else np.arange(len(rules))
-    shard = rules.subset(mine)
-    F = len(shard)
-
-    svc = sa.GpuTokenService(local)
-    svc.load_rules_array(shard.flow_id, shard.count, shard.threshold_type, shard.sample_count,
-                         shard.window_interval_ms, shard.namespace, shard.checker)
-
-    N = args.events_per_gpu
+    W = ParamWorkload(args, world, rank, dev) if args.config in ("4", "4cm") else FlowWorkload(args, world, rank, dev)
+    svc, N = W.svc, W.N
     # warmup | untimed per-kernel profile pass (every kernel timed: the breakdown) | timed steps
     # (only the dominant kernel timed, two events per step: its live duration for the roofline)
     pstep = 0 if args.no_profile else args.profile_steps
     steps_total = args.warmup + pstep + args.steps
-    rate = 2.0 * float(shard.count.sum())          # offered rate: 2x the shard's thresholds (per second)
-    ms_per_event = 1000.0 / rate
-    t0 = T.T0_ALIGNED
-    from sentinel_amd.token_service import device_events
-    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
-    ev_b = []
-    acq = torch.ones(N, dtype=torch.int32, device=dev)
-    for s in range(steps_total):
-        idx = torch.randint(0, F, (N,), dtype=torch.int32, device=dev, generator=gen)
-        base = torch.arange(s * N, (s + 1) * N, device=dev, dtype=torch.float64)
-        ts = (t0 + torch.floor(base * ms_per_event)).to(torch.int64)
-        ev_b.append(device_events(idx, acq, ts))
-        del idx, base, ts
-    verdicts = torch.empty(N, dtype=torch.int64, device=dev)
+    ev_b = [W.batch(s) for s in range(steps_total)]
     torch.cuda.synchronize()
+    log(f"config {args.config}: {steps_total} batches of {N} events generated")
 
     ext = torch.cuda.ExternalStream(svc.stream, device=dev)
+    keep_verdicts = []
     for s in range(args.warmup):
-        svc.submit_flow_batch(ev_b[s], verdicts=verdicts)
+        W.submit(ev_b[s])
+        if args.config == "4cm" and len(keep_verdicts) < 2:     # the audited sample: the first two batches
+            keep_verdicts.append(W.verdicts.clone())
     svc.synchronize()
 
     import ctypes as C
@@ -164,17 +438,17 @@ def main():
     if not args.no_profile:
         svc._L.sentinel_profile_enable(svc.handle, 1)
         for s in range(args.warmup, args.warmup + pstep):
-            svc.submit_flow_batch(ev_b[s], verdicts=verdicts)
+            W.submit(ev_b[s])
+            if args.config == "4cm" and len(keep_verdicts) < 2:
+                keep_verdicts.append(W.verdicts.clone())
         svc.synchronize()
         breakdown = read_profile()
         svc._L.sentinel_profile_enable(svc.handle, 0)
         dom = max(breakdown, key=lambda k: breakdown[k]["total_ms"])
         svc._L.sentinel_profile_select(svc.handle, dom.encode())
         svc._L.sentinel_profile_enable(svc.handle, 1)
-    # batch boundaries: one event between consecutive batches (batch k = tev[k] -> tev[k + 1]);
-    # the dominant kernel is bracketed by the engine's HIP events on every `kernel_every`-th timed
-    # step (each event record idles the queue ~5 us)
-    tev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    # the timed steps: barrier + synchronize on both sides, max over ranks; the dominant kernel is
+    # bracketed by the engine's HIP events on every `kernel_every`-th timed step
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -183,9 +457,7 @@ def main():
         s = args.warmup + pstep + k
         if not args.no_profile:
             svc._L.sentinel_profile_gate(svc.handle, 1 if k % args.kernel_every == 0 else 0)
-        tev[k].record(ext)
-        svc.submit_flow_batch(ev_b[s], verdicts=verdicts)
-    tev[args.steps].record(ext)
+        W.submit(ev_b[s])
     svc.synchronize()
     torch.cuda.synchronize()
     if world > 1:
@@ -195,8 +467,6 @@ def main():
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
-    lat = sorted(tev[k].elapsed_time(tev[k + 1]) for k in range(args.steps))
-    p99 = lat[min(len(lat) - 1, int(np.ceil(0.99 * len(lat))) - 1)]
 
     # ---- the dominant kernel's live duration over the timed region (HIP events on the engine stream)
     prof = {}
@@ -205,53 +475,101 @@ def main():
         svc._L.sentinel_profile_enable(svc.handle, 0)
         svc._L.sentinel_profile_select(svc.handle, None)
 
-    # ---- snapshot + RCCL all-gather (config 3's ClusterMetric snapshot; off the decision path)
-    t_snap = int(ev_b[-1][-1, 1].item()) + 1
-    snap = torch.empty((F, 3), dtype=torch.int64, device=dev)
+    # ---- latency loop (untimed): >= 200 batches continuing the trace; K buffers reused with their
+    # timestamps shifted forward in place (so time stays monotone), one torch event per batch boundary
+    # on the engine stream (device batch latency, back to back), then the same batches each followed by
+    # a host synchronize (submit -> verdicts visible to the host, host clock)
+    log("timed steps done; latency loop")
+    K = 8
+    L = max(1, args.latency_batches)
+    lat_b = [W.batch(steps_total + j) for j in range(K)]
+    shift = K * W.span_ms()
     torch.cuda.synchronize()
-    ts0 = time.perf_counter()
-    svc.snapshot_device(t_snap, snap)
-    svc.synchronize()
-    if world > 1:
-        maxf = torch.tensor([F], device=dev)
-        dist.all_reduce(maxf, op=dist.ReduceOp.MAX)
-        pad = torch.zeros((int(maxf.item()), 3), dtype=torch.int64, device=dev)
-        pad[:F] = snap
-        gathered = [torch.empty_like(pad) for _ in range(world)]
-        dist.all_gather(gathered, pad)
-        torch.cuda.synchronize()
-    snap_ms = (time.perf_counter() - ts0) * 1000.0
 
-    # PCIe-inclusive host paths (reported beside `value`, never as it): (i) synchronous 1M-event
-    # batches from pinned host memory (H2D, decide, D2H) -> per-batch latency percentiles, the
-    # north star's "host-fed 1M-event batches for the p99 number"; (ii) the streamed host path:
-    # the step's N events in 1M-event batches pipelined over copy streams (double-buffered).
+    def advance():
+        # the K buffers move one K-batch span forward in time, on the engine stream (ordered with the
+        # batches that read them)
+        with torch.cuda.stream(ext):
+            for b in lat_b:
+                b[:, 1] += shift
+
+    for j in range(min(K, L)):
+        W.submit(lat_b[j])                               # first use of these buffers (not timed)
+    advance()
+    tev = [torch.cuda.Event(enable_timing=True) for _ in range(L + 1)]
+    for i in range(L):
+        if i and i % K == 0:
+            advance()
+        tev[i].record(ext)
+        W.submit(lat_b[i % K])
+    tev[L].record(ext)
+    torch.cuda.synchronize()
+    lat = sorted(tev[i].elapsed_time(tev[i + 1]) for i in range(L))
+    hl = []
+    for i in range(L):
+        if i % K == 0:
+            advance()
+            svc.synchronize()
+        h0 = time.perf_counter()
+        W.submit(lat_b[i % K])
+        svc.synchronize()
+        hl.append((time.perf_counter() - h0) * 1000.0)
+    hl.sort()
+    advance()
+    svc.synchronize()
+    log("latency loop done")
+
+    def pct(xs, q):
+        return xs[min(len(xs) - 1, int(np.ceil(q * len(xs))) - 1)]
+
+    # ---- snapshot + RCCL all-gather (config 3's ClusterMetric snapshot; off the decision path)
+    snap_ms = None
+    if isinstance(W, FlowWorkload):
+        F = W.F
+        t_snap = int(lat_b[-1][-1, 1].item()) + 1
+        snap = torch.empty((F, 3), dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        ts0 = time.perf_counter()
+        svc.snapshot_device(t_snap, snap)
+        svc.synchronize()
+        if world > 1:
+            maxf = torch.tensor([F], device=dev)
+            dist.all_reduce(maxf, op=dist.ReduceOp.MAX)
+            pad = torch.zeros((int(maxf.item()), 3), dtype=torch.int64, device=dev)
+            pad[:F] = snap
+            gathered = [torch.empty_like(pad) for _ in range(world)]
+            dist.all_gather(gathered, pad)
+            torch.cuda.synchronize()
+        snap_ms = (time.perf_counter() - ts0) * 1000.0
+
+    # PCIe-inclusive host paths (config 3 only; reported beside `value`, never as it)
     host_path = None
-    if rank == 0 and not args.no_host_path:
-        import ctypes as C
+    if rank == 0 and not args.no_host_path and args.config == "3":
         m = min(N, 1 << 20)
         hev = torch.empty((N, 2), dtype=torch.int64, pin_memory=True)
-        hev.copy_(ev_b[-1])
+        hev.copy_(lat_b[0])
         hout = torch.empty(N, dtype=torch.int64, pin_memory=True)
         reps = max(1, args.host_reps)
         nbs = (N + m - 1) // m
         bms = np.zeros(nbs, dtype=np.float32)
-        # one untimed call of each leg: staging buffers and copy streams are created on first use
         assert svc._L.sentinel_submit_flow_batch_host(svc.handle, m, C.c_void_p(hev.data_ptr()), None,
                                                       C.c_void_p(hout.data_ptr())) == 0
         assert svc._L.sentinel_submit_flow_stream_host(svc.handle, N, C.c_void_p(hev.data_ptr()), None,
                                                        C.c_void_p(hout.data_ptr()), m, None) == 0
-        hl = []
+        hlp = []
+        hts = hev[:, 1].numpy()          # every rep decides a batch later in time (its timestamps shifted)
         for _ in range(reps):
+            hts += W.span_ms()
             h0 = time.perf_counter()
             rc = svc._L.sentinel_submit_flow_batch_host(svc.handle, m, C.c_void_p(hev.data_ptr()), None,
                                                         C.c_void_p(hout.data_ptr()))
             assert rc == 0
-            hl.append((time.perf_counter() - h0) * 1000.0)
-        hl.sort()
+            hlp.append((time.perf_counter() - h0) * 1000.0)
+        hlp.sort()
         sreps = 3
         s0 = time.perf_counter()
         for _ in range(sreps):
+            hts += W.span_ms()
             rc = svc._L.sentinel_submit_flow_stream_host(svc.handle, N, C.c_void_p(hev.data_ptr()), None,
                                                          C.c_void_p(hout.data_ptr()), m,
                                                          C.c_void_p(bms.ctypes.data))
@@ -259,12 +577,11 @@ def main():
         sdt = (time.perf_counter() - s0) / sreps
         bl = np.sort(bms)
         host_path = {
-            "sync": {"decisions_per_s": round(m * reps / (sum(hl) / 1000.0), 1), "batch": m, "reps": reps,
-                     "median_ms": round(hl[len(hl) // 2], 3),
-                     "p99_ms": round(hl[min(reps - 1, int(np.ceil(0.99 * reps)) - 1)], 3),
+            "sync": {"decisions_per_s": round(m * reps / (sum(hlp) / 1000.0), 1), "batch": m, "reps": reps,
+                     "median_ms": round(hlp[len(hlp) // 2], 3), "p99_ms": round(pct(hlp, 0.99), 3),
                      "note": "pinned host events -> H2D -> decide -> D2H, synchronous per batch, host clock"},
             "streamed": {"decisions_per_s": round(N / sdt, 1), "events": N, "batch": m,
-                         "p99_batch_ms": round(float(bl[min(nbs - 1, int(np.ceil(0.99 * nbs)) - 1)]), 3),
+                         "p99_batch_ms": round(float(pct(list(bl), 0.99)), 3), "batches_per_rep": nbs,
                          "note": "sentinel_submit_flow_stream_host: H2D / decide / D2H of consecutive batches "
                                  "overlapped on side streams; batch latency = HIP events H2D start -> D2H end "
                                  "(includes queueing behind the previous batch)"},
@@ -278,65 +595,50 @@ def main():
     roof = None
     if prof and dom in prof:
         d = prof[dom]
-        bpe = KERNEL_BYTES_PER_EVENT.get(dom)
-        if dom == "process":
-            # per touched flow: read n epochs + n PASS, write epoch + 4 counters; per event: segment record
-            e_f = N / max(1, F)
-            bpe = (args.sample_count * 16 + 40 + 24) / max(1.0, min(e_f, 1e9)) if F else 0.0
-        if dom == "part_fused":
-            # per event: read the 8-B packed value (local key inside), write the 8-B verdict; per
-            # touched flow: read the window header (16 B per bucket) and the 42 B of rule fields,
-            # write back the rolled bucket's 16-B pair, read + write its BLOCK / PASS_REQUEST /
-            # BLOCK_REQUEST counters (3 x 8 B each way, blocked counter rows)
-            e_f = N / max(1, F)
-            bpe = 16.0 + (args.sample_count * 16 + 42 + 16 + 48) / max(1.0, e_f)
-        if dom == "radix_scatter":
-            passes = max(1, round(d["calls"] / max(1, args.steps)))
-            bpe = (32.0 + 24.0 * (passes - 1)) / passes
+        bpe = W.bytes_of(dom, d, args.steps)
         ach = (bpe or 0.0) * d["units_per_call"] / (d["avg_us"] * 1e-6) / 1e9
+        traffic, traffic_src = pmc_traffic(dom, W.shape())
         roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom),
-                "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_latest.json)",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of this workload shape: "
+                                + (traffic_src or "no PMC run of this shape -> null") + ")",
                 "algorithmic_bytes_per_launch": round((bpe or 0.0) * d["units_per_call"], 1),
                 "bytes_per_event": bpe, "avg_us": round(d["avg_us"], 2)}
 
-    # ---- CPU baseline: the oracle ("port") on bounded samples of the same workload, rank 0, N=1.
-    # cpu_baseline = the flow-sharded multi-threaded replay on the box's CPU share (16 threads per
-    # GPU); cpu_baseline_1core = the sequential replay (what one reference JVM thread does per call).
+    # ---- CPU baseline: the oracle ("port") on bounded samples of the same workload, rank 0, N=1
     cpu = cpu1 = None
+    model, ncpu, avail = cpu_info()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle import oracle as O
+        log("cpu baseline")
+        one, mt = W.cpu_baseline(ev_b, min(args.cpu_steps_1core, steps_total), min(args.cpu_steps_mt, steps_total),
+                                 args.cpu_threads)
 
-        def host_steps(k):
-            e = torch.cat([ev_b[s] for s in range(min(k, steps_total))]).cpu().numpy()
-            return (e[:, 0] & 0xFFFFFFFF).astype(np.int32), e[:, 1].copy()
+        def leg(x):
+            m, cdt, cores, how = x
+            return {"value": round(m / cdt, 1), "unit": "decisions/s", "cores": cores, "kind": "port",
+                    "cpu_model": model, "nproc": ncpu, "cpus_available": avail,
+                    "sample": f"the first {m} events of this workload (same rules and trace), {how}, {cdt:.1f} s"}
+        cpu1 = leg(one)
+        cpu = leg(mt) if mt else cpu1
 
-        def fresh():
-            return O.TokenServiceOracle.from_arrays(shard.flow_id, shard.count, shard.threshold_type,
-                                                    shard.sample_count, shard.window_interval_ms,
-                                                    shard.namespace, shard.checker)
-        idx_c, ts_c = host_steps(args.cpu_steps_1core)
-        m = len(ts_c)
-        orc = fresh()
-        c0 = time.perf_counter()
-        orc.replay(idx_c, np.ones(m, np.int32), ts_c)
-        cdt = time.perf_counter() - c0
-        cpu1 = {"value": round(m / cdt, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
-                "sample": f"steps 0..{min(args.cpu_steps_1core, steps_total) - 1} of this workload ({m} events, same rules and trace), "
-                          f"sequential oracle replay, {cdt:.1f} s"}
-        del idx_c, ts_c
-        idx_c, ts_c = host_steps(args.cpu_steps_mt)
-        m = len(ts_c)
-        orc = fresh()
-        c0 = time.perf_counter()
-        used = orc.replay_mt(idx_c, np.ones(m, np.int32), ts_c, args.cpu_threads)[3]
-        cdt = time.perf_counter() - c0
-        cpu = {"value": round(m / cdt, 1), "unit": "decisions/s", "cores": int(used), "kind": "port",
-               "sample": f"steps 0..{min(args.cpu_steps_mt, steps_total) - 1} of this workload ({m} events, same rules and trace), "
-                         f"oracle replay sharded by flow over {used} pthreads, {cdt:.1f} s wall"}
-        del idx_c, ts_c
+    extra = {}
+    if args.config == "4cm" and rank == 0 and world == 1:
+        k = len(keep_verdicts)
+        viol, fb, dec = W.false_blocks(ev_b, k, keep_verdicts)
+        eps_n = float(np.e) / W.cm_width * float(N) * k      # e/w x (requests counted in the audited span)
+        extra["count_min"] = {"depth": W.cm_depth, "width": W.cm_width, "audited_requests": int(dec),
+                              "violations": int(viol), "false_blocks": int(fb),
+                              "false_block_rate": round(fb / max(1, dec), 8),
+                              "eps_N_bound_counts": round(eps_n, 2),
+                              "note": "the sketch's verdicts of the warmup+profile batches replayed on exact counters "
+                                      "(oracle, same admitted history): violations = sketch passed what exact would "
+                                      "block (must be 0); bound: P[overestimate > (e/w) N] <= exp(-d), N = all "
+                                      "requests counted in the window (upper bound used: every audited request)"}
+        st = svc.param_table_stats()
+        extra["param_table"] = st
+    if args.config == "4" and rank == 0:
+        extra["param_table"] = svc.param_table_stats()
 
-    pipeline_bytes = 21.0 + (args.sample_count * 64 + 64 + 16) / max(1.0, N / max(1, F))
     out = {
         "metric": "token decisions/sec (whole node) at 1M flowIds; p99 batch latency",
         "value": round(value, 1),
@@ -349,20 +651,24 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int64+f64",
-        "data": "synthetic (seeded uniform events over the shard's flows; random-init rule table)",
-        "config": {"workload": "config3: 1M flowIds hash-sharded (splitmix64 mod N), cluster GLOBAL rules "
-                               "count~U{10..1000}, n=10 w=100ms, uniform flows, acquire=1, 2x offered load",
-                   "flows_total": args.flows, "flows_this_rank": F, "events_per_gpu_per_step": N,
-                   "parallelism": f"flowid-shard x{world}"},
-        "p99_batch_ms": round(p99, 4),
+        "data": "synthetic (seeded events on the device; random-init rule table)",
+        "config": {"workload": W.workload, "events_per_gpu_per_step": N,
+                   "parallelism": f"flowid-shard x{world}", **W.shape()},
+        "p99_batch_ms": round(pct(lat, 0.99), 4),
         "median_batch_ms": round(lat[len(lat) // 2], 4),
-        "snapshot_allgather_ms": round(snap_ms, 3),
+        "latency_note": (f"{L} batches of an untimed loop after the timed steps: device time per batch between "
+                         f"torch events on the engine stream (back to back); p99_sync_ms = host clock with a "
+                         f"synchronize per batch"),
+        "p99_sync_ms": round(pct(hl, 0.99), 4),
+        "median_sync_ms": round(hl[len(hl) // 2], 4),
+        "snapshot_allgather_ms": None if snap_ms is None else round(snap_ms, 3),
         "host_path": host_path,
-        "pipeline_bytes_per_decision": round(pipeline_bytes, 2),
-        "pipeline_hbm_frac": round(value / world * pipeline_bytes / (HBM_PEAK_GBS * 1e9), 4),
+        "pipeline_bytes_per_decision": round(W.pipeline_bytes(), 2),
+        "pipeline_hbm_frac": round(value / world * W.pipeline_bytes() / (HBM_PEAK_GBS * 1e9), 4),
         "roofline": roof,
         "cpu_baseline": cpu,
         "cpu_baseline_1core": cpu1,
+        **extra,
         "kernels": {k: {"avg_us": round(v["avg_us"], 2), "calls": v["calls"]} for k, v in breakdown.items()},
         "kernels_note": (f"per-kernel HIP-event averages from {pstep} untimed profiled steps after the warmup; the "
                          "timed steps time only the dominant kernel (roofline.avg_us)"),

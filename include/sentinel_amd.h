@@ -234,6 +234,11 @@ int  sentinel_submit_param_multi_batch_host(sentinel_engine_t *eng, int64_t n, c
  * window count).  Switching modes clears the param counters. */
 #define SENTINEL_PARAM_EXACT      0
 #define SENTINEL_PARAM_COUNT_MIN  1
+/* One depth x width sketch for every param rule (keys are unique per (rule, value)): memory
+ * independent of the rule count; the bound is (e / width) x (the total window count of all rules).
+ * Needs one window (sampleCount, intervalMs) for every param rule: a per-rule window could reset a
+ * cell slot another rule's window still counts. */
+#define SENTINEL_PARAM_COUNT_MIN_SHARED  2
 int  sentinel_set_param_mode(sentinel_engine_t *eng, int32_t mode, int32_t depth, int32_t width);
 
 /* Local hot-parameter rule (ParamFlowRule, QPS grade, default control behaviour) as
@@ -349,6 +354,13 @@ int  sentinel_batcher_create(sentinel_engine_t *eng, int32_t max_batch, int32_t 
 int  sentinel_batcher_destroy(sentinel_batcher_t *b);
 int  sentinel_batcher_request_token(sentinel_batcher_t *b, int64_t flow_id, int32_t acquire_count,
                                     int32_t prioritized, int64_t ts, sentinel_token_result_t *out);
+/* Asynchronous variant for event-loop front ends (a Netty handler that writes the response when the
+ * verdict arrives, the native wire server): returns at once; cb(ctx, tag, result) runs on the
+ * dispatcher thread once the request's batch is decided (it must not block). */
+typedef void (*sentinel_token_cb)(void *ctx, uint64_t tag, const sentinel_token_result_t *result);
+int  sentinel_batcher_request_token_async(sentinel_batcher_t *b, int64_t flow_id, int32_t acquire_count,
+                                          int32_t prioritized, int64_t ts, sentinel_token_cb cb, void *ctx,
+                                          uint64_t tag);
 int  sentinel_batcher_stats(sentinel_batcher_t *b, int64_t *batches, int64_t *requests);
 
 /* ---- observability / parity ---- */

@@ -52,6 +52,7 @@ EXPORTS = [
     "sentinel_local_node_stats", "sentinel_set_occupy_timeout", "sentinel_profile_select", "sentinel_profile_gate", "sentinel_set_flow_path",
     "sentinel_param_top_values", "sentinel_param_snapshot_device", "sentinel_flow_window", "sentinel_metric_count",
     "sentinel_reset_metrics", "sentinel_param_table_stats", "sentinel_param_count",
+    "sentinel_batcher_request_token_async",
 ]
 
 STATUS_RELEASE_OK = 6
@@ -61,6 +62,7 @@ CONCURRENT_RELEASE = 1
 
 PARAM_EXACT = 0
 PARAM_COUNT_MIN = 1
+PARAM_COUNT_MIN_SHARED = 2
 
 
 class ServerConfig(C.Structure):
@@ -192,6 +194,7 @@ def load():
         "sentinel_reset_metrics": (C.c_int, [vp, i32, i32]),
         "sentinel_param_table_stats": (C.c_int, [vp, vp]),
         "sentinel_param_count": (i32, [vp]),
+        "sentinel_batcher_request_token_async": (C.c_int, [vp, i64, i32, i32, i64, vp, vp, C.c_uint64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -21,11 +21,24 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in DEPS)
 
 
+TOOLS = {"dropin_bench": os.path.join(ROOT, "tools", "dropin_bench.cpp")}
+
+
 def build(force: bool = False, out: str = OUT, defines=()) -> str:
     if force or needs_build() or out != OUT:
         cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-o", out, *SOURCES]
         subprocess.run(cmd, check=True)
     return out
+
+
+def build_tools() -> None:
+    """Native benchmark / front-end tools linked against the library (tools/, binaries next to them)."""
+    for name, src in TOOLS.items():
+        exe = os.path.join(os.path.dirname(src), name)
+        if os.path.exists(exe) and os.path.getmtime(exe) > max(os.path.getmtime(src), os.path.getmtime(OUT)):
+            continue
+        subprocess.run([HIPCC, "-O2", "-std=c++17", "-o", exe, src, "-L" + _HERE, "-lsentinel_amd",
+                        "-Wl,-rpath,$ORIGIN/../sentinel_amd", "-lpthread"], check=True)
 
 
 if __name__ == "__main__":

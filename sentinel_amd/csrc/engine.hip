@@ -344,6 +344,35 @@ inline unsigned grid_for(int64_t n, int threads = 256) { return (unsigned)std::m
 
 }  // namespace
 
+// flowId -> dense index on the host: open addressing over a power-of-two table (the per-call and
+// batcher front doors look up every request; a node-based map costs several cache misses each).
+struct FlatIndex {
+    std::vector<int64_t> keys;       // 0 = empty (flowIds are > 0)
+    std::vector<int32_t> vals;
+    uint64_t mask = 0;
+    void build(const std::unordered_map<int64_t, int32_t> &m) {
+        uint64_t cap = 16;
+        while (cap < 2 * m.size() + 2) cap <<= 1;
+        keys.assign(cap, 0);
+        vals.assign(cap, -1);
+        mask = cap - 1;
+        for (auto &kv : m) {
+            uint64_t h = mix64((uint64_t)kv.first) & mask;
+            while (keys[h]) h = (h + 1) & mask;
+            keys[h] = kv.first;
+            vals[h] = kv.second;
+        }
+    }
+    int32_t find(int64_t id) const {
+        if (id <= 0) return SENTINEL_IDX_BAD_ID;                // ClusterRuleUtil.validId
+        if (keys.empty()) return SENTINEL_IDX_NO_RULE;
+        for (uint64_t h = mix64((uint64_t)id) & mask;; h = (h + 1) & mask) {
+            if (keys[h] == id) return vals[h];
+            if (!keys[h]) return SENTINEL_IDX_NO_RULE;
+        }
+    }
+};
+
 // ==================================================================== engine
 struct sentinel_engine {
     int device = 0;
@@ -355,6 +384,7 @@ struct sentinel_engine {
     // flows
     std::vector<sentinel_flow_rule_t> rules;
     std::unordered_map<int64_t, int32_t> flow_index;
+    FlatIndex flat_flow;
     std::vector<int32_t> h_flow_n, h_flow_w, h_flow_interval;   // the window of each flow's METRIC
     std::vector<int64_t> h_flow_off;
     // metrics that outlived their rule (a namespace whose rule list became empty keeps METRIC_MAP
@@ -484,6 +514,8 @@ struct sentinel_engine {
     DevBuf w_vslot;                    // slot of every value of a param batch
     DevBuf w_runs;                     // partition path: long-run / oversized-half work lists
     DevBuf w_pscan;                    // partition path: per-group range sums + range starts
+    DevBuf w_qpos, w_vstage;           // partition path, staged verdicts: slot of each event, staged verdicts
+    bool vstage_on = false;            // SENTINEL_VSTAGE=1: stage verdicts (k_part_unsplit)
     DevBuf io_ev, io_fl, io_out, io_vals;
     // streamed host path (sentinel_submit_flow_stream_host): copy streams + two staging slots
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
@@ -576,7 +608,7 @@ struct sentinel_engine {
                          d_prule_Is.as<double>(), d_prule_thr.as<double>(),
                          has_hot ? d_hot_table.as<unsigned long long>() : nullptr, hot_mask, d_hot_thr.as<double>()};
         C.PT = table(pt, 1, header_words(pmax_n));
-        C.CM = CountMin{d_cm.as<uint64_t>(), cm_depth, cm_width, pmax_n};
+        C.CM = CountMin{d_cm.as<uint64_t>(), cm_depth, cm_width, pmax_n, pmode == SENTINEL_PARAM_COUNT_MIN_SHARED};
         C.L = LocalRules{d_lrule_valid.as<uint8_t>(), d_lrule_tok.as<int64_t>(), d_lrule_burst.as<int64_t>(),
                          d_lrule_dur.as<int64_t>(), lhas_hot ? d_lhot_keys.as<unsigned long long>() : nullptr,
                          lhot_mask, d_lhot_tok.as<int64_t>(), d_lstate.as<int64_t>()};
@@ -585,7 +617,7 @@ struct sentinel_engine {
     }
     SlotMeta slot_meta() {
         return SlotMeta{pt.n.as<int32_t>(), pt.w.as<int32_t>(), pt.rcp.as<double>(), pt.Is.as<double>(),
-                        pt.thr.as<double>(), pt.kind.as<uint8_t>()};
+                        pt.thr.as<double>(), pt.kind.as<uint8_t>(), d_slot_rule.as<int32_t>()};
     }
 
     void scan(uint32_t *buf, int64_t n, bool exclusive, hipStream_t s) {
@@ -723,6 +755,11 @@ struct sentinel_engine {
                       const std::vector<int32_t> &imp_rule, std::vector<std::pair<int32_t, std::vector<int64_t>>> *exported);
     int param_reserve(int64_t nv);
     int reset_param_metrics(int32_t sample_count, int32_t interval_ms);
+    bool uniform_param_window() const {
+        for (size_t i = 1; i < h_prule_n.size(); ++i)
+            if (h_prule_n[i] != h_prule_n[0] || h_prule_interval[i] != h_prule_interval[0]) return false;
+        return true;
+    }
     int rebuild_cm();
     int ensure_tokens();
     int rewrite_tokens(bool compact);
@@ -866,9 +903,9 @@ int sentinel_engine::param_rebuild(uint64_t new_cap, const std::vector<int32_t> 
         }
         if (rc) { cleanup(); return SENTINEL_E_NOMEM; }
         (void)hipMemsetAsync(dnewest.p, 0, (size_t)OR * 8, stream);
-        k_ptable_rule_newest<<<grid_for((int64_t)pcap), 256, 0, stream>>>(O, pcap, d_prule_n.as<int32_t>(),
+        k_ptable_rule_newest<<<grid_for((int64_t)pcap), 256, 0, stream>>>(O, pcap, OR, d_prule_n.as<int32_t>(),
                                                                          dnewest.as<unsigned long long>());
-        k_ptable_rebuild<<<grid_for((int64_t)pcap), 256, 0, stream>>>(O, pcap, dmap.as<int32_t>(), d_prule_n.as<int32_t>(),
+        k_ptable_rebuild<<<grid_for((int64_t)pcap), 256, 0, stream>>>(O, pcap, OR, dmap.as<int32_t>(), d_prule_n.as<int32_t>(),
                                                                      dnewest.as<unsigned long long>(), N, live,
                                                                      dxout.as<int64_t>(), xstride, xcount, xcap);
     }
@@ -882,10 +919,12 @@ int sentinel_engine::param_rebuild(uint64_t new_cap, const std::vector<int32_t> 
                                                         dnrn.as<int32_t>(), N, live);
     }
     unsigned long long cnt[2] = {0, 0};
-    if (hipGetLastError() != hipSuccess || hipMemcpyAsync(cnt, dcount.p, 16, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-        hipStreamSynchronize(stream) != hipSuccess) {
+    hipError_t he = hipGetLastError();
+    if (he == hipSuccess) he = hipMemcpyAsync(cnt, dcount.p, 16, hipMemcpyDeviceToHost, stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(stream);
+    if (he != hipSuccess) {
         cleanup();
-        return fail(SENTINEL_E_DEVICE, "param table rebuild failed");
+        return fail(SENTINEL_E_DEVICE, std::string("param table rebuild failed: ") + hipGetErrorString(he));
     }
     if (exported && any_export && cnt[1] > 0) {
         const uint64_t nx = std::min<uint64_t>(cnt[1], xcap);
@@ -980,8 +1019,9 @@ int sentinel_engine::reset_param_metrics(int32_t sample_count, int32_t interval_
 
 // Count-min cells for every param rule, zeroed (count 0 = nothing counted).
 int sentinel_engine::rebuild_cm() {
-    if (pmode != SENTINEL_PARAM_COUNT_MIN) return 0;
-    const size_t R = std::max<size_t>(prules.size(), 1);
+    if (pmode == SENTINEL_PARAM_EXACT) return 0;
+    // one sketch per rule, or one for every rule (SHARED: a single window for all param rules)
+    const size_t R = pmode == SENTINEL_PARAM_COUNT_MIN_SHARED ? 1 : std::max<size_t>(prules.size(), 1);
     const size_t bytes = R * (size_t)cm_depth * (size_t)cm_width * (size_t)pmax_n * 8;
     if (bytes > ((size_t)96 << 30)) return fail(SENTINEL_E_NOMEM, "count-min sketch would exceed 96 GiB");
     int rc = d_cm.ensure(bytes);
@@ -1105,7 +1145,7 @@ int sentinel_engine::rebuild_limiters() {
 template <int NMAX>
 static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTable &FT, const uint32_t *rstart,
                                int lb, const EventSrc &src, const Verdicts &V, int64_t n, hipStream_t s,
-                               uint32_t *ctl, unsigned long long *stat) {
+                               uint32_t *ctl, unsigned long long *stat, uint64_t *vstage, const uint32_t *qpos) {
     // ctl: [0] long-run count, [1] oversized-half count, [2, 2 + 2 nparts) oversized halves, then long runs
     uint32_t *nlong = ctl, *nbig = ctl + 1, *big = ctl + 2;
     uint32_t *long_runs = big + 2 * (size_t)nparts;
@@ -1116,17 +1156,18 @@ static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTa
 #define SENTINEL_ALLBIG_PCT 90
 #endif
     const bool all_big = n > (int64_t)nparts * (int64_t)(PH_KEYS * SENTINEL_ALLBIG_PCT / 100);
+    if (all_big) vstage = nullptr;    // k_part_half does not run: every verdict is written directly
     if (!all_big) {
         e->launch("part_fused", n, s, [&] {
             const dim3 g(16u * (unsigned)((nparts + 7) / 8));
             if (part_coop(lb))      // <= 256 flows per half: cooperative verdict sweep
                 k_part_half<NMAX, true><<<g, PH_THREADS, 0, s>>>(FT, pval, gsval, rstart, lb, nparts,
                                                                  (int32_t)e->rules.size(), src, V, long_runs,
-                                                                 nlong, big, nbig, stat);
+                                                                 nlong, big, nbig, stat, vstage);
             else
                 k_part_half<NMAX, false><<<g, PH_THREADS, 0, s>>>(FT, pval, gsval, rstart, lb, nparts,
                                                                   (int32_t)e->rules.size(), src, V, long_runs,
-                                                                  nlong, big, nbig, stat);
+                                                                  nlong, big, nbig, stat, vstage);
         });
     }
     e->launch("part_big", n, s, [&] {
@@ -1137,6 +1178,11 @@ static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTa
     e->launch("part_long", n, s, [&] {   // hot flows (runs > LONG_RUN events): a workgroup each
         k_part_long<NMAX><<<256, PL_THREADS, 0, s>>>(FT, gsval, long_runs, nlong, src, V, stat, e->h_part_stat);
     });
+    if (vstage)
+        e->launch("part_unsplit", n, s, [&] {
+            const int64_t nch = (n + PU_CHUNK - 1) / PU_CHUNK;
+            k_part_unsplit<<<(unsigned)(8 * ((nch + 7) / 8)), PU_THREADS, 0, s>>>(n, qpos, vstage, V.out);
+        });
 }
 
 static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
@@ -1180,18 +1226,27 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
         k_part_offsets<<<g2, PS_THREADS, 0, s>>>(hist, nb, nparts, gsum, rtot, rstart);
     });
     const EventSrc src{ev, nullptr, fl, false};
+    uint32_t *qpos = nullptr;
+    uint64_t *vstage = nullptr;
+    if (e->vstage_on) {
+        rc = e->w_qpos.ensure((size_t)n * 4);
+        rc |= e->w_vstage.ensure((size_t)n * 8);
+        if (rc) return rc;
+        qpos = e->w_qpos.as<uint32_t>();
+        vstage = e->w_vstage.as<uint64_t>();
+    }
     e->launch("part_scatter", n, s, [&] {
         k_part_scatter<<<dim3((unsigned)nb), dim3(PT_THREADS), 0, s>>>(e->flow_plain ? nullptr : fkey, src,
                                                                          e->w_sval.as<uint64_t>(), n, finvalid, lb,
-                                                                         pbits, hist, nb, nparts, F);
+                                                                         pbits, hist, nb, nparts, F, qpos);
     });
     const KeyTable FT = e->table(e->ft, NEV, 0);
     const Verdicts V{out, fkey, finvalid};
     const int mx = e->flow_max_n;
-    if (mx <= 2) launch_part_decide<2>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
-    else if (mx <= 4) launch_part_decide<4>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
-    else if (mx <= 10) launch_part_decide<10>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
-    else launch_part_decide<16>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
+    if (mx <= 2) launch_part_decide<2>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat, vstage, qpos);
+    else if (mx <= 4) launch_part_decide<4>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat, vstage, qpos);
+    else if (mx <= 10) launch_part_decide<10>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat, vstage, qpos);
+    else launch_part_decide<16>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat, vstage, qpos);
     HIP_OK(hipGetLastError());
     return 0;
 }
@@ -1257,7 +1312,7 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
                          const uint64_t *values, int64_t n_values, uint64_t *out, hipStream_t s);
 
 static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, uint64_t *out, hipStream_t s) {
-    if (e->pmode == SENTINEL_PARAM_COUNT_MIN) return submit_prules(e, PMODE_CM, n, ev, nullptr, nullptr, 0, out, s);
+    if (e->pmode != SENTINEL_PARAM_EXACT) return submit_prules(e, PMODE_CM, n, ev, nullptr, nullptr, 0, out, s);
     if (n <= 0) return 0;
     if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
     int rc = e->ensure_ws(n);
@@ -1486,6 +1541,7 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
         e->flow_path = v == "sorted" ? 1 : v == "partition" ? 2 : 0;
     }
     if (const char *c = getenv("SENTINEL_SEGMENTS")) e->fused_segments = std::string(c) != "split";
+    if (const char *c = getenv("SENTINEL_VSTAGE")) e->vstage_on = std::string(c) == "1";
     if (const char *c = getenv("SENTINEL_PARAM_CAPACITY")) {
         uint64_t v = strtoull(c, nullptr, 10);
         uint64_t p = 1024;
@@ -1522,7 +1578,7 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
                       &e->d_lrule_dur, &e->d_lrule_w, &e->d_lrule_rcp, &e->d_lrule_kind, &e->d_lhot_keys,
                       &e->d_lhot_tok, &e->d_ltable, &e->d_lstate, &e->d_now, &e->d_conc_thr, &e->d_seg1_w,
                       &e->d_seg1_rcp, &e->d_seg1_kind, &e->d_tok_keys, &e->d_tok_fid, &e->d_tok_fidx,
-                      &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->w_runs, &e->w_pscan, &e->d_lres_state,
+                      &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->w_runs, &e->w_pscan, &e->w_qpos, &e->w_vstage, &e->d_lres_state,
                       &e->d_lres_count, &e->d_lres_w, &e->d_lres_rcp, &e->d_lres_kind})
         b->release();
     for (int k = 0; k < 2; ++k) {
@@ -1816,6 +1872,7 @@ int sentinel_engine::install_flows(std::vector<sentinel_flow_rule_t> &&nr, std::
     cleanup();
     rules = std::move(nr);
     flow_index = std::move(nidx);
+    flat_flow.build(flow_index);
     off.resize(F);
     h_flow_off = std::move(off);
     h_flow_n = std::move(gn);
@@ -1884,16 +1941,14 @@ int32_t sentinel_param_count(sentinel_engine_t *e) { return e ? (int32_t)e->prul
 
 int sentinel_lookup_flow_idx(sentinel_engine_t *e, int64_t n, const int64_t *ids, int32_t *out) {
     if (!e || n < 0 || (n > 0 && (!ids || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
-    for (int64_t i = 0; i < n; ++i) {
-        if (ids[i] <= 0) { out[i] = SENTINEL_IDX_BAD_ID; continue; }   // ClusterRuleUtil.validId
-        auto it = e->flow_index.find(ids[i]);
-        out[i] = it == e->flow_index.end() ? SENTINEL_IDX_NO_RULE : it->second;
-    }
+    std::lock_guard<std::mutex> g(e->mu);
+    for (int64_t i = 0; i < n; ++i) out[i] = e->flat_flow.find(ids[i]);
     return 0;
 }
 
 int sentinel_lookup_param_idx(sentinel_engine_t *e, int64_t n, const int64_t *ids, int32_t *out) {
     if (!e || n < 0 || (n > 0 && (!ids || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
     for (int64_t i = 0; i < n; ++i) {
         if (ids[i] <= 0) { out[i] = SENTINEL_IDX_BAD_ID; continue; }
         auto it = e->param_index.find(ids[i]);
@@ -1963,6 +2018,10 @@ int sentinel_load_param_rules(sentinel_engine_t *e, const sentinel_param_rule_t 
         }
         maxn = std::max(maxn, gn[i]);
     }
+    if (e->pmode == SENTINEL_PARAM_COUNT_MIN_SHARED)
+        for (size_t i = 1; i < R; ++i)
+            if (gn[i] != gn[0] || gint[i] != gint[0])
+                return fail(SENTINEL_E_INVALID, "a shared count-min sketch needs one window for every param rule");
     // imported records are re-strided to the new table: (2 + 2 maxn) words each
     const int64_t istride = 2 + 2 * (int64_t)maxn;
     for (int64_t fid : revived) {
@@ -2046,11 +2105,32 @@ int sentinel_submit_flow_batch(sentinel_engine_t *e, int64_t n, const sentinel_e
     return submit_flow(e, n, (const Event *)ev, flags, (uint64_t *)out, stream ? (hipStream_t)stream : e->stream);
 }
 
+// H2D, decide, D2H of host events, synchronous, with the engine lock held.
+static int submit_flow_host_locked(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev, const uint8_t *flags,
+                                   sentinel_verdict_t *out);
+
 int sentinel_submit_flow_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev,
                                     const uint8_t *flags, sentinel_verdict_t *out) {
     if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
     if (n == 0) return 0;
     std::lock_guard<std::mutex> g(e->mu);
+    return submit_flow_host_locked(e, n, ev, flags, out);
+}
+
+// The per-call front doors: flowIds are mapped to dense indices and the batch decided under ONE
+// engine lock, so a concurrent rule reload cannot slip between the lookup and the decision (the
+// reference looks the rule up inside requestToken, DefaultTokenService.java:42).  ev[i].flow_idx is
+// overwritten with the dense index.
+static int submit_flow_ids_host(sentinel_engine_t *e, int64_t n, const int64_t *ids, sentinel_event_t *ev,
+                                const uint8_t *flags, sentinel_verdict_t *out) {
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> g(e->mu);
+    for (int64_t i = 0; i < n; ++i) ev[i].flow_idx = e->flat_flow.find(ids[i]);
+    return submit_flow_host_locked(e, n, ev, flags, out);
+}
+
+static int submit_flow_host_locked(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev, const uint8_t *flags,
+                                   sentinel_verdict_t *out) {
     HIP_OK(hipSetDevice(e->device));
     hipStream_t s = e->stream;
     int rc = 0;
@@ -2148,11 +2228,19 @@ int sentinel_submit_param_batch(sentinel_engine_t *e, int64_t n, const sentinel_
     return submit_param(e, n, (const ParamEvent *)ev, (uint64_t *)out, stream ? (hipStream_t)stream : e->stream);
 }
 
+static int submit_param_host_locked(sentinel_engine_t *e, int64_t n, const sentinel_param_event_t *ev,
+                                    sentinel_verdict_t *out);
+
 int sentinel_submit_param_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_param_event_t *ev,
                                      sentinel_verdict_t *out) {
     if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
     if (n == 0) return 0;
     std::lock_guard<std::mutex> g(e->mu);
+    return submit_param_host_locked(e, n, ev, out);
+}
+
+static int submit_param_host_locked(sentinel_engine_t *e, int64_t n, const sentinel_param_event_t *ev,
+                                    sentinel_verdict_t *out) {
     HIP_OK(hipSetDevice(e->device));
     hipStream_t s = e->stream;
     int rc = 0;
@@ -2173,7 +2261,7 @@ int sentinel_submit_param_multi_batch(sentinel_engine_t *e, int64_t n, const sen
         return fail(SENTINEL_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
-    return submit_prules(e, e->pmode == SENTINEL_PARAM_COUNT_MIN ? PMODE_CM : PMODE_EXACT, n, nullptr,
+    return submit_prules(e, e->pmode != SENTINEL_PARAM_EXACT ? PMODE_CM : PMODE_EXACT, n, nullptr,
                          (const MultiEvent *)ev, values, n_values, (uint64_t *)out, stream ? (hipStream_t)stream : e->stream);
 }
 
@@ -2183,19 +2271,22 @@ int sentinel_submit_param_multi_batch_host(sentinel_engine_t *e, int64_t n, cons
         return fail(SENTINEL_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
-    return submit_prules_host(e, e->pmode == SENTINEL_PARAM_COUNT_MIN ? PMODE_CM : PMODE_EXACT, n, ev, values,
+    return submit_prules_host(e, e->pmode != SENTINEL_PARAM_EXACT ? PMODE_CM : PMODE_EXACT, n, ev, values,
                               n_values, out);
 }
 
 int sentinel_set_param_mode(sentinel_engine_t *e, int32_t mode, int32_t depth, int32_t width) {
-    if (!e || (mode != SENTINEL_PARAM_EXACT && mode != SENTINEL_PARAM_COUNT_MIN)) return fail(SENTINEL_E_INVALID, "bad param mode");
-    if (mode == SENTINEL_PARAM_COUNT_MIN && (depth < 1 || depth > 16 || width < 16 || (width & (width - 1)) != 0))
+    if (!e || (mode != SENTINEL_PARAM_EXACT && mode != SENTINEL_PARAM_COUNT_MIN && mode != SENTINEL_PARAM_COUNT_MIN_SHARED))
+        return fail(SENTINEL_E_INVALID, "bad param mode");
+    if (mode != SENTINEL_PARAM_EXACT && (depth < 1 || depth > 16 || width < 16 || (width & (width - 1)) != 0))
         return fail(SENTINEL_E_INVALID, "count-min needs 1 <= depth <= 16 and a power-of-two width >= 16");
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
     HIP_OK(hipStreamSynchronize(e->stream));
+    if (mode == SENTINEL_PARAM_COUNT_MIN_SHARED && !e->uniform_param_window())
+        return fail(SENTINEL_E_INVALID, "a shared count-min sketch needs one window for every param rule");
     e->pmode = mode;
-    if (mode == SENTINEL_PARAM_COUNT_MIN) {
+    if (mode != SENTINEL_PARAM_EXACT) {
         e->cm_depth = depth;
         e->cm_width = (uint32_t)width;
     }
@@ -2527,12 +2618,11 @@ int sentinel_request_token(sentinel_engine_t *e, int64_t flow_id, int32_t acquir
                            sentinel_token_result_t *out) {
     if (!e || !out) return fail(SENTINEL_E_INVALID, "null argument");
     sentinel_event_t ev;
-    sentinel_lookup_flow_idx(e, 1, &flow_id, &ev.flow_idx);
     ev.acquire = acquire;
     ev.ts = ts;
     uint8_t fl = prio ? SENTINEL_FLAG_PRIORITIZED : 0;
     sentinel_verdict_t v{0, SENTINEL_STATUS_FAIL, 0};
-    int rc = sentinel_submit_flow_batch_host(e, 1, &ev, &fl, &v);
+    int rc = submit_flow_ids_host(e, 1, &flow_id, &ev, &fl, &v);
     out->status = rc ? SENTINEL_STATUS_FAIL : v.status;
     out->remaining = rc ? 0 : v.remaining;
     out->wait_in_ms = rc ? 0 : v.wait_in_ms;
@@ -2544,12 +2634,20 @@ int sentinel_request_param_token(sentinel_engine_t *e, int64_t flow_id, int32_t 
                                  int64_t ts, sentinel_token_result_t *out) {
     if (!e || !out) return fail(SENTINEL_E_INVALID, "null argument");
     sentinel_param_event_t ev;
-    sentinel_lookup_param_idx(e, 1, &flow_id, &ev.rule_idx);
     ev.acquire = acquire;
     ev.ts = ts;
     ev.param_key = param_key;
     sentinel_verdict_t v{0, SENTINEL_STATUS_FAIL, 0};
-    int rc = sentinel_submit_param_batch_host(e, 1, &ev, &v);
+    int rc;
+    {
+        std::lock_guard<std::mutex> g(e->mu);   // lookup and decision under one lock (DTS:57)
+        if (flow_id <= 0) ev.rule_idx = SENTINEL_IDX_BAD_ID;
+        else {
+            auto it = e->param_index.find(flow_id);
+            ev.rule_idx = it == e->param_index.end() ? SENTINEL_IDX_NO_RULE : it->second;
+        }
+        rc = submit_param_host_locked(e, 1, &ev, &v);
+    }
     out->status = rc ? SENTINEL_STATUS_FAIL : v.status;
     out->remaining = rc ? 0 : v.remaining;
     out->wait_in_ms = 0;
@@ -2609,10 +2707,11 @@ int sentinel_param_sum(sentinel_engine_t *e, int32_t ridx, uint64_t pkey, int64_
     HIP_OK(hipSetDevice(e->device));
     HIP_OK(hipStreamSynchronize(e->stream));
     *out = 0;
-    if (e->pmode == SENTINEL_PARAM_COUNT_MIN) {   // the sketch estimate (min over rows of the window sum)
+    if (e->pmode != SENTINEL_PARAM_EXACT) {   // the sketch estimate (min over rows of the window sum)
         const int n = e->h_prule_n[ridx];
         const int64_t E = ts / (e->h_prule_interval[ridx] / n);
-        const CountMin C{e->d_cm.as<uint64_t>(), e->cm_depth, e->cm_width, e->pmax_n};
+        const CountMin C{e->d_cm.as<uint64_t>(), e->cm_depth, e->cm_width, e->pmax_n,
+                         e->pmode == SENTINEL_PARAM_COUNT_MIN_SHARED};
         int64_t est = INT64_MAX;
         std::vector<uint64_t> cell(e->pmax_n);
         for (int d = 0; d < e->cm_depth; ++d) {
@@ -2664,7 +2763,7 @@ static int param_top(sentinel_engine_t *e, int64_t ts, int32_t number, hipStream
     const PSlots T{e->d_ptable.as<unsigned long long>(), e->d_slot_rule.as<int32_t>(), e->pt.state.as<int64_t>(),
                    header_words(e->pmax_n), cap - 1};
     const unsigned g = grid_for((int64_t)cap);
-    k_ptop_sums<<<g, 256, 0, s>>>(T, cap, e->d_prule_n.as<int32_t>(), e->d_prule_w.as<int32_t>(),
+    k_ptop_sums<<<g, 256, 0, s>>>(T, cap, R, e->d_prule_n.as<int32_t>(), e->d_prule_w.as<int32_t>(),
                                   e->d_prule_rcp.as<double>(), ts, sums.as<int64_t>());
     HIP_OK(hipMemsetAsync(pr.p, 0, (size_t)R * 8, s));
     HIP_OK(hipMemsetAsync(pk.p, 0, (size_t)R * 8, s));
@@ -2796,11 +2895,20 @@ int sentinel_snapshot(sentinel_engine_t *e, int64_t ts, sentinel_flow_snapshot_t
 // buffers, decides them as one GPU batch in arrival order, and wakes the callers.  Double-buffered:
 // the next batch is gathered while the current one is on the GPU.
 struct BatchReq {
-    sentinel_event_t ev;
-    uint8_t flag;
     sentinel_verdict_t out;
     int rc;
     std::atomic<int> done{0};
+};
+
+// One queued request: a blocked caller (waiter) or an asynchronous one (cb).
+struct BatchItem {
+    int64_t flow_id;
+    sentinel_event_t ev;                 // flow_idx filled by the dispatcher (submit_flow_ids_host)
+    uint8_t flag;
+    BatchReq *waiter;
+    sentinel_token_cb cb;
+    void *ctx;
+    uint64_t tag;
 };
 
 struct sentinel_batcher {
@@ -2809,16 +2917,19 @@ struct sentinel_batcher {
     int32_t max_wait_us = 50;
     std::mutex mu;
     std::condition_variable cv_in, cv_out;
-    std::vector<BatchReq *> queue;
+    std::vector<BatchItem> queue;
     std::thread th;
     bool stop = false;
     sentinel_event_t *h_ev = nullptr;
     uint8_t *h_fl = nullptr;
     sentinel_verdict_t *h_out = nullptr;
+    std::vector<int64_t> h_ids;
     std::atomic<int64_t> batches{0}, requests{0};
+    int64_t callers = 0;               // requesters inside request_token (guarded by mu)
+    std::condition_variable cv_idle;
 
     void run() {
-        std::vector<BatchReq *> cur;
+        std::vector<BatchItem> cur;
         for (;;) {
             {
                 std::unique_lock<std::mutex> lk(mu);
@@ -2828,28 +2939,56 @@ struct sentinel_batcher {
                     cv_in.wait_for(lk, std::chrono::microseconds(max_wait_us),
                                    [&] { return stop || (int32_t)queue.size() >= max_batch; });
                 }
-                const size_t take = std::min<size_t>(queue.size(), (size_t)max_batch);
-                cur.assign(queue.begin(), queue.begin() + take);
-                queue.erase(queue.begin(), queue.begin() + take);
+                cur.clear();
+                if ((int32_t)queue.size() <= max_batch) {
+                    cur.swap(queue);
+                } else {
+                    cur.assign(queue.begin(), queue.begin() + max_batch);
+                    queue.erase(queue.begin(), queue.begin() + max_batch);
+                }
             }
             const int64_t n = (int64_t)cur.size();
+            bool any_sync = false;
+            h_ids.resize(n);
             for (int64_t i = 0; i < n; ++i) {
-                h_ev[i] = cur[i]->ev;
-                h_fl[i] = cur[i]->flag;
+                h_ids[i] = cur[i].flow_id;
+                h_ev[i] = cur[i].ev;
+                h_fl[i] = cur[i].flag;
             }
-            const int rc = sentinel_submit_flow_batch_host(e, n, h_ev, h_fl, h_out);
+            const int rc = submit_flow_ids_host(e, n, h_ids.data(), h_ev, h_fl, h_out);
             for (int64_t i = 0; i < n; ++i) {
-                cur[i]->out = h_out[i];
-                cur[i]->rc = rc;
-                cur[i]->done.store(1, std::memory_order_release);
+                const BatchItem &it = cur[i];
+                if (it.waiter) {
+                    it.waiter->out = h_out[i];
+                    it.waiter->rc = rc;
+                    it.waiter->done.store(1, std::memory_order_release);
+                    any_sync = true;
+                } else {
+                    // engine down -> FAIL (the client falls back to its local check)
+                    sentinel_token_result_t r;
+                    r.status = rc ? SENTINEL_STATUS_FAIL : h_out[i].status;
+                    r.remaining = rc ? 0 : h_out[i].remaining;
+                    r.wait_in_ms = rc ? 0 : h_out[i].wait_in_ms;
+                    r.reserved = 0;
+                    it.cb(it.ctx, it.tag, &r);
+                }
             }
             batches.fetch_add(1);
             requests.fetch_add(n);
-            {
-                std::lock_guard<std::mutex> lk(mu);
+            if (any_sync) {
+                { std::lock_guard<std::mutex> lk(mu); }
+                cv_out.notify_all();
             }
-            cv_out.notify_all();
         }
+    }
+
+    int enqueue(const BatchItem &it) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (stop) return fail(SENTINEL_E_STATE, "batcher stopped");
+        if (it.waiter) ++callers;
+        queue.push_back(it);
+        if ((int32_t)queue.size() == 1 || (int32_t)queue.size() >= max_batch) cv_in.notify_one();
+        return 0;
     }
 };
 
@@ -2880,7 +3019,12 @@ int sentinel_batcher_destroy(sentinel_batcher_t *b) {
         b->stop = true;
     }
     b->cv_in.notify_all();
-    if (b->th.joinable()) b->th.join();
+    if (b->th.joinable()) b->th.join();            // queued requests are decided before it exits
+    {
+        // requesters woken by the last batch still re-take mu before they return: wait for them
+        std::unique_lock<std::mutex> lk(b->mu);
+        b->cv_idle.wait(lk, [&] { return b->callers == 0; });
+    }
     (void)hipHostFree(b->h_ev);
     (void)hipHostFree(b->h_fl);
     (void)hipHostFree(b->h_out);
@@ -2892,25 +3036,37 @@ int sentinel_batcher_request_token(sentinel_batcher_t *b, int64_t flow_id, int32
                                    sentinel_token_result_t *out) {
     if (!b || !out) return fail(SENTINEL_E_INVALID, "null argument");
     BatchReq r;
-    sentinel_lookup_flow_idx(b->e, 1, &flow_id, &r.ev.flow_idx);
-    r.ev.acquire = acquire;
-    r.ev.ts = ts;
-    r.flag = prio ? SENTINEL_FLAG_PRIORITIZED : 0;
-    {
-        std::lock_guard<std::mutex> lk(b->mu);
-        if (b->stop) return fail(SENTINEL_E_STATE, "batcher stopped");
-        b->queue.push_back(&r);
-        if ((int32_t)b->queue.size() == 1 || (int32_t)b->queue.size() >= b->max_batch) b->cv_in.notify_one();
-    }
+    BatchItem it{};
+    it.flow_id = flow_id;
+    it.ev.acquire = acquire;
+    it.ev.ts = ts;
+    it.flag = prio ? SENTINEL_FLAG_PRIORITIZED : 0;
+    it.waiter = &r;
+    if (int rc = b->enqueue(it)) return rc;
     {
         std::unique_lock<std::mutex> lk(b->mu);
         b->cv_out.wait(lk, [&] { return r.done.load(std::memory_order_acquire) != 0; });
+        if (--b->callers == 0) b->cv_idle.notify_all();
     }
     out->status = r.rc ? SENTINEL_STATUS_FAIL : r.out.status;   // engine down -> FAIL (client falls back)
     out->remaining = r.rc ? 0 : r.out.remaining;
     out->wait_in_ms = r.rc ? 0 : r.out.wait_in_ms;
     out->reserved = 0;
     return r.rc;
+}
+
+int sentinel_batcher_request_token_async(sentinel_batcher_t *b, int64_t flow_id, int32_t acquire, int32_t prio,
+                                         int64_t ts, sentinel_token_cb cb, void *ctx, uint64_t tag) {
+    if (!b || !cb) return fail(SENTINEL_E_INVALID, "null argument");
+    BatchItem it{};
+    it.flow_id = flow_id;
+    it.ev.acquire = acquire;
+    it.ev.ts = ts;
+    it.flag = prio ? SENTINEL_FLAG_PRIORITIZED : 0;
+    it.cb = cb;
+    it.ctx = ctx;
+    it.tag = tag;
+    return b->enqueue(it);
 }
 
 int sentinel_batcher_stats(sentinel_batcher_t *b, int64_t *batches, int64_t *requests) {

@@ -9,7 +9,9 @@
 //                every value's window counter is incremented (duplicates twice).  Per-value
 //                state is the exact open-addressing slot of admission.hpp (KIND_PARAM keys).
 //   PMODE_CM     the same checker over a count-min sketch of window counters (opt-in): every
-//                rule owns depth x width cells of n slots {tag = epoch mod 2^24, count}; the
+//                rule owns depth x width cells of n slots {tag = epoch mod 2^24, count} (or every
+//                rule shares one sketch keyed by the rule-unique param key, when all param rules
+//                have one window: then a stale tag is always older by >= n epochs); the
 //                estimate is the minimum over rows of the cell's window sum, so it never
 //                undercounts the value's own passes (the sketch only adds) and a request can be
 //                blocked that exact counters would pass, never the reverse.
@@ -70,6 +72,7 @@ struct SlotMeta {
     double *Is;
     double *thr;
     uint8_t *kind;
+    int32_t *rule;        // the slot's rule (read by the slot-table rebuild and the top-values query)
 };
 
 // Count-min sketch: rule-major [rule][depth][width][nmax] packed cells.
@@ -78,6 +81,7 @@ struct CountMin {
     int32_t depth;
     uint32_t width;       // power of two
     int32_t nmax;
+    bool shared;          // one sketch for every rule (param keys are unique per (rule, value))
 };
 
 constexpr int64_t LOCAL_ABSENT = INT64_MIN;   // CacheMap entry absent
@@ -166,6 +170,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_prule_prep(
                 if (h < 0) { st = ST_FAIL; break; }                    // table full
                 vslot[b + q] = (uint32_t)h;
                 if (!LOCAL) {   // identical values from every writer of this slot
+                    M.rule[h] = e.idx;
                     M.n[h] = R.n[e.idx];
                     M.w[h] = R.w[e.idx];
                     M.rcp[h] = R.rcp_w[e.idx];
@@ -221,7 +226,8 @@ constexpr uint32_t CM_TAG_MASK = (1u << 24) - 1;
 
 __host__ __device__ inline uint64_t *cm_cell(const CountMin &C, uint32_t rule, int d, uint64_t key) {
     const uint64_t col = mix64(key + 0x9E3779B97F4A7C15ull * (uint64_t)(d + 1)) & (uint64_t)(C.width - 1);
-    return C.cells + (((uint64_t)rule * (uint64_t)C.depth + (uint64_t)d) * C.width + col) * (uint64_t)C.nmax;
+    const uint64_t r = C.shared ? 0 : (uint64_t)rule;
+    return C.cells + ((r * (uint64_t)C.depth + (uint64_t)d) * C.width + col) * (uint64_t)C.nmax;
 }
 
 // Window sum of one cell at epoch E: slots tagged with one of the epochs (E-n, E] (a tag 2^24

@@ -49,13 +49,14 @@ __device__ inline int64_t slot_newest(const int64_t *st, int n) {
 }
 
 // Per rule: the newest epoch over its live slots (wave-aggregated when a wave's slots share a rule).
-__global__ __launch_bounds__(256) void k_ptable_rule_newest(PSlots T, uint64_t cap, const int32_t *__restrict__ rn,
+__global__ __launch_bounds__(256) void k_ptable_rule_newest(PSlots T, uint64_t cap, int32_t R,
+                                                            const int32_t *__restrict__ rn,
                                                             unsigned long long *__restrict__ newest) {
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool live = false;
     int32_t r = 0;
     int64_t e = EPOCH_ABSENT;
-    if (s < cap && T.keys[s] != PKEY_EMPTY) {
+    if (s < cap && T.keys[s] != PKEY_EMPTY && (uint32_t)T.rule[s] < (uint32_t)R) {
         r = T.rule[s];
         e = slot_newest(T.state + (int64_t)s * T.stride, rn[r]);
         live = e != EPOCH_ABSENT;
@@ -82,7 +83,7 @@ __global__ __launch_bounds__(256) void k_ptable_rule_newest(PSlots T, uint64_t c
 // moves to the new table (pre-initialised: keys free, state absent) under rule rmap[r]; rmap[r] == -2
 // exports the slot (key, old rule, 2n state words) to `xout` (xcount counts them); -1 drops it.
 // newest[r] - 1 = the rule's newest epoch (0: never seen -> nothing is dead).
-__global__ __launch_bounds__(256) void k_ptable_rebuild(PSlots O, uint64_t ocap, const int32_t *__restrict__ rmap,
+__global__ __launch_bounds__(256) void k_ptable_rebuild(PSlots O, uint64_t ocap, int32_t OR, const int32_t *__restrict__ rmap,
                                                         const int32_t *__restrict__ orn,
                                                         const unsigned long long *__restrict__ newest, PSlots N,
                                                         unsigned long long *__restrict__ live,
@@ -93,6 +94,7 @@ __global__ __launch_bounds__(256) void k_ptable_rebuild(PSlots O, uint64_t ocap,
     const unsigned long long key = O.keys[s];
     if (key == PKEY_EMPTY) return;
     const int32_t r = O.rule[s];
+    if ((uint32_t)r >= (uint32_t)OR) return;                 // never: every live slot has its rule
     const int32_t m = rmap[r];
     if (m == -1) return;
     const int n = orn[r];
@@ -142,13 +144,13 @@ __global__ __launch_bounds__(256) void k_ptable_import(const int64_t *__restrict
 // the sum after currentWindow(): the roll only empties an invalid bucket), and (int) of it, the
 // reference's sort key ((int) b - (int) a, ClusterParamMetric.java:107-113).  Values with no count
 // have no CacheMap entry in the reference and are not candidates.
-__global__ __launch_bounds__(256) void k_ptop_sums(PSlots T, uint64_t cap, const int32_t *__restrict__ rn,
+__global__ __launch_bounds__(256) void k_ptop_sums(PSlots T, uint64_t cap, int32_t R, const int32_t *__restrict__ rn,
                                                    const int32_t *__restrict__ rw, const double *__restrict__ rrcp,
                                                    int64_t ts, int64_t *__restrict__ sum) {
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= cap) return;
     int64_t v = 0;
-    if (T.keys[s] != PKEY_EMPTY) {
+    if (T.keys[s] != PKEY_EMPTY && (uint32_t)T.rule[s] < (uint32_t)R) {   // sum 0: not a candidate
         const int32_t r = T.rule[s];
         const int n = rn[r];
         const int64_t E = epoch_of(ts, rw[r], rrcp[r]);

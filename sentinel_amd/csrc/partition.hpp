@@ -180,7 +180,8 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(const uint32_t *__r
                                                                uint64_t *__restrict__ vals_out, int64_t n,
                                                                uint32_t finvalid, int lb, int pbits,
                                                                const uint32_t *__restrict__ offsets, int64_t nblocks,
-                                                               int32_t nparts, int32_t nflows) {
+                                                               int32_t nparts, int32_t nflows,
+                                                               uint32_t *__restrict__ qpos) {
     __shared__ uint16_t cnt[PT_WAVES][PART_BINS];
     __shared__ uint32_t goff[PART_BINS];
     __shared__ uint32_t loff[PART_BINS];
@@ -263,6 +264,18 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(const uint32_t *__r
         pre += dtot[q];
     }
     __syncthreads();
+    if (qpos)   // each event's slot in the partitioned array (arrival order: coalesced)
+#pragma unroll
+        for (int j = 0; j < PT_ITEMS; ++j) {
+            const int64_t i = base + j * WAVE + lane;
+            if (i >= n) continue;
+            uint32_t qp = 0xFFFFFFFFu;
+            if (rank[j] != 0xFFFFFFFFu) {
+                const uint32_t d = key[j] >> lb;
+                qp = goff[d] + cnt[wave][d] + rank[j];
+            }
+            qpos[i] = qp;
+        }
 #pragma unroll
     for (int j = 0; j < PT_ITEMS; ++j) {
         if (rank[j] == 0xFFFFFFFFu) continue;
@@ -292,6 +305,32 @@ __device__ inline uint64_t run_verdict(double thr, double I_s, int64_t s0, int32
     const double x = small ? (double)((int32_t)s0 + (int32_t)k * a) : (double)wrap_add(s0, wrap_mul((int64_t)k, a));
     return pack_verdict(ST_OK, java_d2i((thr - div_interval(x, I_s)) - (double)a), 0);
 }
+
+// Where a run's verdicts go: straight to the arrival position (the sequence number in the value) or
+// -- staged -- to the event's slot in the partitioned array (the range start plus its range position,
+// `spos` in LDS), from where k_part_unsplit moves every verdict back to arrival order in one coalesced
+// pass.  Staging turns the 8-byte stores at random arrival positions (one partial HBM sector each)
+// into range-local stores that the L2 combines into whole lines.
+struct VDest {
+    uint64_t *out;
+    uint64_t *stage;          // null: direct
+    const uint16_t *spos;     // LDS: range position of each sorted slot (staging only)
+    uint32_t base;            // the range's start in the partitioned array
+    __device__ inline uint32_t pos(const uint64_t *vals, uint32_t i) const {
+        return stage ? base + (uint32_t)spos[i] : ((uint32_t)vals[i] & SEQ_MASK);
+    }
+    __device__ inline void put(const uint64_t *vals, uint32_t i, uint64_t v) const {
+        if (stage) stage[base + (uint32_t)spos[i]] = v;
+        else out[(uint32_t)vals[i] & SEQ_MASK] = v;
+    }
+    __device__ inline Verdicts verdicts(const Verdicts &V) const {
+        Verdicts W = V;
+        if (stage) W.out = stage;
+        return W;
+    }
+};
+
+constexpr uint64_t VSTAGE_SKIP = ~0ull;   // staged slot decided elsewhere (k_part_big / k_part_long)
 
 template <int NMAX>
 struct FlowWindow {
@@ -399,15 +438,16 @@ struct FlowWindow {
 
     // the sequential path over sorted positions [q, q2) of `vals`
     __device__ inline void sequential(const KeyTable &T, uint32_t key, int64_t E, const uint64_t *vals, uint32_t q,
-                                      uint32_t q2, const EventSrc &src, const Verdicts &V) {
+                                      uint32_t q2, const EventSrc &src, const Verdicts &V, const VDest &D) {
         flush();
+        const Verdicts W = D.verdicts(V);
         for (uint32_t i = q; i < q2; ++i) {
             const uint32_t seq = (uint32_t)vals[i] & SEQ_MASK;
             int64_t tt;
             int32_t aa;
             uint8_t fl;
             src.load(seq, tt, aa, fl);
-            seq_event(T, key, ks, E, aa, fl, seq, V);
+            seq_event(T, key, ks, E, aa, fl, D.pos(vals, i), W);
         }
 #pragma unroll
         for (int j = 0; j < NMAX; ++j)
@@ -459,7 +499,8 @@ struct FlowWindow {
 // to the arrival positions.
 template <int NMAX>
 __device__ inline void part_run_w(FlowWindow<NMAX> &fw, const KeyTable &T, uint32_t key, const uint64_t *s_val,
-                                  uint32_t q0, uint32_t q1, const EventSrc &src, const Verdicts &V, int64_t T0) {
+                                  uint32_t q0, uint32_t q1, const EventSrc &src, const Verdicts &V, int64_t T0,
+                                  const VDest &D) {
     uint32_t q = q0;
     while (q < q1) {
         int32_t a;
@@ -474,7 +515,7 @@ __device__ inline void part_run_w(FlowWindow<NMAX> &fw, const KeyTable &T, uint3
             het |= a2 != a || (p2 && fw.kind == KIND_CLUSTER);
         }
         if (fw.slow(E, het)) {
-            fw.sequential(T, key, E, s_val, q, q2, src, V);
+            fw.sequential(T, key, E, s_val, q, q2, src, V, D);
         } else {
             int64_t s0;
             uint32_t K;
@@ -491,7 +532,7 @@ __device__ inline void part_run_w(FlowWindow<NMAX> &fw, const KeyTable &T, uint3
                 if (acc == 0x123456789ull) V.out[0] = acc;
             }
 #else
-            for (uint32_t k = 0; k < len; ++k) V.out[(uint32_t)s_val[q + k] & SEQ_MASK] = fw.verdict(s0, a, K, k, small);
+            for (uint32_t k = 0; k < len; ++k) D.put(s_val, q + k, fw.verdict(s0, a, K, k, small));
 #endif
 #endif
         }
@@ -511,7 +552,7 @@ __device__ inline void part_run_w(FlowWindow<NMAX> &fw, const KeyTable &T, uint3
 // (k_part_half's cooperative verdict sweep writes them with every lane of the workgroup).
 template <int NMAX, bool DEFER = false>
 __device__ inline bool part_run_single(FlowWindow<NMAX> &fw, const uint64_t *s_val, uint32_t q0, uint32_t q1,
-                                       const EventSrc &src, const Verdicts &V, int64_t T0, int64_t *d_s0 = nullptr,
+                                       const EventSrc &src, const VDest &D, int64_t T0, int64_t *d_s0 = nullptr,
                                        uint32_t *d_K = nullptr, int32_t *d_a = nullptr, bool *d_small = nullptr) {
     if (fw.ks.hs == 2) return false;
     fw.E0 = epoch_of(T0, fw.w, fw.rcp);
@@ -582,12 +623,11 @@ __device__ inline bool part_run_single(FlowWindow<NMAX> &fw, const uint64_t *s_v
 #if defined(SENTINEL_DIAG_NOVERDICT)     // cost diagnostic only (no output)
     uint64_t acc = 0;
     for (uint32_t k = 0; k < len; ++k) acc ^= fw.verdict(s0, a, K, k, small) ^ s_val[q0 + k];
-    if (acc == 0x123456789ull) V.out[0] = acc;
+    if (acc == 0x123456789ull) D.out[0] = acc;
 #elif defined(SENTINEL_DIAG_VLINEAR)     // cost diagnostic only (wrong output): flow-contiguous stores
-    for (uint32_t k = 0; k < len; ++k) V.out[(blockIdx.x * blockDim.x + threadIdx.x) * 8 + (k & 7)] = fw.verdict(s0, a, K, k, small);
+    for (uint32_t k = 0; k < len; ++k) D.out[(blockIdx.x * blockDim.x + threadIdx.x) * 8 + (k & 7)] = fw.verdict(s0, a, K, k, small);
 #else
-    for (uint32_t k = 0; k < len; ++k)
-        V.out[(uint32_t)s_val[q0 + k] & SEQ_MASK] = fw.verdict(s0, a, K, k, small);
+    for (uint32_t k = 0; k < len; ++k) D.put(s_val, q0 + k, fw.verdict(s0, a, K, k, small));
 #endif
     return true;
 }
@@ -601,7 +641,8 @@ constexpr uint32_t COOP_SKIP = 1u << 31, COOP_SMALL = 1u << 30;
 // the first / second segment relative to q0.
 template <int NMAX>
 __device__ inline void part_run_defer(FlowWindow<NMAX> &fw, const KeyTable &T, uint32_t key, const uint64_t *s_val,
-                                      uint32_t q0, uint32_t q1, const EventSrc &src, const Verdicts &V, int64_t T0,
+                                      uint32_t q0, uint32_t q1, const EventSrc &src, const Verdicts &V,
+                                      const VDest &D, int64_t T0,
                                       int64_t *s0o, uint32_t *reco, int32_t *ao, uint32_t &len1, uint32_t &len12,
                                       const uint32_t *segb = nullptr, const uint32_t *hetb = nullptr) {
     reco[0] = reco[1] = COOP_SKIP;
@@ -635,7 +676,7 @@ __device__ inline void part_run_defer(FlowWindow<NMAX> &fw, const KeyTable &T, u
             }
         }
         if (fw.slow(E, het)) {
-            fw.sequential(T, key, E, s_val, q, q2, src, V);
+            fw.sequential(T, key, E, s_val, q, q2, src, V, D);
         } else {
             int64_t s0;
             uint32_t K;
@@ -647,7 +688,7 @@ __device__ inline void part_run_defer(FlowWindow<NMAX> &fw, const KeyTable &T, u
                 reco[si] = K | (small ? COOP_SMALL : 0u);
                 ao[si] = a;
             } else {
-                for (uint32_t k = 0; k < len; ++k) V.out[(uint32_t)s_val[q + k] & SEQ_MASK] = fw.verdict(s0, a, K, k, small);
+                for (uint32_t k = 0; k < len; ++k) D.put(s_val, q + k, fw.verdict(s0, a, K, k, small));
             }
         }
         if (si == 0) len1 = q2 - q0;
@@ -663,7 +704,7 @@ __device__ inline void part_run(const KeyTable &T, uint32_t key, const uint64_t 
                                 const EventSrc &src, const Verdicts &V, int64_t T0) {
     FlowWindow<NMAX> fw;
     fw.load(T, key, T0);
-    part_run_w<NMAX>(fw, T, key, s_val, q0, q1, src, V, T0);
+    part_run_w<NMAX>(fw, T, key, s_val, q0, q1, src, V, T0, VDest{V.out, nullptr, nullptr, 0});
 }
 
 // Runs longer than this are decided by a whole workgroup (k_part_long): one lane walking a hot
@@ -768,7 +809,7 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
                     const uint32_t en = sgi + 1 < ns ? seg_start[sgi + 1] : cn;
                     const int64_t Es = seg_E[sgi];
                     if (fw.slow(Es, seg_flag[sgi] & 1u)) {
-                        fw.sequential(T, key, Es, sval, c0 + st, c0 + en, src, V);
+                        fw.sequential(T, key, Es, sval, c0 + st, c0 + en, src, V, VDest{V.out, nullptr, nullptr, 0});
                         seg_flag[sgi] |= 2u;
                     } else {
                         int64_t s0;
@@ -879,8 +920,9 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     KeyTable T, const uint64_t *__restrict__ pval, uint64_t *__restrict__ gsval,
     const uint32_t *__restrict__ rstart, int lb, int32_t nranges, int32_t nflows, EventSrc src, Verdicts V,
     uint32_t *__restrict__ long_runs, uint32_t *__restrict__ nlong, uint32_t *__restrict__ big,
-    uint32_t *__restrict__ nbig, unsigned long long *__restrict__ max_range) {
+    uint32_t *__restrict__ nbig, unsigned long long *__restrict__ max_range, uint64_t *__restrict__ vstage) {
     __shared__ uint64_t sv[PH_CAP];
+    __shared__ uint16_t spos[PH_CAP];      // range position of each sorted slot (arrival order inside the range)
     // the ballot ranking's per-wave counters and (after the sort) the cooperative verdict records,
     // one per flow of the half, share one LDS buffer
     constexpr int CF = COOP ? PH_COOP_FLOWS : 1;
@@ -902,7 +944,9 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     // parallel segment marking for halves of <= 128 flows: per-flow epoch parameters, then one bit per
     // sorted event for "segment start" and "heterogeneous" (acquire differs from its predecessor's or
     // a prioritized cluster request)
-    constexpr int CB = COOP ? PH_COOP_FLOWS / 2 : 1;
+    // flows of the halves the bits path serves: hb <= min(PH_COOP_HB, PH_COOP_SINGLE_HB - 1)
+    constexpr int CB = COOP ? (1 << (PH_COOP_HB < PH_COOP_SINGLE_HB - 1 ? PH_COOP_HB : PH_COOP_SINGLE_HB - 1)) : 1;
+    static_assert(!COOP || CB <= PH_COOP_FLOWS, "bits-path records fit the coop flow count");
     constexpr int MW = COOP ? (int)(PH_CAP + 31) / 32 : 1;
     __shared__ int64_t p_E0[CB];
     __shared__ double p_rcp[CB];
@@ -922,9 +966,18 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     const uint32_t pstart = rstart[p];
     const uint32_t pend = rstart[p + 1];
     const uint32_t size = pend - pstart;
+    const uint32_t hmask = (1u << hb) - 1u;
+    // local flow of a value, or 0xFFFFFFFF: not this half's (recomputed where used: no registers)
+    auto local = [&](uint64_t v) -> uint32_t {
+        const uint32_t k = (uint32_t)(v >> VAL_KEY_SHIFT);
+        return (v != ~0ull && (k >> hb) == h) ? (k & hmask) : 0xFFFFFFFFu;
+    };
     if (t == 0 && h == 0 && max_range) atomicMax(max_range, (unsigned long long)size);   // skew statistic
     if (size > PH_KEYS) {                                 // block-uniform
         if (t == 0) big[atomicAdd(nbig, 1u)] = (p << 1) | h;
+        if (vstage)                                       // k_part_big writes these verdicts itself
+            for (uint32_t q = t; q < size; q += PH_THREADS)
+                if (local(pval[pstart + q]) != 0xFFFFFFFFu) vstage[pstart + q] = VSTAGE_SKIP;
         return;
     }
     PF_STAMP(0);
@@ -932,13 +985,7 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     // range position j * PH_THREADS + t: the workgroup sweeps the range in arrival order, so the
     // slots handed out below come out nearly in arrival order and the per-run sort has little to do.
     const uint32_t b0 = (uint32_t)wave * (PH_ITEMS * WAVE);
-    const uint32_t hmask = (1u << hb) - 1u;
     uint64_t val[PH_ITEMS];                               // every value load in flight at once
-    // local flow of a value, or 0xFFFFFFFF: not this half's (recomputed where used: no registers)
-    auto local = [&](uint64_t v) -> uint32_t {
-        const uint32_t k = (uint32_t)(v >> VAL_KEY_SHIFT);
-        return (v != ~0ull && (k >> hb) == h) ? (k & hmask) : 0xFFFFFFFFu;
-    };
 #pragma unroll
     for (int j = 0; j < PH_ITEMS; ++j) {
         const uint32_t q = j * PH_THREADS + t;
@@ -963,6 +1010,12 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     const uint32_t start = block_exclusive_scan(c, waves_tot, &total);
     if (total > PH_CAP) {                                 // block-uniform: the half does not fit in LDS
         if (t == 0) big[atomicAdd(nbig, 1u)] = (p << 1) | h;
+        if (vstage)
+#pragma unroll
+            for (int j = 0; j < PH_ITEMS; ++j) {
+                const uint32_t q = j * PH_THREADS + t;
+                if (q < size && local(val[j]) != 0xFFFFFFFFu) vstage[pstart + q] = VSTAGE_SKIP;
+            }
         return;
     }
     if (c) atomicMax(&s_cmax, c);
@@ -976,19 +1029,26 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
 #pragma unroll
         for (int j = 0; j < PH_ITEMS; ++j) {
             const uint32_t kj = local(val[j]);
-            if (kj != 0xFFFFFFFFu) sv[atomicAdd(&base[kj], 1u)] = val[j];
+            if (kj != 0xFFFFFFFFu) {
+                const uint32_t slot = atomicAdd(&base[kj], 1u);
+                sv[slot] = val[j];
+                spos[slot] = (uint16_t)(j * PH_THREADS + t);
+            }
         }
         __syncthreads();
+        // range position order = arrival order inside the range (the multi-split is stable)
         for (uint32_t i = start + 1; i < start + c; ++i) {
             const uint64_t v = sv[i];
-            const uint32_t sq = (uint32_t)v & SEQ_MASK;
+            const uint16_t sq = spos[i];
             uint32_t j = i;
             for (; j > start; --j) {
-                const uint64_t u = sv[j - 1];
-                if (((uint32_t)u & SEQ_MASK) < sq) break;
-                sv[j] = u;
+                const uint16_t u = spos[j - 1];
+                if (u < sq) break;
+                sv[j] = sv[j - 1];
+                spos[j] = u;
             }
             sv[j] = v;
+            spos[j] = sq;
         }
     } else {
         // a long run somewhere: stable ranking with ballots (arrival order kept by construction),
@@ -1030,7 +1090,9 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
         for (int j = 0; j < PH_ITEMS; ++j) {
             const uint32_t kj = local(val[j]);
             if (kj == 0xFFFFFFFFu) continue;
-            sv[base[kj] + cnt[wave][kj] + rank[j]] = val[j];
+            const uint32_t slot = base[kj] + cnt[wave][kj] + rank[j];
+            sv[slot] = val[j];
+            spos[slot] = (uint16_t)(b0 + j * WAVE + lane);
         }
     }
     __syncthreads();
@@ -1049,7 +1111,11 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     }
     __syncthreads();
     for (uint32_t l = 0; l < s_nlong; ++l)
-        for (uint32_t q = t; q < s_long[l][1]; q += PH_THREADS) gsval[goff + s_long[l][0] + q] = sv[s_long[l][0] + q];
+        for (uint32_t q = t; q < s_long[l][1]; q += PH_THREADS) {
+            gsval[goff + s_long[l][0] + q] = sv[s_long[l][0] + q];
+            if (vstage) vstage[pstart + spos[s_long[l][0] + q]] = VSTAGE_SKIP;   // k_part_long writes these
+        }
+    const VDest D{V.out, vstage, spos, pstart};
     if (COOP) {                                           // launched only when 2^hb <= PH_COOP_FLOWS
 #ifndef SENTINEL_NO_COOP_BITS
         const bool bits = hb < PH_COOP_SINGLE_HB;         // block-uniform
@@ -1106,12 +1172,12 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
                 // (hb <= 7) a run straddles an epoch boundary often and the walk alone is cheaper
                 // (measured: 125k flows +4%, 250k +1%; 500k flows -1% without it)
                 if (hb >= PH_COOP_SINGLE_HB &&
-                    part_run_single<NMAX, true>(fw, sv, start, start + c, src, V, T0, &s0[0], &rec[0], &a[0], &small)) {
+                    part_run_single<NMAX, true>(fw, sv, start, start + c, src, D, T0, &s0[0], &rec[0], &a[0], &small)) {
                     rec[0] |= small ? COOP_SMALL : 0u;
                     len1 = len12 = c;
                 } else {
                     fw.load_header(T0);
-                    part_run_defer<NMAX>(fw, T, key, sv, start, start + c, src, V, T0, s0, rec, a, len1, len12,
+                    part_run_defer<NMAX>(fw, T, key, sv, start, start + c, src, V, D, T0, s0, rec, a, len1, len12,
                                          bits ? segb : nullptr, bits ? hetb : nullptr);
                 }
                 c_thr[t] = fw.thr;
@@ -1137,13 +1203,12 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
             const uint32_t sg = k < l1 ? 0u : 1u;
             const uint32_t rec = c_K[sg * CF + kj];
             if (rec & COOP_SKIP) continue;                        // sequential segment: written by the walk
-            V.out[(uint32_t)v & SEQ_MASK] = run_verdict(c_thr[kj], c_is[kj], c_s0[sg * CF + kj], c_a[sg * CF + kj],
-                                                        rec & (COOP_SMALL - 1u), sg ? k - l1 : k,
-                                                        (rec & COOP_SMALL) != 0);
+            D.put(sv, i, run_verdict(c_thr[kj], c_is[kj], c_s0[sg * CF + kj], c_a[sg * CF + kj],
+                                     rec & (COOP_SMALL - 1u), sg ? k - l1 : k, (rec & COOP_SMALL) != 0));
         }
-    } else if (c > 0 && c <= LONG_RUN && !part_run_single<NMAX>(fw, sv, start, start + c, src, V, T0)) {
+    } else if (c > 0 && c <= LONG_RUN && !part_run_single<NMAX>(fw, sv, start, start + c, src, D, T0)) {
         fw.load_header(T0);
-        part_run_w<NMAX>(fw, T, key, sv, start, start + c, src, V, T0);
+        part_run_w<NMAX>(fw, T, key, sv, start, start + c, src, V, T0, D);
     }
 #ifdef SENTINEL_DIAG_PHASES
     __syncthreads();
@@ -1248,6 +1313,39 @@ __global__ __launch_bounds__(PH_THREADS) void k_part_big(
         }
         if (c > 0 && c <= LONG_RUN) part_run<NMAX>(T, key, dst, start, start + c, src, V, T0);
         __syncthreads();                                  // LDS reuse by the next entry
+    }
+}
+
+// Staged verdicts back to arrival order: out[i] = stage[qpos[i]] (qpos written by k_part_scatter, 0xFFFFFFFF
+// for events decided by the prep kernel; VSTAGE_SKIP marks verdicts k_part_big / k_part_long wrote
+// themselves).  Chunks of consecutive arrival positions are assigned XCD by XCD (block b runs on XCD
+// b mod 8), so the ~64 workgroups an XCD runs at once cover a contiguous stretch of the batch and the
+// staged lines they gather (a few consecutive slots per range) are fetched from HBM once, then hit in
+// that XCD's L2.
+constexpr int PU_THREADS = 256;
+constexpr int PU_ITEMS = 8;
+constexpr int PU_CHUNK = PU_THREADS * PU_ITEMS;
+__global__ __launch_bounds__(PU_THREADS) void k_part_unsplit(int64_t n, const uint32_t *__restrict__ qpos,
+                                                             const uint64_t *__restrict__ stage,
+                                                             uint64_t *__restrict__ out) {
+    const int64_t nchunks = (n + PU_CHUNK - 1) / PU_CHUNK;
+    const int64_t per_xcd = (nchunks + 7) / 8;
+    const int64_t c = (int64_t)(blockIdx.x & 7u) * per_xcd + (int64_t)(blockIdx.x >> 3);
+    if (c >= nchunks) return;
+    const int64_t i0 = c * PU_CHUNK;
+    uint32_t q[PU_ITEMS];
+#pragma unroll
+    for (int j = 0; j < PU_ITEMS; ++j) {
+        const int64_t i = i0 + j * PU_THREADS + threadIdx.x;
+        q[j] = i < n ? qpos[i] : 0xFFFFFFFFu;
+    }
+    uint64_t v[PU_ITEMS];
+#pragma unroll
+    for (int j = 0; j < PU_ITEMS; ++j) v[j] = q[j] != 0xFFFFFFFFu ? stage[q[j]] : VSTAGE_SKIP;
+#pragma unroll
+    for (int j = 0; j < PU_ITEMS; ++j) {
+        const int64_t i = i0 + j * PU_THREADS + threadIdx.x;
+        if (v[j] != VSTAGE_SKIP) out[i] = v[j];
     }
 }
 
