@@ -145,6 +145,7 @@ struct BatchWork {
     int64_t *seg_epoch;
     int32_t *seg_acq;
     uint8_t *seg_het;            // heterogeneous / prioritized segment
+    uint8_t *seg_prio;           // segment holds a prioritized cluster request (the sequential path)
     uint8_t *seg_done;           // decided by the sequential path
     int64_t *seg_s0;             // PASS sum at segment start (after the roll)
     uint32_t *seg_k;             // number of passing events
@@ -190,6 +191,18 @@ struct KeyState {
     // ClusterMetric.add of a decided homogeneous segment on slot `slot` (CFC:76-77,100-101):
     // BLOCK += nb*a, PASS_REQUEST += K, BLOCK_REQUEST += nb, from the slot's previous values
     // (zero for a fresh bucket, whose other counters are cleared: LeapArray.resetWindowTo)
+    // the same for a heterogeneous segment: BLOCK += sum of blocked acquires, PASS_REQUEST += passes,
+    // BLOCK_REQUEST += blocks
+    __device__ inline void book_rest_sums(int slot, bool fresh, int64_t blk, int64_t preq, int64_t breq,
+                                          int64_t add_blk, int64_t add_preq, int64_t add_breq) const {
+        if (fresh) { blk = 0; preq = 0; breq = 0; }
+        rc(slot, EV_BLOCK - 1) = wrap_add(blk, add_blk);
+        rc(slot, EV_PASS_REQUEST - 1) = wrap_add(preq, add_preq);
+        rc(slot, EV_BLOCK_REQUEST - 1) = wrap_add(breq, add_breq);
+        if (fresh)
+#pragma unroll
+            for (int c = 3; c < 6; ++c) rc(slot, c) = 0;
+    }
     __device__ inline void book_rest(int slot, bool fresh, int64_t blk, int64_t preq, int64_t breq, int64_t nb,
                                      int32_t a, uint32_t K) const {
         if (fresh) { blk = 0; preq = 0; breq = 0; }
@@ -305,6 +318,51 @@ __device__ inline bool admits(uint8_t kind, double thr, double I_s, int64_t x, i
 
 __device__ inline double remaining_of(double thr, double I_s, int64_t x, int32_t a) {
     return (thr - div_interval((double)x, I_s)) - (double)a;
+}
+
+// A segment whose events share the epoch but not the acquire count, with no prioritized cluster
+// request, no pending occupy transfer and no slot newer than its epoch: the reference state machine
+// (seq_event) reduced to what such a segment can reach.  Every event reads the same rolled window, so
+// the running PASS sum lives in a register -- x = S0 + passed, event k passes iff the checker's test
+// holds for (x, a_k) in Java operation order (ClusterFlowChecker.java:67-82,
+// SimpleClusterFlowChecker.java:41-64, ClusterParamFlowChecker.java:62-70) -- and the counters are
+// booked once at the end instead of per event in global memory.
+struct HetSums {
+    int64_t pass, npass, block, nblock;
+};
+
+// Events are fetched HW at a time (independent loads in flight together, values kept in registers
+// for the verdict stores); once not even an acquire of 1 is admitted (acquire >= 1 past validation,
+// admits monotone in both arguments) the rest of the segment is blocked without evaluating the test.
+// load(k) -> the k-th packed value, acq(v) -> its acquire count, put(v, verdict).
+template <uint32_t HW, class Load, class Acq, class Put>
+__device__ inline HetSums het_walk(uint8_t kind, double thr, double I_s, int64_t s0, uint32_t len, Load load, Acq acq,
+                                   Put put) {
+    HetSums h{0, 0, 0, 0};
+    bool dead = false;
+    for (uint32_t k0 = 0; k0 < len; k0 += HW) {
+        uint64_t vv[HW];
+#pragma unroll
+        for (uint32_t j = 0; j < HW; ++j) vv[j] = k0 + j < len ? load(k0 + j) : 0ull;
+        if (!dead) dead = !admits(kind, thr, I_s, wrap_add(s0, h.pass), 1);
+#pragma unroll
+        for (uint32_t j = 0; j < HW; ++j) {
+            if (k0 + j >= len) continue;
+            const int32_t a = acq(vv[j]);
+            const double next = dead ? -1.0 : remaining_of(thr, I_s, wrap_add(s0, h.pass), a);
+            const bool ok = kind == KIND_PARAM ? !(next < 0.0) : next >= 0.0;
+            if (ok) {
+                h.pass = wrap_add(h.pass, a);
+                h.npass += 1;
+                put(vv[j], pack_verdict(ST_OK, java_d2i(next), 0));
+            } else {
+                h.block = wrap_add(h.block, a);
+                h.nblock += 1;
+                put(vv[j], pack_verdict(ST_BLOCKED, 0, 0));
+            }
+        }
+    }
+    return h;
 }
 
 __device__ inline void reject_limited(const Verdicts &V, uint32_t seq) {
@@ -627,6 +685,7 @@ __global__ __launch_bounds__(SEG_THREADS) void k_segments(KeyTable T, BatchWork 
             W.seg_acq[g - 1] = acq[j];
         }
         if (badmask & (1u << j)) W.seg_het[g - 1] = 1;
+        if (prio[j]) W.seg_prio[g - 1] = 1;
         s_key[q] = g;                // 1-based segment id
         const bool last = (i == n - 1) || (j + 1 < SEG_ITEMS ? key[j + 1] == invalid : W.skey[i + 1] == invalid);
         if (last) {
@@ -657,7 +716,7 @@ __global__ __launch_bounds__(256) void k_seg_mark(BatchWork W, int64_t n) {
         W.seg_epoch[g - 1] = W.h_epoch[i];
         W.seg_acq[g - 1] = W.h_acq[i];
     }
-    if (W.bad[i]) W.seg_het[g - 1] = 1;
+    if (W.bad[i]) { W.seg_het[g - 1] = 1; W.seg_prio[g - 1] = 1; }   // (split path: prio not told apart)
     if (i == nv - 1) {
         W.seg_start[g] = (uint32_t)nv;
         *W.nseg = g;
@@ -727,13 +786,80 @@ __global__ __launch_bounds__(256) void k_process(KeyTable T, BatchWork W, EventS
 // (NMAX >= n).  All header lines are requested at once with 16-byte loads, so each line of the
 // state crosses the memory system once per batch; only the rolled slot's pair and its rest line
 // are written back.  Slow segments fall back to the sequential path on global memory.
+// A key with more events than this and a heterogeneous-acquire segment is handed to the workgroup
+// kernels (k_part_long, cooperative walk) instead of one lane walking every event (the engine's
+// default; SENTINEL_HOT_HET_RUN overrides it).
+constexpr uint32_t HOT_HET_RUN = 4096;
+
+// Hot runs handed to the workgroup kernels (k_long_scan -> k_part_long -> k_long_dead).  Run r =
+// {q0, q1, key, first chunk} over the sorted values; its events are cut in LR_CHUNK-event chunks
+// numbered consecutively over the batch (chunk_run[g] = run of chunk g), each with a summary record.
+constexpr uint32_t LR_CHUNK = 4096;
+constexpr uint32_t LR_UNIFORM = 1u;    // one epoch, no prioritized cluster request
+constexpr uint32_t LR_DEAD = 2u;       // every event blocked: k_long_dead writes the verdicts
+struct LongRec {
+    int64_t E;            // epoch of the chunk's first event
+    int64_t acq;          // sum of the chunk's acquire counts
+    uint32_t cnt;         // events
+    uint32_t flags;
+    int64_t pad;
+};
+struct LongRuns {
+    uint32_t *nrun;       // runs pushed
+    uint32_t *nchunk;     // chunks pushed
+    uint32_t *runs;       // 4 words per run
+    uint32_t *chunk_run;
+    LongRec *rec;         // null: no chunk summaries this batch (k_part_long decides every chunk)
+    uint32_t *host_chunks;  // pinned: the batch's chunk count, a hint for the next batch's launch
+    __device__ inline void push(uint32_t q0, uint32_t q1, uint32_t key) const {
+        const uint32_t nch = (q1 - q0 + LR_CHUNK - 1) / LR_CHUNK;
+        const uint32_t j = atomicAdd(nrun, 1u);
+        const uint32_t cb = atomicAdd(nchunk, nch);
+        runs[4 * (uint64_t)j] = q0;
+        runs[4 * (uint64_t)j + 1] = q1;
+        runs[4 * (uint64_t)j + 2] = key;
+        runs[4 * (uint64_t)j + 3] = cb;
+        for (uint32_t c = 0; c < nch; ++c) chunk_run[cb + c] = j;
+    }
+};
+// capacities for a batch of n events whose runs are all longer than min_run
+inline size_t long_runs_cap(int64_t n, uint32_t min_run) { return (size_t)n / min_run + 2; }
+inline size_t long_chunks_cap(int64_t n, uint32_t min_run) {
+    return (size_t)n / LR_CHUNK + long_runs_cap(n, min_run) + 1;
+}
+
+// Keys with more events than this and a heterogeneous-acquire segment (but not hot enough for the
+// workgroup kernels) are walked by one wave each (k_process_wave): {count, first segment of each key}.
+constexpr uint32_t WAVE_HET_RUN = 48;
+struct WaveRuns {
+    uint32_t *n;
+    uint32_t *g0;
+};
+
 template <int NMAX>
-__global__ __launch_bounds__(256) void k_process_reg(KeyTable T, BatchWork W, EventSrc src, Verdicts V, int64_t n) {
+__global__ __launch_bounds__(256) void k_process_reg(KeyTable T, BatchWork W, EventSrc src, Verdicts V, int64_t n,
+                                                     LongRuns L = LongRuns{}, WaveRuns WR = WaveRuns{},
+                                                     uint32_t hot_run = HOT_HET_RUN) {
     const int64_t g0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t S = (int64_t)*W.nseg;
     if (g0 >= S || (int64_t)*W.nvalid == 0) return;
     const uint32_t key = W.seg_key[g0];
     if (g0 > 0 && W.seg_key[g0 - 1] == key) return;    // not the first segment of its key
+    if (L.nrun) {
+        int64_t ge = g0;
+        bool het = false;
+        for (; ge < S && W.seg_key[ge] == key; ++ge) het |= W.seg_het[ge] && !W.seg_prio[ge];
+        const uint32_t q0 = W.seg_start[g0], q1 = W.seg_start[ge];
+        if (het && q1 - q0 > hot_run) {
+            L.push(q0, q1, key);
+            for (int64_t g = g0; g < ge; ++g) W.seg_done[g] = 1;
+            return;
+        }
+        if (het && WR.n && q1 - q0 > WAVE_HET_RUN) {
+            WR.g0[atomicAdd(WR.n, 1u)] = (uint32_t)g0;
+            return;
+        }
+    }
     const KeyState ks = key_state(T, key);
     const int nsc = ks.n;
     const uint8_t kind = T.kind[key];
@@ -758,10 +884,42 @@ __global__ __launch_bounds__(256) void k_process_reg(KeyTable T, BatchWork W, Ev
         const uint32_t st = W.seg_start[g];
         const uint32_t len = W.seg_start[g + 1] - st;
         const int64_t E = W.seg_epoch[g];
-        bool slow = W.seg_het[g] || occ_pending;
+        bool slow = W.seg_prio[g] || occ_pending;
 #pragma unroll
         for (int j = 0; j < NMAX; ++j) slow |= (ep[j] != EPOCH_ABSENT && ep[j] > E);
-        if (slow) {
+        if (!slow && W.seg_het[g]) {          // heterogeneous acquire counts: the register walk
+            const int slot = (int)(E % nsc);
+            bool fresh = false;
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j)
+                if (j == slot && ep[j] != E) { fresh = true; ep[j] = E; ps[j] = 0; }
+            int64_t s0 = 0;
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j)
+                if (ep[j] != EPOCH_ABSENT && ep[j] > E - nsc) s0 = wrap_add(s0, ps[j]);
+            const int64_t T0 = src.t0();
+            const HetSums hs = het_walk<16>(
+                kind, thr, I_s, s0, len, [&](uint32_t k) { return W.sval[st + k]; },
+                [&](uint64_t v) {
+                    int64_t t;
+                    int32_t a;
+                    bool pr;
+                    src.unpack(v, T0, t, a, pr);
+                    return a;
+                },
+                [&](uint64_t v, uint64_t vd) { V.out[(uint32_t)v & SEQ_MASK] = vd; });
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j)
+                if (j == slot) { ps[j] = wrap_add(ps[j], hs.pass); dirty |= 1u << j; }
+            if (ks.seven) {
+                int64_t blk = 0, preq = 0, breq = 0;
+                if (!fresh) { blk = ks.rc(slot, 0); preq = ks.rc(slot, 1); breq = ks.rc(slot, 2); }
+                ks.book_rest_sums(slot, fresh, blk, preq, breq, hs.block, hs.npass, hs.nblock);
+            }
+            W.seg_done[g] = 1;
+            continue;
+        }
+        if (slow || W.seg_het[g]) {
 #pragma unroll
             for (int j = 0; j < NMAX; ++j)
                 if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.pair(j)) = longlong2{ep[j], ps[j]};
@@ -815,6 +973,209 @@ __global__ __launch_bounds__(256) void k_process_reg(KeyTable T, BatchWork W, Ev
 #pragma unroll
     for (int j = 0; j < NMAX; ++j)
         if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.pair(j)) = longlong2{ep[j], ps[j]};
+}
+
+// Wave-wide greedy walk (k_process_wave, and coop_het past its first failure): events i in [0, len),
+// fetched by fetch(i, a, dst) 64 at a time, one per lane, decided as het_walk would, in rounds that
+// each settle at least one event (wave scans and ballots, no barriers):
+//   P: lanes >= cur pass while admits(x + their exclusive acquire prefix): first failing lane f;
+//   S: f blocked; the next pass is the first lane c > f with admits(x, a_c) (x does not grow until
+//      then, admits is monotone in x); (f, c) blocked, c passes.
+// Once not even an acquire of 1 is admitted, the rest is blocked without tests.  x, npass and acq
+// (the acquire total) are updated in every lane.
+template <class Fetch>
+__device__ inline void wave_walk(uint8_t kind, double thr, double I_s, uint32_t len, int64_t &x, int64_t &npass,
+                                 int64_t &acq_total, Fetch fetch) {
+    const uint32_t lane = lane_id();
+    bool dead = false;
+    for (uint32_t c0 = 0; c0 < len; c0 += WAVE) {
+        const uint32_t cnt = min((uint32_t)WAVE, len - c0);
+        const bool valid = lane < cnt;
+        int32_t a = 0;
+        uint64_t *dst = nullptr;
+        if (valid) fetch(c0 + lane, a, dst);
+        {
+            int64_t sa = a;
+#pragma unroll
+            for (int off = 1; off < WAVE; off <<= 1) sa += __shfl_xor(sa, off, WAVE);
+            acq_total = wrap_add(acq_total, sa);
+        }
+        uint32_t cur = 0;
+        while (cur < cnt) {
+            if (!dead) dead = !admits(kind, thr, I_s, x, 1);
+            if (dead) {
+                if (valid && lane >= cur) *dst = pack_verdict(ST_BLOCKED, 0, 0);
+                break;
+            }
+            // P round
+            const int64_t m = (valid && lane >= cur) ? (int64_t)a : 0;
+            int64_t inc = m;
+#pragma unroll
+            for (int off = 1; off < WAVE; off <<= 1) {
+                const int64_t u = __shfl_up(inc, off, WAVE);
+                if ((int)lane >= off) inc += u;
+            }
+            const int64_t pre = inc - m;
+            const bool fail = valid && lane >= cur && !admits(kind, thr, I_s, wrap_add(x, pre), a);
+            const unsigned long long fm = __ballot(fail);
+            const uint32_t f = fm ? (uint32_t)__ffsll((long long)fm) - 1 : cnt;
+            if (valid && lane >= cur && lane < f)
+                *dst = pack_verdict(ST_OK, java_d2i(remaining_of(thr, I_s, wrap_add(x, pre), a)), 0);
+            npass += (int64_t)(f - cur);
+            if (f >= cnt) {
+                x = wrap_add(x, __shfl(inc, (int)cnt - 1, WAVE));
+                break;
+            }
+            x = wrap_add(x, __shfl(pre, (int)f, WAVE));
+            // S round
+            const bool cand = valid && lane > f && admits(kind, thr, I_s, x, a);
+            const unsigned long long cm = __ballot(cand);
+            const uint32_t c = cm ? (uint32_t)__ffsll((long long)cm) - 1 : cnt;
+            if (valid && lane >= f && lane < c) *dst = pack_verdict(ST_BLOCKED, 0, 0);
+            if (lane == c && c < cnt) *dst = pack_verdict(ST_OK, java_d2i(remaining_of(thr, I_s, x, a)), 0);
+            if (c >= cnt) break;
+            x = wrap_add(x, (int64_t)__shfl(a, (int)c, WAVE));
+            npass += 1;
+            cur = c + 1;
+        }
+    }
+}
+
+// A heterogeneous segment [st, st + len) of the sorted values, walked by one wave.
+__device__ inline HetSums wave_het(uint8_t kind, double thr, double I_s, int64_t x, const uint64_t *sval, uint32_t st,
+                                   uint32_t len, const EventSrc &src, int64_t T0, uint64_t *out) {
+    const int64_t x0 = x;
+    int64_t npass = 0, tot = 0;
+    wave_walk(kind, thr, I_s, len, x, npass, tot, [&](uint32_t i, int32_t &a, uint64_t *&dst) {
+        const uint64_t v = sval[st + i];
+        int64_t t;
+        bool pr;
+        src.unpack(v, T0, t, a, pr);
+        dst = out + ((uint32_t)v & SEQ_MASK);
+    });
+    HetSums h;
+    h.pass = wrap_add(x, -x0);
+    h.npass = npass;
+    h.block = wrap_add(tot, -h.pass);
+    h.nblock = (int64_t)len - npass;
+    return h;
+}
+
+// One wave per key of the wave list (k_process_reg's keys of WAVE_HET_RUN..HOT_HET_RUN events with a
+// heterogeneous segment): the key's segments in order, the window header in every lane's VGPRs (the
+// same values: uniform), memory written by lane 0.  Closed-form segments leave {s0, K} for
+// k_verdict; heterogeneous ones are decided by wave_het; prioritized / pending-occupy / clock-went-
+// back ones take the sequential path in lane 0, after which every lane re-reads the header.
+template <int NMAX>
+__global__ __launch_bounds__(256) void k_process_wave(KeyTable T, BatchWork W, EventSrc src, Verdicts V, WaveRuns WR) {
+    const uint32_t total = *WR.n;
+    const uint32_t lane = lane_id();
+    const int64_t T0 = src.t0();
+    for (uint32_t wi = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE; wi < total;
+         wi += gridDim.x * blockDim.x / WAVE) {
+        const int64_t S = (int64_t)*W.nseg;
+        const int64_t g0 = WR.g0[wi];
+        const uint32_t key = W.seg_key[g0];
+        const KeyState ks = key_state(T, key);
+        const int nsc = ks.n;
+        const uint8_t kind = T.kind[key];
+        const double thr = T.thr[key];
+        const double I_s = T.I_s[key];
+        int64_t ep[NMAX], ps[NMAX];
+        uint32_t dirty = 0;
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j) {
+            if (j < nsc) {
+                const longlong2 v = *reinterpret_cast<const longlong2 *>(ks.pair(j));
+                ep[j] = v.x;
+                ps[j] = v.y;
+            } else {
+                ep[j] = EPOCH_ABSENT;
+                ps[j] = 0;
+            }
+        }
+        bool occ_pending = ks.seven && kind == KIND_CLUSTER && T.has_occ[key];
+        for (int64_t g = g0; g < S && W.seg_key[g] == key; ++g) {
+            const uint32_t st = W.seg_start[g];
+            const uint32_t len = W.seg_start[g + 1] - st;
+            const int64_t E = W.seg_epoch[g];
+            bool slow = W.seg_prio[g] || occ_pending;
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j) slow |= (ep[j] != EPOCH_ABSENT && ep[j] > E);
+            if (slow) {
+                if (lane == 0) {
+#pragma unroll
+                    for (int j = 0; j < NMAX; ++j)
+                        if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.pair(j)) = longlong2{ep[j], ps[j]};
+                    for (uint32_t i = st; i < st + len; ++i) {
+                        const uint32_t seq = (uint32_t)W.sval[i] & SEQ_MASK;
+                        int64_t t;
+                        int32_t a;
+                        uint8_t fl;
+                        src.load(seq, t, a, fl);
+                        seq_event(T, key, ks, E, a, fl, seq, V);
+                    }
+                    W.seg_done[g] = 1;
+#pragma unroll
+                    for (int j = 0; j < NMAX; ++j)
+                        if (j < nsc) { ep[j] = ks.ep(j); ps[j] = ks.cnt(EV_PASS, j); }
+                    occ_pending = ks.seven && kind == KIND_CLUSTER && T.has_occ[key];
+                }
+                dirty = 0;
+#pragma unroll
+                for (int j = 0; j < NMAX; ++j) {
+                    ep[j] = __shfl(ep[j], 0, WAVE);
+                    ps[j] = __shfl(ps[j], 0, WAVE);
+                }
+                occ_pending = __shfl((int)occ_pending, 0, WAVE) != 0;
+                continue;
+            }
+            const int slot = (int)(E % nsc);
+            bool fresh = false;
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j)
+                if (j == slot && ep[j] != E) { fresh = true; ep[j] = E; ps[j] = 0; }
+            int64_t s0 = 0;
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j)
+                if (ep[j] != EPOCH_ABSENT && ep[j] > E - nsc) s0 = wrap_add(s0, ps[j]);
+            int64_t blk = 0, preq = 0, breq = 0;
+            if (ks.seven && !fresh) { blk = ks.rc(slot, 0); preq = ks.rc(slot, 1); breq = ks.rc(slot, 2); }
+            if (W.seg_het[g]) {
+                const HetSums hs = wave_het(kind, thr, I_s, s0, W.sval, st, len, src, T0, V.out);
+#pragma unroll
+                for (int j = 0; j < NMAX; ++j)
+                    if (j == slot) { ps[j] = wrap_add(ps[j], hs.pass); dirty |= 1u << j; }
+                if (lane == 0) {
+                    if (ks.seven) ks.book_rest_sums(slot, fresh, blk, preq, breq, hs.block, hs.npass, hs.nblock);
+                    W.seg_done[g] = 1;
+                }
+                continue;
+            }
+            const int32_t a = W.seg_acq[g];
+            uint32_t lo = 0, hi = len;                      // K = first p with !admits(S0 + p*a)
+            while (lo < hi) {
+                const uint32_t mid = lo + (hi - lo) / 2;
+                if (admits(kind, thr, I_s, wrap_add(s0, wrap_mul((int64_t)mid, a)), a)) lo = mid + 1;
+                else hi = mid;
+            }
+            const uint32_t K = lo;
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j)
+                if (j == slot) { ps[j] = wrap_add(ps[j], wrap_mul((int64_t)K, a)); dirty |= 1u << j; }
+            if (lane == 0) {
+                if (ks.seven) ks.book_rest(slot, fresh, blk, preq, breq, (int64_t)(len - K), a, K);
+                W.seg_s0[g] = s0;
+                W.seg_k[g] = K;
+                W.seg_done[g] = 0;
+            }
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j)
+                if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.pair(j)) = longlong2{ep[j], ps[j]};
+        }
+    }
 }
 
 // K1+K3 with a lane group per key (G lanes, up to PROC_SLOTS_PER_LANE slots per lane, so

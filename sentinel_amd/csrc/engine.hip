@@ -374,6 +374,23 @@ struct FlatIndex {
 };
 
 // ==================================================================== engine
+// Hot-run work list laid out after `head` words of a control buffer: runs (4 words each), the
+// chunk -> run map, then the 32-byte chunk records.
+static size_t long_runs_bytes(int64_t n, uint32_t min_run, size_t head) {
+    const size_t words = head + 4 * long_runs_cap(n, min_run) + long_chunks_cap(n, min_run);
+    return ((words * 4 + 31) & ~(size_t)31) + long_chunks_cap(n, min_run) * sizeof(LongRec);
+}
+static LongRuns long_runs_at(uint32_t *ctl, int64_t n, uint32_t min_run, size_t head) {
+    LongRuns L;
+    L.nrun = ctl;
+    L.nchunk = ctl + 2;
+    L.runs = ctl + head;
+    L.chunk_run = L.runs + 4 * long_runs_cap(n, min_run);
+    const size_t words = head + 4 * long_runs_cap(n, min_run) + long_chunks_cap(n, min_run);
+    L.rec = reinterpret_cast<LongRec *>(reinterpret_cast<char *>(ctl) + ((words * 4 + 31) & ~(size_t)31));
+    return L;
+}
+
 struct sentinel_engine {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -407,6 +424,8 @@ struct sentinel_engine {
     // range > 8x the mean): then the sorted path for the next 1024 batches, then one probe again
     DevBuf d_part_stat;
     unsigned long long *h_part_stat = nullptr;   // pinned mirror, written asynchronously after each batch
+    uint32_t *h_long_chunks = nullptr;           // pinned: hot-run chunks of a recent batch (launch hint)
+    uint32_t hot_het_run = HOT_HET_RUN;          // sorted path: heterogeneous keys above this go to k_part_long
     int64_t flow_batches = 0, sorted_until = -1;
     bool diag_linear = false;  // SENTINEL_DIAG_LINEAR=1: verdicts in sorted order (cost diagnostic, wrong output)   // SENTINEL_PROCESS: 0 reg (default), 1 group, 2 thread-in-memory
     int64_t flow_state_words = 0;
@@ -492,6 +511,27 @@ struct sentinel_engine {
         prof_pending.push_back({name, a, b, units});
     }
 
+    // the hot-run kernels: chunk summaries, the per-run walk, the dead chunks' verdicts
+    template <int NM>
+    void launch_long(const KeyTable &T, const uint64_t *sval, const LongRuns &L, const EventSrc &src, const Verdicts &V,
+                     int64_t n, uint32_t min_run, hipStream_t s, const unsigned long long *stat,
+                     unsigned long long *host_stat) {
+        // the chunk summaries pay off only for batches with hot runs: launched when an earlier batch had
+        // some (the count comes back through pinned memory; without them every chunk is decided in full)
+        if (!h_long_chunks) {
+            if (hipHostMalloc((void **)&h_long_chunks, 4, 0) != hipSuccess) h_long_chunks = nullptr;
+            else *h_long_chunks = 1;
+        }
+        LongRuns LL = L;
+        LL.host_chunks = h_long_chunks;
+        const bool recs = !h_long_chunks || *(volatile uint32_t *)h_long_chunks > 0;
+        if (!recs) LL.rec = nullptr;
+        const unsigned gc = (unsigned)std::min<size_t>(long_chunks_cap(n, min_run), 2048);
+        if (recs) k_long_scan<<<gc, LS_THREADS, 0, s>>>(T, sval, LL, src);
+        k_part_long<NM><<<256, PL_THREADS, 0, s>>>(T, sval, LL, src, V, stat, host_stat);
+        if (recs) k_long_dead<<<gc, LS_THREADS, 0, s>>>(sval, LL, V);
+    }
+
     void prof_collect() {
         for (auto &r : prof_pending) {
             (void)hipEventSynchronize(r.b);
@@ -510,12 +550,10 @@ struct sentinel_engine {
 
     // batch workspace
     DevBuf w_fkey, w_lkey, w_skey, w_sval, w_ktmp, w_vtmp, w_fhist, w_lhist, w_parts, w_segid, w_bad, w_hep,
-        w_hacq, w_segstart, w_segkey, w_segep, w_segacq, w_het, w_done, w_s0, w_k, w_counters;
+        w_hacq, w_segstart, w_segkey, w_segep, w_segacq, w_het, w_prio, w_done, w_s0, w_k, w_counters;
     DevBuf w_vslot;                    // slot of every value of a param batch
     DevBuf w_runs;                     // partition path: long-run / oversized-half work lists
     DevBuf w_pscan;                    // partition path: per-group range sums + range starts
-    DevBuf w_qpos, w_vstage;           // partition path, staged verdicts: slot of each event, staged verdicts
-    bool vstage_on = false;            // SENTINEL_VSTAGE=1: stage verdicts (k_part_unsplit)
     DevBuf io_ev, io_fl, io_out, io_vals;
     // streamed host path (sentinel_submit_flow_stream_host): copy streams + two staging slots
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
@@ -530,7 +568,7 @@ struct sentinel_engine {
         for (DevBuf *b : {&w_fkey, &w_lkey, &w_skey, &w_ktmp, &w_segid, &w_segkey, &w_k, &w_hacq, &w_segacq})
             rc |= b->ensure(c * 4);
         for (DevBuf *b : {&w_hep, &w_segep, &w_s0, &w_sval, &w_vtmp}) rc |= b->ensure(c * 8);
-        for (DevBuf *b : {&w_bad, &w_het, &w_done}) rc |= b->ensure(c);
+        for (DevBuf *b : {&w_bad, &w_het, &w_prio, &w_done}) rc |= b->ensure(c);
         rc |= w_fhist.ensure((size_t)(hist_words(c, MAX_PASSES) + 64) * 4);
         rc |= w_lhist.ensure((size_t)hist_words(c, MAX_PASSES) * 4);
         rc |= w_parts.ensure((size_t)(scan_parts(std::max<int64_t>(c, hist_words(c, MAX_PASSES))) + 16) * 8);
@@ -554,6 +592,7 @@ struct sentinel_engine {
         W.seg_epoch = w_segep.as<int64_t>();
         W.seg_acq = w_segacq.as<int32_t>();
         W.seg_het = w_het.as<uint8_t>();
+        W.seg_prio = w_prio.as<uint8_t>();
         W.seg_done = w_done.as<uint8_t>();
         W.seg_s0 = w_s0.as<int64_t>();
         W.seg_k = w_k.as<uint32_t>();
@@ -699,6 +738,7 @@ struct sentinel_engine {
         sort(keys, n, bits, hist, src, s);
         const unsigned g = grid_for(n);
         (void)hipMemsetAsync(W.seg_het, 0, (size_t)n, s);
+        (void)hipMemsetAsync(W.seg_prio, 0, (size_t)n, s);
         if (fused_segments) {
             const int64_t nt = (n + SEG_TILE - 1) / SEG_TILE;
             unsigned long long *status = w_parts.as<unsigned long long>();
@@ -716,22 +756,50 @@ struct sentinel_engine {
 
     // The generic pipeline: sort by key, segment, decide, scatter.
     void run_pipeline(const KeyTable &T, const uint32_t *keys, uint32_t *hist, int64_t n, int bits,
-                      const EventSrc &src, const Verdicts &V, hipStream_t s, int max_n, bool limiter) {
+                      const EventSrc &src, const Verdicts &V, hipStream_t s, int max_n, bool limiter,
+                      bool hot_het = false) {
         sort_segments(T, keys, hist, n, bits, src, s);
         BatchWork W = work();
         const unsigned g = grid_for(n);
+        // flow tables: keys hotter than HOT_HET_RUN with heterogeneous acquires go to the hot-run kernels
+        // (and keys of WAVE_HET_RUN..HOT_HET_RUN events to k_process_wave)
+        LongRuns LR{};
+        WaveRuns WR{};
+        if (hot_het && max_n <= 16 && process_impl == 0) {
+            const size_t lb = long_runs_bytes(n, hot_het_run, 4);
+            if (w_runs.ensure(lb + 4 * ((size_t)n / WAVE_HET_RUN + 2)) == 0) {
+                LR = long_runs_at(w_runs.as<uint32_t>(), n, hot_het_run, 4);
+                WR.n = w_runs.as<uint32_t>() + 3;
+                WR.g0 = reinterpret_cast<uint32_t *>(w_runs.as<char>() + lb);
+                (void)hipMemsetAsync(w_runs.p, 0, 16, s);
+            }
+        }
+        auto hot = [&](auto nmax) {
+            constexpr int NM = decltype(nmax)::value;
+            if (WR.n)
+                launch("process_wave", n, s, [&] {
+                    const unsigned gw = (unsigned)std::min<int64_t>(n / WAVE_HET_RUN / 4 + 1, 2048);
+                    k_process_wave<NM><<<gw, 256, 0, s>>>(T, W, src, V, WR);
+                });
+            if (LR.nrun) launch("part_long", n, s, [&] { launch_long<NM>(T, W.sval, LR, src, V, n, hot_het_run, s, nullptr, nullptr); });
+        };
         if (max_n <= PROC_G * PROC_SLOTS_PER_LANE && process_impl == 1)
             launch("process", n, s, [&] {
                 k_process_grp<<<std::min<unsigned>(grid_for(n * PROC_G), 8192), 256, 0, s>>>(T, W, src, V, n);
             });
-        else if (max_n <= 2 && process_impl == 0)
-            launch("process", n, s, [&] { k_process_reg<2><<<g, 256, 0, s>>>(T, W, src, V, n); });
-        else if (max_n <= 4 && process_impl == 0)
-            launch("process", n, s, [&] { k_process_reg<4><<<g, 256, 0, s>>>(T, W, src, V, n); });
-        else if (max_n <= 10 && process_impl == 0)
-            launch("process", n, s, [&] { k_process_reg<10><<<g, 256, 0, s>>>(T, W, src, V, n); });
-        else if (max_n <= 16 && process_impl == 0)
-            launch("process", n, s, [&] { k_process_reg<16><<<g, 256, 0, s>>>(T, W, src, V, n); });
+        else if (max_n <= 2 && process_impl == 0) {
+            launch("process", n, s, [&] { k_process_reg<2><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run); });
+            hot(std::integral_constant<int, 2>{});
+        } else if (max_n <= 4 && process_impl == 0) {
+            launch("process", n, s, [&] { k_process_reg<4><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run); });
+            hot(std::integral_constant<int, 4>{});
+        } else if (max_n <= 10 && process_impl == 0) {
+            launch("process", n, s, [&] { k_process_reg<10><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run); });
+            hot(std::integral_constant<int, 10>{});
+        } else if (max_n <= 16 && process_impl == 0) {
+            launch("process", n, s, [&] { k_process_reg<16><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run); });
+            hot(std::integral_constant<int, 16>{});
+        }
         else
             launch("process", n, s, [&] { k_process<<<g, 256, 0, s>>>(T, W, src, V, n); });
         if (limiter) launch("verdict", n, s, [&] { k_verdict<true, false><<<g, 256, 0, s>>>(T, W, V, n); });
@@ -1145,10 +1213,11 @@ int sentinel_engine::rebuild_limiters() {
 template <int NMAX>
 static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTable &FT, const uint32_t *rstart,
                                int lb, const EventSrc &src, const Verdicts &V, int64_t n, hipStream_t s,
-                               uint32_t *ctl, unsigned long long *stat, uint64_t *vstage, const uint32_t *qpos) {
+                               uint32_t *ctl, unsigned long long *stat) {
     // ctl: [0] long-run count, [1] oversized-half count, [2, 2 + 2 nparts) oversized halves, then long runs
-    uint32_t *nlong = ctl, *nbig = ctl + 1, *big = ctl + 2;
-    uint32_t *long_runs = big + 2 * (size_t)nparts;
+    // ctl: [0] runs, [1] oversized halves, [2] chunks, [3] -, [4, 4 + 2 nparts) oversized halves, then the runs
+    uint32_t *nbig = ctl + 1, *big = ctl + 4;
+    const LongRuns LR = long_runs_at(ctl, n, LONG_RUN, 4 + 2 * (size_t)nparts);
     const uint64_t *pval = e->w_sval.as<uint64_t>();
     uint64_t *gsval = e->w_vtmp.as<uint64_t>();
     // a batch whose mean range does not fit goes straight to the HBM-sorting kernel
@@ -1156,33 +1225,27 @@ static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTa
 #define SENTINEL_ALLBIG_PCT 90
 #endif
     const bool all_big = n > (int64_t)nparts * (int64_t)(PH_KEYS * SENTINEL_ALLBIG_PCT / 100);
-    if (all_big) vstage = nullptr;    // k_part_half does not run: every verdict is written directly
     if (!all_big) {
         e->launch("part_fused", n, s, [&] {
             const dim3 g(16u * (unsigned)((nparts + 7) / 8));
             if (part_coop(lb))      // <= 256 flows per half: cooperative verdict sweep
                 k_part_half<NMAX, true><<<g, PH_THREADS, 0, s>>>(FT, pval, gsval, rstart, lb, nparts,
-                                                                 (int32_t)e->rules.size(), src, V, long_runs,
-                                                                 nlong, big, nbig, stat, vstage);
+                                                                 (int32_t)e->rules.size(), src, V, LR,
+                                                                 big, nbig, stat);
             else
                 k_part_half<NMAX, false><<<g, PH_THREADS, 0, s>>>(FT, pval, gsval, rstart, lb, nparts,
-                                                                  (int32_t)e->rules.size(), src, V, long_runs,
-                                                                  nlong, big, nbig, stat, vstage);
+                                                                  (int32_t)e->rules.size(), src, V, LR,
+                                                                  big, nbig, stat);
         });
     }
     e->launch("part_big", n, s, [&] {
         k_part_big<NMAX><<<all_big ? 2u * (unsigned)nparts : (unsigned)std::min<int32_t>(2 * nparts, 256), PH_THREADS, 0, s>>>(
-            FT, pval, gsval, rstart, lb, nparts, src, V, long_runs, nlong, all_big ? nullptr : big, nbig,
+            FT, pval, gsval, rstart, lb, nparts, src, V, LR, all_big ? nullptr : big, nbig,
             stat);
     });
     e->launch("part_long", n, s, [&] {   // hot flows (runs > LONG_RUN events): a workgroup each
-        k_part_long<NMAX><<<256, PL_THREADS, 0, s>>>(FT, gsval, long_runs, nlong, src, V, stat, e->h_part_stat);
+        e->launch_long<NMAX>(FT, gsval, LR, src, V, n, LONG_RUN, s, stat, e->h_part_stat);
     });
-    if (vstage)
-        e->launch("part_unsplit", n, s, [&] {
-            const int64_t nch = (n + PU_CHUNK - 1) / PU_CHUNK;
-            k_part_unsplit<<<(unsigned)(8 * ((nch + 7) / 8)), PU_THREADS, 0, s>>>(n, qpos, vstage, V.out);
-        });
 }
 
 static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
@@ -1202,7 +1265,7 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
     uint32_t *gsum = e->w_pscan.as<uint32_t>();
     uint32_t *rstart = gsum + (size_t)ng * nparts;
     uint32_t *rtot = rstart + nparts + 1;
-    rc = e->w_runs.ensure((2 + 2 * (size_t)nparts + 3 * ((size_t)n / LONG_RUN + 2)) * 4);
+    rc = e->w_runs.ensure(long_runs_bytes(n, LONG_RUN, 4 + 2 * (size_t)nparts));
     if (rc) return rc;
     if (!e->d_part_stat.p) {
         rc = e->d_part_stat.ensure(8);
@@ -1226,27 +1289,18 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
         k_part_offsets<<<g2, PS_THREADS, 0, s>>>(hist, nb, nparts, gsum, rtot, rstart);
     });
     const EventSrc src{ev, nullptr, fl, false};
-    uint32_t *qpos = nullptr;
-    uint64_t *vstage = nullptr;
-    if (e->vstage_on) {
-        rc = e->w_qpos.ensure((size_t)n * 4);
-        rc |= e->w_vstage.ensure((size_t)n * 8);
-        if (rc) return rc;
-        qpos = e->w_qpos.as<uint32_t>();
-        vstage = e->w_vstage.as<uint64_t>();
-    }
     e->launch("part_scatter", n, s, [&] {
         k_part_scatter<<<dim3((unsigned)nb), dim3(PT_THREADS), 0, s>>>(e->flow_plain ? nullptr : fkey, src,
                                                                          e->w_sval.as<uint64_t>(), n, finvalid, lb,
-                                                                         pbits, hist, nb, nparts, F, qpos);
+                                                                         pbits, hist, nb, nparts, F);
     });
     const KeyTable FT = e->table(e->ft, NEV, 0);
     const Verdicts V{out, fkey, finvalid};
     const int mx = e->flow_max_n;
-    if (mx <= 2) launch_part_decide<2>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat, vstage, qpos);
-    else if (mx <= 4) launch_part_decide<4>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat, vstage, qpos);
-    else if (mx <= 10) launch_part_decide<10>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat, vstage, qpos);
-    else launch_part_decide<16>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat, vstage, qpos);
+    if (mx <= 2) launch_part_decide<2>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
+    else if (mx <= 4) launch_part_decide<4>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
+    else if (mx <= 10) launch_part_decide<10>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
+    else launch_part_decide<16>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
     HIP_OK(hipGetLastError());
     return 0;
 }
@@ -1302,7 +1356,7 @@ static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const u
     }
     if (F > 0) {
         KeyTable FT = e->table(e->ft, NEV, 0);
-        e->run_pipeline(FT, fkey, e->w_fhist.as<uint32_t>(), n, fbits, src, V, s, e->flow_max_n, false);
+        e->run_pipeline(FT, fkey, e->w_fhist.as<uint32_t>(), n, fbits, src, V, s, e->flow_max_n, false, true);
     }
     HIP_OK(hipGetLastError());
     return 0;
@@ -1536,12 +1590,12 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
     if (const char *c = getenv("SENTINEL_VERDICT_NT")) e->verdict_nt = std::string(c) == "1";
     if (const char *c = getenv("SENTINEL_SCAN")) e->use_lookback = std::string(c) != "3pass";
     if (const char *c = getenv("SENTINEL_DIAG_LINEAR")) e->diag_linear = std::string(c) == "1";
+    if (const char *c = getenv("SENTINEL_HOT_HET_RUN")) e->hot_het_run = (uint32_t)std::max(WAVE_HET_RUN, (uint32_t)atoi(c));
     if (const char *c = getenv("SENTINEL_FLOW_PATH")) {
         const std::string v(c);
         e->flow_path = v == "sorted" ? 1 : v == "partition" ? 2 : 0;
     }
     if (const char *c = getenv("SENTINEL_SEGMENTS")) e->fused_segments = std::string(c) != "split";
-    if (const char *c = getenv("SENTINEL_VSTAGE")) e->vstage_on = std::string(c) == "1";
     if (const char *c = getenv("SENTINEL_PARAM_CAPACITY")) {
         uint64_t v = strtoull(c, nullptr, 10);
         uint64_t p = 1024;
@@ -1572,13 +1626,13 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
                       &e->d_prule_rcp, &e->d_prule_Is, &e->d_prule_thr, &e->d_ptable, &e->d_slot_rule,
                       &e->d_hot_table, &e->d_hot_thr, &e->w_fkey, &e->w_lkey, &e->w_skey, &e->w_sval, &e->w_ktmp,
                       &e->w_vtmp, &e->w_fhist, &e->w_lhist, &e->w_parts, &e->w_segid, &e->w_bad, &e->w_hep,
-                      &e->w_hacq, &e->w_segstart, &e->w_segkey, &e->w_segep, &e->w_segacq, &e->w_het, &e->w_done,
+                      &e->w_hacq, &e->w_segstart, &e->w_segkey, &e->w_segep, &e->w_segacq, &e->w_het, &e->w_prio, &e->w_done,
                       &e->w_s0, &e->w_k, &e->w_counters, &e->io_ev, &e->io_fl, &e->io_out, &e->io_vals, &e->w_vslot,
                       &e->d_prule_kind, &e->d_cm, &e->d_lrule_valid, &e->d_lrule_tok, &e->d_lrule_burst,
                       &e->d_lrule_dur, &e->d_lrule_w, &e->d_lrule_rcp, &e->d_lrule_kind, &e->d_lhot_keys,
                       &e->d_lhot_tok, &e->d_ltable, &e->d_lstate, &e->d_now, &e->d_conc_thr, &e->d_seg1_w,
                       &e->d_seg1_rcp, &e->d_seg1_kind, &e->d_tok_keys, &e->d_tok_fid, &e->d_tok_fidx,
-                      &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->w_runs, &e->w_pscan, &e->w_qpos, &e->w_vstage, &e->d_lres_state,
+                      &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->w_runs, &e->w_pscan, &e->d_lres_state,
                       &e->d_lres_count, &e->d_lres_w, &e->d_lres_rcp, &e->d_lres_kind})
         b->release();
     for (int k = 0; k < 2; ++k) {
@@ -1591,6 +1645,7 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
     if (e->s_h2d) (void)hipStreamDestroy(e->s_h2d);
     if (e->s_d2h) (void)hipStreamDestroy(e->s_d2h);
     if (e->h_part_stat) (void)hipHostFree(e->h_part_stat);
+    if (e->h_long_chunks) (void)hipHostFree(e->h_long_chunks);
     e->d_part_stat.release();
     (void)hipStreamDestroy(e->stream);
     delete e;

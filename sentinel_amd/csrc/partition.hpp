@@ -57,7 +57,7 @@ __global__ __launch_bounds__(PP_THREADS) void k_part_prep(int64_t n, const Event
                                                             uint32_t *__restrict__ ctl_zero,
                                                             unsigned long long *__restrict__ stat_zero) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {        // the batch's work-list counters and skew statistic
-        if (ctl_zero) { ctl_zero[0] = 0; ctl_zero[1] = 0; }
+        if (ctl_zero) { ctl_zero[0] = 0; ctl_zero[1] = 0; ctl_zero[2] = 0; }
         if (stat_zero) *stat_zero = 0;
     }
     __shared__ uint32_t h[PART_BINS];
@@ -180,8 +180,7 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(const uint32_t *__r
                                                                uint64_t *__restrict__ vals_out, int64_t n,
                                                                uint32_t finvalid, int lb, int pbits,
                                                                const uint32_t *__restrict__ offsets, int64_t nblocks,
-                                                               int32_t nparts, int32_t nflows,
-                                                               uint32_t *__restrict__ qpos) {
+                                                               int32_t nparts, int32_t nflows) {
     __shared__ uint16_t cnt[PT_WAVES][PART_BINS];
     __shared__ uint32_t goff[PART_BINS];
     __shared__ uint32_t loff[PART_BINS];
@@ -264,18 +263,6 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(const uint32_t *__r
         pre += dtot[q];
     }
     __syncthreads();
-    if (qpos)   // each event's slot in the partitioned array (arrival order: coalesced)
-#pragma unroll
-        for (int j = 0; j < PT_ITEMS; ++j) {
-            const int64_t i = base + j * WAVE + lane;
-            if (i >= n) continue;
-            uint32_t qp = 0xFFFFFFFFu;
-            if (rank[j] != 0xFFFFFFFFu) {
-                const uint32_t d = key[j] >> lb;
-                qp = goff[d] + cnt[wave][d] + rank[j];
-            }
-            qpos[i] = qp;
-        }
 #pragma unroll
     for (int j = 0; j < PT_ITEMS; ++j) {
         if (rank[j] == 0xFFFFFFFFu) continue;
@@ -305,32 +292,6 @@ __device__ inline uint64_t run_verdict(double thr, double I_s, int64_t s0, int32
     const double x = small ? (double)((int32_t)s0 + (int32_t)k * a) : (double)wrap_add(s0, wrap_mul((int64_t)k, a));
     return pack_verdict(ST_OK, java_d2i((thr - div_interval(x, I_s)) - (double)a), 0);
 }
-
-// Where a run's verdicts go: straight to the arrival position (the sequence number in the value) or
-// -- staged -- to the event's slot in the partitioned array (the range start plus its range position,
-// `spos` in LDS), from where k_part_unsplit moves every verdict back to arrival order in one coalesced
-// pass.  Staging turns the 8-byte stores at random arrival positions (one partial HBM sector each)
-// into range-local stores that the L2 combines into whole lines.
-struct VDest {
-    uint64_t *out;
-    uint64_t *stage;          // null: direct
-    const uint16_t *spos;     // LDS: range position of each sorted slot (staging only)
-    uint32_t base;            // the range's start in the partitioned array
-    __device__ inline uint32_t pos(const uint64_t *vals, uint32_t i) const {
-        return stage ? base + (uint32_t)spos[i] : ((uint32_t)vals[i] & SEQ_MASK);
-    }
-    __device__ inline void put(const uint64_t *vals, uint32_t i, uint64_t v) const {
-        if (stage) stage[base + (uint32_t)spos[i]] = v;
-        else out[(uint32_t)vals[i] & SEQ_MASK] = v;
-    }
-    __device__ inline Verdicts verdicts(const Verdicts &V) const {
-        Verdicts W = V;
-        if (stage) W.out = stage;
-        return W;
-    }
-};
-
-constexpr uint64_t VSTAGE_SKIP = ~0ull;   // staged slot decided elsewhere (k_part_big / k_part_long)
 
 template <int NMAX>
 struct FlowWindow {
@@ -438,16 +399,15 @@ struct FlowWindow {
 
     // the sequential path over sorted positions [q, q2) of `vals`
     __device__ inline void sequential(const KeyTable &T, uint32_t key, int64_t E, const uint64_t *vals, uint32_t q,
-                                      uint32_t q2, const EventSrc &src, const Verdicts &V, const VDest &D) {
+                                      uint32_t q2, const EventSrc &src, const Verdicts &V) {
         flush();
-        const Verdicts W = D.verdicts(V);
         for (uint32_t i = q; i < q2; ++i) {
             const uint32_t seq = (uint32_t)vals[i] & SEQ_MASK;
             int64_t tt;
             int32_t aa;
             uint8_t fl;
             src.load(seq, tt, aa, fl);
-            seq_event(T, key, ks, E, aa, fl, D.pos(vals, i), W);
+            seq_event(T, key, ks, E, aa, fl, seq, V);
         }
 #pragma unroll
         for (int j = 0; j < NMAX; ++j)
@@ -488,6 +448,67 @@ struct FlowWindow {
         }
     }
 
+    // heterogeneous-acquire segment at E (not prioritized, nothing pending, no newer slot): roll the
+    // slot, return the window's PASS sum; het_book adds the segment's sums afterwards
+    __device__ inline int64_t het_begin(int64_t E, bool &fresh) {
+        const int slot = (int)(E % nsc);
+        fresh = false;
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j)
+            if (j == slot && ep[j] != E) { fresh = true; ep[j] = E; ps[j] = 0; }
+        int64_t s0 = 0;
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j)
+            if (ep[j] != EPOCH_ABSENT && ep[j] > E - nsc) s0 = wrap_add(s0, ps[j]);
+        return s0;
+    }
+
+    __device__ inline void het_book(int64_t E, bool fresh, const HetSums &h) {
+        const int slot = (int)(E % nsc);
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j)
+            if (j == slot) { ps[j] = wrap_add(ps[j], h.pass); dirty |= 1u << j; }
+        if (ks.seven) {
+            int64_t blk = 0, preq = 0, breq = 0;
+            if (!fresh) { blk = ks.rc(slot, 0); preq = ks.rc(slot, 1); breq = ks.rc(slot, 2); }
+            ks.book_rest_sums(slot, fresh, blk, preq, breq, h.block, h.npass, h.nblock);
+        }
+    }
+
+    // after deciding events at epoch E: nothing more can pass at E (not even an acquire of 1) -- the
+    // slot of E is rolled, no slot is newer, no occupy transfer is pending
+    __device__ inline bool dead_at(int64_t E) const {
+        if (occ_pending) return false;
+        const int slot = (int)(E % nsc);
+        bool rolled = false, newer = false;
+        int64_t sum = 0;
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j) {
+            if (ep[j] == EPOCH_ABSENT) continue;
+            newer |= ep[j] > E;
+            if (ep[j] > E - nsc) sum = wrap_add(sum, ps[j]);
+            if (j == slot) rolled = ep[j] == E;
+        }
+        return rolled && !newer && !admits(kind, thr, I_s, sum, 1);
+    }
+
+    // the whole heterogeneous segment [q, q2) by this lane (het_walk on the rolled window)
+    __device__ inline void hetero(int64_t E, const uint64_t *vals, uint32_t q, uint32_t q2, const EventSrc &src,
+                                  const Verdicts &V, int64_t T0) {
+        bool fresh;
+        const int64_t s0 = het_begin(E, fresh);
+        const HetSums h = het_walk<2>(          // (few registers: this runs inside the lane walkers)
+            kind, thr, I_s, s0, q2 - q, [&](uint32_t k) { return vals[q + k]; },
+            [&](uint64_t v) {
+                int32_t a;
+                bool pr;
+                (void)event(v, src, T0, a, pr);
+                return a;
+            },
+            [&](uint64_t v, uint64_t vd) { V.out[(uint32_t)v & SEQ_MASK] = vd; });
+        het_book(E, fresh, h);
+    }
+
     // `small`: every S0 + k*a of the segment fits in int32, so the int64 -> double conversion is one
     // v_cvt_f64_i32 (same value)
     __device__ inline uint64_t verdict(int64_t s0, int32_t a, uint32_t K, uint32_t k, bool small) const {
@@ -499,23 +520,25 @@ struct FlowWindow {
 // to the arrival positions.
 template <int NMAX>
 __device__ inline void part_run_w(FlowWindow<NMAX> &fw, const KeyTable &T, uint32_t key, const uint64_t *s_val,
-                                  uint32_t q0, uint32_t q1, const EventSrc &src, const Verdicts &V, int64_t T0,
-                                  const VDest &D) {
+                                  uint32_t q0, uint32_t q1, const EventSrc &src, const Verdicts &V, int64_t T0) {
     uint32_t q = q0;
     while (q < q1) {
         int32_t a;
         bool prio;
         const int64_t E = fw.event(s_val[q], src, T0, a, prio);
-        bool het = prio && fw.kind == KIND_CLUSTER;
+        bool pr = prio && fw.kind == KIND_CLUSTER, ah = false;
         uint32_t q2 = q + 1;
         for (; q2 < q1; ++q2) {                       // the segment: same epoch
             int32_t a2;
             bool p2;
             if (fw.event(s_val[q2], src, T0, a2, p2) != E) break;
-            het |= a2 != a || (p2 && fw.kind == KIND_CLUSTER);
+            ah |= a2 != a;
+            pr |= p2 && fw.kind == KIND_CLUSTER;
         }
-        if (fw.slow(E, het)) {
-            fw.sequential(T, key, E, s_val, q, q2, src, V, D);
+        if (fw.slow(E, pr)) {
+            fw.sequential(T, key, E, s_val, q, q2, src, V);
+        } else if (ah) {
+            fw.hetero(E, s_val, q, q2, src, V, T0);
         } else {
             int64_t s0;
             uint32_t K;
@@ -532,7 +555,7 @@ __device__ inline void part_run_w(FlowWindow<NMAX> &fw, const KeyTable &T, uint3
                 if (acc == 0x123456789ull) V.out[0] = acc;
             }
 #else
-            for (uint32_t k = 0; k < len; ++k) D.put(s_val, q + k, fw.verdict(s0, a, K, k, small));
+            for (uint32_t k = 0; k < len; ++k) V.out[(uint32_t)s_val[q + k] & SEQ_MASK] = fw.verdict(s0, a, K, k, small);
 #endif
 #endif
         }
@@ -552,7 +575,7 @@ __device__ inline void part_run_w(FlowWindow<NMAX> &fw, const KeyTable &T, uint3
 // (k_part_half's cooperative verdict sweep writes them with every lane of the workgroup).
 template <int NMAX, bool DEFER = false>
 __device__ inline bool part_run_single(FlowWindow<NMAX> &fw, const uint64_t *s_val, uint32_t q0, uint32_t q1,
-                                       const EventSrc &src, const VDest &D, int64_t T0, int64_t *d_s0 = nullptr,
+                                       const EventSrc &src, const Verdicts &V, int64_t T0, int64_t *d_s0 = nullptr,
                                        uint32_t *d_K = nullptr, int32_t *d_a = nullptr, bool *d_small = nullptr) {
     if (fw.ks.hs == 2) return false;
     fw.E0 = epoch_of(T0, fw.w, fw.rcp);
@@ -623,11 +646,12 @@ __device__ inline bool part_run_single(FlowWindow<NMAX> &fw, const uint64_t *s_v
 #if defined(SENTINEL_DIAG_NOVERDICT)     // cost diagnostic only (no output)
     uint64_t acc = 0;
     for (uint32_t k = 0; k < len; ++k) acc ^= fw.verdict(s0, a, K, k, small) ^ s_val[q0 + k];
-    if (acc == 0x123456789ull) D.out[0] = acc;
+    if (acc == 0x123456789ull) V.out[0] = acc;
 #elif defined(SENTINEL_DIAG_VLINEAR)     // cost diagnostic only (wrong output): flow-contiguous stores
-    for (uint32_t k = 0; k < len; ++k) D.out[(blockIdx.x * blockDim.x + threadIdx.x) * 8 + (k & 7)] = fw.verdict(s0, a, K, k, small);
+    for (uint32_t k = 0; k < len; ++k) V.out[(blockIdx.x * blockDim.x + threadIdx.x) * 8 + (k & 7)] = fw.verdict(s0, a, K, k, small);
 #else
-    for (uint32_t k = 0; k < len; ++k) D.put(s_val, q0 + k, fw.verdict(s0, a, K, k, small));
+    for (uint32_t k = 0; k < len; ++k)
+        V.out[(uint32_t)s_val[q0 + k] & SEQ_MASK] = fw.verdict(s0, a, K, k, small);
 #endif
     return true;
 }
@@ -641,10 +665,10 @@ constexpr uint32_t COOP_SKIP = 1u << 31, COOP_SMALL = 1u << 30;
 // the first / second segment relative to q0.
 template <int NMAX>
 __device__ inline void part_run_defer(FlowWindow<NMAX> &fw, const KeyTable &T, uint32_t key, const uint64_t *s_val,
-                                      uint32_t q0, uint32_t q1, const EventSrc &src, const Verdicts &V,
-                                      const VDest &D, int64_t T0,
+                                      uint32_t q0, uint32_t q1, const EventSrc &src, const Verdicts &V, int64_t T0,
                                       int64_t *s0o, uint32_t *reco, int32_t *ao, uint32_t &len1, uint32_t &len12,
-                                      const uint32_t *segb = nullptr, const uint32_t *hetb = nullptr) {
+                                      const uint32_t *segb = nullptr, const uint32_t *hetb = nullptr,
+                                      const uint32_t *prib = nullptr) {
     reco[0] = reco[1] = COOP_SKIP;
     len1 = len12 = 0;
     uint32_t q = q0;
@@ -653,30 +677,35 @@ __device__ inline void part_run_defer(FlowWindow<NMAX> &fw, const KeyTable &T, u
         int32_t a;
         bool prio;
         const int64_t E = fw.event(s_val[q], src, T0, a, prio);
-        bool het = prio && fw.kind == KIND_CLUSTER;
+        bool pr = prio && fw.kind == KIND_CLUSTER, ah = false;
         uint32_t q2 = q + 1;
         if (segb) {
-            // segment starts / heterogeneous positions marked by the whole workgroup (k_part_half)
+            // segment starts / acquire-differs / prioritized positions marked by the whole workgroup
+            // (k_part_half)
             uint32_t wi = q2 >> 5;
             uint32_t m = q2 < q1 ? segb[wi] & (~0u << (q2 & 31)) : 0u;
             while (!m && (wi + 1) * 32 < q1) m = segb[++wi];
             q2 = m ? min(q1, wi * 32 + (uint32_t)__ffs(m) - 1) : q1;
             for (uint32_t hw = q >> 5; hw <= (q2 - 1) >> 5; ++hw) {
-                uint32_t hm = hetb[hw];
-                if (hw == q >> 5) hm &= ~0u << (q & 31);
-                if (hw == (q2 - 1) >> 5 && ((q2 & 31) != 0)) hm &= (1u << (q2 & 31)) - 1u;
-                het |= hm != 0;
+                uint32_t msk = ~0u;
+                if (hw == q >> 5) msk &= ~0u << (q & 31);
+                if (hw == (q2 - 1) >> 5 && ((q2 & 31) != 0)) msk &= (1u << (q2 & 31)) - 1u;
+                ah |= (hetb[hw] & msk) != 0;
+                pr |= (prib[hw] & msk) != 0;
             }
         } else {
             for (; q2 < q1; ++q2) {
                 int32_t a2;
                 bool p2;
                 if (fw.event(s_val[q2], src, T0, a2, p2) != E) break;
-                het |= a2 != a || (p2 && fw.kind == KIND_CLUSTER);
+                ah |= a2 != a;
+                pr |= p2 && fw.kind == KIND_CLUSTER;
             }
         }
-        if (fw.slow(E, het)) {
-            fw.sequential(T, key, E, s_val, q, q2, src, V, D);
+        if (fw.slow(E, pr)) {
+            fw.sequential(T, key, E, s_val, q, q2, src, V);
+        } else if (ah) {
+            fw.hetero(E, s_val, q, q2, src, V, T0);
         } else {
             int64_t s0;
             uint32_t K;
@@ -688,7 +717,7 @@ __device__ inline void part_run_defer(FlowWindow<NMAX> &fw, const KeyTable &T, u
                 reco[si] = K | (small ? COOP_SMALL : 0u);
                 ao[si] = a;
             } else {
-                for (uint32_t k = 0; k < len; ++k) D.put(s_val, q + k, fw.verdict(s0, a, K, k, small));
+                for (uint32_t k = 0; k < len; ++k) V.out[(uint32_t)s_val[q + k] & SEQ_MASK] = fw.verdict(s0, a, K, k, small);
             }
         }
         if (si == 0) len1 = q2 - q0;
@@ -704,7 +733,7 @@ __device__ inline void part_run(const KeyTable &T, uint32_t key, const uint64_t 
                                 const EventSrc &src, const Verdicts &V, int64_t T0) {
     FlowWindow<NMAX> fw;
     fw.load(T, key, T0);
-    part_run_w<NMAX>(fw, T, key, s_val, q0, q1, src, V, T0, VDest{V.out, nullptr, nullptr, 0});
+    part_run_w<NMAX>(fw, T, key, s_val, q0, q1, src, V, T0);
 }
 
 // Runs longer than this are decided by a whole workgroup (k_part_long): one lane walking a hot
@@ -714,45 +743,292 @@ constexpr int PL_THREADS = 512;
 constexpr int PL_ITEMS = 8;
 constexpr int PL_CHUNK = PL_THREADS * PL_ITEMS;
 
-// One workgroup per long run (grid-stride over the deferred list): chunks of 4096 events; per
-// chunk every lane computes the epochs of its 8 contiguous events, segment heads come from a block
-// scan, lane 0 walks the chunk's segments with the window in its VGPRs (closed form or sequential),
-// then all lanes write the verdicts.  A chunk boundary only splits a segment in two consecutive
+// Block-wide exclusive scan of one int64 per thread (per-wave totals in lds_waves[THREADS / WAVE]).
+__device__ inline int64_t block_exclusive_scan64(int64_t v, int64_t *lds_waves, int64_t *total) {
+    const int lane = (int)lane_id();
+    const int wave = threadIdx.x / WAVE;
+    int64_t inc = v;
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) {
+        const int64_t u = __shfl_up(inc, off, WAVE);
+        if (lane >= off) inc += u;
+    }
+    if (lane == WAVE - 1) lds_waves[wave] = inc;
+    __syncthreads();
+    int64_t base = 0, tot = 0;
+    const int nw = blockDim.x / WAVE;
+    for (int w = 0; w < nw; ++w) {
+        const int64_t x = lds_waves[w];
+        if (w < wave) base += x;
+        tot += x;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + inc - v;
+}
+
+// LDS scratch of the cooperative heterogeneous walk
+struct HetLds {
+    int64_t waves[16];
+    uint32_t first[2];
+    int64_t acq, np;
+};
+
+// A heterogeneous-acquire segment decided by the whole workgroup (k_part_long): chunk positions
+// [st, en), thread t owning positions t*ITEMS + k with acquire a[k] (also staged in LDS, a_lds).  The
+// greedy walk of het_walk: one workgroup round first -- every event passes while admits(x + the sum
+// of the acquires before it): a block scan and a block min of the first failing position f settle
+// [st, f) -- then, if the window saturated, wave 0 alone walks [f, en) with wave_walk (from there on
+// passes are rare: at most the remaining capacity / min acquire of them, each a wave round, no
+// workgroup barriers).  Returns the segment's sums (all lanes).
+template <int ITEMS>
+__device__ inline HetSums coop_het(uint32_t st, uint32_t en, const int32_t (&a)[ITEMS], const int32_t *a_lds,
+                                   int64_t x, uint8_t kind, double thr, double I_s, const uint64_t *cval, uint64_t *out,
+                                   HetLds &L) {
+    const uint32_t t0 = threadIdx.x * ITEMS;
+    const int64_t x0 = x;
+    int64_t mine = 0;
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k)
+        if (t0 + k >= st && t0 + k < en) mine += a[k];
+    if (threadIdx.x == 0) L.first[0] = en;
+    int64_t total_acq;
+    const int64_t pre = block_exclusive_scan64(mine, L.waves, &total_acq);   // (its barriers order the init)
+    const bool live = admits(kind, thr, I_s, x, 1);
+    uint32_t myf = en;
+    int64_t pk = pre;
+    if (live) {
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            const uint32_t q = t0 + k;
+            if (q >= st && q < en) {
+                if (myf == en && !admits(kind, thr, I_s, wrap_add(x, pk), a[k])) myf = q;
+                pk += a[k];
+            }
+        }
+    } else {
+        myf = st;
+    }
+    if (myf < en) atomicMin(&L.first[0], myf);
+    __syncthreads();
+    const uint32_t f = L.first[0];
+    pk = pre;
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        const uint32_t q = t0 + k;
+        if (q >= st && q < f) {
+            out[(uint32_t)cval[q] & SEQ_MASK] = pack_verdict(ST_OK, java_d2i(remaining_of(thr, I_s, wrap_add(x, pk), a[k])), 0);
+            pk += a[k];
+        }
+        if (q == f && f < en) L.acq = pk;     // the passed sum before f (its prefix)
+    }
+    int64_t npass = (int64_t)(f - st);
+    __syncthreads();
+    if (f >= en) {
+        x = wrap_add(x, total_acq);
+    } else {
+        x = wrap_add(x, L.acq);
+        if (threadIdx.x < WAVE) {
+            int64_t np = 0, tot = 0;
+            wave_walk(kind, thr, I_s, en - f, x, np, tot, [&](uint32_t i, int32_t &ai, uint64_t *&dst) {
+                ai = a_lds[f + i];
+                dst = out + ((uint32_t)cval[f + i] & SEQ_MASK);
+            });
+            if (threadIdx.x == 0) { L.acq = x; L.np = np; }
+        }
+        __syncthreads();
+        x = L.acq;
+        npass += L.np;
+        __syncthreads();
+    }
+    HetSums h;
+    h.pass = wrap_add(x, -x0);
+    h.npass = npass;
+    h.block = wrap_add(total_acq, -h.pass);
+    h.nblock = (int64_t)(en - st) - npass;
+    return h;
+}
+
+// Hot runs, three kernels.  k_long_scan (every chunk of every run in parallel): the chunk's summary
+// {first epoch, acquire sum, events, one epoch and no prioritized request?}.  k_part_long (one
+// workgroup per run, chunks in order): a chunk that lies wholly in the epoch at which the window
+// went dead -- not even an acquire of 1 admitted, no occupy transfer pending, no newer slot -- is
+// only booked (BLOCK += its acquire sum, BLOCK_REQUEST += its events: a few scalar adds) and
+// flagged; every other chunk is decided in full (below).  k_long_dead (every chunk in parallel)
+// writes the flagged chunks' BLOCKED verdicts.  A saturated hot flow thus costs its live prefix plus
+// a streaming pass, not a serial walk over its events.
+static_assert(LR_CHUNK == (uint32_t)PL_CHUNK, "chunk records match the k_part_long chunk");
+constexpr int LS_THREADS = 256;
+constexpr int LS_ITEMS = LR_CHUNK / LS_THREADS;
+
+__device__ inline void long_chunk(const LongRuns &L, uint32_t g, uint32_t &q0c, uint32_t &cn, uint32_t &key) {
+    const uint32_t r = L.chunk_run[g];
+    const uint32_t q0 = L.runs[4 * (uint64_t)r], q1 = L.runs[4 * (uint64_t)r + 1];
+    key = L.runs[4 * (uint64_t)r + 2];
+    q0c = q0 + (g - L.runs[4 * (uint64_t)r + 3]) * LR_CHUNK;
+    cn = min(LR_CHUNK, q1 - q0c);
+}
+
+__global__ __launch_bounds__(LS_THREADS) void k_long_scan(KeyTable T, const uint64_t *__restrict__ sval, LongRuns L,
+                                                          EventSrc src) {
+    __shared__ int64_t w_min[LS_THREADS / WAVE], w_max[LS_THREADS / WAVE], w_sum[LS_THREADS / WAVE];
+    __shared__ uint32_t w_pr[LS_THREADS / WAVE];
+    const uint32_t total = *L.nchunk;
+    const int64_t T0 = src.t0();
+    for (uint32_t g = blockIdx.x; g < total; g += gridDim.x) {
+        uint32_t q0c, cn, key;
+        long_chunk(L, g, q0c, cn, key);
+        const int32_t w = T.w[key];
+        const double rcp = T.rcp_w[key];
+        const bool cluster = T.kind[key] == KIND_CLUSTER;
+        int64_t mn = INT64_MAX, mx = INT64_MIN, sum = 0;
+        uint32_t pr = 0;
+        uint64_t v[LS_ITEMS];
+#pragma unroll
+        for (int k = 0; k < LS_ITEMS; ++k) {
+            const uint32_t q = k * LS_THREADS + threadIdx.x;
+            v[k] = q < cn ? sval[q0c + q] : 0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < LS_ITEMS; ++k) {
+            const uint32_t q = k * LS_THREADS + threadIdx.x;
+            if (q >= cn) continue;
+            int64_t t;
+            int32_t a;
+            bool prio;
+            src.unpack(v[k], T0, t, a, prio);
+            const int64_t E = epoch_of(t, w, rcp);
+            mn = E < mn ? E : mn;
+            mx = E > mx ? E : mx;
+            sum += a;
+            pr |= (prio && cluster) ? 1u : 0u;
+        }
+#pragma unroll
+        for (int off = WAVE / 2; off > 0; off >>= 1) {
+            const int64_t a1 = __shfl_xor(mn, off, WAVE), a2 = __shfl_xor(mx, off, WAVE), a3 = __shfl_xor(sum, off, WAVE);
+            mn = a1 < mn ? a1 : mn;
+            mx = a2 > mx ? a2 : mx;
+            sum += a3;
+            pr |= __shfl_xor(pr, off, WAVE);
+        }
+        const int wave = threadIdx.x / WAVE;
+        if (lane_id() == 0) { w_min[wave] = mn; w_max[wave] = mx; w_sum[wave] = sum; w_pr[wave] = pr; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int i = 1; i < LS_THREADS / WAVE; ++i) {
+                mn = w_min[i] < mn ? w_min[i] : mn;
+                mx = w_max[i] > mx ? w_max[i] : mx;
+                sum += w_sum[i];
+                pr |= w_pr[i];
+            }
+            LongRec R;
+            R.E = mn;
+            R.acq = sum;
+            R.cnt = cn;
+            R.flags = (mn == mx && !pr) ? LR_UNIFORM : 0u;
+            R.pad = 0;
+            L.rec[g] = R;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(LS_THREADS) void k_long_dead(const uint64_t *__restrict__ sval, LongRuns L, Verdicts V) {
+    const uint32_t total = *L.nchunk;
+    for (uint32_t g = blockIdx.x; g < total; g += gridDim.x) {
+        if (!(L.rec[g].flags & LR_DEAD)) continue;
+        uint32_t q0c, cn, key;
+        long_chunk(L, g, q0c, cn, key);
+#pragma unroll
+        for (int k = 0; k < LS_ITEMS; ++k) {
+            const uint32_t q = k * LS_THREADS + threadIdx.x;
+            if (q < cn) V.out[(uint32_t)sval[q0c + q] & SEQ_MASK] = pack_verdict(ST_BLOCKED, 0, 0);
+        }
+    }
+}
+
+// k_part_long: one workgroup per run (grid-stride over the runs), its chunks in order.  A chunk
+// decided in full: every lane computes the epochs of its 8 contiguous events, segment heads come
+// from a block scan, lane 0 walks the chunk's segments with the window in its VGPRs (closed form or
+// sequential) up to a heterogeneous-acquire one, which the workgroup decides (coop_het), then all
+// lanes write the closed-form verdicts.  A chunk boundary only splits a segment in two consecutive
 // segments of the same epoch, which the window algebra treats identically.
+constexpr int PL_RECS = 256;     // chunk records staged in LDS at a time
 template <int NMAX>
-__global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint64_t *__restrict__ sval,
-                                                          const uint32_t *__restrict__ long_runs,
-                                                          const uint32_t *__restrict__ nlong, EventSrc src, Verdicts V,
+__global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint64_t *__restrict__ sval, LongRuns L,
+                                                          EventSrc src, Verdicts V,
                                                           const unsigned long long *__restrict__ stat,
                                                           unsigned long long *__restrict__ host_stat) {
     // the last kernel of a partition batch publishes the skew statistic to pinned host memory
     if (host_stat && blockIdx.x == 0 && threadIdx.x == 0)
         __hip_atomic_store(host_stat, *stat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (L.host_chunks && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(L.host_chunks, *L.nchunk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __shared__ uint16_t seg_start[PL_CHUNK + 1];
     __shared__ int64_t seg_E[PL_CHUNK];
     __shared__ int32_t seg_a[PL_CHUNK];
     __shared__ int64_t seg_s0[PL_CHUNK];
     __shared__ uint32_t seg_K[PL_CHUNK];
-    __shared__ uint32_t seg_flag[PL_CHUNK];      // bit0 heterogeneous, bit1 decided sequentially
+    __shared__ uint32_t seg_flag[PL_CHUNK];      // bit0 prioritized, bit1 verdicts written, bit2 acquire differs
     __shared__ int64_t l_E[PL_THREADS];
     __shared__ int32_t l_a[PL_THREADS];
     __shared__ uint32_t waves_tot[PL_THREADS / WAVE];
     __shared__ uint32_t s_nseg;
-    const uint32_t total = *nlong;
+    __shared__ HetLds hl;
+    __shared__ uint32_t s_het;
+    __shared__ int64_t s_hx;
+    __shared__ LongRec recs[PL_RECS];
+    __shared__ int32_t a_lds[PL_CHUNK];          // the chunk's acquire counts (coop_het's wave walk)
+    __shared__ uint32_t s_dead;                  // the window is dead at epoch s_deadE
+    __shared__ int64_t s_deadE;
+    const uint32_t total = *L.nrun;
     const int64_t T0 = src.t0();
     for (uint32_t r = blockIdx.x; r < total; r += gridDim.x) {
-        const uint32_t q0 = long_runs[3 * (uint64_t)r], q1 = long_runs[3 * (uint64_t)r + 1];
-        const uint32_t key = long_runs[3 * (uint64_t)r + 2];
+        const uint32_t q0 = L.runs[4 * (uint64_t)r], q1 = L.runs[4 * (uint64_t)r + 1];
+        const uint32_t key = L.runs[4 * (uint64_t)r + 2], cb = L.runs[4 * (uint64_t)r + 3];
+        const uint32_t nch = (q1 - q0 + PL_CHUNK - 1) / PL_CHUNK;
         FlowWindow<NMAX> fw;                      // meaningful in lane 0 only
-        if (threadIdx.x == 0) fw.load(T, key, T0);
+        if (threadIdx.x == 0) {
+            fw.load(T, key, T0);
+            s_dead = 0;
+        }
         const int32_t w = T.w[key];
         const double rcp = T.rcp_w[key];
-        const bool cluster = T.kind[key] == KIND_CLUSTER;
-        for (uint32_t c0 = q0; c0 < q1; c0 += PL_CHUNK) {
+        const uint8_t kind = T.kind[key];
+        const bool cluster = kind == KIND_CLUSTER;
+        const double thr = T.thr[key], I_s = T.I_s[key];
+        bool h_fresh = false;                     // lane 0: the cooperative segment's rolled slot was fresh
+        HetSums dsum{0, 0, 0, 0};                 // lane 0: dead chunks booked but not yet written back
+#ifdef SENTINEL_DIAG_LONG
+        uint32_t d_full = 0, d_dead = 0, d_deadflag = 0, d_unif = 0;
+#endif
+        for (uint32_t ci = 0; ci < nch; ++ci) {
+            if (L.rec && ci % PL_RECS == 0) {
+                __syncthreads();
+                for (uint32_t j = threadIdx.x; j < PL_RECS && ci + j < nch; j += PL_THREADS) recs[j] = L.rec[cb + ci + j];
+                __syncthreads();
+            }
+            const LongRec &R = recs[ci % PL_RECS];
+            if (L.rec && s_dead && (R.flags & LR_UNIFORM) && R.E == s_deadE) {     // uniform: LDS values only
+                if (threadIdx.x == 0) {
+#ifdef SENTINEL_DIAG_LONG
+                    ++d_dead;
+#endif
+                    dsum.block = wrap_add(dsum.block, R.acq);
+                    dsum.nblock += R.cnt;
+                    L.rec[cb + ci].flags = R.flags | LR_DEAD;
+                }
+                continue;
+            }
+            if (threadIdx.x == 0 && dsum.nblock) {
+                fw.het_book(s_deadE, false, dsum);
+                dsum = HetSums{0, 0, 0, 0};
+            }
+            const uint32_t c0 = q0 + ci * PL_CHUNK;
             const uint32_t cn = min((uint32_t)PL_CHUNK, q1 - c0);
             int64_t E[PL_ITEMS];
             int32_t a[PL_ITEMS];
-            uint32_t heads = 0, bad = 0;
+            uint32_t heads = 0, bad = 0, ahet = 0;
 #pragma unroll
             for (int k = 0; k < PL_ITEMS; ++k) {
                 const uint32_t qq = threadIdx.x * PL_ITEMS + k;
@@ -768,6 +1044,8 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
             }
             l_E[threadIdx.x] = E[PL_ITEMS - 1];
             l_a[threadIdx.x] = a[PL_ITEMS - 1];
+#pragma unroll
+            for (int k = 0; k < PL_ITEMS; ++k) a_lds[threadIdx.x * PL_ITEMS + k] = a[k];
             for (uint32_t g = threadIdx.x; g < PL_CHUNK; g += PL_THREADS) seg_flag[g] = 0;
             __syncthreads();
             int64_t pe = threadIdx.x ? l_E[threadIdx.x - 1] : 0;
@@ -777,7 +1055,7 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
                 const uint32_t qq = threadIdx.x * PL_ITEMS + k;
                 if (qq < cn) {
                     if (qq == 0 || E[k] != pe) heads |= 1u << k;
-                    else if (a[k] != pa) bad |= 1u << k;
+                    else if (a[k] != pa) ahet |= 1u << k;
                 }
                 pe = E[k];
                 pa = a[k];
@@ -800,27 +1078,56 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
             __syncthreads();
 #pragma unroll
             for (int k = 0; k < PL_ITEMS; ++k)
-                if ((bad & (1u << k)) && threadIdx.x * PL_ITEMS + k < cn) atomicOr(&seg_flag[gid[k]], 1u);
+                if (threadIdx.x * PL_ITEMS + k < cn && ((bad | ahet) & (1u << k)))
+                    atomicOr(&seg_flag[gid[k]], ((bad >> k) & 1u) | (((ahet >> k) & 1u) << 2));
             __syncthreads();
-            if (threadIdx.x == 0) {
-                const uint32_t ns = s_nseg;
-                for (uint32_t sgi = 0; sgi < ns; ++sgi) {
-                    const uint32_t st = seg_start[sgi];
-                    const uint32_t en = sgi + 1 < ns ? seg_start[sgi + 1] : cn;
-                    const int64_t Es = seg_E[sgi];
-                    if (fw.slow(Es, seg_flag[sgi] & 1u)) {
-                        fw.sequential(T, key, Es, sval, c0 + st, c0 + en, src, V, VDest{V.out, nullptr, nullptr, 0});
-                        seg_flag[sgi] |= 2u;
-                    } else {
-                        int64_t s0;
-                        uint32_t K;
-                        fw.fast(Es, seg_a[sgi], en - st, s0, K);
-                        seg_s0[sgi] = s0;
-                        seg_K[sgi] = K;
+            // lane 0 walks the segments (closed form / sequential) up to the next heterogeneous-acquire
+            // one, which the whole workgroup decides (coop_het); then lane 0 goes on
+            const uint32_t ns = s_nseg;
+            uint32_t from = 0;
+            for (;;) {
+                if (threadIdx.x == 0) {
+                    uint32_t sgi = from;
+                    for (; sgi < ns; ++sgi) {
+                        const uint32_t st = seg_start[sgi];
+                        const uint32_t en = sgi + 1 < ns ? seg_start[sgi + 1] : cn;
+                        const int64_t Es = seg_E[sgi];
+                        if (fw.slow(Es, seg_flag[sgi] & 1u)) {
+                            fw.sequential(T, key, Es, sval, c0 + st, c0 + en, src, V);
+                            seg_flag[sgi] |= 2u;
+                        } else if (seg_flag[sgi] & 4u) {
+                            s_hx = fw.het_begin(Es, h_fresh);
+                            seg_flag[sgi] |= 2u;
+                            break;
+                        } else {
+                            int64_t s0;
+                            uint32_t K;
+                            fw.fast(Es, seg_a[sgi], en - st, s0, K);
+                            seg_s0[sgi] = s0;
+                            seg_K[sgi] = K;
+                        }
+                    }
+                    s_het = sgi;
+                    if (sgi >= ns) {               // the chunk is decided: is the window dead now?
+                        const int64_t El = seg_E[ns - 1];
+                        s_dead = fw.dead_at(El) ? 1u : 0u;
+                        s_deadE = El;
+#ifdef SENTINEL_DIAG_LONG
+                        ++d_full;
+                        d_deadflag += s_dead;
+                        d_unif += (L.rec && (R.flags & LR_UNIFORM)) ? 1u : 0u;
+#endif
                     }
                 }
+                __syncthreads();
+                const uint32_t hs = s_het;
+                if (hs >= ns) break;
+                const uint32_t st = seg_start[hs];
+                const uint32_t en = hs + 1 < ns ? seg_start[hs + 1] : cn;
+                const HetSums sums = coop_het<PL_ITEMS>(st, en, a, a_lds, s_hx, kind, thr, I_s, sval + c0, V.out, hl);
+                if (threadIdx.x == 0) fw.het_book(seg_E[hs], h_fresh, sums);
+                from = hs + 1;
             }
-            __syncthreads();
 #pragma unroll
             for (int k = 0; k < PL_ITEMS; ++k) {
                 const uint32_t qq = threadIdx.x * PL_ITEMS + k;
@@ -830,7 +1137,7 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
                 const uint32_t seq = (uint32_t)sval[c0 + qq] & SEQ_MASK;
                 uint64_t v;
                 if (qq - seg_start[sg] < seg_K[sg])
-                    v = pack_verdict(ST_OK, java_d2i(remaining_of(T.thr[key], T.I_s[key],
+                    v = pack_verdict(ST_OK, java_d2i(remaining_of(thr, I_s,
                                                                   wrap_add(seg_s0[sg], wrap_mul((int64_t)(qq - seg_start[sg]), seg_a[sg])),
                                                                   seg_a[sg])), 0);
                 else
@@ -839,7 +1146,15 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
             }
             __syncthreads();
         }
-        if (threadIdx.x == 0) fw.flush();
+        if (threadIdx.x == 0) {
+            if (dsum.nblock) fw.het_book(s_deadE, false, dsum);
+            fw.flush();
+#ifdef SENTINEL_DIAG_LONG
+            if (nch >= 8)
+                printf("long run key %u chunks %u full %u dead %u deadflag %u uniform %u recs %d thr %f kind %d occ %d\n", key,
+                       nch, d_full, d_dead, d_deadflag, d_unif, L.rec != nullptr, thr, (int)kind, (int)fw.occ_pending);
+#endif
+        }
         __syncthreads();
     }
 }
@@ -919,10 +1234,9 @@ template <int NMAX, bool COOP>
 __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     KeyTable T, const uint64_t *__restrict__ pval, uint64_t *__restrict__ gsval,
     const uint32_t *__restrict__ rstart, int lb, int32_t nranges, int32_t nflows, EventSrc src, Verdicts V,
-    uint32_t *__restrict__ long_runs, uint32_t *__restrict__ nlong, uint32_t *__restrict__ big,
-    uint32_t *__restrict__ nbig, unsigned long long *__restrict__ max_range, uint64_t *__restrict__ vstage) {
+    LongRuns LR, uint32_t *__restrict__ big,
+    uint32_t *__restrict__ nbig, unsigned long long *__restrict__ max_range) {
     __shared__ uint64_t sv[PH_CAP];
-    __shared__ uint16_t spos[PH_CAP];      // range position of each sorted slot (arrival order inside the range)
     // the ballot ranking's per-wave counters and (after the sort) the cooperative verdict records,
     // one per flow of the half, share one LDS buffer
     constexpr int CF = COOP ? PH_COOP_FLOWS : 1;
@@ -944,7 +1258,6 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     // parallel segment marking for halves of <= 128 flows: per-flow epoch parameters, then one bit per
     // sorted event for "segment start" and "heterogeneous" (acquire differs from its predecessor's or
     // a prioritized cluster request)
-    // flows of the halves the bits path serves: hb <= min(PH_COOP_HB, PH_COOP_SINGLE_HB - 1)
     constexpr int CB = COOP ? (1 << (PH_COOP_HB < PH_COOP_SINGLE_HB - 1 ? PH_COOP_HB : PH_COOP_SINGLE_HB - 1)) : 1;
     static_assert(!COOP || CB <= PH_COOP_FLOWS, "bits-path records fit the coop flow count");
     constexpr int MW = COOP ? (int)(PH_CAP + 31) / 32 : 1;
@@ -953,7 +1266,7 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     __shared__ int32_t p_r0[CB], p_w[CB];
     __shared__ float p_rcpf[CB];
     __shared__ uint32_t p_start[CB], p_cl[CB];
-    __shared__ uint32_t segb[MW], hetb[MW];
+    __shared__ uint32_t segb[MW], hetb[MW], prib[MW];
 #endif
     uint32_t p, h;
     half_of_block(blockIdx.x, p, h);
@@ -966,18 +1279,9 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     const uint32_t pstart = rstart[p];
     const uint32_t pend = rstart[p + 1];
     const uint32_t size = pend - pstart;
-    const uint32_t hmask = (1u << hb) - 1u;
-    // local flow of a value, or 0xFFFFFFFF: not this half's (recomputed where used: no registers)
-    auto local = [&](uint64_t v) -> uint32_t {
-        const uint32_t k = (uint32_t)(v >> VAL_KEY_SHIFT);
-        return (v != ~0ull && (k >> hb) == h) ? (k & hmask) : 0xFFFFFFFFu;
-    };
     if (t == 0 && h == 0 && max_range) atomicMax(max_range, (unsigned long long)size);   // skew statistic
     if (size > PH_KEYS) {                                 // block-uniform
         if (t == 0) big[atomicAdd(nbig, 1u)] = (p << 1) | h;
-        if (vstage)                                       // k_part_big writes these verdicts itself
-            for (uint32_t q = t; q < size; q += PH_THREADS)
-                if (local(pval[pstart + q]) != 0xFFFFFFFFu) vstage[pstart + q] = VSTAGE_SKIP;
         return;
     }
     PF_STAMP(0);
@@ -985,7 +1289,13 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     // range position j * PH_THREADS + t: the workgroup sweeps the range in arrival order, so the
     // slots handed out below come out nearly in arrival order and the per-run sort has little to do.
     const uint32_t b0 = (uint32_t)wave * (PH_ITEMS * WAVE);
+    const uint32_t hmask = (1u << hb) - 1u;
     uint64_t val[PH_ITEMS];                               // every value load in flight at once
+    // local flow of a value, or 0xFFFFFFFF: not this half's (recomputed where used: no registers)
+    auto local = [&](uint64_t v) -> uint32_t {
+        const uint32_t k = (uint32_t)(v >> VAL_KEY_SHIFT);
+        return (v != ~0ull && (k >> hb) == h) ? (k & hmask) : 0xFFFFFFFFu;
+    };
 #pragma unroll
     for (int j = 0; j < PH_ITEMS; ++j) {
         const uint32_t q = j * PH_THREADS + t;
@@ -1010,12 +1320,6 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     const uint32_t start = block_exclusive_scan(c, waves_tot, &total);
     if (total > PH_CAP) {                                 // block-uniform: the half does not fit in LDS
         if (t == 0) big[atomicAdd(nbig, 1u)] = (p << 1) | h;
-        if (vstage)
-#pragma unroll
-            for (int j = 0; j < PH_ITEMS; ++j) {
-                const uint32_t q = j * PH_THREADS + t;
-                if (q < size && local(val[j]) != 0xFFFFFFFFu) vstage[pstart + q] = VSTAGE_SKIP;
-            }
         return;
     }
     if (c) atomicMax(&s_cmax, c);
@@ -1029,26 +1333,19 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
 #pragma unroll
         for (int j = 0; j < PH_ITEMS; ++j) {
             const uint32_t kj = local(val[j]);
-            if (kj != 0xFFFFFFFFu) {
-                const uint32_t slot = atomicAdd(&base[kj], 1u);
-                sv[slot] = val[j];
-                spos[slot] = (uint16_t)(j * PH_THREADS + t);
-            }
+            if (kj != 0xFFFFFFFFu) sv[atomicAdd(&base[kj], 1u)] = val[j];
         }
         __syncthreads();
-        // range position order = arrival order inside the range (the multi-split is stable)
         for (uint32_t i = start + 1; i < start + c; ++i) {
             const uint64_t v = sv[i];
-            const uint16_t sq = spos[i];
+            const uint32_t sq = (uint32_t)v & SEQ_MASK;
             uint32_t j = i;
             for (; j > start; --j) {
-                const uint16_t u = spos[j - 1];
-                if (u < sq) break;
-                sv[j] = sv[j - 1];
-                spos[j] = u;
+                const uint64_t u = sv[j - 1];
+                if (((uint32_t)u & SEQ_MASK) < sq) break;
+                sv[j] = u;
             }
             sv[j] = v;
-            spos[j] = sq;
         }
     } else {
         // a long run somewhere: stable ranking with ballots (arrival order kept by construction),
@@ -1090,9 +1387,7 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
         for (int j = 0; j < PH_ITEMS; ++j) {
             const uint32_t kj = local(val[j]);
             if (kj == 0xFFFFFFFFu) continue;
-            const uint32_t slot = base[kj] + cnt[wave][kj] + rank[j];
-            sv[slot] = val[j];
-            spos[slot] = (uint16_t)(b0 + j * WAVE + lane);
+            sv[base[kj] + cnt[wave][kj] + rank[j]] = val[j];
         }
     }
     __syncthreads();
@@ -1101,26 +1396,19 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     // (half 0 at the range start, half 1 at its end).
     const uint32_t goff = pstart + (h ? size - total : 0u);
     if (c > LONG_RUN) {
-        const uint32_t j = atomicAdd(nlong, 1u);
-        long_runs[3 * (uint64_t)j] = goff + start;
-        long_runs[3 * (uint64_t)j + 1] = goff + start + c;
-        long_runs[3 * (uint64_t)j + 2] = key;
+        LR.push(goff + start, goff + start + c, key);
         const uint32_t l = atomicAdd(&s_nlong, 1u);
         s_long[l][0] = start;
         s_long[l][1] = c;
     }
     __syncthreads();
     for (uint32_t l = 0; l < s_nlong; ++l)
-        for (uint32_t q = t; q < s_long[l][1]; q += PH_THREADS) {
-            gsval[goff + s_long[l][0] + q] = sv[s_long[l][0] + q];
-            if (vstage) vstage[pstart + spos[s_long[l][0] + q]] = VSTAGE_SKIP;   // k_part_long writes these
-        }
-    const VDest D{V.out, vstage, spos, pstart};
+        for (uint32_t q = t; q < s_long[l][1]; q += PH_THREADS) gsval[goff + s_long[l][0] + q] = sv[s_long[l][0] + q];
     if (COOP) {                                           // launched only when 2^hb <= PH_COOP_FLOWS
 #ifndef SENTINEL_NO_COOP_BITS
         const bool bits = hb < PH_COOP_SINGLE_HB;         // block-uniform
         if (bits) {
-            for (uint32_t j = t; j < (uint32_t)MW; j += PH_THREADS) { segb[j] = 0; hetb[j] = 0; }
+            for (uint32_t j = t; j < (uint32_t)MW; j += PH_THREADS) { segb[j] = 0; hetb[j] = 0; prib[j] = 0; }
             if (t < (1u << hb) && c > 0) {
                 p_E0[t] = epoch_of(T0, fw.w, fw.rcp);
                 p_r0[t] = (int32_t)(T0 - p_E0[t] * (int64_t)fw.w);
@@ -1144,22 +1432,23 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
                 bool pi;
                 const int64_t Ei = lw.event(v, src, T0, ai, pi);
                 bool st = i == p_start[kj];
-                bool het = pi && p_cl[kj];
+                bool het = false;
                 if (!st) {
                     int32_t ap;
                     bool pp;
                     const int64_t Ep = lw.event(sv[i - 1], src, T0, ap, pp);
                     st = Ep != Ei;
-                    if (!st) het |= ai != ap;
+                    if (!st) het = ai != ap;
                 }
                 if (st) atomicOr(&segb[i >> 5], 1u << (i & 31));
                 if (het) atomicOr(&hetb[i >> 5], 1u << (i & 31));
+                if (pi && p_cl[kj]) atomicOr(&prib[i >> 5], 1u << (i & 31));
             }
             __syncthreads();
         }
 #else
         const bool bits = false;
-        const uint32_t *segb = nullptr, *hetb = nullptr;
+        const uint32_t *segb = nullptr, *hetb = nullptr, *prib = nullptr;
 #endif
         if (t < (1u << hb)) {
             int64_t s0[2] = {0, 0};
@@ -1172,13 +1461,13 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
                 // (hb <= 7) a run straddles an epoch boundary often and the walk alone is cheaper
                 // (measured: 125k flows +4%, 250k +1%; 500k flows -1% without it)
                 if (hb >= PH_COOP_SINGLE_HB &&
-                    part_run_single<NMAX, true>(fw, sv, start, start + c, src, D, T0, &s0[0], &rec[0], &a[0], &small)) {
+                    part_run_single<NMAX, true>(fw, sv, start, start + c, src, V, T0, &s0[0], &rec[0], &a[0], &small)) {
                     rec[0] |= small ? COOP_SMALL : 0u;
                     len1 = len12 = c;
                 } else {
                     fw.load_header(T0);
-                    part_run_defer<NMAX>(fw, T, key, sv, start, start + c, src, V, D, T0, s0, rec, a, len1, len12,
-                                         bits ? segb : nullptr, bits ? hetb : nullptr);
+                    part_run_defer<NMAX>(fw, T, key, sv, start, start + c, src, V, T0, s0, rec, a, len1, len12,
+                                         bits ? segb : nullptr, bits ? hetb : nullptr, bits ? prib : nullptr);
                 }
                 c_thr[t] = fw.thr;
                 c_is[t] = fw.I_s;
@@ -1203,12 +1492,13 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
             const uint32_t sg = k < l1 ? 0u : 1u;
             const uint32_t rec = c_K[sg * CF + kj];
             if (rec & COOP_SKIP) continue;                        // sequential segment: written by the walk
-            D.put(sv, i, run_verdict(c_thr[kj], c_is[kj], c_s0[sg * CF + kj], c_a[sg * CF + kj],
-                                     rec & (COOP_SMALL - 1u), sg ? k - l1 : k, (rec & COOP_SMALL) != 0));
+            V.out[(uint32_t)v & SEQ_MASK] = run_verdict(c_thr[kj], c_is[kj], c_s0[sg * CF + kj], c_a[sg * CF + kj],
+                                                        rec & (COOP_SMALL - 1u), sg ? k - l1 : k,
+                                                        (rec & COOP_SMALL) != 0);
         }
-    } else if (c > 0 && c <= LONG_RUN && !part_run_single<NMAX>(fw, sv, start, start + c, src, D, T0)) {
+    } else if (c > 0 && c <= LONG_RUN && !part_run_single<NMAX>(fw, sv, start, start + c, src, V, T0)) {
         fw.load_header(T0);
-        part_run_w<NMAX>(fw, T, key, sv, start, start + c, src, V, T0, D);
+        part_run_w<NMAX>(fw, T, key, sv, start, start + c, src, V, T0);
     }
 #ifdef SENTINEL_DIAG_PHASES
     __syncthreads();
@@ -1225,7 +1515,7 @@ template <int NMAX>
 __global__ __launch_bounds__(PH_THREADS) void k_part_big(
     KeyTable T, const uint64_t *__restrict__ pval, uint64_t *__restrict__ gsval,
     const uint32_t *__restrict__ rstart, int lb, int32_t nranges, EventSrc src, Verdicts V,
-    uint32_t *__restrict__ long_runs, uint32_t *__restrict__ nlong, const uint32_t *__restrict__ big,
+    LongRuns LR, const uint32_t *__restrict__ big,
     const uint32_t *__restrict__ nbig, unsigned long long *__restrict__ max_range) {
     __shared__ uint16_t cnt[PH_WAVES][PH_BINS];
     __shared__ uint32_t base[PH_BINS];
@@ -1305,47 +1595,9 @@ __global__ __launch_bounds__(PH_THREADS) void k_part_big(
             base[t] += run;
         }
         const uint32_t key = (p << lb) | (h << hb) | t;
-        if (c > LONG_RUN) {
-            const uint32_t j = atomicAdd(nlong, 1u);
-            long_runs[3 * (uint64_t)j] = goff + start;
-            long_runs[3 * (uint64_t)j + 1] = goff + start + c;
-            long_runs[3 * (uint64_t)j + 2] = key;
-        }
+        if (c > LONG_RUN) LR.push(goff + start, goff + start + c, key);
         if (c > 0 && c <= LONG_RUN) part_run<NMAX>(T, key, dst, start, start + c, src, V, T0);
         __syncthreads();                                  // LDS reuse by the next entry
-    }
-}
-
-// Staged verdicts back to arrival order: out[i] = stage[qpos[i]] (qpos written by k_part_scatter, 0xFFFFFFFF
-// for events decided by the prep kernel; VSTAGE_SKIP marks verdicts k_part_big / k_part_long wrote
-// themselves).  Chunks of consecutive arrival positions are assigned XCD by XCD (block b runs on XCD
-// b mod 8), so the ~64 workgroups an XCD runs at once cover a contiguous stretch of the batch and the
-// staged lines they gather (a few consecutive slots per range) are fetched from HBM once, then hit in
-// that XCD's L2.
-constexpr int PU_THREADS = 256;
-constexpr int PU_ITEMS = 8;
-constexpr int PU_CHUNK = PU_THREADS * PU_ITEMS;
-__global__ __launch_bounds__(PU_THREADS) void k_part_unsplit(int64_t n, const uint32_t *__restrict__ qpos,
-                                                             const uint64_t *__restrict__ stage,
-                                                             uint64_t *__restrict__ out) {
-    const int64_t nchunks = (n + PU_CHUNK - 1) / PU_CHUNK;
-    const int64_t per_xcd = (nchunks + 7) / 8;
-    const int64_t c = (int64_t)(blockIdx.x & 7u) * per_xcd + (int64_t)(blockIdx.x >> 3);
-    if (c >= nchunks) return;
-    const int64_t i0 = c * PU_CHUNK;
-    uint32_t q[PU_ITEMS];
-#pragma unroll
-    for (int j = 0; j < PU_ITEMS; ++j) {
-        const int64_t i = i0 + j * PU_THREADS + threadIdx.x;
-        q[j] = i < n ? qpos[i] : 0xFFFFFFFFu;
-    }
-    uint64_t v[PU_ITEMS];
-#pragma unroll
-    for (int j = 0; j < PU_ITEMS; ++j) v[j] = q[j] != 0xFFFFFFFFu ? stage[q[j]] : VSTAGE_SKIP;
-#pragma unroll
-    for (int j = 0; j < PU_ITEMS; ++j) {
-        const int64_t i = i0 + j * PU_THREADS + threadIdx.x;
-        if (v[j] != VSTAGE_SKIP) out[i] = v[j];
     }
 }
 

@@ -82,6 +82,34 @@ def test_heterogeneous_rls_config5(oracle_mod):
     _compare(_engine(rules), _oracle(oracle_mod, rules), rules, ev, batches=2)
 
 
+def test_config5_hot_heterogeneous(oracle_mod):
+    """BASELINE config 5's shape: 2000 RLS rules, Zipf(1.1) -- the hottest flow takes ~17% of a batch,
+    with geometric hitsAddend.  Its heterogeneous segments (hundreds of thousands of events, both below
+    and past the threshold) are decided by a whole workgroup (coop_het) on both flow paths."""
+    rules, ev = T.config5(2_000_000, seed=55, n_flows=2000)
+    _compare(_engine(rules), _oracle(oracle_mod, rules), rules, ev, batches=4)
+
+
+def test_hot_heterogeneous_mixed(oracle_mod):
+    """A hot flow whose heterogeneous segments are interleaved with prioritized requests, a clock that
+    steps back and small thresholds (saturated after a few events) next to huge ones (never
+    saturated): the cooperative walk hands over to the sequential path and back."""
+    rng = np.random.default_rng(57)
+    rules = T.make_rules(64, rng, count_lo=3, count_hi=50, sample_count=2, window_interval_ms=500)
+    rules.count[5] = 1e6
+    n = 400_000
+    idx = rng.integers(0, 64, size=n).astype(np.int32)
+    hot = rng.random(n)
+    idx[hot < 0.45] = 3
+    idx[(hot >= 0.45) & (hot < 0.75)] = 5
+    acq = np.minimum(rng.geometric(0.4, size=n), 40).astype(np.int32)
+    ts = T.timestamps(n, 200_000.0, T.T0_ALIGNED + 3)
+    ts = ts + np.where(rng.random(n) < 0.0005, -rng.integers(0, 900, size=n), 0)
+    flags = (rng.random(n) < 0.0003).astype(np.uint8)
+    ev = T.Events(idx, acq, ts.astype(np.int64), flags)
+    _compare(_engine(rules, occ=0.9), _oracle(oracle_mod, rules, occ=0.9), rules, ev, batches=2)
+
+
 def test_homogeneous_acquire_gt1(oracle_mod):
     rng = np.random.default_rng(7)
     rules = T.make_rules(200, rng, count_lo=5, count_hi=300)
