@@ -839,18 +839,21 @@ struct WaveRuns {
 template <int NMAX>
 __global__ __launch_bounds__(256) void k_process_reg(KeyTable T, BatchWork W, EventSrc src, Verdicts V, int64_t n,
                                                      LongRuns L = LongRuns{}, WaveRuns WR = WaveRuns{},
-                                                     uint32_t hot_run = HOT_HET_RUN) {
+                                                     uint32_t hot_run = HOT_HET_RUN, uint32_t *het_hint = nullptr) {
     const int64_t g0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t S = (int64_t)*W.nseg;
     if (g0 >= S || (int64_t)*W.nvalid == 0) return;
     const uint32_t key = W.seg_key[g0];
     if (g0 > 0 && W.seg_key[g0 - 1] == key) return;    // not the first segment of its key
-    if (L.nrun) {
+    if (L.nrun || het_hint) {
         int64_t ge = g0;
         bool het = false;
         for (; ge < S && W.seg_key[ge] == key; ++ge) het |= W.seg_het[ge] && !W.seg_prio[ge];
         const uint32_t q0 = W.seg_start[g0], q1 = W.seg_start[ge];
-        if (het && q1 - q0 > hot_run) {
+        if (!L.nrun) {           // deferral off this batch: ask for it (pinned host word) if it would pay
+            if (het && q1 - q0 > WAVE_HET_RUN)
+                __hip_atomic_store(het_hint, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else if (het && q1 - q0 > hot_run) {
             L.push(q0, q1, key);
             for (int64_t g = g0; g < ge; ++g) W.seg_done[g] = 1;
             return;
@@ -976,36 +979,36 @@ __global__ __launch_bounds__(256) void k_process_reg(KeyTable T, BatchWork W, Ev
 }
 
 // Wave-wide greedy walk (k_process_wave, and coop_het past its first failure): events i in [0, len),
-// fetched by fetch(i, a, dst) 64 at a time, one per lane, decided as het_walk would, in rounds that
-// each settle at least one event (wave scans and ballots, no barriers):
+// 64 at a time, one per lane (load(i) -> the raw value, issued one window ahead; decode(i, raw, a,
+// dst)), decided as het_walk would, in rounds that each settle at least one event (wave scans and
+// ballots, no barriers):
 //   P: lanes >= cur pass while admits(x + their exclusive acquire prefix): first failing lane f;
 //   S: f blocked; the next pass is the first lane c > f with admits(x, a_c) (x does not grow until
 //      then, admits is monotone in x); (f, c) blocked, c passes.
-// Once not even an acquire of 1 is admitted, the rest is blocked without tests.  x, npass and acq
-// (the acquire total) are updated in every lane.
-template <class Fetch>
-__device__ inline void wave_walk(uint8_t kind, double thr, double I_s, uint32_t len, int64_t &x, int64_t &npass,
-                                 int64_t &acq_total, Fetch fetch) {
+// Stops where not even an acquire of 1 is admitted any more and returns that index (len if never):
+// every event from there on is blocked, which the caller writes with all its lanes.  x, npass and acq
+// (the acquire sum of the events decided here) are updated in every lane.
+template <class Load, class Decode>
+__device__ inline uint32_t wave_walk(uint8_t kind, double thr, double I_s, uint32_t len, int64_t &x, int64_t &npass,
+                                     int64_t &acq, Load load, Decode decode) {
     const uint32_t lane = lane_id();
-    bool dead = false;
+    uint64_t raw = lane < len ? load(lane) : 0ull;
     for (uint32_t c0 = 0; c0 < len; c0 += WAVE) {
         const uint32_t cnt = min((uint32_t)WAVE, len - c0);
         const bool valid = lane < cnt;
+        const uint64_t cur_raw = raw;
+        raw = c0 + WAVE + lane < len ? load(c0 + WAVE + lane) : 0ull;     // next window in flight
         int32_t a = 0;
         uint64_t *dst = nullptr;
-        if (valid) fetch(c0 + lane, a, dst);
-        {
-            int64_t sa = a;
-#pragma unroll
-            for (int off = 1; off < WAVE; off <<= 1) sa += __shfl_xor(sa, off, WAVE);
-            acq_total = wrap_add(acq_total, sa);
-        }
+        if (valid) decode(c0 + lane, cur_raw, a, dst);
         uint32_t cur = 0;
         while (cur < cnt) {
-            if (!dead) dead = !admits(kind, thr, I_s, x, 1);
-            if (dead) {
-                if (valid && lane >= cur) *dst = pack_verdict(ST_BLOCKED, 0, 0);
-                break;
+            if (!admits(kind, thr, I_s, x, 1)) {
+                int64_t sa = lane < cur ? (int64_t)a : 0;
+#pragma unroll
+                for (int off = 1; off < WAVE; off <<= 1) sa += __shfl_xor(sa, off, WAVE);
+                acq = wrap_add(acq, sa);
+                return c0 + cur;
             }
             // P round
             const int64_t m = (valid && lane >= cur) ? (int64_t)a : 0;
@@ -1038,21 +1041,48 @@ __device__ inline void wave_walk(uint8_t kind, double thr, double I_s, uint32_t 
             npass += 1;
             cur = c + 1;
         }
+        int64_t sa = a;
+#pragma unroll
+        for (int off = 1; off < WAVE; off <<= 1) sa += __shfl_xor(sa, off, WAVE);
+        acq = wrap_add(acq, sa);
     }
+    return len;
 }
 
 // A heterogeneous segment [st, st + len) of the sorted values, walked by one wave.
 __device__ inline HetSums wave_het(uint8_t kind, double thr, double I_s, int64_t x, const uint64_t *sval, uint32_t st,
                                    uint32_t len, const EventSrc &src, int64_t T0, uint64_t *out) {
+    const uint32_t lane = lane_id();
     const int64_t x0 = x;
-    int64_t npass = 0, tot = 0;
-    wave_walk(kind, thr, I_s, len, x, npass, tot, [&](uint32_t i, int32_t &a, uint64_t *&dst) {
-        const uint64_t v = sval[st + i];
+    int64_t npass = 0;
+    auto decode = [&](uint32_t, uint64_t v, int32_t &a, uint64_t *&dst) {
         int64_t t;
         bool pr;
         src.unpack(v, T0, t, a, pr);
         dst = out + ((uint32_t)v & SEQ_MASK);
-    });
+    };
+    int64_t tot = 0;
+    const uint32_t dpos = wave_walk(kind, thr, I_s, len, x, npass, tot, [&](uint32_t i) { return sval[st + i]; }, decode);
+    // the blocked tail, 8 windows of loads in flight (its acquires complete the BLOCK sum)
+    int64_t tail = 0;
+    for (uint32_t i0 = dpos; i0 < len; i0 += 8 * WAVE) {
+        uint64_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = i0 + k * WAVE + lane < len ? sval[st + i0 + k * WAVE + lane] : 0ull;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (i0 + k * WAVE + lane < len) {
+                int64_t t;
+                int32_t a;
+                bool pr;
+                src.unpack(v[k], T0, t, a, pr);
+                tail += a;
+                out[(uint32_t)v[k] & SEQ_MASK] = pack_verdict(ST_BLOCKED, 0, 0);
+            }
+    }
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) tail += __shfl_xor(tail, off, WAVE);
+    tot = wrap_add(tot, tail);
     HetSums h;
     h.pass = wrap_add(x, -x0);
     h.npass = npass;
@@ -1067,8 +1097,12 @@ __device__ inline HetSums wave_het(uint8_t kind, double thr, double I_s, int64_t
 // k_verdict; heterogeneous ones are decided by wave_het; prioritized / pending-occupy / clock-went-
 // back ones take the sequential path in lane 0, after which every lane re-reads the header.
 template <int NMAX>
-__global__ __launch_bounds__(256) void k_process_wave(KeyTable T, BatchWork W, EventSrc src, Verdicts V, WaveRuns WR) {
+__global__ __launch_bounds__(256) void k_process_wave(KeyTable T, BatchWork W, EventSrc src, Verdicts V, WaveRuns WR,
+                                                      const uint32_t *nrun, uint32_t *het_hint) {
     const uint32_t total = *WR.n;
+    // keep the deferral on for the next batch only while batches have heterogeneous keys to defer
+    if (het_hint && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(het_hint, (total || *nrun) ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint32_t lane = lane_id();
     const int64_t T0 = src.t0();
     for (uint32_t wi = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE; wi < total;

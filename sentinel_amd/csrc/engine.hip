@@ -425,6 +425,7 @@ struct sentinel_engine {
     DevBuf d_part_stat;
     unsigned long long *h_part_stat = nullptr;   // pinned mirror, written asynchronously after each batch
     uint32_t *h_long_chunks = nullptr;           // pinned: hot-run chunks of a recent batch (launch hint)
+    uint32_t *h_het_hint = nullptr;              // pinned: the sorted path's heterogeneous-key deferral is on
     uint32_t hot_het_run = HOT_HET_RUN;          // sorted path: heterogeneous keys above this go to k_part_long
     int64_t flow_batches = 0, sorted_until = -1;
     bool diag_linear = false;  // SENTINEL_DIAG_LINEAR=1: verdicts in sorted order (cost diagnostic, wrong output)   // SENTINEL_PROCESS: 0 reg (default), 1 group, 2 thread-in-memory
@@ -765,7 +766,14 @@ struct sentinel_engine {
         // (and keys of WAVE_HET_RUN..HOT_HET_RUN events to k_process_wave)
         LongRuns LR{};
         WaveRuns WR{};
+        uint32_t *hint = nullptr;
         if (hot_het && max_n <= 16 && process_impl == 0) {
+            if (!h_het_hint && hipHostMalloc((void **)&h_het_hint, 4, 0) == hipSuccess) *h_het_hint = 1;
+            hint = h_het_hint;
+        }
+        // deferral on while recent batches had heterogeneous keys worth it (else k_process_reg only
+        // raises the pinned hint): batches without them skip two launches
+        if (hint && *(volatile uint32_t *)hint != 0) {
             const size_t lb = long_runs_bytes(n, hot_het_run, 4);
             if (w_runs.ensure(lb + 4 * ((size_t)n / WAVE_HET_RUN + 2)) == 0) {
                 LR = long_runs_at(w_runs.as<uint32_t>(), n, hot_het_run, 4);
@@ -779,7 +787,7 @@ struct sentinel_engine {
             if (WR.n)
                 launch("process_wave", n, s, [&] {
                     const unsigned gw = (unsigned)std::min<int64_t>(n / WAVE_HET_RUN / 4 + 1, 2048);
-                    k_process_wave<NM><<<gw, 256, 0, s>>>(T, W, src, V, WR);
+                    k_process_wave<NM><<<gw, 256, 0, s>>>(T, W, src, V, WR, LR.nrun, hint);
                 });
             if (LR.nrun) launch("part_long", n, s, [&] { launch_long<NM>(T, W.sval, LR, src, V, n, hot_het_run, s, nullptr, nullptr); });
         };
@@ -788,16 +796,16 @@ struct sentinel_engine {
                 k_process_grp<<<std::min<unsigned>(grid_for(n * PROC_G), 8192), 256, 0, s>>>(T, W, src, V, n);
             });
         else if (max_n <= 2 && process_impl == 0) {
-            launch("process", n, s, [&] { k_process_reg<2><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run); });
+            launch("process", n, s, [&] { k_process_reg<2><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run, hint); });
             hot(std::integral_constant<int, 2>{});
         } else if (max_n <= 4 && process_impl == 0) {
-            launch("process", n, s, [&] { k_process_reg<4><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run); });
+            launch("process", n, s, [&] { k_process_reg<4><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run, hint); });
             hot(std::integral_constant<int, 4>{});
         } else if (max_n <= 10 && process_impl == 0) {
-            launch("process", n, s, [&] { k_process_reg<10><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run); });
+            launch("process", n, s, [&] { k_process_reg<10><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run, hint); });
             hot(std::integral_constant<int, 10>{});
         } else if (max_n <= 16 && process_impl == 0) {
-            launch("process", n, s, [&] { k_process_reg<16><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run); });
+            launch("process", n, s, [&] { k_process_reg<16><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run, hint); });
             hot(std::integral_constant<int, 16>{});
         }
         else
@@ -1646,6 +1654,7 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
     if (e->s_d2h) (void)hipStreamDestroy(e->s_d2h);
     if (e->h_part_stat) (void)hipHostFree(e->h_part_stat);
     if (e->h_long_chunks) (void)hipHostFree(e->h_long_chunks);
+    if (e->h_het_hint) (void)hipHostFree(e->h_het_hint);
     e->d_part_stat.release();
     (void)hipStreamDestroy(e->stream);
     delete e;

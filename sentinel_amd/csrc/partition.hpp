@@ -829,16 +829,24 @@ __device__ inline HetSums coop_het(uint32_t st, uint32_t en, const int32_t (&a)[
     } else {
         x = wrap_add(x, L.acq);
         if (threadIdx.x < WAVE) {
-            int64_t np = 0, tot = 0;
-            wave_walk(kind, thr, I_s, en - f, x, np, tot, [&](uint32_t i, int32_t &ai, uint64_t *&dst) {
-                ai = a_lds[f + i];
-                dst = out + ((uint32_t)cval[f + i] & SEQ_MASK);
-            });
-            if (threadIdx.x == 0) { L.acq = x; L.np = np; }
+            int64_t np = 0, acq = 0;
+            const uint32_t d = wave_walk(
+                kind, thr, I_s, en - f, x, np, acq, [&](uint32_t i) { return cval[f + i]; },
+                [&](uint32_t i, uint64_t v, int32_t &ai, uint64_t *&dst) {
+                    ai = a_lds[f + i];
+                    dst = out + ((uint32_t)v & SEQ_MASK);
+                });
+            if (threadIdx.x == 0) { L.acq = x; L.np = np; L.first[1] = f + d; }
         }
         __syncthreads();
         x = L.acq;
         npass += L.np;
+        const uint32_t dead0 = L.first[1];      // from here on every event is blocked
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            const uint32_t q = t0 + k;
+            if (q >= dead0 && q < en) out[(uint32_t)cval[q] & SEQ_MASK] = pack_verdict(ST_BLOCKED, 0, 0);
+        }
         __syncthreads();
     }
     HetSums h;
@@ -953,7 +961,6 @@ __global__ __launch_bounds__(LS_THREADS) void k_long_dead(const uint64_t *__rest
 // sequential) up to a heterogeneous-acquire one, which the workgroup decides (coop_het), then all
 // lanes write the closed-form verdicts.  A chunk boundary only splits a segment in two consecutive
 // segments of the same epoch, which the window algebra treats identically.
-constexpr int PL_RECS = 256;     // chunk records staged in LDS at a time
 template <int NMAX>
 __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint64_t *__restrict__ sval, LongRuns L,
                                                           EventSrc src, Verdicts V,
@@ -977,7 +984,8 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
     __shared__ HetLds hl;
     __shared__ uint32_t s_het;
     __shared__ int64_t s_hx;
-    __shared__ LongRec recs[PL_RECS];
+    __shared__ uint32_t s_stop, s_dcnt;         // dead stretch: first chunk not in it, events in it
+    __shared__ unsigned long long s_dacq;        // ... and their acquire sum
     __shared__ int32_t a_lds[PL_CHUNK];          // the chunk's acquire counts (coop_het's wave walk)
     __shared__ uint32_t s_dead;                  // the window is dead at epoch s_deadE
     __shared__ int64_t s_deadE;
@@ -991,7 +999,15 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
         if (threadIdx.x == 0) {
             fw.load(T, key, T0);
             s_dead = 0;
+            if (L.rec) {                          // already dead at the first chunk's epoch (an earlier batch)?
+                const LongRec R0 = L.rec[cb];
+                if ((R0.flags & LR_UNIFORM) && fw.dead_at(R0.E)) {
+                    s_dead = 1;
+                    s_deadE = R0.E;
+                }
+            }
         }
+        __syncthreads();                          // s_dead is read by every wave below
         const int32_t w = T.w[key];
         const double rcp = T.rcp_w[key];
         const uint8_t kind = T.kind[key];
@@ -1001,29 +1017,50 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
         HetSums dsum{0, 0, 0, 0};                 // lane 0: dead chunks booked but not yet written back
 #ifdef SENTINEL_DIAG_LONG
         uint32_t d_full = 0, d_dead = 0, d_deadflag = 0, d_unif = 0;
+        uint64_t d_t0 = __builtin_amdgcn_s_memrealtime(), d_tfull = 0, d_tc = 0, d_tpro = 0, d_twalk = 0;
 #endif
         for (uint32_t ci = 0; ci < nch; ++ci) {
-            if (L.rec && ci % PL_RECS == 0) {
-                __syncthreads();
-                for (uint32_t j = threadIdx.x; j < PL_RECS && ci + j < nch; j += PL_THREADS) recs[j] = L.rec[cb + ci + j];
-                __syncthreads();
-            }
-            const LongRec &R = recs[ci % PL_RECS];
-            if (L.rec && s_dead && (R.flags & LR_UNIFORM) && R.E == s_deadE) {     // uniform: LDS values only
-                if (threadIdx.x == 0) {
-#ifdef SENTINEL_DIAG_LONG
-                    ++d_dead;
-#endif
-                    dsum.block = wrap_add(dsum.block, R.acq);
-                    dsum.nblock += R.cnt;
-                    L.rec[cb + ci].flags = R.flags | LR_DEAD;
+            if (L.rec && s_dead) {
+                // the dead stretch from ci: chunks wholly in the dead epoch (one epoch, no prioritized
+                // request), PL_THREADS records at a time: booked and flagged in parallel
+                const uint32_t j = ci + threadIdx.x;
+                LongRec R{};
+                bool elig = false;
+                if (j < nch) {
+                    R = L.rec[cb + j];
+                    elig = (R.flags & LR_UNIFORM) && R.E == s_deadE;
                 }
-                continue;
+                if (threadIdx.x == 0) { s_stop = nch; s_dacq = 0; s_dcnt = 0; }
+                __syncthreads();
+                if (!elig && j < nch) atomicMin(&s_stop, j);
+                __syncthreads();
+                const uint32_t stop = min(s_stop, ci + (uint32_t)PL_THREADS);
+                if (stop > ci) {
+                    if (j < stop) {
+                        L.rec[cb + j].flags = R.flags | LR_DEAD;
+                        atomicAdd(&s_dacq, (unsigned long long)R.acq);
+                        atomicAdd(&s_dcnt, R.cnt);
+                    }
+                    __syncthreads();
+                    if (threadIdx.x == 0) {
+#ifdef SENTINEL_DIAG_LONG
+                        d_dead += stop - ci;
+#endif
+                        dsum.block = wrap_add(dsum.block, (int64_t)s_dacq);
+                        dsum.nblock += s_dcnt;
+                    }
+                    __syncthreads();
+                    ci = stop - 1;
+                    continue;
+                }
             }
             if (threadIdx.x == 0 && dsum.nblock) {
                 fw.het_book(s_deadE, false, dsum);
                 dsum = HetSums{0, 0, 0, 0};
             }
+#ifdef SENTINEL_DIAG_LONG
+            d_tc = __builtin_amdgcn_s_memrealtime();
+#endif
             const uint32_t c0 = q0 + ci * PL_CHUNK;
             const uint32_t cn = min((uint32_t)PL_CHUNK, q1 - c0);
             int64_t E[PL_ITEMS];
@@ -1085,6 +1122,9 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
             // one, which the whole workgroup decides (coop_het); then lane 0 goes on
             const uint32_t ns = s_nseg;
             uint32_t from = 0;
+#ifdef SENTINEL_DIAG_LONG
+            d_tpro += __builtin_amdgcn_s_memrealtime() - d_tc;
+#endif
             for (;;) {
                 if (threadIdx.x == 0) {
                     uint32_t sgi = from;
@@ -1115,7 +1155,6 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
 #ifdef SENTINEL_DIAG_LONG
                         ++d_full;
                         d_deadflag += s_dead;
-                        d_unif += (L.rec && (R.flags & LR_UNIFORM)) ? 1u : 0u;
 #endif
                     }
                 }
@@ -1128,6 +1167,9 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
                 if (threadIdx.x == 0) fw.het_book(seg_E[hs], h_fresh, sums);
                 from = hs + 1;
             }
+#ifdef SENTINEL_DIAG_LONG
+            d_twalk += __builtin_amdgcn_s_memrealtime() - d_tc;
+#endif
 #pragma unroll
             for (int k = 0; k < PL_ITEMS; ++k) {
                 const uint32_t qq = threadIdx.x * PL_ITEMS + k;
@@ -1145,14 +1187,20 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
                 V.out[seq] = v;
             }
             __syncthreads();
+#ifdef SENTINEL_DIAG_LONG
+            d_tfull += __builtin_amdgcn_s_memrealtime() - d_tc;
+#endif
         }
         if (threadIdx.x == 0) {
             if (dsum.nblock) fw.het_book(s_deadE, false, dsum);
             fw.flush();
 #ifdef SENTINEL_DIAG_LONG
             if (nch >= 8)
-                printf("long run key %u chunks %u full %u dead %u deadflag %u uniform %u recs %d thr %f kind %d occ %d\n", key,
-                       nch, d_full, d_dead, d_deadflag, d_unif, L.rec != nullptr, thr, (int)kind, (int)fw.occ_pending);
+                printf("long run key %u chunks %u full %u dead %u deadflag %u uniform %u recs %d thr %f kind %d occ %d "
+                       "t_total_us %.1f t_full_us %.1f pro %.1f walk %.1f\n", key,
+                       nch, d_full, d_dead, d_deadflag, d_unif, L.rec != nullptr, thr, (int)kind, (int)fw.occ_pending,
+                       (__builtin_amdgcn_s_memrealtime() - d_t0) / 100.0, d_tfull / 100.0, d_tpro / 100.0,
+                       d_twalk / 100.0);
 #endif
         }
         __syncthreads();
