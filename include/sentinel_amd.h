@@ -262,8 +262,27 @@ int  sentinel_submit_local_param_batch(sentinel_engine_t *eng, int64_t n, const 
                                        void *stream);
 int  sentinel_submit_local_param_batch_host(sentinel_engine_t *eng, int64_t n, const sentinel_param_multi_event_t *events,
                                             const uint64_t *values, int64_t n_values, sentinel_verdict_t *verdicts);
-/* Token bucket of one value: {lastAddTokenTime, tokens} (-1 when absent); returns 1 if present. */
+/* Token bucket of one value: {lastAddTokenTime, tokens} (-1 when absent); returns 1 if present.
+ * For a THREAD grade rule `tokens` is the value's thread count (-1: no entry in the map). */
 int  sentinel_local_param_state(sentinel_engine_t *eng, uint64_t param_key, int64_t *last_add_ms, int64_t *tokens);
+/* Grades of the loaded local rules (ParamFlowRule.grade: 1 QPS = the token bucket above, 0 THREAD);
+ * reset to all-QPS by every sentinel_load_local_param_rules.  A THREAD rule's check passes iff every
+ * value's thread count + 1 <= its threshold (hot-item count, else (long) count:
+ * ParamFlowChecker.passSingleValueCheck, ParamFlowChecker.java:112-122); a passing check adds one to
+ * every value (the entry callback, ParameterMetric.addThreadCount, ParameterMetric.java:184-239).
+ * Counts live per param key, so a rule's keys should encode (resource, paramIdx, value) -- the
+ * reference shares one map per param index (exact when one param rule reads an index). */
+int  sentinel_set_local_param_grades(sentinel_engine_t *eng, const int32_t *grades, int32_t n);
+/* Local param batch with event kinds: kinds[i] == 1 is Entry.exit of a passed entry -- its values'
+ * thread counts drop by one, removed at 0 (ParameterMetric.decreaseThreadCount,
+ * ParameterMetric.java:125-181; answers OK, no-op for QPS rules); anything else a check as in
+ * sentinel_submit_local_param_batch.  kinds may be NULL (all checks). */
+int  sentinel_submit_local_param_batch_ex(sentinel_engine_t *eng, int64_t n, const sentinel_param_multi_event_t *events,
+                                          const uint8_t *kinds, const uint64_t *values, int64_t n_values,
+                                          sentinel_verdict_t *verdicts, void *stream);
+int  sentinel_submit_local_param_batch_ex_host(sentinel_engine_t *eng, int64_t n, const sentinel_param_multi_event_t *events,
+                                               const uint8_t *kinds, const uint64_t *values, int64_t n_values,
+                                               sentinel_verdict_t *verdicts);
 
 /* ---- local SphU.entry admission: DefaultController over a resource's ClusterNode ----
  * FlowSlot -> FlowRuleChecker.passLocalCheck -> DefaultController.canPass (QPS grade, limitApp
@@ -297,6 +316,44 @@ int  sentinel_local_node_stats(sentinel_engine_t *eng, int32_t resource_idx, int
 /* OccupyTimeoutProperty.updateTimeout (OccupyTimeoutProperty.java:64-78): values < 0 or above the
  * node interval are ignored (default 500 ms). */
 int  sentinel_set_occupy_timeout(sentinel_engine_t *eng, int32_t timeout_ms);
+
+/* Resources with QPS and / or THREAD grade DefaultController rules (FlowRuleChecker.checkFlow checks
+ * a resource's rules in order; every rule of a grade must pass, so the smallest count of each grade
+ * decides).  THREAD: cur = (int) curThreadNum (StatisticNode.java:241-243), block iff
+ * (double)(cur + acquire) > count (DefaultController.java:49-51).  The prioritized occupy path only
+ * follows a failing QPS rule, and skips the rules after it, hence THREAD_FIRST.  Counts < 0 drop the
+ * rule (FlowRuleUtil.isValidRule).  24 bytes. */
+#define SENTINEL_LOCAL_QPS           1
+#define SENTINEL_LOCAL_THREAD        2
+#define SENTINEL_LOCAL_THREAD_FIRST  4
+typedef struct {
+    double  qps_count;
+    double  thread_count;
+    int32_t flags;       /* SENTINEL_LOCAL_* */
+    int32_t reserved;
+} sentinel_local_resource_ex_t;
+int  sentinel_load_local_resources_ex(sentinel_engine_t *eng, const sentinel_local_resource_ex_t *res, int32_t n,
+                                      int32_t sample_count, int32_t interval_ms);
+
+/* A local batch of entries and exits.  flags[i]: bit 0 prioritized entry, bit 1 EXIT -- Entry.exit
+ * of an entry that passed (StatisticSlot.exit, StatisticSlot.java:126-164; a blocked entry's exit
+ * books nothing and must not be sent): at ts, SUCCESS += acquire and RT += rt_ms[i] in the second
+ * and minute windows (StatisticNode.addRtAndSuccess, StatisticNode.java:252-258; each bucket keeps
+ * its minRt, MetricBucket.java:132-139), curThreadNum -= 1, and with bit 2 (a business exception
+ * traced on the entry: Tracer.trace -> Entry.setError) EXCEPTION += acquire.  An entry that passes
+ * adds one thread (StatisticSlot.java:62, 82).  Exits answer OK.  flags / rt_ms may be NULL (plain
+ * entries).  Events of one resource are applied in arrival order. */
+int  sentinel_submit_local_batch(sentinel_engine_t *eng, int64_t n, const sentinel_event_t *events, const uint8_t *flags,
+                                 const int64_t *rt_ms, sentinel_verdict_t *verdicts, void *stream);
+int  sentinel_submit_local_batch_host(sentinel_engine_t *eng, int64_t n, const sentinel_event_t *events,
+                                      const uint8_t *flags, const int64_t *rt_ms, sentinel_verdict_t *verdicts);
+/* Read-only view of a resource's node at ts as a roll at ts would leave it: out[0..5] second window
+ * {PASS, BLOCK, EXCEPTION, SUCCESS, RT, minRt}, out[6..12] minute window {PASS, BLOCK,
+ * OCCUPIED_PASS, EXCEPTION, SUCCESS, RT, minRt}, out[13] curThreadNum.  minRt as ArrayMetric.minRt
+ * (ArrayMetric.java:142-153): max(1, min(statisticMaxRt, the valid buckets' minRt)). */
+int  sentinel_local_node_metrics(sentinel_engine_t *eng, int32_t resource_idx, int64_t ts, int64_t *out14);
+/* SentinelConfig.statisticMaxRt (default 5000 ms): a fresh bucket's minRt. */
+int  sentinel_set_statistic_max_rt(sentinel_engine_t *eng, int64_t max_rt_ms);
 
 /* ---- cluster concurrency tokens (thread grade): TokenService.requestConcurrentToken /
  *      releaseConcurrentToken (TokenService.java:56,62) -> ConcurrentClusterFlowChecker
@@ -362,6 +419,41 @@ int  sentinel_batcher_request_token_async(sentinel_batcher_t *b, int64_t flow_id
                                           int32_t prioritized, int64_t ts, sentinel_token_cb cb, void *ctx,
                                           uint64_t tag);
 int  sentinel_batcher_stats(sentinel_batcher_t *b, int64_t *batches, int64_t *requests);
+
+/* ---- one node, several devices ----
+ * One engine per entry of device_ids (a device may repeat: several shards on one GPU); flows are
+ * partitioned shard = splitmix64(flowId) mod n (a flow's verdicts depend only on its own window and
+ * host constants: no exchange on the decision path).  Rule tables are split by shard (the
+ * putMetricIfAbsent orphan rule still sees the whole node's namespace lists); namespace and server
+ * config are broadcast.  Replaces one DefaultTokenService over the whole flowId space.  The
+ * GlobalRequestLimiter couples a namespace's flows: exact only when they share a shard or the
+ * limiter is off. */
+typedef struct sentinel_cluster sentinel_cluster_t;
+int32_t sentinel_shard_of(int64_t flow_id, int32_t n_shards);
+int  sentinel_cluster_create(const int32_t *device_ids, int32_t n, const sentinel_server_config_t *cfg,
+                             sentinel_cluster_t **out);
+int  sentinel_cluster_destroy(sentinel_cluster_t *c);
+int32_t sentinel_cluster_size(sentinel_cluster_t *c);
+int  sentinel_cluster_engine(sentinel_cluster_t *c, int32_t shard, sentinel_engine_t **out);
+int  sentinel_cluster_set_server_config(sentinel_cluster_t *c, const sentinel_server_config_t *cfg);
+int  sentinel_cluster_set_namespaces(sentinel_cluster_t *c, const sentinel_namespace_t *ns, int32_t n);
+int  sentinel_cluster_set_connected_count(sentinel_cluster_t *c, int32_t namespace_idx, int32_t connected);
+int  sentinel_cluster_load_flow_rules(sentinel_cluster_t *c, const sentinel_flow_rule_t *rules, int32_t n);
+int  sentinel_cluster_load_param_rules(sentinel_cluster_t *c, const sentinel_param_rule_t *rules, int32_t n,
+                                       const uint64_t *hot_keys, const int32_t *hot_counts, int32_t n_hot);
+/* requestToken for a host batch of flowIds (flags bit 0: prioritized): routed to the owning shards
+ * (arrival order kept per flow), decided concurrently, verdicts at the arrival positions. */
+int  sentinel_cluster_submit_host(sentinel_cluster_t *c, int64_t n, const int64_t *flow_ids, const int32_t *acquire,
+                                  const int64_t *ts, const uint8_t *flags, sentinel_verdict_t *verdicts);
+int32_t sentinel_cluster_flow_count(sentinel_cluster_t *c);
+/* Every shard's snapshot records at ts, shard after shard; cap >= sentinel_cluster_flow_count. */
+int  sentinel_cluster_snapshot(sentinel_cluster_t *c, int64_t ts, sentinel_flow_snapshot_t *out, int64_t cap,
+                               int64_t *n_out);
+/* The per-call front door over every shard: one batcher (dispatcher thread) per engine, each call
+ * routed to its flow's shard. */
+int  sentinel_cluster_batchers_create(sentinel_cluster_t *c, int32_t max_batch, int32_t max_wait_us);
+int  sentinel_cluster_request_token(sentinel_cluster_t *c, int64_t flow_id, int32_t acquire_count,
+                                    int32_t prioritized, int64_t ts, sentinel_token_result_t *out);
 
 /* ---- observability / parity ---- */
 int  sentinel_synchronize(sentinel_engine_t *eng);

@@ -119,6 +119,10 @@ def lib():
         "orc_local_replay_prio": (None, [vp, dbl, i64, vp, vp, vp, vp, vp]),
         "orc_local_entry": (C.c_int, [vp, dbl, C.c_int, C.c_int, i64, vp]),
         "orc_node_set_occupy_timeout": (None, [vp, C.c_int]),
+        "orc_node_set_max_rt": (None, [vp, i64]),
+        "orc_local_entry_ex": (C.c_int, [vp, dbl, dbl, C.c_int, C.c_int, C.c_int, i64, vp]),
+        "orc_local_exit": (None, [vp, C.c_int, i64, C.c_int, i64]),
+        "orc_node_metrics": (None, [vp, i64, vp]),
         "orc_node_waiting": (i64, [vp, i64]),
         "orc_node_minute_occupied": (i64, [vp, i64]),
         "orc_node_try_occupy_next": (i64, [vp, i64, C.c_int, dbl]),
@@ -136,6 +140,9 @@ def lib():
         "orc_lparam_free": (None, [vp]),
         "orc_lparam_replay": (None, [vp, i64, vp, vp, vp, vp, vp, vp, i64, vp]),
         "orc_lparam_state": (C.c_int, [vp, i32, u64, vp, vp]),
+        "orc_lparam_set_grades": (None, [vp, vp, C.c_int]),
+        "orc_lparam_replay_ex": (None, [vp, i64, vp, vp, vp, vp, vp, vp, i64, vp, vp]),
+        "orc_lparam_thread_count": (C.c_int, [vp, i32, u64]),
         "orc_concurrent_replay": (None, [vp, i64, vp, vp, vp, vp]),
         "orc_concurrent_now_calls": (i32, [vp, i32]),
         "orc_concurrent_token_count": (i64, [vp]),
@@ -223,6 +230,9 @@ class ClusterParamMetric:
         return {int(keys[i]): float(avgs[i]) for i in range(k)}
 
 
+LR_QPS, LR_THREAD, LR_THREAD_FIRST = 1, 2, 4
+
+
 class StatisticNode:
     def __init__(self, sample_count: int = 2, interval_ms: int = 1000):
         self.h = lib().orc_node_new(sample_count, interval_ms)
@@ -265,6 +275,23 @@ class StatisticNode:
         return bool(ok), int(w.value)
 
     def set_occupy_timeout(self, ms): lib().orc_node_set_occupy_timeout(self.h, ms)
+    def set_max_rt(self, ms): lib().orc_node_set_max_rt(self.h, ms)
+
+    # QPS / THREAD grade rules (flags: LR_QPS | LR_THREAD | LR_THREAD_FIRST) and exits
+    def entry_ex(self, qps_count, thread_count, flags, acquire, t, prioritized=False):
+        w = C.c_int64(0)
+        ok = lib().orc_local_entry_ex(self.h, qps_count, thread_count, flags, acquire, int(prioritized), t, C.byref(w))
+        return bool(ok), int(w.value)
+
+    def exit(self, count, rt, t, error=False):
+        lib().orc_local_exit(self.h, count, rt, int(error), t)
+
+    def metrics(self, t) -> np.ndarray:
+        """[sec PASS, BLOCK, EXCEPTION, SUCCESS, RT, minRt, min PASS, BLOCK, OCCUPIED_PASS, EXCEPTION,
+        SUCCESS, RT, minRt, curThreadNum] at t (read-only, no roll)."""
+        out = np.zeros(14, dtype=np.int64)
+        lib().orc_node_metrics(self.h, t, _p(out))
+        return out
     def waiting(self, t): return lib().orc_node_waiting(self.h, t)
     def minute_occupied(self, t): return lib().orc_node_minute_occupied(self.h, t)
     def try_occupy_next(self, t, acquire, threshold): return lib().orc_node_try_occupy_next(self.h, t, acquire, threshold)
@@ -309,7 +336,7 @@ class LocalParamOracle:
     """ParamFlowChecker.passLocalCheck replay, one ParameterMetric per rule (ParamFlowChecker.java:78-202).
     rules: [(count, burst_count, duration_in_sec, {key: hot_count})]; rule index = position."""
 
-    def __init__(self, rules):
+    def __init__(self, rules, grades=None):
         arr = (LocalParamRule * max(len(rules), 1))()
         keys, counts = [], []
         for i, (count, burst, dur, hot) in enumerate(rules):
@@ -320,17 +347,26 @@ class LocalParamOracle:
         hk = np.array(keys or [0], dtype=np.uint64)
         hc = np.array(counts or [0], dtype=np.int32)
         self.h = lib().orc_lparam_new(arr, len(rules), _p(hk), _p(hc), len(keys))
+        if grades is not None:     # 0 THREAD, 1 QPS (default)
+            g = np.ascontiguousarray(grades, dtype=np.int32)
+            lib().orc_lparam_set_grades(self.h, _p(g), len(g))
 
     def __del__(self):
         if getattr(self, "h", None):
             lib().orc_lparam_free(self.h)
 
-    def replay(self, rule_idx, acquire, ts, vbegin, vcount, values) -> np.ndarray:
+    def replay(self, rule_idx, acquire, ts, vbegin, vcount, values, kinds=None) -> np.ndarray:
+        """kinds[i] == 1: an exit (thread counts drop), else a check."""
         r, a, t, b, c, v = _multi_args(rule_idx, acquire, ts, vbegin, vcount, values)
         status = np.zeros(len(t), dtype=np.int8)
-        lib().orc_lparam_replay(self.h, len(t), _p(r), _p(a), _p(t), _p(b), _p(c), _p(v) if len(v) else None,
-                                len(v), _p(status))
+        k = None if kinds is None else np.ascontiguousarray(kinds, dtype=np.uint8)
+        lib().orc_lparam_replay_ex(self.h, len(t), _p(r), _p(a), _p(t), _p(b), _p(c), _p(v) if len(v) else None,
+                                   len(v), _p(k) if k is not None else None, _p(status))
         return status
+
+    def thread_count(self, rule_idx, key) -> int:
+        """-1 when the value has no entry in the thread-count map."""
+        return lib().orc_lparam_thread_count(self.h, int(rule_idx), int(key))
 
     def state(self, rule_idx, key):
         last, tok = C.c_int64(), C.c_int64()

@@ -908,7 +908,10 @@ int orc_engine_param_overflowed(const orc_engine *e) {
 typedef struct {
     leap la;
     int64_t *c;          /* n x 6 MetricBucket counters */
+    int64_t *minrt;      /* n MetricBucket.minRt (MB:38, reset to statisticMaxRt: MB:58-60) */
     int64_t scratch[ORC_M_NEVENTS];
+    int64_t scratch_minrt;
+    const int64_t *max_rt;   /* SentinelConfig.statisticMaxRt() of the node */
     int occupiable;      /* seed new / reset buckets from `borrow` (OBLA:40-64) */
     void *borrow;        /* bucket_array * (FutureBucketLeapArray) */
     int future;          /* FutureBucketLeapArray: deprecated iff time >= windowStart (FBLA:49-52) */
@@ -917,12 +920,15 @@ typedef struct {
 struct orc_stat_node {
     bucket_array sec, min, borrow;
     int occupy_timeout;  /* OccupyTimeoutProperty.occupyTimeout (default 500) */
+    int64_t threads;     /* SN:108 curThreadNum (LongAdder) */
+    int64_t max_rt;      /* SentinelConfig.statisticMaxRt (default 5000, SentinelConfig.java:63) */
 };
 
 static void ba_init(bucket_array *a, int n, int interval) {
     memset(a, 0, sizeof(*a));
     leap_init(&a->la, n, interval);
     a->c = (int64_t *)calloc((size_t)n * ORC_M_NEVENTS, sizeof(int64_t));
+    a->minrt = (int64_t *)calloc((size_t)n, sizeof(int64_t));
 }
 
 static int ba_deprecated(const bucket_array *a, int64_t t, int i) {
@@ -943,8 +949,13 @@ static int64_t *ba_current(bucket_array *a, int64_t t) {
     int i = 0;
     int act = leap_locate(&a->la, t, &i);
     if (act == LA_NULL) return NULL;
-    if (act == LA_DETACHED) { memset(a->scratch, 0, sizeof(a->scratch)); return a->scratch; }
+    if (act == LA_DETACHED) {
+        memset(a->scratch, 0, sizeof(a->scratch));
+        a->scratch_minrt = a->max_rt ? *a->max_rt : 0;
+        return a->scratch;
+    }
     int64_t *b = a->c + (size_t)i * ORC_M_NEVENTS;
+    if ((act == LA_NEW || act == LA_RESET) && a->max_rt) a->minrt[i] = *a->max_rt;   /* initMinRt */
     if (act == LA_NEW) {
         memset(b, 0, sizeof(int64_t) * ORC_M_NEVENTS);
         if (a->occupiable) {                   /* OBLA:40-49 newEmptyBucket(time): reset(borrowBucket) */
@@ -974,23 +985,61 @@ static void ba_add(bucket_array *a, int64_t t, int ev, int64_t x) {
     if (b) b[ev] = wrap_add64(b[ev], x);
 }
 
+/* MetricBucket.addRT (MB:132-139) through ArrayMetric.addRT (AM:249-252): roll, add, keep the min. */
+static void ba_add_rt(bucket_array *a, int64_t t, int64_t rt) {
+    int64_t *b = ba_current(a, t);
+    if (!b) return;
+    b[ORC_M_RT] = wrap_add64(b[ORC_M_RT], rt);
+    int64_t *m = b == a->scratch ? &a->scratch_minrt : &a->minrt[(b - a->c) / ORC_M_NEVENTS];
+    if (rt < *m) *m = rt;
+}
+
+/* Read-only view of the windows as a roll at t would leave them (LA:316-318 after currentWindow):
+ * buckets of the epochs > epoch(t) - n, future buckets included; the bucket the roll would reset
+ * (epoch(t) - n, same slot) is not counted. */
+static int ba_view_valid(const bucket_array *a, int64_t t, int i) {
+    if (!a->la.present[i]) return 0;
+    const int64_t E = t / a->la.win;
+    return a->la.start[i] / a->la.win > E - a->la.n;
+}
+
+/* ArrayMetric.minRt (AM:142-153): max(1, min(statisticMaxRt, minRt of the valid buckets)). */
+static int64_t ba_min_rt(const bucket_array *a, int64_t t, int64_t max_rt) {
+    int64_t rt = max_rt;
+    for (int i = 0; i < a->la.n; i++)
+        if (ba_view_valid(a, t, i) && a->minrt[i] < rt) rt = a->minrt[i];
+    return rt > 1 ? rt : 1;
+}
+
+static int64_t ba_view_sum(const bucket_array *a, int64_t t, int ev) {
+    int64_t s = 0;
+    for (int i = 0; i < a->la.n; i++)
+        if (ba_view_valid(a, t, i)) s = wrap_add64(s, a->c[(size_t)i * ORC_M_NEVENTS + ev]);
+    return s;
+}
+
 orc_stat_node *orc_node_new(int sample_count, int interval_ms) {
     orc_stat_node *nd = (orc_stat_node *)calloc(1, sizeof(*nd));
+    nd->max_rt = 5000;
     ba_init(&nd->sec, sample_count, interval_ms);
     ba_init(&nd->borrow, sample_count, interval_ms);     /* OBLA:36 */
     nd->borrow.future = 1;
     nd->sec.occupiable = 1;
     nd->sec.borrow = &nd->borrow;
     ba_init(&nd->min, 60, 60 * 1000);
+    nd->sec.max_rt = &nd->max_rt;
+    nd->min.max_rt = &nd->max_rt;
     nd->occupy_timeout = 500;                            /* OccupyTimeoutProperty.java:40 */
     return nd;
 }
 
+void orc_node_set_max_rt(orc_stat_node *nd, int64_t ms) { nd->max_rt = ms; }
+
 void orc_node_free(orc_stat_node *nd) {
     if (!nd) return;
-    leap_free(&nd->sec.la); free(nd->sec.c);
-    leap_free(&nd->borrow.la); free(nd->borrow.c);
-    leap_free(&nd->min.la); free(nd->min.c);
+    leap_free(&nd->sec.la); free(nd->sec.c); free(nd->sec.minrt);
+    leap_free(&nd->borrow.la); free(nd->borrow.c); free(nd->borrow.minrt);
+    leap_free(&nd->min.la); free(nd->min.c); free(nd->min.minrt);
     free(nd);
 }
 
@@ -1077,22 +1126,7 @@ int orc_default_controller_check(double node_value, double count, int grade, int
  * Returns 1 pass, 0 block; *wait = waitInMs of a prioritized pass (PriorityWaitException: the
  * entry passes after sleeping, only the thread count and the occupied / waiting counters move). */
 int orc_local_entry(orc_stat_node *nd, double count, int acquire, int prioritized, int64_t t, int64_t *wait) {
-    *wait = 0;
-    if (orc_default_controller_can_pass(nd, count, 1, acquire, 0, t)) {
-        orc_node_add_pass_request(nd, t, acquire);                    /* SS:62-63 */
-        return 1;
-    }
-    if (prioritized) {                                               /* DC:52-64 */
-        const int64_t w = orc_node_try_occupy_next(nd, t, acquire, count);
-        if (w < nd->occupy_timeout) {
-            orc_node_add_waiting(nd, t + w, acquire);
-            orc_node_add_occupied_pass(nd, t, acquire);
-            *wait = w;                                               /* SS:81-95 */
-            return 1;
-        }
-    }
-    orc_node_increase_block_qps(nd, t, acquire);                     /* SS:96-104 */
-    return 0;
+    return orc_local_entry_ex(nd, count, 0.0, ORC_LR_QPS, acquire, prioritized, t, wait);
 }
 
 void orc_local_replay(orc_stat_node *nd, double count, int64_t n, const int32_t *acquire,
@@ -1107,6 +1141,80 @@ void orc_local_replay_prio(orc_stat_node *nd, double count, int64_t n, const int
                            const uint8_t *prio, uint8_t *out_pass, int64_t *out_wait) {
     for (int64_t i = 0; i < n; i++)
         out_pass[i] = (uint8_t)orc_local_entry(nd, count, acquire[i], prio ? (prio[i] & 1) : 0, ts[i], &out_wait[i]);
+}
+
+/* One SphU.entry of a resource with QPS and / or THREAD grade DefaultController rules
+ * (FlowRuleChecker.checkFlow: rules in order, the first failure throws; DC:49-76):
+ *   QPS    cur = (int) passQps      THREAD cur = (int) curThreadNum  (SN:241-243: long -> int cast)
+ *   block iff (double)(cur + acquire) > count, int add wrapping; only a QPS rule's failure of a
+ *   prioritized entry tries tryOccupyNext (PriorityWaitException: the remaining rules are skipped).
+ * Every QPS rule must pass, so `qps_count` is the smallest QPS count (likewise `thread_count`);
+ * flags: ORC_LR_QPS / ORC_LR_THREAD present, ORC_LR_THREAD_FIRST the THREAD rule precedes the QPS
+ * one.  Then StatisticSlot.entry (SS:55-123): pass -> increaseThreadNum + addPassRequest, occupied
+ * pass -> increaseThreadNum, block -> increaseBlockQps.  Returns 1 pass, 0 block. */
+int orc_local_entry_ex(orc_stat_node *nd, double qps_count, double thread_count, int flags, int acquire,
+                       int prioritized, int64_t t, int64_t *wait) {
+    *wait = 0;
+    const int has_q = flags & ORC_LR_QPS, has_t = flags & ORC_LR_THREAD;
+    const int thread_first = (flags & ORC_LR_THREAD_FIRST) != 0;
+    for (int pass = 0; pass < 2; pass++) {
+        const int check_thread = thread_first ? pass == 0 : pass == 1;
+        if (check_thread) {
+            if (!has_t) continue;
+            const int32_t cur = (int32_t)nd->threads;                                  /* SN:242 */
+            const int32_t sum = (int32_t)((uint32_t)cur + (uint32_t)acquire);
+            if ((double)sum > thread_count) goto blocked;
+        } else {
+            if (!has_q) continue;
+            if (orc_default_controller_can_pass(nd, qps_count, 1, acquire, 0, t)) continue;
+            if (prioritized) {                                                         /* DC:52-64 */
+                const int64_t w = orc_node_try_occupy_next(nd, t, acquire, qps_count);
+                if (w < nd->occupy_timeout) {
+                    orc_node_add_waiting(nd, t + w, acquire);
+                    orc_node_add_occupied_pass(nd, t, acquire);
+                    *wait = w;
+                    nd->threads = wrap_add64(nd->threads, 1);                          /* SS:81-82 */
+                    return 1;
+                }
+            }
+            goto blocked;
+        }
+    }
+    nd->threads = wrap_add64(nd->threads, 1);                                          /* SS:62-63 */
+    orc_node_add_pass_request(nd, t, acquire);
+    return 1;
+blocked:
+    orc_node_increase_block_qps(nd, t, acquire);                                       /* SS:96-104 */
+    return 0;
+}
+
+/* Entry.exit of an entry that passed (StatisticSlot.exit, SS:126-164; blocked entries book nothing):
+ * at completeStatTime t, recordCompleteFor -> addRtAndSuccess(rt, count) (SN:252-258: SUCCESS and
+ * RT into both windows, minRt kept per bucket), decreaseThreadNum, and increaseExceptionQps(count)
+ * when the entry carries a business exception (Tracer.trace -> Entry.setError). */
+void orc_local_exit(orc_stat_node *nd, int count, int64_t rt, int error, int64_t t) {
+    ba_add(&nd->sec, t, ORC_M_SUCCESS, count);
+    ba_add_rt(&nd->sec, t, rt);
+    ba_add(&nd->min, t, ORC_M_SUCCESS, count);
+    ba_add_rt(&nd->min, t, rt);
+    nd->threads = wrap_add64(nd->threads, -1);
+    if (error) {
+        ba_add(&nd->sec, t, ORC_M_EXCEPTION, count);
+        ba_add(&nd->min, t, ORC_M_EXCEPTION, count);
+    }
+}
+
+/* Read-only view at t (the valid buckets, no roll): out[0..5] second window {PASS, BLOCK,
+ * EXCEPTION, SUCCESS, RT, minRt}, out[6..12] minute window {PASS, BLOCK, OCCUPIED_PASS, EXCEPTION,
+ * SUCCESS, RT, minRt}, out[13] curThreadNum. */
+void orc_node_metrics(const orc_stat_node *nd, int64_t t, int64_t *out) {
+    const int ev6[5] = {ORC_M_PASS, ORC_M_BLOCK, ORC_M_EXCEPTION, ORC_M_SUCCESS, ORC_M_RT};
+    for (int k = 0; k < 5; k++) out[k] = ba_view_sum(&nd->sec, t, ev6[k]);
+    out[5] = ba_min_rt(&nd->sec, t, nd->max_rt);
+    const int ev7[6] = {ORC_M_PASS, ORC_M_BLOCK, ORC_M_OCCUPIED_PASS, ORC_M_EXCEPTION, ORC_M_SUCCESS, ORC_M_RT};
+    for (int k = 0; k < 6; k++) out[6 + k] = ba_view_sum(&nd->min, t, ev7[k]);
+    out[12] = ba_min_rt(&nd->min, t, nd->max_rt);
+    out[13] = nd->threads;
 }
 
 /* OccupiableBucketLeapArray surface for the reference's own tests (OccupiableBucketLeapArrayTest). */
@@ -1236,6 +1344,8 @@ typedef struct {
     int64_t token_count;      /* (long) rule.count (PFC:139) */
     orc_param_bucket *b;
     kvmap hot;                /* param key -> hot-item count (PFC:138-142) */
+    int grade;                /* RuleConstant.FLOW_GRADE_QPS (1, default) or FLOW_GRADE_THREAD (0) */
+    kvmap threads;            /* ParameterMetric.threadCountMap entry of the rule's param index: key -> count */
 } local_entry;
 
 struct orc_local_engine {
@@ -1254,6 +1364,8 @@ orc_local_engine *orc_lparam_new(const orc_local_param_rule *rules, int n, const
         le->valid = rules[i].count >= 0 && rules[i].burst_count >= 0 && rules[i].duration_in_sec > 0;
         le->token_count = orc_java_d2l(rules[i].count);
         le->b = orc_pbucket_new();
+        le->grade = 1;
+        kv_init(&le->threads);
         kv_init(&le->hot);
         for (int h = 0; h < rules[i].hot_n; h++) {
             const int j = rules[i].hot_begin + h;
@@ -1265,20 +1377,73 @@ orc_local_engine *orc_lparam_new(const orc_local_param_rule *rules, int n, const
 
 void orc_lparam_free(orc_local_engine *e) {
     if (!e) return;
-    for (int i = 0; i < e->n; i++) { orc_pbucket_free(e->rules[i].b); kv_free(&e->rules[i].hot); }
+    for (int i = 0; i < e->n; i++) {
+        orc_pbucket_free(e->rules[i].b);
+        kv_free(&e->rules[i].hot);
+        kv_free(&e->rules[i].threads);
+    }
     free(e->rules);
     free(e);
 }
 
-void orc_lparam_replay(orc_local_engine *e, int64_t n, const int32_t *rule_idx, const int32_t *acquire,
-                      const int64_t *ts, const int32_t *vbegin, const int32_t *vcount, const uint64_t *values,
-                      int64_t n_values, int8_t *status) {
+void orc_lparam_set_grades(orc_local_engine *e, const int32_t *grade, int n) {
+    for (int i = 0; i < n && i < e->n; i++) e->rules[i].grade = grade[i];
+}
+
+/* THREAD grade (PFC:112-122): each value passes iff ++threadCount <= threshold (hot-item count, else
+ * (long) rule.count), threadCount = ParameterMetric.getThreadCount (PM:241-249, absent 0); the
+ * check reads, the entry callback writes: a passing check adds one per value
+ * (ParamFlowStatisticEntryCallback -> PM.addThreadCount, PM:184-239; a repeated value twice). */
+static int lparam_thread_check(local_entry *le, const uint64_t *vals, int32_t c) {
+    for (int j = 0; j < c; j++) {
+        const int64_t *hv = kv_find(&le->hot, vals[j]);
+        const int64_t thr = hv ? *hv : le->token_count;
+        const int64_t *tc = kv_find(&le->threads, vals[j]);
+        const int64_t cur = tc ? *tc : 0;
+        if (!(cur + 1 <= thr)) return 0;
+    }
+    for (int j = 0; j < c; j++) {
+        int64_t *tc = kv_find(&le->threads, vals[j]);
+        if (tc) *tc = (int32_t)((uint32_t)*tc + 1u);                 /* AtomicInteger.incrementAndGet */
+        else kv_insert(&le->threads, vals[j], 1);
+    }
+    return 1;
+}
+
+/* Entry.exit -> ParamFlowStatisticExitCallback -> PM.decreaseThreadCount (PM:125-181): an absent
+ * value gets a 0 entry (putIfAbsent), a present one is decremented and removed at <= 0. */
+static void lparam_thread_exit(local_entry *le, const uint64_t *vals, int32_t c) {
+    for (int j = 0; j < c; j++) {
+        int64_t *tc = kv_find(&le->threads, vals[j]);
+        if (!tc) { kv_insert(&le->threads, vals[j], 0); continue; }
+        const int32_t v = (int32_t)((uint32_t)*tc - 1u);
+        if (v <= 0) kv_erase(&le->threads, vals[j]);
+        else *tc = v;
+    }
+}
+
+int orc_lparam_thread_count(orc_local_engine *e, int32_t idx, uint64_t key) {
+    if (idx < 0 || idx >= e->n) return -1;
+    const int64_t *tc = kv_find(&e->rules[idx].threads, key);
+    return tc ? (int)*tc : -1;
+}
+
+void orc_lparam_replay_ex(orc_local_engine *e, int64_t n, const int32_t *rule_idx, const int32_t *acquire,
+                          const int64_t *ts, const int32_t *vbegin, const int32_t *vcount, const uint64_t *values,
+                          int64_t n_values, const uint8_t *kinds, int8_t *status) {
     for (int64_t i = 0; i < n; i++) {
         const int32_t b = vbegin[i], c = vcount[i];
         if (c < 0 || b < 0 || (int64_t)b + c > n_values) { status[i] = ORC_BAD_REQUEST; continue; }
         const int32_t idx = rule_idx[i];
         if (idx < 0 || idx >= e->n || !e->rules[idx].valid) { status[i] = ORC_NO_RULE_EXISTS; continue; }
         local_entry *le = &e->rules[idx];
+        if (kinds && kinds[i] == 1) {                    /* exit */
+            if (le->grade == 0) lparam_thread_exit(le, values + b, c);
+            status[i] = ORC_OK;
+            continue;
+        }
+        if (c == 0) { status[i] = ORC_OK; continue; }
+        if (le->grade == 0) { status[i] = lparam_thread_check(le, values + b, c) ? ORC_OK : ORC_BLOCKED; continue; }
         int st = ORC_OK;
         for (int j = 0; j < c; j++) {      /* every element must pass, no rollback (PFC:81-94) */
             const uint64_t key = values[b + j];
@@ -1291,6 +1456,12 @@ void orc_lparam_replay(orc_local_engine *e, int64_t n, const int32_t *rule_idx, 
         }
         status[i] = (int8_t)st;
     }
+}
+
+void orc_lparam_replay(orc_local_engine *e, int64_t n, const int32_t *rule_idx, const int32_t *acquire,
+                      const int64_t *ts, const int32_t *vbegin, const int32_t *vcount, const uint64_t *values,
+                      int64_t n_values, int8_t *status) {
+    orc_lparam_replay_ex(e, n, rule_idx, acquire, ts, vbegin, vcount, values, n_values, NULL, status);
 }
 
 int orc_lparam_state(orc_local_engine *e, int32_t idx, uint64_t key, int64_t *last, int64_t *tokens) {

@@ -179,6 +179,13 @@ void   orc_local_replay_prio(orc_stat_node *nd, double count, int64_t n, const i
                              const int64_t *ts, const uint8_t *prio, uint8_t *out_pass, int64_t *out_wait);
 int    orc_local_entry(orc_stat_node *nd, double count, int acquire, int prioritized, int64_t t, int64_t *wait);
 void   orc_node_set_occupy_timeout(orc_stat_node *nd, int ms);
+void   orc_node_set_max_rt(orc_stat_node *nd, int64_t ms);
+/* QPS and / or THREAD grade rules (flags), exits, the full metric view: see the .c */
+enum { ORC_LR_QPS = 1, ORC_LR_THREAD = 2, ORC_LR_THREAD_FIRST = 4 };
+int    orc_local_entry_ex(orc_stat_node *nd, double qps_count, double thread_count, int flags, int acquire,
+                          int prioritized, int64_t t, int64_t *wait);
+void   orc_local_exit(orc_stat_node *nd, int count, int64_t rt, int error, int64_t t);
+void   orc_node_metrics(const orc_stat_node *nd, int64_t t, int64_t *out14);
 int64_t orc_node_waiting(orc_stat_node *nd, int64_t t);                 /* rollingCounterInSecond.waiting() */
 int64_t orc_node_minute_occupied(orc_stat_node *nd, int64_t t);         /* rollingCounterInMinute.occupiedPass() */
 int64_t orc_node_try_occupy_next(orc_stat_node *nd, int64_t t, int acquire, double threshold);
@@ -221,6 +228,13 @@ void orc_lparam_replay(orc_local_engine *e, int64_t n, const int32_t *rule_idx, 
                       const int64_t *ts, const int32_t *vbegin, const int32_t *vcount, const uint64_t *values,
                       int64_t n_values, int8_t *status);
 int  orc_lparam_state(orc_local_engine *e, int32_t idx, uint64_t key, int64_t *last, int64_t *tokens);
+/* THREAD grade rules (grade 0; default 1 = QPS) and exits (kinds[i] == 1: Entry.exit of a passed
+ * entry -> the values' thread counts drop); thread count of a value, -1 when absent. */
+void orc_lparam_set_grades(orc_local_engine *e, const int32_t *grade, int n);
+void orc_lparam_replay_ex(orc_local_engine *e, int64_t n, const int32_t *rule_idx, const int32_t *acquire,
+                          const int64_t *ts, const int32_t *vbegin, const int32_t *vcount, const uint64_t *values,
+                          int64_t n_values, const uint8_t *kinds, int8_t *status);
+int  orc_lparam_thread_count(orc_local_engine *e, int32_t idx, uint64_t key);
 
 /* ---------------- concurrency tokens (ConcurrentClusterFlowChecker) ---------------- */
 /* Mirrors include/sentinel_amd.h's sentinel_concurrent_event_t (kind 0 acquire, 1 release). */

@@ -53,6 +53,14 @@ EXPORTS = [
     "sentinel_param_top_values", "sentinel_param_snapshot_device", "sentinel_flow_window", "sentinel_metric_count",
     "sentinel_reset_metrics", "sentinel_param_table_stats", "sentinel_param_count",
     "sentinel_batcher_request_token_async",
+    "sentinel_set_local_param_grades", "sentinel_submit_local_param_batch_ex", "sentinel_submit_local_param_batch_ex_host",
+    "sentinel_load_local_resources_ex", "sentinel_submit_local_batch", "sentinel_submit_local_batch_host",
+    "sentinel_local_node_metrics", "sentinel_set_statistic_max_rt",
+    "sentinel_shard_of", "sentinel_cluster_create", "sentinel_cluster_destroy", "sentinel_cluster_size",
+    "sentinel_cluster_engine", "sentinel_cluster_set_server_config", "sentinel_cluster_set_namespaces",
+    "sentinel_cluster_set_connected_count", "sentinel_cluster_load_flow_rules", "sentinel_cluster_load_param_rules",
+    "sentinel_cluster_submit_host", "sentinel_cluster_flow_count", "sentinel_cluster_snapshot",
+    "sentinel_cluster_batchers_create", "sentinel_cluster_request_token",
 ]
 
 STATUS_RELEASE_OK = 6
@@ -88,6 +96,15 @@ class ParamRuleC(C.Structure):
 class LocalParamRuleC(C.Structure):
     _fields_ = [("count", C.c_double), ("burst_count", C.c_int64), ("duration_in_sec", C.c_int64),
                 ("hot_begin", C.c_int32), ("hot_n", C.c_int32)]
+
+
+class LocalResourceExC(C.Structure):
+    _fields_ = [("qps_count", C.c_double), ("thread_count", C.c_double), ("flags", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
+LOCAL_QPS, LOCAL_THREAD, LOCAL_THREAD_FIRST = 1, 2, 4
+LOCAL_PRIO, LOCAL_EXIT, LOCAL_ERROR = 1, 2, 4
 
 
 class LocalResourceC(C.Structure):
@@ -184,6 +201,29 @@ def load():
         "sentinel_submit_local_entry_batch_host": (C.c_int, [vp, i64, vp, vp, vp]),
         "sentinel_local_node_stats": (C.c_int, [vp, i32, i64, vp]),
         "sentinel_set_occupy_timeout": (C.c_int, [vp, i32]),
+        "sentinel_set_local_param_grades": (C.c_int, [vp, vp, i32]),
+        "sentinel_submit_local_param_batch_ex": (C.c_int, [vp, i64, vp, vp, vp, i64, vp, vp]),
+        "sentinel_submit_local_param_batch_ex_host": (C.c_int, [vp, i64, vp, vp, vp, i64, vp]),
+        "sentinel_load_local_resources_ex": (C.c_int, [vp, vp, i32, i32, i32]),
+        "sentinel_submit_local_batch": (C.c_int, [vp, i64, vp, vp, vp, vp, vp]),
+        "sentinel_submit_local_batch_host": (C.c_int, [vp, i64, vp, vp, vp, vp]),
+        "sentinel_local_node_metrics": (C.c_int, [vp, i32, i64, vp]),
+        "sentinel_set_statistic_max_rt": (C.c_int, [vp, i64]),
+        "sentinel_shard_of": (i32, [i64, i32]),
+        "sentinel_cluster_create": (C.c_int, [vp, i32, vp, vp]),
+        "sentinel_cluster_destroy": (C.c_int, [vp]),
+        "sentinel_cluster_size": (i32, [vp]),
+        "sentinel_cluster_engine": (C.c_int, [vp, i32, vp]),
+        "sentinel_cluster_set_server_config": (C.c_int, [vp, vp]),
+        "sentinel_cluster_set_namespaces": (C.c_int, [vp, vp, i32]),
+        "sentinel_cluster_set_connected_count": (C.c_int, [vp, i32, i32]),
+        "sentinel_cluster_load_flow_rules": (C.c_int, [vp, vp, i32]),
+        "sentinel_cluster_load_param_rules": (C.c_int, [vp, vp, i32, vp, vp, i32]),
+        "sentinel_cluster_submit_host": (C.c_int, [vp, i64, vp, vp, vp, vp, vp]),
+        "sentinel_cluster_flow_count": (i32, [vp]),
+        "sentinel_cluster_snapshot": (C.c_int, [vp, i64, vp, i64, vp]),
+        "sentinel_cluster_batchers_create": (C.c_int, [vp, i32, i32]),
+        "sentinel_cluster_request_token": (C.c_int, [vp, i64, i32, i32, i64, vp]),
         "sentinel_profile_select": (C.c_int, [vp, C.c_char_p]),
         "sentinel_profile_gate": (C.c_int, [vp, C.c_int]),
         "sentinel_set_flow_path": (C.c_int, [vp, C.c_int]),

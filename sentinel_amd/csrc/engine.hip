@@ -476,7 +476,11 @@ struct sentinel_engine {
     double lres_Is = 1.0;
     int32_t lres_interval = 1000;      // IntervalProperty.INTERVAL of the local nodes
     int32_t occupy_timeout = 500;      // OccupyTimeoutProperty.occupyTimeout (OccupyTimeoutProperty.java:40)
-    DevBuf d_lres_state, d_lres_count, d_lres_w, d_lres_rcp, d_lres_kind;
+    DevBuf d_lres_state, d_lres_count, d_lres_w, d_lres_rcp, d_lres_kind, d_lres_tcount, d_lres_flags;
+    DevBuf w_lslow, io_lrt;
+    DevBuf d_lrule_grade;              // local param rules: 1 QPS, 0 THREAD (sentinel_set_local_param_grades)
+    bool lhas_grade = false;            // local batch: sequential-path marks; host-fed exit response times
+    int64_t lres_max_rt = 5000;        // SentinelConfig.statisticMaxRt (DEFAULT_STATISTIC_MAX_RT)
 
     // concurrency tokens (ConcurrentClusterFlowChecker): nowCalls per flow, token cache in HBM
     DevBuf d_now, d_conc_thr, d_seg1_w, d_seg1_rcp, d_seg1_kind;
@@ -651,7 +655,8 @@ struct sentinel_engine {
         C.CM = CountMin{d_cm.as<uint64_t>(), cm_depth, cm_width, pmax_n, pmode == SENTINEL_PARAM_COUNT_MIN_SHARED};
         C.L = LocalRules{d_lrule_valid.as<uint8_t>(), d_lrule_tok.as<int64_t>(), d_lrule_burst.as<int64_t>(),
                          d_lrule_dur.as<int64_t>(), lhas_hot ? d_lhot_keys.as<unsigned long long>() : nullptr,
-                         lhot_mask, d_lhot_tok.as<int64_t>(), d_lstate.as<int64_t>()};
+                         lhot_mask, d_lhot_tok.as<int64_t>(), d_lstate.as<int64_t>(),
+                         lhas_grade ? d_lrule_grade.as<uint8_t>() : nullptr, nullptr};
         C.vslot = w_vslot.as<uint32_t>();
         return C;
     }
@@ -1371,7 +1376,8 @@ static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const u
 }
 
 static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamEvent *pev, const MultiEvent *mev,
-                         const uint64_t *values, int64_t n_values, uint64_t *out, hipStream_t s);
+                         const uint64_t *values, int64_t n_values, uint64_t *out, hipStream_t s,
+                         const uint8_t *kinds = nullptr);
 
 static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, uint64_t *out, hipStream_t s) {
     if (e->pmode != SENTINEL_PARAM_EXACT) return submit_prules(e, PMODE_CM, n, ev, nullptr, nullptr, 0, out, s);
@@ -1435,7 +1441,8 @@ static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, u
 // count-min counters) and the local token bucket.  Events are single-value (pev) or multi-value
 // (mev + values[0, n_values)).
 static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamEvent *pev, const MultiEvent *mev,
-                         const uint64_t *values, int64_t n_values, uint64_t *out, hipStream_t s) {
+                         const uint64_t *values, int64_t n_values, uint64_t *out, hipStream_t s,
+                         const uint8_t *kinds) {
     if (n <= 0) return 0;
     if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
     int rc = e->ensure_ws(n);
@@ -1461,7 +1468,8 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
         rc = e->param_reserve(nv);            // room for every value of the batch: never FAIL
         if (rc) return rc;
     }
-    const ParamCtx C = e->param_ctx();
+    ParamCtx C = e->param_ctx();
+    C.L.kinds = local ? kinds : nullptr;
     unsigned long long *table = nullptr;
     uint64_t mask = 0;
     if (mode == PMODE_EXACT && R > 0) { table = e->d_ptable.as<unsigned long long>(); mask = e->pcap - 1; }
@@ -1506,18 +1514,21 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
 
 // Host-pointer variant of the per-rule param path: H2D, decide, D2H, synchronous.
 static int submit_prules_host(sentinel_engine_t *e, int mode, int64_t n, const sentinel_param_multi_event_t *ev,
-                              const uint64_t *values, int64_t n_values, sentinel_verdict_t *out) {
+                              const uint64_t *values, int64_t n_values, sentinel_verdict_t *out,
+                              const uint8_t *kinds = nullptr) {
     if (n == 0) return 0;
     hipStream_t s = e->stream;
     int rc = 0;
     rc |= e->io_ev.ensure(n * sizeof(MultiEvent));
     rc |= e->io_vals.ensure(std::max<int64_t>(n_values, 1) * 8);
     rc |= e->io_out.ensure(n * 8);
+    if (kinds) rc |= e->io_fl.ensure(n);
     if (rc) return SENTINEL_E_NOMEM;
     HIP_OK(hipMemcpyAsync(e->io_ev.p, ev, n * sizeof(MultiEvent), hipMemcpyHostToDevice, s));
     if (n_values > 0) HIP_OK(hipMemcpyAsync(e->io_vals.p, values, n_values * 8, hipMemcpyHostToDevice, s));
+    if (kinds) HIP_OK(hipMemcpyAsync(e->io_fl.p, kinds, n, hipMemcpyHostToDevice, s));
     rc = submit_prules(e, mode, n, nullptr, e->io_ev.as<MultiEvent>(), e->io_vals.as<uint64_t>(), n_values,
-                       e->io_out.as<uint64_t>(), s);
+                       e->io_out.as<uint64_t>(), s, kinds ? e->io_fl.as<uint8_t>() : nullptr);
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
@@ -1526,8 +1537,8 @@ static int submit_prules_host(sentinel_engine_t *e, int mode, int64_t n, const s
 
 // Local SphU.entry batches (local_entry.hpp): validation, sort by resource, (resource, epoch of
 // gcd(second bucket, 1000 ms)) segments, one lane per resource, parallel verdicts.
-static int submit_local_entry(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
-                              hipStream_t s) {
+static int submit_local_entry(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, const int64_t *rt,
+                              uint64_t *out, hipStream_t s) {
     if (n <= 0) return 0;
     if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
     int rc = e->ensure_ws(n);
@@ -1537,10 +1548,16 @@ static int submit_local_entry(sentinel_engine_t *e, int64_t n, const Event *ev, 
     const uint32_t rinvalid = ((uint32_t)1 << rbits) - 1;
     uint32_t *fkey = e->w_fkey.as<uint32_t>();
     const int64_t nb = sort_blocks(n);
+    uint8_t *slow = nullptr;
+    if (fl) {
+        rc = e->w_lslow.ensure((size_t)n);
+        if (rc) return rc;
+        slow = e->w_lslow.as<uint8_t>();
+    }
     HIP_OK(hipMemsetAsync(e->w_counters.p, 0, 16, s));
     e->launch("lentry_prep", n, s, [&] {
         k_lentry_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(n, ev, R, out, fkey, rinvalid,
-                                                                        e->w_fhist.as<uint32_t>(), nb);
+                                                                        e->w_fhist.as<uint32_t>(), nb, fl, slow);
     });
     if (R == 0) {
         HIP_OK(hipGetLastError());
@@ -1551,11 +1568,12 @@ static int submit_local_entry(sentinel_engine_t *e, int64_t n, const Event *ev, 
     RT.rcp_w = e->d_lres_rcp.as<double>();
     RT.kind = e->d_lres_kind.as<uint8_t>();
     RT.ncounters = 1;
-    const EventSrc src{ev, nullptr, fl, false};
+    const EventSrc src{ev, nullptr, slow, false};
     e->sort_segments(RT, fkey, e->w_fhist.as<uint32_t>(), n, rbits, src, s);
     const BatchWork W = e->work();
     const LocalNodes L{e->d_lres_state.as<int64_t>(), e->d_lres_count.as<double>(), e->lres_n, e->lres_w, e->lres_Is,
-                       e->lres_interval, e->occupy_timeout};
+                       e->lres_interval, e->occupy_timeout, e->d_lres_tcount.as<double>(),
+                       e->d_lres_flags.as<uint8_t>(), e->lres_max_rt, fl, rt};
     e->launch("lentry_process", n, s, [&] { k_lentry_process<<<grid_for(n), 256, 0, s>>>(L, W, src, out); });
     e->launch("lentry_verdict", n, s, [&] { k_lentry_verdict<<<grid_for(n), 256, 0, s>>>(W, out, n); });
     HIP_OK(hipGetLastError());
@@ -1641,7 +1659,8 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
                       &e->d_lhot_tok, &e->d_ltable, &e->d_lstate, &e->d_now, &e->d_conc_thr, &e->d_seg1_w,
                       &e->d_seg1_rcp, &e->d_seg1_kind, &e->d_tok_keys, &e->d_tok_fid, &e->d_tok_fidx,
                       &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->w_runs, &e->w_pscan, &e->d_lres_state,
-                      &e->d_lres_count, &e->d_lres_w, &e->d_lres_rcp, &e->d_lres_kind})
+                      &e->d_lres_count, &e->d_lres_w, &e->d_lres_rcp, &e->d_lres_kind, &e->d_lres_tcount,
+                      &e->d_lres_flags, &e->w_lslow, &e->io_lrt, &e->d_lrule_grade})
         b->release();
     for (int k = 0; k < 2; ++k) {
         e->st_ev[k].release();
@@ -2424,6 +2443,7 @@ int sentinel_load_local_param_rules(sentinel_engine_t *e, const sentinel_local_p
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(e->stream));
     e->nlrules = n;
+    e->lhas_grade = false;                 // every rule QPS grade until sentinel_set_local_param_grades
     return 0;
 }
 
@@ -2444,6 +2464,40 @@ int sentinel_submit_local_param_batch_host(sentinel_engine_t *e, int64_t n, cons
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
     return submit_prules_host(e, PMODE_LOCAL, n, ev, values, n_values, out);
+}
+
+int sentinel_set_local_param_grades(sentinel_engine_t *e, const int32_t *grades, int32_t n) {
+    if (!e || n < 0 || (n > 0 && !grades)) return fail(SENTINEL_E_INVALID, "bad grades");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    std::vector<uint8_t> gr((size_t)std::max(e->nlrules, 1), 1);
+    for (int32_t i = 0; i < n && i < e->nlrules; ++i) gr[i] = grades[i] == 0 ? 0 : 1;   // FLOW_GRADE_THREAD = 0
+    const int rc = upload(e->d_lrule_grade, gr);
+    if (rc) return rc;
+    e->lhas_grade = true;
+    return 0;
+}
+
+int sentinel_submit_local_param_batch_ex(sentinel_engine_t *e, int64_t n, const sentinel_param_multi_event_t *ev,
+                                         const uint8_t *kinds, const uint64_t *values, int64_t n_values,
+                                         sentinel_verdict_t *out, void *stream) {
+    if (!e || n < 0 || n_values < 0 || (n > 0 && (!ev || !out)) || (n_values > 0 && !values))
+        return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    return submit_prules(e, PMODE_LOCAL, n, nullptr, (const MultiEvent *)ev, values, n_values, (uint64_t *)out,
+                         stream ? (hipStream_t)stream : e->stream, kinds);
+}
+
+int sentinel_submit_local_param_batch_ex_host(sentinel_engine_t *e, int64_t n, const sentinel_param_multi_event_t *ev,
+                                              const uint8_t *kinds, const uint64_t *values, int64_t n_values,
+                                              sentinel_verdict_t *out) {
+    if (!e || n < 0 || n_values < 0 || (n > 0 && (!ev || !out)) || (n_values > 0 && !values))
+        return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    return submit_prules_host(e, PMODE_LOCAL, n, ev, values, n_values, out, kinds);
 }
 
 int sentinel_local_param_state(sentinel_engine_t *e, uint64_t key, int64_t *last_add_ms, int64_t *tokens) {
@@ -2470,8 +2524,8 @@ int sentinel_local_param_state(sentinel_engine_t *e, uint64_t key, int64_t *last
     return 1;
 }
 
-int sentinel_load_local_resources(sentinel_engine_t *e, const sentinel_local_resource_t *res, int32_t n,
-                                  int32_t sample_count, int32_t interval_ms) {
+int sentinel_load_local_resources_ex(sentinel_engine_t *e, const sentinel_local_resource_ex_t *res, int32_t n,
+                                     int32_t sample_count, int32_t interval_ms) {
     if (!e || n < 0 || (n > 0 && !res)) return fail(SENTINEL_E_INVALID, "bad local resources");
     // SampleCountProperty / IntervalProperty validity: positive, INTERVAL % SAMPLE_COUNT == 0
     if (sample_count < 1 || sample_count > LOCAL_NMAX || interval_ms <= 0 || interval_ms % sample_count != 0)
@@ -2482,9 +2536,17 @@ int sentinel_load_local_resources(sentinel_engine_t *e, const sentinel_local_res
     const size_t N = (size_t)std::max(n, 1);
     int32_t w = interval_ms / sample_count, a = w, b = 1000;
     while (b) { const int32_t t = a % b; a = b; b = t; }            // segment length gcd(w, 1000)
-    std::vector<double> count(N, HUGE_VAL);
-    for (int32_t i = 0; i < n; ++i)
-        if (res[i].has_rule && res[i].count >= 0) count[i] = res[i].count;   // invalid rules (count < 0) are dropped
+    std::vector<double> count(N, HUGE_VAL), tcount(N, HUGE_VAL);
+    std::vector<uint8_t> flags(N, 0);
+    for (int32_t i = 0; i < n; ++i) {
+        // FlowRuleUtil.isValidRule: count >= 0 (invalid rules are dropped)
+        uint8_t f = res[i].flags & (LR_QPS | LR_THREAD | LR_THREAD_FIRST);
+        if ((f & LR_QPS) && !(res[i].qps_count >= 0)) f &= (uint8_t)~LR_QPS;
+        if ((f & LR_THREAD) && !(res[i].thread_count >= 0)) f &= (uint8_t)~LR_THREAD;
+        if (f & LR_QPS) count[i] = res[i].qps_count;
+        if (f & LR_THREAD) tcount[i] = res[i].thread_count;
+        flags[i] = f;
+    }
     std::vector<int64_t> st(N * LOCAL_WORDS, 0);
     for (size_t i = 0; i < N; ++i) {
         int64_t *r = st.data() + i * LOCAL_WORDS;
@@ -2494,9 +2556,11 @@ int sentinel_load_local_resources(sentinel_engine_t *e, const sentinel_local_res
     int rc = 0;
     rc |= upload(e->d_lres_state, st);
     rc |= upload(e->d_lres_count, count);
+    rc |= upload(e->d_lres_tcount, tcount);
+    rc |= upload(e->d_lres_flags, flags);
     rc |= upload(e->d_lres_w, std::vector<int32_t>(N, a));
     rc |= upload(e->d_lres_rcp, std::vector<double>(N, 1.0 / (double)a));
-    // KIND_CLUSTER: a prioritized event makes its segment heterogeneous (sequential path)
+    // KIND_CLUSTER: a prioritized entry or an exit makes its segment heterogeneous (sequential path)
     rc |= upload(e->d_lres_kind, std::vector<uint8_t>(N, KIND_CLUSTER));
     if (rc) return rc;
     e->nlres = n;
@@ -2509,12 +2573,65 @@ int sentinel_load_local_resources(sentinel_engine_t *e, const sentinel_local_res
     return 0;
 }
 
+int sentinel_load_local_resources(sentinel_engine_t *e, const sentinel_local_resource_t *res, int32_t n,
+                                  int32_t sample_count, int32_t interval_ms) {
+    if (!e || n < 0 || (n > 0 && !res)) return fail(SENTINEL_E_INVALID, "bad local resources");
+    std::vector<sentinel_local_resource_ex_t> x((size_t)std::max(n, 1));
+    for (int32_t i = 0; i < n; ++i) {
+        x[i].qps_count = res[i].count;
+        x[i].thread_count = 0;
+        x[i].flags = res[i].has_rule ? LR_QPS : 0;
+        x[i].reserved = 0;
+    }
+    return sentinel_load_local_resources_ex(e, x.data(), n, sample_count, interval_ms);
+}
+
+int sentinel_set_statistic_max_rt(sentinel_engine_t *e, int64_t max_rt_ms) {
+    if (!e) return fail(SENTINEL_E_INVALID, "null engine");
+    std::lock_guard<std::mutex> g(e->mu);
+    e->lres_max_rt = max_rt_ms;
+    return 0;
+}
+
+int sentinel_submit_local_batch(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev, const uint8_t *flags,
+                                const int64_t *rt_ms, sentinel_verdict_t *out, void *stream) {
+    if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    return submit_local_entry(e, n, (const Event *)ev, flags, flags ? rt_ms : nullptr, (uint64_t *)out,
+                              stream ? (hipStream_t)stream : e->stream);
+}
+
+int sentinel_submit_local_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev, const uint8_t *flags,
+                                     const int64_t *rt_ms, sentinel_verdict_t *out) {
+    if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    hipStream_t s = e->stream;
+    int rc = 0;
+    rc |= e->io_ev.ensure(n * sizeof(Event));
+    rc |= e->io_out.ensure(n * 8);
+    if (flags) rc |= e->io_fl.ensure(n);
+    if (flags && rt_ms) rc |= e->io_lrt.ensure(n * 8);
+    if (rc) return SENTINEL_E_NOMEM;
+    HIP_OK(hipMemcpyAsync(e->io_ev.p, ev, n * sizeof(Event), hipMemcpyHostToDevice, s));
+    if (flags) HIP_OK(hipMemcpyAsync(e->io_fl.p, flags, n, hipMemcpyHostToDevice, s));
+    if (flags && rt_ms) HIP_OK(hipMemcpyAsync(e->io_lrt.p, rt_ms, n * 8, hipMemcpyHostToDevice, s));
+    rc = submit_local_entry(e, n, e->io_ev.as<Event>(), flags ? e->io_fl.as<uint8_t>() : nullptr,
+                            flags && rt_ms ? e->io_lrt.as<int64_t>() : nullptr, e->io_out.as<uint64_t>(), s);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 8, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    return 0;
+}
+
 int sentinel_submit_local_entry_batch(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev,
                                       const uint8_t *prioritized, sentinel_verdict_t *out, void *stream) {
     if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
-    return submit_local_entry(e, n, (const Event *)ev, prioritized, (uint64_t *)out,
+    return submit_local_entry(e, n, (const Event *)ev, prioritized, nullptr, (uint64_t *)out,
                               stream ? (hipStream_t)stream : e->stream);
 }
 
@@ -2533,7 +2650,7 @@ int sentinel_submit_local_entry_batch_host(sentinel_engine_t *e, int64_t n, cons
     if (rc) return SENTINEL_E_NOMEM;
     HIP_OK(hipMemcpyAsync(e->io_ev.p, ev, n * sizeof(Event), hipMemcpyHostToDevice, s));
     if (prioritized) HIP_OK(hipMemcpyAsync(e->io_fl.p, prioritized, n, hipMemcpyHostToDevice, s));
-    rc = submit_local_entry(e, n, e->io_ev.as<Event>(), prioritized ? e->io_fl.as<uint8_t>() : nullptr,
+    rc = submit_local_entry(e, n, e->io_ev.as<Event>(), prioritized ? e->io_fl.as<uint8_t>() : nullptr, nullptr,
                             e->io_out.as<uint64_t>(), s);
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 8, hipMemcpyDeviceToHost, s));
@@ -2555,8 +2672,8 @@ int sentinel_local_node_stats(sentinel_engine_t *e, int32_t idx, int64_t ts, int
     for (int j = 0; j < e->lres_n; ++j) {
         const int64_t *s = st.data() + LOCAL_SEC_W * j;
         if (s[0] != EPOCH_ABSENT && s[0] > E - e->lres_n && s[0] <= E) {
-            out[0] += s[1];
-            out[1] += s[2];
+            out[0] += s[SC_PASS];
+            out[1] += s[SC_BLOCK];
         }
         const int64_t *b = st.data() + LOCAL_BOR_OFF + LOCAL_BOR_W * j;
         if (b[0] != EPOCH_ABSENT && b[0] * e->lres_w > ts) out[5] += b[1];   // waiting(): future borrows
@@ -2564,11 +2681,45 @@ int sentinel_local_node_stats(sentinel_engine_t *e, int32_t idx, int64_t ts, int
     for (int j = 0; j < LOCAL_MIN_SLOTS; ++j) {
         const int64_t *m = st.data() + LOCAL_MIN_OFF + LOCAL_MIN_W * j;
         if (m[0] != EPOCH_ABSENT && m[0] > E1 - LOCAL_MIN_SLOTS && m[0] <= E1) {
-            out[2] += m[1];
-            out[3] += m[2];
-            out[4] += m[3];
+            out[2] += m[MC_PASS];
+            out[3] += m[MC_BLOCK];
+            out[4] += m[MC_OCC];
         }
     }
+    return 0;
+}
+
+int sentinel_local_node_metrics(sentinel_engine_t *e, int32_t idx, int64_t ts, int64_t *out) {
+    if (!e || !out || ts < 0) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    if (idx < 0 || idx >= e->nlres) return fail(SENTINEL_E_INVALID, "bad resource index");
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    std::vector<int64_t> st(LOCAL_WORDS);
+    HIP_OK(hipMemcpy(st.data(), e->d_lres_state.as<int64_t>() + (int64_t)idx * LOCAL_WORDS, LOCAL_WORDS * 8,
+                     hipMemcpyDeviceToHost));
+    // read-only view of the rolled windows: epochs > E - n (LeapArray.values after currentWindow,
+    // future buckets of a clock that went back included)
+    const int64_t E = ts / e->lres_w, E1 = ts / 1000;
+    for (int k = 0; k < 14; ++k) out[k] = 0;
+    int64_t mrt_s = e->lres_max_rt, mrt_m = e->lres_max_rt;
+    for (int j = 0; j < e->lres_n; ++j) {
+        const int64_t *s = st.data() + LOCAL_SEC_W * j;
+        if (s[0] == EPOCH_ABSENT || s[0] <= E - e->lres_n) continue;
+        const int cols[5] = {SC_PASS, SC_BLOCK, SC_EXC, SC_SUCC, SC_RT};
+        for (int k = 0; k < 5; ++k) out[k] = wrap_add(out[k], s[cols[k]]);
+        mrt_s = std::min(mrt_s, s[SC_MINRT]);
+    }
+    for (int j = 0; j < LOCAL_MIN_SLOTS; ++j) {
+        const int64_t *m = st.data() + LOCAL_MIN_OFF + LOCAL_MIN_W * j;
+        if (m[0] == EPOCH_ABSENT || m[0] <= E1 - LOCAL_MIN_SLOTS) continue;
+        const int cols[6] = {MC_PASS, MC_BLOCK, MC_OCC, MC_EXC, MC_SUCC, MC_RT};
+        for (int k = 0; k < 6; ++k) out[6 + k] = wrap_add(out[6 + k], m[cols[k]]);
+        mrt_m = std::min(mrt_m, m[MC_MINRT]);
+    }
+    out[5] = std::max<int64_t>(1, mrt_s);                 // ArrayMetric.minRt: Math.max(1, rt)
+    out[12] = std::max<int64_t>(1, mrt_m);
+    out[13] = st[LOCAL_THR_OFF];
     return 0;
 }
 
@@ -3138,6 +3289,248 @@ int sentinel_batcher_stats(sentinel_batcher_t *b, int64_t *batches, int64_t *req
     if (batches) *batches = b->batches.load();
     if (requests) *requests = b->requests.load();
     return 0;
+}
+
+}  // extern "C"
+
+// ==================================================================== multi-device engine
+// One engine per entry of device_ids (a device may repeat: several shards on one GPU).  The flowId
+// space is partitioned shard = splitmix64(flowId) mod n: a flow's verdicts depend only
+// on its own window, so the shards never exchange anything on the decision path.  Rule loads are
+// split by shard; a shard whose subset of a namespace is empty while the namespace is not gets one
+// invalid marker rule of that namespace (flowId 0: dropped, but the namespace's raw list stays
+// non-empty), so the putMetricIfAbsent orphan rule sees the whole node's namespace lists.
+struct sentinel_cluster {
+    std::vector<sentinel_engine_t *> eng;
+    std::vector<sentinel_batcher_t *> batchers;
+    std::mutex mu;                                       // one host batch at a time
+    std::vector<std::vector<int64_t>> pos, ids;
+    std::vector<std::vector<sentinel_event_t>> ev;
+    std::vector<std::vector<uint8_t>> fl;
+    std::vector<std::vector<sentinel_verdict_t>> out;
+};
+
+static inline uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+template <class Rule>
+static std::vector<std::vector<Rule>> split_rules(const Rule *rules, int32_t n, int32_t shards) {
+    std::vector<std::vector<Rule>> part((size_t)shards);
+    int32_t max_ns = -1;
+    for (int32_t i = 0; i < n; ++i) {
+        part[(size_t)(splitmix64((uint64_t)rules[i].flow_id) % (uint64_t)shards)].push_back(rules[i]);
+        max_ns = std::max(max_ns, rules[i].namespace_idx);
+    }
+    std::vector<uint8_t> any((size_t)std::max(max_ns + 1, 1), 0);
+    for (int32_t i = 0; i < n; ++i)
+        if (rules[i].namespace_idx >= 0) any[(size_t)rules[i].namespace_idx] = 1;
+    for (int32_t sh = 0; sh < shards; ++sh) {
+        std::vector<uint8_t> mine(any.size(), 0);
+        for (const Rule &r : part[(size_t)sh])
+            if (r.namespace_idx >= 0) mine[(size_t)r.namespace_idx] = 1;
+        for (size_t k = 0; k < any.size(); ++k)
+            if (any[k] && !mine[k]) {
+                Rule m{};
+                m.flow_id = 0;                           // FlowRuleUtil.isValidRule: flowId > 0
+                m.namespace_idx = (int32_t)k;
+                part[(size_t)sh].push_back(m);
+            }
+    }
+    return part;
+}
+
+// run f(shard) on every shard, one host thread each (the shards' devices work concurrently)
+template <class F>
+static int for_shards(sentinel_cluster_t *c, F f) {
+    const size_t n = c->eng.size();
+    if (n == 1) return f(0);
+    std::vector<int> rc(n, 0);
+    std::vector<std::string> err(n);
+    std::vector<std::thread> th;
+    for (size_t i = 0; i < n; ++i)
+        th.emplace_back([&, i] {
+            rc[i] = f((int32_t)i);
+            if (rc[i]) err[i] = g_err;
+        });
+    for (auto &t : th) t.join();
+    for (size_t i = 0; i < n; ++i)
+        if (rc[i]) {
+            g_err = err[i];
+            return rc[i];
+        }
+    return 0;
+}
+
+extern "C" {
+
+int32_t sentinel_shard_of(int64_t flow_id, int32_t n) {
+    return n <= 0 ? -1 : (int32_t)(splitmix64((uint64_t)flow_id) % (uint64_t)n);
+}
+
+int sentinel_cluster_create(const int32_t *device_ids, int32_t n, const sentinel_server_config_t *cfg,
+                            sentinel_cluster_t **out) {
+    if (!device_ids || n <= 0 || !out) return fail(SENTINEL_E_INVALID, "bad device list");
+    auto *c = new sentinel_cluster_t();
+    for (int32_t i = 0; i < n; ++i) {
+        sentinel_engine_t *e = nullptr;
+        const int rc = sentinel_engine_create(device_ids[i], cfg, &e);
+        if (rc) {
+            const std::string msg = g_err;
+            for (auto *x : c->eng) sentinel_engine_destroy(x);
+            delete c;
+            g_err = msg;
+            return rc;
+        }
+        c->eng.push_back(e);
+    }
+    const size_t k = (size_t)n;
+    c->pos.resize(k);
+    c->ids.resize(k);
+    c->ev.resize(k);
+    c->fl.resize(k);
+    c->out.resize(k);
+    *out = c;
+    return 0;
+}
+
+int sentinel_cluster_destroy(sentinel_cluster_t *c) {
+    if (!c) return fail(SENTINEL_E_INVALID, "null cluster");
+    for (auto *b : c->batchers) sentinel_batcher_destroy(b);
+    for (auto *e : c->eng) sentinel_engine_destroy(e);
+    delete c;
+    return 0;
+}
+
+int32_t sentinel_cluster_size(sentinel_cluster_t *c) { return c ? (int32_t)c->eng.size() : 0; }
+
+int sentinel_cluster_engine(sentinel_cluster_t *c, int32_t shard, sentinel_engine_t **out) {
+    if (!c || !out || shard < 0 || shard >= (int32_t)c->eng.size()) return fail(SENTINEL_E_INVALID, "bad shard");
+    *out = c->eng[(size_t)shard];
+    return 0;
+}
+
+int sentinel_cluster_set_server_config(sentinel_cluster_t *c, const sentinel_server_config_t *cfg) {
+    if (!c) return fail(SENTINEL_E_INVALID, "null cluster");
+    return for_shards(c, [&](int32_t i) { return sentinel_set_server_config(c->eng[(size_t)i], cfg); });
+}
+
+int sentinel_cluster_set_namespaces(sentinel_cluster_t *c, const sentinel_namespace_t *ns, int32_t n) {
+    if (!c) return fail(SENTINEL_E_INVALID, "null cluster");
+    return for_shards(c, [&](int32_t i) { return sentinel_set_namespaces(c->eng[(size_t)i], ns, n); });
+}
+
+int sentinel_cluster_set_connected_count(sentinel_cluster_t *c, int32_t namespace_idx, int32_t connected) {
+    if (!c) return fail(SENTINEL_E_INVALID, "null cluster");
+    return for_shards(c, [&](int32_t i) { return sentinel_set_connected_count(c->eng[(size_t)i], namespace_idx, connected); });
+}
+
+int sentinel_cluster_load_flow_rules(sentinel_cluster_t *c, const sentinel_flow_rule_t *rules, int32_t n) {
+    if (!c || n < 0 || (n > 0 && !rules)) return fail(SENTINEL_E_INVALID, "bad rules");
+    std::lock_guard<std::mutex> g(c->mu);
+    const auto part = split_rules(rules, n, (int32_t)c->eng.size());
+    return for_shards(c, [&](int32_t i) {
+        const auto &p = part[(size_t)i];
+        return sentinel_load_flow_rules(c->eng[(size_t)i], p.data(), (int32_t)p.size());
+    });
+}
+
+int sentinel_cluster_load_param_rules(sentinel_cluster_t *c, const sentinel_param_rule_t *rules, int32_t n,
+                                      const uint64_t *hot_keys, const int32_t *hot_counts, int32_t n_hot) {
+    if (!c || n < 0 || (n > 0 && !rules)) return fail(SENTINEL_E_INVALID, "bad rules");
+    std::lock_guard<std::mutex> g(c->mu);
+    const auto part = split_rules(rules, n, (int32_t)c->eng.size());
+    return for_shards(c, [&](int32_t i) {
+        const auto &p = part[(size_t)i];
+        return sentinel_load_param_rules(c->eng[(size_t)i], p.data(), (int32_t)p.size(), hot_keys, hot_counts, n_hot);
+    });
+}
+
+// requestToken for a host batch of flowIds: routed to the owning shards (arrival order kept within
+// each shard: a flow lives on one shard, so its events stay in order), decided concurrently, the
+// verdicts put back at the arrival positions.
+int sentinel_cluster_submit_host(sentinel_cluster_t *c, int64_t n, const int64_t *flow_ids, const int32_t *acquire,
+                                 const int64_t *ts, const uint8_t *flags, sentinel_verdict_t *out) {
+    if (!c || n < 0 || (n > 0 && (!flow_ids || !acquire || !ts || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> g(c->mu);
+    const size_t S = c->eng.size();
+    for (size_t k = 0; k < S; ++k) {
+        c->pos[k].clear();
+        c->ids[k].clear();
+        c->ev[k].clear();
+        c->fl[k].clear();
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        const size_t k = (size_t)(splitmix64((uint64_t)flow_ids[i]) % (uint64_t)S);
+        c->pos[k].push_back(i);
+        c->ids[k].push_back(flow_ids[i]);
+        c->ev[k].push_back(sentinel_event_t{0, acquire[i], ts[i]});
+        c->fl[k].push_back(flags ? flags[i] : (uint8_t)0);
+    }
+    const int rc = for_shards(c, [&](int32_t sh) {
+        const size_t k = (size_t)sh;
+        const int64_t m = (int64_t)c->pos[k].size();
+        c->out[k].resize((size_t)m);
+        if (m == 0) return 0;
+        return submit_flow_ids_host(c->eng[k], m, c->ids[k].data(), c->ev[k].data(), flags ? c->fl[k].data() : nullptr,
+                                    c->out[k].data());
+    });
+    if (rc) return rc;
+    for (size_t k = 0; k < S; ++k)
+        for (size_t j = 0; j < c->pos[k].size(); ++j) out[c->pos[k][j]] = c->out[k][j];
+    return 0;
+}
+
+// Snapshot of every shard's flows at ts, shard after shard (the node-wide ClusterMetricNode list);
+// *n_out = the number of records (cap >= sentinel_cluster_flow_count).
+int32_t sentinel_cluster_flow_count(sentinel_cluster_t *c) {
+    if (!c) return 0;
+    int32_t t = 0;
+    for (auto *e : c->eng) t += sentinel_flow_count(e);
+    return t;
+}
+
+int sentinel_cluster_snapshot(sentinel_cluster_t *c, int64_t ts, sentinel_flow_snapshot_t *out, int64_t cap,
+                              int64_t *n_out) {
+    if (!c || !out || !n_out) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(c->mu);
+    std::vector<int64_t> off(c->eng.size() + 1, 0);
+    for (size_t k = 0; k < c->eng.size(); ++k) off[k + 1] = off[k] + sentinel_flow_count(c->eng[k]);
+    if (off.back() > cap) return fail(SENTINEL_E_INVALID, "snapshot buffer too small");
+    const int rc = for_shards(c, [&](int32_t sh) { return sentinel_snapshot(c->eng[(size_t)sh], ts, out + off[(size_t)sh]); });
+    if (rc) return rc;
+    *n_out = off.back();
+    return 0;
+}
+
+// The concurrent front door over every shard: one batcher (dispatcher thread) per engine; a call is
+// routed to its flow's shard.
+int sentinel_cluster_batchers_create(sentinel_cluster_t *c, int32_t max_batch, int32_t max_wait_us) {
+    if (!c) return fail(SENTINEL_E_INVALID, "null cluster");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->batchers.empty()) return fail(SENTINEL_E_STATE, "batchers exist");
+    for (auto *e : c->eng) {
+        sentinel_batcher_t *b = nullptr;
+        const int rc = sentinel_batcher_create(e, max_batch, max_wait_us, &b);
+        if (rc) {
+            for (auto *x : c->batchers) sentinel_batcher_destroy(x);
+            c->batchers.clear();
+            return rc;
+        }
+        c->batchers.push_back(b);
+    }
+    return 0;
+}
+
+int sentinel_cluster_request_token(sentinel_cluster_t *c, int64_t flow_id, int32_t acquire_count, int32_t prioritized,
+                                   int64_t ts, sentinel_token_result_t *out) {
+    if (!c || c->batchers.empty()) return fail(SENTINEL_E_STATE, "no batchers (sentinel_cluster_batchers_create)");
+    const size_t k = (size_t)(splitmix64((uint64_t)flow_id) % (uint64_t)c->batchers.size());
+    return sentinel_batcher_request_token(c->batchers[k], flow_id, acquire_count, prioritized, ts, out);
 }
 
 }  // extern "C"

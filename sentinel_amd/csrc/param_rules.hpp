@@ -95,7 +95,9 @@ struct LocalRules {
     const unsigned long long *hot_keys;
     uint64_t hot_mask;
     const int64_t *hot_tokens;
-    int64_t *state;           // per slot {lastAddTokenTime, tokens}
+    int64_t *state;           // per slot {lastAddTokenTime, tokens}; THREAD grade: {-, thread count}
+    const uint8_t *grade;     // per rule: 1 QPS (token bucket), 0 THREAD; null: all QPS
+    const uint8_t *kinds;     // per event: 1 = Entry.exit (thread counts drop), else a check; null: checks
 };
 
 struct ParamCtx {
@@ -335,6 +337,39 @@ __device__ inline uint64_t local_check(const ParamCtx &C, uint32_t rule, int64_t
     return pack_verdict(ST_OK, 0, 0);
 }
 
+// THREAD grade (PFC:112-122): each value passes iff ++threadCount <= threshold (hot-item count,
+// else (long) rule.count), threadCount = ParameterMetric.getThreadCount (ParameterMetric.java:241-249,
+// absent 0).  The check only reads; a passing check then adds one per value, as the entry callback
+// does (ParamFlowStatisticEntryCallback -> ParameterMetric.addThreadCount, ParameterMetric.java:184-239;
+// AtomicInteger: 32-bit).
+__device__ inline uint64_t thread_check(const ParamCtx &C, uint32_t rule, const ValueSrc &vs, int32_t b, int32_t cnt) {
+    for (int32_t q = 0; q < cnt; ++q) {
+        const uint64_t key = vs.value((int64_t)b + q);
+        const int64_t h = slot_find(C.L.hot_keys, C.L.hot_mask, key);
+        const int64_t thr = h >= 0 ? C.L.hot_tokens[h] : C.L.tokens[rule];
+        const int64_t c = C.L.state[2 * (int64_t)C.vslot[b + q] + 1];
+        const int64_t cur = c == LOCAL_ABSENT ? 0 : c;
+        if (!(cur + 1 <= thr)) return pack_verdict(ST_BLOCKED, 0, 0);
+    }
+    for (int32_t q = 0; q < cnt; ++q) {
+        int64_t *c = C.L.state + 2 * (int64_t)C.vslot[b + q] + 1;
+        *c = *c == LOCAL_ABSENT ? 1 : (int64_t)(int32_t)((uint32_t)*c + 1u);
+    }
+    return pack_verdict(ST_OK, 0, 0);
+}
+
+// Entry.exit -> ParamFlowStatisticExitCallback -> ParameterMetric.decreaseThreadCount
+// (ParameterMetric.java:125-181): an absent value gets a 0 entry (putIfAbsent), a present one is
+// decremented and removed at <= 0.
+__device__ inline void thread_exit(const ParamCtx &C, int32_t b, int32_t cnt) {
+    for (int32_t q = 0; q < cnt; ++q) {
+        int64_t *c = C.L.state + 2 * (int64_t)C.vslot[b + q] + 1;
+        if (*c == LOCAL_ABSENT) { *c = 0; continue; }
+        const int32_t v = (int32_t)((uint32_t)*c - 1u);
+        *c = v <= 0 ? LOCAL_ABSENT : (int64_t)v;
+    }
+}
+
 // One lane per rule: walks the rule's sorted (arrival-ordered) events through its segments.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_prule_process(ParamCtx C, BatchWork W, const ParamEvent *__restrict__ ev,
@@ -354,7 +389,17 @@ __global__ __launch_bounds__(256) void k_prule_process(ParamCtx C, BatchWork W, 
             const int32_t b = vs.begin(seq);
             const int32_t cnt = vs.count(seq);
             uint64_t v;
-            if (MODE == PMODE_LOCAL) v = local_check(C, rule, e.ts, e.acquire, vs, b, cnt);
+            if (MODE == PMODE_LOCAL) {
+                const bool thread_grade = C.L.grade && C.L.grade[rule] == 0;
+                if (C.L.kinds && C.L.kinds[seq] == 1) {         // exit
+                    if (thread_grade) thread_exit(C, b, cnt);
+                    v = pack_verdict(ST_OK, 0, 0);
+                } else if (thread_grade) {
+                    v = thread_check(C, rule, vs, b, cnt);
+                } else {
+                    v = local_check(C, rule, e.ts, e.acquire, vs, b, cnt);
+                }
+            }
             else if (MODE == PMODE_CM) v = cm_check(C, rule, E, e.acquire, vs, b, cnt);
             else v = exact_check(C, E, e.acquire, b, cnt);
             out[seq] = v;

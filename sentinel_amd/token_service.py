@@ -446,6 +446,22 @@ class GpuTokenService:
                                                              len(vals), _p(out)), "submit_local_param_batch_host")
         return out["status"].astype(np.int8)
 
+    def set_local_param_grades(self, grades):
+        """ParamFlowRule.grade per loaded local rule: 1 QPS (default), 0 THREAD."""
+        g = np.ascontiguousarray(grades, dtype=np.int32)
+        check(self._L.sentinel_set_local_param_grades(self._h, _p(g), len(g)), "set_local_param_grades")
+
+    def submit_local_param_batch_ex_host(self, rule_idx, acquire, ts, value_begin, value_count, values, kinds=None):
+        """As submit_local_param_batch_host, kinds[i] == 1 marking Entry.exit events (thread counts drop)."""
+        ev = self.pack_multi_events(rule_idx, acquire, ts, value_begin, value_count)
+        vals = np.ascontiguousarray(values, dtype=np.uint64)
+        k = None if kinds is None else np.ascontiguousarray(kinds, dtype=np.uint8)
+        out = np.empty(len(ev), dtype=_lib.VERDICT_DTYPE)
+        check(self._L.sentinel_submit_local_param_batch_ex_host(self._h, len(ev), _p(ev), _p(k),
+                                                                _p(vals) if len(vals) else None, len(vals), _p(out)),
+              "submit_local_param_batch_ex_host")
+        return out["status"].astype(np.int8)
+
     def local_param_state(self, key: int):
         last, tok = C.c_int64(), C.c_int64()
         rc = self._L.sentinel_local_param_state(self._h, int(key), C.byref(last), C.byref(tok))
@@ -462,6 +478,42 @@ class GpuTokenService:
             arr[i] = _lib.LocalResourceC(0.0 if c is None else float(c), 0 if c is None else 1, 0)
         check(self._L.sentinel_load_local_resources(self._h, arr, len(counts), int(sample_count), int(interval_ms)),
               "load_local_resources")
+
+    def load_local_resources_ex(self, qps_counts, thread_counts, thread_first=None, sample_count: int = 2,
+                                interval_ms: int = 1000):
+        """Resources with a QPS and / or a THREAD grade rule (None: no rule of that grade);
+        thread_first[i]: the THREAD rule is checked before the QPS one."""
+        n = len(qps_counts)
+        arr = (_lib.LocalResourceExC * max(n, 1))()
+        for i in range(n):
+            q, t = qps_counts[i], thread_counts[i]
+            f = (0 if q is None else _lib.LOCAL_QPS) | (0 if t is None else _lib.LOCAL_THREAD)
+            if thread_first is not None and thread_first[i]:
+                f |= _lib.LOCAL_THREAD_FIRST
+            arr[i] = _lib.LocalResourceExC(0.0 if q is None else float(q), 0.0 if t is None else float(t), f, 0)
+        check(self._L.sentinel_load_local_resources_ex(self._h, arr, n, int(sample_count), int(interval_ms)),
+              "load_local_resources_ex")
+
+    def submit_local_batch_host(self, resource_idx, acquire, ts, flags=None, rt=None):
+        """Entries and exits (flags: LOCAL_PRIO / LOCAL_EXIT / LOCAL_ERROR; rt: exit response times)
+        -> (status, waitInMs)."""
+        ev = self.pack_events(resource_idx, acquire, ts)
+        fl = None if flags is None else np.ascontiguousarray(flags, dtype=np.uint8)
+        r = None if rt is None else np.ascontiguousarray(rt, dtype=np.int64)
+        out = np.empty(len(ev), dtype=_lib.VERDICT_DTYPE)
+        check(self._L.sentinel_submit_local_batch_host(self._h, len(ev), _p(ev), _p(fl), _p(r), _p(out)),
+              "submit_local_batch_host")
+        return out["status"].astype(np.int8), out["wait_in_ms"].astype(np.int64)
+
+    def local_node_metrics(self, resource_idx: int, ts: int) -> np.ndarray:
+        """[second PASS, BLOCK, EXCEPTION, SUCCESS, RT, minRt, minute PASS, BLOCK, OCCUPIED_PASS,
+        EXCEPTION, SUCCESS, RT, minRt, curThreadNum] of the resource's node at ts (read-only)."""
+        out = np.zeros(14, dtype=np.int64)
+        check(self._L.sentinel_local_node_metrics(self._h, int(resource_idx), int(ts), _p(out)), "local_node_metrics")
+        return out
+
+    def set_statistic_max_rt(self, ms: int):
+        check(self._L.sentinel_set_statistic_max_rt(self._h, int(ms)), "set_statistic_max_rt")
 
     def submit_local_entry_batch_host(self, resource_idx, acquire, ts, prioritized=None, with_wait=False):
         """SphU.entry (SphU.entryWithPriority where `prioritized`) for a batch -> status array (OK =
@@ -554,6 +606,90 @@ class GpuTokenService:
         check(self._L.sentinel_snapshot_device(self._h, int(ts), C.c_void_p(out_tensor.data_ptr()),
                                                None if s is None else C.c_void_p(s)), "snapshot_device")
         return out_tensor
+
+
+class GpuTokenCluster:
+    """One TokenService over several engines of one node (sentinel_cluster_*): the flowId space
+    partitioned shard = splitmix64(flowId) mod n, one engine per entry of device_ids (a device may
+    repeat).  Rule tables are split by shard, config is broadcast, host batches are routed and
+    decided concurrently, verdicts come back at the arrival positions."""
+
+    def __init__(self, device_ids: Sequence[int], exceed_count: float = 1.0, max_occupy_ratio: float = 1.0):
+        self._L = _lib.load()
+        self._h = C.c_void_p()
+        ids = np.ascontiguousarray(device_ids, dtype=np.int32)
+        cfg = _lib.ServerConfig(exceed_count, max_occupy_ratio)
+        check(self._L.sentinel_cluster_create(_p(ids), len(ids), C.byref(cfg), C.byref(self._h)), "cluster_create")
+        _LIVE_ENGINES.add(self)
+        self.n = len(ids)
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._L.sentinel_cluster_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def shard_of(self, flow_id: int) -> int:
+        return int(self._L.sentinel_shard_of(int(flow_id), self.n))
+
+    def set_namespaces(self, namespaces: Sequence[ServerNamespace]):
+        arr = (_lib.Namespace * max(len(namespaces), 1))()
+        for i, ns in enumerate(namespaces):
+            arr[i] = _lib.Namespace(int(ns.connected_count), int(bool(ns.has_limiter)), float(ns.max_allowed_qps))
+        check(self._L.sentinel_cluster_set_namespaces(self._h, arr, len(namespaces)), "cluster_set_namespaces")
+
+    def load_rules_array(self, flow_ids, counts, threshold_type=1, sample_count=10, window_interval_ms=1000,
+                         namespace=0, checker=0):
+        n = len(flow_ids)
+        rec = np.zeros(n, dtype=[("flow_id", "<i8"), ("count", "<f8"), ("threshold_type", "<i4"),
+                                 ("sample_count", "<i4"), ("window_interval_ms", "<i4"),
+                                 ("namespace_idx", "<i4"), ("checker", "<i4"), ("reserved", "<i4")])
+        rec["flow_id"] = flow_ids
+        rec["count"] = counts
+        rec["threshold_type"] = threshold_type
+        rec["sample_count"] = sample_count
+        rec["window_interval_ms"] = window_interval_ms
+        rec["namespace_idx"] = namespace
+        rec["checker"] = checker
+        check(self._L.sentinel_cluster_load_flow_rules(self._h, C.c_void_p(rec.ctypes.data), n), "cluster_load_flow_rules")
+
+    def flow_count(self) -> int:
+        return int(self._L.sentinel_cluster_flow_count(self._h))
+
+    def submit_host(self, flow_ids, acquire, ts, flags=None):
+        """requestToken per (flowId, acquire, ts[, prioritized flag]) -> (status, remaining, waitInMs)."""
+        ids = np.ascontiguousarray(flow_ids, dtype=np.int64)
+        a = np.ascontiguousarray(acquire, dtype=np.int32)
+        t = np.ascontiguousarray(ts, dtype=np.int64)
+        fl = None if flags is None else np.ascontiguousarray(flags, dtype=np.uint8)
+        out = np.empty(len(ids), dtype=_lib.VERDICT_DTYPE)
+        check(self._L.sentinel_cluster_submit_host(self._h, len(ids), _p(ids), _p(a), _p(t), _p(fl), _p(out)),
+              "cluster_submit_host")
+        return out["status"].astype(np.int8), out["remaining"].copy(), out["wait_in_ms"].astype(np.int32)
+
+    def snapshot(self, ts: int) -> np.ndarray:
+        n = self.flow_count()
+        out = np.zeros(max(n, 1), dtype=[("flow_id", "<i8"), ("pass_qps", "<f8"), ("block_qps", "<f8")])
+        got = C.c_int64()
+        check(self._L.sentinel_cluster_snapshot(self._h, int(ts), C.c_void_p(out.ctypes.data), len(out), C.byref(got)),
+              "cluster_snapshot")
+        return out[:got.value]
+
+    def start_batchers(self, max_batch: int = 4096, max_wait_us: int = 50):
+        check(self._L.sentinel_cluster_batchers_create(self._h, int(max_batch), int(max_wait_us)), "cluster_batchers_create")
+
+    def request_token(self, rule_id, acquire_count, prioritized=False, ts=None) -> TokenResult:
+        out = _lib.TokenResultC()
+        fid = 0 if rule_id is None else int(rule_id)
+        check(self._L.sentinel_cluster_request_token(self._h, fid, int(acquire_count), int(bool(prioritized)),
+                                                     _now_ms() if ts is None else int(ts), C.byref(out)),
+              "cluster_request_token")
+        return TokenResult(out.status, out.remaining, out.wait_in_ms)
 
 
 class TokenBatcher:
