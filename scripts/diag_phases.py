@@ -27,17 +27,26 @@ for s in range(4):
     idx = torch.randint(0, F, (N,), dtype=torch.int32, device=dev, generator=g)
     base = torch.arange(s * N, (s + 1) * N, device=dev, dtype=torch.float64)
     ts = (T.T0_ALIGNED + torch.floor(base * (1000.0 / rate))).to(torch.int64)
-    svc.submit_flow_batch(device_events(idx, torch.ones(N, dtype=torch.int32, device=dev), ts), verdicts=out)
+    evb = device_events(idx, torch.ones(N, dtype=torch.int32, device=dev), ts)
+    torch.cuda.synchronize()          # the events are made on torch's stream, decided on the engine's
+    svc.submit_flow_batch(evb, verdicts=out)
     svc.synchronize()
 nb = 16 * ((977 + 7) // 8)
-buf = (C.c_ulonglong * (4096 * 5))()
+buf = (C.c_ulonglong * (4096 * 12))()
 assert svc._L.sentinel_diag_phases(buf, 4096) == 0
-a = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 5)[:nb, :4].astype(np.int64)
+full = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 12)[:nb].astype(np.int64)
+print("sequential segments per workgroup (all batches):", full[:, 6].mean(), " heterogeneous:", full[:, 7].mean(),
+      " slow because prioritized:", full[:, 8].mean(), " occupy pending:", full[:, 9].mean(),
+      " newer slot:", full[:, 10].mean())
+a = full[:, :6]
 a = a[(a[:, 0] > 0) & (a[:, 3] > 0)]
 us = 0.01  # wall_clock64 = 100 MHz
 t0 = a[:, 0].min()
 print("span us", (a[:, 3].max() - t0) * us)
-for name, i, j in (("hist+scan", 0, 1), ("sort", 1, 2), ("decide", 2, 3), ("total", 0, 3)):
+phases = [("hist+scan", 0, 1), ("sort", 1, 2), ("decide", 2, 3), ("total", 0, 3)]
+if (a[:, 4] > 0).all() and (a[:, 5] > 0).all():     # cooperative halves: mark / walk / sweep
+    phases += [("  mark", 2, 4), ("  walk", 4, 5), ("  sweep", 5, 3)]
+for name, i, j in phases:
     d = (a[:, j] - a[:, i]) * us
     print(f"{name:10s} mean {d.mean():7.2f} us  p50 {np.median(d):7.2f}  max {d.max():7.2f}")
 st = (a[:, 0] - t0) * us

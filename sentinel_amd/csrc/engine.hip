@@ -1715,7 +1715,7 @@ int sentinel_profile_select(sentinel_engine_t *e, const char *kernel) {
 
 #ifdef SENTINEL_DIAG_PHASES
 int sentinel_diag_phases(unsigned long long *out, int n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), (size_t)n * 5 * 8) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), (size_t)n * 12 * 8) == hipSuccess ? 0 : -1;
 }
 #endif
 

@@ -293,6 +293,15 @@ __device__ inline uint64_t run_verdict(double thr, double I_s, int64_t s0, int32
     return pack_verdict(ST_OK, java_d2i((thr - div_interval(x, I_s)) - (double)a), 0);
 }
 
+#ifdef SENTINEL_DIAG_PHASES     // cost diagnostic: wall-clock stamps per workgroup and phase
+__device__ unsigned long long g_phase[4096][12];
+#define PF_STAMP(i) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_phase[blockIdx.x][i] = wall_clock64(); } while (0)
+#define PF_COUNT(i) do { if (blockIdx.x < 4096) atomicAdd(&g_phase[blockIdx.x][i], 1ull); } while (0)
+#else
+#define PF_STAMP(i) do { } while (0)
+#define PF_COUNT(i) do { } while (0)
+#endif
+
 template <int NMAX>
 struct FlowWindow {
     KeyState ks;
@@ -394,12 +403,26 @@ struct FlowWindow {
         bool s = het || occ_pending;
 #pragma unroll
         for (int j = 0; j < NMAX; ++j) s |= (ep[j] != EPOCH_ABSENT && ep[j] > E);
+#ifdef SENTINEL_DIAG_PHASES
+        if (het) PF_COUNT(8);
+        if (occ_pending) PF_COUNT(9);
+        if (s && !het && !occ_pending) {
+            PF_COUNT(10);
+            if (atomicAdd(&g_phase[4095][11], 1ull) < 6) {
+                printf("newer: blk %u thr %u E %lld nsc %d w %d E0 %lld r0 %d ep:", blockIdx.x, threadIdx.x, (long long)E, nsc,
+                       w, (long long)E0, r0);
+                for (int j = 0; j < NMAX; ++j) printf(" %lld", (long long)ep[j]);
+                printf("\n");
+            }
+        }
+#endif
         return s;
     }
 
     // the sequential path over sorted positions [q, q2) of `vals`
     __device__ inline void sequential(const KeyTable &T, uint32_t key, int64_t E, const uint64_t *vals, uint32_t q,
                                       uint32_t q2, const EventSrc &src, const Verdicts &V) {
+        PF_COUNT(6);
         flush();
         for (uint32_t i = q; i < q2; ++i) {
             const uint32_t seq = (uint32_t)vals[i] & SEQ_MASK;
@@ -495,6 +518,7 @@ struct FlowWindow {
     // the whole heterogeneous segment [q, q2) by this lane (het_walk on the rolled window)
     __device__ inline void hetero(int64_t E, const uint64_t *vals, uint32_t q, uint32_t q2, const EventSrc &src,
                                   const Verdicts &V, int64_t T0) {
+        PF_COUNT(7);
         bool fresh;
         const int64_t s0 = het_begin(E, fresh);
         const HetSums h = het_walk<2>(          // (few registers: this runs inside the lane walkers)
@@ -1246,6 +1270,10 @@ constexpr int PH_MAX_LONG = PH_CAP / (LONG_RUN + 1) + 1;
 #define SENTINEL_PH_SMALL_RUN 64
 #endif
 constexpr uint32_t PH_SMALL_RUN = SENTINEL_PH_SMALL_RUN;   // longest run sorted by its own thread
+#ifndef SENTINEL_PH_BALLOT_FIRST_HB
+#define SENTINEL_PH_BALLOT_FIRST_HB 6
+#endif
+constexpr int PH_BALLOT_FIRST_HB = SENTINEL_PH_BALLOT_FIRST_HB;   // halves of <= 2^this flows rank by ballots only
 // Cooperative verdicts: with at most 2^PH_COOP_HB flows per half (flow tables below 2^19 flows, e.g.
 // a rank's shard of 1M flowIds at N >= 2), lanes own several events each; the owner lane of a
 // single-segment run only computes {S0, K} and all 512 lanes then write the half's verdicts from LDS,
@@ -1271,12 +1299,6 @@ __device__ inline void half_of_block(uint32_t b, uint32_t &p, uint32_t &h) {
     h = (b >> 3) & 1u;
 }
 
-#ifdef SENTINEL_DIAG_PHASES     // cost diagnostic: wall-clock stamps per workgroup and phase
-__device__ unsigned long long g_phase[4096][5];
-#define PF_STAMP(i) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_phase[blockIdx.x][i] = wall_clock64(); } while (0)
-#else
-#define PF_STAMP(i) do { } while (0)
-#endif
 
 template <int NMAX, bool COOP>
 __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
@@ -1344,28 +1366,75 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
         const uint32_t k = (uint32_t)(v >> VAL_KEY_SHIFT);
         return (v != ~0ull && (k >> hb) == h) ? (k & hmask) : 0xFFFFFFFFu;
     };
+    // halves of <= 64 flows (runs of ~64+ events, N = 8 rank shards): the stable ballot ranking from
+    // the start, over wave-contiguous positions -- its per-wave counts give the per-flow counts too,
+    // so there is no counting pass and no second load of the range
+    const bool ballot_first = COOP && hb <= PH_BALLOT_FIRST_HB;   // block-uniform
 #pragma unroll
     for (int j = 0; j < PH_ITEMS; ++j) {
-        const uint32_t q = j * PH_THREADS + t;
+        const uint32_t q = ballot_first ? b0 + j * WAVE + lane : j * PH_THREADS + t;
         val[j] = q < size ? pval[pstart + q] : ~0ull;
     }
     base[t] = 0;
     if (t == 0) { s_nlong = 0; s_cmax = 0; }
+    if (ballot_first) {
+        uint32_t *z = reinterpret_cast<uint32_t *>(&cnt[0][0]);
+        for (int d = t; d < PH_WAVES * PH_BINS / 2; d += PH_THREADS) z[d] = 0;
+    }
     __syncthreads();
     const uint32_t key = (p << lb) | (h << hb) | t;
     // rule fields in flight during the sort: loaded unconditionally (a clamped key for lanes without a
     // flow, never used) so no branch join makes the compiler wait for them before the count phase
     FlowWindow<NMAX> fw;
     fw.load_rule(T, min(key, (uint32_t)nflows - 1u));
+    uint32_t c, start, total;
+    if (ballot_first) {
+        uint32_t rank[PH_ITEMS];
+#pragma unroll
+        for (int j = 0; j < PH_ITEMS; ++j) {
+            const uint32_t kj = local(val[j]);
+            const bool valid = kj != 0xFFFFFFFFu;
+            const uint32_t d = kj & hmask;
+            const uint64_t peers = match_peers<PART_MAX_BITS>(d, valid, hb);
+            uint32_t r = 0;
+            if (valid) r = cnt[wave][d] + mask_rank(peers);
+            __builtin_amdgcn_wave_barrier();
+            if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane) cnt[wave][d] += (uint16_t)__popcll(peers);
+            __builtin_amdgcn_wave_barrier();
+            rank[j] = r;
+        }
+        __syncthreads();
+        uint32_t run = 0;
+#pragma unroll
+        for (int w = 0; w < PH_WAVES; ++w) {
+            const uint32_t x = cnt[w][t];
+            cnt[w][t] = (uint16_t)run;
+            run += x;
+        }
+        c = run;                                          // this thread's flow: events in the half
+        start = block_exclusive_scan(c, waves_tot, &total);
+        if (total > PH_CAP) {                             // block-uniform: the half does not fit in LDS
+            if (t == 0) big[atomicAdd(nbig, 1u)] = (p << 1) | h;
+            return;
+        }
+        base[t] = start;
+        __syncthreads();
+        PF_STAMP(1);
+#pragma unroll
+        for (int j = 0; j < PH_ITEMS; ++j) {
+            const uint32_t kj = local(val[j]);
+            if (kj == 0xFFFFFFFFu) continue;
+            sv[base[kj] + cnt[wave][kj] + rank[j]] = val[j];
+        }
+    } else {
 #pragma unroll
     for (int j = 0; j < PH_ITEMS; ++j) {
         const uint32_t kj = local(val[j]);
         if (kj != 0xFFFFFFFFu) atomicAdd(&base[kj], 1u);
     }
     __syncthreads();
-    const uint32_t c = base[t];                           // this thread's flow: events in the half
-    uint32_t total;
-    const uint32_t start = block_exclusive_scan(c, waves_tot, &total);
+    c = base[t];                                          // this thread's flow: events in the half
+    start = block_exclusive_scan(c, waves_tot, &total);
     if (total > PH_CAP) {                                 // block-uniform: the half does not fit in LDS
         if (t == 0) big[atomicAdd(nbig, 1u)] = (p << 1) | h;
         return;
@@ -1438,6 +1507,7 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
             sv[base[kj] + cnt[wave][kj] + rank[j]] = val[j];
         }
     }
+    }
     __syncthreads();
     PF_STAMP(2);
     // 3. decide.  Hot runs go to k_part_long from HBM: the half's region of gsval is its own
@@ -1494,6 +1564,7 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
             }
             __syncthreads();
         }
+        PF_STAMP(4);
 #else
         const bool bits = false;
         const uint32_t *segb = nullptr, *hetb = nullptr, *prib = nullptr;
@@ -1529,6 +1600,7 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
             c_pos[t] = (uint64_t)start | ((uint64_t)len1 << 16) | ((uint64_t)len12 << 32);
         }
         __syncthreads();
+        PF_STAMP(5);
         // every lane: positions t, t + 512, ... of the half's sorted events (flow key in the value)
         for (uint32_t i = t; i < total; i += PH_THREADS) {
             const uint64_t v = sv[i];
