@@ -1271,7 +1271,7 @@ constexpr int PH_MAX_LONG = PH_CAP / (LONG_RUN + 1) + 1;
 #endif
 constexpr uint32_t PH_SMALL_RUN = SENTINEL_PH_SMALL_RUN;   // longest run sorted by its own thread
 #ifndef SENTINEL_PH_BALLOT_FIRST_HB
-#define SENTINEL_PH_BALLOT_FIRST_HB 6
+#define SENTINEL_PH_BALLOT_FIRST_HB 8
 #endif
 constexpr int PH_BALLOT_FIRST_HB = SENTINEL_PH_BALLOT_FIRST_HB;   // halves of <= 2^this flows rank by ballots only
 // Cooperative verdicts: with at most 2^PH_COOP_HB flows per half (flow tables below 2^19 flows, e.g.
@@ -1366,10 +1366,11 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
         const uint32_t k = (uint32_t)(v >> VAL_KEY_SHIFT);
         return (v != ~0ull && (k >> hb) == h) ? (k & hmask) : 0xFFFFFFFFu;
     };
-    // halves of <= 64 flows (runs of ~64+ events, N = 8 rank shards): the stable ballot ranking from
-    // the start, over wave-contiguous positions -- its per-wave counts give the per-flow counts too,
-    // so there is no counting pass and no second load of the range
-    const bool ballot_first = COOP && hb <= PH_BALLOT_FIRST_HB;   // block-uniform
+    // halves of <= 256 flows (runs of ~17+ events: the N >= 2 rank shards): the stable ballot ranking
+    // from the start, over wave-contiguous positions -- its per-wave counts give the per-flow counts
+    // too, so there is no counting pass and no second load of the range (measured: 500k / 250k / 125k
+    // flows 21.9 / 18.9 / 19.9 -> 24.4 / 24.3 / 24.5e9 decisions/s)
+    const bool ballot_first = hb <= PH_BALLOT_FIRST_HB;          // block-uniform
 #pragma unroll
     for (int j = 0; j < PH_ITEMS; ++j) {
         const uint32_t q = ballot_first ? b0 + j * WAVE + lane : j * PH_THREADS + t;
