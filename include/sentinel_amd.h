@@ -179,6 +179,11 @@ typedef struct {
 
 /* DEVICE pointers; flags (bit0 = prioritized) may be NULL; `stream` is a hipStream_t (NULL = the
  * engine's stream).  Asynchronous. */
+/* Several device-resident batches decided in order on `stream` under one engine lock (one call for a
+ * batcher's queue of device batches); verdicts and counters equal submitting them one by one. */
+int  sentinel_submit_flow_batches(sentinel_engine_t *eng, int32_t n_batches, const int64_t *n,
+                                  const sentinel_event_t *const *events, const uint8_t *const *flags,
+                                  sentinel_verdict_t *const *verdicts, void *stream);
 int  sentinel_submit_flow_batch(sentinel_engine_t *eng, int64_t n, const sentinel_event_t *events,
                                 const uint8_t *flags, sentinel_verdict_t *verdicts, void *stream);
 /* Same with HOST pointers (pinned or pageable): H2D, decide, D2H, synchronous. */
@@ -518,6 +523,8 @@ int  sentinel_set_flow_path(sentinel_engine_t *eng, int path);
 /* Gate the timing of following launches on (1) or off (0) without collecting or clearing what was
  * timed so far (no host synchronisation: callable between the batches of a timed loop). */
 int  sentinel_profile_gate(sentinel_engine_t *eng, int on);
+/* With profiling on, time only every k-th launch of the selected kernel (default 1). */
+int  sentinel_profile_every(sentinel_engine_t *eng, int every);
 int  sentinel_profile_read(sentinel_engine_t *eng, int max, char *names32, double *total_ms,
                            int64_t *calls, int64_t *units);
 

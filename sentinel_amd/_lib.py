@@ -52,7 +52,7 @@ EXPORTS = [
     "sentinel_local_node_stats", "sentinel_set_occupy_timeout", "sentinel_profile_select", "sentinel_profile_gate", "sentinel_set_flow_path",
     "sentinel_param_top_values", "sentinel_param_snapshot_device", "sentinel_flow_window", "sentinel_metric_count",
     "sentinel_reset_metrics", "sentinel_param_table_stats", "sentinel_param_count",
-    "sentinel_batcher_request_token_async",
+    "sentinel_batcher_request_token_async", "sentinel_submit_flow_batches", "sentinel_profile_every",
     "sentinel_set_local_param_grades", "sentinel_submit_local_param_batch_ex", "sentinel_submit_local_param_batch_ex_host",
     "sentinel_load_local_resources_ex", "sentinel_submit_local_batch", "sentinel_submit_local_batch_host",
     "sentinel_local_node_metrics", "sentinel_set_statistic_max_rt",
@@ -209,6 +209,8 @@ def load():
         "sentinel_submit_local_batch_host": (C.c_int, [vp, i64, vp, vp, vp, vp]),
         "sentinel_local_node_metrics": (C.c_int, [vp, i32, i64, vp]),
         "sentinel_set_statistic_max_rt": (C.c_int, [vp, i64]),
+        "sentinel_submit_flow_batches": (C.c_int, [vp, i32, vp, vp, vp, vp, vp]),
+        "sentinel_profile_every": (C.c_int, [vp, i32]),
         "sentinel_shard_of": (i32, [i64, i32]),
         "sentinel_cluster_create": (C.c_int, [vp, i32, vp, vp]),
         "sentinel_cluster_destroy": (C.c_int, [vp]),

@@ -391,6 +391,12 @@ static LongRuns long_runs_at(uint32_t *ctl, int64_t n, uint32_t min_run, size_t 
     return L;
 }
 
+// Buffers of one partition-path batch: the front (prep, scan, scatter) writes them, the back
+// (k_part_half / big / long) reads them.
+struct PartBufs {
+    DevBuf *fkey, *hist, *pscan, *sval, *vtmp, *runs, *stat;
+};
+
 struct sentinel_engine {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -506,9 +512,12 @@ struct sentinel_engine {
         return e;
     }
 
+    int prof_every = 1;                // time every k-th launch of the selected kernel only
+    int64_t prof_count = 0;
     template <class F>
     void launch(const char *name, int64_t units, hipStream_t s, F &&f) {
         if (!prof || (!prof_only.empty() && prof_only != name)) { f(); return; }
+        if (prof_every > 1 && (prof_count++ % prof_every) != 0) { f(); return; }
         hipEvent_t a = get_ev(), b = get_ev();
         (void)hipEventRecord(a, s);
         f();
@@ -582,6 +591,10 @@ struct sentinel_engine {
         if (rc) return SENTINEL_E_NOMEM;
         ws_cap = c;
         return 0;
+    }
+
+    PartBufs part_bufs() {
+        return PartBufs{&w_fkey, &w_fhist, &w_pscan, &w_sval, &w_vtmp, &w_runs, &d_part_stat};
     }
 
     BatchWork work() {
@@ -1226,13 +1239,10 @@ int sentinel_engine::rebuild_limiters() {
 template <int NMAX>
 static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTable &FT, const uint32_t *rstart,
                                int lb, const EventSrc &src, const Verdicts &V, int64_t n, hipStream_t s,
-                               uint32_t *ctl, unsigned long long *stat) {
-    // ctl: [0] long-run count, [1] oversized-half count, [2, 2 + 2 nparts) oversized halves, then long runs
+                               uint32_t *ctl, unsigned long long *stat, const uint64_t *pval, uint64_t *gsval) {
     // ctl: [0] runs, [1] oversized halves, [2] chunks, [3] -, [4, 4 + 2 nparts) oversized halves, then the runs
     uint32_t *nbig = ctl + 1, *big = ctl + 4;
     const LongRuns LR = long_runs_at(ctl, n, LONG_RUN, 4 + 2 * (size_t)nparts);
-    const uint64_t *pval = e->w_sval.as<uint64_t>();
-    uint64_t *gsval = e->w_vtmp.as<uint64_t>();
     // a batch whose mean range does not fit goes straight to the HBM-sorting kernel
 #ifndef SENTINEL_ALLBIG_PCT
 #define SENTINEL_ALLBIG_PCT 90
@@ -1261,75 +1271,109 @@ static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTa
     });
 }
 
-static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
-                            hipStream_t s) {
-    const int32_t F = (int32_t)e->rules.size();
-    const int fbits = bits_for(F);
-    const uint32_t finvalid = ((uint32_t)1 << fbits) - 1;
-    const int lb = std::max(0, fbits - PART_MAX_BITS);
-    const int32_t nparts = (int32_t)(((int64_t)F + (1 << lb) - 1) >> lb);
-    const int pbits = bits_for(nparts - 1 > 0 ? nparts - 1 : 1);
-    const int64_t nb = part_blocks(n);
-    uint32_t *fkey = e->w_fkey.as<uint32_t>();
-    uint32_t *hist = e->w_fhist.as<uint32_t>();             // tile-major range histograms -> offsets
-    const int64_t ng = (nb + PS_GROUP - 1) / PS_GROUP;
-    int rc = e->w_pscan.ensure(((size_t)ng * nparts + 2 * (size_t)nparts + 1) * 4);
+// Geometry of a partition-path batch.
+struct PartGeo {
+    int32_t F;
+    uint32_t finvalid;
+    int lb, pbits;
+    int32_t nparts;
+    int64_t nb, ng;
+};
+static PartGeo part_geo(const sentinel_engine_t *e, int64_t n) {
+    PartGeo g;
+    g.F = (int32_t)e->rules.size();
+    const int fbits = bits_for(g.F);
+    g.finvalid = ((uint32_t)1 << fbits) - 1;
+    g.lb = std::max(0, fbits - PART_MAX_BITS);
+    g.nparts = (int32_t)(((int64_t)g.F + (1 << g.lb) - 1) >> g.lb);
+    g.pbits = bits_for(g.nparts - 1 > 0 ? g.nparts - 1 : 1);
+    g.nb = part_blocks(n);
+    g.ng = (g.nb + PS_GROUP - 1) / PS_GROUP;
+    return g;
+}
+
+// The front of a partition batch (prep + range histogram, scan, multi-split) into buffer set B.
+static int ensure_part_bufs(sentinel_engine_t *e, const PartBufs &B, int64_t n) {
+    const PartGeo g = part_geo(e, n);
+    int rc = B.pscan->ensure(((size_t)g.ng * g.nparts + 2 * (size_t)g.nparts + 1) * 4);
+    rc |= B.runs->ensure(long_runs_bytes(n, LONG_RUN, 4 + 2 * (size_t)g.nparts));
+    rc |= B.stat->ensure(8);
+    return rc;
+}
+
+static int part_front(sentinel_engine_t *e, const PartBufs &B, int64_t n, const Event *ev, const uint8_t *fl,
+                      uint64_t *out, hipStream_t s) {
+    const PartGeo g = part_geo(e, n);
+    int rc = ensure_part_bufs(e, B, n);
     if (rc) return rc;
-    uint32_t *gsum = e->w_pscan.as<uint32_t>();
-    uint32_t *rstart = gsum + (size_t)ng * nparts;
-    uint32_t *rtot = rstart + nparts + 1;
-    rc = e->w_runs.ensure(long_runs_bytes(n, LONG_RUN, 4 + 2 * (size_t)nparts));
-    if (rc) return rc;
-    if (!e->d_part_stat.p) {
-        rc = e->d_part_stat.ensure(8);
-        if (rc) return rc;
+    if (!e->h_part_stat) {
         HIP_OK(hipHostMalloc((void **)&e->h_part_stat, 8, 0));
         *e->h_part_stat = 0;
     }
-    unsigned long long *stat = e->d_part_stat.as<unsigned long long>();
-    uint32_t *ctl = e->w_runs.as<uint32_t>();
+    uint32_t *fkey = B.fkey->as<uint32_t>();
+    uint32_t *hist = B.hist->as<uint32_t>();                // tile-major range histograms -> offsets
+    uint32_t *gsum = B.pscan->as<uint32_t>();
+    uint32_t *rstart = gsum + (size_t)g.ng * g.nparts;
+    uint32_t *rtot = rstart + g.nparts + 1;
+    unsigned long long *stat = B.stat->as<unsigned long long>();
+    uint32_t *ctl = B.runs->as<uint32_t>();
     e->launch("part_prep", n, s, [&] {
-        k_part_prep<<<dim3((unsigned)nb), dim3(PP_THREADS), 0, s>>>(
-            n, ev, F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, e->flow_plain ? nullptr : fkey,
-            finvalid, lb, hist, nb, nparts,
-            ctl, stat);
+        k_part_prep<<<dim3((unsigned)g.nb), dim3(PP_THREADS), 0, s>>>(
+            n, ev, g.F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, e->flow_plain ? nullptr : fkey,
+            g.finvalid, g.lb, hist, g.nb, g.nparts, ctl, stat);
     });
     e->launch("scan", n, s, [&] {
-        const dim3 g2((unsigned)ng, (unsigned)((nparts + PS_THREADS - 1) / PS_THREADS));
-        k_part_colsum<<<g2, PS_THREADS, 0, s>>>(hist, nb, nparts, gsum);
-        k_part_colscan<<<(unsigned)((nparts + PC_THREADS / WAVE - 1) / (PC_THREADS / WAVE)), PC_THREADS, 0, s>>>(
-            gsum, ng, nparts, rtot);
-        k_part_offsets<<<g2, PS_THREADS, 0, s>>>(hist, nb, nparts, gsum, rtot, rstart);
+        const dim3 g2((unsigned)g.ng, (unsigned)((g.nparts + PS_THREADS - 1) / PS_THREADS));
+        k_part_colsum<<<g2, PS_THREADS, 0, s>>>(hist, g.nb, g.nparts, gsum);
+        k_part_colscan<<<(unsigned)((g.nparts + PC_THREADS / WAVE - 1) / (PC_THREADS / WAVE)), PC_THREADS, 0, s>>>(
+            gsum, g.ng, g.nparts, rtot);
+        k_part_offsets<<<g2, PS_THREADS, 0, s>>>(hist, g.nb, g.nparts, gsum, rtot, rstart);
     });
     const EventSrc src{ev, nullptr, fl, false};
     e->launch("part_scatter", n, s, [&] {
-        k_part_scatter<<<dim3((unsigned)nb), dim3(PT_THREADS), 0, s>>>(e->flow_plain ? nullptr : fkey, src,
-                                                                         e->w_sval.as<uint64_t>(), n, finvalid, lb,
-                                                                         pbits, hist, nb, nparts, F);
+        k_part_scatter<<<dim3((unsigned)g.nb), dim3(PT_THREADS), 0, s>>>(e->flow_plain ? nullptr : fkey, src,
+                                                                           B.sval->as<uint64_t>(), n, g.finvalid, g.lb,
+                                                                           g.pbits, hist, g.nb, g.nparts, g.F);
     });
-    const KeyTable FT = e->table(e->ft, NEV, 0);
-    const Verdicts V{out, fkey, finvalid};
-    const int mx = e->flow_max_n;
-    if (mx <= 2) launch_part_decide<2>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
-    else if (mx <= 4) launch_part_decide<4>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
-    else if (mx <= 10) launch_part_decide<10>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
-    else launch_part_decide<16>(e, nparts, FT, rstart, lb, src, V, n, s, ctl, stat);
     HIP_OK(hipGetLastError());
     return 0;
 }
 
-static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
-                       hipStream_t s) {
-    if (n <= 0) return 0;
-    if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
-    int rc = e->ensure_ws(n);
+// The back of a partition batch: sort + decide per half range, oversized halves, hot flows.
+static int part_back(sentinel_engine_t *e, const PartBufs &B, int64_t n, const Event *ev, const uint8_t *fl,
+                     uint64_t *out, hipStream_t s) {
+    const PartGeo g = part_geo(e, n);
+    uint32_t *rstart = B.pscan->as<uint32_t>() + (size_t)g.ng * g.nparts;
+    const EventSrc src{ev, nullptr, fl, false};
+    const KeyTable FT = e->table(e->ft, NEV, 0);
+    const Verdicts V{out, B.fkey->as<uint32_t>(), g.finvalid};
+    uint32_t *ctl = B.runs->as<uint32_t>();
+    unsigned long long *stat = B.stat->as<unsigned long long>();
+    const uint64_t *pval = B.sval->as<uint64_t>();
+    uint64_t *gsval = B.vtmp->as<uint64_t>();
+    const int mx = e->flow_max_n;
+    if (mx <= 2) launch_part_decide<2>(e, g.nparts, FT, rstart, g.lb, src, V, n, s, ctl, stat, pval, gsval);
+    else if (mx <= 4) launch_part_decide<4>(e, g.nparts, FT, rstart, g.lb, src, V, n, s, ctl, stat, pval, gsval);
+    else if (mx <= 10) launch_part_decide<10>(e, g.nparts, FT, rstart, g.lb, src, V, n, s, ctl, stat, pval, gsval);
+    else launch_part_decide<16>(e, g.nparts, FT, rstart, g.lb, src, V, n, s, ctl, stat, pval, gsval);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
+                            hipStream_t s) {
+    const PartBufs B = e->part_bufs();
+    int rc = part_front(e, B, n, ev, fl, out, s);
     if (rc) return rc;
+    return part_back(e, B, n, ev, fl, out, s);
+}
+
+// Partition-local path for this batch?  (No namespace limiter -- a limiter couples flows --, windows of
+// <= 16 buckets, <= 2^20 flows; auto picks it for large flow tables and falls back to the radix sort
+// for 1024 batches after a skewed one: a hot flow serialises its range's workgroup.)
+static bool choose_part(sentinel_engine_t *e, int64_t n) {
     const int32_t F = (int32_t)e->rules.size();
-    const int fbits = bits_for(F);
-    const uint32_t finvalid = ((uint32_t)1 << fbits) - 1;
     const bool lim = e->nlimiters > 0 && !e->flow_plain;
-    // partition-local path: no namespace limiter (a limiter couples flows), windows of <= 16 buckets,
-    // <= 2^20 flows; auto picks it for large flow tables (a hot flow serialises its range's workgroup)
     bool part = !lim && F > 0 && e->flow_max_n <= 16 && bits_for(F) <= 2 * PART_MAX_BITS &&
                 (e->flow_path == 2 || (e->flow_path == 0 && F >= 32768));
     const int64_t batch = e->flow_batches++;
@@ -1347,7 +1391,15 @@ static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const u
             }
         }
     }
-    if (part) return submit_flow_part(e, n, ev, fl, out, s);
+    return part;
+}
+
+static int submit_flow_sorted(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
+                              hipStream_t s) {
+    const int32_t F = (int32_t)e->rules.size();
+    const int fbits = bits_for(F);
+    const uint32_t finvalid = ((uint32_t)1 << fbits) - 1;
+    const bool lim = e->nlimiters > 0 && !e->flow_plain;
     const int lbits = bits_for(e->nlimiters);
     const uint32_t linvalid = ((uint32_t)1 << lbits) - 1;
     uint32_t *fkey = e->w_fkey.as<uint32_t>();
@@ -1373,6 +1425,16 @@ static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const u
     }
     HIP_OK(hipGetLastError());
     return 0;
+}
+
+static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
+                       hipStream_t s) {
+    if (n <= 0) return 0;
+    if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
+    int rc = e->ensure_ws(n);
+    if (rc) return rc;
+    if (choose_part(e, n)) return submit_flow_part(e, n, ev, fl, out, s);
+    return submit_flow_sorted(e, n, ev, fl, out, s);
 }
 
 static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamEvent *pev, const MultiEvent *mev,
@@ -1703,6 +1765,14 @@ int sentinel_profile_gate(sentinel_engine_t *e, int on) {
     if (!e) return fail(SENTINEL_E_INVALID, "null engine");
     std::lock_guard<std::mutex> g(e->mu);
     e->prof = on != 0;
+    return 0;
+}
+
+int sentinel_profile_every(sentinel_engine_t *e, int every) {
+    if (!e || every < 1) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    e->prof_every = every;
+    e->prof_count = 0;
     return 0;
 }
 
@@ -2178,6 +2248,30 @@ int sentinel_load_param_rules(sentinel_engine_t *e, const sentinel_param_rule_t 
     rc = e->rebuild_cm();
     if (rc) return rc;
     return e->rebuild_routes();
+}
+
+// Several device-resident batches decided in order on `stream` under one engine lock: the verdicts and
+// counters equal those of the batches submitted one by one.  (A two-stream variant -- batch k + 1's
+// validation, histogram and multi-split on a side stream under batch k's decisions -- was measured on
+// MI355X at 1M flows: the side stream's kernels only got CUs as k_part_half's workgroups drained, so a
+// batch took 0.325 ms of GPU time against 0.333 ms one by one, with more host time per batch; see
+// DESIGN.md section 6.)
+int sentinel_submit_flow_batches(sentinel_engine_t *e, int32_t nbatch, const int64_t *n,
+                                 const sentinel_event_t *const *ev, const uint8_t *const *flags,
+                                 sentinel_verdict_t *const *out, void *stream) {
+    if (!e || nbatch < 0 || (nbatch > 0 && (!n || !ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    for (int32_t k = 0; k < nbatch; ++k) {
+        if (n[k] < 0 || n[k] > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch size out of range (0 .. 2^28 events)");
+        if (n[k] > 0 && (!ev[k] || !out[k])) return fail(SENTINEL_E_INVALID, "null batch pointer");
+    }
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    for (int32_t k = 0; k < nbatch; ++k) {
+        const int rc = submit_flow(e, n[k], (const Event *)ev[k], flags ? flags[k] : nullptr, (uint64_t *)out[k], s);
+        if (rc) return rc;
+    }
+    return 0;
 }
 
 int sentinel_submit_flow_batch(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev, const uint8_t *flags,

@@ -342,6 +342,19 @@ class GpuTokenService:
         check(rc, "submit_flow_batch")
         return verdicts
 
+    def submit_flow_batches(self, events_list, verdicts_list, flags_list=None, stream=None):
+        """Device batches in order under one engine lock (sentinel_submit_flow_batches): each events tensor int64
+        (n, 2) of sentinel_event_t, each verdict tensor int64 (n,)."""
+        k = len(events_list)
+        ns = (C.c_int64 * max(k, 1))(*[int(e.shape[0]) for e in events_list])
+        evp = (C.c_void_p * max(k, 1))(*[e.data_ptr() for e in events_list])
+        outp = (C.c_void_p * max(k, 1))(*[v.data_ptr() for v in verdicts_list])
+        flp = None if flags_list is None else (C.c_void_p * max(k, 1))(*[f.data_ptr() for f in flags_list])
+        s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        check(self._L.sentinel_submit_flow_batches(self._h, k, ns, evp, flp, outp, None if s is None else C.c_void_p(s)),
+              "submit_flow_batches")
+        return verdicts_list
+
     def set_flow_path(self, path: str):
         """Flow pipeline of the following batches: "auto", "sorted" (global radix sort) or
         "partition" (partition-local); verdicts are identical on every path."""
