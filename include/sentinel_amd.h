@@ -423,7 +423,50 @@ typedef void (*sentinel_token_cb)(void *ctx, uint64_t tag, const sentinel_token_
 int  sentinel_batcher_request_token_async(sentinel_batcher_t *b, int64_t flow_id, int32_t acquire_count,
                                           int32_t prioritized, int64_t ts, sentinel_token_cb cb, void *ctx,
                                           uint64_t tag);
+/* n asynchronous requests in one call (one lock round trip for a front end that decoded many frames
+ * at once): request i is (flow_ids[i], acquire[i], prioritized ? prioritized[i] : 0, ts[i]) with
+ * tag tags[i]. */
+int  sentinel_batcher_request_tokens_async(sentinel_batcher_t *b, int32_t n, const int64_t *flow_ids,
+                                           const int32_t *acquire, const uint8_t *prioritized, const int64_t *ts,
+                                           sentinel_token_cb cb, void *ctx, const uint64_t *tags);
+/* fn(ctx) runs on the dispatcher thread after the callbacks of every decided batch (a front end
+ * flushes its sockets once per batch instead of once per response); NULL removes the hook. */
+int  sentinel_batcher_set_batch_hook(sentinel_batcher_t *b, void (*fn)(void *ctx), void *ctx);
 int  sentinel_batcher_stats(sentinel_batcher_t *b, int64_t *batches, int64_t *requests);
+
+/* ---- native cluster token server (the reference's Netty transport over TCP) ----
+ * The reference's framing and codecs (NettyTransportServer.java:89-92, DefaultRequestEntityDecoder,
+ * Ping/Flow/ParamFlow request decoders, DefaultResponseEntityWriter) in front of one engine: epoll
+ * I/O threads decode frames, FLOW requests go to an internal batcher (one call per socket read),
+ * responses are flushed once per decided batch; PARAM requests of a read are one host batch; PINGs
+ * maintain the namespace's connection set and connectedCount (ConnectionManager). */
+typedef struct sentinel_param_interner sentinel_param_interner_t;
+int  sentinel_param_interner_create(sentinel_param_interner_t **out);
+int  sentinel_param_interner_destroy(sentinel_param_interner_t *it);
+/* (flowId, Java-typed value) -> injective param key, dense from 1 (Java equals(): the type is part
+ * of the key, NaNs canonical, strings by their decoded text).  `value` = the value's wire bytes after
+ * its type byte (ParamFlowRequestDataWriter): big-endian int / long / short / byte / boolean / float
+ * bits / double bits, or a string's UTF-8 bytes. */
+int  sentinel_param_interner_key(sentinel_param_interner_t *it, int64_t flow_id, int32_t type, const uint8_t *value,
+                                 int32_t len, uint64_t *key);
+typedef int64_t (*sentinel_clock_fn)(void *ctx);
+typedef struct {
+    const char *host;                 /* IPv4 bind address, NULL = 127.0.0.1 */
+    int32_t port;                     /* 0 = ephemeral (sentinel_wire_server_port) */
+    int32_t io_threads;               /* epoll loops, >= 1 */
+    int32_t max_batch, max_wait_us;   /* the internal batcher */
+    const char *const *namespaces;    /* the engine's namespace table, in order (PING names) */
+    int32_t n_namespaces;
+    sentinel_param_interner_t *interner;   /* NULL: the server's own */
+    sentinel_clock_fn clock;          /* NULL: wall-clock ms (TimeUtil.currentTimeMillis) */
+    void *clock_ctx;
+} sentinel_wire_config_t;
+typedef struct sentinel_wire_server sentinel_wire_server_t;
+int  sentinel_wire_server_create(sentinel_engine_t *eng, const sentinel_wire_config_t *cfg, sentinel_wire_server_t **out);
+int32_t sentinel_wire_server_port(sentinel_wire_server_t *srv);
+int  sentinel_wire_server_stats(sentinel_wire_server_t *srv, int64_t *flow_requests, int64_t *param_requests,
+                                int64_t *batches, int32_t *connections);
+int  sentinel_wire_server_destroy(sentinel_wire_server_t *srv);
 
 /* ---- one node, several devices ----
  * One engine per entry of device_ids (a device may repeat: several shards on one GPU); flows are
@@ -516,9 +559,11 @@ int  sentinel_profile_enable(sentinel_engine_t *eng, int enable);
 /* Time only the named kernel (NULL or "": every kernel): two events per launch of it instead of two
  * per launch of every kernel, so a timed run keeps its dominant kernel's live duration cheaply. */
 int  sentinel_profile_select(sentinel_engine_t *eng, const char *kernel);
-/* Flow pipeline of the following batches: 0 auto (partition-local for >= 32768 flows, radix sort
- * after a skewed batch), 1 the global radix sort, 2 the partition-local path (where it applies:
- * no namespace limiter, <= 16 buckets).  Verdicts are identical on every path. */
+/* Flow pipeline of the following batches: 0 auto (one launch for batches of <= 4096 events, else
+ * partition-local for >= 32768 flows, radix sort after a skewed batch), 1 the global radix sort,
+ * 2 the partition-local path, 3 the one-launch small-batch kernel over consecutive chunks of 4096
+ * events (2 and 3 where they apply: no namespace limiter, <= 16 buckets).  Verdicts are identical
+ * on every path. */
 int  sentinel_set_flow_path(sentinel_engine_t *eng, int path);
 /* Gate the timing of following launches on (1) or off (0) without collecting or clearing what was
  * timed so far (no host synchronisation: callable between the batches of a timed loop). */

@@ -61,6 +61,10 @@ EXPORTS = [
     "sentinel_cluster_set_connected_count", "sentinel_cluster_load_flow_rules", "sentinel_cluster_load_param_rules",
     "sentinel_cluster_submit_host", "sentinel_cluster_flow_count", "sentinel_cluster_snapshot",
     "sentinel_cluster_batchers_create", "sentinel_cluster_request_token",
+    "sentinel_batcher_request_tokens_async", "sentinel_batcher_set_batch_hook",
+    "sentinel_param_interner_create", "sentinel_param_interner_destroy", "sentinel_param_interner_key",
+    "sentinel_wire_server_create", "sentinel_wire_server_port", "sentinel_wire_server_stats",
+    "sentinel_wire_server_destroy",
 ]
 
 STATUS_RELEASE_OK = 6
@@ -75,6 +79,15 @@ PARAM_COUNT_MIN_SHARED = 2
 
 class ServerConfig(C.Structure):
     _fields_ = [("exceed_count", C.c_double), ("max_occupy_ratio", C.c_double)]
+
+
+CLOCK_FN = C.CFUNCTYPE(C.c_int64, C.c_void_p)
+
+
+class WireConfig(C.Structure):
+    _fields_ = [("host", C.c_char_p), ("port", C.c_int32), ("io_threads", C.c_int32), ("max_batch", C.c_int32),
+                ("max_wait_us", C.c_int32), ("namespaces", C.POINTER(C.c_char_p)), ("n_namespaces", C.c_int32),
+                ("interner", C.c_void_p), ("clock", CLOCK_FN), ("clock_ctx", C.c_void_p)]
 
 
 class Namespace(C.Structure):
@@ -237,6 +250,13 @@ def load():
         "sentinel_param_table_stats": (C.c_int, [vp, vp]),
         "sentinel_param_count": (i32, [vp]),
         "sentinel_batcher_request_token_async": (C.c_int, [vp, i64, i32, i32, i64, vp, vp, C.c_uint64]),
+        "sentinel_param_interner_create": (C.c_int, [C.POINTER(vp)]),
+        "sentinel_param_interner_destroy": (C.c_int, [vp]),
+        "sentinel_param_interner_key": (C.c_int, [vp, i64, i32, vp, i32, C.POINTER(C.c_uint64)]),
+        "sentinel_wire_server_create": (C.c_int, [vp, C.POINTER(WireConfig), C.POINTER(vp)]),
+        "sentinel_wire_server_port": (i32, [vp]),
+        "sentinel_wire_server_stats": (C.c_int, [vp, vp, vp, vp, vp]),
+        "sentinel_wire_server_destroy": (C.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

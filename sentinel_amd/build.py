@@ -7,7 +7,7 @@ import subprocess
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_HERE)
 SOURCES = [os.path.join(_HERE, "csrc", "engine.hip")]
-DEPS = SOURCES + [os.path.join(_HERE, "csrc", f) for f in ("common.hpp", "scan_sort.hpp", "admission.hpp", "param_rules.hpp", "concurrent.hpp", "partition.hpp", "local_entry.hpp", "param_table.hpp")] + [
+DEPS = SOURCES + [os.path.join(_HERE, "csrc", f) for f in ("common.hpp", "scan_sort.hpp", "admission.hpp", "param_rules.hpp", "concurrent.hpp", "partition.hpp", "small.hpp", "wire_server.hpp", "local_entry.hpp", "param_table.hpp")] + [
     os.path.join(ROOT, "include", "sentinel_amd.h")]
 OUT = os.path.join(_HERE, "libsentinel_amd.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -21,7 +21,9 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in DEPS)
 
 
-TOOLS = {"dropin_bench": os.path.join(ROOT, "tools", "dropin_bench.cpp")}
+# name -> (source, links libsentinel_amd)
+TOOLS = {"dropin_bench": (os.path.join(ROOT, "tools", "dropin_bench.cpp"), True),
+         "wire_client": (os.path.join(ROOT, "tools", "wire_client.cpp"), False)}
 
 
 def build(force: bool = False, out: str = OUT, defines=()) -> str:
@@ -33,12 +35,17 @@ def build(force: bool = False, out: str = OUT, defines=()) -> str:
 
 def build_tools() -> None:
     """Native benchmark / front-end tools linked against the library (tools/, binaries next to them)."""
-    for name, src in TOOLS.items():
+    for name, (src, lib) in TOOLS.items():
         exe = os.path.join(os.path.dirname(src), name)
-        if os.path.exists(exe) and os.path.getmtime(exe) > max(os.path.getmtime(src), os.path.getmtime(OUT)):
+        deps = [src, OUT] if lib else [src]
+        if os.path.exists(exe) and os.path.getmtime(exe) > max(os.path.getmtime(d) for d in deps):
             continue
-        subprocess.run([HIPCC, "-O2", "-std=c++17", "-o", exe, src, "-L" + _HERE, "-lsentinel_amd",
-                        "-Wl,-rpath,$ORIGIN/../sentinel_amd", "-lpthread"], check=True)
+        if lib:
+            cmd = [HIPCC, "-O2", "-std=c++17", "-o", exe, src, "-L" + _HERE, "-lsentinel_amd",
+                   "-Wl,-rpath,$ORIGIN/../sentinel_amd", "-lpthread"]
+        else:
+            cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-o", exe, src, "-lpthread"]
+        subprocess.run(cmd, check=True)
 
 
 if __name__ == "__main__":

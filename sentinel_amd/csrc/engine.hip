@@ -33,6 +33,7 @@
 #include "param_rules.hpp"
 #include "param_table.hpp"
 #include "partition.hpp"
+#include "small.hpp"
 #include "local_entry.hpp"
 #include <random>
 #include "scan_sort.hpp"
@@ -425,7 +426,13 @@ struct sentinel_engine {
     bool verdict_nt = false;   // SENTINEL_VERDICT_NT=1: non-temporal verdict stores
     bool use_lookback = true;  // SENTINEL_SCAN=3pass selects the three-kernel scan
     bool fused_segments = true; // SENTINEL_SEGMENTS=split selects heads -> scan -> mark
-    int flow_path = 0;         // SENTINEL_FLOW_PATH: 0 auto, 1 sorted (global radix sort), 2 partition-local
+    int flow_path = 0;         // SENTINEL_FLOW_PATH: 0 auto, 1 sorted (global radix sort), 2 partition-local,
+                               // 3 small (every batch in one-launch chunks of SM_MAX events)
+    // small-batch host path (k_small_flow reads / writes pinned host memory directly)
+    Event *h_sm_ev = nullptr;
+    uint8_t *h_sm_fl = nullptr;
+    uint64_t *h_sm_out = nullptr;
+    uint32_t *h_sm_done = nullptr;
     // auto policy: the partition path unless the last partition batch was skewed (its largest flow
     // range > 8x the mean): then the sorted path for the next 1024 batches, then one probe again
     DevBuf d_part_stat;
@@ -1427,10 +1434,63 @@ static int submit_flow_sorted(sentinel_engine_t *e, int64_t n, const Event *ev, 
     return 0;
 }
 
+// The one-launch small-batch kernel applies: flow rules, no namespace limiter (a limiter couples
+// flows: the sorted path's limiter pass), windows of <= 16 buckets; auto picks it up to SM_MAX events.
+static bool small_ok(const sentinel_engine_t *e) {
+    const bool lim = e->nlimiters > 0 && !e->flow_plain;
+    return !lim && !e->rules.empty() && e->flow_max_n <= 16 && (e->flow_path == 0 || e->flow_path == 3);
+}
+
+// n <= SM_MAX events (device or pinned host pointers) in one launch on s; `done` (pinned, optional)
+// is set to 1 by the kernel once the verdicts are visible to the host.
+static int launch_small(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
+                        hipStream_t s, uint32_t *done = nullptr) {
+    const KeyTable FT = e->table(e->ft, NEV, 0);
+    const int32_t F = (int32_t)e->rules.size();
+    const int32_t *route = e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>();
+    const int mx = e->flow_max_n;
+    const EventSrc src{ev, nullptr, fl, false};
+    e->launch("small", n, s, [&] {
+        if (mx <= 2) k_small_flow<2><<<1, SM_THREADS, 0, s>>>(FT, (uint32_t)n, src, out, F, route, done);
+        else if (mx <= 4) k_small_flow<4><<<1, SM_THREADS, 0, s>>>(FT, (uint32_t)n, src, out, F, route, done);
+        else if (mx <= 10) k_small_flow<10><<<1, SM_THREADS, 0, s>>>(FT, (uint32_t)n, src, out, F, route, done);
+        else k_small_flow<16><<<1, SM_THREADS, 0, s>>>(FT, (uint32_t)n, src, out, F, route, done);
+    });
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+// Wait for a completion flag set by k_small_flow: poll the pinned word (a few us after the kernel's
+// last store, where a stream synchronisation costs tens of us of wake-up), checking the stream for a
+// device error now and then.
+static int wait_done(sentinel_engine_t *e, const uint32_t *flag) {
+    for (uint64_t it = 1;; ++it) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE)) return 0;
+        __builtin_ia32_pause();
+        if ((it & 0xFFFF) == 0) {
+            const hipError_t q = hipStreamQuery(e->stream);
+            if (q == hipSuccess) {                   // the stream drained: the flag must be set now
+                if (__atomic_load_n(flag, __ATOMIC_ACQUIRE)) return 0;
+                return fail(SENTINEL_E_DEVICE, "small batch finished without its completion flag");
+            }
+            if (q != hipErrorNotReady) return fail(SENTINEL_E_DEVICE, hipGetErrorString(q));
+        }
+    }
+}
+
 static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
                        hipStream_t s) {
     if (n <= 0) return 0;
     if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
+    if (small_ok(e) && (n <= SM_MAX || e->flow_path == 3)) {
+        // consecutive chunks decided in order = the whole batch decided in arrival order
+        for (int64_t off = 0; off < n; off += SM_MAX) {
+            const int rc = launch_small(e, std::min<int64_t>(SM_MAX, n - off), ev + off, fl ? fl + off : nullptr,
+                                        out + off, s);
+            if (rc) return rc;
+        }
+        return 0;
+    }
     int rc = e->ensure_ws(n);
     if (rc) return rc;
     if (choose_part(e, n)) return submit_flow_part(e, n, ev, fl, out, s);
@@ -1681,7 +1741,7 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
     if (const char *c = getenv("SENTINEL_HOT_HET_RUN")) e->hot_het_run = (uint32_t)std::max(WAVE_HET_RUN, (uint32_t)atoi(c));
     if (const char *c = getenv("SENTINEL_FLOW_PATH")) {
         const std::string v(c);
-        e->flow_path = v == "sorted" ? 1 : v == "partition" ? 2 : 0;
+        e->flow_path = v == "sorted" ? 1 : v == "partition" ? 2 : v == "small" ? 3 : 0;
     }
     if (const char *c = getenv("SENTINEL_SEGMENTS")) e->fused_segments = std::string(c) != "split";
     if (const char *c = getenv("SENTINEL_PARAM_CAPACITY")) {
@@ -1734,6 +1794,10 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
     if (e->s_h2d) (void)hipStreamDestroy(e->s_h2d);
     if (e->s_d2h) (void)hipStreamDestroy(e->s_d2h);
     if (e->h_part_stat) (void)hipHostFree(e->h_part_stat);
+    if (e->h_sm_ev) (void)hipHostFree(e->h_sm_ev);
+    if (e->h_sm_fl) (void)hipHostFree(e->h_sm_fl);
+    if (e->h_sm_out) (void)hipHostFree(e->h_sm_out);
+    if (e->h_sm_done) (void)hipHostFree(e->h_sm_done);
     if (e->h_long_chunks) (void)hipHostFree(e->h_long_chunks);
     if (e->h_het_hint) (void)hipHostFree(e->h_het_hint);
     e->d_part_stat.release();
@@ -1755,7 +1819,7 @@ int sentinel_profile_enable(sentinel_engine_t *e, int enable) {
 }
 
 int sentinel_set_flow_path(sentinel_engine_t *e, int path) {
-    if (!e || path < 0 || path > 2) return fail(SENTINEL_E_INVALID, "bad flow path");
+    if (!e || path < 0 || path > 3) return fail(SENTINEL_E_INVALID, "bad flow path");
     std::lock_guard<std::mutex> g(e->mu);
     e->flow_path = path;
     return 0;
@@ -2306,11 +2370,48 @@ static int submit_flow_ids_host(sentinel_engine_t *e, int64_t n, const int64_t *
     return submit_flow_host_locked(e, n, ev, flags, out);
 }
 
+// The batcher's launch: flowIds looked up and the batch queued under one engine lock.  Small batches
+// (k_small_flow applies) are launched on pinned ev / flags / out with the completion flag `done`
+// (*async = true: the caller polls it); anything else is decided synchronously here.
+static int submit_flow_ids_pinned(sentinel_engine_t *e, int64_t n, const int64_t *ids, sentinel_event_t *ev,
+                                  const uint8_t *flags, sentinel_verdict_t *out, uint32_t *done, bool *async) {
+    *async = false;
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> g(e->mu);
+    for (int64_t i = 0; i < n; ++i) ev[i].flow_idx = e->flat_flow.find(ids[i]);
+    if (n <= SM_MAX && small_ok(e)) {
+        HIP_OK(hipSetDevice(e->device));
+        __atomic_store_n(done, 0u, __ATOMIC_RELAXED);
+        const int rc = launch_small(e, n, (const Event *)ev, flags, (uint64_t *)out, e->stream, done);
+        *async = rc == 0;
+        return rc;
+    }
+    return submit_flow_host_locked(e, n, ev, flags, out);
+}
+
 static int submit_flow_host_locked(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev, const uint8_t *flags,
                                    sentinel_verdict_t *out) {
     HIP_OK(hipSetDevice(e->device));
     hipStream_t s = e->stream;
     int rc = 0;
+    if (n <= SM_MAX && small_ok(e)) {
+        // pinned staging read / written by the kernel itself: one launch, no copy commands
+        if (!e->h_sm_ev) {
+            HIP_OK(hipHostMalloc((void **)&e->h_sm_ev, SM_MAX * sizeof(Event), 0));
+            HIP_OK(hipHostMalloc((void **)&e->h_sm_fl, SM_MAX, 0));
+            HIP_OK(hipHostMalloc((void **)&e->h_sm_out, SM_MAX * 8, 0));
+            HIP_OK(hipHostMalloc((void **)&e->h_sm_done, 64, 0));
+        }
+        memcpy(e->h_sm_ev, ev, n * sizeof(Event));
+        if (flags) memcpy(e->h_sm_fl, flags, n);
+        *e->h_sm_done = 0;
+        rc = launch_small(e, n, e->h_sm_ev, flags ? e->h_sm_fl : nullptr, e->h_sm_out, s, e->h_sm_done);
+        if (rc) return rc;
+        rc = wait_done(e, e->h_sm_done);
+        if (rc) return rc;
+        memcpy(out, e->h_sm_out, n * 8);
+        return 0;
+    }
     rc |= e->io_ev.ensure(n * sizeof(Event));
     rc |= e->io_fl.ensure(n);
     rc |= e->io_out.ensure(n * 8);
@@ -3200,9 +3301,11 @@ int sentinel_snapshot(sentinel_engine_t *e, int64_t ts, sentinel_flow_snapshot_t
 // The reference TokenService is synchronous per call and called concurrently from Netty worker
 // threads (NettyTransportServer.java:53-54, FlowRequestProcessor.java:36-45).  The batcher keeps
 // that contract: callers block in sentinel_batcher_request_token while a dispatcher thread gathers
-// concurrent requests (up to max_batch, or max_wait_us after the first one) into pinned host
-// buffers, decides them as one GPU batch in arrival order, and wakes the callers.  Double-buffered:
-// the next batch is gathered while the current one is on the GPU.
+// concurrent requests into pinned host buffers and decides them as GPU batches in arrival order.
+// Two batch slots: while batch k is on the GPU (k_small_flow reading and writing the slot's pinned
+// buffers, then raising the slot's completion flag) the dispatcher gathers and launches batch k + 1
+// on the same stream (so k + 1 is decided after k), then hands out k's verdicts.  When the GPU is
+// idle a batch waits up to max_wait_us after its first request (or until max_batch requests).
 struct BatchReq {
     sentinel_verdict_t out;
     int rc;
@@ -3212,7 +3315,7 @@ struct BatchReq {
 // One queued request: a blocked caller (waiter) or an asynchronous one (cb).
 struct BatchItem {
     int64_t flow_id;
-    sentinel_event_t ev;                 // flow_idx filled by the dispatcher (submit_flow_ids_host)
+    sentinel_event_t ev;                 // flow_idx filled at launch (submit_flow_ids_pinned)
     uint8_t flag;
     BatchReq *waiter;
     sentinel_token_cb cb;
@@ -3221,6 +3324,17 @@ struct BatchItem {
 };
 
 struct sentinel_batcher {
+    static constexpr int NSLOT = 2;
+    struct Slot {
+        std::vector<BatchItem> items;
+        std::vector<int64_t> ids;
+        sentinel_event_t *h_ev = nullptr;  // pinned: read by the kernel
+        uint8_t *h_fl = nullptr;
+        sentinel_verdict_t *h_out = nullptr;
+        uint32_t *h_done = nullptr;        // pinned completion flag
+        bool async = false;
+        int rc = 0;
+    };
     sentinel_engine *e = nullptr;
     int32_t max_batch = 4096;
     int32_t max_wait_us = 50;
@@ -3229,64 +3343,103 @@ struct sentinel_batcher {
     std::vector<BatchItem> queue;
     std::thread th;
     bool stop = false;
-    sentinel_event_t *h_ev = nullptr;
-    uint8_t *h_fl = nullptr;
-    sentinel_verdict_t *h_out = nullptr;
-    std::vector<int64_t> h_ids;
+    Slot slot[NSLOT];
     std::atomic<int64_t> batches{0}, requests{0};
     int64_t callers = 0;               // requesters inside request_token (guarded by mu)
     std::condition_variable cv_idle;
+    void (*hook)(void *) = nullptr;    // after each batch's callbacks (sentinel_batcher_set_batch_hook)
+    void *hook_ctx = nullptr;
+
+    void launch(Slot &S) {
+        const int64_t n = (int64_t)S.items.size();
+        S.ids.resize(n);
+        for (int64_t i = 0; i < n; ++i) {
+            S.ids[i] = S.items[i].flow_id;
+            S.h_ev[i] = S.items[i].ev;
+            S.h_fl[i] = S.items[i].flag;
+        }
+        S.rc = submit_flow_ids_pinned(e, n, S.ids.data(), S.h_ev, S.h_fl, S.h_out, S.h_done, &S.async);
+    }
+
+    void complete(Slot &S) {
+        if (S.async && S.rc == 0) S.rc = wait_done(e, S.h_done);
+        const int64_t n = (int64_t)S.items.size();
+        const int rc = S.rc;
+        bool any_sync = false;
+        for (int64_t i = 0; i < n; ++i) {
+            const BatchItem &it = S.items[i];
+            if (it.waiter) {
+                it.waiter->out = S.h_out[i];
+                it.waiter->rc = rc;
+                it.waiter->done.store(1, std::memory_order_release);
+                any_sync = true;
+            } else {
+                // engine down -> FAIL (the client falls back to its local check)
+                sentinel_token_result_t r;
+                r.status = rc ? SENTINEL_STATUS_FAIL : S.h_out[i].status;
+                r.remaining = rc ? 0 : S.h_out[i].remaining;
+                r.wait_in_ms = rc ? 0 : S.h_out[i].wait_in_ms;
+                r.reserved = 0;
+                it.cb(it.ctx, it.tag, &r);
+            }
+        }
+        batches.fetch_add(1);
+        requests.fetch_add(n);
+        S.items.clear();
+        S.async = false;
+        void (*h)(void *);
+        void *hc;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            h = hook;
+            hc = hook_ctx;
+        }
+        if (h) h(hc);
+        if (any_sync) {
+            { std::lock_guard<std::mutex> lk(mu); }
+            cv_out.notify_all();
+        }
+    }
 
     void run() {
-        std::vector<BatchItem> cur;
+        int nin = 0, next = 0;             // batches in flight; the slot the next batch goes to
         for (;;) {
-            {
-                std::unique_lock<std::mutex> lk(mu);
-                cv_in.wait(lk, [&] { return stop || !queue.empty(); });
-                if (stop && queue.empty()) return;
-                if ((int32_t)queue.size() < max_batch && max_wait_us > 0) {
-                    cv_in.wait_for(lk, std::chrono::microseconds(max_wait_us),
-                                   [&] { return stop || (int32_t)queue.size() >= max_batch; });
+            bool took = false;
+            if (nin < NSLOT) {
+                Slot &S = slot[next];
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    if (nin == 0) {
+                        cv_in.wait(lk, [&] { return stop || !queue.empty(); });
+                        if (stop && queue.empty()) return;
+                        if ((int32_t)queue.size() < max_batch && max_wait_us > 0)
+                            cv_in.wait_for(lk, std::chrono::microseconds(max_wait_us),
+                                           [&] { return stop || (int32_t)queue.size() >= max_batch; });
+                    }
+                    if ((int32_t)queue.size() <= max_batch) {
+                        S.items.swap(queue);
+                    } else {
+                        S.items.assign(queue.begin(), queue.begin() + max_batch);
+                        queue.erase(queue.begin(), queue.begin() + max_batch);
+                    }
                 }
-                cur.clear();
-                if ((int32_t)queue.size() <= max_batch) {
-                    cur.swap(queue);
-                } else {
-                    cur.assign(queue.begin(), queue.begin() + max_batch);
-                    queue.erase(queue.begin(), queue.begin() + max_batch);
-                }
-            }
-            const int64_t n = (int64_t)cur.size();
-            bool any_sync = false;
-            h_ids.resize(n);
-            for (int64_t i = 0; i < n; ++i) {
-                h_ids[i] = cur[i].flow_id;
-                h_ev[i] = cur[i].ev;
-                h_fl[i] = cur[i].flag;
-            }
-            const int rc = submit_flow_ids_host(e, n, h_ids.data(), h_ev, h_fl, h_out);
-            for (int64_t i = 0; i < n; ++i) {
-                const BatchItem &it = cur[i];
-                if (it.waiter) {
-                    it.waiter->out = h_out[i];
-                    it.waiter->rc = rc;
-                    it.waiter->done.store(1, std::memory_order_release);
-                    any_sync = true;
-                } else {
-                    // engine down -> FAIL (the client falls back to its local check)
-                    sentinel_token_result_t r;
-                    r.status = rc ? SENTINEL_STATUS_FAIL : h_out[i].status;
-                    r.remaining = rc ? 0 : h_out[i].remaining;
-                    r.wait_in_ms = rc ? 0 : h_out[i].wait_in_ms;
-                    r.reserved = 0;
-                    it.cb(it.ctx, it.tag, &r);
+                if (!S.items.empty()) {
+                    launch(S);
+                    ++nin;
+                    next = (next + 1) % NSLOT;
+                    took = true;
                 }
             }
-            batches.fetch_add(1);
-            requests.fetch_add(n);
-            if (any_sync) {
-                { std::lock_guard<std::mutex> lk(mu); }
-                cv_out.notify_all();
+            if (nin > 0) {
+                const int o = (next - nin + NSLOT) % NSLOT;             // the oldest batch in flight
+                Slot &O = slot[o];
+                // hand out the oldest batch once done; wait for it when nothing new was launched or
+                // every slot is busy
+                const bool ready = !O.async || O.rc != 0 || __atomic_load_n(O.h_done, __ATOMIC_ACQUIRE);
+                if (ready || !took || nin == NSLOT) {
+                    complete(O);
+                    --nin;
+                }
             }
         }
     }
@@ -3310,11 +3463,17 @@ int sentinel_batcher_create(sentinel_engine_t *e, int32_t max_batch, int32_t max
     b->max_batch = max_batch;
     b->max_wait_us = max_wait_us;
     (void)hipSetDevice(e->device);
-    if (hipHostMalloc((void **)&b->h_ev, (size_t)max_batch * sizeof(sentinel_event_t), 0) != hipSuccess ||
-        hipHostMalloc((void **)&b->h_fl, (size_t)max_batch, 0) != hipSuccess ||
-        hipHostMalloc((void **)&b->h_out, (size_t)max_batch * sizeof(sentinel_verdict_t), 0) != hipSuccess) {
-        delete b;
-        return fail(SENTINEL_E_NOMEM, "hipHostMalloc failed");
+    for (auto &S : b->slot) {
+        if (hipHostMalloc((void **)&S.h_ev, (size_t)max_batch * sizeof(sentinel_event_t), 0) != hipSuccess ||
+            hipHostMalloc((void **)&S.h_fl, (size_t)max_batch, 0) != hipSuccess ||
+            hipHostMalloc((void **)&S.h_out, (size_t)max_batch * sizeof(sentinel_verdict_t), 0) != hipSuccess ||
+            hipHostMalloc((void **)&S.h_done, 64, 0) != hipSuccess) {
+            for (auto &T : b->slot)
+                for (void *p : {(void *)T.h_ev, (void *)T.h_fl, (void *)T.h_out, (void *)T.h_done})
+                    if (p) (void)hipHostFree(p);
+            delete b;
+            return fail(SENTINEL_E_NOMEM, "hipHostMalloc failed");
+        }
     }
     b->th = std::thread([b] { b->run(); });
     *out = b;
@@ -3334,9 +3493,8 @@ int sentinel_batcher_destroy(sentinel_batcher_t *b) {
         std::unique_lock<std::mutex> lk(b->mu);
         b->cv_idle.wait(lk, [&] { return b->callers == 0; });
     }
-    (void)hipHostFree(b->h_ev);
-    (void)hipHostFree(b->h_fl);
-    (void)hipHostFree(b->h_out);
+    for (auto &S : b->slot)
+        for (void *p : {(void *)S.h_ev, (void *)S.h_fl, (void *)S.h_out, (void *)S.h_done}) (void)hipHostFree(p);
     delete b;
     return 0;
 }
@@ -3376,6 +3534,38 @@ int sentinel_batcher_request_token_async(sentinel_batcher_t *b, int64_t flow_id,
     it.ctx = ctx;
     it.tag = tag;
     return b->enqueue(it);
+}
+
+int sentinel_batcher_request_tokens_async(sentinel_batcher_t *b, int32_t n, const int64_t *flow_ids,
+                                          const int32_t *acquire, const uint8_t *prio, const int64_t *ts,
+                                          sentinel_token_cb cb, void *ctx, const uint64_t *tags) {
+    if (!b || !cb || n < 0 || (n > 0 && (!flow_ids || !acquire || !ts || !tags)))
+        return fail(SENTINEL_E_INVALID, "bad arguments");
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> lk(b->mu);
+    if (b->stop) return fail(SENTINEL_E_STATE, "batcher stopped");
+    const bool wake = b->queue.empty();
+    for (int32_t i = 0; i < n; ++i) {
+        BatchItem it{};
+        it.flow_id = flow_ids[i];
+        it.ev.acquire = acquire[i];
+        it.ev.ts = ts[i];
+        it.flag = (prio && prio[i]) ? SENTINEL_FLAG_PRIORITIZED : 0;
+        it.cb = cb;
+        it.ctx = ctx;
+        it.tag = tags[i];
+        b->queue.push_back(it);
+    }
+    if (wake || (int32_t)b->queue.size() >= b->max_batch) b->cv_in.notify_one();
+    return 0;
+}
+
+int sentinel_batcher_set_batch_hook(sentinel_batcher_t *b, void (*fn)(void *ctx), void *ctx) {
+    if (!b) return fail(SENTINEL_E_INVALID, "null batcher");
+    std::lock_guard<std::mutex> lk(b->mu);
+    b->hook = fn;
+    b->hook_ctx = ctx;
+    return 0;
 }
 
 int sentinel_batcher_stats(sentinel_batcher_t *b, int64_t *batches, int64_t *requests) {
@@ -3628,3 +3818,5 @@ int sentinel_cluster_request_token(sentinel_cluster_t *c, int64_t flow_id, int32
 }
 
 }  // extern "C"
+
+#include "wire_server.hpp"

@@ -356,9 +356,10 @@ class GpuTokenService:
         return verdicts_list
 
     def set_flow_path(self, path: str):
-        """Flow pipeline of the following batches: "auto", "sorted" (global radix sort) or
-        "partition" (partition-local); verdicts are identical on every path."""
-        check(self._L.sentinel_set_flow_path(self._h, {"auto": 0, "sorted": 1, "partition": 2}[path]),
+        """Flow pipeline of the following batches: "auto", "sorted" (global radix sort),
+        "partition" (partition-local) or "small" (one-launch chunks of 4096 events); verdicts are
+        identical on every path."""
+        check(self._L.sentinel_set_flow_path(self._h, {"auto": 0, "sorted": 1, "partition": 2, "small": 3}[path]),
               "sentinel_set_flow_path")
 
     def submit_flow_batch_host(self, flow_idx, acquire, ts, flags=None):

@@ -518,3 +518,72 @@ class TokenClient:
 
     def close(self):
         self.sock.close()
+
+
+# ------------------------------------------------------------------ native server (C++ behind the ABI)
+
+def _value_bytes(v: TypedValue) -> bytes:
+    """A value's wire bytes after its type byte (string: the UTF-8 bytes, no length)."""
+    if v.tag == PARAM_TYPE_STRING:
+        return str(v.value).encode("utf-8")
+    return _encode_value(v)[1:]
+
+
+class NativeParamInterner:
+    """sentinel_param_interner_*: the native server's (flowId, Java-typed value) -> key table."""
+
+    def __init__(self):
+        from . import _lib
+        import ctypes as C
+        self._L = _lib.load()
+        h = C.c_void_p()
+        _lib.check(self._L.sentinel_param_interner_create(C.byref(h)), "param_interner_create")
+        self.handle = h
+
+    def key(self, flow_id: int, value: TypedValue) -> int:
+        from . import _lib
+        import ctypes as C
+        b = _value_bytes(value)
+        k = C.c_uint64()
+        buf = C.create_string_buffer(b, len(b)) if b else None
+        _lib.check(self._L.sentinel_param_interner_key(self.handle, int(flow_id), int(value.tag), buf, len(b), C.byref(k)),
+                   "param_interner_key")
+        return int(k.value)
+
+    def close(self):
+        if self.handle:
+            self._L.sentinel_param_interner_destroy(self.handle)
+            self.handle = None
+
+
+class NativeTokenServer:
+    """sentinel_wire_server_*: the same protocol and handling as ClusterTokenServer, in C++ (epoll
+    I/O threads, one batcher call per socket read, one flush per decided batch).  `clock()`, when
+    given, replaces the wall clock (it is called from the I/O threads)."""
+
+    def __init__(self, svc: GpuTokenService, namespaces: Sequence[str] = ("default",), host: str = "127.0.0.1",
+                 port: int = 0, io_threads: int = 2, max_batch: int = 4096, max_wait_us: int = 20,
+                 clock: Optional[Callable[[], int]] = None, interner: Optional[NativeParamInterner] = None):
+        from . import _lib
+        import ctypes as C
+        self._L = _lib.load()
+        self.svc = svc
+        self._names = (C.c_char_p * max(len(namespaces), 1))(*[n.encode() for n in namespaces])
+        self._clock = _lib.CLOCK_FN(lambda _ctx: int(clock())) if clock else _lib.CLOCK_FN()
+        cfg = _lib.WireConfig(host.encode(), int(port), int(io_threads), int(max_batch), int(max_wait_us),
+                              self._names, len(namespaces), interner.handle if interner else None, self._clock, None)
+        h = C.c_void_p()
+        _lib.check(self._L.sentinel_wire_server_create(svc.handle, C.byref(cfg), C.byref(h)), "wire_server_create")
+        self.handle = h
+        self.port = int(self._L.sentinel_wire_server_port(h))
+
+    def stats(self):
+        import ctypes as C
+        f, p, b, c = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int32()
+        self._L.sentinel_wire_server_stats(self.handle, C.byref(f), C.byref(p), C.byref(b), C.byref(c))
+        return {"flow_requests": f.value, "param_requests": p.value, "batches": b.value, "connections": c.value}
+
+    def stop(self):
+        if self.handle:
+            self._L.sentinel_wire_server_destroy(self.handle)
+            self.handle = None

@@ -12,10 +12,11 @@ from sentinel_amd import trace as T
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["sorted", "partition"])
+@pytest.fixture(autouse=True, params=["sorted", "partition", "small"])
 def flow_path(request, monkeypatch):
-    """Every flow parity case runs on both flow pipelines: the global radix sort and the
-    partition-local path (SENTINEL_FLOW_PATH is read when an engine is created)."""
+    """Every flow parity case runs on every flow pipeline: the global radix sort, the
+    partition-local path and the one-launch small-batch kernel over 4096-event chunks
+    (SENTINEL_FLOW_PATH is read when an engine is created)."""
     monkeypatch.setenv("SENTINEL_FLOW_PATH", request.param)
     return request.param
 
@@ -448,7 +449,7 @@ def _norm_dump(d, n):
 
 
 def test_path_switches_snapshots_and_epoch_gaps(oracle_mod):
-    """One engine, one flow table written by both pipelines in turn (sentinel_set_flow_path) and by
+    """One engine, one flow table written by all three pipelines in turn (sentinel_set_flow_path) and by
     snapshots (which roll windows) between batches; batches advance by 0, 1, 2..n-1 and >= n epochs,
     some with heterogeneous acquire counts (the general walk).  Every verdict must equal the
     oracle's, and the final windows too (absent == present-and-empty)."""
@@ -461,10 +462,10 @@ def test_path_switches_snapshots_and_epoch_gaps(oracle_mod):
     svc, orc = _engine(rules), _oracle(oracle_mod, rules)
     t = T.T0_ALIGNED + 37
     # (epochs advanced before the batch, pipeline, snapshot before the batch)
-    plan = [(0, "partition", False), (0, "partition", False), (1, "partition", False), (1, "sorted", False),
-            (0, "partition", False), (1, "partition", True), (0, "partition", False), (2, "partition", False),
+    plan = [(0, "partition", False), (0, "partition", False), (1, "small", False), (1, "sorted", False),
+            (0, "partition", False), (1, "partition", True), (0, "partition", False), (2, "small", False),
             (3, "partition", False), (12, "partition", False), (1, "partition", False), (0, "sorted", False),
-            (1, "partition", False), (1, "partition", True), (0, "partition", False), (25, "partition", False)]
+            (1, "small", False), (1, "partition", True), (0, "partition", False), (25, "small", False)]
     for b, (adv, path, snap) in enumerate(plan):
         t += adv * 100
         if snap:

@@ -87,7 +87,7 @@ def _check(svc, orc, F, idx, acq, ts):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["sorted", "partition"])
+@pytest.mark.parametrize("path", ["sorted", "partition", "small"])
 def test_gpu_reload_matches_oracle(oracle_mod, path):
     """Batches -> reload (survivors keep old windows and counters, removals, a changed window, a
     duplicate flowId, an emptied namespace) -> batches -> reload (an orphan comes back) -> server

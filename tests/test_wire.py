@@ -169,3 +169,157 @@ def test_server_end_to_end_against_oracle(oracle_mod):
     assert {a[1][3] for a in answers} <= set(range(1, n_clients + 1))   # connectedCount replies
     assert server.batches >= 1
 
+
+
+def test_native_interner_equality_classes_match_python():
+    """sentinel_param_interner (C++) partitions (flowId, typed value) pairs exactly as the Python
+    ParamKeyInterner does: Java equals() -- the tag separates Integer(1) / Long(1), NaNs collapse,
+    -0.0 != 0.0, strings compare by their decoded text."""
+    nat = W.NativeParamInterner()
+    py = W.ParamKeyInterner()
+    vals = [W.jint(1), W.jlong(1), W.jint(-1), W.jbyte(1), W.jshort(1), W.jbool(True), W.jbool(False),
+            W.jdouble(0.0), W.jdouble(-0.0), W.jdouble(float("nan")), W.TypedValue(W.PARAM_TYPE_DOUBLE, 0x7FF0000000000001),
+            W.jfloat(float("nan")), W.TypedValue(W.PARAM_TYPE_FLOAT, 0x7F800001), W.jfloat(1.5), W.jdouble(1.5),
+            W.jstr("vip"), W.jstr("VIP"), W.jstr(""), W.jstr("été"), W.jint(1)]
+    # Python keys the values its decoder produces (NaN payloads canonical after the float round trip);
+    # the native interner gets the raw wire bits
+    decoded = W.decode_request(W.encode_param_request(1, 7, 1, vals)[2:]).data[2]
+    assert len(decoded) == len(vals)
+    for fid in (7, 8):
+        n = [nat.key(fid, v) for v in vals]
+        p = [py.key(fid, v) for v in decoded]
+        for i in range(len(vals)):
+            for j in range(len(vals)):
+                assert (n[i] == n[j]) == (p[i] == p[j]), (vals[i], vals[j])
+    assert nat.key(7, W.jint(1)) != nat.key(8, W.jint(1))
+    assert min(nat.key(7, v) for v in vals) >= 1
+    nat.close()
+
+
+def _ask(cl, frame):
+    cl.send(frame)
+    return cl.recv()
+
+
+@pytest.mark.gpu
+def test_native_server_sequential_matches_oracle(oracle_mod):
+    """sentinel_wire_server over TCP, one request at a time with a controlled clock: every FLOW and
+    PARAM response equals the oracle replaying the same requests in the same order (connectedCount
+    from the PINGs: AVG_LOCAL thresholds), and the protocol edge cases behave as wire.py's."""
+    import sentinel_amd as sa
+    from sentinel_amd.token_service import ServerNamespace
+    rng = np.random.default_rng(62)
+    F = 120
+    rules, _ = T.config2(1, seed=62, n_flows=F)
+    rules.count[:] = rng.integers(3, 30, size=F)
+    rules.threshold_type[::4] = 0
+    svc = sa.GpuTokenService(0)
+    svc.set_namespaces([ServerNamespace(connected_count=0)])
+    svc.load_rules_array(rules.flow_id, rules.count, rules.threshold_type, rules.sample_count,
+                         rules.window_interval_ms, rules.namespace, rules.checker)
+    interner = W.NativeParamInterner()
+    svc.load_param_rules([sa.ParamFlowRule(count=3.0, cluster_config=sa.ClusterFlowConfig(
+        flow_id=900 + r, threshold_type=1, sample_count=2, window_interval_ms=1000),
+        hot_items={interner.key(900 + r, W.jstr("vip")): 1}) for r in range(6)])
+    now = [T.T0_ALIGNED + 5]
+    server = W.NativeTokenServer(svc, ["default"], clock=lambda: now[0], interner=interner, io_threads=2)
+    try:
+        a, b = W.TokenClient("127.0.0.1", server.port), W.TokenClient("127.0.0.1", server.port)
+        assert _ask(a, W.encode_ping(1, "default")) == (1, 0, 0, 1)
+        assert _ask(b, W.encode_ping(2, "default")) == (2, 0, 0, 2)
+        assert _ask(a, W.encode_ping(3, " \t")) == (3, 0, -1, None)          # blank namespace: BAD
+        assert _ask(a, W._frame(struct.pack(">ib", 4, 0))) == (4, 0, -1, None)   # no data: BAD
+        # frames that produce nothing: too long (skipped), unknown type, flow with null data
+        a.send(struct.pack(">H", 1023) + b"\x01" * 1023)
+        a.send(W._frame(struct.pack(">ib", 5, 9) + b"\0" * 13))
+        a.send(W._frame(struct.pack(">ibq", 6, 1, 5)))
+        orc = oracle_mod.TokenServiceOracle(rules.as_dicts(), namespaces=[dict(connected_count=2)],
+                                            param_rules=[dict(flow_id=900 + r, count=3.0, threshold_type=1,
+                                                              sample_count=2, window_interval_ms=1000) for r in range(6)],
+                                            hot_items={r: [(interner.key(900 + r, W.jstr("vip")), 1)] for r in range(6)})
+        fid_to_idx = {int(f): i for i, f in enumerate(rules.flow_id)}
+        for k in range(500):
+            now[0] += int(rng.integers(0, 40))
+            xid = 100 + k
+            cl = a if k % 3 else b
+            if k % 5 == 4:
+                r = int(rng.integers(0, 7))
+                vals = [W.jstr("vip") if rng.random() < 0.3 else W.jint(int(rng.integers(0, 4)))
+                        for _ in range(int(rng.integers(1, 3)))]
+                got = _ask(cl, W.encode_param_request(xid, 900 + r, 1, vals))
+                keys = np.array([interner.key(900 + r, v) for v in vals], dtype=np.uint64)
+                s, rem = orc.param_multi_replay(np.array([r if r < 6 else -1], np.int32), np.ones(1, np.int32),
+                                                np.array([now[0]], np.int64), np.zeros(1, np.int32),
+                                                np.array([len(vals)], np.int32), keys)
+                assert got == (xid, 2, int(s[0]), (int(rem[0]), 0)), (k, got, s, rem)
+            else:
+                fid = int(rules.flow_id[int(rng.integers(0, F))]) if k % 37 else -5
+                acq = int(rng.integers(0, 3))
+                prio = bool(rng.random() < 0.1)
+                got = _ask(cl, W.encode_flow_request(xid, fid, acq, prio))
+                idx = np.array([fid_to_idx.get(fid, -2 if fid <= 0 else -1)], np.int32)
+                s, rem, wt = orc.replay(idx, np.array([acq], np.int32), np.array([now[0]], np.int64),
+                                        np.array([1 if prio else 0], np.uint8))
+                assert got == (xid, 1, int(s[0]), (int(rem[0]), int(wt[0]))), (k, got, s, rem, wt)
+        st = server.stats()
+        assert st["connections"] == 2 and st["flow_requests"] == 400 and st["param_requests"] == 100
+        a.close()
+        b.close()
+    finally:
+        server.stop()
+        interner.close()
+
+
+@pytest.mark.gpu
+def test_native_server_pipelined_clients():
+    """Many connections with deep pipelines: every request answered exactly once with its own xid,
+    statuses OK / BLOCKED / SHOULD_WAIT only, and a flow's passes within one second never exceed its
+    count (the server clock is frozen, so every request lands in one window)."""
+    import sentinel_amd as sa
+    from sentinel_amd.token_service import ServerNamespace
+    F = 50
+    rules, _ = T.config2(1, seed=63, n_flows=F)
+    rules.count[:] = 40
+    svc = sa.GpuTokenService(0)
+    svc.set_namespaces([ServerNamespace(connected_count=1)])
+    svc.load_rules_array(rules.flow_id, rules.count, rules.threshold_type, rules.sample_count,
+                         rules.window_interval_ms, rules.namespace, rules.checker)
+    server = W.NativeTokenServer(svc, ["default"], clock=lambda: T.T0_ALIGNED + 500, io_threads=3)
+    n_clients, per_client = 8, 2000
+    passes = np.zeros(F, np.int64)
+    lock = threading.Lock()
+    errors = []
+
+    def client(c):
+        try:
+            cl = W.TokenClient("127.0.0.1", server.port)
+            r = np.random.default_rng(200 + c)
+            fids = r.integers(0, F, size=per_client)
+            buf = b"".join(W.encode_flow_request(1 + k, int(rules.flow_id[fids[k]]), 1) for k in range(per_client))
+            cl.send(buf)
+            seen = {}
+            while len(seen) < per_client:
+                xid, typ, status, data = cl.recv()
+                assert typ == 1 and xid not in seen and 1 <= xid <= per_client
+                seen[xid] = status
+            local = np.zeros(F, np.int64)
+            for xid, status in seen.items():
+                assert status in (0, 1)
+                if status == 0:
+                    local[fids[xid - 1]] += 1
+            with lock:
+                passes[:] += local
+            cl.close()
+        except Exception as ex:        # surfaced below
+            errors.append(ex)
+
+    th = [threading.Thread(target=client, args=(c,)) for c in range(n_clients)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    st = server.stats()
+    server.stop()
+    assert not errors, errors
+    assert st["flow_requests"] == n_clients * per_client
+    assert (passes <= 40).all() and passes.sum() == 40 * F        # every flow saturates exactly
