@@ -5,7 +5,9 @@ FETCH_SIZE / WRITE_SIZE are KiB per dispatch; on gfx950 FETCH_SIZE reports half 
 wide coalesced read, so it is doubled.  Output: JSON with, per kernel symbol, the dispatch count and
 the mean corrected read / write bytes per dispatch (the `traffic` of bench.py's roofline).
 
-usage: python scripts/pmc_summary.py <dir holding pmc_fetch/ and pmc_write/>
+usage: python scripts/pmc_summary.py <dir holding pmc_fetch/ and pmc_write/> [bench.json]
+With the bench JSON line of one of the passes, the summary records its workload `shape` (the keys
+bench.py matches before it quotes the traffic of a kernel: config, flows, events, sample_count).
 """
 import csv
 import glob
@@ -47,9 +49,14 @@ def main():
         wb = 1024.0 * sum(w) / len(w) if w else None
         out[k] = {"dispatches": max(len(f), len(w)), "read_bytes_avg": fb, "write_bytes_avg": wb,
                   "traffic_bytes_avg": (fb or 0.0) + (wb or 0.0)}
-    json.dump({"correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count), WRITE_SIZE KiB x1024",
-               "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate runs of bench.py --steps 3 --warmup 1",
-               "kernels": out}, sys.stdout, indent=1)
+    doc = {"correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count), WRITE_SIZE KiB x1024",
+           "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate runs of bench.py --steps 3 --warmup 1",
+           "kernels": out}
+    if len(sys.argv) > 2:
+        with open(sys.argv[2]) as f:
+            cfg = json.loads(f.read().strip().splitlines()[-1])["config"]
+        doc["shape"] = {k: cfg[k] for k in ("config", "flows", "events", "sample_count")}
+    json.dump(doc, sys.stdout, indent=1)
 
 
 if __name__ == "__main__":

@@ -157,6 +157,14 @@ struct BatchWork {
 __device__ inline uint64_t pack_verdict(int status, int32_t remaining, int wait) {
     return (uint64_t)(uint32_t)remaining | ((uint64_t)(uint16_t)(int16_t)status << 32) | ((uint64_t)(uint16_t)wait << 48);
 }
+// A verdict store to its arrival position (random 8-byte writes over the whole output).
+__device__ inline void store_verdict(uint64_t *out, uint32_t seq, uint64_t v) {
+#ifdef SENTINEL_NT_VERDICT
+    __builtin_nontemporal_store(v, out + seq);
+#else
+    out[seq] = v;
+#endif
+}
 __device__ inline void put_verdict(uint64_t *out, uint32_t seq, int status, int32_t remaining, int wait) {
     out[seq] = pack_verdict(status, remaining, wait);
 }

@@ -579,7 +579,7 @@ __device__ inline void part_run_w(FlowWindow<NMAX> &fw, const KeyTable &T, uint3
                 if (acc == 0x123456789ull) V.out[0] = acc;
             }
 #else
-            for (uint32_t k = 0; k < len; ++k) V.out[(uint32_t)s_val[q + k] & SEQ_MASK] = fw.verdict(s0, a, K, k, small);
+            for (uint32_t k = 0; k < len; ++k) store_verdict(V.out, (uint32_t)s_val[q + k] & SEQ_MASK, fw.verdict(s0, a, K, k, small));
 #endif
 #endif
         }
@@ -675,7 +675,7 @@ __device__ inline bool part_run_single(FlowWindow<NMAX> &fw, const uint64_t *s_v
     for (uint32_t k = 0; k < len; ++k) V.out[(blockIdx.x * blockDim.x + threadIdx.x) * 8 + (k & 7)] = fw.verdict(s0, a, K, k, small);
 #else
     for (uint32_t k = 0; k < len; ++k)
-        V.out[(uint32_t)s_val[q0 + k] & SEQ_MASK] = fw.verdict(s0, a, K, k, small);
+        store_verdict(V.out, (uint32_t)s_val[q0 + k] & SEQ_MASK, fw.verdict(s0, a, K, k, small));
 #endif
     return true;
 }
@@ -741,7 +741,7 @@ __device__ inline void part_run_defer(FlowWindow<NMAX> &fw, const KeyTable &T, u
                 reco[si] = K | (small ? COOP_SMALL : 0u);
                 ao[si] = a;
             } else {
-                for (uint32_t k = 0; k < len; ++k) V.out[(uint32_t)s_val[q + k] & SEQ_MASK] = fw.verdict(s0, a, K, k, small);
+                for (uint32_t k = 0; k < len; ++k) store_verdict(V.out, (uint32_t)s_val[q + k] & SEQ_MASK, fw.verdict(s0, a, K, k, small));
             }
         }
         if (si == 0) len1 = q2 - q0;
@@ -1613,9 +1613,9 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
             const uint32_t sg = k < l1 ? 0u : 1u;
             const uint32_t rec = c_K[sg * CF + kj];
             if (rec & COOP_SKIP) continue;                        // sequential segment: written by the walk
-            V.out[(uint32_t)v & SEQ_MASK] = run_verdict(c_thr[kj], c_is[kj], c_s0[sg * CF + kj], c_a[sg * CF + kj],
-                                                        rec & (COOP_SMALL - 1u), sg ? k - l1 : k,
-                                                        (rec & COOP_SMALL) != 0);
+            store_verdict(V.out, (uint32_t)v & SEQ_MASK,
+                          run_verdict(c_thr[kj], c_is[kj], c_s0[sg * CF + kj], c_a[sg * CF + kj],
+                                      rec & (COOP_SMALL - 1u), sg ? k - l1 : k, (rec & COOP_SMALL) != 0));
         }
     } else if (c > 0 && c <= LONG_RUN && !part_run_single<NMAX>(fw, sv, start, start + c, src, V, T0)) {
         fw.load_header(T0);
