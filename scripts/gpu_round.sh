@@ -1,7 +1,8 @@
-# Full GPU round check on one MI355X: parity tests, bench, rocprofv3 kernel stats, and the two
-# PMC passes (FETCH_SIZE, WRITE_SIZE: separate runs, as MI355X_MICROARCH.md prescribes).
+# Full GPU round check on one MI355X: parity tests, bench, rocprofv3 kernel stats, and the PMC
+# traffic of the bench's own shape (scripts/gpu_pmc_shape.sh: separate FETCH_SIZE / WRITE_SIZE runs,
+# as MI355X_MICROARCH.md prescribes, summarised into profiles/pmc/<TAG>_c3.json).
 # Every GPU step has its own time limit; the chain stops at the first failure.
-# Usage (from gpurun): bash scripts/gpu_round.sh [TAG]   -> results under gpurun_out/$TAG
+# Usage (from gpurun): bash scripts/gpu_round.sh [TAG] [--shapes]   -> results under gpurun_out/$TAG
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 TAG=${1:-round}
@@ -16,20 +17,18 @@ tail -3 $O/gpu_tests.log
 echo "== bench"
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
-echo "== per-rank shapes of the scaling bench (1M / N flows per rank, 8M events)"
-for F in 500000 250000 125000; do
-  timeout -k 10 180 python -u bench.py --flows $F --steps 20 --warmup 3 --no-cpu-baseline --no-host-path > $O/bench_flows_$F.json 2> $O/bench_flows_$F.err || { tail -20 $O/bench_flows_$F.err; exit 1; }
-done
-python -c "import json; print(json.dumps({F: {k: json.load(open('$O/bench_flows_%d.json' % F))[k] for k in ('value', 'p99_batch_ms', 'kernels')} for F in (500000, 250000, 125000)}))" > $O/rank_shapes.json && cat $O/rank_shapes.json
+if [ "$2" = "--shapes" ]; then
+  echo "== per-rank shapes of the scaling bench (1M / N flows per rank, 8M events)"
+  for F in 500000 250000 125000; do
+    timeout -k 10 180 python -u bench.py --flows $F --steps 20 --warmup 3 --no-cpu-baseline --no-host-path > $O/bench_flows_$F.json 2> $O/bench_flows_$F.err || { tail -20 $O/bench_flows_$F.err; exit 1; }
+  done
+  python -c "import json; print(json.dumps({F: {k: json.load(open('$O/bench_flows_%d.json' % F))[k] for k in ('value', 'p99_batch_ms', 'kernels')} for F in (500000, 250000, 125000)}))" > $O/rank_shapes.json && cat $O/rank_shapes.json
+fi
 echo "== rocprof stats"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-path > $O/bench_prof.json 2> $O/prof.err || { tail -20 $O/prof.err; exit 1; }
-echo "== pmc FETCH_SIZE"
-timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-host-path > /dev/null 2> $O/pmc_fetch.err || { tail -20 $O/pmc_fetch.err; exit 1; }
-echo "== pmc WRITE_SIZE"
-timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-host-path > /dev/null 2> $O/pmc_write.err || { tail -20 $O/pmc_write.err; exit 1; }
 cd $R
-python scripts/pmc_summary.py $O > $O/pmc_summary.json && cat $O/pmc_summary.json
-# rocprof launches of each kernel split into the bench phases (the host-path batches share the kernels)
 python scripts/trace_summary.py $O/prof/run_kernel_trace.csv warmup:2,profile:3,timed:10 > $O/kernel_trace_summary.json
+echo "== pmc (bench shape)"
+bash scripts/gpu_pmc_shape.sh ${TAG}_c3 || exit 1
 echo "ROUND OK"
