@@ -360,6 +360,74 @@ int  sentinel_local_node_metrics(sentinel_engine_t *eng, int32_t resource_idx, i
 /* SentinelConfig.statisticMaxRt (default 5000 ms): a fresh bucket's minRt. */
 int  sentinel_set_statistic_max_rt(sentinel_engine_t *eng, int64_t max_rt_ms);
 
+/* ---- local rule graph: FlowRuleChecker with every limitApp and strategy ----
+ * Replaces FlowSlot -> FlowRuleChecker.checkFlow / selectNodeByRequesterAndStrategy /
+ * selectReferenceNode (sentinel-core/.../slots/block/flow/FlowRuleChecker.java:44-145) over the nodes
+ * the slot chain builds: a ClusterNode per resource, created by the resource's first entry
+ * (ClusterBuilderSlot.java:74-92); an origin StatisticNode per (resource, origin)
+ * (ClusterNode.getOrCreateOriginNode, ClusterNode.java:101-118); a DefaultNode per (context, resource)
+ * (NodeSelectorSlot) whose thread / pass / block / RT / exception booking also reaches the ClusterNode
+ * (DefaultNode.java:110-143).  Rule selection (limitApp, STRATEGY_DIRECT / RELATE / CHAIN):
+ *   limitApp == origin (not "default" / "other"): DIRECT -> origin node, else the reference node
+ *   limitApp "default":                            DIRECT -> ClusterNode, else the reference node
+ *   limitApp "other", origin matched by no rule of the resource (FlowRuleManager.isOtherOrigin):
+ *                                                  DIRECT -> origin node, else the reference node
+ *   reference node: RELATE -> the refResource's ClusterNode (none before its first entry),
+ *                   CHAIN  -> this DefaultNode iff the context name is refResource;  no node -> pass.
+ * The caller interns strings: origin / limitApp ids 0 = "default", 1 = "other", >= 2 any other name,
+ * -1 = "" (no origin; as a limitApp: blank -> "default"); context-name ids are the CHAIN refResource
+ * ids; node indices are the caller's dense numbering of (resource, origin) and (context, resource). */
+#define SENTINEL_LIMIT_APP_DEFAULT  0
+#define SENTINEL_LIMIT_APP_OTHER    1
+#define SENTINEL_STRATEGY_DIRECT    0
+#define SENTINEL_STRATEGY_RELATE    1
+#define SENTINEL_STRATEGY_CHAIN     2
+#define SENTINEL_GRADE_THREAD       0
+#define SENTINEL_GRADE_QPS          1
+#define SENTINEL_NODE_CLUSTER       0
+#define SENTINEL_NODE_ORIGIN        1
+#define SENTINEL_NODE_DEFAULT       2
+typedef struct {
+    int32_t resource;    /* FlowRule.resource as a resource index */
+    int32_t grade;       /* SENTINEL_GRADE_* (FlowRule.grade) */
+    double  count;
+    int32_t strategy;    /* SENTINEL_STRATEGY_* */
+    int32_t limit_app;   /* limitApp id (see above) */
+    int32_t ref;         /* RELATE: refResource index, CHAIN: refResource context id, -1 blank */
+    int32_t reserved;
+} sentinel_local_rule_t;           /* 32 bytes */
+typedef struct {
+    int32_t origin;        /* context origin id, -1 = "" */
+    int32_t origin_node;   /* index of the (resource, origin) node; ignored when origin == -1 */
+    int32_t context;       /* context-name id */
+    int32_t default_node;  /* index of the (context, resource) DefaultNode */
+} sentinel_local_ctx_t;            /* 16 bytes, one per event */
+/* Loads FlowRuleManager.loadRules' rules (DefaultController, controlBehavior default): invalid ones
+ * dropped as FlowRuleUtil.isValidRule (count < 0, grade not QPS / THREAD, a QPS RELATE / CHAIN rule
+ * with a blank refResource; FlowRuleUtil.java:167-238), duplicates dropped (buildFlowRuleMap's
+ * HashSet), then FlowRuleComparator's stable sort (non-"default" limitApps first,
+ * FlowRuleComparator.java:30-55): pass each resource's rules in FlowRuleManager's order.  Every node
+ * (n_res ClusterNodes, n_origin_nodes, n_default_nodes) starts empty and no ClusterNode exists yet.
+ * The node windows are SampleCountProperty x IntervalProperty as sentinel_load_local_resources. */
+int  sentinel_load_local_rules(sentinel_engine_t *eng, const sentinel_local_rule_t *rules, int32_t n, int32_t n_res,
+                               int32_t n_origin_nodes, int32_t n_default_nodes, int32_t sample_count,
+                               int32_t interval_ms);
+/* A batch of SphU.entry / Entry.exit events with their contexts (flags and rt_ms as
+ * sentinel_submit_local_batch): every rule checked in order on its selected node (DefaultController,
+ * the prioritized occupy path included), then StatisticSlot's booking on the DefaultNode (+ the
+ * ClusterNode) and the origin node (StatisticSlot.java:55-164; the global ENTRY_NODE of EntryType.IN,
+ * read only by SystemSlot, is not kept).  A bad resource or node index answers NO_RULE_EXISTS, ts < 0
+ * FAIL.  Resources joined by RELATE rules are decided in one arrival-ordered pass. */
+int  sentinel_submit_local_graph_batch(sentinel_engine_t *eng, int64_t n, const sentinel_event_t *events,
+                                       const sentinel_local_ctx_t *ctx, const uint8_t *flags, const int64_t *rt_ms,
+                                       sentinel_verdict_t *verdicts, void *stream);
+int  sentinel_submit_local_graph_batch_host(sentinel_engine_t *eng, int64_t n, const sentinel_event_t *events,
+                                            const sentinel_local_ctx_t *ctx, const uint8_t *flags,
+                                            const int64_t *rt_ms, sentinel_verdict_t *verdicts);
+/* sentinel_local_node_metrics of any node: kind SENTINEL_NODE_CLUSTER (resource index),
+ * SENTINEL_NODE_ORIGIN, SENTINEL_NODE_DEFAULT. */
+int  sentinel_local_graph_node_metrics(sentinel_engine_t *eng, int32_t kind, int32_t idx, int64_t ts, int64_t *out14);
+
 /* ---- cluster concurrency tokens (thread grade): TokenService.requestConcurrentToken /
  *      releaseConcurrentToken (TokenService.java:56,62) -> ConcurrentClusterFlowChecker
  *      (sentinel-cluster/.../cluster/flow/ConcurrentClusterFlowChecker.java:48-101) ---- */

@@ -123,6 +123,12 @@ def lib():
         "orc_local_entry_ex": (C.c_int, [vp, dbl, dbl, C.c_int, C.c_int, C.c_int, i64, vp]),
         "orc_local_exit": (None, [vp, C.c_int, i64, C.c_int, i64]),
         "orc_node_metrics": (None, [vp, i64, vp]),
+        "orc_lgraph_new": (vp, [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+        "orc_lgraph_free": (None, [vp]),
+        "orc_lgraph_set_occupy_timeout": (None, [vp, C.c_int]),
+        "orc_lgraph_n_rules": (C.c_int, [vp, C.c_int]),
+        "orc_lgraph_replay": (None, [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "orc_lgraph_node_metrics": (C.c_int, [vp, C.c_int, C.c_int, i64, vp]),
         "orc_node_waiting": (i64, [vp, i64]),
         "orc_node_minute_occupied": (i64, [vp, i64]),
         "orc_node_try_occupy_next": (i64, [vp, i64, C.c_int, dbl]),
@@ -589,3 +595,43 @@ class TokenServiceOracle:
 
     def limiter_sum(self, ns, t):
         return lib().orc_engine_limiter_sum(self.h, ns, t)
+
+
+class LocalGraph:
+    """orc_lgraph: FlowRuleChecker node selection over ClusterNode / origin / DefaultNode
+    (FlowRuleChecker.java:44-145, StatisticSlot.java:55-164)."""
+
+    RULE_DTYPE = np.dtype([("resource", "<i4"), ("grade", "<i4"), ("count", "<f8"), ("strategy", "<i4"),
+                           ("limit_app", "<i4"), ("ref", "<i4"), ("reserved", "<i4")])
+    CTX_DTYPE = np.dtype([("origin", "<i4"), ("origin_node", "<i4"), ("context", "<i4"), ("default_node", "<i4")])
+
+    def __init__(self, rules, n_res, n_origin_nodes, n_default_nodes, sample_count=2, interval_ms=1000):
+        arr = np.ascontiguousarray(rules, dtype=self.RULE_DTYPE)
+        self.h = lib().orc_lgraph_new(_p(arr) if len(arr) else None, len(arr), n_res, n_origin_nodes,
+                                      n_default_nodes, sample_count, interval_ms)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_lgraph_free(self.h)
+            self.h = None
+
+    def set_occupy_timeout(self, ms): lib().orc_lgraph_set_occupy_timeout(self.h, ms)
+    def n_rules(self, res): return lib().orc_lgraph_n_rules(self.h, res)
+
+    def replay(self, res, acquire, ts, ctx, flags=None, rt=None):
+        res = np.ascontiguousarray(res, dtype=np.int32)
+        acquire = np.ascontiguousarray(acquire, dtype=np.int32)
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        cx = np.ascontiguousarray(ctx, dtype=self.CTX_DTYPE)
+        fl = None if flags is None else np.ascontiguousarray(flags, dtype=np.uint8)
+        r = None if rt is None else np.ascontiguousarray(rt, dtype=np.int64)
+        st = np.zeros(len(res), dtype=np.int8)
+        wait = np.zeros(len(res), dtype=np.int32)
+        lib().orc_lgraph_replay(self.h, len(res), _p(res), _p(acquire), _p(ts), _p(cx), _p(fl), _p(r), _p(st), _p(wait))
+        return st, wait.astype(np.int64)
+
+    def node_metrics(self, kind, idx, t) -> np.ndarray:
+        out = np.zeros(14, dtype=np.int64)
+        if lib().orc_lgraph_node_metrics(self.h, kind, idx, t, _p(out)) != 0:
+            raise IndexError("bad node")
+        return out

@@ -1232,6 +1232,212 @@ int64_t orc_node_sec_values(orc_stat_node *nd, int64_t t, int64_t *sum) {
     return k;
 }
 
+/* ------------------------------------------------------------------ local rule graph (a9) */
+/* FlowRuleChecker with every limitApp / strategy (FRC:44-145) over the node graph the slot chain
+ * builds: a ClusterNode per resource (created by its first entry, ClusterBuilderSlot.java:74-92), an
+ * origin StatisticNode per (resource, origin) (ClusterNode.getOrCreateOriginNode, set when the
+ * context's origin is non-empty: CBS:97-100), a DefaultNode per (context, resource) whose
+ * increaseThreadNum / addPassRequest / increaseBlockQps / addRtAndSuccess / decreaseThreadNum /
+ * increaseExceptionQps also reach the ClusterNode (DefaultNode.java:110-143).  Rules of a resource
+ * are checked in list order after FlowRuleUtil.buildFlowRuleMap's stable FlowRuleComparator sort
+ * (non-"default" limitApps first, FlowRuleComparator.java:30-55; the caller passes FlowRuleManager's
+ * order), invalid ones dropped (FlowRuleUtil.isValidRule:167-238). */
+struct orc_lgraph {
+    int n_res, n_on, n_dn;
+    orc_stat_node **cn, **on, **dn;
+    uint8_t *created;          /* ClusterNode exists (ClusterBuilderSlot.clusterNodeMap) */
+    int32_t *roff;             /* rules of resource r: rules[roff[r] .. roff[r + 1]) */
+    orc_local_rule *rules;
+};
+
+static int lrule_valid(const orc_local_rule *r, int n_res) {
+    if (r->resource < 0 || r->resource >= n_res || !(r->count >= 0) || r->strategy < 0) return 0;  /* FRU:168-169 */
+    if (r->grade == 1) {                                       /* QPS: checkStrategyField (FRU:233-238) */
+        if (r->strategy > 2) return 1;                         /* unknown strategy: valid, selects no node */
+        return r->strategy == 0 || r->ref >= 0;
+    }
+    return r->grade == 0;                                      /* THREAD: checkClusterConcurrentField only */
+}
+
+orc_lgraph *orc_lgraph_new(const orc_local_rule *rules, int n, int n_res, int n_origin_nodes, int n_default_nodes,
+                           int sample_count, int interval_ms) {
+    orc_lgraph *g = (orc_lgraph *)calloc(1, sizeof(*g));
+    g->n_res = n_res; g->n_on = n_origin_nodes; g->n_dn = n_default_nodes;
+    g->cn = (orc_stat_node **)calloc((size_t)(n_res > 0 ? n_res : 1), sizeof(void *));
+    g->on = (orc_stat_node **)calloc((size_t)(n_origin_nodes > 0 ? n_origin_nodes : 1), sizeof(void *));
+    g->dn = (orc_stat_node **)calloc((size_t)(n_default_nodes > 0 ? n_default_nodes : 1), sizeof(void *));
+    for (int i = 0; i < n_res; i++) g->cn[i] = orc_node_new(sample_count, interval_ms);
+    for (int i = 0; i < n_origin_nodes; i++) g->on[i] = orc_node_new(sample_count, interval_ms);
+    for (int i = 0; i < n_default_nodes; i++) g->dn[i] = orc_node_new(sample_count, interval_ms);
+    g->created = (uint8_t *)calloc((size_t)(n_res > 0 ? n_res : 1), 1);
+    g->roff = (int32_t *)calloc((size_t)n_res + 1, sizeof(int32_t));
+    g->rules = (orc_local_rule *)calloc((size_t)(n > 0 ? n : 1), sizeof(orc_local_rule));
+    /* per resource: valid rules in the given order, duplicates dropped (the HashSet), then the stable
+     * comparator sort: every non-"default" limitApp before the "default" ones */
+    int k = 0;
+    for (int r = 0; r < n_res; r++) {
+        g->roff[r] = k;
+        for (int pass = 0; pass < 2; pass++)
+            for (int i = 0; i < n; i++) {
+                const orc_local_rule *x = &rules[i];
+                if (x->resource != r || !lrule_valid(x, n_res)) continue;
+                const int lim = x->limit_app < 0 ? ORC_LIMIT_APP_DEFAULT : x->limit_app;   /* blank -> default */
+                if ((lim == ORC_LIMIT_APP_DEFAULT) != (pass == 1)) continue;
+                int dup = 0;
+                for (int j = g->roff[r]; j < k && !dup; j++)
+                    dup = g->rules[j].grade == x->grade && g->rules[j].count == x->count &&
+                          g->rules[j].strategy == x->strategy && g->rules[j].limit_app == lim && g->rules[j].ref == x->ref;
+                if (dup) continue;
+                g->rules[k] = *x;
+                g->rules[k].limit_app = lim;
+                k++;
+            }
+    }
+    g->roff[n_res] = k;
+    return g;
+}
+
+void orc_lgraph_free(orc_lgraph *g) {
+    if (!g) return;
+    for (int i = 0; i < g->n_res; i++) orc_node_free(g->cn[i]);
+    for (int i = 0; i < g->n_on; i++) orc_node_free(g->on[i]);
+    for (int i = 0; i < g->n_dn; i++) orc_node_free(g->dn[i]);
+    free(g->cn); free(g->on); free(g->dn); free(g->created); free(g->roff); free(g->rules); free(g);
+}
+
+void orc_lgraph_set_occupy_timeout(orc_lgraph *g, int ms) {
+    for (int i = 0; i < g->n_res; i++) orc_node_set_occupy_timeout(g->cn[i], ms);
+    for (int i = 0; i < g->n_on; i++) orc_node_set_occupy_timeout(g->on[i], ms);
+    for (int i = 0; i < g->n_dn; i++) orc_node_set_occupy_timeout(g->dn[i], ms);
+}
+
+int orc_lgraph_n_rules(const orc_lgraph *g, int res) { return g->roff[res + 1] - g->roff[res]; }
+
+/* FlowRuleManager.isOtherOrigin (FlowRuleManager.java:113-129) */
+static int lgraph_other_origin(const orc_lgraph *g, int res, int origin) {
+    if (origin < 0) return 0;                                  /* StringUtil.isEmpty(origin) */
+    for (int j = g->roff[res]; j < g->roff[res + 1]; j++)
+        if (g->rules[j].limit_app == origin) return 0;
+    return 1;
+}
+
+/* FRC:87-103 selectReferenceNode */
+static orc_stat_node *lgraph_ref_node(const orc_lgraph *g, const orc_local_rule *r, const orc_local_ctx *c) {
+    if (r->ref < 0) return NULL;                               /* StringUtil.isEmpty(refResource) */
+    if (r->strategy == ORC_STRATEGY_RELATE)                    /* ClusterBuilderSlot.getClusterNode(ref) */
+        return r->ref < g->n_res && g->created[r->ref] ? g->cn[r->ref] : NULL;
+    if (r->strategy == ORC_STRATEGY_CHAIN) return r->ref == c->context ? g->dn[c->default_node] : NULL;
+    return NULL;
+}
+
+/* FRC:110-145 selectNodeByRequesterAndStrategy; filterOrigin: the origin is neither "default" nor
+ * "other" (the interned ids 0 and 1) */
+static orc_stat_node *lgraph_select(const orc_lgraph *g, int res, const orc_local_rule *r, const orc_local_ctx *c) {
+    const int origin = c->origin;
+    orc_stat_node *onode = origin >= 0 ? g->on[c->origin_node] : NULL;
+    if (r->limit_app == origin && origin >= 2) {
+        if (r->strategy == ORC_STRATEGY_DIRECT) return onode;
+        return lgraph_ref_node(g, r, c);
+    } else if (r->limit_app == ORC_LIMIT_APP_DEFAULT) {
+        if (r->strategy == ORC_STRATEGY_DIRECT) return g->cn[res];
+        return lgraph_ref_node(g, r, c);
+    } else if (r->limit_app == ORC_LIMIT_APP_OTHER && lgraph_other_origin(g, res, origin)) {
+        if (r->strategy == ORC_STRATEGY_DIRECT) return onode;
+        return lgraph_ref_node(g, r, c);
+    }
+    return NULL;
+}
+
+/* One SphU.entry(resource) in context c: ClusterBuilderSlot (node creation), FlowSlot (every rule in
+ * order, DefaultController.canPass on the selected node, DC:49-69), StatisticSlot.entry's booking on
+ * the DefaultNode (+ ClusterNode) and the origin node (SS:55-116).  1 pass, 0 block; *wait as
+ * orc_local_entry_ex. */
+int orc_lgraph_entry(orc_lgraph *g, int res, int acquire, int prioritized, int64_t t, const orc_local_ctx *c,
+                     int64_t *wait) {
+    *wait = 0;
+    g->created[res] = 1;
+    orc_stat_node *dn = g->dn[c->default_node], *cn = g->cn[res];
+    orc_stat_node *on = c->origin >= 0 ? g->on[c->origin_node] : NULL;
+    int blocked = 0, occupied = 0;
+    for (int j = g->roff[res]; j < g->roff[res + 1] && !blocked && !occupied; j++) {
+        const orc_local_rule *r = &g->rules[j];
+        orc_stat_node *nd = lgraph_select(g, res, r, c);
+        if (!nd) continue;                                     /* FRC:78-81 no node -> pass */
+        const int32_t cur = r->grade == 0 ? (int32_t)nd->threads : orc_java_d2i(orc_node_pass_qps(nd, t));
+        if (!((double)(int32_t)((uint32_t)cur + (uint32_t)acquire) > r->count)) continue;
+        if (prioritized && r->grade == 1) {                    /* DC:52-64 */
+            const int64_t w = orc_node_try_occupy_next(nd, t, acquire, r->count);
+            if (w < nd->occupy_timeout) {
+                orc_node_add_waiting(nd, t + w, acquire);
+                orc_node_add_occupied_pass(nd, t, acquire);
+                *wait = w;
+                occupied = 1;                                  /* PriorityWaitException */
+                continue;
+            }
+        }
+        blocked = 1;
+    }
+    if (blocked) {                                             /* SS:96-104 */
+        orc_node_increase_block_qps(dn, t, acquire);
+        orc_node_increase_block_qps(cn, t, acquire);
+        if (on) orc_node_increase_block_qps(on, t, acquire);
+        return 0;
+    }
+    dn->threads = wrap_add64(dn->threads, 1);                  /* SS:62-69 / 81-86 */
+    cn->threads = wrap_add64(cn->threads, 1);
+    if (!occupied) {
+        orc_node_add_pass_request(dn, t, acquire);
+        orc_node_add_pass_request(cn, t, acquire);
+    }
+    if (on) {
+        on->threads = wrap_add64(on->threads, 1);
+        if (!occupied) orc_node_add_pass_request(on, t, acquire);
+    }
+    return 1;
+}
+
+/* Entry.exit of a passed entry (SS:126-164): recordCompleteFor(DefaultNode) -- which also books the
+ * ClusterNode -- then recordCompleteFor(origin node). */
+void orc_lgraph_exit(orc_lgraph *g, int res, int count, int64_t rt, int error, int64_t t, const orc_local_ctx *c) {
+    orc_local_exit(g->dn[c->default_node], count, rt, error, t);
+    orc_local_exit(g->cn[res], count, rt, error, t);
+    if (c->origin >= 0) orc_local_exit(g->on[c->origin_node], count, rt, error, t);
+}
+
+/* Arrival-order replay of a batch (flags: bit 0 prioritized, bit 1 exit, bit 2 error); status OK /
+ * BLOCKED, NO_RULE_EXISTS for an unknown resource or node index, FAIL for t < 0 (as the GPU path). */
+void orc_lgraph_replay(orc_lgraph *g, int64_t n, const int32_t *res, const int32_t *acquire, const int64_t *ts,
+                       const orc_local_ctx *ctx, const uint8_t *flags, const int64_t *rt, int8_t *status,
+                       int32_t *wait) {
+    for (int64_t i = 0; i < n; i++) {
+        const orc_local_ctx *c = &ctx[i];
+        wait[i] = 0;
+        if (res[i] < 0 || res[i] >= g->n_res || c->default_node < 0 || c->default_node >= g->n_dn ||
+            (c->origin >= 0 && (c->origin_node < 0 || c->origin_node >= g->n_on))) { status[i] = 3; continue; }
+        if (ts[i] < 0) { status[i] = -1; continue; }
+        const uint8_t f = flags ? flags[i] : 0;
+        if (f & 2) {
+            orc_lgraph_exit(g, res[i], acquire[i], rt ? rt[i] : 0, (f & 4) != 0, ts[i], c);
+            status[i] = 0;
+            continue;
+        }
+        int64_t w;
+        status[i] = orc_lgraph_entry(g, res[i], acquire[i], f & 1, ts[i], c, &w) ? 0 : 1;
+        wait[i] = (int32_t)w;
+    }
+}
+
+/* orc_node_metrics of node `idx` of kind 0 ClusterNode, 1 origin node, 2 DefaultNode */
+int orc_lgraph_node_metrics(orc_lgraph *g, int kind, int idx, int64_t t, int64_t *out14) {
+    orc_stat_node *nd = NULL;
+    if (kind == 0 && idx >= 0 && idx < g->n_res) nd = g->cn[idx];
+    if (kind == 1 && idx >= 0 && idx < g->n_on) nd = g->on[idx];
+    if (kind == 2 && idx >= 0 && idx < g->n_dn) nd = g->dn[idx];
+    if (!nd) return -1;
+    orc_node_metrics(nd, t, out14);
+    return 0;
+}
+
 /* ------------------------------------------------------------------ local param token bucket */
 /* PFC:127-202 passDefaultLocalCheck, single-threaded (every CAS succeeds). The two CacheMaps are
  * ParameterMetric's ruleTokenCounter / ruleTimeCounter (ParameterMetric.java:95-118); LRU

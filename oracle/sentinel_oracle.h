@@ -236,6 +236,39 @@ void orc_lparam_replay_ex(orc_local_engine *e, int64_t n, const int32_t *rule_id
                           int64_t n_values, const uint8_t *kinds, int8_t *status);
 int  orc_lparam_thread_count(orc_local_engine *e, int32_t idx, uint64_t key);
 
+/* ---------------- local rule graph: FlowRuleChecker limitApp / strategy node selection ---------------- */
+/* Mirrors include/sentinel_amd.h's sentinel_local_rule_t / sentinel_local_ctx_t. */
+enum { ORC_LIMIT_APP_DEFAULT = 0, ORC_LIMIT_APP_OTHER = 1 };
+enum { ORC_STRATEGY_DIRECT = 0, ORC_STRATEGY_RELATE = 1, ORC_STRATEGY_CHAIN = 2 };
+typedef struct {
+    int32_t resource;
+    int32_t grade;        /* 1 QPS, 0 THREAD */
+    double  count;
+    int32_t strategy;     /* 0 DIRECT, 1 RELATE, 2 CHAIN */
+    int32_t limit_app;    /* 0 "default", 1 "other", >= 2 an origin id; < 0 blank (-> default) */
+    int32_t ref;          /* RELATE: resource index, CHAIN: context id; -1 blank refResource */
+    int32_t reserved;
+} orc_local_rule;
+typedef struct {
+    int32_t origin;       /* -1 "" (no origin), 0 "default", 1 "other", >= 2 other names */
+    int32_t origin_node;  /* index of ClusterNode(resource).originCountMap[origin] */
+    int32_t context;      /* context-name id */
+    int32_t default_node; /* index of the DefaultNode of (context, resource) */
+} orc_local_ctx;
+typedef struct orc_lgraph orc_lgraph;
+orc_lgraph *orc_lgraph_new(const orc_local_rule *rules, int n, int n_res, int n_origin_nodes, int n_default_nodes,
+                           int sample_count, int interval_ms);
+void orc_lgraph_free(orc_lgraph *g);
+void orc_lgraph_set_occupy_timeout(orc_lgraph *g, int ms);
+int  orc_lgraph_n_rules(const orc_lgraph *g, int res);
+int  orc_lgraph_entry(orc_lgraph *g, int res, int acquire, int prioritized, int64_t t, const orc_local_ctx *c,
+                      int64_t *wait);
+void orc_lgraph_exit(orc_lgraph *g, int res, int count, int64_t rt, int error, int64_t t, const orc_local_ctx *c);
+void orc_lgraph_replay(orc_lgraph *g, int64_t n, const int32_t *res, const int32_t *acquire, const int64_t *ts,
+                       const orc_local_ctx *ctx, const uint8_t *flags, const int64_t *rt, int8_t *status,
+                       int32_t *wait);
+int  orc_lgraph_node_metrics(orc_lgraph *g, int kind, int idx, int64_t t, int64_t *out14);
+
 /* ---------------- concurrency tokens (ConcurrentClusterFlowChecker) ---------------- */
 /* Mirrors include/sentinel_amd.h's sentinel_concurrent_event_t (kind 0 acquire, 1 release). */
 typedef struct {

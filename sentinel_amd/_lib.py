@@ -56,6 +56,8 @@ EXPORTS = [
     "sentinel_set_local_param_grades", "sentinel_submit_local_param_batch_ex", "sentinel_submit_local_param_batch_ex_host",
     "sentinel_load_local_resources_ex", "sentinel_submit_local_batch", "sentinel_submit_local_batch_host",
     "sentinel_local_node_metrics", "sentinel_set_statistic_max_rt",
+    "sentinel_load_local_rules", "sentinel_submit_local_graph_batch", "sentinel_submit_local_graph_batch_host",
+    "sentinel_local_graph_node_metrics",
     "sentinel_shard_of", "sentinel_cluster_create", "sentinel_cluster_destroy", "sentinel_cluster_size",
     "sentinel_cluster_engine", "sentinel_cluster_set_server_config", "sentinel_cluster_set_namespaces",
     "sentinel_cluster_set_connected_count", "sentinel_cluster_load_flow_rules", "sentinel_cluster_load_param_rules",
@@ -141,6 +143,13 @@ CONC_EVENT_DTYPE = np.dtype([("flow_idx", "<i4"), ("acquire", "<i4"), ("token_id
                              ("flags", "<u4")])
 CONC_RESULT_DTYPE = np.dtype([("token_id", "<i8"), ("status", "<i4"), ("reserved", "<i4")])
 VERDICT_DTYPE = np.dtype([("remaining", "<i4"), ("status", "<i2"), ("wait_in_ms", "<u2")])
+# sentinel_local_rule_t / sentinel_local_ctx_t (local rule graph)
+LOCAL_RULE_DTYPE = np.dtype([("resource", "<i4"), ("grade", "<i4"), ("count", "<f8"), ("strategy", "<i4"),
+                             ("limit_app", "<i4"), ("ref", "<i4"), ("reserved", "<i4")])
+LOCAL_CTX_DTYPE = np.dtype([("origin", "<i4"), ("origin_node", "<i4"), ("context", "<i4"), ("default_node", "<i4")])
+LIMIT_APP_DEFAULT, LIMIT_APP_OTHER = 0, 1
+STRATEGY_DIRECT, STRATEGY_RELATE, STRATEGY_CHAIN = 0, 1, 2
+NODE_CLUSTER, NODE_ORIGIN, NODE_DEFAULT = 0, 1, 2
 TOP_PARAMS = 5
 PARAM_SNAPSHOT_DTYPE = np.dtype([("flow_id", "<i8"), ("n_top", "<i4"), ("reserved", "<i4"),
                                  ("key", "<u8", (TOP_PARAMS,)), ("avg", "<f8", (TOP_PARAMS,))])
@@ -221,6 +230,10 @@ def load():
         "sentinel_submit_local_batch": (C.c_int, [vp, i64, vp, vp, vp, vp, vp]),
         "sentinel_submit_local_batch_host": (C.c_int, [vp, i64, vp, vp, vp, vp]),
         "sentinel_local_node_metrics": (C.c_int, [vp, i32, i64, vp]),
+        "sentinel_load_local_rules": (C.c_int, [vp, vp, i32, i32, i32, i32, i32, i32]),
+        "sentinel_submit_local_graph_batch": (C.c_int, [vp, i64, vp, vp, vp, vp, vp, vp]),
+        "sentinel_submit_local_graph_batch_host": (C.c_int, [vp, i64, vp, vp, vp, vp, vp]),
+        "sentinel_local_graph_node_metrics": (C.c_int, [vp, i32, i32, i64, vp]),
         "sentinel_set_statistic_max_rt": (C.c_int, [vp, i64]),
         "sentinel_submit_flow_batches": (C.c_int, [vp, i32, vp, vp, vp, vp, vp]),
         "sentinel_profile_every": (C.c_int, [vp, i32]),

@@ -20,6 +20,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <string>
@@ -491,6 +492,10 @@ struct sentinel_engine {
     int32_t occupy_timeout = 500;      // OccupyTimeoutProperty.occupyTimeout (OccupyTimeoutProperty.java:40)
     DevBuf d_lres_state, d_lres_count, d_lres_w, d_lres_rcp, d_lres_kind, d_lres_tcount, d_lres_flags;
     DevBuf w_lslow, io_lrt;
+    // local rule graph (sentinel_load_local_rules): origin / default nodes, rules, components
+    bool lgraph = false;
+    int32_t lg_on = 0, lg_dn = 0;
+    DevBuf d_lg_on, d_lg_dn, d_lg_created, d_lg_roff, d_lg_rules, d_lg_comp, io_lctx;
     DevBuf d_lrule_grade;              // local param rules: 1 QPS, 0 THREAD (sentinel_set_local_param_grades)
     bool lhas_grade = false;            // local batch: sequential-path marks; host-fed exit response times
     int64_t lres_max_rt = 5000;        // SentinelConfig.statisticMaxRt (DEFAULT_STATISTIC_MAX_RT)
@@ -1662,6 +1667,7 @@ static int submit_prules_host(sentinel_engine_t *e, int mode, int64_t n, const s
 static int submit_local_entry(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, const int64_t *rt,
                               uint64_t *out, hipStream_t s) {
     if (n <= 0) return 0;
+    if (e->lgraph) return fail(SENTINEL_E_STATE, "a local rule graph is loaded: use sentinel_submit_local_graph_batch");
     if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
     int rc = e->ensure_ws(n);
     if (rc) return rc;
@@ -1698,6 +1704,48 @@ static int submit_local_entry(sentinel_engine_t *e, int64_t n, const Event *ev, 
                        e->d_lres_flags.as<uint8_t>(), e->lres_max_rt, fl, rt};
     e->launch("lentry_process", n, s, [&] { k_lentry_process<<<grid_for(n), 256, 0, s>>>(L, W, src, out); });
     e->launch("lentry_verdict", n, s, [&] { k_lentry_verdict<<<grid_for(n), 256, 0, s>>>(W, out, n); });
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+// Local rule graph batches (local_entry.hpp, k_lgraph_*): validation, sort by the resource's RELATE
+// component, one lane per component walking its events in arrival order.
+static int submit_local_graph(sentinel_engine_t *e, int64_t n, const Event *ev, const LocalCtx *ctx,
+                              const uint8_t *fl, const int64_t *rt, uint64_t *out, hipStream_t s) {
+    if (n <= 0) return 0;
+    if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
+    if (!e->lgraph) return fail(SENTINEL_E_STATE, "no local rule graph loaded (sentinel_load_local_rules)");
+    int rc = e->ensure_ws(n);
+    if (rc) return rc;
+    const int32_t R = e->nlres;
+    const int rbits = bits_for(R);
+    const uint32_t rinvalid = ((uint32_t)1 << rbits) - 1;
+    uint32_t *fkey = e->w_fkey.as<uint32_t>();
+    const int64_t nb = sort_blocks(n);
+    const LocalGraph G{e->d_lg_on.as<int64_t>(), e->d_lg_dn.as<int64_t>(), e->d_lg_created.as<uint8_t>(),
+                       e->d_lg_roff.as<int32_t>(), e->d_lg_rules.as<LocalRule>(), ctx, e->d_lg_comp.as<uint32_t>(),
+                       R, e->lg_on, e->lg_dn};
+    HIP_OK(hipMemsetAsync(e->w_counters.p, 0, 16, s));
+    e->launch("lgraph_prep", n, s, [&] {
+        k_lgraph_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(n, ev, G, out, fkey, rinvalid,
+                                                                        e->w_fhist.as<uint32_t>(), nb);
+    });
+    if (R == 0) {
+        HIP_OK(hipGetLastError());
+        return 0;
+    }
+    KeyTable RT{};
+    RT.w = e->d_lres_w.as<int32_t>();
+    RT.rcp_w = e->d_lres_rcp.as<double>();
+    RT.kind = e->d_lres_kind.as<uint8_t>();
+    RT.ncounters = 1;
+    const EventSrc src{ev, nullptr, nullptr, false};
+    e->sort_segments(RT, fkey, e->w_fhist.as<uint32_t>(), n, rbits, src, s);
+    const BatchWork W = e->work();
+    const LocalNodes L{e->d_lres_state.as<int64_t>(), e->d_lres_count.as<double>(), e->lres_n, e->lres_w, e->lres_Is,
+                       e->lres_interval, e->occupy_timeout, e->d_lres_tcount.as<double>(),
+                       e->d_lres_flags.as<uint8_t>(), e->lres_max_rt, fl, rt};
+    e->launch("lgraph_process", n, s, [&] { k_lgraph_process<<<grid_for(n), 256, 0, s>>>(L, G, W, src, out); });
     HIP_OK(hipGetLastError());
     return 0;
 }
@@ -1782,7 +1830,9 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
                       &e->d_seg1_rcp, &e->d_seg1_kind, &e->d_tok_keys, &e->d_tok_fid, &e->d_tok_fidx,
                       &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->w_runs, &e->w_pscan, &e->d_lres_state,
                       &e->d_lres_count, &e->d_lres_w, &e->d_lres_rcp, &e->d_lres_kind, &e->d_lres_tcount,
-                      &e->d_lres_flags, &e->w_lslow, &e->io_lrt, &e->d_lrule_grade})
+                      &e->d_lres_flags, &e->w_lslow, &e->io_lrt, &e->d_lrule_grade,
+                      &e->d_lg_on, &e->d_lg_dn, &e->d_lg_created, &e->d_lg_roff, &e->d_lg_rules, &e->d_lg_comp,
+                      &e->io_lctx})
         b->release();
     for (int k = 0; k < 2; ++k) {
         e->st_ev[k].release();
@@ -2759,6 +2809,7 @@ int sentinel_load_local_resources_ex(sentinel_engine_t *e, const sentinel_local_
     rc |= upload(e->d_lres_kind, std::vector<uint8_t>(N, KIND_CLUSTER));
     if (rc) return rc;
     e->nlres = n;
+    e->lgraph = false;
     e->lres_n = sample_count;
     e->lres_w = w;
     e->lres_g = a;
@@ -2884,15 +2935,12 @@ int sentinel_local_node_stats(sentinel_engine_t *e, int32_t idx, int64_t ts, int
     return 0;
 }
 
-int sentinel_local_node_metrics(sentinel_engine_t *e, int32_t idx, int64_t ts, int64_t *out) {
-    if (!e || !out || ts < 0) return fail(SENTINEL_E_INVALID, "bad arguments");
-    std::lock_guard<std::mutex> g(e->mu);
-    if (idx < 0 || idx >= e->nlres) return fail(SENTINEL_E_INVALID, "bad resource index");
+// StatisticNode counters of one node record (device) at ts -> out14 (caller holds e->mu)
+static int local_node_metrics_at(sentinel_engine_t *e, const int64_t *node, int64_t ts, int64_t *out) {
     HIP_OK(hipSetDevice(e->device));
     HIP_OK(hipStreamSynchronize(e->stream));
     std::vector<int64_t> st(LOCAL_WORDS);
-    HIP_OK(hipMemcpy(st.data(), e->d_lres_state.as<int64_t>() + (int64_t)idx * LOCAL_WORDS, LOCAL_WORDS * 8,
-                     hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(st.data(), node, LOCAL_WORDS * 8, hipMemcpyDeviceToHost));
     // read-only view of the rolled windows: epochs > E - n (LeapArray.values after currentWindow,
     // future buckets of a clock that went back included)
     const int64_t E = ts / e->lres_w, E1 = ts / 1000;
@@ -2915,6 +2963,139 @@ int sentinel_local_node_metrics(sentinel_engine_t *e, int32_t idx, int64_t ts, i
     out[5] = std::max<int64_t>(1, mrt_s);                 // ArrayMetric.minRt: Math.max(1, rt)
     out[12] = std::max<int64_t>(1, mrt_m);
     out[13] = st[LOCAL_THR_OFF];
+    return 0;
+}
+
+int sentinel_local_node_metrics(sentinel_engine_t *e, int32_t idx, int64_t ts, int64_t *out) {
+    if (!e || !out || ts < 0) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    if (idx < 0 || idx >= e->nlres) return fail(SENTINEL_E_INVALID, "bad resource index");
+    return local_node_metrics_at(e, e->d_lres_state.as<int64_t>() + (int64_t)idx * LOCAL_WORDS, ts, out);
+}
+
+int sentinel_local_graph_node_metrics(sentinel_engine_t *e, int32_t kind, int32_t idx, int64_t ts, int64_t *out) {
+    if (!e || !out || ts < 0) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    const int64_t *base = nullptr;
+    int32_t cnt = 0;
+    if (kind == SENTINEL_NODE_CLUSTER) { base = e->d_lres_state.as<int64_t>(); cnt = e->nlres; }
+    else if (kind == SENTINEL_NODE_ORIGIN && e->lgraph) { base = e->d_lg_on.as<int64_t>(); cnt = e->lg_on; }
+    else if (kind == SENTINEL_NODE_DEFAULT && e->lgraph) { base = e->d_lg_dn.as<int64_t>(); cnt = e->lg_dn; }
+    if (!base || idx < 0 || idx >= cnt) return fail(SENTINEL_E_INVALID, "bad node kind or index");
+    return local_node_metrics_at(e, base + (int64_t)idx * LOCAL_WORDS, ts, out);
+}
+
+int sentinel_load_local_rules(sentinel_engine_t *e, const sentinel_local_rule_t *rules, int32_t n, int32_t n_res,
+                              int32_t n_origin_nodes, int32_t n_default_nodes, int32_t sample_count, int32_t interval_ms) {
+    if (!e || n < 0 || (n > 0 && !rules) || n_res < 0 || n_origin_nodes < 0 || n_default_nodes < 0)
+        return fail(SENTINEL_E_INVALID, "bad local rules");
+    // every ClusterNode starts empty (and its resource's single-rule fields unused)
+    std::vector<sentinel_local_resource_ex_t> none((size_t)std::max(n_res, 1));
+    for (auto &x : none) { x.qps_count = 0; x.thread_count = 0; x.flags = 0; x.reserved = 0; }
+    int rc = sentinel_load_local_resources_ex(e, none.data(), n_res, sample_count, interval_ms);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    // FlowRuleUtil.buildFlowRuleMap: invalid rules dropped (isValidRule, FRU:167-238), blank limitApp ->
+    // "default", duplicates dropped (the HashSet), FlowRuleComparator's stable sort (non-"default"
+    // limitApps first); the caller passes FlowRuleManager's order
+    auto valid = [&](const sentinel_local_rule_t &r) {
+        if (r.resource < 0 || r.resource >= n_res || !(r.count >= 0) || r.strategy < 0) return false;
+        if (r.grade == SENTINEL_GRADE_QPS) return r.strategy > SENTINEL_STRATEGY_CHAIN || r.strategy == SENTINEL_STRATEGY_DIRECT || r.ref >= 0;
+        return r.grade == SENTINEL_GRADE_THREAD;
+    };
+    std::vector<std::vector<LocalRule>> per((size_t)std::max(n_res, 1));
+    for (int pass = 0; pass < 2; ++pass)
+        for (int32_t i = 0; i < n; ++i) {
+            const sentinel_local_rule_t &r = rules[i];
+            if (!valid(r)) continue;
+            const int32_t lim = r.limit_app < 0 ? SENTINEL_LIMIT_APP_DEFAULT : r.limit_app;
+            if ((lim == SENTINEL_LIMIT_APP_DEFAULT) != (pass == 1)) continue;
+            LocalRule x{r.count, r.grade, r.strategy, lim, r.ref};
+            auto &v = per[r.resource];
+            bool dup = false;
+            for (const LocalRule &y : v)
+                dup |= y.grade == x.grade && y.count == x.count && y.strategy == x.strategy && y.limit_app == x.limit_app &&
+                       y.ref == x.ref;
+            if (!dup) v.push_back(x);
+        }
+    std::vector<int32_t> roff((size_t)n_res + 1, 0);
+    std::vector<LocalRule> flat;
+    for (int32_t r = 0; r < n_res; ++r) {
+        roff[r] = (int32_t)flat.size();
+        flat.insert(flat.end(), per[r].begin(), per[r].end());
+    }
+    roff[n_res] = (int32_t)flat.size();
+    if (flat.empty()) flat.push_back(LocalRule{0, 0, 0, 0, -1});
+    // components: union-find over the RELATE edges (a rule reads its refResource's ClusterNode)
+    std::vector<uint32_t> par((size_t)std::max(n_res, 1));
+    for (int32_t r = 0; r < n_res; ++r) par[r] = (uint32_t)r;
+    std::function<uint32_t(uint32_t)> find = [&](uint32_t x) { return par[x] == x ? x : (par[x] = find(par[x])); };
+    for (int32_t r = 0; r < n_res; ++r)
+        for (int32_t j = roff[r]; j < roff[r + 1]; ++j)
+            if (flat[j].strategy == SENTINEL_STRATEGY_RELATE && flat[j].ref >= 0 && flat[j].ref < n_res) {
+                const uint32_t a = find((uint32_t)r), b = find((uint32_t)flat[j].ref);
+                if (a != b) par[std::max(a, b)] = std::min(a, b);
+            }
+    std::vector<uint32_t> comp((size_t)std::max(n_res, 1), 0);
+    for (int32_t r = 0; r < n_res; ++r) comp[r] = find((uint32_t)r);
+    auto empty_nodes = [](int32_t cnt) {
+        std::vector<int64_t> st((size_t)std::max(cnt, 1) * LOCAL_WORDS, 0);
+        for (int32_t i = 0; i < cnt; ++i) {
+            int64_t *r = st.data() + (size_t)i * LOCAL_WORDS;
+            for (int j = 0; j < LOCAL_NMAX; ++j) r[LOCAL_SEC_W * j] = r[LOCAL_BOR_OFF + LOCAL_BOR_W * j] = EPOCH_ABSENT;
+            for (int j = 0; j < LOCAL_MIN_SLOTS; ++j) r[LOCAL_MIN_OFF + LOCAL_MIN_W * j] = EPOCH_ABSENT;
+        }
+        return st;
+    };
+    rc = 0;
+    rc |= upload(e->d_lg_on, empty_nodes(n_origin_nodes));
+    rc |= upload(e->d_lg_dn, empty_nodes(n_default_nodes));
+    rc |= upload(e->d_lg_created, std::vector<uint8_t>((size_t)std::max(n_res, 1), 0));
+    rc |= upload(e->d_lg_roff, roff);
+    rc |= upload(e->d_lg_rules, flat);
+    rc |= upload(e->d_lg_comp, comp);
+    if (rc) return rc;
+    e->lg_on = n_origin_nodes;
+    e->lg_dn = n_default_nodes;
+    e->lgraph = true;
+    return 0;
+}
+
+int sentinel_submit_local_graph_batch(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev,
+                                      const sentinel_local_ctx_t *ctx, const uint8_t *flags, const int64_t *rt_ms,
+                                      sentinel_verdict_t *out, void *stream) {
+    if (!e || n < 0 || (n > 0 && (!ev || !ctx || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    return submit_local_graph(e, n, (const Event *)ev, (const LocalCtx *)ctx, flags, flags ? rt_ms : nullptr,
+                              (uint64_t *)out, stream ? (hipStream_t)stream : e->stream);
+}
+
+int sentinel_submit_local_graph_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev,
+                                           const sentinel_local_ctx_t *ctx, const uint8_t *flags, const int64_t *rt_ms,
+                                           sentinel_verdict_t *out) {
+    if (!e || n < 0 || (n > 0 && (!ev || !ctx || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    hipStream_t s = e->stream;
+    int rc = 0;
+    rc |= e->io_ev.ensure(n * sizeof(Event));
+    rc |= e->io_out.ensure(n * 8);
+    rc |= e->io_lctx.ensure(n * sizeof(LocalCtx));
+    if (flags) rc |= e->io_fl.ensure(n);
+    if (flags && rt_ms) rc |= e->io_lrt.ensure(n * 8);
+    if (rc) return SENTINEL_E_NOMEM;
+    HIP_OK(hipMemcpyAsync(e->io_ev.p, ev, n * sizeof(Event), hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(e->io_lctx.p, ctx, n * sizeof(LocalCtx), hipMemcpyHostToDevice, s));
+    if (flags) HIP_OK(hipMemcpyAsync(e->io_fl.p, flags, n, hipMemcpyHostToDevice, s));
+    if (flags && rt_ms) HIP_OK(hipMemcpyAsync(e->io_lrt.p, rt_ms, n * 8, hipMemcpyHostToDevice, s));
+    rc = submit_local_graph(e, n, e->io_ev.as<Event>(), e->io_lctx.as<LocalCtx>(), flags ? e->io_fl.as<uint8_t>() : nullptr,
+                            flags && rt_ms ? e->io_lrt.as<int64_t>() : nullptr, e->io_out.as<uint64_t>(), s);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 8, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
     return 0;
 }
 

@@ -377,6 +377,180 @@ __global__ __launch_bounds__(256) void k_lentry_process(LocalNodes L, BatchWork 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Local rule graph: FlowRuleChecker with every limitApp / strategy (FlowRuleChecker.java:44-145)
+// over the nodes the slot chain builds -- a ClusterNode per resource (created by the resource's
+// first entry, ClusterBuilderSlot.java:74-92), an origin StatisticNode per (resource, origin)
+// (ClusterNode.getOrCreateOriginNode, CBS:97-100) and a DefaultNode per (context, resource) whose
+// booking also reaches the ClusterNode (DefaultNode.java:110-143).  A RELATE rule of resource A reads
+// the ClusterNode of its refResource B, which B's entries write: A and B are one "component" (host
+// union-find over the RELATE edges), and one lane walks a component's events in arrival order
+// through the reference state machine.  Every node is a LOCAL_WORDS StatisticNode record.
+struct LocalRule {
+    double count;
+    int32_t grade;        // 1 QPS, 0 THREAD
+    int32_t strategy;     // 0 DIRECT, 1 RELATE, 2 CHAIN, other: no node
+    int32_t limit_app;    // 0 "default", 1 "other", >= 2 an origin id
+    int32_t ref;          // RELATE: resource index, CHAIN: context id, -1 blank
+};
+struct LocalCtx {
+    int32_t origin;       // -1: "" (no origin node)
+    int32_t origin_node;
+    int32_t context;
+    int32_t default_node;
+};
+struct LocalGraph {
+    int64_t *on_state;            // origin nodes
+    int64_t *dn_state;            // DefaultNodes
+    uint8_t *created;             // ClusterNode exists (ClusterBuilderSlot.clusterNodeMap)
+    const int32_t *roff;          // rules of resource r: [roff[r], roff[r + 1]) (comparator-sorted)
+    const LocalRule *rules;
+    const LocalCtx *ctx;          // per event
+    const uint32_t *comp;         // component of each resource
+    int32_t n_res, n_on, n_dn;
+};
+
+// FRC:87-103 selectReferenceNode
+__device__ inline int64_t *lg_ref_node(const LocalNodes &L, const LocalGraph &G, const LocalRule &r, const LocalCtx &c) {
+    if (r.ref < 0) return nullptr;
+    if (r.strategy == 1) return r.ref < G.n_res && G.created[r.ref] ? L.state + (int64_t)r.ref * LOCAL_WORDS : nullptr;
+    if (r.strategy == 2) return r.ref == c.context ? G.dn_state + (int64_t)c.default_node * LOCAL_WORDS : nullptr;
+    return nullptr;
+}
+
+// FRC:110-145 selectNodeByRequesterAndStrategy (filterOrigin: the origin is not "default" / "other")
+__device__ inline int64_t *lg_select(const LocalNodes &L, const LocalGraph &G, uint32_t res, const LocalRule &r,
+                                     const LocalCtx &c) {
+    int64_t *onode = c.origin >= 0 ? G.on_state + (int64_t)c.origin_node * LOCAL_WORDS : nullptr;
+    if (r.limit_app == c.origin && c.origin >= 2) return r.strategy == 0 ? onode : lg_ref_node(L, G, r, c);
+    if (r.limit_app == 0) return r.strategy == 0 ? L.state + (int64_t)res * LOCAL_WORDS : lg_ref_node(L, G, r, c);
+    if (r.limit_app == 1 && c.origin >= 0) {                  // FlowRuleManager.isOtherOrigin (:113-129)
+        bool other = true;
+        for (int32_t j = G.roff[res]; j < G.roff[res + 1]; ++j) other &= G.rules[j].limit_app != c.origin;
+        if (other) return r.strategy == 0 ? onode : lg_ref_node(L, G, r, c);
+    }
+    return nullptr;
+}
+
+// One SphU.entry(res) in context c: node creation, every rule in order (DefaultController.canPass on
+// the selected node, DC:49-69), StatisticSlot.entry's booking (SS:55-116).
+__device__ inline bool lg_entry(const LocalNodes &L, const LocalGraph &G, uint32_t res, int64_t t, int32_t a, bool prio,
+                                const LocalCtx &c, int32_t *wait) {
+    *wait = 0;
+    G.created[res] = 1;
+    int64_t *cn = L.state + (int64_t)res * LOCAL_WORDS;
+    int64_t *dn = G.dn_state + (int64_t)c.default_node * LOCAL_WORDS;
+    int64_t *on = c.origin >= 0 ? G.on_state + (int64_t)c.origin_node * LOCAL_WORDS : nullptr;
+    bool blocked = false, occupied = false;
+    for (int32_t j = G.roff[res]; j < G.roff[res + 1] && !blocked && !occupied; ++j) {
+        const LocalRule r = G.rules[j];
+        int64_t *nd = lg_select(L, G, res, r, c);
+        if (!nd) continue;                                   // FRC:78-81: no node -> pass
+        int32_t cur;
+        if (r.grade == 0) {
+            cur = (int32_t)nd[LOCAL_THR_OFF];                // (int) curThreadNum
+        } else {
+            const int64_t E = t / L.w;
+            sec_roll(nd, L.n, E, L.max_rt);                  // (int) passQps
+            cur = java_d2i((double)ring_sum<LOCAL_SEC_W>(nd, L.n, E, SC_PASS) / L.I_s);
+        }
+        if (!((double)(int32_t)((uint32_t)cur + (uint32_t)a) > r.count)) continue;
+        if (prio && r.grade == 1) {                          // DC:52-64
+            const int64_t w = local_try_occupy(nd, L, t, a, r.count);
+            if (w < L.occupy_timeout) {
+                const int64_t ft = t + w;                    // addWaitingRequest
+                const int sb = ring_roll<LOCAL_BOR_W>(nd + LOCAL_BOR_OFF, L.n, ft / L.w);
+                if (sb >= 0) nd[LOCAL_BOR_OFF + LOCAL_BOR_W * sb + 1] = wrap_add(nd[LOCAL_BOR_OFF + LOCAL_BOR_W * sb + 1], a);
+                int64_t *mn = nd + LOCAL_MIN_OFF;            // addOccupiedPass (minute)
+                const int s2 = min_roll(nd, L, t / 1000);
+                if (s2 >= 0) {
+                    mn[LOCAL_MIN_W * s2 + MC_OCC] = wrap_add(mn[LOCAL_MIN_W * s2 + MC_OCC], a);
+                    mn[LOCAL_MIN_W * s2 + MC_PASS] = wrap_add(mn[LOCAL_MIN_W * s2 + MC_PASS], a);
+                }
+                *wait = (int32_t)w;
+                occupied = true;                             // PriorityWaitException
+                continue;
+            }
+        }
+        blocked = true;
+    }
+    if (blocked) {                                           // SS:96-104
+        local_book(L, dn, t, SC_BLOCK, MC_BLOCK, a);
+        local_book(L, cn, t, SC_BLOCK, MC_BLOCK, a);
+        if (on) local_book(L, on, t, SC_BLOCK, MC_BLOCK, a);
+        return false;
+    }
+    dn[LOCAL_THR_OFF] = wrap_add(dn[LOCAL_THR_OFF], 1);      // SS:62-69 / 81-86
+    cn[LOCAL_THR_OFF] = wrap_add(cn[LOCAL_THR_OFF], 1);
+    if (!occupied) {
+        local_book(L, dn, t, SC_PASS, MC_PASS, a);
+        local_book(L, cn, t, SC_PASS, MC_PASS, a);
+    }
+    if (on) {
+        on[LOCAL_THR_OFF] = wrap_add(on[LOCAL_THR_OFF], 1);
+        if (!occupied) local_book(L, on, t, SC_PASS, MC_PASS, a);
+    }
+    return true;
+}
+
+// Validation (unknown resource / node index -> NO_RULE_EXISTS, t < 0 -> FAIL) and the sort key: the
+// resource's component.
+__global__ __launch_bounds__(SORT_THREADS) void k_lgraph_prep(int64_t n, const Event *__restrict__ ev, LocalGraph G,
+                                                              uint64_t *__restrict__ out, uint32_t *__restrict__ fkey,
+                                                              uint32_t finvalid, uint32_t *__restrict__ fhist,
+                                                              int64_t nblocks) {
+    __shared__ uint32_t hf[MAX_PASSES][RADIX];
+    for (int d = threadIdx.x; d < MAX_PASSES * RADIX; d += SORT_THREADS) (&hf[0][0])[d] = 0;
+    __syncthreads();
+    const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
+        if (i >= n) break;
+        const Event e = ev[i];
+        const LocalCtx c = G.ctx[i];
+        uint32_t k = finvalid;
+        if (e.idx < 0 || e.idx >= G.n_res || c.default_node < 0 || c.default_node >= G.n_dn ||
+            (c.origin >= 0 && (c.origin_node < 0 || c.origin_node >= G.n_on)))
+            put_verdict(out, (uint32_t)i, ST_NO_RULE_EXISTS, 0, 0);
+        else if (e.ts < 0) put_verdict(out, (uint32_t)i, ST_FAIL, 0, 0);
+        else k = G.comp[e.idx];
+        fkey[i] = k;
+        tile_hist_accumulate(hf, k, 1);
+    }
+    __syncthreads();
+    tile_hist_store(hf, fhist, 1, nblocks);
+}
+
+// One lane per component: every event of the component in arrival order (entries and exits).
+__global__ __launch_bounds__(256) void k_lgraph_process(LocalNodes L, LocalGraph G, BatchWork W, EventSrc src,
+                                                        uint64_t *out) {
+    const int64_t g0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t S = (int64_t)*W.nseg;
+    if (g0 >= S || (int64_t)*W.nvalid == 0) return;
+    const uint32_t key = W.seg_key[g0];
+    if (g0 > 0 && W.seg_key[g0 - 1] == key) return;
+    int64_t g1 = g0 + 1;
+    while (g1 < S && W.seg_key[g1] == key) ++g1;
+    for (uint32_t i = W.seg_start[g0]; i < W.seg_start[g1]; ++i) {
+        const uint32_t seq = (uint32_t)W.sval[i] & SEQ_MASK;
+        const Event e = src.ev[seq];
+        const LocalCtx c = G.ctx[seq];
+        const uint8_t of = L.ofl ? L.ofl[seq] : 0;
+        if (of & LF_EXIT) {                                  // SS:126-164: DefaultNode (+ ClusterNode), origin node
+            const int64_t rt = L.rt ? L.rt[seq] : 0;
+            const bool err = (of & LF_ERROR) != 0;
+            local_seq_exit(L, G.dn_state + (int64_t)c.default_node * LOCAL_WORDS, e.ts, e.acquire, rt, err);
+            local_seq_exit(L, L.state + (int64_t)e.idx * LOCAL_WORDS, e.ts, e.acquire, rt, err);
+            if (c.origin >= 0) local_seq_exit(L, G.on_state + (int64_t)c.origin_node * LOCAL_WORDS, e.ts, e.acquire, rt, err);
+            put_verdict(out, seq, ST_OK, 0, 0);
+            continue;
+        }
+        int32_t wait;
+        const bool ok = lg_entry(L, G, (uint32_t)e.idx, e.ts, e.acquire, (of & LF_PRIO) != 0, c, &wait);
+        put_verdict(out, seq, ok ? ST_OK : ST_BLOCKED, 0, ok ? wait : 0);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_lentry_verdict(BatchWork W, uint64_t *out, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || i >= (int64_t)*W.nvalid) return;

@@ -526,6 +526,40 @@ class GpuTokenService:
         check(self._L.sentinel_local_node_metrics(self._h, int(resource_idx), int(ts), _p(out)), "local_node_metrics")
         return out
 
+    def load_local_rules(self, rules, n_resources: int, n_origin_nodes: int, n_default_nodes: int,
+                         sample_count: int = 2, interval_ms: int = 1000):
+        """FlowRuleManager.loadRules over the local rule graph (FlowRuleChecker with every limitApp
+        and strategy): `rules` is a LOCAL_RULE_DTYPE array (or records of its fields) in
+        FlowRuleManager's order; invalid rules are dropped and the rules sorted as the reference's
+        buildFlowRuleMap does.  Every node starts empty."""
+        arr = np.zeros(len(rules), dtype=_lib.LOCAL_RULE_DTYPE)
+        for i, r in enumerate(rules):
+            arr[i] = tuple(r) if not isinstance(r, np.void) else r
+        check(self._L.sentinel_load_local_rules(self._h, _p(arr) if len(arr) else None, len(arr), int(n_resources),
+                                                int(n_origin_nodes), int(n_default_nodes), int(sample_count),
+                                                int(interval_ms)), "load_local_rules")
+
+    def submit_local_graph_batch_host(self, resource_idx, acquire, ts, ctx, flags=None, rt=None):
+        """Entries / exits with their contexts (LOCAL_CTX_DTYPE: origin, origin_node, context,
+        default_node) -> (status, waitInMs)."""
+        ev = self.pack_events(resource_idx, acquire, ts)
+        cx = np.ascontiguousarray(ctx, dtype=_lib.LOCAL_CTX_DTYPE)
+        if len(cx) != len(ev):
+            raise ValueError("one context per event")
+        fl = None if flags is None else np.ascontiguousarray(flags, dtype=np.uint8)
+        r = None if rt is None else np.ascontiguousarray(rt, dtype=np.int64)
+        out = np.empty(len(ev), dtype=_lib.VERDICT_DTYPE)
+        check(self._L.sentinel_submit_local_graph_batch_host(self._h, len(ev), _p(ev), _p(cx), _p(fl), _p(r), _p(out)),
+              "submit_local_graph_batch_host")
+        return out["status"].astype(np.int8), out["wait_in_ms"].astype(np.int64)
+
+    def local_graph_node_metrics(self, kind: int, idx: int, ts: int) -> np.ndarray:
+        """local_node_metrics of a ClusterNode (NODE_CLUSTER), origin node or DefaultNode."""
+        out = np.zeros(14, dtype=np.int64)
+        check(self._L.sentinel_local_graph_node_metrics(self._h, int(kind), int(idx), int(ts), _p(out)),
+              "local_graph_node_metrics")
+        return out
+
     def set_statistic_max_rt(self, ms: int):
         check(self._L.sentinel_set_statistic_max_rt(self._h, int(ms)), "set_statistic_max_rt")
 
