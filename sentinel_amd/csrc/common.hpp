@@ -76,17 +76,50 @@ constexpr uint64_t PKEY_EMPTY = 0xFFFFFFFFFFFFFFFFull;   // reserved param key (
 // `fresh` (optional) counts the keys this call inserted.
 __device__ inline int64_t slot_insert(unsigned long long *table, uint64_t mask, uint64_t key,
                                       unsigned long long *fresh = nullptr) {
+    // A slot goes EMPTY -> key once and keeps it for the kernel's lifetime, so a plain load that sees
+    // the key (or another key) is final and only an EMPTY slot needs the CAS: a hot key (Zipf values)
+    // is found by reads, not by a queue of atomics on one address.  A stale EMPTY costs one CAS.
     uint64_t h = mix64(key) & mask;
     for (uint64_t probes = 0; probes <= mask; ++probes) {
-        const unsigned long long prev = atomicCAS(&table[h], (unsigned long long)PKEY_EMPTY, (unsigned long long)key);
-        if (prev == PKEY_EMPTY) {
-            if (fresh) atomicAdd(fresh, 1ull);
-            return (int64_t)h;
+        const unsigned long long cur = table[h];
+        if (cur == key) return (int64_t)h;
+        if (cur == PKEY_EMPTY) {
+            const unsigned long long prev = atomicCAS(&table[h], (unsigned long long)PKEY_EMPTY, (unsigned long long)key);
+            if (prev == PKEY_EMPTY) {
+                if (fresh) atomicAdd(fresh, 1ull);
+                return (int64_t)h;
+            }
+            if (prev == key) return (int64_t)h;
         }
-        if (prev == key) return (int64_t)h;
         h = (h + 1) & mask;
     }
     return -1;
+}
+
+// slot_insert counting this thread's fresh inserts in a register (the kernel adds a workgroup's total
+// to the global counter once: a global atomic per fresh key serialises a batch of new values on one
+// address).
+__device__ inline int64_t slot_insert_counted(unsigned long long *table, uint64_t mask, uint64_t key, uint32_t &nfresh) {
+    uint64_t h = mix64(key) & mask;
+    for (uint64_t probes = 0; probes <= mask; ++probes) {
+        const unsigned long long cur = table[h];
+        if (cur == key) return (int64_t)h;
+        if (cur == PKEY_EMPTY) {
+            const unsigned long long prev = atomicCAS(&table[h], (unsigned long long)PKEY_EMPTY, (unsigned long long)key);
+            if (prev == PKEY_EMPTY) { ++nfresh; return (int64_t)h; }
+            if (prev == key) return (int64_t)h;
+        }
+        h = (h + 1) & mask;
+    }
+    return -1;
+}
+
+// Adds every thread's `mine` to *global with one atomic per workgroup (`lds`: a zeroed shared word,
+// all threads of the block call this).
+__device__ inline void block_add_global(unsigned long long *global, uint32_t mine, uint32_t *lds) {
+    if (mine) atomicAdd(lds, mine);
+    __syncthreads();
+    if (threadIdx.x == 0 && *lds && global) atomicAdd(global, (unsigned long long)*lds);
 }
 
 // Read-only lookup; returns the slot or -1.

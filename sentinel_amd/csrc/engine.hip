@@ -167,11 +167,14 @@ __global__ __launch_bounds__(SORT_THREADS) void k_param_prep(
     uint32_t *__restrict__ lkey, uint32_t linvalid, int lpasses, uint32_t *__restrict__ lhist, int64_t nblocks) {
     __shared__ uint32_t hf[MAX_PASSES][RADIX];
     __shared__ uint32_t hl[MAX_PASSES][RADIX];
+    __shared__ uint32_t s_fresh;
     for (int d = threadIdx.x; d < MAX_PASSES * RADIX; d += SORT_THREADS) {
         (&hf[0][0])[d] = 0;
         (&hl[0][0])[d] = 0;
     }
+    if (threadIdx.x == 0) s_fresh = 0;
     __syncthreads();
+    uint32_t nfresh = 0;
     const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
     for (int j = 0; j < SORT_ITEMS; ++j) {
         const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
@@ -186,11 +189,13 @@ __global__ __launch_bounds__(SORT_THREADS) void k_param_prep(
             if (r == ROUTE_TOO_MANY) st = ST_TOO_MANY_REQUEST;
             else if (e.ts < 0) st = ST_FAIL;
             else {
-                const int64_t h = slot_insert(table, cap_mask, e.key, fresh);
+                const int64_t h = slot_insert_counted(table, cap_mask, e.key, nfresh);
                 if (h < 0) st = ST_FAIL;          // table full: the host's param_reserve prevents it
                 else {
                     k = (uint32_t)h;
-                    slot_rule[h] = e.idx;    // identical value from every writer of this slot
+                    // identical value from every writer of this slot: written only when it differs (a
+                    // hot slot is read by every event of its value, not stored to)
+                    if (slot_rule[h] != e.idx) slot_rule[h] = e.idx;
                     if (r >= 0) l = (uint32_t)r;
                 }
             }
@@ -203,7 +208,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_param_prep(
         }
         if (st != 127) put_verdict(out, (uint32_t)i, st, 0, 0);
     }
-    __syncthreads();
+    block_add_global(fresh, nfresh, &s_fresh);              // (synchronises the block)
     tile_hist_store(hf, fhist, fpasses, nblocks);
     if (lkey) tile_hist_store(hl, lhist, lpasses, nblocks);
 }
@@ -227,12 +232,15 @@ __global__ __launch_bounds__(256) void k_param_meta(int64_t n, const uint32_t *_
     double thr = rule_thr[r];
     const int64_t h = slot_find(hot_table, hot_mask, ev[i].key);   // ClusterParamFlowChecker.getRawThreshold (CPFC:113-120)
     if (h >= 0) thr = hot_thr[h];
-    slot_n[s] = rule_n[r];
-    slot_w[s] = rule_w[r];
-    slot_rcp[s] = rule_rcp[r];
-    slot_Is[s] = rule_Is[r];
-    slot_thr[s] = thr;
-    slot_kind[s] = KIND_PARAM;
+    // compare before store: every event of a hot value refreshes the same slot with the same values
+    const int32_t nn = rule_n[r], ww = rule_w[r];
+    const double rc = rule_rcp[r], is = rule_Is[r];
+    if (slot_n[s] != nn) slot_n[s] = nn;
+    if (slot_w[s] != ww) slot_w[s] = ww;
+    if (__double_as_longlong(slot_rcp[s]) != __double_as_longlong(rc)) slot_rcp[s] = rc;
+    if (__double_as_longlong(slot_Is[s]) != __double_as_longlong(is)) slot_Is[s] = is;
+    if (__double_as_longlong(slot_thr[s]) != __double_as_longlong(thr)) slot_thr[s] = thr;
+    if (slot_kind[s] != KIND_PARAM) slot_kind[s] = KIND_PARAM;
 }
 
 // One key's slot (or -1) for the host's read-only queries.
@@ -471,11 +479,15 @@ struct sentinel_engine {
     uint64_t p_live = 0;               // live slots after the last rebuild
     uint64_t p_ub = 0;                 // values submitted since (an upper bound of the fresh inserts)
     DevBuf d_pfresh;                   // device: fresh inserts since the last rebuild
+    // the previous table's buffers, kept as the next rebuild's target (no hipMalloc / hipFree per rebuild)
+    DevBuf sp_keys, sp_rule, sp_state, sp_n, sp_w, sp_rcp, sp_Is, sp_thr, sp_kind;
     uint64_t p_rebuilds = 0;
     int32_t pmode = SENTINEL_PARAM_EXACT;
     int32_t cm_depth = 4;
     uint32_t cm_width = 1024;
     DevBuf d_cm;                       // count-min cells (SENTINEL_PARAM_COUNT_MIN)
+    DevBuf w_cm;                       // shared sketch: rule heads, cursors, grid barrier, level words
+    int cm_sync_blocks = 0;            // co-resident workgroups of k_prule_cm_sync
 
     // local param rules (ParamFlowChecker.passLocalCheck); rule index = load position
     int32_t nlrules = 0;
@@ -966,11 +978,11 @@ int sentinel_engine::param_rebuild(uint64_t new_cap, const std::vector<int32_t> 
                                    std::vector<std::pair<int32_t, std::vector<int64_t>>> *exported) {
     const int64_t nstride = header_words(new_maxn);
     const int64_t ostride = header_words(pmax_n);
-    DevBuf nkeys, nrule, nstate, nn, nw, nrcp, nIs, nthr, nkind, dmap, dnewest, dcount, dxout, dimp, dimprule, dnrn;
+    DevBuf &nkeys = sp_keys, &nrule = sp_rule, &nstate = sp_state, &nn = sp_n, &nw = sp_w, &nrcp = sp_rcp,
+           &nIs = sp_Is, &nthr = sp_thr, &nkind = sp_kind;
+    DevBuf dmap, dnewest, dcount, dxout, dimp, dimprule, dnrn;
     auto cleanup = [&] {
-        for (DevBuf *b : {&nkeys, &nrule, &nstate, &nn, &nw, &nrcp, &nIs, &nthr, &nkind, &dmap, &dnewest, &dcount, &dxout,
-                          &dimp, &dimprule, &dnrn})
-            b->release();
+        for (DevBuf *b : {&dmap, &dnewest, &dcount, &dxout, &dimp, &dimprule, &dnrn}) b->release();
     };
     int rc = 0;
     rc |= nkeys.ensure(new_cap * 8);
@@ -1085,8 +1097,14 @@ int sentinel_engine::param_reserve(int64_t nv) {
     for (size_t i = 0; i < ident.size(); ++i) ident[i] = (int32_t)i;
     int rc = param_rebuild(pcap, ident, pmax_n, h_prule_n, {}, 0, {}, nullptr);        // reclaim dead slots
     if (rc) return rc;
+    // grow until the live slots plus this batch fit, and -- within a memory budget -- until a few more
+    // batches of new values fit too, so that the reclaiming rebuild (a device-wide pass and a host sync)
+    // comes back every few batches, not every batch, under a steady churn of values
+    const uint64_t slot_bytes = 8 + 4 + (uint64_t)header_words(pmax_n) * 8 + 4 + 4 + 8 + 8 + 8 + 1;
+    const uint64_t budget = (uint64_t)8 << 30;            // per table (the rebuild holds two)
     uint64_t cap = pcap;
     while (p_live + (uint64_t)nv > cap / 4 * 3) cap <<= 1;
+    while (p_live + 4 * (uint64_t)nv > cap / 4 * 3 && 2 * cap * slot_bytes <= budget) cap <<= 1;
     if (cap != pcap) {
         rc = param_rebuild(cap, ident, pmax_n, h_prule_n, {}, 0, {}, nullptr);         // grow
         if (rc) return rc;
@@ -1630,6 +1648,37 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
     e->sort_segments(RT, fkey, e->w_fhist.as<uint32_t>(), n, rbits, src, s);
     const BatchWork W = e->work();
     const unsigned g = grid_for(n);
+    if (mode == PMODE_CM && C.CM.shared) {
+        // shared sketch: every rule's lane moves through the epochs together (k_prule_cm_sync)
+        const int64_t H = std::min<int64_t>(n, R);
+        const size_t cbase = ((size_t)2 * H * 4 + 255) & ~(size_t)255;   // control words after heads + cursors
+        rc = e->w_cm.ensure(cbase + 256);
+        if (rc) return rc;
+        uint32_t *heads = e->w_cm.as<uint32_t>();
+        uint32_t *cursor = heads + H;
+        uint32_t *ctl = reinterpret_cast<uint32_t *>(e->w_cm.as<char>() + cbase);
+        unsigned long long *lv = reinterpret_cast<unsigned long long *>(e->w_cm.as<char>() + cbase + 192);
+        HIP_OK(hipMemsetAsync(ctl, 0, 192, s));            // head count, barrier arrivals and generation
+        HIP_OK(hipMemsetAsync(lv, 0xFF, 24, s));
+        if (!e->cm_sync_blocks) {
+            int per_cu = 0, cus = 0;
+            HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(k_prule_cm_sync), 256, 0));
+            HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device));
+            // at most one workgroup per CU: the grid barrier's cost grows with the workgroups
+            e->cm_sync_blocks = std::max(1, std::min(per_cu, 1)) * std::max(1, cus);
+        }
+        const unsigned nblk = (unsigned)std::max<int64_t>(1, std::min<int64_t>(e->cm_sync_blocks, (H + 255) / 256));
+        hipError_t ce = hipSuccess;
+        e->launch("prule_process", n, s, [&] {
+            k_cm_heads<<<g, 256, 0, s>>>(W, heads, ctl);
+            void *args[] = {(void *)&C, (void *)&W, (void *)&evp, (void *)&vs, (void *)&out, (void *)&heads, (void *)&ctl,
+                            (void *)&cursor, (void *)&lv};
+            ce = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(k_prule_cm_sync), dim3(nblk), dim3(256), args, 0, s);
+        });
+        if (ce != hipSuccess) return fail(SENTINEL_E_DEVICE, std::string("cooperative launch failed: ") + hipGetErrorString(ce));
+        HIP_OK(hipGetLastError());
+        return 0;
+    }
     e->launch("prule_process", n, s, [&] {
         if (mode == PMODE_LOCAL) k_prule_process<PMODE_LOCAL><<<g, 256, 0, s>>>(C, W, evp, vs, out, n);
         else if (mode == PMODE_CM) k_prule_process<PMODE_CM><<<g, 256, 0, s>>>(C, W, evp, vs, out, n);
@@ -1832,7 +1881,8 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
                       &e->d_lres_count, &e->d_lres_w, &e->d_lres_rcp, &e->d_lres_kind, &e->d_lres_tcount,
                       &e->d_lres_flags, &e->w_lslow, &e->io_lrt, &e->d_lrule_grade,
                       &e->d_lg_on, &e->d_lg_dn, &e->d_lg_created, &e->d_lg_roff, &e->d_lg_rules, &e->d_lg_comp,
-                      &e->io_lctx})
+                      &e->io_lctx, &e->sp_keys, &e->sp_rule, &e->sp_state, &e->sp_n, &e->sp_w, &e->sp_rcp,
+                      &e->sp_Is, &e->sp_thr, &e->sp_kind, &e->w_cm})
         b->release();
     for (int k = 0; k < 2; ++k) {
         e->st_ev[k].release();

@@ -135,11 +135,14 @@ __global__ __launch_bounds__(SORT_THREADS) void k_prule_prep(
     int64_t nblocks) {
     __shared__ uint32_t hf[MAX_PASSES][RADIX];
     __shared__ uint32_t hl[MAX_PASSES][RADIX];
+    __shared__ uint32_t s_fresh;
     for (int d = threadIdx.x; d < MAX_PASSES * RADIX; d += SORT_THREADS) {
         (&hf[0][0])[d] = 0;
         (&hl[0][0])[d] = 0;
     }
+    if (threadIdx.x == 0) s_fresh = 0;
     __syncthreads();
+    uint32_t nfresh = 0;
     const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
     for (int j = 0; j < SORT_ITEMS; ++j) {
         const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
@@ -168,17 +171,20 @@ __global__ __launch_bounds__(SORT_THREADS) void k_prule_prep(
         if (st == 127 && table) {
             for (int32_t q = 0; q < cnt; ++q) {
                 const uint64_t key = vs.value((int64_t)b + q);
-                const int64_t h = slot_insert(table, cap_mask, key, fresh);
+                const int64_t h = slot_insert_counted(table, cap_mask, key, nfresh);
                 if (h < 0) { st = ST_FAIL; break; }                    // table full
                 vslot[b + q] = (uint32_t)h;
-                if (!LOCAL) {   // identical values from every writer of this slot
-                    M.rule[h] = e.idx;
-                    M.n[h] = R.n[e.idx];
-                    M.w[h] = R.w[e.idx];
-                    M.rcp[h] = R.rcp_w[e.idx];
-                    M.Is[h] = R.I_s[e.idx];
-                    M.thr[h] = value_threshold(R, (uint32_t)e.idx, key);
-                    M.kind[h] = KIND_PARAM;
+                if (!LOCAL) {   // identical values from every writer of this slot: stored only when they differ
+                    const int32_t rn = R.n[e.idx], rw = R.w[e.idx];
+                    const double rc = R.rcp_w[e.idx], is = R.I_s[e.idx];
+                    const double th = value_threshold(R, (uint32_t)e.idx, key);
+                    if (M.rule[h] != e.idx) M.rule[h] = e.idx;
+                    if (M.n[h] != rn) M.n[h] = rn;
+                    if (M.w[h] != rw) M.w[h] = rw;
+                    if (__double_as_longlong(M.rcp[h]) != __double_as_longlong(rc)) M.rcp[h] = rc;
+                    if (__double_as_longlong(M.Is[h]) != __double_as_longlong(is)) M.Is[h] = is;
+                    if (__double_as_longlong(M.thr[h]) != __double_as_longlong(th)) M.thr[h] = th;
+                    if (M.kind[h] != KIND_PARAM) M.kind[h] = KIND_PARAM;
                 }
             }
         }
@@ -192,7 +198,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_prule_prep(
         }
         if (st != 127) put_verdict(out, (uint32_t)i, st, 0, 0);
     }
-    __syncthreads();
+    block_add_global(fresh, nfresh, &s_fresh);              // (synchronises the block)
     tile_hist_store(hf, fhist, 1, nblocks);
     if (lkey) tile_hist_store(hl, lhist, 1, nblocks);
 }
@@ -283,6 +289,155 @@ __device__ inline uint64_t cm_check(const ParamCtx &C, uint32_t rule, int64_t E,
     for (int32_t q = 0; q < cnt; ++q) cm_add(C.CM, rule, vs.value((int64_t)b + q), nsc, E, a);
     if (cnt > 1) remaining = -1.0;
     return pack_verdict(ST_OK, java_d2i(remaining), 0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Shared count-min sketch (one sketch for every rule): the cells are shared between rules, so the
+// rules' lanes must move through the batch's epochs together.  If one rule's lane ran ahead to epoch
+// E + n and reset a cell slot to it, a lagging lane at epoch E would lose the count it had put there
+// and could then admit what the exact checker blocks.  k_prule_cm_sync therefore decides level by
+// level: level E = the smallest epoch any rule still has pending; every lane decides its rules'
+// segments at epochs <= E (a rule's epochs only go up under the documented precondition of
+// per-rule non-decreasing timestamps; a late segment is decided at once rather than waited for),
+// then a grid barrier.  Within a level every cell update is atomic (a CAS loop): rules of the same
+// epoch only add count to each other's cells (over-estimate, never under), so the sketch stays
+// one-sided.  Cells are read with device-scope atomic loads (other CUs' updates, no stale L1).
+__device__ inline uint64_t cm_load(const uint64_t *c) {
+    return __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the n slots of one cell, every load in flight before the sum (device-scope loads: no stale L1)
+constexpr int CM_NMAX = 16;
+__device__ inline int64_t cm_cell_sum_sync(const uint64_t *c, int nsc, int64_t E) {
+    uint64_t x[CM_NMAX];
+#pragma unroll
+    for (int j = 0; j < CM_NMAX; ++j) x[j] = j < nsc ? cm_load(c + j) : 0ull;
+    int64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < CM_NMAX; ++j) {
+        const uint32_t tag = (uint32_t)(x[j] >> CM_COUNT_BITS);
+        if (j < nsc && (((uint32_t)E - tag) & CM_TAG_MASK) < (uint32_t)nsc) s += (int64_t)(x[j] & CM_COUNT_MAX);
+    }
+    return s;
+}
+
+// Add a to the slot of E in every row: same tag -> add (saturating), an older tag -> restart at a, a
+// newer tag (only past the precondition: a rule's clock went back) -> add to the newer slot.
+__device__ inline void cm_add_sync(const CountMin &C, uint32_t rule, uint64_t key, int nsc, int64_t E, int32_t a) {
+    const int j = (int)(E % nsc);
+    const uint32_t te = (uint32_t)E & CM_TAG_MASK;
+    for (int d = 0; d < C.depth; ++d) {
+        unsigned long long *c = reinterpret_cast<unsigned long long *>(cm_cell(C, rule, d, key) + j);
+        unsigned long long x = cm_load(reinterpret_cast<const uint64_t *>(c));
+        for (;;) {
+            const uint32_t tag = (uint32_t)(x >> CM_COUNT_BITS);
+            // (an empty cell, count 0, has no epoch: its tag bits mean nothing)
+            const bool newer = (x & CM_COUNT_MAX) != 0 && tag != te && ((tag - te) & CM_TAG_MASK) < (CM_TAG_MASK >> 1);
+            uint64_t cnt = (tag == te || newer) ? (x & CM_COUNT_MAX) : 0;
+            cnt += (uint64_t)(uint32_t)a;
+            if (cnt > CM_COUNT_MAX) cnt = CM_COUNT_MAX;
+            const unsigned long long y = ((unsigned long long)(newer ? tag : te) << CM_COUNT_BITS) | cnt;
+            const unsigned long long prev = atomicCAS(c, x, y);
+            if (prev == x) break;
+            x = prev;
+        }
+    }
+}
+
+__device__ inline uint64_t cm_check_sync(const ParamCtx &C, uint32_t rule, int64_t E, int32_t a, const ValueSrc &vs,
+                                         int32_t b, int32_t cnt) {
+    const int nsc = C.R.n[rule];
+    const double I_s = C.R.I_s[rule];
+    double remaining = -1.0;
+    for (int32_t q = 0; q < cnt; ++q) {
+        const uint64_t key = vs.value((int64_t)b + q);
+        int64_t est = INT64_MAX;
+        for (int d = 0; d < C.CM.depth; ++d) {
+            const int64_t x = cm_cell_sum_sync(cm_cell(C.CM, rule, d, key), nsc, E);
+            est = x < est ? x : est;
+        }
+        const double next = remaining_of(value_threshold(C.R, rule, key), I_s, est, a);
+        remaining = next;
+        if (next < 0.0) return pack_verdict(ST_BLOCKED, 0, 0);
+    }
+    for (int32_t q = 0; q < cnt; ++q) cm_add_sync(C.CM, rule, vs.value((int64_t)b + q), nsc, E, a);
+    if (cnt > 1) remaining = -1.0;
+    return pack_verdict(ST_OK, java_d2i(remaining), 0);
+}
+
+// First segment of every rule present in the batch -> heads[] (cursor = that segment), count in *nh.
+__global__ __launch_bounds__(256) void k_cm_heads(BatchWork W, uint32_t *__restrict__ heads, uint32_t *__restrict__ nh) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t S = (int64_t)*W.nseg;
+    if (g >= S || (int64_t)*W.nvalid == 0) return;
+    if (g > 0 && W.seg_key[g - 1] == W.seg_key[g]) return;
+    heads[atomicAdd(nh, 1u)] = (uint32_t)g;
+}
+
+// Grid barrier for a cooperative launch (every workgroup resident): arrival count + generation.
+__device__ inline void cm_grid_barrier(unsigned int *count, unsigned int *gen, unsigned int nblocks) {
+    __threadfence();             // every thread's atomics (cells, next-level minimum) complete before arrival
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned int g = __hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (atomicAdd(count, 1u) == nblocks - 1) {
+            __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            while (__hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) __builtin_amdgcn_s_sleep(4);
+        }
+    }
+    __syncthreads();
+}
+
+// Control words (each on its own 64-byte line): ctl[0] head count, ctl[16] barrier arrivals, ctl[32]
+// barrier generation; level words lv[0..2] (64-bit) rotate: level k reads lv[k % 3], gathers the next
+// level's epoch into lv[(k + 1) % 3] (atomicMin; CM_NO_LEVEL = nothing pending) and clears
+// lv[(k + 2) % 3], which nobody touches during level k -- one grid barrier per level.
+// cursor[h] = the next segment of head h's rule.
+constexpr unsigned long long CM_NO_LEVEL = ~0ull;
+__global__ __launch_bounds__(256) void k_prule_cm_sync(ParamCtx C, BatchWork W, const ParamEvent *__restrict__ ev,
+                                                       ValueSrc vs, uint64_t *__restrict__ out,
+                                                       const uint32_t *__restrict__ heads, uint32_t *__restrict__ ctl,
+                                                       uint32_t *__restrict__ cursor, unsigned long long *lv) {
+    const uint32_t H = ctl[0];
+    const int64_t S = (int64_t)*W.nseg;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint32_t h = t0; h < H; h += stride) {           // level 0: the smallest first epoch
+        cursor[h] = heads[h];
+        atomicMin(&lv[0], (unsigned long long)W.seg_epoch[heads[h]]);
+    }
+    cm_grid_barrier(&ctl[16], &ctl[32], gridDim.x);
+    for (uint32_t k = 0;; ++k) {
+        const unsigned long long Eu = __hip_atomic_load(&lv[k % 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (Eu == CM_NO_LEVEL) break;                                  // grid-uniform
+        const int64_t E = (int64_t)Eu;
+        unsigned long long *next = &lv[(k + 1) % 3];
+        if (t0 == 0) __hip_atomic_store(&lv[(k + 2) % 3], CM_NO_LEVEL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t h = t0; h < H; h += stride) {
+            uint32_t g = cursor[h];
+            if (g == 0xFFFFFFFFu) continue;
+            const uint32_t rule = W.seg_key[heads[h]];
+            while ((int64_t)g < S && W.seg_key[g] == rule && W.seg_epoch[g] <= E) {
+                const int64_t Eg = W.seg_epoch[g];
+                const uint32_t end = W.seg_start[g + 1];
+                for (uint32_t i = W.seg_start[g]; i < end; ++i) {
+                    const uint32_t seq = (uint32_t)W.sval[i] & SEQ_MASK;
+                    const ParamEvent e = ev[seq];
+                    out[seq] = cm_check_sync(C, rule, Eg, e.acquire, vs, vs.begin(seq), vs.count(seq));
+                }
+                ++g;
+            }
+            if ((int64_t)g < S && W.seg_key[g] == rule) {
+                cursor[h] = g;
+                atomicMin(next, (unsigned long long)W.seg_epoch[g]);
+            } else {
+                cursor[h] = 0xFFFFFFFFu;
+            }
+        }
+        cm_grid_barrier(&ctl[16], &ctl[32], gridDim.x);
+    }
 }
 
 // ParamFlowChecker.passDefaultLocalCheck (PFC:127-202) on one (rule, value) bucket, single-threaded

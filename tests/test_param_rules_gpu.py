@@ -135,6 +135,28 @@ def test_count_min_is_one_sided(oracle_mod):
     assert viol == 0 and dec == 20_000
 
 
+@pytest.mark.gpu
+def test_shared_count_min_is_one_sided(oracle_mod):
+    """One sketch for every rule (BASELINE config 4's layout), narrow enough that rules collide, on
+    batches spanning ~75 epochs: the rules' lanes move through the epochs together (k_prule_cm_sync),
+    so no lane's reset of a shared cell slot drops a count a lagging rule still needs -- zero
+    violations of one-sidedness, and the false-block rate shrinks with the width."""
+    import sentinel_amd as sa
+    count, hot, rule_idx, vals, keys, ts = T.config4(200_000, seed=53, n_rules=5000, universe=200)
+    acq = np.ones(len(ts), np.int32)
+    rates = {}
+    for width in (1 << 10, 1 << 16):
+        svc, orc = _cluster_pair(oracle_mod, count, hot, sample_count=lambda r: 10)   # one window for all
+        svc.set_param_mode(sa._lib.PARAM_COUNT_MIN_SHARED, depth=4, width=width)
+        st = np.concatenate([svc.submit_param_batch_host(rule_idx[i:i + 50_000], acq[i:i + 50_000], keys[i:i + 50_000],
+                                                         ts[i:i + 50_000])[0] for i in range(0, len(ts), 50_000)])
+        n1 = np.ones(len(ts), np.int32)
+        viol, fb, dec = orc.param_cm_audit(rule_idx, acq, ts, np.arange(len(ts)), n1, keys, st)
+        assert viol == 0 and dec == len(ts), (width, viol)
+        rates[width] = fb / dec
+    assert rates[1 << 10] > rates[1 << 16]
+
+
 def _local_pair(oracle_mod, rules):
     import sentinel_amd as sa
     svc = sa.GpuTokenService(0)

@@ -60,7 +60,9 @@ def test_slot_reclamation_and_growth(oracle_mod, monkeypatch):
         t += 1000
     stats = svc.param_table_stats()
     assert stats["rebuilds"] >= 3, stats
-    assert stats["capacity"] <= 1 << 17, stats          # bounded by the live set, not by history
+    # bounded by the live set plus a few batches of values (the headroom that keeps rebuilds rare), not
+    # by history: holding all ~400k distinct keys at <= 3/4 load would take 2^20 slots
+    assert stats["capacity"] <= 1 << 19, stats
     for i in range(0, 2000, 37):
         r, k = int(ridx[i]), int(keys[i])
         assert svc.param_sum(r, k, int(ts[-1])) == orc.param_sum(r, int(ts[-1]), k)
