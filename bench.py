@@ -415,6 +415,7 @@ def main():
     for s in range(args.warmup):
         W.submit(ev_b[s])
         if args.config == "4cm" and len(keep_verdicts) < 2:     # the audited sample: the first two batches
+            svc.synchronize()                                   # (the engine stream wrote them; torch copies on its own)
             keep_verdicts.append(W.verdicts.clone())
     svc.synchronize()
 
@@ -440,6 +441,7 @@ def main():
         for s in range(args.warmup, args.warmup + pstep):
             W.submit(ev_b[s])
             if args.config == "4cm" and len(keep_verdicts) < 2:
+                svc.synchronize()
                 keep_verdicts.append(W.verdicts.clone())
         svc.synchronize()
         breakdown = read_profile()
@@ -496,15 +498,18 @@ def main():
     for j in range(min(K, L)):
         W.submit(lat_b[j])                               # first use of these buffers (not timed)
     advance()
-    tev = [torch.cuda.Event(enable_timing=True) for _ in range(L + 1)]
+    # a start and an end event per batch: the timestamp shifts of `advance` (8 elementwise kernels,
+    # ~0.4 ms, every K-th batch) run between one batch's end and the next one's start, outside both
+    tev0 = [torch.cuda.Event(enable_timing=True) for _ in range(L)]
+    tev1 = [torch.cuda.Event(enable_timing=True) for _ in range(L)]
     for i in range(L):
         if i and i % K == 0:
             advance()
-        tev[i].record(ext)
+        tev0[i].record(ext)
         W.submit(lat_b[i % K])
-    tev[L].record(ext)
+        tev1[i].record(ext)
     torch.cuda.synchronize()
-    lat = sorted(tev[i].elapsed_time(tev[i + 1]) for i in range(L))
+    lat = sorted(tev0[i].elapsed_time(tev1[i]) for i in range(L))
     hl = []
     for i in range(L):
         if i % K == 0:
@@ -657,8 +662,8 @@ def main():
         "p99_batch_ms": round(pct(lat, 0.99), 4),
         "median_batch_ms": round(lat[len(lat) // 2], 4),
         "latency_note": (f"{L} batches of an untimed loop after the timed steps: device time per batch between "
-                         f"torch events on the engine stream (back to back); p99_sync_ms = host clock with a "
-                         f"synchronize per batch"),
+                         f"a start and an end torch event around each submit on the engine stream (batches back "
+                         f"to back); p99_sync_ms = host clock with a synchronize per batch"),
         "p99_sync_ms": round(pct(hl, 0.99), 4),
         "median_sync_ms": round(hl[len(hl) // 2], 4),
         "snapshot_allgather_ms": None if snap_ms is None else round(snap_ms, 3),

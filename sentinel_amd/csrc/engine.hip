@@ -488,6 +488,8 @@ struct sentinel_engine {
     DevBuf d_cm;                       // count-min cells (SENTINEL_PARAM_COUNT_MIN)
     DevBuf w_cm;                       // shared sketch: rule heads, cursors, grid barrier, level words
     int cm_sync_blocks = 0;            // co-resident workgroups of k_prule_cm_sync
+    int param_path = 0;                // single-value exact requests: 0 per-slot segments, 1 per-rule walk
+    bool cm_force_coop = false;        // shared sketch: always the cooperative kernel (tests)
 
     // local param rules (ParamFlowChecker.passLocalCheck); rule index = load position
     int32_t nlrules = 0;
@@ -1526,6 +1528,10 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
 
 static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, uint64_t *out, hipStream_t s) {
     if (e->pmode != SENTINEL_PARAM_EXACT) return submit_prules(e, PMODE_CM, n, ev, nullptr, nullptr, 0, out, s);
+    // per-rule walk (sort by rule, one lane per rule, each request rolls and sums its value's slot): for
+    // many (rule, value) keys with a few requests each spread over many epochs, where the per-slot
+    // segment pipeline below builds one segment record per request
+    if (e->param_path == 1) return submit_prules(e, PMODE_EXACT, n, ev, nullptr, nullptr, 0, out, s);
     if (n <= 0) return 0;
     if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
     int rc = e->ensure_ws(n);
@@ -1659,7 +1665,8 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
         uint32_t *ctl = reinterpret_cast<uint32_t *>(e->w_cm.as<char>() + cbase);
         unsigned long long *lv = reinterpret_cast<unsigned long long *>(e->w_cm.as<char>() + cbase + 192);
         HIP_OK(hipMemsetAsync(ctl, 0, 192, s));            // head count, barrier arrivals and generation
-        HIP_OK(hipMemsetAsync(lv, 0xFF, 24, s));
+        HIP_OK(hipMemsetAsync(lv, 0xFF, 8, s));            // span: min (all ones) ...
+        HIP_OK(hipMemsetAsync(lv + 1, 0, 8, s));           // ... and max
         if (!e->cm_sync_blocks) {
             int per_cu = 0, cus = 0;
             HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(k_prule_cm_sync), 256, 0));
@@ -1667,10 +1674,26 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
             // at most one workgroup per CU: the grid barrier's cost grows with the workgroups
             e->cm_sync_blocks = std::max(1, std::min(per_cu, 1)) * std::max(1, cus);
         }
+        // the batch's epoch span: one launch per level when it is short (the kernel boundary is the
+        // barrier), the cooperative kernel's grid barrier otherwise
+        const unsigned hb = (unsigned)std::max<int64_t>(1, (H + 255) / 256);
+        k_cm_heads<<<g, 256, 0, s>>>(W, heads, ctl);
+        k_cm_span<<<hb, 256, 0, s>>>(W, heads, ctl, cursor, lv);
+        unsigned long long span[2] = {~0ull, 0};
+        HIP_OK(hipMemcpyAsync(span, lv, 16, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipStreamSynchronize(s));
+        if (span[0] != ~0ull && (int64_t)(span[1] - span[0]) < CM_LEVEL_LAUNCHES && !e->cm_force_coop) {
+            e->launch("prule_process", n, s, [&] {
+                for (int64_t E = (int64_t)span[0]; E <= (int64_t)span[1]; ++E)
+                    k_prule_cm_level<<<hb, 256, 0, s>>>(C, W, evp, vs, out, heads, ctl, cursor, E);
+            });
+            HIP_OK(hipGetLastError());
+            return 0;
+        }
+        HIP_OK(hipMemsetAsync(lv, 0xFF, 24, s));
         const unsigned nblk = (unsigned)std::max<int64_t>(1, std::min<int64_t>(e->cm_sync_blocks, (H + 255) / 256));
         hipError_t ce = hipSuccess;
         e->launch("prule_process", n, s, [&] {
-            k_cm_heads<<<g, 256, 0, s>>>(W, heads, ctl);
             void *args[] = {(void *)&C, (void *)&W, (void *)&evp, (void *)&vs, (void *)&out, (void *)&heads, (void *)&ctl,
                             (void *)&cursor, (void *)&lv};
             ce = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(k_prule_cm_sync), dim3(nblk), dim3(256), args, 0, s);
@@ -1833,6 +1856,8 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
         e->process_impl = v == "group" ? 1 : v == "thread" ? 2 : 0;
     }
     if (const char *c = getenv("SENTINEL_VERDICT_NT")) e->verdict_nt = std::string(c) == "1";
+    if (const char *c = getenv("SENTINEL_PARAM_PATH")) e->param_path = std::string(c) == "rule" ? 1 : 0;
+    if (const char *c = getenv("SENTINEL_CM_LEVELS")) e->cm_force_coop = std::string(c) == "coop";
     if (const char *c = getenv("SENTINEL_SCAN")) e->use_lookback = std::string(c) != "3pass";
     if (const char *c = getenv("SENTINEL_DIAG_LINEAR")) e->diag_linear = std::string(c) == "1";
     if (const char *c = getenv("SENTINEL_HOT_HET_RUN")) e->hot_het_run = (uint32_t)std::max(WAVE_HET_RUN, (uint32_t)atoi(c));

@@ -440,6 +440,49 @@ __global__ __launch_bounds__(256) void k_prule_cm_sync(ParamCtx C, BatchWork W, 
     }
 }
 
+// The same level order with one launch per level (the kernel boundary is the barrier): for batches
+// spanning up to CM_LEVEL_LAUNCHES epochs.  k_cm_span gives the host the batch's epoch range.
+constexpr int64_t CM_LEVEL_LAUNCHES = 4096;
+__global__ __launch_bounds__(256) void k_cm_span(BatchWork W, const uint32_t *__restrict__ heads,
+                                                 const uint32_t *__restrict__ ctl, uint32_t *__restrict__ cursor,
+                                                 unsigned long long *span) {
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= ctl[0]) return;
+    const uint32_t g = heads[h];
+    cursor[h] = g;
+    const int64_t S = (int64_t)*W.nseg;
+    const uint32_t rule = W.seg_key[g];
+    uint32_t l = g;
+    while ((int64_t)l + 1 < S && W.seg_key[l + 1] == rule) ++l;
+    atomicMin(&span[0], (unsigned long long)W.seg_epoch[g]);
+    atomicMax(&span[1], (unsigned long long)W.seg_epoch[l]);
+}
+
+__global__ __launch_bounds__(256) void k_prule_cm_level(ParamCtx C, BatchWork W, const ParamEvent *__restrict__ ev,
+                                                        ValueSrc vs, uint64_t *__restrict__ out,
+                                                        const uint32_t *__restrict__ heads,
+                                                        const uint32_t *__restrict__ ctl, uint32_t *__restrict__ cursor,
+                                                        int64_t E) {
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= ctl[0]) return;
+    uint32_t g = cursor[h];
+    if (g == 0xFFFFFFFFu) return;
+    const int64_t S = (int64_t)*W.nseg;
+    const uint32_t rule = W.seg_key[heads[h]];
+    if (W.seg_epoch[g] > E) return;
+    while ((int64_t)g < S && W.seg_key[g] == rule && W.seg_epoch[g] <= E) {
+        const int64_t Eg = W.seg_epoch[g];
+        const uint32_t end = W.seg_start[g + 1];
+        for (uint32_t i = W.seg_start[g]; i < end; ++i) {
+            const uint32_t seq = (uint32_t)W.sval[i] & SEQ_MASK;
+            const ParamEvent e = ev[seq];
+            out[seq] = cm_check_sync(C, rule, Eg, e.acquire, vs, vs.begin(seq), vs.count(seq));
+        }
+        ++g;
+    }
+    cursor[h] = ((int64_t)g < S && W.seg_key[g] == rule) ? g : 0xFFFFFFFFu;
+}
+
 // ParamFlowChecker.passDefaultLocalCheck (PFC:127-202) on one (rule, value) bucket, single-threaded
 // (every CAS of the reference succeeds).  Returns 1 pass, 0 block, -1 when the time counter exists
 // without a token counter (only after an LRU eviction; the reference spins there).

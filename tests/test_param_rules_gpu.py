@@ -136,12 +136,14 @@ def test_count_min_is_one_sided(oracle_mod):
 
 
 @pytest.mark.gpu
-def test_shared_count_min_is_one_sided(oracle_mod):
+@pytest.mark.parametrize("levels", ["launch", "coop"])
+def test_shared_count_min_is_one_sided(oracle_mod, monkeypatch, levels):
     """One sketch for every rule (BASELINE config 4's layout), narrow enough that rules collide, on
     batches spanning ~75 epochs: the rules' lanes move through the epochs together (k_prule_cm_sync),
     so no lane's reset of a shared cell slot drops a count a lagging rule still needs -- zero
     violations of one-sidedness, and the false-block rate shrinks with the width."""
     import sentinel_amd as sa
+    monkeypatch.setenv("SENTINEL_CM_LEVELS", levels)      # one launch per epoch level, or the grid barrier
     count, hot, rule_idx, vals, keys, ts = T.config4(200_000, seed=53, n_rules=5000, universe=200)
     acq = np.ones(len(ts), np.int32)
     rates = {}
