@@ -89,6 +89,7 @@ def lib():
         "orc_engine_new": (vp, [vp, vp, C.c_int]),
         "orc_engine_free": (None, [vp]),
         "orc_engine_load_flow_rules": (C.c_int, [vp, vp, C.c_int]),
+        "orc_engine_set_connected_count": (None, [vp, C.c_int32, C.c_int32]),
         "orc_request_token": (None, [vp, i32, i32, C.c_int, i64, vp, vp, vp]),
         "orc_flow_replay": (None, [vp, i64, vp, vp, vp, vp, vp, vp, vp]),
         "orc_flow_replay_mt": (C.c_int, [vp, i64, vp, vp, vp, vp, vp, vp, vp, C.c_int]),
@@ -500,6 +501,9 @@ class TokenServiceOracle:
         st, rem = C.c_int8(), C.c_int32()
         lib().orc_request_param_token(self.h, rule_idx, acquire, t, _p(v), len(v), C.byref(st), C.byref(rem))
         return st.value, rem.value
+
+    def set_connected_count(self, ns, connected):
+        lib().orc_engine_set_connected_count(self.h, int(ns), int(connected))
 
     def param_replay(self, rule_idx, acquire, keys, ts):
         n = len(ts)

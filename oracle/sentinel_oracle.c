@@ -849,6 +849,12 @@ int orc_engine_param_window(const orc_engine *e, int32_t idx, int32_t *out2) {
 }
 
 /* CPFC:101-120 calcGlobalThreshold(rule, value) */
+/* ConnectionManager's connected count of a namespace changes (client PING / disconnect): every later
+ * AVG_LOCAL threshold reads it (CFC:38-48, CPFC:101-111). */
+void orc_engine_set_connected_count(orc_engine *e, int32_t ns, int32_t connected) {
+    if (ns >= 0 && ns < e->n_ns) e->ns[ns].connected_count = connected;
+}
+
 static double param_threshold(const orc_engine *e, const orc_param_rule *r, uint64_t v) {
     double count = r->count;
     for (int i = 0; i < r->hot_n; i++)                       /* ParamFlowRule.java:157-162 */

@@ -101,6 +101,7 @@ orc_engine *orc_engine_new(const orc_server_config *cfg, const orc_namespace *ns
 void orc_engine_free(orc_engine *e);
 /* Returns the number of dense flows (valid rules, one per flowId).  Reload semantics in the .c. */
 int  orc_engine_load_flow_rules(orc_engine *e, const orc_flow_rule *rules, int n);
+void orc_engine_set_connected_count(orc_engine *e, int32_t ns, int32_t connected);
 /* Server window change: every metric (flow and param, orphans included) restarts with it. */
 int  orc_engine_reset_metrics(orc_engine *e, int sample_count, int interval_ms);
 int  orc_engine_flow_window(const orc_engine *e, int32_t flow_idx, int32_t *out2);

@@ -874,6 +874,9 @@ struct sentinel_engine {
                       const std::vector<int32_t> &new_rn, const std::vector<int64_t> &imp, int64_t imp_stride,
                       const std::vector<int32_t> &imp_rule, std::vector<std::pair<int32_t, std::vector<int64_t>>> *exported);
     int param_reserve(int64_t nv);
+    int param_thresholds();
+    std::vector<uint64_t> h_phot_keys;          // the loaded param rules' hot items (hot_begin / hot_n index them)
+    std::vector<int32_t> h_phot_counts;
     int reset_param_metrics(int32_t sample_count, int32_t interval_ms);
     bool uniform_param_window() const {
         for (size_t i = 1; i < h_prule_n.size(); ++i)
@@ -1112,6 +1115,49 @@ int sentinel_engine::param_reserve(int64_t nv) {
         if (rc) return rc;
     }
     p_ub = (uint64_t)nv;
+    return 0;
+}
+
+// Param thresholds: ClusterParamFlowChecker.calcGlobalThreshold(rule, value) (CPFC:101-111) -- the
+// hot-item count of the value if any, else rule.count (getRawThreshold, CPFC:113-120), times the
+// namespace's connectedCount for AVG_LOCAL rules.  The reference evaluates it on every request, so
+// it is recomputed whenever a connected count changes (not only at rule load).  Hot items live in a
+// table keyed by param key (param keys are unique per (rule, value)).
+int sentinel_engine::param_thresholds() {
+    const size_t R = prules.size();
+    std::vector<double> thr(std::max<size_t>(R, 1), 0.0);
+    std::vector<std::pair<uint64_t, double>> hot;
+    for (size_t i = 0; i < R; ++i) {
+        const sentinel_param_rule_t &r = prules[i];
+        const int32_t cc = (r.namespace_idx >= 0 && r.namespace_idx < (int32_t)ns.size()) ? ns[r.namespace_idx].connected_count : 0;
+        double c = r.count;
+        if (r.threshold_type != SENTINEL_THRESHOLD_GLOBAL) c = c * (double)cc;
+        thr[i] = c;
+        for (int32_t h = 0; h < r.hot_n; ++h) {
+            const int32_t j = r.hot_begin + h;
+            if (j < 0 || (size_t)j >= h_phot_counts.size()) continue;
+            double hc = (double)h_phot_counts[j];
+            if (r.threshold_type != SENTINEL_THRESHOLD_GLOBAL) hc = hc * (double)cc;
+            hot.emplace_back(h_phot_keys[j], hc);
+        }
+    }
+    uint64_t hcap = 16;
+    while (hcap < 2 * hot.size() + 2) hcap <<= 1;
+    std::vector<uint64_t> hk(hcap, PKEY_EMPTY);
+    std::vector<double> hv(hcap, 0.0);
+    for (auto &kv : hot) {
+        uint64_t h = mix64(kv.first) & (hcap - 1);
+        while (hk[h] != PKEY_EMPTY && hk[h] != kv.first) h = (h + 1) & (hcap - 1);
+        hk[h] = kv.first;
+        hv[h] = kv.second;
+    }
+    int rc = 0;
+    rc |= upload(d_prule_thr, thr);
+    rc |= upload(d_hot_table, hk);
+    rc |= upload(d_hot_thr, hv);
+    if (rc) return rc;
+    hot_mask = hcap - 1;
+    has_hot = !hot.empty();
     return 0;
 }
 
@@ -2014,7 +2060,9 @@ int sentinel_set_namespaces(sentinel_engine_t *e, const sentinel_namespace_t *ns
     e->ns.assign(ns, ns + n);
     int rc = e->rebuild_limiters();
     if (rc) return rc;
-    return e->rebuild_flow_thresholds();
+    rc = e->rebuild_flow_thresholds();
+    if (rc) return rc;
+    return e->param_thresholds();
 }
 
 int sentinel_set_connected_count(sentinel_engine_t *e, int32_t nsi, int32_t connected) {
@@ -2024,7 +2072,9 @@ int sentinel_set_connected_count(sentinel_engine_t *e, int32_t nsi, int32_t conn
     HIP_OK(hipSetDevice(e->device));
     HIP_OK(hipStreamSynchronize(e->stream));
     e->ns[nsi].connected_count = connected;
-    return e->rebuild_flow_thresholds();
+    const int rc = e->rebuild_flow_thresholds();
+    if (rc) return rc;
+    return e->param_thresholds();       // AVG_LOCAL param rules read connectedCount on every request too
 }
 
 int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *rules, int32_t n) {
@@ -2376,24 +2426,11 @@ int sentinel_load_param_rules(sentinel_engine_t *e, const sentinel_param_rule_t 
         }
     }
     std::vector<int32_t> ww(std::max<size_t>(R, 1), 1);
-    std::vector<double> rcp(std::max<size_t>(R, 1), 1.0), Is(std::max<size_t>(R, 1), 1.0), thr(std::max<size_t>(R, 1), 0.0);
-    std::vector<std::pair<uint64_t, double>> hot;
+    std::vector<double> rcp(std::max<size_t>(R, 1), 1.0), Is(std::max<size_t>(R, 1), 1.0);
     for (size_t i = 0; i < R; ++i) {
-        const sentinel_param_rule_t &r = nr[i];
         ww[i] = gint[i] / gn[i];
         rcp[i] = 1.0 / (double)ww[i];
         Is[i] = gint[i] / 1000.0;
-        // calcGlobalThreshold(rule, value) without hot item: count or count*connectedCount (CPFC:101-111)
-        const int32_t cc = (r.namespace_idx >= 0 && r.namespace_idx < (int32_t)e->ns.size()) ? e->ns[r.namespace_idx].connected_count : 0;
-        double c = r.count;
-        if (r.threshold_type != SENTINEL_THRESHOLD_GLOBAL) c = c * (double)cc;
-        thr[i] = c;
-        for (int32_t h = 0; h < r.hot_n; ++h) {
-            const int32_t j = r.hot_begin + h;
-            double hc = (double)hot_counts[j];
-            if (r.threshold_type != SENTINEL_THRESHOLD_GLOBAL) hc = hc * (double)cc;
-            hot.emplace_back(hot_keys[j], hc);
-        }
     }
     int rc = 0;
     if (!e->d_pfresh.p) rc |= e->d_pfresh.ensure(8);
@@ -2416,22 +2453,9 @@ int sentinel_load_param_rules(sentinel_engine_t *e, const sentinel_param_rule_t 
     rc |= upload(e->d_prule_w, ww);
     rc |= upload(e->d_prule_rcp, rcp);
     rc |= upload(e->d_prule_Is, Is);
-    rc |= upload(e->d_prule_thr, thr);
-    // hot-item table keyed by param key (param keys are unique per (rule, value))
-    uint64_t hcap = 16;
-    while (hcap < 2 * hot.size() + 2) hcap <<= 1;
-    std::vector<uint64_t> hk(hcap, PKEY_EMPTY);
-    std::vector<double> hv(hcap, 0.0);
-    for (auto &kv : hot) {
-        uint64_t h = mix64(kv.first) & (hcap - 1);
-        while (hk[h] != PKEY_EMPTY && hk[h] != kv.first) h = (h + 1) & (hcap - 1);
-        hk[h] = kv.first;
-        hv[h] = kv.second;
-    }
-    e->hot_mask = hcap - 1;
-    e->has_hot = !hot.empty();
-    rc |= upload(e->d_hot_table, hk);
-    rc |= upload(e->d_hot_thr, hv);
+    e->h_phot_keys.assign(hot_keys, hot_keys + n_hot);
+    e->h_phot_counts.assign(hot_counts, hot_counts + n_hot);
+    rc |= e->param_thresholds();
     rc |= upload(e->d_prule_kind, std::vector<uint8_t>(std::max<size_t>(R, 1), KIND_PARAM));
     if (rc) return rc;
     rc = e->rebuild_cm();

@@ -14,12 +14,13 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-def _cluster_pair(oracle_mod, count, hot, sample_count=lambda r: 2 if r % 2 else 5, namespaces=None):
+def _cluster_pair(oracle_mod, count, hot, sample_count=lambda r: 2 if r % 2 else 5, namespaces=None,
+                  threshold_type=lambda r: 1):
     import sentinel_amd as sa
     from sentinel_amd.token_service import ServerNamespace
     R = len(count)
     prules = [sa.ParamFlowRule(count=float(count[r]), cluster_config=sa.ClusterFlowConfig(
-        flow_id=r + 1, threshold_type=1, sample_count=sample_count(r), window_interval_ms=1000),
+        flow_id=r + 1, threshold_type=threshold_type(r), sample_count=sample_count(r), window_interval_ms=1000),
         hot_items=hot.get(r, {}), namespace=(r % len(namespaces)) if namespaces else 0) for r in range(R)]
     svc = sa.GpuTokenService(0)
     ns = namespaces or [dict()]
@@ -28,7 +29,7 @@ def _cluster_pair(oracle_mod, count, hot, sample_count=lambda r: 2 if r % 2 else
     orc = oracle_mod.TokenServiceOracle(
         [], namespaces=[dict(connected_count=n.get("connected_count", 0), has_limiter=n.get("has_limiter", 0),
                              max_allowed_qps=n.get("max_allowed_qps", 30000.0)) for n in ns],
-        param_rules=[dict(flow_id=r + 1, count=float(count[r]), threshold_type=1, sample_count=sample_count(r),
+        param_rules=[dict(flow_id=r + 1, count=float(count[r]), threshold_type=threshold_type(r), sample_count=sample_count(r),
                           window_interval_ms=1000, namespace_idx=(r % len(namespaces)) if namespaces else 0)
                      for r in range(R)],
         hot_items={r: list(hot[r].items()) for r in hot})
@@ -157,6 +158,30 @@ def test_shared_count_min_is_one_sided(oracle_mod, monkeypatch, levels):
         assert viol == 0 and dec == len(ts), (width, viol)
         rates[width] = fb / dec
     assert rates[1 << 10] > rates[1 << 16]
+
+
+@pytest.mark.gpu
+def test_avg_local_params_follow_connected_count(oracle_mod):
+    """ClusterParamFlowChecker.calcGlobalThreshold reads ConnectionManager.getConnectedCount on every
+    request (CPFC:101-111): AVG_LOCAL param rules (hot items included) must see a connected count that
+    changes between batches, as clients PING in and leave."""
+    import sentinel_amd as sa
+    count, hot, rule_idx, vals, keys, ts = T.config4(40_000, seed=59, n_rules=40, universe=60)
+    # rules of namespace 0 and 1 alternate; every third rule is GLOBAL, the others AVG_LOCAL
+    svc, orc = _cluster_pair(oracle_mod, count, hot, namespaces=[dict(connected_count=1), dict(connected_count=3)],
+                             threshold_type=lambda r: 1 if r % 3 == 0 else 0)
+    acq = np.ones(len(ts), np.int32)
+    for step, (c0, c1) in enumerate([(1, 3), (4, 0), (2, 5), (0, 1)]):
+        svc.set_connected_count(0, c0)
+        svc.set_connected_count(1, c1)
+        orc.set_connected_count(0, c0)
+        orc.set_connected_count(1, c1)
+        a, b = step * 10_000, (step + 1) * 10_000
+        st_g, rem_g = svc.submit_param_batch_host(rule_idx[a:b], acq[a:b], keys[a:b], ts[a:b])
+        st_o, rem_o = orc.param_replay(rule_idx[a:b], acq[a:b], keys[a:b], ts[a:b])
+        bad = np.nonzero((st_g != st_o) | (rem_g != rem_o))[0]
+        assert len(bad) == 0, (step, len(bad), bad[:5], st_g[bad[:5]], st_o[bad[:5]])
+        assert (st_o == 1).any() and (st_o == 0).any(), step
 
 
 def _local_pair(oracle_mod, rules):
