@@ -52,7 +52,7 @@ KERNEL_BYTES_PER_EVENT = {
     "part_prep": 16.0,        # read the 16-B event (range histogram in LDS; no key array without namespace routes)
     "part_scatter": 24.0,     # read the 16-B event (key re-derived), write the 8-B packed value (local key inside)
     "param_prep": 48.0,       # read the 24-B event, write key 4 + slot rule 4, slot insert (8-B CAS), verdict slot 8
-    "param_meta": 48.0,       # read key 4 + event key 8, rule fields ~16, write the slot's 5 fields (~20 B)
+    "param_meta": 48.0,       # per slot after a rule / threshold / table change: key 8, rule fields ~16, write ~20 B
     "prule_prep": 36.0,       # read the 24-B event + value 8, write key 4
 }
 

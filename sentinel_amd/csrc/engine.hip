@@ -162,7 +162,8 @@ __global__ __launch_bounds__(SORT_THREADS) void k_flow_prep(
 // (rule, value): the host's injective encoding of the Java typed value.
 __global__ __launch_bounds__(SORT_THREADS) void k_param_prep(
     int64_t n, const ParamEvent *__restrict__ ev, int32_t nrules, const int32_t *__restrict__ route,
-    unsigned long long *table, uint64_t cap_mask, int32_t *slot_rule, unsigned long long *fresh,
+    unsigned long long *table, uint64_t cap_mask, int32_t *slot_rule, ParamRules PR, SlotMeta M,
+    unsigned long long *fresh,
     uint64_t *__restrict__ out, uint32_t *__restrict__ fkey, uint32_t finvalid, int fpasses, uint32_t *__restrict__ fhist,
     uint32_t *__restrict__ lkey, uint32_t linvalid, int lpasses, uint32_t *__restrict__ lhist, int64_t nblocks) {
     __shared__ uint32_t hf[MAX_PASSES][RADIX];
@@ -189,13 +190,22 @@ __global__ __launch_bounds__(SORT_THREADS) void k_param_prep(
             if (r == ROUTE_TOO_MANY) st = ST_TOO_MANY_REQUEST;
             else if (e.ts < 0) st = ST_FAIL;
             else {
+                const uint32_t before = nfresh;
                 const int64_t h = slot_insert_counted(table, cap_mask, e.key, nfresh);
                 if (h < 0) st = ST_FAIL;          // table full: the host's param_reserve prevents it
                 else {
                     k = (uint32_t)h;
-                    // identical value from every writer of this slot: written only when it differs (a
-                    // hot slot is read by every event of its value, not stored to)
-                    if (slot_rule[h] != e.idx) slot_rule[h] = e.idx;
+                    // the inserting event writes the slot's rule and window fields once; they only change
+                    // with the rules / thresholds / table, when k_param_meta_all rewrites every slot
+                    if (nfresh != before) {
+                        slot_rule[h] = e.idx;
+                        M.n[h] = PR.n[e.idx];
+                        M.w[h] = PR.w[e.idx];
+                        M.rcp[h] = PR.rcp_w[e.idx];
+                        M.Is[h] = PR.I_s[e.idx];
+                        M.thr[h] = value_threshold(PR, (uint32_t)e.idx, e.key);   // CPFC:113-120
+                        M.kind[h] = KIND_PARAM;
+                    }
                     if (r >= 0) l = (uint32_t)r;
                 }
             }
@@ -213,34 +223,23 @@ __global__ __launch_bounds__(SORT_THREADS) void k_param_prep(
     if (lkey) tile_hist_store(hl, lhist, lpasses, nblocks);
 }
 
-// Per event: refresh the per-slot parameters of its param slot from the rule (identical writes).
-__global__ __launch_bounds__(256) void k_param_meta(int64_t n, const uint32_t *__restrict__ fkey, uint32_t finvalid,
-                                                    const ParamEvent *__restrict__ ev,
-                                                    const int32_t *__restrict__ slot_rule,
-                                                    const int32_t *__restrict__ rule_n, const int32_t *__restrict__ rule_w,
-                                                    const double *__restrict__ rule_rcp, const double *__restrict__ rule_Is,
-                                                    const double *__restrict__ rule_thr,
-                                                    const unsigned long long *__restrict__ hot_table, uint64_t hot_mask,
-                                                    const double *__restrict__ hot_thr,
-                                                    int32_t *slot_n, int32_t *slot_w, double *slot_rcp, double *slot_Is,
-                                                    double *slot_thr, uint8_t *slot_kind) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t s = fkey[i];
-    if (s == finvalid) return;
+// Every live slot's window fields and threshold from its rule (after a rule load, a threshold change
+// or a table rebuild; fresh inserts write their own in k_param_prep).
+__global__ __launch_bounds__(256) void k_param_meta_all(uint64_t cap, const unsigned long long *__restrict__ keys,
+                                                        const int32_t *__restrict__ slot_rule, int32_t nrules,
+                                                        ParamRules PR, SlotMeta M) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= cap) return;
+    const unsigned long long key = keys[s];
+    if (key == PKEY_EMPTY) return;
     const int32_t r = slot_rule[s];
-    double thr = rule_thr[r];
-    const int64_t h = slot_find(hot_table, hot_mask, ev[i].key);   // ClusterParamFlowChecker.getRawThreshold (CPFC:113-120)
-    if (h >= 0) thr = hot_thr[h];
-    // compare before store: every event of a hot value refreshes the same slot with the same values
-    const int32_t nn = rule_n[r], ww = rule_w[r];
-    const double rc = rule_rcp[r], is = rule_Is[r];
-    if (slot_n[s] != nn) slot_n[s] = nn;
-    if (slot_w[s] != ww) slot_w[s] = ww;
-    if (__double_as_longlong(slot_rcp[s]) != __double_as_longlong(rc)) slot_rcp[s] = rc;
-    if (__double_as_longlong(slot_Is[s]) != __double_as_longlong(is)) slot_Is[s] = is;
-    if (__double_as_longlong(slot_thr[s]) != __double_as_longlong(thr)) slot_thr[s] = thr;
-    if (slot_kind[s] != KIND_PARAM) slot_kind[s] = KIND_PARAM;
+    if ((uint32_t)r >= (uint32_t)nrules) return;
+    M.n[s] = PR.n[r];
+    M.w[s] = PR.w[r];
+    M.rcp[s] = PR.rcp_w[r];
+    M.Is[s] = PR.I_s[r];
+    M.thr[s] = value_threshold(PR, (uint32_t)r, key);
+    M.kind[s] = KIND_PARAM;
 }
 
 // One key's slot (or -1) for the host's read-only queries.
@@ -489,6 +488,7 @@ struct sentinel_engine {
     DevBuf w_cm;                       // shared sketch: rule heads, cursors, grid barrier, level words
     int cm_sync_blocks = 0;            // co-resident workgroups of k_prule_cm_sync
     int param_path = 0;                // single-value exact requests: 0 per-slot segments, 1 per-rule walk
+    bool pmeta_dirty = true;           // the slots' window fields / thresholds need k_param_meta_all
     bool cm_force_coop = false;        // shared sketch: always the cooperative kernel (tests)
 
     // local param rules (ParamFlowChecker.passLocalCheck); rule index = load position
@@ -1083,6 +1083,7 @@ int sentinel_engine::param_rebuild(uint64_t new_cap, const std::vector<int32_t> 
     p_live = cnt[0];
     p_ub = 0;
     ++p_rebuilds;
+    pmeta_dirty = true;
     return 0;
 }
 
@@ -1158,6 +1159,7 @@ int sentinel_engine::param_thresholds() {
     if (rc) return rc;
     hot_mask = hcap - 1;
     has_hot = !hot.empty();
+    pmeta_dirty = true;
     return 0;
 }
 
@@ -1602,24 +1604,22 @@ static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, u
     e->launch("param_prep", n, s, [&] {
         k_param_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
             n, ev, have ? R : 0, e->param_plain ? nullptr : e->d_prule_route.as<int32_t>(),
-            e->d_ptable.as<unsigned long long>(), P - 1, e->d_slot_rule.as<int32_t>(),
-            e->d_pfresh.as<unsigned long long>(), out, fkey, pinvalid,
+            e->d_ptable.as<unsigned long long>(), P - 1, e->d_slot_rule.as<int32_t>(), e->param_ctx().R,
+            e->slot_meta(), e->d_pfresh.as<unsigned long long>(), out, fkey, pinvalid,
             1, e->w_fhist.as<uint32_t>(), lkey, linvalid, 1, e->w_lhist.as<uint32_t>(), nb);
     });
     if (!have) {
         HIP_OK(hipGetLastError());
         return 0;
     }
-    e->launch("param_meta", n, s, [&] {
-        k_param_meta<<<grid_for(n), 256, 0, s>>>(n, fkey, pinvalid, ev, e->d_slot_rule.as<int32_t>(),
-                                                 e->d_prule_n.as<int32_t>(), e->d_prule_w.as<int32_t>(),
-                                                 e->d_prule_rcp.as<double>(), e->d_prule_Is.as<double>(),
-                                                 e->d_prule_thr.as<double>(),
-                                                 e->has_hot ? e->d_hot_table.as<unsigned long long>() : nullptr,
-                                                 e->hot_mask, e->d_hot_thr.as<double>(), e->pt.n.as<int32_t>(),
-                                                 e->pt.w.as<int32_t>(), e->pt.rcp.as<double>(), e->pt.Is.as<double>(),
-                                                 e->pt.thr.as<double>(), e->pt.kind.as<uint8_t>());
-    });
+    if (e->pmeta_dirty) {                  // rules / thresholds / table changed since the last batch
+        e->launch("param_meta", n, s, [&] {
+            k_param_meta_all<<<grid_for((int64_t)P), 256, 0, s>>>(P, e->d_ptable.as<unsigned long long>(),
+                                                                  e->d_slot_rule.as<int32_t>(), R, e->param_ctx().R,
+                                                                  e->slot_meta());
+        });
+        e->pmeta_dirty = false;
+    }
     Verdicts V{out, fkey, pinvalid};
     if (lim) {
         KeyTable LT = e->table(e->lt, 1, e->lim_stride);
