@@ -610,6 +610,30 @@ def main():
                 "algorithmic_bytes_per_launch": round((bpe or 0.0) * d["units_per_call"], 1),
                 "bytes_per_event": bpe, "avg_us": round(d["avg_us"], 2)}
 
+    # ---- rule reload at the workload's size (ClusterFlowRuleManager.loadRules: putMetricIfAbsent keeps
+    # surviving flowIds' windows, the device remaps the blocked tables): 5% of the flowIds removed, 5% of
+    # the survivors with a new window (they keep their old metric), 5% new flowIds; host clock around the
+    # call, which returns with the new table in place (untimed region, after every other leg)
+    reload_ms = None
+    if isinstance(W, FlowWorkload) and args.config in ("3", "2"):
+        r = W.rules
+        F = len(r.flow_id)
+        keep = np.arange(F) % 20 != 7
+        fid = np.concatenate([r.flow_id[keep], r.flow_id.max() + 1 + np.arange(F // 20, dtype=np.int64)])
+        cnt = np.concatenate([r.count[keep], r.count[: F // 20]])
+        sc = np.concatenate([r.sample_count[keep], r.sample_count[: F // 20]]).astype(np.int32)
+        sc[: len(sc) // 20] = np.where(sc[: len(sc) // 20] % 2 == 0, sc[: len(sc) // 20] // 2, sc[: len(sc) // 20])
+        tt = np.full(len(fid), 1, np.int32)
+        wi = np.full(len(fid), 1000, np.int32)
+        ns = np.zeros(len(fid), np.int32)
+        ck = np.zeros(len(fid), np.int32)
+        svc.synchronize()
+        r0 = time.perf_counter()
+        svc.load_rules_array(fid, cnt, tt, sc, wi, ns, ck)
+        svc.synchronize()
+        reload_ms = (time.perf_counter() - r0) * 1000.0
+        log(f"rule reload of {len(fid)} flows: {reload_ms:.1f} ms")
+
     # ---- CPU baseline: the oracle ("port") on bounded samples of the same workload, rank 0, N=1
     cpu = cpu1 = None
     model, ncpu, avail = cpu_info()
@@ -667,6 +691,7 @@ def main():
         "p99_sync_ms": round(pct(hl, 0.99), 4),
         "median_sync_ms": round(hl[len(hl) // 2], 4),
         "snapshot_allgather_ms": None if snap_ms is None else round(snap_ms, 3),
+        "rule_reload_ms": None if reload_ms is None else round(reload_ms, 2),
         "host_path": host_path,
         "pipeline_bytes_per_decision": round(W.pipeline_bytes(), 2),
         "pipeline_hbm_frac": round(value / world * W.pipeline_bytes() / (HBM_PEAK_GBS * 1e9), 4),

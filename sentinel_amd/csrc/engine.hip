@@ -1397,10 +1397,31 @@ static int part_front(sentinel_engine_t *e, const PartBufs &B, int64_t n, const 
     uint32_t *rtot = rstart + g.nparts + 1;
     unsigned long long *stat = B.stat->as<unsigned long long>();
     uint32_t *ctl = B.runs->as<uint32_t>();
+    // namespace limiters (GlobalRequestLimiter.tryPass before every flow check, CFC:50-57) couple the
+    // flows of a namespace: validation and the limiter pass run first (the sorted path's k_flow_prep and
+    // limiter pipeline, which mark failing events invalid); the multi-split then takes their keys
+    const bool lim = e->nlimiters > 0 && !e->flow_plain;
+    if (lim) {
+        const int lbits = bits_for(e->nlimiters);
+        const uint32_t linvalid = ((uint32_t)1 << lbits) - 1;
+        uint32_t *lkey = e->w_lkey.as<uint32_t>();
+        const int64_t nbs = sort_blocks(n);
+        HIP_OK(hipMemsetAsync(e->w_counters.p, 0, 16, s));
+        e->launch("flow_prep", n, s, [&] {
+            k_flow_prep<<<dim3((unsigned)nbs), dim3(SORT_THREADS), 0, s>>>(
+                n, ev, g.F, e->d_flow_route.as<int32_t>(), out, fkey, g.finvalid, 1, e->w_fhist.as<uint32_t>(), lkey,
+                linvalid, 1, e->w_lhist.as<uint32_t>(), nbs);
+        });
+        const Verdicts LV{out, fkey, g.finvalid};
+        const KeyTable LT = e->table(e->lt, 1, e->lim_stride);
+        const EventSrc lsrc{ev, nullptr, nullptr, true};
+        e->run_pipeline(LT, lkey, e->w_lhist.as<uint32_t>(), n, lbits, lsrc, LV, s, 10, true);
+    }
     e->launch("part_prep", n, s, [&] {
         k_part_prep<<<dim3((unsigned)g.nb), dim3(PP_THREADS), 0, s>>>(
-            n, ev, g.F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, e->flow_plain ? nullptr : fkey,
-            g.finvalid, g.lb, hist, g.nb, g.nparts, ctl, stat);
+            n, ev, g.F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out,
+            (e->flow_plain || lim) ? nullptr : fkey, g.finvalid, g.lb, hist, g.nb, g.nparts, ctl, stat,
+            lim ? fkey : nullptr);
     });
     e->launch("scan", n, s, [&] {
         const dim3 g2((unsigned)g.ng, (unsigned)((g.nparts + PS_THREADS - 1) / PS_THREADS));
@@ -1448,13 +1469,14 @@ static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, co
     return part_back(e, B, n, ev, fl, out, s);
 }
 
-// Partition-local path for this batch?  (No namespace limiter -- a limiter couples flows --, windows of
-// <= 16 buckets, <= 2^20 flows; auto picks it for large flow tables and falls back to the radix sort
-// for 1024 batches after a skewed one: a hot flow serialises its range's workgroup.)
+// Partition-local path for this batch?  (Windows of <= 16 buckets, <= 2^20 flows; auto picks it for
+// large flow tables and falls back to the radix sort for 1024 batches after a skewed one: a hot flow
+// serialises its range's workgroup.  Namespace limiters run their pass first, in part_front.)
 static bool choose_part(sentinel_engine_t *e, int64_t n) {
     const int32_t F = (int32_t)e->rules.size();
     const bool lim = e->nlimiters > 0 && !e->flow_plain;
-    bool part = !lim && F > 0 && e->flow_max_n <= 16 && bits_for(F) <= 2 * PART_MAX_BITS &&
+    (void)lim;                          // (namespace limiters: the limiter pass runs first, part_front)
+    bool part = F > 0 && e->flow_max_n <= 16 && bits_for(F) <= 2 * PART_MAX_BITS &&
                 (e->flow_path == 2 || (e->flow_path == 0 && F >= 32768));
     const int64_t batch = e->flow_batches++;
     if (part && e->flow_path == 0) {

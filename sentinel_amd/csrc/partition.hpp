@@ -55,7 +55,8 @@ __global__ __launch_bounds__(PP_THREADS) void k_part_prep(int64_t n, const Event
                                                             uint32_t finvalid, int lb, uint32_t *__restrict__ hist,
                                                             int64_t nblocks, int32_t nparts,
                                                             uint32_t *__restrict__ ctl_zero,
-                                                            unsigned long long *__restrict__ stat_zero) {
+                                                            unsigned long long *__restrict__ stat_zero,
+                                                            const uint32_t *__restrict__ keys_pre) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {        // the batch's work-list counters and skew statistic
         if (ctl_zero) { ctl_zero[0] = 0; ctl_zero[1] = 0; ctl_zero[2] = 0; }
         if (stat_zero) *stat_zero = 0;
@@ -77,6 +78,11 @@ __global__ __launch_bounds__(PP_THREADS) void k_part_prep(int64_t n, const Event
         const Event e = evs[j];
         int st = 127;
         uint32_t k = finvalid;
+        if (keys_pre) {       // validated (and limited: GlobalRequestLimiter) upstream, verdicts written there
+            k = keys_pre[i];
+            if (k != finvalid) atomicAdd(&h[k >> lb], 1u);
+            continue;
+        }
         if (e.idx == SENTINEL_IDX_BAD_ID || e.acquire <= 0) st = ST_BAD_REQUEST;      // DTS:38-40
         else if (e.idx < 0 || e.idx >= nflows) st = ST_NO_RULE_EXISTS;               // DTS:42-45
         else if (route && route[e.idx] == ROUTE_TOO_MANY) st = ST_TOO_MANY_REQUEST;  // namespace == null (CFC:50-53)
