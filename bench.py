@@ -273,6 +273,14 @@ class FlowWorkload:
         n = int(self.rules.sample_count.max())
         return 21.0 + (n * 64 + 64 + 16) / max(1.0, self.N / max(1, self.F))
 
+    def pipeline_bytes_engine(self):
+        """The bytes this engine's own layout must move per decision: 16 B event + 8 B verdict, per
+        touched flow the n {epoch, PASS} header pairs read (16 n) and the rolled one written (16), the
+        rolled slot's BLOCK / PASS_REQUEST / BLOCK_REQUEST rows read and written (48) and ~42 B of rule
+        fields (w, 1/w, I_s, threshold, kind, occupy flag)."""
+        n = int(self.rules.sample_count.max())
+        return 24.0 + (16 * n + 16 + 48 + 42) / max(1.0, self.N / max(1, self.F))
+
     def shape(self):
         return {"config": self.args.config, "flows": self.F, "events": self.N,
                 "sample_count": int(self.rules.sample_count.max())}
@@ -695,6 +703,10 @@ def main():
         "host_path": host_path,
         "pipeline_bytes_per_decision": round(W.pipeline_bytes(), 2),
         "pipeline_hbm_frac": round(value / world * W.pipeline_bytes() / (HBM_PEAK_GBS * 1e9), 4),
+        "pipeline_bytes_engine_layout": (round(W.pipeline_bytes_engine(), 2)
+                                         if hasattr(W, "pipeline_bytes_engine") else None),
+        "pipeline_hbm_frac_engine_layout": (round(value / world * W.pipeline_bytes_engine() / (HBM_PEAK_GBS * 1e9), 4)
+                                            if hasattr(W, "pipeline_bytes_engine") else None),
         "roofline": roof,
         "cpu_baseline": cpu,
         "cpu_baseline_1core": cpu1,

@@ -126,17 +126,29 @@ __global__ __launch_bounds__(SORT_THREADS) void k_flow_prep(
     }
     __syncthreads();
     const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
-#pragma unroll 4
+    // every event load of the tile in flight at once, then every route load (a load per item inside
+    // the loop made each thread wait SORT_ITEMS memory round trips in a row)
+    Event evs[SORT_ITEMS];
+    int32_t rts[SORT_ITEMS];
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
+        evs[j] = i < n ? ev[i] : Event{SENTINEL_IDX_BAD_ID, 0, 0};
+    }
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j)
+        rts[j] = (route && evs[j].idx >= 0 && evs[j].idx < nflows) ? route[evs[j].idx] : ROUTE_PLAIN;
+#pragma unroll
     for (int j = 0; j < SORT_ITEMS; ++j) {
         const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
         if (i >= n) break;
-        const Event e = ev[i];
+        const Event e = evs[j];
         int st = 127;   // undecided
         uint32_t k = finvalid, l = linvalid;
         if (e.idx == SENTINEL_IDX_BAD_ID || e.acquire <= 0) st = ST_BAD_REQUEST;
         else if (e.idx < 0 || e.idx >= nflows) st = ST_NO_RULE_EXISTS;
         else {
-            const int32_t r = route ? route[e.idx] : ROUTE_PLAIN;
+            const int32_t r = rts[j];
             if (r == ROUTE_TOO_MANY) st = ST_TOO_MANY_REQUEST;      // namespace == null
             else if (e.ts < 0) st = ST_FAIL;                          // reference: NPE in LeapArray
             else {
@@ -177,10 +189,16 @@ __global__ __launch_bounds__(SORT_THREADS) void k_param_prep(
     __syncthreads();
     uint32_t nfresh = 0;
     const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
+    ParamEvent pevs[SORT_ITEMS];                           // every event load of the tile in flight at once
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
+        if (i < n) pevs[j] = ev[i];
+    }
     for (int j = 0; j < SORT_ITEMS; ++j) {
         const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
         if (i >= n) break;
-        const ParamEvent e = ev[i];
+        const ParamEvent e = pevs[j];
         int st = 127;
         uint32_t k = finvalid, l = linvalid;
         if (e.idx == SENTINEL_IDX_BAD_ID || e.acquire <= 0) st = ST_BAD_REQUEST;
@@ -2115,6 +2133,10 @@ int sentinel_load_flow_rules(sentinel_engine_t *e, const sentinel_flow_rule_t *r
     std::vector<sentinel_flow_rule_t> nr;
     std::unordered_map<int64_t, int32_t> nidx;
     std::vector<int32_t> gn, gint;
+    nr.reserve((size_t)n);                 // (1M-rule reloads: no rehashing / regrowth on the way)
+    nidx.reserve((size_t)n);
+    gn.reserve((size_t)n);
+    gint.reserve((size_t)n);
     for (int32_t i = 0; i < n; ++i) {
         const sentinel_flow_rule_t &r = rules[i];
         if (r.flow_id <= 0 || !(r.count >= 0) || !valid_window(r.sample_count, r.window_interval_ms)) continue;

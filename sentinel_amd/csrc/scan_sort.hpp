@@ -238,7 +238,18 @@ inline int64_t hist_words(int64_t n, int passes) { return sort_blocks(n) * RADIX
 
 // Per-tile digit histograms of every pass, from one read of the keys.  The tile of block b is
 // [b*SORT_TILE, (b+1)*SORT_TILE): the same tiling k_radix_scatter uses.
+// One count per key digit.  When every active lane of the wave holds the same digit (a namespace-limiter
+// key: one or a few namespaces for the whole batch) the first lane adds them all at once instead of 64
+// lanes queueing atomics on one LDS word.
 __device__ inline void tile_hist_accumulate(uint32_t (*h)[RADIX], uint32_t key, int passes) {
+    const uint64_t act = __builtin_amdgcn_read_exec();
+    const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
+    if (__builtin_amdgcn_ballot_w64(key == k0) == act) {
+        if ((uint64_t)1 << lane_id() == (act & (~act + 1)))
+            for (int p = 0; p < passes; ++p)
+                atomicAdd(&h[p][(k0 >> (p * RADIX_BITS)) & (RADIX - 1)], (uint32_t)__popcll(act));
+        return;
+    }
     for (int p = 0; p < passes; ++p) atomicAdd(&h[p][(key >> (p * RADIX_BITS)) & (RADIX - 1)], 1u);
 }
 
