@@ -711,6 +711,158 @@ __global__ __launch_bounds__(SEG_THREADS) void k_segments(KeyTable T, BatchWork 
     }
 }
 
+// k_segments without staging the tile in LDS: each thread reads its own ITEMS contiguous sorted
+// keys and values with 16-byte vector loads (a wave still covers one contiguous stretch), issues
+// every item's window-width gather before the first epoch is computed, and exchanges only its run's
+// first / last element through LDS.  Same outputs and preconditions as k_segments.
+template <int THREADS, int ITEMS>
+__global__ __launch_bounds__(THREADS) void k_segments_v(KeyTable T, BatchWork W, EventSrc src, int64_t n,
+                                                         uint32_t invalid, unsigned long long *status,
+                                                         uint32_t *ticket) {
+    static_assert(ITEMS % 4 == 0, "4 keys / 2 values per vector load");
+    constexpr int TILE = THREADS * ITEMS;
+    __shared__ uint32_t f_key[THREADS + 1];     // first key of every thread's run (+ the next tile's)
+    __shared__ uint32_t l_key[THREADS];
+    __shared__ int64_t l_ep[THREADS];
+    __shared__ int32_t l_acq[THREADS];
+    __shared__ uint32_t waves[THREADS / WAVE];
+    __shared__ uint32_t s_bid, s_prefix;
+    __shared__ uint32_t p_key;
+    __shared__ int64_t p_ep;
+    __shared__ int32_t p_acq;
+    if (threadIdx.x == 0) s_bid = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int64_t bid = s_bid;
+    const int64_t base = bid * TILE;
+    const int64_t i0 = base + (int64_t)threadIdx.x * ITEMS;
+    const int64_t T0 = src.t0();
+    uint32_t key[ITEMS];
+    uint64_t val[ITEMS];
+    const bool full = i0 + ITEMS <= n;
+    if (full) {
+        const uint4 *kp = reinterpret_cast<const uint4 *>(W.skey + i0);
+        const uint4 *vp = reinterpret_cast<const uint4 *>(W.sval + i0);
+#pragma unroll
+        for (int m = 0; m < ITEMS / 4; ++m) {
+            const uint4 k = kp[m];
+            key[4 * m] = k.x; key[4 * m + 1] = k.y; key[4 * m + 2] = k.z; key[4 * m + 3] = k.w;
+        }
+#pragma unroll
+        for (int m = 0; m < ITEMS / 2; ++m) {
+            const uint4 v = vp[m];
+            val[2 * m] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+            val[2 * m + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const bool in = i0 + j < n;
+            key[j] = in ? W.skey[i0 + j] : invalid;
+            val[j] = in ? W.sval[i0 + j] : 0ull;
+        }
+    }
+    if (threadIdx.x == 0) {           // the element just before this tile, and the one after it
+        p_key = invalid;
+        p_ep = 0;
+        p_acq = 0;
+        if (base > 0 && base - 1 < n) {
+            const uint32_t k = W.skey[base - 1];
+            if (k != invalid) {
+                int64_t t;
+                int32_t a;
+                bool pr;
+                src.unpack(W.sval[base - 1], T0, t, a, pr);
+                p_key = k;
+                p_ep = epoch_of(t, T.w[k], T.rcp_w[k]);
+                p_acq = a;
+            }
+        }
+        f_key[THREADS] = base + TILE < n ? W.skey[base + TILE] : invalid;
+    }
+    int32_t wv[ITEMS];
+    double rc[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const bool ok = key[j] != invalid;
+        wv[j] = ok ? T.w[key[j]] : 1;
+        rc[j] = ok ? T.rcp_w[key[j]] : 1.0;
+    }
+    int64_t ep[ITEMS];
+    int32_t acq[ITEMS];
+    uint32_t priomask = 0;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        ep[j] = 0;
+        acq[j] = 0;
+        if (key[j] != invalid) {
+            int64_t t;
+            bool pr;
+            src.unpack(val[j], T0, t, acq[j], pr);
+            ep[j] = epoch_of(t, wv[j], rc[j]);
+            if (pr && T.kind[key[j]] == KIND_CLUSTER) priomask |= 1u << j;
+        }
+    }
+    f_key[threadIdx.x] = key[0];
+    l_key[threadIdx.x] = key[ITEMS - 1];
+    l_ep[threadIdx.x] = ep[ITEMS - 1];
+    l_acq[threadIdx.x] = acq[ITEMS - 1];
+    __syncthreads();
+    uint32_t pk = threadIdx.x ? l_key[threadIdx.x - 1] : p_key;
+    int64_t pe = threadIdx.x ? l_ep[threadIdx.x - 1] : p_ep;
+    int32_t pa = threadIdx.x ? l_acq[threadIdx.x - 1] : p_acq;
+    const uint32_t next_key = f_key[threadIdx.x + 1];
+    uint32_t headmask = 0, badmask = 0;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        if (key[j] != invalid) {
+            const bool head = pk != key[j] || pe != ep[j];
+            if (head) headmask |= 1u << j;
+            if ((!head && pa != acq[j]) || (priomask & (1u << j))) badmask |= 1u << j;
+        }
+        pk = key[j];
+        pe = ep[j];
+        pa = acq[j];
+    }
+    uint32_t total;
+    uint32_t g = block_exclusive_scan((uint32_t)__popc(headmask), waves, &total);
+    tile_lookback(bid, total, status, ticket + 1, &s_prefix);
+    __syncthreads();
+    g += s_prefix;                   // segments started before this thread's run
+    uint32_t sid[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const int64_t i = i0 + j;
+        sid[j] = 0;
+        if (key[j] == invalid) continue;
+        if (headmask & (1u << j)) {
+            ++g;
+            W.seg_start[g - 1] = (uint32_t)i;
+            W.seg_key[g - 1] = key[j];
+            W.seg_epoch[g - 1] = ep[j];
+            W.seg_acq[g - 1] = acq[j];
+        }
+        if (badmask & (1u << j)) W.seg_het[g - 1] = 1;
+        if (priomask & (1u << j)) W.seg_prio[g - 1] = 1;
+        sid[j] = g;                  // 1-based segment id
+        const bool last = (i == n - 1) || (j + 1 < ITEMS ? key[j + 1] == invalid : next_key == invalid);
+        if (last) {
+            *W.nvalid = (uint32_t)(i + 1);
+            *W.nseg = g;
+            W.seg_start[g] = (uint32_t)(i + 1);
+        }
+    }
+    if (bid == 0 && threadIdx.x == 0 && key[0] == invalid) { *W.nvalid = 0; *W.nseg = 0; }
+    if (full) {
+        uint4 *sp = reinterpret_cast<uint4 *>(W.segid + i0);
+#pragma unroll
+        for (int m = 0; m < ITEMS / 4; ++m) sp[m] = make_uint4(sid[4 * m], sid[4 * m + 1], sid[4 * m + 2], sid[4 * m + 3]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j)
+            if (i0 + j < n) W.segid[i0 + j] = sid[j];
+    }
+}
+
 // After the inclusive scan of heads: per-segment records.  seg_het must be zeroed beforehand.
 __global__ __launch_bounds__(256) void k_seg_mark(BatchWork W, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

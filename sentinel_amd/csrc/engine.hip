@@ -97,6 +97,17 @@ int upload(DevBuf &b, const std::vector<T> &v) {
     return 0;
 }
 
+// The flow routes as bytes (ROUTE_* or a limiter key < 128); released when a key does not fit, so the
+// kernels gather the 32-bit routes.
+int upload_route8(DevBuf &b, const std::vector<int32_t> &route) {
+    std::vector<int8_t> r8(route.size());
+    for (size_t i = 0; i < route.size(); ++i) {
+        if (route[i] < -128 || route[i] > 127) { b.release(); return 0; }
+        r8[i] = (int8_t)route[i];
+    }
+    return upload(b, r8);
+}
+
 // Device-side key tables (SoA).
 struct TableBufs {
     DevBuf off, n, w, rcp, Is, thr, kind, state, occ, has_occ;
@@ -117,7 +128,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_flow_prep(
     int64_t n, const Event *__restrict__ ev, int32_t nflows, const int32_t *__restrict__ route,
     uint64_t *__restrict__ out, uint32_t *__restrict__ fkey, uint32_t finvalid, int fpasses,
     uint32_t *__restrict__ fhist, uint32_t *__restrict__ lkey, uint32_t linvalid, int lpasses,
-    uint32_t *__restrict__ lhist, int64_t nblocks) {
+    uint32_t *__restrict__ lhist, int64_t nblocks, const int8_t *__restrict__ route8 = nullptr) {
     __shared__ uint32_t hf[MAX_PASSES][RADIX];
     __shared__ uint32_t hl[MAX_PASSES][RADIX];
     for (int d = threadIdx.x; d < MAX_PASSES * RADIX; d += SORT_THREADS) {
@@ -136,8 +147,10 @@ __global__ __launch_bounds__(SORT_THREADS) void k_flow_prep(
         evs[j] = i < n ? ev[i] : Event{SENTINEL_IDX_BAD_ID, 0, 0};
     }
 #pragma unroll
-    for (int j = 0; j < SORT_ITEMS; ++j)
-        rts[j] = (route && evs[j].idx >= 0 && evs[j].idx < nflows) ? route[evs[j].idx] : ROUTE_PLAIN;
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const bool in = evs[j].idx >= 0 && evs[j].idx < nflows;
+        rts[j] = (route8 && in) ? (int32_t)route8[evs[j].idx] : (route && in) ? route[evs[j].idx] : ROUTE_PLAIN;
+    }
 #pragma unroll
     for (int j = 0; j < SORT_ITEMS; ++j) {
         const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
@@ -444,6 +457,9 @@ struct sentinel_engine {
     std::unordered_map<int64_t, Orphan> orphans;
     TableBufs ft;
     DevBuf d_flow_route, d_flow_ids;
+    DevBuf d_flow_route8;            // the same routes as bytes when every limiter key fits (a 4x smaller gather)
+    bool use_route8 = true;          // SENTINEL_ROUTE8=0: gather the 32-bit routes
+    const int8_t *route8() { return use_route8 ? d_flow_route8.as<int8_t>() : nullptr; }
     bool flow_plain = true;          // no flow needs a limiter or namespace check
     int32_t flow_max_n = 1;
     int32_t flow_hblock = 2;        // slots per block of the flow header region (>= every flow's n)
@@ -452,6 +468,7 @@ struct sentinel_engine {
     bool verdict_nt = false;   // SENTINEL_VERDICT_NT=1: non-temporal verdict stores
     bool use_lookback = true;  // SENTINEL_SCAN=3pass selects the three-kernel scan
     bool fused_segments = true; // SENTINEL_SEGMENTS=split selects heads -> scan -> mark
+    int seg_impl = 2;            // fused segments: 0 LDS-staged tile, 1 / 2 per-thread vector runs (256x16 / 512x8)
     int flow_path = 0;         // SENTINEL_FLOW_PATH: 0 auto, 1 sorted (global radix sort), 2 partition-local,
                                // 3 small (every batch in one-launch chunks of SM_MAX events)
     // small-batch host path (k_small_flow reads / writes pinned host memory directly)
@@ -808,7 +825,12 @@ struct sentinel_engine {
             uint32_t *ticket = (uint32_t *)(status + nt);
             (void)hipMemsetAsync(status, 0, (size_t)nt * 8 + 16, s);
             launch("segments", n, s, [&] {
-                k_segments<<<dim3((unsigned)nt), dim3(SEG_THREADS), 0, s>>>(T, W, src, n, invalid, status, ticket);
+                if (seg_impl == 1)
+                    k_segments_v<256, 16><<<dim3((unsigned)nt), dim3(256), 0, s>>>(T, W, src, n, invalid, status, ticket);
+                else if (seg_impl == 2)
+                    k_segments_v<512, 8><<<dim3((unsigned)nt), dim3(512), 0, s>>>(T, W, src, n, invalid, status, ticket);
+                else
+                    k_segments<<<dim3((unsigned)nt), dim3(SEG_THREADS), 0, s>>>(T, W, src, n, invalid, status, ticket);
             });
         } else {
             launch("seg_heads", n, s, [&] { k_seg_heads<<<g, 256, 0, s>>>(T, W, src, n, invalid); });
@@ -1283,6 +1305,8 @@ int sentinel_engine::rebuild_routes() {
     flow_plain = flow_routes(rules, route);
     int rc = upload(d_flow_route, route);
     if (rc) return rc;
+    rc = upload_route8(d_flow_route8, route);
+    if (rc) return rc;
     std::vector<int32_t> proute(prules.size());
     param_plain = true;
     for (size_t i = 0; i < prules.size(); ++i) {
@@ -1427,8 +1451,8 @@ static int part_front(sentinel_engine_t *e, const PartBufs &B, int64_t n, const 
         HIP_OK(hipMemsetAsync(e->w_counters.p, 0, 16, s));
         e->launch("flow_prep", n, s, [&] {
             k_flow_prep<<<dim3((unsigned)nbs), dim3(SORT_THREADS), 0, s>>>(
-                n, ev, g.F, e->d_flow_route.as<int32_t>(), out, fkey, g.finvalid, 1, e->w_fhist.as<uint32_t>(), lkey,
-                linvalid, 1, e->w_lhist.as<uint32_t>(), nbs);
+                n, ev, g.F, e->d_flow_route.as<int32_t>(), out, fkey, g.finvalid, 0, e->w_fhist.as<uint32_t>(), lkey,
+                linvalid, 1, e->w_lhist.as<uint32_t>(), nbs, e->route8());
         });
         const Verdicts LV{out, fkey, g.finvalid};
         const KeyTable LT = e->table(e->lt, 1, e->lim_stride);
@@ -1528,8 +1552,9 @@ static int submit_flow_sorted(sentinel_engine_t *e, int64_t n, const Event *ev, 
     HIP_OK(hipMemsetAsync(e->w_counters.p, 0, 16, s));
     e->launch("flow_prep", n, s, [&] {
         k_flow_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
-            n, ev, F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, fkey, finvalid, 1,
-            e->w_fhist.as<uint32_t>(), lkey, linvalid, 1, e->w_lhist.as<uint32_t>(), nb);
+            n, ev, F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, fkey, finvalid, lim ? 0 : 1,
+            e->w_fhist.as<uint32_t>(), lkey, linvalid, 1, e->w_lhist.as<uint32_t>(), nb,
+            e->flow_plain ? nullptr : e->route8());
     });
     Verdicts V{out, fkey, finvalid};
     EventSrc src{ev, nullptr, fl, false};
@@ -1952,6 +1977,8 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
         e->flow_path = v == "sorted" ? 1 : v == "partition" ? 2 : v == "small" ? 3 : 0;
     }
     if (const char *c = getenv("SENTINEL_SEGMENTS")) e->fused_segments = std::string(c) != "split";
+    if (const char *c = getenv("SENTINEL_SEG_IMPL")) e->seg_impl = atoi(c);
+    if (const char *c = getenv("SENTINEL_ROUTE8")) e->use_route8 = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_PARAM_CAPACITY")) {
         uint64_t v = strtoull(c, nullptr, 10);
         uint64_t p = 1024;
@@ -1978,7 +2005,7 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
     e->ft.release();
     e->lt.release();
     e->pt.release();
-    for (DevBuf *b : {&e->d_flow_route, &e->d_flow_ids, &e->d_prule_route, &e->d_prule_n, &e->d_prule_w,
+    for (DevBuf *b : {&e->d_flow_route, &e->d_flow_route8, &e->d_flow_ids, &e->d_prule_route, &e->d_prule_n, &e->d_prule_w,
                       &e->d_prule_rcp, &e->d_prule_Is, &e->d_prule_thr, &e->d_ptable, &e->d_slot_rule,
                       &e->d_hot_table, &e->d_hot_thr, &e->w_fkey, &e->w_lkey, &e->w_skey, &e->w_sval, &e->w_ktmp,
                       &e->w_vtmp, &e->w_fhist, &e->w_lhist, &e->w_parts, &e->w_segid, &e->w_bad, &e->w_hep,
@@ -2222,10 +2249,10 @@ int sentinel_engine::install_flows(std::vector<sentinel_flow_rule_t> &&nr, std::
     nnv.resize(F1, 1);
     // new device buffers
     TableBufs nft;
-    DevBuf nroute, nids, nnow, ncthr, s1w, s1r, s1k, dsrc, dstg, dstgoff;
+    DevBuf nroute, nroute8, nids, nnow, ncthr, s1w, s1r, s1k, dsrc, dstg, dstgoff;
     auto cleanup = [&] {
         nft.release();
-        for (DevBuf *b : {&nroute, &nids, &nnow, &ncthr, &s1w, &s1r, &s1k, &dsrc, &dstg, &dstgoff}) b->release();
+        for (DevBuf *b : {&nroute, &nroute8, &nids, &nnow, &ncthr, &s1w, &s1r, &s1k, &dsrc, &dstg, &dstgoff}) b->release();
     };
     int rc = 0;
     rc |= upload(nft.off, off);
@@ -2236,6 +2263,7 @@ int sentinel_engine::install_flows(std::vector<sentinel_flow_rule_t> &&nr, std::
     rc |= upload(nft.kind, kind);
     rc |= upload(nft.thr, thr);
     rc |= upload(nroute, route);
+    rc |= upload_route8(nroute8, route);
     rc |= upload(nids, ids);
     rc |= upload(ncthr, cthr);
     rc |= upload(s1w, std::vector<int32_t>(F1, 1 << 30));
@@ -2299,6 +2327,7 @@ int sentinel_engine::install_flows(std::vector<sentinel_flow_rule_t> &&nr, std::
     for (size_t k = 0; k < orphan_old.size(); ++k) orphans[rules[orphan_old[k]].flow_id] = std::move(new_orphans[k]);
     std::swap(ft, nft);
     std::swap(d_flow_route, nroute);
+    std::swap(d_flow_route8, nroute8);
     std::swap(d_flow_ids, nids);
     std::swap(d_now, nnow);
     std::swap(d_conc_thr, ncthr);
