@@ -182,6 +182,92 @@ __global__ __launch_bounds__(SORT_THREADS) void k_flow_prep(
     if (lkey) tile_hist_store(hl, lhist, lpasses, nblocks);
 }
 
+// One namespace limiter (what the reference holds after any namespace-set change with the default
+// namespace only, ClusterServerConfigManager.java:228-257): k_flow_prep's validation and routing, and
+// the limiter pipeline's stable partition, in one pass over the batch.  Requests that reach
+// GlobalRequestLimiter.tryPass (route 0) are packed in arrival order at the front of (skey, sval) --
+// exactly what the radix pass over their limiter key leaves there -- and every other position gets
+// the invalid key (from the back; their order is never read: the pipeline stops at nvalid).  Loads
+// stay coalesced (item j of thread t is event j * L1_THREADS + t of the tile); the arrival-order rank
+// comes from one ballot per item and a scan of the (item, wave) counts; tiles take a ticket and find
+// how many limiter requests precede them by decoupled look-back (status / ticket words cleared first).
+constexpr int L1_THREADS = 512, L1_ITEMS = 8, L1_TILE = L1_THREADS * L1_ITEMS, L1_WAVES = L1_THREADS / WAVE;
+static_assert(L1_ITEMS * L1_WAVES == WAVE, "one (item, wave) count per lane of the scanning wave");
+__global__ __launch_bounds__(L1_THREADS) void k_lim1_prep(
+    int64_t n, const Event *__restrict__ ev, int32_t nflows, const int32_t *__restrict__ route,
+    const int8_t *__restrict__ route8, uint64_t *__restrict__ out, uint32_t *__restrict__ fkey, uint32_t finvalid,
+    uint32_t linvalid, uint32_t *__restrict__ skey, uint64_t *__restrict__ sval, EventSrc src,
+    unsigned long long *status, uint32_t *ticket) {
+    __shared__ uint32_t s_cnt[L1_ITEMS * L1_WAVES];   // [item][wave] limiter requests, then their offsets
+    __shared__ uint32_t s_bid, s_prefix;
+    if (threadIdx.x == 0) s_bid = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int64_t bid = s_bid;
+    const int64_t tile0 = bid * L1_TILE;
+    const int wave = threadIdx.x / WAVE;
+    Event evs[L1_ITEMS];
+#pragma unroll
+    for (int j = 0; j < L1_ITEMS; ++j) {
+        const int64_t i = tile0 + j * L1_THREADS + threadIdx.x;
+        evs[j] = i < n ? ev[i] : Event{SENTINEL_IDX_BAD_ID, 0, 0};
+    }
+    int32_t rts[L1_ITEMS];
+#pragma unroll
+    for (int j = 0; j < L1_ITEMS; ++j) {
+        const bool in = evs[j].idx >= 0 && evs[j].idx < nflows;
+        rts[j] = !in ? ROUTE_PLAIN : route8 ? (int32_t)route8[evs[j].idx] : route[evs[j].idx];
+    }
+    uint64_t bal[L1_ITEMS];
+#pragma unroll
+    for (int j = 0; j < L1_ITEMS; ++j) {
+        const int64_t i = tile0 + j * L1_THREADS + threadIdx.x;
+        const Event e = evs[j];
+        int st = 127;   // undecided
+        uint32_t k = finvalid;
+        bool lim = false;
+        if (e.idx == SENTINEL_IDX_BAD_ID || e.acquire <= 0) st = ST_BAD_REQUEST;
+        else if (e.idx < 0 || e.idx >= nflows) st = ST_NO_RULE_EXISTS;
+        else {
+            const int32_t r = rts[j];
+            if (r == ROUTE_TOO_MANY) st = ST_TOO_MANY_REQUEST;      // namespace == null
+            else if (e.ts < 0) st = ST_FAIL;                          // reference: NPE in LeapArray
+            else {
+                k = (uint32_t)e.idx;
+                lim = r >= 0;
+            }
+        }
+        if (i < n) {
+            fkey[i] = k;
+            if (st != 127) put_verdict(out, (uint32_t)i, st, 0, 0);
+        }
+        bal[j] = __ballot(lim && i < n);
+        if (lane_id() == 0) s_cnt[j * L1_WAVES + wave] = (uint32_t)__popcll(bal[j]);
+    }
+    __syncthreads();
+    if (threadIdx.x < WAVE) {
+        const uint32_t c = s_cnt[threadIdx.x];
+        const uint32_t inc = wave_inclusive_scan(c);
+        s_cnt[threadIdx.x] = inc - c;
+        const uint32_t total = __shfl(inc, WAVE - 1);
+        tile_lookback(bid, total, status, ticket + 1, &s_prefix);
+    }
+    __syncthreads();
+    const int64_t T0 = src.t0();
+#pragma unroll
+    for (int j = 0; j < L1_ITEMS; ++j) {
+        const int64_t i = tile0 + j * L1_THREADS + threadIdx.x;
+        if (i >= n) continue;
+        // limiter requests before event i (global)
+        const int64_t v = (int64_t)s_prefix + s_cnt[j * L1_WAVES + wave] + mask_rank(bal[j]);
+        if ((bal[j] >> lane_id()) & 1) {
+            skey[v] = 0;
+            sval[v] = src.pack_event((uint32_t)i, evs[j], 0, T0);
+        } else {
+            skey[n - 1 - (i - v)] = linvalid;       // i - v other events before i
+        }
+    }
+}
+
 // requestParamToken validation (DTS:51-62) + param slot lookup/insert in the open-addressing
 // table (exact per-value counters: ClusterParamMetric.java:46-82).  Param keys are unique per
 // (rule, value): the host's injective encoding of the Java typed value.
@@ -459,6 +545,7 @@ struct sentinel_engine {
     DevBuf d_flow_route, d_flow_ids;
     DevBuf d_flow_route8;            // the same routes as bytes when every limiter key fits (a 4x smaller gather)
     bool use_route8 = true;          // SENTINEL_ROUTE8=0: gather the 32-bit routes
+    bool lim1 = true;                // one namespace limiter: k_lim1_prep (SENTINEL_LIM1=0: prep + radix pass)
     const int8_t *route8() { return use_route8 ? d_flow_route8.as<int8_t>() : nullptr; }
     bool flow_plain = true;          // no flow needs a limiter or namespace check
     int32_t flow_max_n = 1;
@@ -812,10 +899,10 @@ struct sentinel_engine {
 
     // K2 sort by key + (key, epoch) segment records (W.seg_*).
     void sort_segments(const KeyTable &T, const uint32_t *keys, uint32_t *hist, int64_t n, int bits,
-                       const EventSrc &src, hipStream_t s) {
+                       const EventSrc &src, hipStream_t s, bool presorted = false) {
         BatchWork W = work();
         const uint32_t invalid = ((uint32_t)1 << bits) - 1;
-        sort(keys, n, bits, hist, src, s);
+        if (!presorted) sort(keys, n, bits, hist, src, s);
         const unsigned g = grid_for(n);
         (void)hipMemsetAsync(W.seg_het, 0, (size_t)n, s);
         (void)hipMemsetAsync(W.seg_prio, 0, (size_t)n, s);
@@ -839,11 +926,44 @@ struct sentinel_engine {
         }
     }
 
+    // The limiter pass of a flow batch: validation + routing into fkey (decided verdicts written), then
+    // GlobalRequestLimiter.tryPass for every routed request (failures answer TOO_MANY_REQUEST and
+    // their flow key becomes invalid).  fpasses: pass-0 flow-key histograms wanted from the prep.
+    void limiter_pass(int64_t n, const Event *ev, int32_t F, uint32_t *fkey, uint32_t finvalid, int fpasses,
+                      uint64_t *out, hipStream_t s) {
+        const int lbits = bits_for(nlimiters);
+        const uint32_t linvalid = ((uint32_t)1 << lbits) - 1;
+        const KeyTable LT = table(lt, 1, lim_stride);
+        const EventSrc lsrc{ev, nullptr, nullptr, true};
+        const Verdicts LV{out, fkey, finvalid};
+        (void)hipMemsetAsync(w_counters.p, 0, 16, s);
+        if (nlimiters == 1 && lim1 && fpasses == 0) {
+            const int64_t nt = (n + L1_TILE - 1) / L1_TILE;
+            unsigned long long *status = w_parts.as<unsigned long long>();
+            (void)hipMemsetAsync(status, 0, (size_t)nt * 8 + 16, s);
+            launch("lim_prep", n, s, [&] {
+                k_lim1_prep<<<dim3((unsigned)nt), dim3(L1_THREADS), 0, s>>>(
+                    n, ev, F, d_flow_route.as<int32_t>(), route8(), out, fkey, finvalid, linvalid,
+                    w_skey.as<uint32_t>(), w_sval.as<uint64_t>(), lsrc, status, (uint32_t *)(status + nt));
+            });
+            run_pipeline(LT, nullptr, nullptr, n, lbits, lsrc, LV, s, 10, true, false, true);
+            return;
+        }
+        uint32_t *lkey = w_lkey.as<uint32_t>();
+        const int64_t nbs = sort_blocks(n);
+        launch("flow_prep", n, s, [&] {
+            k_flow_prep<<<dim3((unsigned)nbs), dim3(SORT_THREADS), 0, s>>>(
+                n, ev, F, d_flow_route.as<int32_t>(), out, fkey, finvalid, fpasses, w_fhist.as<uint32_t>(), lkey,
+                linvalid, 1, w_lhist.as<uint32_t>(), nbs, route8());
+        });
+        run_pipeline(LT, lkey, w_lhist.as<uint32_t>(), n, lbits, lsrc, LV, s, 10, true);
+    }
+
     // The generic pipeline: sort by key, segment, decide, scatter.
     void run_pipeline(const KeyTable &T, const uint32_t *keys, uint32_t *hist, int64_t n, int bits,
                       const EventSrc &src, const Verdicts &V, hipStream_t s, int max_n, bool limiter,
-                      bool hot_het = false) {
-        sort_segments(T, keys, hist, n, bits, src, s);
+                      bool hot_het = false, bool presorted = false) {
+        sort_segments(T, keys, hist, n, bits, src, s, presorted);
         BatchWork W = work();
         const unsigned g = grid_for(n);
         // flow tables: keys hotter than HOT_HET_RUN with heterogeneous acquires go to the hot-run kernels
@@ -1443,22 +1563,7 @@ static int part_front(sentinel_engine_t *e, const PartBufs &B, int64_t n, const 
     // flows of a namespace: validation and the limiter pass run first (the sorted path's k_flow_prep and
     // limiter pipeline, which mark failing events invalid); the multi-split then takes their keys
     const bool lim = e->nlimiters > 0 && !e->flow_plain;
-    if (lim) {
-        const int lbits = bits_for(e->nlimiters);
-        const uint32_t linvalid = ((uint32_t)1 << lbits) - 1;
-        uint32_t *lkey = e->w_lkey.as<uint32_t>();
-        const int64_t nbs = sort_blocks(n);
-        HIP_OK(hipMemsetAsync(e->w_counters.p, 0, 16, s));
-        e->launch("flow_prep", n, s, [&] {
-            k_flow_prep<<<dim3((unsigned)nbs), dim3(SORT_THREADS), 0, s>>>(
-                n, ev, g.F, e->d_flow_route.as<int32_t>(), out, fkey, g.finvalid, 0, e->w_fhist.as<uint32_t>(), lkey,
-                linvalid, 1, e->w_lhist.as<uint32_t>(), nbs, e->route8());
-        });
-        const Verdicts LV{out, fkey, g.finvalid};
-        const KeyTable LT = e->table(e->lt, 1, e->lim_stride);
-        const EventSrc lsrc{ev, nullptr, nullptr, true};
-        e->run_pipeline(LT, lkey, e->w_lhist.as<uint32_t>(), n, lbits, lsrc, LV, s, 10, true);
-    }
+    if (lim) e->limiter_pass(n, ev, g.F, fkey, g.finvalid, 0, out, s);
     e->launch("part_prep", n, s, [&] {
         k_part_prep<<<dim3((unsigned)g.nb), dim3(PP_THREADS), 0, s>>>(
             n, ev, g.F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out,
@@ -1544,26 +1649,21 @@ static int submit_flow_sorted(sentinel_engine_t *e, int64_t n, const Event *ev, 
     const int fbits = bits_for(F);
     const uint32_t finvalid = ((uint32_t)1 << fbits) - 1;
     const bool lim = e->nlimiters > 0 && !e->flow_plain;
-    const int lbits = bits_for(e->nlimiters);
-    const uint32_t linvalid = ((uint32_t)1 << lbits) - 1;
     uint32_t *fkey = e->w_fkey.as<uint32_t>();
-    uint32_t *lkey = lim ? e->w_lkey.as<uint32_t>() : nullptr;
-    const int64_t nb = sort_blocks(n);
-    HIP_OK(hipMemsetAsync(e->w_counters.p, 0, 16, s));
-    e->launch("flow_prep", n, s, [&] {
-        k_flow_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
-            n, ev, F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, fkey, finvalid, lim ? 0 : 1,
-            e->w_fhist.as<uint32_t>(), lkey, linvalid, 1, e->w_lhist.as<uint32_t>(), nb,
-            e->flow_plain ? nullptr : e->route8());
-    });
+    if (lim) {
+        e->limiter_pass(n, ev, F, fkey, finvalid, 0, out, s);
+        e->hist_pass0(fkey, n, e->w_fhist.as<uint32_t>(), s);   // the limiter invalidated some keys
+    } else {
+        const int64_t nb = sort_blocks(n);
+        HIP_OK(hipMemsetAsync(e->w_counters.p, 0, 16, s));
+        e->launch("flow_prep", n, s, [&] {
+            k_flow_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
+                n, ev, F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, fkey, finvalid, 1,
+                e->w_fhist.as<uint32_t>(), nullptr, 0, 1, nullptr, nb, e->flow_plain ? nullptr : e->route8());
+        });
+    }
     Verdicts V{out, fkey, finvalid};
     EventSrc src{ev, nullptr, fl, false};
-    if (lim) {
-        KeyTable LT = e->table(e->lt, 1, e->lim_stride);
-        EventSrc lsrc{ev, nullptr, nullptr, true};
-        e->run_pipeline(LT, lkey, e->w_lhist.as<uint32_t>(), n, lbits, lsrc, V, s, 10, true);
-        e->hist_pass0(fkey, n, e->w_fhist.as<uint32_t>(), s);   // the limiter invalidated some keys
-    }
     if (F > 0) {
         KeyTable FT = e->table(e->ft, NEV, 0);
         e->run_pipeline(FT, fkey, e->w_fhist.as<uint32_t>(), n, fbits, src, V, s, e->flow_max_n, false, true);
@@ -1979,6 +2079,7 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
     if (const char *c = getenv("SENTINEL_SEGMENTS")) e->fused_segments = std::string(c) != "split";
     if (const char *c = getenv("SENTINEL_SEG_IMPL")) e->seg_impl = atoi(c);
     if (const char *c = getenv("SENTINEL_ROUTE8")) e->use_route8 = std::string(c) != "0";
+    if (const char *c = getenv("SENTINEL_LIM1")) e->lim1 = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_PARAM_CAPACITY")) {
         uint64_t v = strtoull(c, nullptr, 10);
         uint64_t p = 1024;

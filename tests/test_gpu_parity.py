@@ -168,6 +168,31 @@ def test_namespace_limiter(oracle_mod):
     _compare(_engine(rules, namespaces=ns), _oracle(oracle_mod, rules, namespaces=ns), rules, ev, batches=3)
 
 
+@pytest.mark.parametrize("lim1", ["1", "0"])
+def test_single_namespace_limiter(oracle_mod, monkeypatch, lim1):
+    """One namespace limiter (the reference's state after a namespace-set change with the default
+    namespace): the fused prep + stable partition (k_lim1_prep) and the prep + radix pass, over
+    invalid ids, non-positive acquires, flows of a namespace without limiter or of a null namespace,
+    a clock that steps back now and then, and many look-back tiles.  (ts < 0 is a documented
+    divergence, DESIGN.md section 1, so the trace has none.)"""
+    monkeypatch.setenv("SENTINEL_LIM1", lim1)
+    rng = np.random.default_rng(37)
+    rules = T.make_rules(5000, rng, count_lo=5, count_hi=400)
+    rules.namespace[:] = 0
+    rules.namespace[3::11] = 1
+    rules.namespace[5::97] = 7                  # no such namespace -> TOO_MANY_REQUEST
+    ns = [dict(connected_count=1, has_limiter=1, max_allowed_qps=3100.0), dict(connected_count=2)]
+    n = 150_000
+    idx = T.zipf_indices(5000, 1.05, n, rng).astype(np.int32)
+    idx[rng.random(n) < 0.01] = -2
+    acq = np.ones(n, np.int32)
+    acq[rng.random(n) < 0.01] = 0
+    ts = T.timestamps(n, 20_000.0, T.T0_ALIGNED + 77)
+    ts = ts + np.where(rng.random(n) < 0.02, rng.integers(-250, 1, size=n), 0)
+    ev = T.Events(idx, acq, ts.astype(np.int64))
+    _compare(_engine(rules, namespaces=ns), _oracle(oracle_mod, rules, namespaces=ns), rules, ev, batches=3)
+
+
 def test_clock_backwards_sequential_path(oracle_mod):
     rng = np.random.default_rng(23)
     rules = T.make_rules(40, rng, count_lo=2, count_hi=50, sample_count=4, window_interval_ms=400)
