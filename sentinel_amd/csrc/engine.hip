@@ -292,23 +292,37 @@ __global__ __launch_bounds__(SORT_THREADS) void k_param_prep(
 #pragma unroll
     for (int j = 0; j < SORT_ITEMS; ++j) {
         const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
-        if (i < n) pevs[j] = ev[i];
+        pevs[j] = i < n ? ev[i] : ParamEvent{SENTINEL_IDX_BAD_ID, 0, 0, 0};
     }
+    // then every route load and every first probe of the slot table (a key already in the table is
+    // found there at the table's load factor): one memory round trip for the tile instead of one per
+    // item; the unrolled loop keeps the events in registers (a dynamically indexed array spills)
+    int32_t rts[SORT_ITEMS];
+    unsigned long long first[SORT_ITEMS];
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const bool in = pevs[j].idx >= 0 && pevs[j].idx < nrules;
+        rts[j] = (route && in) ? route[pevs[j].idx] : ROUTE_PLAIN;
+        first[j] = in ? table[mix64(pevs[j].key) & cap_mask] : PKEY_EMPTY;
+    }
+#pragma unroll
     for (int j = 0; j < SORT_ITEMS; ++j) {
         const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
-        if (i >= n) break;
+        if (i >= n) continue;
         const ParamEvent e = pevs[j];
         int st = 127;
         uint32_t k = finvalid, l = linvalid;
         if (e.idx == SENTINEL_IDX_BAD_ID || e.acquire <= 0) st = ST_BAD_REQUEST;
         else if (e.idx < 0 || e.idx >= nrules) st = ST_NO_RULE_EXISTS;
         else {
-            const int32_t r = route ? route[e.idx] : ROUTE_PLAIN;
+            const int32_t r = rts[j];
             if (r == ROUTE_TOO_MANY) st = ST_TOO_MANY_REQUEST;
             else if (e.ts < 0) st = ST_FAIL;
             else {
                 const uint32_t before = nfresh;
-                const int64_t h = slot_insert_counted(table, cap_mask, e.key, nfresh);
+                // a slot goes EMPTY -> key once per kernel, so a first probe that saw the key is final
+                const int64_t h = first[j] == e.key ? (int64_t)(mix64(e.key) & cap_mask)
+                                                    : slot_insert_counted(table, cap_mask, e.key, nfresh);
                 if (h < 0) st = ST_FAIL;          // table full: the host's param_reserve prevents it
                 else {
                     k = (uint32_t)h;
