@@ -997,9 +997,8 @@ struct WaveRuns {
 };
 
 template <int NMAX>
-__global__ __launch_bounds__(256) void k_process_reg(KeyTable T, BatchWork W, EventSrc src, Verdicts V, int64_t n,
-                                                     LongRuns L = LongRuns{}, WaveRuns WR = WaveRuns{},
-                                                     uint32_t hot_run = HOT_HET_RUN, uint32_t *het_hint = nullptr) {
+__device__ __forceinline__ void process_reg_body(KeyTable T, BatchWork W, EventSrc src, Verdicts V, int64_t n,
+                                                 LongRuns L, WaveRuns WR, uint32_t hot_run, uint32_t *het_hint) {
     const int64_t g0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t S = (int64_t)*W.nseg;
     if (g0 >= S || (int64_t)*W.nvalid == 0) return;
@@ -1137,6 +1136,25 @@ __global__ __launch_bounds__(256) void k_process_reg(KeyTable T, BatchWork W, Ev
     for (int j = 0; j < NMAX; ++j)
         if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(ks.pair(j)) = longlong2{ep[j], ps[j]};
 }
+
+template <int NMAX>
+__global__ __launch_bounds__(256) void k_process_reg(KeyTable T, BatchWork W, EventSrc src, Verdicts V, int64_t n,
+                                                     LongRuns L = LongRuns{}, WaveRuns WR = WaveRuns{},
+                                                     uint32_t hot_run = HOT_HET_RUN, uint32_t *het_hint = nullptr) {
+    process_reg_body<NMAX>(T, W, src, V, n, L, WR, hot_run, het_hint);
+}
+
+// The same kernel held to <= 128 VGPRs (4 waves per SIMD, some spills): the param tables' millions of
+// short keys are latency-bound on their window and segment-record loads, where occupancy beats
+// spill-free code (config 4: 1032 -> 845 us; a separate low-register kernel for one-segment keys
+// measured slower overall, `profiles/r02_param4`).
+template <int NMAX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_process_reg_o4(
+    KeyTable T, BatchWork W, EventSrc src, Verdicts V, int64_t n, LongRuns L = LongRuns{}, WaveRuns WR = WaveRuns{},
+    uint32_t hot_run = HOT_HET_RUN, uint32_t *het_hint = nullptr) {
+    process_reg_body<NMAX>(T, W, src, V, n, L, WR, hot_run, het_hint);
+}
+
 
 // Wave-wide greedy walk (k_process_wave, and coop_het past its first failure): events i in [0, len),
 // 64 at a time, one per lane (load(i) -> the raw value, issued one window ahead; decode(i, raw, a,

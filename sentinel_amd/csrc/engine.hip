@@ -566,6 +566,7 @@ struct sentinel_engine {
     int32_t flow_hblock = 2;        // slots per block of the flow header region (>= every flow's n)
     int64_t flow_rest_base = 0;     // word offset of the flow table's blocked rest region
     int process_impl = 0;
+    bool process_occ = true;         // param pipeline: k_process_reg held to 4 waves per SIMD (SENTINEL_PROC_OCC=0: off)
     bool verdict_nt = false;   // SENTINEL_VERDICT_NT=1: non-temporal verdict stores
     bool use_lookback = true;  // SENTINEL_SCAN=3pass selects the three-kernel scan
     bool fused_segments = true; // SENTINEL_SEGMENTS=split selects heads -> scan -> mark
@@ -976,7 +977,7 @@ struct sentinel_engine {
     // The generic pipeline: sort by key, segment, decide, scatter.
     void run_pipeline(const KeyTable &T, const uint32_t *keys, uint32_t *hist, int64_t n, int bits,
                       const EventSrc &src, const Verdicts &V, hipStream_t s, int max_n, bool limiter,
-                      bool hot_het = false, bool presorted = false) {
+                      bool hot_het = false, bool presorted = false, bool occ4 = false) {
         sort_segments(T, keys, hist, n, bits, src, s, presorted);
         BatchWork W = work();
         const unsigned g = grid_for(n);
@@ -1013,18 +1014,19 @@ struct sentinel_engine {
             launch("process", n, s, [&] {
                 k_process_grp<<<std::min<unsigned>(grid_for(n * PROC_G), 8192), 256, 0, s>>>(T, W, src, V, n);
             });
-        else if (max_n <= 2 && process_impl == 0) {
-            launch("process", n, s, [&] { k_process_reg<2><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run, hint); });
-            hot(std::integral_constant<int, 2>{});
-        } else if (max_n <= 4 && process_impl == 0) {
-            launch("process", n, s, [&] { k_process_reg<4><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run, hint); });
-            hot(std::integral_constant<int, 4>{});
-        } else if (max_n <= 10 && process_impl == 0) {
-            launch("process", n, s, [&] { k_process_reg<10><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run, hint); });
-            hot(std::integral_constant<int, 10>{});
-        } else if (max_n <= 16 && process_impl == 0) {
-            launch("process", n, s, [&] { k_process_reg<16><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run, hint); });
-            hot(std::integral_constant<int, 16>{});
+        else if (max_n <= 16 && process_impl == 0) {
+            auto reg = [&](auto nmax) {
+                constexpr int NM = decltype(nmax)::value;
+                launch("process", n, s, [&] {
+                    if (occ4 && process_occ) k_process_reg_o4<NM><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run, hint);
+                    else k_process_reg<NM><<<g, 256, 0, s>>>(T, W, src, V, n, LR, WR, hot_het_run, hint);
+                });
+                hot(nmax);
+            };
+            if (max_n <= 2) reg(std::integral_constant<int, 2>{});
+            else if (max_n <= 4) reg(std::integral_constant<int, 4>{});
+            else if (max_n <= 10) reg(std::integral_constant<int, 10>{});
+            else reg(std::integral_constant<int, 16>{});
         }
         else
             launch("process", n, s, [&] { k_process<<<g, 256, 0, s>>>(T, W, src, V, n); });
@@ -1808,7 +1810,7 @@ static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, u
     }
     KeyTable PT = e->table(e->pt, 1, header_words(e->pmax_n));
     EventSrc src{nullptr, ev, nullptr, false};
-    e->run_pipeline(PT, fkey, e->w_fhist.as<uint32_t>(), n, pbits, src, V, s, e->pmax_n, false);
+    e->run_pipeline(PT, fkey, e->w_fhist.as<uint32_t>(), n, pbits, src, V, s, e->pmax_n, false, false, false, true);
     HIP_OK(hipGetLastError());
     return 0;
 }
@@ -2094,6 +2096,7 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
     if (const char *c = getenv("SENTINEL_SEG_IMPL")) e->seg_impl = atoi(c);
     if (const char *c = getenv("SENTINEL_ROUTE8")) e->use_route8 = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_LIM1")) e->lim1 = std::string(c) != "0";
+    if (const char *c = getenv("SENTINEL_PROC_OCC")) e->process_occ = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_PARAM_CAPACITY")) {
         uint64_t v = strtoull(c, nullptr, 10);
         uint64_t p = 1024;
