@@ -49,6 +49,7 @@ KERNEL_BYTES_PER_EVENT = {
     "segments": 17.0,         # read key 4 + value 8, write segment id 4 + flag 1 (records are per segment)
     "seg_mark": 5.0,          # read segid 4 + flag 1 (segment records are per segment)
     "verdict": 20.0,          # read segid 4 + value 8, write the 8-B verdict
+    "lim_prep": 32.0,         # one-limiter prep: read the 16-B event, write flow key 4 + limiter key 4 + value 8
     "part_prep": 16.0,        # read the 16-B event (range histogram in LDS; no key array without namespace routes)
     "part_scatter": 24.0,     # read the 16-B event (key re-derived), write the 8-B packed value (local key inside)
     "param_prep": 48.0,       # read the 24-B event, write key 4 + slot rule 4, slot insert (8-B CAS), verdict slot 8
@@ -63,7 +64,7 @@ KERNEL_SYMBOLS = {
     "part_prep": ("k_part_prep",), "part_scatter": ("k_part_scatter",),
     "part_fused": ("k_part_half",), "part_big": ("k_part_big",), "part_long": ("k_part_long",),
     "param_prep": ("k_param_prep",), "param_meta": ("k_param_meta",), "prule_prep": ("k_prule_prep",),
-    "prule_process": ("k_prule_process",), "part_unsplit": ("k_part_unsplit",),
+    "prule_process": ("k_prule_process",), "part_unsplit": ("k_part_unsplit",), "lim_prep": ("k_lim1_prep",),
 }
 PMC_DIR = os.path.join(ROOT, "profiles", "pmc")
 

@@ -779,14 +779,14 @@ __global__ __launch_bounds__(THREADS) void k_segments_v(KeyTable T, BatchWork W,
         }
         f_key[THREADS] = base + TILE < n ? W.skey[base + TILE] : invalid;
     }
+    // only the window length is gathered (param tables: one random line per distinct slot); its
+    // reciprocal is the host's 1.0 / w, recomputed (epoch_of is exact for any close reciprocal anyway)
     int32_t wv[ITEMS];
     double rc[ITEMS];
 #pragma unroll
-    for (int j = 0; j < ITEMS; ++j) {
-        const bool ok = key[j] != invalid;
-        wv[j] = ok ? T.w[key[j]] : 1;
-        rc[j] = ok ? T.rcp_w[key[j]] : 1.0;
-    }
+    for (int j = 0; j < ITEMS; ++j) wv[j] = key[j] != invalid ? T.w[key[j]] : 1;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) rc[j] = 1.0 / (double)wv[j];
     int64_t ep[ITEMS];
     int32_t acq[ITEMS];
     uint32_t priomask = 0;
