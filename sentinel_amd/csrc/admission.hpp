@@ -229,6 +229,11 @@ __host__ __device__ inline int32_t header_block_slots(int32_t maxn) {
     return maxn <= 2 ? 2 : maxn <= 4 ? 4 : maxn <= 10 ? 10 : maxn <= 16 ? 16 : maxn;
 }
 
+// Words per param-table slot: the header of the kernel template bucket of the largest n, so that
+// k_process_reg<NMAX> may request all NMAX pairs of a slot before its n is known (one dependent
+// memory round trip less per key).
+__host__ __device__ inline int64_t param_stride(int32_t maxn) { return header_words(header_block_slots(maxn)); }
+
 // Flow-table header region: blocks of HB_KEYS flows, slot-major inside a block, so the 64 lanes
 // of a wave that read slot j of 64 consecutive flows read 1 KB of contiguous memory.
 __host__ __device__ inline int64_t blocked_pair_word(int64_t key, int hblock, int slot) {
@@ -1029,15 +1034,29 @@ __device__ __forceinline__ void process_reg_body(KeyTable T, BatchWork W, EventS
     const double I_s = T.I_s[key];
     int64_t ep[NMAX], ps[NMAX];
     uint32_t dirty = 0;
+    if (T.hblock || T.state_stride >= 2 * NMAX) {
+        // every slot has room for NMAX pairs (blocked flow headers, bucketed param / limiter strides):
+        // the header loads go out with the key's n instead of waiting for it
 #pragma unroll
-    for (int j = 0; j < NMAX; ++j) {
-        if (j < nsc) {
+        for (int j = 0; j < NMAX; ++j) {
             const longlong2 v = *reinterpret_cast<const longlong2 *>(ks.pair(j));
             ep[j] = v.x;
             ps[j] = v.y;
-        } else {
-            ep[j] = EPOCH_ABSENT;
-            ps[j] = 0;
+        }
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j)
+            if (j >= nsc) { ep[j] = EPOCH_ABSENT; ps[j] = 0; }
+    } else {
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j) {
+            if (j < nsc) {
+                const longlong2 v = *reinterpret_cast<const longlong2 *>(ks.pair(j));
+                ep[j] = v.x;
+                ps[j] = v.y;
+            } else {
+                ep[j] = EPOCH_ABSENT;
+                ps[j] = 0;
+            }
         }
     }
     bool occ_pending = ks.seven && kind == KIND_CLUSTER && T.has_occ[key];

@@ -827,7 +827,7 @@ struct sentinel_engine {
         C.R = ParamRules{d_prule_n.as<int32_t>(), d_prule_w.as<int32_t>(), d_prule_rcp.as<double>(),
                          d_prule_Is.as<double>(), d_prule_thr.as<double>(),
                          has_hot ? d_hot_table.as<unsigned long long>() : nullptr, hot_mask, d_hot_thr.as<double>()};
-        C.PT = table(pt, 1, header_words(pmax_n));
+        C.PT = table(pt, 1, param_stride(pmax_n));
         C.CM = CountMin{d_cm.as<uint64_t>(), cm_depth, cm_width, pmax_n, pmode == SENTINEL_PARAM_COUNT_MIN_SHARED};
         C.L = LocalRules{d_lrule_valid.as<uint8_t>(), d_lrule_tok.as<int64_t>(), d_lrule_burst.as<int64_t>(),
                          d_lrule_dur.as<int64_t>(), lhas_hot ? d_lhot_keys.as<unsigned long long>() : nullptr,
@@ -1138,7 +1138,7 @@ int sentinel_engine::rewrite_tokens(bool compact) {
 int sentinel_engine::clear_param_slots() {
     if (!d_ptable.p) return 0;
     const uint64_t P = pcap;
-    const int64_t stride = header_words(pmax_n);
+    const int64_t stride = param_stride(pmax_n);
     HIP_OK(hipMemsetAsync(d_ptable.p, 0xFF, P * 8, stream));
     HIP_OK(hipMemsetAsync(d_pfresh.p, 0, 8, stream));
     k_init_state<<<grid_for((int64_t)P), 256, 0, stream>>>(pt.state.as<int64_t>(), nullptr, stride, nullptr, pmax_n,
@@ -1157,8 +1157,8 @@ int sentinel_engine::param_rebuild(uint64_t new_cap, const std::vector<int32_t> 
                                    const std::vector<int32_t> &new_rn, const std::vector<int64_t> &imp,
                                    int64_t imp_stride, const std::vector<int32_t> &imp_rule,
                                    std::vector<std::pair<int32_t, std::vector<int64_t>>> *exported) {
-    const int64_t nstride = header_words(new_maxn);
-    const int64_t ostride = header_words(pmax_n);
+    const int64_t nstride = param_stride(new_maxn);
+    const int64_t ostride = param_stride(pmax_n);
     DevBuf &nkeys = sp_keys, &nrule = sp_rule, &nstate = sp_state, &nn = sp_n, &nw = sp_w, &nrcp = sp_rcp,
            &nIs = sp_Is, &nthr = sp_thr, &nkind = sp_kind;
     DevBuf dmap, dnewest, dcount, dxout, dimp, dimprule, dnrn;
@@ -1282,7 +1282,7 @@ int sentinel_engine::param_reserve(int64_t nv) {
     // grow until the live slots plus this batch fit, and -- within a memory budget -- until a few more
     // batches of new values fit too, so that the reclaiming rebuild (a device-wide pass and a host sync)
     // comes back every few batches, not every batch, under a steady churn of values
-    const uint64_t slot_bytes = 8 + 4 + (uint64_t)header_words(pmax_n) * 8 + 4 + 4 + 8 + 8 + 8 + 1;
+    const uint64_t slot_bytes = 8 + 4 + (uint64_t)param_stride(pmax_n) * 8 + 4 + 4 + 8 + 8 + 8 + 1;
     const uint64_t budget = (uint64_t)8 << 30;            // per table (the rebuild holds two)
     uint64_t cap = pcap;
     while (p_live + (uint64_t)nv > cap / 4 * 3) cap <<= 1;
@@ -1808,7 +1808,7 @@ static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, u
         e->run_pipeline(LT, lkey, e->w_lhist.as<uint32_t>(), n, lbits, lsrc, V, s, 10, true);
         e->hist_pass0(fkey, n, e->w_fhist.as<uint32_t>(), s);
     }
-    KeyTable PT = e->table(e->pt, 1, header_words(e->pmax_n));
+    KeyTable PT = e->table(e->pt, 1, param_stride(e->pmax_n));
     EventSrc src{nullptr, ev, nullptr, false};
     e->run_pipeline(PT, fkey, e->w_fhist.as<uint32_t>(), n, pbits, src, V, s, e->pmax_n, false, false, false, true);
     HIP_OK(hipGetLastError());
@@ -3613,7 +3613,7 @@ int sentinel_param_sum(sentinel_engine_t *e, int32_t ridx, uint64_t pkey, int64_
     if (h < 0) return 0;
     const int n = e->h_prule_n[ridx];                                     // the metric's window
     const int64_t w = e->h_prule_interval[ridx] / n;
-    const int64_t stride = header_words(e->pmax_n);
+    const int64_t stride = param_stride(e->pmax_n);
     std::vector<int64_t> st(2 * n);
     HIP_OK(hipMemcpy(st.data(), e->pt.state.as<int64_t>() + h * stride, st.size() * 8, hipMemcpyDeviceToHost));
     const int64_t E = ts / w;   // read-only view (no roll): valid slots are epochs in (E - n, E]
@@ -3642,7 +3642,7 @@ static int param_top(sentinel_engine_t *e, int64_t ts, int32_t number, hipStream
     for (DevBuf *b : {&pr, &pk, &cr, &ck}) rc |= b->ensure((size_t)R * 8);
     if (rc) return SENTINEL_E_NOMEM;
     const PSlots T{e->d_ptable.as<unsigned long long>(), e->d_slot_rule.as<int32_t>(), e->pt.state.as<int64_t>(),
-                   header_words(e->pmax_n), cap - 1};
+                   param_stride(e->pmax_n), cap - 1};
     const unsigned g = grid_for((int64_t)cap);
     k_ptop_sums<<<g, 256, 0, s>>>(T, cap, R, e->d_prule_n.as<int32_t>(), e->d_prule_w.as<int32_t>(),
                                   e->d_prule_rcp.as<double>(), ts, sums.as<int64_t>());
