@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${1:-final}
-bash scripts/gpu_round.sh $TAG || exit $?
+bash scripts/gpu_round.sh $TAG ${2:-} || exit $?
 O=gpurun_out/$TAG
 for C in 2 5 3lim 4 4cm; do
   timeout -k 10 240 python -u bench.py --config $C --steps 20 --warmup 3 > $O/bench_$C.json 2> $O/bench_$C.err || { tail -20 $O/bench_$C.err; exit 1; }
