@@ -55,7 +55,8 @@ def main():
     if len(sys.argv) > 2:
         with open(sys.argv[2]) as f:
             cfg = json.loads(f.read().strip().splitlines()[-1])["config"]
-        doc["shape"] = {k: cfg[k] for k in ("config", "flows", "events", "sample_count")}
+        # the workload's own shape keys (bench.py W.shape(): flows or rules, events, sample count)
+        doc["shape"] = {k: v for k, v in cfg.items() if k not in ("workload", "events_per_gpu_per_step", "parallelism")}
     json.dump(doc, sys.stdout, indent=1)
 
 
