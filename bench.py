@@ -14,8 +14,9 @@ already resident in HBM.
   4     hot-parameter cluster rules: 100k resources x Zipf(1.2) over 1000 Long values, exact counters
   4cm   the same on the shared count-min sketch (w=2^20, d=4) + the measured false-block rate vs e*N/w
   5     Envoy RLS rules (SimpleClusterFlowChecker, n=1 / 1000 ms), hitsAddend ~ geometric(0.3) capped at
-        64: heterogeneous acquire -> the sequential per-segment path; plus concurrency-token acquire /
-        release throughput (the thread-grade rules of the config)
+        64: heterogeneous acquire -> the sequential per-segment path
+  5conc the thread-grade half of config 5: concurrency-token acquire / release batches
+        (ConcurrentClusterFlowChecker) on the device-pointer path
   3lim  config 3 with the namespace GlobalRequestLimiter on (the reference creates one per namespace
         after any namespace-set change): the radix-sort path
 
@@ -52,7 +53,8 @@ KERNEL_BYTES_PER_EVENT = {
     "lim_prep": 32.0,         # one-limiter prep: read the 16-B event, write flow key 4 + limiter key 4 + value 8
     "part_prep": 16.0,        # read the 16-B event (range histogram in LDS; no key array without namespace routes)
     "part_scatter": 24.0,     # read the 16-B event (key re-derived), write the 8-B packed value (local key inside)
-    "param_prep": 48.0,       # read the 24-B event, write key 4 + slot rule 4, slot insert (8-B CAS), verdict slot 8
+    "param_prep": 24.0,       # read the 24-B event (range histogram in LDS; rejected requests answered here)
+    "param_scatter": 44.0,    # read the 24-B event, write key 8 + packed value 8 + rule 4
     "param_meta": 48.0,       # per slot after a rule / threshold / table change: key 8, rule fields ~16, write ~20 B
     "prule_prep": 36.0,       # read the 24-B event + value 8, write key 4
 }
@@ -63,8 +65,9 @@ KERNEL_SYMBOLS = {
     "scan": ("k_scan_lookback",), "segments": ("k_segments",), "process": ("k_process",), "verdict": ("k_verdict",),
     "part_prep": ("k_part_prep",), "part_scatter": ("k_part_scatter",),
     "part_fused": ("k_part_half",), "part_big": ("k_part_big",), "part_long": ("k_part_long",),
-    "param_prep": ("k_param_prep",), "param_meta": ("k_param_meta",), "prule_prep": ("k_prule_prep",),
+    "param_prep": ("k_param_prep", "k_pp_prep"), "param_meta": ("k_param_meta",), "prule_prep": ("k_prule_prep",),
     "prule_process": ("k_prule_process",), "part_unsplit": ("k_part_unsplit",), "lim_prep": ("k_lim1_prep",),
+    "param_scatter": ("k_pp_scatter",), "param_decide": ("k_pp_decide",),
 }
 PMC_DIR = os.path.join(ROOT, "profiles", "pmc")
 
@@ -94,6 +97,39 @@ def pmc_traffic(kernel: str, shape: dict):
         if disp:
             return round(tot / disp, 1), f"profiles/pmc/{fn}"
     return None, None
+
+
+def cgroup_cpus():
+    """CPUs the cgroup's CPU quota grants this process (cgroup v2 cpu.max / v1 cfs quota), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            return max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        if q > 0:
+            return max(1, q // per)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_threads_default():
+    """Threads for the sharded CPU baseline: every CPU this process may run on (sched_getaffinity, SURVEY
+    section 8(d): T = nproc), capped by the cgroup's CPU quota when one is set (threads beyond the quota
+    only time-slice on the same share)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    q = cgroup_cpus()
+    return min(avail, q) if q else avail
 
 
 def cpu_info():
@@ -130,7 +166,8 @@ def parse():
     ap.add_argument("--interval-ms", type=int, default=1000)
     ap.add_argument("--cpu-steps-1core", type=int, default=2)
     ap.add_argument("--cpu-steps-mt", type=int, default=12)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="threads of the sharded CPU baseline (default: every CPU this process may run on)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3)
@@ -536,25 +573,27 @@ def main():
     def pct(xs, q):
         return xs[min(len(xs) - 1, int(np.ceil(q * len(xs))) - 1)]
 
-    # ---- snapshot + RCCL all-gather (config 3's ClusterMetric snapshot; off the decision path)
+    # ---- snapshot + RCCL all-gather (the ClusterMetric snapshot, ClusterMetricNodeGenerator: flow records
+    # for the flow configs, top-5 param records for config 4; off the decision path)
+    from sentinel_amd import shard as SH
     snap_ms = None
+    t_snap = int(lat_b[-1][-1, 1].item()) + 1
+    torch.cuda.synchronize()
+    ts0 = time.perf_counter()
     if isinstance(W, FlowWorkload):
-        F = W.F
-        t_snap = int(lat_b[-1][-1, 1].item()) + 1
-        snap = torch.empty((F, 3), dtype=torch.int64, device=dev)
-        torch.cuda.synchronize()
-        ts0 = time.perf_counter()
+        snap = torch.empty((W.F, 3), dtype=torch.int64, device=dev)
         svc.snapshot_device(t_snap, snap)
         svc.synchronize()
         if world > 1:
-            maxf = torch.tensor([F], device=dev)
-            dist.all_reduce(maxf, op=dist.ReduceOp.MAX)
-            pad = torch.zeros((int(maxf.item()), 3), dtype=torch.int64, device=dev)
-            pad[:F] = snap
-            gathered = [torch.empty_like(pad) for _ in range(world)]
-            dist.all_gather(gathered, pad)
-            torch.cuda.synchronize()
-        snap_ms = (time.perf_counter() - ts0) * 1000.0
+            SH.gather_snapshot(snap)
+    else:
+        snap = torch.empty(W.R * SH.PARAM_RECORD_WORDS * 8, dtype=torch.uint8, device=dev)
+        svc.param_snapshot_device(t_snap, snap)
+        svc.synchronize()
+        if world > 1:
+            SH.gather_param_snapshot(snap)
+    torch.cuda.synchronize()
+    snap_ms = (time.perf_counter() - ts0) * 1000.0
 
     # PCIe-inclusive host paths (config 3 only; reported beside `value`, never as it)
     host_path = None
@@ -649,12 +688,12 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline")
         one, mt = W.cpu_baseline(ev_b, min(args.cpu_steps_1core, steps_total), min(args.cpu_steps_mt, steps_total),
-                                 args.cpu_threads)
+                                 args.cpu_threads or cpu_threads_default())
 
         def leg(x):
             m, cdt, cores, how = x
             return {"value": round(m / cdt, 1), "unit": "decisions/s", "cores": cores, "kind": "port",
-                    "cpu_model": model, "nproc": ncpu, "cpus_available": avail,
+                    "cpu_model": model, "nproc": ncpu, "cpus_available": avail, "cgroup_cpu_quota": cgroup_cpus(),
                     "sample": f"the first {m} events of this workload (same rules and trace), {how}, {cdt:.1f} s"}
         cpu1 = leg(one)
         cpu = leg(mt) if mt else cpu1

@@ -517,6 +517,16 @@ int  sentinel_param_interner_destroy(sentinel_param_interner_t *it);
  * bits / double bits, or a string's UTF-8 bytes. */
 int  sentinel_param_interner_key(sentinel_param_interner_t *it, int64_t flow_id, int32_t type, const uint8_t *value,
                                  int32_t len, uint64_t *key);
+/* The same for a request at time ts (ms): the entry's last use.  The interner is bounded: past
+ * max_entries (default 2^23) entries idle for more than idle_ms (default 60000) are forgotten --
+ * exact when idle_ms >= every param rule's interval (such a value has no valid bucket left); if a
+ * flood of distinct values inside that horizon still exceeds the cap, the least recently used go
+ * (the reference bounds its CacheMaps by LRU, ConcurrentLinkedHashMapWrapper.java:35-43).  The wire
+ * server interns only values of flowIds that have a param rule (others answer NO_RULE_EXISTS). */
+int  sentinel_param_interner_key_at(sentinel_param_interner_t *it, int64_t flow_id, int32_t type, const uint8_t *value,
+                                    int32_t len, int64_t ts, uint64_t *key);
+int  sentinel_param_interner_set_limits(sentinel_param_interner_t *it, int64_t max_entries, int64_t idle_ms);
+int  sentinel_param_interner_stats(sentinel_param_interner_t *it, int64_t *entries, int64_t *evicted);
 typedef int64_t (*sentinel_clock_fn)(void *ctx);
 typedef struct {
     const char *host;                 /* IPv4 bind address, NULL = 127.0.0.1 */
@@ -542,8 +552,11 @@ int  sentinel_wire_server_destroy(sentinel_wire_server_t *srv);
  * host constants: no exchange on the decision path).  Rule tables are split by shard (the
  * putMetricIfAbsent orphan rule still sees the whole node's namespace lists); namespace and server
  * config are broadcast.  Replaces one DefaultTokenService over the whole flowId space.  The
- * GlobalRequestLimiter couples a namespace's flows: exact only when they share a shard or the
- * limiter is off. */
+ * GlobalRequestLimiter couples a namespace's flows, so sentinel_cluster_set_namespaces rejects
+ * (SENTINEL_E_INVALID) any namespace with has_limiter when the cluster has more than one shard: each
+ * shard would otherwise apply the full maxAllowedQps to its share and the node could admit up to
+ * n x the cap.  Multi-GPU deployments with limiters shard by namespace instead (one process per GPU,
+ * sentinel_amd/shard.py shard_by_namespace). */
 typedef struct sentinel_cluster sentinel_cluster_t;
 int32_t sentinel_shard_of(int64_t flow_id, int32_t n_shards);
 int  sentinel_cluster_create(const int32_t *device_ids, int32_t n, const sentinel_server_config_t *cfg,

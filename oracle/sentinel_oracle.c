@@ -870,9 +870,23 @@ void orc_request_param_token(orc_engine *e, int32_t idx, int32_t acquire, int64_
     if (idx == -2 || acquire <= 0 || n_values <= 0) { *st = ORC_BAD_REQUEST; *rem = 0; return; }
     if (idx < 0 || idx >= e->n_prules) { *st = ORC_NO_RULE_EXISTS; *rem = 0; return; }
     const orc_param_rule *r = &e->prules[idx].r;
+    if (t < 0 && r->namespace_idx >= 0 && r->namespace_idx < e->n_ns && e->lim[r->namespace_idx]) {
+        /* RequestLimiter.tryPass at t < 0 (RL:81-87): the sum is 0, add(1) dies in currentWindow() == null
+         * (LA:149-152) -> the engine's FAIL stand-in for the NullPointerException */
+        *st = ORC_FAIL; *rem = 0; return;
+    }
     if (!engine_allow_proceed(e, r->namespace_idx, t)) { *st = ORC_TOO_MANY_REQUEST; *rem = 0; return; }
     orc_param_metric *m = e->prules[idx].pm;
     if (!m) { *st = ORC_FAIL; *rem = 0; return; }
+    if (t < 0) {
+        /* LA:149-152 currentWindow(t < 0) == null, LA:375-378 values(t < 0) empty: every getAvg is 0, a
+         * value with (T_v - 0) - a < 0 blocks the request untouched (CPFC:66-70); a request that passes
+         * dies in addValue's currentWindow().value() (ClusterParamMetric.java:69, NullPointerException),
+         * which the engine answers FAIL */
+        for (int i = 0; i < n_values; i++)
+            if ((param_threshold(e, r, values[i]) - 0.0) - (double)acquire < 0) { *st = ORC_BLOCKED; *rem = 0; return; }
+        *st = ORC_FAIL; *rem = 0; return;
+    }
     double remaining = -1;
     int passed = 1;
     for (int i = 0; i < n_values; i++) {

@@ -65,6 +65,7 @@ EXPORTS = [
     "sentinel_cluster_batchers_create", "sentinel_cluster_request_token",
     "sentinel_batcher_request_tokens_async", "sentinel_batcher_set_batch_hook",
     "sentinel_param_interner_create", "sentinel_param_interner_destroy", "sentinel_param_interner_key",
+    "sentinel_param_interner_key_at", "sentinel_param_interner_set_limits", "sentinel_param_interner_stats",
     "sentinel_wire_server_create", "sentinel_wire_server_port", "sentinel_wire_server_stats",
     "sentinel_wire_server_destroy",
 ]
@@ -266,6 +267,9 @@ def load():
         "sentinel_param_interner_create": (C.c_int, [C.POINTER(vp)]),
         "sentinel_param_interner_destroy": (C.c_int, [vp]),
         "sentinel_param_interner_key": (C.c_int, [vp, i64, i32, vp, i32, C.POINTER(C.c_uint64)]),
+        "sentinel_param_interner_key_at": (C.c_int, [vp, i64, i32, vp, i32, i64, C.POINTER(C.c_uint64)]),
+        "sentinel_param_interner_set_limits": (C.c_int, [vp, i64, i64]),
+        "sentinel_param_interner_stats": (C.c_int, [vp, C.POINTER(i64), C.POINTER(i64)]),
         "sentinel_wire_server_create": (C.c_int, [vp, C.POINTER(WireConfig), C.POINTER(vp)]),
         "sentinel_wire_server_port": (i32, [vp]),
         "sentinel_wire_server_stats": (C.c_int, [vp, vp, vp, vp, vp]),

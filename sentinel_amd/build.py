@@ -7,7 +7,7 @@ import subprocess
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_HERE)
 SOURCES = [os.path.join(_HERE, "csrc", "engine.hip")]
-DEPS = SOURCES + [os.path.join(_HERE, "csrc", f) for f in ("common.hpp", "scan_sort.hpp", "admission.hpp", "param_rules.hpp", "concurrent.hpp", "partition.hpp", "small.hpp", "wire_server.hpp", "local_entry.hpp", "param_table.hpp")] + [
+DEPS = SOURCES + [os.path.join(_HERE, "csrc", f) for f in ("common.hpp", "scan_sort.hpp", "admission.hpp", "param_rules.hpp", "concurrent.hpp", "partition.hpp", "small.hpp", "param_part.hpp", "wire_server.hpp", "local_entry.hpp", "param_table.hpp")] + [
     os.path.join(ROOT, "include", "sentinel_amd.h")]
 OUT = os.path.join(_HERE, "libsentinel_amd.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -34,6 +34,7 @@
 #include "param_rules.hpp"
 #include "param_table.hpp"
 #include "partition.hpp"
+#include "param_part.hpp"
 #include "small.hpp"
 #include "local_entry.hpp"
 #include <random>
@@ -317,7 +318,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_param_prep(
         else {
             const int32_t r = rts[j];
             if (r == ROUTE_TOO_MANY) st = ST_TOO_MANY_REQUEST;
-            else if (e.ts < 0) st = ST_FAIL;
+            else if (e.ts < 0) st = r >= 0 ? ST_FAIL : param_negative_ts_status(PR, (uint32_t)e.idx, e.key, e.acquire);
             else {
                 const uint32_t before = nfresh;
                 // a slot goes EMPTY -> key once per kernel, so a first probe that saw the key is final
@@ -624,7 +625,8 @@ struct sentinel_engine {
     DevBuf d_cm;                       // count-min cells (SENTINEL_PARAM_COUNT_MIN)
     DevBuf w_cm;                       // shared sketch: rule heads, cursors, grid barrier, level words
     int cm_sync_blocks = 0;            // co-resident workgroups of k_prule_cm_sync
-    int param_path = 0;                // single-value exact requests: 0 per-slot segments, 1 per-rule walk
+    int param_path = 0;                // single-value exact requests: 0 partition-local (param_part.hpp),
+                                       // 1 per-rule walk, 2 per-slot radix-sort segments
     bool pmeta_dirty = true;           // the slots' window fields / thresholds need k_param_meta_all
     bool cm_force_coop = false;        // shared sketch: always the cooperative kernel (tests)
 
@@ -1755,6 +1757,60 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
                          const uint64_t *values, int64_t n_values, uint64_t *out, hipStream_t s,
                          const uint8_t *kinds = nullptr);
 
+// Single-value exact requests without namespace limiters: the partition-local path (param_part.hpp):
+// prep + range histogram, the partition scan, the stable multi-split by key hash, then one workgroup
+// per range deciding its distinct keys from an LDS-staged table.
+static int submit_param_part(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, uint64_t *out, hipStream_t s) {
+    const int32_t R = (int32_t)e->prules.size();
+    const bool have = R > 0 && e->d_ptable.p;
+    int pbits = 0;                                        // ranges of ~PD_TARGET requests, <= PART_BINS
+    while (pbits < PART_MAX_BITS && ((int64_t)2 << pbits) * PD_TARGET <= n) ++pbits;
+    const int32_t P = 1 << pbits;
+    const int64_t nb = part_blocks(n), ng = (nb + PS_GROUP - 1) / PS_GROUP;
+    int rc = e->w_fhist.ensure((size_t)nb * P * 4);
+    rc |= e->w_pscan.ensure(((size_t)ng * P + 2 * (size_t)P + 1) * 4);
+    if (rc) return rc;
+    uint32_t *hist = e->w_fhist.as<uint32_t>();
+    uint32_t *gsum = e->w_pscan.as<uint32_t>();
+    uint32_t *rstart = gsum + (size_t)ng * P;
+    uint32_t *rtot = rstart + P + 1;
+    const int32_t *route = e->param_plain ? nullptr : e->d_prule_route.as<int32_t>();
+    e->launch("param_prep", n, s, [&] {
+        k_pp_prep<<<dim3((unsigned)nb), dim3(PP_THREADS), 0, s>>>(n, ev, have ? R : 0, route, e->param_ctx().R, out,
+                                                                  pbits, hist, P);
+    });
+    if (!have) {
+        HIP_OK(hipGetLastError());
+        return 0;
+    }
+    e->launch("scan", n, s, [&] {
+        const dim3 g2((unsigned)ng, (unsigned)((P + PS_THREADS - 1) / PS_THREADS));
+        k_part_colsum<<<g2, PS_THREADS, 0, s>>>(hist, nb, P, gsum);
+        k_part_colscan<<<(unsigned)((P + PC_THREADS / WAVE - 1) / (PC_THREADS / WAVE)), PC_THREADS, 0, s>>>(gsum, ng, P,
+                                                                                                          rtot);
+        k_part_offsets<<<g2, PS_THREADS, 0, s>>>(hist, nb, P, gsum, rtot, rstart);
+    });
+    unsigned long long *pkey = e->w_vtmp.as<unsigned long long>();
+    uint64_t *pval = e->w_sval.as<uint64_t>();
+    int32_t *prule = e->w_fkey.as<int32_t>();
+    e->launch("param_scatter", n, s, [&] {
+        k_pp_scatter<<<dim3((unsigned)nb), dim3(PT_THREADS), 0, s>>>(ev, n, R, route, pbits, hist, P, pkey, pval, prule);
+    });
+    const PSlots S{e->d_ptable.as<unsigned long long>(), e->d_slot_rule.as<int32_t>(), e->pt.state.as<int64_t>(),
+                   param_stride(e->pmax_n), e->pcap - 1};
+    const ParamRules PR = e->param_ctx().R;
+    unsigned long long *fresh = e->d_pfresh.as<unsigned long long>();
+    e->launch("param_decide", n, s, [&] {
+        const int hb = header_block_slots(e->pmax_n);
+        if (hb <= 2) k_pp_decide<2><<<(unsigned)P, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, ev, PR, S, out, fresh);
+        else if (hb <= 4) k_pp_decide<4><<<(unsigned)P, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, ev, PR, S, out, fresh);
+        else if (hb <= 10) k_pp_decide<10><<<(unsigned)P, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, ev, PR, S, out, fresh);
+        else k_pp_decide<16><<<(unsigned)P, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, ev, PR, S, out, fresh);
+    });
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
 static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, uint64_t *out, hipStream_t s) {
     if (e->pmode != SENTINEL_PARAM_EXACT) return submit_prules(e, PMODE_CM, n, ev, nullptr, nullptr, 0, out, s);
     // per-rule walk (sort by rule, one lane per rule, each request rolls and sums its value's slot): for
@@ -1771,6 +1827,8 @@ static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, u
         rc = e->param_reserve(n);             // room for every value of the batch: never FAIL
         if (rc) return rc;
     }
+    const bool plim = e->nlimiters > 0 && !e->param_plain && R > 0;
+    if (e->param_path == 0 && !plim && e->pmax_n <= 16) return submit_param_part(e, n, ev, out, s);
     const uint64_t P = e->pcap;
     const int pbits = bits_for((int64_t)P);
     const uint32_t pinvalid = ((uint32_t)1 << pbits) - 1;
@@ -2083,7 +2141,10 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
         e->process_impl = v == "group" ? 1 : v == "thread" ? 2 : 0;
     }
     if (const char *c = getenv("SENTINEL_VERDICT_NT")) e->verdict_nt = std::string(c) == "1";
-    if (const char *c = getenv("SENTINEL_PARAM_PATH")) e->param_path = std::string(c) == "rule" ? 1 : 0;
+    if (const char *c = getenv("SENTINEL_PARAM_PATH")) {
+        const std::string v(c);
+        e->param_path = v == "rule" ? 1 : v == "slot" ? 2 : 0;
+    }
     if (const char *c = getenv("SENTINEL_CM_LEVELS")) e->cm_force_coop = std::string(c) == "coop";
     if (const char *c = getenv("SENTINEL_SCAN")) e->use_lookback = std::string(c) != "3pass";
     if (const char *c = getenv("SENTINEL_DIAG_LINEAR")) e->diag_linear = std::string(c) == "1";
@@ -4175,6 +4236,14 @@ int sentinel_cluster_set_server_config(sentinel_cluster_t *c, const sentinel_ser
 
 int sentinel_cluster_set_namespaces(sentinel_cluster_t *c, const sentinel_namespace_t *ns, int32_t n) {
     if (!c) return fail(SENTINEL_E_INVALID, "null cluster");
+    // a namespace's GlobalRequestLimiter counts every request of the namespace (GlobalRequestLimiter
+    // .java:46-55); with flows split by flowId hash each shard would run its own limiter at the full
+    // maxAllowedQps and the node could admit up to n times the cap, so limiters need one shard
+    if (c->eng.size() > 1 && ns)
+        for (int32_t i = 0; i < n; ++i)
+            if (ns[i].has_limiter)
+                return fail(SENTINEL_E_INVALID, "namespace limiters (has_limiter) need a single-shard cluster: "
+                                                "a flowId-hash split would apply the cap per shard");
     return for_shards(c, [&](int32_t i) { return sentinel_set_namespaces(c->eng[(size_t)i], ns, n); });
 }
 

@@ -118,6 +118,16 @@ __device__ inline double value_threshold(const ParamRules &R, uint32_t rule, uin
     return h >= 0 ? R.hot_thr[h] : R.thr[rule];
 }
 
+// A cluster param request at ts < 0 (no namespace limiter): LeapArray.currentWindow(t < 0) == null
+// (LeapArray.java:149-152) and values(t < 0) is empty (:375-378), so every value's getAvg is 0; a value
+// with (T_v - 0) - a < 0 blocks the request with no counter touched (CPFC:66-70), and a request that
+// would pass dies in addValue's currentWindow().value() (ClusterParamMetric.java:69,
+// NullPointerException), which the engine answers FAIL.  With a namespace limiter the limiter's add dies
+// first (FAIL).
+__device__ inline int param_negative_ts_status(const ParamRules &R, uint32_t rule, uint64_t key, int32_t a) {
+    return ((value_threshold(R, rule, key) - 0.0) - (double)a < 0.0) ? ST_BLOCKED : ST_FAIL;
+}
+
 // ------------------------------------------------------------------ prep
 
 // Validation + routing of single- or multi-value events, slot of every value, sort keys (rule
@@ -164,7 +174,15 @@ __global__ __launch_bounds__(SORT_THREADS) void k_prule_prep(
             else {
                 const int32_t r = route ? route[e.idx] : ROUTE_PLAIN;
                 if (r == ROUTE_TOO_MANY) st = ST_TOO_MANY_REQUEST;   // namespace == null
-                else if (e.ts < 0) st = ST_FAIL;                       // reference: NPE in LeapArray
+                else if (e.ts < 0) {                                   // param_negative_ts_status
+                    st = ST_FAIL;
+                    if (r < 0 && !bad_range)
+                        for (int32_t q = 0; q < cnt; ++q)
+                            if (param_negative_ts_status(R, (uint32_t)e.idx, vs.value((int64_t)b + q), e.acquire) == ST_BLOCKED) {
+                                st = ST_BLOCKED;
+                                break;
+                            }
+                }
                 else if (r >= 0) l = (uint32_t)r;
             }
         }

@@ -116,9 +116,45 @@ inline bool java_blank(const std::string &s) {
 
 // Injective (flowId, Java-typed value) -> 64-bit param key, dense from 1 (the all-ones key is
 // reserved by the engine): the native counterpart of wire.py's ParamKeyInterner.
+//
+// Bounded: every entry remembers the last request time that used it.  Past max_entries, entries idle
+// for longer than idle_ms are forgotten -- exact whenever idle_ms >= every param rule's interval: such
+// a value has no valid bucket left (LeapArray.values keeps t - start <= interval, LeapArray.java:375-390),
+// so its next request under a fresh key reads the same empty window the reference's CacheMaps give it
+// (the engine reclaims the old key's slot as dead, param_table.hpp).  If a flood of distinct values
+// inside the horizon still exceeds the cap, the least recently used entries go (the reference bounds
+// the same per-rule maps by LRU eviction, ConcurrentLinkedHashMapWrapper.java:35-43: parity unpinned
+// there, as for the engine's own tables).
 struct sentinel_param_interner {
+    struct Ent { uint64_t key; int64_t last; };
     std::mutex mu;
-    std::unordered_map<std::string, uint64_t> ids;
+    std::unordered_map<std::string, Ent> ids;
+    uint64_t next_id = 1;
+    int64_t max_entries = (int64_t)1 << 23;
+    int64_t idle_ms = 60000;
+    int64_t now = INT64_MIN;                 // the newest request time seen
+    int64_t evicted = 0;
+
+    void shrink_locked() {
+        const int64_t horizon = now == INT64_MIN ? INT64_MIN : now - idle_ms;
+        for (auto it = ids.begin(); it != ids.end();) {
+            if (it->second.last < horizon) { it = ids.erase(it); ++evicted; }
+            else ++it;
+        }
+        if ((int64_t)ids.size() < max_entries) return;
+        // still full: least recently used first, down to 3/4 of the cap
+        std::vector<int64_t> lasts;
+        lasts.reserve(ids.size());
+        for (auto &kv : ids) lasts.push_back(kv.second.last);
+        const size_t drop = ids.size() - (size_t)(max_entries / 4 * 3);
+        std::nth_element(lasts.begin(), lasts.begin() + (drop - 1), lasts.end());
+        const int64_t cut = lasts[drop - 1];
+        size_t dropped = 0;
+        for (auto it = ids.begin(); it != ids.end() && dropped < drop;) {
+            if (it->second.last <= cut) { it = ids.erase(it); ++dropped; ++evicted; }
+            else ++it;
+        }
+    }
 
     // canonical value: Java equals() semantics -- the type tag is part of the key, NaNs collapse to
     // doubleToLongBits / floatToIntBits' canonical NaN, booleans to 0 / 1, strings by their decoded text
@@ -149,7 +185,8 @@ struct sentinel_param_interner {
         }
     }
 
-    bool key(int64_t flow_id, int type, const uint8_t *v, int32_t len, uint64_t &k) {
+    // ts: the request's time (INT64_MIN: the newest time seen so far)
+    bool key(int64_t flow_id, int type, const uint8_t *v, int32_t len, uint64_t &k, int64_t ts = INT64_MIN) {
         std::string c;
         if (!canonical(type, v, len, c)) return false;
         std::string s(9, '\0');
@@ -157,10 +194,18 @@ struct sentinel_param_interner {
         s[8] = (char)type;
         s += c;
         std::lock_guard<std::mutex> g(mu);
+        if (ts > now) now = ts;
+        const int64_t t = ts == INT64_MIN ? now : ts;
         auto it = ids.find(s);
-        if (it != ids.end()) { k = it->second; return true; }
-        k = (uint64_t)ids.size() + 1;
-        ids.emplace(std::move(s), k);
+        if (it != ids.end()) {
+            if (t > it->second.last) it->second.last = t;
+            k = it->second.key;
+            return true;
+        }
+        if ((int64_t)ids.size() >= max_entries) shrink_locked();
+        k = next_id++;
+        if (k == ~0ull) k = next_id++;              // (the reserved all-ones key: never reached in practice)
+        ids.emplace(std::move(s), Ent{k, t});
         return true;
     }
 };
@@ -365,9 +410,11 @@ struct ReadBatch {
     std::vector<int32_t> pxid;
     std::vector<sentinel_param_multi_event_t> pev;
     std::vector<uint64_t> pvals;
+    std::vector<uint8_t> pnorule;                 // no param rule for the flowId when decoded
+    std::unordered_map<int64_t, int32_t> prule_cache;   // flowId -> param rule index, this read
     void clear() {
         fid.clear(); fts.clear(); facq.clear(); fprio.clear(); ftag.clear();
-        pfid.clear(); pxid.clear(); pev.clear(); pvals.clear();
+        pfid.clear(); pxid.clear(); pev.clear(); pvals.clear(); pnorule.clear(); prule_cache.clear();
     }
 };
 
@@ -472,6 +519,15 @@ inline bool sentinel_wire_server::on_readable(wire::Loop &L, wire::Conn *c) {
             const int32_t cnt = (int32_t)wire::be(d + 8, 4);
             const int32_t amount = (int32_t)wire::be(d + 12, 4);
             if (amount <= 0) continue;                     // null data
+            // no rule for the flowId: NO_RULE_EXISTS (DefaultTokenService.java:57-60) without interning
+            // anything (untrusted values of unknown flowIds never reach the interner)
+            auto rit = B.prule_cache.find(fid);
+            if (rit == B.prule_cache.end()) {
+                int32_t ridx = -1;
+                if (sentinel_lookup_param_idx(e, 1, &fid, &ridx) != 0) ridx = -1;
+                rit = B.prule_cache.emplace(fid, ridx).first;
+            }
+            const bool has_rule = rit->second >= 0;
             size_t q = 16;
             bool ok = true;
             const size_t v0 = B.pvals.size();
@@ -493,8 +549,8 @@ inline bool sentinel_wire_server::on_readable(wire::Loop &L, wire::Conn *c) {
                     default: continue;                     // unknown type: only its byte consumed
                 }
                 if (q + (size_t)w > dl) { ok = false; break; }
-                uint64_t key;
-                interner->key(fid, t, d + q, w, key);
+                uint64_t key = 1;
+                if (has_rule) interner->key(fid, t, d + q, w, key, ts);
                 B.pvals.push_back(key);
                 q += (size_t)w;
             }
@@ -507,6 +563,7 @@ inline bool sentinel_wire_server::on_readable(wire::Loop &L, wire::Conn *c) {
             B.pev.push_back(pe);
             B.pfid.push_back(fid);
             B.pxid.push_back(xid);
+            B.pnorule.push_back(!has_rule);
         }
         // any other type: no decoder, nothing emitted
     }
@@ -531,7 +588,7 @@ inline bool sentinel_wire_server::on_readable(wire::Loop &L, wire::Conn *c) {
         std::vector<int32_t> idx(n);
         std::vector<sentinel_verdict_t> out(n);
         int rc = sentinel_lookup_param_idx(e, n, B.pfid.data(), idx.data());
-        for (int64_t i = 0; i < n; ++i) B.pev[i].rule_idx = idx[i];
+        for (int64_t i = 0; i < n; ++i) B.pev[i].rule_idx = B.pnorule[i] ? -1 : idx[i];
         if (!rc) rc = sentinel_submit_param_multi_batch_host(e, n, B.pev.data(), B.pvals.data(),
                                                              (int64_t)B.pvals.size(), out.data());
         for (int64_t i = 0; i < n; ++i)
@@ -592,8 +649,30 @@ int sentinel_param_interner_destroy(sentinel_param_interner_t *it) {
 
 int sentinel_param_interner_key(sentinel_param_interner_t *it, int64_t flow_id, int32_t type, const uint8_t *value,
                                 int32_t len, uint64_t *key) {
+    return sentinel_param_interner_key_at(it, flow_id, type, value, len, INT64_MIN, key);
+}
+
+int sentinel_param_interner_key_at(sentinel_param_interner_t *it, int64_t flow_id, int32_t type, const uint8_t *value,
+                                   int32_t len, int64_t ts, uint64_t *key) {
     if (!it || !key || len < 0 || (len > 0 && !value)) return fail(SENTINEL_E_INVALID, "bad arguments");
-    if (!it->key(flow_id, type, value, len, *key)) return fail(SENTINEL_E_INVALID, "unsupported type or value width");
+    if (!it->key(flow_id, type, value, len, *key, ts)) return fail(SENTINEL_E_INVALID, "unsupported type or value width");
+    return 0;
+}
+
+int sentinel_param_interner_set_limits(sentinel_param_interner_t *it, int64_t max_entries, int64_t idle_ms) {
+    if (!it || max_entries < 4 || idle_ms < 0) return fail(SENTINEL_E_INVALID, "bad interner limits");
+    std::lock_guard<std::mutex> g(it->mu);
+    it->max_entries = max_entries;
+    it->idle_ms = idle_ms;
+    if ((int64_t)it->ids.size() > max_entries) it->shrink_locked();
+    return 0;
+}
+
+int sentinel_param_interner_stats(sentinel_param_interner_t *it, int64_t *entries, int64_t *evicted) {
+    if (!it) return fail(SENTINEL_E_INVALID, "null interner");
+    std::lock_guard<std::mutex> g(it->mu);
+    if (entries) *entries = (int64_t)it->ids.size();
+    if (evicted) *evicted = it->evicted;
     return 0;
 }
 

@@ -136,10 +136,18 @@ class GpuTokenService:
         self.device = device
         self.sample_counts = {}
         self._flow_rules = []
+        self._servers = weakref.WeakSet()    # native wire servers running on this engine
         if namespaces is not None:
             self.set_namespaces(namespaces)
 
+    def _attach_server(self, srv):
+        self._servers.add(srv)
+
     def close(self):
+        """Destroys the engine; native wire servers still running on it are stopped first (their I/O
+        and dispatcher threads hold the engine pointer)."""
+        for srv in list(getattr(self, "_servers", ())):
+            srv.stop()
         if getattr(self, "_h", None) and self._h.value:
             self._L.sentinel_engine_destroy(self._h)
             self._h = C.c_void_p()

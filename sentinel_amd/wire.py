@@ -540,20 +540,39 @@ class NativeParamInterner:
         _lib.check(self._L.sentinel_param_interner_create(C.byref(h)), "param_interner_create")
         self.handle = h
 
-    def key(self, flow_id: int, value: TypedValue) -> int:
+    def key(self, flow_id: int, value: TypedValue, ts: Optional[int] = None) -> int:
+        """The value's key; `ts` (ms) is the request time that last used it (None: no aging)."""
         from . import _lib
         import ctypes as C
         b = _value_bytes(value)
         k = C.c_uint64()
         buf = C.create_string_buffer(b, len(b)) if b else None
-        _lib.check(self._L.sentinel_param_interner_key(self.handle, int(flow_id), int(value.tag), buf, len(b), C.byref(k)),
-                   "param_interner_key")
+        t = -(1 << 63) if ts is None else int(ts)
+        _lib.check(self._L.sentinel_param_interner_key_at(self.handle, int(flow_id), int(value.tag), buf, len(b), t,
+                                                          C.byref(k)), "param_interner_key")
         return int(k.value)
+
+    def set_limits(self, max_entries: int, idle_ms: int):
+        from . import _lib
+        _lib.check(self._L.sentinel_param_interner_set_limits(self.handle, int(max_entries), int(idle_ms)),
+                   "param_interner_set_limits")
+
+    def stats(self):
+        import ctypes as C
+        n, ev = C.c_int64(), C.c_int64()
+        self._L.sentinel_param_interner_stats(self.handle, C.byref(n), C.byref(ev))
+        return {"entries": n.value, "evicted": ev.value}
 
     def close(self):
         if self.handle:
             self._L.sentinel_param_interner_destroy(self.handle)
             self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class NativeTokenServer:
@@ -573,9 +592,24 @@ class NativeTokenServer:
         cfg = _lib.WireConfig(host.encode(), int(port), int(io_threads), int(max_batch), int(max_wait_us),
                               self._names, len(namespaces), interner.handle if interner else None, self._clock, None)
         h = C.c_void_p()
+        self.handle = None
+        self.interner = interner         # kept alive as long as the server may use it
         _lib.check(self._L.sentinel_wire_server_create(svc.handle, C.byref(cfg), C.byref(h)), "wire_server_create")
         self.handle = h
         self.port = int(self._L.sentinel_wire_server_port(h))
+        svc._attach_server(self)         # the service keeps the server and stops it before it closes
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.stop()
+
+    def __del__(self):
+        try:
+            self.stop()
+        except Exception:
+            pass
 
     def stats(self):
         import ctypes as C

@@ -71,3 +71,27 @@ def test_cluster_batchers_route_per_call(oracle_mod):
         passed = sum(1 for k, r in results.items() if k % 64 == f and r.status == 0)
         assert passed == min(30, int(rules.count[f])), (f, passed, rules.count[f])
     cl.close()
+
+
+@pytest.mark.gpu
+def test_cluster_rejects_per_shard_namespace_limiters():
+    """A namespace GlobalRequestLimiter split over flowId-hash shards would admit up to n x the cap:
+    a multi-shard cluster refuses has_limiter namespaces; a single-shard cluster accepts and applies
+    them exactly (GlobalRequestLimiter.java:46-55)."""
+    import sentinel_amd as sa
+    from sentinel_amd.token_service import ServerNamespace
+    cl = sa.GpuTokenCluster([0, 0])
+    with pytest.raises(sa.SentinelError):
+        cl.set_namespaces([ServerNamespace(connected_count=1, has_limiter=True, max_allowed_qps=10.0)])
+    cl.set_namespaces([ServerNamespace(connected_count=1, has_limiter=False)])     # no limiter: fine
+    cl.close()
+    one = sa.GpuTokenCluster([0])
+    one.set_namespaces([ServerNamespace(connected_count=1, has_limiter=True, max_allowed_qps=10.0)])
+    rng = np.random.default_rng(6)
+    rules = T.make_rules(50, rng, count_lo=1000, count_hi=2000, sample_count=10, window_interval_ms=1000)
+    one.load_rules_array(rules.flow_id, rules.count, rules.threshold_type, rules.sample_count,
+                         rules.window_interval_ms, rules.namespace, rules.checker)
+    fids = rules.flow_id[rng.integers(0, 50, size=200)]
+    st, _, _ = one.submit_host(fids, np.ones(200, np.int32), np.full(200, T.T0_ALIGNED + 1, np.int64))
+    assert int((st == 0).sum()) == 10 and int((st == -2).sum()) == 190     # the node-wide cap of 10 QPS
+    one.close()

@@ -275,9 +275,10 @@ def test_snapshot_matches_oracle_avgs(oracle_mod):
         assert snap["block_qps"][f] == float(d[valid, 2].sum()) / I_s
 
 
-@pytest.mark.parametrize("path", ["slot", "rule"])
+@pytest.mark.parametrize("path", ["part", "slot", "rule"])
 def test_param_single_value_bitexact(oracle_mod, monkeypatch, path):
-    """Exact single-value requests through the per-slot segment pipeline and the per-rule walk."""
+    """Exact single-value requests through the partition-local path (default), the per-slot segment
+    pipeline and the per-rule walk."""
     monkeypatch.setenv("SENTINEL_PARAM_PATH", path)
     count, hot, rule_idx, vals, keys, ts = T.config4(120_000, seed=4, n_rules=200, universe=300)
     import sentinel_amd as sa

@@ -128,3 +128,51 @@ def test_top_values_match_oracle(oracle_mod):
     for r in range(R):
         assert rec["flow_id"][r] == 7000 + r and rec["n_top"][r] == len(top[r])
         assert [(int(k), float(v)) for k, v in zip(rec["key"][r][:len(top[r])], rec["avg"][r][:len(top[r])])] == top[r]
+
+
+@pytest.mark.parametrize("path", ["part", "slot"])
+def test_param_part_edges_bitexact(oracle_mod, monkeypatch, path):
+    """Edge cases of the partition-local param path (param_part.hpp) against the oracle: one key hot
+    enough to span many LDS chunks (and ranges far larger than a chunk), acquire counts past the packed
+    field (escaped: read back from the event), a batch whose timestamps jump by 20 hours (ts - T0 past
+    the packed 27-bit field), invalid requests (acquire <= 0, unknown rule, ts < 0) mixed in, hot items,
+    and a second batch continuing every window.  Timestamps are non-decreasing per rule (the documented
+    precondition of exact param parity)."""
+    monkeypatch.setenv("SENTINEL_PARAM_PATH", path)
+    R = 64
+    rng = np.random.default_rng(29)
+    prules = [dict(flow_id=500 + r, count=float(rng.integers(3, 400)), sample_count=(2, 4, 5, 10)[r % 4],
+                   window_interval_ms=1000) for r in range(R)]
+    fids = np.array([r["flow_id"] for r in prules], dtype=np.uint64)
+    hot_key = int((fids[3] << np.uint64(32)) | np.uint64(7))
+    prules[3]["hot"] = {hot_key: 50_000}
+    svc = _svc(prules)
+    orc = oracle_mod.TokenServiceOracle([], param_rules=prules,
+                                        hot_items={3: [(hot_key, 50_000)]})
+    t0 = T.T0_ALIGNED + 13
+    for batch in range(2):
+        m = 60_000
+        ts = np.sort(t0 + rng.integers(0, 3000, size=m)).astype(np.int64)
+        ts[m // 2:] += 20 * 3600 * 1000                  # a 20 h jump inside the batch
+        ridx = rng.integers(0, R, size=m).astype(np.int32)
+        vals = T.zipf_indices(400, 1.1, m, rng, permute=False).astype(np.uint64)
+        keys = (fids[ridx] << np.uint64(32)) | vals
+        hot = rng.random(m) < 0.5                          # half the batch on one key (~15 chunks)
+        ridx[hot] = 3
+        keys[hot] = hot_key
+        acq = np.where(rng.random(m) < 0.1, rng.integers(400, 3000, size=m), 1).astype(np.int32)
+        bad = rng.random(m)
+        acq[bad < 0.002] = 0                               # BAD_REQUEST
+        ridx[(bad >= 0.002) & (bad < 0.004)] = R + 5       # NO_RULE_EXISTS
+        ts[(bad >= 0.004) & (bad < 0.005)] = -1            # FAIL (the reference's NPE)
+        st_g, rem_g = svc.submit_param_batch_host(ridx, acq, keys, ts)
+        st_o, rem_o = orc.param_replay(ridx, acq, keys, ts)
+        mis = np.nonzero((st_g != st_o) | (rem_g != rem_o))[0]
+        assert len(mis) == 0, (batch, len(mis), mis[:5], st_g[mis[:5]], st_o[mis[:5]], rem_g[mis[:5]], rem_o[mis[:5]])
+        assert {-4, -1, 0, 1, 3} <= set(np.unique(st_o).tolist())
+        t0 = int(ts.max()) + 1
+    t = t0
+    for i in range(0, 3000, 41):
+        r, k = int(ridx[i]), int(keys[i])
+        if 0 <= r < R:
+            assert svc.param_sum(r, k, t) == orc.param_sum(r, t, k)

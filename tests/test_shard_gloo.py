@@ -102,3 +102,67 @@ def test_owner_is_deterministic_and_balanced():
     counts = np.bincount(o, minlength=8)
     assert counts.min() > 0.98 * counts.mean()
     assert np.array_equal(o, SH.owner_of(ids, 8))
+
+
+def _param_trace():
+    rng = np.random.default_rng(44)
+    R = 240
+    prules = [dict(flow_id=9000 + 7 * r, count=float(rng.integers(20, 200)), sample_count=4, window_interval_ms=1000)
+              for r in range(R)]
+    m = 40_000
+    ts = T.timestamps(m, 30_000.0, T.T0_ALIGNED + 3)
+    ridx = rng.integers(0, R, size=m).astype(np.int32)
+    vals = T.zipf_indices(50, 1.3, m, rng, permute=False).astype(np.uint64)
+    fids = np.array([p["flow_id"] for p in prules], dtype=np.uint64)
+    keys = (fids[ridx] << np.uint64(20)) | vals
+    acq = rng.integers(1, 3, size=m).astype(np.int32)
+    return prules, ridx, acq, keys, ts
+
+
+def _param_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from oracle import oracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        prules, ridx, acq, keys, ts = _param_trace()
+        fids = np.array([p["flow_id"] for p in prules], dtype=np.int64)
+        mine = SH.local_rule_subset(fids, rank, world)
+        remap = -np.ones(len(prules), np.int64)
+        remap[mine] = np.arange(len(mine))
+        pos = SH.split_batch(SH.owner_of(fids, world)[ridx], world)[rank]
+        orc = O.TokenServiceOracle([], param_rules=[prules[i] for i in mine])
+        orc.param_replay(remap[ridx[pos]].astype(np.int32), acq[pos], keys[pos], ts[pos])
+        t = int(ts[-1]) + 1
+        tops = [orc.param_top_values(i, t) for i in range(len(mine))]
+        gathered = SH.gather_param_snapshot(SH.param_snapshot_records(fids[mine], tops))
+        q.put((rank, SH.unpack_param_snapshot(gathered)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_param_snapshot_equals_single_engine():
+    """The snapshot's param leg (ClusterMetricNodeGenerator.paramToMetricNode, top-5 values per param
+    rule) all-gathered over two gloo ranks equals one engine's getTopValues for every rule."""
+    import torch.multiprocessing as mp
+    from oracle import oracle as O
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_param_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    prules, ridx, acq, keys, ts = _param_trace()
+    orc = O.TokenServiceOracle([], param_rules=prules)
+    orc.param_replay(ridx, acq, keys, ts)
+    t = int(ts[-1]) + 1
+    want = {p["flow_id"]: orc.param_top_values(i, t) for i, p in enumerate(prules)}
+    assert res[0][1] == res[1][1]                  # every rank holds the same gathered snapshot
+    assert res[0][1] == want
+    assert any(len(v) == 5 for v in want.values())

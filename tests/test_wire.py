@@ -196,6 +196,27 @@ def test_native_interner_equality_classes_match_python():
     nat.close()
 
 
+def test_native_interner_is_bounded():
+    """A flood of distinct values cannot grow the native interner without limit: past max_entries,
+    values idle for longer than idle_ms go first (exact: their windows are empty), then the least
+    recently used; a value in use keeps its key; keys are never reused."""
+    nat = W.NativeParamInterner()
+    nat.set_limits(1000, 5000)
+    hot = nat.key(7, W.jlong(-1), ts=0)
+    seen = set()
+    for i in range(20_000):
+        t = i                                       # 1 ms apart: the last 5000 are inside the horizon
+        seen.add(nat.key(7, W.jlong(i), ts=t))
+        if i % 100 == 0:
+            assert nat.key(7, W.jlong(-1), ts=t) == hot      # recently used: same key
+        assert nat.stats()["entries"] <= 1000
+    st = nat.stats()
+    assert st["evicted"] >= 19_000 and len(seen) == 20_000  # keys are unique, never recycled
+    # an idle value comes back with a fresh key (its window expired; the reference's CacheMaps are empty too)
+    assert nat.key(7, W.jlong(0), ts=20_000) not in seen
+    nat.close()
+
+
 def _ask(cl, frame):
     cl.send(frame)
     return cl.recv()
