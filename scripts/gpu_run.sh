@@ -7,6 +7,7 @@
 #   prof=<config>[,<args>]       rocprofv3 --kernel-trace --stats of a short bench run of that config
 #   pmc=<tag>,<config>[,<args>]  separate FETCH_SIZE / WRITE_SIZE passes -> profiles/pmc/<tag>.json
 #   smoke                        __graft_entry__.smoke()
+#   stream                       scripts/host_stream_study.py under rocprofv3 kernel + memory-copy trace
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 TAG=$1; shift
@@ -41,6 +42,10 @@ for S in "$@"; do
       A=${S#pmc=}; T=${A%%,*}; B=${A#*,}; C=${B%%,*}; X=""; [ "$B" != "$C" ] && X=${B#*,}; X=${X//,/ }
       echo "== pmc $T ($C $X)"
       bash scripts/gpu_pmc_shape.sh $T --config $C $X || exit 1 ;;
+    stream)
+      echo "== host stream study"
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/stream_$n -o run -- python $R/scripts/host_stream_study.py > $O/stream_$n.log 2> $O/stream_$n.err ) || { tail -20 $O/stream_$n.err; exit 1; }
+      cat $O/stream_$n.log ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
 done
