@@ -67,7 +67,7 @@ KERNEL_SYMBOLS = {
     "part_fused": ("k_part_half",), "part_big": ("k_part_big",), "part_long": ("k_part_long",),
     "param_prep": ("k_param_prep", "k_pp_prep"), "param_meta": ("k_param_meta",), "prule_prep": ("k_prule_prep",),
     "prule_process": ("k_prule_process",), "part_unsplit": ("k_part_unsplit",), "lim_prep": ("k_lim1_prep",),
-    "param_scatter": ("k_pp_scatter",), "param_decide": ("k_pp_decide",),
+    "param_scatter": ("k_pp_scatter",), "param_group": ("k_pp_group",), "param_decide": ("k_pp_walk", "k_pp_decide"),
 }
 PMC_DIR = os.path.join(ROOT, "profiles", "pmc")
 
@@ -427,12 +427,20 @@ class ParamWorkload:
         if dom == "radix_scatter":
             passes = max(1, round(d["calls"] / max(1, steps)))
             return (32.0 + 24.0 * (passes - 1)) / passes
-        if dom == "param_decide":
-            # per request: read key 8 + packed value 8 + rule 4 from the multi-split, write the 8-B verdict;
-            # per distinct (rule, value) key: the slot probe 8, its n {epoch, count} pairs read (16 n) and
-            # the rolled pair written back (16), the rule's window fields + threshold (~24 B)
+        if dom == "param_group":
+            # per request: the range's keys read once per sub-range workgroup (8 B x S, L2-shared), its
+            # packed value 8 + rule 4 read, the grouped value written 8; per distinct key a 16-B record
+            nsub = 1
+            while 1024 * nsub * 1024 < self.N and nsub < 256:
+                nsub *= 2
             e_k = self.N / max(1, self._dk) if hasattr(self, "_dk") else 1.0
-            return 28.0 + (8 + 16 * self.n + 16 + 24) / e_k
+            return 8.0 * nsub + 20.0 + 16.0 / e_k
+        if dom == "param_decide":
+            # per request: read the 8-B grouped value, write the 8-B verdict; per distinct (rule, value)
+            # key: its 16-B record, the slot probe 8, its n {epoch, count} pairs read (16 n) and the
+            # rolled pair written back (16), the rule's window fields + threshold (~24 B)
+            e_k = self.N / max(1, self._dk) if hasattr(self, "_dk") else 1.0
+            return 16.0 + (16 + 8 + 16 * self.n + 16 + 24) / e_k
         if dom == "process":
             # per touched (rule, value) slot: read n {epoch, count} pairs, write one; per event: segment record
             return 24.0 + (self.n * 16 + 16) / 4.0

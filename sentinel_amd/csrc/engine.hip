@@ -25,6 +25,7 @@
 #include <thread>
 #include <string>
 #include <unordered_map>
+#include <deque>
 #include <vector>
 
 #include "../../include/sentinel_amd.h"
@@ -337,6 +338,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_param_prep(
                         M.Is[h] = PR.I_s[e.idx];
                         M.thr[h] = value_threshold(PR, (uint32_t)e.idx, e.key);   // CPFC:113-120
                         M.kind[h] = KIND_PARAM;
+                        slot_state_init(M.state, M.stride, (uint64_t)h, PR.n[e.idx]);
                     }
                     if (r >= 0) l = (uint32_t)r;
                 }
@@ -600,6 +602,8 @@ struct sentinel_engine {
     std::vector<sentinel_param_rule_t> prules;
     std::unordered_map<int64_t, int32_t> param_index;
     DevBuf d_prule_route, d_prule_n, d_prule_w, d_prule_rcp, d_prule_Is, d_prule_thr;
+    DevBuf d_prule_rec, d_prule_hot;   // packed per-rule records (k_prule_pack) + has-hot-items flags
+    bool prec_dirty = true;
     DevBuf d_ptable, d_slot_rule, d_hot_table, d_hot_thr;
     bool param_plain = true;
     TableBufs pt;
@@ -616,6 +620,12 @@ struct sentinel_engine {
     uint64_t p_live = 0;               // live slots after the last rebuild
     uint64_t p_ub = 0;                 // values submitted since (an upper bound of the fresh inserts)
     DevBuf d_pfresh;                   // device: fresh inserts since the last rebuild
+    // pinned mirror {batch ordinal, d_pfresh after it} written by the device after every partition-path
+    // param batch: the reserve check knows the exact fresh count up to a recent batch without a sync
+    unsigned long long *h_pfresh = nullptr;
+    uint64_t p_ord = 0;                // param batches reserved so far
+    uint64_t p_reset_ord = 0;          // first batch ordinal after d_pfresh was last zeroed
+    std::deque<std::pair<uint64_t, uint64_t>> p_pending;   // (ordinal, values) reserved since the reset
     // the previous table's buffers, kept as the next rebuild's target (no hipMalloc / hipFree per rebuild)
     DevBuf sp_keys, sp_rule, sp_state, sp_n, sp_w, sp_rcp, sp_Is, sp_thr, sp_kind;
     uint64_t p_rebuilds = 0;
@@ -840,7 +850,8 @@ struct sentinel_engine {
     }
     SlotMeta slot_meta() {
         return SlotMeta{pt.n.as<int32_t>(), pt.w.as<int32_t>(), pt.rcp.as<double>(), pt.Is.as<double>(),
-                        pt.thr.as<double>(), pt.kind.as<uint8_t>(), d_slot_rule.as<int32_t>()};
+                        pt.thr.as<double>(), pt.kind.as<uint8_t>(), d_slot_rule.as<int32_t>(), pt.state.as<int64_t>(),
+                        param_stride(pmax_n)};
     }
 
     void scan(uint32_t *buf, int64_t n, bool exclusive, hipStream_t s) {
@@ -1187,8 +1198,7 @@ int sentinel_engine::param_rebuild(uint64_t new_cap, const std::vector<int32_t> 
         cleanup();
         return fail(SENTINEL_E_DEVICE, "memset failed");
     }
-    k_init_state<<<grid_for((int64_t)new_cap), 256, 0, stream>>>(nstate.as<int64_t>(), nullptr, nstride, nullptr, new_maxn,
-                                                                 nstride, (int64_t)new_cap);
+    // (no state initialisation: every slot is written by the rebuild / import below or by its fresh insert)
     const PSlots N{nkeys.as<unsigned long long>(), nrule.as<int32_t>(), nstate.as<int64_t>(), nstride, new_cap - 1};
     const PSlots O{d_ptable.as<unsigned long long>(), d_slot_rule.as<int32_t>(), pt.state.as<int64_t>(), ostride, pcap - 1};
     unsigned long long *live = dcount.as<unsigned long long>();
@@ -1260,6 +1270,8 @@ int sentinel_engine::param_rebuild(uint64_t new_cap, const std::vector<int32_t> 
     pmax_n = new_maxn;
     p_live = cnt[0];
     p_ub = 0;
+    p_reset_ord = p_ord;
+    p_pending.clear();
     ++p_rebuilds;
     pmeta_dirty = true;
     return 0;
@@ -1272,11 +1284,38 @@ int sentinel_engine::param_rebuild(uint64_t new_cap, const std::vector<int32_t> 
 int sentinel_engine::param_reserve(int64_t nv) {
     if (!d_ptable.p) return 0;
     const uint64_t lim = pcap / 4 * 3;
-    if (p_live + p_ub + (uint64_t)nv <= lim) { p_ub += (uint64_t)nv; return 0; }
+    const uint64_t ord = p_ord++;
+    if (p_live + p_ub + (uint64_t)nv <= lim) {
+        p_ub += (uint64_t)nv;
+        p_pending.emplace_back(ord, (uint64_t)nv);
+        return 0;
+    }
+    if (h_pfresh) {                 // the device's last published count: exact up to that batch
+        const uint64_t seq = ((volatile unsigned long long *)h_pfresh)[0];
+        const uint64_t pub = ((volatile unsigned long long *)h_pfresh)[1];
+        if (seq != ~0ull && seq >= p_reset_ord && seq < ord) {
+            while (!p_pending.empty() && p_pending.front().first <= seq) p_pending.pop_front();
+            uint64_t after = 0;
+            for (auto &x : p_pending) after += x.second;
+            if (p_live + pub + after + (uint64_t)nv <= lim) {
+                p_ub = pub + after + (uint64_t)nv;
+                p_pending.emplace_back(ord, (uint64_t)nv);
+                return 0;
+            }
+        }
+    }
     unsigned long long fresh = 0;
     HIP_OK(hipMemcpyAsync(&fresh, d_pfresh.p, 8, hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
-    if (p_live + fresh + (uint64_t)nv <= lim) { p_live += fresh; p_ub = (uint64_t)nv; HIP_OK(hipMemsetAsync(d_pfresh.p, 0, 8, stream)); return 0; }
+    p_pending.clear();
+    if (p_live + fresh + (uint64_t)nv <= lim) {
+        p_live += fresh;
+        p_ub = (uint64_t)nv;
+        HIP_OK(hipMemsetAsync(d_pfresh.p, 0, 8, stream));
+        p_reset_ord = ord;
+        p_pending.emplace_back(ord, (uint64_t)nv);
+        return 0;
+    }
     std::vector<int32_t> ident(prules.size());
     for (size_t i = 0; i < ident.size(); ++i) ident[i] = (int32_t)i;
     int rc = param_rebuild(pcap, ident, pmax_n, h_prule_n, {}, 0, {}, nullptr);        // reclaim dead slots
@@ -1285,15 +1324,18 @@ int sentinel_engine::param_reserve(int64_t nv) {
     // batches of new values fit too, so that the reclaiming rebuild (a device-wide pass and a host sync)
     // comes back every few batches, not every batch, under a steady churn of values
     const uint64_t slot_bytes = 8 + 4 + (uint64_t)param_stride(pmax_n) * 8 + 4 + 4 + 8 + 8 + 8 + 1;
-    const uint64_t budget = (uint64_t)8 << 30;            // per table (the rebuild holds two)
+    const uint64_t budget = (uint64_t)24 << 30;           // per table (the rebuild holds two): 288 GB of HBM
     uint64_t cap = pcap;
     while (p_live + (uint64_t)nv > cap / 4 * 3) cap <<= 1;
-    while (p_live + 4 * (uint64_t)nv > cap / 4 * 3 && 2 * cap * slot_bytes <= budget) cap <<= 1;
+    while (p_live + 8 * (uint64_t)nv > cap / 4 * 3 && 2 * cap * slot_bytes <= budget) cap <<= 1;
     if (cap != pcap) {
         rc = param_rebuild(cap, ident, pmax_n, h_prule_n, {}, 0, {}, nullptr);         // grow
         if (rc) return rc;
     }
     p_ub = (uint64_t)nv;
+    p_reset_ord = ord;              // (param_rebuild zeroed d_pfresh)
+    p_pending.clear();
+    p_pending.emplace_back(ord, (uint64_t)nv);
     return 0;
 }
 
@@ -1337,7 +1379,13 @@ int sentinel_engine::param_thresholds() {
     if (rc) return rc;
     hot_mask = hcap - 1;
     has_hot = !hot.empty();
+    {
+        std::vector<uint8_t> hf(std::max<size_t>(R, 1), 0);
+        for (size_t i = 0; i < R; ++i) hf[i] = prules[i].hot_n > 0;
+        if (upload(d_prule_hot, hf)) return SENTINEL_E_NOMEM;
+    }
     pmeta_dirty = true;
+    prec_dirty = true;
     return 0;
 }
 
@@ -1361,6 +1409,7 @@ int sentinel_engine::reset_param_metrics(int32_t sample_count, int32_t interval_
     rc |= upload(d_prule_rcp, rcp);
     rc |= upload(d_prule_Is, Is);
     if (rc) return rc;
+    prec_dirty = true;
     pmax_n = sample_count;
     if (d_ptable.p) {
         rc = param_rebuild(pcap, std::vector<int32_t>(R, -1), pmax_n, h_prule_n, {}, 0, {}, nullptr);
@@ -1777,7 +1826,7 @@ static int submit_param_part(sentinel_engine_t *e, int64_t n, const ParamEvent *
     const int32_t *route = e->param_plain ? nullptr : e->d_prule_route.as<int32_t>();
     e->launch("param_prep", n, s, [&] {
         k_pp_prep<<<dim3((unsigned)nb), dim3(PP_THREADS), 0, s>>>(n, ev, have ? R : 0, route, e->param_ctx().R, out,
-                                                                  pbits, hist, P);
+                                                                  pbits, hist, P, e->w_counters.as<uint32_t>());
     });
     if (!have) {
         HIP_OK(hipGetLastError());
@@ -1799,14 +1848,41 @@ static int submit_param_part(sentinel_engine_t *e, int64_t n, const ParamEvent *
     const PSlots S{e->d_ptable.as<unsigned long long>(), e->d_slot_rule.as<int32_t>(), e->pt.state.as<int64_t>(),
                    param_stride(e->pmax_n), e->pcap - 1};
     const ParamRules PR = e->param_ctx().R;
+    if (e->prec_dirty || e->d_prule_rec.bytes < (size_t)R * sizeof(PRuleRec)) {
+        if (e->d_prule_rec.ensure((size_t)R * sizeof(PRuleRec))) return SENTINEL_E_NOMEM;
+        k_prule_pack<<<(unsigned)((R + 255) / 256), 256, 0, s>>>(R, PR, e->d_prule_hot.p ? e->d_prule_hot.as<uint8_t>() : nullptr,
+                                                                e->d_prule_rec.as<PRuleRec>());
+        e->prec_dirty = false;
+    }
+    const PRuleRec *RR = e->d_prule_rec.as<PRuleRec>();
     unsigned long long *fresh = e->d_pfresh.as<unsigned long long>();
-    e->launch("param_decide", n, s, [&] {
-        const int hb = header_block_slots(e->pmax_n);
-        if (hb <= 2) k_pp_decide<2><<<(unsigned)P, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, ev, PR, S, out, fresh);
-        else if (hb <= 4) k_pp_decide<4><<<(unsigned)P, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, ev, PR, S, out, fresh);
-        else if (hb <= 10) k_pp_decide<10><<<(unsigned)P, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, ev, PR, S, out, fresh);
-        else k_pp_decide<16><<<(unsigned)P, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, ev, PR, S, out, fresh);
+    // sub-ranges of <= PG_TARGET requests on average: one LDS chunk each (XCD-aware grid, k_pp_group)
+    int sbits = 0;
+    while (sbits < 8 && (int64_t)P * ((int64_t)1 << sbits) * PG_TARGET < n) ++sbits;
+    const unsigned ggrid = (unsigned)(((P + 7) / 8) * 8 * (1 << sbits));
+    uint64_t *gval = e->w_hep.as<uint64_t>();
+    const PKeyRecs RC{e->w_segep.as<unsigned long long>(), e->w_s0.as<uint2>(), e->w_k.as<int32_t>(),
+                      e->w_counters.as<uint32_t>()};
+    const int hb = header_block_slots(e->pmax_n);
+    e->launch("param_group", n, s, [&] {
+        if (hb <= 2) k_pp_group<2><<<ggrid, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, pbits, sbits, ev, PR, RR, S, out, fresh, gval, RC);
+        else if (hb <= 4) k_pp_group<4><<<ggrid, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, pbits, sbits, ev, PR, RR, S, out, fresh, gval, RC);
+        else if (hb <= 10) k_pp_group<10><<<ggrid, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, pbits, sbits, ev, PR, RR, S, out, fresh, gval, RC);
+        else k_pp_group<16><<<ggrid, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, pbits, sbits, ev, PR, RR, S, out, fresh, gval, RC);
     });
+    e->launch("param_decide", n, s, [&] {
+        const unsigned wg = (unsigned)std::min<int64_t>(2048, (n + 255) / 256);
+        if (hb <= 2) k_pp_walk<2><<<wg, 256, 0, s>>>(RC, gval, ev, PR, RR, S, out, fresh);
+        else if (hb <= 4) k_pp_walk<4><<<wg, 256, 0, s>>>(RC, gval, ev, PR, RR, S, out, fresh);
+        else if (hb <= 10) k_pp_walk<10><<<wg, 256, 0, s>>>(RC, gval, ev, PR, RR, S, out, fresh);
+        else k_pp_walk<16><<<wg, 256, 0, s>>>(RC, gval, ev, PR, RR, S, out, fresh);
+    });
+    if (!e->h_pfresh) {
+        HIP_OK(hipHostMalloc((void **)&e->h_pfresh, 16, 0));
+        e->h_pfresh[0] = ~0ull;
+        e->h_pfresh[1] = 0;
+    }
+    k_pfresh_publish<<<1, 1, 0, s>>>(fresh, e->p_ord - 1, e->h_pfresh);
     HIP_OK(hipGetLastError());
     return 0;
 }
@@ -2185,7 +2261,7 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
     e->lt.release();
     e->pt.release();
     for (DevBuf *b : {&e->d_flow_route, &e->d_flow_route8, &e->d_flow_ids, &e->d_prule_route, &e->d_prule_n, &e->d_prule_w,
-                      &e->d_prule_rcp, &e->d_prule_Is, &e->d_prule_thr, &e->d_ptable, &e->d_slot_rule,
+                      &e->d_prule_rcp, &e->d_prule_Is, &e->d_prule_thr, &e->d_prule_rec, &e->d_prule_hot, &e->d_ptable, &e->d_slot_rule,
                       &e->d_hot_table, &e->d_hot_thr, &e->w_fkey, &e->w_lkey, &e->w_skey, &e->w_sval, &e->w_ktmp,
                       &e->w_vtmp, &e->w_fhist, &e->w_lhist, &e->w_parts, &e->w_segid, &e->w_bad, &e->w_hep,
                       &e->w_hacq, &e->w_segstart, &e->w_segkey, &e->w_segep, &e->w_segacq, &e->w_het, &e->w_prio, &e->w_done,
@@ -2211,6 +2287,7 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
     if (e->s_h2d) (void)hipStreamDestroy(e->s_h2d);
     if (e->s_d2h) (void)hipStreamDestroy(e->s_d2h);
     if (e->h_part_stat) (void)hipHostFree(e->h_part_stat);
+    if (e->h_pfresh) (void)hipHostFree(e->h_pfresh);
     if (e->h_sm_ev) (void)hipHostFree(e->h_sm_ev);
     if (e->h_sm_fl) (void)hipHostFree(e->h_sm_fl);
     if (e->h_sm_out) (void)hipHostFree(e->h_sm_out);
@@ -2267,6 +2344,10 @@ int sentinel_profile_select(sentinel_engine_t *e, const char *kernel) {
 #ifdef SENTINEL_DIAG_PHASES
 int sentinel_diag_phases(unsigned long long *out, int n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), (size_t)n * 12 * 8) == hipSuccess ? 0 : -1;
+}
+int sentinel_diag_phases_clear() {
+    static std::vector<unsigned long long> z(4096 * 12, 0ull);
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z.data(), z.size() * 8) == hipSuccess ? 0 : -1;
 }
 #endif
 
@@ -2705,6 +2786,7 @@ int sentinel_load_param_rules(sentinel_engine_t *e, const sentinel_param_rule_t 
     rc |= upload(e->d_prule_w, ww);
     rc |= upload(e->d_prule_rcp, rcp);
     rc |= upload(e->d_prule_Is, Is);
+    e->prec_dirty = true;
     e->h_phot_keys.assign(hot_keys, hot_keys + n_hot);
     e->h_phot_counts.assign(hot_counts, hot_counts + n_hot);
     rc |= e->param_thresholds();

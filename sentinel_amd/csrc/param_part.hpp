@@ -13,13 +13,14 @@
 //   scan          the partition path's 2D scan of the tile-major histograms (partition.hpp)
 //   k_pp_scatter  stable multi-split of the valid requests into their ranges: param key, packed
 //                 {arrival position, acquire, ts - T0} and rule index, three coalesced arrays
-//   k_pp_decide   one workgroup per range, in chunks of PD_CAP requests (arrival order): the chunk's
-//                 distinct keys are staged in an LDS open-addressing table (the north star's
-//                 "LDS-staged" table: a key's HBM slot is probed once per chunk, not once per
-//                 request), its requests ranked stably by LDS entry with ballots and placed in
-//                 (key, arrival) order, then one lane per distinct key probes / inserts the HBM
-//                 slot, holds the window in VGPRs, decides the key's requests in arrival order and
-//                 writes the verdicts to their arrival positions and the rolled pairs back.
+//   k_pp_group    one workgroup per (range, sub-range of 2^sbits): the sub-range's requests (arrival
+//                 order) grouped by key in an LDS open-addressing table (the north star's "LDS-staged"
+//                 table: a key's HBM slot is probed once per batch, not once per request), ranked
+//                 stably with ballots and placed in (key, arrival) order; written out as grouped
+//                 values + one record per distinct key
+//   k_pp_walk     one lane per distinct key, no LDS: probes / inserts the key's HBM slot, holds the
+//                 window in VGPRs, decides the key's requests in arrival order and writes the
+//                 verdicts to their arrival positions and the rolled pairs back
 //
 // Replaces the per-slot radix-sort pipeline (k_param_prep -> 3 radix passes -> k_segments_v ->
 // k_process_reg_o4 -> k_verdict): per request it reads the 24-B event twice, moves 20 B through
@@ -92,8 +93,10 @@ __device__ inline int pp_status(const ParamEvent &e, int32_t nrules, const int32
 __global__ __launch_bounds__(PP_THREADS) void k_pp_prep(int64_t n, const ParamEvent *__restrict__ ev, int32_t nrules,
                                                          const int32_t *__restrict__ route, ParamRules PR,
                                                          uint64_t *__restrict__ out, int pbits,
-                                                         uint32_t *__restrict__ hist, int32_t nparts) {
+                                                         uint32_t *__restrict__ hist, int32_t nparts,
+                                                         uint32_t *__restrict__ zero_word) {
     __shared__ uint32_t h[PART_BINS];
+    if (blockIdx.x == 0 && threadIdx.x == 0 && zero_word) *zero_word = 0;   // the batch's key-record count
     const int64_t tile0 = (int64_t)blockIdx.x * PT_TILE;
     ParamEvent evs[PP_ITEMS];                         // every event load of the tile in flight at once
 #pragma unroll
@@ -225,24 +228,26 @@ __global__ __launch_bounds__(PT_THREADS) void k_pp_scatter(const ParamEvent *__r
 #ifndef SENTINEL_PD_THREADS
 #define SENTINEL_PD_THREADS 256
 #endif
-#ifndef SENTINEL_PD_ITEMS
-#define SENTINEL_PD_ITEMS 8
-#endif
 #ifndef SENTINEL_PD_HBITS
 #define SENTINEL_PD_HBITS 11
 #endif
 constexpr int PD_THREADS = SENTINEL_PD_THREADS;
 constexpr int PD_WAVES = PD_THREADS / WAVE;
-constexpr int PD_ITEMS = SENTINEL_PD_ITEMS;
-constexpr uint32_t PD_CAP = PD_THREADS * PD_ITEMS;      // requests per chunk
+#ifndef SENTINEL_PG_ITEMS
+#define SENTINEL_PG_ITEMS 5
+#endif
+constexpr int PG_ITEMS = SENTINEL_PG_ITEMS;
+constexpr uint32_t PG_CAP = PD_THREADS * PG_ITEMS;      // requests per chunk
 constexpr int PD_HBITS = SENTINEL_PD_HBITS;
 constexpr uint32_t PD_HT = 1u << PD_HBITS;              // LDS hash entries per round
 constexpr int PD_PROBES = 32;                           // a key not placed within this many probes waits a round
 constexpr int PD_EPT = PD_HT / PD_THREADS;               // entries per thread in the scans
 static_assert(PD_HT % PD_THREADS == 0, "entries per thread");
-static_assert(PD_CAP <= 65535, "16-bit wave counters");
-// requests per range the host aims at (ranges <= PART_BINS)
+static_assert(PG_CAP <= 65535 && PG_CAP < PD_HT, "16-bit wave counters, table larger than a chunk");
+static_assert(PD_THREADS * 4 <= (int)PG_CAP, "a scan tile fits an empty chunk");
+// requests per range the host aims at (ranges <= PART_BINS), and per sub-range (<= 0.8 PG_CAP)
 constexpr int64_t PD_TARGET = 2048;
+constexpr int64_t PG_TARGET = PG_CAP * 4 / 5;
 
 // Insert / find a key in the chunk's LDS table; -1: not within PD_PROBES probes (full neighbourhood).
 // All requests of one key agree: entries never change once set, so every request of a key that fails
@@ -266,6 +271,25 @@ __device__ inline int pd_insert(unsigned long long *hkey, int32_t *hrule, unsign
     return -1;
 }
 
+// A param rule's window fields and threshold in one 32-byte record (k_prule_pack): a key's walk reads
+// one line for its rule instead of five arrays, and looks up the hot-item table only when the rule has
+// hot items.
+struct PRuleRec {
+    double rcp_w;
+    double I_s;
+    double thr;          // rule count (x connectedCount for AVG_LOCAL)
+    int32_t w;
+    int32_t nf;          // n | has_hot_items << 16
+};
+static_assert(sizeof(PRuleRec) == 32, "one record per half line");
+
+__global__ __launch_bounds__(256) void k_prule_pack(int32_t R, ParamRules PR, const uint8_t *__restrict__ hot,
+                                                    PRuleRec *__restrict__ rec) {
+    const int32_t r = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (r >= R) return;
+    rec[r] = PRuleRec{PR.rcp_w[r], PR.I_s[r], PR.thr[r], PR.w[r], PR.n[r] | ((hot && hot[r]) ? 0x10000 : 0)};
+}
+
 // One key's requests [q0, q1) of sv (arrival order) against its exact HBM slot: the ClusterParamFlowChecker
 // state machine per request (CPFC:58-86 for one value: roll = LeapArray.currentWindow, sum over the valid
 // buckets, R = (T_v - sum / I_s) - a, pass iff !(R < 0) -> addValue), the window {epoch, count} x NMAX in
@@ -273,31 +297,42 @@ __device__ inline int pd_insert(unsigned long long *hkey, int32_t *hrule, unsign
 // backwards for this key) is the detached-bucket case (LeapArray.java:241-246): the sum reads the array,
 // the add is lost.
 template <int NMAX>
-__device__ inline void pd_walk(const ParamRules &PR, const PSlots &S, unsigned long long key, int32_t rule,
-                               const uint64_t *sv, uint32_t q0, uint32_t q1, const ParamEvent *ev, int64_t T0,
-                               uint64_t *out, uint32_t &nfresh) {
-    const int nsc = PR.n[rule];
-    const int32_t w = PR.w[rule];
-    const double rcp = PR.rcp_w[rule];
-    const double I_s = PR.I_s[rule];
-    const double thr = value_threshold(PR, (uint32_t)rule, key);        // CPFC:101-120
+__device__ inline void pd_walk(const ParamRules &PR, const PRuleRec *RR, const PSlots &S, unsigned long long key,
+                               int32_t rule, const uint64_t *sv, uint32_t q0, uint32_t q1, const ParamEvent *ev,
+                               int64_t T0, uint64_t *out, uint32_t &nfresh) {
+    const PRuleRec rr = RR[rule];
+    const int nsc = rr.nf & 0xFFFF;
+    const int32_t w = rr.w;
+    const double rcp = rr.rcp_w;
+    const double I_s = rr.I_s;
+    const double thr = (rr.nf >> 16) ? value_threshold(PR, (uint32_t)rule, key) : rr.thr;   // CPFC:101-120
     const uint32_t before = nfresh;
     const int64_t h = slot_insert_counted(S.keys, S.mask, key, nfresh);
     if (h < 0) {                                                         // table full: param_reserve prevents it
         for (uint32_t q = q0; q < q1; ++q) put_verdict(out, (uint32_t)sv[q] & SEQ_MASK, ST_FAIL, 0, 0);
         return;
     }
-    if (nfresh != before) S.rule[h] = rule;                              // read by the rebuild / top values
+    const bool fresh = nfresh != before;
+    if (fresh) S.rule[h] = rule;                                         // read by the rebuild / top values
     int64_t *st = S.state + h * S.stride;
     int64_t ep[NMAX], ct[NMAX];
+    uint32_t dirty = 0;
+    if (fresh) {                                                         // (the table's state is not pre-initialised)
 #pragma unroll
-    for (int j = 0; j < NMAX; ++j) {                                     // in bounds: stride >= 2 NMAX words
-        const longlong2 v = *reinterpret_cast<const longlong2 *>(st + 2 * j);
-        ep[j] = j < nsc ? v.x : EPOCH_ABSENT;
-        ct[j] = j < nsc ? v.y : 0;
+        for (int j = 0; j < NMAX; ++j) {
+            ep[j] = EPOCH_ABSENT;
+            ct[j] = 0;
+            if (j < nsc) dirty |= 1u << j;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j) {                                 // in bounds: stride >= 2 NMAX words
+            const longlong2 v = *reinterpret_cast<const longlong2 *>(st + 2 * j);
+            ep[j] = j < nsc ? v.x : EPOCH_ABSENT;
+            ct[j] = j < nsc ? v.y : 0;
+        }
     }
     const double rcpn = 1.0 / (double)nsc;
-    uint32_t dirty = 0;
     int64_t curE = -1, sum = 0;
     int slot = -1;
 #pragma unroll 1
@@ -343,21 +378,58 @@ __device__ inline void pd_walk(const ParamRules &PR, const PSlots &S, unsigned l
         if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(st + 2 * j) = longlong2{ep[j], ct[j]};
 }
 
+#ifdef SENTINEL_DIAG_PHASES     // per workgroup: [0] start, [3] end, [4..6] phase sums, [7] rounds, [8] keys
+#define PD_ACC(i, v) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_phase[blockIdx.x][i] += (v); } while (0)
+#define PD_NOW() wall_clock64()
+#else
+#define PD_ACC(i, v) do { } while (0)
+#define PD_NOW() 0ull
+#endif
+
+// Sub-range of a param key inside its range: the sbits hash bits right below the range digit.
+__device__ inline uint32_t pp_sub(uint64_t h, int pbits, int sbits) {
+    return sbits ? (uint32_t)((h << pbits) >> (64 - sbits)) : 0u;
+}
+
+// Per-key records the grouping kernel hands to the walk kernel: the key, its rule, and its requests'
+// run [start, start + count) in the grouped value array (arrival order inside the run).
+struct PKeyRecs {
+    unsigned long long *key;
+    uint2 *run;              // {start, count}
+    int32_t *rule;
+    uint32_t *count;         // records written (zeroed by k_pp_prep)
+};
+
+// k_pp_group: one workgroup per (range, sub-range): the S = 2^sbits workgroups of a range read the
+// range's keys (one L2-resident pass each: they share blockIdx % 8, hence an XCD, and are dispatched
+// together) and each keeps its sub-range's requests, compacted in arrival order (positions only, in
+// LDS).  A sub-range that fits one chunk (PG_CAP requests: the common case, the host sizes S for it)
+// is grouped by key in the LDS table -- distinct keys ranked stably with per-wave ballots, runs placed
+// in (key, arrival) order -- and written out as one coalesced run of grouped values plus one record per
+// distinct key; k_pp_walk decides the keys.  A larger sub-range (a skewed batch) is decided here, chunk
+// after chunk in arrival order, one lane per distinct key of the chunk (a key spanning chunks is walked
+// once per chunk, in order).
 template <int NMAX>
-__global__ __launch_bounds__(PD_THREADS) void k_pp_decide(const unsigned long long *__restrict__ pkey,
-                                                           const uint64_t *__restrict__ pval,
-                                                           const int32_t *__restrict__ prule,
-                                                           const uint32_t *__restrict__ rstart, int32_t nranges,
-                                                           const ParamEvent *__restrict__ ev, ParamRules PR, PSlots S,
-                                                           uint64_t *__restrict__ out, unsigned long long *fresh) {
+__global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long long *__restrict__ pkey,
+                                                          const uint64_t *__restrict__ pval,
+                                                          const int32_t *__restrict__ prule,
+                                                          const uint32_t *__restrict__ rstart, int32_t nranges,
+                                                          int pbits, int sbits, const ParamEvent *__restrict__ ev,
+                                                          ParamRules PR, const PRuleRec *__restrict__ RR, PSlots S,
+                                                          uint64_t *__restrict__ out, unsigned long long *fresh,
+                                                          uint64_t *__restrict__ gval, PKeyRecs RC) {
+    __shared__ uint32_t cq[PG_CAP];                   // the chunk's requests: positions in pkey / pval / prule
+    __shared__ uint64_t sv[PG_CAP];                   // grouped values
     __shared__ unsigned long long hkey[PD_HT];
     __shared__ int32_t hrule[PD_HT];
     __shared__ uint16_t cnt[PD_WAVES][PD_HT];
     __shared__ uint32_t hstart[PD_HT + 1];
-    __shared__ uint64_t sv[PD_CAP];
     __shared__ uint32_t waves_tot[PD_WAVES];
-    __shared__ uint32_t s_fresh;
-    const uint32_t p = blockIdx.x;
+    __shared__ uint32_t s_fresh, s_rbase;
+    const uint32_t nsub = 1u << sbits;
+    const uint32_t b = blockIdx.x;
+    const uint32_t p = (b / (8u * nsub)) * 8u + b % 8u;
+    const uint32_t sub = (b / 8u) % nsub;
     if ((int32_t)p >= nranges) return;                                   // block-uniform
     const int wave = threadIdx.x / WAVE;
     const uint32_t lane = lane_id();
@@ -366,23 +438,27 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_decide(const unsigned long lo
     const uint32_t r0 = rstart[p], r1 = rstart[p + 1];
     const int64_t T0 = pp_t0(ev);
     uint32_t nfresh = 0;
-    for (uint32_t c0 = r0; c0 < r1; c0 += PD_CAP) {
-        const uint32_t csz = min(PD_CAP, r1 - c0);
-        // chunk item j of this lane: chunk position wave * PD_ITEMS * 64 + j * 64 + lane (wave-contiguous,
-        // so the ballot ranking below keeps arrival order)
-        uint32_t pend = 0;                                               // items still to decide (bit j)
+    uint32_t below = 0;                                                  // this thread's requests of lower sub-ranges
+    bool slow = false;                                                   // a chunk was decided before the scan ended
+    uint32_t m = 0;                                                      // compacted requests (block-uniform)
+    PF_STAMP(0);
+
+    // decide / emit cq[0, m): rounds while the LDS table is full for some key
+    auto chunk = [&](bool emit, uint32_t gbase) {
+        uint32_t pend = 0;
 #pragma unroll
-        for (int j = 0; j < PD_ITEMS; ++j)
-            if ((uint32_t)wave * (PD_ITEMS * WAVE) + j * WAVE + lane < csz) pend |= 1u << j;
-        for (;;) {                                                       // rounds: keys past a full table wait
-            // the pending items (re)loaded each round: nothing but `pend` stays live across the walk
-            unsigned long long k[PD_ITEMS];
-            uint64_t v[PD_ITEMS];
-            int32_t ru[PD_ITEMS];
+        for (int j = 0; j < PG_ITEMS; ++j)
+            if ((uint32_t)wave * (PG_ITEMS * WAVE) + j * WAVE + lane < m) pend |= 1u << j;
+        uint32_t roff = 0;                                               // grouped values emitted by earlier rounds
+        for (;;) {
+            const unsigned long long pt0 = PD_NOW();
+            unsigned long long k[PG_ITEMS];
+            uint64_t v[PG_ITEMS];
+            int32_t ru[PG_ITEMS];
 #pragma unroll
-            for (int j = 0; j < PD_ITEMS; ++j) {
-                const uint32_t q = c0 + (uint32_t)wave * (PD_ITEMS * WAVE) + j * WAVE + lane;
+            for (int j = 0; j < PG_ITEMS; ++j) {
                 if (pend & (1u << j)) {
+                    const uint32_t q = cq[(uint32_t)wave * (PG_ITEMS * WAVE) + j * WAVE + lane];
                     k[j] = pkey[q];
                     v[j] = pval[q];
                     ru[j] = prule[q];
@@ -394,17 +470,18 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_decide(const unsigned long lo
                 for (uint32_t d = t; d < PD_WAVES * PD_HT / 2; d += PD_THREADS) z[d] = 0;
             }
             __syncthreads();
-            int eid[PD_ITEMS];
+            int eid[PG_ITEMS];
 #pragma unroll
-            for (int j = 0; j < PD_ITEMS; ++j) {
+            for (int j = 0; j < PG_ITEMS; ++j) {
                 eid[j] = -1;
                 if (pend & (1u << j))
                     eid[j] = pd_insert(hkey, hrule, k[j], ru[j], (uint32_t)(mix64(k[j]) >> 32) & (PD_HT - 1));
             }
             __syncthreads();
-            uint32_t rank[PD_ITEMS];
+            const unsigned long long pt1 = PD_NOW();
+            uint32_t rank[PG_ITEMS];
 #pragma unroll
-            for (int j = 0; j < PD_ITEMS; ++j) {
+            for (int j = 0; j < PG_ITEMS; ++j) {
                 const bool valid = eid[j] >= 0;
                 const uint32_t d = valid ? (uint32_t)eid[j] : 0u;
                 const uint64_t peers = match_peers<PD_HBITS>(d, valid, PD_HBITS);
@@ -416,7 +493,8 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_decide(const unsigned long lo
                 rank[j] = r;
             }
             __syncthreads();
-            // per entry: exclusive over waves in place, then an exclusive scan over entries -> run starts
+            // per entry: exclusive over waves in place, then one exclusive scan over entries of
+            // {requests : 16 | distinct keys : 16} -> run starts and each key's place in the key list
             uint32_t tot[PD_EPT];
             uint32_t mine = 0;
 #pragma unroll
@@ -430,32 +508,144 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_decide(const unsigned long lo
                     run += x;
                 }
                 tot[q] = run;
-                mine += run;
+                mine += run | (run ? 0x10000u : 0u);
             }
             uint32_t total;
             uint32_t pre = block_exclusive_scan(mine, waves_tot, &total);
+            uint32_t kpos = pre >> 16;
+            pre &= 0xFFFFu;
 #pragma unroll
             for (int q = 0; q < PD_EPT; ++q) {
                 hstart[t * PD_EPT + q] = pre;
                 pre += tot[q];
             }
-            if (t == 0) hstart[PD_HT] = total;
+            const uint32_t nkeys = total >> 16;
+            const uint32_t placed = total & 0xFFFFu;
+            if (t == 0) hstart[PD_HT] = placed;
+            if (emit && t == 0) s_rbase = atomicAdd(RC.count, nkeys);
             __syncthreads();
 #pragma unroll
-            for (int j = 0; j < PD_ITEMS; ++j) {
+            for (int j = 0; j < PG_ITEMS; ++j) {
                 if (eid[j] < 0) continue;
                 const uint32_t e = (uint32_t)eid[j];
                 sv[hstart[e] + cnt[wave][e] + rank[j]] = v[j];
                 pend &= ~(1u << j);
             }
             __syncthreads();
+            // the distinct keys listed densely (over the wave counters, free now)
+            uint16_t *klist = &cnt[0][0];
+#pragma unroll
+            for (int q = 0; q < PD_EPT; ++q)
+                if (tot[q]) klist[kpos++] = (uint16_t)(t * PD_EPT + q);
+            __syncthreads();
+            const unsigned long long pt2 = PD_NOW();
+            if (emit) {
+                for (uint32_t i = t; i < placed; i += PD_THREADS) gval[gbase + roff + i] = sv[i];
+                const uint32_t rb = s_rbase;
+                for (uint32_t q = t; q < nkeys; q += PD_THREADS) {
+                    const uint32_t e = klist[q];
+                    RC.key[rb + q] = hkey[e];
+                    RC.run[rb + q] = make_uint2(gbase + roff + hstart[e], hstart[e + 1] - hstart[e]);
+                    RC.rule[rb + q] = hrule[e];
+                }
+            } else {
 #pragma unroll 1
-            for (uint32_t e = t; e < PD_HT; e += PD_THREADS) {
-                const uint32_t s0 = hstart[e], s1 = hstart[e + 1];
-                if (s1 > s0) pd_walk<NMAX>(PR, S, hkey[e], hrule[e], sv, s0, s1, ev, T0, out, nfresh);
+                for (uint32_t q = t; q < nkeys; q += PD_THREADS) {
+                    const uint32_t e = klist[q];
+                    pd_walk<NMAX>(PR, RR, S, hkey[e], hrule[e], sv, hstart[e], hstart[e + 1], ev, T0, out, nfresh);
+                }
             }
-            if (!__syncthreads_or(pend != 0)) break;                     // (also: the walk is done with the LDS)
+            roff += placed;
+            const int more = __syncthreads_or(pend != 0);                // (also: done with the LDS)
+            const unsigned long long pt3 = PD_NOW();
+            PD_ACC(4, pt1 - pt0);
+            PD_ACC(5, pt2 - pt1);
+            PD_ACC(6, pt3 - pt2);
+            PD_ACC(7, 1ull);
+            PD_ACC(8, (unsigned long long)nkeys);
+            if (!more) break;
         }
+    };
+
+    // scan the range in tiles of PD_THREADS x 4 keys (4 consecutive keys per thread: the compaction
+    // below keeps arrival order), keep this sub-range's positions
+    for (uint32_t q0 = r0; q0 < r1; q0 += PD_THREADS * 4) {
+        const uint32_t qa = q0 + t * 4;
+        uint32_t mk = 0;                                                 // bit i: key qa + i is ours
+        if (qa + 4 <= r1 && (qa & 1u) == 0) {
+            const ulonglong2 a = *reinterpret_cast<const ulonglong2 *>(pkey + qa);
+            const ulonglong2 c = *reinterpret_cast<const ulonglong2 *>(pkey + qa + 2);
+            const unsigned long long kk[4] = {a.x, a.y, c.x, c.y};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t sd = pp_sub(mix64(kk[i]), pbits, sbits);
+                mk |= (sd == sub ? 1u : 0u) << i;
+                below += sd < sub;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (qa + i >= r1) break;
+                const uint32_t sd = pp_sub(mix64(pkey[qa + i]), pbits, sbits);
+                mk |= (sd == sub ? 1u : 0u) << i;
+                below += sd < sub;
+            }
+        }
+        uint32_t tile_n;
+        const uint32_t off = block_exclusive_scan((uint32_t)__popc(mk), waves_tot, &tile_n);
+        if (m + tile_n > PG_CAP) {                                       // the chunk is full: decide it now
+            slow = true;
+            chunk(false, 0);
+            m = 0;
+        }
+        uint32_t w = m + off;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (mk & (1u << i)) cq[w++] = qa + i;
+        m += tile_n;
+        __syncthreads();
+    }
+    if (m) {
+        if (slow) {
+            chunk(false, 0);
+        } else {
+            uint32_t nb;
+            const uint32_t base = block_exclusive_scan(below, waves_tot, &nb);   // (only the total is used)
+            (void)base;
+            chunk(true, r0 + nb);
+        }
+    }
+    PF_STAMP(3);
+    block_add_global(fresh, nfresh, &s_fresh);
+}
+
+// The exact param table's fresh-insert count after batch `ord`, mirrored to pinned host memory (value
+// first, then the ordinal: a host that reads the ordinal and then the value sees a count at least as
+// new as that batch's -- the count only grows until the host resets it with the stream drained).
+__global__ void k_pfresh_publish(const unsigned long long *fresh, unsigned long long ord, unsigned long long *host) {
+    const unsigned long long f = *(volatile const unsigned long long *)fresh;
+    __hip_atomic_store(&host[1], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+    __hip_atomic_store(&host[0], ord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// k_pp_walk: one lane per distinct key of the grouped sub-ranges (PKeyRecs), no LDS, register-lean
+// so that several waves per SIMD hide the key's memory round trips (slot probe / insert, window, rule
+// fields): the ClusterParamFlowChecker state machine over the key's run (pd_walk).
+template <int NMAX>
+__global__ __launch_bounds__(256) void k_pp_walk(PKeyRecs RC, const uint64_t *__restrict__ gval,
+                                                  const ParamEvent *__restrict__ ev, ParamRules PR,
+                                                  const PRuleRec *__restrict__ RR, PSlots S,
+                                                  uint64_t *__restrict__ out, unsigned long long *fresh) {
+    __shared__ uint32_t s_fresh;
+    if (threadIdx.x == 0) s_fresh = 0;
+    __syncthreads();
+    const uint32_t nrec = *RC.count;
+    const int64_t T0 = pp_t0(ev);
+    uint32_t nfresh = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nrec; i += gridDim.x * blockDim.x) {
+        const uint2 run = RC.run[i];
+        pd_walk<NMAX>(PR, RR, S, RC.key[i], RC.rule[i], gval, run.x, run.x + run.y, ev, T0, out, nfresh);
     }
     block_add_global(fresh, nfresh, &s_fresh);
 }

@@ -73,7 +73,16 @@ struct SlotMeta {
     double *thr;
     uint8_t *kind;
     int32_t *rule;        // the slot's rule (read by the slot-table rebuild and the top-values query)
+    int64_t *state;       // the slots' windows (stride words each): a fresh insert writes its n absent pairs
+    int64_t stride;
 };
+
+// A freshly inserted slot's window: n absent buckets (the table's state is not pre-initialised: a
+// rebuild only clears the keys, the inserting thread writes the window before any kernel reads it).
+__device__ inline void slot_state_init(int64_t *state, int64_t stride, uint64_t h, int n) {
+    int64_t *st = state + (int64_t)h * stride;
+    for (int j = 0; j < n; ++j) *reinterpret_cast<longlong2 *>(st + 2 * j) = longlong2{EPOCH_ABSENT, 0};
+}
 
 // Count-min sketch: rule-major [rule][depth][width][nmax] packed cells.
 struct CountMin {
@@ -189,11 +198,13 @@ __global__ __launch_bounds__(SORT_THREADS) void k_prule_prep(
         if (st == 127 && table) {
             for (int32_t q = 0; q < cnt; ++q) {
                 const uint64_t key = vs.value((int64_t)b + q);
+                const uint32_t before = nfresh;
                 const int64_t h = slot_insert_counted(table, cap_mask, key, nfresh);
                 if (h < 0) { st = ST_FAIL; break; }                    // table full
                 vslot[b + q] = (uint32_t)h;
                 if (!LOCAL) {   // identical values from every writer of this slot: stored only when they differ
                     const int32_t rn = R.n[e.idx], rw = R.w[e.idx];
+                    if (nfresh != before) slot_state_init(M.state, M.stride, (uint64_t)h, rn);
                     const double rc = R.rcp_w[e.idx], is = R.I_s[e.idx];
                     const double th = value_threshold(R, (uint32_t)e.idx, key);
                     if (M.rule[h] != e.idx) M.rule[h] = e.idx;
