@@ -16,9 +16,10 @@ already resident in HBM.
   5     Envoy RLS rules (SimpleClusterFlowChecker, n=1 / 1000 ms), hitsAddend ~ geometric(0.3) capped at
         64: heterogeneous acquire -> the sequential per-segment path
   5conc the thread-grade half of config 5: concurrency-token acquire / release batches
-        (ConcurrentClusterFlowChecker) on the device-pointer path
+        (ConcurrentClusterFlowChecker, sentinel_submit_concurrent_batch on device pointers): 20k
+        thread-grade rules, Zipf(1.1) flows, every batch releases the tokens the previous batch acquired
   3lim  config 3 with the namespace GlobalRequestLimiter on (the reference creates one per namespace
-        after any namespace-set change): the radix-sort path
+        after any namespace-set change): the limiter pass, then the partition path
 
 Prints ONE JSON line (rank 0).  Extra fields: p99 batch latency from >= 200 batches of an untimed
 latency loop (device events, and host clock with a synchronize per batch), per-kernel profile, the
@@ -57,6 +58,8 @@ KERNEL_BYTES_PER_EVENT = {
     "param_scatter": 44.0,    # read the 24-B event, write key 8 + packed value 8 + rule 4
     "param_meta": 48.0,       # per slot after a rule / threshold / table change: key 8, rule fields ~16, write ~20 B
     "prule_prep": 36.0,       # read the 24-B event + value 8, write key 4
+    "conc_prep": 32.0,        # read the 24-B event (+ a release's token probe 8), write flow key 4 (+ slot 4)
+    "conc_runs": 12.0,        # sorted keys read twice (heads, runs) + the flag written / scanned
 }
 
 # rocprofv3 kernel symbols behind each engine profile name (for the PMC traffic of the roofline).
@@ -67,7 +70,9 @@ KERNEL_SYMBOLS = {
     "part_fused": ("k_part_half",), "part_big": ("k_part_big",), "part_long": ("k_part_long",),
     "param_prep": ("k_param_prep", "k_pp_prep"), "param_meta": ("k_param_meta",), "prule_prep": ("k_prule_prep",),
     "prule_process": ("k_prule_process",), "part_unsplit": ("k_part_unsplit",), "lim_prep": ("k_lim1_prep",),
-    "param_scatter": ("k_pp_scatter",), "param_group": ("k_pp_group",), "param_decide": ("k_pp_walk", "k_pp_decide"),
+    "param_scatter": ("k_pp_scatter",), "param_group": ("k_pp_group",),
+    "conc_prep": ("k_conc_prep",), "conc_runs": ("k_conc_heads", "k_conc_runs"),
+    "conc_process": ("k_conc_process",), "conc_info": ("k_conc_info",), "conc_chunks": ("k_conc_chunks",), "param_decide": ("k_pp_walk", "k_pp_decide"),
 }
 PMC_DIR = os.path.join(ROOT, "profiles", "pmc")
 
@@ -159,7 +164,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="3", choices=["3", "2", "4", "4cm", "5", "3lim"])
+    ap.add_argument("--config", default="3", choices=["3", "2", "4", "4cm", "5", "5conc", "3lim"])
     ap.add_argument("--events-per-gpu", type=int, default=None)
     ap.add_argument("--flows", type=int, default=None)
     ap.add_argument("--sample-count", type=int, default=None)
@@ -453,6 +458,118 @@ class ParamWorkload:
         return {"config": self.args.config, "rules": self.R, "events": self.N, "sample_count": self.n}
 
 
+class ConcWorkload:
+    """Concurrency-token batches of config 5's thread-grade half (sentinel_concurrent_event_t): a fixed
+    pattern of acquire / release positions; batch s + 1 releases, at its release positions, the tokens
+    batch s handed out at its acquire positions (a client holding a token releases it one batch later;
+    blocked acquires hold no token, so their release answers ALREADY_RELEASE).  The release token ids
+    are gathered on the engine stream from the previous batch's results before each submit (part of
+    the timed step: it is the clients' traffic)."""
+
+    def __init__(self, args, world, rank, dev):
+        import torch
+        import sentinel_amd as sa
+        from sentinel_amd import trace as T
+        self.T, self.torch, self.dev, self.args = T, torch, dev, args
+        rng = np.random.default_rng(55)
+        flows = args.flows or 20_000
+        rules = T.make_rules(flows, rng, count_lo=50, count_hi=5000, sample_count=1, window_interval_ms=1000)
+        mine = np.nonzero(T.shard_of(rules.flow_id, world) == rank)[0] if world > 1 else np.arange(len(rules))
+        self.rules = rules.subset(mine)
+        self.F = len(self.rules)
+        self.N = args.events_per_gpu or 4 * 1024 * 1024
+        self.svc = sa.GpuTokenService(dev.index or 0)
+        r = self.rules
+        self.svc.load_rules_array(r.flow_id, r.count, r.threshold_type, r.sample_count, r.window_interval_ms,
+                                  r.namespace, r.checker)
+        N = self.N
+        # half of the positions acquire, the other half release the previous batch's acquires (a random
+        # pairing of the two position sets)
+        perm = rng.permutation(N)
+        self.acq_pos = np.sort(perm[: N // 2])
+        self.rel_pos = np.sort(perm[N // 2:])
+        src = rng.permutation(len(self.acq_pos))[: len(self.rel_pos)]
+        self.g = torch.Generator(device=dev).manual_seed(3000 + rank)
+        self.acq_pos_d = torch.from_numpy(self.acq_pos.astype(np.int64)).to(dev)
+        self.rel_pos_d = torch.from_numpy(self.rel_pos.astype(np.int64)).to(dev)
+        self.rel_src_d = torch.from_numpy(self.acq_pos[src].astype(np.int64)).to(dev)
+        w = 1.0 / np.power(np.arange(1, self.F + 1, dtype=np.float64), 1.1)
+        self.zipf_cdf = torch.from_numpy(np.cumsum(w) / w.sum()).to(dev)
+        self.zipf_perm = torch.from_numpy(np.random.default_rng(9).permutation(self.F).astype(np.int32)).to(dev)
+        self.results = [torch.zeros((N, 2), dtype=torch.int64, device=dev) for _ in range(2)]
+        self.k = 0
+        self.verdicts = self.results[0]
+        self.workload = (f"config5conc: {self.F} thread-grade cluster rules (ConcurrentClusterFlowChecker, count~U{{50..5000}}), "
+                         f"Zipf(1.1) flows, {N}-event batches of half acquires (1 token) and half releases of the "
+                         f"previous batch's tokens, device-pointer path")
+        self.kept = []
+
+    def batch(self, s):
+        torch, N = self.torch, self.N
+        u = torch.rand(N, dtype=torch.float64, device=self.dev, generator=self.g)
+        idx = self.zipf_perm[torch.clamp(torch.searchsorted(self.zipf_cdf, u, right=True), max=self.F - 1)]
+        kind = torch.zeros(N, dtype=torch.int32, device=self.dev)
+        kind[self.rel_pos_d] = 1
+        return self.svc.concurrent_events(idx, torch.ones(N, dtype=torch.int32, device=self.dev),
+                                          torch.zeros(N, dtype=torch.int64, device=self.dev), kind,
+                                          torch.ones(N, dtype=torch.int32, device=self.dev))
+
+    def span_ms(self):
+        return 0
+
+    def submit(self, b):
+        torch = self.torch
+        prev, cur = self.results[self.k % 2], self.results[(self.k + 1) % 2]
+        ext = torch.cuda.ExternalStream(self.svc.stream, device=self.dev)
+        with torch.cuda.stream(ext):                       # the releases name the previous batch's tokens
+            b[:, 1].index_copy_(0, self.rel_pos_d, prev[:, 0].index_select(0, self.rel_src_d))
+        self.svc.submit_concurrent_batch(b, results=cur)
+        self.verdicts = cur
+        self.k += 1
+        if len(self.kept) < 3:
+            self.svc.synchronize()
+            self.kept.append((b.clone(), cur.clone()))
+
+    def cpu_baseline(self, batches, k1, kmt, threads):
+        from oracle import oracle as O
+        r = self.rules
+        orc = O.TokenServiceOracle.from_arrays(r.flow_id, r.count, r.threshold_type, r.sample_count,
+                                               r.window_interval_ms, r.namespace, r.checker)
+        evs = []
+        for b, res in self.kept[:k1]:
+            e = b.cpu().numpy()
+            ev = np.zeros(len(e), dtype=orc.CONC_EVENT)
+            ev["flow_idx"] = (e[:, 0] & 0xFFFFFFFF).astype(np.int32)
+            ev["acquire"] = (e[:, 0] >> 32).astype(np.int32)
+            ev["token_id"] = e[:, 1]
+            ev["kind"] = (e[:, 2] & 0xFFFFFFFF).astype(np.int32)
+            ev["flags"] = (e[:, 2] >> 32).astype(np.int32)
+            evs.append((ev, res[:, 0].cpu().numpy()))
+        c0 = time.perf_counter()
+        m = 0
+        for ev, ids in evs:
+            orc.concurrent_replay(ev, ids)
+            m += len(ev)
+        cdt = time.perf_counter() - c0
+        return (m, cdt, 1, "sequential oracle replay (ConcurrentClusterFlowChecker, the engine's token ids)"), None
+
+    def bytes_of(self, dom, d, steps):
+        if dom in ("conc_process", "conc_chunks"):
+            # per event: sorted value 8 + event 24 read, result 16 written; per acquire that passes a
+            # token insert (probe 8 + record 24); per release its token record read 8 + tombstone 8
+            return 8 + 24 + 16 + 0.5 * 16 + 0.5 * 16
+        if dom == "radix_scatter":
+            passes = max(1, round(d["calls"] / max(1, steps)))
+            return (32.0 + 24.0 * (passes - 1)) / passes
+        return KERNEL_BYTES_PER_EVENT.get(dom)
+
+    def pipeline_bytes(self):
+        return 24.0 + 16.0 + 8.0 + 16.0
+
+    def shape(self):
+        return {"config": self.args.config, "flows": self.F, "events": self.N}
+
+
 def main():
     args = parse()
     import torch
@@ -466,7 +583,12 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    W = ParamWorkload(args, world, rank, dev) if args.config in ("4", "4cm") else FlowWorkload(args, world, rank, dev)
+    if args.config in ("4", "4cm"):
+        W = ParamWorkload(args, world, rank, dev)
+    elif args.config == "5conc":
+        W = ConcWorkload(args, world, rank, dev)
+    else:
+        W = FlowWorkload(args, world, rank, dev)
     svc, N = W.svc, W.N
     # warmup | untimed per-kernel profile pass (every kernel timed: the breakdown) | timed steps
     # (only the dominant kernel timed, two events per step: its live duration for the roofline)
@@ -602,7 +724,9 @@ def main():
     t_snap = int(lat_b[-1][-1, 1].item()) + 1
     torch.cuda.synchronize()
     ts0 = time.perf_counter()
-    if isinstance(W, FlowWorkload):
+    if isinstance(W, ConcWorkload):
+        ts0 = None                                       # (no windowed metrics: the snapshot is the flow configs')
+    elif isinstance(W, FlowWorkload):
         snap = torch.empty((W.F, 3), dtype=torch.int64, device=dev)
         svc.snapshot_device(t_snap, snap)
         svc.synchronize()
@@ -615,7 +739,7 @@ def main():
         if world > 1:
             SH.gather_param_snapshot(snap)
     torch.cuda.synchronize()
-    snap_ms = (time.perf_counter() - ts0) * 1000.0
+    snap_ms = None if ts0 is None else (time.perf_counter() - ts0) * 1000.0
 
     # PCIe-inclusive host paths (config 3 only; reported beside `value`, never as it)
     host_path = None

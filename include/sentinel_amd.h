@@ -460,6 +460,14 @@ typedef struct {
  * them from UUID.randomUUID(), TokenCacheNode.java:63). */
 int  sentinel_submit_concurrent_batch_host(sentinel_engine_t *eng, int64_t n, const sentinel_concurrent_event_t *events,
                                            sentinel_concurrent_result_t *results);
+/* The same on DEVICE pointers, asynchronous on `stream` (null: the engine's stream), like
+ * sentinel_submit_flow_batch: replaces a batch of TokenService.requestConcurrentToken /
+ * releaseConcurrentToken calls (TokenService.java:56,62; DefaultTokenService.java:64-83).  A release
+ * names a token issued by an earlier batch (token ids come back with the results); the first release
+ * of a token in a batch finds it, later ones answer ALREADY_RELEASE.  The token cache is kept below 3/4
+ * full from a host-side bound; a batch that could cross it synchronises and compacts the cache. */
+int  sentinel_submit_concurrent_batch(sentinel_engine_t *eng, int64_t n, const sentinel_concurrent_event_t *events,
+                                      sentinel_concurrent_result_t *results, void *stream);
 /* CurrentConcurrencyManager.get(flowId) of a loaded flow. */
 int  sentinel_concurrent_now_calls(sentinel_engine_t *eng, int32_t flow_idx, int32_t *now_calls);
 /* TokenCacheNodeManager.getSize(). */

@@ -46,7 +46,8 @@ EXPORTS = [
     "sentinel_submit_param_multi_batch", "sentinel_submit_param_multi_batch_host", "sentinel_set_param_mode",
     "sentinel_load_local_param_rules", "sentinel_submit_local_param_batch", "sentinel_submit_local_param_batch_host",
     "sentinel_local_param_state",
-    "sentinel_submit_concurrent_batch_host", "sentinel_concurrent_now_calls", "sentinel_concurrent_token_count",
+    "sentinel_submit_concurrent_batch_host", "sentinel_submit_concurrent_batch", "sentinel_concurrent_now_calls",
+    "sentinel_concurrent_token_count",
     "sentinel_concurrent_expire",
     "sentinel_load_local_resources", "sentinel_submit_local_entry_batch", "sentinel_submit_local_entry_batch_host",
     "sentinel_local_node_stats", "sentinel_set_occupy_timeout", "sentinel_profile_select", "sentinel_profile_gate", "sentinel_set_flow_path",
@@ -216,6 +217,7 @@ def load():
         "sentinel_submit_local_param_batch_host": (C.c_int, [vp, i64, vp, vp, i64, vp]),
         "sentinel_local_param_state": (C.c_int, [vp, u64, vp, vp]),
         "sentinel_submit_concurrent_batch_host": (C.c_int, [vp, i64, vp, vp]),
+        "sentinel_submit_concurrent_batch": (C.c_int, [vp, i64, vp, vp, vp]),
         "sentinel_concurrent_now_calls": (C.c_int, [vp, i32, vp]),
         "sentinel_concurrent_token_count": (C.c_int, [vp, vp]),
         "sentinel_concurrent_expire": (C.c_int, [vp, i64, vp]),

@@ -54,6 +54,41 @@ __device__ inline int64_t token_find(const TokenTable &T, uint64_t id) {
     return -1;
 }
 
+// Insert a fresh token id (never in the table): the first free slot on its probe path, a tombstone
+// included -- released tokens' slots are reused, so the cache does not fill up with tombstones under a
+// steady acquire / release churn (lookups skip tombstones and stop at an empty slot, which a reuse
+// never creates or removes).  `tomb` tells whether a tombstone was taken.
+__device__ inline int64_t token_insert(const TokenTable &T, uint64_t id, bool &tomb) {
+    uint64_t h = mix64(id) & T.mask;
+    for (uint64_t p = 0; p <= T.mask; ++p) {
+        const unsigned long long k = T.keys[h];
+        if (k == PKEY_EMPTY || k == TOKEN_TOMB) {
+            if (atomicCAS(&T.keys[h], k, (unsigned long long)id) == k) {
+                tomb = k == TOKEN_TOMB;
+                return (int64_t)h;
+            }
+            continue;                                     // lost the slot: look at it again
+        }
+        h = (h + 1) & T.mask;
+    }
+    return -1;
+}
+
+// Device compaction of the token cache into a fresh table (tombstones dropped, capacity possibly
+// larger): every live token re-placed with its record; counts = {live, 0}.
+__global__ __launch_bounds__(256) void k_tok_rebuild(TokenTable O, uint64_t ocap, TokenTable N) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ocap) return;
+    const unsigned long long k = O.keys[s];
+    if (k == PKEY_EMPTY || k == TOKEN_TOMB) return;
+    uint64_t h = mix64(k) & N.mask;
+    while (atomicCAS(&N.keys[h], (unsigned long long)PKEY_EMPTY, k) != PKEY_EMPTY) h = (h + 1) & N.mask;
+    N.flow_id[h] = O.flow_id[s];
+    N.flow_idx[h] = O.flow_idx[s];
+    N.acquire[h] = O.acquire[s];
+    atomicAdd(&N.counts[0], 1ull);
+}
+
 // Result record {token_id, status}: two 8-byte stores.
 __device__ inline void put_conc(uint64_t *out, uint32_t i, int64_t token, int status) {
     out[2 * (uint64_t)i] = (uint64_t)token;
@@ -61,11 +96,15 @@ __device__ inline void put_conc(uint64_t *out, uint32_t i, int64_t token, int st
 }
 
 // DefaultTokenService.requestConcurrentToken validation (DTS:64-75, 89-91) and release lookup;
-// sort key = flow index (acquire: the rule; release: the token's flow); pass-0 histograms.
+// sort key = flow index (acquire: the rule; release: the token's flow); pass-0 histograms.  A found
+// release records its token slot (relslot) and claims it with its arrival position (atomicMin): the
+// first release of a token in the batch is the one that finds it cached (CCFC:82-86), later ones of
+// the same token answer ALREADY_RELEASE.  Tokens issued in this batch are not yet known to any client.
 __global__ __launch_bounds__(SORT_THREADS) void k_conc_prep(int64_t n, const ConcEvent *__restrict__ ev, int32_t nflows,
                                                             TokenTable TT, uint64_t *__restrict__ out,
                                                             uint32_t *__restrict__ fkey, uint32_t finvalid,
-                                                            uint32_t *__restrict__ fhist, int64_t nblocks) {
+                                                            uint32_t *__restrict__ fhist, int64_t nblocks,
+                                                            uint32_t *__restrict__ relslot, uint32_t *__restrict__ claim) {
     __shared__ uint32_t hf[MAX_PASSES][RADIX];
     for (int d = threadIdx.x; d < MAX_PASSES * RADIX; d += SORT_THREADS) (&hf[0][0])[d] = 0;
     __syncthreads();
@@ -84,7 +123,11 @@ __global__ __launch_bounds__(SORT_THREADS) void k_conc_prep(int64_t n, const Con
             const int64_t h = token_find(TT, (uint64_t)e.token);             // CCFC:82-86
             if (h < 0) st = ST_ALREADY_RELEASE;
             else if (TT.flow_idx[h] < 0) st = ST_NO_RULE_EXISTS;             // CCFC:87-91
-            else k = (uint32_t)TT.flow_idx[h];
+            else {
+                k = (uint32_t)TT.flow_idx[h];
+                relslot[i] = (uint32_t)h;
+                atomicMin(&claim[h], (uint32_t)i);
+            }
         } else {
             st = ST_BAD_REQUEST;
         }
@@ -96,57 +139,505 @@ __global__ __launch_bounds__(SORT_THREADS) void k_conc_prep(int64_t n, const Con
     tile_hist_store(hf, fhist, 1, nblocks);
 }
 
-// One lane per flow: nowCalls in a register, the flow's acquires / releases in arrival order.
-__global__ __launch_bounds__(256) void k_conc_process(BatchWork W, const ConcEvent *__restrict__ ev,
-                                                      int32_t *__restrict__ now_calls, const double *__restrict__ thr,
-                                                      const int64_t *__restrict__ flow_ids, TokenTable TT,
-                                                      uint64_t id_base, uint64_t *__restrict__ out) {
-    const int64_t g0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t S = (int64_t)*W.nseg;
-    if (g0 >= S || (int64_t)*W.nvalid == 0) return;
-    const uint32_t flow = W.seg_key[g0];
-    if (g0 > 0 && W.seg_key[g0 - 1] == flow) return;
-    int32_t now = now_calls[flow];
-    const double threshold = thr[flow];
-    for (int64_t g = g0; g < S; ++g) {
-        if (g > g0 && W.seg_key[g] != flow) break;
-        const uint32_t end = W.seg_start[g + 1];
-        for (uint32_t i = W.seg_start[g]; i < end; ++i) {
-            const uint32_t seq = (uint32_t)W.sval[i] & SEQ_MASK;
-            const ConcEvent e = ev[seq];
-            if (e.kind == CONC_ACQUIRE) {
-                // CCFC:57-71: int + int (wraps) compared with the double threshold
-                if ((double)(int32_t)((uint32_t)now + (uint32_t)e.acquire) > threshold) {
-                    put_conc(out, seq, 0, ST_BLOCKED);
-                    continue;
-                }
-                const uint64_t id = id_base + seq;                            // TokenCacheNode.java:59-70
-                const int64_t h = slot_insert(TT.keys, TT.mask, id);
-                if (h < 0) {                                                 // token cache full
-                    put_conc(out, seq, 0, ST_FAIL);
-                    continue;
-                }
-                TT.flow_id[h] = flow_ids[flow];
-                TT.flow_idx[h] = (int32_t)flow;
-                TT.acquire[h] = e.acquire;
-                atomicAdd(&TT.counts[0], 1ull);
-                now = (int32_t)((uint32_t)now + (uint32_t)e.acquire);
-                put_conc(out, seq, (int64_t)id, ST_OK);
-            } else {
-                const int64_t h = token_find(TT, (uint64_t)e.token);         // CCFC:82-100
-                if (h < 0) {                                                 // released earlier in this batch
-                    put_conc(out, seq, 0, ST_ALREADY_RELEASE);
-                    continue;
-                }
-                TT.keys[h] = TOKEN_TOMB;
-                atomicAdd(&TT.counts[0], ~0ull);
-                atomicAdd(&TT.counts[1], 1ull);
-                now = (int32_t)((uint32_t)now - (uint32_t)TT.acquire[h]);
-                put_conc(out, seq, 0, ST_RELEASE_OK);
+// Flow runs of the sorted batch: head flags (a valid key differing from its predecessor), scanned by
+// the engine, then each head's run start; the last valid element publishes the valid count and the
+// number of runs.
+__global__ __launch_bounds__(256) void k_conc_heads(const uint32_t *__restrict__ skey, int64_t n, uint32_t invalid,
+                                                    uint32_t *__restrict__ flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = skey[i];
+    flag[i] = (k != invalid && (i == 0 || skey[i - 1] != k)) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(256) void k_conc_runs(const uint32_t *__restrict__ skey, int64_t n, uint32_t invalid,
+                                                   const uint32_t *__restrict__ pos, uint32_t *__restrict__ run_start,
+                                                   uint32_t *__restrict__ ctl) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = skey[i];
+    if (k == invalid) return;
+    const bool head = i == 0 || skey[i - 1] != k;
+    if (head) run_start[pos[i]] = (uint32_t)i;
+    if (i + 1 == n || skey[i + 1] == invalid) {          // the last valid element
+        const uint32_t nruns = pos[i] + (head ? 1u : 0u);
+        run_start[nruns] = (uint32_t)(i + 1);
+        ctl[0] = nruns;
+    }
+}
+
+// One event of a flow's run decided by the reference state machine (CCFC:48-101), `now` in a register.
+struct ConcCtx {
+    const ConcEvent *ev;
+    const uint64_t *sval;
+    const uint32_t *relslot;
+    uint32_t *claim;
+    TokenTable TT;
+    const int64_t *flow_ids;
+    uint64_t id_base;
+    uint64_t *out;
+#ifdef SENTINEL_CONC_TRACE
+    uint64_t *trace;
+#endif
+};
+
+__device__ inline void conc_seq_event(const ConcCtx &C, uint32_t flow, double threshold, int32_t &now, uint32_t i,
+                                      int64_t &dlive, int64_t &dtomb) {
+    const uint32_t seq = (uint32_t)C.sval[i] & SEQ_MASK;
+    const ConcEvent e = C.ev[seq];
+    if (e.kind == CONC_ACQUIRE) {
+        // CCFC:57-71: int + int (wraps) compared with the double threshold
+        if ((double)(int32_t)((uint32_t)now + (uint32_t)e.acquire) > threshold) {
+            put_conc(C.out, seq, 0, ST_BLOCKED);
+            return;
+        }
+        const uint64_t id = C.id_base + seq;                                  // TokenCacheNode.java:59-70
+        bool tomb = false;
+        const int64_t h = token_insert(C.TT, id, tomb);
+        if (h < 0) {                                                          // token cache full
+            put_conc(C.out, seq, 0, ST_FAIL);
+            return;
+        }
+        if (tomb) --dtomb;
+        C.TT.flow_id[h] = C.flow_ids[flow];
+        C.TT.flow_idx[h] = (int32_t)flow;
+        C.TT.acquire[h] = e.acquire;
+        ++dlive;
+        now = (int32_t)((uint32_t)now + (uint32_t)e.acquire);
+        put_conc(C.out, seq, (int64_t)id, ST_OK);
+    } else {
+        const uint32_t h = C.relslot[seq];
+        if (C.claim[h] != seq) {                                              // an earlier release took it
+            put_conc(C.out, seq, 0, ST_ALREADY_RELEASE);
+            return;
+        }
+        C.claim[h] = ~0u;
+        C.TT.keys[h] = TOKEN_TOMB;                                            // CCFC:92-100
+        --dlive;
+        ++dtomb;
+        now = (int32_t)((uint32_t)now - (uint32_t)C.TT.acquire[h]);
+        put_conc(C.out, seq, 0, ST_RELEASE_OK);
+    }
+}
+
+// The effect of one decided scan element: a passing unit acquire takes a token, a failing one answers
+// BLOCKED; a release that found its token frees it; anything else is ALREADY_RELEASE.
+__device__ inline void conc_apply_item(const ConcCtx &C, uint32_t flow, int kind, bool pass, uint32_t seq, uint32_t h,
+                                       int32_t amount, int64_t &dlive, int64_t &dtomb) {
+    if (kind == 0) {
+        if (!pass) {
+            put_conc(C.out, seq, 0, ST_BLOCKED);
+            return;
+        }
+        const uint64_t id = C.id_base + seq;
+        bool tomb = false;
+        const int64_t hs = token_insert(C.TT, id, tomb);
+        if (hs < 0) {
+            put_conc(C.out, seq, 0, ST_FAIL);
+            return;
+        }
+        if (tomb) --dtomb;
+        C.TT.flow_id[hs] = C.flow_ids[flow];
+        C.TT.flow_idx[hs] = (int32_t)flow;
+        C.TT.acquire[hs] = amount;
+        ++dlive;
+        put_conc(C.out, seq, (int64_t)id, ST_OK);
+    } else if (kind == 1) {
+        C.claim[h] = ~0u;
+        C.TT.keys[h] = TOKEN_TOMB;
+        --dlive;
+        ++dtomb;
+        put_conc(C.out, seq, 0, ST_RELEASE_OK);
+    } else {
+        put_conc(C.out, seq, 0, ST_ALREADY_RELEASE);
+    }
+}
+
+constexpr uint32_t CONC_LANE_RUN = 64;      // longer runs are decided in chunks by workgroups
+constexpr uint32_t CONC_CHUNK = 1024;       // events of a long run per workgroup step (4 per thread)
+
+// The greedy admission of unit acquires with releases interleaved is a (min, +) recurrence: while the
+// in-flight count y is <= the largest admissible T' (the largest y with !((double)(y + 1) > threshold),
+// minus one), an acquire maps y to min(y + 1, T') (it passes iff y < T') and a release of r tokens maps
+// y to y - r.  Both are x -> min(x + P, C); composition (P1, C1) then (P2, C2) = (P1 + P2,
+// min(C1 + P2, C2)) is associative, so the chunks of one long run are decided in parallel with a
+// decoupled look-back over their compositions.
+constexpr int64_t CONC_INF = (int64_t)1 << 60;
+struct MinPlus { int64_t p, c; };
+__device__ inline MinPlus mp_then(MinPlus a, MinPlus b) {
+    const int64_t ac = a.c >= CONC_INF ? CONC_INF : a.c + b.p;
+    return MinPlus{a.p + b.p, ac < b.c ? ac : b.c};
+}
+__device__ inline int64_t mp_apply(MinPlus f, int64_t y) { return f.c >= CONC_INF ? y + f.p : min(y + f.p, f.c); }
+
+__device__ inline int64_t conc_tprime(double threshold) {
+    if (threshold != threshold || threshold >= (double)(CONC_INF / 4)) return CONC_INF / 4;   // NaN: never >
+    if (threshold <= -(double)(CONC_INF / 4)) return -(CONC_INF / 4);
+    return (int64_t)floor(threshold);
+}
+
+constexpr int CB_THREADS = 256;
+constexpr int CB_WAVES = CB_THREADS / WAVE;
+
+// Inclusive block scan of MinPlus over the 256 threads (wave shuffles, then the waves' totals, which
+// stay in lds[] for the caller).
+__device__ inline MinPlus mp_block_inclusive(MinPlus v, MinPlus *lds) {
+    const uint32_t lane = lane_id();
+    const int wave = threadIdx.x / WAVE;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const int64_t pp = __shfl_up(v.p, o, WAVE);
+        const int64_t pc = __shfl_up(v.c, o, WAVE);
+        if ((int)lane >= o) v = mp_then(MinPlus{pp, pc}, v);
+    }
+    if (lane == WAVE - 1) lds[wave] = v;
+    __syncthreads();
+    MinPlus pre{0, CONC_INF};
+    for (int w = 0; w < wave; ++w) pre = mp_then(pre, lds[w]);
+    __syncthreads();
+    return mp_then(pre, v);
+}
+// ... and the exclusive value of this thread (the previous thread's inclusive one)
+__device__ inline MinPlus mp_block_exclusive_of(MinPlus inc, const MinPlus *lds) {
+    const uint32_t lane = lane_id();
+    const int wave = threadIdx.x / WAVE;
+    const int64_t pp = __shfl_up(inc.p, 1, WAVE), pc = __shfl_up(inc.c, 1, WAVE);
+    MinPlus ex{pp, pc};
+    if (lane == 0) {
+        ex = MinPlus{0, CONC_INF};
+        for (int w = 0; w < wave; ++w) ex = mp_then(ex, lds[w]);
+    }
+    return ex;
+}
+
+// Long runs of a batch: per run slot its run, nowCalls before the batch, T', whether every acquire
+// asks for one token and the sum of |amounts| (the scan's eligibility); per chunk its slot, its index
+// in the run and the look-back status {epoch << 2 | 1 aggregate / 2 inclusive, composition}.
+struct ConcBig {
+    uint32_t *run;
+    int32_t *now0;
+    int64_t *tp;
+    uint32_t *unit;
+    unsigned long long *mag;
+    uint2 *chunks;           // [slot] {first chunk, chunk count}
+    uint32_t *chunk_slot;
+    uint32_t *chunk_j;
+    uint32_t *flag;
+    MinPlus *agg;
+    MinPlus *inc;
+    uint32_t *ctl;           // [0] runs, [1] long runs, [2] chunks, [3] chunk ticket
+    uint32_t epoch;
+};
+
+// One lane per flow run of <= CONC_LANE_RUN events: the run in arrival order; longer runs are cut into
+// chunks for k_conc_chunks.
+__global__ __launch_bounds__(256) void k_conc_process(ConcCtx C, const uint32_t *__restrict__ run_start,
+                                                      const uint32_t *__restrict__ skey, int32_t *__restrict__ now_calls,
+                                                      const double *__restrict__ thr, ConcBig G) {
+    __shared__ unsigned long long s_cnt[2];
+    if (threadIdx.x < 2) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t dlive = 0, dtomb = 0;
+    if (r < G.ctl[0]) {
+        const uint32_t b = run_start[r], e = run_start[r + 1];
+        const uint32_t flow = skey[b];
+        if (e - b > CONC_LANE_RUN) {
+            const uint32_t slot = atomicAdd(&G.ctl[1], 1u);
+            const uint32_t nch = (e - b + CONC_CHUNK - 1) / CONC_CHUNK;
+            const uint32_t first = atomicAdd(&G.ctl[2], nch);
+            G.run[slot] = r;
+            G.now0[slot] = now_calls[flow];
+            G.tp[slot] = conc_tprime(thr[flow]);
+            G.unit[slot] = 1u;
+            G.mag[slot] = 0ull;
+            G.chunks[slot] = make_uint2(first, nch);
+            for (uint32_t j = 0; j < nch; ++j) {
+                G.chunk_slot[first + j] = slot;
+                G.chunk_j[first + j] = j;
             }
+        } else {
+            int32_t now = now_calls[flow];
+            const double threshold = thr[flow];
+            for (uint32_t i = b; i < e; ++i) conc_seq_event(C, flow, threshold, now, i, dlive, dtomb);
+            now_calls[flow] = now;
         }
     }
-    now_calls[flow] = now;
+    if (dlive) atomicAdd(&s_cnt[0], (unsigned long long)dlive);
+    if (dtomb) atomicAdd(&s_cnt[1], (unsigned long long)dtomb);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (s_cnt[0]) atomicAdd(&C.TT.counts[0], (unsigned long long)s_cnt[0]);
+        if (s_cnt[1]) atomicAdd(&C.TT.counts[1], (unsigned long long)s_cnt[1]);
+    }
+}
+
+// Event i of a long run as a scan element: kind 0 acquire, 1 release that finds its token (its
+// amount), 2 neither (a later release of a token already released in this batch).
+__device__ inline void conc_item(const ConcCtx &C, uint32_t i, int &kind, int32_t &amt, uint32_t &seq, uint32_t &h) {
+    seq = (uint32_t)C.sval[i] & SEQ_MASK;
+    const ConcEvent ev = C.ev[seq];
+    kind = 2;
+    amt = 0;
+    h = 0;
+    if (ev.kind == CONC_ACQUIRE) {
+        kind = 0;
+        amt = ev.acquire;
+    } else {
+        h = C.relslot[seq];
+        if (C.claim[h] == seq) { kind = 1; amt = C.TT.acquire[h]; }
+    }
+}
+
+// Eligibility of the long runs for the scan: every acquire of 1 token, and the int sums cannot wrap.
+__global__ __launch_bounds__(256) void k_conc_info(ConcCtx C, const uint32_t *__restrict__ run_start, ConcBig G) {
+    const uint32_t nch = G.ctl[2];
+    for (uint32_t c = blockIdx.x; c < nch; c += gridDim.x) {
+        const uint32_t slot = G.chunk_slot[c], j = G.chunk_j[c];
+        const uint32_t r = G.run[slot];
+        const uint32_t b = run_start[r] + j * CONC_CHUNK, e = min(run_start[r + 1], b + CONC_CHUNK);
+        bool unit = true;
+        unsigned long long mag = 0;
+        for (uint32_t i = b + threadIdx.x; i < e; i += blockDim.x) {
+            int kind;
+            int32_t amt;
+            uint32_t seq, h;
+            conc_item(C, i, kind, amt, seq, h);
+            if (kind == 0 && amt != 1) unit = false;
+            if (kind != 2) mag += (unsigned long long)(amt < 0 ? -(int64_t)amt : (int64_t)amt);
+        }
+        if (!unit) atomicAnd(&G.unit[slot], 0u);
+        if (mag) atomicAdd(&G.mag[slot], mag);
+    }
+}
+
+// A long run that cannot take the scan (an acquire of several tokens, an int sum that could wrap, or
+// nowCalls above T' when the batch starts): one workgroup walks it in 256-event chunks -- a chunk of
+// unit acquires whose sums cannot wrap by the scan (phase A: while y > T' only releases move y; phase
+// B: the (min, +) scan), any other chunk by thread 0 with the state machine.
+__device__ inline void conc_run_serial(const ConcCtx &C, uint32_t b, uint32_t e, uint32_t flow, double threshold,
+                                       int32_t *now_calls, MinPlus *s_mp, int64_t *s_red, int64_t *s_y0,
+                                       int32_t *s_now, int64_t &dlive, int64_t &dtomb) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t lane = lane_id();
+    const int wave = t / WAVE;
+    const int64_t Tp = conc_tprime(threshold);
+    if (t == 0) *s_now = now_calls[flow];
+    __syncthreads();
+    for (uint32_t c0 = b; c0 < e; c0 += CB_THREADS) {
+        const uint32_t i = c0 + t;
+        const bool act = i < e;
+        int kind = 2;
+        int32_t amt = 0;
+        uint32_t seq = 0, h = 0;
+        if (act) conc_item(C, i, kind, amt, seq, h);
+        const int64_t x = *s_now;
+        const bool unit = __syncthreads_and(kind != 0 || amt == 1);
+        int64_t mag = kind == 2 ? 0 : (amt < 0 ? -(int64_t)amt : (int64_t)amt);
+#pragma unroll
+        for (int o = WAVE / 2; o >= 1; o >>= 1) mag += __shfl_xor(mag, o, WAVE);
+        if (lane == 0) s_red[wave] = mag;
+        __syncthreads();
+        int64_t tot = 0;
+        for (int q = 0; q < CB_WAVES; ++q) tot += s_red[q];
+        __syncthreads();
+        if (!(unit && (x < 0 ? -x : x) + tot < (int64_t)INT32_MAX)) {         // block-uniform
+            if (t == 0) {
+                int32_t now = (int32_t)x;
+                const uint32_t c1 = min(e, c0 + CB_THREADS);
+                for (uint32_t q = c0; q < c1; ++q) conc_seq_event(C, flow, threshold, now, q, dlive, dtomb);
+                *s_now = now;
+            }
+            __syncthreads();
+            continue;
+        }
+        uint32_t first = 0;                               // first lane of phase B
+        bool never = false;                               // y stays > T' through the chunk
+        if (x > Tp) {                                     // phase A (block-uniform)
+            const MinPlus racc = mp_block_inclusive(MinPlus{kind == 1 ? -(int64_t)amt : 0, CONC_INF}, s_mp);
+            const bool reach = act && x + racc.p <= Tp;
+            const uint64_t bal = __builtin_amdgcn_ballot_w64(reach);
+            if (lane == 0) s_red[wave] = bal ? (int64_t)(wave * WAVE + __ffsll((unsigned long long)bal) - 1) : (int64_t)CB_THREADS;
+            __syncthreads();
+            int64_t k = CB_THREADS;
+            for (int q = 0; q < CB_WAVES; ++q) k = s_red[q] < k ? s_red[q] : k;
+            if (k >= CB_THREADS) {
+                never = true;
+                if (t == CB_THREADS - 1) *s_y0 = x + racc.p;                   // every release applied
+            } else if ((int64_t)t == k) {
+                *s_y0 = x + racc.p;
+            }
+            __syncthreads();
+            first = (uint32_t)(k + 1);
+        } else if (t == 0) {
+            *s_y0 = x;
+        }
+        __syncthreads();
+        const int64_t y0 = *s_y0;
+        bool pass = false;
+        if (!never) {                                     // phase B (block-uniform)
+            MinPlus el{0, CONC_INF};
+            if (t >= first && act) {
+                if (kind == 0) el = MinPlus{1, Tp};
+                else if (kind == 1) el = MinPlus{-(int64_t)amt, CONC_INF};
+            }
+            const MinPlus inc = mp_block_inclusive(el, s_mp);
+            const MinPlus exl = mp_block_exclusive_of(inc, s_mp);
+            pass = kind == 0 && t >= first && act && mp_apply(exl, y0) < Tp;
+            if (t == CB_THREADS - 1) *s_now = (int32_t)mp_apply(inc, y0);
+        } else if (t == 0) {
+            *s_now = (int32_t)y0;
+        }
+        if (act) conc_apply_item(C, flow, kind, pass, seq, h, 1, dlive, dtomb);
+        __syncthreads();
+    }
+    if (t == 0) now_calls[flow] = *s_now;
+}
+
+// Chunks of long runs, one workgroup step each, taken in ticket order (a chunk's predecessors in its
+// run were taken earlier, so the look-back always completes).  An eligible run's chunk composes its
+// 1024 events (4 consecutive per thread), publishes the composition, looks back over its run's
+// earlier chunks for the prefix and decides its events from y = prefix(nowCalls); the run's last chunk
+// writes nowCalls.  An ineligible run is walked whole by the workgroup that takes its first chunk.
+__global__ __launch_bounds__(CB_THREADS) void k_conc_chunks(ConcCtx C, const uint32_t *__restrict__ run_start,
+                                                            const uint32_t *__restrict__ skey, int32_t *__restrict__ now_calls,
+                                                            const double *__restrict__ thr, ConcBig G) {
+    __shared__ MinPlus s_mp[CB_WAVES];
+    __shared__ int64_t s_red[CB_WAVES];
+    __shared__ int64_t s_y0;
+    __shared__ int32_t s_now;
+    __shared__ uint32_t s_ticket;
+    __shared__ MinPlus s_prefix;
+    __shared__ unsigned long long s_cnt[2];
+    const uint32_t t = threadIdx.x;
+    if (t < 2) s_cnt[t] = 0;
+    int64_t dlive = 0, dtomb = 0;
+    const uint32_t nch = G.ctl[2];
+    for (;;) {
+        if (t == 0) s_ticket = atomicAdd(&G.ctl[3], 1u);
+        __syncthreads();
+        const uint32_t c = s_ticket;
+        __syncthreads();
+        if (c >= nch) break;
+        const uint32_t slot = G.chunk_slot[c], j = G.chunk_j[c];
+        const uint32_t r = G.run[slot];
+        const uint32_t rb = run_start[r], re = run_start[r + 1];
+        const uint32_t flow = skey[rb];
+        const int64_t now0 = G.now0[slot];
+        const int64_t Tp = G.tp[slot];
+#ifdef SENTINEL_CONC_NOSCAN
+        const bool ok = false;
+#else
+        const bool ok = G.unit[slot] && (now0 < 0 ? -now0 : now0) + (int64_t)G.mag[slot] < (int64_t)INT32_MAX && now0 <= Tp;
+#endif
+        if (!ok) {                                        // block-uniform
+            if (j == 0) conc_run_serial(C, rb, re, flow, thr[flow], now_calls, s_mp, s_red, &s_y0, &s_now, dlive, dtomb);
+            continue;
+        }
+        const uint32_t b = rb + j * CONC_CHUNK;
+        int kind[4] = {2, 2, 2, 2};
+        int32_t amt[4] = {0, 0, 0, 0};
+        MinPlus mine{0, CONC_INF};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = b + t * 4 + q;
+            if (i < re) {
+                int k2;
+                int32_t a2;
+                uint32_t s2, h2;
+                conc_item(C, i, k2, a2, s2, h2);
+                kind[q] = k2;
+                amt[q] = a2;
+            }
+            const MinPlus el = kind[q] == 0 ? MinPlus{1, Tp} : kind[q] == 1 ? MinPlus{-(int64_t)amt[q], CONC_INF}
+                                                                           : MinPlus{0, CONC_INF};
+            mine = mp_then(mine, el);
+        }
+        const MinPlus inc = mp_block_inclusive(mine, s_mp);
+        const MinPlus exl = mp_block_exclusive_of(inc, s_mp);
+        // the chunk's composition: published by thread 255, then the last wave looks back over the run's
+        // earlier chunks 64 at a time (each lane waits for one chunk's flag; the window is composed
+        // earliest first up to the nearest inclusive prefix)
+        const uint32_t cf = G.chunks[slot].x;
+        if (t == CB_THREADS - 1) {
+            if (j == 0) {
+                G.inc[c] = inc;
+                __threadfence();
+                __hip_atomic_store(&G.flag[c], (G.epoch << 2) | 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_prefix = MinPlus{0, CONC_INF};
+            } else {
+                G.agg[c] = inc;
+                __threadfence();
+                __hip_atomic_store(&G.flag[c], (G.epoch << 2) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (j > 0 && t >= CB_THREADS - WAVE) {                               // last wave (block-uniform j)
+            const uint32_t lane = t - (CB_THREADS - WAVE);
+            MinPlus pre{0, CONC_INF};                                        // chunks between the window and c
+            uint32_t top = c;                                                // the window ends below top
+            for (;;) {
+                const int64_t p = (int64_t)top - 1 - lane;                   // lane 0: the nearest chunk
+                uint32_t f = 0;
+                MinPlus v{0, CONC_INF};
+                if (p >= (int64_t)cf) {
+                    do {
+                        f = __hip_atomic_load(&G.flag[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    } while ((f >> 2) != G.epoch || (f & 3u) == 0);
+                    __threadfence();
+                    v = (f & 3u) == 2u ? G.inc[p] : G.agg[p];
+                }
+                const uint64_t incl = __builtin_amdgcn_ballot_w64(p >= (int64_t)cf && (f & 3u) == 2u);
+                const uint32_t valid = (uint32_t)min<int64_t>(WAVE, (int64_t)top - (int64_t)cf);
+                const uint32_t last = incl ? (uint32_t)(__ffsll((unsigned long long)incl) - 1) : valid - 1;
+                // compose lanes last .. 0 (earliest first): a shuffle chain in lane 0
+                MinPlus w{0, CONC_INF};
+                for (int l = (int)last; l >= 0; --l) {
+                    const int64_t pp = __shfl(v.p, l, WAVE), pc = __shfl(v.c, l, WAVE);
+                    w = mp_then(w, MinPlus{pp, pc});
+                }
+                pre = mp_then(w, pre);
+                if (incl || top - cf <= (uint32_t)WAVE) break;               // reached an inclusive prefix / chunk cf
+                top -= WAVE;
+            }
+            if (lane == WAVE - 1) {                                          // thread 255
+                s_prefix = pre;
+                const MinPlus acc = mp_then(pre, inc);
+                G.inc[c] = acc;
+                __threadfence();
+                __hip_atomic_store(&G.flag[c], (G.epoch << 2) | 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (j + 1 == G.chunks[slot].y) now_calls[flow] = (int32_t)mp_apply(acc, now0);
+            }
+        } else if (j == 0 && t == CB_THREADS - 1 && j + 1 == G.chunks[slot].y) {
+            now_calls[flow] = (int32_t)mp_apply(inc, now0);
+        }
+        __syncthreads();
+        int64_t y = mp_apply(mp_then(s_prefix, exl), now0);   // before this thread's first event
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = b + t * 4 + q;
+            if (i < re) {
+                // (the event's position and token slot re-read here: carried in registers from the load
+                // loop above, the kind-2 results of a chunk were measured landing at position 0)
+                const uint32_t sq = (uint32_t)C.sval[i] & SEQ_MASK;
+                const uint32_t hq = kind[q] == 1 ? C.relslot[sq] : 0u;
+#ifdef SENTINEL_CONC_TRACE
+                C.trace[i] = ((uint64_t)(uint32_t)kind[q] << 32) | sq | ((uint64_t)t << 40);
+#endif
+                const bool pass = kind[q] == 0 && y < Tp;
+                if (kind[q] == 0) y = min(y + 1, Tp);
+                else if (kind[q] == 1) y -= amt[q];
+                conc_apply_item(C, flow, kind[q], pass, sq, hq, 1, dlive, dtomb);
+            }
+        }
+        __syncthreads();
+    }
+    if (dlive) atomicAdd(&s_cnt[0], (unsigned long long)dlive);
+    if (dtomb) atomicAdd(&s_cnt[1], (unsigned long long)dtomb);
+    __syncthreads();
+    if (t == 0) {
+        if (s_cnt[0]) atomicAdd(&C.TT.counts[0], (unsigned long long)s_cnt[0]);
+        if (s_cnt[1]) atomicAdd(&C.TT.counts[1], (unsigned long long)s_cnt[1]);
+    }
 }
 
 // RegularExpireStrategy.clearToken (RegularExpireStrategy.java:94-124): with the reference's own

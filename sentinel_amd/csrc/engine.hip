@@ -666,6 +666,11 @@ struct sentinel_engine {
     // concurrency tokens (ConcurrentClusterFlowChecker): nowCalls per flow, token cache in HBM
     DevBuf d_now, d_conc_thr, d_seg1_w, d_seg1_rcp, d_seg1_kind;
     DevBuf d_tok_keys, d_tok_fid, d_tok_fidx, d_tok_acq, d_tok_counts, d_tok_ticket;
+    DevBuf d_tok_claim;                // per token slot: the first release of it in the batch (~0 between batches)
+    DevBuf w_cbig;                     // long concurrency runs: slots + chunks (look-back flags zeroed on allocation)
+    int64_t cbig_n = 0;
+    uint32_t conc_epoch = 0;
+    uint64_t tok_ub = 0;               // upper bound of live + tombstoned token slots (no device read per batch)
     uint64_t tcap = (uint64_t)1 << 22;
     uint64_t tok_salt = 0, tok_counter = 1;
 
@@ -1074,7 +1079,9 @@ struct sentinel_engine {
     }
     int rebuild_cm();
     int ensure_tokens();
-    int rewrite_tokens(bool compact);
+    int rewrite_tokens(bool compact, uint64_t new_cap = 0);
+    int rebuild_tokens_device(uint64_t new_cap, hipStream_t s);
+    DevBuf sp_tok_keys, sp_tok_fid, sp_tok_fidx, sp_tok_acq, sp_tok_claim;   // the next compaction's target
     TokenTable token_table() {
         return TokenTable{d_tok_keys.as<unsigned long long>(), d_tok_fid.as<int64_t>(), d_tok_fidx.as<int32_t>(),
                           d_tok_acq.as<int32_t>(), tcap - 1, d_tok_counts.as<unsigned long long>()};
@@ -1096,8 +1103,11 @@ int sentinel_engine::ensure_tokens() {
     rc |= d_tok_acq.ensure(tcap * 4);
     rc |= d_tok_counts.ensure(16);
     rc |= d_tok_ticket.ensure(8);
+    rc |= d_tok_claim.ensure(tcap * 4);
     if (rc) return SENTINEL_E_NOMEM;
     HIP_OK(hipMemsetAsync(d_tok_keys.p, 0xFF, tcap * 8, stream));
+    HIP_OK(hipMemsetAsync(d_tok_claim.p, 0xFF, tcap * 4, stream));
+    tok_ub = 0;
     HIP_OK(hipMemsetAsync(d_tok_counts.p, 0, 16, stream));
     HIP_OK(hipStreamSynchronize(stream));
     std::random_device rd;                 // token ids: {salt:23 | counter:40}, opaque to clients like UUID bits
@@ -1108,19 +1118,33 @@ int sentinel_engine::ensure_tokens() {
 // Host rewrite of the token cache: remap every live token's flow index from its flowId (after a
 // rule load: tokens of removed flows answer NO_RULE_EXISTS until the flowId comes back), and
 // optionally drop tombstones by re-inserting the live tokens into a fresh table.
-int sentinel_engine::rewrite_tokens(bool compact) {
+int sentinel_engine::rewrite_tokens(bool compact, uint64_t new_cap) {
     if (!d_tok_keys.p) return 0;
-    std::vector<uint64_t> keys(tcap);
-    std::vector<int64_t> fid(tcap);
-    std::vector<int32_t> acq(tcap);
-    HIP_OK(hipMemcpy(keys.data(), d_tok_keys.p, tcap * 8, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(fid.data(), d_tok_fid.p, tcap * 8, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(acq.data(), d_tok_acq.p, tcap * 4, hipMemcpyDeviceToHost));
+    const uint64_t ocap = tcap;
+    const uint64_t ncap = new_cap > ocap ? new_cap : ocap;   // growing re-places every token
+    if (ncap != ocap) compact = true;
+    std::vector<uint64_t> keys(ocap);
+    std::vector<int64_t> fid(ocap);
+    std::vector<int32_t> acq(ocap);
+    HIP_OK(hipMemcpy(keys.data(), d_tok_keys.p, ocap * 8, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(fid.data(), d_tok_fid.p, ocap * 8, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(acq.data(), d_tok_acq.p, ocap * 4, hipMemcpyDeviceToHost));
+    if (ncap != ocap) {
+        for (DevBuf *b : {&d_tok_keys, &d_tok_fid, &d_tok_fidx, &d_tok_acq, &d_tok_claim}) b->release();
+        int rc = d_tok_keys.ensure(ncap * 8);
+        rc |= d_tok_fid.ensure(ncap * 8);
+        rc |= d_tok_fidx.ensure(ncap * 4);
+        rc |= d_tok_acq.ensure(ncap * 4);
+        rc |= d_tok_claim.ensure(ncap * 4);
+        if (rc) return SENTINEL_E_NOMEM;
+        HIP_OK(hipMemset(d_tok_claim.p, 0xFF, ncap * 4));
+        tcap = ncap;
+    }
     std::vector<uint64_t> nk(tcap, PKEY_EMPTY);
     std::vector<int64_t> nf(tcap, 0);
     std::vector<int32_t> nx(tcap, -1), na(tcap, 0);
     uint64_t live = 0, dead = 0;
-    for (uint64_t h = 0; h < tcap; ++h) {
+    for (uint64_t h = 0; h < ocap; ++h) {
         if (keys[h] == PKEY_EMPTY) continue;
         if (keys[h] == TOKEN_TOMB) {
             if (!compact) { nk[h] = TOKEN_TOMB; ++dead; }
@@ -1139,11 +1163,40 @@ int sentinel_engine::rewrite_tokens(bool compact) {
         ++live;
     }
     const unsigned long long counts[2] = {live, dead};
+    tok_ub = live + dead;
     HIP_OK(hipMemcpy(d_tok_keys.p, nk.data(), tcap * 8, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(d_tok_fid.p, nf.data(), tcap * 8, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(d_tok_fidx.p, nx.data(), tcap * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(d_tok_acq.p, na.data(), tcap * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(d_tok_counts.p, counts, 16, hipMemcpyHostToDevice));
+    return 0;
+}
+
+// Token cache compaction on the device (no host copy): the live tokens move into the spare buffers
+// (re-sized to new_cap), which then become the cache; stream-ordered, no synchronisation.
+int sentinel_engine::rebuild_tokens_device(uint64_t new_cap, hipStream_t s) {
+    const uint64_t ocap = tcap, ncap = std::max(new_cap, ocap);
+    int rc = 0;
+    rc |= sp_tok_keys.ensure(ncap * 8);
+    rc |= sp_tok_fid.ensure(ncap * 8);
+    rc |= sp_tok_fidx.ensure(ncap * 4);
+    rc |= sp_tok_acq.ensure(ncap * 4);
+    rc |= sp_tok_claim.ensure(ncap * 4);
+    if (rc) return SENTINEL_E_NOMEM;
+    HIP_OK(hipMemsetAsync(sp_tok_keys.p, 0xFF, ncap * 8, s));
+    HIP_OK(hipMemsetAsync(sp_tok_claim.p, 0xFF, ncap * 4, s));
+    HIP_OK(hipMemsetAsync(d_tok_counts.p, 0, 16, s));
+    const TokenTable O = token_table();
+    const TokenTable N{sp_tok_keys.as<unsigned long long>(), sp_tok_fid.as<int64_t>(), sp_tok_fidx.as<int32_t>(),
+                       sp_tok_acq.as<int32_t>(), ncap - 1, d_tok_counts.as<unsigned long long>()};
+    k_tok_rebuild<<<grid_for((int64_t)ocap), 256, 0, s>>>(O, ocap, N);
+    HIP_OK(hipGetLastError());
+    std::swap(d_tok_keys, sp_tok_keys);
+    std::swap(d_tok_fid, sp_tok_fid);
+    std::swap(d_tok_fidx, sp_tok_fidx);
+    std::swap(d_tok_acq, sp_tok_acq);
+    std::swap(d_tok_claim, sp_tok_claim);
+    tcap = ncap;
     return 0;
 }
 
@@ -2270,7 +2323,8 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
                       &e->d_lrule_dur, &e->d_lrule_w, &e->d_lrule_rcp, &e->d_lrule_kind, &e->d_lhot_keys,
                       &e->d_lhot_tok, &e->d_ltable, &e->d_lstate, &e->d_now, &e->d_conc_thr, &e->d_seg1_w,
                       &e->d_seg1_rcp, &e->d_seg1_kind, &e->d_tok_keys, &e->d_tok_fid, &e->d_tok_fidx,
-                      &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->w_runs, &e->w_pscan, &e->d_lres_state,
+                      &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->d_tok_claim, &e->w_cbig, &e->sp_tok_keys,
+                      &e->sp_tok_fid, &e->sp_tok_fidx, &e->sp_tok_acq, &e->sp_tok_claim, &e->w_runs, &e->w_pscan, &e->d_lres_state,
                       &e->d_lres_count, &e->d_lres_w, &e->d_lres_rcp, &e->d_lres_kind, &e->d_lres_tcount,
                       &e->d_lres_flags, &e->w_lslow, &e->io_lrt, &e->d_lrule_grade,
                       &e->d_lg_on, &e->d_lg_dn, &e->d_lg_created, &e->d_lg_roff, &e->d_lg_rules, &e->d_lg_comp,
@@ -3541,6 +3595,102 @@ int sentinel_set_occupy_timeout(sentinel_engine_t *e, int32_t timeout_ms) {
     return 0;
 }
 
+// A batch of concurrency-token acquires / releases (device pointers) on stream s, engine lock held.
+// The token cache is kept below 3/4 of its slots (live + tombstones) from a host-side upper bound, so
+// only a batch that could cross it reads the device counts and compacts the tombstones (a sync).
+static int submit_concurrent(sentinel_engine_t *e, int64_t n, const ConcEvent *dev, uint64_t *dout, hipStream_t s) {
+    if (n <= 0) return 0;
+    if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
+    int rc = e->ensure_tokens();
+    if (rc) return rc;
+    if ((double)(e->tok_ub + (uint64_t)n) > 0.75 * (double)e->tcap) {
+        if (s != e->stream) HIP_OK(hipStreamSynchronize(s));
+        HIP_OK(hipStreamSynchronize(e->stream));
+        unsigned long long counts[2];
+        HIP_OK(hipMemcpy(counts, e->d_tok_counts.p, 16, hipMemcpyDeviceToHost));
+        e->tok_ub = counts[0] + counts[1];
+        if ((double)(e->tok_ub + (uint64_t)n) > 0.75 * (double)e->tcap) {
+            // drop the tombstones, and grow until the live tokens plus a few batches fit
+            uint64_t nc = e->tcap;
+            while ((double)(counts[0] + 4 * (uint64_t)n) > 0.75 * (double)nc && nc < ((uint64_t)1 << 32)) nc <<= 1;
+            rc = e->rebuild_tokens_device(nc, s);
+            if (rc) return rc;
+            e->tok_ub = counts[0];
+        }
+    }
+    e->tok_ub += (uint64_t)n;                    // at most one new token per event
+    rc = e->ensure_ws(n);
+    if (rc) return SENTINEL_E_NOMEM;
+    const int32_t F = (int32_t)e->rules.size();
+    const int fbits = bits_for(F);
+    const uint32_t finvalid = ((uint32_t)1 << fbits) - 1;
+    uint32_t *fkey = e->w_fkey.as<uint32_t>();
+    uint32_t *relslot = e->w_k.as<uint32_t>();
+    uint32_t *claim = e->d_tok_claim.as<uint32_t>();
+    const int64_t nb = sort_blocks(n);
+    const TokenTable TT = e->token_table();
+    e->launch("conc_prep", n, s, [&] {
+        k_conc_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(n, dev, F, TT, dout, fkey, finvalid,
+                                                                      e->w_fhist.as<uint32_t>(), nb, relslot, claim);
+    });
+    if (F > 0) {
+        const EventSrc src{nullptr, (const ParamEvent *)dev, nullptr, false};
+        e->sort(fkey, n, fbits, e->w_fhist.as<uint32_t>(), src, s);
+        const uint32_t *skey = e->w_skey.as<uint32_t>();
+        uint32_t *flag = e->w_segid.as<uint32_t>();
+        uint32_t *run_start = e->w_segstart.as<uint32_t>();
+        uint32_t *ctl = e->w_counters.as<uint32_t>();           // [0] runs, [1] long runs, [2] chunks, [3] ticket
+        // long-run work lists, sized for this batch: slots <= n / (CONC_LANE_RUN + 1), chunks <= slots + n / CONC_CHUNK
+        const int64_t ms = n / (CONC_LANE_RUN + 1) + 1, mc = ms + n / CONC_CHUNK + 1;
+        auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
+        const int64_t o_run = 0, o_now = o_run + al(ms * 4), o_tp = o_now + al(ms * 4), o_unit = o_tp + al(ms * 8),
+                      o_mag = o_unit + al(ms * 4), o_ch = o_mag + al(ms * 8), o_cs = o_ch + al(ms * 8),
+                      o_cj = o_cs + al(mc * 4), o_fl = o_cj + al(mc * 4), o_agg = o_fl + al(mc * 4),
+                      o_inc = o_agg + al(mc * 16), o_end = o_inc + al(mc * 16);
+        if (n > e->cbig_n) {
+            e->w_cbig.release();
+            if (e->w_cbig.ensure((size_t)o_end)) return SENTINEL_E_NOMEM;
+            HIP_OK(hipMemsetAsync(e->w_cbig.p, 0, (size_t)o_end, s));   // look-back flags of no epoch
+            e->cbig_n = n;
+        }
+        e->conc_epoch = (e->conc_epoch + 1) & 0x3FFFFFFFu;
+        if (e->conc_epoch == 0) e->conc_epoch = 1;
+        char *gb = e->w_cbig.as<char>();
+        const ConcBig G{(uint32_t *)(gb + o_run), (int32_t *)(gb + o_now), (int64_t *)(gb + o_tp), (uint32_t *)(gb + o_unit),
+                        (unsigned long long *)(gb + o_mag), (uint2 *)(gb + o_ch), (uint32_t *)(gb + o_cs),
+                        (uint32_t *)(gb + o_cj), (uint32_t *)(gb + o_fl), (MinPlus *)(gb + o_agg), (MinPlus *)(gb + o_inc),
+                        ctl, e->conc_epoch};
+        HIP_OK(hipMemsetAsync(ctl, 0, 16, s));
+        e->launch("conc_runs", n, s, [&] {
+            k_conc_heads<<<grid_for(n), 256, 0, s>>>(skey, n, finvalid, flag);
+        });
+        e->scan(flag, n, true, s);
+        e->launch("conc_runs", n, s, [&] {
+            k_conc_runs<<<grid_for(n), 256, 0, s>>>(skey, n, finvalid, flag, run_start, ctl);
+        });
+        const uint64_t id_base = (e->tok_salt << 40) | e->tok_counter;
+#ifdef SENTINEL_CONC_TRACE
+        HIP_OK(hipMemsetAsync(e->w_vtmp.p, 0xFF, n * 8, s));
+        const ConcCtx C{dev, e->w_sval.as<uint64_t>(), relslot, claim, TT, e->d_flow_ids.as<int64_t>(), id_base, dout,
+                        e->w_vtmp.as<uint64_t>()};
+#else
+        const ConcCtx C{dev, e->w_sval.as<uint64_t>(), relslot, claim, TT, e->d_flow_ids.as<int64_t>(), id_base, dout};
+#endif
+        const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, mc));
+        e->launch("conc_process", n, s, [&] {
+            k_conc_process<<<grid_for(n), 256, 0, s>>>(C, run_start, skey, e->d_now.as<int32_t>(),
+                                                       e->d_conc_thr.as<double>(), G);
+        });
+        e->launch("conc_info", n, s, [&] { k_conc_info<<<g, 256, 0, s>>>(C, run_start, G); });
+        e->launch("conc_chunks", n, s, [&] {
+            k_conc_chunks<<<g, CB_THREADS, 0, s>>>(C, run_start, skey, e->d_now.as<int32_t>(), e->d_conc_thr.as<double>(), G);
+        });
+        e->tok_counter += (uint64_t)n;
+    }
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
 int sentinel_submit_concurrent_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_concurrent_event_t *ev,
                                           sentinel_concurrent_result_t *out) {
     if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
@@ -3548,52 +3698,40 @@ int sentinel_submit_concurrent_batch_host(sentinel_engine_t *e, int64_t n, const
     if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
-    int rc = e->ensure_tokens();
-    if (rc) return rc;
     hipStream_t s = e->stream;
-    unsigned long long counts[2];
-    HIP_OK(hipMemcpy(counts, e->d_tok_counts.p, 16, hipMemcpyDeviceToHost));
-    if ((double)(counts[0] + counts[1] + (uint64_t)n) > 0.75 * (double)e->tcap && counts[1] > 0) {
-        rc = e->rewrite_tokens(true);        // drop tombstones before the table clogs
-        if (rc) return rc;
-    }
-    rc = e->ensure_ws(n);
-    rc |= e->io_ev.ensure(n * sizeof(ConcEvent));
+    int rc = e->io_ev.ensure(n * sizeof(ConcEvent));
     rc |= e->io_out.ensure(n * 16);
     if (rc) return SENTINEL_E_NOMEM;
     HIP_OK(hipMemcpyAsync(e->io_ev.p, ev, n * sizeof(ConcEvent), hipMemcpyHostToDevice, s));
-    const ConcEvent *dev = e->io_ev.as<ConcEvent>();
-    uint64_t *dout = e->io_out.as<uint64_t>();
-    const int32_t F = (int32_t)e->rules.size();
-    const int fbits = bits_for(F);
-    const uint32_t finvalid = ((uint32_t)1 << fbits) - 1;
-    uint32_t *fkey = e->w_fkey.as<uint32_t>();
-    const int64_t nb = sort_blocks(n);
-    const TokenTable TT = e->token_table();
-    HIP_OK(hipMemsetAsync(e->w_counters.p, 0, 16, s));
-    e->launch("conc_prep", n, s, [&] {
-        k_conc_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(n, dev, F, TT, dout, fkey, finvalid,
-                                                                      e->w_fhist.as<uint32_t>(), nb);
-    });
-    if (F > 0) {
-        KeyTable T1{};
-        T1.w = e->d_seg1_w.as<int32_t>();
-        T1.rcp_w = e->d_seg1_rcp.as<double>();
-        T1.kind = e->d_seg1_kind.as<uint8_t>();
-        T1.ncounters = 1;
-        const EventSrc src{nullptr, (const ParamEvent *)dev, nullptr, false};
-        e->sort_segments(T1, fkey, e->w_fhist.as<uint32_t>(), n, fbits, src, s);
-        const BatchWork W = e->work();
-        const uint64_t id_base = (e->tok_salt << 40) | e->tok_counter;
-        e->launch("conc_process", n, s, [&] {
-            k_conc_process<<<grid_for(n), 256, 0, s>>>(W, dev, e->d_now.as<int32_t>(), e->d_conc_thr.as<double>(),
-                                                       e->d_flow_ids.as<int64_t>(), TT, id_base, dout);
-        });
-        e->tok_counter += (uint64_t)n;
-    }
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(out, dout, n * 16, hipMemcpyDeviceToHost, s));
+    rc = submit_concurrent(e, n, e->io_ev.as<ConcEvent>(), e->io_out.as<uint64_t>(), s);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 16, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
+    return 0;
+}
+
+int sentinel_submit_concurrent_batch(sentinel_engine_t *e, int64_t n, const sentinel_concurrent_event_t *ev,
+                                     sentinel_concurrent_result_t *out, void *stream) {
+    if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    return submit_concurrent(e, n, (const ConcEvent *)ev, (uint64_t *)out, stream ? (hipStream_t)stream : e->stream);
+}
+
+// Debug: the last concurrency batch's sorted keys / values, run starts, counters and the long-run slot 0.
+int sentinel_debug_conc_state(sentinel_engine_t *e, int64_t n, uint32_t *skey, uint64_t *sval, uint32_t *run_start,
+                              uint32_t *ctl, uint32_t *relslot) {
+    if (!e) return -1;
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipStreamSynchronize(e->stream));
+    HIP_OK(hipMemcpy(skey, e->w_skey.p, n * 4, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(sval, e->w_sval.p, n * 8, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(run_start, e->w_segstart.p, (n + 1) * 4, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(ctl, e->w_counters.p, 16, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(relslot, e->w_k.p, n * 4, hipMemcpyDeviceToHost));
+#ifdef SENTINEL_CONC_TRACE
+    HIP_OK(hipMemcpy(sval, e->w_vtmp.p, n * 8, hipMemcpyDeviceToHost));     // (the trace instead of the values)
+#endif
     return 0;
 }
 

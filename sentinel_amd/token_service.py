@@ -300,6 +300,30 @@ class GpuTokenService:
               "submit_concurrent_batch_host")
         return out["status"].astype(np.int8), out["token_id"].copy()
 
+    def submit_concurrent_batch(self, events, results=None, stream=None):
+        """Concurrency-token acquires / releases on device tensors (sentinel_submit_concurrent_batch):
+        `events` int64 (n, 3) of sentinel_concurrent_event_t records (word0 = acquire << 32 | flow_idx,
+        word1 = token_id, word2 = flags << 32 | kind); `results` int64 (n, 2) of
+        sentinel_concurrent_result_t ({token_id, status}).  Asynchronous on `stream`."""
+        import torch
+        n = int(events.shape[0])
+        if results is None:
+            results = torch.empty((n, 2), dtype=torch.int64, device=events.device)
+        s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        check(self._L.sentinel_submit_concurrent_batch(self._h, n, C.c_void_p(events.data_ptr()),
+                                                       C.c_void_p(results.data_ptr()),
+                                                       None if s is None else C.c_void_p(s)),
+              "submit_concurrent_batch")
+        return results
+
+    @staticmethod
+    def concurrent_events(flow_idx, acquire, token_id, kind, flags):
+        """(n, 3) int64 device tensor of sentinel_concurrent_event_t from torch tensors."""
+        import torch
+        w0 = (acquire.to(torch.int64) << 32) | (flow_idx.to(torch.int64) & 0xFFFFFFFF)
+        w2 = (flags.to(torch.int64) << 32) | (kind.to(torch.int64) & 0xFFFFFFFF)
+        return torch.stack([w0, token_id.to(torch.int64), w2], dim=1).contiguous()
+
     def concurrent_now_calls(self, flow_idx: int) -> int:
         v = C.c_int32()
         check(self._L.sentinel_concurrent_now_calls(self._h, int(flow_idx), C.byref(v)), "concurrent_now_calls")

@@ -119,3 +119,129 @@ def test_gpu_concurrent_batches_match_oracle(oracle_mod):
             assert svc.concurrent_expire(1000) == orc.concurrent_expire_all()
             outstanding = []
     assert {0, 1, 3, 6, 7, -4} <= set(np.unique(st_o).tolist()) | {6, 7}
+
+
+def _device_batch(svc, fidx, acq, tok, kind, flags):
+    import torch
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
+    ev = svc.concurrent_events(t(fidx.astype(np.int32)), t(acq.astype(np.int32)), t(tok.astype(np.int64)),
+                               t(kind.astype(np.int32)), t(flags.astype(np.int32)))
+    res = torch.full((len(kind), 2), -99, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()            # the events (and the fill) were made on torch's stream
+    svc.submit_concurrent_batch(ev, results=res)
+    svc.synchronize()
+    r = res.cpu().numpy()
+    assert (r[:, 1] != -99).all(), "an event without a result"
+    return r[:, 1].astype(np.int32).astype(np.int8), r[:, 0].copy()
+
+
+@pytest.mark.gpu
+def test_gpu_concurrent_device_hot_flows_match_oracle(oracle_mod):
+    """The device-pointer path (sentinel_submit_concurrent_batch) on hot flows: runs of thousands of
+    events go to the workgroup kernel (k_conc_big: unit-acquire chunks by the (min, +) scan, others by
+    the state machine), fractional / tiny / AVG_LOCAL thresholds, duplicate releases in a batch, and a
+    reload that lowers the counts while tokens are out (nowCalls above the new threshold: phase A)."""
+    import sentinel_amd as sa
+    from sentinel_amd.token_service import ServerNamespace
+    rng = np.random.default_rng(404)
+    F = 64
+
+    def make_rules(ids, scale=1.0):
+        return [_rule(int(f), float(np.round(rng.uniform(0.5, 400.0) * scale, 1)), int(rng.integers(0, 2)))
+                for f in ids]
+    rules = make_rules(np.arange(1, F + 1))
+    svc = sa.GpuTokenService(0)
+    svc.set_namespaces([ServerNamespace(connected_count=2)])
+
+    def load(rs):
+        svc.load_flow_rules([sa.FlowRule(count=r["count"], cluster_config=sa.ClusterFlowConfig(
+            flow_id=r["flow_id"], threshold_type=r["threshold_type"])) for r in rs])
+    load(rules)
+    orc = oracle_mod.TokenServiceOracle(rules, namespaces=[dict(connected_count=2)])
+    outstanding = []
+    for b in range(10):
+        if b == 5:   # every count divided by 4: flows with tokens out start above their threshold
+            rules = [dict(r, count=float(np.round(r["count"] / 4.0, 1))) for r in rules]
+            load(rules)
+            orc.reload_flow_rules(rules)
+        n = int(rng.integers(20_000, 40_000))
+        kind = (rng.random(n) < 0.45).astype(np.int32)
+        if not outstanding:
+            kind[:] = 0
+        fidx = T.zipf_indices(len(rules), 1.3, n, rng)
+        acq = np.ones(n, np.int32)
+        if b % 3 == 2:
+            acq[rng.random(n) < 0.02] = 2                                   # some chunks leave the scan
+        flags = np.ones(n, np.int32)
+        tok = np.zeros(n, np.int64)
+        rel = np.nonzero(kind == 1)[0]
+        if len(rel):
+            pick = rng.integers(0, len(outstanding), size=len(rel))
+            tok[rel] = np.array(outstanding, np.int64)[pick]                # repeats -> ALREADY_RELEASE
+            tok[rel[::97]] = 777                                             # never issued
+        st_g, tok_g = _device_batch(svc, fidx, acq, tok, kind, flags)
+        ev = np.zeros(n, dtype=orc.CONC_EVENT)
+        ev["flow_idx"], ev["acquire"], ev["token_id"], ev["kind"], ev["flags"] = fidx, acq, tok, kind, flags
+        st_o, tok_o = orc.concurrent_replay(ev, tok_g)
+        bad = np.nonzero(st_g != st_o)[0]
+        assert len(bad) == 0, (b, len(bad), bad[:5], st_g[bad[:5]], st_o[bad[:5]], kind[bad[:5]], fidx[bad[:5]])
+        ok = st_g == 0
+        assert (tok_g[ok] != 0).all() and len(np.unique(tok_g[ok])) == int(ok.sum())
+        released = set(tok[(kind == 1) & (st_g == 6)].tolist())
+        outstanding = [t for t in outstanding if t not in released] + tok_g[ok].tolist()
+        for f in range(len(rules)):
+            assert svc.concurrent_now_calls(f) == orc.concurrent_now_calls(f), (b, f)
+        assert svc.concurrent_token_count() == orc.concurrent_token_count()
+    assert {0, 1, 6, 7} <= set(np.unique(st_o).tolist())
+
+
+@pytest.mark.gpu
+def test_gpu_qps_and_concurrent_batches_interleaved(oracle_mod):
+    """QPS requestToken batches (ClusterFlowChecker) and concurrency-token batches
+    (ConcurrentClusterFlowChecker) interleaved on one engine and one rule table, against the oracle
+    doing the same: the two checkers keep separate state (the flow's ClusterMetric vs nowCalls / the
+    token cache) and neither batch kind disturbs the other."""
+    import sentinel_amd as sa
+    rng = np.random.default_rng(505)
+    F = 300
+    rules = [_rule(int(f), float(rng.integers(2, 60)), 1) for f in range(1, F + 1)]
+    svc = sa.GpuTokenService(0)
+    svc.load_flow_rules([sa.FlowRule(count=r["count"], cluster_config=sa.ClusterFlowConfig(
+        flow_id=r["flow_id"], threshold_type=1)) for r in rules])
+    orc = oracle_mod.TokenServiceOracle(rules)
+    t = T.T0_ALIGNED + 3
+    outstanding = []
+    for b in range(8):
+        if b % 2 == 0:
+            n = 30_000
+            idx = T.zipf_indices(F, 1.1, n, rng)
+            acq = rng.integers(1, 3, size=n).astype(np.int32)
+            ts = np.sort(t + rng.integers(0, 1500, size=n)).astype(np.int64)
+            t += 1500
+            st_g, rem_g, _ = svc.submit_flow_batch_host(idx, acq, ts)
+            st_o, rem_o = orc.replay(idx, acq, ts)[:2]
+            bad = np.nonzero((st_g != st_o) | (rem_g != rem_o))[0]
+            assert len(bad) == 0, (b, len(bad), bad[:5])
+        else:
+            n = 20_000
+            kind = (rng.random(n) < 0.4).astype(np.int32)
+            if not outstanding:
+                kind[:] = 0
+            fidx = T.zipf_indices(F, 1.1, n, rng)
+            acq = np.ones(n, np.int32)
+            tok = np.zeros(n, np.int64)
+            rel = np.nonzero(kind == 1)[0]
+            if len(rel):
+                tok[rel] = np.array(outstanding, np.int64)[rng.integers(0, len(outstanding), size=len(rel))]
+            st_g, tok_g = _device_batch(svc, fidx, acq, tok, kind, np.ones(n, np.int32))
+            ev = np.zeros(n, dtype=orc.CONC_EVENT)
+            ev["flow_idx"], ev["acquire"], ev["token_id"], ev["kind"], ev["flags"] = fidx, acq, tok, kind, 1
+            st_o, _ = orc.concurrent_replay(ev, tok_g)
+            bad = np.nonzero(st_g != st_o)[0]
+            assert len(bad) == 0, (b, len(bad), bad[:5], st_g[bad[:5]], st_o[bad[:5]])
+            ok = st_g == 0
+            released = set(tok[(kind == 1) & (st_g == 6)].tolist())
+            outstanding = [x for x in outstanding if x not in released] + tok_g[ok].tolist()
+    for f in range(0, F, 11):
+        assert svc.concurrent_now_calls(f) == orc.concurrent_now_calls(f)
