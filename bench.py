@@ -449,6 +449,10 @@ class ParamWorkload:
         if dom == "process":
             # per touched (rule, value) slot: read n {epoch, count} pairs, write one; per event: segment record
             return 24.0 + (self.n * 16 + 16) / 4.0
+        if dom == "prule_process" and self.cm:
+            # per request: its sorted value 8 + event 24 read, the verdict 8 written; per row of the sketch
+            # the value's cell (a ring of 2 n 8-B slots) read and one slot read-modify-written (8 + 8)
+            return 8 + 24 + 8 + self.cm_depth * (2 * self.n * 8 + 16)
         return KERNEL_BYTES_PER_EVENT.get(dom)
 
     def pipeline_bytes(self):

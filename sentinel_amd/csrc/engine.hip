@@ -845,7 +845,7 @@ struct sentinel_engine {
                          d_prule_Is.as<double>(), d_prule_thr.as<double>(),
                          has_hot ? d_hot_table.as<unsigned long long>() : nullptr, hot_mask, d_hot_thr.as<double>()};
         C.PT = table(pt, 1, param_stride(pmax_n));
-        C.CM = CountMin{d_cm.as<uint64_t>(), cm_depth, cm_width, pmax_n, pmode == SENTINEL_PARAM_COUNT_MIN_SHARED};
+        C.CM = CountMin{d_cm.as<uint64_t>(), cm_depth, cm_width, cm_slots(), pmode == SENTINEL_PARAM_COUNT_MIN_SHARED};
         C.L = LocalRules{d_lrule_valid.as<uint8_t>(), d_lrule_tok.as<int64_t>(), d_lrule_burst.as<int64_t>(),
                          d_lrule_dur.as<int64_t>(), lhas_hot ? d_lhot_keys.as<unsigned long long>() : nullptr,
                          lhot_mask, d_lhot_tok.as<int64_t>(), d_lstate.as<int64_t>(),
@@ -1078,6 +1078,7 @@ struct sentinel_engine {
         return true;
     }
     int rebuild_cm();
+    int32_t cm_slots() const { return pmode == SENTINEL_PARAM_COUNT_MIN_SHARED ? 2 * pmax_n : pmax_n; }
     int ensure_tokens();
     int rewrite_tokens(bool compact, uint64_t new_cap = 0);
     int rebuild_tokens_device(uint64_t new_cap, hipStream_t s);
@@ -1476,7 +1477,7 @@ int sentinel_engine::rebuild_cm() {
     if (pmode == SENTINEL_PARAM_EXACT) return 0;
     // one sketch per rule, or one for every rule (SHARED: a single window for all param rules)
     const size_t R = pmode == SENTINEL_PARAM_COUNT_MIN_SHARED ? 1 : std::max<size_t>(prules.size(), 1);
-    const size_t bytes = R * (size_t)cm_depth * (size_t)cm_width * (size_t)pmax_n * 8;
+    const size_t bytes = R * (size_t)cm_depth * (size_t)cm_width * (size_t)cm_slots() * 8;
     if (bytes > ((size_t)96 << 30)) return fail(SENTINEL_E_NOMEM, "count-min sketch would exceed 96 GiB");
     int rc = d_cm.ensure(bytes);
     if (rc) return rc;
@@ -1836,6 +1837,25 @@ static int wait_done(sentinel_engine_t *e, const uint32_t *flag) {
     }
 }
 
+// A device submit on a caller's stream is ordered after everything already queued on the engine
+// stream (a batcher's or the wire server's small-batch kernels: the engine lock does not wait for
+// them) and before whatever the engine stream runs next -- one event each way.
+struct ForeignStream {
+    sentinel_engine_t *e;
+    hipStream_t s;
+    ForeignStream(sentinel_engine_t *e_, hipStream_t s_) : e(e_), s(s_) {
+        if (s != e->stream) join(e->stream, s);
+    }
+    ~ForeignStream() {
+        if (s != e->stream) join(s, e->stream);
+    }
+    void join(hipStream_t from, hipStream_t to) {
+        hipEvent_t ev = e->get_ev();
+        if (ev && hipEventRecord(ev, from) == hipSuccess) (void)hipStreamWaitEvent(to, ev, 0);
+        if (ev) e->ev_pool.push_back(ev);
+    }
+};
+
 static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
                        hipStream_t s) {
     if (n <= 0) return 0;
@@ -2097,9 +2117,10 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
         HIP_OK(hipMemcpyAsync(span, lv, 16, hipMemcpyDeviceToHost, s));
         HIP_OK(hipStreamSynchronize(s));
         if (span[0] != ~0ull && (int64_t)(span[1] - span[0]) < CM_LEVEL_LAUNCHES && !e->cm_force_coop) {
+            const int band = e->pmax_n;                   // one launch per band of n epochs (ring of 2 n slots)
             e->launch("prule_process", n, s, [&] {
-                for (int64_t E = (int64_t)span[0]; E <= (int64_t)span[1]; ++E)
-                    k_prule_cm_level<<<hb, 256, 0, s>>>(C, W, evp, vs, out, heads, ctl, cursor, E);
+                for (int64_t E = (int64_t)span[0]; E <= (int64_t)span[1]; E += band)
+                    k_prule_cm_level<<<hb, 256, 0, s>>>(C, W, evp, vs, out, heads, ctl, cursor, E, band);
             });
             HIP_OK(hipGetLastError());
             return 0;
@@ -2108,8 +2129,9 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
         const unsigned nblk = (unsigned)std::max<int64_t>(1, std::min<int64_t>(e->cm_sync_blocks, (H + 255) / 256));
         hipError_t ce = hipSuccess;
         e->launch("prule_process", n, s, [&] {
+            int band = e->pmax_n;
             void *args[] = {(void *)&C, (void *)&W, (void *)&evp, (void *)&vs, (void *)&out, (void *)&heads, (void *)&ctl,
-                            (void *)&cursor, (void *)&lv};
+                            (void *)&cursor, (void *)&lv, (void *)&band};
             ce = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(k_prule_cm_sync), dim3(nblk), dim3(256), args, 0, s);
         });
         if (ce != hipSuccess) return fail(SENTINEL_E_DEVICE, std::string("cooperative launch failed: ") + hipGetErrorString(ce));
@@ -2868,6 +2890,7 @@ int sentinel_submit_flow_batches(sentinel_engine_t *e, int32_t nbatch, const int
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
     hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    const ForeignStream fs_(e, s);
     for (int32_t k = 0; k < nbatch; ++k) {
         const int rc = submit_flow(e, n[k], (const Event *)ev[k], flags ? flags[k] : nullptr, (uint64_t *)out[k], s);
         if (rc) return rc;
@@ -2880,7 +2903,9 @@ int sentinel_submit_flow_batch(sentinel_engine_t *e, int64_t n, const sentinel_e
     if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
-    return submit_flow(e, n, (const Event *)ev, flags, (uint64_t *)out, stream ? (hipStream_t)stream : e->stream);
+    hipStream_t fs_s = stream ? (hipStream_t)stream : e->stream;
+    const ForeignStream fs_(e, fs_s);
+    return submit_flow(e, n, (const Event *)ev, flags, (uint64_t *)out, fs_s);
 }
 
 // H2D, decide, D2H of host events, synchronous, with the engine lock held.
@@ -3040,7 +3065,9 @@ int sentinel_submit_param_batch(sentinel_engine_t *e, int64_t n, const sentinel_
     if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
-    return submit_param(e, n, (const ParamEvent *)ev, (uint64_t *)out, stream ? (hipStream_t)stream : e->stream);
+    hipStream_t fs_s = stream ? (hipStream_t)stream : e->stream;
+    const ForeignStream fs_(e, fs_s);
+    return submit_param(e, n, (const ParamEvent *)ev, (uint64_t *)out, fs_s);
 }
 
 static int submit_param_host_locked(sentinel_engine_t *e, int64_t n, const sentinel_param_event_t *ev,
@@ -3076,8 +3103,10 @@ int sentinel_submit_param_multi_batch(sentinel_engine_t *e, int64_t n, const sen
         return fail(SENTINEL_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
+    hipStream_t fs_s = stream ? (hipStream_t)stream : e->stream;
+    const ForeignStream fs_(e, fs_s);
     return submit_prules(e, e->pmode != SENTINEL_PARAM_EXACT ? PMODE_CM : PMODE_EXACT, n, nullptr,
-                         (const MultiEvent *)ev, values, n_values, (uint64_t *)out, stream ? (hipStream_t)stream : e->stream);
+                         (const MultiEvent *)ev, values, n_values, (uint64_t *)out, fs_s);
 }
 
 int sentinel_submit_param_multi_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_param_multi_event_t *ev,
@@ -3185,8 +3214,10 @@ int sentinel_submit_local_param_batch(sentinel_engine_t *e, int64_t n, const sen
         return fail(SENTINEL_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
+    hipStream_t fs_s = stream ? (hipStream_t)stream : e->stream;
+    const ForeignStream fs_(e, fs_s);
     return submit_prules(e, PMODE_LOCAL, n, nullptr, (const MultiEvent *)ev, values, n_values, (uint64_t *)out,
-                         stream ? (hipStream_t)stream : e->stream);
+                         fs_s);
 }
 
 int sentinel_submit_local_param_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_param_multi_event_t *ev,
@@ -3218,8 +3249,10 @@ int sentinel_submit_local_param_batch_ex(sentinel_engine_t *e, int64_t n, const 
         return fail(SENTINEL_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
+    hipStream_t fs_s = stream ? (hipStream_t)stream : e->stream;
+    const ForeignStream fs_(e, fs_s);
     return submit_prules(e, PMODE_LOCAL, n, nullptr, (const MultiEvent *)ev, values, n_values, (uint64_t *)out,
-                         stream ? (hipStream_t)stream : e->stream, kinds);
+                         fs_s, kinds);
 }
 
 int sentinel_submit_local_param_batch_ex_host(sentinel_engine_t *e, int64_t n, const sentinel_param_multi_event_t *ev,
@@ -3331,8 +3364,10 @@ int sentinel_submit_local_batch(sentinel_engine_t *e, int64_t n, const sentinel_
     if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
+    hipStream_t fs_s = stream ? (hipStream_t)stream : e->stream;
+    const ForeignStream fs_(e, fs_s);
     return submit_local_entry(e, n, (const Event *)ev, flags, flags ? rt_ms : nullptr, (uint64_t *)out,
-                              stream ? (hipStream_t)stream : e->stream);
+                              fs_s);
 }
 
 int sentinel_submit_local_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev, const uint8_t *flags,
@@ -3364,8 +3399,10 @@ int sentinel_submit_local_entry_batch(sentinel_engine_t *e, int64_t n, const sen
     if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
+    hipStream_t fs_s = stream ? (hipStream_t)stream : e->stream;
+    const ForeignStream fs_(e, fs_s);
     return submit_local_entry(e, n, (const Event *)ev, prioritized, nullptr, (uint64_t *)out,
-                              stream ? (hipStream_t)stream : e->stream);
+                              fs_s);
 }
 
 int sentinel_submit_local_entry_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev,
@@ -3555,8 +3592,10 @@ int sentinel_submit_local_graph_batch(sentinel_engine_t *e, int64_t n, const sen
     if (!e || n < 0 || (n > 0 && (!ev || !ctx || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
+    hipStream_t fs_s = stream ? (hipStream_t)stream : e->stream;
+    const ForeignStream fs_(e, fs_s);
     return submit_local_graph(e, n, (const Event *)ev, (const LocalCtx *)ctx, flags, flags ? rt_ms : nullptr,
-                              (uint64_t *)out, stream ? (hipStream_t)stream : e->stream);
+                              (uint64_t *)out, fs_s);
 }
 
 int sentinel_submit_local_graph_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev,
@@ -3715,7 +3754,9 @@ int sentinel_submit_concurrent_batch(sentinel_engine_t *e, int64_t n, const sent
     if (!e || n < 0 || (n > 0 && (!ev || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(e->mu);
     HIP_OK(hipSetDevice(e->device));
-    return submit_concurrent(e, n, (const ConcEvent *)ev, (uint64_t *)out, stream ? (hipStream_t)stream : e->stream);
+    hipStream_t fs_s = stream ? (hipStream_t)stream : e->stream;
+    const ForeignStream fs_(e, fs_s);
+    return submit_concurrent(e, n, (const ConcEvent *)ev, (uint64_t *)out, fs_s);
 }
 
 // Debug: the last concurrency batch's sorted keys / values, run starts, counters and the long-run slot 0.
@@ -3872,13 +3913,13 @@ int sentinel_param_sum(sentinel_engine_t *e, int32_t ridx, uint64_t pkey, int64_
     if (e->pmode != SENTINEL_PARAM_EXACT) {   // the sketch estimate (min over rows of the window sum)
         const int n = e->h_prule_n[ridx];
         const int64_t E = ts / (e->h_prule_interval[ridx] / n);
-        const CountMin C{e->d_cm.as<uint64_t>(), e->cm_depth, e->cm_width, e->pmax_n,
+        const CountMin C{e->d_cm.as<uint64_t>(), e->cm_depth, e->cm_width, e->cm_slots(),
                          e->pmode == SENTINEL_PARAM_COUNT_MIN_SHARED};
         int64_t est = INT64_MAX;
-        std::vector<uint64_t> cell(e->pmax_n);
+        std::vector<uint64_t> cell(e->cm_slots());
         for (int d = 0; d < e->cm_depth; ++d) {
             HIP_OK(hipMemcpy(cell.data(), cm_cell(C, (uint32_t)ridx, d, pkey), cell.size() * 8, hipMemcpyDeviceToHost));
-            est = std::min(est, cm_cell_sum(cell.data(), n, E));
+            est = std::min(est, cm_cell_sum(cell.data(), n, E, (int)cell.size()));
         }
         *out = est;
         return 0;
@@ -4001,6 +4042,7 @@ int sentinel_param_snapshot_device(sentinel_engine_t *e, int64_t ts, sentinel_pa
     const int32_t R = (int32_t)e->prules.size();
     if (R == 0) return 0;
     hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    const ForeignStream fs_(e, s);
     if (s != e->stream) HIP_OK(hipStreamSynchronize(e->stream));
     DevBuf dc, dk, ds, ids;
     int rc = param_top(e, ts, SENTINEL_TOP_PARAMS, s, dc, dk, ds);
@@ -4024,6 +4066,7 @@ int sentinel_snapshot_device(sentinel_engine_t *e, int64_t ts, sentinel_flow_sna
     if (F == 0) return 0;
     if (ts < 0) return fail(SENTINEL_E_INVALID, "negative timestamp");
     hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    const ForeignStream fs_(e, s);
     KeyTable FT = e->table(e->ft, NEV, 0);
     k_snapshot<<<grid_for(F), 256, 0, s>>>(FT, F, ts, e->d_flow_ids.as<int64_t>(), d_out);
     HIP_OK(hipGetLastError());

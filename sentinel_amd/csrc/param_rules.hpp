@@ -89,7 +89,7 @@ struct CountMin {
     uint64_t *cells;
     int32_t depth;
     uint32_t width;       // power of two
-    int32_t nmax;
+    int32_t nmax;         // slots per cell: n (per-rule sketch), 2 n (shared: a ring of two windows)
     bool shared;          // one sketch for every rule (param keys are unique per (rule, value))
 };
 
@@ -268,10 +268,12 @@ __host__ __device__ inline uint64_t *cm_cell(const CountMin &C, uint32_t rule, i
 }
 
 // Window sum of one cell at epoch E: slots tagged with one of the epochs (E-n, E] (a tag 2^24
-// epochs stale aliases into the window: it can only add, never remove, count).
-__host__ __device__ inline int64_t cm_cell_sum(const uint64_t *c, int nsc, int64_t E) {
+// epochs stale aliases into the window: it can only add, never remove, count).  `slots`: n, or 2 n
+// in the shared sketch's ring.
+__host__ __device__ inline int64_t cm_cell_sum(const uint64_t *c, int nsc, int64_t E, int slots = 0) {
     int64_t s = 0;
-    for (int j = 0; j < nsc; ++j) {
+    if (slots <= 0) slots = nsc;
+    for (int j = 0; j < slots; ++j) {
         const uint64_t x = c[j];
         const uint32_t tag = (uint32_t)(x >> CM_COUNT_BITS);
         if ((((uint32_t)E - tag) & CM_TAG_MASK) < (uint32_t)nsc) s += (int64_t)(x & CM_COUNT_MAX);
@@ -322,30 +324,34 @@ __device__ inline uint64_t cm_check(const ParamCtx &C, uint32_t rule, int64_t E,
 
 // ---------------------------------------------------------------------------------------------
 // Shared count-min sketch (one sketch for every rule): the cells are shared between rules, so the
-// rules' lanes must move through the batch's epochs together.  If one rule's lane ran ahead to epoch
-// E + n and reset a cell slot to it, a lagging lane at epoch E would lose the count it had put there
-// and could then admit what the exact checker blocks.  k_prule_cm_sync therefore decides level by
-// level: level E = the smallest epoch any rule still has pending; every lane decides its rules'
-// segments at epochs <= E (a rule's epochs only go up under the documented precondition of
-// per-rule non-decreasing timestamps; a late segment is decided at once rather than waited for),
-// then a grid barrier.  Within a level every cell update is atomic (a CAS loop): rules of the same
-// epoch only add count to each other's cells (over-estimate, never under), so the sketch stays
-// one-sided.  Cells are read with device-scope atomic loads (other CUs' updates, no stale L1).
+// rules' lanes must move through the batch's epochs together.  If one rule's lane ran far ahead and
+// reset a cell slot, a lagging lane would lose the count it had put there and could then admit what
+// the exact checker blocks.  Each shared cell therefore keeps a ring of 2 n slots (epoch E in slot
+// E mod 2n): a lane at epoch E' resets the slot of E' - 2n, and as long as every lane is within n
+// epochs of the slowest one (at L: it needs epochs > L - n), no reset can remove a count anybody still
+// reads.  k_prule_cm_sync decides band by band: band start L = the smallest epoch any rule still has
+// pending; every lane decides its rules' segments at epochs < L + n (a rule's epochs only go up
+// under the documented precondition of per-rule non-decreasing timestamps; a late segment is decided
+// at once rather than waited for), then a grid barrier -- n times fewer barriers than one per
+// epoch.  Within a band every cell update is atomic (a CAS loop): concurrent rules only add count to
+// each other's cells (over-estimate, never under), so the sketch stays one-sided.  Cells are read with
+// device-scope atomic loads (other CUs' updates, no stale L1).
 __device__ inline uint64_t cm_load(const uint64_t *c) {
     return __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // the n slots of one cell, every load in flight before the sum (device-scope loads: no stale L1)
-constexpr int CM_NMAX = 16;
+constexpr int CM_NMAX = 32;                   // ring slots (2 n, n <= 16)
 __device__ inline int64_t cm_cell_sum_sync(const uint64_t *c, int nsc, int64_t E) {
     uint64_t x[CM_NMAX];
+    const int slots = 2 * nsc;
 #pragma unroll
-    for (int j = 0; j < CM_NMAX; ++j) x[j] = j < nsc ? cm_load(c + j) : 0ull;
+    for (int j = 0; j < CM_NMAX; ++j) x[j] = j < slots ? cm_load(c + j) : 0ull;
     int64_t s = 0;
 #pragma unroll
     for (int j = 0; j < CM_NMAX; ++j) {
         const uint32_t tag = (uint32_t)(x[j] >> CM_COUNT_BITS);
-        if (j < nsc && (((uint32_t)E - tag) & CM_TAG_MASK) < (uint32_t)nsc) s += (int64_t)(x[j] & CM_COUNT_MAX);
+        if (j < slots && (((uint32_t)E - tag) & CM_TAG_MASK) < (uint32_t)nsc) s += (int64_t)(x[j] & CM_COUNT_MAX);
     }
     return s;
 }
@@ -353,7 +359,7 @@ __device__ inline int64_t cm_cell_sum_sync(const uint64_t *c, int nsc, int64_t E
 // Add a to the slot of E in every row: same tag -> add (saturating), an older tag -> restart at a, a
 // newer tag (only past the precondition: a rule's clock went back) -> add to the newer slot.
 __device__ inline void cm_add_sync(const CountMin &C, uint32_t rule, uint64_t key, int nsc, int64_t E, int32_t a) {
-    const int j = (int)(E % nsc);
+    const int j = (int)(E % (2 * nsc));
     const uint32_t te = (uint32_t)E & CM_TAG_MASK;
     for (int d = 0; d < C.depth; ++d) {
         unsigned long long *c = reinterpret_cast<unsigned long long *>(cm_cell(C, rule, d, key) + j);
@@ -428,7 +434,7 @@ constexpr unsigned long long CM_NO_LEVEL = ~0ull;
 __global__ __launch_bounds__(256) void k_prule_cm_sync(ParamCtx C, BatchWork W, const ParamEvent *__restrict__ ev,
                                                        ValueSrc vs, uint64_t *__restrict__ out,
                                                        const uint32_t *__restrict__ heads, uint32_t *__restrict__ ctl,
-                                                       uint32_t *__restrict__ cursor, unsigned long long *lv) {
+                                                       uint32_t *__restrict__ cursor, unsigned long long *lv, int band) {
     const uint32_t H = ctl[0];
     const int64_t S = (int64_t)*W.nseg;
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -448,7 +454,7 @@ __global__ __launch_bounds__(256) void k_prule_cm_sync(ParamCtx C, BatchWork W, 
             uint32_t g = cursor[h];
             if (g == 0xFFFFFFFFu) continue;
             const uint32_t rule = W.seg_key[heads[h]];
-            while ((int64_t)g < S && W.seg_key[g] == rule && W.seg_epoch[g] <= E) {
+            while ((int64_t)g < S && W.seg_key[g] == rule && W.seg_epoch[g] < E + band) {
                 const int64_t Eg = W.seg_epoch[g];
                 const uint32_t end = W.seg_start[g + 1];
                 for (uint32_t i = W.seg_start[g]; i < end; ++i) {
@@ -491,15 +497,15 @@ __global__ __launch_bounds__(256) void k_prule_cm_level(ParamCtx C, BatchWork W,
                                                         ValueSrc vs, uint64_t *__restrict__ out,
                                                         const uint32_t *__restrict__ heads,
                                                         const uint32_t *__restrict__ ctl, uint32_t *__restrict__ cursor,
-                                                        int64_t E) {
+                                                        int64_t E, int band) {
     const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
     if (h >= ctl[0]) return;
     uint32_t g = cursor[h];
     if (g == 0xFFFFFFFFu) return;
     const int64_t S = (int64_t)*W.nseg;
     const uint32_t rule = W.seg_key[heads[h]];
-    if (W.seg_epoch[g] > E) return;
-    while ((int64_t)g < S && W.seg_key[g] == rule && W.seg_epoch[g] <= E) {
+    if (W.seg_epoch[g] >= E + band) return;
+    while ((int64_t)g < S && W.seg_key[g] == rule && W.seg_epoch[g] < E + band) {
         const int64_t Eg = W.seg_epoch[g];
         const uint32_t end = W.seg_start[g + 1];
         for (uint32_t i = W.seg_start[g]; i < end; ++i) {

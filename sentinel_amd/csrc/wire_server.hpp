@@ -443,7 +443,9 @@ inline void sentinel_wire_server::flow_done(uint64_t tag, const sentinel_token_r
 inline bool sentinel_wire_server::on_readable(wire::Loop &L, wire::Conn *c) {
     uint8_t tmp[65536];
     bool eof = false;
-    for (;;) {
+    // at most 4 x 64 KB per readiness event (level-triggered: the rest raises the next one), so one
+    // client streaming requests cannot hold this loop thread or grow its buffer without bound
+    for (int reads = 0; reads < 4; ++reads) {
         const ssize_t r = ::recv(c->fd, tmp, sizeof tmp, 0);
         if (r > 0) { c->rbuf.insert(c->rbuf.end(), tmp, tmp + r); if ((size_t)r < sizeof tmp) break; continue; }
         if (r == 0) { eof = true; break; }

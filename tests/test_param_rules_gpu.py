@@ -161,6 +161,25 @@ def test_shared_count_min_is_one_sided(oracle_mod, monkeypatch, levels):
 
 
 @pytest.mark.gpu
+def test_shared_count_min_full_size_audit(oracle_mod):
+    """BASELINE config 4's count-min mode at its own size: 100k hot-parameter rules, Zipf values over
+    1000 per rule, 2M requests in 4 batches, the shared sketch at d = 4, w = 2^20 (bench config 4cm):
+    every sketch verdict replayed on exact counters with the same admitted history -- zero
+    one-sidedness violations -- and a false-block rate far below the e/w bound."""
+    import sentinel_amd as sa
+    count, hot, rule_idx, vals, keys, ts = T.config4(2_000_000, seed=61, n_rules=100_000, universe=1000)
+    acq = np.ones(len(ts), np.int32)
+    svc, orc = _cluster_pair(oracle_mod, count, hot, sample_count=lambda r: 10)
+    svc.set_param_mode(sa._lib.PARAM_COUNT_MIN_SHARED, depth=4, width=1 << 20)
+    st = np.concatenate([svc.submit_param_batch_host(rule_idx[i:i + 500_000], acq[i:i + 500_000], keys[i:i + 500_000],
+                                                     ts[i:i + 500_000])[0] for i in range(0, len(ts), 500_000)])
+    n1 = np.ones(len(ts), np.int32)
+    viol, fb, dec = orc.param_cm_audit(rule_idx, acq, ts, np.arange(len(ts)), n1, keys, st)
+    assert viol == 0 and dec == len(ts), viol
+    assert fb / dec < 1e-4, fb / dec
+
+
+@pytest.mark.gpu
 def test_avg_local_params_follow_connected_count(oracle_mod):
     """ClusterParamFlowChecker.calcGlobalThreshold reads ConnectionManager.getConnectedCount on every
     request (CPFC:101-111): AVG_LOCAL param rules (hot items included) must see a connected count that
