@@ -253,7 +253,10 @@ __device__ inline void conc_apply_item(const ConcCtx &C, uint32_t flow, int kind
     }
 }
 
-constexpr uint32_t CONC_LANE_RUN = 64;      // longer runs are decided in chunks by workgroups
+#ifndef SENTINEL_CONC_LANE_RUN
+#define SENTINEL_CONC_LANE_RUN 64
+#endif
+constexpr uint32_t CONC_LANE_RUN = SENTINEL_CONC_LANE_RUN;   // longer runs are decided in chunks by workgroups
 constexpr uint32_t CONC_CHUNK = 1024;       // events of a long run per workgroup step (4 per thread)
 
 // The greedy admission of unit acquires with releases interleaved is a (min, +) recurrence: while the
@@ -276,6 +279,10 @@ __device__ inline int64_t conc_tprime(double threshold) {
     return (int64_t)floor(threshold);
 }
 
+#ifndef SENTINEL_CONC_TICKETS
+#define SENTINEL_CONC_TICKETS 4
+#endif
+constexpr uint32_t CONC_TICKETS = SENTINEL_CONC_TICKETS;
 constexpr int CB_THREADS = 256;
 constexpr int CB_WAVES = CB_THREADS / WAVE;
 
@@ -513,11 +520,18 @@ __global__ __launch_bounds__(CB_THREADS) void k_conc_chunks(ConcCtx C, const uin
     if (t < 2) s_cnt[t] = 0;
     int64_t dlive = 0, dtomb = 0;
     const uint32_t nch = G.ctl[2];
+    // tickets are taken CONC_TICKETS at a time (one counter for every workgroup: one atomic per chunk
+    // serialised ~10k atomics on one address); a block of tickets is decided in order
+    uint32_t cur = 0, lim = 0;
     for (;;) {
-        if (t == 0) s_ticket = atomicAdd(&G.ctl[3], 1u);
-        __syncthreads();
-        const uint32_t c = s_ticket;
-        __syncthreads();
+        if (cur == lim) {
+            if (t == 0) s_ticket = atomicAdd(&G.ctl[3], (uint32_t)CONC_TICKETS);
+            __syncthreads();
+            cur = s_ticket;
+            lim = cur + CONC_TICKETS;
+            __syncthreads();
+        }
+        const uint32_t c = cur++;
         if (c >= nch) break;
         const uint32_t slot = G.chunk_slot[c], j = G.chunk_j[c];
         const uint32_t r = G.run[slot];
