@@ -70,7 +70,7 @@ KERNEL_SYMBOLS = {
     "part_fused": ("k_part_half",), "part_big": ("k_part_big",), "part_long": ("k_part_long",),
     "param_prep": ("k_param_prep", "k_pp_prep"), "param_meta": ("k_param_meta",), "prule_prep": ("k_prule_prep",),
     "prule_process": ("k_prule_process",), "part_unsplit": ("k_part_unsplit",), "lim_prep": ("k_lim1_prep",),
-    "param_scatter": ("k_pp_scatter",), "param_group": ("k_pp_group",),
+    "param_scatter": ("k_pp_scatter",), "param_group": ("k_pp_group",), "param_cm_read": ("k_pp_cm_read",), "param_cm_walk": ("k_pp_cm_walk",),
     "conc_prep": ("k_conc_prep",), "conc_runs": ("k_conc_heads", "k_conc_runs"),
     "conc_process": ("k_conc_process",), "conc_info": ("k_conc_info",), "conc_chunks": ("k_conc_chunks",), "param_decide": ("k_pp_walk", "k_pp_decide"),
 }
@@ -449,6 +449,16 @@ class ParamWorkload:
         if dom == "process":
             # per touched (rule, value) slot: read n {epoch, count} pairs, write one; per event: segment record
             return 24.0 + (self.n * 16 + 16) / 4.0
+        if dom in ("param_cm_walk", "param_cm_read"):
+            # walk, per request: the grouped value read 8, the verdict written 8 (+ M(E) 8 for the requests
+            # within n epochs of the previous batch); per distinct key: its 16-B record, the rule record 32,
+            # per sketch row one slot read-modify-written (8 + 8) per admitted epoch (>= 1).  read, per
+            # request: the grouped value 8; per key in the first n epochs: d rings of 2 n 8-B slots
+            e_k = self.N / max(1, self._dk) if hasattr(self, "_dk") else 1.0
+            frac_early = min(1.0, self.interval / max(1.0, float(self.span_ms())))
+            if dom == "param_cm_read":
+                return 8.0 + 8.0 * frac_early + (16 + 32 + frac_early * self.cm_depth * 2 * self.n * 8) / e_k
+            return 16.0 + 8.0 * frac_early + (16 + 32 + self.cm_depth * 16) / e_k
         if dom == "prule_process" and self.cm:
             # per request: its sorted value 8 + event 24 read, the verdict 8 written; per row of the sketch
             # the value's cell (a ring of 2 n 8-B slots) read and one slot read-modify-written (8 + 8)

@@ -623,6 +623,9 @@ struct sentinel_engine {
     // pinned mirror {batch ordinal, d_pfresh after it} written by the device after every partition-path
     // param batch: the reserve check knows the exact fresh count up to a recent batch without a sync
     unsigned long long *h_pfresh = nullptr;
+    unsigned long long *h_cmband = nullptr;     // shared count-min bands: {min ts, ~max ts, overflow} read back
+    DevBuf d_cmband;
+    bool cm_keys = true;               // shared sketch: key-parallel bands (k_pp_cm_band) when the batch allows
     uint64_t p_ord = 0;                // param batches reserved so far
     uint64_t p_reset_ord = 0;          // first batch ordinal after d_pfresh was last zeroed
     std::deque<std::pair<uint64_t, uint64_t>> p_pending;   // (ordinal, values) reserved since the reset
@@ -1482,6 +1485,10 @@ int sentinel_engine::rebuild_cm() {
     int rc = d_cm.ensure(bytes);
     if (rc) return rc;
     HIP_OK(hipMemsetAsync(d_cm.p, 0, bytes, stream));
+    if (pmode == SENTINEL_PARAM_COUNT_MIN_SHARED) {       // the key walk's control words: cleared cells
+        if (d_cmband.ensure(64)) return SENTINEL_E_NOMEM;
+        k_set_i64<<<1, 64, 0, stream>>>(d_cmband.as<long long>() + 1, (long long)CM_EHI_NONE);
+    }
     HIP_OK(hipStreamSynchronize(stream));
     return 0;
 }
@@ -1899,7 +1906,7 @@ static int submit_param_part(sentinel_engine_t *e, int64_t n, const ParamEvent *
     const int32_t *route = e->param_plain ? nullptr : e->d_prule_route.as<int32_t>();
     e->launch("param_prep", n, s, [&] {
         k_pp_prep<<<dim3((unsigned)nb), dim3(PP_THREADS), 0, s>>>(n, ev, have ? R : 0, route, e->param_ctx().R, out,
-                                                                  pbits, hist, P, e->w_counters.as<uint32_t>());
+                                                                  pbits, hist, P, e->w_counters.as<uint32_t>(), nullptr);
     });
     if (!have) {
         HIP_OK(hipGetLastError());
@@ -1935,7 +1942,7 @@ static int submit_param_part(sentinel_engine_t *e, int64_t n, const ParamEvent *
     const unsigned ggrid = (unsigned)(((P + 7) / 8) * 8 * (1 << sbits));
     uint64_t *gval = e->w_hep.as<uint64_t>();
     const PKeyRecs RC{e->w_segep.as<unsigned long long>(), e->w_s0.as<uint2>(), e->w_k.as<int32_t>(),
-                      e->w_counters.as<uint32_t>()};
+                      e->w_counters.as<uint32_t>(), nullptr};
     const int hb = header_block_slots(e->pmax_n);
     e->launch("param_group", n, s, [&] {
         if (hb <= 2) k_pp_group<2><<<ggrid, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, pbits, sbits, ev, PR, RR, S, out, fresh, gval, RC);
@@ -1960,7 +1967,106 @@ static int submit_param_part(sentinel_engine_t *e, int64_t n, const ParamEvent *
     return 0;
 }
 
+// Single-value requests on the shared count-min sketch without namespace limiters: the partition-local
+// grouping (k_pp_prep -> scan -> k_pp_scatter -> k_pp_group, emit only), then the two-phase key walk
+// (k_pp_cm_read: every read of the batch; k_pp_cm_walk: decisions and adds; param_part.hpp).  One
+// synchronisation reads whether every sub-range fit one chunk; a batch with a sub-range over PG_CAP
+// requests (heavy skew: a key split over chunks) is decided by the per-rule lanes (submit_prules),
+// which answer the invalid requests the same way.  Returns 1 = fall back.
+static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, uint64_t *out, hipStream_t s) {
+    const int32_t R = (int32_t)e->prules.size();
+    if (R == 0 || !e->d_cmband.p) return 1;
+    int pbits = 0;
+    while (pbits < PART_MAX_BITS && ((int64_t)2 << pbits) * PD_TARGET <= n) ++pbits;
+    const int32_t P = 1 << pbits;
+    const int64_t nb = part_blocks(n), ng = (nb + PS_GROUP - 1) / PS_GROUP;
+    int rc = e->w_fhist.ensure((size_t)nb * P * 4);
+    rc |= e->w_pscan.ensure(((size_t)ng * P + 2 * (size_t)P + 1) * 4);
+    if (rc) return rc;
+    if (!e->h_cmband) HIP_OK(hipHostMalloc((void **)&e->h_cmband, 32, 0));
+    uint32_t *hist = e->w_fhist.as<uint32_t>();
+    uint32_t *gsum = e->w_pscan.as<uint32_t>();
+    uint32_t *rstart = gsum + (size_t)ng * P;
+    uint32_t *rtot = rstart + P + 1;
+    unsigned long long *flag = e->d_cmband.as<unsigned long long>();          // [0] overflow
+    long long *ctl = e->d_cmband.as<long long>() + 1;                          // [1..3] E_hi, E_hi seen, emax
+    const int32_t *route = e->param_plain ? nullptr : e->d_prule_route.as<int32_t>();
+    const ParamCtx C = e->param_ctx();
+    HIP_OK(hipMemsetAsync(flag, 0xFF, 8, s));            // cleared by k_pp_group on a sub-range overflow
+    e->launch("param_prep", n, s, [&] {
+        k_pp_prep<<<dim3((unsigned)nb), dim3(PP_THREADS), 0, s>>>(n, ev, R, route, C.R, out, pbits, hist, P,
+                                                                  e->w_counters.as<uint32_t>(), nullptr);
+    });
+    e->launch("scan", n, s, [&] {
+        const dim3 g2((unsigned)ng, (unsigned)((P + PS_THREADS - 1) / PS_THREADS));
+        k_part_colsum<<<g2, PS_THREADS, 0, s>>>(hist, nb, P, gsum);
+        k_part_colscan<<<(unsigned)((P + PC_THREADS / WAVE - 1) / (PC_THREADS / WAVE)), PC_THREADS, 0, s>>>(gsum, ng, P,
+                                                                                                          rtot);
+        k_part_offsets<<<g2, PS_THREADS, 0, s>>>(hist, nb, P, gsum, rtot, rstart);
+    });
+    unsigned long long *pkey = e->w_vtmp.as<unsigned long long>();
+    uint64_t *pval = e->w_sval.as<uint64_t>();
+    int32_t *prule = e->w_fkey.as<int32_t>();
+    e->launch("param_scatter", n, s, [&] {
+        k_pp_scatter<<<dim3((unsigned)nb), dim3(PT_THREADS), 0, s>>>(ev, n, R, route, pbits, hist, P, pkey, pval, prule);
+    });
+    if (e->prec_dirty || e->d_prule_rec.bytes < (size_t)R * sizeof(PRuleRec)) {
+        if (e->d_prule_rec.ensure((size_t)R * sizeof(PRuleRec))) return SENTINEL_E_NOMEM;
+        k_prule_pack<<<(unsigned)((R + 255) / 256), 256, 0, s>>>(R, C.R, e->d_prule_hot.p ? e->d_prule_hot.as<uint8_t>() : nullptr,
+                                                                e->d_prule_rec.as<PRuleRec>());
+        e->prec_dirty = false;
+    }
+    const PRuleRec *RR = e->d_prule_rec.as<PRuleRec>();
+    // sub-ranges of <= PG_CAP / 2 requests on average: a sub-range over PG_CAP (which sends the batch to
+    // the per-rule lanes) is then a > 2x deviation (at PG_TARGET = 0.8 PG_CAP, Zipf-heavy keys made it
+    // about one sub-range per 4M-request batch)
+    int sbits = 0;
+    while (sbits < 8 && (int64_t)P * ((int64_t)1 << sbits) * (PG_CAP / 2) < n) ++sbits;
+    const unsigned ggrid = (unsigned)(((P + 7) / 8) * 8 * (1 << sbits));
+    uint64_t *gval = e->w_hep.as<uint64_t>();
+    const PKeyRecs RC{e->w_segep.as<unsigned long long>(), e->w_s0.as<uint2>(), e->w_k.as<int32_t>(),
+                      e->w_counters.as<uint32_t>(), flag};
+    const PSlots S{};
+    e->launch("param_group", n, s, [&] {
+        k_pp_group<2, true><<<ggrid, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, pbits, sbits, ev, C.R, RR, S, out,
+                                                         nullptr, gval, RC);
+    });
+    HIP_OK(hipMemcpyAsync(e->h_cmband, flag, 8, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (e->h_cmband[0] != ~0ull) return 1;
+    const int32_t nsc = e->pmax_n;
+    int64_t *mv = e->w_sval.as<int64_t>();                // (the packed values are dead after the grouping)
+    const unsigned wg = (unsigned)std::min<int64_t>(2048, (n + 255) / 256);
+    const bool d4 = C.CM.depth <= 4;
+    e->launch("param_cm_read", n, s, [&] {
+        if (d4 && nsc <= 2) k_pp_cm_read<2, 4><<<wg, 256, 0, s>>>(RC, gval, ev, RR, C.CM, mv, ctl);
+        else if (d4 && nsc <= 4) k_pp_cm_read<4, 4><<<wg, 256, 0, s>>>(RC, gval, ev, RR, C.CM, mv, ctl);
+        else if (d4 && nsc <= 10) k_pp_cm_read<10, 4><<<wg, 256, 0, s>>>(RC, gval, ev, RR, C.CM, mv, ctl);
+        else if (d4) k_pp_cm_read<16, 4><<<wg, 256, 0, s>>>(RC, gval, ev, RR, C.CM, mv, ctl);
+        else if (nsc <= 4) k_pp_cm_read<4, 16><<<wg, 256, 0, s>>>(RC, gval, ev, RR, C.CM, mv, ctl);
+        else k_pp_cm_read<16, 16><<<wg, 256, 0, s>>>(RC, gval, ev, RR, C.CM, mv, ctl);
+    });
+    e->launch("param_cm_walk", n, s, [&] {
+        if (d4 && nsc <= 2) k_pp_cm_walk<2, 4><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, out);
+        else if (d4 && nsc <= 4) k_pp_cm_walk<4, 4><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, out);
+        else if (d4 && nsc <= 10) k_pp_cm_walk<10, 4><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, out);
+        else if (d4) k_pp_cm_walk<16, 4><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, out);
+        else if (nsc <= 4) k_pp_cm_walk<4, 16><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, out);
+        else k_pp_cm_walk<16, 16><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, out);
+    });
+    k_pp_cm_ehi<<<1, 64, 0, s>>>(ctl);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
 static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, uint64_t *out, hipStream_t s) {
+    if (e->pmode == SENTINEL_PARAM_COUNT_MIN_SHARED && e->cm_keys && n > 0 && n <= MAX_BATCH && e->pmax_n <= 16 &&
+        !(e->nlimiters > 0 && !e->param_plain)) {
+        int rc = e->ensure_ws(n);
+        if (rc) return rc;
+        rc = submit_param_cm_part(e, n, ev, out, s);
+        if (rc != 1) return rc;
+    }
     if (e->pmode != SENTINEL_PARAM_EXACT) return submit_prules(e, PMODE_CM, n, ev, nullptr, nullptr, 0, out, s);
     // per-rule walk (sort by rule, one lane per rule, each request rolls and sums its value's slot): for
     // many (rule, value) keys with a few requests each spread over many epochs, where the per-slot
@@ -2116,6 +2222,11 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
         unsigned long long span[2] = {~0ull, 0};
         HIP_OK(hipMemcpyAsync(span, lv, 16, hipMemcpyDeviceToHost, s));
         HIP_OK(hipStreamSynchronize(s));
+        if (e->d_cmband.p && span[0] != ~0ull) {         // the key walk's E_hi covers these adds too
+            long long *ctl = e->d_cmband.as<long long>() + 1;
+            k_set_i64<<<1, 64, 0, s>>>(ctl + 2, (long long)span[1]);
+            k_pp_cm_ehi<<<1, 64, 0, s>>>(ctl);
+        }
         if (span[0] != ~0ull && (int64_t)(span[1] - span[0]) < CM_LEVEL_LAUNCHES && !e->cm_force_coop) {
             const int band = e->pmax_n;                   // one launch per band of n epochs (ring of 2 n slots)
             e->launch("prule_process", n, s, [&] {
@@ -2296,7 +2407,10 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
         const std::string v(c);
         e->param_path = v == "rule" ? 1 : v == "slot" ? 2 : 0;
     }
-    if (const char *c = getenv("SENTINEL_CM_LEVELS")) e->cm_force_coop = std::string(c) == "coop";
+    if (const char *c = getenv("SENTINEL_CM_LEVELS")) {
+        e->cm_force_coop = std::string(c) == "coop";
+        e->cm_keys = std::string(c) == "keys";         // "launch" / "coop": always the per-rule lanes
+    }
     if (const char *c = getenv("SENTINEL_SCAN")) e->use_lookback = std::string(c) != "3pass";
     if (const char *c = getenv("SENTINEL_DIAG_LINEAR")) e->diag_linear = std::string(c) == "1";
     if (const char *c = getenv("SENTINEL_HOT_HET_RUN")) e->hot_het_run = (uint32_t)std::max(WAVE_HET_RUN, (uint32_t)atoi(c));
@@ -2364,6 +2478,7 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
     if (e->s_d2h) (void)hipStreamDestroy(e->s_d2h);
     if (e->h_part_stat) (void)hipHostFree(e->h_part_stat);
     if (e->h_pfresh) (void)hipHostFree(e->h_pfresh);
+    if (e->h_cmband) (void)hipHostFree(e->h_cmband);
     if (e->h_sm_ev) (void)hipHostFree(e->h_sm_ev);
     if (e->h_sm_fl) (void)hipHostFree(e->h_sm_fl);
     if (e->h_sm_out) (void)hipHostFree(e->h_sm_out);

@@ -94,9 +94,13 @@ __global__ __launch_bounds__(PP_THREADS) void k_pp_prep(int64_t n, const ParamEv
                                                          const int32_t *__restrict__ route, ParamRules PR,
                                                          uint64_t *__restrict__ out, int pbits,
                                                          uint32_t *__restrict__ hist, int32_t nparts,
-                                                         uint32_t *__restrict__ zero_word) {
+                                                         uint32_t *__restrict__ zero_word,
+                                                         unsigned long long *__restrict__ tspan) {
     __shared__ uint32_t h[PART_BINS];
+    __shared__ unsigned long long s_span[2];
     if (blockIdx.x == 0 && threadIdx.x == 0 && zero_word) *zero_word = 0;   // the batch's key-record count
+    if (threadIdx.x == 0) { s_span[0] = ~0ull; s_span[1] = ~0ull; }
+    unsigned long long tmin = ~0ull, tnmax = ~0ull;    // this thread's valid requests: min ts, min ~ts
     const int64_t tile0 = (int64_t)blockIdx.x * PT_TILE;
     ParamEvent evs[PP_ITEMS];                         // every event load of the tile in flight at once
 #pragma unroll
@@ -112,11 +116,31 @@ __global__ __launch_bounds__(PP_THREADS) void k_pp_prep(int64_t n, const ParamEv
         if (i >= n) break;
         int st = pp_status(evs[j], nrules, route);
         if (st == PP_NEG_TS) st = param_negative_ts_status(PR, (uint32_t)evs[j].idx, evs[j].key, evs[j].acquire);
-        if (st == 127) atomicAdd(&h[pp_digit(mix64(evs[j].key), pbits)], 1u);
-        else put_verdict(out, (uint32_t)i, st, 0, 0);
+        if (st == 127) {
+            atomicAdd(&h[pp_digit(mix64(evs[j].key), pbits)], 1u);
+            tmin = min(tmin, (unsigned long long)evs[j].ts);                // ts >= 0 here
+            tnmax = min(tnmax, ~(unsigned long long)evs[j].ts);
+        } else {
+            put_verdict(out, (uint32_t)i, st, 0, 0);
+        }
+    }
+    if (tspan) {                                          // (block-uniform) the batch's ts range
+#pragma unroll
+        for (int o = WAVE / 2; o > 0; o >>= 1) {
+            tmin = min(tmin, (unsigned long long)__shfl_xor(tmin, o, WAVE));
+            tnmax = min(tnmax, (unsigned long long)__shfl_xor(tnmax, o, WAVE));
+        }
+        if (lane_id() == 0 && tmin != ~0ull) {
+            atomicMin(&s_span[0], tmin);
+            atomicMin(&s_span[1], tnmax);
+        }
     }
     __syncthreads();
     for (int d = threadIdx.x; d < nparts; d += PP_THREADS) hist[(int64_t)blockIdx.x * nparts + d] = h[d];
+    if (tspan && threadIdx.x == 0 && s_span[0] != ~0ull) {
+        atomicMin(&tspan[0], s_span[0]);
+        atomicMin(&tspan[1], s_span[1]);
+    }
 }
 
 // Stable multi-split by range digit (the k_part_scatter scheme: one ballot per digit bit, wave-private
@@ -398,6 +422,7 @@ struct PKeyRecs {
     uint2 *run;              // {start, count}
     int32_t *rule;
     uint32_t *count;         // records written (zeroed by k_pp_prep)
+    unsigned long long *overflow;   // shared count-min: cleared when a sub-range exceeds one chunk (else null)
 };
 
 // k_pp_group: one workgroup per (range, sub-range): the S = 2^sbits workgroups of a range read the
@@ -409,7 +434,7 @@ struct PKeyRecs {
 // distinct key; k_pp_walk decides the keys.  A larger sub-range (a skewed batch) is decided here, chunk
 // after chunk in arrival order, one lane per distinct key of the chunk (a key spanning chunks is walked
 // once per chunk, in order).
-template <int NMAX>
+template <int NMAX, bool CM = false>
 __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long long *__restrict__ pkey,
                                                           const uint64_t *__restrict__ pval,
                                                           const int32_t *__restrict__ prule,
@@ -548,7 +573,7 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
                     RC.run[rb + q] = make_uint2(gbase + roff + hstart[e], hstart[e + 1] - hstart[e]);
                     RC.rule[rb + q] = hrule[e];
                 }
-            } else {
+            } else if constexpr (!CM) {
 #pragma unroll 1
                 for (uint32_t q = t; q < nkeys; q += PD_THREADS) {
                     const uint32_t e = klist[q];
@@ -594,6 +619,10 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
         uint32_t tile_n;
         const uint32_t off = block_exclusive_scan((uint32_t)__popc(mk), waves_tot, &tile_n);
         if (m + tile_n > PG_CAP) {                                       // the chunk is full: decide it now
+            if (CM) {                          // (block-uniform) the band walk needs one run per key: the host
+                if (t == 0) atomicAnd(RC.overflow, 0ull);             // falls back to the per-rule lanes
+                return;
+            }
             slow = true;
             chunk(false, 0);
             m = 0;
@@ -648,6 +677,224 @@ __global__ __launch_bounds__(256) void k_pp_walk(PKeyRecs RC, const uint64_t *__
         pd_walk<NMAX>(PR, RR, S, RC.key[i], RC.rule[i], gval, run.x, run.x + run.y, ev, T0, out, nfresh);
     }
     block_add_global(fresh, nfresh, &s_fresh);
+}
+
+// ---------------------------------------------------------------- shared count-min, key-parallel
+// Shared count-min sketch (SENTINEL_PARAM_COUNT_MIN_SHARED) on the grouped keys: one lane per distinct
+// (rule, value) key instead of one lane per rule, in two phases per batch.
+//
+//   k_pp_cm_read  every key's requests whose window can still hold counts of earlier batches (epoch
+//                 E < E_hi + n, E_hi = the newest epoch any earlier batch added) get
+//                 M(E) = min over the d rows of the cell's window sum, from the cells as the earlier
+//                 batches left them (nothing of this batch has been added yet: kernel boundary)
+//   k_pp_cm_walk  one lane per key walks its requests in arrival order with the key's own admitted
+//                 counts of this batch in a register window ({epoch, count} x n, as the exact walk):
+//                 est = M(E) + own window sum, R = (T_v - est / I_s) - a, pass iff !(R < 0)
+//                 (cm_check_sync for one value); each own epoch's count is added to the key's d cells
+//                 when it leaves the register window or the walk ends
+//
+// est >= the key's exact window count (its earlier-batch counts are in every row's cell, its own
+// counts of this batch are in the register window), so the sketch stays one-sided; other keys' counts
+// of this batch are not seen (fewer false blocks than a sequential sketch).  Because every read of the
+// batch precedes every add, a ring-slot reset by an add (epoch E' restarting the slot of E' - 2n) can
+// no longer remove a count somebody still reads: no bands, no grid barriers, and a batch's verdicts
+// depend only on the cells as the earlier batches left them (the adds' order only decides which epoch
+// a colliding slot is tagged with when two keys' epochs 2n apart meet in it; the count is kept either
+// way).  Precondition, as for the per-rule lanes: the requests' clock does not go back across batches
+// (the server's one clock: TimeUtil.currentTimeMillis).
+constexpr int64_t CM_EHI_NONE = INT64_MIN;       // no earlier batch added anything (cleared cells)
+constexpr int64_t CM_EHI_ANY = INT64_MAX;        // unknown (the per-rule lanes ran): always read
+
+template <int NMAX>
+__device__ inline int64_t cm_cell_sum_vec(const uint64_t *c, int nsc, int64_t E) {
+    const ulonglong2 *c2 = reinterpret_cast<const ulonglong2 *>(c);   // 2 n slots, 16-B aligned (n words x 16)
+    ulonglong2 x[NMAX];
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) x[j] = j < nsc ? c2[j] : make_ulonglong2(0ull, 0ull);
+    int64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+        if (j >= nsc) break;
+        const uint32_t ta = (uint32_t)(x[j].x >> CM_COUNT_BITS), tb = (uint32_t)(x[j].y >> CM_COUNT_BITS);
+        if ((((uint32_t)E - ta) & CM_TAG_MASK) < (uint32_t)nsc) s += (int64_t)(x[j].x & CM_COUNT_MAX);
+        if ((((uint32_t)E - tb) & CM_TAG_MASK) < (uint32_t)nsc) s += (int64_t)(x[j].y & CM_COUNT_MAX);
+    }
+    return s;
+}
+
+__device__ inline bool cm_needs_read(int64_t E, int64_t ehi, int nsc) {
+    if (ehi == CM_EHI_NONE) return false;
+    if (ehi == CM_EHI_ANY) return true;
+    return E < ehi + nsc;
+}
+
+// ctl: [0] E_hi (newest epoch added by earlier batches), [1] E_hi as this batch's read saw it,
+// [2] this batch's newest request epoch (atomicMax by the walk)
+template <int NMAX, int DMAX>
+__global__ __launch_bounds__(256) void k_pp_cm_read(PKeyRecs RC, const uint64_t *__restrict__ gval,
+                                                     const ParamEvent *__restrict__ ev,
+                                                     const PRuleRec *__restrict__ RR, CountMin CM,
+                                                     int64_t *__restrict__ mv, long long *__restrict__ ctl) {
+    const uint32_t nrec = *RC.count;
+    const int64_t T0 = pp_t0(ev);
+    const int64_t ehi = ctl[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctl[1] = ehi;
+        ctl[2] = CM_EHI_NONE;
+    }
+    if (ehi == CM_EHI_NONE) return;                       // (grid-uniform) nothing to read
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nrec; i += gridDim.x * blockDim.x) {
+        const uint2 run = RC.run[i];
+        const PRuleRec rr = RR[RC.rule[i]];
+        const int nsc = rr.nf & 0xFFFF;
+        const unsigned long long key = RC.key[i];
+        int64_t lastE = 0, lastM = 0;
+        bool have = false;
+#pragma unroll 1
+        for (uint32_t q = run.x; q < run.x + run.y; ++q) {
+            int64_t t;
+            int32_t a;
+            pp_unpack(gval[q], T0, ev, t, a);
+            const int64_t E = epoch_of(t, rr.w, rr.rcp_w);
+#ifdef SENTINEL_DIAG_CM_BREAK                             // cost diagnostic only (assumes monotone runs)
+            if (!cm_needs_read(E, ehi, nsc)) break;
+#endif
+            if (!cm_needs_read(E, ehi, nsc)) continue;
+            if (!have || E != lastE) {
+#ifdef SENTINEL_DIAG_CM_NOREAD                            // cost diagnostic only (wrong estimates)
+                int64_t m = 0;
+#else
+                int64_t m = INT64_MAX;
+#endif
+#ifndef SENTINEL_DIAG_CM_NOREAD
+#pragma unroll
+                for (int d = 0; d < DMAX; ++d) {
+                    if (d >= CM.depth) break;
+                    const int64_t x = cm_cell_sum_vec<NMAX>(cm_cell(CM, 0, d, key), nsc, E);
+                    m = x < m ? x : m;
+                }
+#endif
+                lastE = E;
+                lastM = m;
+                have = true;
+            }
+            mv[q] = lastM;
+        }
+    }
+}
+
+template <int DMAX>
+__device__ inline void cm_flush(const CountMin &CM, unsigned long long key, int nsc, int64_t E, int64_t a) {
+#ifdef SENTINEL_DIAG_CM_NOADD                             // cost diagnostic only (wrong counters)
+    return;
+#endif
+    const int js = (int)(E % (2 * nsc));
+    const uint32_t te = (uint32_t)E & CM_TAG_MASK;
+    unsigned long long *c[DMAX];
+    unsigned long long x[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {                      // every row's first CAS in flight at once
+        if (d >= CM.depth) break;
+        c[d] = reinterpret_cast<unsigned long long *>(cm_cell(CM, 0, d, key) + js);
+        x[d] = atomicCAS(c[d], 0ull, ((unsigned long long)te << CM_COUNT_BITS) |
+                                     (unsigned long long)((uint64_t)a > CM_COUNT_MAX ? CM_COUNT_MAX : (uint64_t)a));
+    }
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+        if (d >= CM.depth) break;
+        if (x[d] != 0ull) cm_slot_add(c[d], x[d], te, a);   // the slot was not empty: read-modify-write
+    }
+}
+
+template <int NMAX, int DMAX>
+__global__ __launch_bounds__(256) void k_pp_cm_walk(PKeyRecs RC, const uint64_t *__restrict__ gval,
+                                                     const ParamEvent *__restrict__ ev, ParamRules PR,
+                                                     const PRuleRec *__restrict__ RR, CountMin CM,
+                                                     const int64_t *__restrict__ mv, long long *__restrict__ ctl,
+                                                     uint64_t *__restrict__ out) {
+    const uint32_t nrec = *RC.count;
+    const int64_t T0 = pp_t0(ev);
+    const int64_t ehi = ctl[1];
+    int64_t emax = CM_EHI_NONE;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nrec; i += gridDim.x * blockDim.x) {
+        const uint2 run = RC.run[i];
+        const int32_t rule = RC.rule[i];
+        const PRuleRec rr = RR[rule];
+        const int nsc = rr.nf & 0xFFFF;
+        const unsigned long long key = RC.key[i];
+        const double thr = (rr.nf >> 16) ? value_threshold(PR, (uint32_t)rule, key) : rr.thr;   // CPFC:101-120
+        const double rcpn = 1.0 / (double)nsc;
+        int64_t ep[NMAX], ct[NMAX];                       // this batch's own admitted counts per epoch
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j) { ep[j] = EPOCH_ABSENT; ct[j] = 0; }
+        int64_t curE = EPOCH_ABSENT, own = 0;
+        int slot = 0;
+#pragma unroll 1
+        for (uint32_t q = run.x; q < run.x + run.y; ++q) {
+            const uint64_t v = gval[q];
+            int64_t t;
+            int32_t a;
+            pp_unpack(v, T0, ev, t, a);
+            const int64_t E = epoch_of(t, rr.w, rr.rcp_w);
+            emax = E > emax ? E : emax;
+            const bool late = curE != EPOCH_ABSENT && E < curE;   // (outside the precondition)
+            int64_t mine = own;
+            if (late) {                                   // every own count that may be in its window (and newer:
+                mine = 0;                                 // over-counts, never under); its add goes to curE's slot
+#pragma unroll
+                for (int j = 0; j < NMAX; ++j)
+                    if (ep[j] != EPOCH_ABSENT && ep[j] > E - nsc) mine += ct[j];
+            } else if (E != curE) {
+                curE = E;
+                slot = (int)(E - epoch_of(E, nsc, rcpn) * nsc);
+#pragma unroll
+                for (int j = 0; j < NMAX; ++j) {
+                    if (j != slot || ep[j] == E) continue;
+                    if (ct[j] > 0) cm_flush<DMAX>(CM, key, nsc, ep[j], ct[j]);   // leaves the register window
+                    ep[j] = E;
+                    ct[j] = 0;
+                }
+                own = 0;                                  // own counts inside the window (E - n, E]
+#pragma unroll
+                for (int j = 0; j < NMAX; ++j)
+                    if (ep[j] != EPOCH_ABSENT && ep[j] > E - nsc) own += ct[j];
+                mine = own;
+            }
+            const int64_t m = cm_needs_read(E, ehi, nsc) ? mv[q] : 0;
+            const double next = remaining_of(thr, rr.I_s, m + mine, a);
+            uint64_t vd;
+            if (!(next < 0.0)) {                                          // CPFC:64-66, then addValue
+#pragma unroll
+                for (int j = 0; j < NMAX; ++j)
+                    if (j == slot) ct[j] += a;
+                own += a;
+                vd = pack_verdict(ST_OK, java_d2i(next), 0);
+            } else {
+                vd = pack_verdict(ST_BLOCKED, 0, 0);
+            }
+            store_verdict(out, (uint32_t)v & SEQ_MASK, vd);
+        }
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j)
+            if (ct[j] > 0) cm_flush<DMAX>(CM, key, nsc, ep[j], ct[j]);
+    }
+    // the batch's newest epoch -> E_hi for the next batch's reads (ctl[0] is read by k_pp_cm_read only)
+    for (int o = WAVE / 2; o > 0; o >>= 1) {
+        const int64_t y = __shfl_xor(emax, o, WAVE);
+        emax = y > emax ? y : emax;
+    }
+    if (lane_id() == 0 && emax != CM_EHI_NONE) atomicMax(reinterpret_cast<long long *>(&ctl[2]), (long long)emax);
+}
+
+// E_hi <- max(E_hi, this batch's newest epoch) (after k_pp_cm_walk); CM_EHI_ANY stays.
+__global__ void k_pp_cm_ehi(long long *ctl) {
+    if (threadIdx.x != 0) return;
+    const long long e = ctl[2], h = ctl[0];
+    if (h != CM_EHI_ANY && e != CM_EHI_NONE && (h == CM_EHI_NONE || e > h)) ctl[0] = e;
+}
+
+__global__ void k_set_i64(long long *p, long long v) {
+    if (threadIdx.x == 0) *p = v;
 }
 
 }  // namespace sentinel

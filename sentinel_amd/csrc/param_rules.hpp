@@ -356,26 +356,30 @@ __device__ inline int64_t cm_cell_sum_sync(const uint64_t *c, int nsc, int64_t E
     return s;
 }
 
-// Add a to the slot of E in every row: same tag -> add (saturating), an older tag -> restart at a, a
-// newer tag (only past the precondition: a rule's clock went back) -> add to the newer slot.
-__device__ inline void cm_add_sync(const CountMin &C, uint32_t rule, uint64_t key, int nsc, int64_t E, int32_t a) {
+// Add a to one cell slot of epoch E (te = its tag): same tag -> add (saturating), an older tag -> restart
+// at a, a newer tag (only past the precondition: a rule's clock went back) -> add to the newer slot.
+// `x` = the caller's guess of the slot's current word (a failed CAS returns the real one).
+__device__ inline void cm_slot_add(unsigned long long *c, unsigned long long x, uint32_t te, int64_t a) {
+    for (;;) {
+        const uint32_t tag = (uint32_t)(x >> CM_COUNT_BITS);
+        // (an empty cell, count 0, has no epoch: its tag bits mean nothing)
+        const bool newer = (x & CM_COUNT_MAX) != 0 && tag != te && ((tag - te) & CM_TAG_MASK) < (CM_TAG_MASK >> 1);
+        uint64_t cnt = (tag == te || newer) ? (x & CM_COUNT_MAX) : 0;
+        cnt = (uint64_t)a > CM_COUNT_MAX - cnt ? CM_COUNT_MAX : cnt + (uint64_t)a;   // (a >= 0)
+        const unsigned long long y = ((unsigned long long)(newer ? tag : te) << CM_COUNT_BITS) | cnt;
+        const unsigned long long prev = atomicCAS(c, x, y);
+        if (prev == x) break;
+        x = prev;
+    }
+}
+
+// Add a to the slot of E in every row.
+__device__ inline void cm_add_sync(const CountMin &C, uint32_t rule, uint64_t key, int nsc, int64_t E, int64_t a) {
     const int j = (int)(E % (2 * nsc));
     const uint32_t te = (uint32_t)E & CM_TAG_MASK;
     for (int d = 0; d < C.depth; ++d) {
         unsigned long long *c = reinterpret_cast<unsigned long long *>(cm_cell(C, rule, d, key) + j);
-        unsigned long long x = cm_load(reinterpret_cast<const uint64_t *>(c));
-        for (;;) {
-            const uint32_t tag = (uint32_t)(x >> CM_COUNT_BITS);
-            // (an empty cell, count 0, has no epoch: its tag bits mean nothing)
-            const bool newer = (x & CM_COUNT_MAX) != 0 && tag != te && ((tag - te) & CM_TAG_MASK) < (CM_TAG_MASK >> 1);
-            uint64_t cnt = (tag == te || newer) ? (x & CM_COUNT_MAX) : 0;
-            cnt += (uint64_t)(uint32_t)a;
-            if (cnt > CM_COUNT_MAX) cnt = CM_COUNT_MAX;
-            const unsigned long long y = ((unsigned long long)(newer ? tag : te) << CM_COUNT_BITS) | cnt;
-            const unsigned long long prev = atomicCAS(c, x, y);
-            if (prev == x) break;
-            x = prev;
-        }
+        cm_slot_add(c, cm_load(reinterpret_cast<const uint64_t *>(c)), te, a);
     }
 }
 

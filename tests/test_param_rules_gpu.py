@@ -137,14 +137,16 @@ def test_count_min_is_one_sided(oracle_mod):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("levels", ["launch", "coop"])
+@pytest.mark.parametrize("levels", ["keys", "launch", "coop"])
 def test_shared_count_min_is_one_sided(oracle_mod, monkeypatch, levels):
     """One sketch for every rule (BASELINE config 4's layout), narrow enough that rules collide, on
-    batches spanning ~75 epochs: the rules' lanes move through the epochs together (k_prule_cm_sync),
-    so no lane's reset of a shared cell slot drops a count a lagging rule still needs -- zero
-    violations of one-sidedness, and the false-block rate shrinks with the width."""
+    batches spanning ~75 epochs: the lanes move through the epochs together, band by band (one lane
+    per (rule, value) key: k_pp_cm_band; one lane per rule: k_prule_cm_level / k_prule_cm_sync), so no
+    lane's reset of a shared cell slot drops a count a lagging lane still needs -- zero violations of
+    one-sidedness, and the false-block rate shrinks with the width."""
     import sentinel_amd as sa
-    monkeypatch.setenv("SENTINEL_CM_LEVELS", levels)      # one launch per epoch level, or the grid barrier
+    # key-parallel bands (the default), one launch per band of rule lanes, or the grid barrier
+    monkeypatch.setenv("SENTINEL_CM_LEVELS", levels)
     count, hot, rule_idx, vals, keys, ts = T.config4(200_000, seed=53, n_rules=5000, universe=200)
     acq = np.ones(len(ts), np.int32)
     rates = {}
