@@ -1992,7 +1992,7 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
     long long *ctl = e->d_cmband.as<long long>() + 1;                          // [1..3] E_hi, E_hi seen, emax
     const int32_t *route = e->param_plain ? nullptr : e->d_prule_route.as<int32_t>();
     const ParamCtx C = e->param_ctx();
-    HIP_OK(hipMemsetAsync(flag, 0xFF, 8, s));            // cleared by k_pp_group on a sub-range overflow
+    HIP_OK(hipMemsetAsync(flag, 0, 8, s));               // set by k_pp_group on a sub-range overflow
     e->launch("param_prep", n, s, [&] {
         k_pp_prep<<<dim3((unsigned)nb), dim3(PP_THREADS), 0, s>>>(n, ev, R, route, C.R, out, pbits, hist, P,
                                                                   e->w_counters.as<uint32_t>(), nullptr);
@@ -2033,7 +2033,7 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
     });
     HIP_OK(hipMemcpyAsync(e->h_cmband, flag, 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    if (e->h_cmband[0] != ~0ull) return 1;
+    if (e->h_cmband[0] != 0ull) return 1;
     const int32_t nsc = e->pmax_n;
     int64_t *mv = e->w_sval.as<int64_t>();                // (the packed values are dead after the grouping)
     const unsigned wg = (unsigned)std::min<int64_t>(2048, (n + 255) / 256);

@@ -422,7 +422,7 @@ struct PKeyRecs {
     uint2 *run;              // {start, count}
     int32_t *rule;
     uint32_t *count;         // records written (zeroed by k_pp_prep)
-    unsigned long long *overflow;   // shared count-min: cleared when a sub-range exceeds one chunk (else null)
+    unsigned long long *overflow;   // shared count-min: set when a sub-range exceeds one chunk (else null)
 };
 
 // k_pp_group: one workgroup per (range, sub-range): the S = 2^sbits workgroups of a range read the
@@ -619,8 +619,8 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
         uint32_t tile_n;
         const uint32_t off = block_exclusive_scan((uint32_t)__popc(mk), waves_tot, &tile_n);
         if (m + tile_n > PG_CAP) {                                       // the chunk is full: decide it now
-            if (CM) {                          // (block-uniform) the band walk needs one run per key: the host
-                if (t == 0) atomicAnd(RC.overflow, 0ull);             // falls back to the per-rule lanes
+            if (CM) {                          // (block-uniform) the key walk needs one run per key: the host
+                if (t == 0) atomicOr(RC.overflow, 1ull);              // falls back to the per-rule lanes
                 return;
             }
             slow = true;
@@ -705,21 +705,43 @@ __global__ __launch_bounds__(256) void k_pp_walk(PKeyRecs RC, const uint64_t *__
 constexpr int64_t CM_EHI_NONE = INT64_MIN;       // no earlier batch added anything (cleared cells)
 constexpr int64_t CM_EHI_ANY = INT64_MAX;        // unknown (the per-rule lanes ran): always read
 
-template <int NMAX>
-__device__ inline int64_t cm_cell_sum_vec(const uint64_t *c, int nsc, int64_t E) {
-    const ulonglong2 *c2 = reinterpret_cast<const ulonglong2 *>(c);   // 2 n slots, 16-B aligned (n words x 16)
-    ulonglong2 x[NMAX];
+// min over the d rows of the cell's window sum at E, reading only the n ring slots of the epochs
+// (E - n, E] (contiguous modulo 2 n: one or two lines per row instead of the whole 2 n ring), every
+// row's loads in flight at once.  Plain loads: nothing of this batch has been added yet.
+template <int NMAX, int DMAX>
+__device__ inline int64_t cm_window_min(const CountMin &CM, unsigned long long key, int nsc, int64_t E) {
+    constexpr int DR = DMAX < 4 ? DMAX : 4;               // rows per round (<= 4 x NMAX words in flight)
+    const int slots = 2 * nsc;
+    const int j0 = (int)((E + 1) % slots);                // slot of epoch E - n + 1 (= E + 1 - 2n + n)
+    const int first = (j0 + nsc) % slots;                 // (E - n + 1) mod 2n
+    int64_t m = INT64_MAX;
+    for (int d0 = 0; d0 < CM.depth; d0 += DR) {
+        uint64_t x[DR][NMAX];
 #pragma unroll
-    for (int j = 0; j < NMAX; ++j) x[j] = j < nsc ? c2[j] : make_ulonglong2(0ull, 0ull);
-    int64_t s = 0;
+        for (int r = 0; r < DR; ++r) {
+            const bool on = d0 + r < CM.depth;
+            const uint64_t *c = on ? cm_cell(CM, 0, d0 + r, key) : CM.cells;
 #pragma unroll
-    for (int j = 0; j < NMAX; ++j) {
-        if (j >= nsc) break;
-        const uint32_t ta = (uint32_t)(x[j].x >> CM_COUNT_BITS), tb = (uint32_t)(x[j].y >> CM_COUNT_BITS);
-        if ((((uint32_t)E - ta) & CM_TAG_MASK) < (uint32_t)nsc) s += (int64_t)(x[j].x & CM_COUNT_MAX);
-        if ((((uint32_t)E - tb) & CM_TAG_MASK) < (uint32_t)nsc) s += (int64_t)(x[j].y & CM_COUNT_MAX);
+            for (int k = 0; k < NMAX; ++k) {
+                int j = first + k;
+                j = j >= slots ? j - slots : j;
+                x[r][k] = (on && k < nsc) ? c[j] : 0ull;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < DR; ++r) {
+            if (d0 + r >= CM.depth) break;
+            int64_t sum = 0;
+#pragma unroll
+            for (int k = 0; k < NMAX; ++k) {
+                if (k >= nsc) break;
+                const uint32_t tag = (uint32_t)(x[r][k] >> CM_COUNT_BITS);
+                if ((((uint32_t)E - tag) & CM_TAG_MASK) < (uint32_t)nsc) sum += (int64_t)(x[r][k] & CM_COUNT_MAX);
+            }
+            m = sum < m ? sum : m;
+        }
     }
-    return s;
+    return m;
 }
 
 __device__ inline bool cm_needs_read(int64_t E, int64_t ehi, int nsc) {
@@ -735,7 +757,6 @@ __global__ __launch_bounds__(256) void k_pp_cm_read(PKeyRecs RC, const uint64_t 
                                                      const ParamEvent *__restrict__ ev,
                                                      const PRuleRec *__restrict__ RR, CountMin CM,
                                                      int64_t *__restrict__ mv, long long *__restrict__ ctl) {
-    const uint32_t nrec = *RC.count;
     const int64_t T0 = pp_t0(ev);
     const int64_t ehi = ctl[0];
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -743,6 +764,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_read(PKeyRecs RC, const uint64_t 
         ctl[2] = CM_EHI_NONE;
     }
     if (ehi == CM_EHI_NONE) return;                       // (grid-uniform) nothing to read
+    const uint32_t nrec = *RC.count;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nrec; i += gridDim.x * blockDim.x) {
         const uint2 run = RC.run[i];
         const PRuleRec rr = RR[RC.rule[i]];
@@ -767,12 +789,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_read(PKeyRecs RC, const uint64_t 
                 int64_t m = INT64_MAX;
 #endif
 #ifndef SENTINEL_DIAG_CM_NOREAD
-#pragma unroll
-                for (int d = 0; d < DMAX; ++d) {
-                    if (d >= CM.depth) break;
-                    const int64_t x = cm_cell_sum_vec<NMAX>(cm_cell(CM, 0, d, key), nsc, E);
-                    m = x < m ? x : m;
-                }
+                m = cm_window_min<NMAX, DMAX>(CM, key, nsc, E);
 #endif
                 lastE = E;
                 lastM = m;
@@ -796,13 +813,12 @@ __device__ inline void cm_flush(const CountMin &CM, unsigned long long key, int 
     for (int d = 0; d < DMAX; ++d) {                      // every row's first CAS in flight at once
         if (d >= CM.depth) break;
         c[d] = reinterpret_cast<unsigned long long *>(cm_cell(CM, 0, d, key) + js);
-        x[d] = atomicCAS(c[d], 0ull, ((unsigned long long)te << CM_COUNT_BITS) |
-                                     (unsigned long long)((uint64_t)a > CM_COUNT_MAX ? CM_COUNT_MAX : (uint64_t)a));
-    }
+        x[d] = *c[d];                                     // a plain load as the CAS's guess (atomics run at the
+    }                                                     // memory side: one CAS instead of a failed one + retry)
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) {
         if (d >= CM.depth) break;
-        if (x[d] != 0ull) cm_slot_add(c[d], x[d], te, a);   // the slot was not empty: read-modify-write
+        cm_slot_add(c[d], x[d], te, a);
     }
 }
 
@@ -812,10 +828,10 @@ __global__ __launch_bounds__(256) void k_pp_cm_walk(PKeyRecs RC, const uint64_t 
                                                      const PRuleRec *__restrict__ RR, CountMin CM,
                                                      const int64_t *__restrict__ mv, long long *__restrict__ ctl,
                                                      uint64_t *__restrict__ out) {
-    const uint32_t nrec = *RC.count;
     const int64_t T0 = pp_t0(ev);
     const int64_t ehi = ctl[1];
     int64_t emax = CM_EHI_NONE;
+    const uint32_t nrec = *RC.count;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nrec; i += gridDim.x * blockDim.x) {
         const uint2 run = RC.run[i];
         const int32_t rule = RC.rule[i];
