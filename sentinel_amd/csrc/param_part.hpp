@@ -705,27 +705,30 @@ __global__ __launch_bounds__(256) void k_pp_walk(PKeyRecs RC, const uint64_t *__
 constexpr int64_t CM_EHI_NONE = INT64_MIN;       // no earlier batch added anything (cleared cells)
 constexpr int64_t CM_EHI_ANY = INT64_MAX;        // unknown (the per-rule lanes ran): always read
 
-// min over the d rows of the cell's window sum at E, reading only the n ring slots of the epochs
-// (E - n, E] (contiguous modulo 2 n: one or two lines per row instead of the whole 2 n ring), every
-// row's loads in flight at once.  Plain loads: nothing of this batch has been added yet.
+// min over the d rows of the cell's window sum at E, reading only the ring slots of the epochs
+// (E - n, E]: n / 2 + 1 aligned 16-byte pairs (contiguous modulo the ring: one or two lines per row
+// instead of the whole 2 n ring; the one or two extra slots hold epochs outside the window and fail
+// the tag test), every row's loads in flight at once.  Plain loads: nothing of this batch has been
+// added yet.
 template <int NMAX, int DMAX>
 __device__ inline int64_t cm_window_min(const CountMin &CM, unsigned long long key, int nsc, int64_t E) {
-    constexpr int DR = DMAX < 4 ? DMAX : 4;               // rows per round (<= 4 x NMAX words in flight)
-    const int slots = 2 * nsc;
-    const int j0 = (int)((E + 1) % slots);                // slot of epoch E - n + 1 (= E + 1 - 2n + n)
-    const int first = (j0 + nsc) % slots;                 // (E - n + 1) mod 2n
+    constexpr int DR = DMAX < 4 ? DMAX : 4;               // rows per round
+    constexpr int NP = NMAX / 2 + 1;                      // pairs per row, at most
+    const int np = nsc / 2 + 1 < nsc ? nsc / 2 + 1 : nsc; // (the ring holds nsc pairs)
+    const int first = (int)((E + 1 + nsc) % (2 * nsc));  // slot of epoch E - n + 1
+    const int p0 = first >> 1;
     int64_t m = INT64_MAX;
     for (int d0 = 0; d0 < CM.depth; d0 += DR) {
-        uint64_t x[DR][NMAX];
+        ulonglong2 x[DR][NP];
 #pragma unroll
         for (int r = 0; r < DR; ++r) {
             const bool on = d0 + r < CM.depth;
-            const uint64_t *c = on ? cm_cell(CM, 0, d0 + r, key) : CM.cells;
+            const ulonglong2 *c = reinterpret_cast<const ulonglong2 *>(on ? cm_cell(CM, 0, d0 + r, key) : CM.cells);
 #pragma unroll
-            for (int k = 0; k < NMAX; ++k) {
-                int j = first + k;
-                j = j >= slots ? j - slots : j;
-                x[r][k] = (on && k < nsc) ? c[j] : 0ull;
+            for (int k = 0; k < NP; ++k) {
+                int pk = p0 + k;
+                pk = pk >= nsc ? pk - nsc : pk;
+                x[r][k] = (on && k < np) ? c[pk] : make_ulonglong2(0ull, 0ull);
             }
         }
 #pragma unroll
@@ -733,10 +736,11 @@ __device__ inline int64_t cm_window_min(const CountMin &CM, unsigned long long k
             if (d0 + r >= CM.depth) break;
             int64_t sum = 0;
 #pragma unroll
-            for (int k = 0; k < NMAX; ++k) {
-                if (k >= nsc) break;
-                const uint32_t tag = (uint32_t)(x[r][k] >> CM_COUNT_BITS);
-                if ((((uint32_t)E - tag) & CM_TAG_MASK) < (uint32_t)nsc) sum += (int64_t)(x[r][k] & CM_COUNT_MAX);
+            for (int k = 0; k < NP; ++k) {
+                if (k >= np) break;
+                const uint32_t ta = (uint32_t)(x[r][k].x >> CM_COUNT_BITS), tb = (uint32_t)(x[r][k].y >> CM_COUNT_BITS);
+                if ((((uint32_t)E - ta) & CM_TAG_MASK) < (uint32_t)nsc) sum += (int64_t)(x[r][k].x & CM_COUNT_MAX);
+                if ((((uint32_t)E - tb) & CM_TAG_MASK) < (uint32_t)nsc) sum += (int64_t)(x[r][k].y & CM_COUNT_MAX);
             }
             m = sum < m ? sum : m;
         }
