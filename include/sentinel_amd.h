@@ -242,7 +242,10 @@ int  sentinel_submit_param_multi_batch_host(sentinel_engine_t *eng, int64_t n, c
 /* One depth x width sketch for every param rule (keys are unique per (rule, value)): memory
  * independent of the rule count; the bound is (e / width) x (the total window count of all rules).
  * Needs one window (sampleCount, intervalMs) for every param rule: a per-rule window could reset a
- * cell slot another rule's window still counts. */
+ * cell slot another rule's window still counts.  Single-value batches are decided one (rule, value)
+ * key per lane: a request's estimate is the cells as the earlier batches left them plus its own key's
+ * admitted count in this batch (other keys' counts of the same batch are added after it), still never
+ * below the exact count; precondition: request timestamps do not go back across batches. */
 #define SENTINEL_PARAM_COUNT_MIN_SHARED  2
 int  sentinel_set_param_mode(sentinel_engine_t *eng, int32_t mode, int32_t depth, int32_t width);
 
