@@ -592,9 +592,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # SENTINEL_BENCH_ONE_DEVICE=1: every rank on cuda:0 over gloo -- a rehearsal of the N-rank path on a
+    # one-GPU box (sharding, barriers, max-over-ranks timing, the snapshot all-gathers); never a result
+    one_dev = os.environ.get("SENTINEL_BENCH_ONE_DEVICE") == "1"
+    if one_dev:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if one_dev:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
     if args.config in ("4", "4cm"):
@@ -669,7 +677,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    el = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if one_dev else dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())

@@ -60,6 +60,8 @@ def gather_records(local, group=None):
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
+    if dist.get_backend(group) == "gloo" and local.is_cuda:   # (gloo gathers host tensors)
+        return gather_records(local.cpu(), group).to(local.device)
     n = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
