@@ -69,6 +69,28 @@ __device__ inline void pp_unpack(uint64_t v, int64_t T0, const ParamEvent *ev, i
     a = (int32_t)af;
 }
 
+// A key's run of grouped values read 4 ahead of its walk (a run is walked one request after the other;
+// without the look-ahead every request waits for its own load: a hot key's run is a chain of round trips).
+// Used by the count-min kernels (walk 1520 -> 1470 us); the exact walk measured no gain (551 vs 574 us).
+struct RunQueue {
+    const uint64_t *p;
+    uint32_t q, end;
+    uint64_t b[4];
+    __device__ inline RunQueue(const uint64_t *src, uint32_t q0, uint32_t q1) : p(src), q(q0), end(q1) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) b[k] = q0 + k < q1 ? p[q0 + k] : 0ull;
+    }
+    __device__ inline uint64_t next() {                 // the value at q (caller checks q < end), then q + 1
+        const uint64_t v = b[0];
+        b[0] = b[1];
+        b[1] = b[2];
+        b[2] = b[3];
+        b[3] = q + 4 < end ? p[q + 4] : 0ull;
+        ++q;
+        return v;
+    }
+};
+
 // Range digit of a param key: the top pbits of its hash (the HBM slot uses the low bits, the LDS
 // table bits [32, 32 + PD_HBITS)).
 __device__ inline uint32_t pp_digit(uint64_t h, int pbits) {
@@ -776,11 +798,12 @@ __global__ __launch_bounds__(256) void k_pp_cm_read(PKeyRecs RC, const uint64_t 
         const unsigned long long key = RC.key[i];
         int64_t lastE = 0, lastM = 0;
         bool have = false;
+        RunQueue rq(gval, run.x, run.x + run.y);
 #pragma unroll 1
         for (uint32_t q = run.x; q < run.x + run.y; ++q) {
             int64_t t;
             int32_t a;
-            pp_unpack(gval[q], T0, ev, t, a);
+            pp_unpack(rq.next(), T0, ev, t, a);
             const int64_t E = epoch_of(t, rr.w, rr.rcp_w);
 #ifdef SENTINEL_DIAG_CM_BREAK                             // cost diagnostic only (assumes monotone runs)
             if (!cm_needs_read(E, ehi, nsc)) break;
@@ -849,9 +872,10 @@ __global__ __launch_bounds__(256) void k_pp_cm_walk(PKeyRecs RC, const uint64_t 
         for (int j = 0; j < NMAX; ++j) { ep[j] = EPOCH_ABSENT; ct[j] = 0; }
         int64_t curE = EPOCH_ABSENT, own = 0;
         int slot = 0;
+        RunQueue rq(gval, run.x, run.x + run.y);
 #pragma unroll 1
         for (uint32_t q = run.x; q < run.x + run.y; ++q) {
-            const uint64_t v = gval[q];
+            const uint64_t v = rq.next();
             int64_t t;
             int32_t a;
             pp_unpack(v, T0, ev, t, a);
