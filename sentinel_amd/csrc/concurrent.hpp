@@ -655,6 +655,33 @@ __global__ __launch_bounds__(CB_THREADS) void k_conc_chunks(ConcCtx C, const uin
     }
 }
 
+// Tombstone sweep of the whole token cache (between batches): a tombstone whose successor slot is empty
+// ends no probe chain (every cached token's chain from its home slot is unbroken, so it cannot pass
+// through a slot followed by an empty one), so it may become empty itself, and so may the tombstones
+// right before it.  Nothing is inserted during the sweep, so an empty successor stays empty.  Run when the
+// host's bound on live + tombstones nears the compaction threshold: at a low load factor most released
+// tokens sit alone in their cluster, so the sweep (one coalesced pass over the keys) usually makes the
+// compaction (a rehash of every live token into a new table) unnecessary.
+__global__ __launch_bounds__(256) void k_tok_sweep(TokenTable TT) {
+    __shared__ unsigned long long s_freed;
+    if (threadIdx.x == 0) s_freed = 0;
+    __syncthreads();
+    uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long freed = 0;
+    if (h <= TT.mask && TT.keys[h] == TOKEN_TOMB && TT.keys[(h + 1) & TT.mask] == PKEY_EMPTY) {
+        for (int k = 0; k < 256; ++k) {                   // (bounded walk back)
+            if (atomicCAS(&TT.keys[h], (unsigned long long)TOKEN_TOMB, (unsigned long long)PKEY_EMPTY) != TOKEN_TOMB)
+                break;
+            ++freed;
+            h = (h - 1) & TT.mask;
+            if (TT.keys[h] != TOKEN_TOMB) break;
+        }
+    }
+    if (freed) atomicAdd(&s_freed, freed);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_freed) atomicAdd(&TT.counts[1], 0ull - s_freed);
+}
+
 // RegularExpireStrategy.clearToken (RegularExpireStrategy.java:94-124): with the reference's own
 // conditions every cached token qualifies (clientTimeout / resourceTimeout are durations compared
 // with the wall clock), so a sweep removes up to `max_tokens` tokens and returns their counts to

@@ -3763,6 +3763,13 @@ static int submit_concurrent(sentinel_engine_t *e, int64_t n, const ConcEvent *d
         unsigned long long counts[2];
         HIP_OK(hipMemcpy(counts, e->d_tok_counts.p, 16, hipMemcpyDeviceToHost));
         e->tok_ub = counts[0] + counts[1];
+        if ((double)(e->tok_ub + (uint64_t)n) > 0.75 * (double)e->tcap && counts[1] > 0) {
+            // first the tombstone sweep (one pass over the keys), then the counts again
+            k_tok_sweep<<<(unsigned)((e->tcap + 255) / 256), 256, 0, e->stream>>>(e->token_table());
+            HIP_OK(hipMemcpyAsync(counts, e->d_tok_counts.p, 16, hipMemcpyDeviceToHost, e->stream));
+            HIP_OK(hipStreamSynchronize(e->stream));
+            e->tok_ub = counts[0] + counts[1];
+        }
         if ((double)(e->tok_ub + (uint64_t)n) > 0.75 * (double)e->tcap) {
             // drop the tombstones, and grow until the live tokens plus a few batches fit
             uint64_t nc = e->tcap;

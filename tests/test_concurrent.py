@@ -67,9 +67,15 @@ def test_gpu_reference_sequence():
 
 
 @pytest.mark.gpu
-def test_gpu_concurrent_batches_match_oracle(oracle_mod):
+@pytest.mark.parametrize("capacity", [None, "16384"])
+def test_gpu_concurrent_batches_match_oracle(oracle_mod, monkeypatch, capacity):
+    """capacity 16384: the token cache starts small, so batches keep crossing the host's bound on live +
+    tombstones -- the tombstone sweep (k_tok_sweep), the compaction and the growth all run between
+    batches and every later release must still find its token."""
     import sentinel_amd as sa
     from sentinel_amd.token_service import ServerNamespace
+    if capacity:
+        monkeypatch.setenv("SENTINEL_TOKEN_CAPACITY", capacity)
     rng = np.random.default_rng(71)
     F = 400
 
