@@ -538,6 +538,9 @@ int  sentinel_param_interner_key_at(sentinel_param_interner_t *it, int64_t flow_
                                     int32_t len, int64_t ts, uint64_t *key);
 int  sentinel_param_interner_set_limits(sentinel_param_interner_t *it, int64_t max_entries, int64_t idle_ms);
 int  sentinel_param_interner_stats(sentinel_param_interner_t *it, int64_t *entries, int64_t *evicted);
+/* Full passes over the map so far: each ends at or below 3/4 of max_entries, so a pass runs at most
+ * once per max_entries / 4 new values (bounded work per insert under a steady flood of values). */
+int  sentinel_param_interner_scans(sentinel_param_interner_t *it, int64_t *scans);
 typedef int64_t (*sentinel_clock_fn)(void *ctx);
 typedef struct {
     const char *host;                 /* IPv4 bind address, NULL = 127.0.0.1 */
@@ -641,6 +644,9 @@ int64_t sentinel_metric_count(sentinel_engine_t *eng);
 int  sentinel_reset_metrics(sentinel_engine_t *eng, int32_t sample_count, int32_t interval_ms);
 /* Param slot table statistics: {capacity, live slots after the last rebuild, rebuilds so far}. */
 int  sentinel_param_table_stats(sentinel_engine_t *eng, int64_t *out3);
+/* Shared count-min sketch batches so far: {decided by the two-phase key walk, sent to the per-rule lanes
+ * because one key-hash sub-range held more requests than one LDS chunk}. */
+int  sentinel_param_cm_stats(sentinel_engine_t *eng, int64_t *out2);
 /* The engine's own stream (hipStream_t). */
 void *sentinel_engine_stream(sentinel_engine_t *eng);
 /* Per-kernel timing with HIP events recorded on the launch stream (for roofline reporting).

@@ -211,11 +211,16 @@ __device__ inline void conc_seq_event(const ConcCtx &C, uint32_t flow, double th
             put_conc(C.out, seq, 0, ST_ALREADY_RELEASE);
             return;
         }
+        // the token's amount is read BEFORE its slot becomes a tombstone: once it is one, an insert of
+        // any other flow (another lane of this kernel) may take the slot and write its own amount there;
+        // the release-ordered store keeps the load ahead of it
+        const int32_t amt = C.TT.acquire[h];
         C.claim[h] = ~0u;
-        C.TT.keys[h] = TOKEN_TOMB;                                            // CCFC:92-100
+        __hip_atomic_store(&C.TT.keys[h], (unsigned long long)TOKEN_TOMB, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_AGENT);                         // CCFC:92-100
         --dlive;
         ++dtomb;
-        now = (int32_t)((uint32_t)now - (uint32_t)C.TT.acquire[h]);
+        now = (int32_t)((uint32_t)now - (uint32_t)amt);
         put_conc(C.out, seq, 0, ST_RELEASE_OK);
     }
 }
@@ -242,9 +247,9 @@ __device__ inline void conc_apply_item(const ConcCtx &C, uint32_t flow, int kind
         C.TT.acquire[hs] = amount;
         ++dlive;
         put_conc(C.out, seq, (int64_t)id, ST_OK);
-    } else if (kind == 1) {
+    } else if (kind == 1) {                               // (the amount was read by conc_item, before this)
         C.claim[h] = ~0u;
-        C.TT.keys[h] = TOKEN_TOMB;
+        __hip_atomic_store(&C.TT.keys[h], (unsigned long long)TOKEN_TOMB, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         --dlive;
         ++dtomb;
         put_conc(C.out, seq, 0, ST_RELEASE_OK);

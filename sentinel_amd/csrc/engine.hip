@@ -625,7 +625,9 @@ struct sentinel_engine {
     unsigned long long *h_pfresh = nullptr;
     unsigned long long *h_cmband = nullptr;     // shared count-min bands: {min ts, ~max ts, overflow} read back
     DevBuf d_cmband;
-    bool cm_keys = true;               // shared sketch: key-parallel bands (k_pp_cm_band) when the batch allows
+    bool cm_keys = true;               // shared sketch: the two-phase key walk (k_pp_cm_read / _walk) when allowed
+    uint64_t cm_key_batches = 0;       // shared-sketch batches decided by the key walk
+    uint64_t cm_overflows = 0;         // ... sent to the per-rule lanes (a sub-range over PG_CAP requests)
     uint64_t p_ord = 0;                // param batches reserved so far
     uint64_t p_reset_ord = 0;          // first batch ordinal after d_pfresh was last zeroed
     std::deque<std::pair<uint64_t, uint64_t>> p_pending;   // (ordinal, values) reserved since the reset
@@ -1369,6 +1371,9 @@ int sentinel_engine::param_reserve(int64_t nv) {
         p_live += fresh;
         p_ub = (uint64_t)nv;
         HIP_OK(hipMemsetAsync(d_pfresh.p, 0, 8, stream));
+        // finished before returning: this batch's kernels may run on a caller's stream that waited on the
+        // engine stream before the reset was queued, and their fresh-insert adds must land after it
+        HIP_OK(hipStreamSynchronize(stream));
         p_reset_ord = ord;
         p_pending.emplace_back(ord, (uint64_t)nv);
         return 0;
@@ -2033,7 +2038,11 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
     });
     HIP_OK(hipMemcpyAsync(e->h_cmband, flag, 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    if (e->h_cmband[0] != 0ull) return 1;
+    if (e->h_cmband[0] != 0ull) {
+        ++e->cm_overflows;
+        return 1;
+    }
+    ++e->cm_key_batches;
     const int32_t nsc = e->pmax_n;
     int64_t *mv = e->w_sval.as<int64_t>();                // (the packed values are dead after the grouping)
     const unsigned wg = (unsigned)std::min<int64_t>(2048, (n + 255) / 256);
@@ -2843,6 +2852,14 @@ int sentinel_param_table_stats(sentinel_engine_t *e, int64_t *out3) {
     out3[0] = e->d_ptable.p ? (int64_t)e->pcap : 0;
     out3[1] = (int64_t)e->p_live;
     out3[2] = (int64_t)e->p_rebuilds;
+    return 0;
+}
+
+int sentinel_param_cm_stats(sentinel_engine_t *e, int64_t *out2) {
+    if (!e || !out2) return fail(SENTINEL_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(e->mu);
+    out2[0] = (int64_t)e->cm_key_batches;
+    out2[1] = (int64_t)e->cm_overflows;
     return 0;
 }
 

@@ -246,12 +246,14 @@ __global__ __launch_bounds__(PT_THREADS) void k_pp_scatter(const ParamEvent *__r
         stage[pos[j]] = evs[j].key;
     }
     __syncthreads();
+    // dst < n: p - loff[d] < this tile's count of digit d, which equals k_pp_prep's hist entry for (tile, d)
+    // -- both kernels tile by PT_TILE (PP_ITEMS = PT_TILE / PP_THREADS) and count exactly the requests with
+    // pp_status == 127 (prep's PP_NEG_TS conversion yields BLOCKED / FAIL, never 127) -- so dst lies in
+    // [goff[d], goff[d] + hist[tile][d]) inside range d's [rstart[d], rstart[d + 1]) and rstart[P] <= n
     auto write_out = [&](auto put) {
         for (uint32_t p = threadIdx.x; p < total; p += PT_THREADS) {
             const uint32_t d = sdig[p];
-            const uint32_t dst = goff[d] + p - loff[d];
-            if (dst >= (uint64_t)n) continue;          // guard: a corrupt offset must never write out of bounds
-            put(dst, p);
+            put(goff[d] + p - loff[d], p);
         }
     };
     write_out([&](uint32_t dst, uint32_t p) { okey[dst] = stage[p]; });

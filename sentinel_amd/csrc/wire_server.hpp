@@ -135,18 +135,26 @@ struct sentinel_param_interner {
     int64_t now = INT64_MIN;                 // the newest request time seen
     int64_t evicted = 0;
 
+    int64_t scans = 0;                       // full passes over the map (each frees >= cap / 4 entries)
+
+    // Called when the map is full.  Every pass ends at or below the 3/4 low-water mark, so the next one
+    // comes only after cap / 4 more inserts: O(1) amortised per insert even under a steady flood of
+    // distinct values that expire one by one (an idle pass that freed a single entry used to leave the
+    // map full, and every following insert rescanned it).
     void shrink_locked() {
+        ++scans;
         const int64_t horizon = now == INT64_MIN ? INT64_MIN : now - idle_ms;
         for (auto it = ids.begin(); it != ids.end();) {
             if (it->second.last < horizon) { it = ids.erase(it); ++evicted; }
             else ++it;
         }
-        if ((int64_t)ids.size() < max_entries) return;
-        // still full: least recently used first, down to 3/4 of the cap
+        const int64_t low = max_entries / 4 * 3;
+        if ((int64_t)ids.size() <= low) return;
+        // still above the low-water mark: least recently used first, down to it
         std::vector<int64_t> lasts;
         lasts.reserve(ids.size());
         for (auto &kv : ids) lasts.push_back(kv.second.last);
-        const size_t drop = ids.size() - (size_t)(max_entries / 4 * 3);
+        const size_t drop = ids.size() - (size_t)low;
         std::nth_element(lasts.begin(), lasts.begin() + (drop - 1), lasts.end());
         const int64_t cut = lasts[drop - 1];
         size_t dropped = 0;
@@ -410,7 +418,7 @@ struct ReadBatch {
     std::vector<int32_t> pxid;
     std::vector<sentinel_param_multi_event_t> pev;
     std::vector<uint64_t> pvals;
-    std::vector<uint8_t> pnorule;                 // no param rule for the flowId when decoded
+    std::vector<int32_t> pnorule;                 // < 0: the flowId's lookup when decoded (NO_RULE / BAD_ID)
     std::unordered_map<int64_t, int32_t> prule_cache;   // flowId -> param rule index, this read
     void clear() {
         fid.clear(); fts.clear(); facq.clear(); fprio.clear(); ftag.clear();
@@ -526,7 +534,7 @@ inline bool sentinel_wire_server::on_readable(wire::Loop &L, wire::Conn *c) {
             auto rit = B.prule_cache.find(fid);
             if (rit == B.prule_cache.end()) {
                 int32_t ridx = -1;
-                if (sentinel_lookup_param_idx(e, 1, &fid, &ridx) != 0) ridx = -1;
+                if (sentinel_lookup_param_idx(e, 1, &fid, &ridx) != 0) ridx = SENTINEL_IDX_NO_RULE;
                 rit = B.prule_cache.emplace(fid, ridx).first;
             }
             const bool has_rule = rit->second >= 0;
@@ -565,7 +573,7 @@ inline bool sentinel_wire_server::on_readable(wire::Loop &L, wire::Conn *c) {
             B.pev.push_back(pe);
             B.pfid.push_back(fid);
             B.pxid.push_back(xid);
-            B.pnorule.push_back(!has_rule);
+            B.pnorule.push_back(has_rule ? 0 : rit->second);
         }
         // any other type: no decoder, nothing emitted
     }
@@ -590,7 +598,9 @@ inline bool sentinel_wire_server::on_readable(wire::Loop &L, wire::Conn *c) {
         std::vector<int32_t> idx(n);
         std::vector<sentinel_verdict_t> out(n);
         int rc = sentinel_lookup_param_idx(e, n, B.pfid.data(), idx.data());
-        for (int64_t i = 0; i < n; ++i) B.pev[i].rule_idx = B.pnorule[i] ? -1 : idx[i];
+        // a flowId without a rule keeps its decode-time lookup: SENTINEL_IDX_BAD_ID for flowId <= 0 answers
+        // BAD_REQUEST (DefaultTokenService.notValidRequest runs before the rule lookup), NO_RULE otherwise
+        for (int64_t i = 0; i < n; ++i) B.pev[i].rule_idx = B.pnorule[i] < 0 ? B.pnorule[i] : idx[i];
         if (!rc) rc = sentinel_submit_param_multi_batch_host(e, n, B.pev.data(), B.pvals.data(),
                                                              (int64_t)B.pvals.size(), out.data());
         for (int64_t i = 0; i < n; ++i)
@@ -675,6 +685,13 @@ int sentinel_param_interner_stats(sentinel_param_interner_t *it, int64_t *entrie
     std::lock_guard<std::mutex> g(it->mu);
     if (entries) *entries = (int64_t)it->ids.size();
     if (evicted) *evicted = it->evicted;
+    return 0;
+}
+
+int sentinel_param_interner_scans(sentinel_param_interner_t *it, int64_t *scans) {
+    if (!it || !scans) return fail(SENTINEL_E_INVALID, "null interner");
+    std::lock_guard<std::mutex> g(it->mu);
+    *scans = it->scans;
     return 0;
 }
 

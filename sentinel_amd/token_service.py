@@ -644,6 +644,12 @@ class GpuTokenService:
         check(self._L.sentinel_param_table_stats(self._h, _p(out)), "param_table_stats")
         return dict(capacity=int(out[0]), live=int(out[1]), rebuilds=int(out[2]))
 
+    def param_cm_stats(self):
+        """{key_walk, overflow}: shared count-min batches decided by the key walk / by the per-rule lanes."""
+        out = np.zeros(2, dtype=np.int64)
+        check(self._L.sentinel_param_cm_stats(self._h, _p(out)), "param_cm_stats")
+        return dict(key_walk=int(out[0]), overflow=int(out[1]))
+
     def param_top_values(self, ts: int, number: int = _lib.TOP_PARAMS):
         """getTopValues(number) of every param rule at ts -> list (per rule index) of [(key, avg)]."""
         n_rules = self.param_count()

@@ -560,8 +560,10 @@ class NativeParamInterner:
     def stats(self):
         import ctypes as C
         n, ev = C.c_int64(), C.c_int64()
+        sc = C.c_int64()
         self._L.sentinel_param_interner_stats(self.handle, C.byref(n), C.byref(ev))
-        return {"entries": n.value, "evicted": ev.value}
+        self._L.sentinel_param_interner_scans(self.handle, C.byref(sc))
+        return {"entries": n.value, "evicted": ev.value, "scans": sc.value}
 
     def close(self):
         if self.handle:

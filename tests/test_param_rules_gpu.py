@@ -140,12 +140,13 @@ def test_count_min_is_one_sided(oracle_mod):
 @pytest.mark.parametrize("levels", ["keys", "launch", "coop"])
 def test_shared_count_min_is_one_sided(oracle_mod, monkeypatch, levels):
     """One sketch for every rule (BASELINE config 4's layout), narrow enough that rules collide, on
-    batches spanning ~75 epochs: the lanes move through the epochs together, band by band (one lane
-    per (rule, value) key: k_pp_cm_band; one lane per rule: k_prule_cm_level / k_prule_cm_sync), so no
-    lane's reset of a shared cell slot drops a count a lagging lane still needs -- zero violations of
+    batches spanning ~75 epochs.  "keys" (the default): the two-phase key walk, one lane per (rule, value)
+    key (k_pp_cm_read: every read of the batch, then k_pp_cm_walk: decisions and adds); "launch" /
+    "coop": one lane per rule moving through the epochs band by band (k_prule_cm_level / k_prule_cm_sync).
+    Either way no reset of a shared cell slot drops a count a check still needs -- zero violations of
     one-sidedness, and the false-block rate shrinks with the width."""
     import sentinel_amd as sa
-    # key-parallel bands (the default), one launch per band of rule lanes, or the grid barrier
+    # the key walk (the default), one launch per band of rule lanes, or the grid barrier
     monkeypatch.setenv("SENTINEL_CM_LEVELS", levels)
     count, hot, rule_idx, vals, keys, ts = T.config4(200_000, seed=53, n_rules=5000, universe=200)
     acq = np.ones(len(ts), np.int32)
@@ -265,3 +266,58 @@ def test_local_param_bitexact(oracle_mod):
         lo_, to_ = orc.state(r, int(k[j]))
         lg, tg = svc.local_param_state(int(k[j]))
         assert (lg, tg) == (lo_, to_), (j, lg, tg, lo_, to_)
+
+
+def _hot_key_batches(n_batches=3, n=30_000, hot_reqs=3000, seed=58):
+    """Config-4-shaped batches where, in the first two, one (rule, value) key takes `hot_reqs` requests
+    (> PG_CAP = 1280, one LDS chunk of k_pp_group) spread over the batch; the last batch has no such key."""
+    count, hot, rule_idx, vals, keys, ts = T.config4(n * n_batches, seed=seed, n_rules=500, universe=100)
+    rng = np.random.default_rng(seed)
+    rule_idx, keys = rule_idx.copy(), keys.copy()
+    for b in range(n_batches - 1):
+        pos = b * n + rng.choice(n, size=hot_reqs, replace=False)
+        rule_idx[pos] = 7
+        keys[pos] = (np.uint64(7) << np.uint64(20)) | np.uint64(3)
+    return count, hot, rule_idx, keys, ts
+
+
+def test_shared_count_min_subrange_over_chunk_falls_back(oracle_mod):
+    """A shared count-min batch with one key over PG_CAP requests: its key-hash sub-range cannot be grouped
+    in one LDS chunk, so k_pp_group raises the overflow flag (no workgroup decides or emits anything for
+    it) and the whole batch goes to the per-rule lanes -- the path that faulted while the key walk was
+    being built.  The fallback batches and the key-walk batch after them are audited
+    on exact counters replaying the sketch's own decisions: zero one-sidedness violations."""
+    import sentinel_amd as sa
+    count, hot, rule_idx, keys, ts = _hot_key_batches()
+    svc, orc = _cluster_pair(oracle_mod, count, hot, sample_count=lambda r: 10)
+    svc.set_param_mode(sa._lib.PARAM_COUNT_MIN_SHARED, depth=4, width=1 << 12)
+    acq = np.ones(len(ts), np.int32)
+    n = 30_000
+    st = []
+    for b in range(3):
+        s = slice(b * n, (b + 1) * n)
+        st.append(svc.submit_param_batch_host(rule_idx[s], acq[s], keys[s], ts[s])[0])
+        assert svc.param_cm_stats() == dict(key_walk=max(0, b - 1), overflow=min(b + 1, 2)), (b, svc.param_cm_stats())
+    st = np.concatenate(st)
+    viol, fb, dec = orc.param_cm_audit(rule_idx, acq, ts, np.arange(len(ts)), np.ones(len(ts), np.int32), keys, st)
+    assert viol == 0 and dec == len(ts), (viol, dec)
+    hk = keys == ((np.uint64(7) << np.uint64(20)) | np.uint64(3))
+    assert (st[hk] == 0).any() and (st[hk] == 1).any()
+
+
+def test_exact_subrange_over_chunk_bitexact(oracle_mod):
+    """The exact twin of the batches above: the hot key's sub-range is decided inside k_pp_group, chunk
+    after chunk in arrival order (the key walked once per chunk), bit for bit against the oracle."""
+    count, hot, rule_idx, keys, ts = _hot_key_batches()
+    svc, orc = _cluster_pair(oracle_mod, count, hot, sample_count=lambda r: 10)
+    acq = np.where(np.arange(len(ts)) % 7 == 0, 2, 1).astype(np.int32)
+    n = 30_000
+    for b in range(3):
+        s = slice(b * n, (b + 1) * n)
+        sg, rg = svc.submit_param_batch_host(rule_idx[s], acq[s], keys[s], ts[s])
+        so, ro = orc.param_replay(rule_idx[s], acq[s], keys[s], ts[s])
+        bad = np.nonzero((sg != so) | (rg != ro))[0]
+        assert len(bad) == 0, (b, len(bad), bad[:5], sg[bad[:5]], so[bad[:5]], rg[bad[:5]], ro[bad[:5]])
+    t = int(ts[-1])
+    hk = int((np.uint64(7) << np.uint64(20)) | np.uint64(3))
+    assert svc.param_sum(7, hk, t) == orc.param_sum(7, t, hk)

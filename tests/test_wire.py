@@ -217,6 +217,22 @@ def test_native_interner_is_bounded():
     nat.close()
 
 
+def test_native_interner_steady_churn_scans_rarely():
+    """Distinct values arriving 1 ms apart with idle_ms just under the cap's span: every insert past the
+    cap finds exactly one idle entry.  Each full pass must end at the 3/4 low-water mark, so passes run
+    at most once per cap / 4 inserts (one pass per insert before the hysteresis)."""
+    nat = W.NativeParamInterner()
+    nat.set_limits(1000, 999)
+    n = 20_000
+    for i in range(n):
+        nat.key(7, W.jlong(i), ts=i)
+        assert nat.stats()["entries"] <= 1000
+    st = nat.stats()
+    assert st["scans"] <= n // 250 + 2, st
+    assert nat.key(7, W.jlong(n - 1), ts=n) is not None
+    nat.close()
+
+
 def _ask(cl, frame):
     cl.send(frame)
     return cl.recv()
@@ -264,12 +280,13 @@ def test_native_server_sequential_matches_oracle(oracle_mod):
             xid = 100 + k
             cl = a if k % 3 else b
             if k % 5 == 4:
-                r = int(rng.integers(0, 7))
+                r = int(rng.integers(0, 8))          # 6: no rule; 7: flowId 0 or < 0 (BAD_REQUEST)
+                fid = 900 + r if r < 7 else int(rng.integers(-3, 1))
                 vals = [W.jstr("vip") if rng.random() < 0.3 else W.jint(int(rng.integers(0, 4)))
                         for _ in range(int(rng.integers(1, 3)))]
-                got = _ask(cl, W.encode_param_request(xid, 900 + r, 1, vals))
-                keys = np.array([interner.key(900 + r, v) for v in vals], dtype=np.uint64)
-                s, rem = orc.param_multi_replay(np.array([r if r < 6 else -1], np.int32), np.ones(1, np.int32),
+                got = _ask(cl, W.encode_param_request(xid, fid, 1, vals))
+                keys = np.array([interner.key(fid, v) for v in vals], dtype=np.uint64)
+                s, rem = orc.param_multi_replay(np.array([r if r < 6 else (-1 if r == 6 else -2)], np.int32), np.ones(1, np.int32),
                                                 np.array([now[0]], np.int64), np.zeros(1, np.int32),
                                                 np.array([len(vals)], np.int32), keys)
                 assert got == (xid, 2, int(s[0]), (int(rem[0]), 0)), (k, got, s, rem)
