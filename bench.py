@@ -409,7 +409,13 @@ class ParamWorkload:
         c0 = time.perf_counter()
         orc.param_replay(ridx, acq, keys, ts)
         cdt = time.perf_counter() - c0
-        return (len(ts), cdt, 1, "sequential oracle replay (ClusterParamFlowChecker, exact counters)"), None
+        one = (len(ts), cdt, 1, "sequential oracle replay (ClusterParamFlowChecker, exact counters)")
+        ridx, acq, keys, ts = self._host(batches, kmt)
+        orc = self._oracle()
+        c0 = time.perf_counter()
+        used = orc.param_replay_mt(ridx, acq, keys, ts, threads)[2]
+        cdt = time.perf_counter() - c0
+        return one, (len(ts), cdt, int(used), f"oracle replay sharded by rule over {used} pthreads (exact counters)")
 
     def false_blocks(self, batches, k, svc_verdicts):
         """Count-min audit: the sketch's verdicts replayed on exact counters (same admitted history):
@@ -550,7 +556,7 @@ class ConcWorkload:
         orc = O.TokenServiceOracle.from_arrays(r.flow_id, r.count, r.threshold_type, r.sample_count,
                                                r.window_interval_ms, r.namespace, r.checker)
         evs = []
-        for b, res in self.kept[:k1]:
+        for b, res in self.kept:
             e = b.cpu().numpy()
             ev = np.zeros(len(e), dtype=orc.CONC_EVENT)
             ev["flow_idx"] = (e[:, 0] & 0xFFFFFFFF).astype(np.int32)
@@ -561,11 +567,21 @@ class ConcWorkload:
             evs.append((ev, res[:, 0].cpu().numpy()))
         c0 = time.perf_counter()
         m = 0
-        for ev, ids in evs:
+        for ev, ids in evs[:k1]:
             orc.concurrent_replay(ev, ids)
             m += len(ev)
         cdt = time.perf_counter() - c0
-        return (m, cdt, 1, "sequential oracle replay (ConcurrentClusterFlowChecker, the engine's token ids)"), None
+        one = (m, cdt, 1, "sequential oracle replay (ConcurrentClusterFlowChecker, the engine's token ids)")
+        orc = O.TokenServiceOracle.from_arrays(r.flow_id, r.count, r.threshold_type, r.sample_count,
+                                               r.window_interval_ms, r.namespace, r.checker)
+        all_ev = np.concatenate([ev for ev, _ in evs])
+        all_ids = np.concatenate([ids for _, ids in evs])
+        c0 = time.perf_counter()
+        used = orc.concurrent_replay_mt(all_ev, all_ids, threads)[2]
+        cdt = time.perf_counter() - c0
+        return one, (len(all_ev), cdt, int(used),
+                     f"oracle replay sharded by flow over {used} pthreads (a token cache per thread, releases routed "
+                     f"to their token's thread; the engine's token ids)")
 
     def bytes_of(self, dom, d, steps):
         if dom in ("conc_process", "conc_chunks"):

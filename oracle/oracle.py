@@ -103,6 +103,7 @@ def lib():
         "orc_engine_load_param_rules": (C.c_int, [vp, vp, C.c_int, vp, vp, C.c_int]),
         "orc_request_param_token": (None, [vp, i32, i32, i64, vp, C.c_int, vp, vp]),
         "orc_param_replay": (None, [vp, i64, vp, vp, vp, vp, vp, vp]),
+        "orc_param_replay_mt": (C.c_int, [vp, i64, vp, vp, vp, vp, vp, vp, C.c_int]),
         "orc_engine_param_sum": (i64, [vp, i32, i64, u64]),
         "orc_engine_param_overflowed": (C.c_int, [vp]),
         "orc_node_new": (vp, [C.c_int, C.c_int]),
@@ -151,6 +152,7 @@ def lib():
         "orc_lparam_replay_ex": (None, [vp, i64, vp, vp, vp, vp, vp, vp, i64, vp, vp]),
         "orc_lparam_thread_count": (C.c_int, [vp, i32, u64]),
         "orc_concurrent_replay": (None, [vp, i64, vp, vp, vp, vp]),
+        "orc_concurrent_replay_mt": (C.c_int, [vp, i64, vp, vp, vp, vp, C.c_int]),
         "orc_concurrent_now_calls": (i32, [vp, i32]),
         "orc_concurrent_token_count": (i64, [vp]),
         "orc_concurrent_expire_all": (i64, [vp]),
@@ -516,6 +518,19 @@ class TokenServiceOracle:
         lib().orc_param_replay(self.h, n, _p(rule_idx), _p(acquire), _p(keys), _p(ts), _p(status), _p(remaining))
         return status, remaining
 
+    def param_replay_mt(self, rule_idx, acquire, keys, ts, nthreads):
+        """Rule-sharded multi-threaded param replay; returns (status, remaining, threads_used)."""
+        n = len(ts)
+        rule_idx = np.ascontiguousarray(rule_idx, dtype=np.int32)
+        acquire = np.ascontiguousarray(acquire, dtype=np.int32)
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        status = np.zeros(n, dtype=np.int8)
+        remaining = np.zeros(n, dtype=np.int32)
+        used = lib().orc_param_replay_mt(self.h, n, _p(rule_idx), _p(acquire), _p(keys), _p(ts), _p(status),
+                                         _p(remaining), int(nthreads))
+        return status, remaining, used
+
     def param_multi_replay(self, rule_idx, acquire, ts, vbegin, vcount, values):
         r, a, t, b, c, v = _multi_args(rule_idx, acquire, ts, vbegin, vcount, values)
         status = np.zeros(len(t), dtype=np.int8)
@@ -592,6 +607,16 @@ class TokenServiceOracle:
         tok = np.zeros(len(ev), dtype=np.int64)
         lib().orc_concurrent_replay(self.h, len(ev), _p(ev), _p(ids), _p(st), _p(tok))
         return st, tok
+
+    def concurrent_replay_mt(self, events: np.ndarray, new_ids, nthreads):
+        """Flow-sharded multi-threaded concurrency replay on a fresh oracle (own token cache per thread,
+        releases routed to the thread that issued their token); returns (status, token_id, threads_used)."""
+        ev = np.ascontiguousarray(events, dtype=self.CONC_EVENT)
+        ids = np.ascontiguousarray(new_ids, dtype=np.int64)
+        st = np.zeros(len(ev), dtype=np.int8)
+        tok = np.zeros(len(ev), dtype=np.int64)
+        used = lib().orc_concurrent_replay_mt(self.h, len(ev), _p(ev), _p(ids), _p(st), _p(tok), int(nthreads))
+        return st, tok, used
 
     def concurrent_now_calls(self, idx): return lib().orc_concurrent_now_calls(self.h, idx)
     def concurrent_token_count(self): return lib().orc_concurrent_token_count(self.h)

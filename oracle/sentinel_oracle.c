@@ -463,6 +463,17 @@ typedef struct {
     orc_param_metric *pm;
 } param_entry;
 
+/* TokenCacheNodeManager's cache: tokenId -> record {flowId, acquireCount, alive} (one per engine; a
+ * flow-sharded replay gives every thread its own). */
+typedef struct {
+    kvmap index;
+    int64_t *fid;
+    int32_t *acq;
+    uint8_t *alive;
+    int64_t n, cap, live;
+} orc_tok;
+static void tok_free(orc_tok *t);
+
 struct orc_engine {
     orc_server_config cfg;
     orc_namespace *ns;
@@ -481,11 +492,7 @@ struct orc_engine {
     /* concurrency tokens (ConcurrentClusterFlowChecker) */
     kvmap now_calls;          /* flowId -> nowCalls (CurrentConcurrencyManager) */
     kvmap rule_by_fid;        /* flowId -> rule index (ClusterFlowRuleManager.getFlowRuleById) */
-    kvmap tok_index;          /* tokenId -> record (TokenCacheNodeManager) */
-    int64_t *tok_fid;
-    int32_t *tok_acq;
-    uint8_t *tok_alive;
-    int64_t tok_n, tok_cap, tok_live;
+    orc_tok tok;              /* TokenCacheNodeManager */
 };
 
 orc_engine *orc_engine_new(const orc_server_config *cfg, const orc_namespace *ns, int n_ns) {
@@ -512,8 +519,8 @@ void orc_engine_free(orc_engine *e) {
     kv_free(&e->metric_map); kv_free(&e->param_metric_map);
     free(e->ns); free(e->lim); free(e->rules); free(e->cm); free(e->prules);
     free(e->hot_keys); free(e->hot_counts);
-    kv_free(&e->now_calls); kv_free(&e->rule_by_fid); kv_free(&e->tok_index);
-    free(e->tok_fid); free(e->tok_acq); free(e->tok_alive);
+    kv_free(&e->now_calls); kv_free(&e->rule_by_fid);
+    tok_free(&e->tok);
     free(e);
 }
 
@@ -907,6 +914,49 @@ void orc_param_replay(orc_engine *e, int64_t n, const int32_t *rule_idx, const i
                       const uint64_t *param_key, const int64_t *ts, int8_t *status, int32_t *remaining) {
     for (int64_t i = 0; i < n; i++)
         orc_request_param_token(e, rule_idx[i], acquire[i], ts[i], &param_key[i], 1, &status[i], &remaining[i]);
+}
+
+/* Rule-sharded multi-threaded param replay (CPU baseline only): thread k owns the
+ * rules with rule_idx mod T == k (each rule's ClusterParamMetric is its own); without namespace
+ * limiters (they couple rules) it is one thread. */
+typedef struct {
+    orc_engine *e;
+    int64_t n;
+    const int32_t *rule_idx, *acquire;
+    const uint64_t *param_key;
+    const int64_t *ts;
+    int8_t *status;
+    int32_t *remaining;
+    int T, k;
+} param_mt_arg;
+
+static void *param_mt_worker(void *p) {
+    param_mt_arg *a = (param_mt_arg *)p;
+    for (int64_t i = 0; i < a->n; i++) {
+        const int32_t r = a->rule_idx[i];
+        if ((r >= 0 ? (int)(r % a->T) : 0) != a->k) continue;
+        orc_request_param_token(a->e, r, a->acquire[i], a->ts[i], &a->param_key[i], 1, &a->status[i], &a->remaining[i]);
+    }
+    return NULL;
+}
+
+int orc_param_replay_mt(orc_engine *e, int64_t n, const int32_t *rule_idx, const int32_t *acquire,
+                        const uint64_t *param_key, const int64_t *ts, int8_t *status, int32_t *remaining, int nthreads) {
+    for (int i = 0; i < e->n_ns; i++)
+        if (e->lim[i]) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    if (nthreads <= 1) {
+        orc_param_replay(e, n, rule_idx, acquire, param_key, ts, status, remaining);
+        return 1;
+    }
+    pthread_t th[256];
+    param_mt_arg args[256];
+    for (int k = 0; k < nthreads; k++) {
+        args[k] = (param_mt_arg){e, n, rule_idx, acquire, param_key, ts, status, remaining, nthreads, k};
+        pthread_create(&th[k], NULL, param_mt_worker, &args[k]);
+    }
+    for (int k = 0; k < nthreads; k++) pthread_join(th[k], NULL);
+    return nthreads;
 }
 
 int64_t orc_engine_param_sum(orc_engine *e, int32_t idx, int64_t t, uint64_t key) {
@@ -1709,46 +1759,117 @@ static double conc_threshold(const orc_engine *e, const orc_flow_rule *r) {     
     return r->count * (double)cc;
 }
 
+static void tok_free(orc_tok *t) {
+    kv_free(&t->index);
+    free(t->fid); free(t->acq); free(t->alive);
+    memset(t, 0, sizeof(*t));
+}
+
+/* One event of ConcurrentClusterFlowChecker (CCFC:48-101) against token cache `tk`; nowCalls lives in
+ * the engine's map (values updated in place: the map's layout does not change during a replay). */
+static void conc_event(orc_engine *e, orc_tok *tk, const orc_concurrent_event *x, int64_t new_id, int8_t *status,
+                       int64_t *token_out) {
+    *token_out = 0;
+    if (x->kind == 0) {
+        if (!(x->flags & 1u) || x->flow_idx == -2 || x->acquire <= 0) { *status = ORC_BAD_REQUEST; return; }
+        if (x->flow_idx < 0 || x->flow_idx >= e->n_rules || !e->cm[x->flow_idx]) { *status = ORC_NO_RULE_EXISTS; return; }
+        const orc_flow_rule *r = &e->rules[x->flow_idx];
+        int64_t *now = kv_find(&e->now_calls, (uint64_t)r->flow_id);
+        if (!now) { *status = ORC_FAIL; return; }                                  /* CCFC:51-54 */
+        const int32_t sum = (int32_t)((uint32_t)(int32_t)*now + (uint32_t)x->acquire);
+        if ((double)sum > conc_threshold(e, r)) { *status = ORC_BLOCKED; return; }  /* CCFC:57-69 */
+        *now = (int32_t)((uint32_t)(int32_t)*now + (uint32_t)x->acquire);         /* CCFC:70 */
+        if (tk->n == tk->cap) {
+            tk->cap = tk->cap ? 2 * tk->cap : 1024;
+            tk->fid = (int64_t *)realloc(tk->fid, (size_t)tk->cap * sizeof(int64_t));
+            tk->acq = (int32_t *)realloc(tk->acq, (size_t)tk->cap * sizeof(int32_t));
+            tk->alive = (uint8_t *)realloc(tk->alive, (size_t)tk->cap);
+        }
+        tk->fid[tk->n] = r->flow_id;
+        tk->acq[tk->n] = x->acquire;
+        tk->alive[tk->n] = 1;
+        *kv_insert(&tk->index, (uint64_t)new_id, 0) = tk->n++;
+        tk->live++;
+        *status = ORC_OK;
+        *token_out = new_id;
+    } else if (x->kind == 1) {
+        const int64_t *rec = kv_find(&tk->index, (uint64_t)x->token_id);           /* CCFC:82-86 */
+        if (!rec || !tk->alive[*rec]) { *status = 7; return; }                     /* ALREADY_RELEASE */
+        if (!kv_find(&e->rule_by_fid, (uint64_t)tk->fid[*rec])) { *status = ORC_NO_RULE_EXISTS; return; }
+        tk->alive[*rec] = 0;                                                        /* CCFC:92-98 */
+        tk->live--;
+        int64_t *now = kv_find(&e->now_calls, (uint64_t)tk->fid[*rec]);
+        *now = (int32_t)((uint32_t)(int32_t)*now - (uint32_t)tk->acq[*rec]);
+        *status = 6;                                                                /* RELEASE_OK */
+    } else {
+        *status = ORC_BAD_REQUEST;
+    }
+}
+
 void orc_concurrent_replay(orc_engine *e, int64_t n, const orc_concurrent_event *ev, const int64_t *new_ids,
                            int8_t *status, int64_t *token_out) {
+    for (int64_t i = 0; i < n; i++) conc_event(e, &e->tok, &ev[i], new_ids[i], &status[i], &token_out[i]);
+}
+
+/* Flow-sharded multi-threaded concurrency replay (CPU baseline only, SURVEY section 8(d): T threads
+ * sharded by flow).  Thread k owns the flows with flow_idx mod T == k and a token cache of its own; a
+ * release goes to the thread whose flow issued its token (token -> owner from the acquires that pass
+ * with new_ids[i] != 0: a sharded server routes a token id to its shard), an unknown token to thread 0
+ * (ALREADY_RELEASE).  Each flow still sees its events in arrival order.  Valid on a fresh engine (no
+ * tokens cached before the call); the engine's own token cache is left untouched. */
+typedef struct {
+    orc_engine *e;
+    int64_t n;
+    const orc_concurrent_event *ev;
+    const int64_t *new_ids;
+    const uint8_t *owner;
+    int8_t *status;
+    int64_t *token_out;
+    int k;
+} conc_mt_arg;
+
+static void *conc_mt_worker(void *p) {
+    conc_mt_arg *a = (conc_mt_arg *)p;
+    orc_tok tk;
+    memset(&tk, 0, sizeof(tk));
+    kv_init(&tk.index);
+    for (int64_t i = 0; i < a->n; i++)
+        if (a->owner[i] == a->k) conc_event(a->e, &tk, &a->ev[i], a->new_ids[i], &a->status[i], &a->token_out[i]);
+    tok_free(&tk);
+    return NULL;
+}
+
+int orc_concurrent_replay_mt(orc_engine *e, int64_t n, const orc_concurrent_event *ev, const int64_t *new_ids,
+                             int8_t *status, int64_t *token_out, int nthreads) {
+    if (nthreads > 255) nthreads = 255;
+    if (nthreads <= 1) {
+        orc_concurrent_replay(e, n, ev, new_ids, status, token_out);
+        return 1;
+    }
+    uint8_t *owner = (uint8_t *)malloc((size_t)(n > 0 ? n : 1));
+    kvmap tok_owner;                                       /* token id -> owning thread */
+    kv_init(&tok_owner);
     for (int64_t i = 0; i < n; i++) {
         const orc_concurrent_event *x = &ev[i];
-        token_out[i] = 0;
         if (x->kind == 0) {
-            if (!(x->flags & 1u) || x->flow_idx == -2 || x->acquire <= 0) { status[i] = ORC_BAD_REQUEST; continue; }
-            if (x->flow_idx < 0 || x->flow_idx >= e->n_rules || !e->cm[x->flow_idx]) { status[i] = ORC_NO_RULE_EXISTS; continue; }
-            const orc_flow_rule *r = &e->rules[x->flow_idx];
-            int64_t *now = kv_find(&e->now_calls, (uint64_t)r->flow_id);
-            if (!now) { status[i] = ORC_FAIL; continue; }                          /* CCFC:51-54 */
-            const int32_t sum = (int32_t)((uint32_t)(int32_t)*now + (uint32_t)x->acquire);
-            if ((double)sum > conc_threshold(e, r)) { status[i] = ORC_BLOCKED; continue; }   /* CCFC:57-69 */
-            *now = (int32_t)((uint32_t)(int32_t)*now + (uint32_t)x->acquire);     /* CCFC:70 */
-            if (e->tok_n == e->tok_cap) {
-                e->tok_cap = e->tok_cap ? 2 * e->tok_cap : 1024;
-                e->tok_fid = (int64_t *)realloc(e->tok_fid, (size_t)e->tok_cap * sizeof(int64_t));
-                e->tok_acq = (int32_t *)realloc(e->tok_acq, (size_t)e->tok_cap * sizeof(int32_t));
-                e->tok_alive = (uint8_t *)realloc(e->tok_alive, (size_t)e->tok_cap);
-            }
-            e->tok_fid[e->tok_n] = r->flow_id;
-            e->tok_acq[e->tok_n] = x->acquire;
-            e->tok_alive[e->tok_n] = 1;
-            *kv_insert(&e->tok_index, (uint64_t)new_ids[i], 0) = e->tok_n++;
-            e->tok_live++;
-            status[i] = ORC_OK;
-            token_out[i] = new_ids[i];
-        } else if (x->kind == 1) {
-            const int64_t *rec = kv_find(&e->tok_index, (uint64_t)x->token_id);     /* CCFC:82-86 */
-            if (!rec || !e->tok_alive[*rec]) { status[i] = 7; continue; }           /* ALREADY_RELEASE */
-            if (!kv_find(&e->rule_by_fid, (uint64_t)e->tok_fid[*rec])) { status[i] = ORC_NO_RULE_EXISTS; continue; }
-            e->tok_alive[*rec] = 0;                                                 /* CCFC:92-98 */
-            e->tok_live--;
-            int64_t *now = kv_find(&e->now_calls, (uint64_t)e->tok_fid[*rec]);
-            *now = (int32_t)((uint32_t)(int32_t)*now - (uint32_t)e->tok_acq[*rec]);
-            status[i] = 6;                                                          /* RELEASE_OK */
+            const int k = x->flow_idx >= 0 ? (int)(x->flow_idx % nthreads) : 0;
+            owner[i] = (uint8_t)k;
+            if (new_ids[i]) *kv_insert(&tok_owner, (uint64_t)new_ids[i], 0) = k;
         } else {
-            status[i] = ORC_BAD_REQUEST;
+            const int64_t *k = x->kind == 1 ? kv_find(&tok_owner, (uint64_t)x->token_id) : NULL;
+            owner[i] = (uint8_t)(k ? *k : 0);
         }
     }
+    pthread_t th[255];
+    conc_mt_arg args[255];
+    for (int k = 0; k < nthreads; k++) {
+        args[k] = (conc_mt_arg){e, n, ev, new_ids, owner, status, token_out, k};
+        pthread_create(&th[k], NULL, conc_mt_worker, &args[k]);
+    }
+    for (int k = 0; k < nthreads; k++) pthread_join(th[k], NULL);
+    kv_free(&tok_owner);
+    free(owner);
+    return nthreads;
 }
 
 int32_t orc_concurrent_now_calls(orc_engine *e, int32_t flow_idx) {
@@ -1757,19 +1878,19 @@ int32_t orc_concurrent_now_calls(orc_engine *e, int32_t flow_idx) {
     return now ? (int32_t)*now : 0;
 }
 
-int64_t orc_concurrent_token_count(orc_engine *e) { return e->tok_live; }
+int64_t orc_concurrent_token_count(orc_engine *e) { return e->tok.live; }
 
 /* RegularExpireStrategy.clearToken with <= executeCount cached tokens: every token qualifies and
  * leaves the cache; nowCalls of a still-present flowId gets the count back (RES:94-136). */
 int64_t orc_concurrent_expire_all(orc_engine *e) {
     int64_t removed = 0;
-    for (int64_t t = 0; t < e->tok_n; t++) {
-        if (!e->tok_alive[t]) continue;
-        e->tok_alive[t] = 0;
-        e->tok_live--;
+    for (int64_t t = 0; t < e->tok.n; t++) {
+        if (!e->tok.alive[t]) continue;
+        e->tok.alive[t] = 0;
+        e->tok.live--;
         removed++;
-        int64_t *now = kv_find(&e->now_calls, (uint64_t)e->tok_fid[t]);
-        if (now) *now = (int32_t)((uint32_t)(int32_t)*now - (uint32_t)e->tok_acq[t]);
+        int64_t *now = kv_find(&e->now_calls, (uint64_t)e->tok.fid[t]);
+        if (now) *now = (int32_t)((uint32_t)(int32_t)*now - (uint32_t)e->tok.acq[t]);
     }
     return removed;
 }

@@ -149,6 +149,9 @@ void orc_request_param_token(orc_engine *e, int32_t rule_idx, int32_t acquire, i
 /* Batch of single-value requests in seq order. */
 void orc_param_replay(orc_engine *e, int64_t n, const int32_t *rule_idx, const int32_t *acquire,
                       const uint64_t *param_key, const int64_t *ts, int8_t *status, int32_t *remaining);
+/* rule-sharded over nthreads (CPU baseline); returns the threads used */
+int  orc_param_replay_mt(orc_engine *e, int64_t n, const int32_t *rule_idx, const int32_t *acquire,
+                         const uint64_t *param_key, const int64_t *ts, int8_t *status, int32_t *remaining, int nthreads);
 int64_t orc_engine_param_sum(orc_engine *e, int32_t rule_idx, int64_t t, uint64_t key);
 int  orc_engine_param_top_values(orc_engine *e, int32_t rule_idx, int64_t t, int number, uint64_t *keys, double *avgs);
 int  orc_engine_param_window(const orc_engine *e, int32_t rule_idx, int32_t *out2);
@@ -282,6 +285,9 @@ typedef struct {
 
 void orc_concurrent_replay(orc_engine *e, int64_t n, const orc_concurrent_event *ev, const int64_t *new_ids,
                            int8_t *status, int64_t *token_out);
+/* flow-sharded over nthreads (CPU baseline); returns the threads used */
+int  orc_concurrent_replay_mt(orc_engine *e, int64_t n, const orc_concurrent_event *ev, const int64_t *new_ids,
+                              int8_t *status, int64_t *token_out, int nthreads);
 int32_t orc_concurrent_now_calls(orc_engine *e, int32_t flow_idx);
 int64_t orc_concurrent_token_count(orc_engine *e);
 int64_t orc_concurrent_expire_all(orc_engine *e);

@@ -7,6 +7,7 @@ import json
 import math
 import os
 
+import numpy as np
 import pytest
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
@@ -199,3 +200,55 @@ def test_mt_replay_equals_sequential(oracle_mod):
     assert b[3] == 4
     for x, y in zip(a, b[:3]):
         assert (x == y).all()
+
+
+def test_param_mt_replay_equals_sequential(oracle_mod):
+    """Config 4's multi-threaded CPU baseline (rule-sharded) is the same replay as the sequential oracle."""
+    from sentinel_amd import trace as T
+    count, hot, rule_idx, vals, keys, ts = T.config4(200_000, seed=12, n_rules=3000, universe=200)
+    prules = [dict(flow_id=r + 1, count=float(count[r]), threshold_type=1, sample_count=10, window_interval_ms=1000)
+              for r in range(len(count))]
+    acq = np.ones(len(ts), np.int32)
+
+    def orc():
+        return oracle_mod.TokenServiceOracle([], param_rules=prules, hot_items={r: list(h.items()) for r, h in hot.items()})
+    a = orc().param_replay(rule_idx, acq, keys, ts)
+    s, r, used = orc().param_replay_mt(rule_idx, acq, keys, ts, 4)
+    assert used == 4 and (a[0] == s).all() and (a[1] == r).all()
+    assert (s == 0).any() and (s == 1).any()
+
+
+def test_concurrent_mt_replay_equals_sequential(oracle_mod):
+    """Config 5conc's multi-threaded CPU baseline (flow-sharded, a token cache per thread, releases routed to
+    the thread that issued their token) answers exactly as the sequential replay, over several batches."""
+    from sentinel_amd import trace as T
+    rng = np.random.default_rng(31)
+    F, n, nb = 500, 20_000, 4
+    rules = [dict(flow_id=f + 1, count=float(rng.integers(1, 40)), threshold_type=1, sample_count=10,
+                  window_interval_ms=1000, namespace_idx=0, checker=0) for f in range(F)]
+    ref = oracle_mod.TokenServiceOracle(rules)
+    evs, ids = [], []
+    outstanding = np.zeros(0, np.int64)
+    next_id = 1
+    for b in range(nb):
+        ev = np.zeros(n, dtype=ref.CONC_EVENT)
+        kind = (rng.random(n) < 0.45).astype(np.int32) if len(outstanding) else np.zeros(n, np.int32)
+        ev["kind"] = kind
+        ev["flow_idx"] = T.zipf_indices(F, 1.1, n, rng)
+        ev["acquire"] = rng.integers(1, 3, size=n)
+        ev["flags"] = 1
+        rel = np.nonzero(kind == 1)[0]
+        if len(rel):
+            ev["token_id"][rel] = outstanding[rng.integers(0, len(outstanding), size=len(rel))]
+        nid = np.arange(next_id, next_id + n, dtype=np.int64)
+        next_id += n
+        st, tok = ref.concurrent_replay(ev, nid)
+        ids.append(np.where(st == 0, nid, 0))               # the engine's ids of the passing acquires
+        evs.append((ev, st))
+        released = set(ev["token_id"][(kind == 1) & (st == 6)].tolist())
+        outstanding = np.array([t for t in outstanding.tolist() if t not in released] + tok[st == 0].tolist(), np.int64)
+    all_ev = np.concatenate([e for e, _ in evs])
+    st_mt, tok_mt, used = oracle_mod.TokenServiceOracle(rules).concurrent_replay_mt(all_ev, np.concatenate(ids), 4)
+    assert used == 4
+    assert (st_mt == np.concatenate([s for _, s in evs])).all()
+    assert {0, 1, 6, 7} <= set(np.unique(st_mt).tolist())
