@@ -8,9 +8,10 @@
 //
 // A batch mixes acquires and releases of many flows.  Acquires and releases of one flow do not
 // commute (nowCalls is not a monotone function of the event order), so events are grouped by flow
-// (K2 radix sort, arrival order kept) and one lane walks each flow's events in order.  The token
-// cache is one open-addressing table in HBM shared by all lanes: inserts CAS an empty slot, a
-// release turns its slot into a tombstone (only the owning flow's lane ever touches a token).
+// (K2 radix sort, arrival order kept) and each flow's run is decided in arrival order (below: the
+// elements gathered in parallel, short runs by one lane, long runs by a (min, +) scan).  The token
+// cache is one open-addressing table in HBM: inserts CAS an empty slot or a tombstone, a release
+// turns its slot into a tombstone.
 #pragma once
 
 #include "admission.hpp"
@@ -166,96 +167,57 @@ __global__ __launch_bounds__(256) void k_conc_runs(const uint32_t *__restrict__ 
     }
 }
 
-// One event of a flow's run decided by the reference state machine (CCFC:48-101), `now` in a register.
-struct ConcCtx {
-    const ConcEvent *ev;
-    const uint64_t *sval;
-    const uint32_t *relslot;
-    uint32_t *claim;
-    TokenTable TT;
-    const int64_t *flow_ids;
-    uint64_t id_base;
-    uint64_t *out;
-#ifdef SENTINEL_CONC_TRACE
-    uint64_t *trace;
-#endif
+// ---------------------------------------------------------------- decisions
+// After the sort a flow's events form a contiguous run in arrival order.  The batch is decided in four
+// data-parallel steps, so that no lane walks a chain of dependent gathers:
+//   k_conc_elems   one thread per sorted position gathers the event once and writes its element:
+//                  elem > 0 an acquire of elem tokens, elem < 0 a release of -elem tokens that found its
+//                  token cached and claimed it (the batch's first release of it, k_conc_prep), 0 a
+//                  release that answers ALREADY_RELEASE; relh = the released token's slot
+//   k_conc_lanes   one lane per run of <= CONC_LANE_RUN events: the CCFC:48-101 recurrence over the run's
+//                  elements (nowCalls in a register, integer work only), one pass byte per acquire;
+//                  longer runs are registered for the chunk kernels
+//   k_conc_info / k_conc_chunks   long runs in 1024-event chunks: a (min, +) scan with a decoupled
+//                  look-back for unit-acquire runs, a workgroup walk otherwise
+//   k_conc_apply   one thread per sorted position: a passing acquire takes a token (insert into the
+//                  cache, id = id_base + arrival position), a failing one answers BLOCKED, a claimed
+//                  release tombstones its token, the rest answer ALREADY_RELEASE
+// A release's amount is read in k_conc_elems, a kernel before any tombstone store, so a slot reused by an
+// insert of this batch can never hand a release someone else's amount.
+struct ConcElems {
+    int32_t *elem;
+    uint32_t *relh;
+    uint8_t *pass;
 };
 
-__device__ inline void conc_seq_event(const ConcCtx &C, uint32_t flow, double threshold, int32_t &now, uint32_t i,
-                                      int64_t &dlive, int64_t &dtomb) {
-    const uint32_t seq = (uint32_t)C.sval[i] & SEQ_MASK;
-    const ConcEvent e = C.ev[seq];
+__global__ __launch_bounds__(256) void k_conc_elems(const ConcEvent *__restrict__ ev, const uint64_t *__restrict__ sval,
+                                                    const uint32_t *__restrict__ skey, uint32_t invalid, int64_t n,
+                                                    const uint32_t *__restrict__ relslot,
+                                                    const uint32_t *__restrict__ claim, TokenTable TT, ConcElems X) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || skey[i] == invalid) return;             // invalid events were answered by k_conc_prep
+    const uint32_t seq = (uint32_t)sval[i] & SEQ_MASK;
+    const ConcEvent e = ev[seq];
+    int32_t x = 0;
     if (e.kind == CONC_ACQUIRE) {
-        // CCFC:57-71: int + int (wraps) compared with the double threshold
-        if ((double)(int32_t)((uint32_t)now + (uint32_t)e.acquire) > threshold) {
-            put_conc(C.out, seq, 0, ST_BLOCKED);
-            return;
-        }
-        const uint64_t id = C.id_base + seq;                                  // TokenCacheNode.java:59-70
-        bool tomb = false;
-        const int64_t h = token_insert(C.TT, id, tomb);
-        if (h < 0) {                                                          // token cache full
-            put_conc(C.out, seq, 0, ST_FAIL);
-            return;
-        }
-        if (tomb) --dtomb;
-        C.TT.flow_id[h] = C.flow_ids[flow];
-        C.TT.flow_idx[h] = (int32_t)flow;
-        C.TT.acquire[h] = e.acquire;
-        ++dlive;
-        now = (int32_t)((uint32_t)now + (uint32_t)e.acquire);
-        put_conc(C.out, seq, (int64_t)id, ST_OK);
+        x = e.acquire;                                    // > 0 (validated)
     } else {
-        const uint32_t h = C.relslot[seq];
-        if (C.claim[h] != seq) {                                              // an earlier release took it
-            put_conc(C.out, seq, 0, ST_ALREADY_RELEASE);
-            return;
+        const uint32_t h = relslot[seq];
+        if (claim[h] == seq) {                            // CCFC:82-86: this release finds its token
+            x = -TT.acquire[h];
+            X.relh[i] = h;
         }
-        // the token's amount is read BEFORE its slot becomes a tombstone: once it is one, an insert of
-        // any other flow (another lane of this kernel) may take the slot and write its own amount there;
-        // the release-ordered store keeps the load ahead of it
-        const int32_t amt = C.TT.acquire[h];
-        C.claim[h] = ~0u;
-        __hip_atomic_store(&C.TT.keys[h], (unsigned long long)TOKEN_TOMB, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_AGENT);                         // CCFC:92-100
-        --dlive;
-        ++dtomb;
-        now = (int32_t)((uint32_t)now - (uint32_t)amt);
-        put_conc(C.out, seq, 0, ST_RELEASE_OK);
     }
+    X.elem[i] = x;
 }
 
-// The effect of one decided scan element: a passing unit acquire takes a token, a failing one answers
-// BLOCKED; a release that found its token frees it; anything else is ALREADY_RELEASE.
-__device__ inline void conc_apply_item(const ConcCtx &C, uint32_t flow, int kind, bool pass, uint32_t seq, uint32_t h,
-                                       int32_t amount, int64_t &dlive, int64_t &dtomb) {
-    if (kind == 0) {
-        if (!pass) {
-            put_conc(C.out, seq, 0, ST_BLOCKED);
-            return;
-        }
-        const uint64_t id = C.id_base + seq;
-        bool tomb = false;
-        const int64_t hs = token_insert(C.TT, id, tomb);
-        if (hs < 0) {
-            put_conc(C.out, seq, 0, ST_FAIL);
-            return;
-        }
-        if (tomb) --dtomb;
-        C.TT.flow_id[hs] = C.flow_ids[flow];
-        C.TT.flow_idx[hs] = (int32_t)flow;
-        C.TT.acquire[hs] = amount;
-        ++dlive;
-        put_conc(C.out, seq, (int64_t)id, ST_OK);
-    } else if (kind == 1) {                               // (the amount was read by conc_item, before this)
-        C.claim[h] = ~0u;
-        __hip_atomic_store(&C.TT.keys[h], (unsigned long long)TOKEN_TOMB, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        --dlive;
-        ++dtomb;
-        put_conc(C.out, seq, 0, ST_RELEASE_OK);
-    } else {
-        put_conc(C.out, seq, 0, ST_ALREADY_RELEASE);
-    }
+// CCFC:57-70 for one acquire of `a` tokens at nowCalls `now`: int + int (wraps) compared with the double
+// threshold; passes -> now += a.
+__device__ inline bool conc_acquire(int32_t &now, int32_t a, double threshold) {
+    const int32_t sum = (int32_t)((uint32_t)now + (uint32_t)a);
+    if ((double)sum > threshold) return false;
+    now = sum;
+    return true;
 }
 
 #ifndef SENTINEL_CONC_LANE_RUN
@@ -284,10 +246,11 @@ __device__ inline int64_t conc_tprime(double threshold) {
     return (int64_t)floor(threshold);
 }
 
-#ifndef SENTINEL_CONC_TICKETS
-#define SENTINEL_CONC_TICKETS 1
-#endif
-constexpr uint32_t CONC_TICKETS = SENTINEL_CONC_TICKETS;
+// the scan element of a unit-acquire run's element x
+__device__ inline MinPlus conc_mp(int32_t x, int64_t Tp) {
+    return x > 0 ? MinPlus{1, Tp} : x < 0 ? MinPlus{(int64_t)x, CONC_INF} : MinPlus{0, CONC_INF};
+}
+
 constexpr int CB_THREADS = 256;
 constexpr int CB_WAVES = CB_THREADS / WAVE;
 
@@ -341,68 +304,48 @@ struct ConcBig {
     uint32_t epoch;
 };
 
-// One lane per flow run of <= CONC_LANE_RUN events: the run in arrival order; longer runs are cut into
-// chunks for k_conc_chunks.
-__global__ __launch_bounds__(256) void k_conc_process(ConcCtx C, const uint32_t *__restrict__ run_start,
-                                                      const uint32_t *__restrict__ skey, int32_t *__restrict__ now_calls,
-                                                      const double *__restrict__ thr, ConcBig G) {
-    __shared__ unsigned long long s_cnt[2];
-    if (threadIdx.x < 2) s_cnt[threadIdx.x] = 0;
-    __syncthreads();
+// One lane per flow run of <= CONC_LANE_RUN events: the run's elements in arrival order (read 8 at a time);
+// longer runs are cut into chunks for k_conc_chunks.
+__global__ __launch_bounds__(256) void k_conc_lanes(const uint32_t *__restrict__ run_start,
+                                                    const uint32_t *__restrict__ skey, int32_t *__restrict__ now_calls,
+                                                    const double *__restrict__ thr, ConcElems X, ConcBig G) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    int64_t dlive = 0, dtomb = 0;
-    if (r < G.ctl[0]) {
-        const uint32_t b = run_start[r], e = run_start[r + 1];
-        const uint32_t flow = skey[b];
-        if (e - b > CONC_LANE_RUN) {
-            const uint32_t slot = atomicAdd(&G.ctl[1], 1u);
-            const uint32_t nch = (e - b + CONC_CHUNK - 1) / CONC_CHUNK;
-            const uint32_t first = atomicAdd(&G.ctl[2], nch);
-            G.run[slot] = r;
-            G.now0[slot] = now_calls[flow];
-            G.tp[slot] = conc_tprime(thr[flow]);
-            G.unit[slot] = 1u;
-            G.mag[slot] = 0ull;
-            G.chunks[slot] = make_uint2(first, nch);
-            for (uint32_t j = 0; j < nch; ++j) {
-                G.chunk_slot[first + j] = slot;
-                G.chunk_j[first + j] = j;
-            }
-        } else {
-            int32_t now = now_calls[flow];
-            const double threshold = thr[flow];
-            for (uint32_t i = b; i < e; ++i) conc_seq_event(C, flow, threshold, now, i, dlive, dtomb);
-            now_calls[flow] = now;
+    if (r >= G.ctl[0]) return;
+    const uint32_t b = run_start[r], e = run_start[r + 1];
+    const uint32_t flow = skey[b];
+    if (e - b > CONC_LANE_RUN) {
+        const uint32_t slot = atomicAdd(&G.ctl[1], 1u);
+        const uint32_t nch = (e - b + CONC_CHUNK - 1) / CONC_CHUNK;
+        const uint32_t first = atomicAdd(&G.ctl[2], nch);
+        G.run[slot] = r;
+        G.now0[slot] = now_calls[flow];
+        G.tp[slot] = conc_tprime(thr[flow]);
+        G.unit[slot] = 1u;
+        G.mag[slot] = 0ull;
+        G.chunks[slot] = make_uint2(first, nch);
+        for (uint32_t j = 0; j < nch; ++j) {
+            G.chunk_slot[first + j] = slot;
+            G.chunk_j[first + j] = j;
+        }
+        return;
+    }
+    int32_t now = now_calls[flow];
+    const double threshold = thr[flow];
+    for (uint32_t i0 = b; i0 < e; i0 += 8) {
+        int32_t x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = i0 + k < e ? X.elem[i0 + k] : 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (x[k] > 0) X.pass[i0 + k] = conc_acquire(now, x[k], threshold) ? 1 : 0;
+            else if (x[k] < 0) now = (int32_t)((uint32_t)now + (uint32_t)x[k]);     // CCFC:97-98
         }
     }
-    if (dlive) atomicAdd(&s_cnt[0], (unsigned long long)dlive);
-    if (dtomb) atomicAdd(&s_cnt[1], (unsigned long long)dtomb);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (s_cnt[0]) atomicAdd(&C.TT.counts[0], (unsigned long long)s_cnt[0]);
-        if (s_cnt[1]) atomicAdd(&C.TT.counts[1], (unsigned long long)s_cnt[1]);
-    }
-}
-
-// Event i of a long run as a scan element: kind 0 acquire, 1 release that finds its token (its
-// amount), 2 neither (a later release of a token already released in this batch).
-__device__ inline void conc_item(const ConcCtx &C, uint32_t i, int &kind, int32_t &amt, uint32_t &seq, uint32_t &h) {
-    seq = (uint32_t)C.sval[i] & SEQ_MASK;
-    const ConcEvent ev = C.ev[seq];
-    kind = 2;
-    amt = 0;
-    h = 0;
-    if (ev.kind == CONC_ACQUIRE) {
-        kind = 0;
-        amt = ev.acquire;
-    } else {
-        h = C.relslot[seq];
-        if (C.claim[h] == seq) { kind = 1; amt = C.TT.acquire[h]; }
-    }
+    now_calls[flow] = now;
 }
 
 // Eligibility of the long runs for the scan: every acquire of 1 token, and the int sums cannot wrap.
-__global__ __launch_bounds__(256) void k_conc_info(ConcCtx C, const uint32_t *__restrict__ run_start, ConcBig G) {
+__global__ __launch_bounds__(256) void k_conc_info(const uint32_t *__restrict__ run_start, ConcElems X, ConcBig G) {
     const uint32_t nch = G.ctl[2];
     for (uint32_t c = blockIdx.x; c < nch; c += gridDim.x) {
         const uint32_t slot = G.chunk_slot[c], j = G.chunk_j[c];
@@ -411,25 +354,24 @@ __global__ __launch_bounds__(256) void k_conc_info(ConcCtx C, const uint32_t *__
         bool unit = true;
         unsigned long long mag = 0;
         for (uint32_t i = b + threadIdx.x; i < e; i += blockDim.x) {
-            int kind;
-            int32_t amt;
-            uint32_t seq, h;
-            conc_item(C, i, kind, amt, seq, h);
-            if (kind == 0 && amt != 1) unit = false;
-            if (kind != 2) mag += (unsigned long long)(amt < 0 ? -(int64_t)amt : (int64_t)amt);
+            const int32_t x = X.elem[i];
+            if (x > 1) unit = false;
+            mag += (unsigned long long)(x < 0 ? -(int64_t)x : (int64_t)x);
         }
-        if (!unit) atomicAnd(&G.unit[slot], 0u);
-        if (mag) atomicAdd(&G.mag[slot], mag);
+        if (__syncthreads_or(!unit) && threadIdx.x == 0) atomicAnd(&G.unit[slot], 0u);
+#pragma unroll
+        for (int o = WAVE / 2; o >= 1; o >>= 1) mag += __shfl_xor(mag, o, WAVE);
+        if (lane_id() == 0 && mag) atomicAdd(&G.mag[slot], mag);
     }
 }
 
-// A long run that cannot take the scan (an acquire of several tokens, an int sum that could wrap, or
-// nowCalls above T' when the batch starts): one workgroup walks it in 256-event chunks -- a chunk of
-// unit acquires whose sums cannot wrap by the scan (phase A: while y > T' only releases move y; phase
-// B: the (min, +) scan), any other chunk by thread 0 with the state machine.
-__device__ inline void conc_run_serial(const ConcCtx &C, uint32_t b, uint32_t e, uint32_t flow, double threshold,
+// A long run that cannot take the whole-run scan (an acquire of several tokens, an int sum that could
+// wrap, or nowCalls above T' when the batch starts): one workgroup walks it in 256-event steps -- a step
+// of unit acquires whose sums cannot wrap by the scan (phase A: while y > T' only releases move y;
+// phase B: the (min, +) scan), any other step by thread 0 with the recurrence.
+__device__ inline void conc_run_serial(const ConcElems &X, uint32_t b, uint32_t e, uint32_t flow, double threshold,
                                        int32_t *now_calls, MinPlus *s_mp, int64_t *s_red, int64_t *s_y0,
-                                       int32_t *s_now, int64_t &dlive, int64_t &dtomb) {
+                                       int32_t *s_now) {
     const uint32_t t = threadIdx.x;
     const uint32_t lane = lane_id();
     const int wave = t / WAVE;
@@ -439,13 +381,10 @@ __device__ inline void conc_run_serial(const ConcCtx &C, uint32_t b, uint32_t e,
     for (uint32_t c0 = b; c0 < e; c0 += CB_THREADS) {
         const uint32_t i = c0 + t;
         const bool act = i < e;
-        int kind = 2;
-        int32_t amt = 0;
-        uint32_t seq = 0, h = 0;
-        if (act) conc_item(C, i, kind, amt, seq, h);
-        const int64_t x = *s_now;
-        const bool unit = __syncthreads_and(kind != 0 || amt == 1);
-        int64_t mag = kind == 2 ? 0 : (amt < 0 ? -(int64_t)amt : (int64_t)amt);
+        const int32_t x = act ? X.elem[i] : 0;
+        const int64_t y = *s_now;
+        const bool unit = __syncthreads_and(x <= 1);
+        int64_t mag = x < 0 ? -(int64_t)x : (int64_t)x;
 #pragma unroll
         for (int o = WAVE / 2; o >= 1; o >>= 1) mag += __shfl_xor(mag, o, WAVE);
         if (lane == 0) s_red[wave] = mag;
@@ -453,21 +392,25 @@ __device__ inline void conc_run_serial(const ConcCtx &C, uint32_t b, uint32_t e,
         int64_t tot = 0;
         for (int q = 0; q < CB_WAVES; ++q) tot += s_red[q];
         __syncthreads();
-        if (!(unit && (x < 0 ? -x : x) + tot < (int64_t)INT32_MAX)) {         // block-uniform
+        if (!(unit && (y < 0 ? -y : y) + tot < (int64_t)INT32_MAX)) {          // block-uniform
             if (t == 0) {
-                int32_t now = (int32_t)x;
+                int32_t now = (int32_t)y;
                 const uint32_t c1 = min(e, c0 + CB_THREADS);
-                for (uint32_t q = c0; q < c1; ++q) conc_seq_event(C, flow, threshold, now, q, dlive, dtomb);
+                for (uint32_t q = c0; q < c1; ++q) {
+                    const int32_t xq = X.elem[q];
+                    if (xq > 0) X.pass[q] = conc_acquire(now, xq, threshold) ? 1 : 0;
+                    else if (xq < 0) now = (int32_t)((uint32_t)now + (uint32_t)xq);
+                }
                 *s_now = now;
             }
             __syncthreads();
             continue;
         }
         uint32_t first = 0;                               // first lane of phase B
-        bool never = false;                               // y stays > T' through the chunk
-        if (x > Tp) {                                     // phase A (block-uniform)
-            const MinPlus racc = mp_block_inclusive(MinPlus{kind == 1 ? -(int64_t)amt : 0, CONC_INF}, s_mp);
-            const bool reach = act && x + racc.p <= Tp;
+        bool never = false;                               // y stays > T' through the step
+        if (y > Tp) {                                     // phase A (block-uniform)
+            const MinPlus racc = mp_block_inclusive(MinPlus{x < 0 ? (int64_t)x : 0, CONC_INF}, s_mp);
+            const bool reach = act && y + racc.p <= Tp;
             const uint64_t bal = __builtin_amdgcn_ballot_w64(reach);
             if (lane == 0) s_red[wave] = bal ? (int64_t)(wave * WAVE + __ffsll((unsigned long long)bal) - 1) : (int64_t)CB_THREADS;
             __syncthreads();
@@ -475,32 +418,28 @@ __device__ inline void conc_run_serial(const ConcCtx &C, uint32_t b, uint32_t e,
             for (int q = 0; q < CB_WAVES; ++q) k = s_red[q] < k ? s_red[q] : k;
             if (k >= CB_THREADS) {
                 never = true;
-                if (t == CB_THREADS - 1) *s_y0 = x + racc.p;                   // every release applied
+                if (t == CB_THREADS - 1) *s_y0 = y + racc.p;                   // every release applied
             } else if ((int64_t)t == k) {
-                *s_y0 = x + racc.p;
+                *s_y0 = y + racc.p;
             }
             __syncthreads();
             first = (uint32_t)(k + 1);
         } else if (t == 0) {
-            *s_y0 = x;
+            *s_y0 = y;
         }
         __syncthreads();
         const int64_t y0 = *s_y0;
         bool pass = false;
         if (!never) {                                     // phase B (block-uniform)
-            MinPlus el{0, CONC_INF};
-            if (t >= first && act) {
-                if (kind == 0) el = MinPlus{1, Tp};
-                else if (kind == 1) el = MinPlus{-(int64_t)amt, CONC_INF};
-            }
+            const MinPlus el = (t >= first && act) ? conc_mp(x, Tp) : MinPlus{0, CONC_INF};
             const MinPlus inc = mp_block_inclusive(el, s_mp);
             const MinPlus exl = mp_block_exclusive_of(inc, s_mp);
-            pass = kind == 0 && t >= first && act && mp_apply(exl, y0) < Tp;
+            pass = x > 0 && t >= first && act && mp_apply(exl, y0) < Tp;
             if (t == CB_THREADS - 1) *s_now = (int32_t)mp_apply(inc, y0);
         } else if (t == 0) {
             *s_now = (int32_t)y0;
         }
-        if (act) conc_apply_item(C, flow, kind, pass, seq, h, 1, dlive, dtomb);
+        if (act && x > 0) X.pass[i] = pass ? 1 : 0;
         __syncthreads();
     }
     if (t == 0) now_calls[flow] = *s_now;
@@ -508,36 +447,25 @@ __device__ inline void conc_run_serial(const ConcCtx &C, uint32_t b, uint32_t e,
 
 // Chunks of long runs, one workgroup step each, taken in ticket order (a chunk's predecessors in its
 // run were taken earlier, so the look-back always completes).  An eligible run's chunk composes its
-// 1024 events (4 consecutive per thread), publishes the composition, looks back over its run's
-// earlier chunks for the prefix and decides its events from y = prefix(nowCalls); the run's last chunk
+// 1024 elements (4 consecutive per thread), publishes the composition, looks back over its run's
+// earlier chunks for the prefix and decides its acquires from y = prefix(nowCalls); the run's last chunk
 // writes nowCalls.  An ineligible run is walked whole by the workgroup that takes its first chunk.
-__global__ __launch_bounds__(CB_THREADS) void k_conc_chunks(ConcCtx C, const uint32_t *__restrict__ run_start,
+__global__ __launch_bounds__(CB_THREADS) void k_conc_chunks(const uint32_t *__restrict__ run_start,
                                                             const uint32_t *__restrict__ skey, int32_t *__restrict__ now_calls,
-                                                            const double *__restrict__ thr, ConcBig G) {
+                                                            const double *__restrict__ thr, ConcElems X, ConcBig G) {
     __shared__ MinPlus s_mp[CB_WAVES];
     __shared__ int64_t s_red[CB_WAVES];
     __shared__ int64_t s_y0;
     __shared__ int32_t s_now;
     __shared__ uint32_t s_ticket;
     __shared__ MinPlus s_prefix;
-    __shared__ unsigned long long s_cnt[2];
     const uint32_t t = threadIdx.x;
-    if (t < 2) s_cnt[t] = 0;
-    int64_t dlive = 0, dtomb = 0;
     const uint32_t nch = G.ctl[2];
-    // tickets are taken CONC_TICKETS at a time, a block decided in order (measured on --config 5conc:
-    // 1 ticket 0.82 ms, 4 tickets 3.7 ms, 16 tickets 4.4 ms -- a workgroup holding several chunks of a
-    // hot run decides them one after the other)
-    uint32_t cur = 0, lim = 0;
     for (;;) {
-        if (cur == lim) {
-            if (t == 0) s_ticket = atomicAdd(&G.ctl[3], (uint32_t)CONC_TICKETS);
-            __syncthreads();
-            cur = s_ticket;
-            lim = cur + CONC_TICKETS;
-            __syncthreads();
-        }
-        const uint32_t c = cur++;
+        if (t == 0) s_ticket = atomicAdd(&G.ctl[3], 1u);
+        __syncthreads();
+        const uint32_t c = s_ticket;
+        __syncthreads();
         if (c >= nch) break;
         const uint32_t slot = G.chunk_slot[c], j = G.chunk_j[c];
         const uint32_t r = G.run[slot];
@@ -545,33 +473,19 @@ __global__ __launch_bounds__(CB_THREADS) void k_conc_chunks(ConcCtx C, const uin
         const uint32_t flow = skey[rb];
         const int64_t now0 = G.now0[slot];
         const int64_t Tp = G.tp[slot];
-#ifdef SENTINEL_CONC_NOSCAN
-        const bool ok = false;
-#else
         const bool ok = G.unit[slot] && (now0 < 0 ? -now0 : now0) + (int64_t)G.mag[slot] < (int64_t)INT32_MAX && now0 <= Tp;
-#endif
         if (!ok) {                                        // block-uniform
-            if (j == 0) conc_run_serial(C, rb, re, flow, thr[flow], now_calls, s_mp, s_red, &s_y0, &s_now, dlive, dtomb);
+            if (j == 0) conc_run_serial(X, rb, re, flow, thr[flow], now_calls, s_mp, s_red, &s_y0, &s_now);
             continue;
         }
         const uint32_t b = rb + j * CONC_CHUNK;
-        int kind[4] = {2, 2, 2, 2};
-        int32_t amt[4] = {0, 0, 0, 0};
+        int32_t x[4];
         MinPlus mine{0, CONC_INF};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const uint32_t i = b + t * 4 + q;
-            if (i < re) {
-                int k2;
-                int32_t a2;
-                uint32_t s2, h2;
-                conc_item(C, i, k2, a2, s2, h2);
-                kind[q] = k2;
-                amt[q] = a2;
-            }
-            const MinPlus el = kind[q] == 0 ? MinPlus{1, Tp} : kind[q] == 1 ? MinPlus{-(int64_t)amt[q], CONC_INF}
-                                                                           : MinPlus{0, CONC_INF};
-            mine = mp_then(mine, el);
+            x[q] = i < re ? X.elem[i] : 0;
+            mine = mp_then(mine, conc_mp(x[q], Tp));
         }
         const MinPlus inc = mp_block_inclusive(mine, s_mp);
         const MinPlus exl = mp_block_exclusive_of(inc, s_mp);
@@ -635,28 +549,69 @@ __global__ __launch_bounds__(CB_THREADS) void k_conc_chunks(ConcCtx C, const uin
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const uint32_t i = b + t * 4 + q;
-            if (i < re) {
-                // (the event's position and token slot re-read here: carried in registers from the load
-                // loop above, the kind-2 results of a chunk were measured landing at position 0)
-                const uint32_t sq = (uint32_t)C.sval[i] & SEQ_MASK;
-                const uint32_t hq = kind[q] == 1 ? C.relslot[sq] : 0u;
-#ifdef SENTINEL_CONC_TRACE
-                C.trace[i] = ((uint64_t)(uint32_t)kind[q] << 32) | sq | ((uint64_t)t << 40);
-#endif
-                const bool pass = kind[q] == 0 && y < Tp;
-                if (kind[q] == 0) y = min(y + 1, Tp);
-                else if (kind[q] == 1) y -= amt[q];
-                conc_apply_item(C, flow, kind[q], pass, sq, hq, 1, dlive, dtomb);
+            if (i < re && x[q] > 0) {
+                X.pass[i] = y < Tp ? 1 : 0;
+                y = min(y + 1, Tp);
+            } else if (i < re && x[q] < 0) {
+                y += x[q];
             }
         }
         __syncthreads();
     }
-    if (dlive) atomicAdd(&s_cnt[0], (unsigned long long)dlive);
+}
+
+// The effects, one thread per sorted position (CCFC:57-100): a passing acquire takes a token
+// (TokenCacheNode, id = id_base + arrival position), a failing one answers BLOCKED; a claimed release
+// frees its slot (a tombstone: probe chains continue through it) and answers RELEASE_OK; any other
+// release ALREADY_RELEASE.  Cache counts {live, tombstones} by one atomic pair per workgroup.
+__global__ __launch_bounds__(256) void k_conc_apply(const uint64_t *__restrict__ sval, const uint32_t *__restrict__ skey,
+                                                    uint32_t invalid, int64_t n, ConcElems X, uint32_t *__restrict__ claim,
+                                                    TokenTable TT, const int64_t *__restrict__ flow_ids, uint64_t id_base,
+                                                    uint64_t *__restrict__ out) {
+    __shared__ unsigned long long s_cnt[2];
+    if (threadIdx.x < 2) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t dlive = 0, dtomb = 0;
+    const uint32_t flow = i < n ? skey[i] : invalid;
+    if (flow != invalid) {
+        const uint32_t seq = (uint32_t)sval[i] & SEQ_MASK;
+        const int32_t x = X.elem[i];
+        if (x > 0) {
+            if (!X.pass[i]) {
+                put_conc(out, seq, 0, ST_BLOCKED);                            // CCFC:57-69
+            } else {
+                const uint64_t id = id_base + seq;                            // TokenCacheNode.java:59-70
+                bool tomb = false;
+                const int64_t h = token_insert(TT, id, tomb);
+                if (h < 0) {                                                  // token cache full
+                    put_conc(out, seq, 0, ST_FAIL);
+                } else {
+                    if (tomb) --dtomb;
+                    TT.flow_id[h] = flow_ids[flow];
+                    TT.flow_idx[h] = (int32_t)flow;
+                    TT.acquire[h] = x;
+                    ++dlive;
+                    put_conc(out, seq, (int64_t)id, ST_OK);
+                }
+            }
+        } else if (x < 0) {
+            const uint32_t h = X.relh[i];
+            claim[h] = ~0u;
+            __hip_atomic_store(&TT.keys[h], (unsigned long long)TOKEN_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            --dlive;                                                          // CCFC:92-100
+            ++dtomb;
+            put_conc(out, seq, 0, ST_RELEASE_OK);
+        } else {
+            put_conc(out, seq, 0, ST_ALREADY_RELEASE);
+        }
+    }
+    if (dlive) atomicAdd(&s_cnt[0], (unsigned long long)dlive);    // (two's complement: wraps to a decrement)
     if (dtomb) atomicAdd(&s_cnt[1], (unsigned long long)dtomb);
     __syncthreads();
-    if (t == 0) {
-        if (s_cnt[0]) atomicAdd(&C.TT.counts[0], (unsigned long long)s_cnt[0]);
-        if (s_cnt[1]) atomicAdd(&C.TT.counts[1], (unsigned long long)s_cnt[1]);
+    if (threadIdx.x == 0) {
+        if (s_cnt[0]) atomicAdd(&TT.counts[0], s_cnt[0]);
+        if (s_cnt[1]) atomicAdd(&TT.counts[1], s_cnt[1]);
     }
 }
 

@@ -623,8 +623,8 @@ struct sentinel_engine {
     // pinned mirror {batch ordinal, d_pfresh after it} written by the device after every partition-path
     // param batch: the reserve check knows the exact fresh count up to a recent batch without a sync
     unsigned long long *h_pfresh = nullptr;
-    unsigned long long *h_cmband = nullptr;     // shared count-min bands: {min ts, ~max ts, overflow} read back
-    DevBuf d_cmband;
+    unsigned long long *h_cmband = nullptr;     // shared count-min key walk: the sub-range overflow flag read back
+    DevBuf d_cmband;                   // [0] overflow flag, [1..3] E_hi, E_hi seen by the read, the batch's newest epoch
     bool cm_keys = true;               // shared sketch: the two-phase key walk (k_pp_cm_read / _walk) when allowed
     uint64_t cm_key_batches = 0;       // shared-sketch batches decided by the key walk
     uint64_t cm_overflows = 0;         // ... sent to the per-rule lanes (a sub-range over PG_CAP requests)
@@ -752,6 +752,7 @@ struct sentinel_engine {
         w_hacq, w_segstart, w_segkey, w_segep, w_segacq, w_het, w_prio, w_done, w_s0, w_k, w_counters;
     DevBuf w_vslot;                    // slot of every value of a param batch
     DevBuf w_runs;                     // partition path: long-run / oversized-half work lists
+    DevBuf w_runrec;                   // partition path, split kernels: {start in gsval, events} per flow
     DevBuf w_pscan;                    // partition path: per-group range sums + range starts
     DevBuf io_ev, io_fl, io_out, io_vals;
     // streamed host path (sentinel_submit_flow_stream_host): copy streams + two staging slots
@@ -1623,7 +1624,23 @@ static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTa
 #define SENTINEL_ALLBIG_PCT 90
 #endif
     const bool all_big = n > (int64_t)nparts * (int64_t)(PH_KEYS * SENTINEL_ALLBIG_PCT / 100);
-    if (!all_big) {
+#ifdef SENTINEL_PART_FUSED
+    const bool split = false;
+#else
+    // halves of 512 flows (flow tables of 2^19..2^20 flows): the LDS sort and the decisions in two kernels
+    const bool split = !part_coop(lb) && lb == PART_MAX_BITS;
+#endif
+    if (!all_big && split) {
+        uint2 *runrec = e->w_runrec.as<uint2>();
+        e->launch("part_sort", n, s, [&] {
+            k_part_sort<<<16u * (unsigned)((nparts + 7) / 8), PH_THREADS, 0, s>>>(pval, gsval, rstart, lb, nparts, LR, big,
+                                                                              nbig, stat, runrec);
+        });
+        e->launch("part_decide", n, s, [&] {
+            k_part_decide<NMAX><<<32u * (unsigned)((nparts + 7) / 8), 256, 0, s>>>(FT, gsval, runrec, lb, nparts,
+                                                                                 (int32_t)e->rules.size(), src, V);
+        });
+    } else if (!all_big) {
         e->launch("part_fused", n, s, [&] {
             const dim3 g(16u * (unsigned)((nparts + 7) / 8));
             if (part_coop(lb))      // <= 256 flows per half: cooperative verdict sweep
@@ -1673,6 +1690,7 @@ static int ensure_part_bufs(sentinel_engine_t *e, const PartBufs &B, int64_t n) 
     int rc = B.pscan->ensure(((size_t)g.ng * g.nparts + 2 * (size_t)g.nparts + 1) * 4);
     rc |= B.runs->ensure(long_runs_bytes(n, LONG_RUN, 4 + 2 * (size_t)g.nparts));
     rc |= B.stat->ensure(8);
+    if (g.lb == PART_MAX_BITS) rc |= e->w_runrec.ensure(((size_t)g.nparts << g.lb) * sizeof(uint2));
     return rc;
 }
 
@@ -3847,21 +3865,22 @@ static int submit_concurrent(sentinel_engine_t *e, int64_t n, const ConcEvent *d
             k_conc_runs<<<grid_for(n), 256, 0, s>>>(skey, n, finvalid, flag, run_start, ctl);
         });
         const uint64_t id_base = (e->tok_salt << 40) | e->tok_counter;
-#ifdef SENTINEL_CONC_TRACE
-        HIP_OK(hipMemsetAsync(e->w_vtmp.p, 0xFF, n * 8, s));
-        const ConcCtx C{dev, e->w_sval.as<uint64_t>(), relslot, claim, TT, e->d_flow_ids.as<int64_t>(), id_base, dout,
-                        e->w_vtmp.as<uint64_t>()};
-#else
-        const ConcCtx C{dev, e->w_sval.as<uint64_t>(), relslot, claim, TT, e->d_flow_ids.as<int64_t>(), id_base, dout};
-#endif
-        const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, mc));
-        e->launch("conc_process", n, s, [&] {
-            k_conc_process<<<grid_for(n), 256, 0, s>>>(C, run_start, skey, e->d_now.as<int32_t>(),
-                                                       e->d_conc_thr.as<double>(), G);
+        const ConcElems X{e->w_hacq.as<int32_t>(), e->w_segacq.as<uint32_t>(), e->w_done.as<uint8_t>()};
+        e->launch("conc_elems", n, s, [&] {
+            k_conc_elems<<<grid_for(n), 256, 0, s>>>(dev, e->w_sval.as<uint64_t>(), skey, finvalid, n, relslot, claim, TT, X);
         });
-        e->launch("conc_info", n, s, [&] { k_conc_info<<<g, 256, 0, s>>>(C, run_start, G); });
+        const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, mc));
+        e->launch("conc_lanes", n, s, [&] {
+            k_conc_lanes<<<grid_for(n), 256, 0, s>>>(run_start, skey, e->d_now.as<int32_t>(), e->d_conc_thr.as<double>(),
+                                                     X, G);
+        });
+        e->launch("conc_info", n, s, [&] { k_conc_info<<<g, 256, 0, s>>>(run_start, X, G); });
         e->launch("conc_chunks", n, s, [&] {
-            k_conc_chunks<<<g, CB_THREADS, 0, s>>>(C, run_start, skey, e->d_now.as<int32_t>(), e->d_conc_thr.as<double>(), G);
+            k_conc_chunks<<<g, CB_THREADS, 0, s>>>(run_start, skey, e->d_now.as<int32_t>(), e->d_conc_thr.as<double>(), X, G);
+        });
+        e->launch("conc_apply", n, s, [&] {
+            k_conc_apply<<<grid_for(n), 256, 0, s>>>(e->w_sval.as<uint64_t>(), skey, finvalid, n, X, claim, TT,
+                                                     e->d_flow_ids.as<int64_t>(), id_base, dout);
         });
         e->tok_counter += (uint64_t)n;
     }
@@ -3896,23 +3915,6 @@ int sentinel_submit_concurrent_batch(sentinel_engine_t *e, int64_t n, const sent
     hipStream_t fs_s = stream ? (hipStream_t)stream : e->stream;
     const ForeignStream fs_(e, fs_s);
     return submit_concurrent(e, n, (const ConcEvent *)ev, (uint64_t *)out, fs_s);
-}
-
-// Debug: the last concurrency batch's sorted keys / values, run starts, counters and the long-run slot 0.
-int sentinel_debug_conc_state(sentinel_engine_t *e, int64_t n, uint32_t *skey, uint64_t *sval, uint32_t *run_start,
-                              uint32_t *ctl, uint32_t *relslot) {
-    if (!e) return -1;
-    std::lock_guard<std::mutex> g(e->mu);
-    HIP_OK(hipStreamSynchronize(e->stream));
-    HIP_OK(hipMemcpy(skey, e->w_skey.p, n * 4, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(sval, e->w_sval.p, n * 8, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(run_start, e->w_segstart.p, (n + 1) * 4, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(ctl, e->w_counters.p, 16, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(relslot, e->w_k.p, n * 4, hipMemcpyDeviceToHost));
-#ifdef SENTINEL_CONC_TRACE
-    HIP_OK(hipMemcpy(sval, e->w_vtmp.p, n * 8, hipMemcpyDeviceToHost));     // (the trace instead of the values)
-#endif
-    return 0;
 }
 
 int sentinel_concurrent_now_calls(sentinel_engine_t *e, int32_t flow_idx, int32_t *now_calls) {

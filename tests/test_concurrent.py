@@ -251,3 +251,45 @@ def test_gpu_qps_and_concurrent_batches_interleaved(oracle_mod):
             outstanding = [x for x in outstanding if x not in released] + tok_g[ok].tolist()
     for f in range(0, F, 11):
         assert svc.concurrent_now_calls(f) == orc.concurrent_now_calls(f)
+
+
+@pytest.mark.gpu
+def test_gpu_concurrent_mixed_amounts_tombstone_reuse(oracle_mod, monkeypatch):
+    """Acquires of 1..5 tokens and releases of the previous batches' tokens share every batch, on 3000
+    flows, through a small token cache: inserts of a batch reuse the tombstones its own releases leave.
+    A release's amount must be its own token's (read before its slot can be reused), so nowCalls of
+    every flow and every status equal the oracle's."""
+    import sentinel_amd as sa
+    monkeypatch.setenv("SENTINEL_TOKEN_CAPACITY", "16384")
+    rng = np.random.default_rng(808)
+    F = 3000
+    rules = [_rule(int(f), float(rng.integers(4, 40)), 1) for f in range(1, F + 1)]
+    svc = sa.GpuTokenService(0)
+    svc.load_flow_rules([sa.FlowRule(count=r["count"], cluster_config=sa.ClusterFlowConfig(
+        flow_id=r["flow_id"], threshold_type=1)) for r in rules])
+    orc = oracle_mod.TokenServiceOracle(rules)
+    outstanding = []
+    for b in range(10):
+        n = 24_000
+        kind = (rng.random(n) < 0.5).astype(np.int32)
+        if not outstanding:
+            kind[:] = 0
+        fidx = T.zipf_indices(F, 0.9, n, rng)
+        acq = rng.integers(1, 6, size=n).astype(np.int32)
+        tok = np.zeros(n, np.int64)
+        rel = np.nonzero(kind == 1)[0]
+        if len(rel):
+            pool = np.array(outstanding, np.int64)
+            tok[rel] = pool[rng.permutation(len(pool))[:len(rel)]] if len(pool) >= len(rel) else pool[rng.integers(0, len(pool), size=len(rel))]
+        st_g, tok_g = _device_batch(svc, fidx, acq, tok, kind, np.ones(n, np.int32))
+        ev = np.zeros(n, dtype=orc.CONC_EVENT)
+        ev["flow_idx"], ev["acquire"], ev["token_id"], ev["kind"], ev["flags"] = fidx, acq, tok, kind, 1
+        st_o, _ = orc.concurrent_replay(ev, tok_g)
+        bad = np.nonzero(st_g != st_o)[0]
+        assert len(bad) == 0, (b, len(bad), bad[:5], st_g[bad[:5]], st_o[bad[:5]])
+        released = set(tok[(kind == 1) & (st_g == 6)].tolist())
+        outstanding = [x for x in outstanding if x not in released] + tok_g[st_g == 0].tolist()
+        for f in range(0, F, 13):
+            assert svc.concurrent_now_calls(f) == orc.concurrent_now_calls(f), (b, f)
+        assert svc.concurrent_token_count() == orc.concurrent_token_count()
+    assert (st_o == 6).any() and (st_o == 1).any() and (st_o == 0).any()

@@ -439,16 +439,19 @@ def test_partition_ballot_ranking_split_halves(oracle_mod):
     _compare(_engine(rules), _oracle(oracle_mod, rules), rules, ev, batches=2)
 
 
-def test_partition_oversized_half(oracle_mod):
-    """65536 flows (64 per range): one half of one range gets ~7000 events (more than fit in LDS)
-    while its range stays under the key capacity, so that half goes through k_part_big and the
-    other half through k_part_half, both writing the same range."""
+@pytest.mark.parametrize("hot_frac", [0.024, 0.045])
+def test_partition_oversized_half(oracle_mod, hot_frac):
+    """65536 flows (64 per range): one half of one range gets ~7000 events (0.024: more than fit in
+    LDS while its range stays under the key capacity, so that half is sorted through HBM and the other
+    half stays in LDS, both writing the same range) or ~13500 (0.045: the range exceeds the key
+    capacity, both halves through HBM).  Oversized halves are listed by k_part_half and decided by
+    k_part_big."""
     rng = np.random.default_rng(47)
     F = 65536
     rules = T.make_rules(F, rng, count_lo=5, count_hi=500, sample_count=10, window_interval_ms=1000)
     n = 300_000
     idx = rng.integers(0, F, size=n).astype(np.int32)
-    hot = rng.random(n) < 0.024                    # ~7200 events into flows 352..383 (range 5, half 1)
+    hot = rng.random(n) < hot_frac                 # into flows 352..383 (range 5, half 1)
     idx[hot] = 352 + rng.integers(0, 32, size=int(hot.sum()))
     ts = T.timestamps(n, 400_000.0, T.T0_ALIGNED + 3)
     ev = T.Events(idx, np.ones(n, np.int32), ts.astype(np.int64), None)
