@@ -307,6 +307,14 @@ class FlowWorkload:
             # the rolled bucket's 16-B pair, read + write its BLOCK / PASS_REQUEST / BLOCK_REQUEST
             # counters (3 x 8 B each way, blocked counter rows)
             return 16.0 + (n * 16 + 42 + 16 + 48) / max(1.0, e_f)
+        if dom == "part_decide":
+            # the fused kernel's decide half: per event the sorted value read back from gsval (8) and the
+            # verdict (8); per touched flow its run record (8), the window header (16 n), the rule fields
+            # (42), the rolled pair written (16), the rolled slot's three rest counters read + written (48)
+            return 16.0 + (8 + n * 16 + 42 + 16 + 48) / max(1.0, e_f)
+        if dom == "part_sort":
+            # per event: the packed value read (8) and written to gsval (8); per flow its run record (8)
+            return 16.0 + 8.0 / max(1.0, e_f)
         if dom == "radix_scatter":
             passes = max(1, round(d["calls"] / max(1, steps)))
             return (32.0 + 24.0 * (passes - 1)) / passes

@@ -4100,32 +4100,48 @@ static int param_top(sentinel_engine_t *e, int64_t ts, int32_t number, hipStream
     HIP_OK(hipMemsetAsync(dcount.p, 0, (size_t)std::max(R, 1) * 4, s));
     if (R == 0 || !e->d_ptable.p || e->pmode != SENTINEL_PARAM_EXACT) return 0;
     const uint64_t cap = e->pcap;
-    DevBuf sums, pr, pk, cr, ck;
-    rc |= sums.ensure(cap * 8);
+    // candidate list {key, rule, sum} (slots with a non-zero window sum at ts), sized for the live slots
+    // (live after the last rebuild + the reserved upper bound of inserts since); a longer list than that
+    // (never expected) reruns the selection with room for the whole table
+    uint64_t mc = std::min<uint64_t>(cap, e->p_live + e->p_ub + 1);
+  again:
+    DevBuf ckey, crule, csum, cn, pr, pk, cr, ck;
+    rc |= ckey.ensure(mc * 8);
+    rc |= crule.ensure(mc * 4);
+    rc |= csum.ensure(mc * 8);
+    rc |= cn.ensure(8);
     for (DevBuf *b : {&pr, &pk, &cr, &ck}) rc |= b->ensure((size_t)R * 8);
     if (rc) return SENTINEL_E_NOMEM;
     const PSlots T{e->d_ptable.as<unsigned long long>(), e->d_slot_rule.as<int32_t>(), e->pt.state.as<int64_t>(),
                    param_stride(e->pmax_n), cap - 1};
-    const unsigned g = grid_for((int64_t)cap);
-    k_ptop_sums<<<g, 256, 0, s>>>(T, cap, R, e->d_prule_n.as<int32_t>(), e->d_prule_w.as<int32_t>(),
-                                  e->d_prule_rcp.as<double>(), ts, sums.as<int64_t>());
+    const TopCands C{ckey.as<unsigned long long>(), crule.as<int32_t>(), csum.as<int64_t>(), cn.as<unsigned long long>(), mc};
+    HIP_OK(hipMemsetAsync(cn.p, 0, 8, s));
+    k_ptop_sums<<<grid_for((int64_t)cap), 256, 0, s>>>(T, cap, R, e->d_prule_n.as<int32_t>(), e->d_prule_w.as<int32_t>(),
+                                                       e->d_prule_rcp.as<double>(), ts, C);
     HIP_OK(hipMemsetAsync(pr.p, 0, (size_t)R * 8, s));
     HIP_OK(hipMemsetAsync(pk.p, 0, (size_t)R * 8, s));
     HIP_OK(hipMemsetAsync(cr.p, 0, (size_t)R * 8, s));
     HIP_OK(hipMemsetAsync(ck.p, 0xFF, (size_t)R * 8, s));
+    const unsigned g = (unsigned)std::min<uint64_t>(2048, (mc + 255) / 256);   // grid-stride over the candidates
     for (int k = 0; k < number; ++k) {
-        k_ptop_best_sum<<<g, 256, 0, s>>>(T, cap, sums.as<int64_t>(), pr.as<unsigned long long>(), pk.as<unsigned long long>(),
-                                         cr.as<unsigned long long>());
-        k_ptop_best_key<<<g, 256, 0, s>>>(T, cap, sums.as<int64_t>(), pr.as<unsigned long long>(), pk.as<unsigned long long>(),
+        k_ptop_best_sum<<<g, 256, 0, s>>>(C, pr.as<unsigned long long>(), pk.as<unsigned long long>(), cr.as<unsigned long long>());
+        k_ptop_best_key<<<g, 256, 0, s>>>(C, pr.as<unsigned long long>(), pk.as<unsigned long long>(),
                                          cr.as<unsigned long long>(), ck.as<unsigned long long>());
-        k_ptop_take<<<g, 256, 0, s>>>(T, cap, sums.as<int64_t>(), cr.as<unsigned long long>(), ck.as<unsigned long long>(), k,
-                                     number, dkey.as<uint64_t>(), dsum.as<int64_t>());
+        k_ptop_take<<<g, 256, 0, s>>>(C, cr.as<unsigned long long>(), ck.as<unsigned long long>(), k, number,
+                                     dkey.as<uint64_t>(), dsum.as<int64_t>());
         k_ptop_advance<<<grid_for(R), 256, 0, s>>>(R, pr.as<unsigned long long>(), pk.as<unsigned long long>(),
                                                   cr.as<unsigned long long>(), ck.as<unsigned long long>(), dcount.as<int32_t>());
     }
     HIP_OK(hipGetLastError());
+    unsigned long long found = 0;
+    HIP_OK(hipMemcpyAsync(&found, cn.p, 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));        // the temporaries are freed below
-    for (DevBuf *b : {&sums, &pr, &pk, &cr, &ck}) b->release();
+    for (DevBuf *b : {&ckey, &crule, &csum, &cn, &pr, &pk, &cr, &ck}) b->release();
+    if (found > mc && mc < cap) {
+        mc = cap;
+        HIP_OK(hipMemsetAsync(dcount.p, 0, (size_t)std::max(R, 1) * 4, s));
+        goto again;
+    }
     return 0;
 }
 

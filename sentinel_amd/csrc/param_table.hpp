@@ -143,22 +143,45 @@ __global__ __launch_bounds__(256) void k_ptable_import(const int64_t *__restrict
 // Per live slot at time ts: the value's window sum over its valid buckets (a read-only view equals
 // the sum after currentWindow(): the roll only empties an invalid bucket), and (int) of it, the
 // reference's sort key ((int) b - (int) a, ClusterParamMetric.java:107-113).  Values with no count
-// have no CacheMap entry in the reference and are not candidates.
+// have no CacheMap entry in the reference and are not candidates: only slots with a non-zero sum are
+// appended (wave-aggregated) to a compact candidate list {key, rule, sum}, and the selection rounds run
+// over that list instead of the whole table.
+struct TopCands {
+    unsigned long long *key;
+    int32_t *rule;
+    int64_t *sum;
+    unsigned long long *n;      // candidates found (may exceed cap: the caller retries with a larger list)
+    unsigned long long cap;
+};
+
 __global__ __launch_bounds__(256) void k_ptop_sums(PSlots T, uint64_t cap, int32_t R, const int32_t *__restrict__ rn,
                                                    const int32_t *__restrict__ rw, const double *__restrict__ rrcp,
-                                                   int64_t ts, int64_t *__restrict__ sum) {
+                                                   int64_t ts, TopCands C) {
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= cap) return;
     int64_t v = 0;
-    if (T.keys[s] != PKEY_EMPTY && (uint32_t)T.rule[s] < (uint32_t)R) {   // sum 0: not a candidate
-        const int32_t r = T.rule[s];
+    unsigned long long key = PKEY_EMPTY;
+    int32_t r = 0;
+    if (s < cap) key = T.keys[s];
+    if (key != PKEY_EMPTY && (uint32_t)(r = T.rule[s]) < (uint32_t)R) {   // sum 0: not a candidate
         const int n = rn[r];
         const int64_t E = epoch_of(ts, rw[r], rrcp[r]);
         const int64_t *st = T.state + (int64_t)s * T.stride;
         for (int j = 0; j < n; ++j)
             if (st[2 * j] != EPOCH_ABSENT && st[2 * j] > E - n) v = wrap_add(v, st[2 * j + 1]);
     }
-    sum[s] = v;
+    const uint64_t act = __builtin_amdgcn_ballot_w64(v != 0);
+    if (!act) return;
+    const uint32_t lane = lane_id();
+    const int first = __ffsll((unsigned long long)act) - 1;
+    unsigned long long base = 0;
+    if ((int)lane == first) base = atomicAdd(C.n, (unsigned long long)__popcll(act));
+    base = __shfl(base, first, WAVE);
+    const unsigned long long k = base + (unsigned long long)__popcll(act & ((1ull << lane) - 1ull));
+    if (v != 0 && k < C.cap) {
+        C.key[k] = key;
+        C.rule[k] = r;
+        C.sum[k] = v;
+    }
 }
 
 // Order (int) sum descending, key ascending; `prev` = the rule's previous pick (none in round 0).
@@ -169,47 +192,43 @@ __device__ inline bool top_after(uint64_t rk, uint64_t key, uint64_t prk, uint64
 }
 
 // Round phase A: best (int) sum among the candidates after the previous pick.
-__global__ __launch_bounds__(256) void k_ptop_best_sum(PSlots T, uint64_t cap, const int64_t *__restrict__ sum,
-                                                       const unsigned long long *__restrict__ prev_rank,
+__global__ __launch_bounds__(256) void k_ptop_best_sum(TopCands C, const unsigned long long *__restrict__ prev_rank,
                                                        const unsigned long long *__restrict__ prev_key,
                                                        unsigned long long *__restrict__ cand_rank) {
-    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= cap) return;
-    const unsigned long long key = T.keys[s];
-    if (key == PKEY_EMPTY || sum[s] == 0) return;
-    const int32_t r = T.rule[s];
-    const uint64_t rk = top_rank(sum[s]);
-    if (top_after(rk, key, prev_rank[r], prev_key[r])) atomicMax(&cand_rank[r], (unsigned long long)rk);
+    const unsigned long long m = *C.n < C.cap ? *C.n : C.cap;
+    for (unsigned long long k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (uint64_t)gridDim.x * blockDim.x) {
+        const int32_t r = C.rule[k];
+        const uint64_t rk = top_rank(C.sum[k]);
+        if (top_after(rk, C.key[k], prev_rank[r], prev_key[r])) atomicMax(&cand_rank[r], (unsigned long long)rk);
+    }
 }
 
 // Round phase B: smallest key with that (int) sum (after the previous pick).
-__global__ __launch_bounds__(256) void k_ptop_best_key(PSlots T, uint64_t cap, const int64_t *__restrict__ sum,
-                                                       const unsigned long long *__restrict__ prev_rank,
+__global__ __launch_bounds__(256) void k_ptop_best_key(TopCands C, const unsigned long long *__restrict__ prev_rank,
                                                        const unsigned long long *__restrict__ prev_key,
                                                        const unsigned long long *__restrict__ cand_rank,
                                                        unsigned long long *__restrict__ cand_key) {
-    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= cap) return;
-    const unsigned long long key = T.keys[s];
-    if (key == PKEY_EMPTY || sum[s] == 0) return;
-    const int32_t r = T.rule[s];
-    const uint64_t rk = top_rank(sum[s]);
-    if (rk == cand_rank[r] && top_after(rk, key, prev_rank[r], prev_key[r])) atomicMin(&cand_key[r], key);
+    const unsigned long long m = *C.n < C.cap ? *C.n : C.cap;
+    for (unsigned long long k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (uint64_t)gridDim.x * blockDim.x) {
+        const int32_t r = C.rule[k];
+        const uint64_t rk = top_rank(C.sum[k]);
+        const unsigned long long key = C.key[k];
+        if (rk == cand_rank[r] && top_after(rk, key, prev_rank[r], prev_key[r])) atomicMin(&cand_key[r], key);
+    }
 }
 
 // Round phase C: the pick's long sum (keys are unique) -> the rule's k-th entry.
-__global__ __launch_bounds__(256) void k_ptop_take(PSlots T, uint64_t cap, const int64_t *__restrict__ sum,
-                                                   const unsigned long long *__restrict__ cand_rank,
-                                                   const unsigned long long *__restrict__ cand_key, int k, int number,
+__global__ __launch_bounds__(256) void k_ptop_take(TopCands C, const unsigned long long *__restrict__ cand_rank,
+                                                   const unsigned long long *__restrict__ cand_key, int kth, int number,
                                                    uint64_t *__restrict__ out_key, int64_t *__restrict__ out_sum) {
-    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= cap) return;
-    const unsigned long long key = T.keys[s];
-    if (key == PKEY_EMPTY || sum[s] == 0) return;
-    const int32_t r = T.rule[s];
-    if (cand_rank[r] != 0 && key == cand_key[r]) {
-        out_key[(int64_t)r * number + k] = key;
-        out_sum[(int64_t)r * number + k] = sum[s];
+    const unsigned long long m = *C.n < C.cap ? *C.n : C.cap;
+    for (unsigned long long k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (uint64_t)gridDim.x * blockDim.x) {
+        const int32_t r = C.rule[k];
+        const unsigned long long key = C.key[k];
+        if (cand_rank[r] != 0 && key == cand_key[r]) {
+            out_key[(int64_t)r * number + kth] = key;
+            out_sum[(int64_t)r * number + kth] = C.sum[k];
+        }
     }
 }
 
