@@ -745,7 +745,10 @@ def main():
         W.submit(lat_b[i % K])
         tev1[i].record(ext)
     torch.cuda.synchronize()
-    lat = sorted(tev0[i].elapsed_time(tev1[i]) for i in range(L))
+    lat_seq = [tev0[i].elapsed_time(tev1[i]) for i in range(L)]
+    lat = sorted(lat_seq)
+    slow = sorted(range(L), key=lambda i: -lat_seq[i])[:8]
+    log("slowest batches of the latency loop (index: ms): " + ", ".join(f"{i}: {lat_seq[i]:.3f}" for i in sorted(slow)))
     hl = []
     for i in range(L):
         if i % K == 0:

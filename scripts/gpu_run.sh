@@ -21,7 +21,7 @@ for S in "$@"; do
     tests*)
       SEL=${S#tests}; SEL=${SEL#=}; SEL=${SEL:-tests}
       echo "== tests $SEL"
-      timeout -k 10 600 python -u -m pytest $SEL -m gpu -x -v --timeout 240 --timeout-method thread > $O/tests_$n.log 2>&1
+      timeout -k 10 600 python -u -m pytest $SEL -m gpu -x -v --timeout 120 --timeout-method thread > $O/tests_$n.log 2>&1
       rc=$?; tail -3 $O/tests_$n.log
       [ $rc -eq 0 ] || { grep -E "Error|assert|FAIL" $O/tests_$n.log | head -30; exit $rc; } ;;
     smoke)

@@ -59,18 +59,27 @@ __device__ inline int64_t token_find(const TokenTable &T, uint64_t id) {
 // included -- released tokens' slots are reused, so the cache does not fill up with tombstones under a
 // steady acquire / release churn (lookups skip tombstones and stop at an empty slot, which a reuse
 // never creates or removes).  `tomb` tells whether a tombstone was taken.
+// Many inserts run at once (k_conc_apply): a lost CAS re-examines the slot with the value the CAS
+// returned -- a plain re-load could keep answering the stale free slot from this CU's cache and spin.
 __device__ inline int64_t token_insert(const TokenTable &T, uint64_t id, bool &tomb) {
     uint64_t h = mix64(id) & T.mask;
-    for (uint64_t p = 0; p <= T.mask; ++p) {
-        const unsigned long long k = T.keys[h];
+    unsigned long long k = T.keys[h];
+    for (uint64_t p = 0; p <= T.mask;) {
         if (k == PKEY_EMPTY || k == TOKEN_TOMB) {
-            if (atomicCAS(&T.keys[h], k, (unsigned long long)id) == k) {
+            const unsigned long long prev = atomicCAS(&T.keys[h], k, (unsigned long long)id);
+            if (prev == k) {
                 tomb = k == TOKEN_TOMB;
                 return (int64_t)h;
             }
-            continue;                                     // lost the slot: look at it again
+            k = prev;                                     // taken (or changed) meanwhile: look again
+#ifdef SENTINEL_CONC_GUARD
+            if (++p > T.mask) { printf("token_insert: CAS spin id %llx h %llu\n", (unsigned long long)id, (unsigned long long)h); return -1; }
+#endif
+            continue;
         }
         h = (h + 1) & T.mask;
+        ++p;
+        k = T.keys[h];
     }
     return -1;
 }
@@ -366,83 +375,19 @@ __global__ __launch_bounds__(256) void k_conc_info(const uint32_t *__restrict__ 
 }
 
 // A long run that cannot take the whole-run scan (an acquire of several tokens, an int sum that could
-// wrap, or nowCalls above T' when the batch starts): one workgroup walks it in 256-event steps -- a step
-// of unit acquires whose sums cannot wrap by the scan (phase A: while y > T' only releases move y;
-// phase B: the (min, +) scan), any other step by thread 0 with the recurrence.
-__device__ inline void conc_run_serial(const ConcElems &X, uint32_t b, uint32_t e, uint32_t flow, double threshold,
-                                       int32_t *now_calls, MinPlus *s_mp, int64_t *s_red, int64_t *s_y0,
-                                       int32_t *s_now) {
-    const uint32_t t = threadIdx.x;
-    const uint32_t lane = lane_id();
-    const int wave = t / WAVE;
-    const int64_t Tp = conc_tprime(threshold);
-    if (t == 0) *s_now = now_calls[flow];
-    __syncthreads();
-    for (uint32_t c0 = b; c0 < e; c0 += CB_THREADS) {
-        const uint32_t i = c0 + t;
-        const bool act = i < e;
-        const int32_t x = act ? X.elem[i] : 0;
-        const int64_t y = *s_now;
-        const bool unit = __syncthreads_and(x <= 1);
-        int64_t mag = x < 0 ? -(int64_t)x : (int64_t)x;
+// wrap, or nowCalls above T' when the batch starts): its elements walked by one thread with the
+// CCFC:57-98 recurrence (integer work on the gathered elements only: rare runs, no barriers).
+__device__ inline void conc_run_serial(const ConcElems &X, uint32_t b, uint32_t e, double threshold, int32_t &now) {
+    for (uint32_t i0 = b; i0 < e; i0 += 8) {
+        int32_t x[8];
 #pragma unroll
-        for (int o = WAVE / 2; o >= 1; o >>= 1) mag += __shfl_xor(mag, o, WAVE);
-        if (lane == 0) s_red[wave] = mag;
-        __syncthreads();
-        int64_t tot = 0;
-        for (int q = 0; q < CB_WAVES; ++q) tot += s_red[q];
-        __syncthreads();
-        if (!(unit && (y < 0 ? -y : y) + tot < (int64_t)INT32_MAX)) {          // block-uniform
-            if (t == 0) {
-                int32_t now = (int32_t)y;
-                const uint32_t c1 = min(e, c0 + CB_THREADS);
-                for (uint32_t q = c0; q < c1; ++q) {
-                    const int32_t xq = X.elem[q];
-                    if (xq > 0) X.pass[q] = conc_acquire(now, xq, threshold) ? 1 : 0;
-                    else if (xq < 0) now = (int32_t)((uint32_t)now + (uint32_t)xq);
-                }
-                *s_now = now;
-            }
-            __syncthreads();
-            continue;
+        for (int k = 0; k < 8; ++k) x[k] = i0 + k < e ? X.elem[i0 + k] : 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (x[k] > 0) X.pass[i0 + k] = conc_acquire(now, x[k], threshold) ? 1 : 0;
+            else if (x[k] < 0) now = (int32_t)((uint32_t)now + (uint32_t)x[k]);     // CCFC:97-98
         }
-        uint32_t first = 0;                               // first lane of phase B
-        bool never = false;                               // y stays > T' through the step
-        if (y > Tp) {                                     // phase A (block-uniform)
-            const MinPlus racc = mp_block_inclusive(MinPlus{x < 0 ? (int64_t)x : 0, CONC_INF}, s_mp);
-            const bool reach = act && y + racc.p <= Tp;
-            const uint64_t bal = __builtin_amdgcn_ballot_w64(reach);
-            if (lane == 0) s_red[wave] = bal ? (int64_t)(wave * WAVE + __ffsll((unsigned long long)bal) - 1) : (int64_t)CB_THREADS;
-            __syncthreads();
-            int64_t k = CB_THREADS;
-            for (int q = 0; q < CB_WAVES; ++q) k = s_red[q] < k ? s_red[q] : k;
-            if (k >= CB_THREADS) {
-                never = true;
-                if (t == CB_THREADS - 1) *s_y0 = y + racc.p;                   // every release applied
-            } else if ((int64_t)t == k) {
-                *s_y0 = y + racc.p;
-            }
-            __syncthreads();
-            first = (uint32_t)(k + 1);
-        } else if (t == 0) {
-            *s_y0 = y;
-        }
-        __syncthreads();
-        const int64_t y0 = *s_y0;
-        bool pass = false;
-        if (!never) {                                     // phase B (block-uniform)
-            const MinPlus el = (t >= first && act) ? conc_mp(x, Tp) : MinPlus{0, CONC_INF};
-            const MinPlus inc = mp_block_inclusive(el, s_mp);
-            const MinPlus exl = mp_block_exclusive_of(inc, s_mp);
-            pass = x > 0 && t >= first && act && mp_apply(exl, y0) < Tp;
-            if (t == CB_THREADS - 1) *s_now = (int32_t)mp_apply(inc, y0);
-        } else if (t == 0) {
-            *s_now = (int32_t)y0;
-        }
-        if (act && x > 0) X.pass[i] = pass ? 1 : 0;
-        __syncthreads();
     }
-    if (t == 0) now_calls[flow] = *s_now;
 }
 
 // Chunks of long runs, one workgroup step each, taken in ticket order (a chunk's predecessors in its
@@ -454,13 +399,13 @@ __global__ __launch_bounds__(CB_THREADS) void k_conc_chunks(const uint32_t *__re
                                                             const uint32_t *__restrict__ skey, int32_t *__restrict__ now_calls,
                                                             const double *__restrict__ thr, ConcElems X, ConcBig G) {
     __shared__ MinPlus s_mp[CB_WAVES];
-    __shared__ int64_t s_red[CB_WAVES];
-    __shared__ int64_t s_y0;
-    __shared__ int32_t s_now;
     __shared__ uint32_t s_ticket;
     __shared__ MinPlus s_prefix;
     const uint32_t t = threadIdx.x;
     const uint32_t nch = G.ctl[2];
+#ifdef SENTINEL_CONC_GUARD
+    if (blockIdx.x == 0 && t == 0) printf("k_conc_chunks: %u chunks, %u long runs, %u runs\n", nch, G.ctl[1], G.ctl[0]);
+#endif
     for (;;) {
         if (t == 0) s_ticket = atomicAdd(&G.ctl[3], 1u);
         __syncthreads();
@@ -475,7 +420,11 @@ __global__ __launch_bounds__(CB_THREADS) void k_conc_chunks(const uint32_t *__re
         const int64_t Tp = G.tp[slot];
         const bool ok = G.unit[slot] && (now0 < 0 ? -now0 : now0) + (int64_t)G.mag[slot] < (int64_t)INT32_MAX && now0 <= Tp;
         if (!ok) {                                        // block-uniform
-            if (j == 0) conc_run_serial(X, rb, re, flow, thr[flow], now_calls, s_mp, s_red, &s_y0, &s_now);
+            if (j == 0 && t == 0) {
+                int32_t now = now_calls[flow];
+                conc_run_serial(X, rb, re, thr[flow], now);
+                now_calls[flow] = now;
+            }
             continue;
         }
         const uint32_t b = rb + j * CONC_CHUNK;
@@ -514,8 +463,14 @@ __global__ __launch_bounds__(CB_THREADS) void k_conc_chunks(const uint32_t *__re
                 uint32_t f = 0;
                 MinPlus v{0, CONC_INF};
                 if (p >= (int64_t)cf) {
+#ifdef SENTINEL_CONC_GUARD
+                    uint64_t spins = 0;
+#endif
                     do {
                         f = __hip_atomic_load(&G.flag[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef SENTINEL_CONC_GUARD
+                        if (++spins == (1ull << 24)) { printf("look-back spin: chunk %u waits for %lld flag %x epoch %u\n", c, (long long)p, f, G.epoch); f = (G.epoch << 2) | 2u; }
+#endif
                     } while ((f >> 2) != G.epoch || (f & 3u) == 0);
                     __threadfence();
                     v = (f & 3u) == 2u ? G.inc[p] : G.agg[p];

@@ -355,6 +355,12 @@ __device__ inline void pd_walk(const ParamRules &PR, const PRuleRec *RR, const P
     const double I_s = rr.I_s;
     const double thr = (rr.nf >> 16) ? value_threshold(PR, (uint32_t)rule, key) : rr.thr;   // CPFC:101-120
     const uint32_t before = nfresh;
+#ifdef SENTINEL_PW_PREFETCH
+    // most keys sit at their home slot: its window lines are touched (one dword each) together with the
+    // probe, so the window load after the probe finds them in L2 / the Infinity Cache
+    const uint32_t *hw = reinterpret_cast<const uint32_t *>(S.state + (int64_t)(mix64(key) & S.mask) * S.stride);
+    const uint32_t pfa = hw[0], pfb = S.stride > 16 ? hw[32] : 0u;     // (records over 128 B span two lines)
+#endif
     const int64_t h = slot_insert_counted(S.keys, S.mask, key, nfresh);
     if (h < 0) {                                                         // table full: param_reserve prevents it
         for (uint32_t q = q0; q < q1; ++q) put_verdict(out, (uint32_t)sv[q] & SEQ_MASK, ST_FAIL, 0, 0);
@@ -424,6 +430,9 @@ __device__ inline void pd_walk(const ParamRules &PR, const PRuleRec *RR, const P
 #pragma unroll
     for (int j = 0; j < NMAX; ++j)
         if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(st + 2 * j) = longlong2{ep[j], ct[j]};
+#ifdef SENTINEL_PW_PREFETCH
+    asm volatile("" ::"v"(pfa), "v"(pfb));
+#endif
 }
 
 #ifdef SENTINEL_DIAG_PHASES     // per workgroup: [0] start, [3] end, [4..6] phase sums, [7] rounds, [8] keys
