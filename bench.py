@@ -58,8 +58,9 @@ KERNEL_BYTES_PER_EVENT = {
     "param_scatter": 44.0,    # read the 24-B event, write key 8 + packed value 8 + rule 4
     "param_meta": 48.0,       # per slot after a rule / threshold / table change: key 8, rule fields ~16, write ~20 B
     "prule_prep": 36.0,       # read the 24-B event + value 8, write key 4
-    "conc_prep": 32.0,        # read the 24-B event (+ a release's token probe 8), write flow key 4 (+ slot 4)
-    "conc_runs": 12.0,        # sorted keys read twice (heads, runs) + the flag written / scanned
+    "conc_prep": 38.0,        # read the 24-B event (+ a release's token probe 8), write flow key 4 + aux word 8
+    "conc_apply": 52.5,       # read key 4 + value 8 + element 4 (+ pass 1 per acquire), write the 16-B result;
+                              # per passing acquire (half the events) a token insert: probe 8 + record 32
 }
 
 # rocprofv3 kernel symbols behind each engine profile name (for the PMC traffic of the roofline).
@@ -71,8 +72,8 @@ KERNEL_SYMBOLS = {
     "param_prep": ("k_param_prep", "k_pp_prep"), "param_meta": ("k_param_meta",), "prule_prep": ("k_prule_prep",),
     "prule_process": ("k_prule_process",), "part_unsplit": ("k_part_unsplit",), "lim_prep": ("k_lim1_prep",),
     "param_scatter": ("k_pp_scatter",), "param_group": ("k_pp_group",), "param_cm_read": ("k_pp_cm_read",), "param_cm_walk": ("k_pp_cm_walk",),
-    "conc_prep": ("k_conc_prep",), "conc_runs": ("k_conc_heads", "k_conc_runs"),
-    "conc_process": ("k_conc_process",), "conc_info": ("k_conc_info",), "conc_chunks": ("k_conc_chunks",), "param_decide": ("k_pp_walk", "k_pp_decide"),
+    "conc_prep": ("k_conc_prep",), "conc_scan": ("k_conc_scan",), "conc_apply": ("k_conc_apply",),
+    "param_decide": ("k_pp_walk", "k_pp_decide"),
 }
 PMC_DIR = os.path.join(ROOT, "profiles", "pmc")
 
@@ -307,14 +308,6 @@ class FlowWorkload:
             # the rolled bucket's 16-B pair, read + write its BLOCK / PASS_REQUEST / BLOCK_REQUEST
             # counters (3 x 8 B each way, blocked counter rows)
             return 16.0 + (n * 16 + 42 + 16 + 48) / max(1.0, e_f)
-        if dom == "part_decide":
-            # the fused kernel's decide half: per event the sorted value read back from gsval (8) and the
-            # verdict (8); per touched flow its run record (8), the window header (16 n), the rule fields
-            # (42), the rolled pair written (16), the rolled slot's three rest counters read + written (48)
-            return 16.0 + (8 + n * 16 + 42 + 16 + 48) / max(1.0, e_f)
-        if dom == "part_sort":
-            # per event: the packed value read (8) and written to gsval (8); per flow its run record (8)
-            return 16.0 + 8.0 / max(1.0, e_f)
         if dom == "radix_scatter":
             passes = max(1, round(d["calls"] / max(1, steps)))
             return (32.0 + 24.0 * (passes - 1)) / passes
@@ -592,10 +585,10 @@ class ConcWorkload:
                      f"to their token's thread; the engine's token ids)")
 
     def bytes_of(self, dom, d, steps):
-        if dom in ("conc_process", "conc_chunks"):
-            # per event: sorted value 8 + event 24 read, result 16 written; per acquire that passes a
-            # token insert (probe 8 + record 24); per release its token record read 8 + tombstone 8
-            return 8 + 24 + 16 + 0.5 * 16 + 0.5 * 16
+        if dom == "conc_scan":
+            # per event: sorted key 4 + value 8 read, the 8-B aux word gathered, element 4 written (+ pass
+            # byte per acquire); per release (half the events) its 32-B token record read and written back
+            return 4 + 8 + 8 + 4 + 0.5 * 1 + 0.5 * (32 + 32)
         if dom == "radix_scatter":
             passes = max(1, round(d["calls"] / max(1, steps)))
             return (32.0 + 24.0 * (passes - 1)) / passes

@@ -8,10 +8,9 @@
 //
 // A batch mixes acquires and releases of many flows.  Acquires and releases of one flow do not
 // commute (nowCalls is not a monotone function of the event order), so events are grouped by flow
-// (K2 radix sort, arrival order kept) and each flow's run is decided in arrival order (below: the
-// elements gathered in parallel, short runs by one lane, long runs by a (min, +) scan).  The token
-// cache is one open-addressing table in HBM: inserts CAS an empty slot or a tombstone, a release
-// turns its slot into a tombstone.
+// (K2 radix sort, arrival order kept) and each flow's run is decided in arrival order (below: one
+// segmented (min, +) scan over the sorted batch).  The token cache is one open-addressing table in
+// HBM: inserts CAS an empty slot or a tombstone, a release empties its slot or leaves a tombstone.
 #pragma once
 
 #include "admission.hpp"
@@ -35,19 +34,38 @@ constexpr uint64_t TOKEN_TOMB = 0xFFFFFFFFFFFFFFFEull;    // released token (pro
 constexpr int ST_RELEASE_OK = 6;                          // TokenResultStatus.RELEASE_OK
 constexpr int ST_ALREADY_RELEASE = 7;                     // TokenResultStatus.ALREADY_RELEASE
 
-struct TokenTable {
-    unsigned long long *keys;    // token id, PKEY_EMPTY or TOKEN_TOMB
-    int64_t *flow_id;
-    int32_t *flow_idx;           // -1: the flow's rule is gone (release -> NO_RULE_EXISTS)
-    int32_t *acquire;
-    uint64_t mask;
-    unsigned long long *counts;  // [0] live tokens, [1] tombstones
+// One 32-byte record per cache slot (a probe, an insert with its fields, a release's claim, amount and
+// tombstone all touch one line of the slot; memset 0xFF = empty slot, no claim).
+struct TokRec {
+    unsigned long long key;      // token id, PKEY_EMPTY or TOKEN_TOMB
+    int64_t flow_id;
+    int32_t flow_idx;            // -1: the flow's rule is gone (release -> NO_RULE_EXISTS)
+    int32_t acquire;
+    uint32_t claim;              // arrival position of the batch's first release of the token (~0 between batches)
+    uint32_t pad;
 };
+static_assert(sizeof(TokRec) == 32, "one half line per slot");
+
+struct TokenTable {
+    TokRec *rec;
+    uint64_t mask;
+    unsigned long long *counts;  // {live tokens, tombstones} deltas, striped (tok_count_add; the host sums them)
+};
+
+// The cache counts are updated by one atomic pair per workgroup; many workgroups adding to one address
+// queue at one memory channel (16K of them cost a batch ~60 us), so the pair is striped over
+// TOK_CNT_LANES lines by workgroup index and summed by the host when it needs them.
+constexpr int TOK_CNT_LANES = 64;
+constexpr int TOK_CNT_STRIDE = 16;                              // 128 B apart
+constexpr size_t TOK_CNT_BYTES = (size_t)TOK_CNT_LANES * TOK_CNT_STRIDE * 8;
+__device__ inline void tok_count_add(const TokenTable &T, int which, unsigned long long v) {
+    atomicAdd(&T.counts[(blockIdx.x & (TOK_CNT_LANES - 1)) * TOK_CNT_STRIDE + which], v);
+}
 
 __device__ inline int64_t token_find(const TokenTable &T, uint64_t id) {
     uint64_t h = mix64(id) & T.mask;
     for (uint64_t p = 0; p <= T.mask; ++p) {
-        const unsigned long long k = T.keys[h];
+        const unsigned long long k = T.rec[h].key;
         if (k == PKEY_EMPTY) return -1;
         if (k == id) return (int64_t)h;
         h = (h + 1) & T.mask;
@@ -63,23 +81,20 @@ __device__ inline int64_t token_find(const TokenTable &T, uint64_t id) {
 // returned -- a plain re-load could keep answering the stale free slot from this CU's cache and spin.
 __device__ inline int64_t token_insert(const TokenTable &T, uint64_t id, bool &tomb) {
     uint64_t h = mix64(id) & T.mask;
-    unsigned long long k = T.keys[h];
+    unsigned long long k = T.rec[h].key;
     for (uint64_t p = 0; p <= T.mask;) {
         if (k == PKEY_EMPTY || k == TOKEN_TOMB) {
-            const unsigned long long prev = atomicCAS(&T.keys[h], k, (unsigned long long)id);
+            const unsigned long long prev = atomicCAS(&T.rec[h].key, k, (unsigned long long)id);
             if (prev == k) {
                 tomb = k == TOKEN_TOMB;
                 return (int64_t)h;
             }
             k = prev;                                     // taken (or changed) meanwhile: look again
-#ifdef SENTINEL_CONC_GUARD
-            if (++p > T.mask) { printf("token_insert: CAS spin id %llx h %llu\n", (unsigned long long)id, (unsigned long long)h); return -1; }
-#endif
             continue;
         }
         h = (h + 1) & T.mask;
         ++p;
-        k = T.keys[h];
+        k = T.rec[h].key;
     }
     return -1;
 }
@@ -89,14 +104,14 @@ __device__ inline int64_t token_insert(const TokenTable &T, uint64_t id, bool &t
 __global__ __launch_bounds__(256) void k_tok_rebuild(TokenTable O, uint64_t ocap, TokenTable N) {
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= ocap) return;
-    const unsigned long long k = O.keys[s];
-    if (k == PKEY_EMPTY || k == TOKEN_TOMB) return;
-    uint64_t h = mix64(k) & N.mask;
-    while (atomicCAS(&N.keys[h], (unsigned long long)PKEY_EMPTY, k) != PKEY_EMPTY) h = (h + 1) & N.mask;
-    N.flow_id[h] = O.flow_id[s];
-    N.flow_idx[h] = O.flow_idx[s];
-    N.acquire[h] = O.acquire[s];
-    atomicAdd(&N.counts[0], 1ull);
+    const TokRec r = O.rec[s];
+    if (r.key == PKEY_EMPTY || r.key == TOKEN_TOMB) return;
+    uint64_t h = mix64(r.key) & N.mask;
+    while (atomicCAS(&N.rec[h].key, (unsigned long long)PKEY_EMPTY, r.key) != PKEY_EMPTY) h = (h + 1) & N.mask;
+    N.rec[h].flow_id = r.flow_id;
+    N.rec[h].flow_idx = r.flow_idx;
+    N.rec[h].acquire = r.acquire;
+    tok_count_add(N, 0, 1ull);
 }
 
 // Result record {token_id, status}: two 8-byte stores.
@@ -105,16 +120,19 @@ __device__ inline void put_conc(uint64_t *out, uint32_t i, int64_t token, int st
     out[2 * (uint64_t)i + 1] = (uint64_t)(uint32_t)status;
 }
 
+// Per valid event, by arrival position: an acquire's amount, or AUX_RELEASE | the released token's slot.
+constexpr uint64_t AUX_RELEASE = 1ull << 63;
+
 // DefaultTokenService.requestConcurrentToken validation (DTS:64-75, 89-91) and release lookup;
 // sort key = flow index (acquire: the rule; release: the token's flow); pass-0 histograms.  A found
-// release records its token slot (relslot) and claims it with its arrival position (atomicMin): the
+// release records its token slot (aux) and claims it with its arrival position (atomicMin): the
 // first release of a token in the batch is the one that finds it cached (CCFC:82-86), later ones of
 // the same token answer ALREADY_RELEASE.  Tokens issued in this batch are not yet known to any client.
 __global__ __launch_bounds__(SORT_THREADS) void k_conc_prep(int64_t n, const ConcEvent *__restrict__ ev, int32_t nflows,
                                                             TokenTable TT, uint64_t *__restrict__ out,
                                                             uint32_t *__restrict__ fkey, uint32_t finvalid,
                                                             uint32_t *__restrict__ fhist, int64_t nblocks,
-                                                            uint32_t *__restrict__ relslot, uint32_t *__restrict__ claim) {
+                                                            uint64_t *__restrict__ aux) {
     __shared__ uint32_t hf[MAX_PASSES][RADIX];
     for (int d = threadIdx.x; d < MAX_PASSES * RADIX; d += SORT_THREADS) (&hf[0][0])[d] = 0;
     __syncthreads();
@@ -128,15 +146,18 @@ __global__ __launch_bounds__(SORT_THREADS) void k_conc_prep(int64_t n, const Con
         if (e.kind == CONC_ACQUIRE) {
             if (!(e.flags & 1) || e.idx == SENTINEL_IDX_BAD_ID || e.acquire <= 0) st = ST_BAD_REQUEST;
             else if (e.idx < 0 || e.idx >= nflows) st = ST_NO_RULE_EXISTS;
-            else k = (uint32_t)e.idx;
+            else {
+                k = (uint32_t)e.idx;
+                aux[i] = (uint64_t)(uint32_t)e.acquire;                     // an acquire: its amount (> 0)
+            }
         } else if (e.kind == CONC_RELEASE) {
             const int64_t h = token_find(TT, (uint64_t)e.token);             // CCFC:82-86
             if (h < 0) st = ST_ALREADY_RELEASE;
-            else if (TT.flow_idx[h] < 0) st = ST_NO_RULE_EXISTS;             // CCFC:87-91
+            else if (TT.rec[h].flow_idx < 0) st = ST_NO_RULE_EXISTS;         // CCFC:87-91
             else {
-                k = (uint32_t)TT.flow_idx[h];
-                relslot[i] = (uint32_t)h;
-                atomicMin(&claim[h], (uint32_t)i);
+                k = (uint32_t)TT.rec[h].flow_idx;
+                aux[i] = AUX_RELEASE | (uint64_t)h;                          // a release: its token's slot
+                atomicMin(&TT.rec[h].claim, (uint32_t)i);
             }
         } else {
             st = ST_BAD_REQUEST;
@@ -177,48 +198,30 @@ __global__ __launch_bounds__(256) void k_conc_runs(const uint32_t *__restrict__ 
 }
 
 // ---------------------------------------------------------------- decisions
-// After the sort a flow's events form a contiguous run in arrival order.  The batch is decided in four
-// data-parallel steps, so that no lane walks a chain of dependent gathers:
-//   k_conc_elems   one thread per sorted position gathers the event once and writes its element:
-//                  elem > 0 an acquire of elem tokens, elem < 0 a release of -elem tokens that found its
-//                  token cached and claimed it (the batch's first release of it, k_conc_prep), 0 a
-//                  release that answers ALREADY_RELEASE; relh = the released token's slot
-//   k_conc_lanes   one lane per run of <= CONC_LANE_RUN events: the CCFC:48-101 recurrence over the run's
-//                  elements (nowCalls in a register, integer work only), one pass byte per acquire;
-//                  longer runs are registered for the chunk kernels
-//   k_conc_info / k_conc_chunks   long runs in 1024-event chunks: a (min, +) scan with a decoupled
-//                  look-back for unit-acquire runs, a workgroup walk otherwise
-//   k_conc_apply   one thread per sorted position: a passing acquire takes a token (insert into the
-//                  cache, id = id_base + arrival position), a failing one answers BLOCKED, a claimed
-//                  release tombstones its token, the rest answer ALREADY_RELEASE
-// A release's amount is read in k_conc_elems, a kernel before any tombstone store, so a slot reused by an
-// insert of this batch can never hand a release someone else's amount.
+// After the sort a flow's events form a contiguous segment in arrival order, and the batch is decided
+// by one segmented scan over the sorted positions (k_conc_scan), so that no lane walks a chain of
+// dependent gathers and no per-run bookkeeping is needed:
+//   element   one per sorted position, gathered once: x > 0 an acquire of x tokens, x < 0 a release of
+//             -x tokens that found its token cached and claimed it (the batch's first release of it,
+//             k_conc_prep; its slot is freed right there), 0 a release that answers ALREADY_RELEASE
+//   scan      the greedy admission of unit acquires with releases interleaved is a (min, +)
+//             recurrence: with T' = floor(threshold), an acquire passes iff the in-flight count y < T'
+//             (CCFC:57-70: !((double)(y + 1) > threshold)), and while y <= T' it maps y to
+//             min(y + 1, T'); a release of r tokens maps y to y - r (CCFC:92-98).  Both are
+//             x -> min(x + P, C), closed under composition; a segment head resets the composition, so
+//             the whole batch is one segmented scan with a decoupled look-back over tiles (a tile with
+//             a head publishes its inclusive state at once, so look-backs are short)
+//   fallback  a segment that the scan cannot decide exactly -- an amount other than 1, nowCalls above T'
+//             at the start, or an int sum that could wrap -- is walked by one thread (k_conc_serial)
+//   effects   one thread per sorted position (k_conc_apply): a passing acquire takes a token (insert
+//             into the cache, id = id_base + arrival position), a failing one answers BLOCKED; the
+//             segment's last position stores nowCalls
+// A release's amount is read in k_conc_scan, a kernel before any insert of the batch, so a slot reused
+// by an insert can never hand a release someone else's amount.
 struct ConcElems {
     int32_t *elem;
-    uint32_t *relh;
     uint8_t *pass;
 };
-
-__global__ __launch_bounds__(256) void k_conc_elems(const ConcEvent *__restrict__ ev, const uint64_t *__restrict__ sval,
-                                                    const uint32_t *__restrict__ skey, uint32_t invalid, int64_t n,
-                                                    const uint32_t *__restrict__ relslot,
-                                                    const uint32_t *__restrict__ claim, TokenTable TT, ConcElems X) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || skey[i] == invalid) return;             // invalid events were answered by k_conc_prep
-    const uint32_t seq = (uint32_t)sval[i] & SEQ_MASK;
-    const ConcEvent e = ev[seq];
-    int32_t x = 0;
-    if (e.kind == CONC_ACQUIRE) {
-        x = e.acquire;                                    // > 0 (validated)
-    } else {
-        const uint32_t h = relslot[seq];
-        if (claim[h] == seq) {                            // CCFC:82-86: this release finds its token
-            x = -TT.acquire[h];
-            X.relh[i] = h;
-        }
-    }
-    X.elem[i] = x;
-}
 
 // CCFC:57-70 for one acquire of `a` tokens at nowCalls `now`: int + int (wraps) compared with the double
 // threshold; passes -> now += a.
@@ -229,18 +232,6 @@ __device__ inline bool conc_acquire(int32_t &now, int32_t a, double threshold) {
     return true;
 }
 
-#ifndef SENTINEL_CONC_LANE_RUN
-#define SENTINEL_CONC_LANE_RUN 64
-#endif
-constexpr uint32_t CONC_LANE_RUN = SENTINEL_CONC_LANE_RUN;   // longer runs are decided in chunks by workgroups
-constexpr uint32_t CONC_CHUNK = 1024;       // events of a long run per workgroup step (4 per thread)
-
-// The greedy admission of unit acquires with releases interleaved is a (min, +) recurrence: while the
-// in-flight count y is <= the largest admissible T' (the largest y with !((double)(y + 1) > threshold),
-// minus one), an acquire maps y to min(y + 1, T') (it passes iff y < T') and a release of r tokens maps
-// y to y - r.  Both are x -> min(x + P, C); composition (P1, C1) then (P2, C2) = (P1 + P2,
-// min(C1 + P2, C2)) is associative, so the chunks of one long run are decided in parallel with a
-// decoupled look-back over their compositions.
 constexpr int64_t CONC_INF = (int64_t)1 << 60;
 struct MinPlus { int64_t p, c; };
 __device__ inline MinPlus mp_then(MinPlus a, MinPlus b) {
@@ -255,273 +246,299 @@ __device__ inline int64_t conc_tprime(double threshold) {
     return (int64_t)floor(threshold);
 }
 
-// the scan element of a unit-acquire run's element x
-__device__ inline MinPlus conc_mp(int32_t x, int64_t Tp) {
-    return x > 0 ? MinPlus{1, Tp} : x < 0 ? MinPlus{(int64_t)x, CONC_INF} : MinPlus{0, CONC_INF};
+// Segmented scan state: the composition since the last segment head in the range (or of the whole
+// range when it holds none), the position of that head, and whether an amount other than +-1 occurred
+// since it.
+constexpr uint32_t CONC_NO_HEAD = 0xFFFFFFFFu;
+struct ConcSeg {
+    int64_t p, c;
+    uint32_t head;
+    uint32_t nu;
+};
+__device__ inline ConcSeg cs_identity() { return ConcSeg{0, CONC_INF, CONC_NO_HEAD, 0u}; }
+__device__ inline ConcSeg cs_then(const ConcSeg &a, const ConcSeg &b) {
+    if (b.head != CONC_NO_HEAD) return b;
+    const MinPlus f = mp_then(MinPlus{a.p, a.c}, MinPlus{b.p, b.c});
+    return ConcSeg{f.p, f.c, a.head, a.nu | b.nu};
+}
+__device__ inline ConcSeg cs_shfl(const ConcSeg &v, int src) {
+    return ConcSeg{__shfl(v.p, src, WAVE), __shfl(v.c, src, WAVE), (uint32_t)__shfl((int)v.head, src, WAVE),
+                   (uint32_t)__shfl((int)v.nu, src, WAVE)};
+}
+__device__ inline ConcSeg cs_shfl_up(const ConcSeg &v, int o) {
+    return ConcSeg{__shfl_up(v.p, o, WAVE), __shfl_up(v.c, o, WAVE), (uint32_t)__shfl_up((int)v.head, o, WAVE),
+                   (uint32_t)__shfl_up((int)v.nu, o, WAVE)};
 }
 
-constexpr int CB_THREADS = 256;
-constexpr int CB_WAVES = CB_THREADS / WAVE;
+constexpr int CS_THREADS = 256;
+constexpr int CS_WAVES = CS_THREADS / WAVE;
+#ifndef SENTINEL_CONC_ITEMS
+#define SENTINEL_CONC_ITEMS 8
+#endif
+constexpr int CS_ITEMS = SENTINEL_CONC_ITEMS;               // consecutive sorted positions per thread
+constexpr int64_t CS_TILE = (int64_t)CS_THREADS * CS_ITEMS;
 
-// Inclusive block scan of MinPlus over the 256 threads (wave shuffles, then the waves' totals, which
-// stay in lds[] for the caller).
-__device__ inline MinPlus mp_block_inclusive(MinPlus v, MinPlus *lds) {
-    const uint32_t lane = lane_id();
-    const int wave = threadIdx.x / WAVE;
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        const int64_t pp = __shfl_up(v.p, o, WAVE);
-        const int64_t pc = __shfl_up(v.c, o, WAVE);
-        if ((int)lane >= o) v = mp_then(MinPlus{pp, pc}, v);
-    }
-    if (lane == WAVE - 1) lds[wave] = v;
-    __syncthreads();
-    MinPlus pre{0, CONC_INF};
-    for (int w = 0; w < wave; ++w) pre = mp_then(pre, lds[w]);
-    __syncthreads();
-    return mp_then(pre, v);
-}
-// ... and the exclusive value of this thread (the previous thread's inclusive one)
-__device__ inline MinPlus mp_block_exclusive_of(MinPlus inc, const MinPlus *lds) {
-    const uint32_t lane = lane_id();
-    const int wave = threadIdx.x / WAVE;
-    const int64_t pp = __shfl_up(inc.p, 1, WAVE), pc = __shfl_up(inc.c, 1, WAVE);
-    MinPlus ex{pp, pc};
-    if (lane == 0) {
-        ex = MinPlus{0, CONC_INF};
-        for (int w = 0; w < wave; ++w) ex = mp_then(ex, lds[w]);
-    }
-    return ex;
-}
-
-// Long runs of a batch: per run slot its run, nowCalls before the batch, T', whether every acquire
-// asks for one token and the sum of |amounts| (the scan's eligibility); per chunk its slot, its index
-// in the run and the look-back status {epoch << 2 | 1 aggregate / 2 inclusive, composition}.
-struct ConcBig {
-    uint32_t *run;
-    int32_t *now0;
-    int64_t *tp;
-    uint32_t *unit;
-    unsigned long long *mag;
-    uint2 *chunks;           // [slot] {first chunk, chunk count}
-    uint32_t *chunk_slot;
-    uint32_t *chunk_j;
+// Per tile the look-back status {epoch << 2 | 1 aggregate / 2 inclusive} and state; the tile ticket and
+// the fallback list; per flow nowCalls after the batch.
+struct ConcScan {
     uint32_t *flag;
-    MinPlus *agg;
-    MinPlus *inc;
-    uint32_t *ctl;           // [0] runs, [1] long runs, [2] chunks, [3] chunk ticket
+    ConcSeg *agg;
+    ConcSeg *inc;
+    uint32_t *ctl;           // [0] tile ticket, [1] segments left to k_conc_serial
+    uint32_t *serial;        // their head positions
+    int32_t *fin;            // [flow] nowCalls after the batch (stored by k_conc_apply)
     uint32_t epoch;
 };
 
-// One lane per flow run of <= CONC_LANE_RUN events: the run's elements in arrival order (read 8 at a time);
-// longer runs are cut into chunks for k_conc_chunks.
-__global__ __launch_bounds__(256) void k_conc_lanes(const uint32_t *__restrict__ run_start,
-                                                    const uint32_t *__restrict__ skey, int32_t *__restrict__ now_calls,
-                                                    const double *__restrict__ thr, ConcElems X, ConcBig G) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= G.ctl[0]) return;
-    const uint32_t b = run_start[r], e = run_start[r + 1];
-    const uint32_t flow = skey[b];
-    if (e - b > CONC_LANE_RUN) {
-        const uint32_t slot = atomicAdd(&G.ctl[1], 1u);
-        const uint32_t nch = (e - b + CONC_CHUNK - 1) / CONC_CHUNK;
-        const uint32_t first = atomicAdd(&G.ctl[2], nch);
-        G.run[slot] = r;
-        G.now0[slot] = now_calls[flow];
-        G.tp[slot] = conc_tprime(thr[flow]);
-        G.unit[slot] = 1u;
-        G.mag[slot] = 0ull;
-        G.chunks[slot] = make_uint2(first, nch);
-        for (uint32_t j = 0; j < nch; ++j) {
-            G.chunk_slot[first + j] = slot;
-            G.chunk_j[first + j] = j;
+// A claimed release frees its token's slot (CCFC:92-100).  No insert runs in the same kernel, and
+// concurrent releases only turn slots from occupied to tombstone / empty, so an empty successor seen
+// here stays empty and a stale plain read can only show an older, occupied successor (the release then
+// leaves a tombstone the next sweep may free).  A slot followed by an empty one ends no probe chain, so
+// it becomes empty, and so do the tombstones right before it (as k_tok_sweep); otherwise it becomes a
+// tombstone.  In a sparse cache almost every release empties its slot.
+__device__ inline void token_free(const TokenTable &TT, uint32_t h, TokRec r, int64_t &dtomb) {
+    const unsigned long long nxt = TT.rec[(h + 1) & TT.mask].key;
+    const unsigned long long prv = TT.rec[(h - 1) & TT.mask].key;
+    r.claim = ~0u;
+    r.key = nxt == PKEY_EMPTY ? PKEY_EMPTY : TOKEN_TOMB;
+    TT.rec[h] = r;                                        // the whole record: no partial-sector write
+    if (nxt == PKEY_EMPTY) {
+        if (prv == TOKEN_TOMB) {
+            uint64_t g = (h - 1) & TT.mask;
+            for (int k = 0; k < 256; ++k) {               // (bounded walk back over tombstones)
+                if (atomicCAS(&TT.rec[g].key, (unsigned long long)TOKEN_TOMB, (unsigned long long)PKEY_EMPTY) != TOKEN_TOMB) break;
+                --dtomb;
+                g = (g - 1) & TT.mask;
+            }
         }
-        return;
-    }
-    int32_t now = now_calls[flow];
-    const double threshold = thr[flow];
-    for (uint32_t i0 = b; i0 < e; i0 += 8) {
-        int32_t x[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) x[k] = i0 + k < e ? X.elem[i0 + k] : 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            if (x[k] > 0) X.pass[i0 + k] = conc_acquire(now, x[k], threshold) ? 1 : 0;
-            else if (x[k] < 0) now = (int32_t)((uint32_t)now + (uint32_t)x[k]);     // CCFC:97-98
-        }
-    }
-    now_calls[flow] = now;
-}
-
-// Eligibility of the long runs for the scan: every acquire of 1 token, and the int sums cannot wrap.
-__global__ __launch_bounds__(256) void k_conc_info(const uint32_t *__restrict__ run_start, ConcElems X, ConcBig G) {
-    const uint32_t nch = G.ctl[2];
-    for (uint32_t c = blockIdx.x; c < nch; c += gridDim.x) {
-        const uint32_t slot = G.chunk_slot[c], j = G.chunk_j[c];
-        const uint32_t r = G.run[slot];
-        const uint32_t b = run_start[r] + j * CONC_CHUNK, e = min(run_start[r + 1], b + CONC_CHUNK);
-        bool unit = true;
-        unsigned long long mag = 0;
-        for (uint32_t i = b + threadIdx.x; i < e; i += blockDim.x) {
-            const int32_t x = X.elem[i];
-            if (x > 1) unit = false;
-            mag += (unsigned long long)(x < 0 ? -(int64_t)x : (int64_t)x);
-        }
-        if (__syncthreads_or(!unit) && threadIdx.x == 0) atomicAnd(&G.unit[slot], 0u);
-#pragma unroll
-        for (int o = WAVE / 2; o >= 1; o >>= 1) mag += __shfl_xor(mag, o, WAVE);
-        if (lane_id() == 0 && mag) atomicAdd(&G.mag[slot], mag);
+    } else {
+        ++dtomb;
     }
 }
 
-// A long run that cannot take the whole-run scan (an acquire of several tokens, an int sum that could
-// wrap, or nowCalls above T' when the batch starts): its elements walked by one thread with the
-// CCFC:57-98 recurrence (integer work on the gathered elements only: rare runs, no barriers).
-__device__ inline void conc_run_serial(const ConcElems &X, uint32_t b, uint32_t e, double threshold, int32_t &now) {
-    for (uint32_t i0 = b; i0 < e; i0 += 8) {
-        int32_t x[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) x[k] = i0 + k < e ? X.elem[i0 + k] : 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            if (x[k] > 0) X.pass[i0 + k] = conc_acquire(now, x[k], threshold) ? 1 : 0;
-            else if (x[k] < 0) now = (int32_t)((uint32_t)now + (uint32_t)x[k]);     // CCFC:97-98
-        }
-    }
-}
-
-// Chunks of long runs, one workgroup step each, taken in ticket order (a chunk's predecessors in its
-// run were taken earlier, so the look-back always completes).  An eligible run's chunk composes its
-// 1024 elements (4 consecutive per thread), publishes the composition, looks back over its run's
-// earlier chunks for the prefix and decides its acquires from y = prefix(nowCalls); the run's last chunk
-// writes nowCalls.  An ineligible run is walked whole by the workgroup that takes its first chunk.
-__global__ __launch_bounds__(CB_THREADS) void k_conc_chunks(const uint32_t *__restrict__ run_start,
-                                                            const uint32_t *__restrict__ skey, int32_t *__restrict__ now_calls,
-                                                            const double *__restrict__ thr, ConcElems X, ConcBig G) {
-    __shared__ MinPlus s_mp[CB_WAVES];
-    __shared__ uint32_t s_ticket;
-    __shared__ MinPlus s_prefix;
+// The batch's decisions: each workgroup takes a tile of CS_TILE sorted positions in ticket order (a
+// tile's predecessors were taken earlier, so its look-back always completes), gathers the elements
+// (freeing the claimed releases' slots), scans them, looks back for the state before the tile and
+// decides its acquires; a segment's last position stores nowCalls after the batch, or hands the segment
+// to k_conc_serial.
+__global__ __launch_bounds__(CS_THREADS) void k_conc_scan(const uint64_t *__restrict__ aux, const uint64_t *__restrict__ sval,
+                                                          const uint32_t *__restrict__ skey, uint32_t invalid, int64_t n,
+                                                          TokenTable TT, const double *__restrict__ thr,
+                                                          const int32_t *__restrict__ now_calls, ConcElems X, ConcScan S) {
+    __shared__ ConcSeg s_w[CS_WAVES];
+    __shared__ ConcSeg s_prefix;
+    __shared__ uint32_t s_tile;
+    __shared__ unsigned long long s_cnt[2];
     const uint32_t t = threadIdx.x;
-    const uint32_t nch = G.ctl[2];
-#ifdef SENTINEL_CONC_GUARD
-    if (blockIdx.x == 0 && t == 0) printf("k_conc_chunks: %u chunks, %u long runs, %u runs\n", nch, G.ctl[1], G.ctl[0]);
-#endif
-    for (;;) {
-        if (t == 0) s_ticket = atomicAdd(&G.ctl[3], 1u);
-        __syncthreads();
-        const uint32_t c = s_ticket;
-        __syncthreads();
-        if (c >= nch) break;
-        const uint32_t slot = G.chunk_slot[c], j = G.chunk_j[c];
-        const uint32_t r = G.run[slot];
-        const uint32_t rb = run_start[r], re = run_start[r + 1];
-        const uint32_t flow = skey[rb];
-        const int64_t now0 = G.now0[slot];
-        const int64_t Tp = G.tp[slot];
-        const bool ok = G.unit[slot] && (now0 < 0 ? -now0 : now0) + (int64_t)G.mag[slot] < (int64_t)INT32_MAX && now0 <= Tp;
-        if (!ok) {                                        // block-uniform
-            if (j == 0 && t == 0) {
-                int32_t now = now_calls[flow];
-                conc_run_serial(X, rb, re, thr[flow], now);
-                now_calls[flow] = now;
-            }
-            continue;
-        }
-        const uint32_t b = rb + j * CONC_CHUNK;
-        int32_t x[4];
-        MinPlus mine{0, CONC_INF};
+    const uint32_t lane = lane_id();
+    const int wave = (int)(t / WAVE);
+    if (t == 0) {
+        s_tile = atomicAdd(&S.ctl[0], 1u);
+        s_prefix = cs_identity();
+    }
+    if (t < 2) s_cnt[t] = 0;
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const int64_t b = (int64_t)tile * CS_TILE + (int64_t)t * CS_ITEMS;
+
+    uint32_t k[CS_ITEMS];
+    int32_t x[CS_ITEMS];
+    int64_t tp[CS_ITEMS];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t i = b + t * 4 + q;
-            x[q] = i < re ? X.elem[i] : 0;
-            mine = mp_then(mine, conc_mp(x[q], Tp));
+    for (int q = 0; q < CS_ITEMS; ++q) k[q] = b + q < n ? skey[b + q] : invalid;
+    const uint32_t kprev = b > 0 && b - 1 < n ? skey[b - 1] : invalid;
+    const uint32_t knext = b + CS_ITEMS < n ? skey[b + CS_ITEMS] : invalid;
+    int64_t dtomb = 0;
+    unsigned long long freed = 0;
+    uint32_t kc = invalid;
+    int64_t tc = 0;
+#pragma unroll
+    for (int q = 0; q < CS_ITEMS; ++q) {
+        x[q] = 0;
+        tp[q] = 0;
+        if (k[q] == invalid) continue;
+        const uint32_t seq = (uint32_t)sval[b + q] & SEQ_MASK;
+        const uint64_t a = aux[seq];
+        if (!(a & AUX_RELEASE)) {
+            x[q] = (int32_t)a;                            // an acquire: > 0 (validated)
+        } else {
+            const uint32_t h = (uint32_t)a;
+            const TokRec r = TT.rec[h];                   // claim and amount: one line
+            if (r.claim == seq) {                         // CCFC:82-86: this release finds its token
+                x[q] = -r.acquire;
+                token_free(TT, h, r, dtomb);
+                ++freed;
+            }
         }
-        const MinPlus inc = mp_block_inclusive(mine, s_mp);
-        const MinPlus exl = mp_block_exclusive_of(inc, s_mp);
-        // the chunk's composition: published by thread 255, then the last wave looks back over the run's
-        // earlier chunks 64 at a time (each lane waits for one chunk's flag; the window is composed
-        // earliest first up to the nearest inclusive prefix)
-        const uint32_t cf = G.chunks[slot].x;
-        if (t == CB_THREADS - 1) {
-            if (j == 0) {
-                G.inc[c] = inc;
+        if (k[q] != kc) {
+            kc = k[q];
+            tc = conc_tprime(thr[kc]);
+        }
+        tp[q] = tc;
+    }
+    if (freed) atomicAdd(&s_cnt[0], 0ull - freed);        // (one live token less per release)
+    if (dtomb) atomicAdd(&s_cnt[1], (unsigned long long)dtomb);
+
+    // this thread's composition, the wave's and the block's inclusive scan
+    ConcSeg mine = cs_identity();
+#pragma unroll
+    for (int q = 0; q < CS_ITEMS; ++q) {
+        if (k[q] == invalid) continue;
+        const bool head = k[q] != (q ? k[q - 1] : kprev);
+        const int32_t v = x[q];
+        const ConcSeg el{(int64_t)v, v > 0 ? tp[q] : CONC_INF, head ? (uint32_t)(b + q) : CONC_NO_HEAD,
+                         (v > 1 || v < -1) ? 1u : 0u};
+        mine = cs_then(mine, el);
+    }
+    ConcSeg inc = mine;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const ConcSeg u = cs_shfl_up(inc, o);
+        if ((int)lane >= o) inc = cs_then(u, inc);
+    }
+    if (lane == WAVE - 1) s_w[wave] = inc;
+    __syncthreads();
+    ConcSeg wpre = cs_identity(), tagg = cs_identity();
+#pragma unroll
+    for (int w = 0; w < CS_WAVES; ++w) {
+        if (w < wave) wpre = cs_then(wpre, s_w[w]);
+        tagg = cs_then(tagg, s_w[w]);
+    }
+    ConcSeg excl = cs_shfl_up(inc, 1);
+    if (lane == 0) excl = cs_identity();
+    excl = cs_then(wpre, excl);                           // the tile's positions before this thread's
+
+    // publish the tile's state; look back over earlier tiles (last wave, 64 tiles at a time, each lane
+    // waiting for one tile's flag; the window composed earliest first up to the nearest inclusive state)
+    const bool early = tile == 0 || tagg.head != CONC_NO_HEAD;          // inclusive without a prefix
+    if (t == CS_THREADS - 1) {
+        if (early) S.inc[tile] = tagg;
+        else S.agg[tile] = tagg;
+        __threadfence();
+        __hip_atomic_store(&S.flag[tile], (S.epoch << 2) | (early ? 2u : 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tile > 0 && t >= CS_THREADS - WAVE) {
+        ConcSeg pre = cs_identity();                      // tiles between the window and this one
+        int64_t top = tile;                               // the window ends below top
+        for (;;) {
+            const int64_t p = top - 1 - (int64_t)lane;    // lane 0: the nearest tile
+            // (a position before tile 0 reads as an inclusive identity)
+            const uint32_t f = p >= 0 ? __hip_atomic_load(&S.flag[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : ((S.epoch << 2) | 2u);
+            const bool ready = (f >> 2) == S.epoch && (f & 3u) != 0;
+            const uint64_t incl = __builtin_amdgcn_ballot_w64(ready && (f & 3u) == 2u);
+            const uint64_t waiting = __builtin_amdgcn_ballot_w64(!ready);
+            const int first = incl ? __ffsll((unsigned long long)incl) - 1 : WAVE;   // the nearest inclusive state
+            const uint64_t need = first >= WAVE - 1 ? ~0ull : ((2ull << first) - 1);
+            if (waiting & need) {                         // wait only for the tiles up to it
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            __threadfence();
+            ConcSeg v = cs_identity();
+            if (p >= 0 && (int)lane <= first) v = (f & 3u) == 2u ? S.inc[p] : S.agg[p];
+            ConcSeg w = cs_identity();                    // lanes min(first, 63) .. 0, earliest first
+            for (int l = min(first, WAVE - 1); l >= 0; --l) w = cs_then(w, cs_shfl(v, l));
+            pre = cs_then(w, pre);
+            if (first < WAVE) break;
+            top -= WAVE;
+        }
+        if (t == CS_THREADS - 1) {
+            s_prefix = pre;
+            if (!early) {
+                S.inc[tile] = cs_then(pre, tagg);
                 __threadfence();
-                __hip_atomic_store(&G.flag[c], (G.epoch << 2) | 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s_prefix = MinPlus{0, CONC_INF};
+                __hip_atomic_store(&S.flag[tile], (S.epoch << 2) | 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        if (s_cnt[0]) tok_count_add(TT, 0, s_cnt[0]);
+        if (s_cnt[1]) tok_count_add(TT, 1, s_cnt[1]);
+    }
+    const ConcSeg E = cs_then(s_prefix, excl);            // the sorted positions before this thread's
+
+    // decide: y = nowCalls before each position (y0 = nowCalls before the batch at a segment head)
+    int64_t y = 0, n0 = 0;
+    uint32_t hd = E.head, nu = E.nu;
+    bool started = false;
+#pragma unroll
+    for (int q = 0; q < CS_ITEMS; ++q) {
+        if (k[q] == invalid) continue;
+        const int64_t i = b + q;
+        const bool head = k[q] != (q ? k[q - 1] : kprev);
+        if (head || !started) {
+            n0 = now_calls[k[q]];
+            if (head) {
+                y = n0;
+                hd = (uint32_t)i;
+                nu = 0;
             } else {
-                G.agg[c] = inc;
-                __threadfence();
-                __hip_atomic_store(&G.flag[c], (G.epoch << 2) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                y = mp_apply(MinPlus{E.p, E.c}, n0);
+            }
+            started = true;
+        }
+        const int32_t v = x[q];
+        if (v > 1 || v < -1) nu = 1;
+        X.elem[i] = v;
+        if (v > 0) {
+            X.pass[i] = y < tp[q] ? 1 : 0;
+            y = min(y + 1, tp[q]);
+        } else {
+            y += v;
+        }
+        if ((q + 1 < CS_ITEMS ? k[q + 1] : knext) != k[q]) {                 // the segment's last position
+            const int64_t len = i - (int64_t)hd + 1;
+            if (!nu && n0 <= tp[q] && (n0 < 0 ? -n0 : n0) + len < (int64_t)INT32_MAX) {
+                S.fin[k[q]] = (int32_t)y;
+            } else {
+                S.serial[atomicAdd(&S.ctl[1], 1u)] = hd;
             }
         }
-        if (j > 0 && t >= CB_THREADS - WAVE) {                               // last wave (block-uniform j)
-            const uint32_t lane = t - (CB_THREADS - WAVE);
-            MinPlus pre{0, CONC_INF};                                        // chunks between the window and c
-            uint32_t top = c;                                                // the window ends below top
-            for (;;) {
-                const int64_t p = (int64_t)top - 1 - lane;                   // lane 0: the nearest chunk
-                uint32_t f = 0;
-                MinPlus v{0, CONC_INF};
-                if (p >= (int64_t)cf) {
-#ifdef SENTINEL_CONC_GUARD
-                    uint64_t spins = 0;
-#endif
-                    do {
-                        f = __hip_atomic_load(&G.flag[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#ifdef SENTINEL_CONC_GUARD
-                        if (++spins == (1ull << 24)) { printf("look-back spin: chunk %u waits for %lld flag %x epoch %u\n", c, (long long)p, f, G.epoch); f = (G.epoch << 2) | 2u; }
-#endif
-                    } while ((f >> 2) != G.epoch || (f & 3u) == 0);
-                    __threadfence();
-                    v = (f & 3u) == 2u ? G.inc[p] : G.agg[p];
-                }
-                const uint64_t incl = __builtin_amdgcn_ballot_w64(p >= (int64_t)cf && (f & 3u) == 2u);
-                const uint32_t valid = (uint32_t)min<int64_t>(WAVE, (int64_t)top - (int64_t)cf);
-                const uint32_t last = incl ? (uint32_t)(__ffsll((unsigned long long)incl) - 1) : valid - 1;
-                // compose lanes last .. 0 (earliest first): a shuffle chain in lane 0
-                MinPlus w{0, CONC_INF};
-                for (int l = (int)last; l >= 0; --l) {
-                    const int64_t pp = __shfl(v.p, l, WAVE), pc = __shfl(v.c, l, WAVE);
-                    w = mp_then(w, MinPlus{pp, pc});
-                }
-                pre = mp_then(w, pre);
-                if (incl || top - cf <= (uint32_t)WAVE) break;               // reached an inclusive prefix / chunk cf
-                top -= WAVE;
-            }
-            if (lane == WAVE - 1) {                                          // thread 255
-                s_prefix = pre;
-                const MinPlus acc = mp_then(pre, inc);
-                G.inc[c] = acc;
-                __threadfence();
-                __hip_atomic_store(&G.flag[c], (G.epoch << 2) | 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (j + 1 == G.chunks[slot].y) now_calls[flow] = (int32_t)mp_apply(acc, now0);
-            }
-        } else if (j == 0 && t == CB_THREADS - 1 && j + 1 == G.chunks[slot].y) {
-            now_calls[flow] = (int32_t)mp_apply(inc, now0);
-        }
-        __syncthreads();
-        int64_t y = mp_apply(mp_then(s_prefix, exl), now0);   // before this thread's first event
+    }
+}
+
+// Segments the scan cannot decide: one thread walks each with the CCFC:57-98 recurrence (integer work
+// on the elements only; amounts other than 1 and nowCalls above T' are rare).
+__global__ __launch_bounds__(256) void k_conc_serial(const uint32_t *__restrict__ skey, int64_t n,
+                                                     const int32_t *__restrict__ now_calls,
+                                                     const double *__restrict__ thr, ConcElems X, ConcScan S) {
+    const uint32_t cnt = S.ctl[1];
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < cnt; r += gridDim.x * blockDim.x) {
+        const int64_t b = S.serial[r];
+        const uint32_t flow = skey[b];
+        int32_t now = now_calls[flow];
+        const double threshold = thr[flow];
+        for (int64_t i0 = b;; i0 += 8) {
+            uint32_t kk[8];
+            int32_t xx[8];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t i = b + t * 4 + q;
-            if (i < re && x[q] > 0) {
-                X.pass[i] = y < Tp ? 1 : 0;
-                y = min(y + 1, Tp);
-            } else if (i < re && x[q] < 0) {
-                y += x[q];
+            for (int q = 0; q < 8; ++q) {
+                kk[q] = i0 + q < n ? skey[i0 + q] : ~flow;
+                xx[q] = kk[q] == flow ? X.elem[i0 + q] : 0;
             }
+            bool end = false;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                if (kk[q] != flow) { end = true; break; }
+                if (xx[q] > 0) X.pass[i0 + q] = conc_acquire(now, xx[q], threshold) ? 1 : 0;
+                else if (xx[q] < 0) now = (int32_t)((uint32_t)now + (uint32_t)xx[q]);     // CCFC:97-98
+            }
+            if (end) break;
         }
-        __syncthreads();
+        S.fin[flow] = now;
     }
 }
 
 // The effects, one thread per sorted position (CCFC:57-100): a passing acquire takes a token
 // (TokenCacheNode, id = id_base + arrival position), a failing one answers BLOCKED; a claimed release
-// frees its slot (a tombstone: probe chains continue through it) and answers RELEASE_OK; any other
-// release ALREADY_RELEASE.  Cache counts {live, tombstones} by one atomic pair per workgroup.
+// (freed by k_conc_scan) answers RELEASE_OK, any other release ALREADY_RELEASE; a segment's last position
+// stores the flow's nowCalls.  Cache counts {live, tombstones} by one atomic pair per workgroup.
 __global__ __launch_bounds__(256) void k_conc_apply(const uint64_t *__restrict__ sval, const uint32_t *__restrict__ skey,
-                                                    uint32_t invalid, int64_t n, ConcElems X, uint32_t *__restrict__ claim,
+                                                    uint32_t invalid, int64_t n, ConcElems X,
                                                     TokenTable TT, const int64_t *__restrict__ flow_ids, uint64_t id_base,
+                                                    const int32_t *__restrict__ fin, int32_t *__restrict__ now_calls,
                                                     uint64_t *__restrict__ out) {
     __shared__ unsigned long long s_cnt[2];
     if (threadIdx.x < 2) s_cnt[threadIdx.x] = 0;
@@ -543,30 +560,24 @@ __global__ __launch_bounds__(256) void k_conc_apply(const uint64_t *__restrict__
                     put_conc(out, seq, 0, ST_FAIL);
                 } else {
                     if (tomb) --dtomb;
-                    TT.flow_id[h] = flow_ids[flow];
-                    TT.flow_idx[h] = (int32_t)flow;
-                    TT.acquire[h] = x;
+                    TT.rec[h] = TokRec{id, flow_ids[flow], (int32_t)flow, x, ~0u, 0u};   // (whole record)
                     ++dlive;
                     put_conc(out, seq, (int64_t)id, ST_OK);
                 }
             }
         } else if (x < 0) {
-            const uint32_t h = X.relh[i];
-            claim[h] = ~0u;
-            __hip_atomic_store(&TT.keys[h], (unsigned long long)TOKEN_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            --dlive;                                                          // CCFC:92-100
-            ++dtomb;
             put_conc(out, seq, 0, ST_RELEASE_OK);
         } else {
             put_conc(out, seq, 0, ST_ALREADY_RELEASE);
         }
+        if (i + 1 == n || skey[i + 1] != flow) now_calls[flow] = fin[flow];
     }
-    if (dlive) atomicAdd(&s_cnt[0], (unsigned long long)dlive);    // (two's complement: wraps to a decrement)
-    if (dtomb) atomicAdd(&s_cnt[1], (unsigned long long)dtomb);
+    if (dlive) atomicAdd(&s_cnt[0], (unsigned long long)dlive);
+    if (dtomb) atomicAdd(&s_cnt[1], (unsigned long long)dtomb);    // (two's complement: wraps to a decrement)
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (s_cnt[0]) atomicAdd(&TT.counts[0], s_cnt[0]);
-        if (s_cnt[1]) atomicAdd(&TT.counts[1], s_cnt[1]);
+        if (s_cnt[0]) tok_count_add(TT, 0, s_cnt[0]);
+        if (s_cnt[1]) tok_count_add(TT, 1, s_cnt[1]);
     }
 }
 
@@ -583,18 +594,18 @@ __global__ __launch_bounds__(256) void k_tok_sweep(TokenTable TT) {
     __syncthreads();
     uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long freed = 0;
-    if (h <= TT.mask && TT.keys[h] == TOKEN_TOMB && TT.keys[(h + 1) & TT.mask] == PKEY_EMPTY) {
+    if (h <= TT.mask && TT.rec[h].key == TOKEN_TOMB && TT.rec[(h + 1) & TT.mask].key == PKEY_EMPTY) {
         for (int k = 0; k < 256; ++k) {                   // (bounded walk back)
-            if (atomicCAS(&TT.keys[h], (unsigned long long)TOKEN_TOMB, (unsigned long long)PKEY_EMPTY) != TOKEN_TOMB)
+            if (atomicCAS(&TT.rec[h].key, (unsigned long long)TOKEN_TOMB, (unsigned long long)PKEY_EMPTY) != TOKEN_TOMB)
                 break;
             ++freed;
             h = (h - 1) & TT.mask;
-            if (TT.keys[h] != TOKEN_TOMB) break;
+            if (TT.rec[h].key != TOKEN_TOMB) break;
         }
     }
     if (freed) atomicAdd(&s_freed, freed);
     __syncthreads();
-    if (threadIdx.x == 0 && s_freed) atomicAdd(&TT.counts[1], 0ull - s_freed);
+    if (threadIdx.x == 0 && s_freed) tok_count_add(TT, 1, 0ull - s_freed);
 }
 
 // RegularExpireStrategy.clearToken (RegularExpireStrategy.java:94-124): with the reference's own
@@ -605,14 +616,14 @@ __global__ __launch_bounds__(256) void k_conc_expire(TokenTable TT, int32_t *now
                                                      unsigned long long *ticket) {
     const uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (h > TT.mask) return;
-    const unsigned long long k = TT.keys[h];
+    const unsigned long long k = TT.rec[h].key;
     if (k == PKEY_EMPTY || k == TOKEN_TOMB) return;
     if (atomicAdd(ticket, 1ull) >= max_tokens) return;
-    TT.keys[h] = TOKEN_TOMB;
-    atomicAdd(&TT.counts[0], ~0ull);
-    atomicAdd(&TT.counts[1], 1ull);
-    const int32_t f = TT.flow_idx[h];
-    if (f >= 0) atomicSub(&now_calls[f], TT.acquire[h]);
+    TT.rec[h].key = TOKEN_TOMB;
+    tok_count_add(TT, 0, ~0ull);
+    tok_count_add(TT, 1, 1ull);
+    const int32_t f = TT.rec[h].flow_idx;
+    if (f >= 0) atomicSub(&now_calls[f], TT.rec[h].acquire);
 }
 
 }  // namespace sentinel

@@ -670,10 +670,9 @@ struct sentinel_engine {
 
     // concurrency tokens (ConcurrentClusterFlowChecker): nowCalls per flow, token cache in HBM
     DevBuf d_now, d_conc_thr, d_seg1_w, d_seg1_rcp, d_seg1_kind;
-    DevBuf d_tok_keys, d_tok_fid, d_tok_fidx, d_tok_acq, d_tok_counts, d_tok_ticket;
-    DevBuf d_tok_claim;                // per token slot: the first release of it in the batch (~0 between batches)
-    DevBuf w_cbig;                     // long concurrency runs: slots + chunks (look-back flags zeroed on allocation)
-    int64_t cbig_n = 0;
+    DevBuf d_tok_rec, d_tok_counts, d_tok_ticket;   // token cache: one TokRec per slot (concurrent.hpp)
+    DevBuf w_cbig;                     // concurrency scan: tile states, fallback list, nowCalls (flags zeroed on allocation)
+    int64_t cbig_n = 0;                // its bytes
     uint32_t conc_epoch = 0;
     uint64_t tok_ub = 0;               // upper bound of live + tombstoned token slots (no device read per batch)
     uint64_t tcap = (uint64_t)1 << 22;
@@ -752,7 +751,6 @@ struct sentinel_engine {
         w_hacq, w_segstart, w_segkey, w_segep, w_segacq, w_het, w_prio, w_done, w_s0, w_k, w_counters;
     DevBuf w_vslot;                    // slot of every value of a param batch
     DevBuf w_runs;                     // partition path: long-run / oversized-half work lists
-    DevBuf w_runrec;                   // partition path, split kernels: {start in gsval, events} per flow
     DevBuf w_pscan;                    // partition path: per-group range sums + range starts
     DevBuf io_ev, io_fl, io_out, io_vals;
     // streamed host path (sentinel_submit_flow_stream_host): copy streams + two staging slots
@@ -1088,34 +1086,40 @@ struct sentinel_engine {
     int ensure_tokens();
     int rewrite_tokens(bool compact, uint64_t new_cap = 0);
     int rebuild_tokens_device(uint64_t new_cap, hipStream_t s);
-    DevBuf sp_tok_keys, sp_tok_fid, sp_tok_fidx, sp_tok_acq, sp_tok_claim;   // the next compaction's target
+    DevBuf sp_tok_rec;                 // the next compaction's target
     TokenTable token_table() {
-        return TokenTable{d_tok_keys.as<unsigned long long>(), d_tok_fid.as<int64_t>(), d_tok_fidx.as<int32_t>(),
-                          d_tok_acq.as<int32_t>(), tcap - 1, d_tok_counts.as<unsigned long long>()};
+        return TokenTable{d_tok_rec.as<TokRec>(), tcap - 1, d_tok_counts.as<unsigned long long>()};
+    }
+    // {live, tombstones}: the striped counters summed (stream-ordered copy on s, synchronised)
+    int token_counts(unsigned long long out[2], hipStream_t s) {
+        unsigned long long h[TOK_CNT_LANES * TOK_CNT_STRIDE];
+        HIP_OK(hipMemcpyAsync(h, d_tok_counts.p, TOK_CNT_BYTES, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipStreamSynchronize(s));
+        out[0] = out[1] = 0;
+        for (int l = 0; l < TOK_CNT_LANES; ++l) {
+            out[0] += h[l * TOK_CNT_STRIDE];
+            out[1] += h[l * TOK_CNT_STRIDE + 1];
+        }
+        return 0;
     }
 };
 
 // Token cache: allocated on first use (SENTINEL_TOKEN_CAPACITY slots, default 4M).
 int sentinel_engine::ensure_tokens() {
-    if (d_tok_keys.p) return 0;
+    if (d_tok_rec.p) return 0;
     if (const char *c = getenv("SENTINEL_TOKEN_CAPACITY")) {
         uint64_t v = strtoull(c, nullptr, 10), p = 1024;
         while (p < v) p <<= 1;
         tcap = p;
     }
     int rc = 0;
-    rc |= d_tok_keys.ensure(tcap * 8);
-    rc |= d_tok_fid.ensure(tcap * 8);
-    rc |= d_tok_fidx.ensure(tcap * 4);
-    rc |= d_tok_acq.ensure(tcap * 4);
-    rc |= d_tok_counts.ensure(16);
+    rc |= d_tok_rec.ensure(tcap * sizeof(TokRec));
+    rc |= d_tok_counts.ensure(TOK_CNT_BYTES);
     rc |= d_tok_ticket.ensure(8);
-    rc |= d_tok_claim.ensure(tcap * 4);
     if (rc) return SENTINEL_E_NOMEM;
-    HIP_OK(hipMemsetAsync(d_tok_keys.p, 0xFF, tcap * 8, stream));
-    HIP_OK(hipMemsetAsync(d_tok_claim.p, 0xFF, tcap * 4, stream));
+    HIP_OK(hipMemsetAsync(d_tok_rec.p, 0xFF, tcap * sizeof(TokRec), stream));   // empty keys, no claims
     tok_ub = 0;
-    HIP_OK(hipMemsetAsync(d_tok_counts.p, 0, 16, stream));
+    HIP_OK(hipMemsetAsync(d_tok_counts.p, 0, TOK_CNT_BYTES, stream));
     HIP_OK(hipStreamSynchronize(stream));
     std::random_device rd;                 // token ids: {salt:23 | counter:40}, opaque to clients like UUID bits
     tok_salt = ((uint64_t)rd() ^ ((uint64_t)rd() << 11)) & ((1ull << 23) - 1);
@@ -1126,56 +1130,46 @@ int sentinel_engine::ensure_tokens() {
 // rule load: tokens of removed flows answer NO_RULE_EXISTS until the flowId comes back), and
 // optionally drop tombstones by re-inserting the live tokens into a fresh table.
 int sentinel_engine::rewrite_tokens(bool compact, uint64_t new_cap) {
-    if (!d_tok_keys.p) return 0;
+    if (!d_tok_rec.p) return 0;
     const uint64_t ocap = tcap;
     const uint64_t ncap = new_cap > ocap ? new_cap : ocap;   // growing re-places every token
     if (ncap != ocap) compact = true;
-    std::vector<uint64_t> keys(ocap);
-    std::vector<int64_t> fid(ocap);
-    std::vector<int32_t> acq(ocap);
-    HIP_OK(hipMemcpy(keys.data(), d_tok_keys.p, ocap * 8, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(fid.data(), d_tok_fid.p, ocap * 8, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(acq.data(), d_tok_acq.p, ocap * 4, hipMemcpyDeviceToHost));
+    std::vector<TokRec> old(ocap);
+    HIP_OK(hipMemcpy(old.data(), d_tok_rec.p, ocap * sizeof(TokRec), hipMemcpyDeviceToHost));
     if (ncap != ocap) {
-        for (DevBuf *b : {&d_tok_keys, &d_tok_fid, &d_tok_fidx, &d_tok_acq, &d_tok_claim}) b->release();
-        int rc = d_tok_keys.ensure(ncap * 8);
-        rc |= d_tok_fid.ensure(ncap * 8);
-        rc |= d_tok_fidx.ensure(ncap * 4);
-        rc |= d_tok_acq.ensure(ncap * 4);
-        rc |= d_tok_claim.ensure(ncap * 4);
-        if (rc) return SENTINEL_E_NOMEM;
-        HIP_OK(hipMemset(d_tok_claim.p, 0xFF, ncap * 4));
+        d_tok_rec.release();
+        if (d_tok_rec.ensure(ncap * sizeof(TokRec))) return SENTINEL_E_NOMEM;
         tcap = ncap;
     }
-    std::vector<uint64_t> nk(tcap, PKEY_EMPTY);
-    std::vector<int64_t> nf(tcap, 0);
-    std::vector<int32_t> nx(tcap, -1), na(tcap, 0);
+    TokRec empty;
+    memset(&empty, 0xFF, sizeof(empty));
+    std::vector<TokRec> nr(tcap, empty);
     uint64_t live = 0, dead = 0;
     for (uint64_t h = 0; h < ocap; ++h) {
-        if (keys[h] == PKEY_EMPTY) continue;
-        if (keys[h] == TOKEN_TOMB) {
-            if (!compact) { nk[h] = TOKEN_TOMB; ++dead; }
+        const TokRec &o = old[h];
+        if (o.key == PKEY_EMPTY) continue;
+        if (o.key == TOKEN_TOMB) {
+            if (!compact) { nr[h].key = TOKEN_TOMB; ++dead; }
             continue;
         }
         uint64_t d = h;
         if (compact) {
-            d = mix64(keys[h]) & (tcap - 1);
-            while (nk[d] != PKEY_EMPTY) d = (d + 1) & (tcap - 1);
+            d = mix64(o.key) & (tcap - 1);
+            while (nr[d].key != PKEY_EMPTY) d = (d + 1) & (tcap - 1);
         }
-        auto it = flow_index.find(fid[h]);
-        nk[d] = keys[h];
-        nf[d] = fid[h];
-        nx[d] = it == flow_index.end() ? -1 : it->second;
-        na[d] = acq[h];
+        auto it = flow_index.find(o.flow_id);
+        nr[d].key = o.key;
+        nr[d].flow_id = o.flow_id;
+        nr[d].flow_idx = it == flow_index.end() ? -1 : it->second;
+        nr[d].acquire = o.acquire;
         ++live;
     }
-    const unsigned long long counts[2] = {live, dead};
+    std::vector<unsigned long long> counts(TOK_CNT_LANES * TOK_CNT_STRIDE, 0ull);
+    counts[0] = live;
+    counts[1] = dead;
     tok_ub = live + dead;
-    HIP_OK(hipMemcpy(d_tok_keys.p, nk.data(), tcap * 8, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(d_tok_fid.p, nf.data(), tcap * 8, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(d_tok_fidx.p, nx.data(), tcap * 4, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(d_tok_acq.p, na.data(), tcap * 4, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(d_tok_counts.p, counts, 16, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_tok_rec.p, nr.data(), tcap * sizeof(TokRec), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_tok_counts.p, counts.data(), TOK_CNT_BYTES, hipMemcpyHostToDevice));
     return 0;
 }
 
@@ -1184,25 +1178,15 @@ int sentinel_engine::rewrite_tokens(bool compact, uint64_t new_cap) {
 int sentinel_engine::rebuild_tokens_device(uint64_t new_cap, hipStream_t s) {
     const uint64_t ocap = tcap, ncap = std::max(new_cap, ocap);
     int rc = 0;
-    rc |= sp_tok_keys.ensure(ncap * 8);
-    rc |= sp_tok_fid.ensure(ncap * 8);
-    rc |= sp_tok_fidx.ensure(ncap * 4);
-    rc |= sp_tok_acq.ensure(ncap * 4);
-    rc |= sp_tok_claim.ensure(ncap * 4);
+    rc |= sp_tok_rec.ensure(ncap * sizeof(TokRec));
     if (rc) return SENTINEL_E_NOMEM;
-    HIP_OK(hipMemsetAsync(sp_tok_keys.p, 0xFF, ncap * 8, s));
-    HIP_OK(hipMemsetAsync(sp_tok_claim.p, 0xFF, ncap * 4, s));
-    HIP_OK(hipMemsetAsync(d_tok_counts.p, 0, 16, s));
+    HIP_OK(hipMemsetAsync(sp_tok_rec.p, 0xFF, ncap * sizeof(TokRec), s));
+    HIP_OK(hipMemsetAsync(d_tok_counts.p, 0, TOK_CNT_BYTES, s));
     const TokenTable O = token_table();
-    const TokenTable N{sp_tok_keys.as<unsigned long long>(), sp_tok_fid.as<int64_t>(), sp_tok_fidx.as<int32_t>(),
-                       sp_tok_acq.as<int32_t>(), ncap - 1, d_tok_counts.as<unsigned long long>()};
+    const TokenTable N{sp_tok_rec.as<TokRec>(), ncap - 1, d_tok_counts.as<unsigned long long>()};
     k_tok_rebuild<<<grid_for((int64_t)ocap), 256, 0, s>>>(O, ocap, N);
     HIP_OK(hipGetLastError());
-    std::swap(d_tok_keys, sp_tok_keys);
-    std::swap(d_tok_fid, sp_tok_fid);
-    std::swap(d_tok_fidx, sp_tok_fidx);
-    std::swap(d_tok_acq, sp_tok_acq);
-    std::swap(d_tok_claim, sp_tok_claim);
+    std::swap(d_tok_rec, sp_tok_rec);
     tcap = ncap;
     return 0;
 }
@@ -1624,23 +1608,7 @@ static void launch_part_decide(sentinel_engine_t *e, int32_t nparts, const KeyTa
 #define SENTINEL_ALLBIG_PCT 90
 #endif
     const bool all_big = n > (int64_t)nparts * (int64_t)(PH_KEYS * SENTINEL_ALLBIG_PCT / 100);
-#ifdef SENTINEL_PART_FUSED
-    const bool split = false;
-#else
-    // halves of 512 flows (flow tables of 2^19..2^20 flows): the LDS sort and the decisions in two kernels
-    const bool split = !part_coop(lb) && lb == PART_MAX_BITS;
-#endif
-    if (!all_big && split) {
-        uint2 *runrec = e->w_runrec.as<uint2>();
-        e->launch("part_sort", n, s, [&] {
-            k_part_sort<<<16u * (unsigned)((nparts + 7) / 8), PH_THREADS, 0, s>>>(pval, gsval, rstart, lb, nparts, LR, big,
-                                                                              nbig, stat, runrec);
-        });
-        e->launch("part_decide", n, s, [&] {
-            k_part_decide<NMAX><<<32u * (unsigned)((nparts + 7) / 8), 256, 0, s>>>(FT, gsval, runrec, lb, nparts,
-                                                                                 (int32_t)e->rules.size(), src, V);
-        });
-    } else if (!all_big) {
+    if (!all_big) {
         e->launch("part_fused", n, s, [&] {
             const dim3 g(16u * (unsigned)((nparts + 7) / 8));
             if (part_coop(lb))      // <= 256 flows per half: cooperative verdict sweep
@@ -1690,7 +1658,6 @@ static int ensure_part_bufs(sentinel_engine_t *e, const PartBufs &B, int64_t n) 
     int rc = B.pscan->ensure(((size_t)g.ng * g.nparts + 2 * (size_t)g.nparts + 1) * 4);
     rc |= B.runs->ensure(long_runs_bytes(n, LONG_RUN, 4 + 2 * (size_t)g.nparts));
     rc |= B.stat->ensure(8);
-    if (g.lb == PART_MAX_BITS) rc |= e->w_runrec.ensure(((size_t)g.nparts << g.lb) * sizeof(uint2));
     return rc;
 }
 
@@ -2485,9 +2452,8 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
                       &e->d_prule_kind, &e->d_cm, &e->d_lrule_valid, &e->d_lrule_tok, &e->d_lrule_burst,
                       &e->d_lrule_dur, &e->d_lrule_w, &e->d_lrule_rcp, &e->d_lrule_kind, &e->d_lhot_keys,
                       &e->d_lhot_tok, &e->d_ltable, &e->d_lstate, &e->d_now, &e->d_conc_thr, &e->d_seg1_w,
-                      &e->d_seg1_rcp, &e->d_seg1_kind, &e->d_tok_keys, &e->d_tok_fid, &e->d_tok_fidx,
-                      &e->d_tok_acq, &e->d_tok_counts, &e->d_tok_ticket, &e->d_tok_claim, &e->w_cbig, &e->sp_tok_keys,
-                      &e->sp_tok_fid, &e->sp_tok_fidx, &e->sp_tok_acq, &e->sp_tok_claim, &e->w_runs, &e->w_pscan, &e->d_lres_state,
+                      &e->d_seg1_rcp, &e->d_seg1_kind, &e->d_tok_rec,
+                      &e->d_tok_counts, &e->d_tok_ticket, &e->w_cbig, &e->sp_tok_rec, &e->w_runs, &e->w_pscan, &e->d_lres_state,
                       &e->d_lres_count, &e->d_lres_w, &e->d_lres_rcp, &e->d_lres_kind, &e->d_lres_tcount,
                       &e->d_lres_flags, &e->w_lslow, &e->io_lrt, &e->d_lrule_grade,
                       &e->d_lg_on, &e->d_lg_dn, &e->d_lg_created, &e->d_lg_roff, &e->d_lg_rules, &e->d_lg_comp,
@@ -3796,19 +3762,23 @@ static int submit_concurrent(sentinel_engine_t *e, int64_t n, const ConcEvent *d
         if (s != e->stream) HIP_OK(hipStreamSynchronize(s));
         HIP_OK(hipStreamSynchronize(e->stream));
         unsigned long long counts[2];
-        HIP_OK(hipMemcpy(counts, e->d_tok_counts.p, 16, hipMemcpyDeviceToHost));
+        if (int rc2 = e->token_counts(counts, e->stream)) return rc2;
         e->tok_ub = counts[0] + counts[1];
-        if ((double)(e->tok_ub + (uint64_t)n) > 0.75 * (double)e->tcap && counts[1] > 0) {
+        if ((double)(e->tok_ub + (uint64_t)n) > 0.75 * (double)e->tcap && counts[1] > e->tcap / 64) {
             // first the tombstone sweep (one pass over the keys), then the counts again
             k_tok_sweep<<<(unsigned)((e->tcap + 255) / 256), 256, 0, e->stream>>>(e->token_table());
-            HIP_OK(hipMemcpyAsync(counts, e->d_tok_counts.p, 16, hipMemcpyDeviceToHost, e->stream));
-            HIP_OK(hipStreamSynchronize(e->stream));
+            if (int rc2 = e->token_counts(counts, e->stream)) return rc2;
             e->tok_ub = counts[0] + counts[1];
         }
         if ((double)(e->tok_ub + (uint64_t)n) > 0.75 * (double)e->tcap) {
-            // drop the tombstones, and grow until the live tokens plus a few batches fit
+            // drop the tombstones, and grow until the live tokens plus a few batches fit (a crossing of the bound
+            // costs one host synchronisation; releases empty their slots, so it rarely needs a sweep)
             uint64_t nc = e->tcap;
             while ((double)(counts[0] + 4 * (uint64_t)n) > 0.75 * (double)nc && nc < ((uint64_t)1 << 32)) nc <<= 1;
+#ifndef SENTINEL_TOK_HEADROOM
+#define SENTINEL_TOK_HEADROOM 4
+#endif
+            while ((double)(counts[0] + SENTINEL_TOK_HEADROOM * (uint64_t)n) > 0.75 * (double)nc && nc < ((uint64_t)1 << 28)) nc <<= 1;
             rc = e->rebuild_tokens_device(nc, s);
             if (rc) return rc;
             e->tok_ub = counts[0];
@@ -3821,66 +3791,50 @@ static int submit_concurrent(sentinel_engine_t *e, int64_t n, const ConcEvent *d
     const int fbits = bits_for(F);
     const uint32_t finvalid = ((uint32_t)1 << fbits) - 1;
     uint32_t *fkey = e->w_fkey.as<uint32_t>();
-    uint32_t *relslot = e->w_k.as<uint32_t>();
-    uint32_t *claim = e->d_tok_claim.as<uint32_t>();
+    uint64_t *aux = e->w_hep.as<uint64_t>();                  // per valid event: amount / released slot
     const int64_t nb = sort_blocks(n);
     const TokenTable TT = e->token_table();
     e->launch("conc_prep", n, s, [&] {
         k_conc_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(n, dev, F, TT, dout, fkey, finvalid,
-                                                                      e->w_fhist.as<uint32_t>(), nb, relslot, claim);
+                                                                      e->w_fhist.as<uint32_t>(), nb, aux);
     });
     if (F > 0) {
         const EventSrc src{nullptr, (const ParamEvent *)dev, nullptr, false};
         e->sort(fkey, n, fbits, e->w_fhist.as<uint32_t>(), src, s);
         const uint32_t *skey = e->w_skey.as<uint32_t>();
-        uint32_t *flag = e->w_segid.as<uint32_t>();
-        uint32_t *run_start = e->w_segstart.as<uint32_t>();
-        uint32_t *ctl = e->w_counters.as<uint32_t>();           // [0] runs, [1] long runs, [2] chunks, [3] ticket
-        // long-run work lists, sized for this batch: slots <= n / (CONC_LANE_RUN + 1), chunks <= slots + n / CONC_CHUNK
-        const int64_t ms = n / (CONC_LANE_RUN + 1) + 1, mc = ms + n / CONC_CHUNK + 1;
+        const uint64_t *sval = e->w_sval.as<uint64_t>();
+        uint32_t *ctl = e->w_counters.as<uint32_t>();           // [0] tile ticket, [1] fallback segments
+        // scan tiles (look-back flags, zeroed on allocation, and states), fallback list, nowCalls after the batch
+        const int64_t nt = (n + CS_TILE - 1) / CS_TILE, segs = std::min<int64_t>(n, F);
         auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
-        const int64_t o_run = 0, o_now = o_run + al(ms * 4), o_tp = o_now + al(ms * 4), o_unit = o_tp + al(ms * 8),
-                      o_mag = o_unit + al(ms * 4), o_ch = o_mag + al(ms * 8), o_cs = o_ch + al(ms * 8),
-                      o_cj = o_cs + al(mc * 4), o_fl = o_cj + al(mc * 4), o_agg = o_fl + al(mc * 4),
-                      o_inc = o_agg + al(mc * 16), o_end = o_inc + al(mc * 16);
-        if (n > e->cbig_n) {
+        const int64_t o_fl = 0, o_agg = o_fl + al(nt * 4), o_inc = o_agg + al(nt * (int64_t)sizeof(ConcSeg)),
+                      o_ser = o_inc + al(nt * (int64_t)sizeof(ConcSeg)), o_fin = o_ser + al(segs * 4),
+                      o_end = o_fin + al((int64_t)F * 4);
+        if (o_end > e->cbig_n) {
             e->w_cbig.release();
             if (e->w_cbig.ensure((size_t)o_end)) return SENTINEL_E_NOMEM;
             HIP_OK(hipMemsetAsync(e->w_cbig.p, 0, (size_t)o_end, s));   // look-back flags of no epoch
-            e->cbig_n = n;
+            e->cbig_n = o_end;
         }
         e->conc_epoch = (e->conc_epoch + 1) & 0x3FFFFFFFu;
         if (e->conc_epoch == 0) e->conc_epoch = 1;
         char *gb = e->w_cbig.as<char>();
-        const ConcBig G{(uint32_t *)(gb + o_run), (int32_t *)(gb + o_now), (int64_t *)(gb + o_tp), (uint32_t *)(gb + o_unit),
-                        (unsigned long long *)(gb + o_mag), (uint2 *)(gb + o_ch), (uint32_t *)(gb + o_cs),
-                        (uint32_t *)(gb + o_cj), (uint32_t *)(gb + o_fl), (MinPlus *)(gb + o_agg), (MinPlus *)(gb + o_inc),
-                        ctl, e->conc_epoch};
-        HIP_OK(hipMemsetAsync(ctl, 0, 16, s));
-        e->launch("conc_runs", n, s, [&] {
-            k_conc_heads<<<grid_for(n), 256, 0, s>>>(skey, n, finvalid, flag);
+        const ConcScan S{(uint32_t *)(gb + o_fl), (ConcSeg *)(gb + o_agg), (ConcSeg *)(gb + o_inc), ctl,
+                         (uint32_t *)(gb + o_ser), (int32_t *)(gb + o_fin), e->conc_epoch};
+        HIP_OK(hipMemsetAsync(ctl, 0, 8, s));
+        const ConcElems X{e->w_hacq.as<int32_t>(), e->w_done.as<uint8_t>()};
+        int32_t *now_calls = e->d_now.as<int32_t>();
+        const double *thr = e->d_conc_thr.as<double>();
+        e->launch("conc_scan", n, s, [&] {
+            k_conc_scan<<<(unsigned)nt, CS_THREADS, 0, s>>>(aux, sval, skey, finvalid, n, TT, thr, now_calls, X, S);
         });
-        e->scan(flag, n, true, s);
-        e->launch("conc_runs", n, s, [&] {
-            k_conc_runs<<<grid_for(n), 256, 0, s>>>(skey, n, finvalid, flag, run_start, ctl);
+        e->launch("conc_serial", n, s, [&] {
+            k_conc_serial<<<grid_for(segs), 256, 0, s>>>(skey, n, now_calls, thr, X, S);
         });
         const uint64_t id_base = (e->tok_salt << 40) | e->tok_counter;
-        const ConcElems X{e->w_hacq.as<int32_t>(), e->w_segacq.as<uint32_t>(), e->w_done.as<uint8_t>()};
-        e->launch("conc_elems", n, s, [&] {
-            k_conc_elems<<<grid_for(n), 256, 0, s>>>(dev, e->w_sval.as<uint64_t>(), skey, finvalid, n, relslot, claim, TT, X);
-        });
-        const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, mc));
-        e->launch("conc_lanes", n, s, [&] {
-            k_conc_lanes<<<grid_for(n), 256, 0, s>>>(run_start, skey, e->d_now.as<int32_t>(), e->d_conc_thr.as<double>(),
-                                                     X, G);
-        });
-        e->launch("conc_info", n, s, [&] { k_conc_info<<<g, 256, 0, s>>>(run_start, X, G); });
-        e->launch("conc_chunks", n, s, [&] {
-            k_conc_chunks<<<g, CB_THREADS, 0, s>>>(run_start, skey, e->d_now.as<int32_t>(), e->d_conc_thr.as<double>(), X, G);
-        });
         e->launch("conc_apply", n, s, [&] {
-            k_conc_apply<<<grid_for(n), 256, 0, s>>>(e->w_sval.as<uint64_t>(), skey, finvalid, n, X, claim, TT,
-                                                     e->d_flow_ids.as<int64_t>(), id_base, dout);
+            k_conc_apply<<<grid_for(n), 256, 0, s>>>(sval, skey, finvalid, n, X, TT, e->d_flow_ids.as<int64_t>(), id_base,
+                                                     S.fin, now_calls, dout);
         });
         e->tok_counter += (uint64_t)n;
     }
@@ -3933,9 +3887,8 @@ int sentinel_concurrent_token_count(sentinel_engine_t *e, int64_t *count) {
     *count = 0;
     if (!e->d_tok_counts.p) return 0;
     HIP_OK(hipSetDevice(e->device));
-    HIP_OK(hipStreamSynchronize(e->stream));
     unsigned long long c[2];
-    HIP_OK(hipMemcpy(c, e->d_tok_counts.p, 16, hipMemcpyDeviceToHost));
+    if (int rc2 = e->token_counts(c, e->stream)) return rc2;
     *count = (int64_t)c[0];
     return 0;
 }
@@ -3944,7 +3897,7 @@ int sentinel_concurrent_expire(sentinel_engine_t *e, int64_t max_tokens, int64_t
     if (!e || !removed || max_tokens < 0) return fail(SENTINEL_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(e->mu);
     *removed = 0;
-    if (!e->d_tok_keys.p || max_tokens == 0) return 0;
+    if (!e->d_tok_rec.p || max_tokens == 0) return 0;
     HIP_OK(hipSetDevice(e->device));
     HIP_OK(hipMemsetAsync(e->d_tok_ticket.p, 0, 8, e->stream));
     k_conc_expire<<<grid_for((int64_t)e->tcap), 256, 0, e->stream>>>(e->token_table(), e->d_now.as<int32_t>(),

@@ -355,12 +355,6 @@ __device__ inline void pd_walk(const ParamRules &PR, const PRuleRec *RR, const P
     const double I_s = rr.I_s;
     const double thr = (rr.nf >> 16) ? value_threshold(PR, (uint32_t)rule, key) : rr.thr;   // CPFC:101-120
     const uint32_t before = nfresh;
-#ifdef SENTINEL_PW_PREFETCH
-    // most keys sit at their home slot: its window lines are touched (one dword each) together with the
-    // probe, so the window load after the probe finds them in L2 / the Infinity Cache
-    const uint32_t *hw = reinterpret_cast<const uint32_t *>(S.state + (int64_t)(mix64(key) & S.mask) * S.stride);
-    const uint32_t pfa = hw[0], pfb = S.stride > 16 ? hw[32] : 0u;     // (records over 128 B span two lines)
-#endif
     const int64_t h = slot_insert_counted(S.keys, S.mask, key, nfresh);
     if (h < 0) {                                                         // table full: param_reserve prevents it
         for (uint32_t q = q0; q < q1; ++q) put_verdict(out, (uint32_t)sv[q] & SEQ_MASK, ST_FAIL, 0, 0);
@@ -430,9 +424,6 @@ __device__ inline void pd_walk(const ParamRules &PR, const PRuleRec *RR, const P
 #pragma unroll
     for (int j = 0; j < NMAX; ++j)
         if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(st + 2 * j) = longlong2{ep[j], ct[j]};
-#ifdef SENTINEL_PW_PREFETCH
-    asm volatile("" ::"v"(pfa), "v"(pfb));
-#endif
 }
 
 #ifdef SENTINEL_DIAG_PHASES     // per workgroup: [0] start, [3] end, [4..6] phase sums, [7] rounds, [8] keys
@@ -509,7 +500,7 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
             if ((uint32_t)wave * (PG_ITEMS * WAVE) + j * WAVE + lane < m) pend |= 1u << j;
         uint32_t roff = 0;                                               // grouped values emitted by earlier rounds
         for (;;) {
-            const unsigned long long pt0 = PD_NOW();
+            [[maybe_unused]] const unsigned long long pt0 = PD_NOW();
             unsigned long long k[PG_ITEMS];
             uint64_t v[PG_ITEMS];
             int32_t ru[PG_ITEMS];
@@ -536,7 +527,7 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
                     eid[j] = pd_insert(hkey, hrule, k[j], ru[j], (uint32_t)(mix64(k[j]) >> 32) & (PD_HT - 1));
             }
             __syncthreads();
-            const unsigned long long pt1 = PD_NOW();
+            [[maybe_unused]] const unsigned long long pt1 = PD_NOW();
             uint32_t rank[PG_ITEMS];
 #pragma unroll
             for (int j = 0; j < PG_ITEMS; ++j) {
@@ -596,7 +587,7 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
             for (int q = 0; q < PD_EPT; ++q)
                 if (tot[q]) klist[kpos++] = (uint16_t)(t * PD_EPT + q);
             __syncthreads();
-            const unsigned long long pt2 = PD_NOW();
+            [[maybe_unused]] const unsigned long long pt2 = PD_NOW();
             if (emit) {
                 for (uint32_t i = t; i < placed; i += PD_THREADS) gval[gbase + roff + i] = sv[i];
                 const uint32_t rb = s_rbase;
@@ -615,7 +606,7 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
             }
             roff += placed;
             const int more = __syncthreads_or(pend != 0);                // (also: done with the LDS)
-            const unsigned long long pt3 = PD_NOW();
+            [[maybe_unused]] const unsigned long long pt3 = PD_NOW();
             PD_ACC(4, pt1 - pt0);
             PD_ACC(5, pt2 - pt1);
             PD_ACC(6, pt3 - pt2);

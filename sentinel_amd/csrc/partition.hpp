@@ -1633,191 +1633,6 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
 #endif
 }
 
-// ---------------------------------------------------------------------------------------------
-// Split variant of k_part_half for halves of 512 flows (flow tables of 2^19..2^20 flows, the config-3
-// shape): the LDS sort and the decisions in two kernels, so that neither carries the other's registers.
-//   k_part_sort    phases 1-2 of k_part_half (range values -> per-flow counts -> LDS slots in
-//                  (flow, arrival) order), then the sorted half written to gsval (coalesced) and one
-//                  record {start in gsval, events} per flow
-//   k_part_decide  one lane per flow, no LDS: rule fields, window header, the flow's run read back from
-//                  gsval, closed form / general walk (part_run_single / part_run_w), verdicts
-// Oversized halves and long runs go to k_part_big / k_part_long exactly as from k_part_half (their
-// flows get a zero record, which k_part_decide skips).
-#ifndef SENTINEL_PS_MINB
-#define SENTINEL_PS_MINB 6
-#endif
-// run record {start in gsval, events | flags}: RR_SKIP = decided elsewhere (a long run: k_part_long),
-// RR_NODATA = the half was not sorted here (oversized: k_part_big)
-constexpr uint32_t RR_SKIP = 0x80000000u, RR_NODATA = 0xFFFFFFFFu;
-__global__ __launch_bounds__(PH_THREADS, SENTINEL_PS_MINB) void k_part_sort(
-    const uint64_t *__restrict__ pval, uint64_t *__restrict__ gsval, const uint32_t *__restrict__ rstart, int lb,
-    int32_t nranges, LongRuns LR, uint32_t *__restrict__ big, uint32_t *__restrict__ nbig,
-    unsigned long long *__restrict__ max_range, uint2 *__restrict__ runrec) {
-    __shared__ uint64_t sv[PH_CAP];
-    __shared__ uint32_t base[PH_BINS];
-    __shared__ uint16_t cnt[PH_WAVES][PH_BINS];
-    __shared__ uint32_t waves_tot[PH_WAVES];
-    __shared__ uint32_t s_cmax;
-    uint32_t p, h;
-    half_of_block(blockIdx.x, p, h);
-    const int hb = lb > 0 ? lb - 1 : 0;
-    if ((int32_t)p >= nranges || (lb == 0 && h == 1)) return;
-
-    const uint32_t t = threadIdx.x;
-    const uint32_t pstart = rstart[p];
-    const uint32_t pend = rstart[p + 1];
-    const uint32_t size = pend - pstart;
-    const uint32_t key = (p << lb) | (h << hb) | t;
-    if (t == 0 && h == 0 && max_range) atomicMax(max_range, (unsigned long long)size);   // skew statistic
-    if (size > PH_KEYS) {                                 // block-uniform
-        runrec[key] = make_uint2(0u, RR_NODATA);
-        if (t == 0) big[atomicAdd(nbig, 1u)] = (p << 1) | h;
-        return;
-    }
-    const uint32_t hmask = (1u << hb) - 1u;
-    uint64_t val[PH_ITEMS];
-#pragma unroll
-    for (int j = 0; j < PH_ITEMS; ++j) {
-        const uint32_t q = j * PH_THREADS + t;
-        val[j] = q < size ? pval[pstart + q] : ~0ull;
-    }
-    auto local = [&](uint64_t v) -> uint32_t {
-        const uint32_t k = (uint32_t)(v >> VAL_KEY_SHIFT);
-        return (v != ~0ull && (k >> hb) == h) ? (k & hmask) : 0xFFFFFFFFu;
-    };
-    base[t] = 0;
-    if (t == 0) s_cmax = 0;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < PH_ITEMS; ++j) {
-        const uint32_t kj = local(val[j]);
-        if (kj != 0xFFFFFFFFu) atomicAdd(&base[kj], 1u);
-    }
-    __syncthreads();
-    const uint32_t c = base[t];
-    uint32_t total;
-    const uint32_t start = block_exclusive_scan(c, waves_tot, &total);
-    if (total > PH_CAP) {                                 // block-uniform: the half does not fit in LDS
-        runrec[key] = make_uint2(0u, RR_NODATA);
-        if (t == 0) big[atomicAdd(nbig, 1u)] = (p << 1) | h;
-        return;
-    }
-    if (c) atomicMax(&s_cmax, c);
-    base[t] = start;
-    __syncthreads();
-    const uint32_t goff = pstart + (h ? size - total : 0u);
-    if (s_cmax <= PH_SMALL_RUN) {
-        // unordered slots by LDS atomics, then each thread insertion-sorts its own run by arrival position
-#pragma unroll
-        for (int j = 0; j < PH_ITEMS; ++j) {
-            const uint32_t kj = local(val[j]);
-            if (kj != 0xFFFFFFFFu) sv[atomicAdd(&base[kj], 1u)] = val[j];
-        }
-        __syncthreads();
-        for (uint32_t i = start + 1; i < start + c; ++i) {
-            const uint64_t v = sv[i];
-            const uint32_t sq = (uint32_t)v & SEQ_MASK;
-            uint32_t j = i;
-            for (; j > start; --j) {
-                const uint64_t u = sv[j - 1];
-                if (((uint32_t)u & SEQ_MASK) < sq) break;
-                sv[j] = u;
-            }
-            sv[j] = v;
-        }
-    } else {
-        // a long run somewhere: stable ranking with ballots over wave-contiguous blocks of the range
-        // (positions in the range are in arrival order: k_part_scatter is stable), as k_part_half
-        const int wave = threadIdx.x / WAVE;
-        const uint32_t lane = lane_id();
-        const uint32_t b0 = (uint32_t)wave * (PH_ITEMS * WAVE);
-#pragma unroll
-        for (int j = 0; j < PH_ITEMS; ++j) {
-            const uint32_t q = b0 + j * WAVE + lane;
-            val[j] = q < size ? pval[pstart + q] : ~0ull;
-        }
-        {
-            uint32_t *z = reinterpret_cast<uint32_t *>(&cnt[0][0]);
-            for (int d = t; d < PH_WAVES * PH_BINS / 2; d += PH_THREADS) z[d] = 0;
-        }
-        __syncthreads();
-        uint32_t rank[PH_ITEMS];
-#pragma unroll
-        for (int j = 0; j < PH_ITEMS; ++j) {
-            const uint32_t kj = local(val[j]);
-            const bool valid = kj != 0xFFFFFFFFu;
-            const uint32_t d = kj & hmask;
-            const uint64_t peers = match_peers<PART_MAX_BITS>(d, valid, hb);
-            uint32_t r = 0;
-            if (valid) r = cnt[wave][d] + mask_rank(peers);
-            __builtin_amdgcn_wave_barrier();
-            if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane) cnt[wave][d] += (uint16_t)__popcll(peers);
-            __builtin_amdgcn_wave_barrier();
-            rank[j] = r;
-        }
-        __syncthreads();
-        uint32_t run = 0;
-#pragma unroll
-        for (int w = 0; w < PH_WAVES; ++w) {
-            const uint32_t x = cnt[w][t];
-            cnt[w][t] = (uint16_t)run;
-            run += x;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < PH_ITEMS; ++j) {
-            const uint32_t kj = local(val[j]);
-            if (kj == 0xFFFFFFFFu) continue;
-            sv[base[kj] + cnt[wave][kj] + rank[j]] = val[j];          // base = flow starts here
-        }
-    }
-    __syncthreads();
-    for (uint32_t i = t; i < total; i += PH_THREADS) gsval[goff + i] = sv[i];
-    if (c > LONG_RUN) {
-        LR.push(goff + start, goff + start + c, key);
-        runrec[key] = make_uint2(goff + start, RR_SKIP | c);
-    } else {
-        runrec[key] = make_uint2(goff + start, c);
-    }
-}
-
-// XCD-aware: decide block b takes flows of range p = (b / 32) * 8 + b % 8 (quarter (b / 8) % 4), the
-// XCD whose L2 the sort kernel wrote that range's sorted values through.  The quarter's runs are one
-// contiguous stretch of gsval (flows in order inside a sorted half): loaded into LDS with coalesced
-// loads, then every lane reads its run from LDS.
-#ifndef SENTINEL_PD_MINB
-#define SENTINEL_PD_MINB 4
-#endif
-constexpr uint32_t PD_QCAP = PH_CAP;                     // a quarter's events (a half fits PH_CAP)
-template <int NMAX>
-__global__ __launch_bounds__(256, SENTINEL_PD_MINB) void k_part_decide(KeyTable T, const uint64_t *__restrict__ gsval,
-                                                                        const uint2 *__restrict__ runrec, int lb,
-                                                                        int32_t nranges, int32_t nflows, EventSrc src,
-                                                                        Verdicts V) {
-    __shared__ uint64_t sv[PD_QCAP];
-    const uint32_t b = blockIdx.x;
-    const uint32_t p = (b / 32u) * 8u + b % 8u, qtr = (b / 8u) % 4u;
-    if ((int32_t)p >= nranges || lb != PART_MAX_BITS) return;            // block-uniform
-    const uint32_t key0 = (p << lb) + qtr * 256u;
-    if (key0 >= (uint32_t)nflows) return;                               // block-uniform
-    const uint32_t key = key0 + threadIdx.x;
-    FlowWindow<NMAX> fw;
-    fw.load_rule(T, min(key, (uint32_t)nflows - 1u));                  // in flight during the staging
-    const uint2 r = runrec[key];
-    const uint2 rf = runrec[key0], rl = runrec[key0 + 255u];
-    if (rf.y == RR_NODATA) return;                                       // block-uniform: k_part_big's half
-    const uint32_t lo = rf.x, hi = rl.x + (rl.y & ~RR_SKIP);
-    for (uint32_t i = threadIdx.x; i < hi - lo; i += 256u) sv[i] = gsval[lo + i];
-    __syncthreads();
-    if (key >= (uint32_t)nflows || r.y == 0 || (r.y & RR_SKIP)) return;
-    const int64_t T0 = src.t0();
-    const uint32_t q0 = r.x - lo, q1 = q0 + r.y;
-    if (!part_run_single<NMAX>(fw, sv, q0, q1, src, V, T0)) {
-        fw.load_header(T0);
-        part_run_w<NMAX>(fw, T, key, sv, q0, q1, src, V, T0);
-    }
-}
-
 // Oversized halves (or every half, `big == nullptr`): the same decision with the half sorted into
 // HBM in chunks (any size).  Entry = (range << 1) | half.
 constexpr int PB_ITEMS = 8;
