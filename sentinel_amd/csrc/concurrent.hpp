@@ -132,7 +132,10 @@ __global__ __launch_bounds__(SORT_THREADS) void k_conc_prep(int64_t n, const Con
                                                             TokenTable TT, uint64_t *__restrict__ out,
                                                             uint32_t *__restrict__ fkey, uint32_t finvalid,
                                                             uint32_t *__restrict__ fhist, int64_t nblocks,
-                                                            uint64_t *__restrict__ aux) {
+                                                            uint64_t *__restrict__ aux, unsigned long long *__restrict__ desc,
+                                                            int64_t ndesc) {
+    for (int64_t j = (int64_t)blockIdx.x * SORT_THREADS + threadIdx.x; j < ndesc; j += (int64_t)gridDim.x * SORT_THREADS)
+        desc[j] = 0;                                      // k_conc_scan's look-back descriptors: not yet
     __shared__ uint32_t hf[MAX_PASSES][RADIX];
     for (int d = threadIdx.x; d < MAX_PASSES * RADIX; d += SORT_THREADS) (&hf[0][0])[d] = 0;
     __syncthreads();
@@ -247,47 +250,68 @@ __device__ inline int64_t conc_tprime(double threshold) {
 }
 
 // Segmented scan state: the composition since the last segment head in the range (or of the whole
-// range when it holds none), the position of that head, and whether an amount other than +-1 occurred
-// since it.
-constexpr uint32_t CONC_NO_HEAD = 0xFFFFFFFFu;
+// range when it holds none), whether the range holds a head, and whether an amount other than +-1
+// occurred since the last head (such a segment is left to k_conc_serial).
 struct ConcSeg {
     int64_t p, c;
-    uint32_t head;
+    uint32_t hd;
     uint32_t nu;
 };
-__device__ inline ConcSeg cs_identity() { return ConcSeg{0, CONC_INF, CONC_NO_HEAD, 0u}; }
+__device__ inline ConcSeg cs_identity() { return ConcSeg{0, CONC_INF, 0u, 0u}; }
 __device__ inline ConcSeg cs_then(const ConcSeg &a, const ConcSeg &b) {
-    if (b.head != CONC_NO_HEAD) return b;
+    if (b.hd) return b;
     const MinPlus f = mp_then(MinPlus{a.p, a.c}, MinPlus{b.p, b.c});
-    return ConcSeg{f.p, f.c, a.head, a.nu | b.nu};
+    return ConcSeg{f.p, f.c, a.hd, a.nu | b.nu};
 }
 __device__ inline ConcSeg cs_shfl(const ConcSeg &v, int src) {
-    return ConcSeg{__shfl(v.p, src, WAVE), __shfl(v.c, src, WAVE), (uint32_t)__shfl((int)v.head, src, WAVE),
+    return ConcSeg{__shfl(v.p, src, WAVE), __shfl(v.c, src, WAVE), (uint32_t)__shfl((int)v.hd, src, WAVE),
                    (uint32_t)__shfl((int)v.nu, src, WAVE)};
 }
 __device__ inline ConcSeg cs_shfl_up(const ConcSeg &v, int o) {
-    return ConcSeg{__shfl_up(v.p, o, WAVE), __shfl_up(v.c, o, WAVE), (uint32_t)__shfl_up((int)v.head, o, WAVE),
+    return ConcSeg{__shfl_up(v.p, o, WAVE), __shfl_up(v.c, o, WAVE), (uint32_t)__shfl_up((int)v.hd, o, WAVE),
                    (uint32_t)__shfl_up((int)v.nu, o, WAVE)};
+}
+
+// A tile's look-back descriptor is one 64-bit word, published and read with relaxed agent-scope atomics
+// (no fence: on gfx950 an agent-scope release writes back the XCD's L2 and an acquire invalidates it):
+//   bits 0-1 status (0 not yet, 1 aggregate, 2 inclusive), 2 head, 3 not-unit, 4 c = infinity,
+//   5-33 p, 34-62 d = c - T' of the state's flow (29-bit two's complement each).
+// Within a unit segment |p| and |d| are at most its length (< 2^28, MAX_BATCH); a larger value only
+// occurs in a segment that is not unit, and saturates with the not-unit bit set.  The state's composition
+// belongs to the flow of the range's last element, which is the reader's first flow whenever the reader
+// uses it (otherwise the reader's first element is a head), so d is rebased on the reader's T'.
+constexpr int64_t CS_LIM = ((int64_t)1 << 28) - 1;
+__device__ inline uint64_t cs_pack(const ConcSeg &v, int64_t tp, uint64_t status) {
+    uint64_t nu = v.nu;
+    int64_t p = v.p;
+    if (p > CS_LIM || p < -CS_LIM) { p = p > 0 ? CS_LIM : -CS_LIM; nu = 1; }
+    const bool inf = v.c >= CONC_INF;
+    int64_t d = inf ? 0 : v.c - tp;
+    if (d > CS_LIM || d < -CS_LIM) { d = d > 0 ? CS_LIM : -CS_LIM; nu = 1; }
+    return status | (uint64_t)(v.hd ? 1 : 0) << 2 | nu << 3 | (uint64_t)(inf ? 1 : 0) << 4 |
+           ((uint64_t)p & 0x1FFFFFFFull) << 5 | ((uint64_t)d & 0x1FFFFFFFull) << 34;
+}
+__device__ inline ConcSeg cs_unpack(uint64_t w, int64_t tp) {
+    const int64_t p = (int64_t)(w << 30) >> 35;
+    const int64_t d = (int64_t)(w << 1) >> 35;
+    return ConcSeg{p, (w >> 4) & 1 ? CONC_INF : tp + d, (uint32_t)(w >> 2) & 1u, (uint32_t)(w >> 3) & 1u};
 }
 
 constexpr int CS_THREADS = 256;
 constexpr int CS_WAVES = CS_THREADS / WAVE;
 #ifndef SENTINEL_CONC_ITEMS
-#define SENTINEL_CONC_ITEMS 8
+#define SENTINEL_CONC_ITEMS 4
 #endif
 constexpr int CS_ITEMS = SENTINEL_CONC_ITEMS;               // consecutive sorted positions per thread
 constexpr int64_t CS_TILE = (int64_t)CS_THREADS * CS_ITEMS;
 
-// Per tile the look-back status {epoch << 2 | 1 aggregate / 2 inclusive} and state; the tile ticket and
-// the fallback list; per flow nowCalls after the batch.
+// Per tile the look-back descriptor (zeroed by k_conc_prep); the tile ticket and the fallback list; per
+// flow nowCalls after the batch.
 struct ConcScan {
-    uint32_t *flag;
-    ConcSeg *agg;
-    ConcSeg *inc;
+    unsigned long long *desc;
     uint32_t *ctl;           // [0] tile ticket, [1] segments left to k_conc_serial
-    uint32_t *serial;        // their head positions
+    uint32_t *serial;        // their last positions
     int32_t *fin;            // [flow] nowCalls after the batch (stored by k_conc_apply)
-    uint32_t epoch;
 };
 
 // A claimed release frees its token's slot (CCFC:92-100).  No insert runs in the same kernel, and
@@ -327,7 +351,9 @@ __global__ __launch_bounds__(CS_THREADS) void k_conc_scan(const uint64_t *__rest
                                                           const int32_t *__restrict__ now_calls, ConcElems X, ConcScan S) {
     __shared__ ConcSeg s_w[CS_WAVES];
     __shared__ ConcSeg s_prefix;
+    __shared__ int64_t s_tpl, s_tpf;
     __shared__ uint32_t s_tile;
+    __shared__ bool s_lb;
     __shared__ unsigned long long s_cnt[2];
     const uint32_t t = threadIdx.x;
     const uint32_t lane = lane_id();
@@ -379,16 +405,22 @@ __global__ __launch_bounds__(CS_THREADS) void k_conc_scan(const uint64_t *__rest
     if (freed) atomicAdd(&s_cnt[0], 0ull - freed);        // (one live token less per release)
     if (dtomb) atomicAdd(&s_cnt[1], (unsigned long long)dtomb);
 
-    // this thread's composition, the wave's and the block's inclusive scan
+    // this thread's composition, the wave's and the block's inclusive scan; T' of the tile's first and
+    // last valid elements (the descriptor's rebasing)
     ConcSeg mine = cs_identity();
 #pragma unroll
     for (int q = 0; q < CS_ITEMS; ++q) {
         if (k[q] == invalid) continue;
         const bool head = k[q] != (q ? k[q - 1] : kprev);
         const int32_t v = x[q];
-        const ConcSeg el{(int64_t)v, v > 0 ? tp[q] : CONC_INF, head ? (uint32_t)(b + q) : CONC_NO_HEAD,
-                         (v > 1 || v < -1) ? 1u : 0u};
+        const ConcSeg el{(int64_t)v, v > 0 ? tp[q] : CONC_INF, head ? 1u : 0u, (v > 1 || v < -1) ? 1u : 0u};
         mine = cs_then(mine, el);
+        if ((q + 1 < CS_ITEMS ? k[q + 1] : knext) == invalid || (t == CS_THREADS - 1 && q == CS_ITEMS - 1))
+            s_tpl = tp[q];                                // the tile's last valid element
+    }
+    if (t == 0) {
+        s_tpf = tp[0];
+        s_lb = tile > 0 && k[0] != invalid && k[0] == kprev;    // the tile continues a segment
     }
     ConcSeg inc = mine;
 #pragma unroll
@@ -408,35 +440,32 @@ __global__ __launch_bounds__(CS_THREADS) void k_conc_scan(const uint64_t *__rest
     if (lane == 0) excl = cs_identity();
     excl = cs_then(wpre, excl);                           // the tile's positions before this thread's
 
-    // publish the tile's state; look back over earlier tiles (last wave, 64 tiles at a time, each lane
-    // waiting for one tile's flag; the window composed earliest first up to the nearest inclusive state)
-    const bool early = tile == 0 || tagg.head != CONC_NO_HEAD;          // inclusive without a prefix
-    if (t == CS_THREADS - 1) {
-        if (early) S.inc[tile] = tagg;
-        else S.agg[tile] = tagg;
-        __threadfence();
-        __hip_atomic_store(&S.flag[tile], (S.epoch << 2) | (early ? 2u : 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (tile > 0 && t >= CS_THREADS - WAVE) {
+    // publish the tile's descriptor: inclusive at once unless the tile continues a segment with no head
+    // of its own; such a tile looks back over earlier tiles (last wave, 64 tiles at a time, waiting only
+    // for the tiles up to the nearest inclusive descriptor, composed earliest first)
+    const bool lb = s_lb;
+    const bool early = !lb || tagg.hd;
+    const int64_t tpl = s_tpl, tpf = s_tpf;
+    if (t == CS_THREADS - 1)
+        __hip_atomic_store(&S.desc[tile], cs_pack(tagg, tpl, early ? 2u : 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lb && t >= CS_THREADS - WAVE) {
         ConcSeg pre = cs_identity();                      // tiles between the window and this one
         int64_t top = tile;                               // the window ends below top
         for (;;) {
             const int64_t p = top - 1 - (int64_t)lane;    // lane 0: the nearest tile
             // (a position before tile 0 reads as an inclusive identity)
-            const uint32_t f = p >= 0 ? __hip_atomic_load(&S.flag[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                      : ((S.epoch << 2) | 2u);
-            const bool ready = (f >> 2) == S.epoch && (f & 3u) != 0;
-            const uint64_t incl = __builtin_amdgcn_ballot_w64(ready && (f & 3u) == 2u);
-            const uint64_t waiting = __builtin_amdgcn_ballot_w64(!ready);
-            const int first = incl ? __ffsll((unsigned long long)incl) - 1 : WAVE;   // the nearest inclusive state
+            const uint64_t f = p >= 0 ? __hip_atomic_load(&S.desc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : (2ull | 1ull << 4);
+            const uint64_t st = f & 3u;
+            const uint64_t incl = __builtin_amdgcn_ballot_w64(st == 2u);
+            const uint64_t waiting = __builtin_amdgcn_ballot_w64(st == 0u);
+            const int first = incl ? __ffsll((unsigned long long)incl) - 1 : WAVE;   // the nearest inclusive one
             const uint64_t need = first >= WAVE - 1 ? ~0ull : ((2ull << first) - 1);
-            if (waiting & need) {                         // wait only for the tiles up to it
+            if (waiting & need) {
                 __builtin_amdgcn_s_sleep(1);
                 continue;
             }
-            __threadfence();
-            ConcSeg v = cs_identity();
-            if (p >= 0 && (int)lane <= first) v = (f & 3u) == 2u ? S.inc[p] : S.agg[p];
+            const ConcSeg v = (int)lane <= first ? cs_unpack(f, tpf) : cs_identity();
             ConcSeg w = cs_identity();                    // lanes min(first, 63) .. 0, earliest first
             for (int l = min(first, WAVE - 1); l >= 0; --l) w = cs_then(w, cs_shfl(v, l));
             pre = cs_then(w, pre);
@@ -445,11 +474,9 @@ __global__ __launch_bounds__(CS_THREADS) void k_conc_scan(const uint64_t *__rest
         }
         if (t == CS_THREADS - 1) {
             s_prefix = pre;
-            if (!early) {
-                S.inc[tile] = cs_then(pre, tagg);
-                __threadfence();
-                __hip_atomic_store(&S.flag[tile], (S.epoch << 2) | 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            if (!early)
+                __hip_atomic_store(&S.desc[tile], cs_pack(cs_then(pre, tagg), tpl, 2u), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     __syncthreads();
@@ -459,9 +486,9 @@ __global__ __launch_bounds__(CS_THREADS) void k_conc_scan(const uint64_t *__rest
     }
     const ConcSeg E = cs_then(s_prefix, excl);            // the sorted positions before this thread's
 
-    // decide: y = nowCalls before each position (y0 = nowCalls before the batch at a segment head)
+    // decide: y = nowCalls before each position (nowCalls before the batch at a segment head)
     int64_t y = 0, n0 = 0;
-    uint32_t hd = E.head, nu = E.nu;
+    uint32_t nu = E.nu;
     bool started = false;
 #pragma unroll
     for (int q = 0; q < CS_ITEMS; ++q) {
@@ -472,7 +499,6 @@ __global__ __launch_bounds__(CS_THREADS) void k_conc_scan(const uint64_t *__rest
             n0 = now_calls[k[q]];
             if (head) {
                 y = n0;
-                hd = (uint32_t)i;
                 nu = 0;
             } else {
                 y = mp_apply(MinPlus{E.p, E.c}, n0);
@@ -489,25 +515,33 @@ __global__ __launch_bounds__(CS_THREADS) void k_conc_scan(const uint64_t *__rest
             y += v;
         }
         if ((q + 1 < CS_ITEMS ? k[q + 1] : knext) != k[q]) {                 // the segment's last position
-            const int64_t len = i - (int64_t)hd + 1;
-            if (!nu && n0 <= tp[q] && (n0 < 0 ? -n0 : n0) + len < (int64_t)INT32_MAX) {
+            // exact while every amount is +-1, nowCalls starts at or below T' and cannot wrap an int
+            if (!nu && n0 <= tp[q] && (n0 < 0 ? -n0 : n0) + n < (int64_t)INT32_MAX) {
                 S.fin[k[q]] = (int32_t)y;
             } else {
-                S.serial[atomicAdd(&S.ctl[1], 1u)] = hd;
+                S.serial[atomicAdd(&S.ctl[1], 1u)] = (uint32_t)i;
             }
         }
     }
 }
 
 // Segments the scan cannot decide: one thread walks each with the CCFC:57-98 recurrence (integer work
-// on the elements only; amounts other than 1 and nowCalls above T' are rare).
+// on the elements only; amounts other than 1 and nowCalls above T' are rare).  The list holds the
+// segments' last positions; the first is found by a binary search of the sorted keys.
 __global__ __launch_bounds__(256) void k_conc_serial(const uint32_t *__restrict__ skey, int64_t n,
                                                      const int32_t *__restrict__ now_calls,
                                                      const double *__restrict__ thr, ConcElems X, ConcScan S) {
     const uint32_t cnt = S.ctl[1];
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < cnt; r += gridDim.x * blockDim.x) {
-        const int64_t b = S.serial[r];
-        const uint32_t flow = skey[b];
+        const int64_t last = S.serial[r];
+        const uint32_t flow = skey[last];
+        int64_t lo = 0, hi = last;                        // the first position whose key is `flow`
+        while (lo < hi) {
+            const int64_t m = (lo + hi) >> 1;
+            if (skey[m] < flow) lo = m + 1;
+            else hi = m;
+        }
+        const int64_t b = lo;
         int32_t now = now_calls[flow];
         const double threshold = thr[flow];
         for (int64_t i0 = b;; i0 += 8) {

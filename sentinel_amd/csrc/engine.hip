@@ -671,9 +671,8 @@ struct sentinel_engine {
     // concurrency tokens (ConcurrentClusterFlowChecker): nowCalls per flow, token cache in HBM
     DevBuf d_now, d_conc_thr, d_seg1_w, d_seg1_rcp, d_seg1_kind;
     DevBuf d_tok_rec, d_tok_counts, d_tok_ticket;   // token cache: one TokRec per slot (concurrent.hpp)
-    DevBuf w_cbig;                     // concurrency scan: tile states, fallback list, nowCalls (flags zeroed on allocation)
+    DevBuf w_cbig;                     // concurrency scan: tile descriptors, fallback list, nowCalls after the batch
     int64_t cbig_n = 0;                // its bytes
-    uint32_t conc_epoch = 0;
     uint64_t tok_ub = 0;               // upper bound of live + tombstoned token slots (no device read per batch)
     uint64_t tcap = (uint64_t)1 << 22;
     uint64_t tok_salt = 0, tok_counter = 1;
@@ -3794,33 +3793,27 @@ static int submit_concurrent(sentinel_engine_t *e, int64_t n, const ConcEvent *d
     uint64_t *aux = e->w_hep.as<uint64_t>();                  // per valid event: amount / released slot
     const int64_t nb = sort_blocks(n);
     const TokenTable TT = e->token_table();
+    // scan tiles' look-back descriptors (zeroed by k_conc_prep), fallback list, nowCalls after the batch
+    const int64_t nt = (n + CS_TILE - 1) / CS_TILE, segs = std::min<int64_t>(n, std::max<int32_t>(F, 1));
+    auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
+    const int64_t o_desc = 0, o_ser = o_desc + al(nt * 8), o_fin = o_ser + al(segs * 4), o_end = o_fin + al((int64_t)F * 4 + 4);
+    if (o_end > e->cbig_n) {
+        e->w_cbig.release();
+        if (e->w_cbig.ensure((size_t)o_end)) return SENTINEL_E_NOMEM;
+        e->cbig_n = o_end;
+    }
+    char *gb = e->w_cbig.as<char>();
+    uint32_t *ctl = e->w_counters.as<uint32_t>();               // [0] tile ticket, [1] fallback segments
+    const ConcScan S{(unsigned long long *)(gb + o_desc), ctl, (uint32_t *)(gb + o_ser), (int32_t *)(gb + o_fin)};
     e->launch("conc_prep", n, s, [&] {
         k_conc_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(n, dev, F, TT, dout, fkey, finvalid,
-                                                                      e->w_fhist.as<uint32_t>(), nb, aux);
+                                                                      e->w_fhist.as<uint32_t>(), nb, aux, S.desc, nt);
     });
     if (F > 0) {
         const EventSrc src{nullptr, (const ParamEvent *)dev, nullptr, false};
         e->sort(fkey, n, fbits, e->w_fhist.as<uint32_t>(), src, s);
         const uint32_t *skey = e->w_skey.as<uint32_t>();
         const uint64_t *sval = e->w_sval.as<uint64_t>();
-        uint32_t *ctl = e->w_counters.as<uint32_t>();           // [0] tile ticket, [1] fallback segments
-        // scan tiles (look-back flags, zeroed on allocation, and states), fallback list, nowCalls after the batch
-        const int64_t nt = (n + CS_TILE - 1) / CS_TILE, segs = std::min<int64_t>(n, F);
-        auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
-        const int64_t o_fl = 0, o_agg = o_fl + al(nt * 4), o_inc = o_agg + al(nt * (int64_t)sizeof(ConcSeg)),
-                      o_ser = o_inc + al(nt * (int64_t)sizeof(ConcSeg)), o_fin = o_ser + al(segs * 4),
-                      o_end = o_fin + al((int64_t)F * 4);
-        if (o_end > e->cbig_n) {
-            e->w_cbig.release();
-            if (e->w_cbig.ensure((size_t)o_end)) return SENTINEL_E_NOMEM;
-            HIP_OK(hipMemsetAsync(e->w_cbig.p, 0, (size_t)o_end, s));   // look-back flags of no epoch
-            e->cbig_n = o_end;
-        }
-        e->conc_epoch = (e->conc_epoch + 1) & 0x3FFFFFFFu;
-        if (e->conc_epoch == 0) e->conc_epoch = 1;
-        char *gb = e->w_cbig.as<char>();
-        const ConcScan S{(uint32_t *)(gb + o_fl), (ConcSeg *)(gb + o_agg), (ConcSeg *)(gb + o_inc), ctl,
-                         (uint32_t *)(gb + o_ser), (int32_t *)(gb + o_fin), e->conc_epoch};
         HIP_OK(hipMemsetAsync(ctl, 0, 8, s));
         const ConcElems X{e->w_hacq.as<int32_t>(), e->w_done.as<uint8_t>()};
         int32_t *now_calls = e->d_now.as<int32_t>();
