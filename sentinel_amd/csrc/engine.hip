@@ -1086,6 +1086,12 @@ struct sentinel_engine {
     int rewrite_tokens(bool compact, uint64_t new_cap = 0);
     int rebuild_tokens_device(uint64_t new_cap, hipStream_t s);
     DevBuf sp_tok_rec;                 // the next compaction's target
+    // getTopValues scratch (param_top), kept between calls: candidate list {key, rule, sum} + its count,
+    // per-rule selection state, the results and the rules' flowIds (grow-only: no allocation per snapshot)
+    struct TopScratch {
+        DevBuf ckey, crule, csum, cn, pr, pk, cr, ck, dc, dk, ds, ids, rank, fkey, frule, fsum;
+        std::vector<int64_t> h_ids;    // the flowIds in `ids` (uploaded again only when the rules change)
+    } topw;
     TokenTable token_table() {
         return TokenTable{d_tok_rec.as<TokRec>(), tcap - 1, d_tok_counts.as<unsigned long long>()};
     }
@@ -2440,6 +2446,10 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
     e->prof_collect();
     for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
     e->ft.release();
+    for (DevBuf *b : {&e->topw.ckey, &e->topw.crule, &e->topw.csum, &e->topw.cn, &e->topw.pr, &e->topw.pk, &e->topw.cr,
+                      &e->topw.ck, &e->topw.dc, &e->topw.dk, &e->topw.ds, &e->topw.ids, &e->topw.rank, &e->topw.fkey,
+                      &e->topw.frule, &e->topw.fsum})
+        b->release();
     e->lt.release();
     e->pt.release();
     for (DevBuf *b : {&e->d_flow_route, &e->d_flow_route8, &e->d_flow_ids, &e->d_prule_route, &e->d_prule_n, &e->d_prule_w,
@@ -4035,60 +4045,71 @@ int sentinel_param_sum(sentinel_engine_t *e, int32_t ridx, uint64_t pkey, int64_
 
 // getTopValues(number) of every param rule at ts into device arrays count[R], key[R][number], sum[R][number]
 // (param_table.hpp, k_ptop_*): number rounds of a per-rule selection over the live slots.
-static int param_top(sentinel_engine_t *e, int64_t ts, int32_t number, hipStream_t s, DevBuf &dcount, DevBuf &dkey,
-                     DevBuf &dsum) {
+static int param_top(sentinel_engine_t *e, int64_t ts, int32_t number, hipStream_t s) {
     const int32_t R = (int32_t)e->prules.size();
+    auto &W = e->topw;
     int rc = 0;
-    rc |= dcount.ensure((size_t)std::max(R, 1) * 4);
-    rc |= dkey.ensure((size_t)std::max(R, 1) * number * 8);
-    rc |= dsum.ensure((size_t)std::max(R, 1) * number * 8);
+    rc |= W.dc.ensure((size_t)std::max(R, 1) * 4);
+    rc |= W.dk.ensure((size_t)std::max(R, 1) * number * 8);
+    rc |= W.ds.ensure((size_t)std::max(R, 1) * number * 8);
     if (rc) return SENTINEL_E_NOMEM;
-    HIP_OK(hipMemsetAsync(dcount.p, 0, (size_t)std::max(R, 1) * 4, s));
+    HIP_OK(hipMemsetAsync(W.dc.p, 0, (size_t)std::max(R, 1) * 4, s));
     if (R == 0 || !e->d_ptable.p || e->pmode != SENTINEL_PARAM_EXACT) return 0;
     const uint64_t cap = e->pcap;
     // candidate list {key, rule, sum} (slots with a non-zero window sum at ts), sized for the live slots
     // (live after the last rebuild + the reserved upper bound of inserts since); a longer list than that
     // (never expected) reruns the selection with room for the whole table
     uint64_t mc = std::min<uint64_t>(cap, e->p_live + e->p_ub + 1);
-  again:
-    DevBuf ckey, crule, csum, cn, pr, pk, cr, ck;
-    rc |= ckey.ensure(mc * 8);
-    rc |= crule.ensure(mc * 4);
-    rc |= csum.ensure(mc * 8);
-    rc |= cn.ensure(8);
-    for (DevBuf *b : {&pr, &pk, &cr, &ck}) rc |= b->ensure((size_t)R * 8);
-    if (rc) return SENTINEL_E_NOMEM;
-    const PSlots T{e->d_ptable.as<unsigned long long>(), e->d_slot_rule.as<int32_t>(), e->pt.state.as<int64_t>(),
-                   param_stride(e->pmax_n), cap - 1};
-    const TopCands C{ckey.as<unsigned long long>(), crule.as<int32_t>(), csum.as<int64_t>(), cn.as<unsigned long long>(), mc};
-    HIP_OK(hipMemsetAsync(cn.p, 0, 8, s));
-    k_ptop_sums<<<grid_for((int64_t)cap), 256, 0, s>>>(T, cap, R, e->d_prule_n.as<int32_t>(), e->d_prule_w.as<int32_t>(),
-                                                       e->d_prule_rcp.as<double>(), ts, C);
-    HIP_OK(hipMemsetAsync(pr.p, 0, (size_t)R * 8, s));
-    HIP_OK(hipMemsetAsync(pk.p, 0, (size_t)R * 8, s));
-    HIP_OK(hipMemsetAsync(cr.p, 0, (size_t)R * 8, s));
-    HIP_OK(hipMemsetAsync(ck.p, 0xFF, (size_t)R * 8, s));
-    const unsigned g = (unsigned)std::min<uint64_t>(2048, (mc + 255) / 256);   // grid-stride over the candidates
-    for (int k = 0; k < number; ++k) {
-        k_ptop_best_sum<<<g, 256, 0, s>>>(C, pr.as<unsigned long long>(), pk.as<unsigned long long>(), cr.as<unsigned long long>());
-        k_ptop_best_key<<<g, 256, 0, s>>>(C, pr.as<unsigned long long>(), pk.as<unsigned long long>(),
-                                         cr.as<unsigned long long>(), ck.as<unsigned long long>());
-        k_ptop_take<<<g, 256, 0, s>>>(C, cr.as<unsigned long long>(), ck.as<unsigned long long>(), k, number,
-                                     dkey.as<uint64_t>(), dsum.as<int64_t>());
-        k_ptop_advance<<<grid_for(R), 256, 0, s>>>(R, pr.as<unsigned long long>(), pk.as<unsigned long long>(),
-                                                  cr.as<unsigned long long>(), ck.as<unsigned long long>(), dcount.as<int32_t>());
+    // finalists (candidates at or above their rule's number-th largest rank): a few per rule
+    const uint64_t fc = std::min<uint64_t>(mc, (uint64_t)R * (uint64_t)(4 * number) + 4096);
+    for (;;) {
+        rc |= W.ckey.ensure(mc * 8);
+        rc |= W.crule.ensure(mc * 4);
+        rc |= W.csum.ensure(mc * 8);
+        rc |= W.cn.ensure(16);
+        rc |= W.fkey.ensure(fc * 8);
+        rc |= W.frule.ensure(fc * 4);
+        rc |= W.fsum.ensure(fc * 8);
+        rc |= W.rank.ensure((size_t)R * number * 8);
+        for (DevBuf *b : {&W.pr, &W.pk, &W.cr, &W.ck}) rc |= b->ensure((size_t)R * 8);
+        if (rc) return SENTINEL_E_NOMEM;
+        unsigned long long *pr = W.pr.as<unsigned long long>(), *pk = W.pk.as<unsigned long long>(),
+                           *cr = W.cr.as<unsigned long long>(), *ck = W.ck.as<unsigned long long>();
+        unsigned long long *cn = W.cn.as<unsigned long long>();
+        const PSlots T{e->d_ptable.as<unsigned long long>(), e->d_slot_rule.as<int32_t>(), e->pt.state.as<int64_t>(),
+                       param_stride(e->pmax_n), cap - 1};
+        const TopCands C{W.ckey.as<unsigned long long>(), W.crule.as<int32_t>(), W.csum.as<int64_t>(), cn, mc};
+        const TopCands F{W.fkey.as<unsigned long long>(), W.frule.as<int32_t>(), W.fsum.as<int64_t>(), cn + 1, fc};
+        HIP_OK(hipMemsetAsync(cn, 0, 16, s));
+        HIP_OK(hipMemsetAsync(W.rank.p, 0, (size_t)R * number * 8, s));
+        k_ptop_sums<<<grid_for((int64_t)cap), 256, 0, s>>>(T, cap, R, e->d_prule_n.as<int32_t>(), e->d_prule_w.as<int32_t>(),
+                                                           e->d_prule_rcp.as<double>(), ts, C,
+                                                           W.rank.as<unsigned long long>(), number);
+        const unsigned gc = (unsigned)std::min<uint64_t>(2048, (mc + 255) / 256);
+        k_ptop_final<<<gc, 256, 0, s>>>(C, W.rank.as<unsigned long long>(), number, F);
+        unsigned long long found[2] = {0, 0};
+        HIP_OK(hipMemcpyAsync(found, cn, 16, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipStreamSynchronize(s));
+        if (found[0] > mc && mc < cap) {             // (never expected) room for the whole table
+            mc = cap;
+            continue;
+        }
+        const TopCands &L = found[1] <= fc ? F : C;  // rounds over the finalists (the whole list if they overflow)
+        HIP_OK(hipMemsetAsync(pr, 0, (size_t)R * 8, s));
+        HIP_OK(hipMemsetAsync(pk, 0, (size_t)R * 8, s));
+        HIP_OK(hipMemsetAsync(cr, 0, (size_t)R * 8, s));
+        HIP_OK(hipMemsetAsync(ck, 0xFF, (size_t)R * 8, s));
+        const uint64_t ln = std::min<uint64_t>(found[1] <= fc ? found[1] : found[0], L.cap);
+        const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(2048, (ln + 255) / 256));
+        for (int k = 0; k < number; ++k) {
+            k_ptop_best_sum<<<g, 256, 0, s>>>(L, pr, pk, cr);
+            k_ptop_best_key<<<g, 256, 0, s>>>(L, pr, pk, cr, ck);
+            k_ptop_take<<<g, 256, 0, s>>>(L, cr, ck, k, number, W.dk.as<uint64_t>(), W.ds.as<int64_t>());
+            k_ptop_advance<<<grid_for(R), 256, 0, s>>>(R, pr, pk, cr, ck, W.dc.as<int32_t>());
+        }
+        HIP_OK(hipGetLastError());
+        return 0;
     }
-    HIP_OK(hipGetLastError());
-    unsigned long long found = 0;
-    HIP_OK(hipMemcpyAsync(&found, cn.p, 8, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));        // the temporaries are freed below
-    for (DevBuf *b : {&ckey, &crule, &csum, &cn, &pr, &pk, &cr, &ck}) b->release();
-    if (found > mc && mc < cap) {
-        mc = cap;
-        HIP_OK(hipMemsetAsync(dcount.p, 0, (size_t)std::max(R, 1) * 4, s));
-        goto again;
-    }
-    return 0;
 }
 
 int sentinel_param_top_values(sentinel_engine_t *e, int64_t ts, int32_t number, int32_t *count, uint64_t *keys,
@@ -4098,14 +4119,13 @@ int sentinel_param_top_values(sentinel_engine_t *e, int64_t ts, int32_t number, 
     HIP_OK(hipSetDevice(e->device));
     HIP_OK(hipStreamSynchronize(e->stream));
     const int32_t R = (int32_t)e->prules.size();
-    DevBuf dc, dk, ds;
-    int rc = param_top(e, ts, number, e->stream, dc, dk, ds);
+    int rc = param_top(e, ts, number, e->stream);
     if (rc) return rc;
     std::vector<int64_t> sum((size_t)R * number);
     if (R > 0) {
-        HIP_OK(hipMemcpy(count, dc.p, (size_t)R * 4, hipMemcpyDeviceToHost));
-        HIP_OK(hipMemcpy(keys, dk.p, (size_t)R * number * 8, hipMemcpyDeviceToHost));
-        HIP_OK(hipMemcpy(sum.data(), ds.p, (size_t)R * number * 8, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(count, e->topw.dc.p, (size_t)R * 4, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(keys, e->topw.dk.p, (size_t)R * number * 8, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(sum.data(), e->topw.ds.p, (size_t)R * number * 8, hipMemcpyDeviceToHost));
     }
     for (int32_t r = 0; r < R; ++r) {
         const double I_s = e->h_prule_interval[r] / 1000.0;
@@ -4147,15 +4167,18 @@ int sentinel_param_snapshot_device(sentinel_engine_t *e, int64_t ts, sentinel_pa
     hipStream_t s = stream ? (hipStream_t)stream : e->stream;
     const ForeignStream fs_(e, s);
     if (s != e->stream) HIP_OK(hipStreamSynchronize(e->stream));
-    DevBuf dc, dk, ds, ids;
-    int rc = param_top(e, ts, SENTINEL_TOP_PARAMS, s, dc, dk, ds);
+    auto &W = e->topw;
+    int rc = param_top(e, ts, SENTINEL_TOP_PARAMS, s);
     if (rc) return rc;
     std::vector<int64_t> fid(R);
     for (int32_t r = 0; r < R; ++r) fid[r] = e->prules[r].flow_id;
-    rc = upload(ids, fid);
-    if (rc) return rc;
-    k_ptop_records<<<grid_for(R), 256, 0, s>>>(R, ids.as<int64_t>(), dc.as<int32_t>(), dk.as<uint64_t>(), ds.as<int64_t>(),
-                                              e->d_prule_Is.as<double>(), d_out);
+    if (fid != W.h_ids || !W.ids.p) {
+        rc = upload(W.ids, fid);
+        if (rc) return rc;
+        W.h_ids.swap(fid);
+    }
+    k_ptop_records<<<grid_for(R), 256, 0, s>>>(R, W.ids.as<int64_t>(), W.dc.as<int32_t>(), W.dk.as<uint64_t>(),
+                                              W.ds.as<int64_t>(), e->d_prule_Is.as<double>(), d_out);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(s));
     return 0;

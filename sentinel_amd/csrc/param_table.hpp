@@ -154,41 +154,120 @@ struct TopCands {
     unsigned long long cap;
 };
 
+__device__ inline uint64_t top_rank(int64_t v) { return ((uint64_t)1 << 32) | ((uint32_t)(int32_t)v ^ 0x80000000u); }
+
+// Per rule the `number` largest ranks with multiplicity (0 = none), by an atomicMax cascade: a slot
+// keeps the larger of its value and the incoming one and passes the smaller on, so slot j ends with the
+// (j+1)-th largest rank of everything inserted.  A rank at or below the rule's last slot cannot change
+// the multiset (a stale read of that slot is lower, so the test never skips a rank that belongs).
+__device__ inline void top_cascade(unsigned long long *top, int number, unsigned long long v) {
+    if (v <= top[number - 1]) return;
+    for (int j = 0; j < number && v; ++j) {
+        const unsigned long long o = atomicMax(&top[j], v);
+        v = o < v ? o : v;
+    }
+}
+
+// One wave per 64 consecutive slots.  A slot's {epoch, count} pairs lie in one contiguous run of the
+// state region, so its window sum is read by a 16-lane group (lane j loads pair j, one 16-B load, then a
+// 16-lane reduction): the wave's live slots go through four at a time, each load instruction reading
+// four contiguous runs instead of 64 scattered ones.
 __global__ __launch_bounds__(256) void k_ptop_sums(PSlots T, uint64_t cap, int32_t R, const int32_t *__restrict__ rn,
                                                    const int32_t *__restrict__ rw, const double *__restrict__ rrcp,
-                                                   int64_t ts, TopCands C) {
-    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    int64_t v = 0;
+                                                   int64_t ts, TopCands C, unsigned long long *__restrict__ toprank,
+                                                   int number) {
+    const uint32_t lane = lane_id();
+    const uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~(uint32_t)(WAVE - 1));
+    const uint64_t s = base + lane;
     unsigned long long key = PKEY_EMPTY;
-    int32_t r = 0;
+    int32_t r = -1;
     if (s < cap) key = T.keys[s];
-    if (key != PKEY_EMPTY && (uint32_t)(r = T.rule[s]) < (uint32_t)R) {   // sum 0: not a candidate
-        const int n = rn[r];
-        const int64_t E = epoch_of(ts, rw[r], rrcp[r]);
-        const int64_t *st = T.state + (int64_t)s * T.stride;
-        for (int j = 0; j < n; ++j)
-            if (st[2 * j] != EPOCH_ABSENT && st[2 * j] > E - n) v = wrap_add(v, st[2 * j + 1]);
+    if (key != PKEY_EMPTY) {
+        r = T.rule[s];
+        if ((uint32_t)r >= (uint32_t)R) r = -1;
     }
+    uint64_t live = __builtin_amdgcn_ballot_w64(r >= 0);
+    const int grp = (int)(lane >> 4), j = (int)(lane & 15);
+    uint64_t v = 0;                                       // this lane's slot's sum (wrapping, like wrap_add)
+    while (live) {
+        int pos[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            pos[q] = live ? __ffsll((unsigned long long)live) - 1 : -1;
+            live &= live ? live - 1 : 0;
+        }
+        const int p = pos[grp];
+        const int32_t rg = __shfl(r, p < 0 ? 0 : p, WAVE);
+        uint64_t part = 0;
+        if (p >= 0) {
+            const int n = rn[rg];
+            if (j < n) {
+                const int64_t E = epoch_of(ts, rw[rg], rrcp[rg]);
+                const longlong2 b = ((const longlong2 *)(T.state + (int64_t)(base + p) * T.stride))[j];
+                if (b.x != EPOCH_ABSENT && b.x > E - n) part = (uint64_t)b.y;
+            }
+        }
+#pragma unroll
+        for (int o = 8; o >= 1; o >>= 1) part += __shfl_xor(part, o, WAVE);     // within the 16-lane group
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint64_t g = __shfl(part, q * 16, WAVE);
+            if ((int)lane == pos[q]) v = g;
+        }
+    }
+#ifndef SENTINEL_TOP_NOCASCADE
+    if (v != 0) top_cascade(toprank + (int64_t)r * number, number, top_rank((int64_t)v));
+#endif
     const uint64_t act = __builtin_amdgcn_ballot_w64(v != 0);
     if (!act) return;
-    const uint32_t lane = lane_id();
     const int first = __ffsll((unsigned long long)act) - 1;
-    unsigned long long base = 0;
-    if ((int)lane == first) base = atomicAdd(C.n, (unsigned long long)__popcll(act));
-    base = __shfl(base, first, WAVE);
-    const unsigned long long k = base + (unsigned long long)__popcll(act & ((1ull << lane) - 1ull));
+    unsigned long long cb = 0;
+    if ((int)lane == first) cb = atomicAdd(C.n, (unsigned long long)__popcll(act));
+    cb = __shfl(cb, first, WAVE);
+    const unsigned long long k = cb + (unsigned long long)__popcll(act & ((1ull << lane) - 1ull));
     if (v != 0 && k < C.cap) {
         C.key[k] = key;
         C.rule[k] = r;
-        C.sum[k] = v;
+        C.sum[k] = (int64_t)v;
     }
 }
 
 // Order (int) sum descending, key ascending; `prev` = the rule's previous pick (none in round 0).
-__device__ inline uint64_t top_rank(int64_t v) { return ((uint64_t)1 << 32) | ((uint32_t)(int32_t)v ^ 0x80000000u); }
 
 __device__ inline bool top_after(uint64_t rk, uint64_t key, uint64_t prk, uint64_t pkey) {
     return prk == 0 || rk < prk || (rk == prk && key > pkey);
+}
+
+// The finalists: candidates ranked at or above their rule's number-th largest rank (every other
+// candidate has `number` better ones), appended to a short list F the selection rounds then run over
+// (ties at that rank are kept, so the key order among them is decided by the rounds as before).
+__global__ __launch_bounds__(256) void k_ptop_final(TopCands C, const unsigned long long *__restrict__ toprank, int number,
+                                                    TopCands F) {
+    const unsigned long long m = *C.n < C.cap ? *C.n : C.cap;
+    for (unsigned long long k0 = (uint64_t)blockIdx.x * blockDim.x; k0 < m; k0 += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned long long k = k0 + threadIdx.x;
+        bool fin = false;
+        int32_t r = 0;
+        int64_t v = 0;
+        if (k < m) {
+            r = C.rule[k];
+            v = C.sum[k];
+            fin = top_rank(v) >= toprank[(int64_t)r * number + number - 1];
+        }
+        const uint64_t act = __builtin_amdgcn_ballot_w64(fin);
+        if (!act) continue;
+        const uint32_t lane = lane_id();
+        const int first = __ffsll((unsigned long long)act) - 1;
+        unsigned long long base = 0;
+        if ((int)lane == first) base = atomicAdd(F.n, (unsigned long long)__popcll(act));
+        base = __shfl(base, first, WAVE);
+        const unsigned long long j = base + (unsigned long long)__popcll(act & ((1ull << lane) - 1ull));
+        if (fin && j < F.cap) {
+            F.key[j] = C.key[k];
+            F.rule[j] = r;
+            F.sum[j] = v;
+        }
+    }
 }
 
 // Round phase A: best (int) sum among the candidates after the previous pick.
