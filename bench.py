@@ -586,9 +586,10 @@ class ConcWorkload:
 
     def bytes_of(self, dom, d, steps):
         if dom == "conc_scan":
-            # per event: sorted key 4 + value 8 read, the 8-B aux word gathered, element 4 written (+ pass
-            # byte per acquire); per release (half the events) its 32-B token record read and written back
-            return 4 + 8 + 8 + 4 + 0.5 * 1 + 0.5 * (32 + 32)
+            # per event: sorted key 4 + value 8 read (the value carries the amount / token slot), element
+            # 4 written (+ pass byte per acquire); per release (half the events) its 32-B token record read
+            # and written back
+            return 4 + 8 + 4 + 0.5 * 1 + 0.5 * (32 + 32)
         if dom == "radix_scatter":
             passes = max(1, round(d["calls"] / max(1, steps)))
             return (32.0 + 24.0 * (passes - 1)) / passes

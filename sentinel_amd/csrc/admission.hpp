@@ -87,6 +87,7 @@ struct EventSrc {
     const ParamEvent *pev;
     const uint8_t *flags;    // may be null
     bool unit_acquire;       // limiter: acquire == 1 for every request
+    const uint64_t *vals = nullptr;   // precomputed sorted values by arrival position (concurrency tokens)
 
     __device__ inline void load(uint32_t s, int64_t &ts, int32_t &a, uint8_t &fl) const {
         if (ev) { const Event e = ev[s]; ts = e.ts; a = e.acquire; }
@@ -99,6 +100,7 @@ struct EventSrc {
 
     // Sorted value of arrival position s (layout above).
     __device__ inline uint64_t pack(uint32_t s, int64_t T0) const {
+        if (vals) return vals[s];
         int64_t t;
         int32_t a;
         uint8_t fl;

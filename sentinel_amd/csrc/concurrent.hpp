@@ -120,8 +120,14 @@ __device__ inline void put_conc(uint64_t *out, uint32_t i, int64_t token, int st
     out[2 * (uint64_t)i + 1] = (uint64_t)(uint32_t)status;
 }
 
-// Per valid event, by arrival position: an acquire's amount, or AUX_RELEASE | the released token's slot.
-constexpr uint64_t AUX_RELEASE = 1ull << 63;
+// The sorted value of an event (written by k_conc_prep by arrival position, moved by the sort): the
+// arrival position (SEQ_MASK bits), a release bit, and an acquire's amount or the released token's slot
+// (35 bits: the token cache stays below 2^32 slots), so the scan reads everything from its sorted values.
+constexpr int CV_REL_BIT = 28;
+constexpr int CV_PAY_SHIFT = 29;
+__device__ inline uint64_t conc_value(uint32_t seq, bool release, uint64_t payload) {
+    return (uint64_t)seq | (uint64_t)(release ? 1 : 0) << CV_REL_BIT | payload << CV_PAY_SHIFT;
+}
 
 // DefaultTokenService.requestConcurrentToken validation (DTS:64-75, 89-91) and release lookup;
 // sort key = flow index (acquire: the rule; release: the token's flow); pass-0 histograms.  A found
@@ -146,12 +152,13 @@ __global__ __launch_bounds__(SORT_THREADS) void k_conc_prep(int64_t n, const Con
         const ConcEvent e = ev[i];
         int st = 127;
         uint32_t k = finvalid;
+        uint64_t cv = conc_value((uint32_t)i, false, 0);
         if (e.kind == CONC_ACQUIRE) {
             if (!(e.flags & 1) || e.idx == SENTINEL_IDX_BAD_ID || e.acquire <= 0) st = ST_BAD_REQUEST;
             else if (e.idx < 0 || e.idx >= nflows) st = ST_NO_RULE_EXISTS;
             else {
                 k = (uint32_t)e.idx;
-                aux[i] = (uint64_t)(uint32_t)e.acquire;                     // an acquire: its amount (> 0)
+                cv = conc_value((uint32_t)i, false, (uint32_t)e.acquire);   // an acquire: its amount (> 0)
             }
         } else if (e.kind == CONC_RELEASE) {
             const int64_t h = token_find(TT, (uint64_t)e.token);             // CCFC:82-86
@@ -159,13 +166,14 @@ __global__ __launch_bounds__(SORT_THREADS) void k_conc_prep(int64_t n, const Con
             else if (TT.rec[h].flow_idx < 0) st = ST_NO_RULE_EXISTS;         // CCFC:87-91
             else {
                 k = (uint32_t)TT.rec[h].flow_idx;
-                aux[i] = AUX_RELEASE | (uint64_t)h;                          // a release: its token's slot
+                cv = conc_value((uint32_t)i, true, (uint64_t)h);             // a release: its token's slot
                 atomicMin(&TT.rec[h].claim, (uint32_t)i);
             }
         } else {
             st = ST_BAD_REQUEST;
         }
         fkey[i] = k;
+        aux[i] = cv;
         tile_hist_accumulate(hf, k, 1);
         if (st != 127) put_conc(out, (uint32_t)i, 0, st);
     }
@@ -345,7 +353,7 @@ __device__ inline void token_free(const TokenTable &TT, uint32_t h, TokRec r, in
 // (freeing the claimed releases' slots), scans them, looks back for the state before the tile and
 // decides its acquires; a segment's last position stores nowCalls after the batch, or hands the segment
 // to k_conc_serial.
-__global__ __launch_bounds__(CS_THREADS) void k_conc_scan(const uint64_t *__restrict__ aux, const uint64_t *__restrict__ sval,
+__global__ __launch_bounds__(CS_THREADS) void k_conc_scan(const uint64_t *__restrict__ sval,
                                                           const uint32_t *__restrict__ skey, uint32_t invalid, int64_t n,
                                                           TokenTable TT, const double *__restrict__ thr,
                                                           const int32_t *__restrict__ now_calls, ConcElems X, ConcScan S) {
@@ -383,12 +391,12 @@ __global__ __launch_bounds__(CS_THREADS) void k_conc_scan(const uint64_t *__rest
         x[q] = 0;
         tp[q] = 0;
         if (k[q] == invalid) continue;
-        const uint32_t seq = (uint32_t)sval[b + q] & SEQ_MASK;
-        const uint64_t a = aux[seq];
-        if (!(a & AUX_RELEASE)) {
-            x[q] = (int32_t)a;                            // an acquire: > 0 (validated)
+        const uint64_t w = sval[b + q];
+        const uint32_t seq = (uint32_t)w & SEQ_MASK;
+        if (!((w >> CV_REL_BIT) & 1)) {
+            x[q] = (int32_t)(w >> CV_PAY_SHIFT);          // an acquire: > 0 (validated)
         } else {
-            const uint32_t h = (uint32_t)a;
+            const uint32_t h = (uint32_t)(w >> CV_PAY_SHIFT);
             const TokRec r = TT.rec[h];                   // claim and amount: one line
             if (r.claim == seq) {                         // CCFC:82-86: this release finds its token
                 x[q] = -r.acquire;

@@ -3800,7 +3800,7 @@ static int submit_concurrent(sentinel_engine_t *e, int64_t n, const ConcEvent *d
     const int fbits = bits_for(F);
     const uint32_t finvalid = ((uint32_t)1 << fbits) - 1;
     uint32_t *fkey = e->w_fkey.as<uint32_t>();
-    uint64_t *aux = e->w_hep.as<uint64_t>();                  // per valid event: amount / released slot
+    uint64_t *aux = e->w_hep.as<uint64_t>();                  // sorted values by arrival position (conc_value)
     const int64_t nb = sort_blocks(n);
     const TokenTable TT = e->token_table();
     // scan tiles' look-back descriptors (zeroed by k_conc_prep), fallback list, nowCalls after the batch
@@ -3820,7 +3820,7 @@ static int submit_concurrent(sentinel_engine_t *e, int64_t n, const ConcEvent *d
                                                                       e->w_fhist.as<uint32_t>(), nb, aux, S.desc, nt);
     });
     if (F > 0) {
-        const EventSrc src{nullptr, (const ParamEvent *)dev, nullptr, false};
+        const EventSrc src{nullptr, (const ParamEvent *)dev, nullptr, false, aux};
         e->sort(fkey, n, fbits, e->w_fhist.as<uint32_t>(), src, s);
         const uint32_t *skey = e->w_skey.as<uint32_t>();
         const uint64_t *sval = e->w_sval.as<uint64_t>();
@@ -3829,7 +3829,7 @@ static int submit_concurrent(sentinel_engine_t *e, int64_t n, const ConcEvent *d
         int32_t *now_calls = e->d_now.as<int32_t>();
         const double *thr = e->d_conc_thr.as<double>();
         e->launch("conc_scan", n, s, [&] {
-            k_conc_scan<<<(unsigned)nt, CS_THREADS, 0, s>>>(aux, sval, skey, finvalid, n, TT, thr, now_calls, X, S);
+            k_conc_scan<<<(unsigned)nt, CS_THREADS, 0, s>>>(sval, skey, finvalid, n, TT, thr, now_calls, X, S);
         });
         e->launch("conc_serial", n, s, [&] {
             k_conc_serial<<<grid_for(segs), 256, 0, s>>>(skey, n, now_calls, thr, X, S);
