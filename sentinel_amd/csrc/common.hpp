@@ -72,6 +72,16 @@ __host__ __device__ inline int64_t java_d2l(double d) {
 
 constexpr uint64_t PKEY_EMPTY = 0xFFFFFFFFFFFFFFFFull;   // reserved param key (empty table slot)
 
+// Batch counters that many workgroups add to (fresh inserts): one atomic per workgroup on a single
+// address queues every workgroup of a launch at one memory channel, so the counter is striped over
+// CNT_LANES lines by workgroup index and its readers sum the lanes (k_pfresh_publish, the engine).
+constexpr int CNT_LANES = 64;
+constexpr int CNT_STRIDE = 16;                                  // 128 B apart
+constexpr size_t CNT_BYTES = (size_t)CNT_LANES * CNT_STRIDE * 8;
+__device__ inline unsigned long long *cnt_lane(unsigned long long *c) {
+    return c + (blockIdx.x & (CNT_LANES - 1)) * CNT_STRIDE;
+}
+
 // Find or insert `key` in an open-addressing table of 2^k slots; returns the slot or -1 (full).
 // `fresh` (optional) counts the keys this call inserted.
 __device__ inline int64_t slot_insert(unsigned long long *table, uint64_t mask, uint64_t key,
@@ -86,7 +96,7 @@ __device__ inline int64_t slot_insert(unsigned long long *table, uint64_t mask, 
         if (cur == PKEY_EMPTY) {
             const unsigned long long prev = atomicCAS(&table[h], (unsigned long long)PKEY_EMPTY, (unsigned long long)key);
             if (prev == PKEY_EMPTY) {
-                if (fresh) atomicAdd(fresh, 1ull);
+                if (fresh) atomicAdd(cnt_lane(fresh), 1ull);
                 return (int64_t)h;
             }
             if (prev == key) return (int64_t)h;
@@ -137,7 +147,7 @@ __device__ inline int64_t slot_insert_counted(unsigned long long *table, uint64_
 __device__ inline void block_add_global(unsigned long long *global, uint32_t mine, uint32_t *lds) {
     if (mine) atomicAdd(lds, mine);
     __syncthreads();
-    if (threadIdx.x == 0 && *lds && global) atomicAdd(global, (unsigned long long)*lds);
+    if (threadIdx.x == 0 && *lds && global) atomicAdd(cnt_lane(global), (unsigned long long)*lds);
 }
 
 // Read-only lookup; returns the slot or -1.

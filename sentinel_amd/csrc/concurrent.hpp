@@ -53,13 +53,13 @@ struct TokenTable {
 };
 
 // The cache counts are updated by one atomic pair per workgroup; many workgroups adding to one address
-// queue at one memory channel (16K of them cost a batch ~60 us), so the pair is striped over
-// TOK_CNT_LANES lines by workgroup index and summed by the host when it needs them.
-constexpr int TOK_CNT_LANES = 64;
-constexpr int TOK_CNT_STRIDE = 16;                              // 128 B apart
-constexpr size_t TOK_CNT_BYTES = (size_t)TOK_CNT_LANES * TOK_CNT_STRIDE * 8;
+// queue at one memory channel (16K of them cost a batch ~60 us), so the pair is striped like the other
+// batch counters (common.hpp, cnt_lane) and summed by the host when it needs them.
+constexpr int TOK_CNT_LANES = CNT_LANES;
+constexpr int TOK_CNT_STRIDE = CNT_STRIDE;
+constexpr size_t TOK_CNT_BYTES = CNT_BYTES;
 __device__ inline void tok_count_add(const TokenTable &T, int which, unsigned long long v) {
-    atomicAdd(&T.counts[(blockIdx.x & (TOK_CNT_LANES - 1)) * TOK_CNT_STRIDE + which], v);
+    atomicAdd(cnt_lane(T.counts) + which, v);
 }
 
 __device__ inline int64_t token_find(const TokenTable &T, uint64_t id) {

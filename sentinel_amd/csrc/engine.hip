@@ -1202,7 +1202,7 @@ int sentinel_engine::clear_param_slots() {
     const uint64_t P = pcap;
     const int64_t stride = param_stride(pmax_n);
     HIP_OK(hipMemsetAsync(d_ptable.p, 0xFF, P * 8, stream));
-    HIP_OK(hipMemsetAsync(d_pfresh.p, 0, 8, stream));
+    HIP_OK(hipMemsetAsync(d_pfresh.p, 0, CNT_BYTES, stream));
     k_init_state<<<grid_for((int64_t)P), 256, 0, stream>>>(pt.state.as<int64_t>(), nullptr, stride, nullptr, pmax_n,
                                                            stride, (int64_t)P);
     HIP_OK(hipStreamSynchronize(stream));
@@ -1312,8 +1312,8 @@ int sentinel_engine::param_rebuild(uint64_t new_cap, const std::vector<int32_t> 
     std::swap(pt.thr, nthr);
     std::swap(pt.kind, nkind);
     cleanup();
-    if (!d_pfresh.p && d_pfresh.ensure(8)) return SENTINEL_E_NOMEM;
-    HIP_OK(hipMemsetAsync(d_pfresh.p, 0, 8, stream));
+    if (!d_pfresh.p && d_pfresh.ensure(CNT_BYTES)) return SENTINEL_E_NOMEM;
+    HIP_OK(hipMemsetAsync(d_pfresh.p, 0, CNT_BYTES, stream));
     HIP_OK(hipStreamSynchronize(stream));
     pcap = new_cap;
     pmax_n = new_maxn;
@@ -1353,14 +1353,15 @@ int sentinel_engine::param_reserve(int64_t nv) {
             }
         }
     }
-    unsigned long long fresh = 0;
-    HIP_OK(hipMemcpyAsync(&fresh, d_pfresh.p, 8, hipMemcpyDeviceToHost, stream));
+    unsigned long long lanes[CNT_LANES * CNT_STRIDE], fresh = 0;
+    HIP_OK(hipMemcpyAsync(lanes, d_pfresh.p, CNT_BYTES, hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
+    for (int l = 0; l < CNT_LANES; ++l) fresh += lanes[l * CNT_STRIDE];
     p_pending.clear();
     if (p_live + fresh + (uint64_t)nv <= lim) {
         p_live += fresh;
         p_ub = (uint64_t)nv;
-        HIP_OK(hipMemsetAsync(d_pfresh.p, 0, 8, stream));
+        HIP_OK(hipMemsetAsync(d_pfresh.p, 0, CNT_BYTES, stream));
         // finished before returning: this batch's kernels may run on a caller's stream that waited on the
         // engine stream before the reset was queued, and their fresh-insert adds must land after it
         HIP_OK(hipStreamSynchronize(stream));
@@ -2967,7 +2968,7 @@ int sentinel_load_param_rules(sentinel_engine_t *e, const sentinel_param_rule_t 
         Is[i] = gint[i] / 1000.0;
     }
     int rc = 0;
-    if (!e->d_pfresh.p) rc |= e->d_pfresh.ensure(8);
+    if (!e->d_pfresh.p) rc |= e->d_pfresh.ensure(CNT_BYTES);
     if (rc) return SENTINEL_E_NOMEM;
     // the slot table: survivors move to their new index, orphans leave for the host, revived ones return
     std::vector<std::pair<int32_t, std::vector<int64_t>>> exported;

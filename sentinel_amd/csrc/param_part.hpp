@@ -676,7 +676,8 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
 // first, then the ordinal: a host that reads the ordinal and then the value sees a count at least as
 // new as that batch's -- the count only grows until the host resets it with the stream drained).
 __global__ void k_pfresh_publish(const unsigned long long *fresh, unsigned long long ord, unsigned long long *host) {
-    const unsigned long long f = *(volatile const unsigned long long *)fresh;
+    unsigned long long f = 0;                             // (the striped lanes summed)
+    for (int l = 0; l < CNT_LANES; ++l) f += *(volatile const unsigned long long *)(fresh + l * CNT_STRIDE);
     __hip_atomic_store(&host[1], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __threadfence_system();
     __hip_atomic_store(&host[0], ord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
