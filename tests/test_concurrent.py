@@ -144,10 +144,11 @@ def _device_batch(svc, fidx, acq, tok, kind, flags):
 
 @pytest.mark.gpu
 def test_gpu_concurrent_device_hot_flows_match_oracle(oracle_mod):
-    """The device-pointer path (sentinel_submit_concurrent_batch) on hot flows: runs of thousands of
-    events go to the workgroup kernel (k_conc_big: unit-acquire chunks by the (min, +) scan, others by
-    the state machine), fractional / tiny / AVG_LOCAL thresholds, duplicate releases in a batch, and a
-    reload that lowers the counts while tokens are out (nowCalls above the new threshold: phase A)."""
+    """The device-pointer path (sentinel_submit_concurrent_batch) on hot flows: segments of thousands of
+    events span many scan tiles (k_conc_scan's look-back over tile descriptors); segments with an
+    acquire of 2 tokens and, after the reload that lowers every count while tokens are out, segments
+    starting above their new threshold go to the one-thread walk (k_conc_serial, its start found by a
+    binary search); fractional / tiny / AVG_LOCAL thresholds and duplicate releases in a batch."""
     import sentinel_amd as sa
     from sentinel_amd.token_service import ServerNamespace
     rng = np.random.default_rng(404)
