@@ -1958,7 +1958,7 @@ static int submit_param_part(sentinel_engine_t *e, int64_t n, const ParamEvent *
         e->h_pfresh[0] = ~0ull;
         e->h_pfresh[1] = 0;
     }
-    k_pfresh_publish<<<1, 1, 0, s>>>(fresh, e->p_ord - 1, e->h_pfresh);
+    k_pfresh_publish<<<1, WAVE, 0, s>>>(fresh, e->p_ord - 1, e->h_pfresh);
     HIP_OK(hipGetLastError());
     return 0;
 }

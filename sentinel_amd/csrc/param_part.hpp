@@ -675,11 +675,18 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
 // The exact param table's fresh-insert count after batch `ord`, mirrored to pinned host memory (value
 // first, then the ordinal: a host that reads the ordinal and then the value sees a count at least as
 // new as that batch's -- the count only grows until the host resets it with the stream drained).
-__global__ void k_pfresh_publish(const unsigned long long *fresh, unsigned long long ord, unsigned long long *host) {
-    unsigned long long f = 0;                             // (the striped lanes summed)
-    for (int l = 0; l < CNT_LANES; ++l) f += *(volatile const unsigned long long *)(fresh + l * CNT_STRIDE);
+// One wave: lane l reads counter lane l (all loads in flight at once), a wave sum, lane 0 publishes.
+__global__ __launch_bounds__(WAVE) void k_pfresh_publish(const unsigned long long *fresh, unsigned long long ord,
+                                                         unsigned long long *host) {
+    static_assert(CNT_LANES == WAVE, "one counter lane per lane of the wave");
+    unsigned long long f = *(volatile const unsigned long long *)(fresh + threadIdx.x * CNT_STRIDE);
+#pragma unroll
+    for (int o = WAVE / 2; o >= 1; o >>= 1) f += __shfl_xor(f, o, WAVE);
+    if (threadIdx.x != 0) return;
     __hip_atomic_store(&host[1], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#ifndef SENTINEL_NO_PUBFENCE
     __threadfence_system();
+#endif
     __hip_atomic_store(&host[0], ord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
