@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <atomic>
+#include <memory>
 #include <chrono>
 #include <condition_variable>
 #include <functional>
@@ -601,6 +602,9 @@ struct sentinel_engine {
     // param rules + slots
     std::vector<sentinel_param_rule_t> prules;
     std::unordered_map<int64_t, int32_t> param_index;
+    // read-only copy published at every param rule load: sentinel_lookup_param_idx reads it without the
+    // engine mutex (a wire front end's I/O thread never waits behind a GPU batch)
+    std::shared_ptr<const std::unordered_map<int64_t, int32_t>> param_index_pub;
     DevBuf d_prule_route, d_prule_n, d_prule_w, d_prule_rcp, d_prule_Is, d_prule_thr;
     DevBuf d_prule_rec, d_prule_hot;   // packed per-rule records (k_prule_pack) + has-hot-items flags
     bool prec_dirty = true;
@@ -2875,11 +2879,12 @@ int sentinel_lookup_flow_idx(sentinel_engine_t *e, int64_t n, const int64_t *ids
 
 int sentinel_lookup_param_idx(sentinel_engine_t *e, int64_t n, const int64_t *ids, int32_t *out) {
     if (!e || n < 0 || (n > 0 && (!ids || !out))) return fail(SENTINEL_E_INVALID, "bad arguments");
-    std::lock_guard<std::mutex> g(e->mu);
+    const auto idx = std::atomic_load(&e->param_index_pub);     // (no engine mutex: see param_index_pub)
     for (int64_t i = 0; i < n; ++i) {
         if (ids[i] <= 0) { out[i] = SENTINEL_IDX_BAD_ID; continue; }
-        auto it = e->param_index.find(ids[i]);
-        out[i] = it == e->param_index.end() ? SENTINEL_IDX_NO_RULE : it->second;
+        if (!idx) { out[i] = SENTINEL_IDX_NO_RULE; continue; }
+        auto it = idx->find(ids[i]);
+        out[i] = it == idx->end() ? SENTINEL_IDX_NO_RULE : it->second;
     }
     return 0;
 }
@@ -2982,6 +2987,7 @@ int sentinel_load_param_rules(sentinel_engine_t *e, const sentinel_param_rule_t 
     for (auto &x : exported) e->porphans[e->prules[x.first].flow_id].recs = std::move(x.second);
     e->prules = std::move(nr);
     e->param_index = std::move(nidx);
+    std::atomic_store(&e->param_index_pub, std::make_shared<const std::unordered_map<int64_t, int32_t>>(e->param_index));
     e->h_prule_n = gn;
     e->h_prule_interval = gint;
     rc |= upload(e->d_prule_n, nn_up);
