@@ -684,9 +684,7 @@ __global__ __launch_bounds__(WAVE) void k_pfresh_publish(const unsigned long lon
     for (int o = WAVE / 2; o >= 1; o >>= 1) f += __shfl_xor(f, o, WAVE);
     if (threadIdx.x != 0) return;
     __hip_atomic_store(&host[1], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#ifndef SENTINEL_NO_PUBFENCE
     __threadfence_system();
-#endif
     __hip_atomic_store(&host[0], ord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
