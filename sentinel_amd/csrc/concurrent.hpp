@@ -181,33 +181,6 @@ __global__ __launch_bounds__(SORT_THREADS) void k_conc_prep(int64_t n, const Con
     tile_hist_store(hf, fhist, 1, nblocks);
 }
 
-// Flow runs of the sorted batch: head flags (a valid key differing from its predecessor), scanned by
-// the engine, then each head's run start; the last valid element publishes the valid count and the
-// number of runs.
-__global__ __launch_bounds__(256) void k_conc_heads(const uint32_t *__restrict__ skey, int64_t n, uint32_t invalid,
-                                                    uint32_t *__restrict__ flag) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t k = skey[i];
-    flag[i] = (k != invalid && (i == 0 || skey[i - 1] != k)) ? 1u : 0u;
-}
-
-__global__ __launch_bounds__(256) void k_conc_runs(const uint32_t *__restrict__ skey, int64_t n, uint32_t invalid,
-                                                   const uint32_t *__restrict__ pos, uint32_t *__restrict__ run_start,
-                                                   uint32_t *__restrict__ ctl) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t k = skey[i];
-    if (k == invalid) return;
-    const bool head = i == 0 || skey[i - 1] != k;
-    if (head) run_start[pos[i]] = (uint32_t)i;
-    if (i + 1 == n || skey[i + 1] == invalid) {          // the last valid element
-        const uint32_t nruns = pos[i] + (head ? 1u : 0u);
-        run_start[nruns] = (uint32_t)(i + 1);
-        ctl[0] = nruns;
-    }
-}
-
 // ---------------------------------------------------------------- decisions
 // After the sort a flow's events form a contiguous segment in arrival order, and the batch is decided
 // by one segmented scan over the sorted positions (k_conc_scan), so that no lane walks a chain of
