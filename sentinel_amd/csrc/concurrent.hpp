@@ -146,10 +146,32 @@ __global__ __launch_bounds__(SORT_THREADS) void k_conc_prep(int64_t n, const Con
     for (int d = threadIdx.x; d < MAX_PASSES * RADIX; d += SORT_THREADS) (&hf[0][0])[d] = 0;
     __syncthreads();
     const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
+    // every event of the tile loaded, then every release's home-slot probe (key + flow index) issued,
+    // before any item is decided: the probes of one thread's items are in flight together
+    ConcEvent evs[SORT_ITEMS];
+    unsigned long long hk[SORT_ITEMS];
+    int32_t hf_idx[SORT_ITEMS];
+#pragma unroll
     for (int j = 0; j < SORT_ITEMS; ++j) {
         const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
-        if (i >= n) break;
-        const ConcEvent e = ev[i];
+        if (i < n) evs[j] = ev[i];
+        else evs[j].kind = -1;
+    }
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        hk[j] = PKEY_EMPTY;
+        hf_idx[j] = -1;
+        if (evs[j].kind == CONC_RELEASE) {
+            const uint64_t h = mix64((uint64_t)evs[j].token) & TT.mask;
+            hk[j] = TT.rec[h].key;
+            hf_idx[j] = TT.rec[h].flow_idx;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const int64_t i = tile0 + j * SORT_THREADS + threadIdx.x;
+        if (i >= n) continue;
+        const ConcEvent e = evs[j];
         int st = 127;
         uint32_t k = finvalid;
         uint64_t cv = conc_value((uint32_t)i, false, 0);
@@ -161,11 +183,23 @@ __global__ __launch_bounds__(SORT_THREADS) void k_conc_prep(int64_t n, const Con
                 cv = conc_value((uint32_t)i, false, (uint32_t)e.acquire);   // an acquire: its amount (> 0)
             }
         } else if (e.kind == CONC_RELEASE) {
-            const int64_t h = token_find(TT, (uint64_t)e.token);             // CCFC:82-86
+            int64_t h = -1;                                                  // CCFC:82-86
+            int32_t fidx = -1;
+            const uint64_t h0 = mix64((uint64_t)e.token) & TT.mask;
+            const bool issuable = (uint64_t)e.token != PKEY_EMPTY && (uint64_t)e.token != TOKEN_TOMB;  // (slot markers)
+            if (!issuable) {
+                // never issued (ids stay below 2^63): ALREADY_RELEASE
+            } else if (hk[j] == (unsigned long long)e.token) {               // at its home slot (the common case)
+                h = (int64_t)h0;
+                fidx = hf_idx[j];
+            } else if (hk[j] != PKEY_EMPTY) {                                // further along its probe chain
+                h = token_find(TT, (uint64_t)e.token);
+                if (h >= 0) fidx = TT.rec[h].flow_idx;
+            }
             if (h < 0) st = ST_ALREADY_RELEASE;
-            else if (TT.rec[h].flow_idx < 0) st = ST_NO_RULE_EXISTS;         // CCFC:87-91
+            else if (fidx < 0) st = ST_NO_RULE_EXISTS;                       // CCFC:87-91
             else {
-                k = (uint32_t)TT.rec[h].flow_idx;
+                k = (uint32_t)fidx;
                 cv = conc_value((uint32_t)i, true, (uint64_t)h);             // a release: its token's slot
                 atomicMin(&TT.rec[h].claim, (uint32_t)i);
             }

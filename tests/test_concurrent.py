@@ -187,6 +187,8 @@ def test_gpu_concurrent_device_hot_flows_match_oracle(oracle_mod):
             pick = rng.integers(0, len(outstanding), size=len(rel))
             tok[rel] = np.array(outstanding, np.int64)[pick]                # repeats -> ALREADY_RELEASE
             tok[rel[::97]] = 777                                             # never issued
+            tok[rel[1::389]] = -1                                            # the cache's empty-slot and
+            tok[rel[2::389]] = -2                                            # tombstone markers as ids
         st_g, tok_g = _device_batch(svc, fidx, acq, tok, kind, flags)
         ev = np.zeros(n, dtype=orc.CONC_EVENT)
         ev["flow_idx"], ev["acquire"], ev["token_id"], ev["kind"], ev["flags"] = fidx, acq, tok, kind, flags
