@@ -329,15 +329,15 @@ struct ConcScan {
     int32_t *fin;            // [flow] nowCalls after the batch (stored by k_conc_apply)
 };
 
-// A claimed release frees its token's slot (CCFC:92-100).  No insert runs in the same kernel, and
+// A claimed release frees its token's slot (CCFC:92-100), given its neighbours' keys as read earlier
+// in the same kernel.  No insert runs in the same kernel, and
 // concurrent releases only turn slots from occupied to tombstone / empty, so an empty successor seen
 // here stays empty and a stale plain read can only show an older, occupied successor (the release then
 // leaves a tombstone the next sweep may free).  A slot followed by an empty one ends no probe chain, so
 // it becomes empty, and so do the tombstones right before it (as k_tok_sweep); otherwise it becomes a
 // tombstone.  In a sparse cache almost every release empties its slot.
-__device__ inline void token_free(const TokenTable &TT, uint32_t h, TokRec r, int64_t &dtomb) {
-    const unsigned long long nxt = TT.rec[(h + 1) & TT.mask].key;
-    const unsigned long long prv = TT.rec[(h - 1) & TT.mask].key;
+__device__ inline void token_free(const TokenTable &TT, uint32_t h, TokRec r, unsigned long long nxt,
+                                  unsigned long long prv, int64_t &dtomb) {
     r.claim = ~0u;
     r.key = nxt == PKEY_EMPTY ? PKEY_EMPTY : TOKEN_TOMB;
     TT.rec[h] = r;                                        // the whole record: no partial-sector write
@@ -391,26 +391,44 @@ __global__ __launch_bounds__(CS_THREADS) void k_conc_scan(const uint64_t *__rest
     const uint32_t knext = b + CS_ITEMS < n ? skey[b + CS_ITEMS] : invalid;
     int64_t dtomb = 0;
     unsigned long long freed = 0;
+    // the gathers in phases, each phase's loads of all items in flight together: sorted values, the
+    // released tokens' records, the claimed slots' neighbours; then the slots are freed
+    uint64_t w[CS_ITEMS];
+    TokRec r[CS_ITEMS];
+    bool win[CS_ITEMS];
+    unsigned long long nxt[CS_ITEMS], prv[CS_ITEMS];
+#pragma unroll
+    for (int q = 0; q < CS_ITEMS; ++q) w[q] = k[q] != invalid ? sval[b + q] : 0;
+#pragma unroll
+    for (int q = 0; q < CS_ITEMS; ++q)
+        if (k[q] != invalid && ((w[q] >> CV_REL_BIT) & 1)) r[q] = TT.rec[(uint32_t)(w[q] >> CV_PAY_SHIFT)];
+#pragma unroll
+    for (int q = 0; q < CS_ITEMS; ++q) {
+        x[q] = 0;
+        win[q] = false;
+        if (k[q] == invalid) continue;
+        if (!((w[q] >> CV_REL_BIT) & 1)) {
+            x[q] = (int32_t)(w[q] >> CV_PAY_SHIFT);       // an acquire: > 0 (validated)
+        } else if (r[q].claim == ((uint32_t)w[q] & SEQ_MASK)) {   // CCFC:82-86: this release finds its token
+            x[q] = -r[q].acquire;
+            win[q] = true;
+            const uint32_t h = (uint32_t)(w[q] >> CV_PAY_SHIFT);
+            nxt[q] = TT.rec[(h + 1) & TT.mask].key;
+            prv[q] = TT.rec[(h - 1) & TT.mask].key;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < CS_ITEMS; ++q)
+        if (win[q]) {
+            token_free(TT, (uint32_t)(w[q] >> CV_PAY_SHIFT), r[q], nxt[q], prv[q], dtomb);
+            ++freed;
+        }
     uint32_t kc = invalid;
     int64_t tc = 0;
 #pragma unroll
     for (int q = 0; q < CS_ITEMS; ++q) {
-        x[q] = 0;
         tp[q] = 0;
         if (k[q] == invalid) continue;
-        const uint64_t w = sval[b + q];
-        const uint32_t seq = (uint32_t)w & SEQ_MASK;
-        if (!((w >> CV_REL_BIT) & 1)) {
-            x[q] = (int32_t)(w >> CV_PAY_SHIFT);          // an acquire: > 0 (validated)
-        } else {
-            const uint32_t h = (uint32_t)(w >> CV_PAY_SHIFT);
-            const TokRec r = TT.rec[h];                   // claim and amount: one line
-            if (r.claim == seq) {                         // CCFC:82-86: this release finds its token
-                x[q] = -r.acquire;
-                token_free(TT, h, r, dtomb);
-                ++freed;
-            }
-        }
         if (k[q] != kc) {
             kc = k[q];
             tc = conc_tprime(thr[kc]);
