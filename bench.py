@@ -54,6 +54,8 @@ KERNEL_BYTES_PER_EVENT = {
     "lim_prep": 32.0,         # one-limiter prep: read the 16-B event, write flow key 4 + limiter key 4 + value 8
     "part_prep": 16.0,        # read the 16-B event (range histogram in LDS; no key array without namespace routes)
     "part_scatter": 24.0,     # read the 16-B event (key re-derived), write the 8-B packed value (local key inside)
+    "part_split": 24.0,       # one sweep: read the 16-B event (its second read is served by the Infinity Cache),
+                              # write the 8-B packed value; the digit columns are ~4 KB per workgroup
     "param_prep": 24.0,       # read the 24-B event (range histogram in LDS; rejected requests answered here)
     "param_scatter": 44.0,    # read the 24-B event, write key 8 + packed value 8 + rule 4
     "param_meta": 48.0,       # per slot after a rule / threshold / table change: key 8, rule fields ~16, write ~20 B
@@ -67,7 +69,7 @@ KERNEL_BYTES_PER_EVENT = {
 KERNEL_SYMBOLS = {
     "flow_prep": ("k_flow_prep",), "radix_hist": ("k_radix_hist_pass",), "radix_scatter": ("k_radix_scatter_p",),
     "scan": ("k_scan_lookback",), "segments": ("k_segments",), "process": ("k_process",), "verdict": ("k_verdict",),
-    "part_prep": ("k_part_prep",), "part_scatter": ("k_part_scatter",),
+    "part_prep": ("k_part_prep",), "part_scatter": ("k_part_scatter",), "part_split": ("k_part_split",),
     "part_fused": ("k_part_half",), "part_big": ("k_part_big",), "part_long": ("k_part_long",),
     "param_prep": ("k_param_prep", "k_pp_prep"), "param_meta": ("k_param_meta",), "prule_prep": ("k_prule_prep",),
     "prule_process": ("k_prule_process",), "part_unsplit": ("k_part_unsplit",), "lim_prep": ("k_lim1_prep",),
@@ -242,6 +244,8 @@ class FlowWorkload:
             self.zipf_cdf = torch.from_numpy(np.cumsum(w) / w.sum()).to(dev)
             self.zipf_perm = torch.from_numpy(perm.astype(np.int32)).to(dev)
         self.verdicts = torch.empty(self.N, dtype=torch.int64, device=dev)
+        self.kept = []
+        self.parity_result = None
 
     def batch(self, s):
         """Step s's events (device tensor (N, 2) int64): consecutive in time across steps."""
@@ -264,8 +268,26 @@ class FlowWorkload:
     def span_ms(self):
         return int(np.ceil(self.N * self.ms_per_event)) + 1
 
-    def submit(self, b):
-        self.svc.submit_flow_batch(b, verdicts=self.verdicts)
+    def submit(self, b, keep=False):
+        if keep:                          # a verdict buffer of its own: checked against the CPU baseline's replay
+            v = self.torch.empty(self.N, dtype=self.torch.int64, device=self.dev)
+            self.svc.submit_flow_batch(b, verdicts=v)
+            self.kept.append(v)
+        else:
+            self.svc.submit_flow_batch(b, verdicts=self.verdicts)
+
+    def parity(self, st, rem, wait):
+        """The kept batches' GPU verdicts against the oracle replay of the same events (first batches)."""
+        from sentinel_amd.token_service import decode_verdicts
+        if not self.kept:
+            return None
+        g = [decode_verdicts(v) for v in self.kept]
+        gs, gr, gw = (np.concatenate([x[i] for x in g]) for i in range(3))
+        m = min(len(gs), len(st))
+        bad = int(((gs[:m] != st[:m]) | (gr[:m] != rem[:m]) | (gw[:m] != wait[:m])).sum())
+        return {"parity_checked_events": m, "parity_mismatches": bad,
+                "parity_note": f"status, remaining and waitInMs of the first {len(self.kept)} batches (warmup + "
+                               f"profile steps) against the CPU baseline's oracle replay of the same events"}
 
     def cpu_baseline(self, batches, k1, kmt, threads):
         from oracle import oracle as O
@@ -286,13 +308,17 @@ class FlowWorkload:
         cdt = time.perf_counter() - c0
         one = (len(ts), cdt, 1, "sequential oracle replay")
         if self.namespaces:          # a namespace limiter couples every flow: no sharded replay
+            idx, acq, ts = host_steps(min(len(self.kept), len(batches)))
+            st, rem, wt = fresh().replay(idx, acq, ts)
+            self.parity_result = self.parity(st, rem, wt)
             return one, None
         idx, acq, ts = host_steps(kmt)
         orc = fresh()
         c0 = time.perf_counter()
-        used = orc.replay_mt(idx, acq, ts, threads)[3]
+        st, rem, wt, used = orc.replay_mt(idx, acq, ts, threads)
         cdt = time.perf_counter() - c0
         mt = (len(ts), cdt, int(used), f"oracle replay sharded by flow over {used} pthreads")
+        self.parity_result = self.parity(st, rem, wt)
         return one, mt
 
     def bytes_of(self, dom, d, steps):
@@ -374,6 +400,8 @@ class ParamWorkload:
         self.zipf_cdf = torch.from_numpy(np.cumsum(w) / w.sum()).to(dev)
         self.fid_dev = torch.from_numpy(self.flow_id.astype(np.int64)).to(dev)
         self.verdicts = torch.empty(self.N, dtype=torch.int64, device=dev)
+        self.kept = []
+        self.parity_result = None
         self.workload = (f"config4: {self.R_total} hot-parameter cluster rules (count~U{{5..100}}, hot items), values "
                          f"Zipf(1.2) over 1000 Long keys per resource, n={n} w={self.interval // n}ms, acquire 1, "
                          f"{self.N}-event batches, " + (f"shared count-min sketch d={self.cm_depth} w=2^20"
@@ -393,8 +421,13 @@ class ParamWorkload:
     def span_ms(self):
         return int(np.ceil(self.N * self.ms_per_event)) + 1
 
-    def submit(self, b):
-        self.svc.submit_param_batch(b, verdicts=self.verdicts)
+    def submit(self, b, keep=False):
+        if keep:
+            v = self.torch.empty(self.N, dtype=self.torch.int64, device=self.dev)
+            self.svc.submit_param_batch(b, verdicts=v)
+            self.kept.append(v)
+        else:
+            self.svc.submit_param_batch(b, verdicts=self.verdicts)
 
     def _host(self, batches, k):
         e = self.torch.cat(batches[:k]).cpu().numpy()
@@ -414,8 +447,21 @@ class ParamWorkload:
         ridx, acq, keys, ts = self._host(batches, kmt)
         orc = self._oracle()
         c0 = time.perf_counter()
-        used = orc.param_replay_mt(ridx, acq, keys, ts, threads)[2]
+        st, rem, used = orc.param_replay_mt(ridx, acq, keys, ts, threads)
         cdt = time.perf_counter() - c0
+        if self.kept and not self.cm:
+            from sentinel_amd.token_service import decode_verdicts
+            g = [decode_verdicts(v) for v in self.kept]
+            gs, gr = np.concatenate([x[0] for x in g]), np.concatenate([x[1] for x in g])
+            m = min(len(gs), len(st))
+            self.parity_result = {
+                "parity_checked_events": m, "parity_mismatches": int(((gs[:m] != st[:m]) | (gr[:m] != rem[:m])).sum()),
+                "parity_note": f"status and remaining of the first {len(self.kept)} batches (warmup + profile steps) "
+                               f"against the CPU baseline's oracle replay of the same requests"}
+        elif self.cm:
+            self.parity_result = {"parity_checked_events": 0, "parity_mismatches": None,
+                                  "parity_note": "count-min mode is not exact by design: see count_min (one-sidedness "
+                                                 "audit of the same batches on exact counters)"}
         return one, (len(ts), cdt, int(used), f"oracle replay sharded by rule over {used} pthreads (exact counters)")
 
     def false_blocks(self, batches, k, svc_verdicts):
@@ -524,6 +570,7 @@ class ConcWorkload:
                          f"Zipf(1.1) flows, {N}-event batches of half acquires (1 token) and half releases of the "
                          f"previous batch's tokens, device-pointer path")
         self.kept = []
+        self.parity_result = None
 
     def batch(self, s):
         torch, N = self.torch, self.N
@@ -538,7 +585,7 @@ class ConcWorkload:
     def span_ms(self):
         return 0
 
-    def submit(self, b):
+    def submit(self, b, keep=False):
         torch = self.torch
         prev, cur = self.results[self.k % 2], self.results[(self.k + 1) % 2]
         ext = torch.cuda.ExternalStream(self.svc.stream, device=self.dev)
@@ -547,7 +594,7 @@ class ConcWorkload:
         self.svc.submit_concurrent_batch(b, results=cur)
         self.verdicts = cur
         self.k += 1
-        if len(self.kept) < 3:
+        if keep:                                           # warmup / profile steps only
             self.svc.synchronize()
             self.kept.append((b.clone(), cur.clone()))
 
@@ -578,8 +625,13 @@ class ConcWorkload:
         all_ev = np.concatenate([ev for ev, _ in evs])
         all_ids = np.concatenate([ids for _, ids in evs])
         c0 = time.perf_counter()
-        used = orc.concurrent_replay_mt(all_ev, all_ids, threads)[2]
+        st, _, used = orc.concurrent_replay_mt(all_ev, all_ids, threads)
         cdt = time.perf_counter() - c0
+        gst = np.concatenate([res[:, 1].cpu().numpy() for _, res in self.kept]).astype(np.int32).astype(np.int8)
+        self.parity_result = {
+            "parity_checked_events": int(len(st)), "parity_mismatches": int((gst != st).sum()),
+            "parity_note": f"statuses of the first {len(self.kept)} batches (warmup + profile steps: half acquires, half "
+                           f"releases of the previous batch's tokens) against the CPU baseline's oracle replay"}
         return one, (len(all_ev), cdt, int(used),
                      f"oracle replay sharded by flow over {used} pthreads (a token cache per thread, releases routed "
                      f"to their token's thread; the engine's token ids)")
@@ -641,12 +693,14 @@ def main():
     log(f"config {args.config}: {steps_total} batches of {N} events generated")
 
     ext = torch.cuda.ExternalStream(svc.stream, device=dev)
-    keep_verdicts = []
+    # the first batches (warmup + profile steps, never the timed ones) decide into verdict buffers of their
+    # own, checked against the CPU baseline's oracle replay of the same events (parity_* fields)
+    check = rank == 0 and world == 1 and not args.no_cpu_baseline
+    keep_n = min(args.cpu_steps_mt, args.warmup + pstep) if check else 0
+    if args.config == "4cm":                                    # the count-min audit's sample: the first two batches
+        keep_n = max(keep_n, min(2, args.warmup + pstep))
     for s in range(args.warmup):
-        W.submit(ev_b[s])
-        if args.config == "4cm" and len(keep_verdicts) < 2:     # the audited sample: the first two batches
-            svc.synchronize()                                   # (the engine stream wrote them; torch copies on its own)
-            keep_verdicts.append(W.verdicts.clone())
+        W.submit(ev_b[s], keep=s < keep_n)
     svc.synchronize()
 
     import ctypes as C
@@ -669,10 +723,7 @@ def main():
     if not args.no_profile:
         svc._L.sentinel_profile_enable(svc.handle, 1)
         for s in range(args.warmup, args.warmup + pstep):
-            W.submit(ev_b[s])
-            if args.config == "4cm" and len(keep_verdicts) < 2:
-                svc.synchronize()
-                keep_verdicts.append(W.verdicts.clone())
+            W.submit(ev_b[s], keep=s < keep_n)
         svc.synchronize()
         breakdown = read_profile()
         svc._L.sentinel_profile_enable(svc.handle, 0)
@@ -884,6 +935,8 @@ def main():
 
     # ---- CPU baseline: the oracle ("port") on bounded samples of the same workload, rank 0, N=1
     cpu = cpu1 = None
+    extra_parity = {"parity_checked_events": 0, "parity_mismatches": None,
+                    "parity_note": "not checked in this run (CPU baseline off, or rank > 0 / N > 1)"}
     model, ncpu, avail = cpu_info()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline")
@@ -897,9 +950,13 @@ def main():
                     "sample": f"the first {m} events of this workload (same rules and trace), {how}, {cdt:.1f} s"}
         cpu1 = leg(one)
         cpu = leg(mt) if mt else cpu1
+        if W.parity_result is not None:
+            extra_parity = W.parity_result
+            log(f"parity: {extra_parity['parity_mismatches']} mismatches in {extra_parity['parity_checked_events']} events")
 
     extra = {}
     if args.config == "4cm" and rank == 0 and world == 1:
+        keep_verdicts = W.kept[:2]
         k = len(keep_verdicts)
         viol, fb, dec = W.false_blocks(ev_b, k, keep_verdicts)
         eps_n = float(np.e) / W.cm_width * float(N) * k      # e/w x (requests counted in the audited span)
@@ -951,6 +1008,7 @@ def main():
         "roofline": roof,
         "cpu_baseline": cpu,
         "cpu_baseline_1core": cpu1,
+        **extra_parity,
         **extra,
         "kernels": {k: {"avg_us": round(v["avg_us"], 2), "calls": v["calls"]} for k, v in breakdown.items()},
         "kernels_note": (f"per-kernel HIP-event averages from {pstep} untimed profiled steps after the warmup; the "

@@ -327,6 +327,7 @@ struct ConcScan {
     uint32_t *ctl;           // [0] tile ticket, [1] segments left to k_conc_serial
     uint32_t *serial;        // their last positions
     int32_t *fin;            // [flow] nowCalls after the batch (stored by k_conc_apply)
+    uint32_t *err;           // pinned: set when a look-back spin gave up (engine.hip, check_dev_err)
 };
 
 // A claimed release frees its token's slot (CCFC:92-100), given its neighbours' keys as read earlier
@@ -484,6 +485,7 @@ __global__ __launch_bounds__(CS_THREADS) void k_conc_scan(const uint64_t *__rest
     if (lb && t >= CS_THREADS - WAVE) {
         ConcSeg pre = cs_identity();                      // tiles between the window and this one
         int64_t top = tile;                               // the window ends below top
+        uint32_t spins = 0;
         for (;;) {
             const int64_t p = top - 1 - (int64_t)lane;    // lane 0: the nearest tile
             // (a position before tile 0 reads as an inclusive identity)
@@ -495,6 +497,12 @@ __global__ __launch_bounds__(CS_THREADS) void k_conc_scan(const uint64_t *__rest
             const int first = incl ? __ffsll((unsigned long long)incl) - 1 : WAVE;   // the nearest inclusive one
             const uint64_t need = first >= WAVE - 1 ? ~0ull : ((2ull << first) - 1);
             if (waiting & need) {
+                // tiles take tickets in order and publish without waiting, so a tile's predecessors always
+                // publish: the bound only turns a broken invariant into a reported error instead of a hang
+                if (++spins > (1u << 22)) {
+                    if (lane == 0) __hip_atomic_store(S.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(1);
                 continue;
             }

@@ -52,6 +52,21 @@ namespace {
 
 thread_local std::string g_err;
 
+// Engines per device (k_part_split's grid barrier needs every one of its workgroups resident: two
+// engines on one device could each hold part of the CUs, so the one-sweep partition runs only while
+// its engine is alone on the device).
+std::mutex g_dev_mu;
+std::unordered_map<int, int> g_dev_engines;
+int dev_engines(int device) {
+    std::lock_guard<std::mutex> g(g_dev_mu);
+    auto it = g_dev_engines.find(device);
+    return it == g_dev_engines.end() ? 0 : it->second;
+}
+void dev_engines_add(int device, int d) {
+    std::lock_guard<std::mutex> g(g_dev_mu);
+    g_dev_engines[device] += d;
+}
+
 int fail(int code, const std::string &msg) {
     g_err = msg;
     return code;
@@ -586,6 +601,16 @@ struct sentinel_engine {
     // range > 8x the mean): then the sorted path for the next 1024 batches, then one probe again
     DevBuf d_part_stat;
     unsigned long long *h_part_stat = nullptr;   // pinned mirror, written asynchronously after each batch
+    // one-sweep partition (k_part_split): digit columns + totals, the monotonic arrival counter, the
+    // pinned barrier-timeout word; SENTINEL_PART_SPLIT=0 keeps prep + scan + scatter
+    bool part_split = true;
+    int64_t flow_path_count[4] = {0, 0, 0, 0};   // small, sorted, partition 3-pass, partition one-sweep
+    int num_cu = 0;
+    DevBuf w_split_col, d_split_bar;
+    uint32_t split_arrivals = 0;
+    // pinned words a kernel sets when a bounded spin gave up (the batch's results are invalid): [0] the
+    // one-sweep partition's grid barrier, [1] the concurrency scan's look-back; checked by the next submit
+    uint32_t *h_dev_err = nullptr;
     uint32_t *h_long_chunks = nullptr;           // pinned: hot-run chunks of a recent batch (launch hint)
     uint32_t *h_het_hint = nullptr;              // pinned: the sorted path's heterogeneous-key deferral is on
     uint32_t hot_het_run = HOT_HET_RUN;          // sorted path: heterogeneous keys above this go to k_part_long
@@ -1671,6 +1696,22 @@ static int ensure_part_bufs(sentinel_engine_t *e, const PartBufs &B, int64_t n) 
     return rc;
 }
 
+// One-sweep partition geometry: the fewest events per thread (8, 16 or 32) that cover the batch with at
+// most one 1024-thread workgroup per CU.  False: the batch takes prep + scan + scatter (too large, too
+// small to be worth a persistent launch, knob off, or another engine on this device).
+static bool split_geometry(const sentinel_engine_t *e, int64_t n, int &items, int &G) {
+    if (!e->part_split || e->num_cu <= 0 || n < 65536 || dev_engines(e->device) != 1) return false;
+    for (int it : {8, 16, 32}) {
+        const int64_t g = (n + (int64_t)it * SP_THREADS - 1) / ((int64_t)it * SP_THREADS);
+        if (g <= e->num_cu) {
+            items = it;
+            G = (int)g;
+            return true;
+        }
+    }
+    return false;
+}
+
 static int part_front(sentinel_engine_t *e, const PartBufs &B, int64_t n, const Event *ev, const uint8_t *fl,
                       uint64_t *out, hipStream_t s) {
     const PartGeo g = part_geo(e, n);
@@ -1691,7 +1732,38 @@ static int part_front(sentinel_engine_t *e, const PartBufs &B, int64_t n, const 
     // flows of a namespace: validation and the limiter pass run first (the sorted path's k_flow_prep and
     // limiter pipeline, which mark failing events invalid); the multi-split then takes their keys
     const bool lim = e->nlimiters > 0 && !e->flow_plain;
+    if (!lim && e->flow_plain) {
+        int items = 0, G = 0;
+        if (split_geometry(e, n, items, G)) {
+            const int64_t colw = (int64_t)g.nparts * G + g.nparts;
+            rc = e->w_split_col.ensure((size_t)colw * 4);
+            if (!rc && !e->d_split_bar.p) {
+                rc = e->d_split_bar.ensure(64);
+                if (!rc) rc = hipMemset(e->d_split_bar.p, 0, 64) == hipSuccess ? 0 : SENTINEL_E_DEVICE;
+                e->split_arrivals = 0;
+            }
+            if (rc) return SENTINEL_E_NOMEM;
+            const EventSrc src{ev, nullptr, fl, false};
+            uint32_t *col = e->w_split_col.as<uint32_t>(), *bar = e->d_split_bar.as<uint32_t>();
+            const uint32_t base = e->split_arrivals;
+            e->split_arrivals += 2u * (uint32_t)G;
+            e->flow_path_count[3] += 1;
+            e->launch("part_split", n, s, [&] {
+#define SP_LAUNCH(IT)                                                                                           \
+    k_part_split<IT><<<dim3((unsigned)G), dim3(SP_THREADS), 0, s>>>(n, src, g.F, out, g.lb, g.pbits, g.nparts,  \
+                                                                   B.sval->as<uint64_t>(), rstart, col, bar,   \
+                                                                   base, e->h_dev_err, ctl, stat)
+                if (items == 8) SP_LAUNCH(8);
+                else if (items == 16) SP_LAUNCH(16);
+                else SP_LAUNCH(32);
+#undef SP_LAUNCH
+            });
+            HIP_OK(hipGetLastError());
+            return 0;
+        }
+    }
     if (lim) e->limiter_pass(n, ev, g.F, fkey, g.finvalid, 0, out, s);
+    e->flow_path_count[2] += 1;
     e->launch("part_prep", n, s, [&] {
         k_part_prep<<<dim3((unsigned)g.nb), dim3(PP_THREADS), 0, s>>>(
             n, ev, g.F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out,
@@ -1863,10 +1935,34 @@ struct ForeignStream {
     }
 };
 
+// A kernel of an earlier batch gave up a bounded spin (MI355X_MICROARCH.md: every spin bounded): that
+// batch's results are invalid, so the next submit reports it.  [0]: the one-sweep partition's grid barrier
+// did not complete (its workgroups were not all resident: another persistent kernel on the device) -- the
+// arrival counter is reset and this engine keeps prep + scan + scatter from now on; [1]: the concurrency
+// scan's look-back waited past its bound (cannot happen with ticket-ordered tiles; a guard, not a path).
+static int check_dev_err(sentinel_engine_t *e, hipStream_t s) {
+    if (!e->h_dev_err) return 0;
+    const uint32_t e0 = __atomic_load_n(&e->h_dev_err[0], __ATOMIC_ACQUIRE);
+    const uint32_t e1 = __atomic_load_n(&e->h_dev_err[1], __ATOMIC_ACQUIRE);
+    if (!e0 && !e1) return 0;
+    HIP_OK(hipStreamSynchronize(s));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    if (e0) {
+        if (e->d_split_bar.p) HIP_OK(hipMemset(e->d_split_bar.p, 0, 64));
+        e->split_arrivals = 0;
+        e->part_split = false;
+    }
+    e->h_dev_err[0] = 0;
+    e->h_dev_err[1] = 0;
+    return fail(SENTINEL_E_DEVICE, e0 ? "one-sweep partition: grid barrier timed out (an earlier batch's verdicts are invalid)"
+                                      : "concurrency scan: look-back timed out (an earlier batch's results are invalid)");
+}
+
 static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
                        hipStream_t s) {
     if (n <= 0) return 0;
     if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
+    if (int rc0 = check_dev_err(e, s)) return rc0;
     if (small_ok(e) && (n <= SM_MAX || e->flow_path == 3)) {
         // consecutive chunks decided in order = the whole batch decided in arrival order
         for (int64_t off = 0; off < n; off += SM_MAX) {
@@ -1874,11 +1970,13 @@ static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const u
                                         out + off, s);
             if (rc) return rc;
         }
+        e->flow_path_count[0] += 1;
         return 0;
     }
     int rc = e->ensure_ws(n);
     if (rc) return rc;
     if (choose_part(e, n)) return submit_flow_part(e, n, ev, fl, out, s);
+    e->flow_path_count[1] += 1;
     return submit_flow_sorted(e, n, ev, fl, out, s);
 }
 
@@ -2427,6 +2525,8 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
     if (const char *c = getenv("SENTINEL_ROUTE8")) e->use_route8 = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_LIM1")) e->lim1 = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_PROC_OCC")) e->process_occ = std::string(c) != "0";
+    if (const char *c = getenv("SENTINEL_PART_SPLIT")) e->part_split = std::string(c) != "0";
+    if (hipDeviceGetAttribute(&e->num_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) e->num_cu = 0;
     if (const char *c = getenv("SENTINEL_PARAM_CAPACITY")) {
         uint64_t v = strtoull(c, nullptr, 10);
         uint64_t p = 1024;
@@ -2440,6 +2540,12 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
         delete e;
         return rc;
     }
+    if (hipHostMalloc((void **)&e->h_dev_err, 64, 0) != hipSuccess) {
+        delete e;
+        return fail(SENTINEL_E_DEVICE, "hipHostMalloc failed");
+    }
+    memset(e->h_dev_err, 0, 64);
+    dev_engines_add(device, 1);
     *out = e;
     return 0;
 }
@@ -2448,6 +2554,10 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
     if (!e) return 0;
     (void)hipSetDevice(e->device);
     (void)hipStreamSynchronize(e->stream);
+    dev_engines_add(e->device, -1);
+    e->w_split_col.release();
+    e->d_split_bar.release();
+    if (e->h_dev_err) (void)hipHostFree(e->h_dev_err);
     e->prof_collect();
     for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
     e->ft.release();
@@ -2850,6 +2960,13 @@ int sentinel_param_table_stats(sentinel_engine_t *e, int64_t *out3) {
     out3[0] = e->d_ptable.p ? (int64_t)e->pcap : 0;
     out3[1] = (int64_t)e->p_live;
     out3[2] = (int64_t)e->p_rebuilds;
+    return 0;
+}
+
+int sentinel_flow_path_stats(sentinel_engine_t *e, int64_t *out4) {
+    if (!e || !out4) return fail(SENTINEL_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(e->mu);
+    for (int k = 0; k < 4; ++k) out4[k] = e->flow_path_count[k];
     return 0;
 }
 
@@ -3771,6 +3888,7 @@ int sentinel_set_occupy_timeout(sentinel_engine_t *e, int32_t timeout_ms) {
 // only a batch that could cross it reads the device counts and compacts the tombstones (a sync).
 static int submit_concurrent(sentinel_engine_t *e, int64_t n, const ConcEvent *dev, uint64_t *dout, hipStream_t s) {
     if (n <= 0) return 0;
+    if (int rc0 = check_dev_err(e, s)) return rc0;
     if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
     int rc = e->ensure_tokens();
     if (rc) return rc;
@@ -3791,10 +3909,6 @@ static int submit_concurrent(sentinel_engine_t *e, int64_t n, const ConcEvent *d
             // costs one host synchronisation; releases empty their slots, so it rarely needs a sweep)
             uint64_t nc = e->tcap;
             while ((double)(counts[0] + 4 * (uint64_t)n) > 0.75 * (double)nc && nc < ((uint64_t)1 << 32)) nc <<= 1;
-#ifndef SENTINEL_TOK_HEADROOM
-#define SENTINEL_TOK_HEADROOM 4
-#endif
-            while ((double)(counts[0] + SENTINEL_TOK_HEADROOM * (uint64_t)n) > 0.75 * (double)nc && nc < ((uint64_t)1 << 28)) nc <<= 1;
             rc = e->rebuild_tokens_device(nc, s);
             if (rc) return rc;
             e->tok_ub = counts[0];
@@ -3821,7 +3935,8 @@ static int submit_concurrent(sentinel_engine_t *e, int64_t n, const ConcEvent *d
     }
     char *gb = e->w_cbig.as<char>();
     uint32_t *ctl = e->w_counters.as<uint32_t>();               // [0] tile ticket, [1] fallback segments
-    const ConcScan S{(unsigned long long *)(gb + o_desc), ctl, (uint32_t *)(gb + o_ser), (int32_t *)(gb + o_fin)};
+    const ConcScan S{(unsigned long long *)(gb + o_desc), ctl, (uint32_t *)(gb + o_ser), (int32_t *)(gb + o_fin),
+                     e->h_dev_err + 1};
     e->launch("conc_prep", n, s, [&] {
         k_conc_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(n, dev, F, TT, dout, fkey, finvalid,
                                                                       e->w_fhist.as<uint32_t>(), nb, aux, S.desc, nt);
@@ -4128,6 +4243,7 @@ int sentinel_param_top_values(sentinel_engine_t *e, int64_t ts, int32_t number, 
     const int32_t R = (int32_t)e->prules.size();
     int rc = param_top(e, ts, number, e->stream);
     if (rc) return rc;
+    HIP_OK(hipStreamSynchronize(e->stream));     // e->stream is non-blocking: the null-stream copies below do not wait for it
     std::vector<int64_t> sum((size_t)R * number);
     if (R > 0) {
         HIP_OK(hipMemcpy(count, e->topw.dc.p, (size_t)R * 4, hipMemcpyDeviceToHost));

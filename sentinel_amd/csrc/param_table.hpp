@@ -203,8 +203,11 @@ __global__ __launch_bounds__(256) void k_ptop_sums(PSlots T, uint64_t cap, int32
             const int n = rn[rg];
             if (j < n) {
                 const int64_t E = epoch_of(ts, rw[rg], rrcp[rg]);
-                const longlong2 b = ((const longlong2 *)(T.state + (int64_t)(base + p) * T.stride))[j];
-                if (b.x != EPOCH_ABSENT && b.x > E - n) part = (uint64_t)b.y;
+                const longlong2 *run = (const longlong2 *)(T.state + (int64_t)(base + p) * T.stride);
+                for (int jj = j; jj < n; jj += 16) {              // n > 16: lane j also sums pairs j + 16, ...
+                    const longlong2 b = run[jj];
+                    if (b.x != EPOCH_ABSENT && b.x > E - n) part += (uint64_t)b.y;
+                }
             }
         }
 #pragma unroll

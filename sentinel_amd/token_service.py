@@ -650,6 +650,12 @@ class GpuTokenService:
         check(self._L.sentinel_param_cm_stats(self._h, _p(out)), "param_cm_stats")
         return dict(key_walk=int(out[0]), overflow=int(out[1]))
 
+    def flow_path_stats(self):
+        """Flow batches so far by pipeline: {small, sorted, partition (prep + scan + scatter), split (one sweep)}."""
+        out = np.zeros(4, dtype=np.int64)
+        check(self._L.sentinel_flow_path_stats(self._h, _p(out)), "flow_path_stats")
+        return dict(small=int(out[0]), sorted=int(out[1]), partition=int(out[2]), split=int(out[3]))
+
     def param_top_values(self, ts: int, number: int = _lib.TOP_PARAMS):
         """getTopValues(number) of every param rule at ts -> list (per rule index) of [(key, avg)]."""
         n_rules = self.param_count()

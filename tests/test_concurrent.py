@@ -296,3 +296,37 @@ def test_gpu_concurrent_mixed_amounts_tombstone_reuse(oracle_mod, monkeypatch):
             assert svc.concurrent_now_calls(f) == orc.concurrent_now_calls(f), (b, f)
         assert svc.concurrent_token_count() == orc.concurrent_token_count()
     assert (st_o == 6).any() and (st_o == 1).any() and (st_o == 0).any()
+
+
+@pytest.mark.gpu
+def test_gpu_token_inserts_contended(oracle_mod, monkeypatch):
+    """Many passing acquires inserting into a small token cache at once (12k inserts into 16384 slots,
+    every acquire admitted): lost CASes on shared probe paths are the common case here.  Round 4's
+    r04e / r04f hang was token_insert re-reading a slot with a plain load after
+    losing its CAS: the CU's L1 kept answering the stale free key, so the lane retried the same slot
+    up to capacity times.  Bit-exact statuses, unique tokens, and every token released afterwards."""
+    import sentinel_amd as sa
+    from sentinel_amd.token_service import ServerNamespace
+    monkeypatch.setenv("SENTINEL_TOKEN_CAPACITY", "16384")
+    F = 64
+    rules = [_rule(int(f), 1e6, 1) for f in range(1, F + 1)]
+    svc = sa.GpuTokenService(0)
+    svc.set_namespaces([ServerNamespace(connected_count=1)])
+    svc.load_flow_rules([sa.FlowRule(count=r["count"], cluster_config=sa.ClusterFlowConfig(
+        flow_id=r["flow_id"], threshold_type=r["threshold_type"])) for r in rules])
+    orc = oracle_mod.TokenServiceOracle(rules, namespaces=[dict(connected_count=1)])
+    rng = np.random.default_rng(5)
+    n = 12_000
+    fidx = rng.integers(0, F, n).astype(np.int32)
+    acq = np.ones(n, np.int32)
+    kind = np.zeros(n, np.int32)
+    flags = np.ones(n, np.uint32)
+    st_g, tok_g = svc.submit_concurrent_batch_host(fidx, acq, np.zeros(n, np.int64), kind, flags)
+    ev = np.zeros(n, dtype=orc.CONC_EVENT)
+    ev["flow_idx"], ev["acquire"], ev["token_id"], ev["kind"], ev["flags"] = fidx, acq, 0, kind, flags
+    st_o, _ = orc.concurrent_replay(ev, tok_g)
+    assert np.array_equal(st_g, st_o) and (st_g == 0).all()
+    assert len(np.unique(tok_g)) == n and svc.concurrent_token_count() == n
+    rel = np.ones(n, np.int32)
+    st_r, _ = svc.submit_concurrent_batch_host(fidx, acq, tok_g, rel, flags)
+    assert (st_r == 6).all() and svc.concurrent_token_count() == 0

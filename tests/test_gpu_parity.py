@@ -12,12 +12,14 @@ from sentinel_amd import trace as T
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["sorted", "partition", "small"])
+@pytest.fixture(autouse=True, params=["sorted", "partition", "partition3", "small"])
 def flow_path(request, monkeypatch):
     """Every flow parity case runs on every flow pipeline: the global radix sort, the
-    partition-local path and the one-launch small-batch kernel over 4096-event chunks
-    (SENTINEL_FLOW_PATH is read when an engine is created)."""
-    monkeypatch.setenv("SENTINEL_FLOW_PATH", request.param)
+    partition-local path with its one-sweep front (k_part_split, batches of >= 64K events) and with
+    prep + scan + scatter (SENTINEL_PART_SPLIT=0), and the one-launch small-batch kernel over
+    4096-event chunks (both variables are read when an engine is created)."""
+    monkeypatch.setenv("SENTINEL_FLOW_PATH", "partition" if request.param == "partition3" else request.param)
+    monkeypatch.setenv("SENTINEL_PART_SPLIT", "0" if request.param == "partition3" else "1")
     return request.param
 
 

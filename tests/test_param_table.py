@@ -97,13 +97,15 @@ def test_config4_full_size_bitexact(oracle_mod, universe):
           f"over_capacity_bucket={orc.param_overflowed()} table={svc.param_table_stats()}")
 
 
-def test_top_values_match_oracle(oracle_mod):
+@pytest.mark.parametrize("sample_count,interval_ms", [(4, 1000), (20, 1000), (32, 1600)])
+def test_top_values_match_oracle(oracle_mod, sample_count, interval_ms):
     """ClusterParamMetric.getTopValues(5) of every rule (the snapshot's param leg) equals the oracle's,
-    which is pinned by ClusterParamMetricTest (tests/golden/kat_cluster_param_metric.json)."""
+    which is pinned by ClusterParamMetricTest (tests/golden/kat_cluster_param_metric.json).  Sample
+    counts above 16 take k_ptop_sums' lanes over more than one pair of the window."""
     R = 300
     rng = np.random.default_rng(8)
-    prules = [dict(flow_id=7000 + r, count=float(rng.integers(20, 200)), sample_count=4, window_interval_ms=1000)
-              for r in range(R)]
+    prules = [dict(flow_id=7000 + r, count=float(rng.integers(20, 200)), sample_count=sample_count,
+                   window_interval_ms=interval_ms) for r in range(R)]
     svc = _svc(prules)
     orc = oracle_mod.TokenServiceOracle([], param_rules=prules)
     m = 200_000
