@@ -82,8 +82,10 @@ PMC_DIR = os.path.join(ROOT, "profiles", "pmc")
 
 def pmc_traffic(kernel: str, shape: dict):
     """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary of THIS workload shape
-    (profiles/pmc/*.json written by scripts/pmc_summary.py: separate FETCH_SIZE / WRITE_SIZE passes,
-    FETCH doubled on gfx950); None when no PMC run of this shape exists."""
+    (profiles/pmc/*.json written by scripts/pmc_summary.py; since round 5 from the memory-side request
+    counters by request size -- scripts/gpu_pmc_req.sh, reads 128 / 64 / 32 B per request, writes 64 / 32 B,
+    calibrated on known-byte patterns by tools/pmc_calib.cpp -- the newest file of the shape wins); None
+    when no PMC run of this shape exists."""
     try:
         files = sorted(os.listdir(PMC_DIR))
     except OSError:
@@ -103,7 +105,7 @@ def pmc_traffic(kernel: str, shape: dict):
                 tot += v["traffic_bytes_avg"] * v["dispatches"]
                 disp += v["dispatches"]
         if disp:
-            return round(tot / disp, 1), f"profiles/pmc/{fn}"
+            return round(tot / disp, 1), f"profiles/pmc/{fn}: {summ.get('correction', '')}"
     return None, None
 
 
@@ -904,7 +906,7 @@ def main():
         traffic, traffic_src = pmc_traffic(dom, W.shape())
         roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of this workload shape: "
+                "traffic_unit": "HBM bytes per launch (rocprofv3 memory-side requests of this workload shape: "
                                 + (traffic_src or "no PMC run of this shape -> null") + ")",
                 "algorithmic_bytes_per_launch": round((bpe or 0.0) * d["units_per_call"], 1),
                 "bytes_per_event": bpe, "avg_us": round(d["avg_us"], 2)}

@@ -13,7 +13,11 @@ TAG=$1; shift
 O=$R/gpurun_out/pmcreq_$TAG
 mkdir -p $O
 P=$1; shift
-case $P in python|python3) P=$(command -v python3) ;; /*) ;; *) P=$R/$P ;; esac
+case $P in
+  python|python3) P=$(command -v python3); S=$1; shift; case $S in /*) ;; *) S=$R/$S ;; esac; set -- "$S" "$@" ;;
+  /*) ;;
+  *) P=$R/$P ;;
+esac
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 150 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum \
   --output-format csv -d $O/rd -o run -- $P "$@" > $O/rd.out 2> $O/rd.err || { tail -20 $O/rd.err; exit 1; }

@@ -601,9 +601,10 @@ struct sentinel_engine {
     // range > 8x the mean): then the sorted path for the next 1024 batches, then one probe again
     DevBuf d_part_stat;
     unsigned long long *h_part_stat = nullptr;   // pinned mirror, written asynchronously after each batch
-    // one-sweep partition (k_part_split): digit columns + totals, the monotonic arrival counter, the
-    // pinned barrier-timeout word; SENTINEL_PART_SPLIT=0 keeps prep + scan + scatter
-    bool part_split = true;
+    // one-sweep partition (k_part_split): digit columns + totals, the monotonic arrival counter.  Off by
+    // default (SENTINEL_PART_SPLIT=1 turns it on): measured at config 3 it takes 134 us per 8M batch
+    // against 130 us for prep + scan + scatter
+    bool part_split = false;
     int64_t flow_path_count[4] = {0, 0, 0, 0};   // small, sorted, partition 3-pass, partition one-sweep
     int num_cu = 0;
     DevBuf w_split_col, d_split_bar;
@@ -2525,7 +2526,7 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
     if (const char *c = getenv("SENTINEL_ROUTE8")) e->use_route8 = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_LIM1")) e->lim1 = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_PROC_OCC")) e->process_occ = std::string(c) != "0";
-    if (const char *c = getenv("SENTINEL_PART_SPLIT")) e->part_split = std::string(c) != "0";
+    if (const char *c = getenv("SENTINEL_PART_SPLIT")) e->part_split = std::string(c) == "1";
     if (hipDeviceGetAttribute(&e->num_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) e->num_cu = 0;
     if (const char *c = getenv("SENTINEL_PARAM_CAPACITY")) {
         uint64_t v = strtoull(c, nullptr, 10);

@@ -327,9 +327,12 @@ static_assert(SP_TILE == 1 << SP_LOC_BITS && SP_LOC_BITS + PART_MAX_BITS <= 28, 
 typedef __attribute__((address_space(1))) uint32_t sp_gu32;
 #ifdef SENTINEL_SPLIT_STAMPS      // cost diagnostic (tools/split_bench.cpp): wall-clock stamps per workgroup and phase
 __device__ unsigned long long g_split_stamp[1024][8];
+__device__ unsigned long long g_split_round[1024][4];
 #define SP_STAMP(i) do { if (threadIdx.x == 0) g_split_stamp[blockIdx.x][i] = wall_clock64(); } while (0)
+#define SP_RSTAMP(i) do { const unsigned long long now_ = wall_clock64(); if (threadIdx.x == 0) g_split_round[blockIdx.x][i] += now_ - rt_; rt_ = now_; } while (0)
 #else
 #define SP_STAMP(i) do { } while (0)
+#define SP_RSTAMP(i) do { } while (0)
 #endif
 
 __device__ inline void sp_put(uint32_t *p, uint32_t v) {
@@ -500,6 +503,10 @@ __global__ __launch_bounds__(SP_THREADS) void k_part_split(
     };
     load_round(0);
     SP_STAMP(6);
+#ifdef SENTINEL_SPLIT_STAMPS
+    unsigned long long rt_ = wall_clock64();
+    if (t < 4) g_split_round[g][t] = 0;
+#endif
 #pragma unroll 1
     for (int r = 0; r < NR; ++r) {
         for (uint32_t d = t; d < (uint32_t)(SP_WAVES * PART_BINS / 2); d += SP_THREADS)
@@ -528,6 +535,7 @@ __global__ __launch_bounds__(SP_THREADS) void k_part_split(
         }
         if (r + 1 < NR) load_round(r + 1);            // the next round's events in flight from here on
         sp_lds_sync();
+        SP_RSTAMP(0);
         // per digit: exclusive over the waves (in place) and the round's count; the digits' staged starts
         uint32_t run = 0;
 #pragma unroll
@@ -539,6 +547,7 @@ __global__ __launch_bounds__(SP_THREADS) void k_part_split(
         uint32_t total;
         soff[t] = sp_block_exclusive_scan(run, waves_tot, &total);
         sp_lds_sync();
+        SP_RSTAMP(1);
 #pragma unroll
         for (int q = 0; q < SP_RITEMS; ++q) {
             if (v[q] == ~0ull) continue;
@@ -546,6 +555,7 @@ __global__ __launch_bounds__(SP_THREADS) void k_part_split(
             stage[soff[d] + cnt[wave][d] + rk[q]] = v[q];
         }
         sp_lds_sync();
+        SP_RSTAMP(2);
         const int64_t rbase = cbase + (int64_t)r * SP_TILE;
         for (uint32_t p = t; p < total; p += SP_THREADS) {
             const uint64_t x = stage[p];
@@ -558,6 +568,7 @@ __global__ __launch_bounds__(SP_THREADS) void k_part_split(
 #endif
         }
         sp_lds_sync();
+        SP_RSTAMP(3);
         goff[t] += run;
     }
 #ifdef SENTINEL_SPLIT_STAMPS

@@ -330,3 +330,53 @@ def test_gpu_token_inserts_contended(oracle_mod, monkeypatch):
     rel = np.ones(n, np.int32)
     st_r, _ = svc.submit_concurrent_batch_host(fidx, acq, tok_g, rel, flags)
     assert (st_r == 6).all() and svc.concurrent_token_count() == 0
+
+
+@pytest.mark.gpu
+def test_conc_bench_shape_bitexact(oracle_mod):
+    """The bench's own 5conc shape (bench.py ConcWorkload): 20k thread-grade rules (count~U{50..5000}),
+    Zipf(1.1) flows, 4M-event batches of which half acquire one token and half release, at fixed
+    positions, the tokens the previous batch handed out (blocked acquires hold none: ALREADY_RELEASE);
+    3 batches on the device-pointer path, every status, every flow's nowCalls and the cache size against
+    the oracle's sequential replay with the engine's token ids."""
+    import sentinel_amd as sa
+    rng = np.random.default_rng(55)
+    F = 20_000
+    rules = T.make_rules(F, rng, count_lo=50, count_hi=5000, sample_count=1, window_interval_ms=1000)
+    svc = sa.GpuTokenService(0)
+    svc.load_rules_array(rules.flow_id, rules.count, rules.threshold_type, rules.sample_count,
+                         rules.window_interval_ms, rules.namespace, rules.checker)
+    orc = oracle_mod.TokenServiceOracle.from_arrays(rules.flow_id, rules.count, rules.threshold_type,
+                                                    rules.sample_count, rules.window_interval_ms, rules.namespace,
+                                                    rules.checker)
+    N = 4 * 1024 * 1024
+    perm = rng.permutation(N)
+    acq_pos, rel_pos = np.sort(perm[: N // 2]), np.sort(perm[N // 2:])
+    rel_src = acq_pos[rng.permutation(len(acq_pos))[: len(rel_pos)]]
+    w = 1.0 / np.power(np.arange(1, F + 1, dtype=np.float64), 1.1)
+    cdf = np.cumsum(w) / w.sum()
+    zperm = np.random.default_rng(9).permutation(F).astype(np.int32)
+    erng = np.random.default_rng(3000)
+    prev_tok = np.zeros(N, np.int64)
+    for b in range(3):
+        fidx = zperm[np.minimum(np.searchsorted(cdf, erng.random(N), side="right"), F - 1)]
+        kind = np.zeros(N, np.int32)
+        kind[rel_pos] = 1
+        tok = np.zeros(N, np.int64)
+        tok[rel_pos] = prev_tok[rel_src]
+        acq = np.ones(N, np.int32)
+        flags = np.ones(N, np.int32)
+        st_g, tok_g = _device_batch(svc, fidx, acq, tok, kind, flags)
+        ev = np.zeros(N, dtype=orc.CONC_EVENT)
+        ev["flow_idx"], ev["acquire"], ev["token_id"], ev["kind"], ev["flags"] = fidx, acq, tok, kind, flags
+        st_o, _ = orc.concurrent_replay(ev, tok_g)
+        bad = np.nonzero(st_g != st_o)[0]
+        assert len(bad) == 0, (b, len(bad), bad[:5], st_g[bad[:5]], st_o[bad[:5]], kind[bad[:5]])
+        ok = st_g == 0
+        assert len(np.unique(tok_g[ok])) == int(ok.sum())
+        if b > 0:
+            assert {0, 1, 6, 7} <= set(np.unique(st_g).tolist())
+        for f in range(0, F, 37):
+            assert svc.concurrent_now_calls(f) == orc.concurrent_now_calls(f), (b, f)
+        assert svc.concurrent_token_count() == orc.concurrent_token_count()
+        prev_tok = np.where(ok, tok_g, 0)
