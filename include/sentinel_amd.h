@@ -647,6 +647,9 @@ int  sentinel_param_table_stats(sentinel_engine_t *eng, int64_t *out3);
 /* Shared count-min sketch batches so far: {decided by the two-phase key walk, sent to the per-rule lanes
  * because one key-hash sub-range held more requests than one LDS chunk}. */
 int  sentinel_param_cm_stats(sentinel_engine_t *eng, int64_t *out2);
+/* ... of the key-walk batches, those decided by the block-owned walk (each sketch block staged in LDS by
+ * one workgroup: k_pp_cm_block). */
+int  sentinel_param_cm_block_batches(sentinel_engine_t *eng, int64_t *out);
 /* Flow batches so far by pipeline: {small (one launch), sorted (radix sort), partition with prep + scan +
  * scatter, partition with the one-sweep split (k_part_split)}. */
 int  sentinel_flow_path_stats(sentinel_engine_t *eng, int64_t *out4);

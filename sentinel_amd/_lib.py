@@ -52,7 +52,7 @@ EXPORTS = [
     "sentinel_load_local_resources", "sentinel_submit_local_entry_batch", "sentinel_submit_local_entry_batch_host",
     "sentinel_local_node_stats", "sentinel_set_occupy_timeout", "sentinel_profile_select", "sentinel_profile_gate", "sentinel_set_flow_path",
     "sentinel_param_top_values", "sentinel_param_snapshot_device", "sentinel_flow_window", "sentinel_metric_count",
-    "sentinel_reset_metrics", "sentinel_param_table_stats", "sentinel_param_cm_stats", "sentinel_flow_path_stats", "sentinel_param_count",
+    "sentinel_reset_metrics", "sentinel_param_table_stats", "sentinel_param_cm_stats", "sentinel_param_cm_block_batches", "sentinel_flow_path_stats", "sentinel_param_count",
     "sentinel_batcher_request_token_async", "sentinel_submit_flow_batches", "sentinel_profile_every",
     "sentinel_set_local_param_grades", "sentinel_submit_local_param_batch_ex", "sentinel_submit_local_param_batch_ex_host",
     "sentinel_load_local_resources_ex", "sentinel_submit_local_batch", "sentinel_submit_local_batch_host",
@@ -266,6 +266,7 @@ def load():
         "sentinel_param_table_stats": (C.c_int, [vp, vp]),
         "sentinel_param_cm_stats": (C.c_int, [vp, vp]),
         "sentinel_flow_path_stats": (C.c_int, [vp, vp]),
+        "sentinel_param_cm_block_batches": (C.c_int, [vp, vp]),
         "sentinel_param_count": (i32, [vp]),
         "sentinel_batcher_request_token_async": (C.c_int, [vp, i64, i32, i32, i64, vp, vp, C.c_uint64]),
         "sentinel_param_interner_create": (C.c_int, [C.POINTER(vp)]),

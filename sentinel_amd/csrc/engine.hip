@@ -657,6 +657,11 @@ struct sentinel_engine {
     DevBuf d_cmband;                   // [0] overflow flag, [1..3] E_hi, E_hi seen by the read, the batch's newest epoch
     bool cm_keys = true;               // shared sketch: the two-phase key walk (k_pp_cm_read / _walk) when allowed
     uint64_t cm_key_batches = 0;       // shared-sketch batches decided by the key walk
+    uint64_t cm_block_batches = 0;     // ... of which by the block-owned walk (k_pp_cm_block)
+    bool cm_block = true;              // SENTINEL_CM_BLOCK=0: the two-phase global-atomic key walk instead
+    bool cm_debug = false;             // SENTINEL_CM_DEBUG=1: the key walk's geometry on stderr
+    int cm_diag = 0;                   // SENTINEL_CM_DIAG: k_pp_cm_block cost diagnostics (wrong results)
+    DevBuf w_cmsub;                    // block walk: per sub-range {first record, records}
     uint64_t cm_overflows = 0;         // ... sent to the per-rule lanes (a sub-range over PG_CAP requests)
     uint64_t p_ord = 0;                // param batches reserved so far
     uint64_t p_reset_ord = 0;          // first batch ordinal after d_pfresh was last zeroed
@@ -878,7 +883,13 @@ struct sentinel_engine {
                          d_prule_Is.as<double>(), d_prule_thr.as<double>(),
                          has_hot ? d_hot_table.as<unsigned long long>() : nullptr, hot_mask, d_hot_thr.as<double>()};
         C.PT = table(pt, 1, param_stride(pmax_n));
-        C.CM = CountMin{d_cm.as<uint64_t>(), cm_depth, cm_width, cm_slots(), pmode == SENTINEL_PARAM_COUNT_MIN_SHARED};
+        {
+            const uint32_t cols = std::min<uint32_t>(cm_width, CM_BLOCK_COLS);
+            int cb = 0;
+            while (((uint32_t)cols << cb) < cm_width) ++cb;
+            C.CM = CountMin{d_cm.as<uint64_t>(), cm_depth, cm_width, cm_slots(), pmode == SENTINEL_PARAM_COUNT_MIN_SHARED,
+                            cb, cols};
+        }
         C.L = LocalRules{d_lrule_valid.as<uint8_t>(), d_lrule_tok.as<int64_t>(), d_lrule_burst.as<int64_t>(),
                          d_lrule_dur.as<int64_t>(), lhas_hot ? d_lhot_keys.as<unsigned long long>() : nullptr,
                          lhot_mask, d_lhot_tok.as<int64_t>(), d_lstate.as<int64_t>(),
@@ -2121,10 +2132,24 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
     // about one sub-range per 4M-request batch)
     int sbits = 0;
     while (sbits < 8 && (int64_t)P * ((int64_t)1 << sbits) * (PG_CAP / 2) < n) ++sbits;
+    // block-owned walk (k_pp_cm_block) when a sketch block fits LDS; sub-ranges are made narrow enough
+    // (up to 2^8 per range) that one spans at most 4 blocks
+    const size_t blk_bytes = (size_t)C.CM.depth * C.CM.cols * (size_t)C.CM.nmax * 8;
+    bool use_block = e->cm_block && C.CM.shared && C.CM.depth <= 4 && blk_bytes <= 49152 && e->pmax_n <= 16;
+    if (use_block)
+        while (sbits < 8 && pbits + sbits + 2 < C.CM.cbits) ++sbits;
+    const int sb = pbits + sbits;
+    use_block = use_block && sb + 2 >= C.CM.cbits;
+    if (e->cm_debug)
+        fprintf(stderr, "[sentinel] cm key walk: n=%lld pbits=%d sbits=%d cbits=%d cols=%u depth=%d nmax=%d pmax_n=%d "
+                        "shared=%d blk_bytes=%zu block=%d\n", (long long)n, pbits, sbits, C.CM.cbits, C.CM.cols,
+                C.CM.depth, C.CM.nmax, e->pmax_n, (int)C.CM.shared, blk_bytes, (int)use_block);
     const unsigned ggrid = (unsigned)(((P + 7) / 8) * 8 * (1 << sbits));
     uint64_t *gval = e->w_hep.as<uint64_t>();
-    const PKeyRecs RC{e->w_segep.as<unsigned long long>(), e->w_s0.as<uint2>(), e->w_k.as<int32_t>(),
-                      e->w_counters.as<uint32_t>(), flag};
+    if (use_block && e->w_cmsub.ensure(((size_t)P << sbits) * sizeof(uint2))) return SENTINEL_E_NOMEM;
+    PKeyRecs RC{e->w_segep.as<unsigned long long>(), e->w_s0.as<uint2>(), e->w_k.as<int32_t>(),
+                e->w_counters.as<uint32_t>(), flag};
+    if (use_block) RC.sub = e->w_cmsub.as<uint2>();
     const PSlots S{};
     e->launch("param_group", n, s, [&] {
         k_pp_group<2, true><<<ggrid, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, pbits, sbits, ev, C.R, RR, S, out,
@@ -2139,6 +2164,17 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
     ++e->cm_key_batches;
     const int32_t nsc = e->pmax_n;
     int64_t *mv = e->w_sval.as<int64_t>();                // (the packed values are dead after the grouping)
+    if (use_block) {
+        ++e->cm_block_batches;
+        k_set_i64<<<1, 64, 0, s>>>(ctl + 2, (long long)CM_EHI_NONE);
+        e->launch("param_cm_block", n, s, [&] {
+            const dim3 g(1u << C.CM.cbits);
+            k_pp_cm_block<<<g, 256, blk_bytes, s>>>(RC, sb, gval, ev, C.R, RR, C.CM, mv, ctl, out, e->cm_diag);
+        });
+        k_pp_cm_ehi<<<1, 64, 0, s>>>(ctl);
+        HIP_OK(hipGetLastError());
+        return 0;
+    }
     const unsigned wg = (unsigned)std::min<int64_t>(2048, (n + 255) / 256);
     const bool d4 = C.CM.depth <= 4;
     e->launch("param_cm_read", n, s, [&] {
@@ -2527,6 +2563,9 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
     if (const char *c = getenv("SENTINEL_LIM1")) e->lim1 = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_PROC_OCC")) e->process_occ = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_PART_SPLIT")) e->part_split = std::string(c) == "1";
+    if (const char *c = getenv("SENTINEL_CM_BLOCK")) e->cm_block = std::string(c) != "0";
+    if (const char *c = getenv("SENTINEL_CM_DEBUG")) e->cm_debug = std::string(c) == "1";
+    if (const char *c = getenv("SENTINEL_CM_DIAG")) e->cm_diag = atoi(c);
     if (hipDeviceGetAttribute(&e->num_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) e->num_cu = 0;
     if (const char *c = getenv("SENTINEL_PARAM_CAPACITY")) {
         uint64_t v = strtoull(c, nullptr, 10);
@@ -2976,6 +3015,13 @@ int sentinel_param_cm_stats(sentinel_engine_t *e, int64_t *out2) {
     std::lock_guard<std::mutex> g(e->mu);
     out2[0] = (int64_t)e->cm_key_batches;
     out2[1] = (int64_t)e->cm_overflows;
+    return 0;
+}
+
+int sentinel_param_cm_block_batches(sentinel_engine_t *e, int64_t *out) {
+    if (!e || !out) return fail(SENTINEL_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(e->mu);
+    *out = (int64_t)e->cm_block_batches;
     return 0;
 }
 
@@ -4133,8 +4179,7 @@ int sentinel_param_sum(sentinel_engine_t *e, int32_t ridx, uint64_t pkey, int64_
     if (e->pmode != SENTINEL_PARAM_EXACT) {   // the sketch estimate (min over rows of the window sum)
         const int n = e->h_prule_n[ridx];
         const int64_t E = ts / (e->h_prule_interval[ridx] / n);
-        const CountMin C{e->d_cm.as<uint64_t>(), e->cm_depth, e->cm_width, e->cm_slots(),
-                         e->pmode == SENTINEL_PARAM_COUNT_MIN_SHARED};
+        const CountMin C = e->param_ctx().CM;
         int64_t est = INT64_MAX;
         std::vector<uint64_t> cell(e->cm_slots());
         for (int d = 0; d < e->cm_depth; ++d) {

@@ -447,6 +447,9 @@ struct PKeyRecs {
     int32_t *rule;
     uint32_t *count;         // records written (zeroed by k_pp_prep)
     unsigned long long *overflow;   // shared count-min: set when a sub-range exceeds one chunk (else null)
+    // shared count-min block walk (k_pp_cm_block): non-null = each sub-range's records are written at
+    // their sub-range's first grouped-value position, sub[(range << sbits) | sub-range] = {first, count}
+    uint2 *sub = nullptr;
 };
 
 // k_pp_group: one workgroup per (range, sub-range): the S = 2^sbits workgroups of a range read the
@@ -490,6 +493,8 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
     uint32_t below = 0;                                                  // this thread's requests of lower sub-ranges
     bool slow = false;                                                   // a chunk was decided before the scan ended
     uint32_t m = 0;                                                      // compacted requests (block-uniform)
+    uint32_t kemit = 0;                                                  // records emitted (block-uniform)
+    uint32_t kbase = 0;
     PF_STAMP(0);
 
     // decide / emit cq[0, m): rounds while the LDS table is full for some key
@@ -571,7 +576,7 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
             const uint32_t nkeys = total >> 16;
             const uint32_t placed = total & 0xFFFFu;
             if (t == 0) hstart[PD_HT] = placed;
-            if (emit && t == 0) s_rbase = atomicAdd(RC.count, nkeys);
+            if (emit && t == 0 && !RC.sub) s_rbase = atomicAdd(RC.count, nkeys);
             __syncthreads();
 #pragma unroll
             for (int j = 0; j < PG_ITEMS; ++j) {
@@ -590,7 +595,8 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
             [[maybe_unused]] const unsigned long long pt2 = PD_NOW();
             if (emit) {
                 for (uint32_t i = t; i < placed; i += PD_THREADS) gval[gbase + roff + i] = sv[i];
-                const uint32_t rb = s_rbase;
+                const uint32_t rb = RC.sub ? gbase + kemit : s_rbase;      // (records <= requests: inside the run)
+                kbase = gbase;
                 for (uint32_t q = t; q < nkeys; q += PD_THREADS) {
                     const uint32_t e = klist[q];
                     RC.key[rb + q] = hkey[e];
@@ -605,6 +611,7 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
                 }
             }
             roff += placed;
+            if (emit) kemit += nkeys;
             const int more = __syncthreads_or(pend != 0);                // (also: done with the LDS)
             [[maybe_unused]] const unsigned long long pt3 = PD_NOW();
             PD_ACC(4, pt1 - pt0);
@@ -668,6 +675,7 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
             chunk(true, r0 + nb);
         }
     }
+    if (RC.sub && t == 0) RC.sub[(p << sbits) | sub] = make_uint2(kbase, kemit);
     PF_STAMP(3);
     block_add_global(fresh, nfresh, &s_fresh);
 }
@@ -936,6 +944,255 @@ __global__ __launch_bounds__(256) void k_pp_cm_walk(PKeyRecs RC, const uint64_t 
         emax = y > emax ? y : emax;
     }
     if (lane_id() == 0 && emax != CM_EHI_NONE) atomicMax(reinterpret_cast<long long *>(&ctl[2]), (long long)emax);
+}
+
+// ---------------------------------------------------------------- shared count-min, block-owned
+// k_pp_cm_block (round 5): the two phases above in one launch, one 256-thread workgroup per sketch
+// block.  Every cell of a key lies in its block (cm_cell: block = top cbits bits of mix64(key), the bits
+// the partition groups requests by), so a block's cells -- depth x cols x 2n slots, 40 KB at d = 4,
+// n = 10 -- are read from HBM once, staged in LDS, and written back once: the batch moves the sketch as
+// two coalesced streams instead of one memory-side atomic (a 128-B line read + a 64-B write) per row,
+// key and admitted epoch.  Inside the workgroup the phases are those of k_pp_cm_read / k_pp_cm_walk:
+//   A  every key's requests within n epochs of E_hi get M(E) = min over rows of the window sum, from
+//      the block as the earlier batches left it;
+//   B  (barrier: every read precedes every add) each key walks its requests with its own admitted
+//      counts in registers, and adds each epoch's count to its d cells with LDS CAS (cm_slot_add's ring
+//      semantics); keys of one block only meet in LDS.
+// The block's keys: the sub-range(s) whose top (pbits + sbits) hash bits it covers (records written at
+// deterministic positions by k_pp_group, RC.sub); when a sub-range is wider than a block, the block's
+// workgroup filters the sub-range's keys by block.  One-sidedness is unchanged.
+constexpr int CMB_DMAX = 4;                // rows of a block walk (the host checks depth <= 4)
+
+// a key's d cells in the LDS block: word offsets of slot 0 (computed once per key)
+__device__ inline void cm_lds_cells(uint32_t *co, int depth, int nmax, uint32_t cols, unsigned long long key) {
+#pragma unroll
+    for (int d = 0; d < CMB_DMAX; ++d) {
+        if (d >= depth) break;
+        const uint32_t col = (uint32_t)mix64(key + 0x9E3779B97F4A7C15ull * (uint64_t)(d + 1)) & (cols - 1);
+        co[d] = ((uint32_t)d * cols + col) * (uint32_t)nmax;
+    }
+}
+
+__device__ inline int64_t cm_lds_window_min(const unsigned long long *cl, const uint32_t *co, int depth, int nmax,
+                                            int nsc, int64_t E) {
+    int64_t m = INT64_MAX;
+    int js0 = (int)(E % nmax);                            // (epochs are >= 0)
+    js0 = js0 < 0 ? js0 + nmax : js0;
+#pragma unroll
+    for (int d = 0; d < CMB_DMAX; ++d) {
+        if (d >= depth) break;
+        const unsigned long long *c = cl + co[d];
+        int64_t sum = 0;
+        int js = js0;
+        for (int k = 0; k < nsc; ++k) {                   // the window's slots: epochs E .. E - n + 1
+            const uint64_t x = c[js];
+            if ((((uint32_t)E - (uint32_t)(x >> CM_COUNT_BITS)) & CM_TAG_MASK) < (uint32_t)nsc) sum += (int64_t)(x & CM_COUNT_MAX);
+            js = js == 0 ? nmax - 1 : js - 1;
+        }
+        m = sum < m ? sum : m;
+    }
+    return m;
+}
+
+__device__ inline void cm_lds_flush(unsigned long long *cl, const uint32_t *co, int depth, int nmax, int64_t E, int64_t a) {
+    const uint32_t js = (uint32_t)(E % nmax);
+    const uint32_t te = (uint32_t)E & CM_TAG_MASK;
+#pragma unroll
+    for (int d = 0; d < CMB_DMAX; ++d) {
+        if (d >= depth) break;
+        unsigned long long *c = cl + co[d] + js;
+        cm_slot_add(c, *c, te, a);                        // (LDS atomics: ds_cmpst_rtn_b64)
+    }
+}
+
+constexpr uint32_t CMB_VCAP = 640;        // grouped values (and their M) of one block staged in LDS; listed keys
+
+__global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64_t *gval,
+                                                      const ParamEvent *__restrict__ ev, ParamRules PR,
+                                                      const PRuleRec *__restrict__ RR, CountMin CM,
+                                                      int64_t *__restrict__ mv, long long *__restrict__ ctl,
+                                                      uint64_t *__restrict__ out, int diag) {
+    // diag (SENTINEL_CM_DIAG, cost diagnostics only -- wrong verdicts / counters): bit 0 no window reads,
+    // bit 1 no walk, bit 2 no block load / store, bit 3 no key list
+    extern __shared__ __attribute__((aligned(16))) unsigned long long cl[];   // depth x cols x nmax
+    __shared__ uint64_t sv[CMB_VCAP];                     // the block's keys' runs, compacted in key order
+    __shared__ int64_t sm[CMB_VCAP];                      // M(E) of each staged request (phase A)
+    __shared__ uint32_t klist[CMB_VCAP];                  // the block's key records, longest run first
+    __shared__ uint32_t khist[33];
+    __shared__ uint32_t s_waves[256 / WAVE];
+    const uint32_t b = blockIdx.x;
+    const uint32_t t = threadIdx.x;
+    const int64_t T0 = pp_t0(ev);
+    const int64_t ehi = ctl[0];
+    const int depth = CM.depth, nmax = CM.nmax;
+    const uint32_t cols = CM.cols;
+    const uint32_t words = (uint32_t)depth * cols * (uint32_t)nmax;
+    unsigned long long *gcl = reinterpret_cast<unsigned long long *>(CM.cells) + (uint64_t)b * words;
+    // this block's sub-ranges: [s0, s0 + ns); filter by block when a sub-range spans several blocks
+    const int cb = CM.cbits;
+    const uint32_t s0 = sb >= cb ? b << (sb - cb) : b >> (cb - sb);
+    const uint32_t ns = sb >= cb ? 1u << (sb - cb) : 1u;
+    const bool filter = sb < cb;
+    uint32_t nkeys = 0;
+    for (uint32_t s = s0; s < s0 + ns; ++s) nkeys += RC.sub[s].y;
+    if (nkeys == 0) return;                               // (block-uniform) no key: the block stays in HBM
+    if (!(diag & 4))
+        for (uint32_t i = t; i < words / 2; i += blockDim.x)
+            reinterpret_cast<ulonglong2 *>(cl)[i] = reinterpret_cast<const ulonglong2 *>(gcl)[i];
+    auto for_span = [&](auto &&f) {                       // every record of the block's keys
+        for (uint32_t s = s0; s < s0 + ns; ++s) {
+            const uint2 sr = RC.sub[s];
+            for (uint32_t i = t; i < sr.y; i += blockDim.x) {
+                const uint32_t r = sr.x + i;
+                const unsigned long long key = RC.key[r];
+                if (filter && cm_block_of(CM, key) != b) continue;
+                f(r, key);
+            }
+        }
+    };
+    // the keys listed by run length, longest first (a wave walks for as long as its longest run: this
+    // packs the long runs into the first waves); a block with more records than the list holds walks
+    // them in record order
+    const bool listed = nkeys <= CMB_VCAP && !(diag & 8);   // (block-uniform)
+    uint32_t nlisted = 0;
+    if (listed) {
+        if (t < 33) khist[t] = 0;
+        __syncthreads();
+        for_span([&](uint32_t r, unsigned long long) {
+            const uint32_t y = RC.run[r].y;
+            atomicAdd(&khist[31 - (y < 31 ? y : 31)], 1u);
+        });
+        __syncthreads();
+        if (t == 0) {
+            uint32_t acc = 0;
+            for (int i = 0; i < 32; ++i) { const uint32_t x = khist[i]; khist[i] = acc; acc += x; }
+            khist[32] = acc;
+        }
+        __syncthreads();
+        for_span([&](uint32_t r, unsigned long long) {
+            const uint32_t y = RC.run[r].y;
+            klist[atomicAdd(&khist[31 - (y < 31 ? y : 31)], 1u)] = r;
+        });
+        __syncthreads();
+        nlisted = khist[32];
+    }
+    auto for_keys = [&](auto &&f) {                       // (the same keys, in the same order, per thread)
+        if (listed) {
+            for (uint32_t i = t; i < nlisted; i += blockDim.x) {
+                const uint32_t r = klist[i];
+                f(r, RC.key[r]);
+            }
+        } else {
+            for_span(f);
+        }
+    };
+    // the staging offsets: this thread's keys' runs at [voff0, voff0 + myv) of sv / sm; a run that does
+    // not fit CMB_VCAP stays in HBM (gval, and its M in mv)
+    uint32_t myv = 0;
+    for_keys([&](uint32_t r, unsigned long long) { myv += RC.run[r].y; });
+    uint32_t vtot;
+    const uint32_t voff0 = block_exclusive_scan(myv, s_waves, &vtot);   // (its barriers: the block is in LDS)
+    // A. stage the runs; reads (the block as the earlier batches left it)
+    uint32_t vo = voff0;
+    for_keys([&](uint32_t r, unsigned long long key) {
+        const uint2 run = RC.run[r];
+        const bool lds = vo + run.y <= CMB_VCAP;
+        const PRuleRec rr = RR[RC.rule[r]];
+        const int nsc = rr.nf & 0xFFFF;
+        int64_t lastE = 0, lastM = 0;
+        bool have = false;
+        uint32_t co[CMB_DMAX];
+        cm_lds_cells(co, depth, nmax, cols, key);
+        RunQueue rq(gval, run.x, run.x + run.y);
+        for (uint32_t k = 0; k < run.y; ++k) {
+            const uint64_t v = rq.next();
+            if (lds) sv[vo + k] = v;
+            if (ehi == CM_EHI_NONE || (diag & 1)) continue;
+            int64_t tt;
+            int32_t a;
+            pp_unpack(v, T0, ev, tt, a);
+            const int64_t E = epoch_of(tt, rr.w, rr.rcp_w);
+            if (!cm_needs_read(E, ehi, nsc)) continue;
+            if (!have || E != lastE) {
+                lastM = cm_lds_window_min(cl, co, depth, nmax, nsc, E);
+                lastE = E;
+                have = true;
+            }
+            if (lds) sm[vo + k] = lastM;
+            else mv[run.x + k] = lastM;
+        }
+        vo += run.y;
+    });
+    __syncthreads();
+    // B. walks and adds.  A key's own admitted count inside the window (E - n, E] comes from prefix sums
+    // over its run: each request's slot of the staged run is overwritten with the epoch its admitted
+    // count is charged to (monotone along the run), its M slot with Q = the run's admitted sum before it;
+    // own(E) = Q - Q[lo], lo = the run's first request charged to an epoch > E - n.  Each (key, epoch)
+    // count is added to the block's d cells once, when the walk moves past the epoch (reads never see
+    // this batch's adds: they were all done in A).  A late request (E below the run's newest epoch:
+    // outside the precondition) counts every admitted request of the run before it (over, never under)
+    // and is charged to the newest epoch, as k_pp_cm_walk does.
+    int64_t emax = CM_EHI_NONE;
+    vo = voff0;
+    auto walk = [&](uint32_t n_, int64_t *eb, int64_t *qb, const uint64_t *vb, unsigned long long key,
+                    const PRuleRec &rr, double thr) {
+        const int nsc = rr.nf & 0xFFFF;
+        int64_t curE = EPOCH_ABSENT, cnt = 0, Q = 0;
+        uint32_t lo = 0;
+        uint32_t co[CMB_DMAX];
+        cm_lds_cells(co, depth, nmax, cols, key);
+        for (uint32_t k = 0; k < n_; ++k) {
+            const uint64_t v = vb[k];
+            int64_t tt;
+            int32_t a;
+            pp_unpack(v, T0, ev, tt, a);
+            const int64_t E = epoch_of(tt, rr.w, rr.rcp_w);
+            emax = E > emax ? E : emax;
+            const bool late = curE != EPOCH_ABSENT && E < curE;
+            if (!late && E != curE) {
+                if (cnt > 0) cm_lds_flush(cl, co, depth, nmax, curE, cnt);
+                curE = E;
+                cnt = 0;
+                while (lo < k && eb[lo] <= E - nsc) ++lo;
+            }
+            const int64_t own = late ? Q : (lo < k ? Q - qb[lo] : 0);
+            const int64_t m = cm_needs_read(E, ehi, nsc) ? qb[k] : 0;
+            qb[k] = Q;
+            eb[k] = curE;
+            const double next = remaining_of(thr, rr.I_s, m + own, a);
+            uint64_t vd;
+            if (!(next < 0.0)) {                                          // CPFC:64-66, then addValue
+                Q += a;
+                cnt += a;
+                vd = pack_verdict(ST_OK, java_d2i(next), 0);
+            } else {
+                vd = pack_verdict(ST_BLOCKED, 0, 0);
+            }
+            store_verdict(out, (uint32_t)v & SEQ_MASK, vd);
+        }
+        if (cnt > 0) cm_lds_flush(cl, co, depth, nmax, curE, cnt);
+    };
+    if (!(diag & 2)) for_keys([&](uint32_t r, unsigned long long key) {
+        const uint2 run = RC.run[r];
+        const bool lds = vo + run.y <= CMB_VCAP;
+        const int32_t rule = RC.rule[r];
+        const PRuleRec rr = RR[rule];
+        const double thr = (rr.nf >> 16) ? value_threshold(PR, (uint32_t)rule, key) : rr.thr;   // CPFC:101-120
+        if (lds)
+            walk(run.y, reinterpret_cast<int64_t *>(sv + vo), sm + vo, sv + vo, key, rr, thr);
+        else                                              // (the grouped values are dead after this walk)
+            walk(run.y, reinterpret_cast<int64_t *>(gval + run.x), mv + run.x, gval + run.x, key, rr, thr);
+        vo += run.y;
+    });
+    for (int o = WAVE / 2; o > 0; o >>= 1) {
+        const int64_t y = __shfl_xor(emax, o, WAVE);
+        emax = y > emax ? y : emax;
+    }
+    if (lane_id() == 0 && emax != CM_EHI_NONE) atomicMax(reinterpret_cast<long long *>(&ctl[2]), (long long)emax);
+    __syncthreads();
+    if (!(diag & 4))
+        for (uint32_t i = t; i < words / 2; i += blockDim.x)
+            reinterpret_cast<ulonglong2 *>(gcl)[i] = reinterpret_cast<const ulonglong2 *>(cl)[i];
 }
 
 // E_hi <- max(E_hi, this batch's newest epoch) (after k_pp_cm_walk); CM_EHI_ANY stays.

@@ -91,7 +91,13 @@ struct CountMin {
     uint32_t width;       // power of two
     int32_t nmax;         // slots per cell: n (per-rule sketch), 2 n (shared: a ring of two windows)
     bool shared;          // one sketch for every rule (param keys are unique per (rule, value))
+    // shared sketch, round 5: each row's width is cut into 2^cbits blocks of `cols` columns; a key's d
+    // cells all lie in block (top cbits bits of mix64(key)) -- the same bits the partition path groups
+    // requests by -- so one workgroup owns a block and stages it in LDS (k_pp_cm_block)
+    int32_t cbits;
+    uint32_t cols;
 };
+constexpr uint32_t CM_BLOCK_COLS = 64;       // columns per row in one block of the shared sketch
 
 constexpr int64_t LOCAL_ABSENT = INT64_MIN;   // CacheMap entry absent
 
@@ -261,10 +267,22 @@ constexpr int CM_COUNT_BITS = 40;
 constexpr uint64_t CM_COUNT_MAX = (1ull << CM_COUNT_BITS) - 1;
 constexpr uint32_t CM_TAG_MASK = (1u << 24) - 1;
 
+__host__ __device__ inline uint64_t cm_block_of(const CountMin &C, uint64_t key) {
+    return C.cbits ? mix64(key) >> (64 - C.cbits) : 0ull;
+}
+// Row d's cell of a key.  Per-rule sketch: column = an independent hash per row over the full width.
+// Shared sketch: block-major (block, row, column), the column an independent hash per row over the
+// block's `cols` columns -- a row still has width = 2^cbits x cols cells and two keys meet in a row
+// with probability 1 / width, but only keys of the same block can meet (the bound
+// is stated against the block's total count).
 __host__ __device__ inline uint64_t *cm_cell(const CountMin &C, uint32_t rule, int d, uint64_t key) {
-    const uint64_t col = mix64(key + 0x9E3779B97F4A7C15ull * (uint64_t)(d + 1)) & (uint64_t)(C.width - 1);
-    const uint64_t r = C.shared ? 0 : (uint64_t)rule;
-    return C.cells + ((r * (uint64_t)C.depth + (uint64_t)d) * C.width + col) * (uint64_t)C.nmax;
+    const uint64_t hd = mix64(key + 0x9E3779B97F4A7C15ull * (uint64_t)(d + 1));
+    if (C.shared) {
+        const uint64_t col = hd & (uint64_t)(C.cols - 1);
+        return C.cells + ((cm_block_of(C, key) * (uint64_t)C.depth + (uint64_t)d) * C.cols + col) * (uint64_t)C.nmax;
+    }
+    const uint64_t col = hd & (uint64_t)(C.width - 1);
+    return C.cells + (((uint64_t)rule * (uint64_t)C.depth + (uint64_t)d) * C.width + col) * (uint64_t)C.nmax;
 }
 
 // Window sum of one cell at epoch E: slots tagged with one of the epochs (E-n, E] (a tag 2^24

@@ -645,10 +645,13 @@ class GpuTokenService:
         return dict(capacity=int(out[0]), live=int(out[1]), rebuilds=int(out[2]))
 
     def param_cm_stats(self):
-        """{key_walk, overflow}: shared count-min batches decided by the key walk / by the per-rule lanes."""
+        """{key_walk, overflow, block}: shared count-min batches decided by the key walk / by the per-rule
+        lanes, and the key-walk batches decided by the block-owned walk (k_pp_cm_block)."""
         out = np.zeros(2, dtype=np.int64)
         check(self._L.sentinel_param_cm_stats(self._h, _p(out)), "param_cm_stats")
-        return dict(key_walk=int(out[0]), overflow=int(out[1]))
+        blk = np.zeros(1, dtype=np.int64)
+        check(self._L.sentinel_param_cm_block_batches(self._h, _p(blk)), "param_cm_block_batches")
+        return dict(key_walk=int(out[0]), overflow=int(out[1]), block=int(blk[0]))
 
     def flow_path_stats(self):
         """Flow batches so far by pipeline: {small, sorted, partition (prep + scan + scatter), split (one sweep)}."""

@@ -137,17 +137,20 @@ def test_count_min_is_one_sided(oracle_mod):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("levels", ["keys", "launch", "coop"])
+@pytest.mark.parametrize("levels", ["keys", "keys-global", "launch", "coop"])
 def test_shared_count_min_is_one_sided(oracle_mod, monkeypatch, levels):
     """One sketch for every rule (BASELINE config 4's layout), narrow enough that rules collide, on
-    batches spanning ~75 epochs.  "keys" (the default): the two-phase key walk, one lane per (rule, value)
-    key (k_pp_cm_read: every read of the batch, then k_pp_cm_walk: decisions and adds); "launch" /
-    "coop": one lane per rule moving through the epochs band by band (k_prule_cm_level / k_prule_cm_sync).
-    Either way no reset of a shared cell slot drops a count a check still needs -- zero violations of
-    one-sidedness, and the false-block rate shrinks with the width."""
+    batches spanning ~75 epochs.  "keys" (the default): the key walk, one lane per (rule, value) key,
+    every read of the batch before any add -- in one workgroup per sketch block staged in LDS
+    (k_pp_cm_block), or with "keys-global" in two launches on HBM cells (k_pp_cm_read, then k_pp_cm_walk:
+    decisions and memory-side atomic adds); "launch" / "coop": one lane per rule moving through the
+    epochs band by band (k_prule_cm_level / k_prule_cm_sync).  Either way no reset of a shared cell slot
+    drops a count a check still needs -- zero violations of one-sidedness, and the false-block rate
+    shrinks with the width."""
     import sentinel_amd as sa
     # the key walk (the default), one launch per band of rule lanes, or the grid barrier
-    monkeypatch.setenv("SENTINEL_CM_LEVELS", levels)
+    monkeypatch.setenv("SENTINEL_CM_LEVELS", "keys" if levels == "keys-global" else levels)
+    monkeypatch.setenv("SENTINEL_CM_BLOCK", "0" if levels == "keys-global" else "1")
     count, hot, rule_idx, vals, keys, ts = T.config4(200_000, seed=53, n_rules=5000, universe=200)
     acq = np.ones(len(ts), np.int32)
     rates = {}
@@ -160,6 +163,9 @@ def test_shared_count_min_is_one_sided(oracle_mod, monkeypatch, levels):
         viol, fb, dec = orc.param_cm_audit(rule_idx, acq, ts, np.arange(len(ts)), n1, keys, st)
         assert viol == 0 and dec == len(ts), (width, viol)
         rates[width] = fb / dec
+        cs = svc.param_cm_stats()
+        if levels.startswith("keys"):
+            assert cs["key_walk"] >= 1 and cs["block"] == (cs["key_walk"] if levels == "keys" else 0), cs
     assert rates[1 << 10] > rates[1 << 16]
 
 
@@ -180,6 +186,7 @@ def test_shared_count_min_full_size_audit(oracle_mod):
     viol, fb, dec = orc.param_cm_audit(rule_idx, acq, ts, np.arange(len(ts)), n1, keys, st)
     assert viol == 0 and dec == len(ts), viol
     assert fb / dec < 1e-4, fb / dec
+    assert svc.param_cm_stats()["block"] == 4, svc.param_cm_stats()
 
 
 @pytest.mark.gpu
@@ -297,7 +304,8 @@ def test_shared_count_min_subrange_over_chunk_falls_back(oracle_mod):
     for b in range(3):
         s = slice(b * n, (b + 1) * n)
         st.append(svc.submit_param_batch_host(rule_idx[s], acq[s], keys[s], ts[s])[0])
-        assert svc.param_cm_stats() == dict(key_walk=max(0, b - 1), overflow=min(b + 1, 2)), (b, svc.param_cm_stats())
+        assert svc.param_cm_stats() == dict(key_walk=max(0, b - 1), overflow=min(b + 1, 2), block=max(0, b - 1)), \
+            (b, svc.param_cm_stats())
     st = np.concatenate(st)
     viol, fb, dec = orc.param_cm_audit(rule_idx, acq, ts, np.arange(len(ts)), np.ones(len(ts), np.int32), keys, st)
     assert viol == 0 and dec == len(ts), (viol, dec)

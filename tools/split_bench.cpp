@@ -156,6 +156,14 @@ int main(int argc, char **argv) {
         e1 = std::max(e1, (double)(st[(size_t)g * 8 + 7] - t0) * 0.01);
     }
     printf("  last workgroup start %.2f us, last end %.2f us\n", s0, e1);
+    std::vector<unsigned long long> rs((size_t)1024 * 4);
+    CK(hipMemcpyFromSymbol(rs.data(), HIP_SYMBOL(g_split_round), rs.size() * 8));
+    const char *rn[4] = {"rank (+ next loads issued)", "wave offsets + digit scan", "stage", "write-out"};
+    for (int ph = 0; ph < 4; ++ph) {
+        double sum = 0;
+        for (int g = 0; g < G; ++g) sum += (double)rs[(size_t)g * 4 + ph] * 0.01;
+        printf("    rounds: %-26s mean %7.2f us (all rounds)\n", rn[ph], sum / G);
+    }
 #endif
     return bad ? 2 : 0;
 }
