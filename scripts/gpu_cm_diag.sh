@@ -1,5 +1,5 @@
 # k_pp_cm_block cost diagnostics (SENTINEL_CM_DIAG bits: 1 no window reads, 2 no walk, 4 no block load/store, 8 no key list)
 mkdir -p gpurun_out/cmdiag
-for d in 0 1 2 3 4 6 7 8; do
+for d in ${DIAGS:-0 1 2 3 4 6 7 8}; do
   SENTINEL_CM_DIAG=$d timeout -k 10 200 python -u bench.py --config 4cm --steps 10 --warmup 3 --no-cpu-baseline --latency-batches 10 > gpurun_out/cmdiag/d$d.log 2>&1 || exit 1
 done

@@ -2102,10 +2102,12 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
     long long *ctl = e->d_cmband.as<long long>() + 1;                          // [1..3] E_hi, E_hi seen, emax
     const int32_t *route = e->param_plain ? nullptr : e->d_prule_route.as<int32_t>();
     const ParamCtx C = e->param_ctx();
+    unsigned long long *tspan = flag + 5;                                      // [5..6] the batch's ts range
     HIP_OK(hipMemsetAsync(flag, 0, 8, s));               // set by k_pp_group on a sub-range overflow
+    HIP_OK(hipMemsetAsync(tspan, 0xFF, 16, s));
     e->launch("param_prep", n, s, [&] {
         k_pp_prep<<<dim3((unsigned)nb), dim3(PP_THREADS), 0, s>>>(n, ev, R, route, C.R, out, pbits, hist, P,
-                                                                  e->w_counters.as<uint32_t>(), nullptr);
+                                                                  e->w_counters.as<uint32_t>(), tspan);
     });
     e->launch("scan", n, s, [&] {
         const dim3 g2((unsigned)ng, (unsigned)((P + PS_THREADS - 1) / PS_THREADS));
@@ -2169,7 +2171,7 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
         k_set_i64<<<1, 64, 0, s>>>(ctl + 2, (long long)CM_EHI_NONE);
         e->launch("param_cm_block", n, s, [&] {
             const dim3 g(1u << C.CM.cbits);
-            k_pp_cm_block<<<g, 256, blk_bytes, s>>>(RC, sb, gval, ev, C.R, RR, C.CM, mv, ctl, out, e->cm_diag);
+            k_pp_cm_block<<<g, 256, blk_bytes, s>>>(RC, sb, gval, ev, C.R, RR, C.CM, mv, ctl, tspan, out, e->cm_diag);
         });
         k_pp_cm_ehi<<<1, 64, 0, s>>>(ctl);
         HIP_OK(hipGetLastError());
@@ -2186,12 +2188,12 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
         else k_pp_cm_read<16, 16><<<wg, 256, 0, s>>>(RC, gval, ev, RR, C.CM, mv, ctl);
     });
     e->launch("param_cm_walk", n, s, [&] {
-        if (d4 && nsc <= 2) k_pp_cm_walk<2, 4><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, out);
-        else if (d4 && nsc <= 4) k_pp_cm_walk<4, 4><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, out);
-        else if (d4 && nsc <= 10) k_pp_cm_walk<10, 4><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, out);
-        else if (d4) k_pp_cm_walk<16, 4><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, out);
-        else if (nsc <= 4) k_pp_cm_walk<4, 16><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, out);
-        else k_pp_cm_walk<16, 16><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, out);
+        if (d4 && nsc <= 2) k_pp_cm_walk<2, 4><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, tspan, out);
+        else if (d4 && nsc <= 4) k_pp_cm_walk<4, 4><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, tspan, out);
+        else if (d4 && nsc <= 10) k_pp_cm_walk<10, 4><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, tspan, out);
+        else if (d4) k_pp_cm_walk<16, 4><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, tspan, out);
+        else if (nsc <= 4) k_pp_cm_walk<4, 16><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, tspan, out);
+        else k_pp_cm_walk<16, 16><<<wg, 256, 0, s>>>(RC, gval, ev, C.R, RR, C.CM, mv, ctl, tspan, out);
     });
     k_pp_cm_ehi<<<1, 64, 0, s>>>(ctl);
     HIP_OK(hipGetLastError());

@@ -44,6 +44,12 @@ constexpr uint32_t PV_DT_MASK = (1u << PV_DT_BITS) - 1u;
 constexpr uint32_t PV_DT_ESC = 1u << (PV_DT_BITS - 1);       // -2^26
 
 // The batch clock: ts of the first request (clamped: an invalid first request may carry ts < 0).
+// E mod m for an epoch E >= 0 and a small m, by the double reciprocal (epoch_of's method) instead of a
+// 64-bit integer division (~120 instructions on gfx950)
+__device__ inline uint32_t cm_ring_slot(int64_t E, int m, double rcp_m) {
+    return (uint32_t)(E - epoch_of(E, m, rcp_m) * (int64_t)m);
+}
+
 __device__ inline int64_t pp_t0(const ParamEvent *ev) {
     const int64_t t = ev[0].ts;
     return t < 0 ? 0 : t;
@@ -753,7 +759,7 @@ __device__ inline int64_t cm_window_min(const CountMin &CM, unsigned long long k
     constexpr int DR = DMAX < 4 ? DMAX : 4;               // rows per round
     constexpr int NP = NMAX / 2 + 1;                      // pairs per row, at most
     const int np = nsc / 2 + 1 < nsc ? nsc / 2 + 1 : nsc; // (the ring holds nsc pairs)
-    const int first = (int)((E + 1 + nsc) % (2 * nsc));  // slot of epoch E - n + 1
+    const int first = (int)cm_ring_slot(E + 1 + nsc, 2 * nsc, 0.5 / (double)nsc);   // slot of epoch E - n + 1
     const int p0 = first >> 1;
     int64_t m = INT64_MAX;
     for (int d0 = 0; d0 < CM.depth; d0 += DR) {
@@ -848,7 +854,7 @@ __device__ inline void cm_flush(const CountMin &CM, unsigned long long key, int 
 #ifdef SENTINEL_DIAG_CM_NOADD                             // cost diagnostic only (wrong counters)
     return;
 #endif
-    const int js = (int)(E % (2 * nsc));
+    const int js = (int)cm_ring_slot(E, 2 * nsc, 0.5 / (double)nsc);
     const uint32_t te = (uint32_t)E & CM_TAG_MASK;
     unsigned long long *c[DMAX];
     unsigned long long x[DMAX];
@@ -870,9 +876,11 @@ __global__ __launch_bounds__(256) void k_pp_cm_walk(PKeyRecs RC, const uint64_t 
                                                      const ParamEvent *__restrict__ ev, ParamRules PR,
                                                      const PRuleRec *__restrict__ RR, CountMin CM,
                                                      const int64_t *__restrict__ mv, long long *__restrict__ ctl,
+                                                     const unsigned long long *__restrict__ tspan,
                                                      uint64_t *__restrict__ out) {
     const int64_t T0 = pp_t0(ev);
     const int64_t ehi = ctl[1];
+    const int64_t tmax = (int64_t)~tspan[1];              // the batch's newest request (k_pp_prep)
     int64_t emax = CM_EHI_NONE;
     const uint32_t nrec = *RC.count;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nrec; i += gridDim.x * blockDim.x) {
@@ -883,6 +891,9 @@ __global__ __launch_bounds__(256) void k_pp_cm_walk(PKeyRecs RC, const uint64_t 
         const unsigned long long key = RC.key[i];
         const double thr = (rr.nf >> 16) ? value_threshold(PR, (uint32_t)rule, key) : rr.thr;   // CPFC:101-120
         const double rcpn = 1.0 / (double)nsc;
+        // an epoch 2n older than the batch's newest request is in no window of a request within n epochs
+        // of the batch's end (the ring drops it for the next such epoch anyway): its adds are skipped
+        const int64_t Edead = epoch_of(tmax, rr.w, rr.rcp_w) - 2 * (int64_t)nsc;
         int64_t ep[NMAX], ct[NMAX];                       // this batch's own admitted counts per epoch
 #pragma unroll
         for (int j = 0; j < NMAX; ++j) { ep[j] = EPOCH_ABSENT; ct[j] = 0; }
@@ -910,7 +921,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_walk(PKeyRecs RC, const uint64_t 
 #pragma unroll
                 for (int j = 0; j < NMAX; ++j) {
                     if (j != slot || ep[j] == E) continue;
-                    if (ct[j] > 0) cm_flush<DMAX>(CM, key, nsc, ep[j], ct[j]);   // leaves the register window
+                    if (ct[j] > 0 && ep[j] > Edead) cm_flush<DMAX>(CM, key, nsc, ep[j], ct[j]);   // leaves the register window
                     ep[j] = E;
                     ct[j] = 0;
                 }
@@ -936,7 +947,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_walk(PKeyRecs RC, const uint64_t 
         }
 #pragma unroll
         for (int j = 0; j < NMAX; ++j)
-            if (ct[j] > 0) cm_flush<DMAX>(CM, key, nsc, ep[j], ct[j]);
+            if (ct[j] > 0 && ep[j] > Edead) cm_flush<DMAX>(CM, key, nsc, ep[j], ct[j]);
     }
     // the batch's newest epoch -> E_hi for the next batch's reads (ctl[0] is read by k_pp_cm_read only)
     for (int o = WAVE / 2; o > 0; o >>= 1) {
@@ -950,9 +961,9 @@ __global__ __launch_bounds__(256) void k_pp_cm_walk(PKeyRecs RC, const uint64_t 
 // k_pp_cm_block (round 5): the two phases above in one launch, one 256-thread workgroup per sketch
 // block.  Every cell of a key lies in its block (cm_cell: block = top cbits bits of mix64(key), the bits
 // the partition groups requests by), so a block's cells -- depth x cols x 2n slots, 40 KB at d = 4,
-// n = 10 -- are read from HBM once, staged in LDS, and written back once: the batch moves the sketch as
-// two coalesced streams instead of one memory-side atomic (a 128-B line read + a 64-B write) per row,
-// key and admitted epoch.  Inside the workgroup the phases are those of k_pp_cm_read / k_pp_cm_walk:
+// n = 10 -- are read from HBM once (one coalesced stream), staged in LDS, and the slots the batch added
+// to are written back: no memory-side atomic (a 128-B line read + a 64-B write) per row, key and
+// admitted epoch.  Inside the workgroup the phases are those of k_pp_cm_read / k_pp_cm_walk:
 //   A  every key's requests within n epochs of E_hi get M(E) = min over rows of the window sum, from
 //      the block as the earlier batches left it;
 //   B  (barrier: every read precedes every add) each key walks its requests with its own admitted
@@ -974,10 +985,9 @@ __device__ inline void cm_lds_cells(uint32_t *co, int depth, int nmax, uint32_t 
 }
 
 __device__ inline int64_t cm_lds_window_min(const unsigned long long *cl, const uint32_t *co, int depth, int nmax,
-                                            int nsc, int64_t E) {
+                                            double rcp_nmax, int nsc, int64_t E) {
     int64_t m = INT64_MAX;
-    int js0 = (int)(E % nmax);                            // (epochs are >= 0)
-    js0 = js0 < 0 ? js0 + nmax : js0;
+    const int js0 = (int)cm_ring_slot(E, nmax, rcp_nmax);
 #pragma unroll
     for (int d = 0; d < CMB_DMAX; ++d) {
         if (d >= depth) break;
@@ -994,37 +1004,82 @@ __device__ inline int64_t cm_lds_window_min(const unsigned long long *cl, const 
     return m;
 }
 
-__device__ inline void cm_lds_flush(unsigned long long *cl, const uint32_t *co, int depth, int nmax, int64_t E, int64_t a) {
-    const uint32_t js = (uint32_t)(E % nmax);
+// Add a to the slot of E in the key's d cells: every row's slot read at once; a slot already on E (or on
+// a newer epoch: cm_slot_add adds there too) takes a plain LDS add -- no return, no wait -- and only a
+// slot that restarts at E (an older tag) needs the compare-and-swap.  An add racing with a restart to a
+// newer epoch lands in the newer epoch's count (over, never under); a count within 2^39 of saturation
+// takes the CAS (saturating) path.
+__device__ inline void cm_lds_flush(unsigned long long *cl, unsigned long long *dirty, const uint32_t *co, int depth,
+                                    int nmax, double rcp_nmax, int64_t E, int64_t a) {
+    const uint32_t js = cm_ring_slot(E, nmax, rcp_nmax);
     const uint32_t te = (uint32_t)E & CM_TAG_MASK;
+    unsigned long long x[CMB_DMAX];
+#pragma unroll
+    for (int d = 0; d < CMB_DMAX; ++d)
+        if (d < depth) x[d] = cl[co[d] + js];
 #pragma unroll
     for (int d = 0; d < CMB_DMAX; ++d) {
         if (d >= depth) break;
-        unsigned long long *c = cl + co[d] + js;
-        cm_slot_add(c, *c, te, a);                        // (LDS atomics: ds_cmpst_rtn_b64)
+        const uint32_t w = co[d] + js;
+        atomicOr(&dirty[w >> 6], 1ull << (w & 63));       // (written back at the end)
+        unsigned long long *c = cl + w;
+        const uint32_t tag = (uint32_t)(x[d] >> CM_COUNT_BITS);
+        const uint64_t cnt = x[d] & CM_COUNT_MAX;
+        const bool newer = cnt != 0 && tag != te && ((tag - te) & CM_TAG_MASK) < (CM_TAG_MASK >> 1);
+        if ((tag == te || newer) && cnt < (CM_COUNT_MAX >> 1) && (uint64_t)a < (CM_COUNT_MAX >> 1))
+            atomicAdd(c, (unsigned long long)a);          // (ds_add_u64)
+        else
+            cm_slot_add(c, x[d], te, a);                  // (ds_cmpst_rtn_b64)
     }
 }
 
-constexpr uint32_t CMB_VCAP = 640;        // grouped values (and their M) of one block staged in LDS; listed keys
+constexpr uint32_t CMB_VCAP = 576;        // grouped values (and their M) of one block staged in LDS; listed keys
+constexpr uint32_t CMB_WORDS = 6144;      // slots of one block (48 KB: the host checks)
+
+// one key of a block walk: its record and everything the walk reads about it (loaded once, kept in
+// registers from phase A to phase B for the thread's first key)
+struct CmbKey {
+    unsigned long long key;
+    uint2 run;
+    PRuleRec rr;
+    double thr;
+    uint32_t co[CMB_DMAX];
+};
+
+__device__ inline CmbKey cmb_key(const PKeyRecs &RC, const PRuleRec *__restrict__ RR, const ParamRules &PR,
+                                 const CountMin &CM, uint32_t r, unsigned long long key) {
+    CmbKey k;
+    k.key = key;
+    k.run = RC.run[r];
+    const int32_t rule = RC.rule[r];
+    k.rr = RR[rule];
+    k.thr = (k.rr.nf >> 16) ? value_threshold(PR, (uint32_t)rule, key) : k.rr.thr;   // CPFC:101-120
+    cm_lds_cells(k.co, CM.depth, CM.nmax, CM.cols, key);
+    return k;
+}
 
 __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64_t *gval,
                                                       const ParamEvent *__restrict__ ev, ParamRules PR,
                                                       const PRuleRec *__restrict__ RR, CountMin CM,
                                                       int64_t *__restrict__ mv, long long *__restrict__ ctl,
+                                                      const unsigned long long *__restrict__ tspan,
                                                       uint64_t *__restrict__ out, int diag) {
     // diag (SENTINEL_CM_DIAG, cost diagnostics only -- wrong verdicts / counters): bit 0 no window reads,
-    // bit 1 no walk, bit 2 no block load / store, bit 3 no key list
+    // bit 1 no walk, bit 2 no block load / store, bit 3 no key list, bit 4 no adds, bit 5 no verdict stores
     extern __shared__ __attribute__((aligned(16))) unsigned long long cl[];   // depth x cols x nmax
     __shared__ uint64_t sv[CMB_VCAP];                     // the block's keys' runs, compacted in key order
     __shared__ int64_t sm[CMB_VCAP];                      // M(E) of each staged request (phase A)
     __shared__ uint32_t klist[CMB_VCAP];                  // the block's key records, longest run first
     __shared__ uint32_t khist[33];
     __shared__ uint32_t s_waves[256 / WAVE];
+    __shared__ unsigned long long dirty[CMB_WORDS / 64];  // slots this batch added to
     const uint32_t b = blockIdx.x;
     const uint32_t t = threadIdx.x;
     const int64_t T0 = pp_t0(ev);
     const int64_t ehi = ctl[0];
+    const int64_t tmax = (int64_t)~tspan[1];              // the batch's newest request (k_pp_prep)
     const int depth = CM.depth, nmax = CM.nmax;
+    const double rcp_nmax = 1.0 / (double)nmax;
     const uint32_t cols = CM.cols;
     const uint32_t words = (uint32_t)depth * cols * (uint32_t)nmax;
     unsigned long long *gcl = reinterpret_cast<unsigned long long *>(CM.cells) + (uint64_t)b * words;
@@ -1039,6 +1094,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
     if (!(diag & 4))
         for (uint32_t i = t; i < words / 2; i += blockDim.x)
             reinterpret_cast<ulonglong2 *>(cl)[i] = reinterpret_cast<const ulonglong2 *>(gcl)[i];
+    for (uint32_t i = t; i < CMB_WORDS / 64; i += blockDim.x) dirty[i] = 0;
     auto for_span = [&](auto &&f) {                       // every record of the block's keys
         for (uint32_t s = s0; s < s0 + ns; ++s) {
             const uint2 sr = RC.sub[s];
@@ -1058,9 +1114,14 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
     if (listed) {
         if (t < 33) khist[t] = 0;
         __syncthreads();
+        uint32_t m0 = 0, m1 = 0, b0 = 0, b1 = 0, nm = 0;  // (this thread's first two records of the span)
         for_span([&](uint32_t r, unsigned long long) {
             const uint32_t y = RC.run[r].y;
-            atomicAdd(&khist[31 - (y < 31 ? y : 31)], 1u);
+            const uint32_t bk = 31 - (y < 31 ? y : 31);
+            atomicAdd(&khist[bk], 1u);
+            if (nm == 0) { m0 = r; b0 = bk; }
+            else if (nm == 1) { m1 = r; b1 = bk; }
+            ++nm;
         });
         __syncthreads();
         if (t == 0) {
@@ -1069,40 +1130,53 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
             khist[32] = acc;
         }
         __syncthreads();
-        for_span([&](uint32_t r, unsigned long long) {
-            const uint32_t y = RC.run[r].y;
-            klist[atomicAdd(&khist[31 - (y < 31 ? y : 31)], 1u)] = r;
-        });
+        if (nm <= 2) {
+            if (nm > 0) klist[atomicAdd(&khist[b0], 1u)] = m0;
+            if (nm > 1) klist[atomicAdd(&khist[b1], 1u)] = m1;
+        } else {
+            for_span([&](uint32_t r, unsigned long long) {
+                const uint32_t y = RC.run[r].y;
+                klist[atomicAdd(&khist[31 - (y < 31 ? y : 31)], 1u)] = r;
+            });
+        }
         __syncthreads();
         nlisted = khist[32];
     }
+    CmbKey k0;                                            // the thread's first listed key
+    if (listed && t < nlisted) {
+        const uint32_t r = klist[t];
+        k0 = cmb_key(RC, RR, PR, CM, r, RC.key[r]);
+    }
     auto for_keys = [&](auto &&f) {                       // (the same keys, in the same order, per thread)
         if (listed) {
-            for (uint32_t i = t; i < nlisted; i += blockDim.x) {
+            if (t < nlisted) f(k0);
+            for (uint32_t i = t + blockDim.x; i < nlisted; i += blockDim.x) {
                 const uint32_t r = klist[i];
-                f(r, RC.key[r]);
+                f(cmb_key(RC, RR, PR, CM, r, RC.key[r]));
             }
         } else {
-            for_span(f);
+            for_span([&](uint32_t r, unsigned long long key) { f(cmb_key(RC, RR, PR, CM, r, key)); });
         }
     };
     // the staging offsets: this thread's keys' runs at [voff0, voff0 + myv) of sv / sm; a run that does
     // not fit CMB_VCAP stays in HBM (gval, and its M in mv)
     uint32_t myv = 0;
-    for_keys([&](uint32_t r, unsigned long long) { myv += RC.run[r].y; });
+    if (listed) {
+        if (t < nlisted) myv = k0.run.y;
+        for (uint32_t i = t + blockDim.x; i < nlisted; i += blockDim.x) myv += RC.run[klist[i]].y;
+    } else {
+        for_span([&](uint32_t r, unsigned long long) { myv += RC.run[r].y; });
+    }
     uint32_t vtot;
     const uint32_t voff0 = block_exclusive_scan(myv, s_waves, &vtot);   // (its barriers: the block is in LDS)
     // A. stage the runs; reads (the block as the earlier batches left it)
     uint32_t vo = voff0;
-    for_keys([&](uint32_t r, unsigned long long key) {
-        const uint2 run = RC.run[r];
+    for_keys([&](const CmbKey &K) {
+        const uint2 run = K.run;
         const bool lds = vo + run.y <= CMB_VCAP;
-        const PRuleRec rr = RR[RC.rule[r]];
-        const int nsc = rr.nf & 0xFFFF;
+        const int nsc = K.rr.nf & 0xFFFF;
         int64_t lastE = 0, lastM = 0;
         bool have = false;
-        uint32_t co[CMB_DMAX];
-        cm_lds_cells(co, depth, nmax, cols, key);
         RunQueue rq(gval, run.x, run.x + run.y);
         for (uint32_t k = 0; k < run.y; ++k) {
             const uint64_t v = rq.next();
@@ -1111,10 +1185,10 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
             int64_t tt;
             int32_t a;
             pp_unpack(v, T0, ev, tt, a);
-            const int64_t E = epoch_of(tt, rr.w, rr.rcp_w);
+            const int64_t E = epoch_of(tt, K.rr.w, K.rr.rcp_w);
             if (!cm_needs_read(E, ehi, nsc)) continue;
             if (!have || E != lastE) {
-                lastM = cm_lds_window_min(cl, co, depth, nmax, nsc, E);
+                lastM = cm_lds_window_min(cl, K.co, depth, nmax, rcp_nmax, nsc, E);
                 lastE = E;
                 have = true;
             }
@@ -1129,37 +1203,42 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
     // count is charged to (monotone along the run), its M slot with Q = the run's admitted sum before it;
     // own(E) = Q - Q[lo], lo = the run's first request charged to an epoch > E - n.  Each (key, epoch)
     // count is added to the block's d cells once, when the walk moves past the epoch (reads never see
-    // this batch's adds: they were all done in A).  A late request (E below the run's newest epoch:
-    // outside the precondition) counts every admitted request of the run before it (over, never under)
-    // and is charged to the newest epoch, as k_pp_cm_walk does.
+    // this batch's adds: they were all done in A) -- unless the epoch is at least 2n older than the
+    // batch's newest request: no window of a request within n epochs of the batch's end reaches it (the
+    // ring would drop it for the next such epoch anyway).  A late request (E below the run's newest
+    // epoch: outside the precondition) counts every admitted request of the run before it (over, never
+    // under) and is charged to the newest epoch, as k_pp_cm_walk does.
     int64_t emax = CM_EHI_NONE;
     vo = voff0;
-    auto walk = [&](uint32_t n_, int64_t *eb, int64_t *qb, const uint64_t *vb, unsigned long long key,
-                    const PRuleRec &rr, double thr) {
-        const int nsc = rr.nf & 0xFFFF;
+    auto walk = [&](uint32_t n_, int64_t *eb, int64_t *qb, const uint64_t *vb, const CmbKey &K) {
+        const int nsc = K.rr.nf & 0xFFFF;
+        const int64_t Edead = epoch_of(tmax, K.rr.w, K.rr.rcp_w) - 2 * (int64_t)nsc;
         int64_t curE = EPOCH_ABSENT, cnt = 0, Q = 0;
-        uint32_t lo = 0;
-        uint32_t co[CMB_DMAX];
-        cm_lds_cells(co, depth, nmax, cols, key);
+        uint32_t lo = 0;                                  // the window's first request; eb / qb[lo] cached:
+        int64_t elo = 0, qlo = 0;                         // (valid while lo < k)
         for (uint32_t k = 0; k < n_; ++k) {
             const uint64_t v = vb[k];
             int64_t tt;
             int32_t a;
             pp_unpack(v, T0, ev, tt, a);
-            const int64_t E = epoch_of(tt, rr.w, rr.rcp_w);
+            const int64_t E = epoch_of(tt, K.rr.w, K.rr.rcp_w);
             emax = E > emax ? E : emax;
             const bool late = curE != EPOCH_ABSENT && E < curE;
             if (!late && E != curE) {
-                if (cnt > 0) cm_lds_flush(cl, co, depth, nmax, curE, cnt);
+                if (cnt > 0 && curE > Edead && !(diag & 16)) cm_lds_flush(cl, dirty, K.co, depth, nmax, rcp_nmax, curE, cnt);
                 curE = E;
                 cnt = 0;
-                while (lo < k && eb[lo] <= E - nsc) ++lo;
+                while (lo < k && elo <= E - nsc) {
+                    ++lo;
+                    if (lo < k) { elo = eb[lo]; qlo = qb[lo]; }
+                }
             }
-            const int64_t own = late ? Q : (lo < k ? Q - qb[lo] : 0);
+            const int64_t own = late ? Q : (lo < k ? Q - qlo : 0);
             const int64_t m = cm_needs_read(E, ehi, nsc) ? qb[k] : 0;
             qb[k] = Q;
             eb[k] = curE;
-            const double next = remaining_of(thr, rr.I_s, m + own, a);
+            if (lo == k) { elo = curE; qlo = Q; }
+            const double next = remaining_of(K.thr, K.rr.I_s, m + own, a);
             uint64_t vd;
             if (!(next < 0.0)) {                                          // CPFC:64-66, then addValue
                 Q += a;
@@ -1168,20 +1247,17 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
             } else {
                 vd = pack_verdict(ST_BLOCKED, 0, 0);
             }
-            store_verdict(out, (uint32_t)v & SEQ_MASK, vd);
+            if (!(diag & 32)) store_verdict(out, (uint32_t)v & SEQ_MASK, vd);
         }
-        if (cnt > 0) cm_lds_flush(cl, co, depth, nmax, curE, cnt);
+        if (cnt > 0 && curE > Edead && !(diag & 16)) cm_lds_flush(cl, dirty, K.co, depth, nmax, rcp_nmax, curE, cnt);
     };
-    if (!(diag & 2)) for_keys([&](uint32_t r, unsigned long long key) {
-        const uint2 run = RC.run[r];
+    if (!(diag & 2)) for_keys([&](const CmbKey &K) {
+        const uint2 run = K.run;
         const bool lds = vo + run.y <= CMB_VCAP;
-        const int32_t rule = RC.rule[r];
-        const PRuleRec rr = RR[rule];
-        const double thr = (rr.nf >> 16) ? value_threshold(PR, (uint32_t)rule, key) : rr.thr;   // CPFC:101-120
         if (lds)
-            walk(run.y, reinterpret_cast<int64_t *>(sv + vo), sm + vo, sv + vo, key, rr, thr);
+            walk(run.y, reinterpret_cast<int64_t *>(sv + vo), sm + vo, sv + vo, K);
         else                                              // (the grouped values are dead after this walk)
-            walk(run.y, reinterpret_cast<int64_t *>(gval + run.x), mv + run.x, gval + run.x, key, rr, thr);
+            walk(run.y, reinterpret_cast<int64_t *>(gval + run.x), mv + run.x, gval + run.x, K);
         vo += run.y;
     });
     for (int o = WAVE / 2; o > 0; o >>= 1) {
@@ -1190,9 +1266,16 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
     }
     if (lane_id() == 0 && emax != CM_EHI_NONE) atomicMax(reinterpret_cast<long long *>(&ctl[2]), (long long)emax);
     __syncthreads();
+    // write back the slots the batch added to (the rest of the block is unchanged in HBM)
     if (!(diag & 4))
-        for (uint32_t i = t; i < words / 2; i += blockDim.x)
-            reinterpret_cast<ulonglong2 *>(gcl)[i] = reinterpret_cast<const ulonglong2 *>(cl)[i];
+        for (uint32_t i = t; i < (words + 63) / 64; i += blockDim.x) {
+            unsigned long long m = dirty[i];
+            while (m) {
+                const uint32_t w = i * 64 + (uint32_t)(__ffsll(m) - 1);
+                m &= m - 1;
+                gcl[w] = cl[w];
+            }
+        }
 }
 
 // E_hi <- max(E_hi, this batch's newest epoch) (after k_pp_cm_walk); CM_EHI_ANY stays.
