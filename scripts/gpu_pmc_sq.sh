@@ -13,4 +13,4 @@ for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $O/sq$i -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ${BENCH_ARGS} > /dev/null 2> $O/sq$i.err || { tail -5 $O/sq$i.err; exit 1; }
 done
-cd $R && python scripts/pmc_sq_summary.py $O
+cd $R && python scripts/pmc_sq_summary.py $O && rm -rf $O/sq1 $O/sq2 $O/sq3

@@ -857,18 +857,19 @@ __device__ inline void cm_flush(const CountMin &CM, unsigned long long key, int 
     const int js = (int)cm_ring_slot(E, 2 * nsc, 0.5 / (double)nsc);
     const uint32_t te = (uint32_t)E & CM_TAG_MASK;
     unsigned long long *c[DMAX];
-    unsigned long long x[DMAX];
+    unsigned long long x[DMAX], p[DMAX];
 #pragma unroll
-    for (int d = 0; d < DMAX; ++d) {                      // every row's first CAS in flight at once
+    for (int d = 0; d < DMAX; ++d) {                      // every row's guess loaded at once
         if (d >= CM.depth) break;
         c[d] = reinterpret_cast<unsigned long long *>(cm_cell(CM, 0, d, key) + js);
         x[d] = *c[d];                                     // a plain load as the CAS's guess (atomics run at the
     }                                                     // memory side: one CAS instead of a failed one + retry)
 #pragma unroll
-    for (int d = 0; d < DMAX; ++d) {
-        if (d >= CM.depth) break;
-        cm_slot_add(c[d], x[d], te, a);
-    }
+    for (int d = 0; d < DMAX; ++d)                        // every row's first CAS in flight at once
+        if (d < CM.depth) p[d] = atomicCAS(c[d], x[d], cm_slot_next(x[d], te, a));
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d)                        // a lost CAS retries from the value it returned
+        if (d < CM.depth && p[d] != x[d]) cm_slot_add(c[d], p[d], te, a);
 }
 
 template <int NMAX, int DMAX>
@@ -1033,7 +1034,7 @@ __device__ inline void cm_lds_flush(unsigned long long *cl, unsigned long long *
     }
 }
 
-constexpr uint32_t CMB_VCAP = 576;        // grouped values (and their M) of one block staged in LDS; listed keys
+constexpr uint32_t CMB_VCAP = 512;        // grouped values (and their M) of one block staged in LDS; listed keys
 constexpr uint32_t CMB_WORDS = 6144;      // slots of one block (48 KB: the host checks)
 
 // one key of a block walk: its record and everything the walk reads about it (loaded once, kept in

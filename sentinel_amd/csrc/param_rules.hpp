@@ -377,15 +377,18 @@ __device__ inline int64_t cm_cell_sum_sync(const uint64_t *c, int nsc, int64_t E
 // Add a to one cell slot of epoch E (te = its tag): same tag -> add (saturating), an older tag -> restart
 // at a, a newer tag (only past the precondition: a rule's clock went back) -> add to the newer slot.
 // `x` = the caller's guess of the slot's current word (a failed CAS returns the real one).
+__host__ __device__ inline unsigned long long cm_slot_next(unsigned long long x, uint32_t te, int64_t a) {
+    const uint32_t tag = (uint32_t)(x >> CM_COUNT_BITS);
+    // (an empty cell, count 0, has no epoch: its tag bits mean nothing)
+    const bool newer = (x & CM_COUNT_MAX) != 0 && tag != te && ((tag - te) & CM_TAG_MASK) < (CM_TAG_MASK >> 1);
+    uint64_t cnt = (tag == te || newer) ? (x & CM_COUNT_MAX) : 0;
+    cnt = (uint64_t)a > CM_COUNT_MAX - cnt ? CM_COUNT_MAX : cnt + (uint64_t)a;   // (a >= 0)
+    return ((unsigned long long)(newer ? tag : te) << CM_COUNT_BITS) | cnt;
+}
+
 __device__ inline void cm_slot_add(unsigned long long *c, unsigned long long x, uint32_t te, int64_t a) {
     for (;;) {
-        const uint32_t tag = (uint32_t)(x >> CM_COUNT_BITS);
-        // (an empty cell, count 0, has no epoch: its tag bits mean nothing)
-        const bool newer = (x & CM_COUNT_MAX) != 0 && tag != te && ((tag - te) & CM_TAG_MASK) < (CM_TAG_MASK >> 1);
-        uint64_t cnt = (tag == te || newer) ? (x & CM_COUNT_MAX) : 0;
-        cnt = (uint64_t)a > CM_COUNT_MAX - cnt ? CM_COUNT_MAX : cnt + (uint64_t)a;   // (a >= 0)
-        const unsigned long long y = ((unsigned long long)(newer ? tag : te) << CM_COUNT_BITS) | cnt;
-        const unsigned long long prev = atomicCAS(c, x, y);
+        const unsigned long long prev = atomicCAS(c, x, cm_slot_next(x, te, a));
         if (prev == x) break;
         x = prev;
     }

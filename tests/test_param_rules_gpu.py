@@ -140,10 +140,10 @@ def test_count_min_is_one_sided(oracle_mod):
 @pytest.mark.parametrize("levels", ["keys", "keys-global", "launch", "coop"])
 def test_shared_count_min_is_one_sided(oracle_mod, monkeypatch, levels):
     """One sketch for every rule (BASELINE config 4's layout), narrow enough that rules collide, on
-    batches spanning ~75 epochs.  "keys" (the default): the key walk, one lane per (rule, value) key,
+    batches spanning ~75 epochs.  "keys" / "keys-global": the key walk, one lane per (rule, value) key,
     every read of the batch before any add -- in one workgroup per sketch block staged in LDS
-    (k_pp_cm_block), or with "keys-global" in two launches on HBM cells (k_pp_cm_read, then k_pp_cm_walk:
-    decisions and memory-side atomic adds); "launch" / "coop": one lane per rule moving through the
+    (k_pp_cm_block, SENTINEL_CM_BLOCK=1), or (the default) in two launches on HBM cells (k_pp_cm_read, then
+    k_pp_cm_walk: decisions and memory-side atomic adds); "launch" / "coop": one lane per rule moving through the
     epochs band by band (k_prule_cm_level / k_prule_cm_sync).  Either way no reset of a shared cell slot
     drops a count a check still needs -- zero violations of one-sidedness, and the false-block rate
     shrinks with the width."""
@@ -170,12 +170,15 @@ def test_shared_count_min_is_one_sided(oracle_mod, monkeypatch, levels):
 
 
 @pytest.mark.gpu
-def test_shared_count_min_full_size_audit(oracle_mod):
+@pytest.mark.parametrize("block", ["0", "1"])
+def test_shared_count_min_full_size_audit(oracle_mod, monkeypatch, block):
     """BASELINE config 4's count-min mode at its own size: 100k hot-parameter rules, Zipf values over
     1000 per rule, 2M requests in 4 batches, the shared sketch at d = 4, w = 2^20 (bench config 4cm):
     every sketch verdict replayed on exact counters with the same admitted history -- zero
-    one-sidedness violations -- and a false-block rate far below the e/w bound."""
+    one-sidedness violations -- and a false-block rate far below the e/w bound.  Both key walks: the
+    two-phase HBM walk (the default) and the block-owned walk (SENTINEL_CM_BLOCK=1)."""
     import sentinel_amd as sa
+    monkeypatch.setenv("SENTINEL_CM_BLOCK", block)
     count, hot, rule_idx, vals, keys, ts = T.config4(2_000_000, seed=61, n_rules=100_000, universe=1000)
     acq = np.ones(len(ts), np.int32)
     svc, orc = _cluster_pair(oracle_mod, count, hot, sample_count=lambda r: 10)
@@ -186,7 +189,7 @@ def test_shared_count_min_full_size_audit(oracle_mod):
     viol, fb, dec = orc.param_cm_audit(rule_idx, acq, ts, np.arange(len(ts)), n1, keys, st)
     assert viol == 0 and dec == len(ts), viol
     assert fb / dec < 1e-4, fb / dec
-    assert svc.param_cm_stats()["block"] == 4, svc.param_cm_stats()
+    assert svc.param_cm_stats()["block"] == (4 if block == "1" else 0), svc.param_cm_stats()
 
 
 @pytest.mark.gpu
@@ -288,13 +291,14 @@ def _hot_key_batches(n_batches=3, n=30_000, hot_reqs=3000, seed=58):
     return count, hot, rule_idx, keys, ts
 
 
-def test_shared_count_min_subrange_over_chunk_falls_back(oracle_mod):
+def test_shared_count_min_subrange_over_chunk_falls_back(oracle_mod, monkeypatch):
     """A shared count-min batch with one key over PG_CAP requests: its key-hash sub-range cannot be grouped
     in one LDS chunk, so k_pp_group raises the overflow flag (no workgroup decides or emits anything for
     it) and the whole batch goes to the per-rule lanes -- the path that faulted while the key walk was
     being built.  The fallback batches and the key-walk batch after them are audited
     on exact counters replaying the sketch's own decisions: zero one-sidedness violations."""
     import sentinel_amd as sa
+    monkeypatch.setenv("SENTINEL_CM_BLOCK", "1")
     count, hot, rule_idx, keys, ts = _hot_key_batches()
     svc, orc = _cluster_pair(oracle_mod, count, hot, sample_count=lambda r: 10)
     svc.set_param_mode(sa._lib.PARAM_COUNT_MIN_SHARED, depth=4, width=1 << 12)
