@@ -968,8 +968,10 @@ def main():
                               "eps_N_bound_counts": round(eps_n, 2),
                               "note": "the sketch's verdicts of the warmup+profile batches replayed on exact counters "
                                       "(oracle, same admitted history): violations = sketch passed what exact would "
-                                      "block (must be 0); bound: P[overestimate > (e/w) N] <= exp(-d), N = all "
-                                      "requests counted in the window (upper bound used: every audited request)"}
+                                      "block (must be 0); bound (blocked layout): P[overestimate > (e/64) N_B] <= exp(-d), N_B = the "
+                                      "window count of the key's 64-column block, E[N_B] = 64 N / w, so (e/w) N on "
+                                      "average, N = all requests counted in the window (upper bound used: every "
+                                      "audited request)"}
         st = svc.param_table_stats()
         extra["param_table"] = st
     if args.config == "4" and rank == 0:
