@@ -1,6 +1,6 @@
 # Full GPU round check on one MI355X: parity tests, bench, rocprofv3 kernel stats, and the PMC
-# traffic of the bench's own shape (scripts/gpu_pmc_shape.sh: separate FETCH_SIZE / WRITE_SIZE runs,
-# as MI355X_MICROARCH.md prescribes, summarised into profiles/pmc/<TAG>_c3.json).
+# traffic of the bench's own shape (scripts/gpu_pmc_req.sh: the memory-side request counters by size in
+# two separate passes, summarised into gpurun_out/pmcreq_<TAG>_c3/summary.json).
 # Every GPU step has its own time limit; the chain stops at the first failure.
 # Usage (from gpurun): bash scripts/gpu_round.sh [TAG] [--shapes]   -> results under gpurun_out/$TAG
 set -o pipefail
@@ -29,6 +29,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-path > $O/bench_prof.json 2> $O/prof.err || { tail -20 $O/prof.err; exit 1; }
 cd $R
 python scripts/trace_summary.py $O/prof/run_kernel_trace.csv warmup:2,profile:3,timed:10 > $O/kernel_trace_summary.json
-echo "== pmc (bench shape)"
-bash scripts/gpu_pmc_shape.sh ${TAG}_c3 || exit 1
+echo "== pmc (bench shape, memory-side requests by size)"
+bash scripts/gpu_pmc_req.sh ${TAG}_c3 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-host-path > $O/pmc_req.log 2>&1 || { tail -20 $O/pmc_req.log; exit 1; }
+rm -rf $R/gpurun_out/pmcreq_${TAG}_c3/rd $R/gpurun_out/pmcreq_${TAG}_c3/wr
 echo "ROUND OK"
