@@ -663,6 +663,8 @@ struct sentinel_engine {
     bool cm_debug = false;             // SENTINEL_CM_DEBUG=1: the key walk's geometry on stderr
     int cm_diag = 0;                   // SENTINEL_CM_DIAG: k_pp_cm_block cost diagnostics (wrong results)
     DevBuf w_cmsub;                    // block walk: per sub-range {first record, records}
+    DevBuf d_pexpire;                  // exact param table: per slot the getTopValues expire hint (PSlots)
+    bool pexp_valid = false;           // ... every live slot's hint is current (only the key walk wrote since)
     uint64_t cm_overflows = 0;         // ... sent to the per-rule lanes (a sub-range over PG_CAP requests)
     uint64_t p_ord = 0;                // param batches reserved so far
     uint64_t p_reset_ord = 0;          // first batch ordinal after d_pfresh was last zeroed
@@ -1247,6 +1249,7 @@ int sentinel_engine::clear_param_slots() {
     HIP_OK(hipMemsetAsync(d_pfresh.p, 0, CNT_BYTES, stream));
     k_init_state<<<grid_for((int64_t)P), 256, 0, stream>>>(pt.state.as<int64_t>(), nullptr, stride, nullptr, pmax_n,
                                                            stride, (int64_t)P);
+    pexp_valid = false;
     HIP_OK(hipStreamSynchronize(stream));
     p_live = p_ub = 0;
     return 0;
@@ -1345,6 +1348,7 @@ int sentinel_engine::param_rebuild(uint64_t new_cap, const std::vector<int32_t> 
         }
     }
     std::swap(d_ptable, nkeys);
+    pexp_valid = false;                                  // (slots moved: the next snapshot recomputes the hints)
     std::swap(d_slot_rule, nrule);
     std::swap(pt.state, nstate);
     std::swap(pt.n, nn);
@@ -2036,8 +2040,9 @@ static int submit_param_part(sentinel_engine_t *e, int64_t n, const ParamEvent *
     e->launch("param_scatter", n, s, [&] {
         k_pp_scatter<<<dim3((unsigned)nb), dim3(PT_THREADS), 0, s>>>(ev, n, R, route, pbits, hist, P, pkey, pval, prule);
     });
+    uint32_t *pexp = e->d_pexpire.bytes >= e->pcap * 4 ? e->d_pexpire.as<uint32_t>() : nullptr;
     const PSlots S{e->d_ptable.as<unsigned long long>(), e->d_slot_rule.as<int32_t>(), e->pt.state.as<int64_t>(),
-                   param_stride(e->pmax_n), e->pcap - 1};
+                   param_stride(e->pmax_n), e->pcap - 1, pexp};
     const ParamRules PR = e->param_ctx().R;
     if (e->prec_dirty || e->d_prule_rec.bytes < (size_t)R * sizeof(PRuleRec)) {
         if (e->d_prule_rec.ensure((size_t)R * sizeof(PRuleRec))) return SENTINEL_E_NOMEM;
@@ -2226,6 +2231,7 @@ static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, u
     }
     const bool plim = e->nlimiters > 0 && !e->param_plain && R > 0;
     if (e->param_path == 0 && !plim && e->pmax_n <= 16) return submit_param_part(e, n, ev, out, s);
+    e->pexp_valid = false;                                // (the segment pipeline does not keep the hints)
     const uint64_t P = e->pcap;
     const int pbits = bits_for((int64_t)P);
     const uint32_t pinvalid = ((uint32_t)1 << pbits) - 1;
@@ -2300,6 +2306,7 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
         if (s != e->stream) HIP_OK(hipStreamSynchronize(s));
         rc = e->param_reserve(nv);            // room for every value of the batch: never FAIL
         if (rc) return rc;
+        e->pexp_valid = false;                // (the per-rule lanes do not keep the getTopValues hints)
     }
     ParamCtx C = e->param_ctx();
     C.L.kinds = local ? kinds : nullptr;
@@ -4247,8 +4254,18 @@ static int param_top(sentinel_engine_t *e, int64_t ts, int32_t number, hipStream
         unsigned long long *pr = W.pr.as<unsigned long long>(), *pk = W.pk.as<unsigned long long>(),
                            *cr = W.cr.as<unsigned long long>(), *ck = W.ck.as<unsigned long long>();
         unsigned long long *cn = W.cn.as<unsigned long long>();
-        const PSlots T{e->d_ptable.as<unsigned long long>(), e->d_slot_rule.as<int32_t>(), e->pt.state.as<int64_t>(),
-                       param_stride(e->pmax_n), cap - 1};
+        PSlots T{e->d_ptable.as<unsigned long long>(), e->d_slot_rule.as<int32_t>(), e->pt.state.as<int64_t>(),
+                 param_stride(e->pmax_n), cap - 1};
+        if (e->d_pexpire.bytes < cap * 4) {
+            if (e->d_pexpire.ensure(cap * 4)) return SENTINEL_E_NOMEM;
+            e->pexp_valid = false;
+        }
+        T.expire = e->d_pexpire.as<uint32_t>();
+        if (!e->pexp_valid) {                 // every slot's hint from its window, once; then the key walk keeps them
+            k_ptable_expire<<<grid_for((int64_t)cap), 256, 0, s>>>(T, cap, R, e->d_prule_n.as<int32_t>(),
+                                                                   e->d_prule_w.as<int32_t>());
+            e->pexp_valid = true;
+        }
         const TopCands C{W.ckey.as<unsigned long long>(), W.crule.as<int32_t>(), W.csum.as<int64_t>(), cn, mc};
         const TopCands F{W.fkey.as<unsigned long long>(), W.frule.as<int32_t>(), W.fsum.as<int64_t>(), cn + 1, fc};
         HIP_OK(hipMemsetAsync(cn, 0, 16, s));

@@ -430,6 +430,12 @@ __device__ inline void pd_walk(const ParamRules &PR, const PRuleRec *RR, const P
 #pragma unroll
     for (int j = 0; j < NMAX; ++j)
         if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(st + 2 * j) = longlong2{ep[j], ct[j]};
+    if (S.expire) {                                                      // getTopValues hint (param_table.hpp)
+        int64_t nw = EPOCH_ABSENT;
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j) nw = j < nsc && ep[j] > nw ? ep[j] : nw;
+        S.expire[h] = slot_expire_c(nw, nsc, w);
+    }
 }
 
 #ifdef SENTINEL_DIAG_PHASES     // per workgroup: [0] start, [3] end, [4..6] phase sums, [7] rounds, [8] keys

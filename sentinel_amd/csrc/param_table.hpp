@@ -30,7 +30,21 @@ struct PSlots {
     int64_t *state;             // stride words per slot: {epoch, count} x n
     int64_t stride;
     uint64_t mask;              // capacity - 1
+    // getTopValues hint (round 5): per slot the 1024-ms bucket from which its window sums to zero,
+    // ceil((newest epoch + n) * w / 1024) (0: nothing counted), written by the key walk (pd_walk); null
+    // when the engine does not keep it
+    uint32_t *expire = nullptr;
 };
+
+// A window whose newest epoch is e sums to zero at every ts >= (e + n) w: every bucket's epoch is then
+// <= E - n (E = ts / w).  Kept in 1024-ms units, rounded up (so a slot is only ever skipped late).
+__host__ __device__ inline uint32_t slot_expire_c(int64_t newest, int n, int32_t w) {
+    if (newest == EPOCH_ABSENT) return 0u;
+    const int64_t t = (newest + (int64_t)n) * (int64_t)w;
+    if (t <= 0) return 0u;
+    const int64_t c = (t + 1023) >> 10;
+    return c >= (int64_t)0xFFFFFFFF ? 0xFFFFFFFFu : (uint32_t)c;
+}
 
 // Insert a key known to be absent (a rebuild re-inserts unique keys): linear probing.
 __device__ inline int64_t slot_place(unsigned long long *keys, uint64_t mask, uint64_t key) {
@@ -46,6 +60,20 @@ __device__ inline int64_t slot_newest(const int64_t *st, int n) {
     int64_t m = EPOCH_ABSENT;
     for (int j = 0; j < n; ++j) m = st[2 * j] > m ? st[2 * j] : m;
     return m;
+}
+
+// Every slot's expire hint from its window (the rebuild moved slots, or a path other than the key
+// walk wrote windows since the last snapshot).
+__global__ __launch_bounds__(256) void k_ptable_expire(PSlots T, uint64_t cap, int32_t R, const int32_t *__restrict__ rn,
+                                                       const int32_t *__restrict__ rw) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= cap) return;
+    uint32_t x = 0;
+    if (T.keys[s] != PKEY_EMPTY && (uint32_t)T.rule[s] < (uint32_t)R) {
+        const int32_t r = T.rule[s];
+        x = slot_expire_c(slot_newest(T.state + (int64_t)s * T.stride, rn[r]), rn[r], rw[r]);
+    }
+    T.expire[s] = x;
 }
 
 // Per rule: the newest epoch over its live slots (wave-aggregated when a wave's slots share a rule).
@@ -181,7 +209,10 @@ __global__ __launch_bounds__(256) void k_ptop_sums(PSlots T, uint64_t cap, int32
     const uint64_t s = base + lane;
     unsigned long long key = PKEY_EMPTY;
     int32_t r = -1;
-    if (s < cap) key = T.keys[s];
+    // with the expire hints only the slots whose window can still sum to non-zero at ts are read
+    // (4 B per slot instead of the key and the whole window)
+    const bool fresh = !T.expire || (s < cap && T.expire[s] > (uint32_t)((uint64_t)(ts < 0 ? 0 : ts) >> 10));
+    if (s < cap && fresh) key = T.keys[s];
     if (key != PKEY_EMPTY) {
         r = T.rule[s];
         if ((uint32_t)r >= (uint32_t)R) r = -1;

@@ -132,6 +132,58 @@ def test_top_values_match_oracle(oracle_mod, sample_count, interval_ms):
         assert [(int(k), float(v)) for k, v in zip(rec["key"][r][:len(top[r])], rec["avg"][r][:len(top[r])])] == top[r]
 
 
+def test_top_values_expire_hints(oracle_mod):
+    """The snapshot's expire hints (param_table.hpp: per slot the 1024-ms bucket from which its window
+    sums to zero, kept by the key walk; k_ptop_sums then reads only slots whose window can be non-zero):
+    a first snapshot computes them from the windows, later batches through the partition path keep them,
+    and snapshots at times where some slots have just expired, all have, or none has, equal the oracle's
+    getTopValues; a multi-value batch (the per-rule lanes, which do not keep hints) makes the next
+    snapshot recompute them."""
+    R = 200
+    rng = np.random.default_rng(81)
+    prules = [dict(flow_id=9000 + r, count=float(rng.integers(20, 300)), sample_count=10,
+                   window_interval_ms=1000) for r in range(R)]
+    svc = _svc(prules)
+    orc = oracle_mod.TokenServiceOracle([], param_rules=prules)
+    t0 = T.T0_ALIGNED + 17
+
+    def check(ts_list):
+        for t in ts_list:
+            top = svc.param_top_values(t)
+            for r in range(R):
+                assert top[r] == orc.param_top_values(r, t), (t, r, top[r], orc.param_top_values(r, t))
+
+    # (getTopValues rolls the reference's window to its ts -- LeapArray.currentWindow -- so every batch
+    # starts after the previous snapshot time)
+    for b in range(3):
+        m = 60_000
+        ts = np.sort(t0 + rng.integers(0, 2500, size=m)).astype(np.int64)
+        t0 = int(ts[-1]) + 1101 + 50 * b
+        ridx = rng.integers(0, R, size=m).astype(np.int32)
+        vals = T.zipf_indices(80, 1.2, m, rng, permute=False).astype(np.uint64)
+        keys = (np.uint64(9000) + ridx.astype(np.uint64)) << np.uint64(24) | vals
+        acq = rng.integers(1, 3, size=m).astype(np.int32)
+        st_g, _ = svc.submit_param_batch_host(ridx, acq, keys, ts)
+        st_o, _ = orc.param_replay(ridx, acq, keys, ts)
+        assert np.array_equal(st_g, st_o), b
+        te = int(ts[-1])
+        check((te, te + 600, te + 1100))
+    check((te + 2100, te + 4000))
+    t0 = te + 4001
+    # a multi-value batch: the per-rule lanes write windows without hints
+    m = 20_000
+    ts = np.sort(t0 + rng.integers(0, 800, size=m)).astype(np.int64)
+    ridx = rng.integers(0, R, size=m).astype(np.int32)
+    b_, c_, k_ = T.param_value_lists(ridx, rng, universe=80, max_values=3)
+    k_ = (np.uint64(9000) + (k_ >> np.uint64(20))) << np.uint64(24) | (k_ & np.uint64(0xFFFFF))
+    acq = np.ones(m, np.int32)
+    st_g, _ = svc.submit_param_multi_batch_host(ridx, acq, ts, b_, c_, k_)
+    st_o, _ = orc.param_multi_replay(ridx, acq, ts, b_, c_, k_)
+    assert np.array_equal(st_g, st_o)
+    te = int(ts[-1])
+    check((te, te + 950, te + 3000))
+
+
 @pytest.mark.parametrize("path", ["part", "slot"])
 def test_param_part_edges_bitexact(oracle_mod, monkeypatch, path):
     """Edge cases of the partition-local param path (param_part.hpp) against the oracle: one key hot
