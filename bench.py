@@ -806,6 +806,8 @@ def main():
         svc.synchronize()
         hl.append((time.perf_counter() - h0) * 1000.0)
     hl.sort()
+    svc.synchronize()
+    t_snap = int(lat_b[(L - 1) % K][-1, 1].item()) + 1    # right after the newest batch the engine decided
     advance()
     svc.synchronize()
     log("latency loop done")
@@ -817,7 +819,6 @@ def main():
     # for the flow configs, top-5 param records for config 4; off the decision path)
     from sentinel_amd import shard as SH
     snap_ms = snap_first_ms = None
-    t_snap = int(lat_b[-1][-1, 1].item()) + 1
 
     def snapshot_once():
         torch.cuda.synchronize()

@@ -1133,7 +1133,7 @@ struct sentinel_engine {
     // getTopValues scratch (param_top), kept between calls: candidate list {key, rule, sum} + its count,
     // per-rule selection state, the results and the rules' flowIds (grow-only: no allocation per snapshot)
     struct TopScratch {
-        DevBuf ckey, crule, csum, cn, pr, pk, cr, ck, dc, dk, ds, ids, rank, fkey, frule, fsum;
+        DevBuf ckey, crule, csum, cn, pr, pk, cr, ck, dc, dk, ds, ids, rank, fkey, frule, fsum, flist;
         std::vector<int64_t> h_ids;    // the flowIds in `ids` (uploaded again only when the rules change)
     } topw;
     TokenTable token_table() {
@@ -4269,25 +4269,41 @@ static int param_top(sentinel_engine_t *e, int64_t ts, int32_t number, hipStream
         const TopCands C{W.ckey.as<unsigned long long>(), W.crule.as<int32_t>(), W.csum.as<int64_t>(), cn, mc};
         const TopCands F{W.fkey.as<unsigned long long>(), W.frule.as<int32_t>(), W.fsum.as<int64_t>(), cn + 1, fc};
         HIP_OK(hipMemsetAsync(cn, 0, 16, s));
-        HIP_OK(hipMemsetAsync(W.rank.p, 0, (size_t)R * number * 8, s));
-        k_ptop_sums<<<grid_for((int64_t)cap), 256, 0, s>>>(T, cap, R, e->d_prule_n.as<int32_t>(), e->d_prule_w.as<int32_t>(),
-                                                           e->d_prule_rcp.as<double>(), ts, C,
-                                                           W.rank.as<unsigned long long>(), number);
-        const unsigned gc = (unsigned)std::min<uint64_t>(2048, (mc + 255) / 256);
-        k_ptop_final<<<gc, 256, 0, s>>>(C, W.rank.as<unsigned long long>(), number, F);
+        // the sums only (the expire hints leave few candidates: the rank cascade's contended atomics cost
+        // more than selection rounds over all of them); the cascade and the finalists only for a long list
+        // the slots whose window can be non-zero at ts (a coalesced pass over the 4-B hints), then their sums:
+        // every slot of the list in flight at once instead of a dependent chain per 256 slots
+        if (W.flist.ensure(mc * 4)) return SENTINEL_E_NOMEM;
+        HIP_OK(hipMemsetAsync(cn + 1, 0, 8, s));          // (cn[1]: the list's count until the finalists)
+        k_ptop_fresh<<<(unsigned)std::min<uint64_t>(2048, (cap + 255) / 256), 256, 0, s>>>(
+            T.expire, cap, ts, W.flist.as<uint32_t>(), cn + 1, mc);
+        k_ptop_sums<<<(unsigned)std::min<uint64_t>(2048, (mc + 255) / 256), 256, 0, s>>>(
+            T, cap, R, e->d_prule_n.as<int32_t>(), e->d_prule_w.as<int32_t>(), e->d_prule_rcp.as<double>(), ts, C,
+            W.flist.as<uint32_t>(), cn + 1, mc);
         unsigned long long found[2] = {0, 0};
         HIP_OK(hipMemcpyAsync(found, cn, 16, hipMemcpyDeviceToHost, s));
         HIP_OK(hipStreamSynchronize(s));
-        if (found[0] > mc && mc < cap) {             // (never expected) room for the whole table
+        if ((found[0] > mc || found[1] > mc) && mc < cap) {   // (never expected) room for the whole table
             mc = cap;
             continue;
         }
-        const TopCands &L = found[1] <= fc ? F : C;  // rounds over the finalists (the whole list if they overflow)
+        bool fin = false;
+        if (found[0] > fc) {
+            const unsigned gc = (unsigned)std::min<uint64_t>(2048, (mc + 255) / 256);
+            HIP_OK(hipMemsetAsync(cn + 1, 0, 8, s));
+            HIP_OK(hipMemsetAsync(W.rank.p, 0, (size_t)R * number * 8, s));
+            k_ptop_cascade<<<gc, 256, 0, s>>>(C, W.rank.as<unsigned long long>(), number);
+            k_ptop_final<<<gc, 256, 0, s>>>(C, W.rank.as<unsigned long long>(), number, F);
+            HIP_OK(hipMemcpyAsync(found, cn, 16, hipMemcpyDeviceToHost, s));
+            HIP_OK(hipStreamSynchronize(s));
+            fin = found[1] <= fc;
+        }
+        const TopCands &L = fin ? F : C;             // rounds over the finalists, or over every candidate
         HIP_OK(hipMemsetAsync(pr, 0, (size_t)R * 8, s));
         HIP_OK(hipMemsetAsync(pk, 0, (size_t)R * 8, s));
         HIP_OK(hipMemsetAsync(cr, 0, (size_t)R * 8, s));
         HIP_OK(hipMemsetAsync(ck, 0xFF, (size_t)R * 8, s));
-        const uint64_t ln = std::min<uint64_t>(found[1] <= fc ? found[1] : found[0], L.cap);
+        const uint64_t ln = std::min<uint64_t>(fin ? found[1] : found[0], L.cap);
         const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(2048, (ln + 255) / 256));
         for (int k = 0; k < number; ++k) {
             k_ptop_best_sum<<<g, 256, 0, s>>>(L, pr, pk, cr);

@@ -200,70 +200,158 @@ __device__ inline void top_cascade(unsigned long long *top, int number, unsigned
 // state region, so its window sum is read by a 16-lane group (lane j loads pair j, one 16-B load, then a
 // 16-lane reduction): the wave's live slots go through four at a time, each load instruction reading
 // four contiguous runs instead of 64 scattered ones.
+constexpr uint32_t TOP_LDS = 1024;        // candidates a k_ptop_sums workgroup gathers before one global append
+
+// The slots whose window can still sum to non-zero at ts (expire hint > ts in 1024-ms units), listed:
+// a coalesced pass over the 4-B hints, the indices gathered in LDS, one append per TOP_LDS of them.
+__global__ __launch_bounds__(256) void k_ptop_fresh(const uint32_t *__restrict__ expire, uint64_t cap, int64_t ts,
+                                                    uint32_t *__restrict__ list, unsigned long long *__restrict__ list_n,
+                                                    uint64_t list_cap) {
+    __shared__ uint32_t s_idx[TOP_LDS];
+    __shared__ uint32_t s_n;
+    __shared__ unsigned long long s_base;
+    const uint32_t t = threadIdx.x;
+    const uint32_t lane = lane_id();
+    if (t == 0) s_n = 0;
+    __syncthreads();
+    auto flush = [&] {                                    // (block-uniform, after a barrier)
+        const uint32_t m = s_n;
+        if (m == 0) return;
+        if (t == 0) s_base = atomicAdd(list_n, (unsigned long long)m);
+        __syncthreads();
+        const unsigned long long b0 = s_base;
+        for (uint32_t i = t; i < m; i += blockDim.x)
+            if (b0 + i < list_cap) list[b0 + i] = s_idx[i];
+        __syncthreads();
+        if (t == 0) s_n = 0;
+        __syncthreads();
+    };
+    const uint32_t uts = (uint32_t)((uint64_t)(ts < 0 ? 0 : ts) >> 10);
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + t; s - t < cap; s += (uint64_t)gridDim.x * blockDim.x) {
+        const bool fresh = s < cap && expire[s] > uts;
+        const uint64_t act = __builtin_amdgcn_ballot_w64(fresh);
+        if (act) {
+            const int first = __ffsll((unsigned long long)act) - 1;
+            uint32_t wb = 0;
+            if ((int)lane == first) wb = atomicAdd(&s_n, (uint32_t)__popcll(act));
+            wb = __shfl(wb, first, WAVE);
+            if (fresh) s_idx[wb + (uint32_t)__popcll(act & ((1ull << lane) - 1ull))] = (uint32_t)s;
+        }
+        __syncthreads();
+        if (s_n > TOP_LDS - blockDim.x) flush();
+    }
+    flush();
+}
+
 __global__ __launch_bounds__(256) void k_ptop_sums(PSlots T, uint64_t cap, int32_t R, const int32_t *__restrict__ rn,
                                                    const int32_t *__restrict__ rw, const double *__restrict__ rrcp,
-                                                   int64_t ts, TopCands C, unsigned long long *__restrict__ toprank,
-                                                   int number) {
+                                                   int64_t ts, TopCands C, const uint32_t *__restrict__ list,
+                                                   const unsigned long long *__restrict__ list_n, uint64_t list_cap) {
+    // list (k_ptop_fresh): walk only the listed slots; else every slot (with the expire hint test)
+    // candidates gathered in LDS and appended with one atomic per TOP_LDS of them: one atomic per wave on
+    // the list's single counter queued at one memory channel (4.2 ms for ~1M waves at config 4)
+    __shared__ unsigned long long s_key[TOP_LDS];
+    __shared__ int32_t s_rule[TOP_LDS];
+    __shared__ int64_t s_sum[TOP_LDS];
+    __shared__ uint32_t s_n;
+    __shared__ unsigned long long s_base;
+    const uint32_t t = threadIdx.x;
     const uint32_t lane = lane_id();
-    const uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~(uint32_t)(WAVE - 1));
-    const uint64_t s = base + lane;
-    unsigned long long key = PKEY_EMPTY;
-    int32_t r = -1;
-    // with the expire hints only the slots whose window can still sum to non-zero at ts are read
-    // (4 B per slot instead of the key and the whole window)
-    const bool fresh = !T.expire || (s < cap && T.expire[s] > (uint32_t)((uint64_t)(ts < 0 ? 0 : ts) >> 10));
-    if (s < cap && fresh) key = T.keys[s];
-    if (key != PKEY_EMPTY) {
-        r = T.rule[s];
-        if ((uint32_t)r >= (uint32_t)R) r = -1;
+    if (t == 0) s_n = 0;
+    __syncthreads();
+    auto flush = [&] {                                    // (block-uniform, after a barrier)
+        const uint32_t m = s_n;
+        if (m == 0) return;
+        if (t == 0) s_base = atomicAdd(C.n, (unsigned long long)m);
+        __syncthreads();
+        const unsigned long long b0 = s_base;
+        for (uint32_t i = t; i < m; i += blockDim.x)
+            if (b0 + i < C.cap) {
+                C.key[b0 + i] = s_key[i];
+                C.rule[b0 + i] = s_rule[i];
+                C.sum[b0 + i] = s_sum[i];
+            }
+        __syncthreads();
+        if (t == 0) s_n = 0;
+        __syncthreads();
+    };
+    const uint64_t uts = (uint64_t)(ts < 0 ? 0 : ts) >> 10;
+    uint64_t nitems = cap;
+    if (list) {
+        nitems = *list_n;
+        nitems = nitems < list_cap ? nitems : list_cap;
     }
-    uint64_t live = __builtin_amdgcn_ballot_w64(r >= 0);
-    const int grp = (int)(lane >> 4), j = (int)(lane & 15);
-    uint64_t v = 0;                                       // this lane's slot's sum (wrapping, like wrap_add)
-    while (live) {
-        int pos[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            pos[q] = live ? __ffsll((unsigned long long)live) - 1 : -1;
-            live &= live ? live - 1 : 0;
+    for (uint64_t chunk = blockIdx.x; chunk * blockDim.x < nitems; chunk += gridDim.x) {
+        const uint64_t li = chunk * blockDim.x + t;
+        const uint64_t s = li < nitems ? (list ? (uint64_t)list[li] : li) : cap;
+        unsigned long long key = PKEY_EMPTY;
+        int32_t r = -1;
+        // with the expire hints only the slots whose window can still sum to non-zero at ts are read
+        // (4 B per slot instead of the key and the whole window)
+        const bool fresh = list || !T.expire || (s < cap && T.expire[s] > (uint32_t)uts);
+        if (s < cap && fresh) key = T.keys[s];
+        if (key != PKEY_EMPTY) {
+            r = T.rule[s];
+            if ((uint32_t)r >= (uint32_t)R) r = -1;
         }
-        const int p = pos[grp];
-        const int32_t rg = __shfl(r, p < 0 ? 0 : p, WAVE);
-        uint64_t part = 0;
-        if (p >= 0) {
-            const int n = rn[rg];
-            if (j < n) {
-                const int64_t E = epoch_of(ts, rw[rg], rrcp[rg]);
-                const longlong2 *run = (const longlong2 *)(T.state + (int64_t)(base + p) * T.stride);
-                for (int jj = j; jj < n; jj += 16) {              // n > 16: lane j also sums pairs j + 16, ...
-                    const longlong2 b = run[jj];
-                    if (b.x != EPOCH_ABSENT && b.x > E - n) part += (uint64_t)b.y;
+        uint64_t live = __builtin_amdgcn_ballot_w64(r >= 0);
+        const int grp = (int)(lane >> 4), j = (int)(lane & 15);
+        uint64_t v = 0;                                   // this lane's slot's sum (wrapping, like wrap_add)
+        while (live) {
+            int pos[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                pos[q] = live ? __ffsll((unsigned long long)live) - 1 : -1;
+                live &= live ? live - 1 : 0;
+            }
+            const int p = pos[grp];
+            const int32_t rg = __shfl(r, p < 0 ? 0 : p, WAVE);
+            const uint64_t sg = __shfl(s, p < 0 ? 0 : p, WAVE);
+            uint64_t part = 0;
+            if (p >= 0) {
+                const int n = rn[rg];
+                if (j < n) {
+                    const int64_t E = epoch_of(ts, rw[rg], rrcp[rg]);
+                    const longlong2 *run = (const longlong2 *)(T.state + (int64_t)sg * T.stride);
+                    for (int jj = j; jj < n; jj += 16) {          // n > 16: lane j also sums pairs j + 16, ...
+                        const longlong2 b = run[jj];
+                        if (b.x != EPOCH_ABSENT && b.x > E - n) part += (uint64_t)b.y;
+                    }
                 }
             }
-        }
 #pragma unroll
-        for (int o = 8; o >= 1; o >>= 1) part += __shfl_xor(part, o, WAVE);     // within the 16-lane group
+            for (int o = 8; o >= 1; o >>= 1) part += __shfl_xor(part, o, WAVE);     // within the 16-lane group
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint64_t g = __shfl(part, q * 16, WAVE);
-            if ((int)lane == pos[q]) v = g;
+            for (int q = 0; q < 4; ++q) {
+                const uint64_t g = __shfl(part, q * 16, WAVE);
+                if ((int)lane == pos[q]) v = g;
+            }
         }
+        const uint64_t act = __builtin_amdgcn_ballot_w64(v != 0);
+        if (act) {
+            const int first = __ffsll((unsigned long long)act) - 1;
+            uint32_t wb = 0;
+            if ((int)lane == first) wb = atomicAdd(&s_n, (uint32_t)__popcll(act));
+            wb = __shfl(wb, first, WAVE);
+            if (v != 0) {
+                const uint32_t k = wb + (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
+                s_key[k] = key;
+                s_rule[k] = r;
+                s_sum[k] = (int64_t)v;
+            }
+        }
+        __syncthreads();
+        if (s_n > TOP_LDS - blockDim.x) flush();          // (room for the next chunk's candidates)
     }
-#ifndef SENTINEL_TOP_NOCASCADE
-    if (v != 0) top_cascade(toprank + (int64_t)r * number, number, top_rank((int64_t)v));
-#endif
-    const uint64_t act = __builtin_amdgcn_ballot_w64(v != 0);
-    if (!act) return;
-    const int first = __ffsll((unsigned long long)act) - 1;
-    unsigned long long cb = 0;
-    if ((int)lane == first) cb = atomicAdd(C.n, (unsigned long long)__popcll(act));
-    cb = __shfl(cb, first, WAVE);
-    const unsigned long long k = cb + (unsigned long long)__popcll(act & ((1ull << lane) - 1ull));
-    if (v != 0 && k < C.cap) {
-        C.key[k] = key;
-        C.rule[k] = r;
-        C.sum[k] = (int64_t)v;
-    }
+    flush();
+}
+
+// The rank cascade over a candidate list (when k_ptop_sums ran without it and the candidates are too
+// many to run the selection rounds over all of them).
+__global__ __launch_bounds__(256) void k_ptop_cascade(TopCands C, unsigned long long *__restrict__ toprank, int number) {
+    const unsigned long long m = *C.n < C.cap ? *C.n : C.cap;
+    for (unsigned long long k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (uint64_t)gridDim.x * blockDim.x)
+        top_cascade(toprank + (int64_t)C.rule[k] * number, number, top_rank(C.sum[k]));
 }
 
 // Order (int) sum descending, key ascending; `prev` = the rule's previous pick (none in round 0).
