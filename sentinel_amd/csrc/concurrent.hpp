@@ -139,7 +139,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_conc_prep(int64_t n, const Con
                                                             uint32_t *__restrict__ fkey, uint32_t finvalid,
                                                             uint32_t *__restrict__ fhist, int64_t nblocks,
                                                             uint64_t *__restrict__ aux, unsigned long long *__restrict__ desc,
-                                                            int64_t ndesc) {
+                                                            int64_t ndesc, int diag) {
     for (int64_t j = (int64_t)blockIdx.x * SORT_THREADS + threadIdx.x; j < ndesc; j += (int64_t)gridDim.x * SORT_THREADS)
         desc[j] = 0;                                      // k_conc_scan's look-back descriptors: not yet
     __shared__ uint32_t hf[MAX_PASSES][RADIX];
@@ -201,7 +201,8 @@ __global__ __launch_bounds__(SORT_THREADS) void k_conc_prep(int64_t n, const Con
             else {
                 k = (uint32_t)fidx;
                 cv = conc_value((uint32_t)i, true, (uint64_t)h);             // a release: its token's slot
-                atomicMin(&TT.rec[h].claim, (uint32_t)i);
+                if (diag & 1) TT.rec[h].claim = (uint32_t)i;          // cost diagnostic only (wrong with duplicates)
+                else atomicMin(&TT.rec[h].claim, (uint32_t)i);
             }
         } else {
             st = ST_BAD_REQUEST;

@@ -3996,7 +3996,8 @@ static int submit_concurrent(sentinel_engine_t *e, int64_t n, const ConcEvent *d
                      e->h_dev_err + 1};
     e->launch("conc_prep", n, s, [&] {
         k_conc_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(n, dev, F, TT, dout, fkey, finvalid,
-                                                                      e->w_fhist.as<uint32_t>(), nb, aux, S.desc, nt);
+                                                                      e->w_fhist.as<uint32_t>(), nb, aux, S.desc, nt,
+                                                                      e->cm_diag >> 8);
     });
     if (F > 0) {
         const EventSrc src{nullptr, (const ParamEvent *)dev, nullptr, false, aux};
