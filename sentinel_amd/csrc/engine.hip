@@ -658,9 +658,10 @@ struct sentinel_engine {
     bool cm_keys = true;               // shared sketch: the two-phase key walk (k_pp_cm_read / _walk) when allowed
     uint64_t cm_key_batches = 0;       // shared-sketch batches decided by the key walk
     uint64_t cm_block_batches = 0;     // ... of which by the block-owned walk (k_pp_cm_block)
-    bool cm_block = false;             // SENTINEL_CM_BLOCK=1: the block-owned walk (k_pp_cm_block) instead of the
-                                       // two-phase HBM walk (measured at config 4cm: 1009 vs 946 us)
+    bool cm_block = true;              // SENTINEL_CM_BLOCK=0: the two-phase HBM walk instead of the block-owned
+                                       // walk (k_pp_cm_block; config 4cm: 799 vs 946 us)
     bool cm_debug = false;             // SENTINEL_CM_DEBUG=1: the key walk's geometry on stderr
+    bool cm_c32 = true;                // SENTINEL_CM_C32=0: the block walk keeps 64-bit cells in LDS
     int cm_diag = 0;                   // SENTINEL_CM_DIAG: k_pp_cm_block cost diagnostics (wrong results)
     DevBuf w_cmsub;                    // block walk: per sub-range {first record, records}
     DevBuf d_pexpire;                  // exact param table: per slot the getTopValues expire hint (PSlots)
@@ -2099,7 +2100,7 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
     int rc = e->w_fhist.ensure((size_t)nb * P * 4);
     rc |= e->w_pscan.ensure(((size_t)ng * P + 2 * (size_t)P + 1) * 4);
     if (rc) return rc;
-    if (!e->h_cmband) HIP_OK(hipHostMalloc((void **)&e->h_cmband, 32, 0));
+    if (!e->h_cmband) HIP_OK(hipHostMalloc((void **)&e->h_cmband, 64, 0));
     uint32_t *hist = e->w_fhist.as<uint32_t>();
     uint32_t *gsum = e->w_pscan.as<uint32_t>();
     uint32_t *rstart = gsum + (size_t)ng * P;
@@ -2163,12 +2164,17 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
         k_pp_group<2, true><<<ggrid, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, pbits, sbits, ev, C.R, RR, S, out,
                                                          nullptr, gval, RC);
     });
-    HIP_OK(hipMemcpyAsync(e->h_cmband, flag, 8, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(e->h_cmband, flag, 56, hipMemcpyDeviceToHost, s));   // the flag, ..., the ts range
     HIP_OK(hipStreamSynchronize(s));
     if (e->h_cmband[0] != 0ull) {
         ++e->cm_overflows;
         return 1;
     }
+    // 32-bit LDS cells (tags mod 256 around the batch's newest epoch) when the batch spans < 200 epochs
+    const int32_t wsk = e->h_prule_interval.empty() ? 1 : std::max(1, e->h_prule_interval[0] / std::max(1, e->h_prule_n[0]));
+    const int64_t tlo = (int64_t)e->h_cmband[5], thi = (int64_t)~e->h_cmband[6];
+    const bool c32 = use_block && e->cm_c32 && tlo >= 0 && thi >= tlo &&
+                     thi / wsk - tlo / wsk + 2 * (int64_t)e->pmax_n < 200;
     ++e->cm_key_batches;
     const int32_t nsc = e->pmax_n;
     int64_t *mv = e->w_sval.as<int64_t>();                // (the packed values are dead after the grouping)
@@ -2177,7 +2183,14 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
         k_set_i64<<<1, 64, 0, s>>>(ctl + 2, (long long)CM_EHI_NONE);
         e->launch("param_cm_block", n, s, [&] {
             const dim3 g(1u << C.CM.cbits);
-            k_pp_cm_block<<<g, 256, blk_bytes, s>>>(RC, sb, gval, ev, C.R, RR, C.CM, mv, ctl, tspan, out, e->cm_diag);
+            // (SENTINEL_CM_DIAG bits 6 / 7: 24 / 56 KB of unused LDS per workgroup -- an occupancy diagnostic)
+            const size_t pad = (e->cm_diag & 64) ? 24576 : (e->cm_diag & 128) ? 57344 : 0;
+            if (c32)
+                k_pp_cm_block<true><<<g, 256, blk_bytes / 2 + pad, s>>>(RC, sb, gval, ev, C.R, RR, C.CM, mv, ctl, tspan,
+                                                                        out, wsk, 1.0 / (double)wsk, e->cm_diag & 63);
+            else
+                k_pp_cm_block<false><<<g, 256, blk_bytes + pad, s>>>(RC, sb, gval, ev, C.R, RR, C.CM, mv, ctl, tspan,
+                                                                         out, wsk, 1.0 / (double)wsk, e->cm_diag & 63);
         });
         k_pp_cm_ehi<<<1, 64, 0, s>>>(ctl);
         HIP_OK(hipGetLastError());
@@ -2573,8 +2586,9 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
     if (const char *c = getenv("SENTINEL_LIM1")) e->lim1 = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_PROC_OCC")) e->process_occ = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_PART_SPLIT")) e->part_split = std::string(c) == "1";
-    if (const char *c = getenv("SENTINEL_CM_BLOCK")) e->cm_block = std::string(c) == "1";
+    if (const char *c = getenv("SENTINEL_CM_BLOCK")) e->cm_block = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_CM_DEBUG")) e->cm_debug = std::string(c) == "1";
+    if (const char *c = getenv("SENTINEL_CM_C32")) e->cm_c32 = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_CM_DIAG")) e->cm_diag = atoi(c);
     if (hipDeviceGetAttribute(&e->num_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) e->num_cu = 0;
     if (const char *c = getenv("SENTINEL_PARAM_CAPACITY")) {

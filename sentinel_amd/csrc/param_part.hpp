@@ -28,6 +28,8 @@
 // slot's window header and the dirty pairs.
 #pragma once
 
+#include <type_traits>
+
 #include "param_rules.hpp"
 #include "param_table.hpp"
 #include "partition.hpp"
@@ -1040,8 +1042,95 @@ __device__ inline void cm_lds_flush(unsigned long long *cl, unsigned long long *
     }
 }
 
-constexpr uint32_t CMB_VCAP = 512;        // grouped values (and their M) of one block staged in LDS; listed keys
-constexpr uint32_t CMB_WORDS = 6144;      // slots of one block (48 KB: the host checks)
+// 32-bit LDS cells (k_pp_cm_block<true>): {tag : 8 = epoch mod 256, count : 24, saturating}, relative to
+// the batch's newest epoch Eref.  Loaded from the 64-bit HBM slots: a slot more than 255 epochs older than
+// Eref is no window's (the host takes this path only for batches spanning < 200 epochs) and loads empty; a
+// slot newer than Eref (outside the precondition) loads saturated and frozen (never written back); a
+// count at or past 2^24 - 1 loads saturated.  A saturated count reads as "at least 2^40" (over, never
+// under).  Written back only where the batch added, the full tag rebuilt from Eref (or kept when the slot's
+// epoch did not change), a saturated count as CM_COUNT_MAX.  Half the LDS of the 64-bit cells: 5
+// workgroups per CU instead of 3 (the walk is latency-bound: 2 / 1 workgroups per CU measured 1.4x / 2.6x).
+constexpr uint32_t CM32_SAT = 0xFFFFFFu;
+
+__device__ inline uint32_t cm32_load(unsigned long long x, int64_t Eref, bool &frozen) {
+    frozen = false;
+    const uint64_t cnt = x & CM_COUNT_MAX;
+    if (cnt == 0) return 0u;
+    const uint32_t tag = (uint32_t)(x >> CM_COUNT_BITS);
+    const uint32_t d = ((uint32_t)Eref - tag) & CM_TAG_MASK;       // epochs the slot lies before Eref
+    if (d >= (CM_TAG_MASK >> 1)) {                                  // a newer epoch than Eref
+        frozen = true;
+        return (tag & 0xFFu) << 24 | CM32_SAT;
+    }
+    if (d > 255) return 0u;                                         // in no window of this batch
+    return (tag & 0xFFu) << 24 | (uint32_t)(cnt < CM32_SAT ? cnt : CM32_SAT);
+}
+
+__device__ inline unsigned long long cm32_store(uint32_t v, unsigned long long orig, int64_t Eref) {
+    const uint32_t tag8 = v >> 24, cnt = v & CM32_SAT;
+    const uint64_t c64 = cnt == CM32_SAT ? CM_COUNT_MAX : (uint64_t)cnt;
+    const uint32_t otag = (uint32_t)(orig >> CM_COUNT_BITS);
+    const uint32_t d = ((uint32_t)Eref - otag) & CM_TAG_MASK;
+    if ((orig & CM_COUNT_MAX) != 0 && d <= 255 && (otag & 0xFFu) == tag8)   // the slot kept its epoch
+        return (unsigned long long)otag << CM_COUNT_BITS | c64;
+    const uint32_t tag = ((uint32_t)Eref - (((uint32_t)Eref - tag8) & 0xFFu)) & CM_TAG_MASK;
+    return (unsigned long long)tag << CM_COUNT_BITS | c64;
+}
+
+__device__ inline uint32_t cm32_next(uint32_t x, uint32_t te8, int64_t a) {
+    const uint32_t tag = x >> 24, cnt = x & CM32_SAT;
+    const bool newer = cnt != 0 && tag != te8 && ((tag - te8) & 0xFFu) < 0x80u;
+    const uint64_t base = (tag == te8 || newer) ? cnt : 0u;
+    const uint64_t c = base + (uint64_t)a;
+    return (newer ? tag : te8) << 24 | (uint32_t)(c < CM32_SAT ? c : CM32_SAT);
+}
+
+__device__ inline int64_t cm_lds_window_min(const uint32_t *cl, const uint32_t *co, int depth, int nmax,
+                                            double rcp_nmax, int nsc, int64_t E) {
+    int64_t m = INT64_MAX;
+    const int js0 = (int)cm_ring_slot(E, nmax, rcp_nmax);
+#pragma unroll
+    for (int d = 0; d < CMB_DMAX; ++d) {
+        if (d >= depth) break;
+        const uint32_t *c = cl + co[d];
+        int64_t sum = 0;
+        int js = js0;
+        for (int k = 0; k < nsc; ++k) {                   // the window's slots: epochs E .. E - n + 1
+            const uint32_t x = c[js];
+            const uint32_t cnt = x & CM32_SAT;
+            if ((((uint32_t)E - (x >> 24)) & 0xFFu) < (uint32_t)nsc)
+                sum += cnt == CM32_SAT ? ((int64_t)1 << 40) : (int64_t)cnt;
+            js = js == 0 ? nmax - 1 : js - 1;
+        }
+        m = sum < m ? sum : m;
+    }
+    return m;
+}
+
+__device__ inline void cm_lds_flush(uint32_t *cl, unsigned long long *dirty, const uint32_t *co, int depth,
+                                    int nmax, double rcp_nmax, int64_t E, int64_t a) {
+    const uint32_t js = cm_ring_slot(E, nmax, rcp_nmax);
+    const uint32_t te8 = (uint32_t)E & 0xFFu;
+    uint32_t x[CMB_DMAX];
+#pragma unroll
+    for (int d = 0; d < CMB_DMAX; ++d)
+        if (d < depth) x[d] = cl[co[d] + js];
+#pragma unroll
+    for (int d = 0; d < CMB_DMAX; ++d) {
+        if (d >= depth) break;
+        const uint32_t w = co[d] + js;
+        atomicOr(&dirty[w >> 6], 1ull << (w & 63));       // (written back at the end)
+        uint32_t cur = x[d];
+        for (;;) {                                        // (ds_cmpst_rtn_b32)
+            const uint32_t prev = atomicCAS(cl + w, cur, cm32_next(cur, te8, a));
+            if (prev == cur) break;
+            cur = prev;
+        }
+    }
+}
+
+constexpr uint32_t CMB_VCAP = 480;        // grouped values (and their M) of one block staged in LDS; listed keys
+constexpr uint32_t CMB_WORDS = 6144;      // slots of one block (the host checks)
 
 // one key of a block walk: its record and everything the walk reads about it (loaded once, kept in
 // registers from phase A to phase B for the thread's first key)
@@ -1065,15 +1154,20 @@ __device__ inline CmbKey cmb_key(const PKeyRecs &RC, const PRuleRec *__restrict_
     return k;
 }
 
+template <bool C32>
 __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64_t *gval,
                                                       const ParamEvent *__restrict__ ev, ParamRules PR,
                                                       const PRuleRec *__restrict__ RR, CountMin CM,
                                                       int64_t *__restrict__ mv, long long *__restrict__ ctl,
                                                       const unsigned long long *__restrict__ tspan,
-                                                      uint64_t *__restrict__ out, int diag) {
+                                                      uint64_t *__restrict__ out, int32_t wsk, double rcp_wsk,
+                                                      int diag) {
     // diag (SENTINEL_CM_DIAG, cost diagnostics only -- wrong verdicts / counters): bit 0 no window reads,
     // bit 1 no walk, bit 2 no block load / store, bit 3 no key list, bit 4 no adds, bit 5 no verdict stores
-    extern __shared__ __attribute__((aligned(16))) unsigned long long cl[];   // depth x cols x nmax
+    using Cell = typename std::conditional<C32, uint32_t, unsigned long long>::type;
+    extern __shared__ __attribute__((aligned(16))) unsigned long long cl_raw[];
+    Cell *cl = reinterpret_cast<Cell *>(cl_raw);          // depth x cols x nmax
+    __shared__ unsigned long long frozen[C32 ? CMB_WORDS / 64 : 1];
     __shared__ uint64_t sv[CMB_VCAP];                     // the block's keys' runs, compacted in key order
     __shared__ int64_t sm[CMB_VCAP];                      // M(E) of each staged request (phase A)
     __shared__ uint32_t klist[CMB_VCAP];                  // the block's key records, longest run first
@@ -1098,10 +1192,25 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
     uint32_t nkeys = 0;
     for (uint32_t s = s0; s < s0 + ns; ++s) nkeys += RC.sub[s].y;
     if (nkeys == 0) return;                               // (block-uniform) no key: the block stays in HBM
-    if (!(diag & 4))
-        for (uint32_t i = t; i < words / 2; i += blockDim.x)
-            reinterpret_cast<ulonglong2 *>(cl)[i] = reinterpret_cast<const ulonglong2 *>(gcl)[i];
-    for (uint32_t i = t; i < CMB_WORDS / 64; i += blockDim.x) dirty[i] = 0;
+    const int64_t Eref = C32 ? epoch_of(tmax, wsk, rcp_wsk) : 0;
+    for (uint32_t i = t; i < CMB_WORDS / 64; i += blockDim.x) {
+        dirty[i] = 0;
+        if constexpr (C32) frozen[i] = 0;
+    }
+    if constexpr (C32) __syncthreads();                   // (frozen bits set by the load below)
+    if (!(diag & 4)) {
+        for (uint32_t i = t; i < words / 2; i += blockDim.x) {
+            const ulonglong2 x = reinterpret_cast<const ulonglong2 *>(gcl)[i];
+            if constexpr (C32) {
+                bool f0, f1;
+                reinterpret_cast<uint2 *>(cl)[i] = make_uint2(cm32_load(x.x, Eref, f0), cm32_load(x.y, Eref, f1));
+                if (f0 || f1)
+                    atomicOr(&frozen[(2 * i) >> 6], (f0 ? 1ull << ((2 * i) & 63) : 0ull) | (f1 ? 1ull << ((2 * i + 1) & 63) : 0ull));
+            } else {
+                reinterpret_cast<ulonglong2 *>(cl)[i] = x;
+            }
+        }
+    }
     auto for_span = [&](auto &&f) {                       // every record of the block's keys
         for (uint32_t s = s0; s < s0 + ns; ++s) {
             const uint2 sr = RC.sub[s];
@@ -1149,15 +1258,9 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
         __syncthreads();
         nlisted = khist[32];
     }
-    CmbKey k0;                                            // the thread's first listed key
-    if (listed && t < nlisted) {
-        const uint32_t r = klist[t];
-        k0 = cmb_key(RC, RR, PR, CM, r, RC.key[r]);
-    }
     auto for_keys = [&](auto &&f) {                       // (the same keys, in the same order, per thread)
         if (listed) {
-            if (t < nlisted) f(k0);
-            for (uint32_t i = t + blockDim.x; i < nlisted; i += blockDim.x) {
+            for (uint32_t i = t; i < nlisted; i += blockDim.x) {
                 const uint32_t r = klist[i];
                 f(cmb_key(RC, RR, PR, CM, r, RC.key[r]));
             }
@@ -1169,8 +1272,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
     // not fit CMB_VCAP stays in HBM (gval, and its M in mv)
     uint32_t myv = 0;
     if (listed) {
-        if (t < nlisted) myv = k0.run.y;
-        for (uint32_t i = t + blockDim.x; i < nlisted; i += blockDim.x) myv += RC.run[klist[i]].y;
+        for (uint32_t i = t; i < nlisted; i += blockDim.x) myv += RC.run[klist[i]].y;
     } else {
         for_span([&](uint32_t r, unsigned long long) { myv += RC.run[r].y; });
     }
@@ -1277,10 +1379,12 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
     if (!(diag & 4))
         for (uint32_t i = t; i < (words + 63) / 64; i += blockDim.x) {
             unsigned long long m = dirty[i];
+            if constexpr (C32) m &= ~frozen[i];
             while (m) {
                 const uint32_t w = i * 64 + (uint32_t)(__ffsll(m) - 1);
                 m &= m - 1;
-                gcl[w] = cl[w];
+                if constexpr (C32) gcl[w] = cm32_store(cl[w], gcl[w], Eref);
+                else gcl[w] = cl[w];
             }
         }
 }

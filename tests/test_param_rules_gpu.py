@@ -137,20 +137,22 @@ def test_count_min_is_one_sided(oracle_mod):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("levels", ["keys", "keys-global", "launch", "coop"])
+@pytest.mark.parametrize("levels", ["keys", "keys-c64", "keys-global", "launch", "coop"])
 def test_shared_count_min_is_one_sided(oracle_mod, monkeypatch, levels):
     """One sketch for every rule (BASELINE config 4's layout), narrow enough that rules collide, on
     batches spanning ~75 epochs.  "keys" / "keys-global": the key walk, one lane per (rule, value) key,
     every read of the batch before any add -- in one workgroup per sketch block staged in LDS
-    (k_pp_cm_block, SENTINEL_CM_BLOCK=1), or (the default) in two launches on HBM cells (k_pp_cm_read, then
-    k_pp_cm_walk: decisions and memory-side atomic adds); "launch" / "coop": one lane per rule moving through the
+    (k_pp_cm_block, the default; 32-bit LDS cells, or 64-bit with "keys-c64"), or with "keys-global" in two
+    launches on HBM cells (k_pp_cm_read, then k_pp_cm_walk: decisions and memory-side atomic adds); "launch" / "coop": one lane per rule moving through the
     epochs band by band (k_prule_cm_level / k_prule_cm_sync).  Either way no reset of a shared cell slot
     drops a count a check still needs -- zero violations of one-sidedness, and the false-block rate
     shrinks with the width."""
     import sentinel_amd as sa
     # the key walk (the default), one launch per band of rule lanes, or the grid barrier
-    monkeypatch.setenv("SENTINEL_CM_LEVELS", "keys" if levels == "keys-global" else levels)
+    monkeypatch.setenv("SENTINEL_CM_LEVELS", "keys" if levels.startswith("keys") else levels)
     monkeypatch.setenv("SENTINEL_CM_BLOCK", "0" if levels == "keys-global" else "1")
+    # the block walk's LDS cells: 32-bit (tags mod 256 around the batch's newest epoch) or 64-bit
+    monkeypatch.setenv("SENTINEL_CM_C32", "0" if levels == "keys-c64" else "1")
     count, hot, rule_idx, vals, keys, ts = T.config4(200_000, seed=53, n_rules=5000, universe=200)
     acq = np.ones(len(ts), np.int32)
     rates = {}
@@ -165,20 +167,21 @@ def test_shared_count_min_is_one_sided(oracle_mod, monkeypatch, levels):
         rates[width] = fb / dec
         cs = svc.param_cm_stats()
         if levels.startswith("keys"):
-            assert cs["key_walk"] >= 1 and cs["block"] == (cs["key_walk"] if levels == "keys" else 0), cs
+            assert cs["key_walk"] >= 1 and cs["block"] == (0 if levels == "keys-global" else cs["key_walk"]), cs
     assert rates[1 << 10] > rates[1 << 16]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("block", ["0", "1"])
+@pytest.mark.parametrize("block", ["0", "1", "1-c64"])
 def test_shared_count_min_full_size_audit(oracle_mod, monkeypatch, block):
     """BASELINE config 4's count-min mode at its own size: 100k hot-parameter rules, Zipf values over
     1000 per rule, 2M requests in 4 batches, the shared sketch at d = 4, w = 2^20 (bench config 4cm):
     every sketch verdict replayed on exact counters with the same admitted history -- zero
-    one-sidedness violations -- and a false-block rate far below the e/w bound.  Both key walks: the
-    two-phase HBM walk (the default) and the block-owned walk (SENTINEL_CM_BLOCK=1)."""
+    one-sidedness violations -- and a false-block rate far below the e/w bound.  Every key walk: the
+    block-owned walk (the default) with 32-bit or 64-bit LDS cells, and the two-phase HBM walk."""
     import sentinel_amd as sa
-    monkeypatch.setenv("SENTINEL_CM_BLOCK", block)
+    monkeypatch.setenv("SENTINEL_CM_BLOCK", block[0])
+    monkeypatch.setenv("SENTINEL_CM_C32", "0" if block.endswith("c64") else "1")
     count, hot, rule_idx, vals, keys, ts = T.config4(2_000_000, seed=61, n_rules=100_000, universe=1000)
     acq = np.ones(len(ts), np.int32)
     svc, orc = _cluster_pair(oracle_mod, count, hot, sample_count=lambda r: 10)
@@ -189,7 +192,7 @@ def test_shared_count_min_full_size_audit(oracle_mod, monkeypatch, block):
     viol, fb, dec = orc.param_cm_audit(rule_idx, acq, ts, np.arange(len(ts)), n1, keys, st)
     assert viol == 0 and dec == len(ts), viol
     assert fb / dec < 1e-4, fb / dec
-    assert svc.param_cm_stats()["block"] == (4 if block == "1" else 0), svc.param_cm_stats()
+    assert svc.param_cm_stats()["block"] == (4 if block[0] == "1" else 0), svc.param_cm_stats()
 
 
 @pytest.mark.gpu
