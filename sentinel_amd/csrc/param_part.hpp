@@ -1211,7 +1211,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
             }
         }
     }
-    auto for_span = [&](auto &&f) {                       // every record of the block's keys
+    auto for_span = [&](auto &&f) __attribute__((always_inline)) {                       // every record of the block's keys
         for (uint32_t s = s0; s < s0 + ns; ++s) {
             const uint2 sr = RC.sub[s];
             for (uint32_t i = t; i < sr.y; i += blockDim.x) {
@@ -1231,14 +1231,21 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
         if (t < 33) khist[t] = 0;
         __syncthreads();
         uint32_t m0 = 0, m1 = 0, b0 = 0, b1 = 0, nm = 0;  // (this thread's first two records of the span)
-        for_span([&](uint32_t r, unsigned long long) {
-            const uint32_t y = RC.run[r].y;
-            const uint32_t bk = 31 - (y < 31 ? y : 31);
-            atomicAdd(&khist[bk], 1u);
-            if (nm == 0) { m0 = r; b0 = bk; }
-            else if (nm == 1) { m1 = r; b1 = bk; }
-            ++nm;
-        });
+        for (uint32_t s = s0; s < s0 + ns; ++s) {         // (a plain loop and selects: kept in registers)
+            const uint2 sr = RC.sub[s];
+            for (uint32_t i = t; i < sr.y; i += blockDim.x) {
+                const uint32_t r = sr.x + i;
+                if (filter && cm_block_of(CM, RC.key[r]) != b) continue;
+                const uint32_t y = RC.run[r].y;
+                const uint32_t bk = 31 - (y < 31 ? y : 31);
+                atomicAdd(&khist[bk], 1u);
+                m0 = nm == 0 ? r : m0;
+                b0 = nm == 0 ? bk : b0;
+                m1 = nm == 1 ? r : m1;
+                b1 = nm == 1 ? bk : b1;
+                ++nm;
+            }
+        }
         __syncthreads();
         if (t == 0) {
             uint32_t acc = 0;
@@ -1258,14 +1265,14 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
         __syncthreads();
         nlisted = khist[32];
     }
-    auto for_keys = [&](auto &&f) {                       // (the same keys, in the same order, per thread)
+    auto for_keys = [&](auto &&f) __attribute__((always_inline)) {                       // (the same keys, in the same order, per thread)
         if (listed) {
             for (uint32_t i = t; i < nlisted; i += blockDim.x) {
                 const uint32_t r = klist[i];
                 f(cmb_key(RC, RR, PR, CM, r, RC.key[r]));
             }
         } else {
-            for_span([&](uint32_t r, unsigned long long key) { f(cmb_key(RC, RR, PR, CM, r, key)); });
+            for_span([&](uint32_t r, unsigned long long key) __attribute__((always_inline)) { f(cmb_key(RC, RR, PR, CM, r, key)); });
         }
     };
     // the staging offsets: this thread's keys' runs at [voff0, voff0 + myv) of sv / sm; a run that does
@@ -1280,7 +1287,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
     const uint32_t voff0 = block_exclusive_scan(myv, s_waves, &vtot);   // (its barriers: the block is in LDS)
     // A. stage the runs; reads (the block as the earlier batches left it)
     uint32_t vo = voff0;
-    for_keys([&](const CmbKey &K) {
+    for_keys([&](const CmbKey &K) __attribute__((always_inline)) {
         const uint2 run = K.run;
         const bool lds = vo + run.y <= CMB_VCAP;
         const int nsc = K.rr.nf & 0xFFFF;
@@ -1319,7 +1326,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
     // under) and is charged to the newest epoch, as k_pp_cm_walk does.
     int64_t emax = CM_EHI_NONE;
     vo = voff0;
-    auto walk = [&](uint32_t n_, int64_t *eb, int64_t *qb, const uint64_t *vb, const CmbKey &K) {
+    auto walk = [&](uint32_t n_, int64_t *eb, int64_t *qb, const uint64_t *vb, const CmbKey &K) __attribute__((always_inline)) {
         const int nsc = K.rr.nf & 0xFFFF;
         const int64_t Edead = epoch_of(tmax, K.rr.w, K.rr.rcp_w) - 2 * (int64_t)nsc;
         int64_t curE = EPOCH_ABSENT, cnt = 0, Q = 0;
@@ -1360,7 +1367,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
         }
         if (cnt > 0 && curE > Edead && !(diag & 16)) cm_lds_flush(cl, dirty, K.co, depth, nmax, rcp_nmax, curE, cnt);
     };
-    if (!(diag & 2)) for_keys([&](const CmbKey &K) {
+    if (!(diag & 2)) for_keys([&](const CmbKey &K) __attribute__((always_inline)) {
         const uint2 run = K.run;
         const bool lds = vo + run.y <= CMB_VCAP;
         if (lds)
