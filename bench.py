@@ -74,6 +74,7 @@ KERNEL_SYMBOLS = {
     "param_prep": ("k_param_prep", "k_pp_prep"), "param_meta": ("k_param_meta",), "prule_prep": ("k_prule_prep",),
     "prule_process": ("k_prule_process",), "part_unsplit": ("k_part_unsplit",), "lim_prep": ("k_lim1_prep",),
     "param_scatter": ("k_pp_scatter",), "param_group": ("k_pp_group",), "param_cm_read": ("k_pp_cm_read",), "param_cm_walk": ("k_pp_cm_walk",),
+    "param_cm_block": ("k_pp_cm_block",),
     "conc_prep": ("k_conc_prep",), "conc_scan": ("k_conc_scan",), "conc_apply": ("k_conc_apply",),
     "param_decide": ("k_pp_walk", "k_pp_decide"),
 }
@@ -504,6 +505,15 @@ class ParamWorkload:
         if dom == "process":
             # per touched (rule, value) slot: read n {epoch, count} pairs, write one; per event: segment record
             return 24.0 + (self.n * 16 + 16) / 4.0
+        if dom == "param_cm_block":
+            # per batch every sketch block with keys read once (all of them at 4cm: w x d x 2 n 8-B slots), the
+            # slots added to written back; per request the grouped value read 8, the verdict written 8; per
+            # distinct key its 16-B record and the rule record 32, and per live admitted epoch (within 2 n
+            # epochs of the batch's end) one slot per row written (8)
+            e_k = self.N / max(1, self._dk) if hasattr(self, "_dk") else 1.0
+            live = min(1.0, 2.0 * self.interval / max(1.0, float(self.span_ms())))
+            blocks = float(self.cm_width) * self.cm_depth * 2 * self.n * 8 / self.N
+            return blocks + 16.0 + (16 + 32 + live * self.cm_depth * 8) / e_k
         if dom in ("param_cm_walk", "param_cm_read"):
             # walk, per request: the grouped value read 8, the verdict written 8 (+ M(E) 8 for the requests
             # within n epochs of the previous batch); per distinct key: its 16-B record, the rule record 32,
