@@ -1047,8 +1047,8 @@ __device__ inline void cm_lds_flush(unsigned long long *cl, unsigned long long *
 // Eref is no window's (the host takes this path only for batches spanning < 200 epochs) and loads empty; a
 // slot newer than Eref (outside the precondition) loads saturated and frozen (never written back); a
 // count at or past 2^24 - 1 loads saturated.  A saturated count reads as "at least 2^40" (over, never
-// under).  Written back only where the batch added, the full tag rebuilt from Eref (or kept when the slot's
-// epoch did not change), a saturated count as CM_COUNT_MAX.  Half the LDS of the 64-bit cells: 5
+// under).  Written back only where the batch added, the full tag rebuilt from Eref, a saturated count as
+// CM_COUNT_MAX.  Half the LDS of the 64-bit cells: 5
 // workgroups per CU instead of 3 (the walk is latency-bound: 2 / 1 workgroups per CU measured 1.4x / 2.6x).
 constexpr uint32_t CM32_SAT = 0xFFFFFFu;
 
@@ -1066,13 +1066,11 @@ __device__ inline uint32_t cm32_load(unsigned long long x, int64_t Eref, bool &f
     return (tag & 0xFFu) << 24 | (uint32_t)(cnt < CM32_SAT ? cnt : CM32_SAT);
 }
 
-__device__ inline unsigned long long cm32_store(uint32_t v, unsigned long long orig, int64_t Eref) {
+// (a written slot's epoch lies in [Eref - 255, Eref] whether it kept its loaded epoch -- loaded slots
+// outside that range are empty or frozen -- or restarted at an epoch of this batch: the congruent one)
+__device__ inline unsigned long long cm32_store(uint32_t v, int64_t Eref) {
     const uint32_t tag8 = v >> 24, cnt = v & CM32_SAT;
     const uint64_t c64 = cnt == CM32_SAT ? CM_COUNT_MAX : (uint64_t)cnt;
-    const uint32_t otag = (uint32_t)(orig >> CM_COUNT_BITS);
-    const uint32_t d = ((uint32_t)Eref - otag) & CM_TAG_MASK;
-    if ((orig & CM_COUNT_MAX) != 0 && d <= 255 && (otag & 0xFFu) == tag8)   // the slot kept its epoch
-        return (unsigned long long)otag << CM_COUNT_BITS | c64;
     const uint32_t tag = ((uint32_t)Eref - (((uint32_t)Eref - tag8) & 0xFFu)) & CM_TAG_MASK;
     return (unsigned long long)tag << CM_COUNT_BITS | c64;
 }
@@ -1142,14 +1140,22 @@ struct CmbKey {
     uint32_t co[CMB_DMAX];
 };
 
+// full = false (phase A): the shared sketch's rules all have one window (the host checks it when the
+// rules load), so the rule record is not read -- `u` carries the window; phase B reads it for the threshold
 __device__ inline CmbKey cmb_key(const PKeyRecs &RC, const PRuleRec *__restrict__ RR, const ParamRules &PR,
-                                 const CountMin &CM, uint32_t r, unsigned long long key) {
+                                 const CountMin &CM, uint32_t r, unsigned long long key, bool full,
+                                 const PRuleRec &u) {
     CmbKey k;
     k.key = key;
     k.run = RC.run[r];
-    const int32_t rule = RC.rule[r];
-    k.rr = RR[rule];
-    k.thr = (k.rr.nf >> 16) ? value_threshold(PR, (uint32_t)rule, key) : k.rr.thr;   // CPFC:101-120
+    if (full) {
+        const int32_t rule = RC.rule[r];
+        k.rr = RR[rule];
+        k.thr = (k.rr.nf >> 16) ? value_threshold(PR, (uint32_t)rule, key) : k.rr.thr;   // CPFC:101-120
+    } else {
+        k.rr = u;
+        k.thr = 0.0;
+    }
     cm_lds_cells(k.co, CM.depth, CM.nmax, CM.cols, key);
     return k;
 }
@@ -1265,14 +1271,17 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
         __syncthreads();
         nlisted = khist[32];
     }
-    auto for_keys = [&](auto &&f) __attribute__((always_inline)) {                       // (the same keys, in the same order, per thread)
+    const PRuleRec uwin{rcp_wsk, 0.0, 0.0, wsk, CM.nmax / 2};    // the sketch's one window (phase A)
+    auto for_keys = [&](bool full, auto &&f) __attribute__((always_inline)) {   // (same keys, same order per thread)
         if (listed) {
             for (uint32_t i = t; i < nlisted; i += blockDim.x) {
                 const uint32_t r = klist[i];
-                f(cmb_key(RC, RR, PR, CM, r, RC.key[r]));
+                f(cmb_key(RC, RR, PR, CM, r, RC.key[r], full, uwin));
             }
         } else {
-            for_span([&](uint32_t r, unsigned long long key) __attribute__((always_inline)) { f(cmb_key(RC, RR, PR, CM, r, key)); });
+            for_span([&](uint32_t r, unsigned long long key) __attribute__((always_inline)) {
+                f(cmb_key(RC, RR, PR, CM, r, key, full, uwin));
+            });
         }
     };
     // the staging offsets: this thread's keys' runs at [voff0, voff0 + myv) of sv / sm; a run that does
@@ -1287,7 +1296,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
     const uint32_t voff0 = block_exclusive_scan(myv, s_waves, &vtot);   // (its barriers: the block is in LDS)
     // A. stage the runs; reads (the block as the earlier batches left it)
     uint32_t vo = voff0;
-    for_keys([&](const CmbKey &K) __attribute__((always_inline)) {
+    for_keys(false, [&](const CmbKey &K) __attribute__((always_inline)) {
         const uint2 run = K.run;
         const bool lds = vo + run.y <= CMB_VCAP;
         const int nsc = K.rr.nf & 0xFFFF;
@@ -1367,7 +1376,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
         }
         if (cnt > 0 && curE > Edead && !(diag & 16)) cm_lds_flush(cl, dirty, K.co, depth, nmax, rcp_nmax, curE, cnt);
     };
-    if (!(diag & 2)) for_keys([&](const CmbKey &K) __attribute__((always_inline)) {
+    if (!(diag & 2)) for_keys(true, [&](const CmbKey &K) __attribute__((always_inline)) {
         const uint2 run = K.run;
         const bool lds = vo + run.y <= CMB_VCAP;
         if (lds)
@@ -1390,7 +1399,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
             while (m) {
                 const uint32_t w = i * 64 + (uint32_t)(__ffsll(m) - 1);
                 m &= m - 1;
-                if constexpr (C32) gcl[w] = cm32_store(cl[w], gcl[w], Eref);
+                if constexpr (C32) gcl[w] = cm32_store(cl[w], Eref);
                 else gcl[w] = cl[w];
             }
         }
