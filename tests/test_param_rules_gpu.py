@@ -196,6 +196,41 @@ def test_shared_count_min_full_size_audit(oracle_mod, monkeypatch, block):
 
 
 @pytest.mark.gpu
+def test_shared_count_min_block_epoch_edges(oracle_mod, monkeypatch):
+    """The block walk's 32-bit LDS cells hold epochs mod 256 around the batch's newest one, and are used
+    only for batches spanning < 200 epochs.  Batches that stress that: one over ~80 epochs (32-bit cells),
+    one 400 epochs after it (every slot older than 255 epochs loads empty), one spanning ~300 epochs (the
+    64-bit cells take it), one right after it (32-bit again, reading what the 64-bit batch wrote), and one
+    whose first requests sit exactly n epochs after the previous batch's end -- every verdict audited on
+    exact counters replaying the sketch's own decisions: zero one-sidedness violations."""
+    import sentinel_amd as sa
+    monkeypatch.setenv("SENTINEL_CM_BLOCK", "1")
+    monkeypatch.setenv("SENTINEL_CM_C32", "1")
+    count, hot, rule_idx, vals, keys, ts0 = T.config4(250_000, seed=71, n_rules=3000, universe=300)
+    acq = np.ones(len(ts0), np.int32)
+    svc, orc = _cluster_pair(oracle_mod, count, hot, sample_count=lambda r: 10)   # w = 100 ms
+    svc.set_param_mode(sa._lib.PARAM_COUNT_MIN_SHARED, depth=4, width=1 << 14)
+    t = T.T0_ALIGNED + 7
+    spans = [8_000, 3_000, 30_000, 5_000, 6_000]          # ms: 80, 30, 300, 50, 60 epochs
+    gaps = [0, 40_000, 0, 0, 1_000]                       # ms before each batch
+    ts = np.empty(len(ts0), np.int64)
+    st = []
+    per = len(ts0) // len(spans)
+    for b, (span, gap) in enumerate(zip(spans, gaps)):
+        s = slice(b * per, (b + 1) * per)
+        t += gap
+        ts[s] = t + np.floor(np.arange(per, dtype=np.float64) * (span / per)).astype(np.int64)
+        t = int(ts[s][-1]) + 1
+        st.append(svc.submit_param_batch_host(rule_idx[s], acq[s], keys[s], ts[s])[0])
+    m = per * len(spans)
+    st = np.concatenate(st)
+    viol, fb, dec = orc.param_cm_audit(rule_idx[:m], acq[:m], ts[:m], np.arange(m), np.ones(m, np.int32), keys[:m], st)
+    assert viol == 0 and dec == m, (viol, dec)
+    assert (st == 1).any() and (st == 0).any()
+    assert svc.param_cm_stats()["block"] == len(spans), svc.param_cm_stats()
+
+
+@pytest.mark.gpu
 def test_avg_local_params_follow_connected_count(oracle_mod):
     """ClusterParamFlowChecker.calcGlobalThreshold reads ConnectionManager.getConnectedCount on every
     request (CPFC:101-111): AVG_LOCAL param rules (hot items included) must see a connected count that
