@@ -2144,7 +2144,9 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
     // block-owned walk (k_pp_cm_block) when a sketch block fits LDS; sub-ranges are made narrow enough
     // (up to 2^8 per range) that one spans at most 4 blocks
     const size_t blk_bytes = (size_t)C.CM.depth * C.CM.cols * (size_t)C.CM.nmax * 8;
-    bool use_block = e->cm_block && C.CM.shared && C.CM.depth <= 4 && blk_bytes <= 49152 && e->pmax_n <= 16;
+    // (and at least 16 blocks: a narrower sketch would leave the batch to a handful of workgroups)
+    bool use_block = e->cm_block && C.CM.shared && C.CM.depth <= 4 && blk_bytes <= 49152 && e->pmax_n <= 16 &&
+                     C.CM.cbits >= 4;
     if (use_block)
         while (sbits < 8 && pbits + sbits + 2 < C.CM.cbits) ++sbits;
     const int sb = pbits + sbits;
