@@ -2110,8 +2110,9 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
     const int32_t *route = e->param_plain ? nullptr : e->d_prule_route.as<int32_t>();
     const ParamCtx C = e->param_ctx();
     unsigned long long *tspan = flag + 5;                                      // [5..6] the batch's ts range
-    HIP_OK(hipMemsetAsync(flag, 0, 8, s));               // set by k_pp_group on a sub-range overflow
-    HIP_OK(hipMemsetAsync(tspan, 0xFF, 16, s));
+    // the overflow flag (set by k_pp_group), the ts range (k_pp_prep) and the walk's newest epoch, reset
+    // by one launch
+    k_cm_batch_init<<<1, 64, 0, s>>>(flag, tspan, ctl);
     e->launch("param_prep", n, s, [&] {
         k_pp_prep<<<dim3((unsigned)nb), dim3(PP_THREADS), 0, s>>>(n, ev, R, route, C.R, out, pbits, hist, P,
                                                                   e->w_counters.as<uint32_t>(), tspan);
@@ -2181,8 +2182,7 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
     const int32_t nsc = e->pmax_n;
     int64_t *mv = e->w_sval.as<int64_t>();                // (the packed values are dead after the grouping)
     if (use_block) {
-        ++e->cm_block_batches;
-        k_set_i64<<<1, 64, 0, s>>>(ctl + 2, (long long)CM_EHI_NONE);
+        ++e->cm_block_batches;                            // (ctl[2] reset by k_cm_batch_init)
         e->launch("param_cm_block", n, s, [&] {
             const dim3 g(1u << C.CM.cbits);
             // (SENTINEL_CM_DIAG bits 6 / 7: 24 / 56 KB of unused LDS per workgroup -- an occupancy diagnostic)

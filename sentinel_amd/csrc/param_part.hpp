@@ -1412,6 +1412,16 @@ __global__ void k_pp_cm_ehi(long long *ctl) {
     if (h != CM_EHI_ANY && e != CM_EHI_NONE && (h == CM_EHI_NONE || e > h)) ctl[0] = e;
 }
 
+// Per shared count-min key-walk batch: flag = 0, ts range = {~0, ~0} (atomicMin targets), ctl[2] = none.
+__global__ void k_cm_batch_init(unsigned long long *flag, unsigned long long *tspan, long long *ctl) {
+    if (threadIdx.x == 0) {
+        *flag = 0;
+        tspan[0] = ~0ull;
+        tspan[1] = ~0ull;
+        ctl[2] = CM_EHI_NONE;
+    }
+}
+
 __global__ void k_set_i64(long long *p, long long v) {
     if (threadIdx.x == 0) *p = v;
 }
