@@ -2164,7 +2164,7 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
     if (use_block) RC.sub = e->w_cmsub.as<uint2>();
     const PSlots S{};
     e->launch("param_group", n, s, [&] {
-        k_pp_group<2, true><<<ggrid, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, pbits, sbits, ev, C.R, RR, S, out,
+        k_pp_group<2, true, 10><<<ggrid, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, pbits, sbits, ev, C.R, RR, S, out,
                                                          nullptr, gval, RC);
     });
     HIP_OK(hipMemcpyAsync(e->h_cmband, flag, 56, hipMemcpyDeviceToHost, s));   // the flag, ..., the ts range

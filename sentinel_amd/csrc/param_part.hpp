@@ -308,6 +308,7 @@ constexpr int64_t PG_TARGET = PG_CAP * 4 / 5;
 // Insert / find a key in the chunk's LDS table; -1: not within PD_PROBES probes (full neighbourhood).
 // All requests of one key agree: entries never change once set, so every request of a key that fails
 // saw the same PD_PROBES other keys.
+template <uint32_t HT = PD_HT>
 __device__ inline int pd_insert(unsigned long long *hkey, int32_t *hrule, unsigned long long key, int32_t rule,
                                 uint32_t h0) {
     uint32_t h = h0;
@@ -322,7 +323,7 @@ __device__ inline int pd_insert(unsigned long long *hkey, int32_t *hrule, unsign
             }
             if (prev == key) return (int)h;
         }
-        h = (h + 1) & (PD_HT - 1);
+        h = (h + 1) & (HT - 1);
     }
     return -1;
 }
@@ -475,7 +476,9 @@ struct PKeyRecs {
 // distinct key; k_pp_walk decides the keys.  A larger sub-range (a skewed batch) is decided here, chunk
 // after chunk in arrival order, one lane per distinct key of the chunk (a key spanning chunks is walked
 // once per chunk, in order).
-template <int NMAX, bool CM = false>
+// HB: bits of the LDS key table (the count-min grouping, which only emits, uses a 1024-entry table: 40 KB of
+// LDS, 2x the workgroups per CU; a chunk with more distinct keys than the table takes more rounds)
+template <int NMAX, bool CM = false, int HB = PD_HBITS>
 __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long long *__restrict__ pkey,
                                                           const uint64_t *__restrict__ pval,
                                                           const int32_t *__restrict__ prule,
@@ -484,12 +487,15 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
                                                           ParamRules PR, const PRuleRec *__restrict__ RR, PSlots S,
                                                           uint64_t *__restrict__ out, unsigned long long *fresh,
                                                           uint64_t *__restrict__ gval, PKeyRecs RC) {
+    constexpr uint32_t HT = 1u << HB;
+    constexpr int EPT = HT / PD_THREADS;
+    static_assert(HT % PD_THREADS == 0 && HT <= 65536, "entries per thread, 16-bit key list");
     __shared__ uint32_t cq[PG_CAP];                   // the chunk's requests: positions in pkey / pval / prule
     __shared__ uint64_t sv[PG_CAP];                   // grouped values
-    __shared__ unsigned long long hkey[PD_HT];
-    __shared__ int32_t hrule[PD_HT];
-    __shared__ uint16_t cnt[PD_WAVES][PD_HT];
-    __shared__ uint32_t hstart[PD_HT + 1];
+    __shared__ unsigned long long hkey[HT];
+    __shared__ int32_t hrule[HT];
+    __shared__ uint16_t cnt[PD_WAVES][HT];
+    __shared__ uint32_t hstart[HT + 1];
     __shared__ uint32_t waves_tot[PD_WAVES];
     __shared__ uint32_t s_fresh, s_rbase;
     const uint32_t nsub = 1u << sbits;
@@ -532,10 +538,10 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
                     ru[j] = prule[q];
                 }
             }
-            for (uint32_t e = t; e < PD_HT; e += PD_THREADS) hkey[e] = PKEY_EMPTY;
+            for (uint32_t e = t; e < HT; e += PD_THREADS) hkey[e] = PKEY_EMPTY;
             {
                 uint32_t *z = reinterpret_cast<uint32_t *>(&cnt[0][0]);
-                for (uint32_t d = t; d < PD_WAVES * PD_HT / 2; d += PD_THREADS) z[d] = 0;
+                for (uint32_t d = t; d < PD_WAVES * HT / 2; d += PD_THREADS) z[d] = 0;
             }
             __syncthreads();
             int eid[PG_ITEMS];
@@ -543,7 +549,7 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
             for (int j = 0; j < PG_ITEMS; ++j) {
                 eid[j] = -1;
                 if (pend & (1u << j))
-                    eid[j] = pd_insert(hkey, hrule, k[j], ru[j], (uint32_t)(mix64(k[j]) >> 32) & (PD_HT - 1));
+                    eid[j] = pd_insert<HT>(hkey, hrule, k[j], ru[j], (uint32_t)(mix64(k[j]) >> 32) & (HT - 1));
             }
             __syncthreads();
             [[maybe_unused]] const unsigned long long pt1 = PD_NOW();
@@ -552,7 +558,7 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
             for (int j = 0; j < PG_ITEMS; ++j) {
                 const bool valid = eid[j] >= 0;
                 const uint32_t d = valid ? (uint32_t)eid[j] : 0u;
-                const uint64_t peers = match_peers<PD_HBITS>(d, valid, PD_HBITS);
+                const uint64_t peers = match_peers<HB>(d, valid, HB);
                 uint32_t r = 0;
                 if (valid) r = cnt[wave][d] + mask_rank(peers);
                 __builtin_amdgcn_wave_barrier();
@@ -563,11 +569,11 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
             __syncthreads();
             // per entry: exclusive over waves in place, then one exclusive scan over entries of
             // {requests : 16 | distinct keys : 16} -> run starts and each key's place in the key list
-            uint32_t tot[PD_EPT];
+            uint32_t tot[EPT];
             uint32_t mine = 0;
 #pragma unroll
-            for (int q = 0; q < PD_EPT; ++q) {
-                const uint32_t e = t * PD_EPT + q;
+            for (int q = 0; q < EPT; ++q) {
+                const uint32_t e = t * EPT + q;
                 uint32_t run = 0;
 #pragma unroll
                 for (int w = 0; w < PD_WAVES; ++w) {
@@ -583,13 +589,13 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
             uint32_t kpos = pre >> 16;
             pre &= 0xFFFFu;
 #pragma unroll
-            for (int q = 0; q < PD_EPT; ++q) {
-                hstart[t * PD_EPT + q] = pre;
+            for (int q = 0; q < EPT; ++q) {
+                hstart[t * EPT + q] = pre;
                 pre += tot[q];
             }
             const uint32_t nkeys = total >> 16;
             const uint32_t placed = total & 0xFFFFu;
-            if (t == 0) hstart[PD_HT] = placed;
+            if (t == 0) hstart[HT] = placed;
             if (emit && t == 0 && !RC.sub) s_rbase = atomicAdd(RC.count, nkeys);
             __syncthreads();
 #pragma unroll
@@ -603,8 +609,8 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
             // the distinct keys listed densely (over the wave counters, free now)
             uint16_t *klist = &cnt[0][0];
 #pragma unroll
-            for (int q = 0; q < PD_EPT; ++q)
-                if (tot[q]) klist[kpos++] = (uint16_t)(t * PD_EPT + q);
+            for (int q = 0; q < EPT; ++q)
+                if (tot[q]) klist[kpos++] = (uint16_t)(t * EPT + q);
             __syncthreads();
             [[maybe_unused]] const unsigned long long pt2 = PD_NOW();
             if (emit) {
