@@ -54,8 +54,6 @@ KERNEL_BYTES_PER_EVENT = {
     "lim_prep": 32.0,         # one-limiter prep: read the 16-B event, write flow key 4 + limiter key 4 + value 8
     "part_prep": 16.0,        # read the 16-B event (range histogram in LDS; no key array without namespace routes)
     "part_scatter": 24.0,     # read the 16-B event (key re-derived), write the 8-B packed value (local key inside)
-    "part_split": 24.0,       # one sweep: read the 16-B event (its second read is served by the Infinity Cache),
-                              # write the 8-B packed value; the digit columns are ~4 KB per workgroup
     "param_prep": 24.0,       # read the 24-B event (range histogram in LDS; rejected requests answered here)
     "param_scatter": 44.0,    # read the 24-B event, write key 8 + packed value 8 + rule 4
     "param_meta": 48.0,       # per slot after a rule / threshold / table change: key 8, rule fields ~16, write ~20 B
@@ -69,7 +67,7 @@ KERNEL_BYTES_PER_EVENT = {
 KERNEL_SYMBOLS = {
     "flow_prep": ("k_flow_prep",), "radix_hist": ("k_radix_hist_pass",), "radix_scatter": ("k_radix_scatter_p",),
     "scan": ("k_scan_lookback",), "segments": ("k_segments",), "process": ("k_process",), "verdict": ("k_verdict",),
-    "part_prep": ("k_part_prep",), "part_scatter": ("k_part_scatter",), "part_split": ("k_part_split",),
+    "part_prep": ("k_part_prep",), "part_scatter": ("k_part_scatter",),
     "part_fused": ("k_part_half",), "part_big": ("k_part_big",), "part_long": ("k_part_long",),
     "param_prep": ("k_param_prep", "k_pp_prep"), "param_meta": ("k_param_meta",), "prule_prep": ("k_prule_prep",),
     "prule_process": ("k_prule_process",), "part_unsplit": ("k_part_unsplit",), "lim_prep": ("k_lim1_prep",),
@@ -187,6 +185,10 @@ def parse():
     ap.add_argument("--latency-batches", type=int, default=200,
                     help="batches of the untimed latency loop (p99 from these, not from the timed steps)")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-fed legs")
+    ap.add_argument("--output", choices=["arrival", "decide"], default="decide",
+                    help="flow configs: verdicts in arrival order (sentinel_submit_flow_batch) or in decide order "
+                         "with their arrival positions (sentinel_submit_flow_batch_ordered: what the batcher and the "
+                         "wire server consume)")
     ap.add_argument("--host-reps", type=int, default=200)
     return ap.parse_args()
 
@@ -247,6 +249,12 @@ class FlowWorkload:
             self.zipf_cdf = torch.from_numpy(np.cumsum(w) / w.sum()).to(dev)
             self.zipf_perm = torch.from_numpy(perm.astype(np.int32)).to(dev)
         self.verdicts = torch.empty(self.N, dtype=torch.int64, device=dev)
+        self.seq = torch.empty(self.N, dtype=torch.int32, device=dev)
+        self.ordered = args.output == "decide"
+        if self.ordered:
+            self.workload += ("; verdicts in decide order with their arrival positions (sentinel_submit_flow_batch_"
+                              "ordered, the output the batcher / wire server consume: each response keyed by its "
+                              "request)")
         self.kept = []
         self.parity_result = None
 
@@ -274,17 +282,37 @@ class FlowWorkload:
     def submit(self, b, keep=False):
         if keep:                          # a verdict buffer of its own: checked against the CPU baseline's replay
             v = self.torch.empty(self.N, dtype=self.torch.int64, device=self.dev)
-            self.svc.submit_flow_batch(b, verdicts=v)
-            self.kept.append(v)
+            if self.ordered:
+                sq = self.torch.empty(self.N, dtype=self.torch.int32, device=self.dev)
+                self.svc.submit_flow_batch_ordered(b, verdicts=v, seq=sq)
+                self.kept.append((v, sq))
+            else:
+                self.svc.submit_flow_batch(b, verdicts=v)
+                self.kept.append(v)
+        elif self.ordered:
+            self.svc.submit_flow_batch_ordered(b, verdicts=self.verdicts, seq=self.seq)
         else:
             self.svc.submit_flow_batch(b, verdicts=self.verdicts)
+
+    def _arrival(self, k):
+        """A kept batch's verdicts at their arrival positions (decide-order output put back by its seq,
+        after the fact: only for the parity check)."""
+        if not isinstance(k, tuple):
+            return k
+        v, sq = k
+        s = sq.to(self.torch.int64)
+        assert self.torch.equal(self.torch.sort(s).values, self.torch.arange(len(s), device=s.device)), \
+            "decide-order seq is not a permutation"
+        out = self.torch.empty_like(v)
+        out[s] = v
+        return out
 
     def parity(self, st, rem, wait):
         """The kept batches' GPU verdicts against the oracle replay of the same events (first batches)."""
         from sentinel_amd.token_service import decode_verdicts
         if not self.kept:
             return None
-        g = [decode_verdicts(v) for v in self.kept]
+        g = [decode_verdicts(self._arrival(v)) for v in self.kept]
         gs, gr, gw = (np.concatenate([x[i] for x in g]) for i in range(3))
         m = min(len(gs), len(st))
         bad = int(((gs[:m] != st[:m]) | (gr[:m] != rem[:m]) | (gw[:m] != wait[:m])).sum())
@@ -335,8 +363,9 @@ class FlowWorkload:
             # per event: read the 8-B packed value (local key inside), write the 8-B verdict; per
             # touched flow: read the window header (16 B per bucket) and the rule fields, write back
             # the rolled bucket's 16-B pair, read + write its BLOCK / PASS_REQUEST / BLOCK_REQUEST
-            # counters (3 x 8 B each way, blocked counter rows)
-            return 16.0 + (n * 16 + 42 + 16 + 48) / max(1.0, e_f)
+            # counters (3 x 8 B each way, blocked counter rows); decide-order output also writes each
+            # event's 4-B arrival position
+            return (20.0 if self.ordered else 16.0) + (n * 16 + 42 + 16 + 48) / max(1.0, e_f)
         if dom == "radix_scatter":
             passes = max(1, round(d["calls"] / max(1, steps)))
             return (32.0 + 24.0 * (passes - 1)) / passes
@@ -352,11 +381,12 @@ class FlowWorkload:
         rolled slot's BLOCK / PASS_REQUEST / BLOCK_REQUEST rows read and written (48) and ~42 B of rule
         fields (w, 1/w, I_s, threshold, kind, occupy flag)."""
         n = int(self.rules.sample_count.max())
-        return 24.0 + (16 * n + 16 + 48 + 42) / max(1.0, self.N / max(1, self.F))
+        return (28.0 if self.ordered else 24.0) + (16 * n + 16 + 48 + 42) / max(1.0, self.N / max(1, self.F))
 
     def shape(self):
         return {"config": self.args.config, "flows": self.F, "events": self.N,
-                "sample_count": int(self.rules.sample_count.max())}
+                "sample_count": int(self.rules.sample_count.max()),
+                "output": "decide order + arrival positions" if self.ordered else "arrival order"}
 
 
 class ParamWorkload:
@@ -666,6 +696,9 @@ class ConcWorkload:
         return {"config": self.args.config, "flows": self.F, "events": self.N}
 
 
+CM_AUDIT_BATCHES = 6    # consecutive 4cm batches audited on exact counters (each spans ~80 epochs of 100 ms)
+
+
 def main():
     args = parse()
     import torch
@@ -709,8 +742,8 @@ def main():
     # own, checked against the CPU baseline's oracle replay of the same events (parity_* fields)
     check = rank == 0 and world == 1 and not args.no_cpu_baseline
     keep_n = min(args.cpu_steps_mt, args.warmup + pstep) if check else 0
-    if args.config == "4cm":                                    # the count-min audit's sample: the first two batches
-        keep_n = max(keep_n, min(2, args.warmup + pstep))
+    if args.config == "4cm":                                    # the count-min audit's sample: the first six batches
+        keep_n = max(keep_n, min(CM_AUDIT_BATCHES, args.warmup + pstep))   # (~480 epochs: a 140-240-epoch re-touch)
     for s in range(args.warmup):
         W.submit(ev_b[s], keep=s < keep_n)
     svc.synchronize()
@@ -969,7 +1002,7 @@ def main():
 
     extra = {}
     if args.config == "4cm" and rank == 0 and world == 1:
-        keep_verdicts = W.kept[:2]
+        keep_verdicts = W.kept[:CM_AUDIT_BATCHES]
         k = len(keep_verdicts)
         viol, fb, dec = W.false_blocks(ev_b, k, keep_verdicts)
         eps_n = float(np.e) / W.cm_width * float(N) * k      # e/w x (requests counted in the audited span)
@@ -977,7 +1010,7 @@ def main():
                               "violations": int(viol), "false_blocks": int(fb),
                               "false_block_rate": round(fb / max(1, dec), 8),
                               "eps_N_bound_counts": round(eps_n, 2),
-                              "note": "the sketch's verdicts of the warmup+profile batches replayed on exact counters "
+                              "note": f"the sketch's verdicts of the first {k} consecutive batches (warmup + profile) replayed on exact counters "
                                       "(oracle, same admitted history): violations = sketch passed what exact would "
                                       "block (must be 0); bound (blocked layout): P[overestimate > (e/64) N_B] <= exp(-d), N_B = the "
                                       "window count of the key's 64-column block, E[N_B] = 64 N / w, so (e/w) N on "

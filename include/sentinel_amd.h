@@ -189,6 +189,20 @@ int  sentinel_submit_flow_batch(sentinel_engine_t *eng, int64_t n, const sentine
 /* Same with HOST pointers (pinned or pageable): H2D, decide, D2H, synchronous. */
 int  sentinel_submit_flow_batch_host(sentinel_engine_t *eng, int64_t n, const sentinel_event_t *events,
                                      const uint8_t *flags, sentinel_verdict_t *verdicts);
+/* Decide-order output: the same decisions and window counters as sentinel_submit_flow_batch, but
+ * verdicts[j] answers the event at arrival position seq[j] (seq is a permutation of [0, n)) instead of
+ * the event at position j.  The reference answers each requestToken call on its own connection, keyed
+ * by the request's xid (srv/server/handler/TokenServerHandler.java:61-81, ClusterResponse), so a
+ * consumer that routes every verdict by its seq -- the batcher and the wire server do -- never needs
+ * arrival order.  The partition path then writes every flow range's verdicts to its own contiguous
+ * positions (whole lines) instead of 8-byte stores scattered over the batch; batches it does not take
+ * (small, skewed, namespace limiters) come back in arrival order with seq = identity.  DEVICE pointers
+ * (verdicts n x 8 B, seq n x 4 B), asynchronous; the _host variant is H2D, decide, D2H, synchronous. */
+int  sentinel_submit_flow_batch_ordered(sentinel_engine_t *eng, int64_t n, const sentinel_event_t *events,
+                                        const uint8_t *flags, sentinel_verdict_t *verdicts, uint32_t *seq,
+                                        void *stream);
+int  sentinel_submit_flow_batch_ordered_host(sentinel_engine_t *eng, int64_t n, const sentinel_event_t *events,
+                                             const uint8_t *flags, sentinel_verdict_t *verdicts, uint32_t *seq);
 /* Host-fed stream (the north star's pinned host ring + hipMemcpyAsync double-buffering on side
  * streams): decides n HOST events as consecutive batches of `batch` events, batch i+1's H2D and
  * batch i-1's D2H overlapping batch i's decide.  Verdicts equal one sequential replay of all n events
@@ -650,8 +664,8 @@ int  sentinel_param_cm_stats(sentinel_engine_t *eng, int64_t *out2);
 /* ... of the key-walk batches, those decided by the block-owned walk (each sketch block staged in LDS by
  * one workgroup: k_pp_cm_block). */
 int  sentinel_param_cm_block_batches(sentinel_engine_t *eng, int64_t *out);
-/* Flow batches so far by pipeline: {small (one launch), sorted (radix sort), partition with prep + scan +
- * scatter, partition with the one-sweep split (k_part_split)}. */
+/* Flow batches so far by pipeline: {small (one launch), sorted (radix sort), partition (prep + scan +
+ * scatter), of the partition batches those with decide-order output (sentinel_submit_flow_batch_ordered)}. */
 int  sentinel_flow_path_stats(sentinel_engine_t *eng, int64_t *out4);
 /* The engine's own stream (hipStream_t). */
 void *sentinel_engine_stream(sentinel_engine_t *eng);

@@ -37,6 +37,7 @@ EXPORTS = [
     "sentinel_load_flow_rules", "sentinel_load_param_rules", "sentinel_flow_count",
     "sentinel_lookup_flow_idx", "sentinel_lookup_param_idx",
     "sentinel_submit_flow_batch", "sentinel_submit_flow_batch_host", "sentinel_submit_flow_stream_host",
+    "sentinel_submit_flow_batch_ordered", "sentinel_submit_flow_batch_ordered_host",
     "sentinel_submit_param_batch", "sentinel_submit_param_batch_host",
     "sentinel_request_token", "sentinel_request_param_token",
     "sentinel_synchronize", "sentinel_dump_flow", "sentinel_param_sum",
@@ -192,6 +193,8 @@ def load():
         "sentinel_lookup_param_idx": (C.c_int, [vp, i64, vp, vp]),
         "sentinel_submit_flow_batch": (C.c_int, [vp, i64, vp, vp, vp, vp]),
         "sentinel_submit_flow_batch_host": (C.c_int, [vp, i64, vp, vp, vp]),
+        "sentinel_submit_flow_batch_ordered": (C.c_int, [vp, i64, vp, vp, vp, vp, vp]),
+        "sentinel_submit_flow_batch_ordered_host": (C.c_int, [vp, i64, vp, vp, vp, vp]),
         "sentinel_submit_flow_stream_host": (C.c_int, [vp, i64, vp, vp, vp, i64, vp]),
         "sentinel_submit_param_batch": (C.c_int, [vp, i64, vp, vp, vp]),
         "sentinel_submit_param_batch_host": (C.c_int, [vp, i64, vp, vp]),

@@ -177,6 +177,19 @@ struct Verdicts {
     // LIMITER mode: events that fail get status TOO_MANY_REQUEST and flow_key[seq] = flow_key_invalid
     uint32_t *flow_key;
     uint32_t flow_key_invalid;
+    // decide-order output (partition path, sentinel_submit_flow_batch_ordered): the verdict of the event
+    // at sorted position q of a run goes to out[obase + q] -- whole lines, range-local -- and oseq[obase +
+    // q] holds its arrival position (written from the sorted values, not per verdict); null: out[arrival]
+    uint32_t *oseq = nullptr;
+    uint32_t obase = 0;
+    // where the verdict of the event at sorted position q (packed value v) goes
+    __device__ inline uint32_t at(uint32_t q, uint64_t v) const { return oseq ? obase + q : (uint32_t)v & SEQ_MASK; }
+    __device__ inline void put(uint32_t q, uint64_t v, uint64_t vd) const { store_verdict(out, at(q, v), vd); }
+    __device__ inline Verdicts based(uint32_t b) const {
+        Verdicts r = *this;
+        r.obase = b;
+        return r;
+    }
 };
 
 // A key's state: header pair j {epoch, PASS} at base + hs*j (hs = 2: contiguous record;
@@ -349,7 +362,7 @@ struct HetSums {
 // Events are fetched HW at a time (independent loads in flight together, values kept in registers
 // for the verdict stores); once not even an acquire of 1 is admitted (acquire >= 1 past validation,
 // admits monotone in both arguments) the rest of the segment is blocked without evaluating the test.
-// load(k) -> the k-th packed value, acq(v) -> its acquire count, put(v, verdict).
+// load(k) -> the k-th packed value, acq(v) -> its acquire count, put(k, v, verdict).
 template <uint32_t HW, class Load, class Acq, class Put>
 __device__ inline HetSums het_walk(uint8_t kind, double thr, double I_s, int64_t s0, uint32_t len, Load load, Acq acq,
                                    Put put) {
@@ -369,25 +382,27 @@ __device__ inline HetSums het_walk(uint8_t kind, double thr, double I_s, int64_t
             if (ok) {
                 h.pass = wrap_add(h.pass, a);
                 h.npass += 1;
-                put(vv[j], pack_verdict(ST_OK, java_d2i(next), 0));
+                put(k0 + j, vv[j], pack_verdict(ST_OK, java_d2i(next), 0));
             } else {
                 h.block = wrap_add(h.block, a);
                 h.nblock += 1;
-                put(vv[j], pack_verdict(ST_BLOCKED, 0, 0));
+                put(k0 + j, vv[j], pack_verdict(ST_BLOCKED, 0, 0));
             }
         }
     }
     return h;
 }
 
-__device__ inline void reject_limited(const Verdicts &V, uint32_t seq) {
-    put_verdict(V.out, seq, ST_TOO_MANY_REQUEST, 0, 0);
+__device__ inline void reject_limited(const Verdicts &V, uint32_t seq, uint32_t at) {
+    put_verdict(V.out, at, ST_TOO_MANY_REQUEST, 0, 0);
     V.flow_key[seq] = V.flow_key_invalid;
 }
 
 // One event through the reference state machine (the sequential path).
 __device__ inline void seq_event(const KeyTable &T, uint32_t key, const KeyState &S, int64_t E, int32_t a,
-                                 uint8_t flags, uint32_t seq, const Verdicts &V) {
+                                 uint8_t flags, uint32_t seq, const Verdicts &V, uint32_t at) {
+    // (at: where the verdict goes -- seq, or the sorted position in decide-order output; seq keys the
+    // limiter's flow-key invalidation)
     const uint8_t kind = T.kind[key];
     const double thr = T.thr[key];
     const double I_s = T.I_s[key];
@@ -395,7 +410,7 @@ __device__ inline void seq_event(const KeyTable &T, uint32_t key, const KeyState
         roll(T, key, S, E);
         const int64_t sum = window_sum(S, E, EV_PASS);
         if (admits(kind, thr, I_s, sum, 1)) add_counter(T, key, S, E, EV_PASS, 1);
-        else reject_limited(V, seq);
+        else reject_limited(V, seq, at);
         return;
     }
     if (kind == KIND_PARAM) {
@@ -404,9 +419,9 @@ __device__ inline void seq_event(const KeyTable &T, uint32_t key, const KeyState
         const double next = remaining_of(thr, I_s, sum, a);
         if (!(next < 0.0)) {
             add_counter(T, key, S, E, EV_PASS, a);
-            put_verdict(V.out, seq, ST_OK, java_d2i(next), 0);
+            put_verdict(V.out, at, ST_OK, java_d2i(next), 0);
         } else {
-            put_verdict(V.out, seq, ST_BLOCKED, 0, 0);
+            put_verdict(V.out, at, ST_BLOCKED, 0, 0);
         }
         return;
     }
@@ -418,7 +433,7 @@ __device__ inline void seq_event(const KeyTable &T, uint32_t key, const KeyState
         add_counter(T, key, S, E, EV_PASS, a);
         add_counter(T, key, S, E, EV_PASS_REQUEST, 1);
         if (prio) add_counter(T, key, S, E, EV_OCCUPIED_PASS, a);
-        put_verdict(V.out, seq, ST_OK, java_d2i(next), 0);
+        put_verdict(V.out, at, ST_OK, java_d2i(next), 0);
         return;
     }
     if (prio) {
@@ -441,7 +456,7 @@ __device__ inline void seq_event(const KeyTable &T, uint32_t key, const KeyState
                 add_counter(T, key, S, E, EV_WAITING, a);
                 const int wait = 1000 / S.n;
                 if (wait > 0) {
-                    put_verdict(V.out, seq, ST_SHOULD_WAIT, 0, wait);
+                    put_verdict(V.out, at, ST_SHOULD_WAIT, 0, wait);
                     return;
                 }
             }
@@ -450,7 +465,7 @@ __device__ inline void seq_event(const KeyTable &T, uint32_t key, const KeyState
     add_counter(T, key, S, E, EV_BLOCK, a);
     add_counter(T, key, S, E, EV_BLOCK_REQUEST, 1);
     if (prio) add_counter(T, key, S, E, EV_OCCUPIED_BLOCK, a);
-    put_verdict(V.out, seq, ST_BLOCKED, 0, 0);
+    put_verdict(V.out, at, ST_BLOCKED, 0, 0);
 }
 
 // K2 pass with payload: stable scatter of (key, seq|prio, payload) by one 8-bit digit.  The first
@@ -921,7 +936,7 @@ __global__ __launch_bounds__(256) void k_process(KeyTable T, BatchWork W, EventS
                 int32_t a;
                 uint8_t fl;
                 src.load(seq, t, a, fl);
-                seq_event(T, key, ks, E, a, fl, seq, V);
+                seq_event(T, key, ks, E, a, fl, seq, V, seq);
             }
             W.seg_done[g] = 1;
             continue;
@@ -1090,7 +1105,7 @@ __device__ __forceinline__ void process_reg_body(KeyTable T, BatchWork W, EventS
                     src.unpack(v, T0, t, a, pr);
                     return a;
                 },
-                [&](uint64_t v, uint64_t vd) { V.out[(uint32_t)v & SEQ_MASK] = vd; });
+                [&](uint32_t, uint64_t v, uint64_t vd) { V.out[(uint32_t)v & SEQ_MASK] = vd; });
 #pragma unroll
             for (int j = 0; j < NMAX; ++j)
                 if (j == slot) { ps[j] = wrap_add(ps[j], hs.pass); dirty |= 1u << j; }
@@ -1113,7 +1128,7 @@ __device__ __forceinline__ void process_reg_body(KeyTable T, BatchWork W, EventS
                 int32_t a;
                 uint8_t fl;
                 src.load(seq, t, a, fl);
-                seq_event(T, key, ks, E, a, fl, seq, V);
+                seq_event(T, key, ks, E, a, fl, seq, V, seq);
             }
             W.seg_done[g] = 1;
 #pragma unroll
@@ -1346,7 +1361,7 @@ __global__ __launch_bounds__(256) void k_process_wave(KeyTable T, BatchWork W, E
                         int32_t a;
                         uint8_t fl;
                         src.load(seq, t, a, fl);
-                        seq_event(T, key, ks, E, a, fl, seq, V);
+                        seq_event(T, key, ks, E, a, fl, seq, V, seq);
                     }
                     W.seg_done[g] = 1;
 #pragma unroll
@@ -1478,7 +1493,7 @@ __device__ inline void process_key_group(const KeyTable &T, const BatchWork &W, 
                     int32_t a;
                     uint8_t fl;
                     src.load(seq, t, a, fl);
-                    seq_event(T, key, ks, E, a, fl, seq, V);
+                    seq_event(T, key, ks, E, a, fl, seq, V, seq);
                 }
                 W.seg_done[g] = 1;
             }
@@ -1567,7 +1582,7 @@ __global__ __launch_bounds__(256) void k_verdict(KeyTable T, BatchWork W, Verdic
     const uint32_t seq = (uint32_t)W.sval[i] & SEQ_MASK;
     const uint32_t key = W.seg_key[g];
     if (LIMITER) {
-        if (rank >= K) reject_limited(V, seq);
+        if (rank >= K) reject_limited(V, seq, seq);
         return;
     }
     uint64_t v;

@@ -52,21 +52,6 @@ namespace {
 
 thread_local std::string g_err;
 
-// Engines per device (k_part_split's grid barrier needs every one of its workgroups resident: two
-// engines on one device could each hold part of the CUs, so the one-sweep partition runs only while
-// its engine is alone on the device).
-std::mutex g_dev_mu;
-std::unordered_map<int, int> g_dev_engines;
-int dev_engines(int device) {
-    std::lock_guard<std::mutex> g(g_dev_mu);
-    auto it = g_dev_engines.find(device);
-    return it == g_dev_engines.end() ? 0 : it->second;
-}
-void dev_engines_add(int device, int d) {
-    std::lock_guard<std::mutex> g(g_dev_mu);
-    g_dev_engines[device] += d;
-}
-
 int fail(int code, const std::string &msg) {
     g_err = msg;
     return code;
@@ -601,16 +586,15 @@ struct sentinel_engine {
     // range > 8x the mean): then the sorted path for the next 1024 batches, then one probe again
     DevBuf d_part_stat;
     unsigned long long *h_part_stat = nullptr;   // pinned mirror, written asynchronously after each batch
-    // one-sweep partition (k_part_split): digit columns + totals, the monotonic arrival counter.  Off by
-    // default (SENTINEL_PART_SPLIT=1 turns it on): measured at config 3 it takes 134 us per 8M batch
-    // against 130 us for prep + scan + scatter
-    bool part_split = false;
-    int64_t flow_path_count[4] = {0, 0, 0, 0};   // small, sorted, partition 3-pass, partition one-sweep
+    // batches per flow path: small, sorted, partition, [3] of the partition batches those with decide-order
+    // output (sentinel_submit_flow_batch_ordered; until round 5 [3] counted the one-sweep partition front,
+    // removed in round 6 after losing its A/B: 134 vs 130 us at config 3)
+    int64_t flow_path_count[4] = {0, 0, 0, 0};
+    DevBuf d_octr;                               // decide-order batches: rejected-event counters [2]
+    uint32_t opar = 0;                           // ... the current batch's counter
     int num_cu = 0;
-    DevBuf w_split_col, d_split_bar;
-    uint32_t split_arrivals = 0;
-    // pinned words a kernel sets when a bounded spin gave up (the batch's results are invalid): [0] the
-    // one-sweep partition's grid barrier, [1] the concurrency scan's look-back; checked by the next submit
+    // pinned words a kernel sets when a bounded spin gave up (the batch's results are invalid): [0] unused
+    // (was the one-sweep partition's grid barrier), [1] the concurrency scan's look-back (dev_err_synced)
     uint32_t *h_dev_err = nullptr;
     uint32_t *h_long_chunks = nullptr;           // pinned: hot-run chunks of a recent batch (launch hint)
     uint32_t *h_het_hint = nullptr;              // pinned: the sorted path's heterogeneous-key deferral is on
@@ -662,7 +646,8 @@ struct sentinel_engine {
                                        // walk (k_pp_cm_block; config 4cm: 799 vs 946 us)
     bool cm_debug = false;             // SENTINEL_CM_DEBUG=1: the key walk's geometry on stderr
     bool cm_c32 = true;                // SENTINEL_CM_C32=0: the block walk keeps 64-bit cells in LDS
-    int cm_diag = 0;                   // SENTINEL_CM_DIAG: k_pp_cm_block cost diagnostics (wrong results)
+    int cm_diag = 0;                   // SENTINEL_CM_DIAG (read only by a -DSENTINEL_DIAG_CM_ENV build): k_pp_cm_block /
+                                       // k_conc_prep cost diagnostics (wrong results)
     DevBuf w_cmsub;                    // block walk: per sub-range {first record, records}
     DevBuf d_pexpire;                  // exact param table: per slot the getTopValues expire hint (PSlots)
     bool pexp_valid = false;           // ... every live slot's hint is current (only the key walk wrote since)
@@ -1714,24 +1699,8 @@ static int ensure_part_bufs(sentinel_engine_t *e, const PartBufs &B, int64_t n) 
     return rc;
 }
 
-// One-sweep partition geometry: the fewest events per thread (8, 16 or 32) that cover the batch with at
-// most one 1024-thread workgroup per CU.  False: the batch takes prep + scan + scatter (too large, too
-// small to be worth a persistent launch, knob off, or another engine on this device).
-static bool split_geometry(const sentinel_engine_t *e, int64_t n, int &items, int &G) {
-    if (!e->part_split || e->num_cu <= 0 || n < 65536 || dev_engines(e->device) != 1) return false;
-    for (int it : {8, 16, 32}) {
-        const int64_t g = (n + (int64_t)it * SP_THREADS - 1) / ((int64_t)it * SP_THREADS);
-        if (g <= e->num_cu) {
-            items = it;
-            G = (int)g;
-            return true;
-        }
-    }
-    return false;
-}
-
 static int part_front(sentinel_engine_t *e, const PartBufs &B, int64_t n, const Event *ev, const uint8_t *fl,
-                      uint64_t *out, hipStream_t s) {
+                      uint64_t *out, hipStream_t s, uint32_t *oseq = nullptr) {
     const PartGeo g = part_geo(e, n);
     int rc = ensure_part_bufs(e, B, n);
     if (rc) return rc;
@@ -1750,43 +1719,13 @@ static int part_front(sentinel_engine_t *e, const PartBufs &B, int64_t n, const 
     // flows of a namespace: validation and the limiter pass run first (the sorted path's k_flow_prep and
     // limiter pipeline, which mark failing events invalid); the multi-split then takes their keys
     const bool lim = e->nlimiters > 0 && !e->flow_plain;
-    if (!lim && e->flow_plain) {
-        int items = 0, G = 0;
-        if (split_geometry(e, n, items, G)) {
-            const int64_t colw = (int64_t)g.nparts * G + g.nparts;
-            rc = e->w_split_col.ensure((size_t)colw * 4);
-            if (!rc && !e->d_split_bar.p) {
-                rc = e->d_split_bar.ensure(64);
-                if (!rc) rc = hipMemset(e->d_split_bar.p, 0, 64) == hipSuccess ? 0 : SENTINEL_E_DEVICE;
-                e->split_arrivals = 0;
-            }
-            if (rc) return SENTINEL_E_NOMEM;
-            const EventSrc src{ev, nullptr, fl, false};
-            uint32_t *col = e->w_split_col.as<uint32_t>(), *bar = e->d_split_bar.as<uint32_t>();
-            const uint32_t base = e->split_arrivals;
-            e->split_arrivals += 2u * (uint32_t)G;
-            e->flow_path_count[3] += 1;
-            e->launch("part_split", n, s, [&] {
-#define SP_LAUNCH(IT)                                                                                           \
-    k_part_split<IT><<<dim3((unsigned)G), dim3(SP_THREADS), 0, s>>>(n, src, g.F, out, g.lb, g.pbits, g.nparts,  \
-                                                                   B.sval->as<uint64_t>(), rstart, col, bar,   \
-                                                                   base, e->h_dev_err, ctl, stat)
-                if (items == 8) SP_LAUNCH(8);
-                else if (items == 16) SP_LAUNCH(16);
-                else SP_LAUNCH(32);
-#undef SP_LAUNCH
-            });
-            HIP_OK(hipGetLastError());
-            return 0;
-        }
-    }
     if (lim) e->limiter_pass(n, ev, g.F, fkey, g.finvalid, 0, out, s);
     e->flow_path_count[2] += 1;
     e->launch("part_prep", n, s, [&] {
         k_part_prep<<<dim3((unsigned)g.nb), dim3(PP_THREADS), 0, s>>>(
             n, ev, g.F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out,
             (e->flow_plain || lim) ? nullptr : fkey, g.finvalid, g.lb, hist, g.nb, g.nparts, ctl, stat,
-            lim ? fkey : nullptr);
+            lim ? fkey : nullptr, oseq, oseq ? e->d_octr.as<uint32_t>() : nullptr, e->opar);
     });
     e->launch("scan", n, s, [&] {
         const dim3 g2((unsigned)g.ng, (unsigned)((g.nparts + PS_THREADS - 1) / PS_THREADS));
@@ -1807,12 +1746,13 @@ static int part_front(sentinel_engine_t *e, const PartBufs &B, int64_t n, const 
 
 // The back of a partition batch: sort + decide per half range, oversized halves, hot flows.
 static int part_back(sentinel_engine_t *e, const PartBufs &B, int64_t n, const Event *ev, const uint8_t *fl,
-                     uint64_t *out, hipStream_t s) {
+                     uint64_t *out, hipStream_t s, uint32_t *oseq = nullptr) {
     const PartGeo g = part_geo(e, n);
     uint32_t *rstart = B.pscan->as<uint32_t>() + (size_t)g.ng * g.nparts;
     const EventSrc src{ev, nullptr, fl, false};
     const KeyTable FT = e->table(e->ft, NEV, 0);
-    const Verdicts V{out, B.fkey->as<uint32_t>(), g.finvalid};
+    Verdicts V{out, B.fkey->as<uint32_t>(), g.finvalid};
+    V.oseq = oseq;
     uint32_t *ctl = B.runs->as<uint32_t>();
     unsigned long long *stat = B.stat->as<unsigned long long>();
     const uint64_t *pval = B.sval->as<uint64_t>();
@@ -1827,11 +1767,18 @@ static int part_back(sentinel_engine_t *e, const PartBufs &B, int64_t n, const E
 }
 
 static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
-                            hipStream_t s) {
+                            hipStream_t s, uint32_t *oseq = nullptr) {
     const PartBufs B = e->part_bufs();
-    int rc = part_front(e, B, n, ev, fl, out, s);
+    if (oseq && !e->d_octr.p) {                           // the rejected-event counters of decide-order batches
+        if (e->d_octr.ensure(64)) return SENTINEL_E_NOMEM;
+        HIP_OK(hipMemsetAsync(e->d_octr.p, 0, 64, s));
+        e->opar = 0;
+    }
+    int rc = part_front(e, B, n, ev, fl, out, s, oseq);
     if (rc) return rc;
-    return part_back(e, B, n, ev, fl, out, s);
+    rc = part_back(e, B, n, ev, fl, out, s, oseq);
+    if (oseq) e->opar ^= 1u;
+    return rc;
 }
 
 // Partition-local path for this batch?  (Windows of <= 16 buckets, <= 2^20 flows; auto picks it for
@@ -1953,27 +1900,25 @@ struct ForeignStream {
     }
 };
 
-// A kernel of an earlier batch gave up a bounded spin (MI355X_MICROARCH.md: every spin bounded): that
-// batch's results are invalid, so the next submit reports it.  [0]: the one-sweep partition's grid barrier
-// did not complete (its workgroups were not all resident: another persistent kernel on the device) -- the
-// arrival counter is reset and this engine keeps prep + scan + scatter from now on; [1]: the concurrency
-// scan's look-back waited past its bound (cannot happen with ticket-ordered tiles; a guard, not a path).
+// A kernel gave up a bounded spin (MI355X_MICROARCH.md: every spin bounded): the batch it belonged to has
+// invalid results.  [1]: the concurrency scan's look-back waited past its bound (cannot happen with
+// ticket-ordered tiles; a guard, not a path).  Reported where the batch's results are
+// handed back -- every synchronous (host) entry point after its synchronisation, and
+// sentinel_synchronize for batches submitted on device pointers -- so the caller never uses them; a
+// flag still set at the next submit (an asynchronous caller that did not synchronise) fails that submit.
+static int dev_err_synced(sentinel_engine_t *e) {
+    if (!e->h_dev_err) return 0;
+    if (!__atomic_load_n(&e->h_dev_err[1], __ATOMIC_ACQUIRE)) return 0;
+    e->h_dev_err[1] = 0;
+    return fail(SENTINEL_E_DEVICE, "concurrency scan: look-back timed out (the batch's results are invalid)");
+}
+
 static int check_dev_err(sentinel_engine_t *e, hipStream_t s) {
     if (!e->h_dev_err) return 0;
-    const uint32_t e0 = __atomic_load_n(&e->h_dev_err[0], __ATOMIC_ACQUIRE);
-    const uint32_t e1 = __atomic_load_n(&e->h_dev_err[1], __ATOMIC_ACQUIRE);
-    if (!e0 && !e1) return 0;
+    if (!__atomic_load_n(&e->h_dev_err[1], __ATOMIC_ACQUIRE)) return 0;
     HIP_OK(hipStreamSynchronize(s));
     HIP_OK(hipStreamSynchronize(e->stream));
-    if (e0) {
-        if (e->d_split_bar.p) HIP_OK(hipMemset(e->d_split_bar.p, 0, 64));
-        e->split_arrivals = 0;
-        e->part_split = false;
-    }
-    e->h_dev_err[0] = 0;
-    e->h_dev_err[1] = 0;
-    return fail(SENTINEL_E_DEVICE, e0 ? "one-sweep partition: grid barrier timed out (an earlier batch's verdicts are invalid)"
-                                      : "concurrency scan: look-back timed out (an earlier batch's results are invalid)");
+    return dev_err_synced(e);
 }
 
 static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
@@ -1996,6 +1941,43 @@ static int submit_flow(sentinel_engine_t *e, int64_t n, const Event *ev, const u
     if (choose_part(e, n)) return submit_flow_part(e, n, ev, fl, out, s);
     e->flow_path_count[1] += 1;
     return submit_flow_sorted(e, n, ev, fl, out, s);
+}
+
+__global__ void k_iota_u32(uint32_t *p, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = (uint32_t)i;
+}
+
+// Decide-order output (sentinel_submit_flow_batch_ordered): the same decisions and counters as
+// submit_flow, with out[j] = the verdict of the event at arrival position oseq[j] (a permutation of
+// [0, n)).  The partition path writes each half range's verdicts to its own positions -- whole lines
+// instead of 8.4M random 8-byte sectors -- and the arrival positions from its sorted values; a batch the
+// partition path does not take (small batches, the radix path after a skewed batch, namespace limiters)
+// is decided in arrival order and oseq = identity.  The consumer (the batcher, the wire server) answers
+// each request from (oseq[j], out[j]): no arrival-order permutation on the device.
+static int submit_flow_ordered(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
+                               uint32_t *oseq, hipStream_t s) {
+    if (n <= 0) return 0;
+    if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
+    if (int rc0 = check_dev_err(e, s)) return rc0;
+    const bool lim = e->nlimiters > 0 && !e->flow_plain;
+    if (!(small_ok(e) && (n <= SM_MAX || e->flow_path == 3)) && !lim) {
+        int rc = e->ensure_ws(n);
+        if (rc) return rc;
+        if (choose_part(e, n)) {
+            e->flow_path_count[3] += 1;
+            return submit_flow_part(e, n, ev, fl, out, s, oseq);
+        }
+        e->flow_path_count[1] += 1;
+        rc = submit_flow_sorted(e, n, ev, fl, out, s);
+        if (rc) return rc;
+    } else {
+        int rc = submit_flow(e, n, ev, fl, out, s);
+        if (rc) return rc;
+    }
+    k_iota_u32<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(oseq, n);
+    HIP_OK(hipGetLastError());
+    return 0;
 }
 
 static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamEvent *pev, const MultiEvent *mev,
@@ -2173,11 +2155,14 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
         ++e->cm_overflows;
         return 1;
     }
-    // 32-bit LDS cells (tags mod 256 around the batch's newest epoch) when the batch spans < 200 epochs
+    // 32-bit LDS cells (tags mod 256 around Eref = max(the batch's newest epoch, E_hi), cm_eref) when every
+    // age the batch needs -- from Eref back to its oldest epoch less 2n -- is < 200 epochs
     const int32_t wsk = e->h_prule_interval.empty() ? 1 : std::max(1, e->h_prule_interval[0] / std::max(1, e->h_prule_n[0]));
     const int64_t tlo = (int64_t)e->h_cmband[5], thi = (int64_t)~e->h_cmband[6];
+    const int64_t ehi = (int64_t)e->h_cmband[1];          // E_hi (ctl[0]) as the grouping left it
+    const int64_t eref = (ehi != CM_EHI_NONE && ehi != CM_EHI_ANY && ehi > thi / wsk) ? ehi : thi / wsk;
     const bool c32 = use_block && e->cm_c32 && tlo >= 0 && thi >= tlo &&
-                     thi / wsk - tlo / wsk + 2 * (int64_t)e->pmax_n < 200;
+                     eref - tlo / wsk + 2 * (int64_t)e->pmax_n < 200;
     ++e->cm_key_batches;
     const int32_t nsc = e->pmax_n;
     int64_t *mv = e->w_sval.as<int64_t>();                // (the packed values are dead after the grouping)
@@ -2395,7 +2380,8 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
             const int band = e->pmax_n;                   // one launch per band of n epochs (ring of 2 n slots)
             e->launch("prule_process", n, s, [&] {
                 for (int64_t E = (int64_t)span[0]; E <= (int64_t)span[1]; E += band)
-                    k_prule_cm_level<<<hb, 256, 0, s>>>(C, W, evp, vs, out, heads, ctl, cursor, E, band);
+                    k_prule_cm_level<<<hb, 256, 0, s>>>(C, W, evp, vs, out, heads, ctl, cursor, E, band,
+                                                        (int64_t)span[1]);
             });
             HIP_OK(hipGetLastError());
             return 0;
@@ -2405,8 +2391,9 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
         hipError_t ce = hipSuccess;
         e->launch("prule_process", n, s, [&] {
             int band = e->pmax_n;
+            int64_t eref = (int64_t)span[1];             // the batch's newest epoch (cm_slot_next's "newer" test)
             void *args[] = {(void *)&C, (void *)&W, (void *)&evp, (void *)&vs, (void *)&out, (void *)&heads, (void *)&ctl,
-                            (void *)&cursor, (void *)&lv, (void *)&band};
+                            (void *)&cursor, (void *)&lv, (void *)&band, (void *)&eref};
             ce = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(k_prule_cm_sync), dim3(nblk), dim3(256), args, 0, s);
         });
         if (ce != hipSuccess) return fail(SENTINEL_E_DEVICE, std::string("cooperative launch failed: ") + hipGetErrorString(ce));
@@ -2587,11 +2574,12 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
     if (const char *c = getenv("SENTINEL_ROUTE8")) e->use_route8 = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_LIM1")) e->lim1 = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_PROC_OCC")) e->process_occ = std::string(c) != "0";
-    if (const char *c = getenv("SENTINEL_PART_SPLIT")) e->part_split = std::string(c) == "1";
     if (const char *c = getenv("SENTINEL_CM_BLOCK")) e->cm_block = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_CM_DEBUG")) e->cm_debug = std::string(c) == "1";
     if (const char *c = getenv("SENTINEL_CM_C32")) e->cm_c32 = std::string(c) != "0";
+#ifdef SENTINEL_DIAG_CM_ENV   // cost diagnostics that change results: only in a -DSENTINEL_DIAG_CM_ENV build
     if (const char *c = getenv("SENTINEL_CM_DIAG")) e->cm_diag = atoi(c);
+#endif
     if (hipDeviceGetAttribute(&e->num_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) e->num_cu = 0;
     if (const char *c = getenv("SENTINEL_PARAM_CAPACITY")) {
         uint64_t v = strtoull(c, nullptr, 10);
@@ -2611,7 +2599,6 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
         return fail(SENTINEL_E_DEVICE, "hipHostMalloc failed");
     }
     memset(e->h_dev_err, 0, 64);
-    dev_engines_add(device, 1);
     *out = e;
     return 0;
 }
@@ -2620,9 +2607,6 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
     if (!e) return 0;
     (void)hipSetDevice(e->device);
     (void)hipStreamSynchronize(e->stream);
-    dev_engines_add(e->device, -1);
-    e->w_split_col.release();
-    e->d_split_bar.release();
     if (e->h_dev_err) (void)hipHostFree(e->h_dev_err);
     e->prof_collect();
     for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
@@ -2669,6 +2653,7 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
     if (e->h_long_chunks) (void)hipHostFree(e->h_long_chunks);
     if (e->h_het_hint) (void)hipHostFree(e->h_het_hint);
     e->d_part_stat.release();
+    e->d_octr.release();
     (void)hipStreamDestroy(e->stream);
     delete e;
     return 0;
@@ -3230,6 +3215,45 @@ int sentinel_submit_flow_batch(sentinel_engine_t *e, int64_t n, const sentinel_e
     return submit_flow(e, n, (const Event *)ev, flags, (uint64_t *)out, fs_s);
 }
 
+int sentinel_submit_flow_batch_ordered(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev, const uint8_t *flags,
+                                       sentinel_verdict_t *out, uint32_t *out_seq, void *stream) {
+    if (!e || n < 0 || (n > 0 && (!ev || !out || !out_seq))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    hipStream_t fs_s = stream ? (hipStream_t)stream : e->stream;
+    const ForeignStream fs_(e, fs_s);
+    return submit_flow_ordered(e, n, (const Event *)ev, flags, (uint64_t *)out, out_seq, fs_s);
+}
+
+// H2D, decide (decide-order output), D2H of verdicts and arrival positions, synchronous, lock held.
+static int submit_flow_ordered_host_locked(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev,
+                                           const uint8_t *flags, sentinel_verdict_t *out, uint32_t *out_seq) {
+    HIP_OK(hipSetDevice(e->device));
+    hipStream_t s = e->stream;
+    int rc = e->io_ev.ensure(n * sizeof(Event));
+    rc |= e->io_fl.ensure(n);
+    rc |= e->io_out.ensure(n * 12 + 16);
+    if (rc) return SENTINEL_E_NOMEM;
+    uint64_t *dout = e->io_out.as<uint64_t>();
+    uint32_t *dseq = reinterpret_cast<uint32_t *>(dout + n);
+    HIP_OK(hipMemcpyAsync(e->io_ev.p, ev, n * sizeof(Event), hipMemcpyHostToDevice, s));
+    if (flags) HIP_OK(hipMemcpyAsync(e->io_fl.p, flags, n, hipMemcpyHostToDevice, s));
+    rc = submit_flow_ordered(e, n, e->io_ev.as<Event>(), flags ? e->io_fl.as<uint8_t>() : nullptr, dout, dseq, s);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(out_seq, dseq, n * 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    return dev_err_synced(e);
+}
+
+int sentinel_submit_flow_batch_ordered_host(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev,
+                                            const uint8_t *flags, sentinel_verdict_t *out, uint32_t *out_seq) {
+    if (!e || n < 0 || (n > 0 && (!ev || !out || !out_seq))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> g(e->mu);
+    return submit_flow_ordered_host_locked(e, n, ev, flags, out, out_seq);
+}
+
 // H2D, decide, D2H of host events, synchronous, with the engine lock held.
 static int submit_flow_host_locked(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev, const uint8_t *flags,
                                    sentinel_verdict_t *out);
@@ -3257,9 +3281,14 @@ static int submit_flow_ids_host(sentinel_engine_t *e, int64_t n, const int64_t *
 // The batcher's launch: flowIds looked up and the batch queued under one engine lock.  Small batches
 // (k_small_flow applies) are launched on pinned ev / flags / out with the completion flag `done`
 // (*async = true: the caller polls it); anything else is decided synchronously here.
+static int submit_flow_ordered_host_locked(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev,
+                                           const uint8_t *flags, sentinel_verdict_t *out, uint32_t *out_seq);
+
 static int submit_flow_ids_pinned(sentinel_engine_t *e, int64_t n, const int64_t *ids, sentinel_event_t *ev,
-                                  const uint8_t *flags, sentinel_verdict_t *out, uint32_t *done, bool *async) {
+                                  const uint8_t *flags, sentinel_verdict_t *out, uint32_t *done, bool *async,
+                                  uint32_t *seq = nullptr, bool *ordered = nullptr) {
     *async = false;
+    if (ordered) *ordered = false;
     if (n == 0) return 0;
     std::lock_guard<std::mutex> g(e->mu);
     for (int64_t i = 0; i < n; ++i) ev[i].flow_idx = e->flat_flow.find(ids[i]);
@@ -3269,6 +3298,10 @@ static int submit_flow_ids_pinned(sentinel_engine_t *e, int64_t n, const int64_t
         const int rc = launch_small(e, n, (const Event *)ev, flags, (uint64_t *)out, e->stream, done);
         *async = rc == 0;
         return rc;
+    }
+    if (seq && ordered) {                                 // large batch: decide-order output (out[j] <-> seq[j])
+        *ordered = true;
+        return submit_flow_ordered_host_locked(e, n, ev, flags, out, seq);
     }
     return submit_flow_host_locked(e, n, ev, flags, out);
 }
@@ -3306,7 +3339,7 @@ static int submit_flow_host_locked(sentinel_engine_t *e, int64_t n, const sentin
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    return 0;
+    return dev_err_synced(e);
 }
 
 // Host-fed stream: consecutive batches pipelined over three HIP streams.  Batch i's H2D (s_h2d),
@@ -3379,7 +3412,7 @@ int sentinel_submit_flow_stream_host(sentinel_engine_t *e, int64_t n, const sent
             e->ev_pool.push_back(t1[i]);
         }
     }
-    return rc;
+    return rc ? rc : dev_err_synced(e);
 }
 
 int sentinel_submit_param_batch(sentinel_engine_t *e, int64_t n, const sentinel_param_event_t *ev,
@@ -4057,7 +4090,7 @@ int sentinel_submit_concurrent_batch_host(sentinel_engine_t *e, int64_t n, const
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 16, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    return 0;
+    return dev_err_synced(e);
 }
 
 int sentinel_submit_concurrent_batch(sentinel_engine_t *e, int64_t n, const sentinel_concurrent_event_t *ev,
@@ -4155,7 +4188,8 @@ int sentinel_synchronize(sentinel_engine_t *e) {
     if (!e) return fail(SENTINEL_E_INVALID, "null engine");
     HIP_OK(hipSetDevice(e->device));
     HIP_OK(hipStreamSynchronize(e->stream));
-    return 0;
+    std::lock_guard<std::mutex> g(e->mu);
+    return dev_err_synced(e);                            // a batch since the last check gave up a spin
 }
 
 int sentinel_dump_flow(sentinel_engine_t *e, int32_t idx, int64_t *out, int32_t out_len) {
@@ -4474,7 +4508,9 @@ struct sentinel_batcher {
         sentinel_event_t *h_ev = nullptr;  // pinned: read by the kernel
         uint8_t *h_fl = nullptr;
         sentinel_verdict_t *h_out = nullptr;
+        uint32_t *h_seq = nullptr;         // pinned: decide-order output's arrival positions (large batches)
         uint32_t *h_done = nullptr;        // pinned completion flag
+        bool ordered = false;              // h_out[j] answers items[h_seq[j]]
         bool async = false;
         int rc = 0;
     };
@@ -4501,7 +4537,8 @@ struct sentinel_batcher {
             S.h_ev[i] = S.items[i].ev;
             S.h_fl[i] = S.items[i].flag;
         }
-        S.rc = submit_flow_ids_pinned(e, n, S.ids.data(), S.h_ev, S.h_fl, S.h_out, S.h_done, &S.async);
+        S.rc = submit_flow_ids_pinned(e, n, S.ids.data(), S.h_ev, S.h_fl, S.h_out, S.h_done, &S.async, S.h_seq,
+                                      &S.ordered);
     }
 
     void complete(Slot &S) {
@@ -4509,23 +4546,29 @@ struct sentinel_batcher {
         const int64_t n = (int64_t)S.items.size();
         const int rc = S.rc;
         bool any_sync = false;
-        for (int64_t i = 0; i < n; ++i) {
+        // a large batch comes back in decide order: verdict j answers request h_seq[j] (each request is
+        // answered on its own -- by its caller or callback, the wire server by xid -- so no arrival-order
+        // permutation is ever built)
+        const bool ord = S.ordered && rc == 0;
+        for (int64_t j = 0; j < n; ++j) {
+            const int64_t i = ord ? (int64_t)S.h_seq[j] : j;
             const BatchItem &it = S.items[i];
             if (it.waiter) {
-                it.waiter->out = S.h_out[i];
+                it.waiter->out = S.h_out[j];
                 it.waiter->rc = rc;
                 it.waiter->done.store(1, std::memory_order_release);
                 any_sync = true;
             } else {
                 // engine down -> FAIL (the client falls back to its local check)
                 sentinel_token_result_t r;
-                r.status = rc ? SENTINEL_STATUS_FAIL : S.h_out[i].status;
-                r.remaining = rc ? 0 : S.h_out[i].remaining;
-                r.wait_in_ms = rc ? 0 : S.h_out[i].wait_in_ms;
+                r.status = rc ? SENTINEL_STATUS_FAIL : S.h_out[j].status;
+                r.remaining = rc ? 0 : S.h_out[j].remaining;
+                r.wait_in_ms = rc ? 0 : S.h_out[j].wait_in_ms;
                 r.reserved = 0;
                 it.cb(it.ctx, it.tag, &r);
             }
         }
+        S.ordered = false;
         batches.fetch_add(1);
         requests.fetch_add(n);
         S.items.clear();
@@ -4610,9 +4653,10 @@ int sentinel_batcher_create(sentinel_engine_t *e, int32_t max_batch, int32_t max
         if (hipHostMalloc((void **)&S.h_ev, (size_t)max_batch * sizeof(sentinel_event_t), 0) != hipSuccess ||
             hipHostMalloc((void **)&S.h_fl, (size_t)max_batch, 0) != hipSuccess ||
             hipHostMalloc((void **)&S.h_out, (size_t)max_batch * sizeof(sentinel_verdict_t), 0) != hipSuccess ||
+            hipHostMalloc((void **)&S.h_seq, (size_t)max_batch * sizeof(uint32_t), 0) != hipSuccess ||
             hipHostMalloc((void **)&S.h_done, 64, 0) != hipSuccess) {
             for (auto &T : b->slot)
-                for (void *p : {(void *)T.h_ev, (void *)T.h_fl, (void *)T.h_out, (void *)T.h_done})
+                for (void *p : {(void *)T.h_ev, (void *)T.h_fl, (void *)T.h_out, (void *)T.h_seq, (void *)T.h_done})
                     if (p) (void)hipHostFree(p);
             delete b;
             return fail(SENTINEL_E_NOMEM, "hipHostMalloc failed");
@@ -4637,7 +4681,8 @@ int sentinel_batcher_destroy(sentinel_batcher_t *b) {
         b->cv_idle.wait(lk, [&] { return b->callers == 0; });
     }
     for (auto &S : b->slot)
-        for (void *p : {(void *)S.h_ev, (void *)S.h_fl, (void *)S.h_out, (void *)S.h_done}) (void)hipHostFree(p);
+        for (void *p : {(void *)S.h_ev, (void *)S.h_fl, (void *)S.h_out, (void *)S.h_seq, (void *)S.h_done})
+            (void)hipHostFree(p);
     delete b;
     return 0;
 }

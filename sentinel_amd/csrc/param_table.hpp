@@ -238,7 +238,11 @@ __global__ __launch_bounds__(256) void k_ptop_fresh(const uint32_t *__restrict__
             if (fresh) s_idx[wb + (uint32_t)__popcll(act & ((1ull << lane) - 1ull))] = (uint32_t)s;
         }
         __syncthreads();
-        if (s_n > TOP_LDS - blockDim.x) flush();
+        // every wave reads the count before any wave of the next iteration can add to it (a wave that
+        // skipped the flush on a later read would disagree with the others about the flush's barriers)
+        const uint32_t cur = s_n;
+        __syncthreads();
+        if (cur > TOP_LDS - blockDim.x) flush();
     }
     flush();
 }
@@ -341,7 +345,9 @@ __global__ __launch_bounds__(256) void k_ptop_sums(PSlots T, uint64_t cap, int32
             }
         }
         __syncthreads();
-        if (s_n > TOP_LDS - blockDim.x) flush();          // (room for the next chunk's candidates)
+        const uint32_t cur = s_n;                         // (read by every wave before the next iteration's adds)
+        __syncthreads();
+        if (cur > TOP_LDS - blockDim.x) flush();          // (room for the next chunk's candidates)
     }
     flush();
 }

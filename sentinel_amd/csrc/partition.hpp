@@ -56,10 +56,17 @@ __global__ __launch_bounds__(PP_THREADS) void k_part_prep(int64_t n, const Event
                                                             int64_t nblocks, int32_t nparts,
                                                             uint32_t *__restrict__ ctl_zero,
                                                             unsigned long long *__restrict__ stat_zero,
-                                                            const uint32_t *__restrict__ keys_pre) {
+                                                            const uint32_t *__restrict__ keys_pre,
+                                                            uint32_t *__restrict__ oseq = nullptr,
+                                                            uint32_t *__restrict__ octr = nullptr, uint32_t opar = 0) {
+    // oseq (decide-order output): a rejected event's verdict goes to position n - 1 - (its rank among the
+    // batch's rejected events, counted in octr[opar]) -- the valid events fill [0, valid) in the ranges, so
+    // the rejected ones fill [valid, n) -- with its arrival position in oseq; octr[opar ^ 1] is zeroed for
+    // the next such batch (opar alternates per batch: no memset launch)
     if (blockIdx.x == 0 && threadIdx.x == 0) {        // the batch's work-list counters and skew statistic
         if (ctl_zero) { ctl_zero[0] = 0; ctl_zero[1] = 0; ctl_zero[2] = 0; }
         if (stat_zero) *stat_zero = 0;
+        if (octr) octr[opar ^ 1u] = 0;
     }
     __shared__ uint32_t h[PART_BINS];
     const int64_t tile0 = (int64_t)blockIdx.x * PT_TILE;
@@ -90,7 +97,23 @@ __global__ __launch_bounds__(PP_THREADS) void k_part_prep(int64_t n, const Event
         else k = (uint32_t)e.idx;
         if (fkey) fkey[i] = k;
         if (st == 127) atomicAdd(&h[k >> lb], 1u);
-        else put_verdict(out, (uint32_t)i, st, 0, 0);
+        else if (!oseq) put_verdict(out, (uint32_t)i, st, 0, 0);
+        if (oseq) {                                  // (one counter atomic per wave)
+            const bool rej = st != 127;
+            const uint64_t m = __builtin_amdgcn_ballot_w64(rej);
+            if (m) {
+                const uint32_t lane = lane_id();
+                const int lead = __ffsll((unsigned long long)m) - 1;
+                uint32_t b = 0;
+                if ((int)lane == lead) b = atomicAdd(&octr[opar], (uint32_t)__popcll(m));
+                b = __shfl(b, lead, WAVE);
+                if (rej) {
+                    const uint32_t pos = (uint32_t)(n - 1) - (b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull)));
+                    put_verdict(out, pos, st, 0, 0);
+                    oseq[pos] = (uint32_t)i;
+                }
+            }
+        }
     }
     __syncthreads();
     // tile-major: this tile's 4 KB row is one contiguous store
@@ -287,297 +310,6 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(const uint32_t *__r
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// One-sweep partition (round 5): k_part_prep + the three scan launches + k_part_scatter in ONE
-// persistent launch of G <= #CU workgroups of 1024 threads (one per CU, every workgroup resident:
-// <= 128 VGPRs, 104 KB LDS).  The batch is cut into G contiguous chunks of ITEMS x 1024 events, chunk
-// c = the workgroup's index XCD-major (blocks b, b + 8, ... share an XCD, so chunks c and c + 1 do and
-// a range's runs from consecutive chunks meet in one L2):
-//   1. every event of the chunk is read from HBM (16 B), validated (verdicts of rejected events written,
-//      as k_part_prep) and counted into the chunk's digit histogram (LDS atomics), published as row c of
-//      a chunk-major matrix;
-//   2. grid barrier; digit d's column over the G chunks is scanned (exclusive, in place) by one wave of
-//      workgroup d mod G, which also stores the digit's total;
-//   3. grid barrier; every chunk scans the digit totals (range starts) and adds its own column entry:
-//      its output offset per digit; chunk 0 stores the range starts k_part_half reads;
-//   4. the chunk is written out in rounds of SP_TILE consecutive events: read again -- from the 256 MB
-//      Infinity Cache, which holds the 134 MB event array of an 8M batch between steps 1 and 4 -- packed,
-//      ranked within the round (one ballot per digit bit and wave-private LDS counters: stable), staged
-//      in LDS in (digit, arrival) order and stored as contiguous per-range runs by all 1024 threads
-//      (each value stored by its own lane was 64 lines per store instruction: measured 87 us for the
-//      stores of an 8M batch, against 27 us for the same bytes in arrival order).  The next round's
-//      events are requested before the current round is stored.
-// The output is exactly k_part_scatter's: every range holds its events in arrival order.
-// Inter-workgroup hand-offs (MI355X_MICROARCH.md, visibility table, first row): every handed-off word
-// is stored and loaded with agent-scope relaxed atomics (global sc1), every storing wave drains its
-// stores (s_waitcnt vmcnt(0)) before a workgroup barrier, then ONE lane adds to the arrival counter;
-// waiters poll it with sc1 loads.  The counter is monotonic across launches (the host passes the
-// arrival count at launch, `bar_base`), so nothing is zeroed per batch.  Spins are bounded: a barrier
-// that never completes (workgroups not co-resident: another persistent kernel on the device) sets the
-// pinned error word and the batch is reported failed by the next submit (engine.hip), never a hang.
-constexpr int SP_THREADS = 1024;
-constexpr int SP_WAVES = SP_THREADS / WAVE;
-constexpr int SP_MAX_G = 256;                       // workgroups (the host launches <= min(#CU, this))
-constexpr int SP_RITEMS = 8;                        // events per thread per write-out round
-constexpr int SP_TILE = SP_RITEMS * SP_THREADS;     // events per round (staged: 64 KB)
-constexpr uint32_t SP_SPIN_LIMIT = 1u << 22;        // ~seconds of polling
-constexpr int SP_LOC_BITS = 13;                     // a staged value's index in its round
-static_assert(PART_BINS == SP_THREADS, "one digit per thread");
-static_assert(SP_TILE == 1 << SP_LOC_BITS && SP_LOC_BITS + PART_MAX_BITS <= 28, "round index and digit fit the position field");
-typedef __attribute__((address_space(1))) uint32_t sp_gu32;
-#ifdef SENTINEL_SPLIT_STAMPS      // cost diagnostic (tools/split_bench.cpp): wall-clock stamps per workgroup and phase
-__device__ unsigned long long g_split_stamp[1024][8];
-__device__ unsigned long long g_split_round[1024][4];
-#define SP_STAMP(i) do { if (threadIdx.x == 0) g_split_stamp[blockIdx.x][i] = wall_clock64(); } while (0)
-#define SP_RSTAMP(i) do { const unsigned long long now_ = wall_clock64(); if (threadIdx.x == 0) g_split_round[blockIdx.x][i] += now_ - rt_; rt_ = now_; } while (0)
-#else
-#define SP_STAMP(i) do { } while (0)
-#define SP_RSTAMP(i) do { } while (0)
-#endif
-
-__device__ inline void sp_put(uint32_t *p, uint32_t v) {
-    __hip_atomic_store((sp_gu32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline uint32_t sp_get(const uint32_t *p) {
-    return __hip_atomic_load((sp_gu32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Grid barrier over a monotonic arrival counter (every workgroup calls it; `target` = arrivals that
-// complete this barrier).
-__device__ inline void sp_grid_sync(uint32_t *bar, uint32_t target, uint32_t *err) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // every wave: its sc1 stores have landed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add((sp_gu32 *)bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (uint32_t spins = 0;; ++spins) {
-            if ((int32_t)(sp_get(bar) - target) >= 0) break;
-            if (spins > SP_SPIN_LIMIT) {
-                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-    }
-    __syncthreads();
-}
-
-// Workgroup barrier for LDS hand-offs only: __syncthreads() also waits for every outstanding global
-// load and store of the wave (s_waitcnt vmcnt(0)), which would drain the next round's prefetched events
-// and this round's value stores at every barrier of the write-out rounds.
-__device__ inline void sp_lds_sync() {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-// block_exclusive_scan with LDS-only barriers (1024 threads).
-__device__ inline uint32_t sp_block_exclusive_scan(uint32_t v, uint32_t *lds_waves, uint32_t *total) {
-    const int lane = (int)lane_id();
-    const int wave = threadIdx.x / WAVE;
-    const uint32_t inc = wave_inclusive_scan(v);
-    if (lane == WAVE - 1) lds_waves[wave] = inc;
-    sp_lds_sync();
-    uint32_t base = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < SP_WAVES; ++w) {
-        const uint32_t x = lds_waves[w];
-        if (w < wave) base += x;
-        tot += x;
-    }
-    sp_lds_sync();
-    *total = tot;
-    return base + inc - v;
-}
-
-// k_part_prep's validation of one event (DTS:38-45; ts < 0: the reference's NPE in LeapArray -> FAIL);
-// 127 = valid.
-__device__ inline int sp_status(const Event &e, int32_t nflows) {
-    if (e.idx == SENTINEL_IDX_BAD_ID || e.acquire <= 0) return ST_BAD_REQUEST;
-    if (e.idx < 0 || e.idx >= nflows) return ST_NO_RULE_EXISTS;
-    if (e.ts < 0) return ST_FAIL;
-    return 127;
-}
-
-template <int ITEMS>
-__global__ __launch_bounds__(SP_THREADS) void k_part_split(
-    int64_t n, EventSrc src, int32_t nflows, uint64_t *__restrict__ out, int lb, int pbits, int32_t nparts,
-    uint64_t *__restrict__ vals_out, uint32_t *__restrict__ rstart, uint32_t *col, uint32_t *bar, uint32_t bar_base,
-    uint32_t *err, uint32_t *__restrict__ ctl_zero, unsigned long long *__restrict__ stat_zero) {
-    constexpr int CHUNK = ITEMS * SP_THREADS;
-    constexpr int NR = CHUNK / SP_TILE;                        // write-out rounds
-    constexpr int GRP = 8;                                     // step 1: event loads in flight per thread
-    static_assert(ITEMS % SP_RITEMS == 0 && ITEMS % GRP == 0, "whole rounds");
-    __shared__ uint32_t goff[PART_BINS];              // per digit: histogram, then the chunk's output offset
-    __shared__ uint16_t cnt[SP_WAVES][PART_BINS];     // per (wave, digit) in a round: count, then offset
-    __shared__ uint32_t soff[PART_BINS];              // per digit: start of its run in the staged round
-    __shared__ uint64_t stage[SP_TILE];
-    __shared__ uint32_t waves_tot[SP_WAVES];
-    const uint32_t G = gridDim.x, g = blockIdx.x, t = threadIdx.x;
-    const uint32_t c = (G & 7u) == 0 ? (g & 7u) * (G >> 3) + (g >> 3) : g;     // chunk (XCD-major)
-    const int wave = (int)(t / WAVE);
-    const uint32_t lane = lane_id();
-    if (c == 0 && t == 0) {                           // the batch's work-list counters and skew statistic
-        ctl_zero[0] = 0; ctl_zero[1] = 0; ctl_zero[2] = 0;
-        *stat_zero = 0;
-    }
-    goff[t] = 0;
-    const int64_t cbase = (int64_t)c * CHUNK;         // first arrival position of the chunk
-    const int32_t crem = (int32_t)max((int64_t)0, min((int64_t)CHUNK, n - cbase));   // events in the chunk
-    const Event *cev = src.ev + cbase;
-    const uint8_t *cfl = src.flags ? src.flags + cbase : nullptr;
-    uint64_t *cout = out + cbase;
-    const int64_t T0 = src.t0();
-    const uint32_t lmask = (1u << lb) - 1u;
-    __syncthreads();
-    SP_STAMP(0);
-    // 1. read, validate, histogram (item j of thread t = chunk event j * 1024 + t: coalesced)
-#pragma unroll 1
-    for (int j0 = 0; j0 < ITEMS; j0 += GRP) {
-        Event evs[GRP];
-#pragma unroll
-        for (int q = 0; q < GRP; ++q) {
-            const int32_t k = (j0 + q) * SP_THREADS + (int32_t)t;
-            if (k < crem) evs[q] = cev[k];
-        }
-#pragma unroll
-        for (int q = 0; q < GRP; ++q) {
-            const int32_t k = (j0 + q) * SP_THREADS + (int32_t)t;
-            if (k >= crem) continue;
-            const int st = sp_status(evs[q], nflows);
-            if (st == 127) atomicAdd(&goff[(uint32_t)evs[q].idx >> lb], 1u);
-            else cout[k] = pack_verdict(st, 0, 0);
-        }
-    }
-    __syncthreads();
-    SP_STAMP(1);
-    if ((int32_t)t < nparts) sp_put(&col[(int64_t)c * nparts + t], goff[t]);     // row c: one coalesced run
-    sp_grid_sync(bar, bar_base + G, err);
-    SP_STAMP(2);
-    // 2. column scans: digit d by wave d / G of workgroup d mod G, the column's G entries loaded at once
-    for (uint32_t d = g + (uint32_t)wave * G; d < (uint32_t)nparts; d += G * SP_WAVES) {
-        constexpr int CL = SP_MAX_G / WAVE;
-        uint32_t x[CL];
-#pragma unroll
-        for (int i = 0; i < CL; ++i) {
-            const uint32_t k = (uint32_t)i * WAVE + lane;
-            x[i] = k < G ? sp_get(&col[(int64_t)k * nparts + d]) : 0u;
-        }
-        uint32_t carry = 0;
-#pragma unroll
-        for (int i = 0; i < CL; ++i) {
-            const uint32_t k = (uint32_t)i * WAVE + lane;
-            const uint32_t inc = wave_inclusive_scan(x[i]);
-            if (k < G) sp_put(&col[(int64_t)k * nparts + d], carry + inc - x[i]);
-            carry += __shfl(inc, WAVE - 1, WAVE);
-        }
-        if (lane == 0) sp_put(&col[(int64_t)G * nparts + d], carry);
-    }
-    SP_STAMP(3);
-    sp_grid_sync(bar, bar_base + 2 * G, err);
-    SP_STAMP(4);
-    // 3. range starts (every chunk scans the totals) + this chunk's column entry
-    {
-        const bool in = (int32_t)t < nparts;
-        const uint32_t tot = in ? sp_get(&col[(int64_t)G * nparts + t]) : 0u;
-        const uint32_t mine = in ? sp_get(&col[(int64_t)c * nparts + t]) : 0u;
-        uint32_t total;
-        const uint32_t rs = block_exclusive_scan(tot, waves_tot, &total);
-        goff[t] = rs + mine;
-        if (c == 0) {
-            if (in) rstart[t] = rs;
-            if (t == 0) rstart[nparts] = total;
-        }
-    }
-    SP_STAMP(5);
-    // 4. write-out rounds.  Round r = chunk events [r * SP_TILE, (r + 1) * SP_TILE); wave w takes its
-    // 512 consecutive events as 8 items of 64 (arrival order = (wave, item, lane)), so per-wave ranks +
-    // the waves' exclusive counts give the stable order.  The value carries {digit, index in the round}
-    // in its position bits while staged; the store restores the arrival position.
-    Event evs[SP_RITEMS];
-    auto load_round = [&](int r) {
-        int32_t k0 = r * SP_TILE + wave * (SP_RITEMS * WAVE) + (int32_t)lane;
-        asm volatile("" : "+v"(k0));                  // (no address of a later round is computed ahead: VGPRs)
-#pragma unroll
-        for (int q = 0; q < SP_RITEMS; ++q) {
-            const int32_t k = k0 + q * WAVE;
-            if (k < crem) evs[q] = cev[k];
-        }
-    };
-    load_round(0);
-    SP_STAMP(6);
-#ifdef SENTINEL_SPLIT_STAMPS
-    unsigned long long rt_ = wall_clock64();
-    if (t < 4) g_split_round[g][t] = 0;
-#endif
-#pragma unroll 1
-    for (int r = 0; r < NR; ++r) {
-        for (uint32_t d = t; d < (uint32_t)(SP_WAVES * PART_BINS / 2); d += SP_THREADS)
-            reinterpret_cast<uint32_t *>(&cnt[0][0])[d] = 0;
-        sp_lds_sync();
-        uint64_t v[SP_RITEMS];
-        uint32_t rk[SP_RITEMS];
-#pragma unroll
-        for (int q = 0; q < SP_RITEMS; ++q) {
-            const int32_t loc = wave * (SP_RITEMS * WAVE) + q * WAVE + (int32_t)lane;     // index in the round
-            const int32_t k = r * SP_TILE + loc;
-            const Event e = evs[q];
-            const bool valid = k < crem && sp_status(e, nflows) == 127;
-            const uint32_t d = valid ? (uint32_t)e.idx >> lb : 0u;
-            v[q] = ~0ull;
-            if (valid) {
-                const uint8_t fl = cfl ? cfl[k] : 0;
-                v[q] = src.pack_event((d << SP_LOC_BITS) | (uint32_t)loc, e, fl, T0) |
-                       ((uint64_t)((uint32_t)e.idx & lmask) << VAL_KEY_SHIFT);
-            }
-            const uint64_t peers = match_peers<PART_MAX_BITS>(d, valid, pbits);
-            const uint32_t c0 = cnt[wave][d];
-            rk[q] = c0 + mask_rank(peers);
-            if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane)
-                cnt[wave][d] = (uint16_t)(c0 + __popcll(peers));
-        }
-        if (r + 1 < NR) load_round(r + 1);            // the next round's events in flight from here on
-        sp_lds_sync();
-        SP_RSTAMP(0);
-        // per digit: exclusive over the waves (in place) and the round's count; the digits' staged starts
-        uint32_t run = 0;
-#pragma unroll
-        for (int w = 0; w < SP_WAVES; ++w) {
-            const uint32_t x = cnt[w][t];
-            cnt[w][t] = (uint16_t)run;
-            run += x;
-        }
-        uint32_t total;
-        soff[t] = sp_block_exclusive_scan(run, waves_tot, &total);
-        sp_lds_sync();
-        SP_RSTAMP(1);
-#pragma unroll
-        for (int q = 0; q < SP_RITEMS; ++q) {
-            if (v[q] == ~0ull) continue;
-            const uint32_t d = ((uint32_t)v[q] >> SP_LOC_BITS) & (PART_BINS - 1);
-            stage[soff[d] + cnt[wave][d] + rk[q]] = v[q];
-        }
-        sp_lds_sync();
-        SP_RSTAMP(2);
-        const int64_t rbase = cbase + (int64_t)r * SP_TILE;
-        for (uint32_t p = t; p < total; p += SP_THREADS) {
-            const uint64_t x = stage[p];
-            const uint32_t d = ((uint32_t)x >> SP_LOC_BITS) & (PART_BINS - 1);
-            const uint64_t val = (x & ~(uint64_t)SEQ_MASK) | (uint64_t)(rbase + ((uint32_t)x & (SP_TILE - 1)));
-#if defined(SENTINEL_SPLIT_DIAG) && SENTINEL_SPLIT_DIAG == 2      // cost diagnostic: stores in staged order
-            vals_out[rbase + p] = val + goff[d] + soff[d];
-#else
-            vals_out[goff[d] + p - soff[d]] = val;
-#endif
-        }
-        sp_lds_sync();
-        SP_RSTAMP(3);
-        goff[t] += run;
-    }
-#ifdef SENTINEL_SPLIT_STAMPS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    SP_STAMP(7);
-#endif
-}
-
 // A flow's window header {epoch, PASS} x n held in VGPRs while its events are decided in arrival
 // order (the k_process_reg scheme): closed-form homogeneous segments, the reference state machine
 // (seq_event on global memory) for everything else, only dirty pairs written back.
@@ -727,7 +459,7 @@ struct FlowWindow {
             int32_t aa;
             uint8_t fl;
             src.load(seq, tt, aa, fl);
-            seq_event(T, key, ks, E, aa, fl, seq, V);
+            seq_event(T, key, ks, E, aa, fl, seq, V, V.at(i, vals[i]));
         }
 #pragma unroll
         for (int j = 0; j < NMAX; ++j)
@@ -826,7 +558,7 @@ struct FlowWindow {
                 (void)event(v, src, T0, a, pr);
                 return a;
             },
-            [&](uint64_t v, uint64_t vd) { V.out[(uint32_t)v & SEQ_MASK] = vd; });
+            [&](uint32_t k, uint64_t v, uint64_t vd) { V.put(q + k, v, vd); });
         het_book(E, fresh, h);
     }
 
@@ -876,7 +608,7 @@ __device__ inline void part_run_w(FlowWindow<NMAX> &fw, const KeyTable &T, uint3
                 if (acc == 0x123456789ull) V.out[0] = acc;
             }
 #else
-            for (uint32_t k = 0; k < len; ++k) store_verdict(V.out, (uint32_t)s_val[q + k] & SEQ_MASK, fw.verdict(s0, a, K, k, small));
+            for (uint32_t k = 0; k < len; ++k) V.put(q + k, s_val[q + k], fw.verdict(s0, a, K, k, small));
 #endif
 #endif
         }
@@ -971,8 +703,7 @@ __device__ inline bool part_run_single(FlowWindow<NMAX> &fw, const uint64_t *s_v
 #elif defined(SENTINEL_DIAG_VLINEAR)     // cost diagnostic only (wrong output): flow-contiguous stores
     for (uint32_t k = 0; k < len; ++k) V.out[(blockIdx.x * blockDim.x + threadIdx.x) * 8 + (k & 7)] = fw.verdict(s0, a, K, k, small);
 #else
-    for (uint32_t k = 0; k < len; ++k)
-        store_verdict(V.out, (uint32_t)s_val[q0 + k] & SEQ_MASK, fw.verdict(s0, a, K, k, small));
+    for (uint32_t k = 0; k < len; ++k) V.put(q0 + k, s_val[q0 + k], fw.verdict(s0, a, K, k, small));
 #endif
     return true;
 }
@@ -1038,7 +769,7 @@ __device__ inline void part_run_defer(FlowWindow<NMAX> &fw, const KeyTable &T, u
                 reco[si] = K | (small ? COOP_SMALL : 0u);
                 ao[si] = a;
             } else {
-                for (uint32_t k = 0; k < len; ++k) store_verdict(V.out, (uint32_t)s_val[q + k] & SEQ_MASK, fw.verdict(s0, a, K, k, small));
+                for (uint32_t k = 0; k < len; ++k) V.put(q + k, s_val[q + k], fw.verdict(s0, a, K, k, small));
             }
         }
         if (si == 0) len1 = q2 - q0;
@@ -1104,8 +835,9 @@ struct HetLds {
 // workgroup barriers).  Returns the segment's sums (all lanes).
 template <int ITEMS>
 __device__ inline HetSums coop_het(uint32_t st, uint32_t en, const int32_t (&a)[ITEMS], const int32_t *a_lds,
-                                   int64_t x, uint8_t kind, double thr, double I_s, const uint64_t *cval, uint64_t *out,
-                                   HetLds &L) {
+                                   int64_t x, uint8_t kind, double thr, double I_s, const uint64_t *cval,
+                                   const Verdicts &V, HetLds &L) {
+    // (V.obase = the chunk's first position: cval[q]'s verdict goes to V.at(q, cval[q]))
     const uint32_t t0 = threadIdx.x * ITEMS;
     const int64_t x0 = x;
     int64_t mine = 0;
@@ -1138,7 +870,7 @@ __device__ inline HetSums coop_het(uint32_t st, uint32_t en, const int32_t (&a)[
     for (int k = 0; k < ITEMS; ++k) {
         const uint32_t q = t0 + k;
         if (q >= st && q < f) {
-            out[(uint32_t)cval[q] & SEQ_MASK] = pack_verdict(ST_OK, java_d2i(remaining_of(thr, I_s, wrap_add(x, pk), a[k])), 0);
+            V.put(q, cval[q], pack_verdict(ST_OK, java_d2i(remaining_of(thr, I_s, wrap_add(x, pk), a[k])), 0));
             pk += a[k];
         }
         if (q == f && f < en) L.acq = pk;     // the passed sum before f (its prefix)
@@ -1155,7 +887,7 @@ __device__ inline HetSums coop_het(uint32_t st, uint32_t en, const int32_t (&a)[
                 kind, thr, I_s, en - f, x, np, acq, [&](uint32_t i) { return cval[f + i]; },
                 [&](uint32_t i, uint64_t v, int32_t &ai, uint64_t *&dst) {
                     ai = a_lds[f + i];
-                    dst = out + ((uint32_t)v & SEQ_MASK);
+                    dst = V.out + V.at(f + i, v);
                 });
             if (threadIdx.x == 0) { L.acq = x; L.np = np; L.first[1] = f + d; }
         }
@@ -1166,7 +898,7 @@ __device__ inline HetSums coop_het(uint32_t st, uint32_t en, const int32_t (&a)[
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) {
             const uint32_t q = t0 + k;
-            if (q >= dead0 && q < en) out[(uint32_t)cval[q] & SEQ_MASK] = pack_verdict(ST_BLOCKED, 0, 0);
+            if (q >= dead0 && q < en) V.put(q, cval[q], pack_verdict(ST_BLOCKED, 0, 0));
         }
         __syncthreads();
     }
@@ -1271,7 +1003,7 @@ __global__ __launch_bounds__(LS_THREADS) void k_long_dead(const uint64_t *__rest
 #pragma unroll
         for (int k = 0; k < LS_ITEMS; ++k) {
             const uint32_t q = k * LS_THREADS + threadIdx.x;
-            if (q < cn) V.out[(uint32_t)sval[q0c + q] & SEQ_MASK] = pack_verdict(ST_BLOCKED, 0, 0);
+            if (q < cn) V.put(q0c + q, sval[q0c + q], pack_verdict(ST_BLOCKED, 0, 0));
         }
     }
 }
@@ -1484,7 +1216,7 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
                 if (hs >= ns) break;
                 const uint32_t st = seg_start[hs];
                 const uint32_t en = hs + 1 < ns ? seg_start[hs + 1] : cn;
-                const HetSums sums = coop_het<PL_ITEMS>(st, en, a, a_lds, s_hx, kind, thr, I_s, sval + c0, V.out, hl);
+                const HetSums sums = coop_het<PL_ITEMS>(st, en, a, a_lds, s_hx, kind, thr, I_s, sval + c0, V.based(c0), hl);
                 if (threadIdx.x == 0) fw.het_book(seg_E[hs], h_fresh, sums);
                 from = hs + 1;
             }
@@ -1497,7 +1229,6 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
                 if (qq >= cn) continue;
                 const uint32_t sg = gid[k];
                 if (seg_flag[sg] & 2u) continue;
-                const uint32_t seq = (uint32_t)sval[c0 + qq] & SEQ_MASK;
                 uint64_t v;
                 if (qq - seg_start[sg] < seg_K[sg])
                     v = pack_verdict(ST_OK, java_d2i(remaining_of(thr, I_s,
@@ -1505,7 +1236,7 @@ __global__ __launch_bounds__(PL_THREADS) void k_part_long(KeyTable T, const uint
                                                                   seg_a[sg])), 0);
                 else
                     v = pack_verdict(ST_BLOCKED, 0, 0);
-                V.out[seq] = v;
+                V.put(c0 + qq, sval[c0 + qq], v);
             }
             __syncthreads();
 #ifdef SENTINEL_DIAG_LONG
@@ -1811,6 +1542,11 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
     // 3. decide.  Hot runs go to k_part_long from HBM: the half's region of gsval is its own
     // (half 0 at the range start, half 1 at its end).
     const uint32_t goff = pstart + (h ? size - total : 0u);
+    // decide-order output: the half's sorted events own positions [goff, goff + total); their arrival
+    // positions go out in one coalesced sweep, every verdict below to goff + its sorted index
+    const Verdicts VV = V.based(goff);
+    if (V.oseq)
+        for (uint32_t i = t; i < total; i += PH_THREADS) V.oseq[goff + i] = (uint32_t)sv[i] & SEQ_MASK;
     if (c > LONG_RUN) {
         LR.push(goff + start, goff + start + c, key);
         const uint32_t l = atomicAdd(&s_nlong, 1u);
@@ -1878,12 +1614,12 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
                 // (hb <= 7) a run straddles an epoch boundary often and the walk alone is cheaper
                 // (measured: 125k flows +4%, 250k +1%; 500k flows -1% without it)
                 if (hb >= PH_COOP_SINGLE_HB &&
-                    part_run_single<NMAX, true>(fw, sv, start, start + c, src, V, T0, &s0[0], &rec[0], &a[0], &small)) {
+                    part_run_single<NMAX, true>(fw, sv, start, start + c, src, VV, T0, &s0[0], &rec[0], &a[0], &small)) {
                     rec[0] |= small ? COOP_SMALL : 0u;
                     len1 = len12 = c;
                 } else {
                     fw.load_header(T0);
-                    part_run_defer<NMAX>(fw, T, key, sv, start, start + c, src, V, T0, s0, rec, a, len1, len12,
+                    part_run_defer<NMAX>(fw, T, key, sv, start, start + c, src, VV, T0, s0, rec, a, len1, len12,
                                          bits ? segb : nullptr, bits ? hetb : nullptr, bits ? prib : nullptr);
                 }
                 c_thr[t] = fw.thr;
@@ -1910,13 +1646,12 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
             const uint32_t sg = k < l1 ? 0u : 1u;
             const uint32_t rec = c_K[sg * CF + kj];
             if (rec & COOP_SKIP) continue;                        // sequential segment: written by the walk
-            store_verdict(V.out, (uint32_t)v & SEQ_MASK,
-                          run_verdict(c_thr[kj], c_is[kj], c_s0[sg * CF + kj], c_a[sg * CF + kj],
-                                      rec & (COOP_SMALL - 1u), sg ? k - l1 : k, (rec & COOP_SMALL) != 0));
+            VV.put(i, v, run_verdict(c_thr[kj], c_is[kj], c_s0[sg * CF + kj], c_a[sg * CF + kj],
+                                     rec & (COOP_SMALL - 1u), sg ? k - l1 : k, (rec & COOP_SMALL) != 0));
         }
-    } else if (c > 0 && c <= LONG_RUN && !part_run_single<NMAX>(fw, sv, start, start + c, src, V, T0)) {
+    } else if (c > 0 && c <= LONG_RUN && !part_run_single<NMAX>(fw, sv, start, start + c, src, VV, T0)) {
         fw.load_header(T0);
-        part_run_w<NMAX>(fw, T, key, sv, start, start + c, src, V, T0);
+        part_run_w<NMAX>(fw, T, key, sv, start, start + c, src, VV, T0);
     }
 #ifdef SENTINEL_DIAG_PHASES
     __syncthreads();
@@ -2012,9 +1747,11 @@ __global__ __launch_bounds__(PH_THREADS) void k_part_big(
             __syncthreads();
             base[t] += run;
         }
+        if (V.oseq)                                       // decide-order output: positions [goff, goff + total)
+            for (uint32_t q = t; q < total; q += PH_THREADS) V.oseq[goff + q] = (uint32_t)dst[q] & SEQ_MASK;
         const uint32_t key = (p << lb) | (h << hb) | t;
         if (c > LONG_RUN) LR.push(goff + start, goff + start + c, key);
-        if (c > 0 && c <= LONG_RUN) part_run<NMAX>(T, key, dst, start, start + c, src, V, T0);
+        if (c > 0 && c <= LONG_RUN) part_run<NMAX>(T, key, dst, start, start + c, src, V.based(goff), T0);
         __syncthreads();                                  // LDS reuse by the next entry
     }
 }

@@ -374,6 +374,34 @@ class GpuTokenService:
         check(rc, "submit_flow_batch")
         return verdicts
 
+    def submit_flow_batch_ordered(self, events, flags=None, verdicts=None, seq=None, stream=None):
+        """submit_flow_batch with decide-order output (sentinel_submit_flow_batch_ordered): returns
+        (verdicts, seq), int64 (n,) and int32 (n,) device tensors; verdicts[j] answers the event at arrival
+        position seq[j].  Asynchronous on `stream`."""
+        import torch
+        n = int(events.shape[0])
+        if verdicts is None:
+            verdicts = torch.empty(n, dtype=torch.int64, device=events.device)
+        if seq is None:
+            seq = torch.empty(n, dtype=torch.int32, device=events.device)
+        s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        rc = self._L.sentinel_submit_flow_batch_ordered(
+            self._h, n, C.c_void_p(events.data_ptr()), None if flags is None else C.c_void_p(flags.data_ptr()),
+            C.c_void_p(verdicts.data_ptr()), C.c_void_p(seq.data_ptr()), None if s is None else C.c_void_p(s))
+        check(rc, "submit_flow_batch_ordered")
+        return verdicts, seq
+
+    def submit_flow_batch_ordered_host(self, flow_idx, acquire, ts, flags=None):
+        """Host arrays in; (status, remaining, wait_in_ms, seq) numpy arrays out in decide order: entry j
+        answers the event at arrival position seq[j] (synchronous)."""
+        ev = self.pack_events(flow_idx, acquire, ts)
+        flags = None if flags is None else np.ascontiguousarray(flags, dtype=np.uint8)
+        out = np.empty(len(ev), dtype=_lib.VERDICT_DTYPE)
+        seq = np.empty(len(ev), dtype=np.uint32)
+        check(self._L.sentinel_submit_flow_batch_ordered_host(self._h, len(ev), _p(ev), _p(flags), _p(out), _p(seq)),
+              "submit_flow_batch_ordered_host")
+        return out["status"].astype(np.int8), out["remaining"].copy(), out["wait_in_ms"].astype(np.int32), seq
+
     def submit_flow_batches(self, events_list, verdicts_list, flags_list=None, stream=None):
         """Device batches in order under one engine lock (sentinel_submit_flow_batches): each events tensor int64
         (n, 2) of sentinel_event_t, each verdict tensor int64 (n,)."""
@@ -654,10 +682,11 @@ class GpuTokenService:
         return dict(key_walk=int(out[0]), overflow=int(out[1]), block=int(blk[0]))
 
     def flow_path_stats(self):
-        """Flow batches so far by pipeline: {small, sorted, partition (prep + scan + scatter), split (one sweep)}."""
+        """Flow batches so far by pipeline: {small, sorted, partition, ordered (of the partition batches, those
+        with decide-order output: sentinel_submit_flow_batch_ordered)}."""
         out = np.zeros(4, dtype=np.int64)
         check(self._L.sentinel_flow_path_stats(self._h, _p(out)), "flow_path_stats")
-        return dict(small=int(out[0]), sorted=int(out[1]), partition=int(out[2]), split=int(out[3]))
+        return dict(small=int(out[0]), sorted=int(out[1]), partition=int(out[2]), ordered=int(out[3]))
 
     def param_top_values(self, ts: int, number: int = _lib.TOP_PARAMS):
         """getTopValues(number) of every param rule at ts -> list (per rule index) of [(key, avg)]."""

@@ -91,3 +91,67 @@ def test_sync_batcher_survives_reload_and_destroy():
         x.join()
     b.close()
     assert seen and set(seen) == {0}
+
+
+def test_async_batcher_large_batches_decide_order(oracle_mod, monkeypatch):
+    """Batches larger than the one-launch kernel's 4096 events are decided by the partition path with
+    decide-order output (sentinel_submit_flow_batch_ordered): the batcher answers each request from
+    (seq[j], verdict[j]) -- the wire server's path -- with no arrival-order permutation anywhere.
+    60k asynchronous requests in one call (Zipf flows, acquire 1..3, prioritized requests, unknown and
+    invalid flowIds), decided as batches of up to 32768 in arrival order: every callback fires once,
+    with the oracle's verdict for its own request."""
+    import sentinel_amd as sa
+    from sentinel_amd import _lib
+    monkeypatch.setenv("SENTINEL_FLOW_PATH", "partition")
+    n = 60_000
+    rules, ev = T.config2(n, seed=21, n_flows=5000)
+    svc = sa.GpuTokenService(0)
+    svc.load_rules_array(rules.flow_id, rules.count, rules.threshold_type, rules.sample_count,
+                         rules.window_interval_ms, rules.namespace, rules.checker)
+    rng = np.random.default_rng(21)
+    idx = ev.flow_idx.astype(np.int32).copy()
+    acq = rng.integers(1, 4, size=n).astype(np.int32)
+    flags = (rng.random(n) < 0.02).astype(np.uint8)
+    ids = np.asarray(rules.flow_id, dtype=np.int64)[idx]
+    ids[::997] = 10 ** 12 + 5                               # no rule -> NO_RULE_EXISTS
+    idx[::997] = _lib.IDX_NO_RULE
+    ids[::1499] = 0                                         # flowId <= 0 -> BAD_REQUEST
+    idx[::1499] = _lib.IDX_BAD_ID
+    ts = np.ascontiguousarray(ev.ts, dtype=np.int64)
+    L = svc._L
+    L.sentinel_batcher_request_tokens_async.restype = C.c_int
+    L.sentinel_batcher_request_tokens_async.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                       C.c_void_p, CB, C.c_void_p, C.c_void_p]
+    b = C.c_void_p()
+    assert L.sentinel_batcher_create(svc.handle, 32768, 200_000, C.byref(b)) == 0
+    st = np.full(n, -100, np.int32)
+    rem = np.zeros(n, np.int32)
+    wt = np.zeros(n, np.int32)
+    fired = np.zeros(n, np.int32)
+    done = threading.Event()
+    cnt = [0]
+
+    def on_done(ctx, tag, res):
+        r = C.cast(res, C.POINTER(_lib.TokenResultC)).contents
+        st[tag], rem[tag], wt[tag] = r.status, r.remaining, r.wait_in_ms
+        fired[tag] += 1
+        cnt[0] += 1
+        if cnt[0] == n:
+            done.set()
+
+    cb = CB(on_done)
+    tags = np.arange(n, dtype=np.uint64)
+    assert L.sentinel_batcher_request_tokens_async(b, n, ids.ctypes.data, acq.ctypes.data, flags.ctypes.data,
+                                                   ts.ctypes.data, cb, None, tags.ctypes.data) == 0
+    assert done.wait(120)
+    nb, nr = C.c_int64(), C.c_int64()
+    assert L.sentinel_batcher_stats(b, C.byref(nb), C.byref(nr)) == 0
+    L.sentinel_batcher_destroy(b)
+    assert (fired == 1).all()
+    assert nr.value == n and nb.value >= 2
+    assert svc.flow_path_stats()["ordered"] >= 2, svc.flow_path_stats()    # decide-order partition batches
+    orc = oracle_mod.TokenServiceOracle(rules.as_dicts())
+    st_o, rem_o, w_o = orc.replay(idx, acq, ts, flags)
+    bad = np.nonzero((st != st_o) | (rem != rem_o) | (wt != w_o))[0]
+    assert len(bad) == 0, (len(bad), bad[:5], st[bad[:5]], st_o[bad[:5]], rem[bad[:5]], rem_o[bad[:5]])
+    assert {0, 1, sa.TokenResultStatus.NO_RULE_EXISTS, sa.TokenResultStatus.BAD_REQUEST} <= set(np.unique(st_o).tolist())

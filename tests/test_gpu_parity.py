@@ -12,14 +12,40 @@ from sentinel_amd import trace as T
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["sorted", "partition", "partition3", "small"])
+@pytest.fixture(autouse=True, params=["sorted", "partition", "ordered", "small"])
 def flow_path(request, monkeypatch):
     """Every flow parity case runs on every flow pipeline: the global radix sort, the
-    partition-local path with its one-sweep front (k_part_split, batches of >= 64K events) and with
-    prep + scan + scatter (SENTINEL_PART_SPLIT=0), and the one-launch small-batch kernel over
-    4096-event chunks (both variables are read when an engine is created)."""
-    monkeypatch.setenv("SENTINEL_FLOW_PATH", "partition" if request.param == "partition3" else request.param)
-    monkeypatch.setenv("SENTINEL_PART_SPLIT", "0" if request.param == "partition3" else "1")
+    partition-local path (prep + scan + multi-split + k_part_half), the same with decide-order output
+    ("ordered": sentinel_submit_flow_batch_ordered[_host], its verdicts put back at their arrival
+    positions through the returned seq -- a permutation of [0, n) -- before the comparison), and the
+    one-launch small-batch kernel over 4096-event chunks (the variable is read when an engine is
+    created)."""
+    monkeypatch.setenv("SENTINEL_FLOW_PATH", "partition" if request.param == "ordered" else request.param)
+    if request.param == "ordered":
+        from sentinel_amd.token_service import GpuTokenService
+
+        def host(self, flow_idx, acquire, ts, flags=None):
+            st, rem, w, seq = self.submit_flow_batch_ordered_host(flow_idx, acquire, ts, flags)
+            n = len(seq)
+            assert np.array_equal(np.sort(seq), np.arange(n, dtype=np.uint32)), "seq is not a permutation"
+            out = [np.empty_like(st), np.empty_like(rem), np.empty_like(w)]
+            for o, x in zip(out, (st, rem, w)):
+                o[seq.astype(np.int64)] = x
+            return tuple(out)
+
+        def device(self, events, flags=None, verdicts=None, stream=None):
+            import torch
+            v, seq = self.submit_flow_batch_ordered(events, flags=flags, stream=stream)
+            self.synchronize()
+            n = int(events.shape[0])
+            s = seq.to(torch.int64)
+            assert torch.equal(torch.sort(s).values, torch.arange(n, device=s.device)), "seq is not a permutation"
+            out = verdicts if verdicts is not None else torch.empty(n, dtype=torch.int64, device=events.device)
+            out[s] = v
+            return out
+
+        monkeypatch.setattr(GpuTokenService, "submit_flow_batch_host", host)
+        monkeypatch.setattr(GpuTokenService, "submit_flow_batch", device)
     return request.param
 
 

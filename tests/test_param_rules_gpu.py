@@ -230,6 +230,84 @@ def test_shared_count_min_block_epoch_edges(oracle_mod, monkeypatch):
     assert svc.param_cm_stats()["block"] == len(spans), svc.param_cm_stats()
 
 
+# idle gaps (epochs) between a key's admission and its re-admission, all multiples of the ring (2n = 20):
+# 140 / 160 / 240 lie in (128, 256) -- the 32-bit LDS cells' tag mod 256 of the old epoch reads as
+# "newer" under a half-range test -- and 2^23 + 12 in (2^23, 2^24) does the same to the 24-bit HBM tags;
+# 100 and 300 are controls
+RETOUCH_GAPS = (100, 140, 160, 240, 300, (1 << 23) + 12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("walk", ["block32", "block64", "global", "launch", "coop"])
+def test_shared_count_min_retouch_after_idle(oracle_mod, monkeypatch, walk):
+    """a key K admitted up to its threshold at epoch E0, idle for g epochs (g a
+    multiple of the 2n-slot ring, so its ring slot still holds E0), re-admitted at E0 + g at the end of a
+    batch, then probed one epoch later.  The re-admission's add must restart the slot at E0 + g; if it
+    kept E0's tag (a lost add), the probe's window misses the re-admitted count and passes what the exact
+    checker blocks.  A sketch wide for its ~1200 keys (w = 2^16: 1024 blocks of 64 columns, one key per
+    block on average -- narrow enough that small batches still take the block walk), so no collision can
+    hide a lost add;
+    filler batches of other keys (each < 100 epochs) carry the clock across the short gaps.  Every walk
+    of the shared sketch: the block walk with 32-bit or 64-bit LDS cells, the two-phase HBM walk and both
+    per-rule lane schedules.  Every verdict audited on exact counters: zero violations, and the probe
+    blocks all of K's requests."""
+    import sentinel_amd as sa
+    monkeypatch.setenv("SENTINEL_CM_LEVELS", walk if walk in ("launch", "coop") else "keys")
+    monkeypatch.setenv("SENTINEL_CM_BLOCK", "0" if walk == "global" else "1")
+    monkeypatch.setenv("SENTINEL_CM_C32", "0" if walk == "block64" else "1")
+    R, w = 40, 100                                         # rule 0 = K's rule (count 5); 1 s / 10 buckets
+    count = np.full(R, 1e6)
+    count[0] = 5.0
+    kkey = np.uint64(7)                                    # rule 0, value 7
+    rng = np.random.default_rng(91)
+    failures = []
+    for g in RETOUCH_GAPS:
+        svc, orc = _cluster_pair(oracle_mod, count, {}, sample_count=lambda r: 10)
+        svc.set_param_mode(sa._lib.PARAM_COUNT_MIN_SHARED, depth=4, width=1 << 16)
+        t0 = T.T0_ALIGNED + 7
+        E0 = t0 // w
+        batches = []
+
+        def batch(ep_lo, ep_hi, k_epoch=None, n_fill=120):
+            fr = rng.integers(1, R, size=n_fill).astype(np.int32)
+            fk = (fr.astype(np.uint64) << np.uint64(20)) | rng.integers(0, 30, size=n_fill).astype(np.uint64)
+            ft = np.sort(rng.integers(ep_lo * w, ep_hi * w + w, size=n_fill)).astype(np.int64)
+            r, k, t = [fr], [fk], [ft]
+            if k_epoch is not None:                        # K's 10 requests after the filler, in epoch k_epoch
+                t[0] = np.minimum(ft, k_epoch * w)
+                r.append(np.zeros(10, np.int32))
+                k.append(np.full(10, kkey, np.uint64))
+                t.append(k_epoch * w + 3 + np.arange(10, dtype=np.int64))
+            batches.append((np.concatenate(r), np.concatenate(k), np.concatenate(t)))
+
+        batch(E0, E0, k_epoch=E0)                          # K admitted up to its threshold at E0
+        if g < 1000:                                       # filler batches up to E0 + g - 1
+            e = E0 + 1
+            while e < E0 + g - 1:
+                hi = min(e + 90, E0 + g - 1)
+                batch(e, hi)
+                e = hi + 1
+        batch(E0 + g, E0 + g, k_epoch=E0 + g)              # re-admission at the batch's newest epoch
+        batch(E0 + g + 1, E0 + g + 1, k_epoch=E0 + g + 1)  # probe: the window (E0+g-9, E0+g+1] holds 5
+        st = []
+        for r, k, t in batches:
+            st.append(svc.submit_param_batch_host(r, np.ones(len(r), np.int32), k, t)[0])
+        ridx = np.concatenate([b[0] for b in batches])
+        keys = np.concatenate([b[1] for b in batches])
+        ts = np.concatenate([b[2] for b in batches])
+        st = np.concatenate(st)
+        m = len(ts)
+        viol, fb, dec = orc.param_cm_audit(ridx, np.ones(m, np.int32), ts, np.arange(m), np.ones(m, np.int32), keys, st)
+        isk = keys == kkey
+        kst = st[isk].reshape(-1, 10)                      # K's verdicts: admission, re-admission, probe
+        passes = (kst == 0).sum(axis=1).tolist()
+        if viol or dec != m or passes != [5, 5, 0]:
+            failures.append(dict(gap=g, violations=viol, k_passes=passes))
+        if walk in ("block32", "block64"):
+            assert svc.param_cm_stats()["block"] == len(batches), svc.param_cm_stats()
+    assert not failures, failures
+
+
 @pytest.mark.gpu
 def test_avg_local_params_follow_connected_count(oracle_mod):
     """ClusterParamFlowChecker.calcGlobalThreshold reads ConnectionManager.getConnectedCount on every
