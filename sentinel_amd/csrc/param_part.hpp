@@ -1218,12 +1218,24 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
     const int64_t Eref = cm_eref(epoch_of(tmax, wsk, rcp_wsk), ehi);   // (no slot holds a later epoch)
     for (uint32_t i = t; i < CMB_WORDS / 64; i += blockDim.x) dirty[i] = 0;
     if (!(diag & 4)) {
-        for (uint32_t i = t; i < words / 2; i += blockDim.x) {
-            const ulonglong2 x = reinterpret_cast<const ulonglong2 *>(gcl)[i];
+        // every 16-B load of the thread's share of the block in flight before the first LDS store (one
+        // HBM round trip per block instead of one per loop iteration); words / 2 <= CMB_WORDS / 2 = 12 x 256
+        constexpr int LK = CMB_WORDS / 2 / 256;
+        const ulonglong2 *g2 = reinterpret_cast<const ulonglong2 *>(gcl);
+        ulonglong2 xs[LK];
+#pragma unroll
+        for (int k = 0; k < LK; ++k) {
+            const uint32_t i = t + (uint32_t)k * 256u;
+            xs[k] = i < words / 2 ? g2[i] : make_ulonglong2(0ull, 0ull);
+        }
+#pragma unroll
+        for (int k = 0; k < LK; ++k) {
+            const uint32_t i = t + (uint32_t)k * 256u;
+            if (i >= words / 2) break;
             if constexpr (C32) {
-                reinterpret_cast<uint2 *>(cl)[i] = make_uint2(cm32_load(x.x, Eref), cm32_load(x.y, Eref));
+                reinterpret_cast<uint2 *>(cl)[i] = make_uint2(cm32_load(xs[k].x, Eref), cm32_load(xs[k].y, Eref));
             } else {
-                reinterpret_cast<ulonglong2 *>(cl)[i] = x;
+                reinterpret_cast<ulonglong2 *>(cl)[i] = xs[k];
             }
         }
     }
