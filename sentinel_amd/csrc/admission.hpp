@@ -936,7 +936,7 @@ __global__ __launch_bounds__(256) void k_process(KeyTable T, BatchWork W, EventS
                 int32_t a;
                 uint8_t fl;
                 src.load(seq, t, a, fl);
-                seq_event(T, key, ks, E, a, fl, seq, V, seq);
+                seq_event(T, key, ks, E, a, fl, seq, V, V.oseq ? V.obase + i : seq);
             }
             W.seg_done[g] = 1;
             continue;
@@ -1105,7 +1105,7 @@ __device__ __forceinline__ void process_reg_body(KeyTable T, BatchWork W, EventS
                     src.unpack(v, T0, t, a, pr);
                     return a;
                 },
-                [&](uint32_t, uint64_t v, uint64_t vd) { V.out[(uint32_t)v & SEQ_MASK] = vd; });
+                [&](uint32_t k, uint64_t v, uint64_t vd) { V.put(st + k, v, vd); });
 #pragma unroll
             for (int j = 0; j < NMAX; ++j)
                 if (j == slot) { ps[j] = wrap_add(ps[j], hs.pass); dirty |= 1u << j; }
@@ -1128,7 +1128,7 @@ __device__ __forceinline__ void process_reg_body(KeyTable T, BatchWork W, EventS
                 int32_t a;
                 uint8_t fl;
                 src.load(seq, t, a, fl);
-                seq_event(T, key, ks, E, a, fl, seq, V, seq);
+                seq_event(T, key, ks, E, a, fl, seq, V, V.oseq ? V.obase + i : seq);
             }
             W.seg_done[g] = 1;
 #pragma unroll
@@ -1265,15 +1265,15 @@ __device__ inline uint32_t wave_walk(uint8_t kind, double thr, double I_s, uint3
 
 // A heterogeneous segment [st, st + len) of the sorted values, walked by one wave.
 __device__ inline HetSums wave_het(uint8_t kind, double thr, double I_s, int64_t x, const uint64_t *sval, uint32_t st,
-                                   uint32_t len, const EventSrc &src, int64_t T0, uint64_t *out) {
+                                   uint32_t len, const EventSrc &src, int64_t T0, const Verdicts &V) {
     const uint32_t lane = lane_id();
     const int64_t x0 = x;
     int64_t npass = 0;
-    auto decode = [&](uint32_t, uint64_t v, int32_t &a, uint64_t *&dst) {
+    auto decode = [&](uint32_t i, uint64_t v, int32_t &a, uint64_t *&dst) {
         int64_t t;
         bool pr;
         src.unpack(v, T0, t, a, pr);
-        dst = out + ((uint32_t)v & SEQ_MASK);
+        dst = V.out + V.at(st + i, v);
     };
     int64_t tot = 0;
     const uint32_t dpos = wave_walk(kind, thr, I_s, len, x, npass, tot, [&](uint32_t i) { return sval[st + i]; }, decode);
@@ -1291,7 +1291,7 @@ __device__ inline HetSums wave_het(uint8_t kind, double thr, double I_s, int64_t
                 bool pr;
                 src.unpack(v[k], T0, t, a, pr);
                 tail += a;
-                out[(uint32_t)v[k] & SEQ_MASK] = pack_verdict(ST_BLOCKED, 0, 0);
+                V.put(st + i0 + k * WAVE + lane, v[k], pack_verdict(ST_BLOCKED, 0, 0));
             }
     }
 #pragma unroll
@@ -1361,7 +1361,7 @@ __global__ __launch_bounds__(256) void k_process_wave(KeyTable T, BatchWork W, E
                         int32_t a;
                         uint8_t fl;
                         src.load(seq, t, a, fl);
-                        seq_event(T, key, ks, E, a, fl, seq, V, seq);
+                        seq_event(T, key, ks, E, a, fl, seq, V, V.oseq ? V.obase + i : seq);
                     }
                     W.seg_done[g] = 1;
 #pragma unroll
@@ -1390,7 +1390,7 @@ __global__ __launch_bounds__(256) void k_process_wave(KeyTable T, BatchWork W, E
             int64_t blk = 0, preq = 0, breq = 0;
             if (ks.seven && !fresh) { blk = ks.rc(slot, 0); preq = ks.rc(slot, 1); breq = ks.rc(slot, 2); }
             if (W.seg_het[g]) {
-                const HetSums hs = wave_het(kind, thr, I_s, s0, W.sval, st, len, src, T0, V.out);
+                const HetSums hs = wave_het(kind, thr, I_s, s0, W.sval, st, len, src, T0, V);
 #pragma unroll
                 for (int j = 0; j < NMAX; ++j)
                     if (j == slot) { ps[j] = wrap_add(ps[j], hs.pass); dirty |= 1u << j; }
@@ -1493,7 +1493,7 @@ __device__ inline void process_key_group(const KeyTable &T, const BatchWork &W, 
                     int32_t a;
                     uint8_t fl;
                     src.load(seq, t, a, fl);
-                    seq_event(T, key, ks, E, a, fl, seq, V, seq);
+                    seq_event(T, key, ks, E, a, fl, seq, V, V.oseq ? V.obase + i : seq);
                 }
                 W.seg_done[g] = 1;
             }
@@ -1575,11 +1575,12 @@ __global__ __launch_bounds__(256) void k_verdict(KeyTable T, BatchWork W, Verdic
     if (i >= n) return;
     const int64_t nv = (int64_t)*W.nvalid;
     if (i >= nv) return;
+    const uint32_t seq = (uint32_t)W.sval[i] & SEQ_MASK;
+    if (V.oseq) V.oseq[i] = seq;                   // decide-order output: every sorted position's arrival position
     const uint32_t g = W.segid[i] - 1;
     if (W.seg_done[g]) return;
     const uint32_t rank = (uint32_t)i - W.seg_start[g];
     const uint32_t K = W.seg_k[g];
-    const uint32_t seq = (uint32_t)W.sval[i] & SEQ_MASK;
     const uint32_t key = W.seg_key[g];
     if (LIMITER) {
         if (rank >= K) reject_limited(V, seq, seq);
@@ -1593,7 +1594,7 @@ __global__ __launch_bounds__(256) void k_verdict(KeyTable T, BatchWork W, Verdic
     } else {
         v = pack_verdict(ST_BLOCKED, 0, 0);
     }
-    if (LINEAR) V.out[i] = v;          // diagnostic build only: wrong positions, measures scatter cost
+    if (LINEAR || V.oseq) V.out[i] = v;  // decide-order output (LINEAR: the old diagnostic of the same stores)
     else if (NT) __builtin_nontemporal_store(v, V.out + seq);
     else V.out[seq] = v;
 }

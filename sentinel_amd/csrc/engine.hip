@@ -131,7 +131,11 @@ __global__ __launch_bounds__(SORT_THREADS) void k_flow_prep(
     int64_t n, const Event *__restrict__ ev, int32_t nflows, const int32_t *__restrict__ route,
     uint64_t *__restrict__ out, uint32_t *__restrict__ fkey, uint32_t finvalid, int fpasses,
     uint32_t *__restrict__ fhist, uint32_t *__restrict__ lkey, uint32_t linvalid, int lpasses,
-    uint32_t *__restrict__ lhist, int64_t nblocks, const int8_t *__restrict__ route8 = nullptr) {
+    uint32_t *__restrict__ lhist, int64_t nblocks, const int8_t *__restrict__ route8 = nullptr,
+    uint32_t *__restrict__ oseq = nullptr, uint32_t *__restrict__ octr = nullptr, uint32_t opar = 0) {
+    // oseq (decide-order output, no limiters): a decided event goes to position n - 1 - its rank among the
+    // batch's decided events (they sort last, key finvalid: positions [valid, n)), as in k_part_prep
+    if (octr && blockIdx.x == 0 && threadIdx.x == 0) octr[opar ^ 1u] = 0;
     __shared__ uint32_t hf[MAX_PASSES][RADIX];
     __shared__ uint32_t hl[MAX_PASSES][RADIX];
     for (int d = threadIdx.x; d < MAX_PASSES * RADIX; d += SORT_THREADS) {
@@ -178,7 +182,23 @@ __global__ __launch_bounds__(SORT_THREADS) void k_flow_prep(
             lkey[i] = l;
             tile_hist_accumulate(hl, l, lpasses);
         }
-        if (st != 127) put_verdict(out, (uint32_t)i, st, 0, 0);
+        if (st != 127 && !oseq) put_verdict(out, (uint32_t)i, st, 0, 0);
+        if (oseq) {                                  // (one counter atomic per wave)
+            const bool rej = st != 127;
+            const uint64_t m = __builtin_amdgcn_ballot_w64(rej);
+            if (m) {
+                const uint32_t lane = lane_id();
+                const int lead = __ffsll((unsigned long long)m) - 1;
+                uint32_t b = 0;
+                if ((int)lane == lead) b = atomicAdd(&octr[opar], (uint32_t)__popcll(m));
+                b = __shfl(b, lead, WAVE);
+                if (rej) {
+                    const uint32_t pos = (uint32_t)(n - 1) - (b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull)));
+                    put_verdict(out, pos, st, 0, 0);
+                    oseq[pos] = (uint32_t)i;
+                }
+            }
+        }
     }
     __syncthreads();
     tile_hist_store(hf, fhist, fpasses, nblocks);
@@ -1766,14 +1786,20 @@ static int part_back(sentinel_engine_t *e, const PartBufs &B, int64_t n, const E
     return 0;
 }
 
+// the rejected-event counters of decide-order batches (two, alternating per batch: each batch's prep
+// clears the other one)
+static int ensure_octr(sentinel_engine_t *e, hipStream_t s) {
+    if (e->d_octr.p) return 0;
+    if (e->d_octr.ensure(64)) return SENTINEL_E_NOMEM;
+    HIP_OK(hipMemsetAsync(e->d_octr.p, 0, 64, s));
+    e->opar = 0;
+    return 0;
+}
+
 static int submit_flow_part(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
                             hipStream_t s, uint32_t *oseq = nullptr) {
     const PartBufs B = e->part_bufs();
-    if (oseq && !e->d_octr.p) {                           // the rejected-event counters of decide-order batches
-        if (e->d_octr.ensure(64)) return SENTINEL_E_NOMEM;
-        HIP_OK(hipMemsetAsync(e->d_octr.p, 0, 64, s));
-        e->opar = 0;
-    }
+    if (oseq && ensure_octr(e, s)) return SENTINEL_E_NOMEM;
     int rc = part_front(e, B, n, ev, fl, out, s, oseq);
     if (rc) return rc;
     rc = part_back(e, B, n, ev, fl, out, s, oseq);
@@ -1809,12 +1835,14 @@ static bool choose_part(sentinel_engine_t *e, int64_t n) {
 }
 
 static int submit_flow_sorted(sentinel_engine_t *e, int64_t n, const Event *ev, const uint8_t *fl, uint64_t *out,
-                              hipStream_t s) {
+                              hipStream_t s, uint32_t *oseq = nullptr) {
     const int32_t F = (int32_t)e->rules.size();
     const int fbits = bits_for(F);
     const uint32_t finvalid = ((uint32_t)1 << fbits) - 1;
     const bool lim = e->nlimiters > 0 && !e->flow_plain;
     uint32_t *fkey = e->w_fkey.as<uint32_t>();
+    if (lim) oseq = nullptr;                              // (decide order only without namespace limiters)
+    if (oseq && ensure_octr(e, s)) return SENTINEL_E_NOMEM;
     if (lim) {
         e->limiter_pass(n, ev, F, fkey, finvalid, 0, out, s);
         e->hist_pass0(fkey, n, e->w_fhist.as<uint32_t>(), s);   // the limiter invalidated some keys
@@ -1824,15 +1852,18 @@ static int submit_flow_sorted(sentinel_engine_t *e, int64_t n, const Event *ev, 
         e->launch("flow_prep", n, s, [&] {
             k_flow_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
                 n, ev, F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, fkey, finvalid, 1,
-                e->w_fhist.as<uint32_t>(), nullptr, 0, 1, nullptr, nb, e->flow_plain ? nullptr : e->route8());
+                e->w_fhist.as<uint32_t>(), nullptr, 0, 1, nullptr, nb, e->flow_plain ? nullptr : e->route8(),
+                oseq, oseq ? e->d_octr.as<uint32_t>() : nullptr, e->opar);
         });
     }
     Verdicts V{out, fkey, finvalid};
+    V.oseq = oseq;                                        // (sorted positions: obase 0)
     EventSrc src{ev, nullptr, fl, false};
     if (F > 0) {
         KeyTable FT = e->table(e->ft, NEV, 0);
         e->run_pipeline(FT, fkey, e->w_fhist.as<uint32_t>(), n, fbits, src, V, s, e->flow_max_n, false, true);
     }
+    if (oseq) e->opar ^= 1u;
     HIP_OK(hipGetLastError());
     return 0;
 }
@@ -1964,13 +1995,10 @@ static int submit_flow_ordered(sentinel_engine_t *e, int64_t n, const Event *ev,
     if (!(small_ok(e) && (n <= SM_MAX || e->flow_path == 3)) && !lim) {
         int rc = e->ensure_ws(n);
         if (rc) return rc;
-        if (choose_part(e, n)) {
-            e->flow_path_count[3] += 1;
-            return submit_flow_part(e, n, ev, fl, out, s, oseq);
-        }
+        e->flow_path_count[3] += 1;
+        if (choose_part(e, n)) return submit_flow_part(e, n, ev, fl, out, s, oseq);
         e->flow_path_count[1] += 1;
-        rc = submit_flow_sorted(e, n, ev, fl, out, s);
-        if (rc) return rc;
+        return submit_flow_sorted(e, n, ev, fl, out, s, oseq);
     } else {
         int rc = submit_flow(e, n, ev, fl, out, s);
         if (rc) return rc;

@@ -12,16 +12,17 @@ from sentinel_amd import trace as T
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["sorted", "partition", "ordered", "small"])
+@pytest.fixture(autouse=True, params=["sorted", "partition", "ordered", "ordered-sorted", "small"])
 def flow_path(request, monkeypatch):
     """Every flow parity case runs on every flow pipeline: the global radix sort, the
     partition-local path (prep + scan + multi-split + k_part_half), the same with decide-order output
     ("ordered": sentinel_submit_flow_batch_ordered[_host], its verdicts put back at their arrival
-    positions through the returned seq -- a permutation of [0, n) -- before the comparison), and the
-    one-launch small-batch kernel over 4096-event chunks (the variable is read when an engine is
-    created)."""
-    monkeypatch.setenv("SENTINEL_FLOW_PATH", "partition" if request.param == "ordered" else request.param)
-    if request.param == "ordered":
+    positions through the returned seq -- a permutation of [0, n) -- before the comparison; "ordered-sorted":
+    the same output from the radix-sort path), and the one-launch small-batch kernel over 4096-event chunks
+    (the variable is read when an engine is created)."""
+    path = {"ordered": "partition", "ordered-sorted": "sorted"}.get(request.param, request.param)
+    monkeypatch.setenv("SENTINEL_FLOW_PATH", path)
+    if request.param.startswith("ordered"):
         from sentinel_amd.token_service import GpuTokenService
 
         def host(self, flow_idx, acquire, ts, flags=None):
