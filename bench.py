@@ -294,25 +294,12 @@ class FlowWorkload:
         else:
             self.svc.submit_flow_batch(b, verdicts=self.verdicts)
 
-    def _arrival(self, k):
-        """A kept batch's verdicts at their arrival positions (decide-order output put back by its seq,
-        after the fact: only for the parity check)."""
-        if not isinstance(k, tuple):
-            return k
-        v, sq = k
-        s = sq.to(self.torch.int64)
-        assert self.torch.equal(self.torch.sort(s).values, self.torch.arange(len(s), device=s.device)), \
-            "decide-order seq is not a permutation"
-        out = self.torch.empty_like(v)
-        out[s] = v
-        return out
-
     def parity(self, st, rem, wait):
         """The kept batches' GPU verdicts against the oracle replay of the same events (first batches)."""
         from sentinel_amd.token_service import decode_verdicts
         if not self.kept:
             return None
-        g = [decode_verdicts(self._arrival(v)) for v in self.kept]
+        g = [decode_verdicts(arrival_order(self.torch, v)) for v in self.kept]
         gs, gr, gw = (np.concatenate([x[i] for x in g]) for i in range(3))
         m = min(len(gs), len(st))
         bad = int(((gs[:m] != st[:m]) | (gr[:m] != rem[:m]) | (gw[:m] != wait[:m])).sum())
@@ -433,12 +420,16 @@ class ParamWorkload:
         self.zipf_cdf = torch.from_numpy(np.cumsum(w) / w.sum()).to(dev)
         self.fid_dev = torch.from_numpy(self.flow_id.astype(np.int64)).to(dev)
         self.verdicts = torch.empty(self.N, dtype=torch.int64, device=dev)
+        self.seq = torch.empty(self.N, dtype=torch.int32, device=dev)
+        self.ordered = args.output == "decide"
         self.kept = []
         self.parity_result = None
         self.workload = (f"config4: {self.R_total} hot-parameter cluster rules (count~U{{5..100}}, hot items), values "
                          f"Zipf(1.2) over 1000 Long keys per resource, n={n} w={self.interval // n}ms, acquire 1, "
                          f"{self.N}-event batches, " + (f"shared count-min sketch d={self.cm_depth} w=2^20"
-                                                        if self.cm else "exact per-value counters"))
+                                                        if self.cm else "exact per-value counters")
+                         + ("; verdicts in decide order with their arrival positions (sentinel_submit_param_batch_"
+                            "ordered, what the wire server's PARAM path consumes)" if self.ordered else ""))
 
     def batch(self, s):
         torch, N = self.torch, self.N
@@ -457,8 +448,15 @@ class ParamWorkload:
     def submit(self, b, keep=False):
         if keep:
             v = self.torch.empty(self.N, dtype=self.torch.int64, device=self.dev)
-            self.svc.submit_param_batch(b, verdicts=v)
-            self.kept.append(v)
+            if self.ordered:
+                sq = self.torch.empty(self.N, dtype=self.torch.int32, device=self.dev)
+                self.svc.submit_param_batch_ordered(b, verdicts=v, seq=sq)
+                self.kept.append((v, sq))
+            else:
+                self.svc.submit_param_batch(b, verdicts=v)
+                self.kept.append(v)
+        elif self.ordered:
+            self.svc.submit_param_batch_ordered(b, verdicts=self.verdicts, seq=self.seq)
         else:
             self.svc.submit_param_batch(b, verdicts=self.verdicts)
 
@@ -484,7 +482,7 @@ class ParamWorkload:
         cdt = time.perf_counter() - c0
         if self.kept and not self.cm:
             from sentinel_amd.token_service import decode_verdicts
-            g = [decode_verdicts(v) for v in self.kept]
+            g = [decode_verdicts(arrival_order(self.torch, v)) for v in self.kept]
             gs, gr = np.concatenate([x[0] for x in g]), np.concatenate([x[1] for x in g])
             m = min(len(gs), len(st))
             self.parity_result = {
@@ -502,7 +500,7 @@ class ParamWorkload:
         violations (sketch passed, exact would block) must be 0; false blocks are the price of the sketch."""
         ridx, acq, keys, ts = self._host(batches, k)
         from sentinel_amd.token_service import decode_verdicts
-        st = np.concatenate([decode_verdicts(v)[0] for v in svc_verdicts]).astype(np.int8)
+        st = np.concatenate([decode_verdicts(arrival_order(self.torch, v))[0] for v in svc_verdicts]).astype(np.int8)
         orc = self._oracle()
         ones = np.ones(len(ts), np.int32)
         viol, fb, dec = orc.param_cm_audit(ridx, acq, ts, np.arange(len(ts), dtype=np.int32), ones, keys, st)
@@ -525,7 +523,7 @@ class ParamWorkload:
             while 1024 * nsub * 1024 < self.N and nsub < 256:
                 nsub *= 2
             e_k = self.N / max(1, self._dk) if hasattr(self, "_dk") else 1.0
-            return 8.0 * nsub + 20.0 + 16.0 / e_k
+            return 8.0 * nsub + 20.0 + 16.0 / e_k + (4.0 if self.ordered else 0.0)   # (+ seq in decide order)
         if dom == "param_decide":
             # per request: read the 8-B grouped value, write the 8-B verdict; per distinct (rule, value)
             # key: its 16-B record, the slot probe 8, its n {epoch, count} pairs read (16 n) and the
@@ -564,7 +562,8 @@ class ParamWorkload:
         return 24.0 + 8.0 + (self.n * 16 * 2 + 16) / 4.0
 
     def shape(self):
-        return {"config": self.args.config, "rules": self.R, "events": self.N, "sample_count": self.n}
+        return {"config": self.args.config, "rules": self.R, "events": self.N, "sample_count": self.n,
+                "output": "decide order + arrival positions" if self.ordered else "arrival order"}
 
 
 class ConcWorkload:
@@ -697,6 +696,19 @@ class ConcWorkload:
 
 
 CM_AUDIT_BATCHES = 6    # consecutive 4cm batches audited on exact counters (each spans ~80 epochs of 100 ms)
+
+
+def arrival_order(torch, k):
+    """A kept batch's verdicts at their arrival positions: decide-order output (verdicts, seq) is put
+    back through its seq after the fact (the parity check and the count-min audit only)."""
+    if not isinstance(k, tuple):
+        return k
+    v, sq = k
+    s = sq.to(torch.int64)
+    assert torch.equal(torch.sort(s).values, torch.arange(len(s), device=s.device)), "decide-order seq is not a permutation"
+    out = torch.empty_like(v)
+    out[s] = v
+    return out
 
 
 def main():

@@ -215,6 +215,15 @@ int  sentinel_submit_param_batch(sentinel_engine_t *eng, int64_t n, const sentin
                                  sentinel_verdict_t *verdicts, void *stream);
 int  sentinel_submit_param_batch_host(sentinel_engine_t *eng, int64_t n, const sentinel_param_event_t *events,
                                       sentinel_verdict_t *verdicts);
+/* Decide-order output for single-value requestParamToken batches (TokenService.java:46), as
+ * sentinel_submit_flow_batch_ordered: verdicts[j] answers the request at arrival position seq[j].  The
+ * partition-local key walks (exact slots and the shared count-min sketch) write each (rule, value) key's
+ * verdicts at its grouped positions; other paths answer in arrival order with seq = identity.  The wire
+ * server's PARAM requests (TokenServerHandler.java:61-81, one response per xid) take it. */
+int  sentinel_submit_param_batch_ordered(sentinel_engine_t *eng, int64_t n, const sentinel_param_event_t *events,
+                                         sentinel_verdict_t *verdicts, uint32_t *seq, void *stream);
+int  sentinel_submit_param_batch_ordered_host(sentinel_engine_t *eng, int64_t n, const sentinel_param_event_t *events,
+                                              sentinel_verdict_t *verdicts, uint32_t *seq);
 
 /* ---- hot-parameter requests beyond one value, count-min mode, local token bucket ---- */
 

@@ -39,6 +39,7 @@ EXPORTS = [
     "sentinel_submit_flow_batch", "sentinel_submit_flow_batch_host", "sentinel_submit_flow_stream_host",
     "sentinel_submit_flow_batch_ordered", "sentinel_submit_flow_batch_ordered_host",
     "sentinel_submit_param_batch", "sentinel_submit_param_batch_host",
+    "sentinel_submit_param_batch_ordered", "sentinel_submit_param_batch_ordered_host",
     "sentinel_request_token", "sentinel_request_param_token",
     "sentinel_synchronize", "sentinel_dump_flow", "sentinel_param_sum",
     "sentinel_snapshot", "sentinel_snapshot_device", "sentinel_engine_stream",
@@ -198,6 +199,8 @@ def load():
         "sentinel_submit_flow_stream_host": (C.c_int, [vp, i64, vp, vp, vp, i64, vp]),
         "sentinel_submit_param_batch": (C.c_int, [vp, i64, vp, vp, vp]),
         "sentinel_submit_param_batch_host": (C.c_int, [vp, i64, vp, vp]),
+        "sentinel_submit_param_batch_ordered": (C.c_int, [vp, i64, vp, vp, vp, vp]),
+        "sentinel_submit_param_batch_ordered_host": (C.c_int, [vp, i64, vp, vp, vp]),
         "sentinel_request_token": (C.c_int, [vp, i64, i32, i32, i64, vp]),
         "sentinel_request_param_token": (C.c_int, [vp, i64, i32, u64, i64, vp]),
         "sentinel_synchronize": (C.c_int, [vp]),

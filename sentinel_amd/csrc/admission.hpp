@@ -192,6 +192,27 @@ struct Verdicts {
     }
 };
 
+// Decide-order output (Verdicts::oseq): a request decided by validation (rej) goes to position n - 1 - its
+// rank among the batch's rejected requests, counted in *ctr with one atomic per wave -- the pipeline's
+// sorted / grouped requests fill [0, valid), so the rejected ones fill [valid, n) -- with its arrival
+// position in oseq.  Called by every lane of the wave that reached the item (divergent lanes are fine:
+// the ballot sees the active ones).
+__device__ inline void put_rejected_ordered(bool rej, uint64_t *out, uint32_t *oseq, uint32_t *ctr, int64_t n,
+                                            uint32_t seq, int st) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(rej);
+    if (!m) return;
+    const uint32_t lane = lane_id();
+    const int lead = __ffsll((unsigned long long)m) - 1;
+    uint32_t b = 0;
+    if ((int)lane == lead) b = atomicAdd(ctr, (uint32_t)__popcll(m));
+    b = __shfl(b, lead, WAVE);
+    if (rej) {
+        const uint32_t pos = (uint32_t)(n - 1) - (b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull)));
+        put_verdict(out, pos, st, 0, 0);
+        oseq[pos] = seq;
+    }
+}
+
 // A key's state: header pair j {epoch, PASS} at base + hs*j (hs = 2: contiguous record;
 // hs = 2*HB_KEYS: the flow table's blocked slot-major header region); the other six counters of
 // slot j (BLOCK .. WAITING) at rbase + rs*j + rcs*c (rs = 8, rcs = 1: a contiguous rest line;

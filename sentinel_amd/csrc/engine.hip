@@ -183,22 +183,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_flow_prep(
             tile_hist_accumulate(hl, l, lpasses);
         }
         if (st != 127 && !oseq) put_verdict(out, (uint32_t)i, st, 0, 0);
-        if (oseq) {                                  // (one counter atomic per wave)
-            const bool rej = st != 127;
-            const uint64_t m = __builtin_amdgcn_ballot_w64(rej);
-            if (m) {
-                const uint32_t lane = lane_id();
-                const int lead = __ffsll((unsigned long long)m) - 1;
-                uint32_t b = 0;
-                if ((int)lane == lead) b = atomicAdd(&octr[opar], (uint32_t)__popcll(m));
-                b = __shfl(b, lead, WAVE);
-                if (rej) {
-                    const uint32_t pos = (uint32_t)(n - 1) - (b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull)));
-                    put_verdict(out, pos, st, 0, 0);
-                    oseq[pos] = (uint32_t)i;
-                }
-            }
-        }
+        if (oseq) put_rejected_ordered(st != 127, out, oseq, &octr[opar], n, (uint32_t)i, st);
     }
     __syncthreads();
     tile_hist_store(hf, fhist, fpasses, nblocks);
@@ -2015,7 +2000,9 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
 // Single-value exact requests without namespace limiters: the partition-local path (param_part.hpp):
 // prep + range histogram, the partition scan, the stable multi-split by key hash, then one workgroup
 // per range deciding its distinct keys from an LDS-staged table.
-static int submit_param_part(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, uint64_t *out, hipStream_t s) {
+static int submit_param_part(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, uint64_t *out, hipStream_t s,
+                             uint32_t *oseq = nullptr) {
+    if (oseq && ensure_octr(e, s)) return SENTINEL_E_NOMEM;
     const int32_t R = (int32_t)e->prules.size();
     const bool have = R > 0 && e->d_ptable.p;
     int pbits = 0;                                        // ranges of ~PD_TARGET requests, <= PART_BINS
@@ -2032,8 +2019,10 @@ static int submit_param_part(sentinel_engine_t *e, int64_t n, const ParamEvent *
     const int32_t *route = e->param_plain ? nullptr : e->d_prule_route.as<int32_t>();
     e->launch("param_prep", n, s, [&] {
         k_pp_prep<<<dim3((unsigned)nb), dim3(PP_THREADS), 0, s>>>(n, ev, have ? R : 0, route, e->param_ctx().R, out,
-                                                                  pbits, hist, P, e->w_counters.as<uint32_t>(), nullptr);
+                                                                  pbits, hist, P, e->w_counters.as<uint32_t>(), nullptr,
+                                                                  oseq, oseq ? e->d_octr.as<uint32_t>() : nullptr, e->opar);
     });
+    if (oseq) e->opar ^= 1u;                              // (the next decide-order batch's counter, zeroed by this prep)
     if (!have) {
         HIP_OK(hipGetLastError());
         return 0;
@@ -2068,8 +2057,9 @@ static int submit_param_part(sentinel_engine_t *e, int64_t n, const ParamEvent *
     while (sbits < 8 && (int64_t)P * ((int64_t)1 << sbits) * PG_TARGET < n) ++sbits;
     const unsigned ggrid = (unsigned)(((P + 7) / 8) * 8 * (1 << sbits));
     uint64_t *gval = e->w_hep.as<uint64_t>();
-    const PKeyRecs RC{e->w_segep.as<unsigned long long>(), e->w_s0.as<uint2>(), e->w_k.as<int32_t>(),
-                      e->w_counters.as<uint32_t>(), nullptr};
+    PKeyRecs RC{e->w_segep.as<unsigned long long>(), e->w_s0.as<uint2>(), e->w_k.as<int32_t>(),
+                e->w_counters.as<uint32_t>(), nullptr};
+    RC.oseq = oseq;
     const int hb = header_block_slots(e->pmax_n);
     e->launch("param_group", n, s, [&] {
         if (hb <= 2) k_pp_group<2><<<ggrid, PD_THREADS, 0, s>>>(pkey, pval, prule, rstart, P, pbits, sbits, ev, PR, RR, S, out, fresh, gval, RC);
@@ -2100,9 +2090,11 @@ static int submit_param_part(sentinel_engine_t *e, int64_t n, const ParamEvent *
 // synchronisation reads whether every sub-range fit one chunk; a batch with a sub-range over PG_CAP
 // requests (heavy skew: a key split over chunks) is decided by the per-rule lanes (submit_prules),
 // which answer the invalid requests the same way.  Returns 1 = fall back.
-static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, uint64_t *out, hipStream_t s) {
+static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, uint64_t *out, hipStream_t s,
+                                uint32_t *oseq = nullptr) {
     const int32_t R = (int32_t)e->prules.size();
     if (R == 0 || !e->d_cmband.p) return 1;
+    if (oseq && ensure_octr(e, s)) return SENTINEL_E_NOMEM;
     int pbits = 0;
     while (pbits < PART_MAX_BITS && ((int64_t)2 << pbits) * PD_TARGET <= n) ++pbits;
     const int32_t P = 1 << pbits;
@@ -2125,8 +2117,10 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
     k_cm_batch_init<<<1, 64, 0, s>>>(flag, tspan, ctl);
     e->launch("param_prep", n, s, [&] {
         k_pp_prep<<<dim3((unsigned)nb), dim3(PP_THREADS), 0, s>>>(n, ev, R, route, C.R, out, pbits, hist, P,
-                                                                  e->w_counters.as<uint32_t>(), tspan);
+                                                                  e->w_counters.as<uint32_t>(), tspan, oseq,
+                                                                  oseq ? e->d_octr.as<uint32_t>() : nullptr, e->opar);
     });
+    if (oseq) e->opar ^= 1u;                              // (the next decide-order batch's counter, zeroed by this prep)
     e->launch("scan", n, s, [&] {
         const dim3 g2((unsigned)ng, (unsigned)((P + PS_THREADS - 1) / PS_THREADS));
         k_part_colsum<<<g2, PS_THREADS, 0, s>>>(hist, nb, P, gsum);
@@ -2171,6 +2165,7 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
     if (use_block && e->w_cmsub.ensure(((size_t)P << sbits) * sizeof(uint2))) return SENTINEL_E_NOMEM;
     PKeyRecs RC{e->w_segep.as<unsigned long long>(), e->w_s0.as<uint2>(), e->w_k.as<int32_t>(),
                 e->w_counters.as<uint32_t>(), flag};
+    RC.oseq = oseq;
     if (use_block) RC.sub = e->w_cmsub.as<uint2>();
     const PSlots S{};
     e->launch("param_group", n, s, [&] {
@@ -2234,13 +2229,19 @@ static int submit_param_cm_part(sentinel_engine_t *e, int64_t n, const ParamEven
     return 0;
 }
 
-static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, uint64_t *out, hipStream_t s) {
+// oseq (decide-order output): the key walks write grouped positions + arrival positions (ord_done =
+// true); every other path writes arrival order and the caller makes oseq the identity.
+static int submit_param_impl(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, uint64_t *out, hipStream_t s,
+                             uint32_t *oseq, bool &ord_done) {
     if (e->pmode == SENTINEL_PARAM_COUNT_MIN_SHARED && e->cm_keys && n > 0 && n <= MAX_BATCH && e->pmax_n <= 16 &&
         !(e->nlimiters > 0 && !e->param_plain)) {
         int rc = e->ensure_ws(n);
         if (rc) return rc;
-        rc = submit_param_cm_part(e, n, ev, out, s);
-        if (rc != 1) return rc;
+        rc = submit_param_cm_part(e, n, ev, out, s, oseq);
+        if (rc != 1) {
+            ord_done = oseq != nullptr;
+            return rc;
+        }
     }
     if (e->pmode != SENTINEL_PARAM_EXACT) return submit_prules(e, PMODE_CM, n, ev, nullptr, nullptr, 0, out, s);
     // per-rule walk (sort by rule, one lane per rule, each request rolls and sums its value's slot): for
@@ -2258,7 +2259,10 @@ static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, u
         if (rc) return rc;
     }
     const bool plim = e->nlimiters > 0 && !e->param_plain && R > 0;
-    if (e->param_path == 0 && !plim && e->pmax_n <= 16) return submit_param_part(e, n, ev, out, s);
+    if (e->param_path == 0 && !plim && e->pmax_n <= 16) {
+        ord_done = oseq != nullptr;
+        return submit_param_part(e, n, ev, out, s, oseq);
+    }
     e->pexp_valid = false;                                // (the segment pipeline does not keep the hints)
     const uint64_t P = e->pcap;
     const int pbits = bits_for((int64_t)P);
@@ -2300,6 +2304,16 @@ static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, u
     KeyTable PT = e->table(e->pt, 1, param_stride(e->pmax_n));
     EventSrc src{nullptr, ev, nullptr, false};
     e->run_pipeline(PT, fkey, e->w_fhist.as<uint32_t>(), n, pbits, src, V, s, e->pmax_n, false, false, false, true);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, uint64_t *out, hipStream_t s,
+                        uint32_t *oseq = nullptr) {
+    bool ord_done = false;
+    const int rc = submit_param_impl(e, n, ev, out, s, oseq, ord_done);
+    if (rc || !oseq || ord_done || n <= 0) return rc;
+    k_iota_u32<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(oseq, n);
     HIP_OK(hipGetLastError());
     return 0;
 }
@@ -3454,7 +3468,7 @@ int sentinel_submit_param_batch(sentinel_engine_t *e, int64_t n, const sentinel_
 }
 
 static int submit_param_host_locked(sentinel_engine_t *e, int64_t n, const sentinel_param_event_t *ev,
-                                    sentinel_verdict_t *out);
+                                    sentinel_verdict_t *out, uint32_t *out_seq = nullptr);
 
 int sentinel_submit_param_batch_host(sentinel_engine_t *e, int64_t n, const sentinel_param_event_t *ev,
                                      sentinel_verdict_t *out) {
@@ -3465,19 +3479,43 @@ int sentinel_submit_param_batch_host(sentinel_engine_t *e, int64_t n, const sent
 }
 
 static int submit_param_host_locked(sentinel_engine_t *e, int64_t n, const sentinel_param_event_t *ev,
-                                    sentinel_verdict_t *out) {
+                                    sentinel_verdict_t *out, uint32_t *out_seq) {
     HIP_OK(hipSetDevice(e->device));
     hipStream_t s = e->stream;
     int rc = 0;
     rc |= e->io_ev.ensure(n * sizeof(ParamEvent));
-    rc |= e->io_out.ensure(n * 8);
+    rc |= e->io_out.ensure(n * 12 + 16);
     if (rc) return SENTINEL_E_NOMEM;
+    uint64_t *dout = e->io_out.as<uint64_t>();
+    uint32_t *dseq = out_seq ? reinterpret_cast<uint32_t *>(dout + n) : nullptr;
     HIP_OK(hipMemcpyAsync(e->io_ev.p, ev, n * sizeof(ParamEvent), hipMemcpyHostToDevice, s));
-    rc = submit_param(e, n, e->io_ev.as<ParamEvent>(), e->io_out.as<uint64_t>(), s);
+    rc = submit_param(e, n, e->io_ev.as<ParamEvent>(), dout, s, dseq);
     if (rc) return rc;
-    HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 8, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, s));
+    if (out_seq) HIP_OK(hipMemcpyAsync(out_seq, dseq, n * 4, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     return 0;
+}
+
+// Decide-order output for single-value param requests (include/sentinel_amd.h): the key walks write each
+// request's verdict at its grouped position (the requests of one (rule, value) key are contiguous) and
+// its arrival position next to it; other paths answer in arrival order with seq = identity.
+int sentinel_submit_param_batch_ordered(sentinel_engine_t *e, int64_t n, const sentinel_param_event_t *ev,
+                                        sentinel_verdict_t *out, uint32_t *out_seq, void *stream) {
+    if (!e || n < 0 || (n > 0 && (!ev || !out || !out_seq))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIP_OK(hipSetDevice(e->device));
+    hipStream_t fs_s = stream ? (hipStream_t)stream : e->stream;
+    const ForeignStream fs_(e, fs_s);
+    return submit_param(e, n, (const ParamEvent *)ev, (uint64_t *)out, fs_s, out_seq);
+}
+
+int sentinel_submit_param_batch_ordered_host(sentinel_engine_t *e, int64_t n, const sentinel_param_event_t *ev,
+                                             sentinel_verdict_t *out, uint32_t *out_seq) {
+    if (!e || n < 0 || (n > 0 && (!ev || !out || !out_seq))) return fail(SENTINEL_E_INVALID, "bad arguments");
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> g(e->mu);
+    return submit_param_host_locked(e, n, ev, out, out_seq);
 }
 
 int sentinel_submit_param_multi_batch(sentinel_engine_t *e, int64_t n, const sentinel_param_multi_event_t *ev,

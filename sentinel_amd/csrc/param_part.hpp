@@ -125,10 +125,14 @@ __global__ __launch_bounds__(PP_THREADS) void k_pp_prep(int64_t n, const ParamEv
                                                          uint64_t *__restrict__ out, int pbits,
                                                          uint32_t *__restrict__ hist, int32_t nparts,
                                                          uint32_t *__restrict__ zero_word,
-                                                         unsigned long long *__restrict__ tspan) {
+                                                         unsigned long long *__restrict__ tspan,
+                                                         uint32_t *__restrict__ oseq = nullptr,
+                                                         uint32_t *__restrict__ octr = nullptr, uint32_t opar = 0) {
+    // oseq: decide-order output -- rejected requests placed from the end (put_rejected_ordered)
     __shared__ uint32_t h[PART_BINS];
     __shared__ unsigned long long s_span[2];
     if (blockIdx.x == 0 && threadIdx.x == 0 && zero_word) *zero_word = 0;   // the batch's key-record count
+    if (blockIdx.x == 0 && threadIdx.x == 0 && octr) octr[opar ^ 1u] = 0;
     if (threadIdx.x == 0) { s_span[0] = ~0ull; s_span[1] = ~0ull; }
     unsigned long long tmin = ~0ull, tnmax = ~0ull;    // this thread's valid requests: min ts, min ~ts
     const int64_t tile0 = (int64_t)blockIdx.x * PT_TILE;
@@ -150,9 +154,10 @@ __global__ __launch_bounds__(PP_THREADS) void k_pp_prep(int64_t n, const ParamEv
             atomicAdd(&h[pp_digit(mix64(evs[j].key), pbits)], 1u);
             tmin = min(tmin, (unsigned long long)evs[j].ts);                // ts >= 0 here
             tnmax = min(tnmax, ~(unsigned long long)evs[j].ts);
-        } else {
+        } else if (!oseq) {
             put_verdict(out, (uint32_t)i, st, 0, 0);
         }
+        if (oseq) put_rejected_ordered(st != 127, out, oseq, &octr[opar], n, (uint32_t)i, st);
     }
     if (tspan) {                                          // (block-uniform) the batch's ts range
 #pragma unroll
@@ -356,7 +361,8 @@ __global__ __launch_bounds__(256) void k_prule_pack(int32_t R, ParamRules PR, co
 template <int NMAX>
 __device__ inline void pd_walk(const ParamRules &PR, const PRuleRec *RR, const PSlots &S, unsigned long long key,
                                int32_t rule, const uint64_t *sv, uint32_t q0, uint32_t q1, const ParamEvent *ev,
-                               int64_t T0, uint64_t *out, uint32_t &nfresh) {
+                               int64_t T0, uint64_t *out, uint32_t &nfresh, bool ord = false, uint32_t pbase = 0) {
+    // (ord: decide-order output, the verdict of sv[q] at out[pbase + q]; else at its arrival position)
     const PRuleRec rr = RR[rule];
     const int nsc = rr.nf & 0xFFFF;
     const int32_t w = rr.w;
@@ -366,7 +372,7 @@ __device__ inline void pd_walk(const ParamRules &PR, const PRuleRec *RR, const P
     const uint32_t before = nfresh;
     const int64_t h = slot_insert_counted(S.keys, S.mask, key, nfresh);
     if (h < 0) {                                                         // table full: param_reserve prevents it
-        for (uint32_t q = q0; q < q1; ++q) put_verdict(out, (uint32_t)sv[q] & SEQ_MASK, ST_FAIL, 0, 0);
+        for (uint32_t q = q0; q < q1; ++q) put_verdict(out, ord ? pbase + q : (uint32_t)sv[q] & SEQ_MASK, ST_FAIL, 0, 0);
         return;
     }
     const bool fresh = nfresh != before;
@@ -428,7 +434,7 @@ __device__ inline void pd_walk(const ParamRules &PR, const PRuleRec *RR, const P
         } else {
             vd = pack_verdict(ST_BLOCKED, 0, 0);
         }
-        store_verdict(out, (uint32_t)v & SEQ_MASK, vd);
+        store_verdict(out, ord ? pbase + q : (uint32_t)v & SEQ_MASK, vd);
     }
 #pragma unroll
     for (int j = 0; j < NMAX; ++j)
@@ -465,6 +471,10 @@ struct PKeyRecs {
     // shared count-min block walk (k_pp_cm_block): non-null = each sub-range's records are written at
     // their sub-range's first grouped-value position, sub[(range << sbits) | sub-range] = {first, count}
     uint2 *sub = nullptr;
+    // decide-order output (sentinel_submit_param_batch_ordered): the verdict of the request at grouped
+    // position q goes to out[q] and its arrival position to oseq[q] (written by k_pp_group with the
+    // grouped values); null: out[arrival position]
+    uint32_t *oseq = nullptr;
 };
 
 // k_pp_group: one workgroup per (range, sub-range): the S = 2^sbits workgroups of a range read the
@@ -515,6 +525,8 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
     uint32_t m = 0;                                                      // compacted requests (block-uniform)
     uint32_t kemit = 0;                                                  // records emitted (block-uniform)
     uint32_t kbase = 0;
+    uint32_t sbase = 0, soff = 0;                                        // decide order, slow sub-range: its first
+                                                                         // position, requests decided so far
     PF_STAMP(0);
 
     // decide / emit cq[0, m): rounds while the LDS table is full for some key
@@ -614,7 +626,10 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
             __syncthreads();
             [[maybe_unused]] const unsigned long long pt2 = PD_NOW();
             if (emit) {
-                for (uint32_t i = t; i < placed; i += PD_THREADS) gval[gbase + roff + i] = sv[i];
+                for (uint32_t i = t; i < placed; i += PD_THREADS) {
+                    gval[gbase + roff + i] = sv[i];
+                    if (RC.oseq) RC.oseq[gbase + roff + i] = (uint32_t)sv[i] & SEQ_MASK;   // (decide order)
+                }
                 const uint32_t rb = RC.sub ? gbase + kemit : s_rbase;      // (records <= requests: inside the run)
                 kbase = gbase;
                 for (uint32_t q = t; q < nkeys; q += PD_THREADS) {
@@ -624,10 +639,14 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
                     RC.rule[rb + q] = hrule[e];
                 }
             } else if constexpr (!CM) {
+                // (decide order: this round's requests own positions gbase + roff + [0, placed))
+                if (RC.oseq)
+                    for (uint32_t i = t; i < placed; i += PD_THREADS) RC.oseq[gbase + roff + i] = (uint32_t)sv[i] & SEQ_MASK;
 #pragma unroll 1
                 for (uint32_t q = t; q < nkeys; q += PD_THREADS) {
                     const uint32_t e = klist[q];
-                    pd_walk<NMAX>(PR, RR, S, hkey[e], hrule[e], sv, hstart[e], hstart[e + 1], ev, T0, out, nfresh);
+                    pd_walk<NMAX>(PR, RR, S, hkey[e], hrule[e], sv, hstart[e], hstart[e + 1], ev, T0, out, nfresh,
+                                  RC.oseq != nullptr, gbase + roff);
                 }
             }
             roff += placed;
@@ -674,8 +693,20 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
                 if (t == 0) atomicOr(RC.overflow, 1ull);              // falls back to the per-rule lanes
                 return;
             }
+            if (RC.oseq && !slow) {
+                // decide-order output: the sub-range owns grouped positions r0 + (the range's requests of
+                // lower sub-ranges) + [0, its size) -- `below` covers the tiles up to this one, the rest of
+                // the range is counted here (only a sub-range over one chunk pays this second read)
+                uint32_t rest = 0;
+                for (uint32_t qq = q0 + PD_THREADS * 4 + t; qq < r1; qq += PD_THREADS)
+                    rest += pp_sub(mix64(pkey[qq]), pbits, sbits) < sub;
+                uint32_t tot;
+                (void)block_exclusive_scan(below + rest, waves_tot, &tot);
+                sbase = r0 + tot;
+            }
             slow = true;
-            chunk(false, 0);
+            chunk(false, sbase + soff);
+            soff += m;
             m = 0;
         }
         uint32_t w = m + off;
@@ -687,7 +718,7 @@ __global__ __launch_bounds__(PD_THREADS) void k_pp_group(const unsigned long lon
     }
     if (m) {
         if (slow) {
-            chunk(false, 0);
+            chunk(false, sbase + soff);
         } else {
             uint32_t nb;
             const uint32_t base = block_exclusive_scan(below, waves_tot, &nb);   // (only the total is used)
@@ -732,7 +763,8 @@ __global__ __launch_bounds__(256) void k_pp_walk(PKeyRecs RC, const uint64_t *__
     uint32_t nfresh = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nrec; i += gridDim.x * blockDim.x) {
         const uint2 run = RC.run[i];
-        pd_walk<NMAX>(PR, RR, S, RC.key[i], RC.rule[i], gval, run.x, run.x + run.y, ev, T0, out, nfresh);
+        pd_walk<NMAX>(PR, RR, S, RC.key[i], RC.rule[i], gval, run.x, run.x + run.y, ev, T0, out, nfresh,
+                      RC.oseq != nullptr, 0);
     }
     block_add_global(fresh, nfresh, &s_fresh);
 }
@@ -969,7 +1001,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_walk(PKeyRecs RC, const uint64_t 
             } else {
                 vd = pack_verdict(ST_BLOCKED, 0, 0);
             }
-            store_verdict(out, (uint32_t)v & SEQ_MASK, vd);
+            store_verdict(out, RC.oseq ? q : (uint32_t)v & SEQ_MASK, vd);
         }
 #pragma unroll
         for (int j = 0; j < NMAX; ++j)
@@ -1394,7 +1426,7 @@ __global__ __launch_bounds__(256) void k_pp_cm_block(PKeyRecs RC, int sb, uint64
             } else {
                 vd = pack_verdict(ST_BLOCKED, 0, 0);
             }
-            if (!(diag & 32)) store_verdict(out, (uint32_t)v & SEQ_MASK, vd);
+            if (!(diag & 32)) store_verdict(out, RC.oseq ? K.run.x + k : (uint32_t)v & SEQ_MASK, vd);
         }
         if (cnt > 0 && curE > Edead && !(diag & 16)) cm_lds_flush(cl, dirty, K.co, depth, nmax, rcp_nmax, curE, Eref, cnt);
     };

@@ -98,22 +98,7 @@ __global__ __launch_bounds__(PP_THREADS) void k_part_prep(int64_t n, const Event
         if (fkey) fkey[i] = k;
         if (st == 127) atomicAdd(&h[k >> lb], 1u);
         else if (!oseq) put_verdict(out, (uint32_t)i, st, 0, 0);
-        if (oseq) {                                  // (one counter atomic per wave)
-            const bool rej = st != 127;
-            const uint64_t m = __builtin_amdgcn_ballot_w64(rej);
-            if (m) {
-                const uint32_t lane = lane_id();
-                const int lead = __ffsll((unsigned long long)m) - 1;
-                uint32_t b = 0;
-                if ((int)lane == lead) b = atomicAdd(&octr[opar], (uint32_t)__popcll(m));
-                b = __shfl(b, lead, WAVE);
-                if (rej) {
-                    const uint32_t pos = (uint32_t)(n - 1) - (b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull)));
-                    put_verdict(out, pos, st, 0, 0);
-                    oseq[pos] = (uint32_t)i;
-                }
-            }
-        }
+        if (oseq) put_rejected_ordered(st != 127, out, oseq, &octr[opar], n, (uint32_t)i, st);
     }
     __syncthreads();
     // tile-major: this tile's 4 KB row is one contiguous store

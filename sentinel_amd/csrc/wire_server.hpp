@@ -601,11 +601,30 @@ inline bool sentinel_wire_server::on_readable(wire::Loop &L, wire::Conn *c) {
         // a flowId without a rule keeps its decode-time lookup: SENTINEL_IDX_BAD_ID for flowId <= 0 answers
         // BAD_REQUEST (DefaultTokenService.notValidRequest runs before the rule lookup), NO_RULE otherwise
         for (int64_t i = 0; i < n; ++i) B.pev[i].rule_idx = B.pnorule[i] < 0 ? B.pnorule[i] : idx[i];
-        if (!rc) rc = sentinel_submit_param_multi_batch_host(e, n, B.pev.data(), B.pvals.data(),
-                                                             (int64_t)B.pvals.size(), out.data());
-        for (int64_t i = 0; i < n; ++i)
-            response(direct, B.pxid[i], wire::MSG_PARAM, rc ? (int8_t)SENTINEL_STATUS_FAIL : (int8_t)out[i].status, 2,
-                     rc ? 0 : out[i].remaining, 0);
+        bool single = true;                                // every request one value: the single-value key walk
+        for (int64_t i = 0; i < n && single; ++i) single = B.pev[i].value_count == 1;
+        if (single) {
+            // decide-order output (sentinel_submit_param_batch_ordered_host): verdict j answers request
+            // seq[j]; each response carries its own xid (TokenServerHandler.java:61-81), so the read's
+            // responses go out in the order the engine decided them
+            std::vector<sentinel_param_event_t> sev(n);
+            std::vector<uint32_t> seq(n);
+            for (int64_t i = 0; i < n; ++i)
+                sev[i] = sentinel_param_event_t{B.pev[i].rule_idx, B.pev[i].acquire, B.pev[i].ts,
+                                                B.pvals[(size_t)B.pev[i].value_begin]};
+            if (!rc) rc = sentinel_submit_param_batch_ordered_host(e, n, sev.data(), out.data(), seq.data());
+            for (int64_t j = 0; j < n; ++j) {
+                const int64_t i = rc ? j : (int64_t)seq[j];
+                response(direct, B.pxid[i], wire::MSG_PARAM, rc ? (int8_t)SENTINEL_STATUS_FAIL : (int8_t)out[j].status, 2,
+                         rc ? 0 : out[j].remaining, 0);
+            }
+        } else {
+            if (!rc) rc = sentinel_submit_param_multi_batch_host(e, n, B.pev.data(), B.pvals.data(),
+                                                                 (int64_t)B.pvals.size(), out.data());
+            for (int64_t i = 0; i < n; ++i)
+                response(direct, B.pxid[i], wire::MSG_PARAM, rc ? (int8_t)SENTINEL_STATUS_FAIL : (int8_t)out[i].status, 2,
+                         rc ? 0 : out[i].remaining, 0);
+        }
     }
     if (!direct.empty()) {
         std::lock_guard<std::mutex> g(c->wmu);

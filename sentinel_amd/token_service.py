@@ -460,6 +460,31 @@ class GpuTokenService:
         check(self._L.sentinel_submit_param_batch_host(self._h, len(ev), _p(ev), _p(out)), "submit_param_batch_host")
         return out["status"].astype(np.int8), out["remaining"].copy()
 
+    def submit_param_batch_ordered(self, events, verdicts=None, seq=None, stream=None):
+        """submit_param_batch with decide-order output (sentinel_submit_param_batch_ordered): returns
+        (verdicts, seq) device tensors; verdicts[j] answers the request at arrival position seq[j]."""
+        import torch
+        n = int(events.shape[0])
+        if verdicts is None:
+            verdicts = torch.empty(n, dtype=torch.int64, device=events.device)
+        if seq is None:
+            seq = torch.empty(n, dtype=torch.int32, device=events.device)
+        s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        check(self._L.sentinel_submit_param_batch_ordered(self._h, n, C.c_void_p(events.data_ptr()),
+                                                          C.c_void_p(verdicts.data_ptr()), C.c_void_p(seq.data_ptr()),
+                                                          None if s is None else C.c_void_p(s)),
+              "submit_param_batch_ordered")
+        return verdicts, seq
+
+    def submit_param_batch_ordered_host(self, rule_idx, acquire, param_key, ts):
+        """(status, remaining, seq) in decide order: entry j answers the request at arrival position seq[j]."""
+        ev = self.pack_param_events(rule_idx, acquire, param_key, ts)
+        out = np.empty(len(ev), dtype=_lib.VERDICT_DTYPE)
+        seq = np.empty(len(ev), dtype=np.uint32)
+        check(self._L.sentinel_submit_param_batch_ordered_host(self._h, len(ev), _p(ev), _p(out), _p(seq)),
+              "submit_param_batch_ordered_host")
+        return out["status"].astype(np.int8), out["remaining"].copy(), seq
+
     @staticmethod
     def pack_multi_events(rule_idx, acquire, ts, value_begin, value_count) -> np.ndarray:
         ev = np.empty(len(ts), dtype=_lib.MULTI_EVENT_DTYPE)

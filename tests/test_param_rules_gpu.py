@@ -172,7 +172,7 @@ def test_shared_count_min_is_one_sided(oracle_mod, monkeypatch, levels):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("block", ["0", "1", "1-c64"])
+@pytest.mark.parametrize("block", ["0", "1", "1-c64", "1-ordered"])
 def test_shared_count_min_full_size_audit(oracle_mod, monkeypatch, block):
     """BASELINE config 4's count-min mode at its own size: 100k hot-parameter rules, Zipf values over
     1000 per rule, 2M requests in 4 batches, the shared sketch at d = 4, w = 2^20 (bench config 4cm):
@@ -182,6 +182,9 @@ def test_shared_count_min_full_size_audit(oracle_mod, monkeypatch, block):
     import sentinel_amd as sa
     monkeypatch.setenv("SENTINEL_CM_BLOCK", block[0])
     monkeypatch.setenv("SENTINEL_CM_C32", "0" if block.endswith("c64") else "1")
+    if block.endswith("ordered"):                       # decide-order output, put back through its seq
+        from conftest import use_ordered_param_host
+        use_ordered_param_host(monkeypatch)
     count, hot, rule_idx, vals, keys, ts = T.config4(2_000_000, seed=61, n_rules=100_000, universe=1000)
     acq = np.ones(len(ts), np.int32)
     svc, orc = _cluster_pair(oracle_mod, count, hot, sample_count=lambda r: 10)
@@ -407,7 +410,8 @@ def _hot_key_batches(n_batches=3, n=30_000, hot_reqs=3000, seed=58):
     return count, hot, rule_idx, keys, ts
 
 
-def test_shared_count_min_subrange_over_chunk_falls_back(oracle_mod, monkeypatch):
+@pytest.mark.parametrize("output", ["arrival", "ordered"])
+def test_shared_count_min_subrange_over_chunk_falls_back(oracle_mod, monkeypatch, output):
     """A shared count-min batch with one key over PG_CAP requests: its key-hash sub-range cannot be grouped
     in one LDS chunk, so k_pp_group raises the overflow flag (no workgroup decides or emits anything for
     it) and the whole batch goes to the per-rule lanes -- the path that faulted while the key walk was
@@ -415,6 +419,9 @@ def test_shared_count_min_subrange_over_chunk_falls_back(oracle_mod, monkeypatch
     on exact counters replaying the sketch's own decisions: zero one-sidedness violations."""
     import sentinel_amd as sa
     monkeypatch.setenv("SENTINEL_CM_BLOCK", "1")
+    if output == "ordered":
+        from conftest import use_ordered_param_host
+        use_ordered_param_host(monkeypatch)
     count, hot, rule_idx, keys, ts = _hot_key_batches()
     svc, orc = _cluster_pair(oracle_mod, count, hot, sample_count=lambda r: 10)
     svc.set_param_mode(sa._lib.PARAM_COUNT_MIN_SHARED, depth=4, width=1 << 12)
@@ -433,9 +440,14 @@ def test_shared_count_min_subrange_over_chunk_falls_back(oracle_mod, monkeypatch
     assert (st[hk] == 0).any() and (st[hk] == 1).any()
 
 
-def test_exact_subrange_over_chunk_bitexact(oracle_mod):
+@pytest.mark.parametrize("output", ["arrival", "ordered"])
+def test_exact_subrange_over_chunk_bitexact(oracle_mod, monkeypatch, output):
     """The exact twin of the batches above: the hot key's sub-range is decided inside k_pp_group, chunk
-    after chunk in arrival order (the key walked once per chunk), bit for bit against the oracle."""
+    after chunk in arrival order (the key walked once per chunk), bit for bit against the oracle -- also
+    with decide-order output, where that sub-range's positions come from a second count of its range."""
+    if output == "ordered":
+        from conftest import use_ordered_param_host
+        use_ordered_param_host(monkeypatch)
     count, hot, rule_idx, keys, ts = _hot_key_batches()
     svc, orc = _cluster_pair(oracle_mod, count, hot, sample_count=lambda r: 10)
     acq = np.where(np.arange(len(ts)) % 7 == 0, 2, 1).astype(np.int32)

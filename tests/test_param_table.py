@@ -12,6 +12,16 @@ from sentinel_amd import trace as T
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["arrival", "ordered"])
+def param_output(request, monkeypatch):
+    """Every case with verdicts at their arrival positions and with decide-order output
+    (sentinel_submit_param_batch_ordered_host, put back through its seq)."""
+    if request.param == "ordered":
+        from conftest import use_ordered_param_host
+        use_ordered_param_host(monkeypatch)
+    return request.param
+
+
 def _svc(prules, capacity=None, monkeypatch=None):
     import sentinel_amd as sa
     from sentinel_amd.token_service import ServerNamespace
