@@ -601,6 +601,10 @@ class ConcWorkload:
         self.acq_pos_d = torch.from_numpy(self.acq_pos.astype(np.int64)).to(dev)
         self.rel_pos_d = torch.from_numpy(self.rel_pos.astype(np.int64)).to(dev)
         self.rel_src_d = torch.from_numpy(self.acq_pos[src].astype(np.int64)).to(dev)
+        # flat word indices of the same gather / scatter: token id = word 0 of a (N, 2) result row, word 1
+        # of a (N, 3) event row (two 1-D kernels instead of strided index_select / index_copy_)
+        self.rel_dst_w = self.rel_pos_d * 3 + 1
+        self.rel_src_w = self.rel_src_d * 2
         w = 1.0 / np.power(np.arange(1, self.F + 1, dtype=np.float64), 1.1)
         self.zipf_cdf = torch.from_numpy(np.cumsum(w) / w.sum()).to(dev)
         self.zipf_perm = torch.from_numpy(np.random.default_rng(9).permutation(self.F).astype(np.int32)).to(dev)
@@ -631,7 +635,7 @@ class ConcWorkload:
         prev, cur = self.results[self.k % 2], self.results[(self.k + 1) % 2]
         ext = torch.cuda.ExternalStream(self.svc.stream, device=self.dev)
         with torch.cuda.stream(ext):                       # the releases name the previous batch's tokens
-            b[:, 1].index_copy_(0, self.rel_pos_d, prev[:, 0].index_select(0, self.rel_src_d))
+            b.view(-1).index_copy_(0, self.rel_dst_w, prev.view(-1).index_select(0, self.rel_src_w))
         self.svc.submit_concurrent_batch(b, results=cur)
         self.verdicts = cur
         self.k += 1

@@ -498,7 +498,10 @@ template <bool FIRST>
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter_p(
     const uint32_t *__restrict__ keys_in, const uint64_t *__restrict__ vals_in, EventSrc src,
     uint32_t *__restrict__ keys_out, uint64_t *__restrict__ vals_out, int64_t n, int shift,
-    const uint32_t *__restrict__ offsets, int64_t nblocks) {
+    const uint32_t *__restrict__ offsets, int64_t nblocks, uint8_t *__restrict__ z0 = nullptr,
+    uint8_t *__restrict__ z1 = nullptr) {
+    // z0 / z1 (optional): byte arrays of n entries zeroed over this tile's positions -- the segment
+    // flags k_segments sets, cleared here instead of by two fill launches in front of it
     __shared__ uint32_t cnt[SORT_WAVES][RADIX];
     __shared__ uint32_t goff[RADIX];
     __shared__ uint32_t loff[RADIX];
@@ -516,6 +519,18 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter_p(
     const int64_t tile0 = (int64_t)blockIdx.x * SORT_TILE;
     const int64_t base = tile0 + (int64_t)wave * (SORT_ITEMS * WAVE);
     const int64_t T0 = FIRST ? src.t0() : 0;
+    if (z0) {
+        const int64_t end = n - tile0 < SORT_TILE ? n : tile0 + SORT_TILE;
+        const int64_t wend = tile0 + ((end - tile0) & ~(int64_t)3);   // whole words inside [tile0, end)
+        for (int64_t q = tile0 + 4 * (int64_t)threadIdx.x; q < wend; q += 4 * SORT_THREADS) {
+            *reinterpret_cast<uint32_t *>(z0 + q) = 0u;
+            *reinterpret_cast<uint32_t *>(z1 + q) = 0u;
+        }
+        if ((int64_t)threadIdx.x < end - wend) {
+            z0[wend + threadIdx.x] = 0;
+            z1[wend + threadIdx.x] = 0;
+        }
+    }
     uint32_t key[SORT_ITEMS], rank[SORT_ITEMS];
 #pragma unroll
     for (int j = 0; j < SORT_ITEMS; ++j) {
@@ -632,27 +647,24 @@ __global__ __launch_bounds__(256) void k_seg_heads(KeyTable T, BatchWork W, Even
 // sorted batch, compute each event's epoch, (key, epoch) run heads and homogeneity; a block scan
 // plus decoupled look-back gives every event its global segment id; heads write the segment
 // records {start, key, epoch, acquire}, non-homogeneous events flag their segment.  seg_het must
-// be zeroed and the look-back status/ticket words cleared before the launch.
+// be zeroed before the launch (the look-back words need no clearing: LBState).
 constexpr int SEG_THREADS = 256;
 constexpr int SEG_ITEMS = 16;
 constexpr int SEG_TILE = SEG_THREADS * SEG_ITEMS;
 
 __global__ __launch_bounds__(SEG_THREADS) void k_segments(KeyTable T, BatchWork W, EventSrc src, int64_t n,
-                                                          uint32_t invalid, unsigned long long *status,
-                                                          uint32_t *ticket) {
+                                                          uint32_t invalid, LBState L) {
     __shared__ uint32_t s_key[SEG_TILE];
     __shared__ uint64_t s_val[SEG_TILE];
     __shared__ uint32_t l_key[SEG_THREADS];
     __shared__ int64_t l_ep[SEG_THREADS];
     __shared__ int32_t l_acq[SEG_THREADS];
     __shared__ uint32_t waves[SEG_THREADS / WAVE];
-    __shared__ uint32_t s_bid, s_prefix;
+    __shared__ uint32_t s_prefix;
     __shared__ uint32_t p_key;
     __shared__ int64_t p_ep;
     __shared__ int32_t p_acq;
-    if (threadIdx.x == 0) s_bid = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const int64_t bid = s_bid;
+    const int64_t bid = lookback_ticket(L);
     const int64_t base = bid * SEG_TILE;
     const int64_t T0 = src.t0();
 #pragma unroll
@@ -720,7 +732,7 @@ __global__ __launch_bounds__(SEG_THREADS) void k_segments(KeyTable T, BatchWork 
     }
     uint32_t total;
     uint32_t g = block_exclusive_scan((uint32_t)__popc(headmask), waves, &total);
-    tile_lookback(bid, total, status, ticket + 1, &s_prefix);
+    tile_lookback(bid, total, L, &s_prefix);
     __syncthreads();
     g += s_prefix;                   // segments started before this thread's run
 #pragma unroll
@@ -760,8 +772,7 @@ __global__ __launch_bounds__(SEG_THREADS) void k_segments(KeyTable T, BatchWork 
 // first / last element through LDS.  Same outputs and preconditions as k_segments.
 template <int THREADS, int ITEMS>
 __global__ __launch_bounds__(THREADS) void k_segments_v(KeyTable T, BatchWork W, EventSrc src, int64_t n,
-                                                         uint32_t invalid, unsigned long long *status,
-                                                         uint32_t *ticket) {
+                                                         uint32_t invalid, LBState L) {
     static_assert(ITEMS % 4 == 0, "4 keys / 2 values per vector load");
     constexpr int TILE = THREADS * ITEMS;
     __shared__ uint32_t f_key[THREADS + 1];     // first key of every thread's run (+ the next tile's)
@@ -769,13 +780,11 @@ __global__ __launch_bounds__(THREADS) void k_segments_v(KeyTable T, BatchWork W,
     __shared__ int64_t l_ep[THREADS];
     __shared__ int32_t l_acq[THREADS];
     __shared__ uint32_t waves[THREADS / WAVE];
-    __shared__ uint32_t s_bid, s_prefix;
+    __shared__ uint32_t s_prefix;
     __shared__ uint32_t p_key;
     __shared__ int64_t p_ep;
     __shared__ int32_t p_acq;
-    if (threadIdx.x == 0) s_bid = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const int64_t bid = s_bid;
+    const int64_t bid = lookback_ticket(L);
     const int64_t base = bid * TILE;
     const int64_t i0 = base + (int64_t)threadIdx.x * ITEMS;
     const int64_t T0 = src.t0();
@@ -868,7 +877,7 @@ __global__ __launch_bounds__(THREADS) void k_segments_v(KeyTable T, BatchWork W,
     }
     uint32_t total;
     uint32_t g = block_exclusive_scan((uint32_t)__popc(headmask), waves, &total);
-    tile_lookback(bid, total, status, ticket + 1, &s_prefix);
+    tile_lookback(bid, total, L, &s_prefix);
     __syncthreads();
     g += s_prefix;                   // segments started before this thread's run
     uint32_t sid[ITEMS];

@@ -62,8 +62,16 @@ __device__ inline void tok_count_add(const TokenTable &T, int which, unsigned lo
     atomicAdd(cnt_lane(T.counts) + which, v);
 }
 
+// A token's home slot is its id modulo the capacity (round 6): ids are dense -- id_base + the acquire's
+// sorted position in its batch (k_conc_apply) -- so the cache is a ring indexed by id and the inserts of
+// one batch land on consecutive records (coalesced CAS and stores, where a hashed home scattered them over
+// the table); an id whose slot still holds a live older token continues along the probe chain as before.
+// The host keeps live + tombstones below 3/4 of the slots and sizes the ring for several batches of ids,
+// so a batch's ids meet slots its predecessors have mostly released.
+__host__ __device__ inline uint64_t tok_home(uint64_t id, uint64_t mask) { return id & mask; }
+
 __device__ inline int64_t token_find(const TokenTable &T, uint64_t id) {
-    uint64_t h = mix64(id) & T.mask;
+    uint64_t h = tok_home(id, T.mask);
     for (uint64_t p = 0; p <= T.mask; ++p) {
         const unsigned long long k = T.rec[h].key;
         if (k == PKEY_EMPTY) return -1;
@@ -80,7 +88,7 @@ __device__ inline int64_t token_find(const TokenTable &T, uint64_t id) {
 // Many inserts run at once (k_conc_apply): a lost CAS re-examines the slot with the value the CAS
 // returned -- a plain re-load could keep answering the stale free slot from this CU's cache and spin.
 __device__ inline int64_t token_insert(const TokenTable &T, uint64_t id, bool &tomb) {
-    uint64_t h = mix64(id) & T.mask;
+    uint64_t h = tok_home(id, T.mask);
     unsigned long long k = T.rec[h].key;
     for (uint64_t p = 0; p <= T.mask;) {
         if (k == PKEY_EMPTY || k == TOKEN_TOMB) {
@@ -106,7 +114,7 @@ __global__ __launch_bounds__(256) void k_tok_rebuild(TokenTable O, uint64_t ocap
     if (s >= ocap) return;
     const TokRec r = O.rec[s];
     if (r.key == PKEY_EMPTY || r.key == TOKEN_TOMB) return;
-    uint64_t h = mix64(r.key) & N.mask;
+    uint64_t h = tok_home(r.key, N.mask);
     while (atomicCAS(&N.rec[h].key, (unsigned long long)PKEY_EMPTY, r.key) != PKEY_EMPTY) h = (h + 1) & N.mask;
     N.rec[h].flow_id = r.flow_id;
     N.rec[h].flow_idx = r.flow_idx;
@@ -139,9 +147,10 @@ __global__ __launch_bounds__(SORT_THREADS) void k_conc_prep(int64_t n, const Con
                                                             uint32_t *__restrict__ fkey, uint32_t finvalid,
                                                             uint32_t *__restrict__ fhist, int64_t nblocks,
                                                             uint64_t *__restrict__ aux, unsigned long long *__restrict__ desc,
-                                                            int64_t ndesc, int diag) {
+                                                            int64_t ndesc, int diag, uint32_t *__restrict__ sctl = nullptr) {
     for (int64_t j = (int64_t)blockIdx.x * SORT_THREADS + threadIdx.x; j < ndesc; j += (int64_t)gridDim.x * SORT_THREADS)
         desc[j] = 0;                                      // k_conc_scan's look-back descriptors: not yet
+    if (sctl && blockIdx.x == 0 && threadIdx.x < 2) sctl[threadIdx.x] = 0u;   // its tile ticket and fallback count
     __shared__ uint32_t hf[MAX_PASSES][RADIX];
     for (int d = threadIdx.x; d < MAX_PASSES * RADIX; d += SORT_THREADS) (&hf[0][0])[d] = 0;
     __syncthreads();
@@ -162,7 +171,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_conc_prep(int64_t n, const Con
         hk[j] = PKEY_EMPTY;
         hf_idx[j] = -1;
         if (evs[j].kind == CONC_RELEASE) {
-            const uint64_t h = mix64((uint64_t)evs[j].token) & TT.mask;
+            const uint64_t h = tok_home((uint64_t)evs[j].token, TT.mask);
             hk[j] = TT.rec[h].key;
             hf_idx[j] = TT.rec[h].flow_idx;
         }
@@ -185,7 +194,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_conc_prep(int64_t n, const Con
         } else if (e.kind == CONC_RELEASE) {
             int64_t h = -1;                                                  // CCFC:82-86
             int32_t fidx = -1;
-            const uint64_t h0 = mix64((uint64_t)e.token) & TT.mask;
+            const uint64_t h0 = tok_home((uint64_t)e.token, TT.mask);
             const bool issuable = (uint64_t)e.token != PKEY_EMPTY && (uint64_t)e.token != TOKEN_TOMB;  // (slot markers)
             if (!issuable) {
                 // never issued (ids stay below 2^63): ALREADY_RELEASE
@@ -233,7 +242,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_conc_prep(int64_t n, const Con
 //   fallback  a segment that the scan cannot decide exactly -- an amount other than 1, nowCalls above T'
 //             at the start, or an int sum that could wrap -- is walked by one thread (k_conc_serial)
 //   effects   one thread per sorted position (k_conc_apply): a passing acquire takes a token (insert
-//             into the cache, id = id_base + arrival position), a failing one answers BLOCKED; the
+//             into the cache, id = id_base + sorted position), a failing one answers BLOCKED; the
 //             segment's last position stores nowCalls
 // A release's amount is read in k_conc_scan, a kernel before any insert of the batch, so a slot reused
 // by an insert can never hand a release someone else's amount.
@@ -608,7 +617,7 @@ __global__ __launch_bounds__(256) void k_conc_serial(const uint32_t *__restrict_
 }
 
 // The effects, one thread per sorted position (CCFC:57-100): a passing acquire takes a token
-// (TokenCacheNode, id = id_base + arrival position), a failing one answers BLOCKED; a claimed release
+// (TokenCacheNode, id = id_base + sorted position), a failing one answers BLOCKED; a claimed release
 // (freed by k_conc_scan) answers RELEASE_OK, any other release ALREADY_RELEASE; a segment's last position
 // stores the flow's nowCalls.  Cache counts {live, tombstones} by one atomic pair per workgroup.
 __global__ __launch_bounds__(256) void k_conc_apply(const uint64_t *__restrict__ sval, const uint32_t *__restrict__ skey,
@@ -629,7 +638,8 @@ __global__ __launch_bounds__(256) void k_conc_apply(const uint64_t *__restrict__
             if (!X.pass[i]) {
                 put_conc(out, seq, 0, ST_BLOCKED);                            // CCFC:57-69
             } else {
-                const uint64_t id = id_base + seq;                            // TokenCacheNode.java:59-70
+                const uint64_t id = id_base + (uint64_t)i;                    // TokenCacheNode.java:59-70 (unique;
+                                                                              // names its ring slot)
                 bool tomb = false;
                 const int64_t h = token_insert(TT, id, tomb);
                 if (h < 0) {                                                  // token cache full

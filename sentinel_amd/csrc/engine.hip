@@ -198,19 +198,16 @@ __global__ __launch_bounds__(SORT_THREADS) void k_flow_prep(
 // the invalid key (from the back; their order is never read: the pipeline stops at nvalid).  Loads
 // stay coalesced (item j of thread t is event j * L1_THREADS + t of the tile); the arrival-order rank
 // comes from one ballot per item and a scan of the (item, wave) counts; tiles take a ticket and find
-// how many limiter requests precede them by decoupled look-back (status / ticket words cleared first).
+// how many limiter requests precede them by decoupled look-back (generation-tagged words, LBState).
 constexpr int L1_THREADS = 512, L1_ITEMS = 8, L1_TILE = L1_THREADS * L1_ITEMS, L1_WAVES = L1_THREADS / WAVE;
 static_assert(L1_ITEMS * L1_WAVES == WAVE, "one (item, wave) count per lane of the scanning wave");
 __global__ __launch_bounds__(L1_THREADS) void k_lim1_prep(
     int64_t n, const Event *__restrict__ ev, int32_t nflows, const int32_t *__restrict__ route,
     const int8_t *__restrict__ route8, uint64_t *__restrict__ out, uint32_t *__restrict__ fkey, uint32_t finvalid,
-    uint32_t linvalid, uint32_t *__restrict__ skey, uint64_t *__restrict__ sval, EventSrc src,
-    unsigned long long *status, uint32_t *ticket) {
+    uint32_t linvalid, uint32_t *__restrict__ skey, uint64_t *__restrict__ sval, EventSrc src, LBState L) {
     __shared__ uint32_t s_cnt[L1_ITEMS * L1_WAVES];   // [item][wave] limiter requests, then their offsets
-    __shared__ uint32_t s_bid, s_prefix;
-    if (threadIdx.x == 0) s_bid = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const int64_t bid = s_bid;
+    __shared__ uint32_t s_prefix;
+    const int64_t bid = lookback_ticket(L);
     const int64_t tile0 = bid * L1_TILE;
     const int wave = threadIdx.x / WAVE;
     Event evs[L1_ITEMS];
@@ -257,7 +254,7 @@ __global__ __launch_bounds__(L1_THREADS) void k_lim1_prep(
         const uint32_t inc = wave_inclusive_scan(c);
         s_cnt[threadIdx.x] = inc - c;
         const uint32_t total = __shfl(inc, WAVE - 1);
-        tile_lookback(bid, total, status, ticket + 1, &s_prefix);
+        tile_lookback(bid, total, L, &s_prefix);
     }
     __syncthreads();
     const int64_t T0 = src.t0();
@@ -780,6 +777,7 @@ struct sentinel_engine {
     DevBuf w_vslot;                    // slot of every value of a param batch
     DevBuf w_runs;                     // partition path: long-run / oversized-half work lists
     DevBuf w_pscan;                    // partition path: per-group range sums + range starts
+    DevBuf w_lb;                       // look-back words (LBState): zero between launches, the kernels re-clean them
     DevBuf io_ev, io_fl, io_out, io_vals;
     // streamed host path (sentinel_submit_flow_stream_host): copy streams + two staging slots
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
@@ -800,9 +798,37 @@ struct sentinel_engine {
         rc |= w_parts.ensure((size_t)(scan_parts(std::max<int64_t>(c, hist_words(c, MAX_PASSES))) + 16) * 8);
         rc |= w_segstart.ensure((c + 1) * 4);
         rc |= w_counters.ensure(64);
+        {
+            // every look-back user's tiles: the scan of the radix histograms, the segments, the limiter prep
+            const size_t lbw = 256 + (size_t)(scan_parts(std::max<int64_t>(c, hist_words(c, MAX_PASSES))) + 16) * 8;
+            if (lbw > w_lb.bytes) {
+                rc |= w_lb.ensure(lbw);
+                if (!rc && hipMemset(w_lb.p, 0, w_lb.bytes) != hipSuccess) rc = SENTINEL_E_DEVICE;
+                lb_gen = 0;
+                lb_tickets = 0;
+            }
+        }
         if (rc) return SENTINEL_E_NOMEM;
         ws_cap = c;
         return 0;
+    }
+
+    // The look-back words of the next launch of `ntiles` workgroups (each takes one ticket).  ensure_ws
+    // sizes the buffer for every batch; a larger user grows it here (zeroed on the stream first).
+    uint32_t lb_gen = 0, lb_tickets = 0;
+    LBState lb_state(int64_t ntiles, hipStream_t s) {
+        const size_t want = 256 + (size_t)ntiles * 8;
+        if (want > w_lb.bytes && w_lb.ensure(want) == 0) lb_zero(s);
+        if (++lb_gen > LB_GEN_MASK) lb_zero(s);
+        const LBState L{reinterpret_cast<unsigned long long *>(w_lb.as<char>() + 256), w_lb.as<uint32_t>(), lb_gen,
+                        lb_tickets};
+        lb_tickets += (uint32_t)ntiles;
+        return L;
+    }
+    void lb_zero(hipStream_t s) {
+        (void)hipMemsetAsync(w_lb.p, 0, w_lb.bytes, s);
+        lb_gen = 1;
+        lb_tickets = 0;
     }
 
     PartBufs part_bufs() {
@@ -901,13 +927,10 @@ struct sentinel_engine {
         if (n <= 0) return;
         const int64_t nb = scan_parts(n);
         if (use_lookback) {
-            // status words (8 B per tile) then the ticket and error words, zeroed together
-            unsigned long long *status = w_parts.as<unsigned long long>();
-            uint32_t *ticket = (uint32_t *)(status + nb);
-            (void)hipMemsetAsync(status, 0, (size_t)nb * 8 + 16, s);
+            const LBState L = lb_state(nb, s);   // (self-cleaning: no memset in front of the launch)
             launch("scan", n, s, [&] {
-                if (exclusive) k_scan_lookback<true><<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, buf, n, status, ticket, ticket + 1);
-                else k_scan_lookback<false><<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, buf, n, status, ticket, ticket + 1);
+                if (exclusive) k_scan_lookback<true><<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, buf, n, L);
+                else k_scan_lookback<false><<<dim3((unsigned)nb), dim3(SCAN_THREADS), 0, s>>>(buf, buf, n, L);
             });
             return;
         }
@@ -923,7 +946,8 @@ struct sentinel_engine {
     // K2: stable LSD radix sort of (key, seq|prio, payload) by the low `bits` key bits into
     // (skey, sval).  `hist` holds pass 0's per-tile digit histograms (built by the prep
     // kernel from the same tiles); later passes histogram their own input.
-    void sort(const uint32_t *keys_in, int64_t n, int bits, uint32_t *hist, const EventSrc &src, hipStream_t s) {
+    void sort(const uint32_t *keys_in, int64_t n, int bits, uint32_t *hist, const EventSrc &src, hipStream_t s,
+              uint8_t *z0 = nullptr, uint8_t *z1 = nullptr) {
         const int64_t nb = sort_blocks(n);
         const int passes = passes_for(bits);
         uint32_t *kb[2];
@@ -949,7 +973,7 @@ struct sentinel_engine {
             if (p == 0)
                 launch("radix_scatter", n, s, [&] {
                     k_radix_scatter_p<true><<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(kin, vin, src, ko, vo, n,
-                                                                                               shift, hist, nb);
+                                                                                               shift, hist, nb, z0, z1);
                 });
             else
                 launch("radix_scatter", n, s, [&] {
@@ -973,22 +997,23 @@ struct sentinel_engine {
                        const EventSrc &src, hipStream_t s, bool presorted = false) {
         BatchWork W = work();
         const uint32_t invalid = ((uint32_t)1 << bits) - 1;
-        if (!presorted) sort(keys, n, bits, hist, src, s);
+        if (!presorted) {
+            sort(keys, n, bits, hist, src, s, W.seg_het, W.seg_prio);   // (the first pass clears the flags)
+        } else {
+            (void)hipMemsetAsync(W.seg_het, 0, (size_t)n, s);
+            (void)hipMemsetAsync(W.seg_prio, 0, (size_t)n, s);
+        }
         const unsigned g = grid_for(n);
-        (void)hipMemsetAsync(W.seg_het, 0, (size_t)n, s);
-        (void)hipMemsetAsync(W.seg_prio, 0, (size_t)n, s);
         if (fused_segments) {
             const int64_t nt = (n + SEG_TILE - 1) / SEG_TILE;
-            unsigned long long *status = w_parts.as<unsigned long long>();
-            uint32_t *ticket = (uint32_t *)(status + nt);
-            (void)hipMemsetAsync(status, 0, (size_t)nt * 8 + 16, s);
+            const LBState L = lb_state(nt, s);
             launch("segments", n, s, [&] {
                 if (seg_impl == 1)
-                    k_segments_v<256, 16><<<dim3((unsigned)nt), dim3(256), 0, s>>>(T, W, src, n, invalid, status, ticket);
+                    k_segments_v<256, 16><<<dim3((unsigned)nt), dim3(256), 0, s>>>(T, W, src, n, invalid, L);
                 else if (seg_impl == 2)
-                    k_segments_v<512, 8><<<dim3((unsigned)nt), dim3(512), 0, s>>>(T, W, src, n, invalid, status, ticket);
+                    k_segments_v<512, 8><<<dim3((unsigned)nt), dim3(512), 0, s>>>(T, W, src, n, invalid, L);
                 else
-                    k_segments<<<dim3((unsigned)nt), dim3(SEG_THREADS), 0, s>>>(T, W, src, n, invalid, status, ticket);
+                    k_segments<<<dim3((unsigned)nt), dim3(SEG_THREADS), 0, s>>>(T, W, src, n, invalid, L);
             });
         } else {
             launch("seg_heads", n, s, [&] { k_seg_heads<<<g, 256, 0, s>>>(T, W, src, n, invalid); });
@@ -1010,12 +1035,11 @@ struct sentinel_engine {
         (void)hipMemsetAsync(w_counters.p, 0, 16, s);
         if (nlimiters == 1 && lim1 && fpasses == 0) {
             const int64_t nt = (n + L1_TILE - 1) / L1_TILE;
-            unsigned long long *status = w_parts.as<unsigned long long>();
-            (void)hipMemsetAsync(status, 0, (size_t)nt * 8 + 16, s);
+            const LBState L = lb_state(nt, s);
             launch("lim_prep", n, s, [&] {
                 k_lim1_prep<<<dim3((unsigned)nt), dim3(L1_THREADS), 0, s>>>(
                     n, ev, F, d_flow_route.as<int32_t>(), route8(), out, fkey, finvalid, linvalid,
-                    w_skey.as<uint32_t>(), w_sval.as<uint64_t>(), lsrc, status, (uint32_t *)(status + nt));
+                    w_skey.as<uint32_t>(), w_sval.as<uint64_t>(), lsrc, L);
             });
             run_pipeline(LT, nullptr, nullptr, n, lbits, lsrc, LV, s, 10, true, false, true);
             return;
@@ -1194,7 +1218,7 @@ int sentinel_engine::rewrite_tokens(bool compact, uint64_t new_cap) {
         }
         uint64_t d = h;
         if (compact) {
-            d = mix64(o.key) & (tcap - 1);
+            d = tok_home(o.key, tcap - 1);
             while (nr[d].key != PKEY_EMPTY) d = (d + 1) & (tcap - 1);
         }
         auto it = flow_index.find(o.flow_id);
@@ -1833,7 +1857,8 @@ static int submit_flow_sorted(sentinel_engine_t *e, int64_t n, const Event *ev, 
         e->hist_pass0(fkey, n, e->w_fhist.as<uint32_t>(), s);   // the limiter invalidated some keys
     } else {
         const int64_t nb = sort_blocks(n);
-        HIP_OK(hipMemsetAsync(e->w_counters.p, 0, 16, s));
+        // (nvalid / nseg: the fused segment kernel always writes both)
+        if (!e->fused_segments) HIP_OK(hipMemsetAsync(e->w_counters.p, 0, 16, s));
         e->launch("flow_prep", n, s, [&] {
             k_flow_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(
                 n, ev, F, e->flow_plain ? nullptr : e->d_flow_route.as<int32_t>(), out, fkey, finvalid, 1,
@@ -2670,7 +2695,7 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
                       &e->d_lhot_tok, &e->d_ltable, &e->d_lstate, &e->d_now, &e->d_conc_thr, &e->d_seg1_w,
                       &e->d_seg1_rcp, &e->d_seg1_kind, &e->d_tok_rec,
                       &e->d_tok_counts, &e->d_tok_ticket, &e->w_cbig, &e->sp_tok_rec, &e->w_runs, &e->w_pscan, &e->d_lres_state,
-                      &e->d_lres_count, &e->d_lres_w, &e->d_lres_rcp, &e->d_lres_kind, &e->d_lres_tcount,
+                      &e->d_lres_count, &e->w_lb, &e->d_lres_w, &e->d_lres_rcp, &e->d_lres_kind, &e->d_lres_tcount,
                       &e->d_lres_flags, &e->w_lslow, &e->io_lrt, &e->d_lrule_grade,
                       &e->d_lg_on, &e->d_lg_dn, &e->d_lg_created, &e->d_lg_roff, &e->d_lg_rules, &e->d_lg_comp,
                       &e->io_lctx, &e->sp_keys, &e->sp_rule, &e->sp_state, &e->sp_n, &e->sp_w, &e->sp_rcp,
@@ -4112,14 +4137,13 @@ static int submit_concurrent(sentinel_engine_t *e, int64_t n, const ConcEvent *d
     e->launch("conc_prep", n, s, [&] {
         k_conc_prep<<<dim3((unsigned)nb), dim3(SORT_THREADS), 0, s>>>(n, dev, F, TT, dout, fkey, finvalid,
                                                                       e->w_fhist.as<uint32_t>(), nb, aux, S.desc, nt,
-                                                                      e->cm_diag >> 8);
+                                                                      e->cm_diag >> 8, ctl);
     });
     if (F > 0) {
         const EventSrc src{nullptr, (const ParamEvent *)dev, nullptr, false, aux};
         e->sort(fkey, n, fbits, e->w_fhist.as<uint32_t>(), src, s);
         const uint32_t *skey = e->w_skey.as<uint32_t>();
         const uint64_t *sval = e->w_sval.as<uint64_t>();
-        HIP_OK(hipMemsetAsync(ctl, 0, 8, s));
         const ConcElems X{e->w_hacq.as<int32_t>(), e->w_done.as<uint8_t>()};
         int32_t *now_calls = e->d_now.as<int32_t>();
         const double *thr = e->d_conc_thr.as<double>();

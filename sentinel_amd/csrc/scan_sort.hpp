@@ -135,40 +135,66 @@ inline int64_t scan_parts(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 
 // Single-pass device scan with decoupled look-back (one launch instead of three).  Tiles take a
 // dynamic id from an atomic ticket, so every tile's predecessors have started; a tile publishes
-// its aggregate, then its inclusive prefix, in ONE 64-bit word {flag:2 | value:32} with agent-scope
-// relaxed atomics (the payload is the flag: no separate release/acquire pair is needed).  One wave
-// looks back over 64 predecessors at a time.  Spins are bounded; on timeout the tile records an
-// error word and proceeds (wrong result, never a hang).
+// its aggregate, then its inclusive prefix, in ONE 64-bit word {flag:2 | generation:30 | value:32}
+// with agent-scope relaxed atomics (the payload is the flag: no separate release/acquire pair is
+// needed).  One wave looks back over 64 predecessors at a time.  Spins are bounded; on timeout the
+// tile records an error word and proceeds (wrong result, never a hang).
+//
+// No memset in front of a launch (round 6: a fill kernel costs ~5 us on the stream, and the radix path
+// ran up to six per batch): every launch carries a generation, and a word of another generation reads
+// as "not published yet"; the ticket is never reset -- the host passes how many tickets earlier
+// launches took (tbase; 32-bit arithmetic, wraps).  The words live in their own buffer (LBState),
+// zeroed when allocated (generation 0 is never a launch's) and again when the 30-bit generation wraps.
+// (A self-cleaning variant -- the last workgroup to finish zeroing the words -- was measured first:
+// its end-of-workgroup counter round trip made the segment kernel 40 -> 45 us.)
 constexpr uint64_t LB_AGG = 1ull << 62;
 constexpr uint64_t LB_PREFIX = 2ull << 62;
 constexpr uint64_t LB_FLAGS = 3ull << 62;
+constexpr uint32_t LB_GEN_MASK = (1u << 30) - 1;
 
+// ctl: [0] tile ticket (never reset), [2] error (sticky: a timed-out look-back)
+struct LBState {
+    unsigned long long *status;
+    uint32_t *ctl;
+    uint32_t gen;        // this launch's generation, in [1, 2^30)
+    uint32_t tbase;      // tickets taken by earlier launches
+};
+
+// This workgroup's tile id (call from every thread; thread 0 takes the ticket).
+__device__ inline uint32_t lookback_ticket(const LBState &L) {
+    __shared__ uint32_t s_tid;
+    if (threadIdx.x == 0) s_tid = atomicAdd(&L.ctl[0], 1u) - L.tbase;
+    __syncthreads();
+    return s_tid;
+}
 
 // Decoupled look-back for tile b with aggregate `total`: wave 0 publishes the aggregate, sums
 // predecessors 64 at a time until it meets an inclusive prefix, publishes its own prefix and
 // leaves the exclusive prefix in *s_prefix (LDS).  Call from every thread of the block; a
 // __syncthreads() must follow before *s_prefix is read.
-__device__ inline void tile_lookback(int64_t b, uint32_t total, unsigned long long *status, uint32_t *error,
-                                     uint32_t *s_prefix) {
+__device__ inline void tile_lookback(int64_t b, uint32_t total, const LBState &L, uint32_t *s_prefix) {
     if (threadIdx.x >= WAVE) return;
+    unsigned long long *status = L.status;
     const int lane = threadIdx.x;
+    const uint64_t g = (uint64_t)L.gen << 32;
     uint32_t prefix = 0;
     if (b == 0) {
-        if (lane == 0) __hip_atomic_store(&status[0], LB_PREFIX | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(&status[0], LB_PREFIX | g | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-        if (lane == 0) __hip_atomic_store(&status[b], LB_AGG | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(&status[b], LB_AGG | g | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int64_t hi = b - 1;
         uint32_t spins = 0;
         for (;;) {
             const int64_t p = hi - lane;
-            const uint64_t st = p >= 0 ? __hip_atomic_load(&status[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                       : LB_PREFIX;
+            uint64_t st = p >= 0 ? __hip_atomic_load(&status[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                 : (LB_PREFIX | g);
+            if (((st >> 32) & LB_GEN_MASK) != L.gen) st = 0;   // an earlier launch's word: not yet
             const uint64_t not_ready = __ballot((st & LB_FLAGS) == 0);
             const uint64_t is_prefix = __ballot((st & LB_FLAGS) == LB_PREFIX);
             const int first_prefix = is_prefix ? __ffsll((unsigned long long)is_prefix) - 1 : WAVE;
             const uint64_t need = first_prefix >= WAVE - 1 ? ~0ull : ((2ull << first_prefix) - 1);
             if (not_ready & need) {
-                if (++spins > (1u << 22)) { if (lane == 0) *error = 1; break; }
+                if (++spins > (1u << 22)) { if (lane == 0) L.ctl[2] = 1; break; }
                 __builtin_amdgcn_s_sleep(1);
                 continue;
             }
@@ -180,21 +206,18 @@ __device__ inline void tile_lookback(int64_t b, uint32_t total, unsigned long lo
             hi -= WAVE;
         }
         if (lane == 0)
-            __hip_atomic_store(&status[b], LB_PREFIX | (uint32_t)(prefix + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&status[b], LB_PREFIX | g | (uint32_t)(prefix + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (lane == 0) *s_prefix = prefix;
 }
 
 template <bool EXCLUSIVE>
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan_lookback(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
-                                                                int64_t n, unsigned long long *status, uint32_t *ticket,
-                                                                uint32_t *error) {
+                                                                int64_t n, LBState L) {
     __shared__ uint32_t tile[SCAN_TILE];
     __shared__ uint32_t waves[SCAN_THREADS / WAVE];
-    __shared__ uint32_t s_bid, s_prefix;
-    if (threadIdx.x == 0) s_bid = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const int64_t b = s_bid;
+    __shared__ uint32_t s_prefix;
+    const int64_t b = lookback_ticket(L);
     const int64_t base = b * SCAN_TILE;
 #pragma unroll
     for (int j = 0; j < SCAN_ITEMS; ++j) {
@@ -211,7 +234,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_lookback(const uint32_t *
     }
     uint32_t total;
     uint32_t run = block_exclusive_scan(sum, waves, &total);
-    tile_lookback(b, total, status, error, &s_prefix);
+    tile_lookback(b, total, L, &s_prefix);
     __syncthreads();
     run += s_prefix;
 #pragma unroll
