@@ -591,12 +591,14 @@ class ConcWorkload:
         self.svc.load_rules_array(r.flow_id, r.count, r.threshold_type, r.sample_count, r.window_interval_ms,
                                   r.namespace, r.checker)
         N = self.N
-        # half of the positions acquire, the other half release the previous batch's acquires (a random
-        # pairing of the two position sets)
+        # half of the positions acquire, the other half release the previous batch's acquires: a random
+        # subset of the acquires, released in the order they were acquired (clients hand tokens back first
+        # in, first out; the released tokens' flows are as random as before, and the glue's gather / scatter
+        # runs over increasing positions -- 64 us per step as a random pairing, scripts/glue_study.py)
         perm = rng.permutation(N)
         self.acq_pos = np.sort(perm[: N // 2])
         self.rel_pos = np.sort(perm[N // 2:])
-        src = rng.permutation(len(self.acq_pos))[: len(self.rel_pos)]
+        src = np.sort(rng.permutation(len(self.acq_pos))[: len(self.rel_pos)])
         self.g = torch.Generator(device=dev).manual_seed(3000 + rank)
         self.acq_pos_d = torch.from_numpy(self.acq_pos.astype(np.int64)).to(dev)
         self.rel_pos_d = torch.from_numpy(self.rel_pos.astype(np.int64)).to(dev)

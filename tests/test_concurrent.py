@@ -336,7 +336,8 @@ def test_gpu_token_inserts_contended(oracle_mod, monkeypatch):
 def test_conc_bench_shape_bitexact(oracle_mod):
     """The bench's own 5conc shape (bench.py ConcWorkload): 20k thread-grade rules (count~U{50..5000}),
     Zipf(1.1) flows, 4M-event batches of which half acquire one token and half release, at fixed
-    positions, the tokens the previous batch handed out (blocked acquires hold none: ALREADY_RELEASE);
+    positions, the tokens the previous batch handed out, first in first out (blocked acquires hold none:
+    ALREADY_RELEASE);
     3 batches on the device-pointer path, every status, every flow's nowCalls and the cache size against
     the oracle's sequential replay with the engine's token ids."""
     import sentinel_amd as sa
@@ -352,7 +353,7 @@ def test_conc_bench_shape_bitexact(oracle_mod):
     N = 4 * 1024 * 1024
     perm = rng.permutation(N)
     acq_pos, rel_pos = np.sort(perm[: N // 2]), np.sort(perm[N // 2:])
-    rel_src = acq_pos[rng.permutation(len(acq_pos))[: len(rel_pos)]]
+    rel_src = acq_pos[np.sort(rng.permutation(len(acq_pos))[: len(rel_pos)])]   # (first in, first out)
     w = 1.0 / np.power(np.arange(1, F + 1, dtype=np.float64), 1.1)
     cdf = np.cumsum(w) / w.sum()
     zperm = np.random.default_rng(9).permutation(F).astype(np.int32)
