@@ -153,6 +153,7 @@ struct BatchWork {
     uint32_t *seg_k;             // number of passing events
     uint32_t *nvalid;            // device: events with a valid key
     uint32_t *nseg;              // device: number of segments
+    uint32_t *zero4 = nullptr;   // four words the segment kernel zeroes (the hot-run list counters: no memset)
 };
 
 // Packed TokenResult: {int32 remaining; int16 status; uint16 waitInMs} as one 8-byte store.
@@ -666,6 +667,7 @@ __global__ __launch_bounds__(SEG_THREADS) void k_segments(KeyTable T, BatchWork 
     __shared__ int32_t p_acq;
     const int64_t bid = lookback_ticket(L);
     const int64_t base = bid * SEG_TILE;
+    if (W.zero4 && bid == 0 && threadIdx.x < 4) W.zero4[threadIdx.x] = 0u;
     const int64_t T0 = src.t0();
 #pragma unroll
     for (int j = 0; j < SEG_ITEMS; ++j) {
@@ -786,6 +788,7 @@ __global__ __launch_bounds__(THREADS) void k_segments_v(KeyTable T, BatchWork W,
     __shared__ int32_t p_acq;
     const int64_t bid = lookback_ticket(L);
     const int64_t base = bid * TILE;
+    if (W.zero4 && bid == 0 && threadIdx.x < 4) W.zero4[threadIdx.x] = 0u;
     const int64_t i0 = base + (int64_t)threadIdx.x * ITEMS;
     const int64_t T0 = src.t0();
     uint32_t key[ITEMS];

@@ -777,7 +777,8 @@ struct sentinel_engine {
     DevBuf w_vslot;                    // slot of every value of a param batch
     DevBuf w_runs;                     // partition path: long-run / oversized-half work lists
     DevBuf w_pscan;                    // partition path: per-group range sums + range starts
-    DevBuf w_lb;                       // look-back words (LBState): zero between launches, the kernels re-clean them
+    DevBuf w_lb;                       // look-back words (LBState): generation-tagged, zeroed when allocated
+    uint32_t *seg_zero = nullptr;      // four counters the next segment kernel zeroes (BatchWork.zero4)
     DevBuf io_ev, io_fl, io_out, io_vals;
     // streamed host path (sentinel_submit_flow_stream_host): copy streams + two staging slots
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
@@ -852,6 +853,7 @@ struct sentinel_engine {
         W.seg_done = w_done.as<uint8_t>();
         W.seg_s0 = w_s0.as<int64_t>();
         W.seg_k = w_k.as<uint32_t>();
+        W.zero4 = seg_zero;
         W.nvalid = w_counters.as<uint32_t>();
         W.nseg = w_counters.as<uint32_t>() + 1;
         return W;
@@ -1058,8 +1060,6 @@ struct sentinel_engine {
     void run_pipeline(const KeyTable &T, const uint32_t *keys, uint32_t *hist, int64_t n, int bits,
                       const EventSrc &src, const Verdicts &V, hipStream_t s, int max_n, bool limiter,
                       bool hot_het = false, bool presorted = false, bool occ4 = false) {
-        sort_segments(T, keys, hist, n, bits, src, s, presorted);
-        BatchWork W = work();
         const unsigned g = grid_for(n);
         // flow tables: keys hotter than HOT_HET_RUN with heterogeneous acquires go to the hot-run kernels
         // (and keys of WAVE_HET_RUN..HOT_HET_RUN events to k_process_wave)
@@ -1078,17 +1078,43 @@ struct sentinel_engine {
                 LR = long_runs_at(w_runs.as<uint32_t>(), n, hot_het_run, 4);
                 WR.n = w_runs.as<uint32_t>() + 3;
                 WR.g0 = reinterpret_cast<uint32_t *>(w_runs.as<char>() + lb);
-                (void)hipMemsetAsync(w_runs.p, 0, 16, s);
+                if (fused_segments) seg_zero = w_runs.as<uint32_t>();    // (k_segments zeroes the four counters)
+                else (void)hipMemsetAsync(w_runs.p, 0, 16, s);
             }
         }
+        sort_segments(T, keys, hist, n, bits, src, s, presorted);
+        seg_zero = nullptr;
+        BatchWork W = work();
+        // the hot runs (a few keys, a workgroup each: the launches leave most of the chip idle) go on the aux
+        // stream, concurrently with the wave runs and the verdict kernel: their keys, events and verdict
+        // positions are disjoint, and k_process_reg already marked their segments done (k_verdict skips
+        // them); the batch's stream waits for them before anything after this pipeline
+        hipEvent_t join = nullptr;
         auto hot = [&](auto nmax) {
             constexpr int NM = decltype(nmax)::value;
+            if (LR.nrun) {
+                hipStream_t hs = s;
+                if (hot_fork && aux_stream()) {
+                    hipEvent_t fork = get_ev();
+                    join = get_ev();
+                    if (fork && join && hipEventRecord(fork, s) == hipSuccess &&
+                        hipStreamWaitEvent(s_aux, fork, 0) == hipSuccess)
+                        hs = s_aux;
+                    if (fork) ev_pool.push_back(fork);
+                }
+                launch("part_long", n, hs, [&] { launch_long<NM>(T, W.sval, LR, src, V, n, hot_het_run, hs, nullptr, nullptr); });
+                if (hs != s) {
+                    (void)hipEventRecord(join, hs);
+                } else if (join) {
+                    ev_pool.push_back(join);
+                    join = nullptr;
+                }
+            }
             if (WR.n)
                 launch("process_wave", n, s, [&] {
                     const unsigned gw = (unsigned)std::min<int64_t>(n / WAVE_HET_RUN / 4 + 1, 2048);
                     k_process_wave<NM><<<gw, 256, 0, s>>>(T, W, src, V, WR, LR.nrun, hint);
                 });
-            if (LR.nrun) launch("part_long", n, s, [&] { launch_long<NM>(T, W.sval, LR, src, V, n, hot_het_run, s, nullptr, nullptr); });
         };
         if (max_n <= PROC_G * PROC_SLOTS_PER_LANE && process_impl == 1)
             launch("process", n, s, [&] {
@@ -1114,6 +1140,18 @@ struct sentinel_engine {
         else if (verdict_nt) launch("verdict", n, s, [&] { k_verdict<false, true><<<g, 256, 0, s>>>(T, W, V, n); });
         else if (diag_linear) launch("verdict", n, s, [&] { k_verdict<false, false, true><<<g, 256, 0, s>>>(T, W, V, n); });
         else launch("verdict", n, s, [&] { k_verdict<false, false><<<g, 256, 0, s>>>(T, W, V, n); });
+        if (join) {
+            (void)hipStreamWaitEvent(s, join, 0);
+            ev_pool.push_back(join);
+        }
+    }
+
+    // The engine's second compute stream (created on first use): hot runs concurrent with the rest.
+    hipStream_t s_aux = nullptr;
+    bool hot_fork = true;              // SENTINEL_HOT_FORK=0: the hot runs on the batch's stream, in order
+    bool aux_stream() {
+        if (!s_aux && hipStreamCreateWithFlags(&s_aux, hipStreamNonBlocking) != hipSuccess) s_aux = nullptr;
+        return s_aux != nullptr;
     }
 
     int rebuild_flow_thresholds();
@@ -2637,6 +2675,7 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
         e->flow_path = v == "sorted" ? 1 : v == "partition" ? 2 : v == "small" ? 3 : 0;
     }
     if (const char *c = getenv("SENTINEL_SEGMENTS")) e->fused_segments = std::string(c) != "split";
+    if (const char *c = getenv("SENTINEL_HOT_FORK")) e->hot_fork = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_SEG_IMPL")) e->seg_impl = atoi(c);
     if (const char *c = getenv("SENTINEL_ROUTE8")) e->use_route8 = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_LIM1")) e->lim1 = std::string(c) != "0";
@@ -2709,6 +2748,7 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
         if (e->x_comp[k]) (void)hipEventDestroy(e->x_comp[k]);
     }
     if (e->s_h2d) (void)hipStreamDestroy(e->s_h2d);
+    if (e->s_aux) (void)hipStreamDestroy(e->s_aux);
     if (e->s_d2h) (void)hipStreamDestroy(e->s_d2h);
     if (e->h_part_stat) (void)hipHostFree(e->h_part_stat);
     if (e->h_pfresh) (void)hipHostFree(e->h_pfresh);
