@@ -439,7 +439,11 @@ __device__ inline void pd_walk(const ParamRules &PR, const PRuleRec *RR, const P
 #pragma unroll
     for (int j = 0; j < NMAX; ++j)
         if (dirty & (1u << j)) *reinterpret_cast<longlong2 *>(st + 2 * j) = longlong2{ep[j], ct[j]};
+#ifdef SENTINEL_DIAG_NOEXPIRE   // cost diagnostic only (stale top-values hints): no hint store
+    if (false) {
+#else
     if (S.expire) {                                                      // getTopValues hint (param_table.hpp)
+#endif
         int64_t nw = EPOCH_ABSENT;
 #pragma unroll
         for (int j = 0; j < NMAX; ++j) nw = j < nsc && ep[j] > nw ? ep[j] : nw;
