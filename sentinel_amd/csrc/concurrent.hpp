@@ -122,10 +122,10 @@ __global__ __launch_bounds__(256) void k_tok_rebuild(TokenTable O, uint64_t ocap
     tok_count_add(N, 0, 1ull);
 }
 
-// Result record {token_id, status}: two 8-byte stores.
+// Result record {token_id, status}: one 16-byte store (one write request per scattered record).
 __device__ inline void put_conc(uint64_t *out, uint32_t i, int64_t token, int status) {
-    out[2 * (uint64_t)i] = (uint64_t)token;
-    out[2 * (uint64_t)i + 1] = (uint64_t)(uint32_t)status;
+    *reinterpret_cast<ulonglong2 *>(out + 2 * (uint64_t)i) =
+        make_ulonglong2((unsigned long long)token, (unsigned long long)(uint32_t)status);
 }
 
 // The sorted value of an event (written by k_conc_prep by arrival position, moved by the sort): the
