@@ -9,7 +9,11 @@ dev = torch.device("cuda:0")
 rng = np.random.default_rng(1)
 perm = rng.permutation(N)
 acq = np.sort(perm[: N // 2]); rel = np.sort(perm[N // 2:])
+import sys
+fifo = len(sys.argv) > 1 and sys.argv[1] == "fifo"
 src = acq[rng.permutation(len(acq))[: len(rel)]]
+if fifo:                                  # the bench's pairing since round 6: first in, first out
+    src = acq[np.sort(rng.permutation(len(acq))[: len(rel)])]
 b = torch.zeros((N, 3), dtype=torch.int64, device=dev)
 prev = torch.arange(2 * N, dtype=torch.int64, device=dev).view(N, 2)
 rel_d = torch.from_numpy(rel.astype(np.int64)).to(dev)
@@ -17,6 +21,10 @@ src_d = torch.from_numpy(src.astype(np.int64)).to(dev)
 dst_w = rel_d * 3 + 1
 src_w = src_d * 2
 bf, pf = b.view(-1), prev.view(-1)
+# every row's token word from one gather (acquire rows read a zero word appended at the end)
+src_all = torch.full((N,), 2 * N, dtype=torch.int64, device=dev)
+src_all[rel_d] = src_w
+pf = torch.cat([pf, torch.zeros(1, dtype=torch.int64, device=dev)])
 variants = {
     "strided index_copy_/index_select": lambda: b[:, 1].index_copy_(0, rel_d, prev[:, 0].index_select(0, src_d)),
     "flat index_copy_/index_select": lambda: bf.index_copy_(0, dst_w, pf.index_select(0, src_w)),
@@ -24,6 +32,7 @@ variants = {
     "flat index_put_/take": lambda: bf.index_put_((dst_w,), pf.take(src_w)),
     "flat scatter_/take": lambda: bf.scatter_(0, dst_w, pf.take(src_w)),
     "flat put_/take": lambda: bf.put_(dst_w, pf.take(src_w)),
+    "column: gather all rows, strided copy": lambda: b[:, 1].copy_(pf.take(src_all)),
 }
 ref = None
 for name, f in variants.items():
