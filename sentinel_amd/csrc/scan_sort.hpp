@@ -160,10 +160,20 @@ struct LBState {
     uint32_t tbase;      // tickets taken by earlier launches
 };
 
-// This workgroup's tile id (call from every thread; thread 0 takes the ticket).
+// This workgroup's tile id (call from every thread; thread 0 takes the ticket).  A ticket outside the
+// grid (the host's count of earlier tickets out of step -- a launch that never ran) must not index the
+// status words: the workgroup records the error and takes its block index (wrong results, reported in
+// ctl[2]; never an out-of-bounds store).
 __device__ inline uint32_t lookback_ticket(const LBState &L) {
     __shared__ uint32_t s_tid;
-    if (threadIdx.x == 0) s_tid = atomicAdd(&L.ctl[0], 1u) - L.tbase;
+    if (threadIdx.x == 0) {
+        uint32_t id = atomicAdd(&L.ctl[0], 1u) - L.tbase;
+        if (id >= gridDim.x) {
+            L.ctl[2] = 2u;
+            id = blockIdx.x;
+        }
+        s_tid = id;
+    }
     __syncthreads();
     return s_tid;
 }
