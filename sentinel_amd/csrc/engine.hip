@@ -805,8 +805,10 @@ struct sentinel_engine {
             if (lbw > w_lb.bytes) {
                 rc |= w_lb.ensure(lbw);
                 if (!rc && hipMemset(w_lb.p, 0, w_lb.bytes) != hipSuccess) rc = SENTINEL_E_DEVICE;
-                lb_gen = 0;
-                lb_tickets = 0;
+                if (!rc && lb_tickets0 && hipMemcpy(w_lb.p, &lb_tickets0, 4, hipMemcpyHostToDevice) != hipSuccess)
+                    rc = SENTINEL_E_DEVICE;                  // (the device ticket starts where the host count does)
+                lb_gen = lb_gen0;
+                lb_tickets = lb_tickets0;
             }
         }
         if (rc) return SENTINEL_E_NOMEM;
@@ -817,6 +819,9 @@ struct sentinel_engine {
     // The look-back words of the next launch of `ntiles` workgroups (each takes one ticket).  ensure_ws
     // sizes the buffer for every batch; a larger user grows it here (zeroed on the stream first).
     uint32_t lb_gen = 0, lb_tickets = 0;
+    // (tests: SENTINEL_LB_START=<generation>,<tickets> starts a fresh buffer near the generation wrap and
+    // the 32-bit ticket wrap)
+    uint32_t lb_gen0 = 0, lb_tickets0 = 0;
     LBState lb_state(int64_t ntiles, hipStream_t s) {
         const size_t want = 256 + (size_t)ntiles * 8;
         if (want > w_lb.bytes && w_lb.ensure(want) == 0) lb_zero(s);
@@ -2675,6 +2680,13 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
         e->flow_path = v == "sorted" ? 1 : v == "partition" ? 2 : v == "small" ? 3 : 0;
     }
     if (const char *c = getenv("SENTINEL_SEGMENTS")) e->fused_segments = std::string(c) != "split";
+    if (const char *c = getenv("SENTINEL_LB_START")) {
+        unsigned long g = 0, t = 0;
+        if (sscanf(c, "%lu,%lu", &g, &t) == 2 && g < LB_GEN_MASK) {
+            e->lb_gen0 = (uint32_t)g;
+            e->lb_tickets0 = (uint32_t)t;
+        }
+    }
     if (const char *c = getenv("SENTINEL_HOT_FORK")) e->hot_fork = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_SEG_IMPL")) e->seg_impl = atoi(c);
     if (const char *c = getenv("SENTINEL_ROUTE8")) e->use_route8 = std::string(c) != "0";

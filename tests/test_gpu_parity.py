@@ -90,6 +90,17 @@ def test_config2_small_bitexact(oracle_mod):
     _compare(_engine(rules), _oracle(oracle_mod, rules), rules, ev, batches=3)
 
 
+def test_lookback_generation_and_ticket_wrap(oracle_mod, monkeypatch):
+    """The radix path's look-back words carry a 30-bit launch generation and the tile tickets a host-tracked
+    32-bit base (scan_sort.hpp, LBState): an engine started a few launches before both wrap
+    (SENTINEL_LB_START) decides ten batches across the wraps bit-exactly.  A 20k-event batch takes ~7 tickets
+    over 3 look-back launches, so the ticket count wraps around launch 17 and the generation (which re-zeroes
+    the words) at launch 26 of ~30."""
+    monkeypatch.setenv("SENTINEL_LB_START", f"{(1 << 30) - 26},{(1 << 32) - 40}")
+    rules, ev = T.config2(200_000, seed=21, n_flows=1000)
+    _compare(_engine(rules), _oracle(oracle_mod, rules), rules, ev, batches=10)
+
+
 def test_config3_shape_bitexact(oracle_mod):
     rules, ev = T.config3(300_000, seed=3, n_flows=20_000, sample_count=10, window_interval_ms=1000)
     _compare(_engine(rules), _oracle(oracle_mod, rules), rules, ev, batches=2)
