@@ -41,6 +41,10 @@ constexpr int PT_WAVES = PT_THREADS / WAVE;
 constexpr int PT_ITEMS = SENTINEL_PT_ITEMS;
 constexpr int PT_TILE = PT_THREADS * PT_ITEMS;
 static_assert(PT_THREADS >= 256 && PT_THREADS <= PART_BINS && PT_TILE <= 65535, "partition tile");
+// the partition histograms (part_blocks(n) x PART_BINS words) live in the radix path's histogram buffer,
+// sized for sort_blocks(n) x RADIX x MAX_PASSES words: a tile smaller than SORT_TILE would overrun it
+// (a PT_ITEMS=4 build faulted)
+static_assert(PT_TILE >= SORT_TILE && PART_BINS <= RADIX * MAX_PASSES, "partition histograms fit the radix buffer");
 inline int64_t part_blocks(int64_t n) { return (n + PT_TILE - 1) / PT_TILE; }
 
 // Validation + routing as k_flow_prep; histogram of the range digit of valid events only.
