@@ -131,6 +131,15 @@ def test_config5_hot_heterogeneous(oracle_mod):
     _compare(_engine(rules), _oracle(oracle_mod, rules), rules, ev, batches=4)
 
 
+def test_hot_runs_on_the_batch_stream(oracle_mod, monkeypatch):
+    """The hot runs (launch_long) normally go to the engine's aux stream, concurrent with the wave runs and
+    the verdict kernel (engine.hip, run_pipeline); SENTINEL_HOT_FORK=0 keeps them on the batch's stream in
+    order.  Both schedules decide config 5's hot heterogeneous shape bit-exactly."""
+    monkeypatch.setenv("SENTINEL_HOT_FORK", "0")
+    rules, ev = T.config5(1_000_000, seed=56, n_flows=2000)
+    _compare(_engine(rules), _oracle(oracle_mod, rules), rules, ev, batches=3)
+
+
 def test_hot_heterogeneous_mixed(oracle_mod):
     """A hot flow whose heterogeneous segments are interleaved with prioritized requests, a clock that
     steps back and small thresholds (saturated after a few events) next to huge ones (never
