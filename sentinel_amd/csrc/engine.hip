@@ -602,7 +602,7 @@ struct sentinel_engine {
     uint32_t *h_het_hint = nullptr;              // pinned: the sorted path's heterogeneous-key deferral is on
     uint32_t hot_het_run = HOT_HET_RUN;          // sorted path: heterogeneous keys above this go to k_part_long
     int64_t flow_batches = 0, sorted_until = -1;
-    bool diag_linear = false;  // SENTINEL_DIAG_LINEAR=1: verdicts in sorted order (cost diagnostic, wrong output)   // SENTINEL_PROCESS: 0 reg (default), 1 group, 2 thread-in-memory
+    bool diag_linear = false;  // SENTINEL_DIAG_LINEAR=1 (-DSENTINEL_DIAG_LINEAR_ENV builds): verdicts in sorted order (cost diagnostic, wrong output)
     int64_t flow_state_words = 0;
 
     // namespace limiters (RequestLimiter = UnaryLeapArray(10, 1000))
@@ -2673,7 +2673,9 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
         e->cm_keys = std::string(c) == "keys";         // "launch" / "coop": always the per-rule lanes
     }
     if (const char *c = getenv("SENTINEL_SCAN")) e->use_lookback = std::string(c) != "3pass";
+#ifdef SENTINEL_DIAG_LINEAR_ENV   // wrong output by design (a cost diagnostic): only in a -DSENTINEL_DIAG_LINEAR_ENV build
     if (const char *c = getenv("SENTINEL_DIAG_LINEAR")) e->diag_linear = std::string(c) == "1";
+#endif
     if (const char *c = getenv("SENTINEL_HOT_HET_RUN")) e->hot_het_run = (uint32_t)std::max(WAVE_HET_RUN, (uint32_t)atoi(c));
     if (const char *c = getenv("SENTINEL_FLOW_PATH")) {
         const std::string v(c);
