@@ -607,6 +607,19 @@ class ConcWorkload:
         # of a (N, 3) event row (two 1-D kernels instead of strided index_select / index_copy_)
         self.rel_dst_w = self.rel_pos_d * 3 + 1
         self.rel_src_w = self.rel_src_d * 2
+        # the same gather / scatter as one kernel with 32-bit positions (tools/bench_glue.hip, built by
+        # __graft_entry__.build()); BENCH_GLUE=torch or a missing library keeps the two torch kernels
+        self.glue = None
+        glue_so = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "libbench_glue.so")
+        if os.environ.get("BENCH_GLUE", "kernel") != "torch" and os.path.exists(glue_so):
+            import ctypes
+            lib = ctypes.CDLL(glue_so)
+            lib.bench_glue_forward_tokens.restype = ctypes.c_int
+            lib.bench_glue_forward_tokens.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int64, ctypes.c_void_p]
+            self.glue = lib.bench_glue_forward_tokens
+            self.rel_pos32 = self.rel_pos_d.to(torch.int32)
+            self.rel_src32 = self.rel_src_d.to(torch.int32)
+        self.glue_kind = "tools/bench_glue.hip kernel" if self.glue else "torch index_select + index_copy_"
         w = 1.0 / np.power(np.arange(1, self.F + 1, dtype=np.float64), 1.1)
         self.zipf_cdf = torch.from_numpy(np.cumsum(w) / w.sum()).to(dev)
         self.zipf_perm = torch.from_numpy(np.random.default_rng(9).permutation(self.F).astype(np.int32)).to(dev)
@@ -615,7 +628,8 @@ class ConcWorkload:
         self.verdicts = self.results[0]
         self.workload = (f"config5conc: {self.F} thread-grade cluster rules (ConcurrentClusterFlowChecker, count~U{{50..5000}}), "
                          f"Zipf(1.1) flows, {N}-event batches of half acquires (1 token) and half releases of the "
-                         f"previous batch's tokens, device-pointer path")
+                         f"previous batch's tokens, device-pointer path; release ids forwarded in the timed step "
+                         f"by the {self.glue_kind}")
         self.kept = []
         self.parity_result = None
 
@@ -635,9 +649,16 @@ class ConcWorkload:
     def submit(self, b, keep=False):
         torch = self.torch
         prev, cur = self.results[self.k % 2], self.results[(self.k + 1) % 2]
-        ext = torch.cuda.ExternalStream(self.svc.stream, device=self.dev)
-        with torch.cuda.stream(ext):                       # the releases name the previous batch's tokens
-            b.view(-1).index_copy_(0, self.rel_dst_w, prev.view(-1).index_select(0, self.rel_src_w))
+        if self.glue:                                      # the releases name the previous batch's tokens
+            assert b.is_contiguous() and b.shape == (self.N, 3) and prev.is_contiguous()
+            rc = self.glue(b.data_ptr(), prev.data_ptr(), self.rel_pos32.data_ptr(), self.rel_src32.data_ptr(),
+                           len(self.rel_pos), self.svc.stream)
+            if rc != 0:
+                raise RuntimeError(f"bench_glue_forward_tokens: {rc}")
+        else:
+            ext = torch.cuda.ExternalStream(self.svc.stream, device=self.dev)
+            with torch.cuda.stream(ext):
+                b.view(-1).index_copy_(0, self.rel_dst_w, prev.view(-1).index_select(0, self.rel_src_w))
         self.svc.submit_concurrent_batch(b, results=cur)
         self.verdicts = cur
         self.k += 1

@@ -46,6 +46,13 @@ def build_tools() -> None:
         else:
             cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-o", exe, src, "-lpthread"]
         subprocess.run(cmd, check=True)
+    if not os.path.exists(GLUE_OUT) or os.path.getmtime(GLUE_OUT) <= os.path.getmtime(GLUE_SRC):
+        subprocess.run([HIPCC, *FLAGS, "-o", GLUE_OUT, GLUE_SRC], check=True)
+
+
+# bench.py's client-traffic kernel for --config 5conc (not part of the engine)
+GLUE_SRC = os.path.join(ROOT, "tools", "bench_glue.hip")
+GLUE_OUT = os.path.join(ROOT, "tools", "libbench_glue.so")
 
 
 if __name__ == "__main__":

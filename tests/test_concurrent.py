@@ -381,3 +381,36 @@ def test_conc_bench_shape_bitexact(oracle_mod):
             assert svc.concurrent_now_calls(f) == orc.concurrent_now_calls(f), (b, f)
         assert svc.concurrent_token_count() == orc.concurrent_token_count()
         prev_tok = np.where(ok, tok_g, 0)
+
+
+@pytest.mark.gpu
+def test_bench_glue_forwards_release_tokens():
+    """bench.py's 5conc client traffic (tools/bench_glue.hip): word 1 of event row rel_pos[i] gets word 0
+    of result row rel_src[i]; every other word is untouched -- the numpy statement of the same copy, on a
+    ragged count (not a multiple of the kernel's 1024 items per workgroup)."""
+    import ctypes
+    import os
+    import torch
+    so = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "libbench_glue.so")
+    lib = ctypes.CDLL(so)
+    lib.bench_glue_forward_tokens.restype = ctypes.c_int
+    lib.bench_glue_forward_tokens.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int64, ctypes.c_void_p]
+    rng = np.random.default_rng(77)
+    N = 300_001
+    perm = rng.permutation(N)
+    acq_pos, rel_pos = np.sort(perm[: N // 2]), np.sort(perm[N // 2:])
+    rel_src = acq_pos[np.sort(rng.permutation(len(acq_pos))[: len(rel_pos) - 3])]
+    rel_pos = rel_pos[: len(rel_src)]
+    ev = rng.integers(-2**62, 2**62, size=(N, 3), dtype=np.int64)
+    prev = rng.integers(-2**62, 2**62, size=(N, 2), dtype=np.int64)
+    want = ev.copy()
+    want[rel_pos, 1] = prev[rel_src, 0]
+    dev = torch.device("cuda:0")
+    ev_d, prev_d = torch.from_numpy(ev).to(dev), torch.from_numpy(prev).to(dev)
+    pos_d = torch.from_numpy(rel_pos.astype(np.int32)).to(dev)
+    src_d = torch.from_numpy(rel_src.astype(np.int32)).to(dev)
+    torch.cuda.synchronize()
+    assert lib.bench_glue_forward_tokens(ev_d.data_ptr(), prev_d.data_ptr(), pos_d.data_ptr(), src_d.data_ptr(),
+                                         len(rel_pos), None) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(ev_d.cpu().numpy(), want)
