@@ -596,7 +596,8 @@ struct sentinel_engine {
     uint32_t opar = 0;                           // ... the current batch's counter
     int num_cu = 0;
     // pinned words a kernel sets when a bounded spin gave up (the batch's results are invalid): [0] unused
-    // (was the one-sweep partition's grid barrier), [1] the concurrency scan's look-back (dev_err_synced)
+    // (was the one-sweep partition's grid barrier), [1] the concurrency scan's look-back, [2] the radix
+    // path's look-back (LBState.err: 1 a spin gave up, 2 a tile ticket outside the grid) (dev_err_synced)
     uint32_t *h_dev_err = nullptr;
     uint32_t *h_long_chunks = nullptr;           // pinned: hot-run chunks of a recent batch (launch hint)
     uint32_t *h_het_hint = nullptr;              // pinned: the sorted path's heterogeneous-key deferral is on
@@ -827,7 +828,7 @@ struct sentinel_engine {
         if (want > w_lb.bytes && w_lb.ensure(want) == 0) lb_zero(s);
         if (++lb_gen > LB_GEN_MASK) lb_zero(s);
         const LBState L{reinterpret_cast<unsigned long long *>(w_lb.as<char>() + 256), w_lb.as<uint32_t>(), lb_gen,
-                        lb_tickets};
+                        lb_tickets, h_dev_err + 2};
         lb_tickets += (uint32_t)ntiles;
         return L;
     }
@@ -1992,14 +1993,20 @@ struct ForeignStream {
 // flag still set at the next submit (an asynchronous caller that did not synchronise) fails that submit.
 static int dev_err_synced(sentinel_engine_t *e) {
     if (!e->h_dev_err) return 0;
-    if (!__atomic_load_n(&e->h_dev_err[1], __ATOMIC_ACQUIRE)) return 0;
+    const uint32_t conc = __atomic_load_n(&e->h_dev_err[1], __ATOMIC_ACQUIRE);
+    const uint32_t lb = __atomic_load_n(&e->h_dev_err[2], __ATOMIC_ACQUIRE);
+    if (!conc && !lb) return 0;
     e->h_dev_err[1] = 0;
-    return fail(SENTINEL_E_DEVICE, "concurrency scan: look-back timed out (the batch's results are invalid)");
+    e->h_dev_err[2] = 0;
+    if (conc) return fail(SENTINEL_E_DEVICE, "concurrency scan: look-back timed out (the batch's results are invalid)");
+    return fail(SENTINEL_E_DEVICE, lb == 2 ? "look-back: tile ticket outside the grid (the batch's results are invalid)"
+                                           : "look-back timed out (the batch's results are invalid)");
 }
 
 static int check_dev_err(sentinel_engine_t *e, hipStream_t s) {
     if (!e->h_dev_err) return 0;
-    if (!__atomic_load_n(&e->h_dev_err[1], __ATOMIC_ACQUIRE)) return 0;
+    if (!__atomic_load_n(&e->h_dev_err[1], __ATOMIC_ACQUIRE) && !__atomic_load_n(&e->h_dev_err[2], __ATOMIC_ACQUIRE))
+        return 0;
     HIP_OK(hipStreamSynchronize(s));
     HIP_OK(hipStreamSynchronize(e->stream));
     return dev_err_synced(e);
@@ -2378,6 +2385,7 @@ static int submit_param_impl(sentinel_engine_t *e, int64_t n, const ParamEvent *
 
 static int submit_param(sentinel_engine_t *e, int64_t n, const ParamEvent *ev, uint64_t *out, hipStream_t s,
                         uint32_t *oseq = nullptr) {
+    if (int rc0 = check_dev_err(e, s)) return rc0;
     bool ord_done = false;
     const int rc = submit_param_impl(e, n, ev, out, s, oseq, ord_done);
     if (rc || !oseq || ord_done || n <= 0) return rc;
@@ -2394,6 +2402,7 @@ static int submit_prules(sentinel_engine_t *e, int mode, int64_t n, const ParamE
                          const uint8_t *kinds) {
     if (n <= 0) return 0;
     if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
+    if (int rc0 = check_dev_err(e, s)) return rc0;
     int rc = e->ensure_ws(n);
     if (rc) return rc;
     const bool local = mode == PMODE_LOCAL;
@@ -2539,7 +2548,7 @@ static int submit_prules_host(sentinel_engine_t *e, int mode, int64_t n, const s
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    return 0;
+    return dev_err_synced(e);
 }
 
 // Local SphU.entry batches (local_entry.hpp): validation, sort by resource, (resource, epoch of
@@ -2549,6 +2558,7 @@ static int submit_local_entry(sentinel_engine_t *e, int64_t n, const Event *ev, 
     if (n <= 0) return 0;
     if (e->lgraph) return fail(SENTINEL_E_STATE, "a local rule graph is loaded: use sentinel_submit_local_graph_batch");
     if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
+    if (int rc0 = check_dev_err(e, s)) return rc0;
     int rc = e->ensure_ws(n);
     if (rc) return rc;
     const int32_t R = e->nlres;
@@ -2595,6 +2605,7 @@ static int submit_local_graph(sentinel_engine_t *e, int64_t n, const Event *ev, 
     if (n <= 0) return 0;
     if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
     if (!e->lgraph) return fail(SENTINEL_E_STATE, "no local rule graph loaded (sentinel_load_local_rules)");
+    if (int rc0 = check_dev_err(e, s)) return rc0;
     int rc = e->ensure_ws(n);
     if (rc) return rc;
     const int32_t R = e->nlres;
@@ -3573,7 +3584,7 @@ static int submit_param_host_locked(sentinel_engine_t *e, int64_t n, const senti
     HIP_OK(hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, s));
     if (out_seq) HIP_OK(hipMemcpyAsync(out_seq, dseq, n * 4, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    return 0;
+    return dev_err_synced(e);
 }
 
 // Decide-order output for single-value param requests (include/sentinel_amd.h): the key walks write each
@@ -3891,7 +3902,7 @@ int sentinel_submit_local_batch_host(sentinel_engine_t *e, int64_t n, const sent
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    return 0;
+    return dev_err_synced(e);
 }
 
 int sentinel_submit_local_entry_batch(sentinel_engine_t *e, int64_t n, const sentinel_event_t *ev,
@@ -3925,7 +3936,7 @@ int sentinel_submit_local_entry_batch_host(sentinel_engine_t *e, int64_t n, cons
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    return 0;
+    return dev_err_synced(e);
 }
 
 int sentinel_local_node_stats(sentinel_engine_t *e, int32_t idx, int64_t ts, int64_t *out) {
@@ -4122,7 +4133,7 @@ int sentinel_submit_local_graph_batch_host(sentinel_engine_t *e, int64_t n, cons
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(out, e->io_out.p, n * 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    return 0;
+    return dev_err_synced(e);
 }
 
 int sentinel_set_occupy_timeout(sentinel_engine_t *e, int32_t timeout_ms) {

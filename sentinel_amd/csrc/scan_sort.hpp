@@ -152,24 +152,30 @@ constexpr uint64_t LB_PREFIX = 2ull << 62;
 constexpr uint64_t LB_FLAGS = 3ull << 62;
 constexpr uint32_t LB_GEN_MASK = (1u << 30) - 1;
 
-// ctl: [0] tile ticket (never reset), [2] error (sticky: a timed-out look-back)
+// ctl: [0] tile ticket (never reset)
 struct LBState {
     unsigned long long *status;
     uint32_t *ctl;
     uint32_t gen;        // this launch's generation, in [1, 2^30)
     uint32_t tbase;      // tickets taken by earlier launches
+    uint32_t *err;       // pinned host word: 1 a look-back gave up its spin, 2 a ticket outside the grid
+                         // (the batch's results are invalid; engine.hip, dev_err_synced)
 };
+
+__device__ inline void lookback_error(const LBState &L, uint32_t code) {
+    __hip_atomic_store(L.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // This workgroup's tile id (call from every thread; thread 0 takes the ticket).  A ticket outside the
 // grid (the host's count of earlier tickets out of step -- a launch that never ran) must not index the
-// status words: the workgroup records the error and takes its block index (wrong results, reported in
-// ctl[2]; never an out-of-bounds store).
+// status words: the workgroup records the error and takes its block index (wrong results, reported to
+// the host through L.err; never an out-of-bounds store).
 __device__ inline uint32_t lookback_ticket(const LBState &L) {
     __shared__ uint32_t s_tid;
     if (threadIdx.x == 0) {
         uint32_t id = atomicAdd(&L.ctl[0], 1u) - L.tbase;
         if (id >= gridDim.x) {
-            L.ctl[2] = 2u;
+            lookback_error(L, 2u);
             id = blockIdx.x;
         }
         s_tid = id;
@@ -204,7 +210,7 @@ __device__ inline void tile_lookback(int64_t b, uint32_t total, const LBState &L
             const int first_prefix = is_prefix ? __ffsll((unsigned long long)is_prefix) - 1 : WAVE;
             const uint64_t need = first_prefix >= WAVE - 1 ? ~0ull : ((2ull << first_prefix) - 1);
             if (not_ready & need) {
-                if (++spins > (1u << 22)) { if (lane == 0) L.ctl[2] = 1; break; }
+                if (++spins > (1u << 22)) { if (lane == 0) lookback_error(L, 1u); break; }
                 __builtin_amdgcn_s_sleep(1);
                 continue;
             }
