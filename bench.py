@@ -878,6 +878,8 @@ def main():
     lat = sorted(lat_seq)
     slow = sorted(range(L), key=lambda i: -lat_seq[i])[:8]
     log("slowest batches of the latency loop (index: ms): " + ", ".join(f"{i}: {lat_seq[i]:.3f}" for i in sorted(slow)))
+    if os.environ.get("BENCH_LAT_ALL"):
+        log("latency loop, every batch (ms): " + " ".join(f"{x:.3f}" for x in lat_seq))
     hl = []
     for i in range(L):
         if i % K == 0:

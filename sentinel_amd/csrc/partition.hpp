@@ -612,13 +612,20 @@ __device__ inline void part_run_w(FlowWindow<NMAX> &fw, const KeyTable &T, uint3
 // window header, folded as it arrives, is only needed as {PASS sum of the valid slots, the rolled
 // slot's pair, "a slot is newer than E"}.  The rolled slot's rest line does not depend on the header,
 // so its load is issued together with the header loads: one memory round trip instead of two.
+// A run that crosses one window boundary -- epoch E, then E2 > E from position q0 + len1 on, each part
+// with one acquire count: most flows of the ~1 batch in 10 whose time span holds a boundary at config 3
+// -- is two closed-form segments from the same loads: after the first, every slot is at most E < E2, so
+// the slot of E2 restarts (fresh, no rest line read) and its window sum is the header with the first
+// segment's pair applied (part_run_w's fast(E) then fast(E2), same counters, same verdicts).
 // Returns false, having written nothing, when the run needs the general walk (part_run_w).
-// DEFER: the verdicts are not written here; the segment's {s0, K, a, small} come back to the caller
-// (k_part_half's cooperative verdict sweep writes them with every lane of the workgroup).
+// DEFER: the verdicts are not written here; the segments' {s0, K, a, small} come back to the caller in
+// d_*[0] / d_*[1] with the first segment's length in *d_len1 (the run's length when it is one segment);
+// k_part_half's cooperative verdict sweep writes them with every lane of the workgroup.
 template <int NMAX, bool DEFER = false>
 __device__ inline bool part_run_single(FlowWindow<NMAX> &fw, const uint64_t *s_val, uint32_t q0, uint32_t q1,
                                        const EventSrc &src, const Verdicts &V, int64_t T0, int64_t *d_s0 = nullptr,
-                                       uint32_t *d_K = nullptr, int32_t *d_a = nullptr, bool *d_small = nullptr) {
+                                       uint32_t *d_K = nullptr, int32_t *d_a = nullptr, bool *d_small = nullptr,
+                                       uint32_t *d_len1 = nullptr) {
     if (fw.ks.hs == 2) return false;
     fw.E0 = epoch_of(T0, fw.w, fw.rcp);
     fw.r0 = (int32_t)(T0 - fw.E0 * (int64_t)fw.w);
@@ -626,13 +633,29 @@ __device__ inline bool part_run_single(FlowWindow<NMAX> &fw, const uint64_t *s_v
     int32_t a;
     bool prio;
     const int64_t E = fw.event(s_val[q0], src, T0, a, prio);
-    bool ok = !(prio && fw.kind == KIND_CLUSTER) && !(fw.occ_raw != 0 && fw.ks.seven && fw.kind == KIND_CLUSTER);
+    const bool cl = fw.kind == KIND_CLUSTER;
+    bool ok = !(prio && cl) && !(fw.occ_raw != 0 && fw.ks.seven && cl);
+    const uint32_t len = q1 - q0;
+    uint32_t len1 = len;                                  // the first segment (epoch E)
+    int64_t E2 = E;
+    int32_t a2 = a;
     for (uint32_t q = q0 + 1; q < q1 && ok; ++q) {
-        int32_t a2;
-        bool p2;
-        ok = fw.event(s_val[q], src, T0, a2, p2) == E && a2 == a && !(p2 && fw.kind == KIND_CLUSTER);
+        int32_t aq;
+        bool pq;
+        const int64_t Eq = fw.event(s_val[q], src, T0, aq, pq);
+        ok = !(pq && cl);
+        if (Eq == E2) {
+            ok = ok && aq == a2;
+        } else if (E2 == E && Eq > E) {                   // the boundary: the second segment starts
+            E2 = Eq;
+            a2 = aq;
+            len1 = q - q0;
+        } else {
+            ok = false;                                   // a third epoch, or the clock went back
+        }
     }
     if (!ok) return false;
+    const bool two = len1 < len;
     const int nsc = fw.nsc;
     const int slot = (int)(E % nsc);
     // header pairs (every slot of the block: in bounds) and the rolled slot's rest line, in flight together
@@ -666,23 +689,59 @@ __device__ inline bool part_run_single(FlowWindow<NMAX> &fw, const uint64_t *s_v
     const bool fresh = ep_s != E;
     const int64_t base = fresh ? 0 : ps_s;
     const int64_t s0 = wrap_add(s_other, base);
-    const uint32_t len = q1 - q0;
-    uint32_t lo = 0, hi = len;                            // K = first p with !admits(S0 + p*a)
+    uint32_t lo = 0, hi = len1;                           // K = first p with !admits(S0 + p*a)
     while (lo < hi) {
         const uint32_t mid = lo + (hi - lo) / 2;
         if (admits(fw.kind, fw.thr, fw.I_s, wrap_add(s0, wrap_mul((int64_t)mid, a)), a)) lo = mid + 1;
         else hi = mid;
     }
     const uint32_t K = lo;
-    const int64_t nb = (int64_t)(len - K);
-    *reinterpret_cast<longlong2 *>(fw.ks.pair(slot)) = longlong2{E, wrap_add(base, wrap_mul((int64_t)K, a))};
-    if (seven) fw.ks.book_rest(slot, fresh, blk, preq, breq, nb, a, K);
-    const bool small = s0 >= 0 && s0 + (int64_t)len * a < (int64_t)INT32_MAX;
+    const int64_t nb = (int64_t)(len1 - K);
+    const int64_t p1 = wrap_add(base, wrap_mul((int64_t)K, a));   // the slot of E after the first segment
+    const bool small = s0 >= 0 && s0 + (int64_t)len1 * a < (int64_t)INT32_MAX;
+    int64_t s2 = 0;
+    uint32_t K2 = 0;
+    bool small2 = false;
+    if (two) {
+        const int slot2 = (int)(E2 % nsc);
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j) {
+            if (j >= nsc || j == slot2) continue;         // (the slot of E2 restarts at 0)
+            const int64_t e = j == slot ? E : hp[j].x;
+            if (e != EPOCH_ABSENT && e > E2 - nsc) s2 = wrap_add(s2, j == slot ? p1 : hp[j].y);
+        }
+        const uint32_t len2 = len - len1;
+        lo = 0;
+        hi = len2;
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            if (admits(fw.kind, fw.thr, fw.I_s, wrap_add(s2, wrap_mul((int64_t)mid, a2)), a2)) lo = mid + 1;
+            else hi = mid;
+        }
+        K2 = lo;
+        small2 = s2 >= 0 && s2 + (int64_t)len2 * a2 < (int64_t)INT32_MAX;
+        if (slot2 != slot) *reinterpret_cast<longlong2 *>(fw.ks.pair(slot)) = longlong2{E, p1};
+        *reinterpret_cast<longlong2 *>(fw.ks.pair(slot2)) = longlong2{E2, wrap_mul((int64_t)K2, a2)};
+        if (seven) {
+            if (slot2 != slot) fw.ks.book_rest(slot, fresh, blk, preq, breq, nb, a, K);
+            fw.ks.book_rest(slot2, true, 0, 0, 0, (int64_t)(len2 - K2), a2, K2);
+        }
+    } else {
+        *reinterpret_cast<longlong2 *>(fw.ks.pair(slot)) = longlong2{E, p1};
+        if (seven) fw.ks.book_rest(slot, fresh, blk, preq, breq, nb, a, K);
+    }
     if (DEFER) {
-        *d_s0 = s0;
-        *d_K = K;
-        *d_a = a;
-        *d_small = small;
+        d_s0[0] = s0;
+        d_K[0] = K;
+        d_a[0] = a;
+        d_small[0] = small;
+        if (two) {
+            d_s0[1] = s2;
+            d_K[1] = K2;
+            d_a[1] = a2;
+            d_small[1] = small2;
+        }
+        *d_len1 = len1;
         return true;
     }
 #if defined(SENTINEL_DIAG_NOVERDICT)     // cost diagnostic only (no output)
@@ -692,7 +751,8 @@ __device__ inline bool part_run_single(FlowWindow<NMAX> &fw, const uint64_t *s_v
 #elif defined(SENTINEL_DIAG_VLINEAR)     // cost diagnostic only (wrong output): flow-contiguous stores
     for (uint32_t k = 0; k < len; ++k) V.out[(blockIdx.x * blockDim.x + threadIdx.x) * 8 + (k & 7)] = fw.verdict(s0, a, K, k, small);
 #else
-    for (uint32_t k = 0; k < len; ++k) V.put(q0 + k, s_val[q0 + k], fw.verdict(s0, a, K, k, small));
+    for (uint32_t k = 0; k < len1; ++k) V.put(q0 + k, s_val[q0 + k], fw.verdict(s0, a, K, k, small));
+    for (uint32_t k = len1; k < len; ++k) V.put(q0 + k, s_val[q0 + k], fw.verdict(s2, a2, K2, k - len1, small2));
 #endif
     return true;
 }
@@ -1598,14 +1658,15 @@ __global__ __launch_bounds__(PH_THREADS, SENTINEL_PH_MINB) void k_part_half(
             int32_t a[2] = {0, 0};
             uint32_t len1 = 0, len12 = 0;
             if (c > 0 && c <= LONG_RUN) {
-                bool small;
+                bool small[2];
                 // the single-segment pre-pass pays off only for short runs: with >= ~34 events per flow
                 // (hb <= 7) a run straddles an epoch boundary often and the walk alone is cheaper
                 // (measured: 125k flows +4%, 250k +1%; 500k flows -1% without it)
                 if (hb >= PH_COOP_SINGLE_HB &&
-                    part_run_single<NMAX, true>(fw, sv, start, start + c, src, VV, T0, &s0[0], &rec[0], &a[0], &small)) {
-                    rec[0] |= small ? COOP_SMALL : 0u;
-                    len1 = len12 = c;
+                    part_run_single<NMAX, true>(fw, sv, start, start + c, src, VV, T0, s0, rec, a, small, &len1)) {
+                    rec[0] |= small[0] ? COOP_SMALL : 0u;
+                    if (len1 < c) rec[1] |= small[1] ? COOP_SMALL : 0u;   // (a second segment: its K)
+                    len12 = c;
                 } else {
                     fw.load_header(T0);
                     part_run_defer<NMAX>(fw, T, key, sv, start, start + c, src, VV, T0, s0, rec, a, len1, len12,

@@ -421,6 +421,43 @@ def test_bench_rank_shapes_bitexact(oracle_mod, world):
         assert np.array_equal(svc.dump_flow(int(f), 10), orc.dump_flow(int(f))), f
 
 
+@pytest.mark.parametrize("F", [1_000_000, 400_000])
+def test_window_boundary_inside_batch(oracle_mod, F):
+    """Batches whose time span holds a window boundary (T0 + 1 s: a boundary of every rule's window): a flow's
+    run is two homogeneous segments, epoch E then E2 (partition.hpp, part_run_single's two-segment closed
+    form -- 1M flows: one thread per flow; 400k: the cooperative verdict sweep).  Windows n = 10 / 2 / 1 over
+    1 s (with n = 1 both segments share one slot), acquire counts that change at the boundary, small
+    thresholds (blocked events in both segments), and batches before / across / after the boundary so the
+    rolled slots carry state; bit-exact statuses, remaining and window counters."""
+    import torch
+    from sentinel_amd.token_service import decode_verdicts, device_events
+    rng = np.random.default_rng(29)
+    rules = T.make_rules(F, rng, count_lo=1, count_hi=30, sample_count=10, window_interval_ms=1000)
+    rules.sample_count[1::3] = 2
+    rules.sample_count[2::3] = 1
+    svc = _engine(rules)
+    orc = oracle_mod.TokenServiceOracle.from_arrays(rules.flow_id, rules.count, rules.threshold_type,
+                                                    rules.sample_count, rules.window_interval_ms,
+                                                    rules.namespace, rules.checker)
+    n = 4 * 1024 * 1024
+    erng = np.random.default_rng(30)
+    for b, (t_lo, t_hi) in enumerate([(985, 993), (996, 1004), (1004, 1012)]):
+        idx = erng.integers(0, F, n, dtype=np.int32)
+        ts = (T.T0_ALIGNED + t_lo + np.floor(np.arange(n, dtype=np.float64) * ((t_hi - t_lo) / n))).astype(np.int64)
+        acq = (1 + (idx.astype(np.int64) + (ts >= T.T0_ALIGNED + 1000)) % 3).astype(np.int32)
+        v = svc.submit_flow_batch(device_events(torch.from_numpy(idx).cuda(), torch.from_numpy(acq).cuda(),
+                                                torch.from_numpy(ts).cuda()))
+        svc.synchronize()
+        st_g, rem_g, _ = decode_verdicts(v)
+        st_o, rem_o, _, _ = orc.replay_mt(idx, acq, ts, 16)
+        bad = np.nonzero((st_g != st_o) | (rem_g != rem_o))[0]
+        assert len(bad) == 0, (F, b, len(bad), bad[:5], st_g[bad[:5]], st_o[bad[:5]])
+        if b == 1:
+            assert 0.05 < float((st_o == 1).mean()) < 0.95, float((st_o == 1).mean())   # both outcomes
+    for f in np.random.default_rng(2).choice(F, 300, replace=False):
+        assert np.array_equal(svc.dump_flow(int(f), int(rules.sample_count[f])), orc.dump_flow(int(f))), f
+
+
 def test_batcher_concurrent_threads():
     """Many threads calling the per-call API concurrently: batched on the GPU, and the result set
     equals a sequential replay in some arrival order (homogeneous acquire => order-free counts)."""
