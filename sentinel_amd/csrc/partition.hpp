@@ -1362,7 +1362,10 @@ constexpr int PH_BALLOT_FIRST_HB = SENTINEL_PH_BALLOT_FIRST_HB;   // halves of <
 #define SENTINEL_PH_COOP_MINHB 0
 #endif
 constexpr int PH_COOP_HB = SENTINEL_PH_COOP_HB;
-constexpr int PH_COOP_SINGLE_HB = 8;               // coop halves with >= 2^8 flows try the single-segment path first
+#ifndef SENTINEL_PH_COOP_SINGLE_HB
+#define SENTINEL_PH_COOP_SINGLE_HB 8
+#endif
+constexpr int PH_COOP_SINGLE_HB = SENTINEL_PH_COOP_SINGLE_HB;   // coop halves with >= 2^this flows try part_run_single first
 constexpr int PH_COOP_FLOWS = 1 << (PH_COOP_HB > 0 ? PH_COOP_HB : 0);
 inline bool part_coop(int lb) {
     const int hb = lb > 0 ? lb - 1 : 0;
