@@ -694,6 +694,24 @@ __global__ __launch_bounds__(256) void k_tok_sweep(TokenTable TT) {
     if (threadIdx.x == 0 && s_freed) tok_count_add(TT, 1, 0ull - s_freed);
 }
 
+// {live tokens, tombstones} of the cache into pinned host memory, stream-ordered after a batch (one
+// wave sums the striped counters): the host reads it once the batch's event has completed, so its bound
+// on live + tombstones tracks the cache without a synchronisation (engine.hip, submit_concurrent).
+__global__ __launch_bounds__(WAVE) void k_tok_snapshot(const unsigned long long *__restrict__ counts,
+                                                      unsigned long long *dst) {
+    const int l = threadIdx.x;
+    long long live = l < TOK_CNT_LANES ? (long long)counts[l * TOK_CNT_STRIDE] : 0;
+    long long tomb = l < TOK_CNT_LANES ? (long long)counts[l * TOK_CNT_STRIDE + 1] : 0;
+    for (int o = WAVE / 2; o > 0; o >>= 1) {
+        live += __shfl_xor(live, o, WAVE);
+        tomb += __shfl_xor(tomb, o, WAVE);
+    }
+    if (l == 0) {
+        __hip_atomic_store(&dst[0], (unsigned long long)live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&dst[1], (unsigned long long)tomb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // RegularExpireStrategy.clearToken (RegularExpireStrategy.java:94-124): with the reference's own
 // conditions every cached token qualifies (clientTimeout / resourceTimeout are durations compared
 // with the wall clock), so a sweep removes up to `max_tokens` tokens and returns their counts to

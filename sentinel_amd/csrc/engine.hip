@@ -701,6 +701,14 @@ struct sentinel_engine {
     DevBuf w_cbig;                     // concurrency scan: tile descriptors, fallback list, nowCalls after the batch
     int64_t cbig_n = 0;                // its bytes
     uint64_t tok_ub = 0;               // upper bound of live + tombstoned token slots (no device read per batch)
+    // the cache's counts after a recent batch (k_tok_snapshot into pinned memory, read once its event has
+    // completed): tok_ub = that count + the events of every batch submitted after it, never a synchronisation
+    unsigned long long *h_tok_snap = nullptr;
+    hipEvent_t tok_snap_ev = nullptr;
+    bool tok_snap_out = false;
+    uint64_t tok_n_total = 0, tok_snap_n = 0;   // events submitted so far / when the snapshot was enqueued
+    uint32_t tok_gen = 0, tok_snap_gen = 0;      // tok_gen: bumped when the cache is replaced or recounted
+    uint64_t tok_grow = 16;                      // SENTINEL_TOKEN_GROW: batches of headroom a compaction sizes for
     uint64_t tcap = (uint64_t)1 << 22;
     uint64_t tok_salt = 0, tok_counter = 1;
 
@@ -1227,6 +1235,9 @@ int sentinel_engine::ensure_tokens() {
     if (rc) return SENTINEL_E_NOMEM;
     HIP_OK(hipMemsetAsync(d_tok_rec.p, 0xFF, tcap * sizeof(TokRec), stream));   // empty keys, no claims
     tok_ub = 0;
+    ++tok_gen;
+    if (!h_tok_snap && hipHostMalloc((void **)&h_tok_snap, 16, 0) != hipSuccess) h_tok_snap = nullptr;
+    if (!tok_snap_ev && hipEventCreateWithFlags(&tok_snap_ev, hipEventDisableTiming) != hipSuccess) tok_snap_ev = nullptr;
     HIP_OK(hipMemsetAsync(d_tok_counts.p, 0, TOK_CNT_BYTES, stream));
     HIP_OK(hipStreamSynchronize(stream));
     std::random_device rd;                 // token ids: {salt:23 | counter:40}, opaque to clients like UUID bits
@@ -1276,6 +1287,7 @@ int sentinel_engine::rewrite_tokens(bool compact, uint64_t new_cap) {
     counts[0] = live;
     counts[1] = dead;
     tok_ub = live + dead;
+    ++tok_gen;
     HIP_OK(hipMemcpy(d_tok_rec.p, nr.data(), tcap * sizeof(TokRec), hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(d_tok_counts.p, counts.data(), TOK_CNT_BYTES, hipMemcpyHostToDevice));
     return 0;
@@ -1296,6 +1308,7 @@ int sentinel_engine::rebuild_tokens_device(uint64_t new_cap, hipStream_t s) {
     HIP_OK(hipGetLastError());
     std::swap(d_tok_rec, sp_tok_rec);
     tcap = ncap;
+    ++tok_gen;
     return 0;
 }
 
@@ -2701,6 +2714,7 @@ int sentinel_engine_create(int device, const sentinel_server_config_t *cfg, sent
         }
     }
     if (const char *c = getenv("SENTINEL_HOT_FORK")) e->hot_fork = std::string(c) != "0";
+    if (const char *c = getenv("SENTINEL_TOKEN_GROW")) e->tok_grow = std::max<uint64_t>(1, strtoull(c, nullptr, 10));
     if (const char *c = getenv("SENTINEL_SEG_IMPL")) e->seg_impl = atoi(c);
     if (const char *c = getenv("SENTINEL_ROUTE8")) e->use_route8 = std::string(c) != "0";
     if (const char *c = getenv("SENTINEL_LIM1")) e->lim1 = std::string(c) != "0";
@@ -2774,6 +2788,8 @@ int sentinel_engine_destroy(sentinel_engine_t *e) {
     }
     if (e->s_h2d) (void)hipStreamDestroy(e->s_h2d);
     if (e->s_aux) (void)hipStreamDestroy(e->s_aux);
+    if (e->tok_snap_ev) (void)hipEventDestroy(e->tok_snap_ev);
+    if (e->h_tok_snap) (void)hipHostFree(e->h_tok_snap);
     if (e->s_d2h) (void)hipStreamDestroy(e->s_d2h);
     if (e->h_part_stat) (void)hipHostFree(e->h_part_stat);
     if (e->h_pfresh) (void)hipHostFree(e->h_pfresh);
@@ -4154,7 +4170,16 @@ static int submit_concurrent(sentinel_engine_t *e, int64_t n, const ConcEvent *d
     if (n > MAX_BATCH) return fail(SENTINEL_E_INVALID, "batch too large (max 2^28 events)");
     int rc = e->ensure_tokens();
     if (rc) return rc;
+    if (e->tok_snap_out && hipEventQuery(e->tok_snap_ev) == hipSuccess) {
+        e->tok_snap_out = false;                  // a completed snapshot: the bound from the device's counts
+        if (e->tok_snap_gen == e->tok_gen) {
+            const uint64_t ub = __atomic_load_n(&e->h_tok_snap[0], __ATOMIC_ACQUIRE) +
+                                __atomic_load_n(&e->h_tok_snap[1], __ATOMIC_ACQUIRE) + (e->tok_n_total - e->tok_snap_n);
+            if (ub < e->tok_ub) e->tok_ub = ub;
+        }
+    }
     if ((double)(e->tok_ub + (uint64_t)n) > 0.75 * (double)e->tcap) {
+        ++e->tok_gen;                             // (recounted below: an older snapshot is dropped)
         if (s != e->stream) HIP_OK(hipStreamSynchronize(s));
         HIP_OK(hipStreamSynchronize(e->stream));
         unsigned long long counts[2];
@@ -4167,16 +4192,20 @@ static int submit_concurrent(sentinel_engine_t *e, int64_t n, const ConcEvent *d
             e->tok_ub = counts[0] + counts[1];
         }
         if ((double)(e->tok_ub + (uint64_t)n) > 0.75 * (double)e->tcap) {
-            // drop the tombstones, and grow until the live tokens plus a few batches fit (a crossing of the bound
-            // costs one host synchronisation; releases empty their slots, so it rarely needs a sweep)
+            // drop the tombstones, and grow until the live tokens plus tok_grow batches fit (a crossing of the
+            // bound costs one host synchronisation).  Ids name their ring slot, so a released token's tombstone is
+            // reused only when the ids come round again: the cache settles at a fixed fraction of live + tombstones,
+            // and the headroom above it must cover the batches the host runs ahead of the device (the bound only
+            // drops when a snapshot completes)
             uint64_t nc = e->tcap;
-            while ((double)(counts[0] + 4 * (uint64_t)n) > 0.75 * (double)nc && nc < ((uint64_t)1 << 32)) nc <<= 1;
+            while ((double)(counts[0] + e->tok_grow * (uint64_t)n) > 0.75 * (double)nc && nc < ((uint64_t)1 << 32)) nc <<= 1;
             rc = e->rebuild_tokens_device(nc, s);
             if (rc) return rc;
             e->tok_ub = counts[0];
         }
     }
     e->tok_ub += (uint64_t)n;                    // at most one new token per event
+    e->tok_n_total += (uint64_t)n;
     rc = e->ensure_ws(n);
     if (rc) return SENTINEL_E_NOMEM;
     const int32_t F = (int32_t)e->rules.size();
@@ -4224,6 +4253,14 @@ static int submit_concurrent(sentinel_engine_t *e, int64_t n, const ConcEvent *d
                                                      S.fin, now_calls, dout);
         });
         e->tok_counter += (uint64_t)n;
+    }
+    if (!e->tok_snap_out && e->tok_snap_ev && e->h_tok_snap) {
+        k_tok_snapshot<<<1, WAVE, 0, s>>>(e->d_tok_counts.as<unsigned long long>(), e->h_tok_snap);
+        if (hipEventRecord(e->tok_snap_ev, s) == hipSuccess) {
+            e->tok_snap_out = true;
+            e->tok_snap_n = e->tok_n_total;
+            e->tok_snap_gen = e->tok_gen;
+        }
     }
     HIP_OK(hipGetLastError());
     return 0;
