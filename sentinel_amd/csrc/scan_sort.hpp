@@ -303,12 +303,31 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist_pass(const uint32_t
                                                                   int64_t nblocks) {
     __shared__ uint32_t h[RADIX];
     for (int d = threadIdx.x; d < RADIX; d += SORT_THREADS) h[d] = 0;
-    __syncthreads();
     const int64_t base = (int64_t)blockIdx.x * SORT_TILE;
-#pragma unroll 4
+    uint32_t k[SORT_ITEMS];                               // every load of the tile in flight at once
+#pragma unroll
     for (int j = 0; j < SORT_ITEMS; ++j) {
-        int64_t i = base + j * SORT_THREADS + threadIdx.x;
-        if (i < n) atomicAdd(&h[(keys[i] >> shift) & (RADIX - 1)], 1u);
+        const int64_t i = base + j * SORT_THREADS + threadIdx.x;
+        k[j] = i < n ? keys[i] : 0u;
+    }
+    __syncthreads();
+    // one LDS add per run of equal digits within a wave: a later pass reads the previous pass's output,
+    // where a hot key's events are contiguous (a Zipf batch sent hundreds of same-address adds per tile
+    // through one LDS bank before)
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int j = 0; j < SORT_ITEMS; ++j) {
+        const bool valid = base + j * SORT_THREADS + threadIdx.x < n;   // (a prefix of the wave's lanes)
+        const uint32_t d = (k[j] >> shift) & (RADIX - 1);
+        const uint32_t dp = __shfl_up(d, 1, WAVE);
+        const bool head = valid && (lane == 0 || d != dp);
+        const uint64_t hm = __ballot(head);
+        const uint32_t nvalid = (uint32_t)__popcll(__ballot(valid));
+        if (head) {
+            const uint64_t above = hm & ~((2ull << lane) - 1ull);    // (lane 63: 2 << 63 == 0, nothing above)
+            const uint32_t end = above ? (uint32_t)__ffsll((long long)above) - 1 : nvalid;
+            atomicAdd(&h[d], end - lane);
+        }
     }
     __syncthreads();
     for (int d = threadIdx.x; d < RADIX; d += SORT_THREADS) hist[(int64_t)d * nblocks + blockIdx.x] = h[d];
