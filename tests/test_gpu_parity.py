@@ -427,8 +427,9 @@ def test_window_boundary_inside_batch(oracle_mod, F):
     run is two homogeneous segments, epoch E then E2 (partition.hpp, part_run_single's two-segment closed
     form -- 1M flows: one thread per flow; 400k: the cooperative verdict sweep).  Windows n = 10 / 2 / 1 over
     1 s (with n = 1 both segments share one slot), acquire counts that change at the boundary, small
-    thresholds (blocked events in both segments), and batches before / across / after the boundary so the
-    rolled slots carry state; bit-exact statuses, remaining and window counters."""
+    thresholds (blocked events in both segments), batches before / across / after the boundary so the
+    rolled slots carry state, and one batch whose halves lie 2 s apart (the second segment's window holds
+    nothing of the first); bit-exact statuses, remaining and window counters."""
     import torch
     from sentinel_amd.token_service import decode_verdicts, device_events
     rng = np.random.default_rng(29)
@@ -441,10 +442,15 @@ def test_window_boundary_inside_batch(oracle_mod, F):
                                                     rules.namespace, rules.checker)
     n = 4 * 1024 * 1024
     erng = np.random.default_rng(30)
-    for b, (t_lo, t_hi) in enumerate([(985, 993), (996, 1004), (1004, 1012)]):
+    # the last batch jumps 2 s between its halves: its second segments start past every slot of the first
+    # (E2 - E >= n for every window)
+    for b, (t_lo, t_hi) in enumerate([(985, 993), (996, 1004), (1004, 1012), (1990, 3998)]):
         idx = erng.integers(0, F, n, dtype=np.int32)
         ts = (T.T0_ALIGNED + t_lo + np.floor(np.arange(n, dtype=np.float64) * ((t_hi - t_lo) / n))).astype(np.int64)
-        acq = (1 + (idx.astype(np.int64) + (ts >= T.T0_ALIGNED + 1000)) % 3).astype(np.int32)
+        if b == 3:
+            ts = np.where(np.arange(n) < n // 2, T.T0_ALIGNED + 1990 + np.arange(n) * 4 // n,
+                          T.T0_ALIGNED + 3994 + np.arange(n) * 4 // n).astype(np.int64)
+        acq = (1 + (idx.astype(np.int64) + (ts >= T.T0_ALIGNED + 1000) + (ts >= T.T0_ALIGNED + 3000)) % 3).astype(np.int32)
         v = svc.submit_flow_batch(device_events(torch.from_numpy(idx).cuda(), torch.from_numpy(acq).cuda(),
                                                 torch.from_numpy(ts).cuda()))
         svc.synchronize()
